@@ -1,0 +1,193 @@
+"""bench.py — SpMV+halo throughput of mul!(y, A, x) (Interfaces.jl:2246-2275) on
+MI355X: the 27-point FE operator (test_fem_sa.jl's pattern in 3D), 256³ nodes
+per GPU, weak scaling over Cartesian parts (1 → (1,1,1), 2 → (2,1,1),
+4 → (2,2,1), 8 → (2,2,2)).
+
+A step = one mul! (halo exchange of x + SpMV of every owned row) with A and x
+resident in HBM.  value = algorithmic bytes of all parts /
+time of K steps (max over ranks) → GB/s.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--n 256] [--kind 27]
+    torchrun --nproc-per-node N bench.py --gpus N ...   (one part per GPU)
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import subprocess
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+PART_SHAPES = {1: (1, 1, 1), 2: (2, 1, 1), 4: (2, 2, 1), 8: (2, 2, 2)}
+DTYPES = {"f64": np.float64, "f32": np.float32, "c128": np.complex128, "c64": np.complex64}
+
+
+def algorithmic_bytes(nnz, n_own, n_ghost, n_snd, n_rcv, S, I=4):
+    """nnz·(S+I) + (n_own+1)·I + (n_own+n_ghost)·S + n_own·S
+    + (n_snd+n_rcv)·(I+2S)."""
+    return nnz * (S + I) + (n_own + 1) * I + (n_own + n_ghost) * S + n_own * S + (n_snd + n_rcv) * (I + 2 * S)
+
+
+def cpu_baseline(kind, seconds=15.0, n=128):
+    """oracle/build/spmv_ref on one host core: the reference's CSC column
+    loop (SparseUtils.jl:157-187) restated in C ("port")."""
+    exe = os.path.join(ROOT, "oracle", "build", "spmv_ref")
+    if not os.path.exists(exe):
+        subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle")], check=True)
+    out = subprocess.run([exe, "--kind", str(kind), "--n", str(n), "--seconds", str(seconds)],
+                         check=True, capture_output=True, text=True).stdout
+    r = json.loads(out.strip().splitlines()[-1])
+    return {"value": round(r["gbps"], 3), "unit": "GB/s", "cores": 1, "kind": "port",
+            "sample": f"{kind}-pt operator {n}^3 nodes ({r['nnz']} nnz), {r['reps']} SpMVs in ~{seconds:.0f} s, "
+                      f"Int64 CSC column loop (SparseUtils.jl:157-187) in C, 1 thread"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--n", type=int, default=256, help="nodes per dim per GPU")
+    ap.add_argument("--kind", type=int, default=27, choices=[7, 27])
+    ap.add_argument("--dtype", default="f64", choices=list(DTYPES))
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    import torch
+    import torch.distributed as dist
+    import pamd
+
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("gloo")
+        backend = pamd.HIPDistributedBackend()
+    else:
+        backend = pamd.HIPBackend(devices=[0])
+    ngpu = world
+    if ngpu not in PART_SHAPES:
+        raise SystemExit(f"--gpus must be one of {sorted(PART_SHAPES)}")
+    shape = PART_SHAPES[ngpu]
+    N = tuple(args.n * s for s in shape)
+    dtype = DTYPES[args.dtype]
+    S = np.dtype(dtype).itemsize
+
+    t_setup = time.perf_counter()
+    parts = backend.get_part_ids(shape)
+    partition = pamd.drivers.stencil_partition(parts, N, args.kind)
+    A = pamd.drivers.stencil_operator(parts, N, args.kind, dtype, partition=partition)
+    rows, cols = A.rows, A.cols
+    rng = np.random.default_rng(20250114 + rank)
+    x = pamd.PVector.from_host(pamd.map_parts(
+        lambda s: rng.uniform(-1, 1, s.num_lids).astype(dtype), cols.partition), cols)
+    y = pamd.PVector.undef(rows, dtype)
+    ctx = backend.context(parts.part_ids[0])
+    ctx.sync()
+    t_setup = time.perf_counter() - t_setup
+
+    # per-part algorithmic bytes
+    p = parts.part_ids[0]
+    info = A.values.local(p).info()
+    s = cols.partition.local(p)
+    ex = cols.exchanger
+    n_snd = len(ex.lids_snd.local(p).data)
+    n_rcv = len(ex.lids_rcv.local(p).data)
+    B_part = algorithmic_bytes(info["nnz"], info["nrows"], s.num_hids, n_snd, n_rcv, S)
+    B_all = B_part
+    if world > 1:
+        t = torch.tensor([float(B_part)], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        B_all = float(t.item())
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    for _ in range(args.warmup):
+        pamd.mul_(y, A, x)
+    ctx.sync()
+    barrier()
+    ctx.sync()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        pamd.mul_(y, A, x)
+    ctx.sync()
+    t1 = time.perf_counter()
+    barrier()
+    elapsed = t1 - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    ms_per_step = 1e3 * elapsed / args.steps
+    value = B_all / (elapsed / args.steps) / 1e9
+
+    # roofline: device time of the SpMV kernels measured with HIP events on
+    # the stream they run on (pa_ctx_last_kernel_ms), averaged over K launches
+    ctx.set_timing(True)
+    kms = []
+    for _ in range(max(5, min(args.steps, 50))):
+        pamd.mul_(y, A, x)
+        a_ms, b_ms = ctx.last_kernel_ms()
+        kms.append(a_ms + b_ms)
+    ctx.set_timing(False)
+    kernel_ms = float(np.mean(kms))
+    spmv_bytes = info["nnz"] * (S + 4) + (info["nrows"] + 1) * 4 + (info["nrows"] + s.num_hids) * S + info["nrows"] * S
+    achieved = spmv_bytes / (kernel_ms * 1e-3) / 1e9
+
+    line = {
+        "metric": "SpMV+halo GB/s (frac of HBM peak), 3D Poisson 27-pt, 1/2/4/8 MI355X",
+        "value": round(value, 2),
+        "unit": "GB/s",
+        "n_gpus": ngpu,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": {"f64": "f64", "f32": "f32", "c128": "c128", "c64": "c64"}[args.dtype],
+        "data": "synthetic (seeded uniform x; operator generated on device)",
+        "config": {
+            "workload": f"mul!(y,A,x) incl. halo, {args.kind}-pt {'FE (test_fem_sa.jl pattern)' if args.kind == 27 else 'FD (test_fdm.jl)'} "
+                        f"operator, {args.n}^3 nodes per GPU, Cartesian parts {shape}",
+            "global_nodes": list(N),
+            "parts": list(shape),
+            "nnz_per_part": info["nnz"],
+            "rows_per_part": info["nrows"],
+            "ghosts_per_part": s.num_hids,
+            "bytes_per_step_all_parts": B_all,
+            "frac_of_hbm_peak": round(value / (HBM_PEAK_GBS * ngpu), 4),
+            "setup_s": round(t_setup, 2),
+        },
+        "roofline": {
+            "bound": "hbm",
+            "achieved": round(achieved, 1),
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4),
+            "traffic": None,
+            "kernel": "k_spmv_sell",
+            "kernel_ms": round(kernel_ms, 4),
+            "algorithmic_bytes_per_launch": spmv_bytes,
+        },
+    }
+    if rank == 0 and ngpu == 1 and not args.no_cpu_baseline:
+        line["cpu_baseline"] = cpu_baseline(args.kind, args.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,192 @@
+/*
+ * pa_hip.h — C-ABI of the MI355X-native backend for PartitionedArrays.jl's
+ * SpMV + halo hot path (libpa_hip.so).
+ *
+ * This is the drop-in boundary.  A Julia `HIPBackend <: AbstractBackend`
+ * binds these symbols with `ccall`; the Python host
+ * package in partitionedarrays.jl_amd/ binds them with ctypes and is the
+ * stand-in for that shim in this repository (no Julia on this image).
+ *
+ * Conventions:
+ *  - every entry point returns int: 0 = ok, <0 = error; the message of the
+ *    last error of the calling thread is in pa_last_error();
+ *  - all index inputs are Julia 1-based (Int32 unless a width is passed);
+ *    they are converted once, at create time;
+ *  - the library copies host inputs and owns all device memory; handles are
+ *    opaque and freed by their *_destroy;
+ *  - a process holds one or more parts ("local parts"); the *_all entry
+ *    points take the arrays of handles of all local parts, in part order,
+ *    mirroring `map_parts` over an AbstractPData.  Neighbours held by the
+ *    same process are served by device copies, neighbours in other processes
+ *    by RCCL point-to-point over xGMI (after pa_comm_init_rank);
+ *  - dtype codes: PA_F32, PA_F64, PA_C64 (ComplexF32), PA_C128 (ComplexF64).
+ *    Scalars (alpha, beta, results) are passed as pointers to host values of
+ *    the vector's element type.
+ */
+#ifndef PA_HIP_H
+#define PA_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum { PA_F32 = 0, PA_F64 = 1, PA_C64 = 2, PA_C128 = 3 };
+enum { PA_REPLACE = 0, PA_ADD = 1 };
+
+typedef struct pa_ctx pa_ctx;
+typedef struct pa_index pa_index;
+typedef struct pa_xchg pa_xchg;
+typedef struct pa_vec pa_vec;
+typedef struct pa_mat pa_mat;
+
+/* ---- errors / library info ------------------------------------------- */
+const char* pa_last_error(void);
+int pa_version(void);
+/* number of visible HIP devices (0 when no GPU). */
+int pa_device_count(int* count);
+
+/* ---- part context ------------------------------------------------------
+ * One context per part: its device, its streams, its scratch.
+ * Replaces the part slot of `get_part_ids(b::AbstractBackend, nparts)`
+ * (Interfaces.jl:24) — part is 1-based, 1 <= part <= nparts.          */
+int pa_ctx_create(int device, int part, int nparts, pa_ctx** out);
+int pa_ctx_destroy(pa_ctx* ctx);
+int pa_ctx_sync(pa_ctx* ctx);
+
+/* RCCL bootstrap for the one-part-per-process mode (the MPIBackend role,
+ * MPIBackend.jl:9-36): rank 0 makes the id, the host broadcasts it (MPI
+ * Bcast / torch.distributed), every rank calls pa_comm_init_rank with
+ * rank = part-1 and nranks = nparts.                                    */
+int pa_comm_unique_id(unsigned char id[128]);
+int pa_comm_init_rank(pa_ctx* ctx, const unsigned char id[128]);
+
+/* ---- index sets --------------------------------------------------------
+ * Device copy of an AbstractIndexSet's oid_to_lid / hid_to_lid
+ * (IndexSets.jl:215-265, 343-421).  1-based Int32 inputs.  Contiguous
+ * layouts (oid_to_lid == 1:noids, hid_to_lid == noids+1:nlids) are detected
+ * and kept as ranges (no device table).                                  */
+int pa_index_create(pa_ctx* ctx, int64_t nlids,
+                    int64_t noids, const int32_t* oid_to_lid,
+                    int64_t nhids, const int32_t* hid_to_lid,
+                    pa_index** out);
+int pa_index_destroy(pa_index* idx);
+
+/* ---- exchanger (halo plan) ----------------------------------------------
+ * `Exchanger{parts_rcv,parts_snd,lids_rcv,lids_snd}` (Interfaces.jl:698-713)
+ * verbatim: parts_* are 1-based part ids, ptrs_* are the 1-based Table ptrs
+ * (length n+1), lids_* the 1-based Table data.                            */
+int pa_xchg_create(pa_ctx* ctx,
+                   int32_t n_rcv, const int32_t* parts_rcv,
+                   const int32_t* ptrs_rcv, const int32_t* lids_rcv,
+                   int32_t n_snd, const int32_t* parts_snd,
+                   const int32_t* ptrs_snd, const int32_t* lids_snd,
+                   pa_xchg** out);
+int pa_xchg_destroy(pa_xchg* xg);
+
+/* ---- vectors (the values of one part of a PVector) --------------------- */
+int pa_vec_create(pa_ctx* ctx, int dtype, int64_t n, pa_vec** out);
+int pa_vec_destroy(pa_vec* v);
+int pa_vec_upload(pa_vec* v, const void* host, int64_t n);
+int pa_vec_download(const pa_vec* v, void* host, int64_t n);
+/* fill!(v, s) (Interfaces.jl:1966-1971), all lids */
+int pa_vec_fill(pa_vec* v, const void* s);
+/* copyto!(dst, src): all lids when same_layout, owned values otherwise
+ * (Interfaces.jl:1659-1667).  idx_* describe each vector's partition.    */
+int pa_vec_copy(pa_vec* dst, const pa_index* idx_dst,
+                const pa_vec* src, const pa_index* idx_src, int same_layout);
+/* Fused broadcast kernels for the CG recurrence (Interfaces.jl:1710-1737),
+ * evaluated exactly as Julia's scalar loop (no FMA contraction):
+ *   mode 0: y[i] = x[i] + a*y[i]     (u .= r .+ β.*u)
+ *   mode 1: y[i] = y[i] + a*x[i]     (x .+= α.*u)
+ *   mode 2: y[i] = y[i] - a*x[i]     (r .-= α.*c)
+ *   mode 3: y[i] = y[i] - x[i]       (r .-= c)
+ *   mode 4: y[i] = a*y[i]            (rmul!, Interfaces.jl:1675)
+ * over all lids when all_lids != 0 (same partition: ghosts too), else over
+ * the owned values through idx (which must describe both vectors).       */
+int pa_vec_axpby(pa_vec* y, const pa_vec* x, const pa_index* idx,
+                 const void* a, int mode, int all_lids);
+
+/* ---- matrices (one part of a PSparseMatrix) ----------------------------
+ * From the reference's local SparseMatrixCSC (1-based colptr/rowval with
+ * index_bytes = 4 or 8, nzval of dtype), with the matrix's rows/cols index
+ * sets.  Builds the owned-row split SELL layout once:
+ * own-column entries in oid order, then ghost-column entries in hid order,
+ * i.e. the summation order of SparseUtils.jl:176-185 applied to the
+ * owned_owned and owned_ghost blocks (Interfaces.jl:2142-2156, 2261-2272).
+ * Stored entries of ghost rows are dropped (the `i>0` filter).            */
+int pa_mat_from_csc(pa_ctx* ctx, int dtype, int index_bytes,
+                    int64_t nrows_lids, int64_t ncols_lids,
+                    const void* colptr, const void* rowval, const void* nzval,
+                    const pa_index* rows, const pa_index* cols,
+                    pa_mat** out);
+/* Replace the stored values keeping the pattern (same CSC nz order),
+ * e.g. after fillstored!/re-assembly (Interfaces.jl:2127-2132).          */
+int pa_mat_set_values(pa_mat* A, const void* nzval);
+int pa_mat_destroy(pa_mat* A);
+/* nnz stored on device (padding included) and owned-row nnz. */
+int pa_mat_info(const pa_mat* A, int64_t* nrows_owned, int64_t* nnz_owned,
+                int64_t* slots, int64_t* nslices, int64_t* nslices_interior);
+
+/* ---- hot path -----------------------------------------------------------
+ * mul!(c, a, b, α, β) (Interfaces.jl:2246-2275) for the n local parts:
+ * starts the halo exchange of x (pack → P2P → unpack into x's ghost lids,
+ * i.e. exchange!(b)), runs the interior slices meanwhile, then the slices
+ * that read ghost values.  y_idx / x_idx are the partitions of c and b
+ * (c.rows / b.rows); x_idx must have the matrix's column layout.
+ * Asynchronous with respect to the host (stream-ordered per part).       */
+int pa_spmv_all(int n, pa_mat* const A[], pa_vec* const y[],
+                const pa_index* const y_idx[],
+                pa_vec* const x[], const pa_index* const x_idx[],
+                pa_xchg* const xg[], const void* alpha, const void* beta);
+
+/* exchange!(combine, values, exchanger) (Interfaces.jl:846-889) for the n
+ * local parts; reverse != 0 uses reverse(exchanger) (Interfaces.jl:796).
+ * With reverse=1, op=PA_ADD and zero_ghosts=1 this is assemble!(v)
+ * (Interfaces.jl:2084-2106).  Contributions to one lid are combined in the
+ * receive-buffer order of the reference (bit-exact).                      */
+int pa_exchange_all(int n, pa_vec* const v[], pa_xchg* const xg[],
+                    const pa_index* const idx[], int op, int reverse,
+                    int zero_ghosts);
+
+/* dot(a,b) (Interfaces.jl:1985-1992) → sum over parts, folded in part
+ * order as reduce(+, …; init=0) (Interfaces.jl:221-238).  result: host
+ * scalar of the vectors' dtype (complex: conj(a)·b).                      */
+int pa_dot_all(int n, const pa_vec* const a[], const pa_index* const ia[],
+               const pa_vec* const b[], const pa_index* const ib[],
+               void* result);
+/* norm(a, 2) (Interfaces.jl:1767-1772); result: host double (the
+ * reference's `(…)^(1/p)` promotes Float32 partials to Float64).          */
+int pa_norm2_all(int n, const pa_vec* const a[], const pa_index* const ia[],
+                 void* result);
+/* sum(a) = reduce(+, a; init=0) over owned values (Interfaces.jl:1973-1983) */
+int pa_sum_all(int n, const pa_vec* const a[], const pa_index* const ia[],
+               void* result);
+
+/* ---- synthetic operators (benchmark driver, not a reference entry point) --
+ * One Cartesian part box [box_lo, box_lo+box_n) of a gdims[0]×gdims[1]×
+ * gdims[2] node grid (0-based coordinates, x fastest), built directly on the
+ * device in the layout pa_mat_from_csc would produce for the CSC that the
+ * drivers assemble: kind 7 = test_fdm.jl's FD Poisson operator (coeffs =
+ * {diag, offdiag}), kind 27 = Q1-hex FE operator of test_fem_sa.jl's
+ * pattern (coeffs = Ke, 8×8 row-major).  Owned lids are the box's nodes in
+ * x-fastest order; shell_lid[(ez*(ny+2)+ey)*(nx+2)+ex] is the 0-based lid of
+ * the node at box-local (ex-1,ey-1,ez-1) of the one-node shell (ghosts), or
+ * -1; NULL when the part has no ghosts.  nlids_cols = noids + nhids.      */
+int pa_mat_stencil(pa_ctx* ctx, int dtype, int kind, const int64_t gdims[3],
+                   const int64_t box_lo[3], const int64_t box_n[3],
+                   int64_t nlids_cols, const int32_t* shell_lid,
+                   const double* coeffs, int ncoeffs, pa_mat** out);
+
+/* ---- timing (PTimer analogue, PTimers.jl) -------------------------------
+ * Average device time of the last `pa_spmv_all` kernels of this context,
+ * measured with HIP events on the stream they ran on.                    */
+int pa_ctx_last_kernel_ms(pa_ctx* ctx, float* spmv_interior_ms,
+                          float* spmv_boundary_ms);
+int pa_ctx_set_timing(pa_ctx* ctx, int enable);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PA_HIP_H */

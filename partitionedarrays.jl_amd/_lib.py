@@ -1,0 +1,128 @@
+"""ctypes binding of libpa_hip.so — the same C-ABI a Julia `HIPBackend` would
+`ccall` (include/pa_hip.h).
+
+There is no CPU fallback: if the shared library is missing, or no HIP device
+is visible, every device operation raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libpa_hip.so")
+
+PA_F32, PA_F64, PA_C64, PA_C128 = 0, 1, 2, 3
+PA_REPLACE, PA_ADD = 0, 1
+
+DTYPES = {
+    np.dtype(np.float32): PA_F32,
+    np.dtype(np.float64): PA_F64,
+    np.dtype(np.complex64): PA_C64,
+    np.dtype(np.complex128): PA_C128,
+}
+NP_OF = {v: k for k, v in DTYPES.items()}
+
+_lib = None
+_p = C.c_void_p
+_i32p = C.POINTER(C.c_int32)
+_i64p = C.POINTER(C.c_int64)
+
+# name: (argtypes)  — every function returns int status
+_SIGS = {
+    "pa_version": [],
+    "pa_device_count": [C.POINTER(C.c_int)],
+    "pa_ctx_create": [C.c_int, C.c_int, C.c_int, C.POINTER(_p)],
+    "pa_ctx_destroy": [_p],
+    "pa_ctx_sync": [_p],
+    "pa_comm_unique_id": [C.c_char_p],
+    "pa_comm_init_rank": [_p, C.c_char_p],
+    "pa_index_create": [_p, C.c_int64, C.c_int64, _i32p, C.c_int64, _i32p, C.POINTER(_p)],
+    "pa_index_destroy": [_p],
+    "pa_xchg_create": [_p, C.c_int32, _i32p, _i32p, _i32p, C.c_int32, _i32p, _i32p, _i32p, C.POINTER(_p)],
+    "pa_xchg_destroy": [_p],
+    "pa_vec_create": [_p, C.c_int, C.c_int64, C.POINTER(_p)],
+    "pa_vec_destroy": [_p],
+    "pa_vec_upload": [_p, _p, C.c_int64],
+    "pa_vec_download": [_p, _p, C.c_int64],
+    "pa_vec_fill": [_p, _p],
+    "pa_vec_copy": [_p, _p, _p, _p, C.c_int],
+    "pa_vec_axpby": [_p, _p, _p, _p, C.c_int, C.c_int],
+    "pa_mat_from_csc": [_p, C.c_int, C.c_int, C.c_int64, C.c_int64, _p, _p, _p, _p, _p, C.POINTER(_p)],
+    "pa_mat_set_values": [_p, _p],
+    "pa_mat_destroy": [_p],
+    "pa_mat_info": [_p, _i64p, _i64p, _i64p, _i64p, _i64p],
+    "pa_mat_stencil": [_p, C.c_int, C.c_int, _i64p, _i64p, _i64p, C.c_int64, _i32p, C.POINTER(C.c_double), C.c_int, C.POINTER(_p)],
+    "pa_spmv_all": [C.c_int, C.POINTER(_p), C.POINTER(_p), C.POINTER(_p), C.POINTER(_p), C.POINTER(_p), C.POINTER(_p), _p, _p],
+    "pa_exchange_all": [C.c_int, C.POINTER(_p), C.POINTER(_p), C.POINTER(_p), C.c_int, C.c_int, C.c_int],
+    "pa_dot_all": [C.c_int, C.POINTER(_p), C.POINTER(_p), C.POINTER(_p), C.POINTER(_p), _p],
+    "pa_norm2_all": [C.c_int, C.POINTER(_p), C.POINTER(_p), _p],
+    "pa_sum_all": [C.c_int, C.POINTER(_p), C.POINTER(_p), _p],
+    "pa_ctx_last_kernel_ms": [_p, C.POINTER(C.c_float), C.POINTER(C.c_float)],
+    "pa_ctx_set_timing": [_p, C.c_int],
+}
+
+EXPORTED = sorted(list(_SIGS) + ["pa_last_error"])
+
+
+class PAError(RuntimeError):
+    pass
+
+
+def _prepare_runtime():
+    # One HIP runtime per process: torch ships its own libamdhip64 with the
+    # same soname; importing torch first makes the dynamic linker reuse it
+    # for libpa_hip.so (two runtimes in one process would not share devices).
+    try:
+        import torch  # noqa: F401
+    except Exception:
+        pass
+
+
+def lib():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise PAError(f"{LIB_PATH} not built: run `python -c 'import __graft_entry__ as g; g.build()'`")
+    _prepare_runtime()
+    L = C.CDLL(LIB_PATH)
+    for name, args in _SIGS.items():
+        f = getattr(L, name)
+        f.argtypes = args
+        f.restype = C.c_int
+    L.pa_last_error.argtypes = []
+    L.pa_last_error.restype = C.c_char_p
+    _lib = L
+    return L
+
+
+def call(name, *args):
+    L = lib()
+    rc = getattr(L, name)(*args)
+    if rc != 0:
+        raise PAError(f"{name}: {L.pa_last_error().decode(errors='replace')}")
+
+
+def device_count() -> int:
+    n = C.c_int(0)
+    call("pa_device_count", C.byref(n))
+    return n.value
+
+
+def i32(a):
+    a = np.ascontiguousarray(a, dtype=np.int32)
+    return a, a.ctypes.data_as(_i32p)
+
+
+def ptr_array(handles):
+    arr = (_p * len(handles))(*[h for h in handles])
+    return arr
+
+
+def scalar_buf(value, dtype):
+    """host buffer holding `value` as dtype (for alpha/beta/fill)."""
+    a = np.array([value], dtype=np.dtype(dtype))
+    return a, a.ctypes.data_as(_p)

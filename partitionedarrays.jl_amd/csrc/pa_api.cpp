@@ -1,0 +1,1025 @@
+// pa_api.cpp — host side of libpa_hip.so: the C-ABI declared in
+// include/pa_hip.h.  Contexts, index sets, the halo plan, the one-time
+// CSC → SELL conversion, the halo transport (device copies between parts of
+// one process, RCCL send/recv between processes) and the reductions' fold.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <numeric>
+#include <string>
+#include <vector>
+
+#include "pa_internal.h"
+
+namespace pa {
+
+static thread_local std::string g_err;
+void set_error(const std::string& msg) { g_err = msg; }
+
+// kernels (pa_kernels.hip)
+void launch_spmv(int64_t nwork, const int32_t* list, const pa_mat* A, const void* x, void* y,
+                 const int32_t* ymap, bool has_alpha, int bmode, const void* alpha,
+                 const void* beta, hipStream_t st);
+void launch_pack(int dtype, int64_t n, const int32_t* lids, const void* v, void* buf,
+                 hipStream_t st);
+void launch_unpack(int dtype, int64_t n, const int32_t* lids, const pa_combine_plan& plan, int op,
+                   const void* buf, void* v, hipStream_t st);
+void launch_fill(int dtype, int64_t n, int64_t base, const int32_t* map, void* v, const void* s,
+                 hipStream_t st);
+void launch_copy(int dtype, int64_t n, const int32_t* dmap, void* d, const int32_t* smap,
+                 const void* s, hipStream_t st);
+void launch_axpby(int dtype, int64_t n, const int32_t* map, void* y, const void* x, const void* a,
+                  int mode, hipStream_t st);
+void launch_reduce(int dtype, int kind, int64_t n, const int32_t* ma, const void* a,
+                   const int32_t* mb, const void* b, void* partials, void* result,
+                   hipStream_t st);
+void launch_stencil_count(const StencilGeom& g, const int32_t* shell, const double* coef,
+                          int64_t nrows, int noids, int H, int32_t* slen, int32_t* sghost,
+                          int32_t* err, hipStream_t st);
+void launch_stencil_fill(const StencilGeom& g, const int32_t* shell, const double* coef,
+                         int64_t nrows, int noids, pa_mat* A, int32_t* err, hipStream_t st);
+
+}  // namespace pa
+
+using namespace pa;
+
+#define PA_FAIL(msg)             \
+  do {                           \
+    pa::set_error(msg);          \
+    return -1;                   \
+  } while (0)
+
+#define HIPC(expr)                                                                       \
+  do {                                                                                   \
+    hipError_t e_ = (expr);                                                              \
+    if (e_ != hipSuccess) {                                                              \
+      pa::set_error(std::string(#expr) + " failed: " + hipGetErrorString(e_));           \
+      return -1;                                                                         \
+    }                                                                                    \
+  } while (0)
+
+#define NCCLC(expr)                                                                      \
+  do {                                                                                   \
+    ncclResult_t r_ = (expr);                                                            \
+    if (r_ != ncclSuccess) {                                                             \
+      pa::set_error(std::string(#expr) + " failed: " + ncclGetErrorString(r_));          \
+      return -1;                                                                         \
+    }                                                                                    \
+  } while (0)
+
+#define CHECK_ARG(cond, msg) \
+  do {                       \
+    if (!(cond)) PA_FAIL(msg); \
+  } while (0)
+
+namespace {
+
+template <typename T>
+int dev_upload(T** dptr, const std::vector<T>& h) {
+  *dptr = nullptr;
+  if (h.empty()) return 0;
+  HIPC(hipMalloc((void**)dptr, h.size() * sizeof(T)));
+  HIPC(hipMemcpy(*dptr, h.data(), h.size() * sizeof(T), hipMemcpyHostToDevice));
+  return 0;
+}
+
+void dev_free(void* p) {
+  if (p) (void)hipFree(p);
+}
+
+bool valid_dtype(int dt) { return dt == PA_F32 || dt == PA_F64 || dt == PA_C64 || dt == PA_C128; }
+
+// scalar helpers on host values of a dtype
+bool scalar_is(int dt, const void* s, double re) {
+  switch (dt) {
+    case PA_F32: return *(const float*)s == (float)re;
+    case PA_F64: return *(const double*)s == re;
+    case PA_C64: { const float* f = (const float*)s; return f[0] == (float)re && f[1] == 0.f; }
+    case PA_C128: { const double* d = (const double*)s; return d[0] == re && d[1] == 0.0; }
+  }
+  return false;
+}
+
+// Build an ordered combine plan for unpack targets `lids` (0-based, buffer order).
+int build_plan(const std::vector<int32_t>& lids, pa_combine_plan* plan) {
+  const int64_t n = (int64_t)lids.size();
+  std::vector<int32_t> order(n);
+  std::iota(order.begin(), order.end(), 0);
+  std::stable_sort(order.begin(), order.end(), [&](int32_t a, int32_t b) { return lids[a] < lids[b]; });
+  std::vector<int32_t> target, ptr{0}, pos;
+  pos.reserve(n);
+  for (int64_t i = 0; i < n; ++i) {
+    const int32_t l = lids[order[i]];
+    if (target.empty() || target.back() != l) {
+      if (!target.empty()) ptr.push_back((int32_t)pos.size());
+      target.push_back(l);
+    }
+    pos.push_back(order[i]);
+  }
+  if (!target.empty()) ptr.push_back((int32_t)pos.size());
+  plan->ntargets = (int64_t)target.size();
+  plan->unique = plan->ntargets == n;
+  if (!plan->unique) {
+    if (dev_upload(&plan->d_target, target)) return -1;
+    if (dev_upload(&plan->d_ptr, ptr)) return -1;
+    if (dev_upload(&plan->d_pos, pos)) return -1;
+  }
+  return 0;
+}
+
+void free_plan(pa_combine_plan& p) {
+  dev_free(p.d_target);
+  dev_free(p.d_ptr);
+  dev_free(p.d_pos);
+  p = pa_combine_plan{};
+}
+
+int finish_sell_layout(pa_mat* A, const std::vector<int32_t>& slen, const std::vector<char>& sghost,
+                       std::vector<int64_t>* soff_out) {
+  const int64_t ns = (int64_t)slen.size();
+  std::vector<int64_t> soff(ns);
+  int64_t acc = 0;
+  for (int64_t s = 0; s < ns; ++s) {
+    soff[s] = acc;
+    acc += (int64_t)slen[s] * A->H;
+  }
+  A->slots = acc;
+  A->nslices = ns;
+  std::vector<int32_t> ilist, blist;
+  for (int64_t s = 0; s < ns; ++s) (sghost[s] ? blist : ilist).push_back((int32_t)s);
+  A->nslices_int = (int64_t)ilist.size();
+  if (dev_upload(&A->d_slice_off, soff)) return -1;
+  if (dev_upload(&A->d_slice_len, slen)) return -1;
+  if (!blist.empty()) {
+    if (dev_upload(&A->d_int_list, ilist)) return -1;
+    if (dev_upload(&A->d_bnd_list, blist)) return -1;
+  }
+  if (soff_out) *soff_out = std::move(soff);
+  return 0;
+}
+
+// The parts of this call, by part id → position.
+struct LocalSet {
+  std::vector<int> pos_of_part;  // index part (1-based) → position or -1
+  int find(int part) const {
+    return (part >= 1 && part < (int)pos_of_part.size()) ? pos_of_part[part] : -1;
+  }
+};
+
+template <typename H>
+LocalSet local_set(int n, H* const* hs) {
+  LocalSet L;
+  int maxp = 0;
+  for (int i = 0; i < n; ++i) maxp = std::max(maxp, hs[i]->ctx->nparts);
+  L.pos_of_part.assign(maxp + 1, -1);
+  for (int i = 0; i < n; ++i) L.pos_of_part[hs[i]->ctx->part] = i;
+  return L;
+}
+
+// Halo transport for n local parts.  dir 0 (forward): send A-layout buffers
+// (ptrs_snd) to parts_snd, receive B-layout (ptrs_rcv) from parts_rcv;
+// dir 1 (reverse): the opposite.  Each part's s_comm first waits for the
+// packs of every sender it copies from (ev_packed), then ev_recvd is
+// recorded on it.
+int transport(int n, pa_xchg* const xg[], int dtype, int dir) {
+  const size_t S = dtype_size(dtype);
+  LocalSet L = local_set(n, xg);
+  bool remote = false;
+  for (int i = 0; i < n; ++i) {
+    pa_xchg* X = xg[i];
+    pa_ctx* c = X->ctx;
+    HIPC(hipSetDevice(c->device));
+    HIPC(hipStreamWaitEvent(c->s_comm, c->ev_packed, 0));
+    const auto& prcv = dir == 0 ? X->parts_rcv : X->parts_snd;
+    for (int32_t q : prcv) {
+      const int j = L.find(q);
+      if (j >= 0) HIPC(hipStreamWaitEvent(c->s_comm, xg[j]->ctx->ev_packed, 0));
+      else remote = true;
+    }
+    const auto& psnd = dir == 0 ? X->parts_snd : X->parts_rcv;
+    for (int32_t q : psnd)
+      if (L.find(q) < 0) remote = true;
+  }
+  if (remote) {
+    for (int i = 0; i < n; ++i)
+      CHECK_ARG(xg[i]->ctx->comm, "halo neighbour is not held by this process and no RCCL communicator was initialised (pa_comm_init_rank)");
+    NCCLC(ncclGroupStart());
+    for (int i = 0; i < n; ++i) {
+      pa_xchg* X = xg[i];
+      pa_ctx* c = X->ctx;
+      ncclComm_t comm = (ncclComm_t)c->comm;
+      const auto& psnd = dir == 0 ? X->parts_snd : X->parts_rcv;
+      const auto& osnd = dir == 0 ? X->ptrs_snd : X->ptrs_rcv;
+      char* bsnd = (char*)(dir == 0 ? X->d_buf_snd : X->d_buf_rcv);
+      const auto& prcv = dir == 0 ? X->parts_rcv : X->parts_snd;
+      const auto& orcv = dir == 0 ? X->ptrs_rcv : X->ptrs_snd;
+      char* brcv = (char*)(dir == 0 ? X->d_buf_rcv : X->d_buf_snd);
+      for (size_t k = 0; k < psnd.size(); ++k) {
+        if (L.find(psnd[k]) >= 0) continue;
+        const size_t cnt = (size_t)(osnd[k + 1] - osnd[k]) * S;
+        ncclResult_t r = ncclSend(bsnd + osnd[k] * S, cnt, ncclUint8, psnd[k] - 1, comm, c->s_comm);
+        if (r != ncclSuccess) { ncclGroupEnd(); PA_FAIL(std::string("ncclSend: ") + ncclGetErrorString(r)); }
+      }
+      for (size_t k = 0; k < prcv.size(); ++k) {
+        if (L.find(prcv[k]) >= 0) continue;
+        const size_t cnt = (size_t)(orcv[k + 1] - orcv[k]) * S;
+        ncclResult_t r = ncclRecv(brcv + orcv[k] * S, cnt, ncclUint8, prcv[k] - 1, comm, c->s_comm);
+        if (r != ncclSuccess) { ncclGroupEnd(); PA_FAIL(std::string("ncclRecv: ") + ncclGetErrorString(r)); }
+      }
+    }
+    NCCLC(ncclGroupEnd());
+  }
+  // local copies: receiver r, segment k from sender q (local), which holds
+  // the matching segment at the position of r in its send list.
+  for (int i = 0; i < n; ++i) {
+    pa_xchg* X = xg[i];
+    pa_ctx* c = X->ctx;
+    HIPC(hipSetDevice(c->device));
+    const auto& prcv = dir == 0 ? X->parts_rcv : X->parts_snd;
+    const auto& orcv = dir == 0 ? X->ptrs_rcv : X->ptrs_snd;
+    char* brcv = (char*)(dir == 0 ? X->d_buf_rcv : X->d_buf_snd);
+    for (size_t k = 0; k < prcv.size(); ++k) {
+      const int j = L.find(prcv[k]);
+      if (j < 0) continue;
+      pa_xchg* Q = xg[j];
+      const auto& qsnd = dir == 0 ? Q->parts_snd : Q->parts_rcv;
+      const auto& qo = dir == 0 ? Q->ptrs_snd : Q->ptrs_rcv;
+      const char* bq = (const char*)(dir == 0 ? Q->d_buf_snd : Q->d_buf_rcv);
+      int m = -1;
+      for (size_t t = 0; t < qsnd.size(); ++t)
+        if (qsnd[t] == c->part) { m = (int)t; break; }
+      CHECK_ARG(m >= 0, "exchanger mismatch: a receiver lists a sender that does not send to it");
+      const int64_t cnt = orcv[k + 1] - orcv[k];
+      CHECK_ARG(cnt == qo[m + 1] - qo[m], "exchanger mismatch: segment lengths differ (SequentialBackend.jl:187)");
+      if (cnt > 0)
+        HIPC(hipMemcpyAsync(brcv + orcv[k] * S, bq + qo[m] * S, (size_t)cnt * S, hipMemcpyDefault, c->s_comm));
+    }
+    HIPC(hipEventRecord(c->ev_recvd, c->s_comm));
+  }
+  return 0;
+}
+
+int check_lids(const pa_xchg* X, const pa_vec* v) {
+  CHECK_ARG(X->max_lid < v->n, "exchanger lids exceed the vector length (BoundsError)");
+  return 0;
+}
+
+// Before packing into the send buffers again, wait for the copies that read
+// them in the previous exchange (local receivers record ev_recvd after their
+// copies; for RCCL sends the part's own ev_recvd covers them).
+int pre_pack_wait(int n, pa_xchg* const xg[]) {
+  LocalSet L = local_set(n, xg);
+  for (int i = 0; i < n; ++i) {
+    pa_ctx* c = xg[i]->ctx;
+    HIPC(hipSetDevice(c->device));
+    HIPC(hipStreamWaitEvent(c->s_main, c->ev_recvd, 0));
+    for (const auto* lst : {&xg[i]->parts_snd, &xg[i]->parts_rcv})
+      for (int32_t q : *lst) {
+        const int j = L.find(q);
+        if (j >= 0 && j != i) HIPC(hipStreamWaitEvent(c->s_main, xg[j]->ctx->ev_recvd, 0));
+      }
+  }
+  return 0;
+}
+
+}  // namespace
+
+// ===========================================================================
+extern "C" {
+
+const char* pa_last_error(void) { return g_err.c_str(); }
+int pa_version(void) { return 1; }
+
+int pa_device_count(int* count) {
+  int c = 0;
+  hipError_t e = hipGetDeviceCount(&c);
+  if (e != hipSuccess) c = 0;
+  *count = c;
+  return 0;
+}
+
+int pa_ctx_create(int device, int part, int nparts, pa_ctx** out) {
+  CHECK_ARG(out, "null out");
+  CHECK_ARG(nparts >= 1 && part >= 1 && part <= nparts, "part must satisfy 1 <= part <= nparts");
+  int ndev = 0;
+  HIPC(hipGetDeviceCount(&ndev));
+  CHECK_ARG(device >= 0 && device < ndev, "invalid device ordinal");
+  HIPC(hipSetDevice(device));
+  pa_ctx* c = new pa_ctx();
+  c->device = device;
+  c->part = part;
+  c->nparts = nparts;
+  int least = 0, greatest = 0;
+  HIPC(hipDeviceGetStreamPriorityRange(&least, &greatest));
+  HIPC(hipStreamCreateWithFlags(&c->s_main, hipStreamNonBlocking));
+  HIPC(hipStreamCreateWithPriority(&c->s_comm, hipStreamNonBlocking, greatest));
+  HIPC(hipMalloc(&c->d_partials, 1024 * 16));
+  HIPC(hipMalloc(&c->d_result, 16));
+  HIPC(hipMalloc(&c->d_gather, (size_t)nparts * 16));
+  HIPC(hipHostMalloc(&c->h_pinned, (size_t)(nparts + 1) * 16));
+  HIPC(hipEventCreateWithFlags(&c->ev_packed, hipEventDisableTiming));
+  HIPC(hipEventCreateWithFlags(&c->ev_recvd, hipEventDisableTiming));
+  for (auto& e : c->ev_t) HIPC(hipEventCreate(&e));
+  *out = c;
+  return 0;
+}
+
+int pa_ctx_destroy(pa_ctx* c) {
+  if (!c) return 0;
+  (void)hipSetDevice(c->device);
+  (void)hipStreamSynchronize(c->s_main);
+  (void)hipStreamSynchronize(c->s_comm);
+  if (c->comm) ncclCommDestroy((ncclComm_t)c->comm);
+  dev_free(c->d_partials);
+  dev_free(c->d_result);
+  dev_free(c->d_gather);
+  if (c->h_pinned) (void)hipHostFree(c->h_pinned);
+  (void)hipEventDestroy(c->ev_packed);
+  (void)hipEventDestroy(c->ev_recvd);
+  for (auto& e : c->ev_t) (void)hipEventDestroy(e);
+  (void)hipStreamDestroy(c->s_main);
+  (void)hipStreamDestroy(c->s_comm);
+  delete c;
+  return 0;
+}
+
+int pa_ctx_sync(pa_ctx* c) {
+  CHECK_ARG(c, "null ctx");
+  HIPC(hipSetDevice(c->device));
+  HIPC(hipStreamSynchronize(c->s_comm));
+  HIPC(hipStreamSynchronize(c->s_main));
+  return 0;
+}
+
+int pa_comm_unique_id(unsigned char id[128]) {
+  ncclUniqueId u;
+  NCCLC(ncclGetUniqueId(&u));
+  static_assert(sizeof(u) == 128, "ncclUniqueId size");
+  std::memcpy(id, &u, 128);
+  return 0;
+}
+
+int pa_comm_init_rank(pa_ctx* c, const unsigned char id[128]) {
+  CHECK_ARG(c, "null ctx");
+  HIPC(hipSetDevice(c->device));
+  ncclUniqueId u;
+  std::memcpy(&u, id, 128);
+  ncclComm_t comm;
+  NCCLC(ncclCommInitRank(&comm, c->nparts, u, c->part - 1));
+  c->comm = comm;
+  return 0;
+}
+
+int pa_ctx_set_timing(pa_ctx* c, int enable) {
+  CHECK_ARG(c, "null ctx");
+  c->timing = enable != 0;
+  return 0;
+}
+
+int pa_ctx_last_kernel_ms(pa_ctx* c, float* int_ms, float* bnd_ms) {
+  CHECK_ARG(c, "null ctx");
+  *int_ms = c->last_int_ms;
+  *bnd_ms = c->last_bnd_ms;
+  return 0;
+}
+
+// ---------------------------------------------------------------------------
+int pa_index_create(pa_ctx* c, int64_t nlids, int64_t noids, const int32_t* oid_to_lid,
+                    int64_t nhids, const int32_t* hid_to_lid, pa_index** out) {
+  CHECK_ARG(c && out, "null argument");
+  CHECK_ARG(nlids >= 0 && noids >= 0 && nhids >= 0 && noids + nhids == nlids,
+            "index set: noids + nhids must equal nlids");
+  CHECK_ARG(nlids < (int64_t)INT32_MAX, "index set larger than Int32 lids");
+  HIPC(hipSetDevice(c->device));
+  pa_index* I = new pa_index();
+  I->ctx = c;
+  I->nlids = nlids;
+  I->noids = noids;
+  I->nhids = nhids;
+  I->h_oid_to_lid.resize(noids);
+  I->h_hid_to_lid.resize(nhids);
+  I->h_lid_to_ohid.assign(nlids, 0);
+  for (int64_t i = 0; i < noids; ++i) {
+    const int32_t l = oid_to_lid[i];
+    if (l < 1 || l > nlids || I->h_lid_to_ohid[l - 1] != 0) { delete I; PA_FAIL("index set: invalid or repeated oid_to_lid entry"); }
+    I->h_oid_to_lid[i] = l - 1;
+    I->h_lid_to_ohid[l - 1] = (int32_t)(i + 1);
+    if (l - 1 != i) I->own_contig = false;
+  }
+  for (int64_t i = 0; i < nhids; ++i) {
+    const int32_t l = hid_to_lid[i];
+    if (l < 1 || l > nlids || I->h_lid_to_ohid[l - 1] != 0) { delete I; PA_FAIL("index set: invalid or repeated hid_to_lid entry"); }
+    I->h_hid_to_lid[i] = l - 1;
+    I->h_lid_to_ohid[l - 1] = (int32_t)(-(i + 1));
+    if (l - 1 != noids + i) I->ghost_contig = false;
+  }
+  if (!I->own_contig && dev_upload(&I->d_oid_to_lid, I->h_oid_to_lid)) { delete I; return -1; }
+  if (!I->ghost_contig && dev_upload(&I->d_hid_to_lid, I->h_hid_to_lid)) { delete I; return -1; }
+  *out = I;
+  return 0;
+}
+
+int pa_index_destroy(pa_index* I) {
+  if (!I) return 0;
+  (void)hipSetDevice(I->ctx->device);
+  dev_free(I->d_oid_to_lid);
+  dev_free(I->d_hid_to_lid);
+  delete I;
+  return 0;
+}
+
+// ---------------------------------------------------------------------------
+int pa_xchg_create(pa_ctx* c, int32_t n_rcv, const int32_t* parts_rcv, const int32_t* ptrs_rcv,
+                   const int32_t* lids_rcv, int32_t n_snd, const int32_t* parts_snd,
+                   const int32_t* ptrs_snd, const int32_t* lids_snd, pa_xchg** out) {
+  CHECK_ARG(c && out, "null argument");
+  CHECK_ARG(n_rcv >= 0 && n_snd >= 0, "negative neighbour count");
+  HIPC(hipSetDevice(c->device));
+  pa_xchg* X = new pa_xchg();
+  X->ctx = c;
+  auto take = [&](int32_t n, const int32_t* parts, const int32_t* ptrs, const int32_t* lids,
+                  std::vector<int32_t>& P, std::vector<int64_t>& O, std::vector<int32_t>& Lh) -> int {
+    P.assign(parts, parts + n);
+    O.resize(n + 1);
+    for (int32_t i = 0; i <= n; ++i) O[i] = (int64_t)(n == 0 && i == 0 ? 1 : ptrs[i]) - 1;
+    for (int32_t i = 0; i < n; ++i) {
+      if (P[i] < 1 || P[i] > c->nparts) PA_FAIL("exchanger: part id out of range");
+      if (O[i + 1] < O[i]) PA_FAIL("exchanger: ptrs not non-decreasing");
+    }
+    if (O[0] != 0) PA_FAIL("exchanger: ptrs[1] must be 1");
+    Lh.resize(O[n]);
+    for (int64_t p = 0; p < O[n]; ++p) {
+      if (lids[p] < 1) PA_FAIL("exchanger: lids must be >= 1");
+      Lh[p] = lids[p] - 1;
+    }
+    return 0;
+  };
+  std::vector<int32_t> hr, hs;
+  if (take(n_rcv, parts_rcv, ptrs_rcv, lids_rcv, X->parts_rcv, X->ptrs_rcv, hr) ||
+      take(n_snd, parts_snd, ptrs_snd, lids_snd, X->parts_snd, X->ptrs_snd, hs)) {
+    delete X;
+    return -1;
+  }
+  for (int32_t l : hr) X->max_lid = std::max<int64_t>(X->max_lid, l);
+  for (int32_t l : hs) X->max_lid = std::max<int64_t>(X->max_lid, l);
+  X->n_rcv_data = (int64_t)hr.size();
+  X->n_snd_data = (int64_t)hs.size();
+  if (dev_upload(&X->d_lids_rcv, hr) || dev_upload(&X->d_lids_snd, hs)) { delete X; return -1; }
+  if (X->n_rcv_data) HIPC(hipMalloc(&X->d_buf_rcv, X->n_rcv_data * 16));
+  if (X->n_snd_data) HIPC(hipMalloc(&X->d_buf_snd, X->n_snd_data * 16));
+  if (build_plan(hr, &X->plan_fwd) || build_plan(hs, &X->plan_rev)) { delete X; return -1; }
+  *out = X;
+  return 0;
+}
+
+int pa_xchg_destroy(pa_xchg* X) {
+  if (!X) return 0;
+  (void)hipSetDevice(X->ctx->device);
+  dev_free(X->d_lids_rcv);
+  dev_free(X->d_lids_snd);
+  dev_free(X->d_buf_rcv);
+  dev_free(X->d_buf_snd);
+  free_plan(X->plan_fwd);
+  free_plan(X->plan_rev);
+  delete X;
+  return 0;
+}
+
+// ---------------------------------------------------------------------------
+int pa_vec_create(pa_ctx* c, int dtype, int64_t n, pa_vec** out) {
+  CHECK_ARG(c && out, "null argument");
+  CHECK_ARG(valid_dtype(dtype), "invalid dtype");
+  CHECK_ARG(n >= 0, "negative length");
+  HIPC(hipSetDevice(c->device));
+  pa_vec* v = new pa_vec();
+  v->ctx = c;
+  v->dtype = dtype;
+  v->n = n;
+  if (n) {
+    hipError_t e = hipMalloc(&v->d, (size_t)n * dtype_size(dtype));
+    if (e != hipSuccess) { delete v; PA_FAIL(std::string("hipMalloc(vector) failed: ") + hipGetErrorString(e)); }
+    HIPC(hipMemsetAsync(v->d, 0, (size_t)n * dtype_size(dtype), c->s_main));
+  }
+  *out = v;
+  return 0;
+}
+
+int pa_vec_destroy(pa_vec* v) {
+  if (!v) return 0;
+  (void)hipSetDevice(v->ctx->device);
+  (void)hipStreamSynchronize(v->ctx->s_main);
+  dev_free(v->d);
+  delete v;
+  return 0;
+}
+
+int pa_vec_upload(pa_vec* v, const void* host, int64_t n) {
+  CHECK_ARG(v && (host || n == 0), "null argument");
+  CHECK_ARG(n == v->n, "upload length differs from vector length");
+  HIPC(hipSetDevice(v->ctx->device));
+  if (n) {
+    HIPC(hipMemcpyAsync(v->d, host, (size_t)n * dtype_size(v->dtype), hipMemcpyHostToDevice, v->ctx->s_main));
+    HIPC(hipStreamSynchronize(v->ctx->s_main));
+  }
+  return 0;
+}
+
+int pa_vec_download(const pa_vec* v, void* host, int64_t n) {
+  CHECK_ARG(v && (host || n == 0), "null argument");
+  CHECK_ARG(n == v->n, "download length differs from vector length");
+  HIPC(hipSetDevice(v->ctx->device));
+  if (n) {
+    HIPC(hipStreamSynchronize(v->ctx->s_comm));
+    HIPC(hipMemcpyAsync(host, v->d, (size_t)n * dtype_size(v->dtype), hipMemcpyDeviceToHost, v->ctx->s_main));
+    HIPC(hipStreamSynchronize(v->ctx->s_main));
+  }
+  return 0;
+}
+
+int pa_vec_fill(pa_vec* v, const void* s) {
+  CHECK_ARG(v && s, "null argument");
+  HIPC(hipSetDevice(v->ctx->device));
+  launch_fill(v->dtype, v->n, 0, nullptr, v->d, s, v->ctx->s_main);
+  HIPC(hipGetLastError());
+  return 0;
+}
+
+int pa_vec_copy(pa_vec* d, const pa_index* id, const pa_vec* s, const pa_index* is, int same_layout) {
+  CHECK_ARG(d && s, "null argument");
+  CHECK_ARG(d->dtype == s->dtype, "copyto!: element types differ");
+  CHECK_ARG(d->ctx == s->ctx, "copyto!: vectors of different parts");
+  HIPC(hipSetDevice(d->ctx->device));
+  if (same_layout) {
+    CHECK_ARG(d->n == s->n, "copyto!: lengths differ");
+    if (d->n) HIPC(hipMemcpyAsync(d->d, s->d, (size_t)d->n * dtype_size(d->dtype), hipMemcpyDeviceToDevice, d->ctx->s_main));
+    return 0;
+  }
+  CHECK_ARG(id && is, "copyto! across partitions needs both index sets");
+  CHECK_ARG(id->noids == is->noids, "copyto!: owned counts differ (oids_are_equal)");
+  launch_copy(d->dtype, id->noids, id->d_oid_to_lid, d->d, is->d_oid_to_lid, s->d, d->ctx->s_main);
+  HIPC(hipGetLastError());
+  return 0;
+}
+
+int pa_vec_axpby(pa_vec* y, const pa_vec* x, const pa_index* idx, const void* a, int mode, int all_lids) {
+  CHECK_ARG(y && a, "null argument");
+  CHECK_ARG(mode >= 0 && mode <= 4, "invalid axpby mode");
+  CHECK_ARG(mode == 4 || (x && x->dtype == y->dtype && x->n == y->n), "axpby: x must match y");
+  HIPC(hipSetDevice(y->ctx->device));
+  if (all_lids) {
+    launch_axpby(y->dtype, y->n, nullptr, y->d, x ? x->d : nullptr, a, mode, y->ctx->s_main);
+  } else {
+    CHECK_ARG(idx && idx->nlids == y->n, "axpby over owned values needs the vector's index set");
+    launch_axpby(y->dtype, idx->noids, idx->d_oid_to_lid, y->d, x ? x->d : nullptr, a, mode, y->ctx->s_main);
+  }
+  HIPC(hipGetLastError());
+  return 0;
+}
+
+// ---------------------------------------------------------------------------
+// CSC → owned-row SELL (one time, host side).  Loop order is the reference's
+// (SparseUtils.jl:176-185 over owned_owned then owned_ghost): columns in oid
+// order, then in hid order; each row's entries are appended in that order.
+int pa_mat_from_csc(pa_ctx* c, int dtype, int index_bytes, int64_t nrows_lids, int64_t ncols_lids,
+                    const void* colptr, const void* rowval, const void* nzval, const pa_index* rows,
+                    const pa_index* cols, pa_mat** out) {
+  CHECK_ARG(c && out && rows && cols, "null argument");
+  CHECK_ARG(valid_dtype(dtype), "invalid dtype");
+  CHECK_ARG(index_bytes == 4 || index_bytes == 8, "index_bytes must be 4 or 8");
+  CHECK_ARG(rows->nlids == nrows_lids && cols->nlids == ncols_lids,
+            "matrix size must be num_lids(rows) x num_lids(cols) (DimensionMismatch)");
+  HIPC(hipSetDevice(c->device));
+  auto cp = [&](int64_t j) -> int64_t {
+    return index_bytes == 8 ? ((const int64_t*)colptr)[j] : ((const int32_t*)colptr)[j];
+  };
+  auto rv = [&](int64_t p) -> int64_t {
+    return index_bytes == 8 ? ((const int64_t*)rowval)[p] : ((const int32_t*)rowval)[p];
+  };
+  const int64_t csc_nnz = ncols_lids > 0 ? cp(ncols_lids) - 1 : 0;
+  CHECK_ARG(csc_nnz >= 0, "colptr[end] must be >= 1");
+  const size_t S = dtype_size(dtype);
+  pa_mat* A = new pa_mat();
+  A->ctx = c;
+  A->dtype = dtype;
+  A->R = sell_rows_per_lane(dtype);
+  A->H = 64 * A->R;
+  A->nrows = rows->noids;
+  A->ncols_lids = ncols_lids;
+  A->csc_nnz = csc_nnz;
+  const int64_t nr = A->nrows;
+  std::vector<int32_t> len(nr, 0);
+  std::vector<char> has_ghost(nr, 0);
+  auto visit = [&](auto&& f) -> int {
+    for (int64_t j = 0; j < cols->noids; ++j) {
+      const int64_t J = cols->h_oid_to_lid[j];
+      for (int64_t p = cp(J) - 1; p < cp(J + 1) - 1; ++p) {
+        const int64_t I = rv(p) - 1;
+        if (I < 0 || I >= nrows_lids) return -1;
+        const int32_t o = rows->h_lid_to_ohid[I];
+        if (o > 0) f(o - 1, J, p, false);
+      }
+    }
+    for (int64_t h = 0; h < cols->nhids; ++h) {
+      const int64_t J = cols->h_hid_to_lid[h];
+      for (int64_t p = cp(J) - 1; p < cp(J + 1) - 1; ++p) {
+        const int64_t I = rv(p) - 1;
+        if (I < 0 || I >= nrows_lids) return -1;
+        const int32_t o = rows->h_lid_to_ohid[I];
+        if (o > 0) f(o - 1, J, p, true);
+      }
+    }
+    return 0;
+  };
+  if (visit([&](int64_t r, int64_t, int64_t, bool g) { ++len[r]; if (g) has_ghost[r] = 1; })) {
+    delete A;
+    PA_FAIL("CSC rowval out of range");
+  }
+  const int64_t ns = (nr + A->H - 1) / A->H;
+  std::vector<int32_t> slen(ns, 0);
+  std::vector<char> sghost(ns, 0);
+  int64_t nnz = 0;
+  for (int64_t r = 0; r < nr; ++r) {
+    slen[r / A->H] = std::max(slen[r / A->H], len[r]);
+    if (has_ghost[r]) sghost[r / A->H] = 1;
+    nnz += len[r];
+  }
+  A->nnz = nnz;
+  std::vector<int64_t> soff;
+  if (finish_sell_layout(A, slen, sghost, &soff)) { pa_mat_destroy(A); return -1; }
+  std::vector<int32_t> hcol(A->slots, -1);
+  std::vector<unsigned char> hval(A->slots * S, 0);
+  A->h_nz_slot.assign(csc_nnz, -1);
+  std::vector<int32_t> cur(nr, 0);
+  const int R = A->R;
+  visit([&](int64_t r, int64_t J, int64_t p, bool) {
+    const int64_t s = r / A->H;
+    const int64_t w = r - s * A->H;
+    const int64_t lane = w / R, rr = w % R;
+    const int64_t slot = soff[s] + ((int64_t)cur[r] * 64 + lane) * R + rr;
+    ++cur[r];
+    hcol[slot] = (int32_t)J;
+    std::memcpy(&hval[slot * S], (const unsigned char*)nzval + p * S, S);
+    A->h_nz_slot[p] = slot;
+  });
+  if (dev_upload(&A->d_col, hcol)) { pa_mat_destroy(A); return -1; }
+  if (A->slots) {
+    HIPC(hipMalloc(&A->d_val, A->slots * S));
+    HIPC(hipMemcpy(A->d_val, hval.data(), A->slots * S, hipMemcpyHostToDevice));
+  }
+  *out = A;
+  return 0;
+}
+
+int pa_mat_set_values(pa_mat* A, const void* nzval) {
+  CHECK_ARG(A && nzval, "null argument");
+  CHECK_ARG((int64_t)A->h_nz_slot.size() == A->csc_nnz, "matrix was not built from a CSC pattern");
+  HIPC(hipSetDevice(A->ctx->device));
+  const size_t S = dtype_size(A->dtype);
+  std::vector<unsigned char> hval(A->slots * S, 0);
+  for (int64_t p = 0; p < A->csc_nnz; ++p) {
+    const int64_t slot = A->h_nz_slot[p];
+    if (slot >= 0) std::memcpy(&hval[slot * S], (const unsigned char*)nzval + p * S, S);
+  }
+  HIPC(hipStreamSynchronize(A->ctx->s_main));
+  if (A->slots) HIPC(hipMemcpy(A->d_val, hval.data(), A->slots * S, hipMemcpyHostToDevice));
+  return 0;
+}
+
+int pa_mat_destroy(pa_mat* A) {
+  if (!A) return 0;
+  (void)hipSetDevice(A->ctx->device);
+  (void)hipStreamSynchronize(A->ctx->s_main);
+  dev_free(A->d_slice_off);
+  dev_free(A->d_slice_len);
+  dev_free(A->d_int_list);
+  dev_free(A->d_bnd_list);
+  dev_free(A->d_col);
+  dev_free(A->d_val);
+  delete A;
+  return 0;
+}
+
+int pa_mat_info(const pa_mat* A, int64_t* nrows, int64_t* nnz, int64_t* slots, int64_t* nslices,
+                int64_t* nslices_int) {
+  CHECK_ARG(A, "null matrix");
+  if (nrows) *nrows = A->nrows;
+  if (nnz) *nnz = A->nnz;
+  if (slots) *slots = A->slots;
+  if (nslices) *nslices = A->nslices;
+  if (nslices_int) *nslices_int = A->nslices_int;
+  return 0;
+}
+
+// ---------------------------------------------------------------------------
+int pa_spmv_all(int n, pa_mat* const A[], pa_vec* const y[], const pa_index* const y_idx[],
+                pa_vec* const x[], const pa_index* const x_idx[], pa_xchg* const xg[],
+                const void* alpha, const void* beta) {
+  CHECK_ARG(n >= 1 && A && y && x && alpha && beta, "null argument");
+  const int dt = A[0]->dtype;
+  bool any_x = false;
+  for (int i = 0; i < n; ++i) {
+    CHECK_ARG(A[i] && y[i] && x[i], "null handle");
+    CHECK_ARG(A[i]->dtype == dt && y[i]->dtype == dt && x[i]->dtype == dt, "mul!: element types differ");
+    CHECK_ARG(x[i]->n == A[i]->ncols_lids, "mul!: length(b.values) != num_lids(a.cols) (DimensionMismatch)");
+    const pa_index* yi = y_idx ? y_idx[i] : nullptr;
+    CHECK_ARG(yi && yi->noids == A[i]->nrows && yi->nlids == y[i]->n,
+              "mul!: c.rows owned ids differ from a.rows (oids_are_equal)");
+    if (x_idx && x_idx[i]) {
+      const pa_index* xi = x_idx[i];
+      CHECK_ARG(xi->nlids == A[i]->ncols_lids, "mul!: b.rows differs from a.cols");
+    }
+    if (xg && xg[i]) any_x = true;
+  }
+  const bool has_alpha = !scalar_is(dt, alpha, 1.0);
+  const int bmode = scalar_is(dt, beta, 0.0) ? 0 : (scalar_is(dt, beta, 1.0) ? 1 : 2);
+
+  if (any_x) {
+    for (int i = 0; i < n; ++i) {
+      CHECK_ARG(xg[i] && xg[i]->ctx == x[i]->ctx, "mul!: exchanger missing for some parts");
+      if (check_lids(xg[i], x[i])) return -1;
+    }
+    if (pre_pack_wait(n, xg)) return -1;
+    for (int i = 0; i < n; ++i) {
+      pa_ctx* c = xg[i]->ctx;
+      HIPC(hipSetDevice(c->device));
+      launch_pack(dt, xg[i]->n_snd_data, xg[i]->d_lids_snd, x[i]->d, xg[i]->d_buf_snd, c->s_main);
+      HIPC(hipEventRecord(c->ev_packed, c->s_main));
+    }
+    if (transport(n, xg, dt, 0)) return -1;
+  }
+  for (int i = 0; i < n; ++i) {
+    pa_ctx* c = A[i]->ctx;
+    HIPC(hipSetDevice(c->device));
+    const int32_t* ymap = y_idx[i]->own_contig ? nullptr : y_idx[i]->d_oid_to_lid;
+    if (c->timing) HIPC(hipEventRecord(c->ev_t[0], c->s_main));
+    // interior slices (no ghost column): overlap with the halo transport
+    if (A[i]->d_int_list)
+      launch_spmv(A[i]->nslices_int, A[i]->d_int_list, A[i], x[i]->d, y[i]->d, ymap, has_alpha, bmode, alpha, beta, c->s_main);
+    else
+      launch_spmv(A[i]->nslices, nullptr, A[i], x[i]->d, y[i]->d, ymap, has_alpha, bmode, alpha, beta, c->s_main);
+    if (c->timing) HIPC(hipEventRecord(c->ev_t[1], c->s_main));
+  }
+  HIPC(hipGetLastError());
+  for (int i = 0; i < n; ++i) {
+    pa_ctx* c = A[i]->ctx;
+    HIPC(hipSetDevice(c->device));
+    if (any_x) {
+      HIPC(hipStreamWaitEvent(c->s_main, c->ev_recvd, 0));
+      launch_unpack(dt, xg[i]->n_rcv_data, xg[i]->d_lids_rcv, xg[i]->plan_fwd, PA_REPLACE,
+                    xg[i]->d_buf_rcv, x[i]->d, c->s_main);
+    }
+    if (c->timing) HIPC(hipEventRecord(c->ev_t[2], c->s_main));
+    if (A[i]->d_bnd_list) {
+      const int32_t* ymap = y_idx[i]->own_contig ? nullptr : y_idx[i]->d_oid_to_lid;
+      launch_spmv(A[i]->nslices - A[i]->nslices_int, A[i]->d_bnd_list, A[i], x[i]->d, y[i]->d, ymap,
+                  has_alpha, bmode, alpha, beta, c->s_main);
+    }
+    if (c->timing) HIPC(hipEventRecord(c->ev_t[3], c->s_main));
+  }
+  HIPC(hipGetLastError());
+  for (int i = 0; i < n; ++i) {
+    pa_ctx* c = A[i]->ctx;
+    if (c->timing) {
+      HIPC(hipEventSynchronize(c->ev_t[3]));
+      HIPC(hipEventElapsedTime(&c->last_int_ms, c->ev_t[0], c->ev_t[1]));
+      HIPC(hipEventElapsedTime(&c->last_bnd_ms, c->ev_t[2], c->ev_t[3]));
+    }
+  }
+  return 0;
+}
+
+int pa_exchange_all(int n, pa_vec* const v[], pa_xchg* const xg[], const pa_index* const idx[], int op,
+                    int reverse, int zero_ghosts) {
+  CHECK_ARG(n >= 1 && v && xg, "null argument");
+  CHECK_ARG(op == PA_REPLACE || op == PA_ADD, "invalid combine op");
+  const int dt = v[0]->dtype;
+  for (int i = 0; i < n; ++i) {
+    CHECK_ARG(v[i] && xg[i], "null handle");
+    CHECK_ARG(v[i]->dtype == dt, "exchange!: element types differ across parts");
+    CHECK_ARG(v[i]->ctx == xg[i]->ctx, "exchange!: vector and exchanger of different parts");
+    if (check_lids(xg[i], v[i])) return -1;
+  }
+  if (pre_pack_wait(n, xg)) return -1;
+  for (int i = 0; i < n; ++i) {
+    pa_xchg* X = xg[i];
+    pa_ctx* c = X->ctx;
+    HIPC(hipSetDevice(c->device));
+    if (!reverse)
+      launch_pack(dt, X->n_snd_data, X->d_lids_snd, v[i]->d, X->d_buf_snd, c->s_main);
+    else
+      launch_pack(dt, X->n_rcv_data, X->d_lids_rcv, v[i]->d, X->d_buf_rcv, c->s_main);
+    HIPC(hipEventRecord(c->ev_packed, c->s_main));
+  }
+  HIPC(hipGetLastError());
+  if (transport(n, xg, dt, reverse ? 1 : 0)) return -1;
+  for (int i = 0; i < n; ++i) {
+    pa_xchg* X = xg[i];
+    pa_ctx* c = X->ctx;
+    HIPC(hipSetDevice(c->device));
+    HIPC(hipStreamWaitEvent(c->s_main, c->ev_recvd, 0));
+    if (!reverse)
+      launch_unpack(dt, X->n_rcv_data, X->d_lids_rcv, X->plan_fwd, op, X->d_buf_rcv, v[i]->d, c->s_main);
+    else
+      launch_unpack(dt, X->n_snd_data, X->d_lids_snd, X->plan_rev, op, X->d_buf_snd, v[i]->d, c->s_main);
+    if (zero_ghosts) {
+      CHECK_ARG(idx && idx[i] && idx[i]->nlids == v[i]->n, "assemble!: index set of the vector required");
+      unsigned char z[16] = {0};
+      launch_fill(dt, idx[i]->nhids, idx[i]->noids, idx[i]->d_hid_to_lid, v[i]->d, z, c->s_main);
+    }
+  }
+  HIPC(hipGetLastError());
+  return 0;
+}
+
+// ---------------------------------------------------------------------------
+namespace {
+
+// kind 0: dot, 1: sum |a|^2, 2: sum a.  Leaves each part's accumulator
+// (double / c128) in host memory `vals` (one per part id 1..P, folded in
+// part order by the caller), covering remote parts through RCCL all-gather.
+int reduce_all(int n, const pa_vec* const a[], const pa_index* const ia[], const pa_vec* const b[],
+               const pa_index* const ib[], int kind, std::vector<c128>* vals) {
+  CHECK_ARG(n >= 1 && a && ia, "null argument");
+  const int dt = a[0]->dtype;
+  const bool cplx = dt == PA_C64 || dt == PA_C128;
+  const int P = a[0]->ctx->nparts;
+  vals->assign(P, c128{0.0, 0.0});
+  std::vector<char> have(P, 0);
+  bool remote_mode = false;
+  for (int i = 0; i < n; ++i) {
+    CHECK_ARG(a[i] && ia[i], "null handle");
+    CHECK_ARG(a[i]->dtype == dt, "element types differ across parts");
+    CHECK_ARG(ia[i]->nlids == a[i]->n, "index set does not describe the vector");
+    if (kind == 0) {
+      CHECK_ARG(b && b[i] && ib && ib[i] && b[i]->dtype == dt && ib[i]->nlids == b[i]->n, "dot: second vector");
+      CHECK_ARG(ia[i]->noids == ib[i]->noids, "dot: owned counts differ");
+    }
+    pa_ctx* c = a[i]->ctx;
+    HIPC(hipSetDevice(c->device));
+    launch_reduce(dt, kind, ia[i]->noids, ia[i]->d_oid_to_lid, a[i]->d,
+                  kind == 0 ? ib[i]->d_oid_to_lid : nullptr, kind == 0 ? b[i]->d : nullptr,
+                  c->d_partials, c->d_result, c->s_main);
+    if (c->comm && n == 1 && P > 1) remote_mode = true;
+  }
+  HIPC(hipGetLastError());
+  const size_t accsz = cplx ? 16 : 8;
+  if (remote_mode) {
+    pa_ctx* c = a[0]->ctx;
+    NCCLC(ncclAllGather(c->d_result, c->d_gather, accsz, ncclUint8, (ncclComm_t)c->comm, c->s_main));
+    HIPC(hipMemcpyAsync(c->h_pinned, c->d_gather, accsz * P, hipMemcpyDeviceToHost, c->s_main));
+    HIPC(hipStreamSynchronize(c->s_main));
+    for (int p = 0; p < P; ++p) {
+      const char* src = (const char*)c->h_pinned + accsz * p;
+      if (cplx) std::memcpy(&(*vals)[p], src, 16);
+      else std::memcpy(&(*vals)[p].re, src, 8);
+      have[p] = 1;
+    }
+  } else {
+    for (int i = 0; i < n; ++i) {
+      pa_ctx* c = a[i]->ctx;
+      HIPC(hipSetDevice(c->device));
+      HIPC(hipMemcpyAsync(c->h_pinned, c->d_result, accsz, hipMemcpyDeviceToHost, c->s_main));
+      HIPC(hipStreamSynchronize(c->s_main));
+      const int p = c->part - 1;
+      if (cplx) std::memcpy(&(*vals)[p], c->h_pinned, 16);
+      else std::memcpy(&(*vals)[p].re, c->h_pinned, 8);
+      have[p] = 1;
+    }
+  }
+  for (int p = 0; p < P; ++p)
+    CHECK_ARG(have[p], "reduction over a subset of the parts: pass every part held by this process, or use one part per process with RCCL");
+  return 0;
+}
+
+}  // namespace
+
+int pa_dot_all(int n, const pa_vec* const a[], const pa_index* const ia[], const pa_vec* const b[],
+               const pa_index* const ib[], void* result) {
+  CHECK_ARG(result, "null result");
+  std::vector<c128> vals;
+  if (reduce_all(n, a, ia, b, ib, 0, &vals)) return -1;
+  // reduce(+, c; init=zero) folded in part order (Interfaces.jl:221-238)
+  c128 s{0.0, 0.0};
+  for (const auto& v : vals) s = s + v;
+  switch (a[0]->dtype) {
+    case PA_F32: *(float*)result = (float)s.re; break;
+    case PA_F64: *(double*)result = s.re; break;
+    case PA_C64: ((float*)result)[0] = (float)s.re; ((float*)result)[1] = (float)s.im; break;
+    case PA_C128: ((double*)result)[0] = s.re; ((double*)result)[1] = s.im; break;
+  }
+  return 0;
+}
+
+int pa_norm2_all(int n, const pa_vec* const a[], const pa_index* const ia[], void* result) {
+  CHECK_ARG(result, "null result");
+  std::vector<c128> vals;
+  if (reduce_all(n, a, ia, nullptr, nullptr, 1, &vals)) return -1;
+  double s = 0.0;
+  for (const auto& v : vals) s = s + v.re;
+  // (…)^(1/p) with p = 2 (Interfaces.jl:1771); Julia promotes to Float64
+  *(double*)result = std::pow(s, 1.0 / 2.0);
+  return 0;
+}
+
+int pa_sum_all(int n, const pa_vec* const a[], const pa_index* const ia[], void* result) {
+  CHECK_ARG(result, "null result");
+  std::vector<c128> vals;
+  if (reduce_all(n, a, ia, nullptr, nullptr, 2, &vals)) return -1;
+  c128 s{0.0, 0.0};
+  for (const auto& v : vals) s = s + v;
+  switch (a[0]->dtype) {
+    case PA_F32: *(float*)result = (float)s.re; break;
+    case PA_F64: *(double*)result = s.re; break;
+    case PA_C64: ((float*)result)[0] = (float)s.re; ((float*)result)[1] = (float)s.im; break;
+    case PA_C128: ((double*)result)[0] = s.re; ((double*)result)[1] = s.im; break;
+  }
+  return 0;
+}
+
+// ---------------------------------------------------------------------------
+// Synthetic Cartesian stencil operator of one part box, built on the device
+// (benchmark driver; equals pa_mat_from_csc of the CSC the oracle's drivers
+// assemble, see tests/test_gpu_parity.py).
+int pa_mat_stencil(pa_ctx* c, int dtype, int kind, const int64_t gdims[3], const int64_t box_lo[3],
+                   const int64_t box_n[3], int64_t nlids_cols, const int32_t* shell_lid,
+                   const double* coeffs, int ncoeffs, pa_mat** out) {
+  CHECK_ARG(c && out && gdims && box_lo && box_n && coeffs, "null argument");
+  CHECK_ARG(valid_dtype(dtype), "invalid dtype");
+  CHECK_ARG(kind == 7 || kind == 27, "kind must be 7 or 27");
+  CHECK_ARG((kind == 7 && ncoeffs == 2) || (kind == 27 && ncoeffs == 64), "coefficient count");
+  for (int d = 0; d < 3; ++d) {
+    CHECK_ARG(gdims[d] >= 2 && box_n[d] >= 1 && box_lo[d] >= 0 && box_lo[d] + box_n[d] <= gdims[d],
+              "box outside the grid");
+  }
+  const int64_t nrows = box_n[0] * box_n[1] * box_n[2];
+  CHECK_ARG(nrows < (int64_t)INT32_MAX && nlids_cols >= nrows && nlids_cols < (int64_t)INT32_MAX, "sizes");
+  HIPC(hipSetDevice(c->device));
+  pa_mat* A = new pa_mat();
+  A->ctx = c;
+  A->dtype = dtype;
+  A->R = sell_rows_per_lane(dtype);
+  A->H = 64 * A->R;
+  A->nrows = nrows;
+  A->ncols_lids = nlids_cols;
+  StencilGeom g;
+  for (int d = 0; d < 3; ++d) { g.N[d] = gdims[d]; g.lo[d] = box_lo[d]; g.n[d] = box_n[d]; }
+  g.kind = kind;
+  const int64_t ns = (nrows + A->H - 1) / A->H;
+  const int64_t ext = (box_n[0] + 2) * (box_n[1] + 2) * (box_n[2] + 2);
+  int32_t *d_shell = nullptr, *d_slen = nullptr, *d_sg = nullptr, *d_err = nullptr;
+  double* d_coef = nullptr;
+  auto cleanup = [&]() { dev_free(d_shell); dev_free(d_slen); dev_free(d_sg); dev_free(d_err); dev_free(d_coef); };
+  if (shell_lid) {
+    HIPC(hipMalloc((void**)&d_shell, ext * 4));
+    HIPC(hipMemcpy(d_shell, shell_lid, ext * 4, hipMemcpyHostToDevice));
+  }
+  HIPC(hipMalloc((void**)&d_coef, ncoeffs * 8));
+  HIPC(hipMemcpy(d_coef, coeffs, ncoeffs * 8, hipMemcpyHostToDevice));
+  HIPC(hipMalloc((void**)&d_slen, std::max<int64_t>(ns, 1) * 4));
+  HIPC(hipMalloc((void**)&d_sg, std::max<int64_t>(ns, 1) * 4));
+  HIPC(hipMalloc((void**)&d_err, 4));
+  HIPC(hipMemset(d_slen, 0, std::max<int64_t>(ns, 1) * 4));
+  HIPC(hipMemset(d_sg, 0, std::max<int64_t>(ns, 1) * 4));
+  HIPC(hipMemset(d_err, 0, 4));
+  launch_stencil_count(g, d_shell, d_coef, nrows, (int)nrows, A->H, d_slen, d_sg, d_err, c->s_main);
+  HIPC(hipGetLastError());
+  HIPC(hipStreamSynchronize(c->s_main));
+  std::vector<int32_t> slen(ns), sg(ns);
+  int32_t herr = 0;
+  HIPC(hipMemcpy(slen.data(), d_slen, ns * 4, hipMemcpyDeviceToHost));
+  HIPC(hipMemcpy(sg.data(), d_sg, ns * 4, hipMemcpyDeviceToHost));
+  HIPC(hipMemcpy(&herr, d_err, 4, hipMemcpyDeviceToHost));
+  if (herr) { cleanup(); delete A; PA_FAIL("stencil: a neighbour inside the domain has no lid (ghost shell table incomplete)"); }
+  std::vector<char> sghost(ns);
+  for (int64_t s = 0; s < ns; ++s) sghost[s] = sg[s] != 0;
+  if (finish_sell_layout(A, slen, sghost, nullptr)) { cleanup(); pa_mat_destroy(A); return -1; }
+  const size_t S = dtype_size(dtype);
+  int64_t nnz_owned = 0;
+  (void)nnz_owned;
+  hipError_t e1 = hipMalloc((void**)&A->d_col, std::max<int64_t>(A->slots, 1) * 4);
+  hipError_t e2 = hipMalloc(&A->d_val, std::max<int64_t>(A->slots, 1) * S);
+  if (e1 != hipSuccess || e2 != hipSuccess) { cleanup(); pa_mat_destroy(A); PA_FAIL("hipMalloc(matrix) failed: out of device memory"); }
+  launch_stencil_fill(g, d_shell, d_coef, nrows, (int)nrows, A, d_err, c->s_main);
+  HIPC(hipGetLastError());
+  HIPC(hipStreamSynchronize(c->s_main));
+  cleanup();
+  // owned nnz: count from the structure (interior rows kind, boundary 1)
+  int64_t nnz = 0;
+  {
+    // rows with Dirichlet status have 1 entry, others `kind`
+    int64_t inner = 1;
+    for (int d = 0; d < 3; ++d) {
+      const int64_t lo = std::max<int64_t>(box_lo[d], 1), hi = std::min<int64_t>(box_lo[d] + box_n[d], gdims[d] - 1);
+      inner *= std::max<int64_t>(0, hi - lo);
+    }
+    nnz = inner * kind + (nrows - inner);
+  }
+  A->nnz = nnz;
+  *out = A;
+  return 0;
+}
+
+}  // extern "C"

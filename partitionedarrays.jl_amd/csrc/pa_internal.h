@@ -1,0 +1,172 @@
+// pa_internal.h — shared types of libpa_hip.so (host API + kernels).
+//
+// Element types follow Julia's arithmetic exactly (no FMA contraction: the
+// whole library is compiled with -ffp-contract=off).  Complex products are
+// Julia's `*(z::Complex, w::Complex)` = (zr*wr - zi*wi, zr*wi + zi*wr)
+// (base/complex.jl), sums are componentwise.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "../../include/pa_hip.h"
+
+namespace pa {
+
+struct alignas(8) c64 {
+  float re, im;
+};
+struct alignas(16) c128 {
+  double re, im;
+};
+
+__host__ __device__ inline c64 operator+(c64 a, c64 b) { return {a.re + b.re, a.im + b.im}; }
+__host__ __device__ inline c64 operator-(c64 a, c64 b) { return {a.re - b.re, a.im - b.im}; }
+__host__ __device__ inline c64 operator*(c64 a, c64 b) {
+  return {a.re * b.re - a.im * b.im, a.re * b.im + a.im * b.re};
+}
+__host__ __device__ inline c128 operator+(c128 a, c128 b) { return {a.re + b.re, a.im + b.im}; }
+__host__ __device__ inline c128 operator-(c128 a, c128 b) { return {a.re - b.re, a.im - b.im}; }
+__host__ __device__ inline c128 operator*(c128 a, c128 b) {
+  return {a.re * b.re - a.im * b.im, a.re * b.im + a.im * b.re};
+}
+
+template <typename T> struct real_of { using type = T; };
+template <> struct real_of<c64> { using type = float; };
+template <> struct real_of<c128> { using type = double; };
+
+template <typename T> __host__ __device__ inline T zero_of() { return T(0); }
+template <> __host__ __device__ inline c64 zero_of<c64>() { return {0.f, 0.f}; }
+template <> __host__ __device__ inline c128 zero_of<c128>() { return {0.0, 0.0}; }
+
+// conj(a)*b, Julia's dot kernel for one element (LinearAlgebra: dot(x,y) = Σ dot(x_i,y_i))
+__host__ __device__ inline float cdot(float a, float b) { return a * b; }
+__host__ __device__ inline double cdot(double a, double b) { return a * b; }
+__host__ __device__ inline c64 cdot(c64 a, c64 b) { return c64{a.re, -a.im} * b; }
+__host__ __device__ inline c128 cdot(c128 a, c128 b) { return c128{a.re, -a.im} * b; }
+// abs2
+__host__ __device__ inline float abs2(float a) { return a * a; }
+__host__ __device__ inline double abs2(double a) { return a * a; }
+__host__ __device__ inline float abs2(c64 a) { return a.re * a.re + a.im * a.im; }
+__host__ __device__ inline double abs2(c128 a) { return a.re * a.re + a.im * a.im; }
+
+inline size_t dtype_size(int dt) {
+  switch (dt) {
+    case PA_F32: return 4;
+    case PA_F64: return 8;
+    case PA_C64: return 8;
+    case PA_C128: return 16;
+  }
+  return 0;
+}
+
+// Rows per lane of the SELL layout so that one lane's value load is 16 B.
+inline int sell_rows_per_lane(int dt) {
+  switch (dt) {
+    case PA_F32: return 4;
+    case PA_F64: return 2;
+    case PA_C64: return 2;
+    case PA_C128: return 1;
+  }
+  return 1;
+}
+
+void set_error(const std::string& msg);
+
+// Cartesian part box of a synthetic stencil operator (pa_mat_stencil).
+struct StencilGeom {
+  int64_t N[3];   // global nodes per dim
+  int64_t lo[3];  // box origin (0-based global coords)
+  int64_t n[3];   // box extent
+  int kind;       // 7 (test_fdm.jl FD) or 27 (Q1 FE, test_fem_sa.jl pattern)
+};
+
+}  // namespace pa
+
+// ---------------------------------------------------------------------------
+// Opaque handle definitions.
+struct pa_ctx {
+  int device = 0;
+  int part = 1;    // 1-based
+  int nparts = 1;
+  hipStream_t s_main = nullptr;   // compute stream
+  hipStream_t s_comm = nullptr;   // halo transport stream (high priority)
+  void* comm = nullptr;           // ncclComm_t (null: no remote transport)
+  // reduction scratch
+  void* d_partials = nullptr;     // per-block partials (max 16 B each)
+  void* d_result = nullptr;       // 16 B final per-part value
+  void* d_gather = nullptr;       // nparts*16 B gathered partials (RCCL mode)
+  void* h_pinned = nullptr;       // pinned host staging (>= nparts*16 B)
+  // timing
+  bool timing = false;
+  hipEvent_t ev_t[4] = {nullptr, nullptr, nullptr, nullptr};
+  float last_int_ms = 0.f, last_bnd_ms = 0.f;
+  // events for the exchange pipeline
+  hipEvent_t ev_packed = nullptr;
+  hipEvent_t ev_recvd = nullptr;
+};
+
+struct pa_index {
+  pa_ctx* ctx = nullptr;
+  int64_t nlids = 0, noids = 0, nhids = 0;
+  bool own_contig = true;    // oid_to_lid == 0..noids-1 (0-based)
+  bool ghost_contig = true;  // hid_to_lid == noids..nlids-1
+  int32_t* d_oid_to_lid = nullptr;  // 0-based, null when own_contig
+  int32_t* d_hid_to_lid = nullptr;  // 0-based, null when ghost_contig
+  std::vector<int32_t> h_oid_to_lid;  // 0-based host copies
+  std::vector<int32_t> h_hid_to_lid;
+  std::vector<int32_t> h_lid_to_ohid;  // reference's lid_to_ohid (1-based ±)
+};
+
+// Ordered combine plan: for each distinct target lid, the buffer positions
+// that land on it, ascending (= the reference's unpack loop order).
+struct pa_combine_plan {
+  int64_t ntargets = 0;
+  bool unique = true;                // every lid at most once → plain scatter
+  int32_t* d_target = nullptr;       // distinct target lids (0-based)
+  int32_t* d_ptr = nullptr;          // ntargets+1
+  int32_t* d_pos = nullptr;          // buffer positions
+};
+
+struct pa_xchg {
+  pa_ctx* ctx = nullptr;
+  std::vector<int32_t> parts_rcv, parts_snd;   // 1-based
+  std::vector<int64_t> ptrs_rcv, ptrs_snd;     // 0-based offsets, size n+1
+  int64_t n_rcv_data = 0, n_snd_data = 0;
+  int64_t max_lid = -1;                        // 0-based, over both lists
+  int32_t* d_lids_rcv = nullptr;               // 0-based
+  int32_t* d_lids_snd = nullptr;
+  void* d_buf_rcv = nullptr;                   // 16 B per slot
+  void* d_buf_snd = nullptr;
+  pa_combine_plan plan_fwd;   // unpack targets = lids_rcv
+  pa_combine_plan plan_rev;   // unpack targets = lids_snd (reverse/assemble)
+};
+
+struct pa_vec {
+  pa_ctx* ctx = nullptr;
+  int dtype = PA_F64;
+  int64_t n = 0;
+  void* d = nullptr;
+};
+
+struct pa_mat {
+  pa_ctx* ctx = nullptr;
+  int dtype = PA_F64;
+  int R = 2;                 // rows per lane
+  int H = 128;               // rows per slice = 64*R
+  int64_t nrows = 0;         // owned rows
+  int64_t ncols_lids = 0;    // x length expected
+  int64_t nnz = 0;           // owned-row nonzeros
+  int64_t slots = 0;         // SELL slots incl. padding
+  int64_t nslices = 0;
+  int64_t nslices_int = 0;   // slices without ghost-column entries
+  int64_t* d_slice_off = nullptr;   // nslices (slot offset of each slice)
+  int32_t* d_slice_len = nullptr;   // nslices (entries per row, max over slice)
+  int32_t* d_int_list = nullptr;    // interior slice ids (null: all interior 0..n-1)
+  int32_t* d_bnd_list = nullptr;    // boundary slice ids
+  int32_t* d_col = nullptr;         // slots, x lid (0-based) or -1 padding
+  void* d_val = nullptr;            // slots
+  std::vector<int64_t> h_nz_slot;   // CSC nz → slot (-1: dropped)
+  int64_t csc_nnz = 0;
+};

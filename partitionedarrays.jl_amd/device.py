@@ -1,0 +1,225 @@
+"""Device objects of the HIP backend: one `PartContext` per part, and cached
+device copies of index sets / exchangers (created once, on first use).
+
+This module is what a Julia `HIPBackend` keeps next to its `AbstractPData`:
+`get_part_ids(HIPBackend(...), nparts)` creates the part contexts.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import sys
+
+import numpy as np
+
+from . import _lib
+from .backends import DistributedBackend, PData, SequentialBackend
+
+
+class PartContext:
+    """pa_ctx: device, streams and scratch of one part."""
+
+    def __init__(self, device: int, part: int, nparts: int):
+        h = C.c_void_p()
+        _lib.call("pa_ctx_create", device, part, nparts, C.byref(h))
+        self.h = h
+        self.device = device
+        self.part = part
+        self.nparts = nparts
+
+    def sync(self):
+        _lib.call("pa_ctx_sync", self.h)
+
+    def set_timing(self, on: bool):
+        _lib.call("pa_ctx_set_timing", self.h, 1 if on else 0)
+
+    def last_kernel_ms(self):
+        a, b = C.c_float(), C.c_float()
+        _lib.call("pa_ctx_last_kernel_ms", self.h, C.byref(a), C.byref(b))
+        return a.value, b.value
+
+    def close(self):
+        """pa_ctx_destroy; every vector/matrix of the part must be gone."""
+        if getattr(self, "h", None) and _lib._lib is not None:
+            _lib._lib.pa_ctx_destroy(self.h)
+            self.h = None
+
+
+class HIPBackend(SequentialBackend):
+    """All parts in this process, part p on device devices[(p-1) % len(devices)]
+    (SequentialBackend semantics, HIP parts)."""
+
+    def __init__(self, devices=None):
+        ndev = _lib.device_count()
+        if ndev == 0:
+            raise _lib.PAError("HIPBackend: no HIP device visible")
+        self.devices = list(devices) if devices is not None else list(range(ndev))
+        self.ctx = {}
+
+    def get_part_ids(self, nparts):
+        ids = super().get_part_ids(nparts)
+        n = ids.num_parts
+        self.ctx = {p: PartContext(self.devices[(p - 1) % len(self.devices)], p, n) for p in ids.part_ids}
+        return ids
+
+    def context(self, part) -> PartContext:
+        return self.ctx[part]
+
+
+class HIPDistributedBackend(DistributedBackend):
+    """One part per process (MPIBackend's role); device = local rank; halo over
+    RCCL.  torch.distributed must be initialised (gloo is enough: it carries
+    the host setup objects and the RCCL unique id)."""
+
+    def __init__(self, device=None, group=None):
+        super().__init__(group)
+        import os
+        self.device = int(os.environ.get("LOCAL_RANK", self.rank)) if device is None else device
+        self.ctx = {}
+
+    def get_part_ids(self, nparts):
+        ids = super().get_part_ids(nparts)
+        n = ids.num_parts
+        part = ids.part_ids[0]
+        c = PartContext(self.device, part, n)
+        if n > 1:
+            buf = C.create_string_buffer(128)
+            if part == 1:
+                _lib.call("pa_comm_unique_id", buf)
+            obj = [bytes(buf.raw) if part == 1 else None]
+            self.dist.broadcast_object_list(obj, src=0, group=self.group)
+            _lib.call("pa_comm_init_rank", c.h, C.c_char_p(obj[0]))
+        self.ctx = {part: c}
+        return ids
+
+    def context(self, part) -> PartContext:
+        return self.ctx[part]
+
+
+def contexts(a: PData):
+    return [a.backend.context(p) for p in a.part_ids]
+
+
+class DeviceIndex:
+    def __init__(self, ctx: PartContext, s):
+        o, op = _lib.i32(s.oid_to_lid)
+        hh, hp = _lib.i32(s.hid_to_lid)
+        h = C.c_void_p()
+        _lib.call("pa_index_create", ctx.h, s.num_lids, s.num_oids, op, s.num_hids, hp, C.byref(h))
+        self.h = h
+
+    def __del__(self):
+        try:
+            if getattr(self, "h", None) and _lib._lib is not None and not sys.is_finalizing():
+                _lib._lib.pa_index_destroy(self.h)
+        except Exception:
+            pass
+
+
+def device_index(ctx: PartContext, s):
+    """cached device copy of IndexSet s on ctx"""
+    key = id(ctx)
+    d = s._device.get(key)
+    if d is None:
+        d = DeviceIndex(ctx, s)
+        s._device[key] = d
+    return d
+
+
+class DeviceExchanger:
+    def __init__(self, ctx: PartContext, parts_rcv, lids_rcv, parts_snd, lids_snd):
+        pr, prp = _lib.i32(parts_rcv)
+        rp, rpp = _lib.i32(lids_rcv.ptrs)
+        rl, rlp = _lib.i32(lids_rcv.data)
+        ps, psp = _lib.i32(parts_snd)
+        sp, spp = _lib.i32(lids_snd.ptrs)
+        sl, slp = _lib.i32(lids_snd.data)
+        h = C.c_void_p()
+        _lib.call("pa_xchg_create", ctx.h, len(pr), prp, rpp, rlp, len(ps), psp, spp, slp, C.byref(h))
+        self.h = h
+
+    def __del__(self):
+        try:
+            if getattr(self, "h", None) and _lib._lib is not None and not sys.is_finalizing():
+                _lib._lib.pa_xchg_destroy(self.h)
+        except Exception:
+            pass
+
+
+def device_exchanger(ctx: PartContext, ex, part):
+    key = (id(ctx), part)
+    d = ex._device.get(key)
+    if d is None:
+        d = DeviceExchanger(ctx, ex.parts_rcv.local(part), ex.lids_rcv.local(part),
+                            ex.parts_snd.local(part), ex.lids_snd.local(part))
+        ex._device[key] = d
+    return d
+
+
+class DeviceVector:
+    """pa_vec: the values of one part of a PVector, in HBM."""
+
+    def __init__(self, ctx: PartContext, dtype, n: int):
+        self.ctx = ctx
+        self.dtype = np.dtype(dtype)
+        self.n = int(n)
+        h = C.c_void_p()
+        _lib.call("pa_vec_create", ctx.h, _lib.DTYPES[self.dtype], self.n, C.byref(h))
+        self.h = h
+
+    def upload(self, a):
+        a = np.ascontiguousarray(a, dtype=self.dtype)
+        if a.shape != (self.n,):
+            raise ValueError(f"upload: expected {self.n} values, got {a.shape}")
+        _lib.call("pa_vec_upload", self.h, a.ctypes.data_as(C.c_void_p), self.n)
+
+    def download(self):
+        a = np.empty(self.n, dtype=self.dtype)
+        _lib.call("pa_vec_download", self.h, a.ctypes.data_as(C.c_void_p), self.n)
+        return a
+
+    def fill(self, v):
+        b, bp = _lib.scalar_buf(v, self.dtype)
+        _lib.call("pa_vec_fill", self.h, bp)
+
+    def __del__(self):
+        try:
+            if getattr(self, "h", None) and _lib._lib is not None and not sys.is_finalizing():
+                _lib._lib.pa_vec_destroy(self.h)
+        except Exception:
+            pass
+
+
+class DeviceMatrix:
+    """pa_mat: one part of a PSparseMatrix in the owned-row SELL layout."""
+
+    def __init__(self, h, ctx: PartContext, dtype):
+        self.h = h
+        self.ctx = ctx
+        self.dtype = np.dtype(dtype)
+
+    @staticmethod
+    def from_csc(ctx: PartContext, csc, rows_idx: DeviceIndex, cols_idx: DeviceIndex, nrows_lids, ncols_lids):
+        colptr = np.ascontiguousarray(csc.colptr, dtype=np.int64)
+        rowval = np.ascontiguousarray(csc.rowval, dtype=np.int64)
+        nzval = np.ascontiguousarray(csc.nzval)
+        h = C.c_void_p()
+        _lib.call("pa_mat_from_csc", ctx.h, _lib.DTYPES[nzval.dtype], 8, nrows_lids, ncols_lids,
+                  colptr.ctypes.data_as(C.c_void_p), rowval.ctypes.data_as(C.c_void_p),
+                  nzval.ctypes.data_as(C.c_void_p), rows_idx.h, cols_idx.h, C.byref(h))
+        return DeviceMatrix(h, ctx, nzval.dtype)
+
+    def set_values(self, nzval):
+        nzval = np.ascontiguousarray(nzval, dtype=self.dtype)
+        _lib.call("pa_mat_set_values", self.h, nzval.ctypes.data_as(C.c_void_p))
+
+    def info(self):
+        v = [C.c_int64() for _ in range(5)]
+        _lib.call("pa_mat_info", self.h, *[C.byref(x) for x in v])
+        return dict(zip(["nrows", "nnz", "slots", "nslices", "nslices_interior"], [x.value for x in v]))
+
+    def __del__(self):
+        try:
+            if getattr(self, "h", None) and _lib._lib is not None and not sys.is_finalizing():
+                _lib._lib.pa_mat_destroy(self.h)
+        except Exception:
+            pass

@@ -1,0 +1,223 @@
+"""Problem drivers: the reference's test problems and the benchmark operators.
+
+* `fdm_problem`  — test_fdm.jl:8-110 (3D 7-point FD Poisson, COO assembly,
+  add_gids, PSparseMatrix(I,J,V,rows,cols; ids=:local)), vectorised.
+* `stencil_partition` / `stencil_operator` — Cartesian part boxes of the 7-pt
+  FD operator and of the 27-pt Q1-hex FE operator (test_fem_sa.jl's pattern
+  in 3D), assembled row-wise as test_fdm.jl does (each part
+  pushes the COO entries of its owned rows, neighbours in lexicographic
+  (z,y,x) order; cols = add_gids(rows, J)).  The partition is computed on the
+  host from the part's face rows; the matrix is generated directly on the
+  device (pa_mat_stencil) in the layout pa_mat_from_csc produces for the
+  assembled CSC — tests/test_gpu_parity.py checks the two are identical.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import _lib
+from .backends import PData, map_parts
+from .device import DeviceMatrix, contexts
+from .prange import (PRange, add_gids, box_of_part, cartesian_gid_to_part, exchanger_from_ids,
+                     linear_index, prange_cartesian, prange_linear, to_lids_)
+from .pvector import PSparseMatrix, PVector
+
+
+# ---------------------------------------------------------------------------
+# test_fdm.jl
+
+FDM_POINTS = [(0, 0, 0), (-1, 0, 0), (1, 0, 0), (0, -1, 0), (0, 1, 0), (0, 0, -1), (0, 0, 1)]
+
+
+def fdm_problem(parts: PData, nx=10, dtype=np.float64):
+    """test_fdm.jl:8-110: returns (A, b, x0, x̂).  u(x) = x₁+x₂, f = 0."""
+    lx = 2.0
+    ns = (nx, nx, nx)
+    n = nx ** 3
+    h = lx / (nx - 1)
+    coeffs = [c / (h * h) for c in (-6, 1, 1, 1, 1, 1, 1)]  # test_fdm.jl:20 (h^2 = h*h)
+    rows = prange_cartesian(parts, ns) if len(parts.shape) == 3 else prange_linear(parts, n)
+
+    def coo(s):
+        gids = s.lid_to_gid[s.oid_to_lid - 1]
+        ci = np.stack([(gids - 1) % nx, ((gids - 1) // nx) % nx, (gids - 1) // (nx * nx)], 1)
+        xi = ci * h
+        uval = xi[:, 0] + xi[:, 1]
+        bnd = np.any((ci == 0) | (ci == nx - 1), axis=1)
+        k = len(gids)
+        Im = np.repeat(s.oid_to_lid.astype(np.int64)[:, None], 7, 1)
+        Jm = np.zeros((k, 7), np.int64)
+        Vm = np.zeros((k, 7))
+        mask = np.zeros((k, 7), bool)
+        Jm[:, 0] = gids
+        Vm[:, 0] = 1.0
+        mask[bnd, 0] = True
+        inner = ~bnd
+        for t, (d, c) in enumerate(zip(FDM_POINTS, coeffs)):
+            cj = ci + np.array(d)
+            Jm[inner, t] = 1 + cj[inner, 0] + nx * cj[inner, 1] + nx * nx * cj[inner, 2]
+            Vm[inner, t] = -c
+            mask[inner, t] = True
+        bv = np.zeros(s.num_lids)
+        xv = np.zeros(s.num_lids)
+        xv[s.oid_to_lid - 1] = uval
+        bv[s.oid_to_lid - 1] = np.where(bnd, uval, 0.0)
+        return Im[mask], Jm[mask], Vm[mask], bv, xv
+    I, J, V, bh, xh = (PData(rows.partition.backend, rows.partition.part_ids, list(t), rows.partition.shape)
+                       for t in zip(*map_parts(coo, rows.partition).parts))
+    cols = add_gids(rows, J)
+    J = to_lids_(J, cols)
+    V = map_parts(lambda v: v.astype(dtype), V)
+    A = PSparseMatrix.from_coo(I, J, V, rows, cols, ids="local")
+    b = PVector.from_host(map_parts(lambda v: v.astype(dtype), bh), rows)
+    x_hat = PVector.from_host(map_parts(lambda v: v.astype(dtype), xh), rows)
+
+    def x0v(s):
+        g = s.lid_to_gid - 1
+        ci = np.stack([g % nx, (g // nx) % nx, g // (nx * nx)], 1)
+        bnd = np.any((ci == 0) | (ci == nx - 1), axis=1)
+        own = s.lid_to_part == s.part
+        xi = ci * h
+        return np.where(bnd & own, xi[:, 0] + xi[:, 1], 0.0).astype(dtype)
+    x0 = PVector.from_host(map_parts(x0v, cols.partition), cols)
+    return A, b, x0, x_hat
+
+
+# ---------------------------------------------------------------------------
+# Cartesian stencil operators (benchmark)
+
+def fd7_coeffs(N, lx=2.0):
+    """test_fdm.jl:18-20,75: stored values −(c/h²): {6/h², −1/h²}"""
+    h = lx / (N - 1)
+    return np.array([-((-6) / (h * h)), -(1 / (h * h))], dtype=np.float64)
+
+
+def q1_hex_ke(h):
+    """h·(K₁⊗M₁⊗M₁ + M₁⊗K₁⊗M₁ + M₁⊗M₁⊗K₁) with K₁=[1 -1;-1 1], M₁=[1/3 1/6;1/6 1/3]
+    (3D analogue of test_fem_sa.jl:17-22), Julia kron order
+    (first factor slowest), evaluated h*((T1+T2)+T3); node e = ex+2ey+4ez."""
+    K1 = [[1.0, -1.0], [-1.0, 1.0]]
+    M1 = [[1.0 / 3.0, 1.0 / 6.0], [1.0 / 6.0, 1.0 / 3.0]]
+    Ke = np.zeros((8, 8))
+    for a in range(8):
+        ax, ay, az = a & 1, (a >> 1) & 1, a >> 2
+        for b in range(8):
+            bx, by, bz = b & 1, (b >> 1) & 1, b >> 2
+            t1 = (K1[az][bz] * M1[ay][by]) * M1[ax][bx]
+            t2 = (M1[az][bz] * K1[ay][by]) * M1[ax][bx]
+            t3 = (M1[az][bz] * M1[ay][by]) * K1[ax][bx]
+            Ke[a, b] = h * ((t1 + t2) + t3)
+    return Ke
+
+
+def stencil_coeffs(kind, N):
+    if kind == 7:
+        return fd7_coeffs(N[0])
+    return q1_hex_ke(2.0 / (N[0] - 1)).ravel()
+
+
+def _offsets(kind):
+    out = []
+    for dz in (-1, 0, 1):
+        for dy in (-1, 0, 1):
+            for dx in (-1, 0, 1):
+                if kind == 7 and (dx != 0) + (dy != 0) + (dz != 0) > 1:
+                    continue
+                out.append((dx, dy, dz))
+    return np.array(out, dtype=np.int64)
+
+
+def _face_ghosts(N, lo, n, kind):
+    """Ghost gids of one part box in first-touch order of the row-wise COO
+    traversal (owned rows in oid order, neighbours lexicographic), i.e. what
+    add_gids!(rows, J) (Interfaces.jl:1515-1533) gives.  Only rows on the box
+    faces can touch ghosts, so only they are traversed."""
+    lo0 = np.array(lo) - 1  # 0-based box origin
+    nn = np.array(n)
+    Nn = np.array(N)
+    axes = [np.arange(k) for k in n]
+    # face rows in ascending oid
+    onface = []
+    for d in range(3):
+        for v in ({0, n[d] - 1}):
+            sl = [slice(None)] * 3
+            sl[2 - d] = v  # meshgrid axes are (z, y, x)
+            onface.append(tuple(sl))
+    mask = np.zeros((n[2], n[1], n[0]), dtype=bool)
+    for sl in onface:
+        mask[sl] = True
+    oids = np.flatnonzero(mask.ravel())  # 0-based oid = x + nx*(y + ny*z)
+    lx = oids % n[0]
+    ly = (oids // n[0]) % n[1]
+    lz = oids // (n[0] * n[1])
+    g = np.stack([lx, ly, lz], 1) + lo0
+    dirichlet = np.any((g == 0) | (g == Nn - 1), axis=1)
+    g = g[~dirichlet]
+    loc = np.stack([lx, ly, lz], 1)[~dirichlet]
+    off = _offsets(kind)
+    nb = g[:, None, :] + off[None, :, :]            # global coords
+    nbl = loc[:, None, :] + off[None, :, :]          # box-local coords
+    outside = np.any((nbl < 0) | (nbl >= nn), axis=2)
+    nbg = nb[outside]                                # row-major = touch order
+    gids = 1 + nbg[:, 0] + N[0] * (nbg[:, 1] + N[1] * nbg[:, 2])
+    u, first = np.unique(gids, return_index=True)
+    return u[np.argsort(first, kind="stable")]
+
+
+def stencil_partition(parts: PData, N: tuple, kind: int):
+    """rows = PRange(parts, N) (Cartesian, Interfaces.jl:1114-1137); cols =
+    rows + ghost layer touched by the stencil rows (first-touch order), with
+    its Exchanger (Interfaces.jl:723-786)."""
+    rows = prange_cartesian(parts, N)
+    cols = rows.copy()
+    g2p = cartesian_gid_to_part(N, parts.shape)
+
+    def add(s):
+        lo, n = box_of_part(N, parts.shape, s.part)
+        gh = _face_ghosts(N, lo, n, kind)
+        s._append_ghosts(gh, g2p(gh))
+        return s
+    map_parts(add, cols.partition)
+    cols.exchanger = exchanger_from_ids(cols.partition)
+    cols.ghost = True
+    return rows, cols
+
+
+def _shell_table(N, lo, n, s):
+    """lid (0-based) of each node of the extended box (one-node shell) that is
+    a ghost of index set s; -1 elsewhere."""
+    if s.num_hids == 0:
+        return None
+    tab = np.full((n[2] + 2) * (n[1] + 2) * (n[0] + 2), -1, dtype=np.int32)
+    gl = s.hid_to_lid.astype(np.int64)
+    g = s.lid_to_gid[gl - 1] - 1
+    gx, gy, gz = g % N[0], (g // N[0]) % N[1], g // (N[0] * N[1])
+    ex = gx - (lo[0] - 1) + 1
+    ey = gy - (lo[1] - 1) + 1
+    ez = gz - (lo[2] - 1) + 1
+    tab[ex + (n[0] + 2) * (ey + (n[1] + 2) * ez)] = (gl - 1).astype(np.int32)
+    return tab
+
+
+def stencil_operator(parts: PData, N: tuple, kind: int, dtype=np.float64, partition=None):
+    """The part-local operators generated on the device (pa_mat_stencil)."""
+    rows, cols = partition if partition is not None else stencil_partition(parts, N, kind)
+    coef = np.ascontiguousarray(stencil_coeffs(kind, N), dtype=np.float64)
+    ctxs = contexts(rows.partition)
+    mats = []
+    for c, s in zip(ctxs, cols.partition.parts):
+        lo, n = box_of_part(N, parts.shape, s.part)
+        tab = _shell_table(N, lo, n, s)
+        gd = (C.c_int64 * 3)(*N)
+        bl = (C.c_int64 * 3)(*[l - 1 for l in lo])
+        bn = (C.c_int64 * 3)(*n)
+        h = C.c_void_p()
+        tp = tab.ctypes.data_as(C.POINTER(C.c_int32)) if tab is not None else None
+        _lib.call("pa_mat_stencil", c.h, _lib.DTYPES[np.dtype(dtype)], kind, gd, bl, bn, s.num_lids, tp,
+                  coef.ctypes.data_as(C.POINTER(C.c_double)), len(coef), C.byref(h))
+        mats.append(DeviceMatrix(h, c, dtype))
+    A = PSparseMatrix(PData(rows.partition.backend, rows.partition.part_ids, mats, rows.partition.shape),
+                      rows, cols)
+    return A

@@ -1,0 +1,347 @@
+"""PVector / PSparseMatrix on HIP parts and the hot path (Interfaces.jl:1576-2757).
+
+Values live in HBM (one pa_vec / pa_mat per part); every operation below is
+a libpa_hip.so call — there is no host fallback.  Host arrays appear only at
+construction (upload of the reference's local CSC / initial values) and when
+the caller asks for them (`to_host`).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import math
+
+import numpy as np
+
+from . import _lib
+from .backends import PData, map_parts
+from .device import (DeviceMatrix, DeviceVector, contexts, device_exchanger, device_index)
+from .prange import PRange, hids_are_equal, oids_are_equal
+
+
+# ---------------------------------------------------------------------------
+# Local CSC (setup): SparseArrays.sparse semantics, SparseUtils.jl:80-94
+
+class CSC:
+    """SparseMatrixCSC{T,Int64}: 1-based colptr/rowval."""
+
+    def __init__(self, m, n, colptr, rowval, nzval):
+        self.m, self.n = int(m), int(n)
+        self.colptr = np.asarray(colptr, dtype=np.int64)
+        self.rowval = np.asarray(rowval, dtype=np.int64)
+        self.nzval = np.asarray(nzval)
+
+    @property
+    def nnz(self):
+        return int(self.colptr[-1] - 1)
+
+
+def compresscoo(I, J, V, m, n) -> CSC:
+    """sparse(I, J, V, m, n, +): duplicates combined with `+` in input order
+    (left fold from the first occurrence), rows ascending within columns."""
+    I = np.asarray(I, dtype=np.int64).ravel()
+    J = np.asarray(J, dtype=np.int64).ravel()
+    V = np.asarray(V).ravel()
+    k = len(I)
+    if k and (I.min() < 1 or I.max() > m or J.min() < 1 or J.max() > n):
+        raise IndexError("compresscoo: index out of bounds")
+    order = np.lexsort((np.arange(k), I, J))
+    Is, Js, Vs = I[order], J[order], V[order]
+    new = np.ones(k, dtype=bool)
+    new[1:] = (Is[1:] != Is[:-1]) | (Js[1:] != Js[:-1])
+    starts = np.flatnonzero(new)
+    sizes = np.diff(np.append(starts, k))
+    acc = Vs[starts].copy()
+    for t in range(1, int(sizes.max()) if k else 1):
+        sel = sizes > t
+        acc[sel] = acc[sel] + Vs[starts[sel] + t]
+    cols = Js[starts]
+    colptr = np.concatenate([[1], 1 + np.cumsum(np.bincount(cols - 1, minlength=n))]).astype(np.int64)
+    return CSC(m, n, colptr, Is[starts], acc)
+
+
+# ---------------------------------------------------------------------------
+# PVector
+
+class PVector:
+    """PVector{T}(values, rows) (Interfaces.jl:1576-1587): values = PData of
+    DeviceVector (num_lids(rows) entries per part)."""
+
+    def __init__(self, values: PData, rows: PRange):
+        self.values = values
+        self.rows = rows
+
+    @property
+    def dtype(self):
+        return self.values.parts[0].dtype if self.values.parts else np.dtype(np.float64)
+
+    def __len__(self):
+        return len(self.rows)
+
+    @staticmethod
+    def undef(rows: PRange, dtype=np.float64) -> "PVector":
+        """PVector{T}(undef, rows) (Interfaces.jl:1869-1878); zero-initialised."""
+        ctxs = contexts(rows.partition)
+        vals = [DeviceVector(c, dtype, s.num_lids) for c, s in zip(ctxs, rows.partition.parts)]
+        return PVector(PData(rows.partition.backend, rows.partition.part_ids, vals, rows.partition.shape), rows)
+
+    @staticmethod
+    def full(v, rows: PRange, dtype=None) -> "PVector":
+        """PVector(v::Number, rows) (Interfaces.jl:1880-1884)"""
+        dtype = dtype or np.asarray(v).dtype
+        a = PVector.undef(rows, dtype)
+        a.fill_(v)
+        return a
+
+    @staticmethod
+    def from_host(host: PData, rows: PRange, dtype=None) -> "PVector":
+        dtype = dtype or np.asarray(host.parts[0]).dtype
+        a = PVector.undef(rows, dtype)
+        for dv, h in zip(a.values.parts, host.parts):
+            dv.upload(h)
+        return a
+
+    def to_host(self) -> PData:
+        return map_parts(lambda v: v.download(), self.values)
+
+    def owned_values(self) -> PData:
+        """owned_values view (Interfaces.jl:1589-1593), as host copies"""
+        return map_parts(lambda v, s: v.download()[s.oid_to_lid - 1], self.values, self.rows.partition)
+
+    def ghost_values(self) -> PData:
+        return map_parts(lambda v, s: v.download()[s.hid_to_lid - 1], self.values, self.rows.partition)
+
+    def similar(self, dtype=None, rows=None) -> "PVector":
+        """similar(a[, T][, axes]) (Interfaces.jl:1615-1633)"""
+        return PVector.undef(rows or self.rows, dtype or self.dtype)
+
+    def fill_(self, v):
+        """fill!(a, v) (Interfaces.jl:1966-1971)"""
+        for dv in self.values.parts:
+            dv.fill(v)
+        return self
+
+    def copy(self) -> "PVector":
+        """copy(b) (Interfaces.jl:1669-1673)"""
+        a = self.similar()
+        copyto_(a, self)
+        return a
+
+
+def _idx(v: PVector):
+    return [device_index(c, s).h for c, s in zip(contexts(v.rows.partition), v.rows.partition.parts)]
+
+
+def copyto_(a: PVector, b: PVector) -> PVector:
+    """copyto!(a, b) (Interfaces.jl:1659-1667): all lids when both share the
+    partition, owned values otherwise."""
+    same = a.rows.partition is b.rows.partition
+    if not same and not oids_are_equal(a.rows, b.rows):
+        raise AssertionError("copyto!: owned ids differ")
+    ia, ib = _idx(a), _idx(b)
+    for da, db, xa, xb in zip(a.values.parts, b.values.parts, ia, ib):
+        _lib.call("pa_vec_copy", da.h, xa, db.h, xb, 1 if same else 0)
+    return a
+
+
+def _bcast(y: PVector, x: PVector, a, mode):
+    all_lids = 1 if (x is None or y.rows is x.rows) else 0
+    if x is not None and not all_lids and not oids_are_equal(y.rows, x.rows):
+        raise AssertionError("broadcast: owned ids differ")
+    iy = _idx(y)
+    buf, bp = _lib.scalar_buf(a if a is not None else 0, y.dtype)
+    xs = x.values.parts if x is not None else [None] * len(y.values.parts)
+    for dy, dx, i in zip(y.values.parts, xs, iy):
+        _lib.call("pa_vec_axpby", dy.h, dx.h if dx is not None else None, i, bp, mode, all_lids)
+    return y
+
+
+def xpby_(u: PVector, r: PVector, beta):
+    """u .= r .+ β .* u"""
+    return _bcast(u, r, beta, 0)
+
+
+def axpy_(x: PVector, alpha, u: PVector):
+    """x .+= α .* u"""
+    return _bcast(x, u, alpha, 1)
+
+
+def axmy_(r: PVector, alpha, c: PVector):
+    """r .-= α .* c"""
+    return _bcast(r, c, alpha, 2)
+
+
+def sub_(r: PVector, c: PVector):
+    """r .-= c"""
+    return _bcast(r, c, None, 3)
+
+
+def rmul_(a: PVector, v):
+    """rmul!(a, v) (Interfaces.jl:1675-1680)"""
+    return _bcast(a, None, v, 4)
+
+
+def _hs(objs):
+    return _lib.ptr_array([o.h if o is not None else None for o in objs])
+
+
+def exchange_(v: PVector) -> PVector:
+    """exchange!(v) (Interfaces.jl:453-458, 2071-2075): owner → ghost values."""
+    ctxs = contexts(v.values)
+    xg = [device_exchanger(c, v.rows.exchanger, p) for c, p in zip(ctxs, v.values.part_ids)]
+    n = len(ctxs)
+    _lib.call("pa_exchange_all", n, _hs(v.values.parts), _hs(xg), _lib.ptr_array(_idx(v)),
+              _lib.PA_REPLACE, 0, 0)
+    return v
+
+
+def assemble_(v: PVector) -> PVector:
+    """assemble!(v) (Interfaces.jl:2084-2106): ghost values added to their
+    owners (reverse exchanger, `+`), then ghost values set to zero."""
+    ctxs = contexts(v.values)
+    xg = [device_exchanger(c, v.rows.exchanger, p) for c, p in zip(ctxs, v.values.part_ids)]
+    _lib.call("pa_exchange_all", len(ctxs), _hs(v.values.parts), _hs(xg), _lib.ptr_array(_idx(v)),
+              _lib.PA_ADD, 1, 1)
+    return v
+
+
+def _scalar_out(dtype):
+    return np.zeros(1, dtype=dtype)
+
+
+def dot(a: PVector, b: PVector):
+    """dot(a, b) (Interfaces.jl:1985-1992)"""
+    out = _scalar_out(a.dtype)
+    n = len(a.values.parts)
+    _lib.call("pa_dot_all", n, _hs(a.values.parts), _lib.ptr_array(_idx(a)), _hs(b.values.parts),
+              _lib.ptr_array(_idx(b)), out.ctypes.data_as(C.c_void_p))
+    return out[0].item()
+
+
+def norm(a: PVector, p=2):
+    """norm(a, 2) (Interfaces.jl:1767-1772)"""
+    if p != 2:
+        raise NotImplementedError("norm(a, p) on HIP parts: p = 2 only")
+    out = np.zeros(1, dtype=np.float64)
+    _lib.call("pa_norm2_all", len(a.values.parts), _hs(a.values.parts), _lib.ptr_array(_idx(a)),
+              out.ctypes.data_as(C.c_void_p))
+    return float(out[0])
+
+
+def psum(a: PVector):
+    """sum(a) (Interfaces.jl:1981-1983)"""
+    out = _scalar_out(a.dtype)
+    _lib.call("pa_sum_all", len(a.values.parts), _hs(a.values.parts), _lib.ptr_array(_idx(a)),
+              out.ctypes.data_as(C.c_void_p))
+    return out[0].item()
+
+
+# ---------------------------------------------------------------------------
+# PSparseMatrix
+
+class PSparseMatrix:
+    """PSparseMatrix(values, rows, cols) (Interfaces.jl:2108-2125): values =
+    PData of DeviceMatrix (owned rows in the SELL layout)."""
+
+    def __init__(self, values: PData, rows: PRange, cols: PRange):
+        self.values = values
+        self.rows = rows
+        self.cols = cols
+
+    @property
+    def dtype(self):
+        return self.values.parts[0].dtype
+
+    @property
+    def shape(self):
+        return (len(self.rows), len(self.cols))
+
+    @staticmethod
+    def from_csc(csc: PData, rows: PRange, cols: PRange) -> "PSparseMatrix":
+        """From each part's local SparseMatrixCSC (num_lids(rows) × num_lids(cols))."""
+        ctxs = contexts(rows.partition)
+        mats = []
+        for c, A, r, s in zip(ctxs, csc.parts, rows.partition.parts, cols.partition.parts):
+            mats.append(DeviceMatrix.from_csc(c, A, device_index(c, r), device_index(c, s),
+                                              r.num_lids, s.num_lids))
+        return PSparseMatrix(PData(rows.partition.backend, rows.partition.part_ids, mats,
+                                   rows.partition.shape), rows, cols)
+
+    @staticmethod
+    def from_coo(I: PData, J: PData, V: PData, rows: PRange, cols: PRange, ids="local"):
+        """PSparseMatrix(I, J, V, rows, cols; ids) (Interfaces.jl:2194-2215, sparse init)"""
+        if ids == "global":
+            I = map_parts(lambda i, s: s.to_lids(i), I, rows.partition)
+            J = map_parts(lambda j, s: s.to_lids(j), J, cols.partition)
+        csc = map_parts(lambda i, j, v, r, s: compresscoo(i, j, v, r.num_lids, s.num_lids),
+                        I, J, V, rows.partition, cols.partition)
+        return PSparseMatrix.from_csc(csc, rows, cols)
+
+    def info(self):
+        return map_parts(lambda m: m.info(), self.values)
+
+
+def mul_(c: PVector, a: PSparseMatrix, b: PVector, alpha=1.0, beta=0.0) -> PVector:
+    """mul!(c, a, b, α, β) (Interfaces.jl:2246-2275): halo exchange of b
+    overlapped with the interior slices, then the slices reading ghosts."""
+    if not (c.rows is a.rows or oids_are_equal(c.rows, a.rows)):
+        raise AssertionError("mul!: c.rows and a.rows own different ids")
+    if not (b.rows is a.cols or (oids_are_equal(a.cols, b.rows) and hids_are_equal(a.cols, b.rows))):
+        raise AssertionError("mul!: b.rows differs from a.cols")
+    if b.rows is not a.cols:
+        for s, t in zip(a.cols.partition.parts, b.rows.partition.parts):
+            if not (np.array_equal(s.oid_to_lid, t.oid_to_lid) and np.array_equal(s.hid_to_lid, t.hid_to_lid)):
+                raise NotImplementedError("mul!: b.rows must have a.cols' local layout")
+    ctxs = contexts(a.values)
+    n = len(ctxs)
+    ex = b.rows.exchanger
+    has_x = any(len(ex.parts_rcv.local(p)) or len(ex.parts_snd.local(p)) for p in b.values.part_ids)
+    xg = [device_exchanger(cx, ex, p) for cx, p in zip(ctxs, b.values.part_ids)] if has_x else None
+    al, alp = _lib.scalar_buf(alpha, a.dtype)
+    be, bep = _lib.scalar_buf(beta, a.dtype)
+    _lib.call("pa_spmv_all", n, _hs(a.values.parts), _hs(c.values.parts), _lib.ptr_array(_idx(c)),
+              _hs(b.values.parts), _lib.ptr_array(_idx(b)), _hs(xg) if xg else None, alp, bep)
+    return c
+
+
+def matvec(a: PSparseMatrix, b: PVector) -> PVector:
+    """Base.:*(a, b) (Interfaces.jl:2605-2610)"""
+    c = PVector.undef(a.rows, a.dtype)
+    return mul_(c, a, b)
+
+
+def cg_(x: PVector, A: PSparseMatrix, b: PVector, reltol=None, abstol=0.0, maxiter=None,
+        history=None):
+    """IterativeSolvers.cg! (v0.9; caller of the hot path at test_fdm.jl:115,
+    test_fem_sa.jl:135), restated over the device operations:
+    u = zero(x); r, c = similar(x); copyto!(r, b); mul!(c, A, x); r .-= c;
+    residual = norm(r); tol = max(reltol*norm(b), abstol); prev = 1; then per
+    iteration β = res²/prev²; u .= r .+ β.*u; mul!(c, A, u);
+    α = res²/dot(u, c); x .+= α.*u; r .-= α.*c; prev = res; res = norm(r)."""
+    real = np.float32 if x.dtype in (np.float32, np.complex64) else np.float64
+    if reltol is None:
+        reltol = math.sqrt(np.finfo(real).eps)
+    if maxiter is None:
+        maxiter = len(A.cols)
+    u = x.similar().fill_(0)
+    r = x.similar()
+    c = x.similar()
+    copyto_(r, b)
+    mul_(c, A, x)
+    sub_(r, c)
+    residual = norm(r)
+    tol = max(reltol * norm(b), abstol)
+    prev = 1.0
+    it = 0
+    while not (it >= maxiter or residual <= tol):
+        beta = residual ** 2 / prev ** 2
+        xpby_(u, r, beta)
+        mul_(c, A, u)
+        alpha = residual ** 2 / dot(u, c)
+        axpy_(x, alpha, u)
+        axmy_(r, alpha, c)
+        prev = residual
+        residual = norm(r)
+        it += 1
+        if history is not None:
+            history.append(residual)
+    return x
