@@ -756,9 +756,10 @@ int pa_spmv_all(int n, pa_mat* const A[], pa_vec* const y[], const pa_index* con
     const int32_t* ymap = y_idx[i]->own_contig ? nullptr : y_idx[i]->d_oid_to_lid;
     if (c->timing) HIPC(hipEventRecord(c->ev_t[0], c->s_main));
     // interior slices (no ghost column): overlap with the halo transport
-    if (A[i]->d_int_list)
-      launch_spmv(A[i]->nslices_int, A[i]->d_int_list, A[i], x[i]->d, y[i]->d, ymap, has_alpha, bmode, alpha, beta, c->s_main);
-    else
+    if (A[i]->d_bnd_list) {  // split layout (the interior list may be empty)
+      if (A[i]->nslices_int > 0)
+        launch_spmv(A[i]->nslices_int, A[i]->d_int_list, A[i], x[i]->d, y[i]->d, ymap, has_alpha, bmode, alpha, beta, c->s_main);
+    } else
       launch_spmv(A[i]->nslices, nullptr, A[i], x[i]->d, y[i]->d, ymap, has_alpha, bmode, alpha, beta, c->s_main);
     if (c->timing) HIPC(hipEventRecord(c->ev_t[1], c->s_main));
   }
