@@ -46,6 +46,11 @@ const char* pa_last_error(void);
 int pa_version(void);
 /* number of visible HIP devices (0 when no GPU). */
 int pa_device_count(int* count);
+/* Process-wide kernel tuning knobs (performance only, results unchanged):
+ * "spmv_flags"  bit 0: non-temporal value/column streams, bit 1: XCD-aware
+ *               slice mapping (default 1);
+ * "spmv_unroll" 4 or 8 entries in flight per lane (default 8).          */
+int pa_tune(const char* key, int value, int* previous);
 
 /* ---- part context ------------------------------------------------------
  * One context per part: its device, its streams, its scratch.

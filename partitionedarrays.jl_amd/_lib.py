@@ -34,6 +34,7 @@ _i64p = C.POINTER(C.c_int64)
 _SIGS = {
     "pa_version": [],
     "pa_device_count": [C.POINTER(C.c_int)],
+    "pa_tune": [C.c_char_p, C.c_int, C.POINTER(C.c_int)],
     "pa_ctx_create": [C.c_int, C.c_int, C.c_int, C.POINTER(_p)],
     "pa_ctx_destroy": [_p],
     "pa_ctx_sync": [_p],
@@ -110,6 +111,13 @@ def device_count() -> int:
     n = C.c_int(0)
     call("pa_device_count", C.byref(n))
     return n.value
+
+
+def tune(key: str, value: int) -> int:
+    """pa_tune: set a process-wide kernel knob, return the previous value."""
+    prev = C.c_int(0)
+    call("pa_tune", key.encode(), int(value), C.byref(prev))
+    return prev.value
 
 
 def i32(a):

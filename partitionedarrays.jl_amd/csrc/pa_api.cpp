@@ -41,6 +41,8 @@ void launch_stencil_count(const StencilGeom& g, const int32_t* shell, const doub
                           int32_t* err, hipStream_t st);
 void launch_stencil_fill(const StencilGeom& g, const int32_t* shell, const double* coef,
                          int64_t nrows, int noids, pa_mat* A, int32_t* err, hipStream_t st);
+extern int g_spmv_flags;
+extern int g_spmv_unroll;
 
 }  // namespace pa
 
@@ -292,6 +294,23 @@ extern "C" {
 
 const char* pa_last_error(void) { return g_err.c_str(); }
 int pa_version(void) { return 1; }
+
+int pa_tune(const char* key, int value, int* previous) {
+  CHECK_ARG(key, "null key");
+  int* slot = nullptr;
+  if (!std::strcmp(key, "spmv_flags")) {
+    CHECK_ARG(value >= 0 && value <= 3, "spmv_flags: bit 0 = non-temporal streams, bit 1 = XCD mapping");
+    slot = &g_spmv_flags;
+  } else if (!std::strcmp(key, "spmv_unroll")) {
+    CHECK_ARG(value == 4 || value == 8, "spmv_unroll must be 4 or 8");
+    slot = &g_spmv_unroll;
+  } else {
+    PA_FAIL(std::string("pa_tune: unknown key ") + key);
+  }
+  if (previous) *previous = *slot;
+  *slot = value;
+  return 0;
+}
 
 int pa_device_count(int* count) {
   int c = 0;

@@ -43,16 +43,83 @@ __device__ inline int64_t xcd_remap(int64_t b, int64_t G) {
 //
 // BMODE: 0 → acc = 0 (β == 0: fill!(co,0)), 1 → acc = y (β == 1),
 //        2 → acc = y*β (rmul!(co,β)).  Interfaces.jl:2262-2263.
-template <typename T, int R, bool ALPHA, int BMODE, bool YMAP, bool LIST>
+// Tuning flags (pa_tune): SPMV_NT — the once-read value/column streams are
+// loaded non-temporally so they do not evict the x planes from L2;
+// SPMV_XCD — XCD-aware slice→block mapping.  U = entries in flight per lane.
+
+enum { SPMV_NT = 1, SPMV_XCD = 2 };
+
+template <int BYTES> struct RawOf;
+template <> struct RawOf<4> { typedef unsigned int type; };
+template <> struct RawOf<8> { typedef unsigned int type __attribute__((ext_vector_type(2))); };
+template <> struct RawOf<16> { typedef unsigned int type __attribute__((ext_vector_type(4))); };
+template <> struct RawOf<32> { typedef unsigned int type __attribute__((ext_vector_type(8))); };
+
+template <bool NT, typename V>
+__device__ __forceinline__ V ld(const V* p) {
+  typedef typename RawOf<sizeof(V)>::type Raw;
+  Raw r;
+  if (NT) r = __builtin_nontemporal_load(reinterpret_cast<const Raw*>(p));
+  else r = *reinterpret_cast<const Raw*>(p);
+  V v;
+  __builtin_memcpy(&v, &r, sizeof(V));
+  return v;
+}
+
+template <typename T, int R, bool ALPHA, bool NT, int U>
+__device__ __forceinline__ void sell_rows(T (&acc)[R], const IPack<R>* __restrict__ cp,
+                                          const Pack<T, R>* __restrict__ vp, int len,
+                                          const T* __restrict__ x, T alpha) {
+  int k = 0;
+  for (; k + U <= len; k += U) {
+    IPack<R> c[U];
+    Pack<T, R> v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) c[u] = ld<NT>(&cp[(k + u) * 64]);
+#pragma unroll
+    for (int u = 0; u < U; ++u) v[u] = ld<NT>(&vp[(k + u) * 64]);
+    T xv[U][R];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const int32_t cc = c[u].c[r];
+        xv[u][r] = x[cc >= 0 ? cc : 0];
+      }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        T xx = xv[u][r];
+        if (ALPHA) xx = xx * alpha;
+        const T t = acc[r] + v[u].v[r] * xx;
+        acc[r] = (c[u].c[r] >= 0) ? t : acc[r];
+      }
+  }
+  for (; k < len; ++k) {
+    const IPack<R> c = ld<NT>(&cp[k * 64]);
+    const Pack<T, R> v = ld<NT>(&vp[k * 64]);
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const int32_t cc = c.c[r];
+      T xx = x[cc >= 0 ? cc : 0];
+      if (ALPHA) xx = xx * alpha;
+      const T t = acc[r] + v.v[r] * xx;
+      acc[r] = (cc >= 0) ? t : acc[r];
+    }
+  }
+}
+
+template <typename T, int R, bool ALPHA, int BMODE, bool YMAP, bool LIST, int U>
 __global__ __launch_bounds__(256) void k_spmv_sell(
     int64_t nwork, const int32_t* __restrict__ list,
     const int64_t* __restrict__ soff, const int32_t* __restrict__ slen,
     const int32_t* __restrict__ col, const T* __restrict__ val,
     const T* __restrict__ x, T* __restrict__ y,
-    const int32_t* __restrict__ ymap, int64_t nrows, T alpha, T beta) {
+    const int32_t* __restrict__ ymap, int64_t nrows, T alpha, T beta, int flags) {
   constexpr int H = 64 * R;
   const int lane = threadIdx.x & 63;
-  const int64_t blk = xcd_remap(blockIdx.x, gridDim.x);
+  const int64_t blk = (flags & SPMV_XCD) ? xcd_remap(blockIdx.x, gridDim.x) : (int64_t)blockIdx.x;
   const int64_t w = blk * 4 + (threadIdx.x >> 6);
   if (w >= nwork) return;
   const int64_t s = LIST ? (int64_t)list[w] : w;
@@ -75,46 +142,8 @@ __global__ __launch_bounds__(256) void k_spmv_sell(
 
   const IPack<R>* __restrict__ cp = reinterpret_cast<const IPack<R>*>(col + off) + lane;
   const Pack<T, R>* __restrict__ vp = reinterpret_cast<const Pack<T, R>*>(val + off) + lane;
-
-  constexpr int U = 4;  // entries in flight per lane per batch
-  int k = 0;
-  for (; k + U <= len; k += U) {
-    IPack<R> c[U];
-    Pack<T, R> v[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) c[u] = cp[(k + u) * 64];
-#pragma unroll
-    for (int u = 0; u < U; ++u) v[u] = vp[(k + u) * 64];
-    T xv[U][R];
-#pragma unroll
-    for (int u = 0; u < U; ++u)
-#pragma unroll
-      for (int r = 0; r < R; ++r) {
-        const int32_t cc = c[u].c[r];
-        xv[u][r] = x[cc >= 0 ? cc : 0];
-      }
-#pragma unroll
-    for (int u = 0; u < U; ++u)
-#pragma unroll
-      for (int r = 0; r < R; ++r) {
-        T xx = xv[u][r];
-        if (ALPHA) xx = xx * alpha;
-        const T t = acc[r] + v[u].v[r] * xx;
-        acc[r] = (c[u].c[r] >= 0) ? t : acc[r];
-      }
-  }
-  for (; k < len; ++k) {
-    const IPack<R> c = cp[k * 64];
-    const Pack<T, R> v = vp[k * 64];
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-      const int32_t cc = c.c[r];
-      T xx = x[cc >= 0 ? cc : 0];
-      if (ALPHA) xx = xx * alpha;
-      const T t = acc[r] + v.v[r] * xx;
-      acc[r] = (cc >= 0) ? t : acc[r];
-    }
-  }
+  if (flags & SPMV_NT) sell_rows<T, R, ALPHA, true, U>(acc, cp, vp, len, x, alpha);
+  else sell_rows<T, R, ALPHA, false, U>(acc, cp, vp, len, x, alpha);
 
   if (!YMAP && row0 + R <= nrows) {
     Pack<T, R> o;
@@ -130,20 +159,34 @@ __global__ __launch_bounds__(256) void k_spmv_sell(
   }
 }
 
-template <typename T, int R, bool ALPHA, int BMODE, bool YMAP>
-static void launch_spmv4(int64_t nwork, const int32_t* list, const pa_mat* A,
+int g_spmv_flags = SPMV_NT;    // pa_tune("spmv_flags"); A/B: profiles/r01_ab_spmv.txt
+int g_spmv_unroll = 8;         // pa_tune("spmv_unroll"): 4 or 8
+
+template <typename T, int R, bool ALPHA, int BMODE, bool YMAP, int U>
+static void launch_spmv5(int64_t nwork, const int32_t* list, const pa_mat* A,
                          const T* x, T* y, const int32_t* ymap, T alpha, T beta,
                          hipStream_t st) {
   const int64_t blocks = (nwork + 3) / 4;
   if (blocks == 0) return;
   if (list)
-    hipLaunchKernelGGL((k_spmv_sell<T, R, ALPHA, BMODE, YMAP, true>), dim3(blocks), dim3(256), 0, st,
+    hipLaunchKernelGGL((k_spmv_sell<T, R, ALPHA, BMODE, YMAP, true, U>), dim3(blocks), dim3(256), 0, st,
                        nwork, list, A->d_slice_off, A->d_slice_len, A->d_col,
-                       (const T*)A->d_val, x, y, ymap, A->nrows, alpha, beta);
+                       (const T*)A->d_val, x, y, ymap, A->nrows, alpha, beta, g_spmv_flags);
   else
-    hipLaunchKernelGGL((k_spmv_sell<T, R, ALPHA, BMODE, YMAP, false>), dim3(blocks), dim3(256), 0, st,
+    hipLaunchKernelGGL((k_spmv_sell<T, R, ALPHA, BMODE, YMAP, false, U>), dim3(blocks), dim3(256), 0, st,
                        nwork, list, A->d_slice_off, A->d_slice_len, A->d_col,
-                       (const T*)A->d_val, x, y, ymap, A->nrows, alpha, beta);
+                       (const T*)A->d_val, x, y, ymap, A->nrows, alpha, beta, g_spmv_flags);
+}
+
+template <typename T, int R, bool ALPHA, int BMODE, bool YMAP>
+static void launch_spmv4(int64_t nwork, const int32_t* list, const pa_mat* A,
+                         const T* x, T* y, const int32_t* ymap, T alpha, T beta,
+                         hipStream_t st) {
+  // the unroll-8 body only for the hot configuration (β == 0, contiguous y)
+  if (g_spmv_unroll == 8 && !ALPHA && BMODE == 0 && !YMAP)
+    launch_spmv5<T, R, ALPHA, BMODE, YMAP, 8>(nwork, list, A, x, y, ymap, alpha, beta, st);
+  else
+    launch_spmv5<T, R, ALPHA, BMODE, YMAP, 4>(nwork, list, A, x, y, ymap, alpha, beta, st);
 }
 
 template <typename T, int R>

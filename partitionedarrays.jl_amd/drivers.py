@@ -32,7 +32,20 @@ FDM_POINTS = [(0, 0, 0), (-1, 0, 0), (1, 0, 0), (0, -1, 0), (0, 1, 0), (0, 0, -1
 
 
 def fdm_problem(parts: PData, nx=10, dtype=np.float64):
-    """test_fdm.jl:8-110: returns (A, b, x0, x̂).  u(x) = x₁+x₂, f = 0."""
+    """test_fdm.jl:8-110 on HIP parts: returns (A, b, x0, x̂) as device objects."""
+    rows, cols, I, J, V, bh, xh, x0h = fdm_host(parts, nx)
+    V = map_parts(lambda v: v.astype(dtype), V)
+    A = PSparseMatrix.from_coo(I, J, V, rows, cols, ids="local")
+    b = PVector.from_host(map_parts(lambda v: v.astype(dtype), bh), rows)
+    x_hat = PVector.from_host(map_parts(lambda v: v.astype(dtype), xh), rows)
+    x0 = PVector.from_host(map_parts(lambda v: v.astype(dtype), x0h), cols)
+    return A, b, x0, x_hat
+
+
+def fdm_host(parts: PData, nx=10):
+    """Host setup of test_fdm.jl:8-110: rows, cols (= add_gids(rows, J)), the
+    COO vectors (I in local row ids, J converted to local col ids) and the
+    host values of b, x̂ (on rows) and x0 (on cols).  u(x) = x₁+x₂, f = 0."""
     lx = 2.0
     ns = (nx, nx, nx)
     n = nx ** 3
@@ -69,10 +82,6 @@ def fdm_problem(parts: PData, nx=10, dtype=np.float64):
                        for t in zip(*map_parts(coo, rows.partition).parts))
     cols = add_gids(rows, J)
     J = to_lids_(J, cols)
-    V = map_parts(lambda v: v.astype(dtype), V)
-    A = PSparseMatrix.from_coo(I, J, V, rows, cols, ids="local")
-    b = PVector.from_host(map_parts(lambda v: v.astype(dtype), bh), rows)
-    x_hat = PVector.from_host(map_parts(lambda v: v.astype(dtype), xh), rows)
 
     def x0v(s):
         g = s.lid_to_gid - 1
@@ -80,9 +89,9 @@ def fdm_problem(parts: PData, nx=10, dtype=np.float64):
         bnd = np.any((ci == 0) | (ci == nx - 1), axis=1)
         own = s.lid_to_part == s.part
         xi = ci * h
-        return np.where(bnd & own, xi[:, 0] + xi[:, 1], 0.0).astype(dtype)
-    x0 = PVector.from_host(map_parts(x0v, cols.partition), cols)
-    return A, b, x0, x_hat
+        return np.where(bnd & own, xi[:, 0] + xi[:, 1], 0.0)
+    x0h = map_parts(x0v, cols.partition)
+    return rows, cols, I, J, V, bh, xh, x0h
 
 
 # ---------------------------------------------------------------------------

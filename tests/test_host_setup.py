@@ -1,0 +1,149 @@
+"""CPU tests of the product's host layer (backends, PRange, Exchanger, COO
+compression, drivers) against the reference's KATs and the oracle."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+GOLD = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "interfaces_kats.json")))
+
+
+def _pd(pamd, parts, vals):
+    return pamd.PData(parts.backend, parts.part_ids, vals, parts.shape)
+
+
+def test_sequential_exchange_kat(pamd):
+    k = GOLD["exchange_scalar"]
+    parts = pamd.sequential.get_part_ids(4)
+    prcv = _pd(pamd, parts, k["parts_rcv"])
+    psnd = _pd(pamd, parts, k["parts_snd"])
+    data = pamd.map_parts(lambda p: [10 * i for i in p], psnd)
+    got = pamd.exchange(data, prcv, psnd)
+    assert got.parts == k["expected_rcv"]
+    assert pamd.preduce(lambda a, b: a + b, parts, 0) == 10
+    assert pamd.xscan_all(lambda a, b: a + b, _pd(pamd, parts, [4, 2, 6, 3]), 1).parts[0] == [1, 5, 7, 13]
+    got = pamd.discover_parts_snd(prcv)
+    assert [list(x) for x in got.parts] == k["parts_snd"]
+
+
+def _kat_partition(pamd, parts):
+    k = GOLD["exchanger"]
+    return _pd(pamd, parts, [pamd.IndexSet(p + 1, k["lid_to_gid"][p], k["lid_to_part"][p]) for p in range(4)])
+
+
+def test_exchanger_kat(pamd):
+    k = GOLD["exchanger"]
+    parts = pamd.sequential.get_part_ids(4)
+    ex = pamd.exchanger_from_ids(_kat_partition(pamd, parts))
+    assert [list(x) for x in ex.parts_snd.parts] == k["expected_parts_snd"]
+    assert [t.tolist() for t in ex.lids_snd.parts] == k["expected_lids_snd"]
+    # neighbour-assisted discover gives the same plan
+    nb = _pd(pamd, parts, [[2, 3, 4], [1, 3, 4], [1, 2, 4], [1, 2, 3]])
+    ex2 = pamd.exchanger_from_ids(_kat_partition(pamd, parts), neighbors=nb)
+    assert [t.tolist() for t in ex2.lids_snd.parts] == k["expected_lids_snd"]
+
+
+def test_exchanger_matches_oracle_random(pamd, O):
+    rng = np.random.default_rng(7)
+    n = 60
+    owner = rng.integers(1, 5, n)
+    for trial in range(3):
+        lists = []
+        for p in range(1, 5):
+            own = [g for g in range(1, n + 1) if owner[g - 1] == p]
+            gh = [int(g) for g in rng.choice(np.arange(1, n + 1), 15, replace=False) if owner[g - 1] != p]
+            lid_to_gid = list(rng.permutation(own + gh))
+            lists.append((lid_to_gid, [int(owner[g - 1]) for g in lid_to_gid]))
+        parts = pamd.sequential.get_part_ids(4)
+        ex = pamd.exchanger_from_ids(_pd(pamd, parts, [pamd.IndexSet(p + 1, *lists[p]) for p in range(4)]))
+        oex = O.exchanger_from_ids(O.PData([O.IndexSet(p + 1, *lists[p]) for p in range(4)]))
+        for p in range(4):
+            assert list(ex.parts_rcv.parts[p]) == list(oex.parts_rcv.parts[p])
+            assert list(ex.parts_snd.parts[p]) == list(oex.parts_snd.parts[p])
+            assert ex.lids_rcv.parts[p].tolist() == oex.lids_rcv.parts[p].tolist()
+            assert ex.lids_snd.parts[p].tolist() == oex.lids_snd.parts[p].tolist()
+
+
+def test_prange_kats(pamd):
+    k = GOLD["prange_noids"]
+    parts = pamd.sequential.get_part_ids(4)
+    r = pamd.prange_noids(parts, _pd(pamd, parts, k["noids"]))
+    assert [s.lid_to_gid.tolist() for s in r.partition.parts] == k["lid_to_gid"]
+    assert r.gid_to_part.parts[0](np.arange(1, 16)).tolist() == k["gid_to_part"]
+    k = GOLD["prange_cartesian"]
+    parts = pamd.sequential.get_part_ids((2, 2))
+    r = pamd.prange_cartesian(parts, (5, 4))
+    assert [s.lid_to_gid.tolist() for s in r.partition.parts] == k["lid_to_gid"]
+    assert r.gid_to_part.parts[0](np.arange(1, 21)).tolist() == k["gid_to_part"]
+    r1 = pamd.prange_linear(pamd.sequential.get_part_ids(3), 10)
+    assert [s.lid_to_gid.tolist() for s in r1.partition.parts] == [[1, 2, 3], [4, 5, 6], [7, 8, 9, 10]]
+
+
+def test_add_gids_first_touch_matches_oracle(pamd, O):
+    rng = np.random.default_rng(3)
+    n = 50
+    parts = pamd.sequential.get_part_ids(4)
+    oparts = O.get_part_ids(4)
+    gids = [list(rng.integers(1, n + 1, 30)) for _ in range(4)]
+    r = pamd.add_gids(pamd.prange_linear(parts, n), _pd(pamd, parts, [np.array(g) for g in gids]))
+    o = O.add_gids(O.prange_linear(oparts, n), O.PData([list(g) for g in gids]))
+    for p in range(4):
+        assert r.partition.parts[p].lid_to_gid.tolist() == o.partition.parts[p].lid_to_gid
+        assert r.partition.parts[p].lid_to_part.tolist() == o.partition.parts[p].lid_to_part
+        assert r.exchanger.lids_snd.parts[p].tolist() == o.exchanger.lids_snd.parts[p].tolist()
+
+
+@pytest.mark.parametrize("dtype", [np.float64, np.float32, np.complex128])
+def test_compresscoo_matches_sparse(pamd, O, dtype):
+    rng = np.random.default_rng(5)
+    m, n, k = 30, 25, 400
+    I = rng.integers(1, m + 1, k)
+    J = rng.integers(1, n + 1, k)
+    V = rng.uniform(-1, 1, k).astype(dtype)
+    if np.dtype(dtype).kind == "c":
+        V = V + 1j * rng.uniform(-1, 1, k)
+    A = pamd.compresscoo(I, J, V, m, n)
+    OV = O.Cx(V.real.copy(), V.imag.copy()) if np.iscomplexobj(V) else V
+    B = O.sparse_csc(I, J, OV, m, n)
+    assert np.array_equal(A.colptr, B.colptr) and np.array_equal(A.rowval, B.rowval)
+    if np.iscomplexobj(V):
+        assert np.array_equal(A.nzval.real, B.nzval.re) and np.array_equal(A.nzval.imag, B.nzval.im)
+    else:
+        assert np.array_equal(A.nzval, B.nzval)
+    k2 = GOLD["sparse_utils"]
+    S = pamd.compresscoo(k2["I"], k2["J"], np.array(k2["V"], float), k2["m"], k2["n"])
+    assert S.nnz == len(k2["dense_nonzeros"])
+
+
+@pytest.mark.parametrize("shape,N,kind", [((2, 2, 1), (12, 10, 9), 27), ((2, 1, 2), (9, 8, 11), 7),
+                                          ((2, 2, 2), (8, 8, 8), 27), ((3, 1, 1), (13, 4, 5), 27)])
+def test_stencil_partition_matches_oracle(pamd, O, shape, N, kind):
+    parts = pamd.sequential.get_part_ids(shape)
+    rows, cols = pamd.drivers.stencil_partition(parts, N, kind)
+    OA = O.stencil_problem(O.get_part_ids(shape), N, kind)
+    for p in parts.part_ids:
+        s, os_ = cols.partition.local(p), OA.cols.partition[p]
+        assert s.lid_to_gid.tolist() == os_.lid_to_gid
+        assert s.lid_to_part.tolist() == os_.lid_to_part
+        ex, oex = cols.exchanger, OA.cols.exchanger
+        assert list(ex.parts_rcv.local(p)) == list(oex.parts_rcv[p])
+        assert list(ex.parts_snd.local(p)) == list(oex.parts_snd[p])
+        assert ex.lids_rcv.local(p).tolist() == oex.lids_rcv[p].tolist()
+        assert ex.lids_snd.local(p).tolist() == oex.lids_snd[p].tolist()
+
+
+@pytest.mark.parametrize("nparts", [4, (2, 2, 2)])
+def test_fdm_host_matches_oracle(pamd, O, nparts):
+    parts = pamd.sequential.get_part_ids(nparts)
+    rows, cols, I, J, V, bh, xh, x0h = pamd.drivers.fdm_host(parts, 10)
+    OA, ob, ox0, oxh = O.fdm_problem(O.get_part_ids(nparts), 10)
+    for p in parts.part_ids:
+        A = pamd.compresscoo(I.local(p), J.local(p), V.local(p), rows.partition.local(p).num_lids,
+                             cols.partition.local(p).num_lids)
+        M = OA.values[p]
+        assert np.array_equal(A.colptr, M.colptr) and np.array_equal(A.rowval, M.rowval)
+        assert np.array_equal(A.nzval, M.nzval)
+        assert np.array_equal(bh.local(p), ob.values[p])
+        assert np.array_equal(xh.local(p), oxh.values[p])
+        assert np.array_equal(x0h.local(p), ox0.values[p])
