@@ -70,10 +70,11 @@ def main():
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group("gloo")
-        backend = pamd.HIPDistributedBackend()
+        backend = pamd.HIPDistributedBackend()      # one part per process, halo over RCCL
+        ngpu = world
     else:
-        backend = pamd.HIPBackend(devices=[0])
-    ngpu = world
+        ngpu = args.gpus
+        backend = pamd.HIPBackend(devices=list(range(ngpu)))  # all parts in this process
     if ngpu not in PART_SHAPES:
         raise SystemExit(f"--gpus must be one of {sorted(PART_SHAPES)}")
     shape = PART_SHAPES[ngpu]
@@ -86,25 +87,31 @@ def main():
     partition = pamd.drivers.stencil_partition(parts, N, args.kind)
     A = pamd.drivers.stencil_operator(parts, N, args.kind, dtype, partition=partition)
     rows, cols = A.rows, A.cols
-    rng = np.random.default_rng(20250114 + rank)
     x = pamd.PVector.from_host(pamd.map_parts(
-        lambda s: rng.uniform(-1, 1, s.num_lids).astype(dtype), cols.partition), cols)
+        lambda s: np.random.default_rng(20250114 + s.part).uniform(-1, 1, s.num_lids).astype(dtype),
+        cols.partition), cols)
     y = pamd.PVector.undef(rows, dtype)
-    ctx = backend.context(parts.part_ids[0])
-    ctx.sync()
+    ctxs = [backend.context(p) for p in parts.part_ids]
+
+    def sync():
+        for c in ctxs:
+            c.sync()
+    sync()
     t_setup = time.perf_counter() - t_setup
 
-    # per-part algorithmic bytes
-    p = parts.part_ids[0]
-    info = A.values.local(p).info()
-    s = cols.partition.local(p)
+    # algorithmic bytes of the local parts
     ex = cols.exchanger
-    n_snd = len(ex.lids_snd.local(p).data)
-    n_rcv = len(ex.lids_rcv.local(p).data)
-    B_part = algorithmic_bytes(info["nnz"], info["nrows"], s.num_hids, n_snd, n_rcv, S)
-    B_all = B_part
+    B_local, infos = 0, {}
+    for p in parts.part_ids:
+        info = A.values.local(p).info()
+        s = cols.partition.local(p)
+        n_snd = len(ex.lids_snd.local(p).data)
+        n_rcv = len(ex.lids_rcv.local(p).data)
+        infos[p] = (info, s.num_hids)
+        B_local += algorithmic_bytes(info["nnz"], info["nrows"], s.num_hids, n_snd, n_rcv, S)
+    B_all = B_local
     if world > 1:
-        t = torch.tensor([float(B_part)], dtype=torch.float64)
+        t = torch.tensor([float(B_local)], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.SUM)
         B_all = float(t.item())
 
@@ -114,13 +121,13 @@ def main():
 
     for _ in range(args.warmup):
         pamd.mul_(y, A, x)
-    ctx.sync()
+    sync()
     barrier()
-    ctx.sync()
+    sync()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         pamd.mul_(y, A, x)
-    ctx.sync()
+    sync()
     t1 = time.perf_counter()
     barrier()
     elapsed = t1 - t0
@@ -131,8 +138,11 @@ def main():
     ms_per_step = 1e3 * elapsed / args.steps
     value = B_all / (elapsed / args.steps) / 1e9
 
-    # roofline: device time of the SpMV kernels measured with HIP events on
-    # the stream they run on (pa_ctx_last_kernel_ms), averaged over K launches
+    # roofline of the first local part: device time of its SpMV kernels, HIP
+    # events on the stream they run on (pa_ctx_last_kernel_ms), mean of K launches
+    p0 = parts.part_ids[0]
+    info, s_nhids = infos[p0]
+    ctx = backend.context(p0)
     ctx.set_timing(True)
     kms = []
     for _ in range(max(5, min(args.steps, 50))):
@@ -140,8 +150,9 @@ def main():
         a_ms, b_ms = ctx.last_kernel_ms()
         kms.append(a_ms + b_ms)
     ctx.set_timing(False)
+    sync()
     kernel_ms = float(np.mean(kms))
-    spmv_bytes = info["nnz"] * (S + 4) + (info["nrows"] + 1) * 4 + (info["nrows"] + s.num_hids) * S + info["nrows"] * S
+    spmv_bytes = info["nnz"] * (S + 4) + (info["nrows"] + 1) * 4 + (info["nrows"] + s_nhids) * S + info["nrows"] * S
     achieved = spmv_bytes / (kernel_ms * 1e-3) / 1e9
 
     line = {
@@ -164,7 +175,8 @@ def main():
             "parts": list(shape),
             "nnz_per_part": info["nnz"],
             "rows_per_part": info["nrows"],
-            "ghosts_per_part": s.num_hids,
+            "ghosts_per_part": s_nhids,
+            "process_model": "one part per process (RCCL halo)" if world > 1 else f"{ngpu} part(s) in one process",
             "bytes_per_step_all_parts": B_all,
             "frac_of_hbm_peak": round(value / (HBM_PEAK_GBS * ngpu), 4),
             "setup_s": round(t_setup, 2),

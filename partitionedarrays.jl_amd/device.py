@@ -73,7 +73,9 @@ class HIPDistributedBackend(DistributedBackend):
     def __init__(self, device=None, group=None):
         super().__init__(group)
         import os
-        self.device = int(os.environ.get("LOCAL_RANK", self.rank)) if device is None else device
+        if device is None:  # local rank, wrapped onto the visible devices
+            device = int(os.environ.get("LOCAL_RANK", self.rank)) % max(1, _lib.device_count())
+        self.device = device
         self.ctx = {}
 
     def get_part_ids(self, nparts):
