@@ -49,7 +49,9 @@ int pa_device_count(int* count);
 /* Process-wide kernel tuning knobs (performance only, results unchanged):
  * "spmv_flags"  bit 0: non-temporal value/column streams, bit 1: XCD-aware
  *               slice mapping (default 1);
- * "spmv_unroll" 4 or 8 entries in flight per lane (default 8).          */
+ * "spmv_unroll" 4 or 8 entries in flight per lane (default 8);
+ * "spmv_format" 1: pattern slices where the matrix has them (default),
+ *               0: int32 column ids everywhere.                          */
 int pa_tune(const char* key, int value, int* previous);
 
 /* ---- part context ------------------------------------------------------
@@ -133,6 +135,12 @@ int pa_mat_destroy(pa_mat* A);
 /* nnz stored on device (padding included) and owned-row nnz. */
 int pa_mat_info(const pa_mat* A, int64_t* nrows_owned, int64_t* nnz_owned,
                 int64_t* slots, int64_t* nslices, int64_t* nslices_interior);
+/* Column encoding chosen at build time: slices whose rows
+ * mostly follow one offset pattern store no column ids ("pattern slices");
+ * their other rows live in a side SELL.                                   */
+int pa_mat_format_info(const pa_mat* A, int64_t* pattern_slices,
+                       int64_t* regular_rows, int64_t* side_rows,
+                       int64_t* side_slots);
 
 /* ---- hot path -----------------------------------------------------------
  * mul!(c, a, b, α, β) (Interfaces.jl:2246-2275) for the n local parts:

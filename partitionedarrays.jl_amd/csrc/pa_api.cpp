@@ -19,10 +19,16 @@ namespace pa {
 static thread_local std::string g_err;
 void set_error(const std::string& msg) { g_err = msg; }
 
-// kernels (pa_kernels.hip)
-void launch_spmv(int64_t nwork, const int32_t* list, const pa_mat* A, const void* x, void* y,
-                 const int32_t* ymap, bool has_alpha, int bmode, const void* alpha,
-                 const void* beta, hipStream_t st);
+// kernels (pa_spmv.hip, pa_kernels.hip)
+void launch_spmv_part(int which, int64_t nwork, const int32_t* list, const pa_mat* A, const void* x,
+                      void* y, const int32_t* ymap, bool has_alpha, int bmode, const void* alpha,
+                      const void* beta, hipStream_t st);
+void launch_pattern_detect(pa_mat* A, int64_t noids, int32_t* kind, int32_t* plen, int32_t* pat,
+                           uint64_t* mask, int32_t* pghost, int32_t* nirreg, hipStream_t st);
+void launch_side_len(pa_mat* A, int64_t n, const int32_t* rows, int32_t* len, int64_t noids,
+                     int32_t* sghost, hipStream_t st);
+void launch_side_fill(pa_mat* A, const int32_t* rows, const int32_t* len, hipStream_t st);
+extern int g_spmv_format;
 void launch_pack(int dtype, int64_t n, const int32_t* lids, const void* v, void* buf,
                  hipStream_t st);
 void launch_unpack(int dtype, int64_t n, const int32_t* lids, const pa_combine_plan& plan, int op,
@@ -160,6 +166,81 @@ int finish_sell_layout(pa_mat* A, const std::vector<int32_t>& slen, const std::v
     if (dev_upload(&A->d_bnd_list, blist)) return -1;
   }
   if (soff_out) *soff_out = std::move(soff);
+  return 0;
+}
+
+// Pattern slices + side SELL from the int32 layout (device detection, host
+// bookkeeping).  noids: owned columns (x lids >= noids are ghosts).
+int finalize_pattern(pa_mat* A, int kmax, int64_t noids) {
+  A->kmax = std::max(kmax, 1);
+  const int64_t ns = A->nslices;
+  if (ns == 0) return 0;
+  hipStream_t st = A->ctx->s_main;
+  const int W = A->H / 64;
+  int32_t *d_pghost = nullptr, *d_nirreg = nullptr;
+  HIPC(hipMalloc((void**)&A->d_kind, ns * 4));
+  HIPC(hipMalloc((void**)&A->d_plen, ns * 4));
+  HIPC(hipMalloc((void**)&A->d_pat, ns * A->kmax * 4));
+  HIPC(hipMalloc((void**)&A->d_mask, ns * W * 8));
+  HIPC(hipMalloc((void**)&d_pghost, ns * 4));
+  HIPC(hipMalloc((void**)&d_nirreg, ns * 4));
+  HIPC(hipMemsetAsync(A->d_mask, 0, ns * W * 8, st));
+  launch_pattern_detect(A, noids, A->d_kind, A->d_plen, A->d_pat, A->d_mask, d_pghost, d_nirreg, st);
+  HIPC(hipGetLastError());
+  std::vector<int32_t> kind(ns), pghost(ns), nirreg(ns);
+  std::vector<uint64_t> mask(ns * W);
+  HIPC(hipMemcpyAsync(kind.data(), A->d_kind, ns * 4, hipMemcpyDeviceToHost, st));
+  HIPC(hipMemcpyAsync(pghost.data(), d_pghost, ns * 4, hipMemcpyDeviceToHost, st));
+  HIPC(hipMemcpyAsync(nirreg.data(), d_nirreg, ns * 4, hipMemcpyDeviceToHost, st));
+  HIPC(hipMemcpyAsync(mask.data(), A->d_mask, ns * W * 8, hipMemcpyDeviceToHost, st));
+  HIPC(hipStreamSynchronize(st));
+  dev_free(d_pghost);
+  dev_free(d_nirreg);
+  std::vector<int32_t> pint, pbnd, side;
+  for (int64_t s = 0; s < ns; ++s) {
+    (pghost[s] ? pbnd : pint).push_back((int32_t)s);
+    if (kind[s]) {
+      ++A->npattern_slices;
+      const int64_t nvalid = std::min<int64_t>(A->H, A->nrows - s * A->H);
+      for (int64_t i = 0; i < nvalid; ++i) {
+        if ((mask[s * W + i / 64] >> (i & 63)) & 1ull) ++A->nregular_rows;
+        else side.push_back((int32_t)(s * A->H + i));
+      }
+    }
+  }
+  A->np_int = (int64_t)pint.size();
+  A->np_bnd = (int64_t)pbnd.size();
+  if (dev_upload(&A->d_pint_list, pint) || dev_upload(&A->d_pbnd_list, pbnd)) return -1;
+  // side SELL
+  A->s_nrows = (int64_t)side.size();
+  if (A->s_nrows > 0) {
+    if (dev_upload(&A->d_s_rowmap, side)) return -1;
+    int32_t* d_dummy = nullptr;
+    A->s_nslices = (A->s_nrows + A->H - 1) / A->H;
+    HIPC(hipMalloc((void**)&A->d_s_rowlen, A->s_nrows * 4));
+    HIPC(hipMalloc((void**)&d_dummy, A->s_nslices * 4));
+    HIPC(hipMemsetAsync(d_dummy, 0, A->s_nslices * 4, st));
+    launch_side_len(A, A->s_nrows, A->d_s_rowmap, A->d_s_rowlen, noids, d_dummy, st);
+    HIPC(hipGetLastError());
+    std::vector<int32_t> rl(A->s_nrows);
+    HIPC(hipMemcpyAsync(rl.data(), A->d_s_rowlen, A->s_nrows * 4, hipMemcpyDeviceToHost, st));
+    HIPC(hipStreamSynchronize(st));
+    dev_free(d_dummy);
+    std::vector<int32_t> slen(A->s_nslices, 0);
+    std::vector<int64_t> soff(A->s_nslices);
+    for (int64_t i = 0; i < A->s_nrows; ++i) slen[i / A->H] = std::max(slen[i / A->H], rl[i]);
+    int64_t acc = 0;
+    for (int64_t s = 0; s < A->s_nslices; ++s) { soff[s] = acc; acc += (int64_t)slen[s] * A->H; }
+    A->s_slots = acc;
+    if (dev_upload(&A->d_s_off, soff) || dev_upload(&A->d_s_len, slen)) return -1;
+    const size_t S = dtype_size(A->dtype);
+    HIPC(hipMalloc((void**)&A->d_s_col, std::max<int64_t>(acc, 1) * 4));
+    HIPC(hipMalloc(&A->d_s_val, std::max<int64_t>(acc, 1) * S));
+    launch_side_fill(A, A->d_s_rowmap, A->d_s_rowlen, st);
+    HIPC(hipGetLastError());
+    HIPC(hipStreamSynchronize(st));
+  }
+  A->has_pat = true;
   return 0;
 }
 
@@ -304,6 +385,9 @@ int pa_tune(const char* key, int value, int* previous) {
   } else if (!std::strcmp(key, "spmv_unroll")) {
     CHECK_ARG(value == 4 || value == 8, "spmv_unroll must be 4 or 8");
     slot = &g_spmv_unroll;
+  } else if (!std::strcmp(key, "spmv_format")) {
+    CHECK_ARG(value == 0 || value == 1, "spmv_format: 0 = int32 columns, 1 = pattern slices");
+    slot = &g_spmv_format;
   } else {
     PA_FAIL(std::string("pa_tune: unknown key ") + key);
   }
@@ -688,6 +772,12 @@ int pa_mat_from_csc(pa_ctx* c, int dtype, int index_bytes, int64_t nrows_lids, i
     HIPC(hipMalloc(&A->d_val, A->slots * S));
     HIPC(hipMemcpy(A->d_val, hval.data(), A->slots * S, hipMemcpyHostToDevice));
   }
+  // pattern slices need "x lid >= noids ⇔ ghost column" (contiguous layout)
+  if (cols->own_contig && cols->ghost_contig) {
+    int kmax = 0;
+    for (int32_t l : slen) kmax = std::max(kmax, l);
+    if (finalize_pattern(A, kmax, cols->noids)) { pa_mat_destroy(A); return -1; }
+  }
   *out = A;
   return 0;
 }
@@ -704,6 +794,11 @@ int pa_mat_set_values(pa_mat* A, const void* nzval) {
   }
   HIPC(hipStreamSynchronize(A->ctx->s_main));
   if (A->slots) HIPC(hipMemcpy(A->d_val, hval.data(), A->slots * S, hipMemcpyHostToDevice));
+  if (A->s_nrows > 0) {  // the side rows carry copies of their values
+    launch_side_fill(A, A->d_s_rowmap, A->d_s_rowlen, A->ctx->s_main);
+    HIPC(hipGetLastError());
+    HIPC(hipStreamSynchronize(A->ctx->s_main));
+  }
   return 0;
 }
 
@@ -717,7 +812,21 @@ int pa_mat_destroy(pa_mat* A) {
   dev_free(A->d_bnd_list);
   dev_free(A->d_col);
   dev_free(A->d_val);
+  for (void* p : {(void*)A->d_kind, (void*)A->d_plen, (void*)A->d_pat, (void*)A->d_mask,
+                  (void*)A->d_pint_list, (void*)A->d_pbnd_list, (void*)A->d_s_off, (void*)A->d_s_len,
+                  (void*)A->d_s_col, A->d_s_val, (void*)A->d_s_rowmap, (void*)A->d_s_rowlen})
+    dev_free(p);
   delete A;
+  return 0;
+}
+
+int pa_mat_format_info(const pa_mat* A, int64_t* pattern_slices, int64_t* regular_rows,
+                       int64_t* side_rows, int64_t* side_slots) {
+  CHECK_ARG(A, "null matrix");
+  if (pattern_slices) *pattern_slices = A->npattern_slices;
+  if (regular_rows) *regular_rows = A->nregular_rows;
+  if (side_rows) *side_rows = A->s_nrows;
+  if (side_slots) *side_slots = A->s_slots;
   return 0;
 }
 
@@ -775,11 +884,14 @@ int pa_spmv_all(int n, pa_mat* const A[], pa_vec* const y[], const pa_index* con
     const int32_t* ymap = y_idx[i]->own_contig ? nullptr : y_idx[i]->d_oid_to_lid;
     if (c->timing) HIPC(hipEventRecord(c->ev_t[0], c->s_main));
     // interior slices (no ghost column): overlap with the halo transport
-    if (A[i]->d_bnd_list) {  // split layout (the interior list may be empty)
+    if (g_spmv_format == 1 && A[i]->has_pat) {
+      launch_spmv_part(0, A[i]->np_int, A[i]->d_pint_list, A[i], x[i]->d, y[i]->d, ymap, has_alpha, bmode, alpha, beta, c->s_main);
+    } else if (A[i]->d_bnd_list) {  // split layout (the interior list may be empty)
       if (A[i]->nslices_int > 0)
-        launch_spmv(A[i]->nslices_int, A[i]->d_int_list, A[i], x[i]->d, y[i]->d, ymap, has_alpha, bmode, alpha, beta, c->s_main);
-    } else
-      launch_spmv(A[i]->nslices, nullptr, A[i], x[i]->d, y[i]->d, ymap, has_alpha, bmode, alpha, beta, c->s_main);
+        launch_spmv_part(1, A[i]->nslices_int, A[i]->d_int_list, A[i], x[i]->d, y[i]->d, ymap, has_alpha, bmode, alpha, beta, c->s_main);
+    } else {
+      launch_spmv_part(1, A[i]->nslices, nullptr, A[i], x[i]->d, y[i]->d, ymap, has_alpha, bmode, alpha, beta, c->s_main);
+    }
     if (c->timing) HIPC(hipEventRecord(c->ev_t[1], c->s_main));
   }
   HIPC(hipGetLastError());
@@ -792,10 +904,14 @@ int pa_spmv_all(int n, pa_mat* const A[], pa_vec* const y[], const pa_index* con
                     xg[i]->d_buf_rcv, x[i]->d, c->s_main);
     }
     if (c->timing) HIPC(hipEventRecord(c->ev_t[2], c->s_main));
-    if (A[i]->d_bnd_list) {
-      const int32_t* ymap = y_idx[i]->own_contig ? nullptr : y_idx[i]->d_oid_to_lid;
-      launch_spmv(A[i]->nslices - A[i]->nslices_int, A[i]->d_bnd_list, A[i], x[i]->d, y[i]->d, ymap,
-                  has_alpha, bmode, alpha, beta, c->s_main);
+    const int32_t* ymap = y_idx[i]->own_contig ? nullptr : y_idx[i]->d_oid_to_lid;
+    if (g_spmv_format == 1 && A[i]->has_pat) {
+      // pattern slices reading ghosts, then the side rows (after the halo)
+      launch_spmv_part(0, A[i]->np_bnd, A[i]->d_pbnd_list, A[i], x[i]->d, y[i]->d, ymap, has_alpha, bmode, alpha, beta, c->s_main);
+      launch_spmv_part(2, A[i]->s_nslices, nullptr, A[i], x[i]->d, y[i]->d, ymap, has_alpha, bmode, alpha, beta, c->s_main);
+    } else if (A[i]->d_bnd_list) {
+      launch_spmv_part(1, A[i]->nslices - A[i]->nslices_int, A[i]->d_bnd_list, A[i], x[i]->d, y[i]->d, ymap,
+                       has_alpha, bmode, alpha, beta, c->s_main);
     }
     if (c->timing) HIPC(hipEventRecord(c->ev_t[3], c->s_main));
   }
@@ -1038,6 +1154,11 @@ int pa_mat_stencil(pa_ctx* c, int dtype, int kind, const int64_t gdims[3], const
     nnz = inner * kind + (nrows - inner);
   }
   A->nnz = nnz;
+  {
+    int kmax = 0;
+    for (int32_t l : slen) kmax = std::max(kmax, l);
+    if (finalize_pattern(A, kmax, nrows)) { pa_mat_destroy(A); return -1; }
+  }
   *out = A;
   return 0;
 }

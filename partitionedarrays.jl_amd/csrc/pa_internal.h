@@ -169,4 +169,27 @@ struct pa_mat {
   void* d_val = nullptr;            // slots
   std::vector<int64_t> h_nz_slot;   // CSC nz → slot (-1: dropped)
   int64_t csc_nnz = 0;
+
+  // Pattern slices (implied columns): in a pattern slice the
+  // rows whose column sequence is `row + pat[k]` (k < plen) are "regular"
+  // (mask bit set) and need no column ids; the other rows of the slice are
+  // computed from the side SELL below.  Values keep their int32-SELL slots.
+  bool has_pat = false;
+  int kmax = 0;                      // pattern stride per slice
+  int32_t* d_kind = nullptr;         // per slice: 1 pattern, 0 int32 columns
+  int32_t* d_plen = nullptr;         // per slice: entries per row (pattern len or int32 len)
+  int32_t* d_pat = nullptr;          // nslices*kmax offsets
+  uint64_t* d_mask = nullptr;        // nslices*(H/64) regular-row bits
+  int32_t* d_pint_list = nullptr;    // pattern mode: slices without ghost reads
+  int32_t* d_pbnd_list = nullptr;    // pattern mode: slices reading ghosts
+  int64_t np_int = 0, np_bnd = 0;
+  int64_t npattern_slices = 0, nregular_rows = 0;
+  // side SELL: the irregular rows of pattern slices (row map → oid)
+  int64_t s_nrows = 0, s_nslices = 0, s_slots = 0;
+  int64_t* d_s_off = nullptr;
+  int32_t* d_s_len = nullptr;
+  int32_t* d_s_col = nullptr;
+  void* d_s_val = nullptr;
+  int32_t* d_s_rowmap = nullptr;
+  int32_t* d_s_rowlen = nullptr;
 };

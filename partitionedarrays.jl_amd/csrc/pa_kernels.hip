@@ -13,223 +13,7 @@
 
 namespace pa {
 
-// ---------------------------------------------------------------------------
-// helpers
-
-template <typename T, int R>
-struct alignas(sizeof(T) * R) Pack {
-  T v[R];
-};
-template <int R>
-struct alignas(4 * R) IPack {
-  int32_t c[R];
-};
-
-// XCD-aware block remap (cdna_hip_programming.md §5.5 T1, bijective variant):
-// hardware block b runs on XCD b%8; give every XCD a contiguous range of
-// logical blocks so that neighbouring slices (which gather the same x
-// planes) share one L2.
-__device__ inline int64_t xcd_remap(int64_t b, int64_t G) {
-  const int64_t q = G >> 3, r = G & 7;
-  const int64_t x = b & 7, i = b >> 3;
-  return x * q + (x < r ? x : r) + i;
-}
-
-// ---------------------------------------------------------------------------
-// SELL SpMV.  One wave per slice of H = 64*R consecutive owned rows; lane l
-// owns rows l*R .. l*R+R-1 of the slice.  Entry k of those rows sits at
-// slot off + (k*64 + l)*R + r, so each wave-instruction streams 64*R
-// consecutive values (16 B per lane) and 64*R consecutive column ids.
-//
-// BMODE: 0 → acc = 0 (β == 0: fill!(co,0)), 1 → acc = y (β == 1),
-//        2 → acc = y*β (rmul!(co,β)).  Interfaces.jl:2262-2263.
-// Tuning flags (pa_tune): SPMV_NT — the once-read value/column streams are
-// loaded non-temporally so they do not evict the x planes from L2;
-// SPMV_XCD — XCD-aware slice→block mapping.  U = entries in flight per lane.
-
-enum { SPMV_NT = 1, SPMV_XCD = 2 };
-
-template <int BYTES> struct RawOf;
-template <> struct RawOf<4> { typedef unsigned int type; };
-template <> struct RawOf<8> { typedef unsigned int type __attribute__((ext_vector_type(2))); };
-template <> struct RawOf<16> { typedef unsigned int type __attribute__((ext_vector_type(4))); };
-template <> struct RawOf<32> { typedef unsigned int type __attribute__((ext_vector_type(8))); };
-
-template <bool NT, typename V>
-__device__ __forceinline__ V ld(const V* p) {
-  typedef typename RawOf<sizeof(V)>::type Raw;
-  Raw r;
-  if (NT) r = __builtin_nontemporal_load(reinterpret_cast<const Raw*>(p));
-  else r = *reinterpret_cast<const Raw*>(p);
-  V v;
-  __builtin_memcpy(&v, &r, sizeof(V));
-  return v;
-}
-
-template <typename T, int R, bool ALPHA, bool NT, int U>
-__device__ __forceinline__ void sell_rows(T (&acc)[R], const IPack<R>* __restrict__ cp,
-                                          const Pack<T, R>* __restrict__ vp, int len,
-                                          const T* __restrict__ x, T alpha) {
-  int k = 0;
-  for (; k + U <= len; k += U) {
-    IPack<R> c[U];
-    Pack<T, R> v[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) c[u] = ld<NT>(&cp[(k + u) * 64]);
-#pragma unroll
-    for (int u = 0; u < U; ++u) v[u] = ld<NT>(&vp[(k + u) * 64]);
-    T xv[U][R];
-#pragma unroll
-    for (int u = 0; u < U; ++u)
-#pragma unroll
-      for (int r = 0; r < R; ++r) {
-        const int32_t cc = c[u].c[r];
-        xv[u][r] = x[cc >= 0 ? cc : 0];
-      }
-#pragma unroll
-    for (int u = 0; u < U; ++u)
-#pragma unroll
-      for (int r = 0; r < R; ++r) {
-        T xx = xv[u][r];
-        if (ALPHA) xx = xx * alpha;
-        const T t = acc[r] + v[u].v[r] * xx;
-        acc[r] = (c[u].c[r] >= 0) ? t : acc[r];
-      }
-  }
-  for (; k < len; ++k) {
-    const IPack<R> c = ld<NT>(&cp[k * 64]);
-    const Pack<T, R> v = ld<NT>(&vp[k * 64]);
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-      const int32_t cc = c.c[r];
-      T xx = x[cc >= 0 ? cc : 0];
-      if (ALPHA) xx = xx * alpha;
-      const T t = acc[r] + v.v[r] * xx;
-      acc[r] = (cc >= 0) ? t : acc[r];
-    }
-  }
-}
-
-template <typename T, int R, bool ALPHA, int BMODE, bool YMAP, bool LIST, int U>
-__global__ __launch_bounds__(256) void k_spmv_sell(
-    int64_t nwork, const int32_t* __restrict__ list,
-    const int64_t* __restrict__ soff, const int32_t* __restrict__ slen,
-    const int32_t* __restrict__ col, const T* __restrict__ val,
-    const T* __restrict__ x, T* __restrict__ y,
-    const int32_t* __restrict__ ymap, int64_t nrows, T alpha, T beta, int flags) {
-  constexpr int H = 64 * R;
-  const int lane = threadIdx.x & 63;
-  const int64_t blk = (flags & SPMV_XCD) ? xcd_remap(blockIdx.x, gridDim.x) : (int64_t)blockIdx.x;
-  const int64_t w = blk * 4 + (threadIdx.x >> 6);
-  if (w >= nwork) return;
-  const int64_t s = LIST ? (int64_t)list[w] : w;
-  const int64_t off = soff[s];
-  const int len = slen[s];
-  const int64_t row0 = s * H + (int64_t)lane * R;
-
-  T acc[R];
-#pragma unroll
-  for (int r = 0; r < R; ++r) {
-    if (BMODE == 0) {
-      acc[r] = zero_of<T>();
-    } else {
-      const int64_t row = row0 + r;
-      T yo = zero_of<T>();
-      if (row < nrows) yo = y[YMAP ? (int64_t)ymap[row] : row];
-      acc[r] = (BMODE == 2) ? yo * beta : yo;
-    }
-  }
-
-  const IPack<R>* __restrict__ cp = reinterpret_cast<const IPack<R>*>(col + off) + lane;
-  const Pack<T, R>* __restrict__ vp = reinterpret_cast<const Pack<T, R>*>(val + off) + lane;
-  if (flags & SPMV_NT) sell_rows<T, R, ALPHA, true, U>(acc, cp, vp, len, x, alpha);
-  else sell_rows<T, R, ALPHA, false, U>(acc, cp, vp, len, x, alpha);
-
-  if (!YMAP && row0 + R <= nrows) {
-    Pack<T, R> o;
-#pragma unroll
-    for (int r = 0; r < R; ++r) o.v[r] = acc[r];
-    *reinterpret_cast<Pack<T, R>*>(y + row0) = o;
-  } else {
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-      const int64_t row = row0 + r;
-      if (row < nrows) y[YMAP ? (int64_t)ymap[row] : row] = acc[r];
-    }
-  }
-}
-
-int g_spmv_flags = SPMV_NT;    // pa_tune("spmv_flags"); A/B: profiles/r01_ab_spmv.txt
-int g_spmv_unroll = 8;         // pa_tune("spmv_unroll"): 4 or 8
-
-template <typename T, int R, bool ALPHA, int BMODE, bool YMAP, int U>
-static void launch_spmv5(int64_t nwork, const int32_t* list, const pa_mat* A,
-                         const T* x, T* y, const int32_t* ymap, T alpha, T beta,
-                         hipStream_t st) {
-  const int64_t blocks = (nwork + 3) / 4;
-  if (blocks == 0) return;
-  if (list)
-    hipLaunchKernelGGL((k_spmv_sell<T, R, ALPHA, BMODE, YMAP, true, U>), dim3(blocks), dim3(256), 0, st,
-                       nwork, list, A->d_slice_off, A->d_slice_len, A->d_col,
-                       (const T*)A->d_val, x, y, ymap, A->nrows, alpha, beta, g_spmv_flags);
-  else
-    hipLaunchKernelGGL((k_spmv_sell<T, R, ALPHA, BMODE, YMAP, false, U>), dim3(blocks), dim3(256), 0, st,
-                       nwork, list, A->d_slice_off, A->d_slice_len, A->d_col,
-                       (const T*)A->d_val, x, y, ymap, A->nrows, alpha, beta, g_spmv_flags);
-}
-
-template <typename T, int R, bool ALPHA, int BMODE, bool YMAP>
-static void launch_spmv4(int64_t nwork, const int32_t* list, const pa_mat* A,
-                         const T* x, T* y, const int32_t* ymap, T alpha, T beta,
-                         hipStream_t st) {
-  // the unroll-8 body only for the hot configuration (β == 0, contiguous y)
-  if (g_spmv_unroll == 8 && !ALPHA && BMODE == 0 && !YMAP)
-    launch_spmv5<T, R, ALPHA, BMODE, YMAP, 8>(nwork, list, A, x, y, ymap, alpha, beta, st);
-  else
-    launch_spmv5<T, R, ALPHA, BMODE, YMAP, 4>(nwork, list, A, x, y, ymap, alpha, beta, st);
-}
-
-template <typename T, int R>
-static void launch_spmv_t(int64_t nwork, const int32_t* list, const pa_mat* A,
-                          const T* x, T* y, const int32_t* ymap, bool has_alpha,
-                          int bmode, T alpha, T beta, hipStream_t st) {
-#define PA_SPMV_CASE(AL, BM)                                                        \
-  if (has_alpha == AL && bmode == BM) {                                             \
-    if (ymap) launch_spmv4<T, R, AL, BM, true>(nwork, list, A, x, y, ymap, alpha, beta, st); \
-    else launch_spmv4<T, R, AL, BM, false>(nwork, list, A, x, y, ymap, alpha, beta, st);     \
-    return;                                                                         \
-  }
-  PA_SPMV_CASE(false, 0)
-  PA_SPMV_CASE(false, 1)
-  PA_SPMV_CASE(false, 2)
-  PA_SPMV_CASE(true, 0)
-  PA_SPMV_CASE(true, 1)
-  PA_SPMV_CASE(true, 2)
-#undef PA_SPMV_CASE
-}
-
-void launch_spmv(int64_t nwork, const int32_t* list, const pa_mat* A,
-                 const void* x, void* y, const int32_t* ymap, bool has_alpha,
-                 int bmode, const void* alpha, const void* beta, hipStream_t st) {
-  switch (A->dtype) {
-    case PA_F32:
-      launch_spmv_t<float, 4>(nwork, list, A, (const float*)x, (float*)y, ymap, has_alpha, bmode,
-                              *(const float*)alpha, *(const float*)beta, st);
-      break;
-    case PA_F64:
-      launch_spmv_t<double, 2>(nwork, list, A, (const double*)x, (double*)y, ymap, has_alpha, bmode,
-                               *(const double*)alpha, *(const double*)beta, st);
-      break;
-    case PA_C64:
-      launch_spmv_t<c64, 2>(nwork, list, A, (const c64*)x, (c64*)y, ymap, has_alpha, bmode,
-                            *(const c64*)alpha, *(const c64*)beta, st);
-      break;
-    case PA_C128:
-      launch_spmv_t<c128, 1>(nwork, list, A, (const c128*)x, (c128*)y, ymap, has_alpha, bmode,
-                             *(const c128*)alpha, *(const c128*)beta, st);
-      break;
-  }
-}
+// SELL SpMV kernels: pa_spmv.hip
 
 // ---------------------------------------------------------------------------
 // Halo pack / unpack (Interfaces.jl:858-866 and 878-886).

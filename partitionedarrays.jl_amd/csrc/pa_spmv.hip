@@ -1,0 +1,493 @@
+// pa_spmv.hip — the hot kernel: owned-row SELL SpMV for gfx950, and the
+// one-time conversion of its int32-column layout to pattern slices.
+//
+// Layout: a slice is H = 64*R consecutive owned rows; lane l
+// owns rows l*R .. l*R+R-1; entry k of those rows sits at slot
+// off[s] + (k*64 + l)*R + r.  A wave-instruction streams 64*R consecutive
+// values (16 B per lane).
+//
+// Two column encodings share the value slots:
+//  * int32 slices: column id (x lid) per slot, -1 = padding;
+//  * pattern slices: the rows whose columns are `row + pat[k]`, k < plen
+//    (mask bit set) carry no column ids at all; the slice's other rows are
+//    computed from a small side SELL (int32 columns + row map).
+// Either way each row is accumulated sequentially in the reference's order
+// (SparseUtils.jl:176-185: owned columns by oid, then ghost columns by hid):
+//   acc = β-init; acc = acc + v_k * (x_{c_k} * α)   (-ffp-contract=off)
+#include "pa_internal.h"
+
+namespace pa {
+
+template <typename T, int R>
+struct alignas(sizeof(T) * R) Pack {
+  T v[R];
+};
+template <int R>
+struct alignas(4 * R) IPack {
+  int32_t c[R];
+};
+
+// XCD-aware block remap (cdna_hip_programming.md §5.5 T1, bijective variant).
+__device__ inline int64_t xcd_remap(int64_t b, int64_t G) {
+  const int64_t q = G >> 3, r = G & 7;
+  const int64_t x = b & 7, i = b >> 3;
+  return x * q + (x < r ? x : r) + i;
+}
+
+enum { SPMV_NT = 1, SPMV_XCD = 2 };
+// Process-wide knobs (pa_tune).  Defaults from the A/B in
+// profiles/r01_ab_spmv.txt: non-temporal streams on, XCD remap off, U = 8.
+int g_spmv_flags = SPMV_NT;
+int g_spmv_unroll = 8;
+int g_spmv_format = 1;  // 1: pattern slices where built, 0: int32 columns only
+
+template <int BYTES> struct RawOf;
+template <> struct RawOf<4> { typedef unsigned int type; };
+template <> struct RawOf<8> { typedef unsigned int type __attribute__((ext_vector_type(2))); };
+template <> struct RawOf<16> { typedef unsigned int type __attribute__((ext_vector_type(4))); };
+
+template <bool NT, typename V>
+__device__ __forceinline__ V ld(const V* p) {
+  typedef typename RawOf<sizeof(V)>::type Raw;
+  Raw r;
+  if (NT) r = __builtin_nontemporal_load(reinterpret_cast<const Raw*>(p));
+  else r = *reinterpret_cast<const Raw*>(p);
+  V v;
+  __builtin_memcpy(&v, &r, sizeof(V));
+  return v;
+}
+
+template <typename T>
+struct SpmvArgs {
+  int64_t nwork;            // slices of this launch
+  const int32_t* list;      // slice ids (null: 0..nwork-1)
+  const int64_t* soff;
+  const int32_t* slen;      // entries per row of the slice
+  const int32_t* col;
+  const T* val;
+  const int32_t* kind;      // per slice 1 = pattern (null: all int32)
+  const int32_t* pat;       // kmax offsets per slice
+  const uint64_t* mask;     // H/64 words per slice
+  int kmax;
+  const int32_t* rowmap;    // structure row → oid (side SELL), null: identity
+  int64_t nrows;            // rows of this structure
+  const T* x;
+  T* y;
+  const int32_t* ymap;      // oid → y lid, null: identity
+  T alpha, beta;
+  int flags;
+};
+
+// int32-column rows: c < 0 is padding (skipped: never multiplied)
+template <typename T, int R, bool ALPHA, bool NT, int U>
+__device__ __forceinline__ void rows_int32(T (&acc)[R], const IPack<R>* __restrict__ cp,
+                                           const Pack<T, R>* __restrict__ vp, int len,
+                                           const T* __restrict__ x, T alpha) {
+  int k = 0;
+  for (; k + U <= len; k += U) {
+    IPack<R> c[U];
+    Pack<T, R> v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) c[u] = ld<NT>(&cp[(k + u) * 64]);
+#pragma unroll
+    for (int u = 0; u < U; ++u) v[u] = ld<NT>(&vp[(k + u) * 64]);
+    T xv[U][R];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const int32_t cc = c[u].c[r];
+        xv[u][r] = x[cc >= 0 ? cc : 0];
+      }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        T xx = xv[u][r];
+        if (ALPHA) xx = xx * alpha;
+        const T t = acc[r] + v[u].v[r] * xx;
+        acc[r] = (c[u].c[r] >= 0) ? t : acc[r];
+      }
+  }
+  for (; k < len; ++k) {
+    const IPack<R> c = ld<NT>(&cp[k * 64]);
+    const Pack<T, R> v = ld<NT>(&vp[k * 64]);
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const int32_t cc = c.c[r];
+      T xx = x[cc >= 0 ? cc : 0];
+      if (ALPHA) xx = xx * alpha;
+      const T t = acc[r] + v.v[r] * xx;
+      acc[r] = (cc >= 0) ? t : acc[r];
+    }
+  }
+}
+
+// pattern rows: column of row `rbase + r` at entry k is rbase + r + pat[k]
+template <typename T, int R, bool ALPHA, bool NT, int U>
+__device__ __forceinline__ void rows_pattern(T (&acc)[R], const int32_t* __restrict__ pat,
+                                             const Pack<T, R>* __restrict__ vp, int len,
+                                             const T* __restrict__ x, int64_t rbase,
+                                             const bool (&ok)[R], T alpha) {
+  int64_t xb[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) xb[r] = ok[r] ? rbase + r : -1;
+  int k = 0;
+  for (; k + U <= len; k += U) {
+    int32_t o[U];
+    Pack<T, R> v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) o[u] = pat[k + u];
+#pragma unroll
+    for (int u = 0; u < U; ++u) v[u] = ld<NT>(&vp[(k + u) * 64]);
+    T xv[U][R];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int r = 0; r < R; ++r) xv[u][r] = x[xb[r] >= 0 ? xb[r] + o[u] : 0];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        T xx = xv[u][r];
+        if (ALPHA) xx = xx * alpha;
+        acc[r] = acc[r] + v[u].v[r] * xx;
+      }
+  }
+  for (; k < len; ++k) {
+    const int32_t o = pat[k];
+    const Pack<T, R> v = ld<NT>(&vp[k * 64]);
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      T xx = x[xb[r] >= 0 ? xb[r] + o : 0];
+      if (ALPHA) xx = xx * alpha;
+      acc[r] = acc[r] + v.v[r] * xx;
+    }
+  }
+}
+
+// BMODE: 0 → acc = 0 (β == 0: fill!(co,0)), 1 → acc = y (β == 1),
+//        2 → acc = y*β (rmul!(co,β)).  Interfaces.jl:2262-2263.
+template <typename T, int R, bool ALPHA, int BMODE, int U>
+__global__ __launch_bounds__(256) void k_spmv_sell(SpmvArgs<T> a) {
+  constexpr int H = 64 * R;
+  const int lane = threadIdx.x & 63;
+  const int64_t blk = (a.flags & SPMV_XCD) ? xcd_remap(blockIdx.x, gridDim.x) : (int64_t)blockIdx.x;
+  const int64_t w = blk * 4 + (threadIdx.x >> 6);
+  if (w >= a.nwork) return;
+  const int64_t s = a.list ? (int64_t)a.list[w] : w;
+  const int64_t off = a.soff[s];
+  const int len = a.slen[s];
+  const int64_t row0 = s * H + (int64_t)lane * R;
+  const bool pattern = a.kind && a.kind[s];
+
+  bool ok[R];
+  if (pattern) {
+    const uint64_t m = a.mask[s * (H / 64) + (lane * R) / 64];
+#pragma unroll
+    for (int r = 0; r < R; ++r) ok[r] = ((m >> ((lane * R + r) & 63)) & 1ull) && (row0 + r < a.nrows);
+  } else {
+#pragma unroll
+    for (int r = 0; r < R; ++r) ok[r] = row0 + r < a.nrows;
+  }
+  int64_t orow[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) orow[r] = ok[r] ? (a.rowmap ? (int64_t)a.rowmap[row0 + r] : row0 + r) : 0;
+
+  T acc[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    if (BMODE == 0) {
+      acc[r] = zero_of<T>();
+    } else {
+      T yo = zero_of<T>();
+      if (ok[r]) yo = a.y[a.ymap ? (int64_t)a.ymap[orow[r]] : orow[r]];
+      acc[r] = (BMODE == 2) ? yo * a.beta : yo;
+    }
+  }
+
+  const Pack<T, R>* __restrict__ vp = reinterpret_cast<const Pack<T, R>*>(a.val + off) + lane;
+  if (pattern) {
+    const int32_t* pat = a.pat + s * a.kmax;
+    if (a.flags & SPMV_NT) rows_pattern<T, R, ALPHA, true, U>(acc, pat, vp, len, a.x, row0, ok, a.alpha);
+    else rows_pattern<T, R, ALPHA, false, U>(acc, pat, vp, len, a.x, row0, ok, a.alpha);
+  } else {
+    const IPack<R>* __restrict__ cp = reinterpret_cast<const IPack<R>*>(a.col + off) + lane;
+    if (a.flags & SPMV_NT) rows_int32<T, R, ALPHA, true, U>(acc, cp, vp, len, a.x, a.alpha);
+    else rows_int32<T, R, ALPHA, false, U>(acc, cp, vp, len, a.x, a.alpha);
+  }
+
+  bool all = true;
+#pragma unroll
+  for (int r = 0; r < R; ++r) all = all && ok[r];
+  if (all && !a.ymap && !a.rowmap) {
+    Pack<T, R> o;
+#pragma unroll
+    for (int r = 0; r < R; ++r) o.v[r] = acc[r];
+    *reinterpret_cast<Pack<T, R>*>(a.y + row0) = o;
+  } else {
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+      if (ok[r]) a.y[a.ymap ? (int64_t)a.ymap[orow[r]] : orow[r]] = acc[r];
+  }
+}
+
+template <typename T, int R, bool ALPHA, int BMODE>
+static void launch_t(const SpmvArgs<T>& a, hipStream_t st) {
+  const int64_t blocks = (a.nwork + 3) / 4;
+  if (blocks == 0) return;
+  if (g_spmv_unroll == 4)
+    hipLaunchKernelGGL((k_spmv_sell<T, R, ALPHA, BMODE, 4>), dim3(blocks), dim3(256), 0, st, a);
+  else
+    hipLaunchKernelGGL((k_spmv_sell<T, R, ALPHA, BMODE, 8>), dim3(blocks), dim3(256), 0, st, a);
+}
+
+template <typename T, int R>
+static void launch_ab(const SpmvArgs<T>& a, bool has_alpha, int bmode, hipStream_t st) {
+  if (!has_alpha) {
+    if (bmode == 0) launch_t<T, R, false, 0>(a, st);
+    else if (bmode == 1) launch_t<T, R, false, 1>(a, st);
+    else launch_t<T, R, false, 2>(a, st);
+  } else {
+    if (bmode == 0) launch_t<T, R, true, 0>(a, st);
+    else if (bmode == 1) launch_t<T, R, true, 1>(a, st);
+    else launch_t<T, R, true, 2>(a, st);
+  }
+}
+
+// which = 0: main structure, pattern mode; 1: main structure, int32 mode;
+// 2: side SELL.  list/nwork select the slices.
+template <typename T, int R>
+static void launch_which(int which, int64_t nwork, const int32_t* list, const pa_mat* A, const void* x,
+                         void* y, const int32_t* ymap, bool has_alpha, int bmode, const void* alpha,
+                         const void* beta, hipStream_t st) {
+  SpmvArgs<T> a{};
+  a.nwork = nwork;
+  a.list = list;
+  a.x = (const T*)x;
+  a.y = (T*)y;
+  a.ymap = ymap;
+  a.alpha = *(const T*)alpha;
+  a.beta = *(const T*)beta;
+  a.flags = g_spmv_flags;
+  if (which == 2) {
+    a.soff = A->d_s_off;
+    a.slen = A->d_s_len;
+    a.col = A->d_s_col;
+    a.val = (const T*)A->d_s_val;
+    a.rowmap = A->d_s_rowmap;
+    a.nrows = A->s_nrows;
+  } else {
+    a.soff = A->d_slice_off;
+    a.col = A->d_col;
+    a.val = (const T*)A->d_val;
+    a.nrows = A->nrows;
+    if (which == 0) {
+      a.slen = A->d_plen;
+      a.kind = A->d_kind;
+      a.pat = A->d_pat;
+      a.mask = A->d_mask;
+      a.kmax = A->kmax;
+    } else {
+      a.slen = A->d_slice_len;
+    }
+  }
+  launch_ab<T, R>(a, has_alpha, bmode, st);
+}
+
+void launch_spmv_part(int which, int64_t nwork, const int32_t* list, const pa_mat* A, const void* x,
+                      void* y, const int32_t* ymap, bool has_alpha, int bmode, const void* alpha,
+                      const void* beta, hipStream_t st) {
+  switch (A->dtype) {
+    case PA_F32: launch_which<float, 4>(which, nwork, list, A, x, y, ymap, has_alpha, bmode, alpha, beta, st); break;
+    case PA_F64: launch_which<double, 2>(which, nwork, list, A, x, y, ymap, has_alpha, bmode, alpha, beta, st); break;
+    case PA_C64: launch_which<c64, 2>(which, nwork, list, A, x, y, ymap, has_alpha, bmode, alpha, beta, st); break;
+    case PA_C128: launch_which<c128, 1>(which, nwork, list, A, x, y, ymap, has_alpha, bmode, alpha, beta, st); break;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Pattern detection (one wave per slice).  Candidate: the middle valid row
+// of the slice; its offsets pat[k] = col_k - row.  A row is regular when its
+// column sequence is exactly row + pat[k] (same length).  A slice becomes a
+// pattern slice when at least half of its valid rows are regular.
+
+template <int R>
+__global__ __launch_bounds__(256) void k_pattern_detect(int64_t nrows, int64_t nslices,
+                                                        const int64_t* __restrict__ soff,
+                                                        const int32_t* __restrict__ slen,
+                                                        const int32_t* __restrict__ col, int64_t noids,
+                                                        int kmax, int32_t* __restrict__ kind,
+                                                        int32_t* __restrict__ plen,
+                                                        int32_t* __restrict__ pat,
+                                                        uint64_t* __restrict__ mask,
+                                                        int32_t* __restrict__ pghost,
+                                                        int32_t* __restrict__ nirreg) {
+  constexpr int H = 64 * R;
+  const int lane = threadIdx.x & 63;
+  const int64_t s = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (s >= nslices) return;
+  const int64_t off = soff[s];
+  const int L = slen[s];
+  const int64_t rem = nrows - s * H;
+  const int nvalid = (int)(rem < H ? rem : H);
+  const int m = nvalid / 2;
+  const int64_t mrow = s * H + m;
+  const int mlane = m / R, mr = m % R;
+  int Lp = 0;
+  for (int k = 0; k < L; ++k) {
+    if (col[off + ((int64_t)k * 64 + mlane) * R + mr] < 0) break;
+    ++Lp;
+  }
+  int nreg = 0;
+  bool ghost_reg = false, ghost_any = false;
+  uint64_t bits[(R + 63) / 64 + 1] = {0};
+  (void)bits;
+  for (int r = 0; r < R; ++r) {
+    const int i = lane * R + r;
+    const int64_t row = s * H + i;
+    const bool valid = i < nvalid;
+    bool reg = valid && Lp > 0;
+    bool g = false;
+    for (int k = 0; k < L; ++k) {
+      const int32_t c = col[off + ((int64_t)k * 64 + lane) * R + r];
+      if (valid && c >= noids) ghost_any = true;
+      if (k < Lp) {
+        const int32_t cm = col[off + ((int64_t)k * 64 + mlane) * R + mr];
+        const int64_t e = row + (int64_t)(cm - mrow);
+        if ((int64_t)c != e) reg = false;
+        if (e >= noids) g = true;
+      } else if (c != -1) {
+        reg = false;
+      }
+    }
+    if (reg) {
+      ++nreg;
+      ghost_reg = ghost_reg || g;
+      atomicOr((unsigned long long*)&mask[s * (H / 64) + i / 64], 1ull << (i & 63));
+    }
+  }
+  // wave sums
+  int tot = nreg;
+  for (int d = 32; d >= 1; d >>= 1) tot += __shfl_xor(tot, d, 64);
+  const bool gr = __any(ghost_reg);
+  const bool ga = __any(ghost_any);
+  const bool is_pat = Lp > 0 && 2 * tot >= nvalid;
+  if (lane == 0) {
+    kind[s] = is_pat ? 1 : 0;
+    plen[s] = is_pat ? Lp : L;
+    pghost[s] = is_pat ? (gr ? 1 : 0) : (ga ? 1 : 0);
+    nirreg[s] = is_pat ? nvalid - tot : 0;
+  }
+  if (is_pat)
+    for (int k = lane; k < Lp; k += 64)
+      pat[s * kmax + k] = col[off + ((int64_t)k * 64 + mlane) * R + mr] - (int32_t)mrow;
+}
+
+void launch_pattern_detect(pa_mat* A, int64_t noids, int32_t* kind, int32_t* plen, int32_t* pat,
+                           uint64_t* mask, int32_t* pghost, int32_t* nirreg, hipStream_t st) {
+  const int64_t blocks = (A->nslices + 3) / 4;
+  if (blocks == 0) return;
+#define PA_DET(RR)                                                                                   \
+  hipLaunchKernelGGL(k_pattern_detect<RR>, dim3(blocks), dim3(256), 0, st, A->nrows, A->nslices,     \
+                     A->d_slice_off, A->d_slice_len, A->d_col, noids, A->kmax, kind, plen, pat, mask, \
+                     pghost, nirreg)
+  switch (A->R) {
+    case 1: PA_DET(1); break;
+    case 2: PA_DET(2); break;
+    case 4: PA_DET(4); break;
+  }
+#undef PA_DET
+}
+
+// Side SELL: the irregular rows (oids, ascending), copied from the int32 layout.
+template <int R>
+__global__ void k_side_len(int64_t n, const int32_t* __restrict__ rows, const int64_t* __restrict__ soff,
+                           const int32_t* __restrict__ slen, const int32_t* __restrict__ col,
+                           int32_t* __restrict__ len, int64_t noids, int32_t* __restrict__ sghost, int sH) {
+  constexpr int H = 64 * R;
+  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int64_t row = rows[i];
+  const int64_t s = row / H;
+  const int w = (int)(row - s * H);
+  const int lane = w / R, r = w % R;
+  int l = 0;
+  bool g = false;
+  for (int k = 0; k < slen[s]; ++k) {
+    const int32_t c = col[soff[s] + ((int64_t)k * 64 + lane) * R + r];
+    if (c < 0) break;
+    if (c >= noids) g = true;
+    ++l;
+  }
+  len[i] = l;
+  if (g) atomicOr(&sghost[i / sH], 1);
+}
+
+template <typename T, int R>
+__global__ void k_side_fill(int64_t n, const int32_t* __restrict__ rows, const int64_t* __restrict__ soff,
+                            const int32_t* __restrict__ col, const T* __restrict__ val,
+                            const int64_t* __restrict__ s_off, const int32_t* __restrict__ s_len,
+                            const int32_t* __restrict__ len, int32_t* __restrict__ s_col,
+                            T* __restrict__ s_val, int64_t s_nslices) {
+  constexpr int H = 64 * R;
+  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (i >= s_nslices * H) return;
+  const int64_t ss = i / H;
+  const int wi = (int)(i - ss * H);
+  const int sl = wi / R, sr = wi % R;
+  int l = 0;
+  int64_t base = 0;
+  int lane = 0, r = 0;
+  if (i < n) {
+    const int64_t row = rows[i];
+    const int64_t s = row / H;
+    const int w = (int)(row - s * H);
+    lane = w / R;
+    r = w % R;
+    l = len[i];
+    base = soff[s];
+  }
+  for (int k = 0; k < s_len[ss]; ++k) {
+    const int64_t dst = s_off[ss] + ((int64_t)k * 64 + sl) * R + sr;
+    if (k < l) {
+      const int64_t src = base + ((int64_t)k * 64 + lane) * R + r;
+      s_col[dst] = col[src];
+      s_val[dst] = val[src];
+    } else {
+      s_col[dst] = -1;
+      s_val[dst] = zero_of<T>();
+    }
+  }
+}
+
+void launch_side_len(pa_mat* A, int64_t n, const int32_t* rows, int32_t* len, int64_t noids,
+                     int32_t* sghost, hipStream_t st) {
+  if (n == 0) return;
+  const dim3 g((unsigned)((n + 255) / 256)), b(256);
+  switch (A->R) {
+    case 1: hipLaunchKernelGGL(k_side_len<1>, g, b, 0, st, n, rows, A->d_slice_off, A->d_slice_len, A->d_col, len, noids, sghost, A->H); break;
+    case 2: hipLaunchKernelGGL(k_side_len<2>, g, b, 0, st, n, rows, A->d_slice_off, A->d_slice_len, A->d_col, len, noids, sghost, A->H); break;
+    case 4: hipLaunchKernelGGL(k_side_len<4>, g, b, 0, st, n, rows, A->d_slice_off, A->d_slice_len, A->d_col, len, noids, sghost, A->H); break;
+  }
+}
+
+template <typename T, int R>
+static void side_fill_t(pa_mat* A, const int32_t* rows, const int32_t* len, hipStream_t st) {
+  const int64_t tot = A->s_nslices * 64 * R;
+  if (tot == 0) return;
+  hipLaunchKernelGGL((k_side_fill<T, R>), dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st,
+                     A->s_nrows, rows, A->d_slice_off, A->d_col, (const T*)A->d_val, A->d_s_off,
+                     A->d_s_len, len, A->d_s_col, (T*)A->d_s_val, A->s_nslices);
+}
+
+void launch_side_fill(pa_mat* A, const int32_t* rows, const int32_t* len, hipStream_t st) {
+  switch (A->dtype) {
+    case PA_F32: side_fill_t<float, 4>(A, rows, len, st); break;
+    case PA_F64: side_fill_t<double, 2>(A, rows, len, st); break;
+    case PA_C64: side_fill_t<c64, 2>(A, rows, len, st); break;
+    case PA_C128: side_fill_t<c128, 1>(A, rows, len, st); break;
+  }
+}
+
+}  // namespace pa

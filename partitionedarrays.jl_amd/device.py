@@ -217,7 +217,11 @@ class DeviceMatrix:
     def info(self):
         v = [C.c_int64() for _ in range(5)]
         _lib.call("pa_mat_info", self.h, *[C.byref(x) for x in v])
-        return dict(zip(["nrows", "nnz", "slots", "nslices", "nslices_interior"], [x.value for x in v]))
+        d = dict(zip(["nrows", "nnz", "slots", "nslices", "nslices_interior"], [x.value for x in v]))
+        f = [C.c_int64() for _ in range(4)]
+        _lib.call("pa_mat_format_info", self.h, *[C.byref(x) for x in f])
+        d.update(zip(["pattern_slices", "regular_rows", "side_rows", "side_slots"], [x.value for x in f]))
+        return d
 
     def __del__(self):
         try:

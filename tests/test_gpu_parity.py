@@ -21,6 +21,14 @@ def be(pamd):
     return pamd.HIPBackend(devices=[0])
 
 
+@pytest.fixture(params=[1, 0], ids=["pattern", "int32"])
+def fmt(request, pamd, be):
+    """Run a test with both column encodings (pa_tune spmv_format)."""
+    prev = pamd._lib.tune("spmv_format", request.param)
+    yield request.param
+    pamd._lib.tune("spmv_format", prev)
+
+
 def _rand(rng, n, dtype):
     dtype = np.dtype(dtype)
     if dtype.kind == "c":
@@ -58,7 +66,7 @@ CASES = [
 
 
 @pytest.mark.parametrize("shape,N,kind,dtype", CASES)
-def test_stencil_spmv_bitexact(be, pamd, O, shape, N, kind, dtype):
+def test_stencil_spmv_bitexact(be, pamd, O, fmt, shape, N, kind, dtype):
     parts = be.get_part_ids(shape)
     A = pamd.drivers.stencil_operator(parts, N, kind, dtype)
     rng = np.random.default_rng(SEED)
@@ -78,7 +86,7 @@ def test_stencil_spmv_bitexact(be, pamd, O, shape, N, kind, dtype):
         assert _eq(O, gx.local(p), ox.values[p]), f"part {p}: exchanged ghost values of b differ"
 
 
-def test_csc_path_equals_stencil_generator(be, pamd, O):
+def test_csc_path_equals_stencil_generator(be, pamd, O, fmt):
     """pa_mat_from_csc of the oracle-assembled CSC == pa_mat_stencil."""
     shape, N, kind = (2, 2, 1), (12, 11, 7), 27
     parts = be.get_part_ids(shape)
@@ -101,7 +109,7 @@ def test_csc_path_equals_stencil_generator(be, pamd, O):
 
 
 @pytest.mark.parametrize("alpha,beta", [(1.0, 1.0), (2.5, 0.5), (-1.0, 0.0), (0.75, -2.0)])
-def test_alpha_beta(be, pamd, O, alpha, beta):
+def test_alpha_beta(be, pamd, O, fmt, alpha, beta):
     shape, N = (2, 1, 2), (9, 7, 10)
     parts = be.get_part_ids(shape)
     A = pamd.drivers.stencil_operator(parts, N, 27)
@@ -161,7 +169,7 @@ def test_dot_norm_sum(be, pamd, O, dtype):
 
 
 @pytest.mark.parametrize("nparts", [4, (2, 2, 2)])
-def test_fdm_cg(be, pamd, O, nparts):
+def test_fdm_cg(be, pamd, O, fmt, nparts):
     """test_fdm.jl end to end on the device: CG converges to x̂ (test_fdm.jl:118)
     and follows the oracle's residual history."""
     parts = be.get_part_ids(nparts)
@@ -182,7 +190,7 @@ def test_fdm_cg(be, pamd, O, nparts):
     np.testing.assert_allclose(hist, ohist, rtol=1e-8)
 
 
-def test_large_fe27_vs_c_oracle(be, pamd, O, tmp_path):
+def test_large_fe27_vs_c_oracle(be, pamd, O, fmt, tmp_path):
     """One part, 48³ FE27 (2.8 M nnz): bit-exact against oracle/build/spmv_ref."""
     ref = os.path.join(ROOT, "oracle", "build", "spmv_ref")
     if not os.path.exists(ref):

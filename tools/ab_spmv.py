@@ -1,6 +1,10 @@
 """A/B the SpMV kernel variants (pa_tune knobs) in ONE process, interleaved
 rounds (cdna_hip_programming.md §5.4 rule 24).  Kernel time from HIP events
-on the SpMV's stream.  Usage: python tools/ab_spmv.py [--n 256] [--rounds 5]"""
+on the SpMV's stream.  Every variant must give the same bits.
+
+  python tools/ab_spmv.py [--n 256] [--kind 27] [--rounds 5]
+                          [--variants flags:unroll:format,...]
+"""
 import argparse
 import os
 import sys
@@ -13,21 +17,28 @@ import pamd  # noqa: E402
 ap = argparse.ArgumentParser()
 ap.add_argument("--n", type=int, default=256)
 ap.add_argument("--kind", type=int, default=27)
+ap.add_argument("--dtype", default="f64")
+ap.add_argument("--shape", default="1,1,1", help="parts (all on device 0)")
 ap.add_argument("--rounds", type=int, default=5)
 ap.add_argument("--reps", type=int, default=10)
-ap.add_argument("--variants", default="2:4,3:4,0:4,1:4,2:8,3:8")
+ap.add_argument("--variants", default="1:8:0,1:8:1,0:8:1,1:4:1")
 a = ap.parse_args()
+dtype = {"f64": np.float64, "f32": np.float32, "c128": np.complex128, "c64": np.complex64}[a.dtype]
 
 be = pamd.HIPBackend(devices=[0])
-parts = be.get_part_ids((1, 1, 1))
-N = (a.n,) * 3
-A = pamd.drivers.stencil_operator(parts, N, a.kind)
-x = pamd.PVector.from_host(pamd.map_parts(lambda s: np.random.default_rng(1).uniform(-1, 1, s.num_lids),
-                                          A.cols.partition), A.cols)
-y = pamd.PVector.undef(A.rows)
-ctx = be.context(1)
-info = A.values.local(1).info()
-B = info["nnz"] * 12 + (info["nrows"] + 1) * 4 + info["nrows"] * 16
+shape = tuple(int(v) for v in a.shape.split(","))
+parts = be.get_part_ids(shape)
+N = tuple(a.n * s for s in shape)
+A = pamd.drivers.stencil_operator(parts, N, a.kind, dtype)
+x = pamd.PVector.from_host(pamd.map_parts(
+    lambda s: np.random.default_rng(s.part).uniform(-1, 1, s.num_lids).astype(dtype), A.cols.partition), A.cols)
+y = pamd.PVector.undef(A.rows, dtype)
+p0 = parts.part_ids[0]
+ctx = be.context(p0)
+info = A.values.local(p0).info()
+S = np.dtype(dtype).itemsize
+nh = A.cols.partition.local(p0).num_hids
+B = info["nnz"] * (S + 4) + (info["nrows"] + 1) * 4 + (info["nrows"] + nh) * S + info["nrows"] * S
 variants = [tuple(int(t) for t in v.split(":")) for v in a.variants.split(",")]
 res = {v: [] for v in variants}
 ref = None
@@ -35,19 +46,20 @@ for rnd in range(a.rounds):
     for v in variants:
         pamd._lib.tune("spmv_flags", v[0])
         pamd._lib.tune("spmv_unroll", v[1])
+        pamd._lib.tune("spmv_format", v[2])
         pamd.mul_(y, A, x)
         ctx.set_timing(True)
         for _ in range(a.reps):
             pamd.mul_(y, A, x)
-            ms = sum(ctx.last_kernel_ms())
-            res[v].append(ms)
+            res[v].append(sum(ctx.last_kernel_ms()))
         ctx.set_timing(False)
-        out = y.to_host().local(1)
+        out = y.to_host().local(p0)
         if ref is None:
             ref = out
         assert np.array_equal(out, ref), f"variant {v} changed the result"
-print(f"n={a.n} kind={a.kind} nnz={info['nnz']} bytes={B}")
+print(f"n={a.n} kind={a.kind} dtype={a.dtype} parts={shape} part {p0}: {info}")
+print(f"algorithmic bytes per SpMV (part {p0}) = {B}")
 for v in variants:
     t = np.array(res[v])
-    print(f"flags={v[0]} unroll={v[1]}: median {np.median(t):.4f} ms  min {t.min():.4f}  "
-          f"-> {B / np.median(t) / 1e6:.0f} GB/s (median), {B / t.min() / 1e6:.0f} (best)")
+    print(f"flags={v[0]} unroll={v[1]} format={'pattern' if v[2] else 'int32'}: median {np.median(t):.4f} ms "
+          f"min {t.min():.4f} -> {B / np.median(t) / 1e6:.0f} GB/s (median), {B / t.min() / 1e6:.0f} (best)")
