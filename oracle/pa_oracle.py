@@ -1269,6 +1269,102 @@ def fdm_problem(parts: PData, nx=10):
     return A, b, x0, xh
 
 
+def assemble_coo_(I: PData, J: PData, V: PData, rows: PRange):
+    """async_assemble!(I, J, V, rows) + wait, Interfaces.jl:2406-2492: COO
+    triplets whose row is owned elsewhere are sent to the owner (their local
+    value set to zero, kept in the list) and appended there; I, J stay global."""
+    to_lids_pr_(I, rows)
+    parts = get_part_ids(rows.partition.shape if len(rows.partition.shape) > 1 else num_parts(rows.partition))
+
+    def setup_rcv(part, prcv, s, i, j, v):
+        owner_to_i = {o: k for k, o in enumerate(prcv)}
+        segs = [[[], [], []] for _ in prcv]
+        for k in range(len(i)):
+            li = i[k]
+            owner = s.lid_to_part[li - 1]
+            if owner != part:
+                seg = segs[owner_to_i[owner]]
+                seg[0].append(s.lid_to_gid[li - 1])
+                seg[1].append(j[k])
+                seg[2].append(v[k])
+                v[k] = v[k] * 0
+        return segs
+    segs = map_parts(setup_rcv, parts, rows.exchanger.parts_rcv, rows.partition, I, J, V)
+    ex = rows.exchanger
+    got = []
+    for t in range(3):
+        data = map_parts(lambda sg: table_from([x[t] for x in sg], dtype=np.float64 if t == 2 else np.int64), segs)
+        got.append(exchange_tables(data, ex.parts_snd, ex.parts_rcv))
+
+    def setup_snd(s, i, j, v, gi, gj, gv):
+        to_gids_(i, s)
+        i.extend(int(x) for x in gi.data)
+        j.extend(int(x) for x in gj.data)
+        return np.concatenate([np.asarray(v, dtype=np.float64), gv.data.astype(np.float64)])
+    V2 = map_parts(setup_snd, rows.partition, I, J, V, *got)
+    return I, J, V2
+
+
+def fem_sa_problem(parts: PData, nx=10):
+    """test_fem_sa.jl:7-132 (2D Q1 FE, Dirichlet u = 1): returns (A, b, x0, x̂)."""
+    lx = 2.0
+    ns = (nx, nx)
+    h = lx / nx
+    Ae = np.array([[4.0, -1.0, -1.0, -2.0], [-1.0, 4.0, -2.0, -1.0],
+                   [-1.0, -2.0, 4.0, -1.0], [-2.0, -1.0, -1.0, 4.0]])
+    Ae = (h / 6) * Ae
+    nsn = (nx + 1, nx + 1)
+    cart = len(parts.shape) == 2
+    cells = prange_cartesian(parts, ns) if cart else prange_linear(parts, nx * nx)
+    enodes = [(1, 1), (2, 1), (1, 2), (2, 2)]  # CartesianIndices((2,2)), first index fastest
+
+    def coo(s):
+        I, J, V = [], [], []
+        for ocell in s.oid_to_lid:
+            gcell = s.lid_to_gid[ocell - 1]
+            cc = cartesian_index(ns, gcell)
+            for erow, ce in enumerate(enodes):
+                cg = (cc[0] + ce[0] - 1, cc[1] + ce[1] - 1)
+                grow = linear_index(nsn, cg)
+                if any(c == 1 or c == nx + 1 for c in cg):
+                    I.append(grow); J.append(grow); V.append(1.0)
+                else:
+                    for ecol, cf in enumerate(enodes):
+                        cgc = (cc[0] + cf[0] - 1, cc[1] + cf[1] - 1)
+                        I.append(grow); J.append(linear_index(nsn, cgc)); V.append(Ae[erow, ecol])
+        return I, J, V
+    I, J, V = unzip(map_parts(coo, cells.partition), 3)
+    rows = prange_cartesian(parts, nsn) if cart else prange_linear(parts, nsn[0] * nsn[1])
+    cols = prange_cartesian(parts, nsn) if cart else prange_linear(parts, nsn[0] * nsn[1])
+    add_gids_(rows, I)
+    I, J, V = assemble_coo_(I, J, V, rows)
+    b = pvector_undef(rows)
+
+    def fill_b(bv, s, sc):
+        for ocell in sc.oid_to_lid:
+            cc = cartesian_index(ns, sc.lid_to_gid[ocell - 1])
+            for ce in enodes:
+                cg = (cc[0] + ce[0] - 1, cc[1] + ce[1] - 1)
+                if any(c == 1 or c == nx + 1 for c in cg):
+                    lid = s.gid_to_lid[linear_index(nsn, cg)]
+                    bv[lid - 1] += 1.0
+    map_parts(fill_b, b.values, rows.partition, cells.partition)
+    add_gids_(cols, J)
+    A = psparse_from_coo(I, J, V, rows, cols, ids="global")
+    assemble_(b)
+    x0 = pvector_undef(cols)
+    xh = pvector_undef(cols)
+
+    def init(xv, hv, s):
+        for lid in s.oid_to_lid:
+            cg = cartesian_index(nsn, s.lid_to_gid[lid - 1])
+            hv[lid - 1] = 1.0
+            if any(c == 1 or c == nx + 1 for c in cg):
+                xv[lid - 1] = 1.0
+    map_parts(init, x0.values, xh.values, cols.partition)
+    return A, b, x0, xh
+
+
 def q1_hex_ke(h):
     """3D Q1 stiffness h*(K1⊗M1⊗M1 + M1⊗K1⊗M1 + M1⊗M1⊗K1) (SURVEY.md §8d,
     the 3D analogue of test_fem_sa.jl:17-22's element matrix), Julia's kron

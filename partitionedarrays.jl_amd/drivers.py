@@ -18,7 +18,7 @@ import ctypes as C
 import numpy as np
 
 from . import _lib
-from .backends import PData, map_parts
+from .backends import PData, map_parts, unzip
 from .device import DeviceMatrix, contexts
 from .prange import (PRange, add_gids, box_of_part, cartesian_gid_to_part, exchanger_from_ids,
                      linear_index, prange_cartesian, prange_linear, to_lids_)
@@ -92,6 +92,84 @@ def fdm_host(parts: PData, nx=10):
         return np.where(bnd & own, xi[:, 0] + xi[:, 1], 0.0)
     x0h = map_parts(x0v, cols.partition)
     return rows, cols, I, J, V, bh, xh, x0h
+
+
+# ---------------------------------------------------------------------------
+# test_fem_sa.jl
+
+def fem_sa_host(parts: PData, nx=10):
+    """Host setup of test_fem_sa.jl:7-132 (2D Q1 FE, u = 1): cells, COO of
+    the owned cells, add_gids!(rows, I), async_assemble!(I, J, V, rows), the
+    rhs b filled through global ids (ghost rows included, before assemble!),
+    add_gids!(cols, J).  Returns rows, cols, I, J, V (global ids), b (host,
+    not yet assembled), x0 and x̂ (host, on cols)."""
+    from .prange import add_gids_, assemble_coo_, prange_cartesian, prange_linear
+    lx = 2.0
+    ns = (nx, nx)
+    h = lx / nx
+    Ae = (h / 6) * np.array([[4.0, -1.0, -1.0, -2.0], [-1.0, 4.0, -2.0, -1.0],
+                             [-1.0, -2.0, 4.0, -1.0], [-2.0, -1.0, -1.0, 4.0]])
+    nsn = (nx + 1, nx + 1)
+    cart = len(parts.shape) == 2
+    cells = prange_cartesian(parts, ns) if cart else prange_linear(parts, nx * nx)
+    enodes = [(0, 0), (1, 0), (0, 1), (1, 1)]  # CartesianIndices((2,2)), x fastest
+
+    def node_gid(cx, cy):
+        return 1 + cx + nsn[0] * cy
+
+    def cell_nodes(gcell):
+        cx, cy = (gcell - 1) % nx, (gcell - 1) // nx
+        return [(cx + ex, cy + ey) for ex, ey in enodes]
+
+    def on_boundary(c):
+        return c[0] in (0, nx) or c[1] in (0, nx)
+
+    def coo(s):
+        I, J, V = [], [], []
+        for ocell in s.oid_to_lid:
+            nodes = cell_nodes(int(s.lid_to_gid[ocell - 1]))
+            for erow, nr in enumerate(nodes):
+                grow = node_gid(*nr)
+                if on_boundary(nr):
+                    I.append(grow); J.append(grow); V.append(1.0)
+                else:
+                    for ecol, nc in enumerate(nodes):
+                        I.append(grow); J.append(node_gid(*nc)); V.append(Ae[erow, ecol])
+        return np.array(I, np.int64), np.array(J, np.int64), np.array(V)
+    I, J, V = unzip(map_parts(coo, cells.partition), 3)
+    mk = (lambda: prange_cartesian(parts, nsn)) if cart else (lambda: prange_linear(parts, nsn[0] * nsn[1]))
+    rows, cols = mk(), mk()
+    add_gids_(rows, I)
+    I, J, V = assemble_coo_(I, J, V, rows)
+
+    def fill_b(s, sc):
+        bv = np.zeros(s.num_lids)
+        for ocell in sc.oid_to_lid:
+            for nr in cell_nodes(int(sc.lid_to_gid[ocell - 1])):
+                if on_boundary(nr):
+                    bv[s.to_lids([node_gid(*nr)])[0] - 1] += 1.0  # u(x) = 1
+        return bv
+    bh = map_parts(fill_b, rows.partition, cells.partition)
+    add_gids_(cols, J)
+
+    def init(s):
+        g = s.lid_to_gid - 1
+        bnd = (g % nsn[0] == 0) | (g % nsn[0] == nx) | (g // nsn[0] == 0) | (g // nsn[0] == nx)
+        own = s.lid_to_part == s.part
+        return np.where(own & bnd, 1.0, 0.0), np.where(own, 1.0, 0.0)
+    x0h, xh = unzip(map_parts(init, cols.partition), 2)
+    return rows, cols, I, J, V, bh, x0h, xh
+
+
+def fem_sa_problem(parts: PData, nx=10):
+    """test_fem_sa.jl on HIP parts: the PSparseMatrix from the assembled COO
+    (ids=:global) and b assembled on the device (assemble!, Interfaces.jl:2101)."""
+    rows, cols, I, J, V, bh, x0h, xh = fem_sa_host(parts, nx)
+    A = PSparseMatrix.from_coo(I, J, V, rows, cols, ids="global")
+    b = PVector.from_host(bh, rows)
+    from .pvector import assemble_
+    assemble_(b)
+    return A, b, PVector.from_host(x0h, cols), PVector.from_host(xh, cols)
 
 
 # ---------------------------------------------------------------------------

@@ -406,6 +406,38 @@ def add_gids(a: PRange, gids: PData, i_to_part: PData = None, neighbors=None) ->
     return add_gids_(a.copy(), gids, i_to_part, neighbors)
 
 
+def assemble_coo_(I: PData, J: PData, V: PData, rows: PRange):
+    """async_assemble!(I, J, V, rows) + wait (Interfaces.jl:2406-2492), host
+    setup: triplets whose row (global id, present in rows) is owned by another
+    part are sent to that owner — segments in rows.exchanger.parts_rcv order,
+    input order inside — their local value is set to zero and kept; received
+    triplets are appended in the receive order.  I, J stay global ids."""
+    def setup(s, prcv, i, j, v):
+        i = np.asarray(i, np.int64)
+        j = np.asarray(j, np.int64)
+        v = np.asarray(v).copy()
+        owner = s.lid_to_part[s.to_lids(i) - 1]
+        remote = owner != s.part
+        seg = np.searchsorted(prcv, owner[remote])
+        o = np.argsort(seg, kind="stable")
+        gi, gj, gv = i[remote][o], j[remote][o], v[remote][o]
+        bounds = np.concatenate([[0], np.cumsum(np.bincount(seg, minlength=len(prcv)))]).astype(np.int64)
+        msgs = [(gi[a:b], gj[a:b], gv[a:b]) for a, b in zip(bounds[:-1], bounds[1:])]
+        v[remote] = 0
+        return (i, j, v), msgs
+    local, msgs = unzip(map_parts(setup, rows.partition, rows.exchanger.parts_rcv, I, J, V), 2)
+    got = exchange(msgs, rows.exchanger.parts_snd, rows.exchanger.parts_rcv)
+
+    def append(loc, g):
+        i, j, v = loc
+        if g:
+            i = np.concatenate([i] + [m[0] for m in g])
+            j = np.concatenate([j] + [m[1] for m in g])
+            v = np.concatenate([v] + [m[2] for m in g])
+        return i, j, v
+    return unzip(map_parts(append, local, got), 3)
+
+
 def to_lids_(ids: PData, a: PRange) -> PData:
     """to_lids! (Interfaces.jl:1541-1543)"""
     def f(g, s):

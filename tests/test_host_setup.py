@@ -147,3 +147,22 @@ def test_fdm_host_matches_oracle(pamd, O, nparts):
         assert np.array_equal(bh.local(p), ob.values[p])
         assert np.array_equal(xh.local(p), oxh.values[p])
         assert np.array_equal(x0h.local(p), ox0.values[p])
+
+
+@pytest.mark.parametrize("nparts", [4, (2, 2)])
+def test_fem_sa_host_matches_oracle(pamd, O, nparts):
+    """test_fem_sa.jl setup: COO assembly (async_assemble!), rows/cols ghost
+    layers and the local CSCs equal the oracle's."""
+    parts = pamd.sequential.get_part_ids(nparts)
+    rows, cols, I, J, V, bh, x0h, xh = pamd.drivers.fem_sa_host(parts, 10)
+    oparts = O.get_part_ids(nparts)
+    OA, ob, ox0, oxh = O.fem_sa_problem(oparts, 10)
+    for p in parts.part_ids:
+        r, c = rows.partition.local(p), cols.partition.local(p)
+        assert r.lid_to_gid.tolist() == OA.rows.partition[p].lid_to_gid
+        assert c.lid_to_gid.tolist() == OA.cols.partition[p].lid_to_gid
+        M = pamd.compresscoo(r.to_lids(I.local(p)), c.to_lids(J.local(p)), V.local(p), r.num_lids, c.num_lids)
+        OM = OA.values[p]
+        assert np.array_equal(M.colptr, OM.colptr) and np.array_equal(M.rowval, OM.rowval)
+        assert np.array_equal(M.nzval, OM.nzval)
+        assert np.array_equal(x0h.local(p)[c.oid_to_lid - 1], ox0.values[p][c.oid_to_lid - 1])
