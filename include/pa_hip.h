@@ -154,6 +154,22 @@ int pa_spmv_all(int n, pa_mat* const A[], pa_vec* const y[],
                 pa_vec* const x[], const pa_index* const x_idx[],
                 pa_xchg* const xg[], const void* alpha, const void* beta);
 
+/* CG fusions (the caller of the hot path, IterativeSolvers.cg! at
+ * test_fdm.jl:115 / test_fem_sa.jl:135):
+ * pa_spmv_dot_all = mul!(c, A, u) followed by dot(u, c), the dot being
+ * accumulated by the SpMV kernel over the owned rows it writes (u = x must
+ * have contiguous owned lids); pa_cg_update_all = x .+= α.*u; r .-= α.*c
+ * (all lids; the four vectors share one partition) and returns norm(r). */
+int pa_spmv_dot_all(int n, pa_mat* const A[], pa_vec* const y[],
+                    const pa_index* const y_idx[],
+                    pa_vec* const x[], const pa_index* const x_idx[],
+                    pa_xchg* const xg[], const void* alpha, const void* beta,
+                    void* dot_result);
+int pa_cg_update_all(int n, pa_vec* const x[], pa_vec* const r[],
+                     const pa_vec* const u[], const pa_vec* const c[],
+                     const pa_index* const idx[], const void* alpha,
+                     double* rnorm);
+
 /* exchange!(combine, values, exchanger) (Interfaces.jl:846-889) for the n
  * local parts; reverse != 0 uses reverse(exchanger) (Interfaces.jl:796).
  * With reverse=1, op=PA_ADD and zero_ghosts=1 this is assemble!(v)

@@ -58,6 +58,8 @@ _SIGS = {
     "pa_mat_format_info": [_p, _i64p, _i64p, _i64p, _i64p],
     "pa_mat_stencil": [_p, C.c_int, C.c_int, _i64p, _i64p, _i64p, C.c_int64, _i32p, C.POINTER(C.c_double), C.c_int, C.POINTER(_p)],
     "pa_spmv_all": [C.c_int, C.POINTER(_p), C.POINTER(_p), C.POINTER(_p), C.POINTER(_p), C.POINTER(_p), C.POINTER(_p), _p, _p],
+    "pa_spmv_dot_all": [C.c_int, C.POINTER(_p), C.POINTER(_p), C.POINTER(_p), C.POINTER(_p), C.POINTER(_p), C.POINTER(_p), _p, _p, _p],
+    "pa_cg_update_all": [C.c_int, C.POINTER(_p), C.POINTER(_p), C.POINTER(_p), C.POINTER(_p), C.POINTER(_p), _p, C.POINTER(C.c_double)],
     "pa_exchange_all": [C.c_int, C.POINTER(_p), C.POINTER(_p), C.POINTER(_p), C.c_int, C.c_int, C.c_int],
     "pa_dot_all": [C.c_int, C.POINTER(_p), C.POINTER(_p), C.POINTER(_p), C.POINTER(_p), _p],
     "pa_norm2_all": [C.c_int, C.POINTER(_p), C.POINTER(_p), _p],

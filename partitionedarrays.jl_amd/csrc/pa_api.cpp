@@ -22,12 +22,15 @@ void set_error(const std::string& msg) { g_err = msg; }
 // kernels (pa_spmv.hip, pa_kernels.hip)
 void launch_spmv_part(int which, int64_t nwork, const int32_t* list, const pa_mat* A, const void* x,
                       void* y, const int32_t* ymap, bool has_alpha, int bmode, const void* alpha,
-                      const void* beta, hipStream_t st);
+                      const void* beta, void* dotp, hipStream_t st);
 void launch_pattern_detect(pa_mat* A, int64_t noids, int32_t* kind, int32_t* plen, int32_t* pat,
                            uint64_t* mask, int32_t* pghost, int32_t* nirreg, hipStream_t st);
 void launch_side_len(pa_mat* A, int64_t n, const int32_t* rows, int32_t* len, int64_t noids,
                      int32_t* sghost, hipStream_t st);
 void launch_side_fill(pa_mat* A, const int32_t* rows, const int32_t* len, hipStream_t st);
+void launch_fold(int cplx, int nb, const void* in, void* out, hipStream_t st);
+void launch_cg_xr(int dtype, int64_t n, int64_t noids, const int32_t* own, void* x, void* r, const void* u,
+                  const void* c, const void* alpha, double* part, int nb, hipStream_t st);
 extern int g_spmv_format;
 void launch_pack(int dtype, int64_t n, const int32_t* lids, const void* v, void* buf,
                  hipStream_t st);
@@ -303,12 +306,14 @@ int transport(int n, pa_xchg* const xg[], int dtype, int dir) {
       for (size_t k = 0; k < psnd.size(); ++k) {
         if (L.find(psnd[k]) >= 0) continue;
         const size_t cnt = (size_t)(osnd[k + 1] - osnd[k]) * S;
+        if (cnt == 0) continue;  // the peer's matching segment is empty too (SequentialBackend.jl:187)
         ncclResult_t r = ncclSend(bsnd + osnd[k] * S, cnt, ncclUint8, psnd[k] - 1, comm, c->s_comm);
         if (r != ncclSuccess) { ncclGroupEnd(); PA_FAIL(std::string("ncclSend: ") + ncclGetErrorString(r)); }
       }
       for (size_t k = 0; k < prcv.size(); ++k) {
         if (L.find(prcv[k]) >= 0) continue;
         const size_t cnt = (size_t)(orcv[k + 1] - orcv[k]) * S;
+        if (cnt == 0) continue;
         ncclResult_t r = ncclRecv(brcv + orcv[k] * S, cnt, ncclUint8, prcv[k] - 1, comm, c->s_comm);
         if (r != ncclSuccess) { ncclGroupEnd(); PA_FAIL(std::string("ncclRecv: ") + ncclGetErrorString(r)); }
       }
@@ -814,7 +819,7 @@ int pa_mat_destroy(pa_mat* A) {
   dev_free(A->d_val);
   for (void* p : {(void*)A->d_kind, (void*)A->d_plen, (void*)A->d_pat, (void*)A->d_mask,
                   (void*)A->d_pint_list, (void*)A->d_pbnd_list, (void*)A->d_s_off, (void*)A->d_s_len,
-                  (void*)A->d_s_col, A->d_s_val, (void*)A->d_s_rowmap, (void*)A->d_s_rowlen})
+                  (void*)A->d_s_col, A->d_s_val, (void*)A->d_s_rowmap, (void*)A->d_s_rowlen, A->d_dotp})
     dev_free(p);
   delete A;
   return 0;
@@ -842,12 +847,26 @@ int pa_mat_info(const pa_mat* A, int64_t* nrows, int64_t* nnz, int64_t* slots, i
 }
 
 // ---------------------------------------------------------------------------
-int pa_spmv_all(int n, pa_mat* const A[], pa_vec* const y[], const pa_index* const y_idx[],
-                pa_vec* const x[], const pa_index* const x_idx[], pa_xchg* const xg[],
-                const void* alpha, const void* beta) {
+// mul! for the n local parts; with want_dot each part's dot(x, y) over its
+// owned rows is accumulated by the SpMV kernel itself (per-slice partials in
+// A->d_dotp, folded by fold_dot) — the CG's `dot(u, c)` after `mul!(c, A, u)`.
+static int spmv_impl(int n, pa_mat* const A[], pa_vec* const y[], const pa_index* const y_idx[],
+                     pa_vec* const x[], const pa_index* const x_idx[], pa_xchg* const xg[],
+                     const void* alpha, const void* beta, bool want_dot) {
   CHECK_ARG(n >= 1 && A && y && x && alpha && beta, "null argument");
   const int dt = A[0]->dtype;
   bool any_x = false;
+  std::vector<void*> dotp(n, nullptr);
+  if (want_dot) {
+    for (int i = 0; i < n; ++i) {
+      CHECK_ARG(x_idx && x_idx[i] && x_idx[i]->own_contig, "fused dot needs b with contiguous owned lids");
+      if (!A[i]->d_dotp) {
+        HIPC(hipSetDevice(A[i]->ctx->device));
+        HIPC(hipMalloc(&A[i]->d_dotp, std::max<int64_t>(A[i]->nslices + A[i]->s_nslices, 1) * 16));
+      }
+      dotp[i] = A[i]->d_dotp;
+    }
+  }
   for (int i = 0; i < n; ++i) {
     CHECK_ARG(A[i] && y[i] && x[i], "null handle");
     CHECK_ARG(A[i]->dtype == dt && y[i]->dtype == dt && x[i]->dtype == dt, "mul!: element types differ");
@@ -885,12 +904,12 @@ int pa_spmv_all(int n, pa_mat* const A[], pa_vec* const y[], const pa_index* con
     if (c->timing) HIPC(hipEventRecord(c->ev_t[0], c->s_main));
     // interior slices (no ghost column): overlap with the halo transport
     if (g_spmv_format == 1 && A[i]->has_pat) {
-      launch_spmv_part(0, A[i]->np_int, A[i]->d_pint_list, A[i], x[i]->d, y[i]->d, ymap, has_alpha, bmode, alpha, beta, c->s_main);
+      launch_spmv_part(0, A[i]->np_int, A[i]->d_pint_list, A[i], x[i]->d, y[i]->d, ymap, has_alpha, bmode, alpha, beta, dotp[i], c->s_main);
     } else if (A[i]->d_bnd_list) {  // split layout (the interior list may be empty)
       if (A[i]->nslices_int > 0)
-        launch_spmv_part(1, A[i]->nslices_int, A[i]->d_int_list, A[i], x[i]->d, y[i]->d, ymap, has_alpha, bmode, alpha, beta, c->s_main);
+        launch_spmv_part(1, A[i]->nslices_int, A[i]->d_int_list, A[i], x[i]->d, y[i]->d, ymap, has_alpha, bmode, alpha, beta, dotp[i], c->s_main);
     } else {
-      launch_spmv_part(1, A[i]->nslices, nullptr, A[i], x[i]->d, y[i]->d, ymap, has_alpha, bmode, alpha, beta, c->s_main);
+      launch_spmv_part(1, A[i]->nslices, nullptr, A[i], x[i]->d, y[i]->d, ymap, has_alpha, bmode, alpha, beta, dotp[i], c->s_main);
     }
     if (c->timing) HIPC(hipEventRecord(c->ev_t[1], c->s_main));
   }
@@ -907,11 +926,16 @@ int pa_spmv_all(int n, pa_mat* const A[], pa_vec* const y[], const pa_index* con
     const int32_t* ymap = y_idx[i]->own_contig ? nullptr : y_idx[i]->d_oid_to_lid;
     if (g_spmv_format == 1 && A[i]->has_pat) {
       // pattern slices reading ghosts, then the side rows (after the halo)
-      launch_spmv_part(0, A[i]->np_bnd, A[i]->d_pbnd_list, A[i], x[i]->d, y[i]->d, ymap, has_alpha, bmode, alpha, beta, c->s_main);
-      launch_spmv_part(2, A[i]->s_nslices, nullptr, A[i], x[i]->d, y[i]->d, ymap, has_alpha, bmode, alpha, beta, c->s_main);
+      launch_spmv_part(0, A[i]->np_bnd, A[i]->d_pbnd_list, A[i], x[i]->d, y[i]->d, ymap, has_alpha, bmode, alpha, beta, dotp[i], c->s_main);
+      launch_spmv_part(2, A[i]->s_nslices, nullptr, A[i], x[i]->d, y[i]->d, ymap, has_alpha, bmode, alpha, beta, dotp[i], c->s_main);
     } else if (A[i]->d_bnd_list) {
       launch_spmv_part(1, A[i]->nslices - A[i]->nslices_int, A[i]->d_bnd_list, A[i], x[i]->d, y[i]->d, ymap,
-                       has_alpha, bmode, alpha, beta, c->s_main);
+                       has_alpha, bmode, alpha, beta, dotp[i], c->s_main);
+    }
+    if (want_dot) {  // fold the slice partials (main, then side in pattern mode) in order
+      const bool pat = g_spmv_format == 1 && A[i]->has_pat;
+      const bool cplx = dt == PA_C64 || dt == PA_C128;
+      launch_fold(cplx, (int)(A[i]->nslices + (pat ? A[i]->s_nslices : 0)), A[i]->d_dotp, c->d_result, c->s_main);
     }
     if (c->timing) HIPC(hipEventRecord(c->ev_t[3], c->s_main));
   }
@@ -973,37 +997,17 @@ int pa_exchange_all(int n, pa_vec* const v[], pa_xchg* const xg[], const pa_inde
 // ---------------------------------------------------------------------------
 namespace {
 
-// kind 0: dot, 1: sum |a|^2, 2: sum a.  Leaves each part's accumulator
-// (double / c128) in host memory `vals` (one per part id 1..P, folded in
-// part order by the caller), covering remote parts through RCCL all-gather.
-int reduce_all(int n, const pa_vec* const a[], const pa_index* const ia[], const pa_vec* const b[],
-               const pa_index* const ib[], int kind, std::vector<c128>* vals) {
-  CHECK_ARG(n >= 1 && a && ia, "null argument");
-  const int dt = a[0]->dtype;
-  const bool cplx = dt == PA_C64 || dt == PA_C128;
-  const int P = a[0]->ctx->nparts;
+// Each local part's d_result (double / c128 accumulator) → host, one entry
+// per part id 1..P (RCCL all-gather when parts live in other processes).
+int gather_results(int n, pa_ctx* const* ctxs, bool cplx, std::vector<c128>* vals) {
+  const int P = ctxs[0]->nparts;
   vals->assign(P, c128{0.0, 0.0});
   std::vector<char> have(P, 0);
-  bool remote_mode = false;
-  for (int i = 0; i < n; ++i) {
-    CHECK_ARG(a[i] && ia[i], "null handle");
-    CHECK_ARG(a[i]->dtype == dt, "element types differ across parts");
-    CHECK_ARG(ia[i]->nlids == a[i]->n, "index set does not describe the vector");
-    if (kind == 0) {
-      CHECK_ARG(b && b[i] && ib && ib[i] && b[i]->dtype == dt && ib[i]->nlids == b[i]->n, "dot: second vector");
-      CHECK_ARG(ia[i]->noids == ib[i]->noids, "dot: owned counts differ");
-    }
-    pa_ctx* c = a[i]->ctx;
-    HIPC(hipSetDevice(c->device));
-    launch_reduce(dt, kind, ia[i]->noids, ia[i]->d_oid_to_lid, a[i]->d,
-                  kind == 0 ? ib[i]->d_oid_to_lid : nullptr, kind == 0 ? b[i]->d : nullptr,
-                  c->d_partials, c->d_result, c->s_main);
-    if (c->comm && n == 1 && P > 1) remote_mode = true;
-  }
-  HIPC(hipGetLastError());
+  const bool remote_mode = ctxs[0]->comm && n == 1 && P > 1;
   const size_t accsz = cplx ? 16 : 8;
   if (remote_mode) {
-    pa_ctx* c = a[0]->ctx;
+    pa_ctx* c = ctxs[0];
+    HIPC(hipSetDevice(c->device));
     NCCLC(ncclAllGather(c->d_result, c->d_gather, accsz, ncclUint8, (ncclComm_t)c->comm, c->s_main));
     HIPC(hipMemcpyAsync(c->h_pinned, c->d_gather, accsz * P, hipMemcpyDeviceToHost, c->s_main));
     HIPC(hipStreamSynchronize(c->s_main));
@@ -1015,7 +1019,7 @@ int reduce_all(int n, const pa_vec* const a[], const pa_index* const ia[], const
     }
   } else {
     for (int i = 0; i < n; ++i) {
-      pa_ctx* c = a[i]->ctx;
+      pa_ctx* c = ctxs[i];
       HIPC(hipSetDevice(c->device));
       HIPC(hipMemcpyAsync(c->h_pinned, c->d_result, accsz, hipMemcpyDeviceToHost, c->s_main));
       HIPC(hipStreamSynchronize(c->s_main));
@@ -1030,7 +1034,102 @@ int reduce_all(int n, const pa_vec* const a[], const pa_index* const ia[], const
   return 0;
 }
 
+// kind 0: dot, 1: sum |a|^2, 2: sum a.  Leaves each part's accumulator
+// (double / c128) in host memory `vals` (one per part id 1..P, folded in
+// part order by the caller), covering remote parts through RCCL all-gather.
+int reduce_all(int n, const pa_vec* const a[], const pa_index* const ia[], const pa_vec* const b[],
+               const pa_index* const ib[], int kind, std::vector<c128>* vals) {
+  CHECK_ARG(n >= 1 && a && ia, "null argument");
+  const int dt = a[0]->dtype;
+  const bool cplx = dt == PA_C64 || dt == PA_C128;
+  for (int i = 0; i < n; ++i) {
+    CHECK_ARG(a[i] && ia[i], "null handle");
+    CHECK_ARG(a[i]->dtype == dt, "element types differ across parts");
+    CHECK_ARG(ia[i]->nlids == a[i]->n, "index set does not describe the vector");
+    if (kind == 0) {
+      CHECK_ARG(b && b[i] && ib && ib[i] && b[i]->dtype == dt && ib[i]->nlids == b[i]->n, "dot: second vector");
+      CHECK_ARG(ia[i]->noids == ib[i]->noids, "dot: owned counts differ");
+    }
+    pa_ctx* c = a[i]->ctx;
+    HIPC(hipSetDevice(c->device));
+    launch_reduce(dt, kind, ia[i]->noids, ia[i]->d_oid_to_lid, a[i]->d,
+                  kind == 0 ? ib[i]->d_oid_to_lid : nullptr, kind == 0 ? b[i]->d : nullptr,
+                  c->d_partials, c->d_result, c->s_main);
+  }
+  HIPC(hipGetLastError());
+  std::vector<pa_ctx*> ctxs(n);
+  for (int i = 0; i < n; ++i) ctxs[i] = a[i]->ctx;
+  return gather_results(n, ctxs.data(), cplx, vals);
+}
+
+void store_scalar(int dt, c128 s, void* result) {
+  switch (dt) {
+    case PA_F32: *(float*)result = (float)s.re; break;
+    case PA_F64: *(double*)result = s.re; break;
+    case PA_C64: ((float*)result)[0] = (float)s.re; ((float*)result)[1] = (float)s.im; break;
+    case PA_C128: ((double*)result)[0] = s.re; ((double*)result)[1] = s.im; break;
+  }
+}
+
 }  // namespace
+
+int pa_spmv_all(int n, pa_mat* const A[], pa_vec* const y[], const pa_index* const y_idx[],
+                pa_vec* const x[], const pa_index* const x_idx[], pa_xchg* const xg[],
+                const void* alpha, const void* beta) {
+  return spmv_impl(n, A, y, y_idx, x, x_idx, xg, alpha, beta, false);
+}
+
+int pa_spmv_dot_all(int n, pa_mat* const A[], pa_vec* const y[], const pa_index* const y_idx[],
+                    pa_vec* const x[], const pa_index* const x_idx[], pa_xchg* const xg[],
+                    const void* alpha, const void* beta, void* dot_result) {
+  CHECK_ARG(dot_result, "null result");
+  if (spmv_impl(n, A, y, y_idx, x, x_idx, xg, alpha, beta, true)) return -1;
+  std::vector<pa_ctx*> ctxs(n);
+  for (int i = 0; i < n; ++i) ctxs[i] = A[i]->ctx;
+  const int dt = A[0]->dtype;
+  std::vector<c128> vals;
+  if (gather_results(n, ctxs.data(), dt == PA_C64 || dt == PA_C128, &vals)) return -1;
+  c128 s{0.0, 0.0};
+  for (const auto& v : vals) s = s + v;  // reduce(+; init=0) in part order
+  store_scalar(dt, s, dot_result);
+  return 0;
+}
+
+int pa_cg_update_all(int n, pa_vec* const x[], pa_vec* const r[], const pa_vec* const u[],
+                     const pa_vec* const c[], const pa_index* const idx[], const void* alpha,
+                     double* rnorm) {
+  CHECK_ARG(n >= 1 && x && r && u && c && idx && alpha && rnorm, "null argument");
+  const int dt = x[0]->dtype;
+  std::vector<pa_ctx*> ctxs(n);
+  for (int i = 0; i < n; ++i) {
+    CHECK_ARG(x[i] && r[i] && u[i] && c[i] && idx[i], "null handle");
+    const int64_t m = x[i]->n;
+    CHECK_ARG(r[i]->n == m && u[i]->n == m && c[i]->n == m && idx[i]->nlids == m,
+              "cg update: vectors must share the partition");
+    CHECK_ARG(r[i]->dtype == dt && u[i]->dtype == dt && c[i]->dtype == dt, "cg update: element types differ");
+    pa_ctx* cx = x[i]->ctx;
+    ctxs[i] = cx;
+    HIPC(hipSetDevice(cx->device));
+    if (idx[i]->own_contig) {
+      const int nb = (int)std::min<int64_t>(1024, std::max<int64_t>(1, (m + 255) / 256));
+      launch_cg_xr(dt, m, idx[i]->noids, nullptr, x[i]->d, r[i]->d, u[i]->d, c[i]->d, alpha,
+                   (double*)cx->d_partials, nb, cx->s_main);
+      launch_fold(0, nb, cx->d_partials, cx->d_result, cx->s_main);
+    } else {  // unfused: two broadcasts and the norm reduction
+      launch_axpby(dt, m, nullptr, x[i]->d, u[i]->d, alpha, 1, cx->s_main);
+      launch_axpby(dt, m, nullptr, r[i]->d, c[i]->d, alpha, 2, cx->s_main);
+      launch_reduce(dt, 1, idx[i]->noids, idx[i]->d_oid_to_lid, r[i]->d, nullptr, nullptr, cx->d_partials,
+                    cx->d_result, cx->s_main);
+    }
+  }
+  HIPC(hipGetLastError());
+  std::vector<c128> vals;
+  if (gather_results(n, ctxs.data(), false, &vals)) return -1;
+  double s = 0.0;
+  for (const auto& v : vals) s = s + v.re;
+  *rnorm = std::pow(s, 1.0 / 2.0);
+  return 0;
+}
 
 int pa_dot_all(int n, const pa_vec* const a[], const pa_index* const ia[], const pa_vec* const b[],
                const pa_index* const ib[], void* result) {

@@ -192,4 +192,5 @@ struct pa_mat {
   void* d_s_val = nullptr;
   int32_t* d_s_rowmap = nullptr;
   int32_t* d_s_rowlen = nullptr;
+  void* d_dotp = nullptr;            // fused dot: one partial per (main + side) slice
 };

@@ -293,6 +293,14 @@ static void reduce_t(int64_t n, const int32_t* ma, const void* a, const int32_t*
                      (A*)result);
 }
 
+// fold nb partials (double, or c128 when cplx) in a fixed order into out[0]
+void launch_fold(int cplx, int nb, const void* in, void* out, hipStream_t st) {
+  if (cplx)
+    hipLaunchKernelGGL((k_reduce_final<c128>), dim3(1), dim3(256), 0, st, nb, (const c128*)in, (c128*)out);
+  else
+    hipLaunchKernelGGL((k_reduce_final<double>), dim3(1), dim3(256), 0, st, nb, (const double*)in, (double*)out);
+}
+
 // result: device accumulator (double or c128) of the part's local value
 void launch_reduce(int dtype, int kind, int64_t n, const int32_t* ma, const void* a,
                    const int32_t* mb, const void* b, void* partials, void* result,

@@ -76,7 +76,24 @@ struct SpmvArgs {
   const int32_t* ymap;      // oid → y lid, null: identity
   T alpha, beta;
   int flags;
+  // fused dot(u, c) (CG): u = x indexed by oid (contiguous own layout);
+  // one partial per slice at dotp[dot_base + s] (deterministic fold later)
+  const T* dotu;
+  void* dotp;
+  int64_t dot_base;
 };
+
+template <typename T> struct DAcc { using type = double; };
+template <> struct DAcc<c64> { using type = c128; };
+template <> struct DAcc<c128> { using type = c128; };
+__device__ inline double dacc(float a) { return (double)a; }
+__device__ inline double dacc(double a) { return a; }
+__device__ inline c128 dacc(c64 a) { return c128{(double)a.re, (double)a.im}; }
+__device__ inline c128 dacc(c128 a) { return a; }
+__device__ inline double shfl_down_acc(double v, int d) { return __shfl_down(v, d, 64); }
+__device__ inline c128 shfl_down_acc(c128 v, int d) {
+  return c128{__shfl_down(v.re, d, 64), __shfl_down(v.im, d, 64)};
+}
 
 // int32-column rows: c < 0 is padding (skipped: never multiplied)
 template <typename T, int R, bool ALPHA, bool NT, int U>
@@ -217,6 +234,17 @@ __global__ __launch_bounds__(256) void k_spmv_sell(SpmvArgs<T> a) {
     else rows_int32<T, R, ALPHA, false, U>(acc, cp, vp, len, a.x, a.alpha);
   }
 
+  if (a.dotp) {  // fused dot(u, c): Σ conj(u_i)·c_i over this slice's rows
+    using DA = typename DAcc<T>::type;
+    DA part = zero_of<DA>();
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+      if (ok[r]) part = part + dacc(cdot(a.dotu[orow[r]], acc[r]));
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) part = part + shfl_down_acc(part, d);
+    if (lane == 0) reinterpret_cast<DA*>(a.dotp)[a.dot_base + s] = part;
+  }
+
   bool all = true;
 #pragma unroll
   for (int r = 0; r < R; ++r) all = all && ok[r];
@@ -260,8 +288,11 @@ static void launch_ab(const SpmvArgs<T>& a, bool has_alpha, int bmode, hipStream
 template <typename T, int R>
 static void launch_which(int which, int64_t nwork, const int32_t* list, const pa_mat* A, const void* x,
                          void* y, const int32_t* ymap, bool has_alpha, int bmode, const void* alpha,
-                         const void* beta, hipStream_t st) {
+                         const void* beta, void* dotp, hipStream_t st) {
   SpmvArgs<T> a{};
+  a.dotu = (const T*)x;
+  a.dotp = dotp;
+  a.dot_base = which == 2 ? A->nslices : 0;
   a.nwork = nwork;
   a.list = list;
   a.x = (const T*)x;
@@ -297,12 +328,51 @@ static void launch_which(int which, int64_t nwork, const int32_t* list, const pa
 
 void launch_spmv_part(int which, int64_t nwork, const int32_t* list, const pa_mat* A, const void* x,
                       void* y, const int32_t* ymap, bool has_alpha, int bmode, const void* alpha,
-                      const void* beta, hipStream_t st) {
+                      const void* beta, void* dotp, hipStream_t st) {
   switch (A->dtype) {
-    case PA_F32: launch_which<float, 4>(which, nwork, list, A, x, y, ymap, has_alpha, bmode, alpha, beta, st); break;
-    case PA_F64: launch_which<double, 2>(which, nwork, list, A, x, y, ymap, has_alpha, bmode, alpha, beta, st); break;
-    case PA_C64: launch_which<c64, 2>(which, nwork, list, A, x, y, ymap, has_alpha, bmode, alpha, beta, st); break;
-    case PA_C128: launch_which<c128, 1>(which, nwork, list, A, x, y, ymap, has_alpha, bmode, alpha, beta, st); break;
+    case PA_F32: launch_which<float, 4>(which, nwork, list, A, x, y, ymap, has_alpha, bmode, alpha, beta, dotp, st); break;
+    case PA_F64: launch_which<double, 2>(which, nwork, list, A, x, y, ymap, has_alpha, bmode, alpha, beta, dotp, st); break;
+    case PA_C64: launch_which<c64, 2>(which, nwork, list, A, x, y, ymap, has_alpha, bmode, alpha, beta, dotp, st); break;
+    case PA_C128: launch_which<c128, 1>(which, nwork, list, A, x, y, ymap, has_alpha, bmode, alpha, beta, dotp, st); break;
+  }
+}
+
+// x .+= α.*u; r .-= α.*c (all lids, Interfaces.jl:1710-1737) and the owned
+// Σ|r|² of norm(r) (1767-1772) in one pass (contiguous owned lids
+// 0..noids-1); per-block partials, folded in block order afterwards.
+template <typename T>
+__global__ __launch_bounds__(256) void k_cg_xr(int64_t n, int64_t noids, const int32_t* __restrict__ own,
+                                               T* __restrict__ x, T* __restrict__ r, const T* __restrict__ u,
+                                               const T* __restrict__ c, T alpha, double* __restrict__ part) {
+  (void)own;
+  double s = 0.0;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    x[i] = x[i] + alpha * u[i];
+    const T ri = r[i] - alpha * c[i];
+    r[i] = ri;
+    if (i < noids) s = s + (double)abs2(ri);
+  }
+  for (int d = 32; d >= 1; d >>= 1) s += __shfl_down(s, d, 64);
+  __shared__ double sm[4];
+  if ((threadIdx.x & 63) == 0) sm[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) part[blockIdx.x] = ((sm[0] + sm[1]) + sm[2]) + sm[3];
+}
+
+template <typename T>
+static void cg_xr_t(int64_t n, int64_t noids, const int32_t* own, void* x, void* r, const void* u,
+                    const void* c, const void* alpha, double* part, int nb, hipStream_t st) {
+  hipLaunchKernelGGL(k_cg_xr<T>, dim3(nb), dim3(256), 0, st, n, noids, own, (T*)x, (T*)r, (const T*)u,
+                     (const T*)c, *(const T*)alpha, part);
+}
+
+void launch_cg_xr(int dtype, int64_t n, int64_t noids, const int32_t* own, void* x, void* r, const void* u,
+                  const void* c, const void* alpha, double* part, int nb, hipStream_t st) {
+  switch (dtype) {
+    case PA_F32: cg_xr_t<float>(n, noids, own, x, r, u, c, alpha, part, nb, st); break;
+    case PA_F64: cg_xr_t<double>(n, noids, own, x, r, u, c, alpha, part, nb, st); break;
+    case PA_C64: cg_xr_t<c64>(n, noids, own, x, r, u, c, alpha, part, nb, st); break;
+    case PA_C128: cg_xr_t<c128>(n, noids, own, x, r, u, c, alpha, part, nb, st); break;
   }
 }
 

@@ -283,6 +283,19 @@ class PSparseMatrix:
 def mul_(c: PVector, a: PSparseMatrix, b: PVector, alpha=1.0, beta=0.0) -> PVector:
     """mul!(c, a, b, α, β) (Interfaces.jl:2246-2275): halo exchange of b
     overlapped with the interior slices, then the slices reading ghosts."""
+    _spmv(c, a, b, alpha, beta, None)
+    return c
+
+
+def mul_dot_(c: PVector, a: PSparseMatrix, b: PVector, alpha=1.0, beta=0.0):
+    """mul!(c, a, b, α, β) then dot(b, c), the dot accumulated by the SpMV
+    kernel (pa_spmv_dot_all).  Returns the dot."""
+    out = _scalar_out(a.dtype)
+    _spmv(c, a, b, alpha, beta, out)
+    return out[0].item()
+
+
+def _spmv(c, a, b, alpha, beta, dot_out):
     if not (c.rows is a.rows or oids_are_equal(c.rows, a.rows)):
         raise AssertionError("mul!: c.rows and a.rows own different ids")
     if not (b.rows is a.cols or (oids_are_equal(a.cols, b.rows) and hids_are_equal(a.cols, b.rows))):
@@ -298,9 +311,23 @@ def mul_(c: PVector, a: PSparseMatrix, b: PVector, alpha=1.0, beta=0.0) -> PVect
     xg = [device_exchanger(cx, ex, p) for cx, p in zip(ctxs, b.values.part_ids)] if has_x else None
     al, alp = _lib.scalar_buf(alpha, a.dtype)
     be, bep = _lib.scalar_buf(beta, a.dtype)
-    _lib.call("pa_spmv_all", n, _hs(a.values.parts), _hs(c.values.parts), _lib.ptr_array(_idx(c)),
-              _hs(b.values.parts), _lib.ptr_array(_idx(b)), _hs(xg) if xg else None, alp, bep)
-    return c
+    args = (n, _hs(a.values.parts), _hs(c.values.parts), _lib.ptr_array(_idx(c)),
+            _hs(b.values.parts), _lib.ptr_array(_idx(b)), _hs(xg) if xg else None, alp, bep)
+    if dot_out is None:
+        _lib.call("pa_spmv_all", *args)
+    else:
+        _lib.call("pa_spmv_dot_all", *args, dot_out.ctypes.data_as(C.c_void_p))
+
+
+def cg_update_(x: PVector, r: PVector, u: PVector, c: PVector, alpha) -> float:
+    """x .+= α.*u; r .-= α.*c; norm(r) in one pass (pa_cg_update_all)."""
+    if not (x.rows is r.rows is u.rows is c.rows):
+        raise ValueError("cg_update_: the four vectors must share one PRange")
+    al, alp = _lib.scalar_buf(alpha, x.dtype)
+    out = C.c_double(0.0)
+    _lib.call("pa_cg_update_all", len(x.values.parts), _hs(x.values.parts), _hs(r.values.parts),
+              _hs(u.values.parts), _hs(c.values.parts), _lib.ptr_array(_idx(x)), alp, C.byref(out))
+    return out.value
 
 
 def matvec(a: PSparseMatrix, b: PVector) -> PVector:
@@ -309,8 +336,13 @@ def matvec(a: PSparseMatrix, b: PVector) -> PVector:
     return mul_(c, a, b)
 
 
+def _own_contig(v: PVector) -> bool:
+    return all(s.num_oids == 0 or (s.oid_to_lid[0] == 1 and s.oid_to_lid[-1] == s.num_oids)
+               for s in v.rows.partition.parts)
+
+
 def cg_(x: PVector, A: PSparseMatrix, b: PVector, reltol=None, abstol=0.0, maxiter=None,
-        history=None):
+        history=None, fused=True):
     """IterativeSolvers.cg! (v0.9; caller of the hot path at test_fdm.jl:115,
     test_fem_sa.jl:135), restated over the device operations:
     u = zero(x); r, c = similar(x); copyto!(r, b); mul!(c, A, x); r .-= c;
@@ -332,15 +364,24 @@ def cg_(x: PVector, A: PSparseMatrix, b: PVector, reltol=None, abstol=0.0, maxit
     tol = max(reltol * norm(b), abstol)
     prev = 1.0
     it = 0
+    # fusions (same arithmetic per element; reduction orders are this
+    # library's deterministic ones): dot(u,c) inside the SpMV, and
+    # x/r updates + norm(r) in one pass
+    fuse = fused and _own_contig(u) and (x.rows is r.rows is u.rows is c.rows)
     while not (it >= maxiter or residual <= tol):
         beta = residual ** 2 / prev ** 2
         xpby_(u, r, beta)
-        mul_(c, A, u)
-        alpha = residual ** 2 / dot(u, c)
-        axpy_(x, alpha, u)
-        axmy_(r, alpha, c)
+        if fuse:
+            alpha = residual ** 2 / mul_dot_(c, A, u)
+            new = cg_update_(x, r, u, c, alpha)
+        else:
+            mul_(c, A, u)
+            alpha = residual ** 2 / dot(u, c)
+            axpy_(x, alpha, u)
+            axmy_(r, alpha, c)
+            new = norm(r)
         prev = residual
-        residual = norm(r)
+        residual = new
         it += 1
         if history is not None:
             history.append(residual)

@@ -36,6 +36,65 @@ def test_fem_sa_cg(be, pamd, O, nparts):
     np.testing.assert_allclose(hist, ohist, rtol=1e-8)
 
 
+@pytest.mark.parametrize("fmt", [1, 0])
+@pytest.mark.parametrize("shape,N,dtype", [((2, 2, 1), (12, 10, 9), np.float64), ((1, 1, 1), (9, 8, 7), np.float64),
+                                           ((2, 1, 2), (10, 7, 9), np.complex128), ((2, 1, 1), (9, 9, 9), np.float32)])
+def test_fused_cg_kernels(be, pamd, O, fmt, shape, N, dtype):
+    """pa_spmv_dot_all: c bit-exact, dot(u,c) to 1e-12; pa_cg_update_all:
+    x, r bit-exact against the broadcasts, norm(r) to 1e-12."""
+    prev = pamd._lib.tune("spmv_format", fmt)
+    try:
+        parts = be.get_part_ids(shape)
+        A = pamd.drivers.stencil_operator(parts, N, 27, dtype)
+        cols = A.cols
+        rng = np.random.default_rng(9)
+
+        def rnd(s):
+            v = rng.uniform(-1, 1, s.num_lids)
+            if np.dtype(dtype).kind == "c":
+                v = v + 1j * rng.uniform(-1, 1, s.num_lids)
+            return v.astype(dtype)
+        vals = {k: {p: rnd(cols.partition.local(p)) for p in parts.part_ids} for k in "xruc"}
+        mk = lambda k: pamd.PVector.from_host(pamd.map_parts(lambda s: vals[k][s.part], cols.partition), cols)
+        u, c = mk("u"), mk("c")
+        d = pamd.mul_dot_(c, A, u)
+        c2 = mk("c")
+        pamd.mul_(c2, A, u)
+        d2 = pamd.dot(u, c2)
+        for p in parts.part_ids:
+            assert np.array_equal(c.to_host().local(p), c2.to_host().local(p))
+        tol = 1e-5 if dtype == np.float32 else 1e-12
+        assert abs(d - d2) <= tol * abs(d2)
+        x, r = mk("x"), mk("r")
+        x2, r2 = mk("x"), mk("r")
+        alpha = np.asarray(0.37 + (0.11j if np.dtype(dtype).kind == "c" else 0), dtype=dtype).item()
+        nr = pamd.cg_update_(x, r, u, c, alpha)
+        pamd.axpy_(x2, alpha, u)
+        pamd.axmy_(r2, alpha, c)
+        nr2 = pamd.norm(r2)
+        for p in parts.part_ids:
+            assert np.array_equal(x.to_host().local(p), x2.to_host().local(p))
+            assert np.array_equal(r.to_host().local(p), r2.to_host().local(p))
+        assert abs(nr - nr2) <= tol * nr2
+    finally:
+        pamd._lib.tune("spmv_format", prev)
+
+
+@pytest.mark.parametrize("fused", [True, False])
+def test_fdm_cg_fused_and_unfused(be, pamd, O, fused):
+    parts = be.get_part_ids((2, 2, 2))
+    A, b, x0, xh = pamd.drivers.fdm_problem(parts, 10)
+    x = x0.copy()
+    hist = []
+    pamd.cg_(x, A, b, history=hist, fused=fused)
+    OA, ob, ox0, oxh = O.fdm_problem(O.get_part_ids((2, 2, 2)), 10)
+    ox = O.PVector(O.map_parts(lambda v: v.copy(), ox0.values), ox0.rows)
+    ohist = []
+    O.cg_(ox, OA, ob, log=ohist)
+    assert len(hist) == len(ohist)
+    np.testing.assert_allclose(hist, ohist, rtol=1e-8)
+
+
 def test_interfaces_diag_matvec_kat(be, pamd):
     """test_interfaces.jl:646-680 on the irregular IndexSet partition (non
     contiguous owned lids on some parts): A = 2I, x = 3 → 6 (owned, then all
