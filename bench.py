@@ -102,6 +102,52 @@ def child_pmc(args):
     be.context(1).sync()
 
 
+def cg_mode(args, pamd, backend, parts, A, ngpu, world, sync):
+    """--cg K: IterativeSolvers.cg! iterations (BASELINE config 4) on the same
+    operator: per iteration 1 mul! (+halo), dot, norm, 3 broadcasts.  Prints
+    its own JSON line (not the headline metric)."""
+    import torch
+    import torch.distributed as dist
+    cols = A.cols
+    dtype = A.dtype
+    b = pamd.PVector.from_host(pamd.map_parts(
+        lambda s: np.random.default_rng(7 + s.part).uniform(-1, 1, s.num_lids).astype(dtype), cols.partition), cols)
+    out = {}
+    for fused in (True, False):
+        x = pamd.PVector.undef(cols, dtype).fill_(0)
+        pamd.cg_(x, A, b, reltol=0.0, maxiter=args.warmup, fused=fused)
+        sync()
+        if world > 1:
+            dist.barrier()
+        x = pamd.PVector.undef(cols, dtype).fill_(0)
+        t0 = time.perf_counter()
+        hist = []
+        pamd.cg_(x, A, b, reltol=0.0, maxiter=args.cg, fused=fused, history=hist)
+        sync()
+        el = time.perf_counter() - t0
+        if world > 1:
+            t = torch.tensor([el], dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el = float(t.item())
+        out[fused] = (1e3 * el / max(1, len(hist)), len(hist), hist[-1] if hist else None)
+    p0 = parts.part_ids[0]
+    info = A.values.local(p0).info()
+    S = np.dtype(dtype).itemsize
+    n = info["nrows"]
+    it_bytes = (info["nnz"] * (S + 4) + (n + 1) * 4 + 2 * n * S) + 12 * n * S  # SpMV + dot 2 + norm 1 + 3 axpy x3
+    rows_all = n * ngpu
+    line = {"metric": "CG iteration time (weak scaling, BASELINE config 4)",
+            "value": round(out[True][0], 4), "unit": "ms/iteration", "higher_is_better": False,
+            "n_gpus": ngpu, "iterations": out[True][1], "scaling": "weak",
+            "dtype": args.dtype, "data": "synthetic (seeded uniform b, x0 = 0)",
+            "config": {"workload": f"cg! on the {args.kind}-pt operator, {args.n}^3 nodes per GPU",
+                       "dofs": rows_all, "unfused_ms_per_iteration": round(out[False][0], 4),
+                       "algorithmic_bytes_per_iteration_per_gpu": it_bytes,
+                       "gbs_per_gpu_fused": round(it_bytes / (out[True][0] * 1e-3) / 1e9, 1),
+                       "final_residual": out[True][2]}}
+    return line
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -114,6 +160,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 HBM-traffic passes")
     ap.add_argument("--child-pmc", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--cg", type=int, default=0, help="time K CG iterations instead (own JSON line)")
     args = ap.parse_args()
     if args.child_pmc:
         return child_pmc(args)
@@ -175,6 +222,14 @@ def main():
     def barrier():
         if world > 1:
             dist.barrier()
+
+    if args.cg > 0:
+        line = cg_mode(args, pamd, backend, parts, A, ngpu, world, sync)
+        if rank == 0:
+            print(json.dumps(line), flush=True)
+        if world > 1:
+            dist.destroy_process_group()
+        return
 
     for _ in range(args.warmup):
         pamd.mul_(y, A, x)

@@ -28,7 +28,7 @@ void launch_pattern_detect(pa_mat* A, int64_t noids, int32_t* kind, int32_t* ple
 void launch_side_len(pa_mat* A, int64_t n, const int32_t* rows, int32_t* len, int64_t noids,
                      int32_t* sghost, hipStream_t st);
 void launch_side_fill(pa_mat* A, const int32_t* rows, const int32_t* len, hipStream_t st);
-void launch_fold(int cplx, int nb, const void* in, void* out, hipStream_t st);
+void launch_fold(int cplx, int nb, const void* in, void* scratch, void* out, hipStream_t st);
 void launch_cg_xr(int dtype, int64_t n, int64_t noids, const int32_t* own, void* x, void* r, const void* u,
                   const void* c, const void* alpha, double* part, int nb, hipStream_t st);
 extern int g_spmv_format;
@@ -424,7 +424,8 @@ int pa_ctx_create(int device, int part, int nparts, pa_ctx** out) {
   HIPC(hipDeviceGetStreamPriorityRange(&least, &greatest));
   HIPC(hipStreamCreateWithFlags(&c->s_main, hipStreamNonBlocking));
   HIPC(hipStreamCreateWithPriority(&c->s_comm, hipStreamNonBlocking, greatest));
-  HIPC(hipMalloc(&c->d_partials, 1024 * 16));
+  HIPC(hipMalloc(&c->d_partials, 8192 * 16));  // block partials (reductions, CG update)
+  HIPC(hipMalloc(&c->d_fold, 256 * 16));
   HIPC(hipMalloc(&c->d_result, 16));
   HIPC(hipMalloc(&c->d_gather, (size_t)nparts * 16));
   HIPC(hipHostMalloc(&c->h_pinned, (size_t)(nparts + 1) * 16));
@@ -442,6 +443,7 @@ int pa_ctx_destroy(pa_ctx* c) {
   (void)hipStreamSynchronize(c->s_comm);
   if (c->comm) ncclCommDestroy((ncclComm_t)c->comm);
   dev_free(c->d_partials);
+  dev_free(c->d_fold);
   dev_free(c->d_result);
   dev_free(c->d_gather);
   if (c->h_pinned) (void)hipHostFree(c->h_pinned);
@@ -935,7 +937,7 @@ static int spmv_impl(int n, pa_mat* const A[], pa_vec* const y[], const pa_index
     if (want_dot) {  // fold the slice partials (main, then side in pattern mode) in order
       const bool pat = g_spmv_format == 1 && A[i]->has_pat;
       const bool cplx = dt == PA_C64 || dt == PA_C128;
-      launch_fold(cplx, (int)(A[i]->nslices + (pat ? A[i]->s_nslices : 0)), A[i]->d_dotp, c->d_result, c->s_main);
+      launch_fold(cplx, (int)(A[i]->nslices + (pat ? A[i]->s_nslices : 0)), A[i]->d_dotp, c->d_fold, c->d_result, c->s_main);
     }
     if (c->timing) HIPC(hipEventRecord(c->ev_t[3], c->s_main));
   }
@@ -1111,10 +1113,10 @@ int pa_cg_update_all(int n, pa_vec* const x[], pa_vec* const r[], const pa_vec* 
     ctxs[i] = cx;
     HIPC(hipSetDevice(cx->device));
     if (idx[i]->own_contig) {
-      const int nb = (int)std::min<int64_t>(1024, std::max<int64_t>(1, (m + 255) / 256));
+      const int nb = (int)std::min<int64_t>(8192, std::max<int64_t>(1, (m + 255) / 256));
       launch_cg_xr(dt, m, idx[i]->noids, nullptr, x[i]->d, r[i]->d, u[i]->d, c[i]->d, alpha,
                    (double*)cx->d_partials, nb, cx->s_main);
-      launch_fold(0, nb, cx->d_partials, cx->d_result, cx->s_main);
+      launch_fold(0, nb, cx->d_partials, cx->d_fold, cx->d_result, cx->s_main);
     } else {  // unfused: two broadcasts and the norm reduction
       launch_axpby(dt, m, nullptr, x[i]->d, u[i]->d, alpha, 1, cx->s_main);
       launch_axpby(dt, m, nullptr, r[i]->d, c[i]->d, alpha, 2, cx->s_main);

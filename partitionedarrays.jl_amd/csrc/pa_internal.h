@@ -95,6 +95,7 @@ struct pa_ctx {
   void* comm = nullptr;           // ncclComm_t (null: no remote transport)
   // reduction scratch
   void* d_partials = nullptr;     // per-block partials (max 16 B each)
+  void* d_fold = nullptr;         // 256*16 B first-level fold of long partial lists
   void* d_result = nullptr;       // 16 B final per-part value
   void* d_gather = nullptr;       // nparts*16 B gathered partials (RCCL mode)
   void* h_pinned = nullptr;       // pinned host staging (>= nparts*16 B)

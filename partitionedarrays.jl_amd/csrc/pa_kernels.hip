@@ -281,6 +281,7 @@ __global__ __launch_bounds__(256) void k_reduce_final(int nb, const A* __restric
 }
 
 constexpr int kReduceBlocks = 1024;
+constexpr int kFoldBlocks = 256;  // == PA_FOLD_SCRATCH / 16
 
 template <typename T, int KIND>
 static void reduce_t(int64_t n, const int32_t* ma, const void* a, const int32_t* mb,
@@ -293,12 +294,37 @@ static void reduce_t(int64_t n, const int32_t* ma, const void* a, const int32_t*
                      (A*)result);
 }
 
-// fold nb partials (double, or c128 when cplx) in a fixed order into out[0]
-void launch_fold(int cplx, int nb, const void* in, void* out, hipStream_t st) {
-  if (cplx)
-    hipLaunchKernelGGL((k_reduce_final<c128>), dim3(1), dim3(256), 0, st, nb, (const c128*)in, (c128*)out);
-  else
-    hipLaunchKernelGGL((k_reduce_final<double>), dim3(1), dim3(256), 0, st, nb, (const double*)in, (double*)out);
+// block b folds the contiguous chunk [b*chunk, min(nb, (b+1)*chunk))
+template <typename A>
+__global__ __launch_bounds__(256) void k_fold_chunks(int nb, int chunk, const A* __restrict__ in,
+                                                     A* __restrict__ out) {
+  const int lo = blockIdx.x * chunk;
+  const int hi = min(nb, lo + chunk);
+  A s = zero_of<A>();
+  for (int i = lo + threadIdx.x; i < hi; i += blockDim.x) s = s + in[i];
+  A r = block_reduce(s);
+  if (threadIdx.x == 0) out[blockIdx.x] = r;
+}
+
+template <typename A>
+static void fold_t(int nb, const A* in, A* scratch, A* out, hipStream_t st) {
+  if (nb <= 2 * kFoldBlocks || !scratch) {
+    hipLaunchKernelGGL((k_reduce_final<A>), dim3(1), dim3(256), 0, st, nb, in, out);
+    return;
+  }
+  // two levels (one block over 10^5 partials is ~150 us): the chunking
+  // depends only on nb, so the result stays run-to-run deterministic
+  const int chunk = (nb + kFoldBlocks - 1) / kFoldBlocks;
+  const int g = (nb + chunk - 1) / chunk;
+  hipLaunchKernelGGL((k_fold_chunks<A>), dim3(g), dim3(256), 0, st, nb, chunk, in, scratch);
+  hipLaunchKernelGGL((k_reduce_final<A>), dim3(1), dim3(256), 0, st, g, (const A*)scratch, out);
+}
+
+// fold nb partials (double, or c128 when cplx) in a fixed order into out[0];
+// scratch holds kFoldBlocks accumulators
+void launch_fold(int cplx, int nb, const void* in, void* scratch, void* out, hipStream_t st) {
+  if (cplx) fold_t<c128>(nb, (const c128*)in, (c128*)scratch, (c128*)out, st);
+  else fold_t<double>(nb, (const double*)in, (double*)scratch, (double*)out, st);
 }
 
 // result: device accumulator (double or c128) of the part's local value

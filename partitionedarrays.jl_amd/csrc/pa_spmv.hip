@@ -340,13 +340,31 @@ void launch_spmv_part(int which, int64_t nwork, const int32_t* list, const pa_ma
 // x .+= α.*u; r .-= α.*c (all lids, Interfaces.jl:1710-1737) and the owned
 // Σ|r|² of norm(r) (1767-1772) in one pass (contiguous owned lids
 // 0..noids-1); per-block partials, folded in block order afterwards.
-template <typename T>
-__global__ __launch_bounds__(256) void k_cg_xr(int64_t n, int64_t noids, const int32_t* __restrict__ own,
-                                               T* __restrict__ x, T* __restrict__ r, const T* __restrict__ u,
-                                               const T* __restrict__ c, T alpha, double* __restrict__ part) {
-  (void)own;
+// V elements per 16 B access (V = 1: unaligned fallback).
+template <typename T, int V>
+__global__ __launch_bounds__(256) void k_cg_xr(int64_t n, int64_t noids, T* __restrict__ x, T* __restrict__ r,
+                                               const T* __restrict__ u, const T* __restrict__ c, T alpha,
+                                               double* __restrict__ part) {
+  using P = Pack<T, V>;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  const int64_t nv = n / V;
   double s = 0.0;
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+  for (int64_t j = t; j < nv; j += stride) {
+    P xv = reinterpret_cast<const P*>(x)[j];
+    P rv = reinterpret_cast<const P*>(r)[j];
+    const P uv = reinterpret_cast<const P*>(u)[j];
+    const P cv = reinterpret_cast<const P*>(c)[j];
+#pragma unroll
+    for (int e = 0; e < V; ++e) {
+      xv.v[e] = xv.v[e] + alpha * uv.v[e];
+      rv.v[e] = rv.v[e] - alpha * cv.v[e];
+      if (j * V + e < noids) s = s + (double)abs2(rv.v[e]);
+    }
+    reinterpret_cast<P*>(x)[j] = xv;
+    reinterpret_cast<P*>(r)[j] = rv;
+  }
+  for (int64_t i = nv * V + t; i < n; i += stride) {
     x[i] = x[i] + alpha * u[i];
     const T ri = r[i] - alpha * c[i];
     r[i] = ri;
@@ -360,19 +378,26 @@ __global__ __launch_bounds__(256) void k_cg_xr(int64_t n, int64_t noids, const i
 }
 
 template <typename T>
-static void cg_xr_t(int64_t n, int64_t noids, const int32_t* own, void* x, void* r, const void* u,
-                    const void* c, const void* alpha, double* part, int nb, hipStream_t st) {
-  hipLaunchKernelGGL(k_cg_xr<T>, dim3(nb), dim3(256), 0, st, n, noids, own, (T*)x, (T*)r, (const T*)u,
-                     (const T*)c, *(const T*)alpha, part);
+static void cg_xr_t(int64_t n, int64_t noids, void* x, void* r, const void* u, const void* c,
+                    const void* alpha, double* part, int nb, hipStream_t st) {
+  constexpr int V = 16 / sizeof(T);
+  const bool aligned = ((uintptr_t)x | (uintptr_t)r | (uintptr_t)u | (uintptr_t)c) % 16 == 0;
+  if (aligned)
+    hipLaunchKernelGGL((k_cg_xr<T, V>), dim3(nb), dim3(256), 0, st, n, noids, (T*)x, (T*)r, (const T*)u,
+                       (const T*)c, *(const T*)alpha, part);
+  else
+    hipLaunchKernelGGL((k_cg_xr<T, 1>), dim3(nb), dim3(256), 0, st, n, noids, (T*)x, (T*)r, (const T*)u,
+                       (const T*)c, *(const T*)alpha, part);
 }
 
 void launch_cg_xr(int dtype, int64_t n, int64_t noids, const int32_t* own, void* x, void* r, const void* u,
                   const void* c, const void* alpha, double* part, int nb, hipStream_t st) {
+  (void)own;  // owned lids are 0..noids-1 (checked by the caller)
   switch (dtype) {
-    case PA_F32: cg_xr_t<float>(n, noids, own, x, r, u, c, alpha, part, nb, st); break;
-    case PA_F64: cg_xr_t<double>(n, noids, own, x, r, u, c, alpha, part, nb, st); break;
-    case PA_C64: cg_xr_t<c64>(n, noids, own, x, r, u, c, alpha, part, nb, st); break;
-    case PA_C128: cg_xr_t<c128>(n, noids, own, x, r, u, c, alpha, part, nb, st); break;
+    case PA_F32: cg_xr_t<float>(n, noids, x, r, u, c, alpha, part, nb, st); break;
+    case PA_F64: cg_xr_t<double>(n, noids, x, r, u, c, alpha, part, nb, st); break;
+    case PA_C64: cg_xr_t<c64>(n, noids, x, r, u, c, alpha, part, nb, st); break;
+    case PA_C128: cg_xr_t<c128>(n, noids, x, r, u, c, alpha, part, nb, st); break;
   }
 }
 

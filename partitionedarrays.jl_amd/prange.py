@@ -446,22 +446,35 @@ def to_lids_(ids: PData, a: PRange) -> PData:
     return map_parts(f, ids, a.partition)
 
 
+def _cached_eq(kind, a: PRange, b: PRange, f):
+    # the @check of mul!/copyto!/broadcasts (Interfaces.jl:1550-1554) is a
+    # gather+bcast per call in the reference; the partitions are immutable
+    # between add_gids! calls, so the answer is cached per (a, b, sizes)
+    key = (kind, id(b.partition), tuple(s.num_lids for s in b.partition.parts),
+           tuple(s.num_lids for s in a.partition.parts))
+    cache = a.__dict__.setdefault("_eq_cache", {})
+    hit = cache.get(key)
+    if hit is None or hit[0] is not b.partition:  # keep b alive: no id reuse
+        c = map_parts(f, a.partition, b.partition)
+        hit = (b.partition, bool(preduce(lambda u, v: u and v, c, True)))
+        cache[key] = hit
+    return hit[1]
+
+
 def oids_are_equal(a: PRange, b: PRange) -> bool:
     """Interfaces.jl:1549-1556"""
     if a.partition is b.partition:
         return True
-    c = map_parts(lambda x, y: bool(np.array_equal(x.lid_to_gid[x.oid_to_lid - 1], y.lid_to_gid[y.oid_to_lid - 1])),
-                  a.partition, b.partition)
-    return bool(preduce(lambda u, v: u and v, c, True))
+    return _cached_eq("oids", a, b, lambda x, y: bool(np.array_equal(x.lid_to_gid[x.oid_to_lid - 1],
+                                                                     y.lid_to_gid[y.oid_to_lid - 1])))
 
 
 def hids_are_equal(a: PRange, b: PRange) -> bool:
     """Interfaces.jl:1558-1565"""
     if a.partition is b.partition:
         return True
-    c = map_parts(lambda x, y: bool(np.array_equal(x.lid_to_gid[x.hid_to_lid - 1], y.lid_to_gid[y.hid_to_lid - 1])),
-                  a.partition, b.partition)
-    return bool(preduce(lambda u, v: u and v, c, True))
+    return _cached_eq("hids", a, b, lambda x, y: bool(np.array_equal(x.lid_to_gid[x.hid_to_lid - 1],
+                                                                     y.lid_to_gid[y.hid_to_lid - 1])))
 
 
 def lids_are_equal(a: PRange, b: PRange) -> bool:
