@@ -1489,3 +1489,112 @@ def _convert_values(v, dtype):
         f = v.astype(np.float32)
         return Cx(f * np.float32(1.0), f * np.float32(0.5))
     raise ValueError(dtype)
+
+
+# ---------------------------------------------------------------------------
+# BASELINE config 5: stencil operators on an irregular (Voronoi, "METIS-like")
+# owner map.  Vectorised restatements for the 128³ size,
+# each checked against the scalar functions above by tests/test_host_setup.py.
+
+def voronoi_owners(N, nparts, seed=20250114):
+    """Owner (1-based) of every gid: nearest of nparts points uniform in the
+    node box [0, N-1]³, ties to the lowest part (the C5 synthetic input)."""
+    rng = np.random.default_rng(seed)
+    pts = rng.uniform(0.0, 1.0, (nparts, 3)) * (np.asarray(N, dtype=np.float64) - 1.0)
+    ng = int(np.prod(N))
+    g = np.arange(ng, dtype=np.int64)
+    x = (g % N[0]).astype(np.float64)
+    y = ((g // N[0]) % N[1]).astype(np.float64)
+    z = (g // (N[0] * N[1])).astype(np.float64)
+    d = np.stack([((x - p[0]) ** 2 + (y - p[1]) ** 2) + (z - p[2]) ** 2 for p in pts], 0)
+    return (np.argmin(d, axis=0) + 1).astype(np.int32)  # argmin: first minimum
+
+
+def stencil_rows_vec(kind, N, gids, coef):
+    """stencil_row_entries for many rows at once: (row position, column gid,
+    value) in row order then neighbour order.  Interior rows all carry the
+    entries of one interior node (taken from stencil_row_entries); Dirichlet
+    rows come from stencil_row_entries row by row."""
+    gids = np.asarray(gids, dtype=np.int64)
+    Nx, Ny, Nz = N
+    g0 = gids - 1
+    gx, gy, gz = g0 % Nx, (g0 // Nx) % Ny, g0 // (Nx * Ny)
+    dirm = (gx == 0) | (gx == Nx - 1) | (gy == 0) | (gy == Ny - 1) | (gz == 0) | (gz == Nz - 1)
+    I, J, V = [], [], []
+    inner = None
+    if (~dirm).any():
+        c = (1, 1, 1)
+        ent = stencil_row_entries(kind, N, c, coef)
+        inner = (np.array([(nb[0] - 1) + Nx * ((nb[1] - 1) + Ny * (nb[2] - 1)) for nb, _ in ent], np.int64),
+                 np.array([v for _, v in ent], np.float64))
+    # rows grouped into runs so the output keeps row order
+    cnt = np.where(dirm, 1, len(inner[0]) if inner is not None else 0)
+    start = np.concatenate([[0], np.cumsum(cnt)[:-1]]).astype(np.int64)
+    nnz = int(cnt.sum())
+    I = np.repeat(np.arange(len(gids), dtype=np.int64), cnt)
+    J = np.zeros(nnz, np.int64)
+    V = np.zeros(nnz, np.float64)
+    for r in np.flatnonzero(dirm):
+        (nb, v), = stencil_row_entries(kind, N, (int(gx[r]), int(gy[r]), int(gz[r])), coef)
+        J[start[r]] = 1 + nb[0] + Nx * (nb[1] + Ny * nb[2])
+        V[start[r]] = v
+    ii = np.flatnonzero(~dirm)
+    if len(ii):
+        k = len(inner[0])
+        pos = start[ii][:, None] + np.arange(k)[None, :]
+        J[pos] = gids[ii][:, None] + inner[0][None, :]
+        V[pos] = inner[1][None, :]
+    return I, J, V
+
+
+def add_gids_owner_vec_(gid_to_part, a: IndexSet, gids):
+    """add_gids_owner_ (first touch, Interfaces.jl:586-592, 618-627) for
+    large gid lists: the unknown gids in order of first occurrence."""
+    gids = np.asarray(gids, dtype=np.int64)
+    known = np.asarray(a.lid_to_gid, dtype=np.int64)
+    new = gids[~np.isin(gids, known)]
+    u, first = np.unique(new, return_index=True)
+    for g in u[np.argsort(first, kind="stable")]:
+        _add_gid_ghost(a, int(g), gid_to_part(int(g)))
+    return a
+
+
+def to_lids_vec(ids, a: IndexSet):
+    """to_lids_ for large id lists (every id must be a local gid)."""
+    keys = np.asarray(a.lid_to_gid, dtype=np.int64)
+    o = np.argsort(keys)
+    i = np.searchsorted(keys[o], ids)
+    assert np.array_equal(keys[o][i], ids)
+    return o[i] + 1
+
+
+def irregular_problem(parts: PData, N: tuple, kind=27, dtype=np.float64, owners=None):
+    """C5 on the oracle: rows = IndexSets of the owned gids in gid order
+    (IndexSets.jl:215-291), gid_to_part = owner map; COO of owned rows with
+    global ids; cols = add_gids(rows, J) (first touch); psparse with
+    ids=:global (Interfaces.jl:2194-2215)."""
+    if owners is None:
+        owners = voronoi_owners(N, num_parts(parts))
+    coef = fd7_coeffs(N[0]) if kind == 7 else q1_hex_ke(2.0 / (N[0] - 1)).ravel()
+    ngids = int(np.prod(N))
+    g2p = lambda g: int(owners[g - 1])
+
+    def mk(part):
+        gids = np.flatnonzero(owners == part) + 1
+        return IndexSet(part, gids, [part] * len(gids), list(range(1, len(gids) + 1)), [])
+    rows = PRange(ngids, map_parts(mk, parts), None, map_parts(lambda _: g2p, parts), False)
+    rows.exchanger = empty_exchanger(rows.partition)
+
+    def coo(s):
+        gids = np.asarray(s.lid_to_gid, np.int64)
+        i, j, v = stencil_rows_vec(kind, N, gids, coef)
+        return gids[i], j, v
+    I, J, V = unzip(map_parts(coo, rows.partition), 3)
+    cols = copy_prange(rows)
+    map_parts(add_gids_owner_vec_, cols.gid_to_part, cols.partition, J)
+    cols.exchanger = exchanger_from_ids(cols.partition)
+    cols.ghost = True
+    Il = map_parts(to_lids_vec, I, rows.partition)
+    Jl = map_parts(to_lids_vec, J, cols.partition)
+    V = map_parts(lambda v: _convert_values(v, dtype), V)
+    return psparse_from_coo(Il, Jl, V, rows, cols, ids="local")

@@ -308,3 +308,138 @@ def stencil_operator(parts: PData, N: tuple, kind: int, dtype=np.float64, partit
     A = PSparseMatrix(PData(rows.partition.backend, rows.partition.part_ids, mats, rows.partition.shape),
                       rows, cols)
     return A
+
+
+# ---------------------------------------------------------------------------
+# BASELINE config 5: the stencil operators on an irregular ("METIS-like")
+# partition — owners from the nearest of P seeded points,
+# rows in gid order, ghosts in first-touch order (add_gids!), the Exchanger
+# from the gather-based discover (Interfaces.jl:515-552, 723-786).
+
+def _row_constants(kind, N):
+    """Values of an interior row (all neighbours present), neighbour order
+    (dz,dy,dx) lexicographic.  kind 27: for each neighbour the Ke entries of
+    the cells holding both nodes, summed in ascending cell gid (the cell
+    loop's COO order combined by sparse, test_fem_sa.jl:40-62)."""
+    coef = stencil_coeffs(kind, N)
+    off = _offsets(kind)
+    if kind == 7:
+        return off, np.array([coef[0] if not d.any() else coef[1] for d in off])
+    vals = []
+    for dx, dy, dz in off:
+        acc = None
+        for cz in (-1, 0):
+            for cy in (-1, 0):
+                for cx in (-1, 0):
+                    bx, by, bz = dx - cx, dy - cy, dz - cz
+                    if not (0 <= bx <= 1 and 0 <= by <= 1 and 0 <= bz <= 1):
+                        continue
+                    a = -cx + 2 * -cy + 4 * -cz
+                    v = coef[a * 8 + bx + 2 * by + 4 * bz]
+                    acc = v if acc is None else acc + v
+        vals.append(acc)
+    return off, np.array(vals, dtype=np.float64)
+
+
+def stencil_entries(kind, N, gids):
+    """COO entries of the rows `gids` (1-based) of the Cartesian stencil
+    operator: (row position, column gid, value), rows in the given order,
+    each row's neighbours in (dz,dy,dx) order.  Dirichlet rows (any
+    coordinate on the boundary) keep the diagonal only: 1 for kind 7
+    (test_fdm.jl:63-69), the number of touching cells for kind 27
+    (test_fem_sa.jl:47-52, one 1.0 per cell)."""
+    gids = np.asarray(gids, dtype=np.int64)
+    g0 = gids - 1
+    Nx, Ny, Nz = N
+    gx, gy, gz = g0 % Nx, (g0 // Nx) % Ny, g0 // (Nx * Ny)
+    dirichlet = ((gx == 0) | (gx == Nx - 1) | (gy == 0) | (gy == Ny - 1) | (gz == 0) | (gz == Nz - 1))
+    off, vals = _row_constants(kind, N)
+    K = len(off)
+    cnt = np.where(dirichlet, 1, K)
+    start = np.concatenate([[0], np.cumsum(cnt)[:-1]]).astype(np.int64)
+    nnz = int(cnt.sum())
+    I = np.repeat(np.arange(len(gids), dtype=np.int64), cnt)
+    J = np.empty(nnz, dtype=np.int64)
+    V = np.empty(nnz, dtype=np.float64)
+    di = np.flatnonzero(dirichlet)
+    J[start[di]] = gids[di]
+    if kind == 7:
+        V[start[di]] = 1.0
+    else:
+        ncell = lambda c, n: np.where((c == 0) | (c == n - 1), 1, 2)
+        V[start[di]] = (ncell(gx[di], Nx) * ncell(gy[di], Ny) * ncell(gz[di], Nz)).astype(np.float64)
+    ii = np.flatnonzero(~dirichlet)
+    lin = off[:, 0] + Nx * (off[:, 1] + Ny * off[:, 2])
+    pos = start[ii][:, None] + np.arange(K)[None, :]
+    J[pos] = gids[ii][:, None] + lin[None, :]
+    V[pos] = vals[None, :]
+    return I, J, V
+
+
+def voronoi_owners(N, nparts, seed=20250114):
+    """gid → part (1-based, int32 array over gids 1..prod(N)): the nearest of
+    `nparts` points drawn uniformly in the node box (ties: lowest part)."""
+    rng = np.random.default_rng(seed)
+    pts = rng.uniform(0.0, 1.0, (nparts, 3)) * (np.array(N, dtype=np.float64) - 1.0)
+    g0 = np.arange(int(np.prod(N)), dtype=np.int64)
+    c = np.stack([g0 % N[0], (g0 // N[0]) % N[1], g0 // (N[0] * N[1])], 1).astype(np.float64)
+    best = np.zeros(len(g0), dtype=np.int32)
+    bd = np.full(len(g0), np.inf)
+    for p in range(nparts):
+        d = ((c[:, 0] - pts[p, 0]) ** 2 + (c[:, 1] - pts[p, 1]) ** 2) + (c[:, 2] - pts[p, 2]) ** 2
+        closer = d < bd
+        best[closer] = p
+        bd[closer] = d[closer]
+    return best + 1
+
+
+def convert_values(v, dtype):
+    """Float32.(A) / A .* (1+0.5im) of BASELINE config 5 (Complex(v*1, v*0.5))."""
+    dtype = np.dtype(dtype)
+    if dtype == np.float64:
+        return v
+    if dtype == np.float32:
+        return v.astype(np.float32)
+    if dtype == np.complex128:
+        out = np.empty(len(v), np.complex128)
+        out.real, out.imag = v * 1.0, v * 0.5
+        return out
+    if dtype == np.complex64:
+        f = v.astype(np.float32)
+        out = np.empty(len(v), np.complex64)
+        out.real, out.imag = f * np.float32(1.0), f * np.float32(0.5)
+        return out
+    raise ValueError(dtype)
+
+
+def irregular_partition(parts: PData, N: tuple, kind: int = 27, owners=None):
+    """C5 setup on the host: rows = PRange(ngids, IndexSets of the owned gids
+    in gid order, gid_to_part); each part's COO of its owned rows (global
+    ids, Float64 values); cols = add_gids(rows, J) (first touch, Exchanger
+    by the gather-based discover).  Returns rows, cols, I, J, V."""
+    from .prange import IndexSet, prange_from_partition
+    if owners is None:
+        owners = voronoi_owners(N, parts.num_parts)
+    ngids = int(np.prod(N))
+    g2p = lambda g: owners[np.asarray(g, np.int64) - 1]
+
+    def mk(part):
+        gids = np.flatnonzero(owners == part).astype(np.int64) + 1
+        return IndexSet(part, gids, np.full(len(gids), part, np.int32), np.arange(1, len(gids) + 1),
+                        np.zeros(0, np.int32))
+    rows = prange_from_partition(ngids, map_parts(mk, parts), map_parts(lambda _: g2p, parts), ghost=False)
+
+    def coo(s):
+        i, j, v = stencil_entries(kind, N, s.lid_to_gid[s.oid_to_lid - 1])
+        return s.lid_to_gid[s.oid_to_lid[i] - 1], j, v
+    I, J, V = unzip(map_parts(coo, rows.partition), 3)
+    cols = add_gids(rows, J)
+    return rows, cols, I, J, V
+
+
+def irregular_problem(parts: PData, N: tuple, kind: int = 27, dtype=np.float64, owners=None):
+    """C5: PSparseMatrix(I, J, V, rows, cols; ids=:global) on the irregular
+    partition, values converted as BASELINE config 5 says."""
+    rows, cols, I, J, V = irregular_partition(parts, N, kind, owners)
+    V = map_parts(lambda v: convert_values(v, dtype), V)
+    return PSparseMatrix.from_coo(I, J, V, rows, cols, ids="global")

@@ -166,3 +166,56 @@ def test_fem_sa_host_matches_oracle(pamd, O, nparts):
         assert np.array_equal(M.colptr, OM.colptr) and np.array_equal(M.rowval, OM.rowval)
         assert np.array_equal(M.nzval, OM.nzval)
         assert np.array_equal(x0h.local(p)[c.oid_to_lid - 1], ox0.values[p][c.oid_to_lid - 1])
+
+
+@pytest.mark.parametrize("kind,N", [(7, (7, 6, 5)), (27, (7, 6, 5)), (27, (5, 9, 4))])
+def test_stencil_entries_vectorised(pamd, O, kind, N):
+    """The vectorised row generators (product and oracle) == the oracle's
+    scalar stencil_row_entries, row by row, entry by entry."""
+    coef = O.fd7_coeffs(N[0]) if kind == 7 else O.q1_hex_ke(2.0 / (N[0] - 1)).ravel()
+    gids = np.random.default_rng(5).permutation(int(np.prod(N))) + 1
+    ref = []
+    for g in gids:
+        c = tuple(x - 1 for x in O.cartesian_index(N, int(g)))
+        for nb, v in O.stencil_row_entries(kind, N, c, coef):
+            ref.append((int(g), O.linear_index(N, tuple(x + 1 for x in nb)), v))
+    R = np.array(ref)
+    for I, J, V in (O.stencil_rows_vec(kind, N, gids, coef), pamd.drivers.stencil_entries(kind, N, gids)):
+        assert np.array_equal(gids[I], R[:, 0]) and np.array_equal(J, R[:, 1])
+        assert np.array_equal(V, R[:, 2])
+
+
+def test_oracle_vectorised_add_gids(O):
+    rng = np.random.default_rng(3)
+    owners = rng.integers(1, 4, 200)
+    g2p = lambda g: int(owners[g - 1])
+    mk = lambda: O.IndexSet(1, [3, 9, 27], [1, 1, 1], [1, 2, 3], [])
+    gids = rng.integers(1, 201, 500)
+    a, b = mk(), mk()
+    O.add_gids_owner_(g2p, a, gids)
+    O.add_gids_owner_vec_(g2p, b, gids)
+    assert a.lid_to_gid == b.lid_to_gid and a.lid_to_part == b.lid_to_part and a.hid_to_lid == b.hid_to_lid
+    assert O.to_lids_vec(np.array(gids), a).tolist() == O.to_lids_(list(gids), a)
+
+
+@pytest.mark.parametrize("nparts,N,kind", [(4, (14, 12, 10), 27), (7, (11, 9, 13), 7), (3, (9, 9, 9), 27)])
+def test_irregular_partition_matches_oracle(pamd, O, nparts, N, kind):
+    """C5 setup: Voronoi owners, first-touch ghosts, gather-discovered
+    Exchanger and local CSCs equal the oracle's."""
+    parts = pamd.sequential.get_part_ids(nparts)
+    rows, cols, I, J, V = pamd.drivers.irregular_partition(parts, N, kind)
+    OA = O.irregular_problem(O.get_part_ids(nparts), N, kind)
+    assert np.array_equal(pamd.drivers.voronoi_owners(N, nparts), O.voronoi_owners(N, nparts))
+    ex, oex = cols.exchanger, OA.cols.exchanger
+    for p in parts.part_ids:
+        r, c = rows.partition.local(p), cols.partition.local(p)
+        oc = OA.cols.partition[p]
+        assert c.lid_to_gid.tolist() == oc.lid_to_gid and c.lid_to_part.tolist() == oc.lid_to_part
+        assert list(ex.parts_rcv.local(p)) == list(oex.parts_rcv[p])
+        assert list(ex.parts_snd.local(p)) == list(oex.parts_snd[p])
+        assert ex.lids_rcv.local(p).tolist() == oex.lids_rcv[p].tolist()
+        assert ex.lids_snd.local(p).tolist() == oex.lids_snd[p].tolist()
+        M = pamd.compresscoo(r.to_lids(I.local(p)), c.to_lids(J.local(p)), V.local(p), r.num_lids, c.num_lids)
+        OM = OA.values[p]
+        assert np.array_equal(M.colptr, OM.colptr) and np.array_equal(M.rowval, OM.rowval)
+        assert np.array_equal(M.nzval, OM.nzval)
