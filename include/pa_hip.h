@@ -131,6 +131,24 @@ int pa_mat_from_csc(pa_ctx* ctx, int dtype, int index_bytes,
 /* Replace the stored values keeping the pattern (same CSC nz order),
  * e.g. after fillstored!/re-assembly (Interfaces.jl:2127-2132).          */
 int pa_mat_set_values(pa_mat* A, const void* nzval);
+/* nonzeros(A) in CSC nz order, ghost rows included (the device keeps the
+ * ghost rows' values beside the SELL slots for exchange!/assemble!(A)).  */
+int pa_mat_get_values(const pa_mat* A, void* nzval);
+/* matrix_exchanger(values, rows, cols) (Interfaces.jl:2300-2372): the
+ * Exchanger whose lids are CSC nz positions k (1-based, Int64 as Julia's
+ * Table{Int}): k_rcv = nonzeros of ghost rows grouped by owner, k_snd = the
+ * owner's nonzeros at the same (gi, gj).  Usable with pa_mat_exchange_all. */
+int pa_mat_xchg_create(pa_mat* A, int32_t n_rcv, const int32_t* parts_rcv,
+                       const int32_t* ptrs_rcv, const int64_t* k_rcv,
+                       int32_t n_snd, const int32_t* parts_snd,
+                       const int32_t* ptrs_snd, const int64_t* k_snd,
+                       pa_xchg** out);
+/* exchange!(A) (Interfaces.jl:2375-2381: op PA_REPLACE, reverse 0) and
+ * assemble!(A) (2383-2404: op PA_ADD, reverse 1, zero_sent 1 — the ghost
+ * rows' values are zeroed after sending) over nonzeros(A), n local parts.
+ * Contributions to one nonzero are combined in the reference's order.     */
+int pa_mat_exchange_all(int n, pa_mat* const A[], pa_xchg* const xg[],
+                        int op, int reverse, int zero_sent);
 int pa_mat_destroy(pa_mat* A);
 /* nnz stored on device (padding included) and owned-row nnz. */
 int pa_mat_info(const pa_mat* A, int64_t* nrows_owned, int64_t* nnz_owned,

@@ -839,6 +839,14 @@ def _zeros(n, dtype):
     return np.zeros(n, dtype)
 
 
+def _zero_like(vs):
+    """zero(eltype(vs)) (+0.0, not x*0 which keeps the sign)"""
+    if isinstance(vs, Cx):
+        z = np.zeros((), dtype=vs.re.dtype)[()]
+        return Cx(z, z)
+    return np.zeros((), dtype=vs.dtype)[()] if isinstance(vs, np.ndarray) else 0.0
+
+
 def _get(vs, i):
     return Cx(vs.re[i], vs.im[i]) if isinstance(vs, Cx) else vs[i]
 
@@ -887,7 +895,7 @@ def assemble_(v: PVector):
 
     def zero(vs, s):
         for l in s.hid_to_lid:
-            _set(vs, l - 1, _get(vs, l - 1) * 0 if not isinstance(vs, Cx) else Cx(vs.re[0] * 0, vs.im[0] * 0))
+            _set(vs, l - 1, _zero_like(vs))
     map_parts(zero, v.values, v.rows.partition)
     return v
 
@@ -1018,7 +1026,7 @@ def psparse_from_coo(I: PData, J: PData, V: PData, rows: PRange, cols: PRange, i
         to_lids_pr_(J, cols)
     vals = map_parts(lambda i, j, v, r, c: sparse_csc(i, j, v, r.num_lids, c.num_lids), I, J, V,
                      rows.partition, cols.partition)
-    return PSparseMatrix(vals, rows, cols)
+    return PSparseMatrix(vals, rows, cols, matrix_exchanger(vals, rows, cols))  # Interfaces.jl:2117
 
 
 def mul_(c: PVector, a: PSparseMatrix, b: PVector, alpha=1.0, beta=0.0, literal=False):
@@ -1598,3 +1606,95 @@ def irregular_problem(parts: PData, N: tuple, kind=27, dtype=np.float64, owners=
     Jl = map_parts(to_lids_vec, J, cols.partition)
     V = map_parts(lambda v: _convert_values(v, dtype), V)
     return psparse_from_coo(Il, Jl, V, rows, cols, ids="local")
+
+
+# ---------------------------------------------------------------------------
+# Matrix nonzero exchange
+
+def nzindex(A: CSC, i0, i1):
+    """nzindex(A::SparseMatrixCSC, i0, i1) SparseUtils.jl:96-104 (-1 if absent)"""
+    r1, r2 = int(A.colptr[i1 - 1]), int(A.colptr[i1]) - 1
+    if r1 > r2:
+        return -1
+    lo, hi = r1, r2 + 1  # searchsortedfirst over rowval[r1:r2] (1-based positions)
+    while lo < hi:
+        mid = (lo + hi) // 2
+        if A.rowval[mid - 1] < i0:
+            lo = mid + 1
+        else:
+            hi = mid
+    return lo if lo <= r2 and A.rowval[lo - 1] == i0 else -1
+
+
+def nz_entries(A: CSC):
+    """nziterator(A) for CSC (SparseUtils.jl:106-150): (k, li, lj) in storage order"""
+    out = []
+    for j in range(1, A.n + 1):
+        for k in range(int(A.colptr[j - 1]), int(A.colptr[j])):
+            out.append((k, int(A.rowval[k - 1]), j))
+    return out
+
+
+def matrix_exchanger(values: PData, rows: PRange, cols: PRange) -> Exchanger:
+    """matrix_exchanger(values, rows, cols) Interfaces.jl:2300-2372, literally."""
+    if not rows.ghost:
+        return empty_exchanger(rows.partition)
+    parts_rcv = rows.exchanger.parts_rcv
+    parts_snd = rows.exchanger.parts_snd
+    parts = get_part_ids(rows.partition.shape if len(rows.partition.shape) > 1 else num_parts(rows.partition))
+
+    def setup_rcv(part, prcv, rl, cl, A):
+        owner_to_i = {o: i for i, o in enumerate(prcv)}
+        counts = [0] * len(prcv)
+        ents = nz_entries(A)
+        for k, li, lj in ents:
+            owner = rl.lid_to_part[li - 1]
+            if owner != part:
+                counts[owner_to_i[owner]] += 1
+        ptrs = counts_to_ptrs(counts)
+        n = int(ptrs[-1] - 1)
+        kd, gi, gj = np.zeros(n, np.int64), np.zeros(n, np.int64), np.zeros(n, np.int64)
+        cur = ptrs.copy()
+        for k, li, lj in ents:
+            owner = rl.lid_to_part[li - 1]
+            if owner != part:
+                i = owner_to_i[owner]
+                p = int(cur[i]) - 1
+                kd[p], gi[p], gj[p] = k, rl.lid_to_gid[li - 1], cl.lid_to_gid[lj - 1]
+                cur[i] += 1
+        return Table(kd, ptrs.copy()), Table(gi, ptrs.copy()), Table(gj, ptrs.copy())
+    k_rcv, gi_rcv, gj_rcv = unzip(map_parts(setup_rcv, parts, parts_rcv, rows.partition, cols.partition,
+                                            values), 3)
+    gi_snd = exchange_tables(gi_rcv, parts_snd, parts_rcv)
+    gj_snd = exchange_tables(gj_rcv, parts_snd, parts_rcv)
+
+    def setup_snd(rl, cl, gi, gj, A):
+        kd = np.zeros(len(gi.data), np.int64)
+        for p in range(len(gi.data)):
+            k = nzindex(A, rl.gid_to_lid[int(gi.data[p])], cl.gid_to_lid[int(gj.data[p])])
+            assert k > 0, "The sparsity pattern of the ghost layer is inconsistent"
+            kd[p] = k
+        return Table(kd, gi.ptrs.copy())
+    k_snd = map_parts(setup_snd, rows.partition, cols.partition, gi_snd, gj_snd, values)
+    return Exchanger(parts_rcv, parts_snd, k_rcv, k_snd)
+
+
+def exchange_matrix_(A: PSparseMatrix):
+    """exchange!(A) Interfaces.jl:2375-2381"""
+    nz = map_parts(lambda M: _CxList(M.nzval) if isinstance(M.nzval, Cx) else M.nzval, A.values)
+    exchange_values_(_replace, nz, nz, A.exchanger)
+    return A
+
+
+def assemble_matrix_(A: PSparseMatrix):
+    """assemble!(A) Interfaces.jl:2383-2404: reverse exchange with +, then
+    nzval[lids_snd.data] .= 0 (lids_snd of the reversed exchanger)."""
+    ex = reverse_exchanger(A.exchanger)
+    nz = map_parts(lambda M: _CxList(M.nzval) if isinstance(M.nzval, Cx) else M.nzval, A.values)
+    exchange_values_(lambda a, b: a + b, nz, nz, ex)
+
+    def zero(M, lids):
+        for k in lids.data:
+            _set(M.nzval, int(k) - 1, _zero_like(M.nzval))
+    map_parts(zero, A.values, ex.lids_snd)
+    return A

@@ -53,6 +53,9 @@ _SIGS = {
     "pa_vec_axpby": [_p, _p, _p, _p, C.c_int, C.c_int],
     "pa_mat_from_csc": [_p, C.c_int, C.c_int, C.c_int64, C.c_int64, _p, _p, _p, _p, _p, C.POINTER(_p)],
     "pa_mat_set_values": [_p, _p],
+    "pa_mat_get_values": [_p, _p],
+    "pa_mat_xchg_create": [_p, C.c_int32, _i32p, _i32p, _i64p, C.c_int32, _i32p, _i32p, _i64p, C.POINTER(_p)],
+    "pa_mat_exchange_all": [C.c_int, C.POINTER(_p), C.POINTER(_p), C.c_int, C.c_int, C.c_int],
     "pa_mat_destroy": [_p],
     "pa_mat_info": [_p, _i64p, _i64p, _i64p, _i64p, _i64p],
     "pa_mat_format_info": [_p, _i64p, _i64p, _i64p, _i64p],

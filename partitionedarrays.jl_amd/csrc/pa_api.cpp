@@ -774,10 +774,19 @@ int pa_mat_from_csc(pa_ctx* c, int dtype, int index_bytes, int64_t nrows_lids, i
     std::memcpy(&hval[slot * S], (const unsigned char*)nzval + p * S, S);
     A->h_nz_slot[p] = slot;
   });
+  // ghost-row nonzeros (dropped by the SpMV, kept for exchange!/assemble!(A))
+  for (int64_t p = 0; p < csc_nnz; ++p)
+    if (A->h_nz_slot[p] < 0) A->h_nz_slot[p] = -(++A->n_gnz);
+  if (A->n_gnz) {
+    hval.resize((A->slots + A->n_gnz) * S);
+    for (int64_t p = 0; p < csc_nnz; ++p)
+      if (A->h_nz_slot[p] < 0)
+        std::memcpy(&hval[(A->slots - A->h_nz_slot[p] - 1) * S], (const unsigned char*)nzval + p * S, S);
+  }
   if (dev_upload(&A->d_col, hcol)) { pa_mat_destroy(A); return -1; }
-  if (A->slots) {
-    HIPC(hipMalloc(&A->d_val, A->slots * S));
-    HIPC(hipMemcpy(A->d_val, hval.data(), A->slots * S, hipMemcpyHostToDevice));
+  if (A->slots + A->n_gnz) {
+    HIPC(hipMalloc(&A->d_val, (A->slots + A->n_gnz) * S));
+    HIPC(hipMemcpy(A->d_val, hval.data(), (A->slots + A->n_gnz) * S, hipMemcpyHostToDevice));
   }
   // pattern slices need "x lid >= noids ⇔ ghost column" (contiguous layout)
   if (cols->own_contig && cols->ghost_contig) {
@@ -789,23 +798,104 @@ int pa_mat_from_csc(pa_ctx* c, int dtype, int index_bytes, int64_t nrows_lids, i
   return 0;
 }
 
+// value index of CSC nz p in d_val (main slot, or ghost-row value after the slots)
+static inline int64_t nz_index(const pa_mat* A, int64_t p) {
+  const int64_t s = A->h_nz_slot[p];
+  return s >= 0 ? s : A->slots - s - 1;
+}
+
+// refresh the side SELL's copies of the irregular rows' values
+static int refresh_side(pa_mat* A, hipStream_t st) {
+  if (A->s_nrows > 0) {
+    launch_side_fill(A, A->d_s_rowmap, A->d_s_rowlen, st);
+    HIPC(hipGetLastError());
+  }
+  return 0;
+}
+
 int pa_mat_set_values(pa_mat* A, const void* nzval) {
   CHECK_ARG(A && nzval, "null argument");
   CHECK_ARG((int64_t)A->h_nz_slot.size() == A->csc_nnz, "matrix was not built from a CSC pattern");
   HIPC(hipSetDevice(A->ctx->device));
   const size_t S = dtype_size(A->dtype);
-  std::vector<unsigned char> hval(A->slots * S, 0);
-  for (int64_t p = 0; p < A->csc_nnz; ++p) {
-    const int64_t slot = A->h_nz_slot[p];
-    if (slot >= 0) std::memcpy(&hval[slot * S], (const unsigned char*)nzval + p * S, S);
-  }
+  const int64_t nv = A->slots + A->n_gnz;
+  std::vector<unsigned char> hval(nv * S, 0);
+  for (int64_t p = 0; p < A->csc_nnz; ++p)
+    std::memcpy(&hval[nz_index(A, p) * S], (const unsigned char*)nzval + p * S, S);
   HIPC(hipStreamSynchronize(A->ctx->s_main));
-  if (A->slots) HIPC(hipMemcpy(A->d_val, hval.data(), A->slots * S, hipMemcpyHostToDevice));
-  if (A->s_nrows > 0) {  // the side rows carry copies of their values
-    launch_side_fill(A, A->d_s_rowmap, A->d_s_rowlen, A->ctx->s_main);
-    HIPC(hipGetLastError());
-    HIPC(hipStreamSynchronize(A->ctx->s_main));
+  if (nv) HIPC(hipMemcpy(A->d_val, hval.data(), nv * S, hipMemcpyHostToDevice));
+  if (refresh_side(A, A->ctx->s_main)) return -1;
+  HIPC(hipStreamSynchronize(A->ctx->s_main));
+  return 0;
+}
+
+int pa_mat_get_values(const pa_mat* A, void* nzval) {
+  CHECK_ARG(A && nzval, "null argument");
+  CHECK_ARG((int64_t)A->h_nz_slot.size() == A->csc_nnz, "matrix was not built from a CSC pattern");
+  HIPC(hipSetDevice(A->ctx->device));
+  const size_t S = dtype_size(A->dtype);
+  const int64_t nv = A->slots + A->n_gnz;
+  std::vector<unsigned char> hval(nv * S, 0);
+  HIPC(hipStreamSynchronize(A->ctx->s_comm));
+  HIPC(hipStreamSynchronize(A->ctx->s_main));
+  if (nv) HIPC(hipMemcpy(hval.data(), A->d_val, nv * S, hipMemcpyDeviceToHost));
+  for (int64_t p = 0; p < A->csc_nnz; ++p)
+    std::memcpy((unsigned char*)nzval + p * S, &hval[nz_index(A, p) * S], S);
+  return 0;
+}
+
+// Matrix exchanger (Interfaces.jl:2312-2372): lids are CSC nz positions k
+// (1-based); they become value indices of d_val.
+int pa_mat_xchg_create(pa_mat* A, int32_t n_rcv, const int32_t* parts_rcv, const int32_t* ptrs_rcv,
+                       const int64_t* k_rcv, int32_t n_snd, const int32_t* parts_snd, const int32_t* ptrs_snd,
+                       const int64_t* k_snd, pa_xchg** out) {
+  CHECK_ARG(A && out, "null argument");
+  CHECK_ARG((int64_t)A->h_nz_slot.size() == A->csc_nnz, "matrix was not built from a CSC pattern");
+  CHECK_ARG(A->slots + A->n_gnz < ((int64_t)1 << 31), "matrix exchanger: value index exceeds int32");
+  CHECK_ARG(n_rcv >= 0 && n_snd >= 0, "negative neighbour count");
+  auto conv = [&](int32_t n, const int32_t* ptrs, const int64_t* k, std::vector<int32_t>& o) -> int {
+    const int64_t m = n > 0 ? (int64_t)ptrs[n] - 1 : 0;
+    CHECK_ARG(m >= 0, "matrix exchanger: bad ptrs");
+    o.resize(m);
+    for (int64_t i = 0; i < m; ++i) {
+      CHECK_ARG(k[i] >= 1 && k[i] <= A->csc_nnz, "matrix exchanger: nz index out of range");
+      o[i] = (int32_t)(nz_index(A, k[i] - 1) + 1);
+    }
+    return 0;
+  };
+  std::vector<int32_t> lr, ls;
+  if (conv(n_rcv, ptrs_rcv, k_rcv, lr) || conv(n_snd, ptrs_snd, k_snd, ls)) return -1;
+  return pa_xchg_create(A->ctx, n_rcv, parts_rcv, ptrs_rcv, lr.data(), n_snd, parts_snd, ptrs_snd, ls.data(),
+                        out);
+}
+
+// exchange!(A) / assemble!(A) (Interfaces.jl:2375-2404) for n local parts:
+// the vector exchange over nonzeros(A); assemble zeroes the sent ghost-row
+// values afterwards (2398) and refreshes the side SELL copies.
+int pa_mat_exchange_all(int n, pa_mat* const A[], pa_xchg* const xg[], int op, int reverse, int zero_sent) {
+  CHECK_ARG(n >= 1 && A && xg, "null argument");
+  std::vector<pa_vec> vs(n);
+  std::vector<pa_vec*> vp(n);
+  for (int i = 0; i < n; ++i) {
+    CHECK_ARG(A[i] && xg[i] && A[i]->ctx == xg[i]->ctx, "exchange!(A): matrix and exchanger of different parts");
+    vs[i].ctx = A[i]->ctx;
+    vs[i].dtype = A[i]->dtype;
+    vs[i].n = A[i]->slots + A[i]->n_gnz;
+    vs[i].d = A[i]->d_val;
+    vp[i] = &vs[i];
   }
+  if (pa_exchange_all(n, vp.data(), xg, nullptr, op, reverse, 0)) return -1;
+  for (int i = 0; i < n; ++i) {
+    pa_ctx* c = A[i]->ctx;
+    HIPC(hipSetDevice(c->device));
+    if (zero_sent) {
+      unsigned char z[16] = {0};
+      if (reverse) launch_fill(A[i]->dtype, xg[i]->n_rcv_data, 0, xg[i]->d_lids_rcv, A[i]->d_val, z, c->s_main);
+      else launch_fill(A[i]->dtype, xg[i]->n_snd_data, 0, xg[i]->d_lids_snd, A[i]->d_val, z, c->s_main);
+    }
+    if (refresh_side(A[i], c->s_main)) return -1;
+  }
+  HIPC(hipGetLastError());
   return 0;
 }
 

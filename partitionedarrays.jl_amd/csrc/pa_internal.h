@@ -167,9 +167,14 @@ struct pa_mat {
   int32_t* d_int_list = nullptr;    // interior slice ids (null: all interior 0..n-1)
   int32_t* d_bnd_list = nullptr;    // boundary slice ids
   int32_t* d_col = nullptr;         // slots, x lid (0-based) or -1 padding
-  void* d_val = nullptr;            // slots
-  std::vector<int64_t> h_nz_slot;   // CSC nz → slot (-1: dropped)
+  void* d_val = nullptr;            // slots, then n_gnz ghost-row values
+  // CSC nz p → its value: main slot (>= 0) or ghost-row value g (-(g+1)).
+  // The ghost rows' nonzeros (stored by FE assembly, never multiplied) sit
+  // after the SELL slots in d_val: the nz exchange/assemble (matrix
+  // exchanger, Interfaces.jl:2312-2404) addresses both through one index.
+  std::vector<int64_t> h_nz_slot;
   int64_t csc_nnz = 0;
+  int64_t n_gnz = 0;
 
   // Pattern slices (implied columns): in a pattern slice the
   // rows whose column sequence is `row + pat[k]` (k < plen) are "regular"

@@ -157,6 +157,23 @@ def device_exchanger(ctx: PartContext, ex, part):
     return d
 
 
+class DeviceMatrixExchanger(DeviceExchanger):
+    """pa_mat_xchg_create: an Exchanger over nonzeros(A) (lids = CSC nz k)."""
+
+    def __init__(self, mat, parts_rcv, k_rcv, parts_snd, k_snd):
+        pr, prp = _lib.i32(parts_rcv)
+        rp, rpp = _lib.i32(k_rcv.ptrs)
+        rk = np.ascontiguousarray(k_rcv.data, dtype=np.int64)
+        ps, psp = _lib.i32(parts_snd)
+        sp, spp = _lib.i32(k_snd.ptrs)
+        sk = np.ascontiguousarray(k_snd.data, dtype=np.int64)
+        h = C.c_void_p()
+        _lib.call("pa_mat_xchg_create", mat.h, len(pr), prp, rpp, rk.ctypes.data_as(C.POINTER(C.c_int64)),
+                  len(ps), psp, spp, sk.ctypes.data_as(C.POINTER(C.c_int64)), C.byref(h))
+        self.h = h
+        self.mat = mat  # the exchanger addresses this matrix's value store
+
+
 class DeviceVector:
     """pa_vec: the values of one part of a PVector, in HBM."""
 
@@ -208,11 +225,22 @@ class DeviceMatrix:
         _lib.call("pa_mat_from_csc", ctx.h, _lib.DTYPES[nzval.dtype], 8, nrows_lids, ncols_lids,
                   colptr.ctypes.data_as(C.c_void_p), rowval.ctypes.data_as(C.c_void_p),
                   nzval.ctypes.data_as(C.c_void_p), rows_idx.h, cols_idx.h, C.byref(h))
-        return DeviceMatrix(h, ctx, nzval.dtype)
+        M = DeviceMatrix(h, ctx, nzval.dtype)
+        M.csc_nnz = len(nzval)
+        return M
 
     def set_values(self, nzval):
         nzval = np.ascontiguousarray(nzval, dtype=self.dtype)
         _lib.call("pa_mat_set_values", self.h, nzval.ctypes.data_as(C.c_void_p))
+
+    def get_values(self):
+        """nonzeros(A) in CSC order, ghost rows included."""
+        n = getattr(self, "csc_nnz", None)
+        if n is None:
+            raise _lib.PAError("matrix was not built from a CSC pattern")
+        a = np.empty(n, dtype=self.dtype)
+        _lib.call("pa_mat_get_values", self.h, a.ctypes.data_as(C.c_void_p))
+        return a
 
     def info(self):
         v = [C.c_int64() for _ in range(5)]

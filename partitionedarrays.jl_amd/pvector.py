@@ -13,9 +13,11 @@ import math
 import numpy as np
 
 from . import _lib
-from .backends import PData, map_parts
-from .device import (DeviceMatrix, DeviceVector, contexts, device_exchanger, device_index)
-from .prange import PRange, hids_are_equal, oids_are_equal
+from .backends import PData, exchange, map_parts, unzip
+from .device import (DeviceMatrix, DeviceMatrixExchanger, DeviceVector, contexts, device_exchanger,
+                     device_index)
+from .helpers import Table, counts_to_ptrs
+from .prange import Exchanger, PRange, empty_exchanger, hids_are_equal, oids_are_equal
 
 
 # ---------------------------------------------------------------------------
@@ -184,8 +186,11 @@ def _hs(objs):
     return _lib.ptr_array([o.h if o is not None else None for o in objs])
 
 
-def exchange_(v: PVector) -> PVector:
-    """exchange!(v) (Interfaces.jl:453-458, 2071-2075): owner → ghost values."""
+def exchange_(v):
+    """exchange!(v) (Interfaces.jl:453-458, 2071-2075): owner → ghost values.
+    For a PSparseMatrix: exchange!(A) over nonzeros(A) (2375-2381)."""
+    if isinstance(v, PSparseMatrix):
+        return _mat_exchange(v, _lib.PA_REPLACE, 0, 0)
     ctxs = contexts(v.values)
     xg = [device_exchanger(c, v.rows.exchanger, p) for c, p in zip(ctxs, v.values.part_ids)]
     n = len(ctxs)
@@ -194,9 +199,13 @@ def exchange_(v: PVector) -> PVector:
     return v
 
 
-def assemble_(v: PVector) -> PVector:
+def assemble_(v):
     """assemble!(v) (Interfaces.jl:2084-2106): ghost values added to their
-    owners (reverse exchanger, `+`), then ghost values set to zero."""
+    owners (reverse exchanger, `+`), then ghost values set to zero.  For a
+    PSparseMatrix: assemble!(A) (2383-2404), the ghost rows' nonzeros added
+    to the owners' and then zeroed."""
+    if isinstance(v, PSparseMatrix):
+        return _mat_exchange(v, _lib.PA_ADD, 1, 1)
     ctxs = contexts(v.values)
     xg = [device_exchanger(c, v.rows.exchanger, p) for c, p in zip(ctxs, v.values.part_ids)]
     _lib.call("pa_exchange_all", len(ctxs), _hs(v.values.parts), _hs(xg), _lib.ptr_array(_idx(v)),
@@ -242,10 +251,13 @@ class PSparseMatrix:
     """PSparseMatrix(values, rows, cols) (Interfaces.jl:2108-2125): values =
     PData of DeviceMatrix (owned rows in the SELL layout)."""
 
-    def __init__(self, values: PData, rows: PRange, cols: PRange):
+    def __init__(self, values: PData, rows: PRange, cols: PRange, exchanger=None):
         self.values = values
         self.rows = rows
         self.cols = cols
+        # matrix_exchanger(values, rows, cols) (Interfaces.jl:2117): nz ids
+        self.exchanger = exchanger if exchanger is not None else empty_exchanger(rows.partition)
+        self._dev_xchg = None
 
     @property
     def dtype(self):
@@ -263,8 +275,9 @@ class PSparseMatrix:
         for c, A, r, s in zip(ctxs, csc.parts, rows.partition.parts, cols.partition.parts):
             mats.append(DeviceMatrix.from_csc(c, A, device_index(c, r), device_index(c, s),
                                               r.num_lids, s.num_lids))
+        ex = matrix_exchanger(csc, rows, cols)
         return PSparseMatrix(PData(rows.partition.backend, rows.partition.part_ids, mats,
-                                   rows.partition.shape), rows, cols)
+                                   rows.partition.shape), rows, cols, ex)
 
     @staticmethod
     def from_coo(I: PData, J: PData, V: PData, rows: PRange, cols: PRange, ids="local"):
@@ -278,6 +291,65 @@ class PSparseMatrix:
 
     def info(self):
         return map_parts(lambda m: m.info(), self.values)
+
+
+def matrix_exchanger(values: PData, rows: PRange, cols: PRange) -> Exchanger:
+    """matrix_exchanger(values, rows, cols) (Interfaces.jl:2300-2372),
+    vectorised: the nonzeros of ghost rows (CSC order k) grouped by the row
+    owner in rows.exchanger.parts_rcv order; their (gi, gj) are sent to the
+    owner, which answers with nzindex of (gi, gj) in its local matrix."""
+    if not rows.ghost:
+        return empty_exchanger(rows.partition)
+    parts_rcv = rows.exchanger.parts_rcv
+    parts_snd = rows.exchanger.parts_snd
+
+    def setup_rcv(prcv, r, c, A):
+        prcv = np.asarray(prcv, dtype=np.int64)
+        li = A.rowval - 1
+        lj = np.repeat(np.arange(A.n), np.diff(A.colptr))
+        owner = r.lid_to_part[li].astype(np.int64)
+        k = np.flatnonzero(owner != r.part)
+        seg = np.searchsorted(prcv, owner[k])
+        if len(k) and (seg.max() >= len(prcv) or not np.array_equal(prcv[seg], owner[k])):
+            raise KeyError("matrix_exchanger: a ghost row's owner is not in parts_rcv")
+        o = np.argsort(seg, kind="stable")
+        k = k[o]
+        ptrs = counts_to_ptrs(np.bincount(seg, minlength=len(prcv)))
+        gi = r.lid_to_gid[li[k]]
+        gj = c.lid_to_gid[lj[k]]
+        return (Table((k + 1).astype(np.int64), ptrs), Table(gi, ptrs.copy()), Table(gj, ptrs.copy()))
+    k_rcv, gi_rcv, gj_rcv = unzip(map_parts(setup_rcv, parts_rcv, rows.partition, cols.partition, values), 3)
+    segs = lambda t: [t[i] for i in range(1, len(t) + 1)]
+    gi_snd = exchange(map_parts(segs, gi_rcv), parts_snd, parts_rcv)
+    gj_snd = exchange(map_parts(segs, gj_rcv), parts_snd, parts_rcv)
+
+    def setup_snd(r, c, gi, gj, A):
+        ptrs = counts_to_ptrs([len(x) for x in gi])
+        gi = np.concatenate(gi).astype(np.int64) if gi else np.zeros(0, np.int64)
+        gj = np.concatenate(gj).astype(np.int64) if gj else np.zeros(0, np.int64)
+        li = r.to_lids(gi) - 1
+        lj = c.to_lids(gj) - 1
+        # nzindex(A, li, lj) (SparseUtils.jl:96-104): CSC order is sorted by (col, row)
+        key = np.repeat(np.arange(A.n, dtype=np.int64), np.diff(A.colptr)) * A.m + (A.rowval - 1)
+        q = lj * A.m + li
+        pos = np.searchsorted(key, q)
+        ok = (pos < len(key)) & (key[np.minimum(pos, max(len(key) - 1, 0))] == q) if len(key) else pos < 0
+        if not np.all(ok):
+            raise AssertionError("The sparsity pattern of the ghost layer is inconsistent")
+        return Table((pos + 1).astype(np.int64), ptrs)
+    k_snd = map_parts(setup_snd, rows.partition, cols.partition, gi_snd, gj_snd, values)
+    return Exchanger(parts_rcv, parts_snd, k_rcv, k_snd)
+
+
+def _mat_exchange(A: "PSparseMatrix", op, reverse, zero_sent):
+    if A._dev_xchg is None:
+        ex = A.exchanger
+        A._dev_xchg = [DeviceMatrixExchanger(M, ex.parts_rcv.local(p), ex.lids_rcv.local(p),
+                                             ex.parts_snd.local(p), ex.lids_snd.local(p))
+                       for M, p in zip(A.values.parts, A.values.part_ids)]
+    _lib.call("pa_mat_exchange_all", len(A._dev_xchg), _hs(A.values.parts), _hs(A._dev_xchg), op, reverse,
+              zero_sent)
+    return A
 
 
 def mul_(c: PVector, a: PSparseMatrix, b: PVector, alpha=1.0, beta=0.0) -> PVector:

@@ -127,3 +127,76 @@ def test_interfaces_diag_matvec_kat(be, pamd):
     pamd.exchange_(v)
     for vv, s in zip(v.to_host().parts, ids.partition.parts):
         assert (vv == 10.0 * s.lid_to_part).all()
+
+
+def _nz_eq(M, OM):
+    return np.array_equal(M.get_values(), OM.nzval)
+
+
+@pytest.mark.parametrize("fmt", [1, 0])
+@pytest.mark.parametrize("nparts", [4, (2, 2)])
+def test_fem_sa_matrix_exchange_assemble(be, pamd, O, nparts, fmt):
+    """exchange!(A) / assemble!(A) (Interfaces.jl:2375-2404) on test_fem_sa's
+    matrix (ghost rows stored by the COO assembly): nonzeros(A) bit-exact
+    against the oracle after each, and mul! with the assembled values."""
+    prev = pamd._lib.tune("spmv_format", fmt)
+    try:
+        parts = be.get_part_ids(nparts)
+        A, b, x0, _ = pamd.drivers.fem_sa_problem(parts, 10)
+        OA, ob, ox0, _ = O.fem_sa_problem(O.get_part_ids(nparts), 10)
+        for M, OM in zip(A.values.parts, OA.values.parts):
+            assert _nz_eq(M, OM)
+        # give the ghost rows values so both directions move data
+        rng = np.random.default_rng(11)
+        for M, OM in zip(A.values.parts, OA.values.parts):
+            v = rng.uniform(-1, 1, len(OM.nzval))
+            M.set_values(v)
+            OM.nzval[:] = v
+        pamd.assemble_(A)
+        O.assemble_matrix_(OA)
+        for M, OM in zip(A.values.parts, OA.values.parts):
+            assert _nz_eq(M, OM)
+        x = pamd.PVector.from_host(pamd.map_parts(lambda s: rng.uniform(-1, 1, s.num_lids), A.cols.partition),
+                                   A.cols)
+        ox = O.PVector(O.PData([v.copy() for v in x.to_host().parts], OA.cols.partition.shape), OA.cols)
+        y = pamd.PVector.undef(A.rows)
+        oy = O.pvector_undef(OA.rows)
+        pamd.mul_(y, A, x)
+        O.mul_(oy, OA, ox)
+        for p in parts.part_ids:
+            s = A.rows.partition.local(p)
+            assert np.array_equal(y.to_host().local(p)[s.oid_to_lid - 1], oy.values[p][s.oid_to_lid - 1])
+        pamd.exchange_(A)
+        O.exchange_matrix_(OA)
+        for M, OM in zip(A.values.parts, OA.values.parts):
+            assert _nz_eq(M, OM)
+    finally:
+        pamd._lib.tune("spmv_format", prev)
+
+
+def test_interfaces_matrix_exchange_kat(be, pamd, O):
+    """test_interfaces.jl:676-683: fillstored!(A, 1) then exchange!(A) and
+    assemble!(A) on the irregular IndexSet partition's diagonal matrix: each
+    owned diagonal ends as 1 + (number of parts ghosting it), ghosts 0."""
+    import json
+    import os
+    k = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "interfaces_kats.json")))["exchanger"]
+    parts = be.get_part_ids(4)
+    sets = [pamd.IndexSet(p + 1, k["lid_to_gid"][p], k["lid_to_part"][p]) for p in range(4)]
+    ids = pamd.prange_from_partition(10, pamd.PData(parts.backend, parts.part_ids, sets, parts.shape))
+    csc = pamd.map_parts(lambda s: pamd.compresscoo(np.arange(1, s.num_lids + 1), np.arange(1, s.num_lids + 1),
+                                                    np.full(s.num_lids, 2.0), s.num_lids, s.num_lids), ids.partition)
+    A = pamd.PSparseMatrix.from_csc(csc, ids, ids)
+    for M, C in zip(A.values.parts, csc.parts):
+        M.set_values(np.ones(C.nnz))
+    pamd.exchange_(A)
+    assert all((M.get_values() == 1.0).all() for M in A.values.parts)
+    pamd.assemble_(A)
+    nghost = {}
+    for s in sets:
+        for g, o in zip(s.lid_to_gid, s.lid_to_part):
+            if o != s.part:
+                nghost[int(g)] = nghost.get(int(g), 0) + 1
+    for M, s in zip(A.values.parts, sets):
+        want = np.where(s.lid_to_part == s.part, 1.0 + np.array([nghost.get(int(g), 0) for g in s.lid_to_gid]), 0.0)
+        assert np.array_equal(M.get_values(), want)

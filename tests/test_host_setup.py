@@ -219,3 +219,40 @@ def test_irregular_partition_matches_oracle(pamd, O, nparts, N, kind):
         OM = OA.values[p]
         assert np.array_equal(M.colptr, OM.colptr) and np.array_equal(M.rowval, OM.rowval)
         assert np.array_equal(M.nzval, OM.nzval)
+
+
+@pytest.mark.parametrize("nparts", [4, (2, 2)])
+def test_matrix_exchanger_matches_oracle(pamd, O, nparts):
+    """matrix_exchanger (Interfaces.jl:2300-2372) of test_fem_sa's matrix, whose
+    local CSCs store ghost rows: the product's vectorised restatement equals
+    the oracle's literal one (parts, nz ids k in both directions)."""
+    parts = pamd.sequential.get_part_ids(nparts)
+    rows, cols, I, J, V, _, _, _ = pamd.drivers.fem_sa_host(parts, 10)
+    csc = pamd.map_parts(lambda i, j, v, r, c: pamd.compresscoo(r.to_lids(i), c.to_lids(j), v, r.num_lids,
+                                                                c.num_lids), I, J, V, rows.partition, cols.partition)
+    ex = pamd.pvector.matrix_exchanger(csc, rows, cols)
+    OA, _, _, _ = O.fem_sa_problem(O.get_part_ids(nparts), 10)
+    oex = OA.exchanger
+    assert sum(len(oex.lids_rcv[p].data) for p in parts.part_ids) > 0
+    for p in parts.part_ids:
+        assert list(ex.parts_rcv.local(p)) == list(oex.parts_rcv[p])
+        assert list(ex.parts_snd.local(p)) == list(oex.parts_snd[p])
+        for a, b in ((ex.lids_rcv.local(p), oex.lids_rcv[p]), (ex.lids_snd.local(p), oex.lids_snd[p])):
+            assert a.data.tolist() == list(b.data) and a.ptrs.tolist() == list(b.ptrs)
+
+
+def test_matrix_exchanger_inconsistent_pattern(pamd):
+    """setup_snd's @check (Interfaces.jl:2360): a ghost-row nonzero the owner
+    does not store raises."""
+    parts = pamd.sequential.get_part_ids(2)
+    rows = pamd.prange_linear(parts, 4)
+    rows = pamd.add_gids(rows, pamd.PData(parts.backend, parts.part_ids, [np.array([3]), np.array([2])],
+                                          parts.shape))
+    cols = rows
+    # part 1 stores (3,3) in its ghost row 3, part 2 owns row 3 but stores only (3,4)
+    c1 = pamd.compresscoo(rows.partition.local(1).to_lids([1, 3]), rows.partition.local(1).to_lids([1, 3]),
+                          [1.0, 1.0], 3, 3)
+    c2 = pamd.compresscoo(rows.partition.local(2).to_lids([3]), rows.partition.local(2).to_lids([4]), [1.0], 3, 3)
+    csc = pamd.PData(parts.backend, parts.part_ids, [c1, c2], parts.shape)
+    with pytest.raises(AssertionError):
+        pamd.pvector.matrix_exchanger(csc, rows, cols)
