@@ -316,6 +316,10 @@ def main():
             "kernel_ms": round(kernel_ms, 4),
             "algorithmic_bytes_per_launch": spmv_bytes,
             "actual_hbm_gbs": None if traffic is None else round(traffic / (kernel_ms * 1e-3) / 1e9, 1),
+            "actual_frac": None if traffic is None else round(traffic / (kernel_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+            "bytes_note": ("achieved/frac count SURVEY.md 8d's format-independent CSR bytes (nnz*(S+4) + ...); "
+                           "pattern slices read no column ids for their regular rows, so frac can exceed 1. "
+                           "actual_frac = PMC traffic / kernel time / peak is the HBM utilisation."),
             "column_format": (f"pattern slices {info['pattern_slices']}/{info['nslices']}, "
                               f"regular rows {info['regular_rows']}/{info['nrows']}, side rows {info['side_rows']}"),
             "int32_columns_kernel_ms": round(kernel_ms_int32, 4),

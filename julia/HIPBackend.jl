@@ -164,6 +164,32 @@ function PartitionedArrays.assemble!(v::PVector{T,<:HIPData}) where T
   mark_device_dirty!(v); v
 end
 
+# exchange!(A) / assemble!(A) over nonzeros (Interfaces.jl:2375-2404); the
+# matrix exchanger (2300-2372) is built on the host as the reference does and
+# handed over with its Int64 nz ids.
+function pa_mat_xchg(A::Ptr{Cvoid}, ex::Exchanger, part)
+  out = Ref{Ptr{Cvoid}}(C_NULL)
+  lr, ls = ex.lids_rcv.parts[part], ex.lids_snd.parts[part]
+  pr, ps = Int32.(ex.parts_rcv.parts[part]), Int32.(ex.parts_snd.parts[part])
+  check(ccall((:pa_mat_xchg_create, libpa), Cint,
+              (Ptr{Cvoid}, Int32, Ptr{Int32}, Ptr{Int32}, Ptr{Int64},
+               Int32, Ptr{Int32}, Ptr{Int32}, Ptr{Int64}, Ref{Ptr{Cvoid}}),
+              A, length(pr), pr, lr.ptrs, Int64.(lr.data), length(ps), ps, ls.ptrs, Int64.(ls.data), out))
+  out[]
+end
+function PartitionedArrays.exchange!(a::PSparseMatrix{T,<:HIPData}) where T
+  A, mx = dev_mat(a), dev_mat_xchg(a)
+  check(ccall((:pa_mat_exchange_all, libpa), Cint,
+              (Cint, Ptr{Ptr{Cvoid}}, Ptr{Ptr{Cvoid}}, Cint, Cint, Cint), length(A), A, mx, 0, 0, 0))
+  a
+end
+function PartitionedArrays.assemble!(a::PSparseMatrix{T,<:HIPData}) where T
+  A, mx = dev_mat(a), dev_mat_xchg(a)
+  check(ccall((:pa_mat_exchange_all, libpa), Cint,
+              (Cint, Ptr{Ptr{Cvoid}}, Ptr{Ptr{Cvoid}}, Cint, Cint, Cint), length(A), A, mx, 1, 1, 1))
+  a
+end
+
 # dot / norm (Interfaces.jl:1767-1772, 1985-1992)
 function LinearAlgebra.dot(a::PVector{T,<:HIPData}, b::PVector{T,<:HIPData}) where T
   r = Ref{T}(zero(T))
