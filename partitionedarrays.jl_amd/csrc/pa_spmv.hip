@@ -95,6 +95,14 @@ __device__ inline c128 shfl_down_acc(c128 v, int d) {
   return c128{__shfl_down(v.re, d, 64), __shfl_down(v.im, d, 64)};
 }
 
+// Branch-free select.  Complex values are selected per component: a select
+// of the whole struct made clang route c128 through scratch (a stack slot
+// indexed by the condition) on every entry.
+__device__ __forceinline__ float pick(bool c, float a, float b) { return c ? a : b; }
+__device__ __forceinline__ double pick(bool c, double a, double b) { return c ? a : b; }
+__device__ __forceinline__ c64 pick(bool c, c64 a, c64 b) { return c64{c ? a.re : b.re, c ? a.im : b.im}; }
+__device__ __forceinline__ c128 pick(bool c, c128 a, c128 b) { return c128{c ? a.re : b.re, c ? a.im : b.im}; }
+
 // int32-column rows: c < 0 is padding (skipped: never multiplied)
 template <typename T, int R, bool ALPHA, bool NT, int U>
 __device__ __forceinline__ void rows_int32(T (&acc)[R], const IPack<R>* __restrict__ cp,
@@ -123,7 +131,7 @@ __device__ __forceinline__ void rows_int32(T (&acc)[R], const IPack<R>* __restri
         T xx = xv[u][r];
         if (ALPHA) xx = xx * alpha;
         const T t = acc[r] + v[u].v[r] * xx;
-        acc[r] = (c[u].c[r] >= 0) ? t : acc[r];
+        acc[r] = pick(c[u].c[r] >= 0, t, acc[r]);
       }
   }
   for (; k < len; ++k) {
@@ -135,7 +143,7 @@ __device__ __forceinline__ void rows_int32(T (&acc)[R], const IPack<R>* __restri
       T xx = x[cc >= 0 ? cc : 0];
       if (ALPHA) xx = xx * alpha;
       const T t = acc[r] + v.v[r] * xx;
-      acc[r] = (cc >= 0) ? t : acc[r];
+      acc[r] = pick(cc >= 0, t, acc[r]);
     }
   }
 }
