@@ -199,9 +199,10 @@ int finalize_pattern(pa_mat* A, int kmax, int64_t noids) {
   HIPC(hipStreamSynchronize(st));
   dev_free(d_pghost);
   dev_free(d_nirreg);
-  std::vector<int32_t> pint, pbnd, side;
+  std::vector<int32_t> pint, pbnd, xint, xbnd, side;
   for (int64_t s = 0; s < ns; ++s) {
-    (pghost[s] ? pbnd : pint).push_back((int32_t)s);
+    if (kind[s]) (pghost[s] ? pbnd : pint).push_back((int32_t)s);
+    else (pghost[s] ? xbnd : xint).push_back((int32_t)s);
     if (kind[s]) {
       ++A->npattern_slices;
       const int64_t nvalid = std::min<int64_t>(A->H, A->nrows - s * A->H);
@@ -213,7 +214,11 @@ int finalize_pattern(pa_mat* A, int kmax, int64_t noids) {
   }
   A->np_int = (int64_t)pint.size();
   A->np_bnd = (int64_t)pbnd.size();
-  if (dev_upload(&A->d_pint_list, pint) || dev_upload(&A->d_pbnd_list, pbnd)) return -1;
+  A->nx_int = (int64_t)xint.size();
+  A->nx_bnd = (int64_t)xbnd.size();
+  if (dev_upload(&A->d_pint_list, pint) || dev_upload(&A->d_pbnd_list, pbnd) ||
+      dev_upload(&A->d_xint_list, xint) || dev_upload(&A->d_xbnd_list, xbnd))
+    return -1;
   // side SELL
   A->s_nrows = (int64_t)side.size();
   if (A->s_nrows > 0) {
@@ -910,7 +915,8 @@ int pa_mat_destroy(pa_mat* A) {
   dev_free(A->d_col);
   dev_free(A->d_val);
   for (void* p : {(void*)A->d_kind, (void*)A->d_plen, (void*)A->d_pat, (void*)A->d_mask,
-                  (void*)A->d_pint_list, (void*)A->d_pbnd_list, (void*)A->d_s_off, (void*)A->d_s_len,
+                  (void*)A->d_pint_list, (void*)A->d_pbnd_list, (void*)A->d_xint_list,
+                  (void*)A->d_xbnd_list, (void*)A->d_s_off, (void*)A->d_s_len,
                   (void*)A->d_s_col, A->d_s_val, (void*)A->d_s_rowmap, (void*)A->d_s_rowlen, A->d_dotp})
     dev_free(p);
   delete A;
@@ -997,6 +1003,7 @@ static int spmv_impl(int n, pa_mat* const A[], pa_vec* const y[], const pa_index
     // interior slices (no ghost column): overlap with the halo transport
     if (g_spmv_format == 1 && A[i]->has_pat) {
       launch_spmv_part(0, A[i]->np_int, A[i]->d_pint_list, A[i], x[i]->d, y[i]->d, ymap, has_alpha, bmode, alpha, beta, dotp[i], c->s_main);
+      launch_spmv_part(1, A[i]->nx_int, A[i]->d_xint_list, A[i], x[i]->d, y[i]->d, ymap, has_alpha, bmode, alpha, beta, dotp[i], c->s_main);
     } else if (A[i]->d_bnd_list) {  // split layout (the interior list may be empty)
       if (A[i]->nslices_int > 0)
         launch_spmv_part(1, A[i]->nslices_int, A[i]->d_int_list, A[i], x[i]->d, y[i]->d, ymap, has_alpha, bmode, alpha, beta, dotp[i], c->s_main);
@@ -1019,6 +1026,7 @@ static int spmv_impl(int n, pa_mat* const A[], pa_vec* const y[], const pa_index
     if (g_spmv_format == 1 && A[i]->has_pat) {
       // pattern slices reading ghosts, then the side rows (after the halo)
       launch_spmv_part(0, A[i]->np_bnd, A[i]->d_pbnd_list, A[i], x[i]->d, y[i]->d, ymap, has_alpha, bmode, alpha, beta, dotp[i], c->s_main);
+      launch_spmv_part(1, A[i]->nx_bnd, A[i]->d_xbnd_list, A[i], x[i]->d, y[i]->d, ymap, has_alpha, bmode, alpha, beta, dotp[i], c->s_main);
       launch_spmv_part(2, A[i]->s_nslices, nullptr, A[i], x[i]->d, y[i]->d, ymap, has_alpha, bmode, alpha, beta, dotp[i], c->s_main);
     } else if (A[i]->d_bnd_list) {
       launch_spmv_part(1, A[i]->nslices - A[i]->nslices_int, A[i]->d_bnd_list, A[i], x[i]->d, y[i]->d, ymap,

@@ -186,9 +186,12 @@ struct pa_mat {
   int32_t* d_plen = nullptr;         // per slice: entries per row (pattern len or int32 len)
   int32_t* d_pat = nullptr;          // nslices*kmax offsets
   uint64_t* d_mask = nullptr;        // nslices*(H/64) regular-row bits
-  int32_t* d_pint_list = nullptr;    // pattern mode: slices without ghost reads
-  int32_t* d_pbnd_list = nullptr;    // pattern mode: slices reading ghosts
+  int32_t* d_pint_list = nullptr;    // pattern mode: pattern slices without ghost reads
+  int32_t* d_pbnd_list = nullptr;    // pattern mode: pattern slices reading ghosts
   int64_t np_int = 0, np_bnd = 0;
+  int32_t* d_xint_list = nullptr;    // pattern mode: int32-column slices without ghost columns
+  int32_t* d_xbnd_list = nullptr;    // pattern mode: int32-column slices with ghost columns
+  int64_t nx_int = 0, nx_bnd = 0;
   int64_t npattern_slices = 0, nregular_rows = 0;
   // side SELL: the irregular rows of pattern slices (row map → oid)
   int64_t s_nrows = 0, s_nslices = 0, s_slots = 0;

@@ -65,7 +65,6 @@ struct SpmvArgs {
   const int32_t* slen;      // entries per row of the slice
   const int32_t* col;
   const T* val;
-  const int32_t* kind;      // per slice 1 = pattern (null: all int32)
   const int32_t* pat;       // kmax offsets per slice
   const uint64_t* mask;     // H/64 words per slice
   int kmax;
@@ -193,7 +192,10 @@ __device__ __forceinline__ void rows_pattern(T (&acc)[R], const int32_t* __restr
 
 // BMODE: 0 → acc = 0 (β == 0: fill!(co,0)), 1 → acc = y (β == 1),
 //        2 → acc = y*β (rmul!(co,β)).  Interfaces.jl:2262-2263.
-template <typename T, int R, bool ALPHA, int BMODE, int U>
+// PAT: the launch's slices are pattern slices (implied columns for the rows
+// of their mask) or int32-column slices; one kernel per kind keeps the hot
+// loop free of the other's code and registers.
+template <typename T, int R, bool ALPHA, int BMODE, int U, bool PAT>
 __global__ __launch_bounds__(256) void k_spmv_sell(SpmvArgs<T> a) {
   constexpr int H = 64 * R;
   const int lane = threadIdx.x & 63;
@@ -204,10 +206,8 @@ __global__ __launch_bounds__(256) void k_spmv_sell(SpmvArgs<T> a) {
   const int64_t off = a.soff[s];
   const int len = a.slen[s];
   const int64_t row0 = s * H + (int64_t)lane * R;
-  const bool pattern = a.kind && a.kind[s];
-
   bool ok[R];
-  if (pattern) {
+  if (PAT) {
     const uint64_t m = a.mask[s * (H / 64) + (lane * R) / 64];
 #pragma unroll
     for (int r = 0; r < R; ++r) ok[r] = ((m >> ((lane * R + r) & 63)) & 1ull) && (row0 + r < a.nrows);
@@ -232,7 +232,7 @@ __global__ __launch_bounds__(256) void k_spmv_sell(SpmvArgs<T> a) {
   }
 
   const Pack<T, R>* __restrict__ vp = reinterpret_cast<const Pack<T, R>*>(a.val + off) + lane;
-  if (pattern) {
+  if (PAT) {
     const int32_t* pat = a.pat + s * a.kmax;
     if (a.flags & SPMV_NT) rows_pattern<T, R, ALPHA, true, U>(acc, pat, vp, len, a.x, row0, ok, a.alpha);
     else rows_pattern<T, R, ALPHA, false, U>(acc, pat, vp, len, a.x, row0, ok, a.alpha);
@@ -268,31 +268,31 @@ __global__ __launch_bounds__(256) void k_spmv_sell(SpmvArgs<T> a) {
   }
 }
 
-template <typename T, int R, bool ALPHA, int BMODE>
+template <typename T, int R, bool ALPHA, int BMODE, bool PAT>
 static void launch_t(const SpmvArgs<T>& a, hipStream_t st) {
   const int64_t blocks = (a.nwork + 3) / 4;
   if (blocks == 0) return;
   if (g_spmv_unroll == 4)
-    hipLaunchKernelGGL((k_spmv_sell<T, R, ALPHA, BMODE, 4>), dim3(blocks), dim3(256), 0, st, a);
+    hipLaunchKernelGGL((k_spmv_sell<T, R, ALPHA, BMODE, 4, PAT>), dim3(blocks), dim3(256), 0, st, a);
   else
-    hipLaunchKernelGGL((k_spmv_sell<T, R, ALPHA, BMODE, 8>), dim3(blocks), dim3(256), 0, st, a);
+    hipLaunchKernelGGL((k_spmv_sell<T, R, ALPHA, BMODE, 8, PAT>), dim3(blocks), dim3(256), 0, st, a);
 }
 
-template <typename T, int R>
+template <typename T, int R, bool PAT>
 static void launch_ab(const SpmvArgs<T>& a, bool has_alpha, int bmode, hipStream_t st) {
   if (!has_alpha) {
-    if (bmode == 0) launch_t<T, R, false, 0>(a, st);
-    else if (bmode == 1) launch_t<T, R, false, 1>(a, st);
-    else launch_t<T, R, false, 2>(a, st);
+    if (bmode == 0) launch_t<T, R, false, 0, PAT>(a, st);
+    else if (bmode == 1) launch_t<T, R, false, 1, PAT>(a, st);
+    else launch_t<T, R, false, 2, PAT>(a, st);
   } else {
-    if (bmode == 0) launch_t<T, R, true, 0>(a, st);
-    else if (bmode == 1) launch_t<T, R, true, 1>(a, st);
-    else launch_t<T, R, true, 2>(a, st);
+    if (bmode == 0) launch_t<T, R, true, 0, PAT>(a, st);
+    else if (bmode == 1) launch_t<T, R, true, 1, PAT>(a, st);
+    else launch_t<T, R, true, 2, PAT>(a, st);
   }
 }
 
-// which = 0: main structure, pattern mode; 1: main structure, int32 mode;
-// 2: side SELL.  list/nwork select the slices.
+// which = 0: pattern slices of the main structure; 1: int32-column slices
+// of the main structure; 2: side SELL.  list/nwork select the slices.
 template <typename T, int R>
 static void launch_which(int which, int64_t nwork, const int32_t* list, const pa_mat* A, const void* x,
                          void* y, const int32_t* ymap, bool has_alpha, int bmode, const void* alpha,
@@ -323,7 +323,6 @@ static void launch_which(int which, int64_t nwork, const int32_t* list, const pa
     a.nrows = A->nrows;
     if (which == 0) {
       a.slen = A->d_plen;
-      a.kind = A->d_kind;
       a.pat = A->d_pat;
       a.mask = A->d_mask;
       a.kmax = A->kmax;
@@ -331,7 +330,8 @@ static void launch_which(int which, int64_t nwork, const int32_t* list, const pa
       a.slen = A->d_slice_len;
     }
   }
-  launch_ab<T, R>(a, has_alpha, bmode, st);
+  if (which == 0) launch_ab<T, R, true>(a, has_alpha, bmode, st);
+  else launch_ab<T, R, false>(a, has_alpha, bmode, st);
 }
 
 void launch_spmv_part(int which, int64_t nwork, const int32_t* list, const pa_mat* A, const void* x,
