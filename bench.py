@@ -113,23 +113,24 @@ def cg_mode(args, pamd, backend, parts, A, ngpu, world, sync):
     b = pamd.PVector.from_host(pamd.map_parts(
         lambda s: np.random.default_rng(7 + s.part).uniform(-1, 1, s.num_lids).astype(dtype), cols.partition), cols)
     out = {}
-    for fused in (True, False):
+    variants = {"device": dict(device=True, batch=16), "fused": dict(fused=True), "unfused": dict(fused=False)}
+    for name, kw in variants.items():
         x = pamd.PVector.undef(cols, dtype).fill_(0)
-        pamd.cg_(x, A, b, reltol=0.0, maxiter=args.warmup, fused=fused)
+        pamd.cg_(x, A, b, reltol=0.0, maxiter=args.warmup, **kw)
         sync()
         if world > 1:
             dist.barrier()
         x = pamd.PVector.undef(cols, dtype).fill_(0)
         t0 = time.perf_counter()
         hist = []
-        pamd.cg_(x, A, b, reltol=0.0, maxiter=args.cg, fused=fused, history=hist)
+        pamd.cg_(x, A, b, reltol=0.0, maxiter=args.cg, history=hist, **kw)
         sync()
         el = time.perf_counter() - t0
         if world > 1:
             t = torch.tensor([el], dtype=torch.float64)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             el = float(t.item())
-        out[fused] = (1e3 * el / max(1, len(hist)), len(hist), hist[-1] if hist else None)
+        out[name] = (1e3 * el / max(1, len(hist)), len(hist), hist[-1] if hist else None)
     p0 = parts.part_ids[0]
     info = A.values.local(p0).info()
     S = np.dtype(dtype).itemsize
@@ -137,14 +138,17 @@ def cg_mode(args, pamd, backend, parts, A, ngpu, world, sync):
     it_bytes = (info["nnz"] * (S + 4) + (n + 1) * 4 + 2 * n * S) + 12 * n * S  # SpMV + dot 2 + norm 1 + 3 axpy x3
     rows_all = n * ngpu
     line = {"metric": "CG iteration time (weak scaling, BASELINE config 4)",
-            "value": round(out[True][0], 4), "unit": "ms/iteration", "higher_is_better": False,
-            "n_gpus": ngpu, "iterations": out[True][1], "scaling": "weak",
+            "value": round(out["device"][0], 4), "unit": "ms/iteration", "higher_is_better": False,
+            "n_gpus": ngpu, "iterations": out["device"][1], "scaling": "weak",
             "dtype": args.dtype, "data": "synthetic (seeded uniform b, x0 = 0)",
             "config": {"workload": f"cg! on the {args.kind}-pt operator, {args.n}^3 nodes per GPU",
-                       "dofs": rows_all, "unfused_ms_per_iteration": round(out[False][0], 4),
+                       "dofs": rows_all, "recurrence": "scalars on the device (pa_cg_solve_all, batch 16)",
+                       "host_driven_fused_ms_per_iteration": round(out["fused"][0], 4),
+                       "host_driven_unfused_ms_per_iteration": round(out["unfused"][0], 4),
                        "algorithmic_bytes_per_iteration_per_gpu": it_bytes,
-                       "gbs_per_gpu_fused": round(it_bytes / (out[True][0] * 1e-3) / 1e9, 1),
-                       "final_residual": out[True][2]}}
+                       "gbs_per_gpu_device": round(it_bytes / (out["device"][0] * 1e-3) / 1e9, 1),
+                       "final_residual": out["device"][2],
+                       "same_history_as_host_driven": out["device"][2] == out["fused"][2]}}
     return line
 
 

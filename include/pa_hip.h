@@ -188,6 +188,26 @@ int pa_cg_update_all(int n, pa_vec* const x[], pa_vec* const r[],
                      const pa_index* const idx[], const void* alpha,
                      double* rnorm);
 
+/* IterativeSolvers.cg!(x, A, b; reltol, abstol, maxiter) (v0.9, not
+ * vendored; called at test_fdm.jl:115, test_fem_sa.jl:135, recurrence in
+ * SURVEY.md §3.5) with the scalar recurrence on the device (SURVEY.md §8f
+ * item 3): u, r, c are the caller's work vectors (CGStateVariables), all
+ * five vectors on a.cols' partition with contiguous owned lids.  Setup as
+ * cg_iterator!: u = 0, r = b - A*x, tolerance = max(reltol*norm(b), abstol).
+ * Then per iteration β = res²/prev², u .= r .+ β.*u, mul!(c,A,u) with
+ * dot(u,c) fused, α = res²/dot, x .+= α.*u, r .-= α.*c, res = norm(r) — the
+ * same arithmetic as the host-driven loop over pa_spmv_dot_all /
+ * pa_cg_update_all, bit for bit.  The host enqueues `batch` iterations
+ * between reads of the device's done flag (iterations after convergence
+ * are no-ops); every rank enqueues the same number, so RCCL calls match.
+ * history (optional, maxiter doubles): the residual after each iteration. */
+int pa_cg_solve_all(int n, pa_mat* const A[], pa_vec* const x[],
+                    const pa_vec* const b[], pa_vec* const u[],
+                    pa_vec* const r[], pa_vec* const c[],
+                    const pa_index* const idx[], pa_xchg* const xg[],
+                    double reltol, double abstol, int64_t maxiter, int batch,
+                    int64_t* iterations, double* residual, double* history);
+
 /* exchange!(combine, values, exchanger) (Interfaces.jl:846-889) for the n
  * local parts; reverse != 0 uses reverse(exchanger) (Interfaces.jl:796).
  * With reverse=1, op=PA_ADD and zero_ghosts=1 this is assemble!(v)

@@ -63,6 +63,9 @@ _SIGS = {
     "pa_spmv_all": [C.c_int, C.POINTER(_p), C.POINTER(_p), C.POINTER(_p), C.POINTER(_p), C.POINTER(_p), C.POINTER(_p), _p, _p],
     "pa_spmv_dot_all": [C.c_int, C.POINTER(_p), C.POINTER(_p), C.POINTER(_p), C.POINTER(_p), C.POINTER(_p), C.POINTER(_p), _p, _p, _p],
     "pa_cg_update_all": [C.c_int, C.POINTER(_p), C.POINTER(_p), C.POINTER(_p), C.POINTER(_p), C.POINTER(_p), _p, C.POINTER(C.c_double)],
+    "pa_cg_solve_all": [C.c_int, C.POINTER(_p), C.POINTER(_p), C.POINTER(_p), C.POINTER(_p), C.POINTER(_p),
+                        C.POINTER(_p), C.POINTER(_p), C.POINTER(_p), C.c_double, C.c_double, C.c_int64, C.c_int,
+                        _i64p, C.POINTER(C.c_double), C.POINTER(C.c_double)],
     "pa_exchange_all": [C.c_int, C.POINTER(_p), C.POINTER(_p), C.POINTER(_p), C.c_int, C.c_int, C.c_int],
     "pa_dot_all": [C.c_int, C.POINTER(_p), C.POINTER(_p), C.POINTER(_p), C.POINTER(_p), _p],
     "pa_norm2_all": [C.c_int, C.POINTER(_p), C.POINTER(_p), _p],

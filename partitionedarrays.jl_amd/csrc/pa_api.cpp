@@ -30,7 +30,11 @@ void launch_side_len(pa_mat* A, int64_t n, const int32_t* rows, int32_t* len, in
 void launch_side_fill(pa_mat* A, const int32_t* rows, const int32_t* len, hipStream_t st);
 void launch_fold(int cplx, int nb, const void* in, void* scratch, void* out, hipStream_t st);
 void launch_cg_xr(int dtype, int64_t n, int64_t noids, const int32_t* own, void* x, void* r, const void* u,
-                  const void* c, const void* alpha, double* part, int nb, hipStream_t st);
+                  const void* c, const void* alpha, const CGState* cst, double* part, int nb, hipStream_t st);
+void launch_cg_xpby(int dtype, int64_t n, void* u, const void* r, const CGState* cst, hipStream_t st);
+void launch_cg_alpha(int dtype, int P, const void* gathered, CGState* cst, hipStream_t st);
+void launch_cg_step(int P, const double* gathered, CGState* cst, double* history, hipStream_t st);
+void launch_gather_ptrs(int P, const void* const* srcs, int accsz, void* out, hipStream_t st);
 extern int g_spmv_format;
 void launch_pack(int dtype, int64_t n, const int32_t* lids, const void* v, void* buf,
                  hipStream_t st);
@@ -433,7 +437,7 @@ int pa_ctx_create(int device, int part, int nparts, pa_ctx** out) {
   HIPC(hipMalloc(&c->d_fold, 256 * 16));
   HIPC(hipMalloc(&c->d_result, 16));
   HIPC(hipMalloc(&c->d_gather, (size_t)nparts * 16));
-  HIPC(hipHostMalloc(&c->h_pinned, (size_t)(nparts + 1) * 16));
+  HIPC(hipHostMalloc(&c->h_pinned, std::max<size_t>((size_t)(nparts + 1) * 16, 256)));  // gathered partials / CG state
   HIPC(hipEventCreateWithFlags(&c->ev_packed, hipEventDisableTiming));
   HIPC(hipEventCreateWithFlags(&c->ev_recvd, hipEventDisableTiming));
   for (auto& e : c->ev_t) HIPC(hipEventCreate(&e));
@@ -1212,7 +1216,7 @@ int pa_cg_update_all(int n, pa_vec* const x[], pa_vec* const r[], const pa_vec* 
     HIPC(hipSetDevice(cx->device));
     if (idx[i]->own_contig) {
       const int nb = (int)std::min<int64_t>(8192, std::max<int64_t>(1, (m + 255) / 256));
-      launch_cg_xr(dt, m, idx[i]->noids, nullptr, x[i]->d, r[i]->d, u[i]->d, c[i]->d, alpha,
+      launch_cg_xr(dt, m, idx[i]->noids, nullptr, x[i]->d, r[i]->d, u[i]->d, c[i]->d, alpha, nullptr,
                    (double*)cx->d_partials, nb, cx->s_main);
       launch_fold(0, nb, cx->d_partials, cx->d_fold, cx->d_result, cx->s_main);
     } else {  // unfused: two broadcasts and the norm reduction
@@ -1227,7 +1231,216 @@ int pa_cg_update_all(int n, pa_vec* const x[], pa_vec* const r[], const pa_vec* 
   if (gather_results(n, ctxs.data(), false, &vals)) return -1;
   double s = 0.0;
   for (const auto& v : vals) s = s + v.re;
-  *rnorm = std::pow(s, 1.0 / 2.0);
+  *rnorm = std::sqrt(s);  // (…)^(1/2), correctly rounded
+  return 0;
+}
+
+// ---------------------------------------------------------------------------
+// Device-driven CG (IterativeSolvers 0.9 cg!): the
+// scalar recurrence lives on the device (CGState per part), so the host
+// enqueues iterations in batches and only reads the done flag between
+// batches.  Each reduction ends in a device all-gather of the part values
+// (RCCL across processes; a gather kernel over the local parts' results in
+// one process), then every part folds them in part order.
+namespace {
+
+struct CGRun {
+  int n = 0, P = 0;
+  bool remote = false;
+  std::vector<pa_ctx*> ctxs;
+  std::vector<CGState*> st;
+  std::vector<double*> hist;
+  std::vector<void**> ptrs;         // local mode: per part, device table of the parts' d_result
+  std::vector<hipEvent_t> ev_red;   // local mode: part value ready
+  std::vector<hipEvent_t> ev_gat;   // local mode: part has gathered
+  ~CGRun() {
+    for (int i = 0; i < n; ++i) {
+      if (i < (int)ctxs.size()) (void)hipSetDevice(ctxs[i]->device);
+      if (i < (int)st.size()) dev_free(st[i]);
+      if (i < (int)hist.size()) dev_free(hist[i]);
+      if (i < (int)ptrs.size()) dev_free(ptrs[i]);
+      if (i < (int)ev_red.size() && ev_red[i]) (void)hipEventDestroy(ev_red[i]);
+      if (i < (int)ev_gat.size() && ev_gat[i]) (void)hipEventDestroy(ev_gat[i]);
+    }
+  }
+};
+
+// every part's d_result (accsz bytes) → d_gather[part-1] of every part
+int cg_gather(CGRun& R, size_t accsz) {
+  if (R.remote) {
+    pa_ctx* c = R.ctxs[0];
+    HIPC(hipSetDevice(c->device));
+    NCCLC(ncclAllGather(c->d_result, c->d_gather, accsz, ncclUint8, (ncclComm_t)c->comm, c->s_main));
+    return 0;
+  }
+  for (int i = 0; i < R.n; ++i) {
+    HIPC(hipSetDevice(R.ctxs[i]->device));
+    HIPC(hipEventRecord(R.ev_red[i], R.ctxs[i]->s_main));
+  }
+  for (int i = 0; i < R.n; ++i) {
+    pa_ctx* c = R.ctxs[i];
+    HIPC(hipSetDevice(c->device));
+    for (int j = 0; j < R.n; ++j)
+      if (j != i) HIPC(hipStreamWaitEvent(c->s_main, R.ev_red[j], 0));
+    launch_gather_ptrs(R.P, (const void* const*)R.ptrs[i], (int)accsz, c->d_gather, c->s_main);
+    HIPC(hipEventRecord(R.ev_gat[i], c->s_main));
+  }
+  // no part overwrites its d_result before every part has read it
+  for (int i = 0; i < R.n; ++i) {
+    pa_ctx* c = R.ctxs[i];
+    HIPC(hipSetDevice(c->device));
+    for (int j = 0; j < R.n; ++j)
+      if (j != i) HIPC(hipStreamWaitEvent(c->s_main, R.ev_gat[j], 0));
+  }
+  return 0;
+}
+
+void scalar_one(int dt, unsigned char out[16], double v) {
+  std::memset(out, 0, 16);
+  switch (dt) {
+    case PA_F32: case PA_C64: { const float f = (float)v; std::memcpy(out, &f, 4); } break;
+    default: std::memcpy(out, &v, 8); break;
+  }
+}
+
+}  // namespace
+
+int pa_cg_solve_all(int n, pa_mat* const A[], pa_vec* const x[], const pa_vec* const b[],
+                    pa_vec* const u[], pa_vec* const r[], pa_vec* const c[],
+                    const pa_index* const idx[], pa_xchg* const xg[], double reltol, double abstol,
+                    int64_t maxiter, int batch, int64_t* iterations, double* residual, double* history) {
+  CHECK_ARG(n >= 1 && A && x && b && u && r && c && idx && iterations && residual, "null argument");
+  CHECK_ARG(batch >= 1, "batch must be >= 1");
+  const int dt = A[0]->dtype;
+  const bool cplx = dt == PA_C64 || dt == PA_C128;
+  CGRun R;
+  R.n = n;
+  R.P = A[0]->ctx->nparts;
+  for (int i = 0; i < n; ++i) {
+    CHECK_ARG(A[i] && x[i] && b[i] && u[i] && r[i] && c[i] && idx[i], "null handle");
+    const int64_t m = x[i]->n;
+    for (const pa_vec* v : {(const pa_vec*)x[i], b[i], (const pa_vec*)u[i], (const pa_vec*)r[i], (const pa_vec*)c[i]}) {
+      CHECK_ARG(v->dtype == dt, "cg!: element types differ");
+      CHECK_ARG(v->n == m && v->ctx == A[i]->ctx, "cg!: x, b and the work vectors must share a.cols' partition");
+    }
+    CHECK_ARG(idx[i]->nlids == m && idx[i]->own_contig, "cg!: the device CG needs contiguous owned lids");
+    CHECK_ARG(A[i]->ctx->nparts == R.P, "cg!: parts of different partitions");
+    R.ctxs.push_back(A[i]->ctx);
+  }
+  R.remote = R.ctxs[0]->comm && n == 1 && R.P > 1;
+  CHECK_ARG(R.remote || n == R.P, "cg!: pass every part held by this process, or use one part per process with RCCL");
+  std::vector<int> part_pos(R.P + 1, -1);
+  for (int i = 0; i < n; ++i) part_pos[R.ctxs[i]->part] = i;
+  R.st.assign(n, nullptr);
+  R.hist.assign(n, nullptr);
+  R.ptrs.assign(n, nullptr);
+  R.ev_red.assign(n, nullptr);
+  R.ev_gat.assign(n, nullptr);
+  for (int i = 0; i < n; ++i) {
+    pa_ctx* cx = R.ctxs[i];
+    HIPC(hipSetDevice(cx->device));
+    HIPC(hipMalloc((void**)&R.st[i], sizeof(CGState)));
+    if (history && maxiter > 0) HIPC(hipMalloc((void**)&R.hist[i], (size_t)maxiter * sizeof(double)));
+    if (!R.remote) {
+      std::vector<void*> tab(R.P, nullptr);
+      for (int p = 1; p <= R.P; ++p) tab[p - 1] = R.ctxs[part_pos[p]]->d_result;
+      if (dev_upload(&R.ptrs[i], tab)) return -1;
+      HIPC(hipEventCreateWithFlags(&R.ev_red[i], hipEventDisableTiming));
+      HIPC(hipEventCreateWithFlags(&R.ev_gat[i], hipEventDisableTiming));
+      for (int j = 0; j < n; ++j) {  // the gather kernel reads the other devices' results
+        const int dj = R.ctxs[j]->device;
+        if (dj == cx->device) continue;
+        int ok = 0;
+        HIPC(hipDeviceCanAccessPeer(&ok, cx->device, dj));
+        CHECK_ARG(ok, "cg!: the device CG over parts on several devices of one process needs peer access");
+        hipError_t e = hipDeviceEnablePeerAccess(dj, 0);
+        if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) HIPC(e);
+        (void)hipGetLastError();
+      }
+    }
+  }
+  // setup (cg_iterator!): u = 0; r = b; c = A*x; r .-= c; residual = norm(r);
+  // tolerance = max(reltol*norm(b), abstol)
+  unsigned char one[16], zero[16];
+  scalar_one(dt, one, 1.0);
+  scalar_one(dt, zero, 0.0);
+  for (int i = 0; i < n; ++i) {
+    HIPC(hipSetDevice(R.ctxs[i]->device));
+    launch_fill(dt, u[i]->n, 0, nullptr, u[i]->d, zero, R.ctxs[i]->s_main);
+    launch_copy(dt, r[i]->n, nullptr, r[i]->d, nullptr, b[i]->d, R.ctxs[i]->s_main);
+  }
+  HIPC(hipGetLastError());
+  if (spmv_impl(n, A, c, idx, x, idx, xg, one, zero, false)) return -1;
+  for (int i = 0; i < n; ++i) {
+    HIPC(hipSetDevice(R.ctxs[i]->device));
+    launch_axpby(dt, r[i]->n, nullptr, r[i]->d, c[i]->d, zero, 3, R.ctxs[i]->s_main);
+  }
+  double res0 = 0.0, nb = 0.0;
+  if (pa_norm2_all(n, (const pa_vec* const*)r, idx, &res0)) return -1;
+  if (pa_norm2_all(n, b, idx, &nb)) return -1;
+  CGState h{};
+  h.res = res0;
+  h.prev = 1.0;
+  h.tol = std::max(reltol * nb, abstol);
+  h.it = 0;
+  h.maxiter = maxiter;
+  h.done = (0 >= maxiter || res0 <= h.tol) ? 1 : 0;
+  for (int i = 0; i < n; ++i) {
+    HIPC(hipSetDevice(R.ctxs[i]->device));
+    HIPC(hipMemcpyAsync(R.st[i], &h, sizeof(CGState), hipMemcpyHostToDevice, R.ctxs[i]->s_main));
+    HIPC(hipStreamSynchronize(R.ctxs[i]->s_main));
+  }
+  const size_t accsz = cplx ? 16 : 8;
+  int64_t enqueued = 0;
+  bool done = h.done != 0;
+  while (!done && enqueued < maxiter) {
+    const int64_t k = std::min<int64_t>(batch, maxiter - enqueued);  // the same on every rank
+    for (int64_t t = 0; t < k; ++t) {
+      for (int i = 0; i < n; ++i) {  // u .= r .+ β.*u
+        HIPC(hipSetDevice(R.ctxs[i]->device));
+        launch_cg_xpby(dt, u[i]->n, u[i]->d, r[i]->d, R.st[i], R.ctxs[i]->s_main);
+      }
+      // mul!(c, A, u) with dot(u, c) accumulated by the SpMV
+      if (spmv_impl(n, A, c, idx, u, idx, xg, one, zero, true)) return -1;
+      if (cg_gather(R, accsz)) return -1;
+      for (int i = 0; i < n; ++i) {  // α = residual² / dot(u, c)
+        HIPC(hipSetDevice(R.ctxs[i]->device));
+        launch_cg_alpha(dt, R.P, R.ctxs[i]->d_gather, R.st[i], R.ctxs[i]->s_main);
+      }
+      for (int i = 0; i < n; ++i) {  // x .+= α.*u; r .-= α.*c; Σ|r|²
+        pa_ctx* cx = R.ctxs[i];
+        HIPC(hipSetDevice(cx->device));
+        const int64_t m = x[i]->n;
+        const int nbk = (int)std::min<int64_t>(8192, std::max<int64_t>(1, (m + 255) / 256));
+        launch_cg_xr(dt, m, idx[i]->noids, nullptr, x[i]->d, r[i]->d, u[i]->d, c[i]->d, nullptr, R.st[i],
+                     (double*)cx->d_partials, nbk, cx->s_main);
+        launch_fold(0, nbk, cx->d_partials, cx->d_fold, cx->d_result, cx->s_main);
+      }
+      if (cg_gather(R, 8)) return -1;
+      for (int i = 0; i < n; ++i) {  // prev = residual; residual = norm(r); it += 1; done?
+        HIPC(hipSetDevice(R.ctxs[i]->device));
+        launch_cg_step(R.P, (const double*)R.ctxs[i]->d_gather, R.st[i], R.hist[i], R.ctxs[i]->s_main);
+      }
+      HIPC(hipGetLastError());
+    }
+    enqueued += k;
+    // every part holds the same state; read part 0's
+    pa_ctx* c0 = R.ctxs[0];
+    HIPC(hipSetDevice(c0->device));
+    HIPC(hipMemcpyAsync(c0->h_pinned, R.st[0], sizeof(CGState), hipMemcpyDeviceToHost, c0->s_main));
+    for (int i = 0; i < n; ++i) {
+      HIPC(hipSetDevice(R.ctxs[i]->device));
+      HIPC(hipStreamSynchronize(R.ctxs[i]->s_main));
+    }
+    std::memcpy(&h, c0->h_pinned, sizeof(CGState));
+    done = h.done != 0;
+  }
+  *iterations = h.it;
+  *residual = h.res;
+  if (history && h.it > 0) {
+    HIPC(hipSetDevice(R.ctxs[0]->device));
+    HIPC(hipMemcpy(history, R.hist[0], (size_t)h.it * sizeof(double), hipMemcpyDeviceToHost));
+  }
   return 0;
 }
 
@@ -1254,8 +1467,9 @@ int pa_norm2_all(int n, const pa_vec* const a[], const pa_index* const ia[], voi
   if (reduce_all(n, a, ia, nullptr, nullptr, 1, &vals)) return -1;
   double s = 0.0;
   for (const auto& v : vals) s = s + v.re;
-  // (…)^(1/p) with p = 2 (Interfaces.jl:1771); Julia promotes to Float64
-  *(double*)result = std::pow(s, 1.0 / 2.0);
+  // (…)^(1/p) with p = 2 (Interfaces.jl:1771); Julia promotes to Float64.
+  // x^0.5 correctly rounded is sqrt(x) (the device CG uses the same)
+  *(double*)result = std::sqrt(s);
   return 0;
 }
 

@@ -74,6 +74,20 @@ inline int sell_rows_per_lane(int dt) {
 
 void set_error(const std::string& msg);
 
+// Device-resident scalars of the device-driven CG (pa_cg_solve_all): the
+// IterativeSolvers 0.9 recurrence state, one copy per part (every part
+// folds the same gathered partials in part order, so all copies agree).
+struct CGState {
+  double res;        // it.residual = norm(r)
+  double prev;       // it.prev_residual
+  double tol;        // max(reltol*norm(b), abstol)
+  int64_t it;        // iterations done
+  int64_t maxiter;
+  int32_t done;      // it >= maxiter || res <= tol
+  int32_t pad;
+  c128 alpha;        // α in the vectors' element type (first sizeof(T) bytes)
+};
+
 // Cartesian part box of a synthetic stencil operator (pa_mat_stencil).
 struct StencilGeom {
   int64_t N[3];   // global nodes per dim

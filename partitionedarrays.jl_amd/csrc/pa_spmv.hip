@@ -16,6 +16,9 @@
 //   acc = β-init; acc = acc + v_k * (x_{c_k} * α)   (-ffp-contract=off)
 #include "pa_internal.h"
 
+#include <algorithm>
+#include <type_traits>
+
 namespace pa {
 
 template <typename T, int R>
@@ -348,11 +351,16 @@ void launch_spmv_part(int which, int64_t nwork, const int32_t* list, const pa_ma
 // x .+= α.*u; r .-= α.*c (all lids, Interfaces.jl:1710-1737) and the owned
 // Σ|r|² of norm(r) (1767-1772) in one pass (contiguous owned lids
 // 0..noids-1); per-block partials, folded in block order afterwards.
-// V elements per 16 B access (V = 1: unaligned fallback).
-template <typename T, int V>
+// V elements per 16 B access (V = 1: unaligned fallback).  DEV: α comes from
+// the device CG state (pa_cg_solve_all) and a finished solve is a no-op.
+template <typename T, int V, bool DEV>
 __global__ __launch_bounds__(256) void k_cg_xr(int64_t n, int64_t noids, T* __restrict__ x, T* __restrict__ r,
                                                const T* __restrict__ u, const T* __restrict__ c, T alpha,
-                                               double* __restrict__ part) {
+                                               const CGState* __restrict__ st, double* __restrict__ part) {
+  if (DEV) {
+    if (st->done) return;
+    alpha = *reinterpret_cast<const T*>(&st->alpha);
+  }
   using P = Pack<T, V>;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
@@ -387,26 +395,156 @@ __global__ __launch_bounds__(256) void k_cg_xr(int64_t n, int64_t noids, T* __re
 
 template <typename T>
 static void cg_xr_t(int64_t n, int64_t noids, void* x, void* r, const void* u, const void* c,
-                    const void* alpha, double* part, int nb, hipStream_t st) {
+                    const void* alpha, const CGState* st, double* part, int nb, hipStream_t st_) {
   constexpr int V = 16 / sizeof(T);
   const bool aligned = ((uintptr_t)x | (uintptr_t)r | (uintptr_t)u | (uintptr_t)c) % 16 == 0;
-  if (aligned)
-    hipLaunchKernelGGL((k_cg_xr<T, V>), dim3(nb), dim3(256), 0, st, n, noids, (T*)x, (T*)r, (const T*)u,
-                       (const T*)c, *(const T*)alpha, part);
-  else
-    hipLaunchKernelGGL((k_cg_xr<T, 1>), dim3(nb), dim3(256), 0, st, n, noids, (T*)x, (T*)r, (const T*)u,
-                       (const T*)c, *(const T*)alpha, part);
+  const T a = alpha ? *(const T*)alpha : zero_of<T>();
+#define PA_XR(VV, DD)                                                                                  \
+  hipLaunchKernelGGL((k_cg_xr<T, VV, DD>), dim3(nb), dim3(256), 0, st_, n, noids, (T*)x, (T*)r,      \
+                     (const T*)u, (const T*)c, a, st, part)
+  if (st) {
+    if (aligned) PA_XR(V, true); else PA_XR(1, true);
+  } else {
+    if (aligned) PA_XR(V, false); else PA_XR(1, false);
+  }
+#undef PA_XR
 }
 
+// alpha: host scalar (st == nullptr) or read from the device CG state
 void launch_cg_xr(int dtype, int64_t n, int64_t noids, const int32_t* own, void* x, void* r, const void* u,
-                  const void* c, const void* alpha, double* part, int nb, hipStream_t st) {
+                  const void* c, const void* alpha, const CGState* st, double* part, int nb, hipStream_t s) {
   (void)own;  // owned lids are 0..noids-1 (checked by the caller)
   switch (dtype) {
-    case PA_F32: cg_xr_t<float>(n, noids, x, r, u, c, alpha, part, nb, st); break;
-    case PA_F64: cg_xr_t<double>(n, noids, x, r, u, c, alpha, part, nb, st); break;
-    case PA_C64: cg_xr_t<c64>(n, noids, x, r, u, c, alpha, part, nb, st); break;
-    case PA_C128: cg_xr_t<c128>(n, noids, x, r, u, c, alpha, part, nb, st); break;
+    case PA_F32: cg_xr_t<float>(n, noids, x, r, u, c, alpha, st, part, nb, s); break;
+    case PA_F64: cg_xr_t<double>(n, noids, x, r, u, c, alpha, st, part, nb, s); break;
+    case PA_C64: cg_xr_t<c64>(n, noids, x, r, u, c, alpha, st, part, nb, s); break;
+    case PA_C128: cg_xr_t<c128>(n, noids, x, r, u, c, alpha, st, part, nb, s); break;
   }
+}
+
+// ---------------------------------------------------------------------------
+// Device-driven CG scalars (pa_cg_solve_all).  The host driver folds the
+// part values in part order in double / c128 and hands scalars over as
+// the vectors' element type; these kernels repeat exactly that arithmetic
+// on one thread so the device recurrence equals the host-driven one.
+
+template <typename T> __device__ inline T real_scalar(double v) { return (T)v; }
+template <> __device__ inline c64 real_scalar<c64>(double v) { return c64{(float)v, 0.f}; }
+template <> __device__ inline c128 real_scalar<c128>(double v) { return c128{v, 0.0}; }
+
+// u .= r .+ β.*u over all lids, β = residual²/prev_residual² (IterativeSolvers
+// 0.9 cg iterate); a finished solve is a no-op
+template <typename T>
+__global__ __launch_bounds__(256) void k_cg_xpby(int64_t n, T* __restrict__ u, const T* __restrict__ r,
+                                                 const CGState* __restrict__ st) {
+  if (st->done) return;
+  const double b = (st->res * st->res) / (st->prev * st->prev);
+  const T a = real_scalar<T>(b);
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    u[i] = r[i] + a * u[i];
+}
+
+// the dot partials of the P parts (accumulators, part order) →
+// dot = reduce(+; init=0) narrowed to T → α = residual² / dot
+template <typename T>
+__global__ void k_cg_alpha(int P, const void* __restrict__ gathered, CGState* __restrict__ st) {
+  if (threadIdx.x != 0 || blockIdx.x != 0 || st->done) return;
+  const double res2 = st->res * st->res;
+  T* out = reinterpret_cast<T*>(&st->alpha);
+  if constexpr (std::is_same<T, float>::value || std::is_same<T, double>::value) {
+    const double* g = (const double*)gathered;
+    double s = 0.0;
+    for (int p = 0; p < P; ++p) s = s + g[p];
+    const double d = (double)(T)s;
+    *out = (T)(res2 / d);
+  } else {
+    const c128* g = (const c128*)gathered;
+    c128 s{0.0, 0.0};
+    for (int p = 0; p < P; ++p) s = s + g[p];
+    double br, bi;
+    if constexpr (std::is_same<T, c64>::value) {
+      br = (double)(float)s.re;
+      bi = (double)(float)s.im;
+    } else {
+      br = s.re;
+      bi = s.im;
+    }
+    // res2 / complex(br, bi), Smith's division as the host driver computes it
+    // (CPython _Py_c_quot with a = res2 + 0im)
+    double qr, qi;
+    const double abr = br < 0 ? -br : br, abi = bi < 0 ? -bi : bi;
+    if (abr >= abi) {
+      if (abr == 0.0) {
+        qr = qi = 0.0;
+      } else {
+        const double ratio = bi / br;
+        const double denom = br + bi * ratio;
+        qr = (res2 + 0.0 * ratio) / denom;
+        qi = (0.0 - res2 * ratio) / denom;
+      }
+    } else {
+      const double ratio = br / bi;
+      const double denom = br * ratio + bi;
+      qr = (res2 * ratio + 0.0) / denom;
+      qi = (0.0 * ratio - res2) / denom;
+    }
+    if constexpr (std::is_same<T, c64>::value) *out = c64{(float)qr, (float)qi};
+    else *out = c128{qr, qi};
+  }
+}
+
+// Σ|r|² partials of the P parts → prev = residual; residual = sqrt(Σ);
+// it += 1; history[it] = residual; done = it >= maxiter || residual <= tol
+__global__ void k_cg_step(int P, const double* __restrict__ gathered, CGState* __restrict__ st,
+                          double* __restrict__ history) {
+  if (threadIdx.x != 0 || blockIdx.x != 0 || st->done) return;
+  double s = 0.0;
+  for (int p = 0; p < P; ++p) s = s + gathered[p];
+  const double res = sqrt(s);
+  st->prev = st->res;
+  st->res = res;
+  const int64_t it = st->it + 1;
+  st->it = it;
+  if (history) history[it - 1] = res;
+  st->done = (it >= st->maxiter || res <= st->tol) ? 1 : 0;
+}
+
+// gathered[p] = *srcs[p] (accsz bytes each): the part values of the parts
+// held by this process, read straight from their devices
+__global__ void k_gather_ptrs(int P, const void* const* __restrict__ srcs, int accsz, char* __restrict__ out) {
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= P) return;
+  const double* s = (const double*)srcs[p];
+  double* d = (double*)(out + (int64_t)p * accsz);
+  d[0] = s[0];
+  if (accsz == 16) d[1] = s[1];
+}
+
+void launch_cg_xpby(int dtype, int64_t n, void* u, const void* r, const CGState* st, hipStream_t s) {
+  const int nb = (int)std::min<int64_t>(8192, std::max<int64_t>(1, (n + 255) / 256));
+  switch (dtype) {
+    case PA_F32: hipLaunchKernelGGL(k_cg_xpby<float>, dim3(nb), dim3(256), 0, s, n, (float*)u, (const float*)r, st); break;
+    case PA_F64: hipLaunchKernelGGL(k_cg_xpby<double>, dim3(nb), dim3(256), 0, s, n, (double*)u, (const double*)r, st); break;
+    case PA_C64: hipLaunchKernelGGL(k_cg_xpby<c64>, dim3(nb), dim3(256), 0, s, n, (c64*)u, (const c64*)r, st); break;
+    case PA_C128: hipLaunchKernelGGL(k_cg_xpby<c128>, dim3(nb), dim3(256), 0, s, n, (c128*)u, (const c128*)r, st); break;
+  }
+}
+
+void launch_cg_alpha(int dtype, int P, const void* gathered, CGState* st, hipStream_t s) {
+  switch (dtype) {
+    case PA_F32: hipLaunchKernelGGL(k_cg_alpha<float>, dim3(1), dim3(64), 0, s, P, gathered, st); break;
+    case PA_F64: hipLaunchKernelGGL(k_cg_alpha<double>, dim3(1), dim3(64), 0, s, P, gathered, st); break;
+    case PA_C64: hipLaunchKernelGGL(k_cg_alpha<c64>, dim3(1), dim3(64), 0, s, P, gathered, st); break;
+    case PA_C128: hipLaunchKernelGGL(k_cg_alpha<c128>, dim3(1), dim3(64), 0, s, P, gathered, st); break;
+  }
+}
+
+void launch_cg_step(int P, const double* gathered, CGState* st, double* history, hipStream_t s) {
+  hipLaunchKernelGGL(k_cg_step, dim3(1), dim3(64), 0, s, P, gathered, st, history);
+}
+
+void launch_gather_ptrs(int P, const void* const* srcs, int accsz, void* out, hipStream_t s) {
+  hipLaunchKernelGGL(k_gather_ptrs, dim3((P + 63) / 64), dim3(64), 0, s, P, srcs, accsz, (char*)out);
 }
 
 // ---------------------------------------------------------------------------

@@ -414,18 +414,24 @@ def _own_contig(v: PVector) -> bool:
 
 
 def cg_(x: PVector, A: PSparseMatrix, b: PVector, reltol=None, abstol=0.0, maxiter=None,
-        history=None, fused=True):
+        history=None, fused=True, device=False, batch=8):
     """IterativeSolvers.cg! (v0.9; caller of the hot path at test_fdm.jl:115,
     test_fem_sa.jl:135), restated over the device operations:
     u = zero(x); r, c = similar(x); copyto!(r, b); mul!(c, A, x); r .-= c;
     residual = norm(r); tol = max(reltol*norm(b), abstol); prev = 1; then per
     iteration β = res²/prev²; u .= r .+ β.*u; mul!(c, A, u);
-    α = res²/dot(u, c); x .+= α.*u; r .-= α.*c; prev = res; res = norm(r)."""
+    α = res²/dot(u, c); x .+= α.*u; r .-= α.*c; prev = res; res = norm(r).
+
+    device=True runs the same recurrence with its scalars on the device
+    (pa_cg_solve_all): the host enqueues `batch` iterations between reads of
+    the done flag; results equal the host-driven fused loop bit for bit."""
     real = np.float32 if x.dtype in (np.float32, np.complex64) else np.float64
     if reltol is None:
         reltol = math.sqrt(np.finfo(real).eps)
     if maxiter is None:
         maxiter = len(A.cols)
+    if device:
+        return _cg_device(x, A, b, reltol, abstol, maxiter, history, batch)
     u = x.similar().fill_(0)
     r = x.similar()
     c = x.similar()
@@ -441,14 +447,14 @@ def cg_(x: PVector, A: PSparseMatrix, b: PVector, reltol=None, abstol=0.0, maxit
     # x/r updates + norm(r) in one pass
     fuse = fused and _own_contig(u) and (x.rows is r.rows is u.rows is c.rows)
     while not (it >= maxiter or residual <= tol):
-        beta = residual ** 2 / prev ** 2
+        beta = (residual * residual) / (prev * prev)  # residual^2 (literal_pow: x*x)
         xpby_(u, r, beta)
         if fuse:
-            alpha = residual ** 2 / mul_dot_(c, A, u)
+            alpha = (residual * residual) / mul_dot_(c, A, u)
             new = cg_update_(x, r, u, c, alpha)
         else:
             mul_(c, A, u)
-            alpha = residual ** 2 / dot(u, c)
+            alpha = (residual * residual) / dot(u, c)
             axpy_(x, alpha, u)
             axmy_(r, alpha, c)
             new = norm(r)
@@ -457,4 +463,30 @@ def cg_(x: PVector, A: PSparseMatrix, b: PVector, reltol=None, abstol=0.0, maxit
         it += 1
         if history is not None:
             history.append(residual)
+    return x
+
+
+def _cg_device(x: PVector, A: PSparseMatrix, b: PVector, reltol, abstol, maxiter, history, batch):
+    if not _own_contig(x):
+        raise ValueError("cg_(device=True): x needs contiguous owned lids")
+    if b.rows is not x.rows:  # copyto!(r, b) across partitions copies the owned values
+        bb = x.similar()
+        copyto_(bb, b)
+        b = bb
+    u, r, c = x.similar(), x.similar(), x.similar()
+    ctxs = contexts(A.values)
+    n = len(ctxs)
+    ex = x.rows.exchanger
+    has_x = any(len(ex.parts_rcv.local(p)) or len(ex.parts_snd.local(p)) for p in x.values.part_ids)
+    xg = [device_exchanger(cx, ex, p) for cx, p in zip(ctxs, x.values.part_ids)] if has_x else None
+    its = C.c_int64(0)
+    res = C.c_double(0.0)
+    hist = np.zeros(max(1, int(maxiter)), dtype=np.float64) if history is not None else None
+    _lib.call("pa_cg_solve_all", n, _hs(A.values.parts), _hs(x.values.parts), _hs(b.values.parts),
+              _hs(u.values.parts), _hs(r.values.parts), _hs(c.values.parts), _lib.ptr_array(_idx(x)),
+              _hs(xg) if xg else None, float(reltol), float(abstol), int(maxiter), int(batch),
+              C.byref(its), C.byref(res),
+              hist.ctypes.data_as(C.POINTER(C.c_double)) if hist is not None else None)
+    if history is not None:
+        history.extend(float(v) for v in hist[:its.value])
     return x

@@ -200,3 +200,83 @@ def test_interfaces_matrix_exchange_kat(be, pamd, O):
     for M, s in zip(A.values.parts, sets):
         want = np.where(s.lid_to_part == s.part, 1.0 + np.array([nghost.get(int(g), 0) for g in s.lid_to_gid]), 0.0)
         assert np.array_equal(M.get_values(), want)
+
+
+def _stencil_rhs(pamd, A, dtype, seed):
+    cols = A.cols
+
+    def rnd(s):
+        r = np.random.default_rng(seed + s.part)
+        v = r.uniform(-1, 1, s.num_lids)
+        if np.dtype(dtype).kind == "c":
+            v = v + 1j * r.uniform(-1, 1, s.num_lids)
+        return v.astype(dtype)
+    return pamd.PVector.from_host(pamd.map_parts(rnd, cols.partition), cols)
+
+
+@pytest.mark.parametrize("shape,N,dtype,batch,maxiter", [
+    ((2, 2, 1), (12, 10, 9), np.float64, 8, 40),    # 4 local parts: device gather kernel
+    ((1, 1, 1), (9, 8, 7), np.float64, 3, 25),      # batch not dividing maxiter
+    ((2, 1, 2), (10, 7, 9), np.complex128, 5, 30),
+    ((2, 1, 1), (9, 9, 9), np.float32, 4, 20),
+    ((2, 2, 2), (8, 8, 8), np.complex64, 7, 20),
+])
+def test_device_cg_equals_host_cg(be, pamd, O, shape, N, dtype, batch, maxiter):
+    """pa_cg_solve_all (scalars on the device, batched enqueue) reproduces the
+    host-driven fused CG bit for bit: x, the residual history, and the
+    iteration count (reltol = 0 → exactly maxiter iterations)."""
+    parts = be.get_part_ids(shape)
+    A = pamd.drivers.stencil_operator(parts, N, 27, dtype)
+    b = _stencil_rhs(pamd, A, dtype, 31)
+    xs = []
+    hs = []
+    for device in (False, True):
+        x = pamd.PVector.undef(A.cols, dtype).fill_(0)
+        h = []
+        pamd.cg_(x, A, b, reltol=0.0, maxiter=maxiter, history=h, fused=True, device=device, batch=batch)
+        xs.append(x.to_host())
+        hs.append(h)
+    assert len(hs[0]) == len(hs[1]) == maxiter
+    assert hs[0] == hs[1]
+    for p in parts.part_ids:
+        assert np.array_equal(xs[0].local(p), xs[1].local(p))
+
+
+@pytest.mark.parametrize("batch", [1, 4, 64])
+def test_device_cg_converges_like_test_fdm(be, pamd, O, batch):
+    """test_fdm.jl's CG with the device recurrence: same iteration count and
+    history as the host-driven loop (convergence stops mid-batch), and
+    norm(x - x̂) < 1e-5 (test_fdm.jl:118)."""
+    parts = be.get_part_ids((2, 2, 2))
+    A, b, x0, xh = pamd.drivers.fdm_problem(parts, 10)
+    x1 = x0.copy()
+    h1 = []
+    pamd.cg_(x1, A, b, history=h1, fused=True)
+    x2 = x0.copy()
+    h2 = []
+    pamd.cg_(x2, A, b, history=h2, device=True, batch=batch)
+    assert h1 == h2 and 0 < len(h2) < 1000
+    d = pamd.map_parts(lambda u, v, s: u[s.oid_to_lid - 1] - v[s.oid_to_lid - 1], x2.to_host(), xh.to_host(),
+                       x2.rows.partition)
+    assert sum(float(np.sum(t ** 2)) for t in d.parts) ** 0.5 < 1e-5
+    for p in parts.part_ids:
+        assert np.array_equal(x1.to_host().local(p), x2.to_host().local(p))
+
+
+def test_device_cg_fem_sa(be, pamd, O):
+    """test_fem_sa.jl's CG (COO-assembled matrix with stored ghost rows) on
+    the device recurrence, against the oracle's residual history."""
+    parts = be.get_part_ids(4)
+    A, b, x0, xh = pamd.drivers.fem_sa_problem(parts, 10)
+    if not all(s.num_oids == 0 or (s.oid_to_lid[0] == 1 and s.oid_to_lid[-1] == s.num_oids)
+               for s in A.cols.partition.parts):
+        pytest.skip("non-contiguous owned lids")
+    x = x0.copy()
+    hist = []
+    pamd.cg_(x, A, b, history=hist, device=True)
+    OA, ob, ox0, oxh = O.fem_sa_problem(O.get_part_ids(4), 10)
+    ox = O.PVector(O.map_parts(lambda v: v.copy(), ox0.values), ox0.rows)
+    ohist = []
+    O.cg_(ox, OA, ob, log=ohist)
+    assert len(hist) == len(ohist)
+    np.testing.assert_allclose(hist, ohist, rtol=1e-8)
