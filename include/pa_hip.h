@@ -128,6 +128,22 @@ int pa_mat_from_csc(pa_ctx* ctx, int dtype, int index_bytes,
                     const void* colptr, const void* rowval, const void* nzval,
                     const pa_index* rows, const pa_index* cols,
                     pa_mat** out);
+/* From COO triplets: PSparseMatrix(I, J, V, rows, cols; ids=:local)
+ * (Interfaces.jl:2194-2244) → sparse(I, J, V, m, n, +) (SparseUtils.jl:
+ * 80-94) on the device (stable radix sort, duplicates summed in input
+ * order), then the same SELL layout as pa_mat_from_csc.  I, J: 1-based
+ * local ids (index_bytes 4 or 8), ncoo entries each; an index out of range
+ * is an error (BoundsError).  *csc_nnz = nnz of the combined CSC; when
+ * colptr_out (ncols_lids+1) / rowval_out (>= ncoo) are non-NULL the CSC
+ * pattern is written there, 1-based, for host setup that needs it
+ * (matrix_exchanger, Interfaces.jl:2300-2372).  The nonzeros' CSC order is
+ * what pa_mat_set_values / pa_mat_get_values / pa_mat_xchg_create use.   */
+int pa_mat_from_coo(pa_ctx* ctx, int dtype, int index_bytes,
+                    int64_t nrows_lids, int64_t ncols_lids, int64_t ncoo,
+                    const void* I, const void* J, const void* V,
+                    const pa_index* rows, const pa_index* cols,
+                    int64_t* csc_nnz, int64_t* colptr_out,
+                    int64_t* rowval_out, pa_mat** out);
 /* Replace the stored values keeping the pattern (same CSC nz order),
  * e.g. after fillstored!/re-assembly (Interfaces.jl:2127-2132).          */
 int pa_mat_set_values(pa_mat* A, const void* nzval);

@@ -17,7 +17,7 @@ from .prange import (Exchanger, IndexSet, PRange, add_gids, add_gids_, discover_
                      empty_exchanger, exchanger_from_ids, hids_are_equal, index_range,
                      lids_are_equal, oids_are_equal, prange_cartesian, prange_from_partition,
                      prange_linear, prange_noids, to_lids_)
-from .device import HIPBackend, HIPDistributedBackend  # noqa: F401
+from .device import DeviceMatrix, HIPBackend, HIPDistributedBackend, device_index  # noqa: F401
 from .pvector import (CSC, PSparseMatrix, PVector, assemble_, axmy_, axpy_, cg_, cg_update_,  # noqa: F401
                       compresscoo, copyto_, dot, exchange_, matvec, mul_, mul_dot_, norm, psum, rmul_,
                       sub_, xpby_)

@@ -36,6 +36,19 @@ void launch_cg_alpha(int dtype, int P, const void* gathered, CGState* cst, hipSt
 void launch_cg_step(int P, const double* gathered, CGState* cst, double* history, hipStream_t st);
 void launch_gather_ptrs(int P, const void* const* srcs, int accsz, void* out, hipStream_t st);
 extern int g_spmv_format;
+// COO → CSC → SELL on the device (pa_coo.hip)
+int coo_compress(int dtype, int index_bytes, int64_t m, int64_t ncols, int64_t n, const void* dI, const void* dJ,
+                 const void* dV, int64_t* nu_out, int32_t** crow, int32_t** ccol, void** cval, int64_t** colptr,
+                 hipStream_t st, hipError_t* err_out);
+int coo_row_order(int64_t nu, const int32_t* crow, const int32_t* ccol, const int32_t* rl2o, const int32_t* cl2o,
+                  int64_t nrows, int64_t noids_c, int64_t ncols, int H, uint64_t** key2, int64_t** idx2,
+                  int64_t** rowptr, int64_t** gflag, int64_t** grank, int32_t** slen, int32_t** sghost,
+                  int64_t* nnz_out, int64_t* ngh_out, hipStream_t st, hipError_t* err_out);
+void coo_fill(int dtype, int64_t nnz, int64_t nu, const uint64_t* key2, const int64_t* idx2, const int64_t* rowptr,
+              const int64_t* soff, int H, int R, int64_t ncols, const int32_t* ccol, const void* cval,
+              const int64_t* gflag, const int64_t* grank, int64_t slots, int32_t* col, void* val, int64_t* nz_slot,
+              hipStream_t st);
+void launch_fill_i32(int64_t n, int32_t* a, int32_t v, hipStream_t st);
 void launch_pack(int dtype, int64_t n, const int32_t* lids, const void* v, void* buf,
                  hipStream_t st);
 void launch_unpack(int dtype, int64_t n, const int32_t* lids, const pa_combine_plan& plan, int op,
@@ -798,6 +811,124 @@ int pa_mat_from_csc(pa_ctx* c, int dtype, int index_bytes, int64_t nrows_lids, i
     HIPC(hipMemcpy(A->d_val, hval.data(), (A->slots + A->n_gnz) * S, hipMemcpyHostToDevice));
   }
   // pattern slices need "x lid >= noids ⇔ ghost column" (contiguous layout)
+  if (cols->own_contig && cols->ghost_contig) {
+    int kmax = 0;
+    for (int32_t l : slen) kmax = std::max(kmax, l);
+    if (finalize_pattern(A, kmax, cols->noids)) { pa_mat_destroy(A); return -1; }
+  }
+  *out = A;
+  return 0;
+}
+
+// sparse(I, J, V, m, n, +) (SparseUtils.jl:80-94) and the SELL build on the
+// device (pa_coo.hip); same layout and nz_slot map as pa_mat_from_csc.
+namespace {
+struct DevBufs {
+  std::vector<void*> p;
+  ~DevBufs() { for (void* q : p) dev_free(q); }
+  void add(void* q) { p.push_back(q); }
+};
+}  // namespace
+
+int pa_mat_from_coo(pa_ctx* c, int dtype, int index_bytes, int64_t nrows_lids, int64_t ncols_lids, int64_t ncoo,
+                    const void* I, const void* J, const void* V, const pa_index* rows, const pa_index* cols,
+                    int64_t* csc_nnz, int64_t* colptr_out, int64_t* rowval_out, pa_mat** out) {
+  CHECK_ARG(c && out && rows && cols && csc_nnz, "null argument");
+  CHECK_ARG(ncoo >= 0 && (ncoo == 0 || (I && J && V)), "null COO arrays");
+  CHECK_ARG(valid_dtype(dtype), "invalid dtype");
+  CHECK_ARG(index_bytes == 4 || index_bytes == 8, "index_bytes must be 4 or 8");
+  CHECK_ARG(rows->nlids == nrows_lids && cols->nlids == ncols_lids,
+            "matrix size must be num_lids(rows) x num_lids(cols) (DimensionMismatch)");
+  HIPC(hipSetDevice(c->device));
+  hipStream_t st = c->s_main;
+  const size_t S = dtype_size(dtype);
+  DevBufs tmp, inp;
+  void *dI = nullptr, *dJ = nullptr, *dV = nullptr;
+  if (ncoo > 0) {
+    HIPC(hipMalloc(&dI, ncoo * index_bytes));
+    inp.add(dI);
+    HIPC(hipMalloc(&dJ, ncoo * index_bytes));
+    inp.add(dJ);
+    HIPC(hipMalloc(&dV, ncoo * S));
+    inp.add(dV);
+    HIPC(hipMemcpy(dI, I, ncoo * index_bytes, hipMemcpyHostToDevice));
+    HIPC(hipMemcpy(dJ, J, ncoo * index_bytes, hipMemcpyHostToDevice));
+    HIPC(hipMemcpy(dV, V, ncoo * S, hipMemcpyHostToDevice));
+  }
+  int64_t nu = 0;
+  int32_t *crow = nullptr, *ccol = nullptr;
+  void* cval = nullptr;
+  int64_t* dcolptr = nullptr;
+  hipError_t e = hipSuccess;
+  const int rc = coo_compress(dtype, index_bytes, nrows_lids, ncols_lids, ncoo, dI, dJ, dV, &nu, &crow, &ccol,
+                              &cval, &dcolptr, st, &e);
+  if (rc < 0) HIPC(e);
+  CHECK_ARG(rc == 0, "sparse: COO index out of range (BoundsError)");
+  tmp.add(crow); tmp.add(ccol); tmp.add(cval); tmp.add(dcolptr);
+  for (void*& q : inp.p) { dev_free(q); q = nullptr; }  // the COO input is no longer needed
+  *csc_nnz = nu;
+  if (colptr_out) {
+    HIPC(hipMemcpy(colptr_out, dcolptr, (ncols_lids + 1) * 8, hipMemcpyDeviceToHost));
+    for (int64_t j = 0; j <= ncols_lids; ++j) colptr_out[j] += 1;
+  }
+  if (rowval_out && nu > 0) {
+    std::vector<int32_t> rv(nu);
+    HIPC(hipMemcpy(rv.data(), crow, nu * 4, hipMemcpyDeviceToHost));
+    for (int64_t p = 0; p < nu; ++p) rowval_out[p] = (int64_t)rv[p] + 1;
+  }
+  int32_t *rl2o = nullptr, *cl2o = nullptr;
+  if (dev_upload(&rl2o, rows->h_lid_to_ohid) || dev_upload(&cl2o, cols->h_lid_to_ohid)) return -1;
+  tmp.add(rl2o); tmp.add(cl2o);
+
+  pa_mat* A = new pa_mat();
+  A->ctx = c;
+  A->dtype = dtype;
+  A->R = sell_rows_per_lane(dtype);
+  A->H = 64 * A->R;
+  A->nrows = rows->noids;
+  A->ncols_lids = ncols_lids;
+  A->csc_nnz = nu;
+  uint64_t* key2 = nullptr;
+  int64_t *idx2 = nullptr, *rowptr = nullptr, *gflag = nullptr, *grank = nullptr, *nzs = nullptr;
+  int32_t *slen_d = nullptr, *sghost_d = nullptr;
+  int64_t nnz = 0, ngh = 0;
+  if (coo_row_order(nu, crow, ccol, rl2o, cl2o, A->nrows, cols->noids, ncols_lids, A->H, &key2, &idx2, &rowptr,
+                    &gflag, &grank, &slen_d, &sghost_d, &nnz, &ngh, st, &e)) {
+    delete A;
+    HIPC(e);
+  }
+  tmp.add(key2); tmp.add(idx2); tmp.add(rowptr); tmp.add(gflag); tmp.add(grank); tmp.add(slen_d); tmp.add(sghost_d);
+  A->nnz = nnz;
+  const int64_t ns = (A->nrows + A->H - 1) / A->H;
+  std::vector<int32_t> slen(ns), sg(ns);
+  std::vector<char> sghost(ns);
+  if (ns > 0) {
+    HIPC(hipMemcpy(slen.data(), slen_d, ns * 4, hipMemcpyDeviceToHost));
+    HIPC(hipMemcpy(sg.data(), sghost_d, ns * 4, hipMemcpyDeviceToHost));
+  }
+  for (int64_t s = 0; s < ns; ++s) sghost[s] = sg[s] ? 1 : 0;
+  if (finish_sell_layout(A, slen, sghost, nullptr)) { pa_mat_destroy(A); return -1; }
+  if (A->slots > 0) {
+    HIPC(hipMalloc((void**)&A->d_col, A->slots * 4));
+    launch_fill_i32(A->slots, A->d_col, -1, st);
+  }
+  if (A->slots + ngh > 0) {
+    HIPC(hipMalloc(&A->d_val, (A->slots + ngh) * S));
+    HIPC(hipMemsetAsync(A->d_val, 0, (A->slots + ngh) * S, st));
+  }
+  if (nu > 0) {
+    HIPC(hipMalloc((void**)&nzs, nu * 8));
+    tmp.add(nzs);
+  }
+  coo_fill(dtype, nnz, nu, key2, idx2, rowptr, A->d_slice_off, A->H, A->R, ncols_lids, ccol, cval, gflag, grank,
+           A->slots, A->d_col, A->d_val, nzs, st);
+  HIPC(hipGetLastError());
+  A->n_gnz = ngh;
+  A->h_nz_slot.resize(nu);
+  if (nu > 0) {
+    HIPC(hipMemcpyAsync(A->h_nz_slot.data(), nzs, nu * 8, hipMemcpyDeviceToHost, st));
+  }
+  HIPC(hipStreamSynchronize(st));
   if (cols->own_contig && cols->ghost_contig) {
     int kmax = 0;
     for (int32_t l : slen) kmax = std::max(kmax, l);

@@ -229,6 +229,28 @@ class DeviceMatrix:
         M.csc_nnz = len(nzval)
         return M
 
+    @staticmethod
+    def from_coo(ctx: PartContext, I, J, V, rows_idx: DeviceIndex, cols_idx: DeviceIndex, nrows_lids, ncols_lids):
+        """sparse(I, J, V, m, n, +) and the SELL build on the device
+        (pa_mat_from_coo).  Returns (matrix, colptr, rowval): the CSC pattern
+        (1-based) for the host setup that needs it (matrix_exchanger)."""
+        I = np.ascontiguousarray(I, dtype=np.int64).ravel()
+        J = np.ascontiguousarray(J, dtype=np.int64).ravel()
+        V = np.ascontiguousarray(V).ravel()
+        if not (len(I) == len(J) == len(V)):
+            raise ValueError("sparse: I, J and V must have the same length")
+        colptr = np.empty(ncols_lids + 1, dtype=np.int64)
+        rowval = np.empty(max(1, len(I)), dtype=np.int64)
+        nnz = C.c_int64(0)
+        h = C.c_void_p()
+        _lib.call("pa_mat_from_coo", ctx.h, _lib.DTYPES[V.dtype], 8, nrows_lids, ncols_lids, len(I),
+                  I.ctypes.data_as(C.c_void_p), J.ctypes.data_as(C.c_void_p), V.ctypes.data_as(C.c_void_p),
+                  rows_idx.h, cols_idx.h, C.byref(nnz), colptr.ctypes.data_as(C.POINTER(C.c_int64)),
+                  rowval.ctypes.data_as(C.POINTER(C.c_int64)), C.byref(h))
+        M = DeviceMatrix(h, ctx, V.dtype)
+        M.csc_nnz = nnz.value
+        return M, colptr, rowval[:nnz.value].copy()
+
     def set_values(self, nzval):
         nzval = np.ascontiguousarray(nzval, dtype=self.dtype)
         _lib.call("pa_mat_set_values", self.h, nzval.ctypes.data_as(C.c_void_p))

@@ -285,9 +285,18 @@ class PSparseMatrix:
         if ids == "global":
             I = map_parts(lambda i, s: s.to_lids(i), I, rows.partition)
             J = map_parts(lambda j, s: s.to_lids(j), J, cols.partition)
-        csc = map_parts(lambda i, j, v, r, s: compresscoo(i, j, v, r.num_lids, s.num_lids),
-                        I, J, V, rows.partition, cols.partition)
-        return PSparseMatrix.from_csc(csc, rows, cols)
+        # sparse(I, J, V) on the device (pa_mat_from_coo); the host keeps the
+        # CSC pattern only, for matrix_exchanger
+        ctxs = contexts(rows.partition)
+        mats, pats = [], []
+        for c, i, j, v, r, s in zip(ctxs, I.parts, J.parts, V.parts, rows.partition.parts, cols.partition.parts):
+            M, colptr, rowval = DeviceMatrix.from_coo(c, i, j, v, device_index(c, r), device_index(c, s),
+                                                      r.num_lids, s.num_lids)
+            mats.append(M)
+            pats.append(CSC(r.num_lids, s.num_lids, colptr, rowval, np.zeros(0)))
+        backend, pids, shape = rows.partition.backend, rows.partition.part_ids, rows.partition.shape
+        ex = matrix_exchanger(PData(backend, pids, pats, shape), rows, cols)
+        return PSparseMatrix(PData(backend, pids, mats, shape), rows, cols, ex)
 
     def info(self):
         return map_parts(lambda m: m.info(), self.values)
