@@ -207,6 +207,43 @@ function LinearAlgebra.norm(a::PVector{T,<:HIPData}, p::Real=2) where T
   r[]
 end
 
+# PSparseMatrix(I, J, V, rows, cols; ids=:local) (Interfaces.jl:2194-2244):
+# sparse(I,J,V,m,n,+) on the device; the CSC pattern comes back for the
+# host-side matrix_exchanger (2300-2372).
+function pa_mat_coo(ctx::PartCtx, I::Vector{Int64}, J::Vector{Int64}, V::Vector{Tv},
+                    m::Integer, n::Integer, rows_h, cols_h) where Tv
+  out = Ref{Ptr{Cvoid}}(C_NULL)
+  nnz = Ref{Int64}(0)
+  colptr = Vector{Int64}(undef, n + 1)
+  rowval = Vector{Int64}(undef, length(I))
+  check(ccall((:pa_mat_from_coo, libpa), Cint,
+              (Ptr{Cvoid}, Cint, Cint, Int64, Int64, Int64, Ptr{Int64}, Ptr{Int64}, Ptr{Tv},
+               Ptr{Cvoid}, Ptr{Cvoid}, Ref{Int64}, Ptr{Int64}, Ptr{Int64}, Ref{Ptr{Cvoid}}),
+              ctx.h, dtype_code(Tv), 8, m, n, length(I), I, J, V, rows_h, cols_h,
+              nnz, colptr, rowval, out))
+  out[], colptr, resize!(rowval, nnz[])
+end
+
+# IterativeSolvers.cg! (v0.9) on HIP parts: the whole recurrence on the device
+# (scalars included); same iterates as the generic cg! over mul!/dot/norm.
+function IterativeSolvers.cg!(x::PVector{T,<:HIPData}, A::PSparseMatrix{T,<:HIPData},
+                              b::PVector{T,<:HIPData};
+                              abstol::Real=zero(real(T)), reltol::Real=sqrt(eps(real(T))),
+                              maxiter::Int=size(A, 2), log::Bool=false, kwargs...) where T
+  u, r, c = similar(x), similar(x), similar(x)
+  bb = b.rows === x.rows ? b : copyto!(similar(x), b)
+  its = Ref{Int64}(0); res = Ref{Float64}(0.0)
+  hist = log ? Vector{Float64}(undef, maxiter) : Ptr{Float64}(C_NULL)
+  check(ccall((:pa_cg_solve_all, libpa), Cint,
+              (Cint, Ptr{Ptr{Cvoid}}, Ptr{Ptr{Cvoid}}, Ptr{Ptr{Cvoid}}, Ptr{Ptr{Cvoid}},
+               Ptr{Ptr{Cvoid}}, Ptr{Ptr{Cvoid}}, Ptr{Ptr{Cvoid}}, Ptr{Ptr{Cvoid}},
+               Float64, Float64, Int64, Cint, Ref{Int64}, Ref{Float64}, Ptr{Float64}),
+              num_parts(x.values), dev_mat(A), dev_vec(x), dev_vec(bb), dev_vec(u), dev_vec(r),
+              dev_vec(c), dev_idx(x.rows), dev_xchg(x.rows), reltol, abstol, maxiter, 16, its, res, hist))
+  mark_host_dirty!(x)
+  log ? (x, resize!(hist, its[])) : x
+end
+
 # dev_vec / dev_idx / dev_xchg / dev_mat / mark_device_dirty!: the handle
 # cache and host/device coherence (INTEGRATION.md §3) — omitted here.
 
