@@ -644,9 +644,19 @@ def _id_tensor_product(d_to_dlid_to_gdid, d_to_ngdids):
     return out
 
 
+def _oid_first(ngids, np_, p):
+    """first(_oid_to_gid(ngids, np, p)): Julia's `first` of a UnitRange is its
+    start, also for an empty range (a part that owns no ids)."""
+    _olength = ngids // np_
+    _offset = _olength * (p - 1)
+    _rem = ngids % np_
+    offset = _offset if _rem < (np_ - p + 1) else _offset + p - (np_ - _rem) - 1
+    return 1 + offset
+
+
 def _part_to_firstgid(ngids, np_):
     """Interfaces.jl:1493-1495"""
-    return [_oid_to_gid(ngids, np_, p)[0] for p in range(1, np_ + 1)]
+    return [_oid_first(ngids, np_, p) for p in range(1, np_ + 1)]
 
 
 def linear_gid_to_part(part_to_firstgid):
@@ -674,7 +684,7 @@ def prange_linear(parts: PData, ngids: int) -> PRange:
 
     def mk(part):
         o = _oid_to_gid(ngids, np_, part)
-        return index_range(part, len(o), o[0])
+        return index_range(part, len(o), _oid_first(ngids, np_, part))
     partition = map_parts(mk, parts)
     g2p = map_parts(lambda _: linear_gid_to_part(p2f), parts)
     return prange(ngids, partition, g2p, ghost=False)

@@ -1,0 +1,108 @@
+"""Edge cases of the device path against the oracle: parts that own no ids
+(PRange(parts, n) with n < nparts, test_interfaces.jl's linear PRange rule),
+parts without neighbours, an empty COO, and the CG on such partitions."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def be(pamd):
+    if pamd.device_count() == 0:
+        pytest.fail("no HIP device visible: the GPU tests need the MI355X")
+    return pamd.HIPBackend(devices=[0])
+
+
+def _tridiag(n, part_rows):
+    """global-id COO of the owned rows of a 1-D Laplacian-like matrix."""
+    I, J, V = [], [], []
+    for g in part_rows:
+        for d, v in ((-1, -1.0), (0, 4.0), (1, -1.5)):
+            if 1 <= g + d <= n:
+                I.append(g)
+                J.append(g + d)
+                V.append(v + 0.01 * g)
+    return np.array(I, np.int64), np.array(J, np.int64), np.array(V)
+
+
+def _build(pamd, O, parts, n, nparts):
+    rows = pamd.prange_linear(parts, n)
+    coo = {p: _tridiag(n, rows.partition.local(p).lid_to_gid[rows.partition.local(p).oid_to_lid - 1])
+           for p in parts.part_ids}
+    mk = lambda k: pamd.PData(parts.backend, parts.part_ids, [coo[p][k] for p in parts.part_ids], parts.shape)
+    cols = pamd.add_gids(rows, mk(1))
+    A = pamd.PSparseMatrix.from_coo(mk(0), mk(1), mk(2), rows, cols, ids="global")
+    oparts = O.get_part_ids(nparts)
+    orows = O.prange_linear(oparts, n)
+    oI = O.PData([list(coo[p][0]) for p in parts.part_ids])
+    oJ = O.PData([list(coo[p][1]) for p in parts.part_ids])
+    oV = O.PData([coo[p][2].copy() for p in parts.part_ids])
+    ocols = O.add_gids(orows, oJ)
+    OA = O.psparse_from_coo(oI, oJ, oV, orows, ocols, ids="global")
+    return A, OA
+
+
+@pytest.mark.parametrize("n,nparts", [(3, 4), (2, 4), (5, 8), (1, 3)])
+def test_empty_parts_spmv_exchange_reductions(be, pamd, O, n, nparts):
+    parts = be.get_part_ids(nparts)
+    A, OA = _build(pamd, O, parts, n, nparts)
+    assert any(s.num_oids == 0 for s in A.rows.partition.parts)  # at least one empty part
+    rng = np.random.default_rng(2)
+    xs = {p: rng.uniform(-1, 1, A.cols.partition.local(p).num_lids) for p in parts.part_ids}
+    x = pamd.PVector.from_host(pamd.map_parts(lambda s: xs[s.part], A.cols.partition), A.cols)
+    y = pamd.PVector.undef(A.rows)
+    pamd.mul_(y, A, x)
+    ox = O.PVector(O.map_parts(lambda s: xs[s.part].copy(), OA.cols.partition), OA.cols)
+    oy = O.pvector_undef(OA.rows)
+    O.mul_(oy, OA, ox)
+    for p in parts.part_ids:
+        s = A.rows.partition.local(p)
+        own = s.oid_to_lid - 1
+        assert np.array_equal(y.to_host().local(p)[own], oy.values[p][own])
+        assert np.array_equal(x.to_host().local(p), ox.values[p])  # ghosts after the halo
+    # exchange! / assemble! on the column partition
+    v = pamd.PVector.from_host(pamd.map_parts(lambda s: xs[s.part], A.cols.partition), A.cols)
+    ov = O.PVector(O.map_parts(lambda s: xs[s.part].copy(), OA.cols.partition), OA.cols)
+    pamd.assemble_(v)
+    O.assemble_(ov)
+    for p in parts.part_ids:
+        assert np.array_equal(v.to_host().local(p), ov.values[p])
+    assert abs(pamd.dot(x, x) - O.dot(ox, ox)) <= 1e-12 * abs(O.dot(ox, ox))
+    assert abs(pamd.norm(y) - O.norm(oy)) <= 1e-12 * max(1e-300, O.norm(oy))
+
+
+@pytest.mark.parametrize("device", [False, True])
+def test_empty_parts_cg(be, pamd, O, device):
+    """CG on a partition with empty parts: host-driven == device-driven, and
+    the residual history follows the oracle's."""
+    n, nparts = 6, 8
+    parts = be.get_part_ids(nparts)
+    A, OA = _build(pamd, O, parts, n, nparts)
+    bh = {p: np.ones(A.cols.partition.local(p).num_lids) for p in parts.part_ids}
+    b = pamd.PVector.from_host(pamd.map_parts(lambda s: bh[s.part], A.cols.partition), A.cols)
+    x = pamd.PVector.undef(A.cols).fill_(0)
+    hist = []
+    pamd.cg_(x, A, b, history=hist, device=device, batch=2)
+    ob = O.PVector(O.map_parts(lambda s: bh[s.part].copy(), OA.cols.partition), OA.cols)
+    ox = O.pvector_undef(OA.cols)
+    ohist = []
+    O.cg_(ox, OA, ob, log=ohist)
+    assert len(hist) == len(ohist) > 0
+    np.testing.assert_allclose(hist, ohist, rtol=1e-8, atol=1e-14)
+
+
+def test_single_part_no_halo_and_empty_matrix(be, pamd):
+    """One part (no exchanger traffic) and a matrix with no stored entries:
+    mul! writes β*y = 0 on owned values, ghost values untouched."""
+    parts = be.get_part_ids(1)
+    rows = pamd.prange_linear(parts, 10)
+    e = pamd.PData(parts.backend, [1], [np.zeros(0, np.int64)], parts.shape)
+    A = pamd.PSparseMatrix.from_coo(e, e, pamd.PData(parts.backend, [1], [np.zeros(0)], parts.shape),
+                                    rows, rows, ids="global")
+    x = pamd.PVector.full(1.0, rows)
+    y = pamd.PVector.full(7.0, rows)
+    pamd.mul_(y, A, x)
+    assert np.all(y.to_host().local(1) == 0.0)
+    pamd.mul_(y, A, x, 2.0, 1.0)
+    assert np.all(y.to_host().local(1) == 0.0)
