@@ -92,6 +92,18 @@ int pa_xchg_create(pa_ctx* ctx,
                    pa_xchg** out);
 int pa_xchg_destroy(pa_xchg* xg);
 
+/* Global ids on the device.
+ * pa_index_set_gids: attach lid_to_gid (num_lids 1-based gids) to the
+ * index set; the library keeps a sorted gid → lid table on the device.
+ * pa_add_gids: add_gids!(a, gids) (Interfaces.jl:579-603, 618-627) — the
+ * n gids that are not local ids of the set, each once, in first-touch order,
+ * into new_gids (capacity cap; *n_new is set even when it exceeds cap, and
+ * the call then fails so the caller can retry).  The host appends them as
+ * ghosts with their owners (gid_to_part) and builds the Exchanger.       */
+int pa_index_set_gids(pa_index* idx, const int64_t* lid_to_gid);
+int pa_add_gids(pa_index* idx, int64_t n, const int64_t* gids, int64_t cap,
+                int64_t* new_gids, int64_t* n_new);
+
 /* ---- vectors (the values of one part of a PVector) --------------------- */
 int pa_vec_create(pa_ctx* ctx, int dtype, int64_t n, pa_vec** out);
 int pa_vec_destroy(pa_vec* v);
@@ -133,12 +145,14 @@ int pa_mat_from_csc(pa_ctx* ctx, int dtype, int index_bytes,
  * 80-94) on the device (stable radix sort, duplicates summed in input
  * order), then the same SELL layout as pa_mat_from_csc.  I, J: 1-based
  * local ids (index_bytes 4 or 8), ncoo entries each; an index out of range
- * is an error (BoundsError).  *csc_nnz = nnz of the combined CSC; when
+ * is an error (BoundsError).  ids_global = 1 (ids=:global): I, J are Int64
+ * global ids, mapped by to_lids! on the device through the gid tables of
+ * rows and cols (pa_index_set_gids; an unknown gid is a KeyError).  *csc_nnz = nnz of the combined CSC; when
  * colptr_out (ncols_lids+1) / rowval_out (>= ncoo) are non-NULL the CSC
  * pattern is written there, 1-based, for host setup that needs it
  * (matrix_exchanger, Interfaces.jl:2300-2372).  The nonzeros' CSC order is
  * what pa_mat_set_values / pa_mat_get_values / pa_mat_xchg_create use.   */
-int pa_mat_from_coo(pa_ctx* ctx, int dtype, int index_bytes,
+int pa_mat_from_coo(pa_ctx* ctx, int dtype, int index_bytes, int ids_global,
                     int64_t nrows_lids, int64_t ncols_lids, int64_t ncoo,
                     const void* I, const void* J, const void* V,
                     const pa_index* rows, const pa_index* cols,

@@ -52,8 +52,10 @@ _SIGS = {
     "pa_vec_copy": [_p, _p, _p, _p, C.c_int],
     "pa_vec_axpby": [_p, _p, _p, _p, C.c_int, C.c_int],
     "pa_mat_from_csc": [_p, C.c_int, C.c_int, C.c_int64, C.c_int64, _p, _p, _p, _p, _p, C.POINTER(_p)],
-    "pa_mat_from_coo": [_p, C.c_int, C.c_int, C.c_int64, C.c_int64, C.c_int64, _p, _p, _p, _p, _p, _i64p, _i64p,
-                        _i64p, C.POINTER(_p)],
+    "pa_mat_from_coo": [_p, C.c_int, C.c_int, C.c_int, C.c_int64, C.c_int64, C.c_int64, _p, _p, _p, _p, _p, _i64p,
+                        _i64p, _i64p, C.POINTER(_p)],
+    "pa_index_set_gids": [_p, _i64p],
+    "pa_add_gids": [_p, C.c_int64, _i64p, C.c_int64, _i64p, _i64p],
     "pa_mat_set_values": [_p, _p],
     "pa_mat_get_values": [_p, _p],
     "pa_mat_xchg_create": [_p, C.c_int32, _i32p, _i32p, _i64p, C.c_int32, _i32p, _i32p, _i64p, C.POINTER(_p)],

@@ -49,6 +49,10 @@ void coo_fill(int dtype, int64_t nnz, int64_t nu, const uint64_t* key2, const in
               const int64_t* gflag, const int64_t* grank, int64_t slots, int32_t* col, void* val, int64_t* nz_slot,
               hipStream_t st);
 void launch_fill_i32(int64_t n, int32_t* a, int32_t v, hipStream_t st);
+int gid_table(int64_t n, const int64_t* d_lid_to_gid, uint64_t** sgid, int64_t** slid, hipStream_t st);
+int gids_to_lids(int64_t n, int64_t* ids, const uint64_t* sgid, const int64_t* slid, int64_t nl, hipStream_t st);
+int gids_first_touch(int64_t n, const int64_t* gids, const uint64_t* sgid, const int64_t* slid, int64_t nl,
+                     int64_t** out, int64_t* m_out, hipStream_t st);
 void launch_pack(int dtype, int64_t n, const int32_t* lids, const void* v, void* buf,
                  hipStream_t st);
 void launch_unpack(int dtype, int64_t n, const int32_t* lids, const pa_combine_plan& plan, int op,
@@ -559,7 +563,62 @@ int pa_index_destroy(pa_index* I) {
   (void)hipSetDevice(I->ctx->device);
   dev_free(I->d_oid_to_lid);
   dev_free(I->d_hid_to_lid);
+  dev_free(I->d_sgid);
+  dev_free(I->d_slid);
   delete I;
+  return 0;
+}
+
+// gid → lid table of the index set (lid_to_gid: nlids 1-based gids), sorted
+// on the device; used by pa_add_gids and pa_mat_from_coo(ids_global=1).
+int pa_index_set_gids(pa_index* I, const int64_t* lid_to_gid) {
+  CHECK_ARG(I && (lid_to_gid || I->nlids == 0), "null argument");
+  pa_ctx* c = I->ctx;
+  HIPC(hipSetDevice(c->device));
+  dev_free(I->d_sgid);
+  dev_free(I->d_slid);
+  I->d_sgid = nullptr;
+  I->d_slid = nullptr;
+  int64_t* d = nullptr;
+  if (I->nlids > 0) {
+    std::vector<int64_t> h(lid_to_gid, lid_to_gid + I->nlids);
+    for (int64_t g : h) CHECK_ARG(g >= 1, "lid_to_gid: gids are 1-based");
+    if (dev_upload(&d, h)) return -1;
+    const int rc = gid_table(I->nlids, d, &I->d_sgid, &I->d_slid, c->s_main);
+    dev_free(d);
+    CHECK_ARG(rc == 0, "pa_index_set_gids: device sort failed");
+  }
+  I->has_gids = true;
+  return 0;
+}
+
+// add_gids!(a, gids) (Interfaces.jl:579-603, 618-627): the gids that are not
+// local ids of the index set, each once, in first-touch order → new_gids
+// (cap entries available; *n_new is set even when it exceeds cap, which is
+// then an error so the caller can retry with a larger buffer).
+int pa_add_gids(pa_index* I, int64_t n, const int64_t* gids, int64_t cap, int64_t* new_gids, int64_t* n_new) {
+  CHECK_ARG(I && n_new && (n == 0 || gids), "null argument");
+  CHECK_ARG(I->has_gids, "pa_add_gids: call pa_index_set_gids first");
+  pa_ctx* c = I->ctx;
+  HIPC(hipSetDevice(c->device));
+  *n_new = 0;
+  if (n == 0) return 0;
+  int64_t* d = nullptr;
+  HIPC(hipMalloc((void**)&d, n * 8));
+  hipError_t e = hipMemcpy(d, gids, n * 8, hipMemcpyHostToDevice);
+  if (e != hipSuccess) { dev_free(d); HIPC(e); }
+  int64_t* out = nullptr;
+  int64_t m = 0;
+  const int rc = gids_first_touch(n, d, I->d_sgid, I->d_slid, I->nlids, &out, &m, c->s_main);
+  dev_free(d);
+  CHECK_ARG(rc == 0, "pa_add_gids: device pass failed");
+  *n_new = m;
+  if (m > cap || (m > 0 && !new_gids)) { dev_free(out); PA_FAIL("pa_add_gids: new_gids buffer too small (see *n_new)"); }
+  if (m > 0) {
+    e = hipMemcpy(new_gids, out, m * 8, hipMemcpyDeviceToHost);
+    dev_free(out);
+    HIPC(e);
+  }
   return 0;
 }
 
@@ -830,10 +889,12 @@ struct DevBufs {
 };
 }  // namespace
 
-int pa_mat_from_coo(pa_ctx* c, int dtype, int index_bytes, int64_t nrows_lids, int64_t ncols_lids, int64_t ncoo,
-                    const void* I, const void* J, const void* V, const pa_index* rows, const pa_index* cols,
-                    int64_t* csc_nnz, int64_t* colptr_out, int64_t* rowval_out, pa_mat** out) {
+int pa_mat_from_coo(pa_ctx* c, int dtype, int index_bytes, int ids_global, int64_t nrows_lids, int64_t ncols_lids,
+                    int64_t ncoo, const void* I, const void* J, const void* V, const pa_index* rows,
+                    const pa_index* cols, int64_t* csc_nnz, int64_t* colptr_out, int64_t* rowval_out, pa_mat** out) {
   CHECK_ARG(c && out && rows && cols && csc_nnz, "null argument");
+  CHECK_ARG(!ids_global || (index_bytes == 8 && rows->has_gids && cols->has_gids),
+            "ids=:global needs Int64 ids and pa_index_set_gids on rows and cols");
   CHECK_ARG(ncoo >= 0 && (ncoo == 0 || (I && J && V)), "null COO arrays");
   CHECK_ARG(valid_dtype(dtype), "invalid dtype");
   CHECK_ARG(index_bytes == 4 || index_bytes == 8, "index_bytes must be 4 or 8");
@@ -854,6 +915,12 @@ int pa_mat_from_coo(pa_ctx* c, int dtype, int index_bytes, int64_t nrows_lids, i
     HIPC(hipMemcpy(dI, I, ncoo * index_bytes, hipMemcpyHostToDevice));
     HIPC(hipMemcpy(dJ, J, ncoo * index_bytes, hipMemcpyHostToDevice));
     HIPC(hipMemcpy(dV, V, ncoo * S, hipMemcpyHostToDevice));
+    if (ids_global) {  // to_lids!(I, rows); to_lids!(J, cols) (Interfaces.jl:2206-2209, 1541-1543)
+      const int r1 = gids_to_lids(ncoo, (int64_t*)dI, rows->d_sgid, rows->d_slid, rows->nlids, st);
+      const int r2 = r1 ? r1 : gids_to_lids(ncoo, (int64_t*)dJ, cols->d_sgid, cols->d_slid, cols->nlids, st);
+      CHECK_ARG(r1 >= 0 && r2 >= 0, "to_lids!: device pass failed");
+      CHECK_ARG(r1 == 0 && r2 == 0, "to_lids!: a global id is not a local id of the part (KeyError)");
+    }
   }
   int64_t nu = 0;
   int32_t *crow = nullptr, *ccol = nullptr;

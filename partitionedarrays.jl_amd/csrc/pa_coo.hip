@@ -385,3 +385,171 @@ void launch_fill_i32(int64_t n, int32_t* a, int32_t v, hipStream_t st) {
 }
 
 }  // namespace pa
+
+// ---------------------------------------------------------------------------
+// Global ids on the device: the gid → lid table of an
+// index set (sorted gids + their lids), `to_lids!` (Interfaces.jl:1541-1543)
+// and the first-touch ghost discovery of `add_gids!` (579-603, 1515-1533).
+
+namespace pa {
+
+__global__ void k_iota_i64(int64_t n, int64_t* __restrict__ a) {
+  for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < n; k += (int64_t)gridDim.x * blockDim.x)
+    a[k] = k;
+}
+
+// lid (0-based) of gid, or -1: binary search in the sorted gid table
+__device__ inline int64_t gid_lookup(int64_t g, const uint64_t* __restrict__ sgid, const int64_t* __restrict__ slid,
+                                     int64_t nl) {
+  int64_t lo = 0, hi = nl;
+  while (lo < hi) {
+    const int64_t mid = (lo + hi) >> 1;
+    if ((int64_t)sgid[mid] < g) lo = mid + 1; else hi = mid;
+  }
+  return (lo < nl && (int64_t)sgid[lo] == g) ? slid[lo] : -1;
+}
+
+// ids (1-based gids) → 1-based lids in place; *bad = 1 if a gid is absent
+__global__ void k_to_lids(int64_t n, int64_t* __restrict__ ids, const uint64_t* __restrict__ sgid,
+                          const int64_t* __restrict__ slid, int64_t nl, int* __restrict__ bad) {
+  for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < n; k += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t l = gid_lookup(ids[k], sgid, slid, nl);
+    if (l < 0) *bad = 1;
+    ids[k] = l + 1;
+  }
+}
+
+// flag[k] = gid absent from the table
+__global__ void k_absent(int64_t n, const int64_t* __restrict__ gids, const uint64_t* __restrict__ sgid,
+                         const int64_t* __restrict__ slid, int64_t nl, int64_t* __restrict__ flag) {
+  for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < n; k += (int64_t)gridDim.x * blockDim.x)
+    flag[k] = gid_lookup(gids[k], sgid, slid, nl) < 0 ? 1 : 0;
+}
+
+__global__ void k_compact(int64_t n, const int64_t* __restrict__ gids, const int64_t* __restrict__ flag,
+                          const int64_t* __restrict__ pos, uint64_t* __restrict__ key, int64_t* __restrict__ val) {
+  for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < n; k += (int64_t)gridDim.x * blockDim.x)
+    if (flag[k]) {
+      key[pos[k]] = (uint64_t)gids[k];
+      val[pos[k]] = k;
+    }
+}
+
+// after sorting (gid, position) pairs: at each distinct gid, its first
+// position becomes the key and the gid the payload
+__global__ void k_first_touch(int64_t m, const uint64_t* __restrict__ key, const int64_t* __restrict__ val,
+                              const int64_t* __restrict__ head, const int64_t* __restrict__ rank,
+                              uint64_t* __restrict__ key2, int64_t* __restrict__ val2) {
+  for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < m; k += (int64_t)gridDim.x * blockDim.x)
+    if (head[k]) {
+      key2[rank[k] - 1] = (uint64_t)val[k];
+      val2[rank[k] - 1] = (int64_t)key[k];
+    }
+}
+
+// sorted (gid, lid) table of lid_to_gid (device input, n lids)
+int gid_table(int64_t n, const int64_t* d_lid_to_gid, uint64_t** sgid, int64_t** slid, hipStream_t st) {
+  *sgid = nullptr;
+  *slid = nullptr;
+  if (n <= 0) return 0;
+  int64_t maxg = 0;
+  if (hipMalloc((void**)sgid, n * 8) != hipSuccess || hipMalloc((void**)slid, n * 8) != hipSuccess) return -1;
+  if (hipMemcpyAsync(*sgid, d_lid_to_gid, n * 8, hipMemcpyDeviceToDevice, st) != hipSuccess) return -1;
+  hipLaunchKernelGGL(k_iota_i64, grid1(n), dim3(256), 0, st, n, *slid);
+  // the largest gid bounds the radix passes
+  {
+    size_t tb = 0;
+    void* tmp = nullptr;
+    int64_t* dmax = nullptr;
+    if (hipMalloc((void**)&dmax, 8) != hipSuccess) return -1;
+    hipError_t e = rocprim::reduce(nullptr, tb, d_lid_to_gid, dmax, (int64_t)0, (size_t)n, rocprim::maximum<int64_t>(), st);
+    if (e == hipSuccess) e = hipMalloc(&tmp, tb ? tb : 1);
+    if (e == hipSuccess) e = rocprim::reduce(tmp, tb, d_lid_to_gid, dmax, (int64_t)0, (size_t)n, rocprim::maximum<int64_t>(), st);
+    if (e == hipSuccess) e = hipMemcpyAsync(&maxg, dmax, 8, hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    if (tmp) (void)hipFree(tmp);
+    (void)hipFree(dmax);
+    if (e != hipSuccess) return -1;
+  }
+  return sort_pairs(*sgid, *slid, n, bits_for((uint64_t)(maxg > 0 ? maxg : 1)), st) == hipSuccess ? 0 : -1;
+}
+
+// ids (n, device, 1-based gids) → 1-based lids; returns 1 if a gid is absent
+int gids_to_lids(int64_t n, int64_t* ids, const uint64_t* sgid, const int64_t* slid, int64_t nl, hipStream_t st) {
+  if (n <= 0) return 0;
+  int* bad = nullptr;
+  int hbad = 0;
+  if (hipMalloc((void**)&bad, sizeof(int)) != hipSuccess) return -1;
+  hipError_t e = hipMemsetAsync(bad, 0, sizeof(int), st);
+  hipLaunchKernelGGL(k_to_lids, grid1(n), dim3(256), 0, st, n, ids, sgid, slid, nl, bad);
+  if (e == hipSuccess) e = hipMemcpyAsync(&hbad, bad, sizeof(int), hipMemcpyDeviceToHost, st);
+  if (e == hipSuccess) e = hipStreamSynchronize(st);
+  (void)hipFree(bad);
+  if (e != hipSuccess) return -1;
+  return hbad ? 1 : 0;
+}
+
+// add_gids!: the gids (device, n) absent from the table, each once, in order
+// of first occurrence.  *out (device, *m entries) is owned by the caller.
+int gids_first_touch(int64_t n, const int64_t* gids, const uint64_t* sgid, const int64_t* slid, int64_t nl,
+                     int64_t** out, int64_t* m_out, hipStream_t st) {
+  *out = nullptr;
+  *m_out = 0;
+  if (n <= 0) return 0;
+  int64_t *flag = nullptr, *pos = nullptr, *val = nullptr, *head = nullptr, *rank = nullptr, *val2 = nullptr;
+  uint64_t *key = nullptr, *key2 = nullptr;
+  int64_t m = 0, lastf = 0, u = 0, maxg = 0;
+  hipError_t e = hipMalloc((void**)&flag, n * 8);
+  if (e == hipSuccess) e = hipMalloc((void**)&pos, n * 8);
+  if (e != hipSuccess) goto fail;
+  hipLaunchKernelGGL(k_absent, grid1(n), dim3(256), 0, st, n, gids, sgid, slid, nl, flag);
+  e = exclusive_sum(flag, pos, n, st);
+  if (e == hipSuccess) e = hipMemcpy(&m, pos + n - 1, 8, hipMemcpyDeviceToHost);
+  if (e == hipSuccess) e = hipMemcpy(&lastf, flag + n - 1, 8, hipMemcpyDeviceToHost);
+  if (e != hipSuccess) goto fail;
+  m += lastf;
+  if (m > 0) {
+    e = hipMalloc((void**)&key, m * 8);
+    if (e == hipSuccess) e = hipMalloc((void**)&val, m * 8);
+    if (e != hipSuccess) goto fail;
+    hipLaunchKernelGGL(k_compact, grid1(n), dim3(256), 0, st, n, gids, flag, pos, key, val);
+    (void)hipFree(flag); flag = nullptr;
+    (void)hipFree(pos); pos = nullptr;
+    {
+      size_t tb = 0;
+      void* tmp = nullptr;
+      int64_t* dmax = nullptr;
+      e = hipMalloc((void**)&dmax, 8);
+      if (e == hipSuccess) e = rocprim::reduce(nullptr, tb, (const int64_t*)key, dmax, (int64_t)0, (size_t)m, rocprim::maximum<int64_t>(), st);
+      if (e == hipSuccess) e = hipMalloc(&tmp, tb ? tb : 1);
+      if (e == hipSuccess) e = rocprim::reduce(tmp, tb, (const int64_t*)key, dmax, (int64_t)0, (size_t)m, rocprim::maximum<int64_t>(), st);
+      if (e == hipSuccess) e = hipMemcpyAsync(&maxg, dmax, 8, hipMemcpyDeviceToHost, st);
+      if (e == hipSuccess) e = hipStreamSynchronize(st);
+      if (tmp) (void)hipFree(tmp);
+      if (dmax) (void)hipFree(dmax);
+      if (e != hipSuccess) goto fail;
+    }
+    e = sort_pairs(key, val, m, bits_for((uint64_t)(maxg > 0 ? maxg : 1)), st);
+    if (e == hipSuccess) e = hipMalloc((void**)&head, m * 8);
+    if (e == hipSuccess) e = hipMalloc((void**)&rank, m * 8);
+    if (e != hipSuccess) goto fail;
+    hipLaunchKernelGGL(k_heads, grid1(m), dim3(256), 0, st, m, key, head);
+    e = inclusive_sum(head, rank, m, st);
+    if (e == hipSuccess) e = hipMemcpy(&u, rank + m - 1, 8, hipMemcpyDeviceToHost);
+    if (e == hipSuccess) e = hipMalloc((void**)&key2, u * 8);
+    if (e == hipSuccess) e = hipMalloc((void**)&val2, u * 8);
+    if (e != hipSuccess) goto fail;
+    hipLaunchKernelGGL(k_first_touch, grid1(m), dim3(256), 0, st, m, key, val, head, rank, key2, val2);
+    e = sort_pairs(key2, val2, u, bits_for((uint64_t)n), st);
+    if (e != hipSuccess) goto fail;
+    *out = val2;
+    val2 = nullptr;
+    *m_out = u;
+  }
+fail:
+  for (void* p : {(void*)flag, (void*)pos, (void*)val, (void*)head, (void*)rank, (void*)val2, (void*)key, (void*)key2})
+    if (p) (void)hipFree(p);
+  return e == hipSuccess ? 0 : -1;
+}
+
+}  // namespace pa

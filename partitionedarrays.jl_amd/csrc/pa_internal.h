@@ -132,6 +132,10 @@ struct pa_index {
   std::vector<int32_t> h_oid_to_lid;  // 0-based host copies
   std::vector<int32_t> h_hid_to_lid;
   std::vector<int32_t> h_lid_to_ohid;  // reference's lid_to_ohid (1-based ±)
+  // gid → lid table (pa_index_set_gids): gids sorted ascending, their lids
+  uint64_t* d_sgid = nullptr;
+  int64_t* d_slid = nullptr;
+  bool has_gids = false;
 };
 
 // Ordered combine plan: for each distinct target lid, the buffer positions

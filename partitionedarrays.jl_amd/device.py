@@ -127,6 +127,36 @@ def device_index(ctx: PartContext, s):
     return d
 
 
+def device_index_gids(ctx: PartContext, s):
+    """device_index with its gid → lid table attached (pa_index_set_gids)."""
+    d = device_index(ctx, s)
+    if not getattr(d, "has_gids", False):
+        g = np.ascontiguousarray(s.lid_to_gid, dtype=np.int64)
+        _lib.call("pa_index_set_gids", d.h, g.ctypes.data_as(C.POINTER(C.c_int64)))
+        d.has_gids = True
+    return d
+
+
+def device_first_touch(ctx: PartContext, s, gids):
+    """add_gids! discovery on the device (pa_add_gids): the gids that are not
+    local ids of s, each once, in first-touch order."""
+    d = device_index_gids(ctx, s)
+    gids = np.ascontiguousarray(gids, dtype=np.int64).ravel()
+    L = _lib.lib()
+    cap = min(len(gids), max(4096, len(gids) // 16))
+    while True:
+        out = np.empty(max(1, cap), dtype=np.int64)
+        n_new = C.c_int64(0)
+        rc = L.pa_add_gids(d.h, len(gids), gids.ctypes.data_as(C.POINTER(C.c_int64)), cap,
+                           out.ctypes.data_as(C.POINTER(C.c_int64)), C.byref(n_new))
+        if rc == 0:
+            return out[:n_new.value].copy()
+        if n_new.value > cap:
+            cap = n_new.value
+            continue
+        raise _lib.PAError(f"pa_add_gids: {L.pa_last_error().decode(errors='replace')}")
+
+
 class DeviceExchanger:
     def __init__(self, ctx: PartContext, parts_rcv, lids_rcv, parts_snd, lids_snd):
         pr, prp = _lib.i32(parts_rcv)
@@ -230,10 +260,13 @@ class DeviceMatrix:
         return M
 
     @staticmethod
-    def from_coo(ctx: PartContext, I, J, V, rows_idx: DeviceIndex, cols_idx: DeviceIndex, nrows_lids, ncols_lids):
+    def from_coo(ctx: PartContext, I, J, V, rows_idx: DeviceIndex, cols_idx: DeviceIndex, nrows_lids, ncols_lids,
+                 ids_global=False):
         """sparse(I, J, V, m, n, +) and the SELL build on the device
-        (pa_mat_from_coo).  Returns (matrix, colptr, rowval): the CSC pattern
-        (1-based) for the host setup that needs it (matrix_exchanger)."""
+        (pa_mat_from_coo; ids_global: I, J are gids mapped by to_lids! on the
+        device, the indices need their gid tables).  Returns (matrix, colptr,
+        rowval): the CSC pattern (1-based lids) for the host setup that needs
+        it (matrix_exchanger)."""
         I = np.ascontiguousarray(I, dtype=np.int64).ravel()
         J = np.ascontiguousarray(J, dtype=np.int64).ravel()
         V = np.ascontiguousarray(V).ravel()
@@ -243,7 +276,8 @@ class DeviceMatrix:
         rowval = np.empty(max(1, len(I)), dtype=np.int64)
         nnz = C.c_int64(0)
         h = C.c_void_p()
-        _lib.call("pa_mat_from_coo", ctx.h, _lib.DTYPES[V.dtype], 8, nrows_lids, ncols_lids, len(I),
+        _lib.call("pa_mat_from_coo", ctx.h, _lib.DTYPES[V.dtype], 8, 1 if ids_global else 0, nrows_lids, ncols_lids,
+                  len(I),
                   I.ctypes.data_as(C.c_void_p), J.ctypes.data_as(C.c_void_p), V.ctypes.data_as(C.c_void_p),
                   rows_idx.h, cols_idx.h, C.byref(nnz), colptr.ctypes.data_as(C.POINTER(C.c_int64)),
                   rowval.ctypes.data_as(C.POINTER(C.c_int64)), C.byref(h))

@@ -395,7 +395,18 @@ def add_gids_(a: PRange, gids: PData, i_to_part: PData = None, neighbors=None) -
     else:
         if a.gid_to_part is None:
             raise ValueError("DomainError: the PRange has no gid_to_part; pass the owners")
-        map_parts(lambda f, s, g: s.add_gids_owner(f, g), a.gid_to_part, a.partition, gids)
+        backend = a.partition.backend
+        if hasattr(backend, "context"):  # HIP parts: first-touch discovery on the device
+            from .device import device_first_touch
+
+            def dev(f, s, g):
+                new = device_first_touch(backend.context(s.part), s, g)
+                if len(new):
+                    s._append_ghosts(new, f(new))
+                return s
+            map_parts(dev, a.gid_to_part, a.partition, gids)
+        else:
+            map_parts(lambda f, s, g: s.add_gids_owner(f, g), a.gid_to_part, a.partition, gids)
     a.exchanger = exchanger_from_ids(a.partition, neighbors)
     a.ghost = True
     return a

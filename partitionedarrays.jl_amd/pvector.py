@@ -15,7 +15,7 @@ import numpy as np
 from . import _lib
 from .backends import PData, exchange, map_parts, unzip
 from .device import (DeviceMatrix, DeviceMatrixExchanger, DeviceVector, contexts, device_exchanger,
-                     device_index)
+                     device_index, device_index_gids)
 from .helpers import Table, counts_to_ptrs
 from .prange import Exchanger, PRange, empty_exchanger, hids_are_equal, oids_are_equal
 
@@ -282,16 +282,16 @@ class PSparseMatrix:
     @staticmethod
     def from_coo(I: PData, J: PData, V: PData, rows: PRange, cols: PRange, ids="local"):
         """PSparseMatrix(I, J, V, rows, cols; ids) (Interfaces.jl:2194-2215, sparse init)"""
-        if ids == "global":
-            I = map_parts(lambda i, s: s.to_lids(i), I, rows.partition)
-            J = map_parts(lambda j, s: s.to_lids(j), J, cols.partition)
-        # sparse(I, J, V) on the device (pa_mat_from_coo); the host keeps the
-        # CSC pattern only, for matrix_exchanger
+        # to_lids! (ids=:global) and sparse(I, J, V) on the device
+        # (pa_mat_from_coo); the host keeps the CSC pattern only, for
+        # matrix_exchanger
+        glob = ids == "global"
+        idx = device_index_gids if glob else device_index
         ctxs = contexts(rows.partition)
         mats, pats = [], []
         for c, i, j, v, r, s in zip(ctxs, I.parts, J.parts, V.parts, rows.partition.parts, cols.partition.parts):
-            M, colptr, rowval = DeviceMatrix.from_coo(c, i, j, v, device_index(c, r), device_index(c, s),
-                                                      r.num_lids, s.num_lids)
+            M, colptr, rowval = DeviceMatrix.from_coo(c, i, j, v, idx(c, r), idx(c, s), r.num_lids, s.num_lids,
+                                                      ids_global=glob)
             mats.append(M)
             pats.append(CSC(r.num_lids, s.num_lids, colptr, rowval, np.zeros(0)))
         backend, pids, shape = rows.partition.backend, rows.partition.part_ids, rows.partition.shape

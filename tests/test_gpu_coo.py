@@ -111,7 +111,7 @@ def test_device_sparse_int32_and_bounds(be, pamd):
     rowval = np.empty(200, np.int64)
     nnz = C.c_int64()
     h = C.c_void_p()
-    L.call("pa_mat_from_coo", ctx.h, L.PA_F64, 4, s.num_lids, s.num_lids, 200, I4.ctypes.data_as(C.c_void_p),
+    L.call("pa_mat_from_coo", ctx.h, L.PA_F64, 4, 0, s.num_lids, s.num_lids, 200, I4.ctypes.data_as(C.c_void_p),
            J4.ctypes.data_as(C.c_void_p), V.ctypes.data_as(C.c_void_p), idx.h, idx.h, C.byref(nnz),
            colptr.ctypes.data_as(C.POINTER(C.c_int64)), rowval.ctypes.data_as(C.POINTER(C.c_int64)), C.byref(h))
     M4 = pamd.DeviceMatrix(h, ctx, np.float64)
@@ -130,3 +130,44 @@ def test_device_sparse_int32_and_bounds(be, pamd):
     y.fill_(5.0)
     pamd.mul_(y, A0, x)
     assert np.all(y.to_host().local(1)[s.oid_to_lid - 1] == 0.0)
+
+
+@pytest.mark.parametrize("N,nparts", [((24, 22, 20), 8), ((13, 11, 9), 3)])
+def test_device_add_gids_and_to_lids(be, pamd, N, nparts):
+    """add_gids!(rows, J) with the first-touch discovery on the device
+    (pa_add_gids) gives the same ghost layer (gids, owners, order) and
+    Exchanger as the host restatement; PSparseMatrix(...; ids=:global) with
+    to_lids! on the device equals the host-mapped build."""
+    drv = pamd.drivers
+    owners = drv.voronoi_owners(N, nparts)
+    parts_h = pamd.sequential.get_part_ids(nparts)
+    rows_h, cols_h, I_h, J_h, V_h = drv.irregular_partition(parts_h, N, 27, owners)
+    parts = be.get_part_ids(nparts)
+    rows, cols, I, J, V = drv.irregular_partition(parts, N, 27, owners)
+    for p in parts.part_ids:
+        a, b = cols.partition.local(p), cols_h.partition.local(p)
+        assert np.array_equal(a.lid_to_gid, b.lid_to_gid) and np.array_equal(a.lid_to_part, b.lid_to_part)
+        assert np.array_equal(a.hid_to_lid, b.hid_to_lid)
+        for t in ("lids_rcv", "lids_snd"):
+            ta, tb = getattr(cols.exchanger, t).local(p), getattr(cols_h.exchanger, t).local(p)
+            assert np.array_equal(ta.data, tb.data) and np.array_equal(ta.ptrs, tb.ptrs)
+        assert np.array_equal(cols.exchanger.parts_rcv.local(p), cols_h.exchanger.parts_rcv.local(p))
+        assert np.array_equal(cols.exchanger.parts_snd.local(p), cols_h.exchanger.parts_snd.local(p))
+    A = pamd.PSparseMatrix.from_coo(I, J, V, rows, cols, ids="global")
+    Il = pamd.map_parts(lambda i, s: s.to_lids(i), I, rows.partition)
+    Jl = pamd.map_parts(lambda j, s: s.to_lids(j), J, cols.partition)
+    B = pamd.PSparseMatrix.from_coo(Il, Jl, V, rows, cols, ids="local")
+    for p in parts.part_ids:
+        assert np.array_equal(A.values.local(p).get_values(), B.values.local(p).get_values())
+        assert A.values.local(p).info() == B.values.local(p).info()
+
+
+def test_device_to_lids_unknown_gid(be, pamd):
+    parts = be.get_part_ids(1)
+    rows = pamd.prange_linear(parts, 10)
+    s = rows.partition.local(1)
+    ctx = be.context(1)
+    I = np.array([1, 2, 11])
+    with pytest.raises(pamd.PAError, match="KeyError"):
+        pamd.DeviceMatrix.from_coo(ctx, I, I, np.ones(3), pamd.device.device_index_gids(ctx, s),
+                                   pamd.device.device_index_gids(ctx, s), 10, 10, ids_global=True)
