@@ -35,18 +35,36 @@ def algorithmic_bytes(nnz, n_own, n_ghost, n_snd, n_rcv, S, I=4):
     return nnz * (S + I) + (n_own + 1) * I + (n_own + n_ghost) * S + n_own * S + (n_snd + n_rcv) * (I + 2 * S)
 
 
+def host_cores():
+    """host cores this process may use, capped at the GPU box's share (16)"""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    return max(1, min(16, n))
+
+
 def cpu_baseline(kind, seconds=15.0, n=128):
-    """oracle/build/spmv_ref on one host core: the reference's CSC column
-    loop (SparseUtils.jl:157-187) restated in C ("port")."""
+    """oracle/build/spmv_ref: the reference's CSC column loop
+    (SparseUtils.jl:157-187) restated in C ("port"), run as MPIBackend would
+    run it on this host: one rank per core (--ranks), each with the CSC of
+    its block of rows, a barrier per SpMV.  A short 1-core run rides along."""
     exe = os.path.join(ROOT, "oracle", "build", "spmv_ref")
     if not os.path.exists(exe):
         subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle")], check=True)
-    out = subprocess.run([exe, "--kind", str(kind), "--n", str(n), "--seconds", str(seconds)],
-                         check=True, capture_output=True, text=True).stdout
-    r = json.loads(out.strip().splitlines()[-1])
-    return {"value": round(r["gbps"], 3), "unit": "GB/s", "cores": 1, "kind": "port",
-            "sample": f"{kind}-pt operator {n}^3 nodes ({r['nnz']} nnz), {r['reps']} SpMVs in ~{seconds:.0f} s, "
-                      f"Int64 CSC column loop (SparseUtils.jl:157-187) in C, 1 thread"}
+
+    def run(ranks, secs):
+        out = subprocess.run([exe, "--kind", str(kind), "--n", str(n), "--seconds", str(secs), "--ranks", str(ranks)],
+                             check=True, capture_output=True, text=True).stdout
+        return json.loads(out.strip().splitlines()[-1])
+    cores = host_cores()
+    r = run(cores, 0.7 * seconds)
+    r1 = run(1, 0.3 * seconds)
+    return {"value": round(r["gbps"], 3), "unit": "GB/s", "cores": cores, "kind": "port",
+            "sample": f"{kind}-pt operator {n}^3 nodes ({r['nnz']} nnz), {r['reps']} SpMVs in ~{0.7 * seconds:.0f} s, "
+                      f"Int64 CSC column loop (SparseUtils.jl:157-187) in C, {cores} MPIBackend-like ranks "
+                      f"(threads, row blocks of PRange(parts, n), barrier per SpMV)",
+            "single_core_gbps": round(r1["gbps"], 3)}
 
 
 def pmc_traffic(args, steps=5):

@@ -15,13 +15,20 @@
  *    both nodes in ascending cell order), or test_fdm.jl's 7-point operator,
  *    assembled as `sparse` does (CSC, rows ascending in each column).
  *
- * Usage: spmv_ref --kind 27|7 --n N [--seconds S] [--reps R]
+ * Usage: spmv_ref --kind 27|7 --n N [--seconds S] [--reps R] [--ranks P]
  *                 [--xin file --yout file]   (raw float64 in/out, length N^3)
+ * --ranks P (P > 1) restates MPIBackend with P ranks on P host threads: the
+ * rows are split into P contiguous blocks (PRange(parts, n), Interfaces.jl:
+ * 1014-1030); each rank holds the CSC of its owned rows over its local
+ * columns (owned + ghost, ghosts appended) and runs the same column loop on
+ * its own copy of x, then all ranks meet at a barrier (the halo exchange and
+ * the max-over-ranks timing of PTimer).
  * Prints one JSON line {"rows","nnz","reps","sec_per_spmv","gbps",...}.
  * Bytes per SpMV use the same algorithmic formula as bench.py (SURVEY.md
  * §8d, Int32 index width): nnz*(8+4) + (n+1)*4 + n*8 (x) + n*8 (y).
  */
-#define _POSIX_C_SOURCE 199309L
+#define _POSIX_C_SOURCE 200809L
+#include <pthread.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -121,17 +128,101 @@ static int row_entries(int64_t r, int64_t* cols, double* vals) {
   return k;
 }
 
+/* ---- MPIBackend-like ranks on threads -------------------------------- */
+typedef struct {
+  int64_t r0, r1;          /* owned global rows [r0, r1) */
+  int64_t c0, nc;          /* local columns: global c0 .. c0+nc-1 (owned + ghosts) */
+  int64_t *colptr, *rowval;
+  double *nzval, *x, *y;
+  int32_t* invrows;        /* local row lid → ohid (all owned here) */
+} Rank;
+
+static pthread_barrier_t g_bar;
+static volatile int g_stop;
+static int g_reps_target;
+static double g_seconds;
+static int g_done;
+
+static void rank_build(Rank* R, const double* B) {
+  const int64_t nrow = R->r1 - R->r0;
+  int64_t cols[27];
+  double vals[27];
+  int64_t lo = R->r0, hi = R->r1 - 1;
+  for (int64_t r = R->r0; r < R->r1; ++r) {
+    int k = row_entries(r, cols, vals);
+    for (int t = 0; t < k; ++t) {
+      if (cols[t] < lo) lo = cols[t];
+      if (cols[t] > hi) hi = cols[t];
+    }
+  }
+  R->c0 = lo;
+  R->nc = hi - lo + 1;
+  R->colptr = calloc((size_t)R->nc + 1, sizeof(int64_t));
+  int64_t nnz = 0;
+  for (int64_t r = R->r0; r < R->r1; ++r) {
+    int k = row_entries(r, cols, vals);
+    for (int t = 0; t < k; ++t) R->colptr[cols[t] - lo + 1]++;
+    nnz += k;
+  }
+  for (int64_t j = 0; j < R->nc; ++j) R->colptr[j + 1] += R->colptr[j];
+  R->rowval = malloc((size_t)(nnz > 0 ? nnz : 1) * sizeof(int64_t));
+  R->nzval = malloc((size_t)(nnz > 0 ? nnz : 1) * sizeof(double));
+  int64_t* cur = malloc((size_t)R->nc * sizeof(int64_t));
+  memcpy(cur, R->colptr, (size_t)R->nc * sizeof(int64_t));
+  for (int64_t r = R->r0; r < R->r1; ++r) {
+    int k = row_entries(r, cols, vals);
+    for (int t = 0; t < k; ++t) {
+      int64_t p = cur[cols[t] - lo]++;
+      R->rowval[p] = r - R->r0 + 1;
+      R->nzval[p] = vals[t];
+    }
+  }
+  free(cur);
+  for (int64_t j = 0; j <= R->nc; ++j) R->colptr[j] += 1;
+  R->invrows = malloc((size_t)(nrow > 0 ? nrow : 1) * sizeof(int32_t));
+  for (int64_t i = 0; i < nrow; ++i) R->invrows[i] = (int32_t)(i + 1);
+  R->x = malloc((size_t)R->nc * sizeof(double));
+  memcpy(R->x, B + lo, (size_t)R->nc * sizeof(double));
+  R->y = malloc((size_t)(nrow > 0 ? nrow : 1) * sizeof(double));
+}
+
+static void* rank_run(void* arg) {
+  Rank* R = (Rank*)arg;
+  const int64_t nrow = R->r1 - R->r0;
+  const double alpha = 1.0;
+  double t0 = 0.0;
+  for (int it = 0;; ++it) {
+    pthread_barrier_wait(&g_bar);
+    if (it == 0) t0 = now();
+    if (g_stop) break;
+    memset(R->y, 0, (size_t)(nrow > 0 ? nrow : 1) * sizeof(double));
+    for (int64_t j = 0; j < R->nc; ++j) {
+      const double axj = R->x[j] * alpha;
+      for (int64_t p = R->colptr[j] - 1; p < R->colptr[j + 1] - 1; ++p) {
+        const int32_t i = R->invrows[R->rowval[p] - 1];
+        if (i > 0) R->y[i - 1] += R->nzval[p] * axj;
+      }
+    }
+    if (pthread_barrier_wait(&g_bar) == PTHREAD_BARRIER_SERIAL_THREAD) {
+      ++g_done;
+      if (g_reps_target > 0 ? g_done >= g_reps_target : (now() - t0) >= g_seconds) g_stop = 1;
+    }
+  }
+  return NULL;
+}
+
 int main(int argc, char** argv) {
   N = 64;
   kind = 27;
   double seconds = 10.0;
-  int reps = 0;
+  int reps = 0, ranks = 1;
   const char *xin = NULL, *yout = NULL;
   for (int i = 1; i < argc; ++i) {
     if (!strcmp(argv[i], "--n") && i + 1 < argc) N = atoll(argv[++i]);
     else if (!strcmp(argv[i], "--kind") && i + 1 < argc) kind = atoi(argv[++i]);
     else if (!strcmp(argv[i], "--seconds") && i + 1 < argc) seconds = atof(argv[++i]);
     else if (!strcmp(argv[i], "--reps") && i + 1 < argc) reps = atoi(argv[++i]);
+    else if (!strcmp(argv[i], "--ranks") && i + 1 < argc) ranks = atoi(argv[++i]);
     else if (!strcmp(argv[i], "--xin") && i + 1 < argc) xin = argv[++i];
     else if (!strcmp(argv[i], "--yout") && i + 1 < argc) yout = argv[++i];
     else { fprintf(stderr, "unknown argument %s\n", argv[i]); return 2; }
@@ -183,6 +274,43 @@ int main(int argc, char** argv) {
       B[i] = ((double)(s >> 11) / 9007199254740992.0) * 2.0 - 1.0;
     }
   }
+  if (ranks > 1) {
+    Rank* Rk = calloc((size_t)ranks, sizeof(Rank));
+    pthread_t* th = malloc((size_t)ranks * sizeof(pthread_t));
+    for (int q = 0; q < ranks; ++q) { /* _oid_to_gid (Interfaces.jl:1307-1319), 0-based */
+      const int64_t ol = n / ranks, rem = n % ranks;
+      const int p = q + 1;
+      int64_t len = ol, off = ol * (p - 1);
+      if (!(rem < (ranks - p + 1))) { len = ol + 1; off = ol * (p - 1) + p - (ranks - rem) - 1; }
+      Rk[q].r0 = off;
+      Rk[q].r1 = off + len;
+      rank_build(&Rk[q], B);
+    }
+    pthread_barrier_init(&g_bar, NULL, (unsigned)ranks);
+    g_reps_target = reps;
+    g_seconds = seconds;
+    double t0 = now();
+    for (int q = 0; q < ranks; ++q) pthread_create(&th[q], NULL, rank_run, &Rk[q]);
+    for (int q = 0; q < ranks; ++q) pthread_join(th[q], NULL);
+    double t1 = now();
+    const double per = (t1 - t0) / g_done;
+    const double bytes = (double)nnz * 12.0 + (double)(n + 1) * 4.0 + (double)n * 16.0;
+    double cs = 0.0;
+    for (int q = 0; q < ranks; ++q)
+      for (int64_t i = 0; i < Rk[q].r1 - Rk[q].r0; ++i) {
+        cs += Rk[q].y[i];
+        Cv[Rk[q].r0 + i] = Rk[q].y[i];
+      }
+    if (yout) {
+      FILE* f = fopen(yout, "wb");
+      fwrite(Cv, sizeof(double), (size_t)n, f);
+      fclose(f);
+    }
+    printf("{\"kind\": %d, \"n_per_dim\": %lld, \"rows\": %lld, \"nnz\": %lld, \"ranks\": %d, \"reps\": %d, "
+           "\"sec_per_spmv\": %.9g, \"gbps\": %.6g, \"bytes_per_spmv\": %.0f, \"checksum\": %.17g}\n",
+           kind, (long long)N, (long long)n, (long long)nnz, ranks, g_done, per, bytes / per / 1e9, bytes, cs);
+    return 0;
+  }
   const double alpha = 1.0;
   const int rflag = 1;
   int done = 0;
@@ -210,7 +338,7 @@ int main(int argc, char** argv) {
   }
   double cs = 0.0;
   for (int64_t i = 0; i < n; ++i) cs += Cv[i];
-  printf("{\"kind\": %d, \"n_per_dim\": %lld, \"rows\": %lld, \"nnz\": %lld, \"reps\": %d, "
+  printf("{\"kind\": %d, \"n_per_dim\": %lld, \"rows\": %lld, \"nnz\": %lld, \"ranks\": 1, \"reps\": %d, "
          "\"sec_per_spmv\": %.9g, \"gbps\": %.6g, \"bytes_per_spmv\": %.0f, \"checksum\": %.17g}\n",
          kind, (long long)N, (long long)n, (long long)nnz, done, per, bytes / per / 1e9, bytes, cs);
   return 0;

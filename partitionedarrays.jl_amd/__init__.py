@@ -21,4 +21,5 @@ from .device import DeviceMatrix, HIPBackend, HIPDistributedBackend, device_inde
 from .pvector import (CSC, PSparseMatrix, PVector, assemble_, axmy_, axpy_, cg_, cg_update_,  # noqa: F401
                       compresscoo, copyto_, dot, exchange_, matvec, mul_, mul_dot_, norm, psum, rmul_,
                       sub_, xpby_)
+from .ptimers import PTimer  # noqa: F401
 from . import drivers  # noqa: F401

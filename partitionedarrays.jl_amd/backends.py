@@ -203,8 +203,22 @@ sequential = SequentialBackend()
 
 
 def prun(driver, backend: AbstractBackend, nparts):
-    """prun(driver, b, nparts) Interfaces.jl:33-36"""
-    return driver(backend.get_part_ids(nparts))
+    """prun(driver, b, nparts) Interfaces.jl:33-36.  With one part per
+    process an exception ends the whole job, as MPIBackend's prun does with
+    MPI.Abort (MPIBackend.jl:21-36): this process exits at once, and the
+    other ranks' pending collectives fail instead of waiting for it."""
+    if not isinstance(backend, DistributedBackend):
+        return driver(backend.get_part_ids(nparts))
+    try:
+        return driver(backend.get_part_ids(nparts))
+    except BaseException:
+        import os
+        import sys
+        import traceback
+        traceback.print_exc()
+        sys.stderr.flush()
+        sys.stdout.flush()
+        os._exit(1)
 
 
 # -- collectives over PData (Interfaces.jl:127-340) ---------------------------

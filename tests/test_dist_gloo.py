@@ -110,3 +110,85 @@ def test_distributed_setup_matches_sequential(pamd, O, world, shape, N, kind):
         assert out["parts_snd"] == cols.exchanger.parts_snd.local(p).tolist() == list(OA.cols.exchanger.parts_snd[p])
         assert out["lids_rcv"] == cols.exchanger.lids_rcv.local(p).tolist()
         assert out["lids_snd"] == cols.exchanger.lids_snd.local(p).tolist() == OA.cols.exchanger.lids_snd[p].tolist()
+
+
+def _fail_if(p, fail_part):
+    if p == fail_part:
+        raise AssertionError("boom")  # test_exception.jl: one part's @assert fails
+    return p
+
+
+def _worker_timer_abort(rank, world, port, fail_part, q):
+    sys.path.insert(0, ROOT)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import time
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import pamd
+
+    def driver(parts):
+        t = pamd.PTimer(parts)
+        t.tic_(barrier=True)
+        time.sleep(0.01 * parts.part_ids[0])
+        t.toc_("sleep")
+        q.put((rank, "timer", t.data))
+        if fail_part:
+            pamd.map_parts(lambda p: _fail_if(p, fail_part), parts)
+            pamd.preduce(lambda a, b: a + b, parts, 0)
+        return True
+    pamd.prun(driver, pamd.DistributedBackend(), world)
+    q.put((rank, "done", None))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("fail_part", [0, 2])
+def test_ptimer_and_prun_abort(fail_part):
+    """PTimer min/max/avg over 4 processes on MAIN (PTimers.jl:40-59); with a
+    failing part every process exits (non-zero) instead of hanging
+    (MPIBackend.jl:21-36, test_exception.jl)."""
+    world = 4
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_worker_timer_abort, args=(r, world, port, fail_part, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    msgs = []
+    import queue
+    import time
+    t_end = time.time() + 120
+    while time.time() < t_end and any(p.is_alive() for p in ps):
+        try:
+            msgs.append(q.get(timeout=0.5))
+        except queue.Empty:
+            pass
+    for p in ps:
+        p.join(timeout=10)
+    while True:
+        try:
+            msgs.append(q.get(timeout=0.5))
+        except queue.Empty:
+            break
+    assert all(p.exitcode is not None for p in ps), "a rank hung"
+    timers = {r: d for r, k, d in msgs if k == "timer"}
+    assert set(timers) == set(range(world))
+    d = timers[0]["sleep"]
+    assert d["min"] >= 0.009 and d["max"] >= 0.039 and d["min"] <= d["avg"] <= d["max"]
+    assert all(timers[r] == {} for r in range(1, world))
+    if fail_part:
+        assert all(p.exitcode != 0 for p in ps)
+    else:
+        assert all(p.exitcode == 0 for p in ps)
+        assert sorted(r for r, k, _ in msgs if k == "done") == list(range(world))
+
+
+def test_ptimer_sequential(pamd):
+    parts = pamd.sequential.get_part_ids(3)
+    t = pamd.PTimer(parts)
+    t.tic_()
+    t.toc_("a")
+    t.toc_("b")
+    d = t.data
+    assert set(d) == {"a", "b"} and all(v["min"] == v["max"] == v["avg"] for v in d.values())
+    assert "Section" in t.report()
