@@ -411,7 +411,8 @@ int pa_tune(const char* key, int value, int* previous) {
   CHECK_ARG(key, "null key");
   int* slot = nullptr;
   if (!std::strcmp(key, "spmv_flags")) {
-    CHECK_ARG(value >= 0 && value <= 3, "spmv_flags: bit 0 = non-temporal streams, bit 1 = XCD mapping");
+    CHECK_ARG(value >= 0 && value <= 7,
+              "spmv_flags: bit 0 = non-temporal streams, bit 1 = XCD mapping, bit 2 = 16 B x runs (pattern rows)");
     slot = &g_spmv_flags;
   } else if (!std::strcmp(key, "spmv_unroll")) {
     CHECK_ARG(value == 4 || value == 8, "spmv_unroll must be 4 or 8");
@@ -690,9 +691,13 @@ int pa_vec_create(pa_ctx* c, int dtype, int64_t n, pa_vec** out) {
   v->dtype = dtype;
   v->n = n;
   if (n) {
-    hipError_t e = hipMalloc(&v->d, (size_t)n * dtype_size(dtype));
+    // kVecPad bytes on both sides: the SpMV's 16 B x runs may start up to
+    // 3 elements before lid 0 or end up to 3 after the last lid
+    const size_t bytes = (size_t)n * dtype_size(dtype) + 2 * kVecPad;
+    hipError_t e = hipMalloc(&v->base, bytes);
     if (e != hipSuccess) { delete v; PA_FAIL(std::string("hipMalloc(vector) failed: ") + hipGetErrorString(e)); }
-    HIPC(hipMemsetAsync(v->d, 0, (size_t)n * dtype_size(dtype), c->s_main));
+    v->d = (char*)v->base + kVecPad;
+    HIPC(hipMemsetAsync(v->base, 0, bytes, c->s_main));
   }
   *out = v;
   return 0;
@@ -702,7 +707,7 @@ int pa_vec_destroy(pa_vec* v) {
   if (!v) return 0;
   (void)hipSetDevice(v->ctx->device);
   (void)hipStreamSynchronize(v->ctx->s_main);
-  dev_free(v->d);
+  dev_free(v->base);
   delete v;
   return 0;
 }

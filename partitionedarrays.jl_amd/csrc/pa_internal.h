@@ -162,11 +162,14 @@ struct pa_xchg {
   pa_combine_plan plan_rev;   // unpack targets = lids_snd (reverse/assemble)
 };
 
+constexpr size_t kVecPad = 64;  // bytes before and after a vector's values (pa_vec_create)
+
 struct pa_vec {
   pa_ctx* ctx = nullptr;
   int dtype = PA_F64;
   int64_t n = 0;
-  void* d = nullptr;
+  void* d = nullptr;      // the values (base + kVecPad)
+  void* base = nullptr;   // the allocation (owned; null for views)
 };
 
 struct pa_mat {

@@ -37,10 +37,12 @@ __device__ inline int64_t xcd_remap(int64_t b, int64_t G) {
   return x * q + (x < r ? x : r) + i;
 }
 
-enum { SPMV_NT = 1, SPMV_XCD = 2 };
-// Process-wide knobs (pa_tune).  Defaults from the A/B in
-// profiles/r01_ab_spmv.txt: non-temporal streams on, XCD remap off, U = 8.
-int g_spmv_flags = SPMV_NT;
+enum { SPMV_NT = 1, SPMV_XCD = 2, SPMV_XPAIR = 4 };
+// Process-wide knobs (pa_tune).  Defaults from the A/Bs in
+// profiles/r01_ab_spmv.txt and profiles/r01/ab_xpair.txt: non-temporal
+// streams on, XCD remap off, U = 8, 16 B x runs on (FE27 256³: F64 −9 %,
+// F32 −33 %, C64 −5 % kernel time).
+int g_spmv_flags = SPMV_NT | SPMV_XPAIR;
 int g_spmv_unroll = 8;
 int g_spmv_format = 1;  // 1: pattern slices where built, 0: int32 columns only
 
@@ -150,15 +152,34 @@ __device__ __forceinline__ void rows_int32(T (&acc)[R], const IPack<R>* __restri
   }
 }
 
-// pattern rows: column of row `rbase + r` at entry k is rbase + r + pat[k]
-template <typename T, int R, bool ALPHA, bool NT, int U>
+// the R consecutive x values x[i .. i+R-1] as one 16 B load (i only
+// dword-aligned: global loads need 4 B alignment); pa_vec pads 64 B on both
+// sides, so i in [-(R-1), n-1] stays inside the allocation
+typedef unsigned int u4a __attribute__((ext_vector_type(4))) __attribute__((aligned(4)));
+template <typename T, int R>
+__device__ __forceinline__ Pack<T, R> ld_xrun(const T* p) {
+  static_assert(sizeof(Pack<T, R>) == 16, "16 B runs");
+  const u4a r = *reinterpret_cast<const u4a*>(p);
+  Pack<T, R> v;
+  __builtin_memcpy(&v, &r, 16);
+  return v;
+}
+
+// pattern rows: column of row `rbase + r` at entry k is rbase + r + pat[k].
+// XP: the lane's R rows read R consecutive x values per entry, fetched as
+// one 16 B run (rows that are not regular get values they never use).
+template <typename T, int R, bool ALPHA, bool NT, int U, bool XP>
 __device__ __forceinline__ void rows_pattern(T (&acc)[R], const int32_t* __restrict__ pat,
                                              const Pack<T, R>* __restrict__ vp, int len,
                                              const T* __restrict__ x, int64_t rbase,
                                              const bool (&ok)[R], T alpha) {
   int64_t xb[R];
+  bool any = false;
 #pragma unroll
-  for (int r = 0; r < R; ++r) xb[r] = ok[r] ? rbase + r : -1;
+  for (int r = 0; r < R; ++r) {
+    xb[r] = ok[r] ? rbase + r : -1;
+    any = any || ok[r];
+  }
   int k = 0;
   for (; k + U <= len; k += U) {
     int32_t o[U];
@@ -168,10 +189,19 @@ __device__ __forceinline__ void rows_pattern(T (&acc)[R], const int32_t* __restr
 #pragma unroll
     for (int u = 0; u < U; ++u) v[u] = ld<NT>(&vp[(k + u) * 64]);
     T xv[U][R];
+    if constexpr (XP && R > 1) {
 #pragma unroll
-    for (int u = 0; u < U; ++u)
+      for (int u = 0; u < U; ++u) {
+        const Pack<T, R> xr = ld_xrun<T, R>(x + (any ? rbase + o[u] : 0));
 #pragma unroll
-      for (int r = 0; r < R; ++r) xv[u][r] = x[xb[r] >= 0 ? xb[r] + o[u] : 0];
+        for (int r = 0; r < R; ++r) xv[u][r] = xr.v[r];
+      }
+    } else {
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int r = 0; r < R; ++r) xv[u][r] = x[xb[r] >= 0 ? xb[r] + o[u] : 0];
+    }
 #pragma unroll
     for (int u = 0; u < U; ++u)
 #pragma unroll
@@ -237,8 +267,13 @@ __global__ __launch_bounds__(256) void k_spmv_sell(SpmvArgs<T> a) {
   const Pack<T, R>* __restrict__ vp = reinterpret_cast<const Pack<T, R>*>(a.val + off) + lane;
   if (PAT) {
     const int32_t* pat = a.pat + s * a.kmax;
-    if (a.flags & SPMV_NT) rows_pattern<T, R, ALPHA, true, U>(acc, pat, vp, len, a.x, row0, ok, a.alpha);
-    else rows_pattern<T, R, ALPHA, false, U>(acc, pat, vp, len, a.x, row0, ok, a.alpha);
+    if (a.flags & SPMV_XPAIR) {
+      if (a.flags & SPMV_NT) rows_pattern<T, R, ALPHA, true, U, true>(acc, pat, vp, len, a.x, row0, ok, a.alpha);
+      else rows_pattern<T, R, ALPHA, false, U, true>(acc, pat, vp, len, a.x, row0, ok, a.alpha);
+    } else {
+      if (a.flags & SPMV_NT) rows_pattern<T, R, ALPHA, true, U, false>(acc, pat, vp, len, a.x, row0, ok, a.alpha);
+      else rows_pattern<T, R, ALPHA, false, U, false>(acc, pat, vp, len, a.x, row0, ok, a.alpha);
+    }
   } else {
     const IPack<R>* __restrict__ cp = reinterpret_cast<const IPack<R>*>(a.col + off) + lane;
     if (a.flags & SPMV_NT) rows_int32<T, R, ALPHA, true, U>(acc, cp, vp, len, a.x, a.alpha);
