@@ -36,6 +36,7 @@ void launch_cg_alpha(int dtype, int P, const void* gathered, CGState* cst, hipSt
 void launch_cg_step(int P, const double* gathered, CGState* cst, double* history, hipStream_t st);
 void launch_gather_ptrs(int P, const void* const* srcs, int accsz, void* out, hipStream_t st);
 extern int g_spmv_format;
+int g_halo_pull = 1;  // pa_tune("halo_pull"): pull-unpack between parts of one process
 // COO → CSC → SELL on the device (pa_coo.hip)
 int coo_compress(int dtype, int index_bytes, int64_t m, int64_t ncols, int64_t n, const void* dI, const void* dJ,
                  const void* dV, int64_t* nu_out, int32_t** crow, int32_t** ccol, void** cval, int64_t** colptr,
@@ -57,6 +58,8 @@ void launch_pack(int dtype, int64_t n, const int32_t* lids, const void* v, void*
                  hipStream_t st);
 void launch_unpack(int dtype, int64_t n, const int32_t* lids, const pa_combine_plan& plan, int op,
                    const void* buf, void* v, hipStream_t st);
+void launch_pull(int dtype, int64_t n, const int32_t* lids, const pa_combine_plan& plan, int op, const int32_t* bid,
+                 const int64_t* elem, const void* const* bases, void* v, hipStream_t st);
 void launch_fill(int dtype, int64_t n, int64_t base, const int32_t* map, void* v, const void* s,
                  hipStream_t st);
 void launch_copy(int dtype, int64_t n, const int32_t* dmap, void* d, const int32_t* smap,
@@ -291,15 +294,94 @@ LocalSet local_set(int n, H* const* hs) {
   return L;
 }
 
+// Pull table of receiver i for direction dir (see pa_pull): built once per
+// set of local senders; ok = false when a sender's device is not reachable
+// by peer access (then the staging copies below are used).
+int build_pull(int i, int n, pa_xchg* const xg[], const LocalSet& L, int dtype, int dir) {
+  pa_xchg* X = xg[i];
+  pa_ctx* c = X->ctx;
+  pa_pull& P = X->pull[dir];
+  const auto& prcv = dir == 0 ? X->parts_rcv : X->parts_snd;
+  const auto& orcv = dir == 0 ? X->ptrs_rcv : X->ptrs_snd;
+  void* own = dir == 0 ? X->d_buf_rcv : X->d_buf_snd;
+  std::vector<const void*> key;
+  key.push_back((const void*)(intptr_t)dtype_size(dtype));
+  for (int32_t q : prcv) {
+    const int j = L.find(q);
+    key.push_back(j >= 0 ? (const void*)xg[j] : nullptr);
+    key.push_back(j >= 0 ? (dir == 0 ? xg[j]->d_buf_snd : xg[j]->d_buf_rcv) : own);
+  }
+  if (P.built && P.key == key) return 0;
+  dev_free(P.d_bid);
+  dev_free(P.d_elem);
+  dev_free(P.d_bases);
+  P = pa_pull{};
+  P.built = true;
+  P.key = key;
+  HIPC(hipSetDevice(c->device));
+  std::vector<void*> bases;
+  auto base_id = [&](void* b) {
+    for (size_t t = 0; t < bases.size(); ++t)
+      if (bases[t] == b) return (int32_t)t;
+    bases.push_back(b);
+    return (int32_t)(bases.size() - 1);
+  };
+  const int64_t nslots = orcv.empty() ? 0 : orcv.back();
+  std::vector<int32_t> bid(nslots);
+  std::vector<int64_t> elem(nslots);
+  for (size_t k = 0; k < prcv.size(); ++k) {
+    const int j = L.find(prcv[k]);
+    const int64_t cnt = orcv[k + 1] - orcv[k];
+    if (j < 0) {  // remote sender: RCCL delivers into this part's own buffer
+      const int32_t b = base_id(own);
+      for (int64_t t = 0; t < cnt; ++t) { bid[orcv[k] + t] = b; elem[orcv[k] + t] = orcv[k] + t; }
+      continue;
+    }
+    pa_xchg* Q = xg[j];
+    const auto& qsnd = dir == 0 ? Q->parts_snd : Q->parts_rcv;
+    const auto& qo = dir == 0 ? Q->ptrs_snd : Q->ptrs_rcv;
+    int m = -1;
+    for (size_t t = 0; t < qsnd.size(); ++t)
+      if (qsnd[t] == c->part) { m = (int)t; break; }
+    CHECK_ARG(m >= 0, "exchanger mismatch: a receiver lists a sender that does not send to it");
+    CHECK_ARG(cnt == qo[m + 1] - qo[m], "exchanger mismatch: segment lengths differ (SequentialBackend.jl:187)");
+    const int qdev = Q->ctx->device;
+    if (qdev != c->device) {
+      int can = 0;
+      HIPC(hipDeviceCanAccessPeer(&can, c->device, qdev));
+      if (!can) return 0;  // P.ok stays false
+      hipError_t e = hipDeviceEnablePeerAccess(qdev, 0);
+      if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) HIPC(e);
+      (void)hipGetLastError();
+    }
+    const int32_t b = base_id(dir == 0 ? Q->d_buf_snd : Q->d_buf_rcv);
+    for (int64_t t = 0; t < cnt; ++t) { bid[orcv[k] + t] = b; elem[orcv[k] + t] = qo[m] + t; }
+  }
+  if (dev_upload(&P.d_bid, bid) || dev_upload(&P.d_elem, elem) || dev_upload(&P.d_bases, bases)) return -1;
+  P.ok = true;
+  return 0;
+}
+
 // Halo transport for n local parts.  dir 0 (forward): send A-layout buffers
 // (ptrs_snd) to parts_snd, receive B-layout (ptrs_rcv) from parts_rcv;
 // dir 1 (reverse): the opposite.  Each part's s_comm first waits for the
-// packs of every sender it copies from (ev_packed), then ev_recvd is
-// recorded on it.
-int transport(int n, pa_xchg* const xg[], int dtype, int dir) {
+// packs of every sender it reads from (ev_packed), then ev_recvd is recorded
+// on it.  Senders in other processes: RCCL into the receive buffer.
+// Senders in this process: when every part's pull table is usable and the
+// target vectors v are given, s_comm runs one pull-unpack kernel per part
+// that combines (op) the values straight from the senders' buffers into
+// v[i] (*unpacked = true; the caller must not unpack again); otherwise
+// device-to-device copies into the receive buffer.
+int transport(int n, pa_xchg* const xg[], int dtype, int dir, int op, pa_vec* const v[], bool* unpacked) {
   const size_t S = dtype_size(dtype);
   LocalSet L = local_set(n, xg);
   bool remote = false;
+  *unpacked = false;
+  bool pull = v != nullptr && g_halo_pull;
+  for (int i = 0; i < n && pull; ++i) {
+    if (build_pull(i, n, xg, L, dtype, dir)) return -1;
+    pull = xg[i]->pull[dir].ok;
+  }
   for (int i = 0; i < n; ++i) {
     pa_xchg* X = xg[i];
     pa_ctx* c = X->ctx;
@@ -346,33 +428,45 @@ int transport(int n, pa_xchg* const xg[], int dtype, int dir) {
     }
     NCCLC(ncclGroupEnd());
   }
-  // local copies: receiver r, segment k from sender q (local), which holds
-  // the matching segment at the position of r in its send list.
   for (int i = 0; i < n; ++i) {
     pa_xchg* X = xg[i];
     pa_ctx* c = X->ctx;
     HIPC(hipSetDevice(c->device));
-    const auto& prcv = dir == 0 ? X->parts_rcv : X->parts_snd;
-    const auto& orcv = dir == 0 ? X->ptrs_rcv : X->ptrs_snd;
-    char* brcv = (char*)(dir == 0 ? X->d_buf_rcv : X->d_buf_snd);
-    for (size_t k = 0; k < prcv.size(); ++k) {
-      const int j = L.find(prcv[k]);
-      if (j < 0) continue;
-      pa_xchg* Q = xg[j];
-      const auto& qsnd = dir == 0 ? Q->parts_snd : Q->parts_rcv;
-      const auto& qo = dir == 0 ? Q->ptrs_snd : Q->ptrs_rcv;
-      const char* bq = (const char*)(dir == 0 ? Q->d_buf_snd : Q->d_buf_rcv);
-      int m = -1;
-      for (size_t t = 0; t < qsnd.size(); ++t)
-        if (qsnd[t] == c->part) { m = (int)t; break; }
-      CHECK_ARG(m >= 0, "exchanger mismatch: a receiver lists a sender that does not send to it");
-      const int64_t cnt = orcv[k + 1] - orcv[k];
-      CHECK_ARG(cnt == qo[m + 1] - qo[m], "exchanger mismatch: segment lengths differ (SequentialBackend.jl:187)");
-      if (cnt > 0)
-        HIPC(hipMemcpyAsync(brcv + orcv[k] * S, bq + qo[m] * S, (size_t)cnt * S, hipMemcpyDefault, c->s_comm));
+    if (pull) {
+      const pa_pull& P = X->pull[dir];
+      if (dir == 0)
+        launch_pull(dtype, X->n_rcv_data, X->d_lids_rcv, X->plan_fwd, op, P.d_bid, P.d_elem,
+                    (const void* const*)P.d_bases, v[i]->d, c->s_comm);
+      else
+        launch_pull(dtype, X->n_snd_data, X->d_lids_snd, X->plan_rev, op, P.d_bid, P.d_elem,
+                    (const void* const*)P.d_bases, v[i]->d, c->s_comm);
+    } else {
+      // staging copies: receiver r, segment k from sender q (local), which
+      // holds the matching segment at the position of r in its send list
+      const auto& prcv = dir == 0 ? X->parts_rcv : X->parts_snd;
+      const auto& orcv = dir == 0 ? X->ptrs_rcv : X->ptrs_snd;
+      char* brcv = (char*)(dir == 0 ? X->d_buf_rcv : X->d_buf_snd);
+      for (size_t k = 0; k < prcv.size(); ++k) {
+        const int j = L.find(prcv[k]);
+        if (j < 0) continue;
+        pa_xchg* Q = xg[j];
+        const auto& qsnd = dir == 0 ? Q->parts_snd : Q->parts_rcv;
+        const auto& qo = dir == 0 ? Q->ptrs_snd : Q->ptrs_rcv;
+        const char* bq = (const char*)(dir == 0 ? Q->d_buf_snd : Q->d_buf_rcv);
+        int m = -1;
+        for (size_t t = 0; t < qsnd.size(); ++t)
+          if (qsnd[t] == c->part) { m = (int)t; break; }
+        CHECK_ARG(m >= 0, "exchanger mismatch: a receiver lists a sender that does not send to it");
+        const int64_t cnt = orcv[k + 1] - orcv[k];
+        CHECK_ARG(cnt == qo[m + 1] - qo[m], "exchanger mismatch: segment lengths differ (SequentialBackend.jl:187)");
+        if (cnt > 0)
+          HIPC(hipMemcpyAsync(brcv + orcv[k] * S, bq + qo[m] * S, (size_t)cnt * S, hipMemcpyDefault, c->s_comm));
+      }
     }
     HIPC(hipEventRecord(c->ev_recvd, c->s_comm));
   }
+  HIPC(hipGetLastError());
+  *unpacked = pull;
   return 0;
 }
 
@@ -417,6 +511,9 @@ int pa_tune(const char* key, int value, int* previous) {
   } else if (!std::strcmp(key, "spmv_unroll")) {
     CHECK_ARG(value == 4 || value == 8, "spmv_unroll must be 4 or 8");
     slot = &g_spmv_unroll;
+  } else if (!std::strcmp(key, "halo_pull")) {
+    CHECK_ARG(value == 0 || value == 1, "halo_pull: 1 = receivers read the senders' buffers (one kernel), 0 = staging copies");
+    slot = &g_halo_pull;
   } else if (!std::strcmp(key, "spmv_format")) {
     CHECK_ARG(value == 0 || value == 1, "spmv_format: 0 = int32 columns, 1 = pattern slices");
     slot = &g_spmv_format;
@@ -676,6 +773,11 @@ int pa_xchg_destroy(pa_xchg* X) {
   dev_free(X->d_buf_snd);
   free_plan(X->plan_fwd);
   free_plan(X->plan_rev);
+  for (auto& t : X->pull) {
+    dev_free(t.d_bid);
+    dev_free(t.d_elem);
+    dev_free(t.d_bases);
+  }
   delete X;
   return 0;
 }
@@ -1187,6 +1289,7 @@ static int spmv_impl(int n, pa_mat* const A[], pa_vec* const y[], const pa_index
   }
   const bool has_alpha = !scalar_is(dt, alpha, 1.0);
   const int bmode = scalar_is(dt, beta, 0.0) ? 0 : (scalar_is(dt, beta, 1.0) ? 1 : 2);
+  bool pulled = false;
 
   if (any_x) {
     for (int i = 0; i < n; ++i) {
@@ -1200,7 +1303,7 @@ static int spmv_impl(int n, pa_mat* const A[], pa_vec* const y[], const pa_index
       launch_pack(dt, xg[i]->n_snd_data, xg[i]->d_lids_snd, x[i]->d, xg[i]->d_buf_snd, c->s_main);
       HIPC(hipEventRecord(c->ev_packed, c->s_main));
     }
-    if (transport(n, xg, dt, 0)) return -1;
+    if (transport(n, xg, dt, 0, PA_REPLACE, x, &pulled)) return -1;
   }
   for (int i = 0; i < n; ++i) {
     pa_ctx* c = A[i]->ctx;
@@ -1225,8 +1328,9 @@ static int spmv_impl(int n, pa_mat* const A[], pa_vec* const y[], const pa_index
     HIPC(hipSetDevice(c->device));
     if (any_x) {
       HIPC(hipStreamWaitEvent(c->s_main, c->ev_recvd, 0));
-      launch_unpack(dt, xg[i]->n_rcv_data, xg[i]->d_lids_rcv, xg[i]->plan_fwd, PA_REPLACE,
-                    xg[i]->d_buf_rcv, x[i]->d, c->s_main);
+      if (!pulled)
+        launch_unpack(dt, xg[i]->n_rcv_data, xg[i]->d_lids_rcv, xg[i]->plan_fwd, PA_REPLACE,
+                      xg[i]->d_buf_rcv, x[i]->d, c->s_main);
     }
     if (c->timing) HIPC(hipEventRecord(c->ev_t[2], c->s_main));
     const int32_t* ymap = y_idx[i]->own_contig ? nullptr : y_idx[i]->d_oid_to_lid;
@@ -1281,16 +1385,19 @@ int pa_exchange_all(int n, pa_vec* const v[], pa_xchg* const xg[], const pa_inde
     HIPC(hipEventRecord(c->ev_packed, c->s_main));
   }
   HIPC(hipGetLastError());
-  if (transport(n, xg, dt, reverse ? 1 : 0)) return -1;
+  bool pulled = false;
+  if (transport(n, xg, dt, reverse ? 1 : 0, op, v, &pulled)) return -1;
   for (int i = 0; i < n; ++i) {
     pa_xchg* X = xg[i];
     pa_ctx* c = X->ctx;
     HIPC(hipSetDevice(c->device));
     HIPC(hipStreamWaitEvent(c->s_main, c->ev_recvd, 0));
-    if (!reverse)
+    if (pulled) {
+    } else if (!reverse) {
       launch_unpack(dt, X->n_rcv_data, X->d_lids_rcv, X->plan_fwd, op, X->d_buf_rcv, v[i]->d, c->s_main);
-    else
+    } else {
       launch_unpack(dt, X->n_snd_data, X->d_lids_snd, X->plan_rev, op, X->d_buf_snd, v[i]->d, c->s_main);
+    }
     if (zero_ghosts) {
       CHECK_ARG(idx && idx[i] && idx[i]->nlids == v[i]->n, "assemble!: index set of the vector required");
       unsigned char z[16] = {0};

@@ -148,8 +148,21 @@ struct pa_combine_plan {
   int32_t* d_pos = nullptr;          // buffer positions
 };
 
+// Pull table of one exchange direction (parts of one process): receive slot
+// p of this part reads bases[bid[p]][elem[p]] — a sender's send buffer, or
+// this part's own receive buffer for segments that came over RCCL.
+struct pa_pull {
+  bool built = false;
+  bool ok = false;                   // false: peers not reachable, use staging copies
+  std::vector<const void*> key;      // the local senders' buffers the table was built for
+  int32_t* d_bid = nullptr;
+  int64_t* d_elem = nullptr;
+  void** d_bases = nullptr;
+};
+
 struct pa_xchg {
   pa_ctx* ctx = nullptr;
+  pa_pull pull[2];                             // [0] forward, [1] reverse
   std::vector<int32_t> parts_rcv, parts_snd;   // 1-based
   std::vector<int64_t> ptrs_rcv, ptrs_snd;     // 0-based offsets, size n+1
   int64_t n_rcv_data = 0, n_snd_data = 0;

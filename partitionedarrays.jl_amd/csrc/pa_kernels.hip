@@ -90,6 +90,72 @@ static void unpack_t(int64_t n, const int32_t* lids, const pa_combine_plan& plan
   }
 }
 
+// Pull-unpack (parts of one process): receive slot p reads its value straight
+// from the sender's send buffer, bases[bid[p]][elem[p]] (peer memory over
+// xGMI when the sender is on another device) — no staging copy.
+template <typename T, int OP>
+__global__ void k_pull_unique(int64_t n, const int32_t* __restrict__ lids, const int32_t* __restrict__ bid,
+                              const int64_t* __restrict__ elem, const T* const* __restrict__ bases,
+                              T* __restrict__ v) {
+  for (int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; p < n;
+       p += (int64_t)gridDim.x * blockDim.x) {
+    const int32_t l = lids[p];
+    const T b = bases[bid[p]][elem[p]];
+    v[l] = (OP == PA_ADD) ? v[l] + b : b;
+  }
+}
+
+template <typename T, int OP>
+__global__ void k_pull_ordered(int64_t ntargets, const int32_t* __restrict__ target,
+                               const int32_t* __restrict__ ptr, const int32_t* __restrict__ pos,
+                               const int32_t* __restrict__ bid, const int64_t* __restrict__ elem,
+                               const T* const* __restrict__ bases, T* __restrict__ v) {
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < ntargets;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    const int32_t l = target[t];
+    T acc = v[l];
+    for (int32_t q = ptr[t]; q < ptr[t + 1]; ++q) {
+      const int32_t s = pos[q];
+      const T b = bases[bid[s]][elem[s]];
+      acc = (OP == PA_ADD) ? acc + b : b;
+    }
+    v[l] = acc;
+  }
+}
+
+template <typename T>
+static void pull_t(int64_t n, const int32_t* lids, const pa_combine_plan& plan, int op, const int32_t* bid,
+                   const int64_t* elem, const void* const* bases, void* v, hipStream_t st) {
+  if (n <= 0) return;
+  const T* const* b = (const T* const*)bases;
+  if (plan.unique) {
+    if (op == PA_ADD)
+      hipLaunchKernelGGL((k_pull_unique<T, PA_ADD>), dim3(grid_for(n)), dim3(256), 0, st, n, lids, bid, elem, b,
+                         (T*)v);
+    else
+      hipLaunchKernelGGL((k_pull_unique<T, PA_REPLACE>), dim3(grid_for(n)), dim3(256), 0, st, n, lids, bid, elem,
+                         b, (T*)v);
+  } else {
+    const int64_t nt = plan.ntargets;
+    if (op == PA_ADD)
+      hipLaunchKernelGGL((k_pull_ordered<T, PA_ADD>), dim3(grid_for(nt)), dim3(256), 0, st, nt, plan.d_target,
+                         plan.d_ptr, plan.d_pos, bid, elem, b, (T*)v);
+    else
+      hipLaunchKernelGGL((k_pull_ordered<T, PA_REPLACE>), dim3(grid_for(nt)), dim3(256), 0, st, nt, plan.d_target,
+                         plan.d_ptr, plan.d_pos, bid, elem, b, (T*)v);
+  }
+}
+
+void launch_pull(int dtype, int64_t n, const int32_t* lids, const pa_combine_plan& plan, int op, const int32_t* bid,
+                 const int64_t* elem, const void* const* bases, void* v, hipStream_t st) {
+  switch (dtype) {
+    case PA_F32: pull_t<float>(n, lids, plan, op, bid, elem, bases, v, st); break;
+    case PA_F64: pull_t<double>(n, lids, plan, op, bid, elem, bases, v, st); break;
+    case PA_C64: pull_t<c64>(n, lids, plan, op, bid, elem, bases, v, st); break;
+    case PA_C128: pull_t<c128>(n, lids, plan, op, bid, elem, bases, v, st); break;
+  }
+}
+
 void launch_pack(int dtype, int64_t n, const int32_t* lids, const void* v, void* buf,
                  hipStream_t st) {
   switch (dtype) {

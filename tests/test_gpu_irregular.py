@@ -79,7 +79,16 @@ def test_irregular_spmv_bitexact(be, pamd, O, N, nparts, dtype, fmt):
         pamd._lib.tune("spmv_format", prev)
 
 
-def test_irregular_exchange_assemble_dot(be, pamd, O):
+@pytest.mark.parametrize("pull", [1, 0])
+def test_irregular_exchange_assemble_dot(be, pamd, O, pull):
+    prev = pamd._lib.tune("halo_pull", pull)
+    try:
+        _irregular_exchange_assemble_dot(be, pamd, O)
+    finally:
+        pamd._lib.tune("halo_pull", prev)
+
+
+def _irregular_exchange_assemble_dot(be, pamd, O):
     N, nparts = BIG
     parts = be.get_part_ids(nparts)
     rows, cols, _, _, _ = pamd.drivers.irregular_partition(parts, N, 27)

@@ -29,6 +29,15 @@ def fmt(request, pamd, be):
     pamd._lib.tune("spmv_format", prev)
 
 
+@pytest.fixture(params=[1, 0], ids=["pull", "copies"])
+def halo(request, pamd, be):
+    """Run a test with both in-process halo transports (pa_tune halo_pull):
+    receivers read the senders' buffers in one kernel, or staging copies."""
+    prev = pamd._lib.tune("halo_pull", request.param)
+    yield request.param
+    pamd._lib.tune("halo_pull", prev)
+
+
 def _rand(rng, n, dtype):
     dtype = np.dtype(dtype)
     if dtype.kind == "c":
@@ -66,7 +75,7 @@ CASES = [
 
 
 @pytest.mark.parametrize("shape,N,kind,dtype", CASES)
-def test_stencil_spmv_bitexact(be, pamd, O, fmt, shape, N, kind, dtype):
+def test_stencil_spmv_bitexact(be, pamd, O, fmt, halo, shape, N, kind, dtype):
     parts = be.get_part_ids(shape)
     A = pamd.drivers.stencil_operator(parts, N, kind, dtype)
     rng = np.random.default_rng(SEED)
@@ -127,7 +136,7 @@ def test_alpha_beta(be, pamd, O, fmt, alpha, beta):
         assert np.array_equal(y.to_host().local(p), oy.values[p])
 
 
-def test_exchange_assemble_bitexact(be, pamd, O):
+def test_exchange_assemble_bitexact(be, pamd, O, halo):
     shape, N = (2, 2, 2), (9, 8, 10)
     parts = be.get_part_ids(shape)
     A = pamd.drivers.stencil_operator(parts, N, 27)

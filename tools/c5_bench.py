@@ -1,0 +1,62 @@
+"""BASELINE config 5 on one GPU: FE27 on a Voronoi ("METIS-like") partition,
+all parts on device 0, F64/F32/C128/C64.  Reports mul! time (halo included:
+device copies between the parts), algorithmic GB/s over all parts, and the
+column-encoding coverage (pattern slices / regular rows) of the parts.
+
+    python tools/c5_bench.py [--n 128] [--parts 8] [--dtypes f64,f32,c128,c64]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import pamd  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--n", type=int, default=128)
+ap.add_argument("--parts", type=int, default=8)
+ap.add_argument("--dtypes", default="f64,f32,c128,c64")
+ap.add_argument("--steps", type=int, default=20)
+a = ap.parse_args()
+DT = {"f64": np.float64, "f32": np.float32, "c128": np.complex128, "c64": np.complex64}
+be = pamd.HIPBackend(devices=[0])
+parts = be.get_part_ids(a.parts)
+N = (a.n,) * 3
+owners = pamd.drivers.voronoi_owners(N, a.parts)
+for name in a.dtypes.split(","):
+    dtype = DT[name]
+    t0 = time.perf_counter()
+    A = pamd.drivers.irregular_problem(parts, N, 27, dtype, owners=owners)
+    setup = time.perf_counter() - t0
+    x = pamd.PVector.from_host(pamd.map_parts(
+        lambda s: np.random.default_rng(s.part).uniform(-1, 1, s.num_lids).astype(dtype), A.cols.partition), A.cols)
+    y = pamd.PVector.undef(A.rows, dtype)
+    S = np.dtype(dtype).itemsize
+    B = 0
+    info = {}
+    for p in parts.part_ids:
+        f = A.values.local(p).info()
+        s = A.cols.partition.local(p)
+        ex = A.cols.exchanger
+        B += (f["nnz"] * (S + 4) + (f["nrows"] + 1) * 4 + (f["nrows"] + s.num_hids) * S + f["nrows"] * S
+              + (len(ex.lids_snd.local(p).data) + len(ex.lids_rcv.local(p).data)) * (4 + 2 * S))
+        for k in ("nslices", "pattern_slices", "nrows", "regular_rows", "side_rows"):
+            info[k] = info.get(k, 0) + f[k]
+    for _ in range(3):
+        pamd.mul_(y, A, x)
+    for p in parts.part_ids:
+        be.context(p).sync()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        pamd.mul_(y, A, x)
+    for p in parts.part_ids:
+        be.context(p).sync()
+    t = (time.perf_counter() - t0) / a.steps
+    print(json.dumps({"config": f"C5 FE27 {a.n}^3 Voronoi {a.parts} parts on 1 GPU", "dtype": name,
+                      "ms_per_mul": round(1e3 * t, 4), "gbs_algorithmic_all_parts": round(B / t / 1e9, 1),
+                      "setup_s": round(setup, 2), "format": info}), flush=True)
