@@ -37,6 +37,7 @@ void launch_cg_step(int P, const double* gathered, CGState* cst, double* history
 void launch_gather_ptrs(int P, const void* const* srcs, int accsz, void* out, hipStream_t st);
 extern int g_spmv_format;
 int g_halo_pull = 1;  // pa_tune("halo_pull"): pull-unpack between parts of one process
+int g_comm_cus = 0;   // pa_tune("comm_cus"): CUs reserved for the comm stream (0: priority stream instead)
 // COO → CSC → SELL on the device (pa_coo.hip)
 int coo_compress(int dtype, int index_bytes, int64_t m, int64_t ncols, int64_t n, const void* dI, const void* dJ,
                  const void* dV, int64_t* nu_out, int32_t** crow, int32_t** ccol, void** cval, int64_t** colptr,
@@ -76,6 +77,7 @@ void launch_stencil_fill(const StencilGeom& g, const int32_t* shell, const doubl
                          int64_t nrows, int noids, pa_mat* A, int32_t* err, hipStream_t st);
 extern int g_spmv_flags;
 extern int g_spmv_unroll;
+extern int g_spmv_lds;
 
 }  // namespace pa
 
@@ -508,9 +510,15 @@ int pa_tune(const char* key, int value, int* previous) {
     CHECK_ARG(value >= 0 && value <= 7,
               "spmv_flags: bit 0 = non-temporal streams, bit 1 = XCD mapping, bit 2 = 16 B x runs (pattern rows)");
     slot = &g_spmv_flags;
+  } else if (!std::strcmp(key, "spmv_lds")) {
+    CHECK_ARG(value >= 0 && value <= 160 * 1024, "spmv_lds: bytes of LDS per SpMV block (occupancy cap)");
+    slot = &g_spmv_lds;
   } else if (!std::strcmp(key, "spmv_unroll")) {
     CHECK_ARG(value == 4 || value == 8, "spmv_unroll must be 4 or 8");
     slot = &g_spmv_unroll;
+  } else if (!std::strcmp(key, "comm_cus")) {
+    CHECK_ARG(value >= 0 && value <= 64, "comm_cus: 0..64 CUs reserved for the halo stream (contexts created afterwards)");
+    slot = &g_comm_cus;
   } else if (!std::strcmp(key, "halo_pull")) {
     CHECK_ARG(value == 0 || value == 1, "halo_pull: 1 = receivers read the senders' buffers (one kernel), 0 = staging copies");
     slot = &g_halo_pull;
@@ -546,8 +554,26 @@ int pa_ctx_create(int device, int part, int nparts, pa_ctx** out) {
   c->nparts = nparts;
   int least = 0, greatest = 0;
   HIPC(hipDeviceGetStreamPriorityRange(&least, &greatest));
-  HIPC(hipStreamCreateWithFlags(&c->s_main, hipStreamNonBlocking));
-  HIPC(hipStreamCreateWithPriority(&c->s_comm, hipStreamNonBlocking, greatest));
+  int ncu = 0;
+  HIPC(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device));
+  if (g_comm_cus > 0 && g_comm_cus < ncu) {
+    // k CUs spread over the chip run the halo stream; the compute stream
+    // keeps the rest, so packs/RCCL/pull-unpack never queue behind a
+    // grid-filling SpMV
+    const int k = g_comm_cus, words = (ncu + 31) / 32;
+    std::vector<uint32_t> mm(words, 0), mc(words, 0);
+    for (int cu = 0; cu < ncu; ++cu) mm[cu / 32] |= 1u << (cu % 32);
+    for (int i = 0; i < k; ++i) {
+      const int cu = i * (ncu / k) + (ncu / k - 1);
+      mm[cu / 32] &= ~(1u << (cu % 32));
+      mc[cu / 32] |= 1u << (cu % 32);
+    }
+    HIPC(hipExtStreamCreateWithCUMask(&c->s_main, (uint32_t)words, mm.data()));
+    HIPC(hipExtStreamCreateWithCUMask(&c->s_comm, (uint32_t)words, mc.data()));
+  } else {
+    HIPC(hipStreamCreateWithFlags(&c->s_main, hipStreamNonBlocking));
+    HIPC(hipStreamCreateWithPriority(&c->s_comm, hipStreamNonBlocking, greatest));
+  }
   HIPC(hipMalloc(&c->d_partials, 8192 * 16));  // block partials (reductions, CG update)
   HIPC(hipMalloc(&c->d_fold, 256 * 16));
   HIPC(hipMalloc(&c->d_result, 16));

@@ -44,6 +44,9 @@ enum { SPMV_NT = 1, SPMV_XCD = 2, SPMV_XPAIR = 4 };
 // F32 −33 %, C64 −5 % kernel time).
 int g_spmv_flags = SPMV_NT | SPMV_XPAIR;
 int g_spmv_unroll = 8;
+// dynamic LDS per SpMV block (unused by the kernel): caps the blocks per CU,
+// i.e. the waves streaming at once (160 KB LDS per CU)
+int g_spmv_lds = 0;
 int g_spmv_format = 1;  // 1: pattern slices where built, 0: int32 columns only
 
 template <int BYTES> struct RawOf;
@@ -311,9 +314,9 @@ static void launch_t(const SpmvArgs<T>& a, hipStream_t st) {
   const int64_t blocks = (a.nwork + 3) / 4;
   if (blocks == 0) return;
   if (g_spmv_unroll == 4)
-    hipLaunchKernelGGL((k_spmv_sell<T, R, ALPHA, BMODE, 4, PAT>), dim3(blocks), dim3(256), 0, st, a);
+    hipLaunchKernelGGL((k_spmv_sell<T, R, ALPHA, BMODE, 4, PAT>), dim3(blocks), dim3(256), g_spmv_lds, st, a);
   else
-    hipLaunchKernelGGL((k_spmv_sell<T, R, ALPHA, BMODE, 8, PAT>), dim3(blocks), dim3(256), 0, st, a);
+    hipLaunchKernelGGL((k_spmv_sell<T, R, ALPHA, BMODE, 8, PAT>), dim3(blocks), dim3(256), g_spmv_lds, st, a);
 }
 
 template <typename T, int R, bool PAT>

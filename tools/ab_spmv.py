@@ -21,8 +21,11 @@ ap.add_argument("--dtype", default="f64")
 ap.add_argument("--shape", default="1,1,1", help="parts (all on device 0)")
 ap.add_argument("--rounds", type=int, default=5)
 ap.add_argument("--reps", type=int, default=10)
-ap.add_argument("--variants", default="1:8:0,1:8:1,0:8:1,1:4:1")
+ap.add_argument("--variants", default="1:8:0,1:8:1,0:8:1,1:4:1",
+                help="flags:unroll:format[:lds_bytes],...")
+ap.add_argument("--comm-cus", type=int, default=0, help="pa_tune comm_cus before the contexts exist")
 a = ap.parse_args()
+pamd._lib.tune("comm_cus", a.comm_cus)
 dtype = {"f64": np.float64, "f32": np.float32, "c128": np.complex128, "c64": np.complex64}[a.dtype]
 
 be = pamd.HIPBackend(devices=[0])
@@ -40,6 +43,7 @@ S = np.dtype(dtype).itemsize
 nh = A.cols.partition.local(p0).num_hids
 B = info["nnz"] * (S + 4) + (info["nrows"] + 1) * 4 + (info["nrows"] + nh) * S + info["nrows"] * S
 variants = [tuple(int(t) for t in v.split(":")) for v in a.variants.split(",")]
+variants = [v if len(v) == 4 else v + (0,) for v in variants]
 res = {v: [] for v in variants}
 ref = None
 for rnd in range(a.rounds):
@@ -47,6 +51,7 @@ for rnd in range(a.rounds):
         pamd._lib.tune("spmv_flags", v[0])
         pamd._lib.tune("spmv_unroll", v[1])
         pamd._lib.tune("spmv_format", v[2])
+        pamd._lib.tune("spmv_lds", v[3])
         pamd.mul_(y, A, x)
         ctx.set_timing(True)
         for _ in range(a.reps):
@@ -61,5 +66,5 @@ print(f"n={a.n} kind={a.kind} dtype={a.dtype} parts={shape} part {p0}: {info}")
 print(f"algorithmic bytes per SpMV (part {p0}) = {B}")
 for v in variants:
     t = np.array(res[v])
-    print(f"flags={v[0]} unroll={v[1]} format={'pattern' if v[2] else 'int32'}: median {np.median(t):.4f} ms "
+    print(f"flags={v[0]} unroll={v[1]} format={'pattern' if v[2] else 'int32'} lds={v[3]}: median {np.median(t):.4f} ms "
           f"min {t.min():.4f} -> {B / np.median(t) / 1e6:.0f} GB/s (median), {B / t.min() / 1e6:.0f} (best)")
