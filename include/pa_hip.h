@@ -52,7 +52,12 @@ int pa_device_count(int* count);
  *               (default 5);
  * "spmv_unroll" 4 or 8 entries in flight per lane (default 8);
  * "spmv_format" 1: pattern slices where the matrix has them (default),
- *               0: int32 column ids everywhere.                          */
+ *               0: int32 column ids everywhere;
+ * "long_rows_exact" 1: long rows summed in the reference's order (default),
+ *               0: lane-strided partial sums + tree (within 1e-12);
+ * "halo_pull"   1: parts of one process read their neighbours' packed
+ *               buffers directly (default), 0: staging copies;
+ * "spmv_lds", "comm_cus": occupancy / CU-mask experiments (default 0).    */
 int pa_tune(const char* key, int value, int* previous);
 
 /* ---- part context ------------------------------------------------------
@@ -190,6 +195,12 @@ int pa_mat_info(const pa_mat* A, int64_t* nrows_owned, int64_t* nnz_owned,
 int pa_mat_format_info(const pa_mat* A, int64_t* pattern_slices,
                        int64_t* regular_rows, int64_t* side_rows,
                        int64_t* side_slots);
+
+/* Long rows (row-length histogram): rows with more than max(256, 8 × the
+ * 90th-percentile row length) entries leave the SELL and run one wave per
+ * row over their own CSR (in the reference's summation order unless
+ * pa_tune("long_rows_exact", 0)).  Number of such rows and their nonzeros. */
+int pa_mat_long_rows(const pa_mat* A, int64_t* n_long, int64_t* n_long_nnz);
 
 /* ---- hot path -----------------------------------------------------------
  * mul!(c, a, b, α, β) (Interfaces.jl:2246-2275) for the n local parts:

@@ -46,11 +46,15 @@ int coo_row_order(int64_t nu, const int32_t* crow, const int32_t* ccol, const in
                   int64_t nrows, int64_t noids_c, int64_t ncols, int H, uint64_t** key2, int64_t** idx2,
                   int64_t** rowptr, int64_t** gflag, int64_t** grank, int32_t** slen, int32_t** sghost,
                   int64_t* nnz_out, int64_t* ngh_out, hipStream_t st, hipError_t* err_out);
+void coo_slices(int64_t ns, int64_t nrows, int H, const int64_t* rowptr, const uint64_t* key2, int64_t ncols,
+                int64_t noids_c, const int32_t* lidx, int32_t* slen, int32_t* sghost, hipStream_t st);
 void coo_fill(int dtype, int64_t nnz, int64_t nu, const uint64_t* key2, const int64_t* idx2, const int64_t* rowptr,
               const int64_t* soff, int H, int R, int64_t ncols, const int32_t* ccol, const void* cval,
               const int64_t* gflag, const int64_t* grank, int64_t slots, int32_t* col, void* val, int64_t* nz_slot,
-              hipStream_t st);
+              const int32_t* lidx, const int64_t* lptr, int32_t* lcol, int64_t long_off, hipStream_t st);
 void launch_fill_i32(int64_t n, int32_t* a, int32_t v, hipStream_t st);
+void launch_spmv_long(const pa_mat* A, const void* x, void* y, const int32_t* ymap, bool has_alpha, int bmode,
+                      const void* alpha, const void* beta, void* dotp, int64_t dot_base, hipStream_t st);
 int gid_table(int64_t n, const int64_t* d_lid_to_gid, uint64_t** sgid, int64_t** slid, hipStream_t st);
 int gids_to_lids(int64_t n, int64_t* ids, const uint64_t* sgid, const int64_t* slid, int64_t nl, hipStream_t st);
 int gids_first_touch(int64_t n, const int64_t* gids, const uint64_t* sgid, const int64_t* slid, int64_t nl,
@@ -78,6 +82,7 @@ void launch_stencil_fill(const StencilGeom& g, const int32_t* shell, const doubl
 extern int g_spmv_flags;
 extern int g_spmv_unroll;
 extern int g_spmv_lds;
+extern int g_long_exact;
 
 }  // namespace pa
 
@@ -174,6 +179,59 @@ void free_plan(pa_combine_plan& p) {
   p = pa_combine_plan{};
 }
 
+// Row-length histogram → long rows: a row is long when it has more than
+// max(kLongMin, 8 × the 90th-percentile length) entries.  Such rows would pad
+// every row of their SELL slice to their length; they run in k_spmv_long.
+constexpr int32_t kLongMin = 256;
+int32_t long_threshold(const std::vector<int32_t>& len) {
+  if (len.empty()) return INT32_MAX;
+  std::vector<int32_t> t(len);
+  const size_t k = (t.size() * 9) / 10;
+  std::nth_element(t.begin(), t.begin() + k, t.end());
+  const int64_t thr = std::max<int64_t>(kLongMin, 8 * (int64_t)t[k]);
+  return (int32_t)std::min<int64_t>(thr, INT32_MAX);
+}
+
+// device arrays of the long rows (rows ascending, CSR pointers) and the
+// per-slice skip mask of the int32 kernel
+int upload_long(pa_mat* A, const std::vector<int32_t>& lrows, const std::vector<int64_t>& lptr,
+                const std::vector<int32_t>& lcol) {
+  A->n_long = (int64_t)lrows.size();
+  A->h_long_rows = lrows;
+  if (A->n_long == 0) return 0;
+  const int64_t ns = (A->nrows + A->H - 1) / A->H, W = A->H / 64;
+  std::vector<int32_t> sflags(ns, 0);
+  std::vector<uint64_t> lmask(ns * W, 0);
+  for (int32_t r : lrows) {
+    const int64_t s = r / A->H, i = r - s * A->H;
+    sflags[s] = 1;
+    lmask[s * W + i / 64] |= 1ull << (i & 63);
+  }
+  if (dev_upload(&A->d_long_row, lrows) || dev_upload(&A->d_long_ptr, lptr) || dev_upload(&A->d_sflags, sflags) ||
+      dev_upload(&A->d_lmask, lmask))
+    return -1;
+  // chunks for the parallel (non-exact) mode: consecutive kLongChunk
+  // entries; chunk c ends where chunk c+1 starts (the last at lptr.back())
+  constexpr int64_t kLongChunk = 4096;
+  std::vector<int64_t> cstart, rchunk{0};
+  for (size_t i = 0; i < lrows.size(); ++i) {
+    for (int64_t b = lptr[i]; b < lptr[i + 1]; b += kLongChunk) cstart.push_back(b);
+    rchunk.push_back((int64_t)cstart.size());
+  }
+  A->n_lchunks = (int64_t)cstart.size();
+  cstart.push_back(lptr.back());
+  if (dev_upload(&A->d_lchunk_start, cstart) || dev_upload(&A->d_lrow_chunk, rchunk)) return -1;
+  HIPC(hipMalloc(&A->d_lpart, std::max<int64_t>(A->n_lchunks, 1) * 16));
+  if (!lcol.empty() && dev_upload(&A->d_long_col, lcol)) return -1;
+  return 0;
+}
+
+inline bool is_long_row(const pa_mat* A, int64_t r) {
+  return A->n_long > 0 && std::binary_search(A->h_long_rows.begin(), A->h_long_rows.end(), (int32_t)r);
+}
+
+inline int64_t nvals(const pa_mat* A) { return A->slots + A->n_gnz + A->n_lnz; }
+
 int finish_sell_layout(pa_mat* A, const std::vector<int32_t>& slen, const std::vector<char>& sghost,
                        std::vector<int64_t>* soff_out) {
   const int64_t ns = (int64_t)slen.size();
@@ -234,7 +292,7 @@ int finalize_pattern(pa_mat* A, int kmax, int64_t noids) {
       const int64_t nvalid = std::min<int64_t>(A->H, A->nrows - s * A->H);
       for (int64_t i = 0; i < nvalid; ++i) {
         if ((mask[s * W + i / 64] >> (i & 63)) & 1ull) ++A->nregular_rows;
-        else side.push_back((int32_t)(s * A->H + i));
+        else if (!is_long_row(A, s * A->H + i)) side.push_back((int32_t)(s * A->H + i));
       }
     }
   }
@@ -516,6 +574,9 @@ int pa_tune(const char* key, int value, int* previous) {
   } else if (!std::strcmp(key, "spmv_unroll")) {
     CHECK_ARG(value == 4 || value == 8, "spmv_unroll must be 4 or 8");
     slot = &g_spmv_unroll;
+  } else if (!std::strcmp(key, "long_rows_exact")) {
+    CHECK_ARG(value == 0 || value == 1, "long_rows_exact: 1 = reference summation order, 0 = lane-strided tree (1e-12)");
+    slot = &g_long_exact;
   } else if (!std::strcmp(key, "comm_cus")) {
     CHECK_ARG(value >= 0 && value <= 64, "comm_cus: 0..64 CUs reserved for the halo stream (contexts created afterwards)");
     slot = &g_comm_cus;
@@ -962,23 +1023,45 @@ int pa_mat_from_csc(pa_ctx* c, int dtype, int index_bytes, int64_t nrows_lids, i
     PA_FAIL("CSC rowval out of range");
   }
   const int64_t ns = (nr + A->H - 1) / A->H;
+  // long rows (row-length histogram) leave the SELL
+  const int32_t thr = long_threshold(len);
+  std::vector<int32_t> lidx(nr, -1), lrows;
+  std::vector<int64_t> lptr{0};
+  for (int64_t r = 0; r < nr; ++r)
+    if (len[r] > thr) {
+      lidx[r] = (int32_t)lrows.size();
+      lrows.push_back((int32_t)r);
+      lptr.push_back(lptr.back() + len[r]);
+    }
+  A->n_lnz = lptr.back();
   std::vector<int32_t> slen(ns, 0);
   std::vector<char> sghost(ns, 0);
   int64_t nnz = 0;
   for (int64_t r = 0; r < nr; ++r) {
+    nnz += len[r];
+    if (lidx[r] >= 0) continue;
     slen[r / A->H] = std::max(slen[r / A->H], len[r]);
     if (has_ghost[r]) sghost[r / A->H] = 1;
-    nnz += len[r];
   }
   A->nnz = nnz;
   std::vector<int64_t> soff;
   if (finish_sell_layout(A, slen, sghost, &soff)) { pa_mat_destroy(A); return -1; }
   std::vector<int32_t> hcol(A->slots, -1);
   std::vector<unsigned char> hval(A->slots * S, 0);
+  std::vector<int32_t> lcol(A->n_lnz);
+  std::vector<unsigned char> lval(A->n_lnz * S);
+  std::vector<int64_t> lpos(csc_nnz, -1);  // CSC nz → position in the long CSR
   A->h_nz_slot.assign(csc_nnz, -1);
   std::vector<int32_t> cur(nr, 0);
   const int R = A->R;
   visit([&](int64_t r, int64_t J, int64_t p, bool) {
+    if (lidx[r] >= 0) {  // long row: its CSR, in the same (reference) order
+      const int64_t t = lptr[lidx[r]] + cur[r]++;
+      lcol[t] = (int32_t)J;
+      std::memcpy(&lval[t * S], (const unsigned char*)nzval + p * S, S);
+      lpos[p] = t;
+      return;
+    }
     const int64_t s = r / A->H;
     const int64_t w = r - s * A->H;
     const int64_t lane = w / R, rr = w % R;
@@ -988,20 +1071,24 @@ int pa_mat_from_csc(pa_ctx* c, int dtype, int index_bytes, int64_t nrows_lids, i
     std::memcpy(&hval[slot * S], (const unsigned char*)nzval + p * S, S);
     A->h_nz_slot[p] = slot;
   });
-  // ghost-row nonzeros (dropped by the SpMV, kept for exchange!/assemble!(A))
+  // ghost-row nonzeros (dropped by the SpMV, kept for exchange!/assemble!(A)),
+  // then the long rows' values: both after the SELL slots in d_val
   for (int64_t p = 0; p < csc_nnz; ++p)
-    if (A->h_nz_slot[p] < 0) A->h_nz_slot[p] = -(++A->n_gnz);
-  if (A->n_gnz) {
-    hval.resize((A->slots + A->n_gnz) * S);
-    for (int64_t p = 0; p < csc_nnz; ++p)
-      if (A->h_nz_slot[p] < 0)
-        std::memcpy(&hval[(A->slots - A->h_nz_slot[p] - 1) * S], (const unsigned char*)nzval + p * S, S);
-  }
+    if (A->h_nz_slot[p] < 0 && lpos[p] < 0) A->h_nz_slot[p] = -(++A->n_gnz);
+  A->long_off = A->slots + A->n_gnz;
+  for (int64_t p = 0; p < csc_nnz; ++p)
+    if (lpos[p] >= 0) A->h_nz_slot[p] = -(A->n_gnz + lpos[p] + 1);
+  hval.resize(nvals(A) * S);
+  for (int64_t p = 0; p < csc_nnz; ++p)
+    if (A->h_nz_slot[p] < 0 && lpos[p] < 0)
+      std::memcpy(&hval[(A->slots - A->h_nz_slot[p] - 1) * S], (const unsigned char*)nzval + p * S, S);
+  if (A->n_lnz) std::memcpy(&hval[A->long_off * S], lval.data(), A->n_lnz * S);
   if (dev_upload(&A->d_col, hcol)) { pa_mat_destroy(A); return -1; }
-  if (A->slots + A->n_gnz) {
-    HIPC(hipMalloc(&A->d_val, (A->slots + A->n_gnz) * S));
-    HIPC(hipMemcpy(A->d_val, hval.data(), (A->slots + A->n_gnz) * S, hipMemcpyHostToDevice));
+  if (nvals(A)) {
+    HIPC(hipMalloc(&A->d_val, nvals(A) * S));
+    HIPC(hipMemcpy(A->d_val, hval.data(), nvals(A) * S, hipMemcpyHostToDevice));
   }
+  if (upload_long(A, lrows, lptr, lcol)) { pa_mat_destroy(A); return -1; }
   // pattern slices need "x lid >= noids ⇔ ghost column" (contiguous layout)
   if (cols->own_contig && cols->ghost_contig) {
     int kmax = 0;
@@ -1100,6 +1187,35 @@ int pa_mat_from_coo(pa_ctx* c, int dtype, int index_bytes, int ids_global, int64
   tmp.add(key2); tmp.add(idx2); tmp.add(rowptr); tmp.add(gflag); tmp.add(grank); tmp.add(slen_d); tmp.add(sghost_d);
   A->nnz = nnz;
   const int64_t ns = (A->nrows + A->H - 1) / A->H;
+  // row-length histogram → long rows (they leave the SELL, see long_threshold)
+  std::vector<int32_t> lrows;
+  std::vector<int64_t> lptr{0};
+  int32_t *lidx_d = nullptr, *lcol_d = nullptr;
+  int64_t* lptr_d = nullptr;
+  if (A->nrows > 0) {
+    std::vector<int64_t> rp(A->nrows + 1);
+    HIPC(hipMemcpy(rp.data(), rowptr, (A->nrows + 1) * 8, hipMemcpyDeviceToHost));
+    std::vector<int32_t> len(A->nrows);
+    for (int64_t r = 0; r < A->nrows; ++r) len[r] = (int32_t)(rp[r + 1] - rp[r]);
+    const int32_t thr = long_threshold(len);
+    std::vector<int32_t> lidx(A->nrows, -1);
+    for (int64_t r = 0; r < A->nrows; ++r)
+      if (len[r] > thr) {
+        lidx[r] = (int32_t)lrows.size();
+        lrows.push_back((int32_t)r);
+        lptr.push_back(lptr.back() + len[r]);
+      }
+    if (!lrows.empty()) {
+      if (dev_upload(&lidx_d, lidx) || dev_upload(&lptr_d, lptr)) return -1;
+      tmp.add(lidx_d);
+      tmp.add(lptr_d);
+      HIPC(hipMalloc((void**)&lcol_d, lptr.back() * 4));
+    }
+  }
+  A->n_lnz = lptr.back();
+  coo_slices(ns, A->nrows, A->H, rowptr, key2, ncols_lids, cols->noids, lidx_d, slen_d, sghost_d, st);
+  HIPC(hipGetLastError());
+  HIPC(hipStreamSynchronize(st));  // the copies below run on the null stream
   std::vector<int32_t> slen(ns), sg(ns);
   std::vector<char> sghost(ns);
   if (ns > 0) {
@@ -1112,18 +1228,21 @@ int pa_mat_from_coo(pa_ctx* c, int dtype, int index_bytes, int ids_global, int64
     HIPC(hipMalloc((void**)&A->d_col, A->slots * 4));
     launch_fill_i32(A->slots, A->d_col, -1, st);
   }
-  if (A->slots + ngh > 0) {
-    HIPC(hipMalloc(&A->d_val, (A->slots + ngh) * S));
-    HIPC(hipMemsetAsync(A->d_val, 0, (A->slots + ngh) * S, st));
+  A->n_gnz = ngh;
+  A->long_off = A->slots + ngh;
+  if (nvals(A) > 0) {
+    HIPC(hipMalloc(&A->d_val, nvals(A) * S));
+    HIPC(hipMemsetAsync(A->d_val, 0, nvals(A) * S, st));
   }
   if (nu > 0) {
     HIPC(hipMalloc((void**)&nzs, nu * 8));
     tmp.add(nzs);
   }
   coo_fill(dtype, nnz, nu, key2, idx2, rowptr, A->d_slice_off, A->H, A->R, ncols_lids, ccol, cval, gflag, grank,
-           A->slots, A->d_col, A->d_val, nzs, st);
+           A->slots, A->d_col, A->d_val, nzs, lidx_d, lptr_d, lcol_d, A->long_off, st);
   HIPC(hipGetLastError());
-  A->n_gnz = ngh;
+  if (upload_long(A, lrows, lptr, {})) { pa_mat_destroy(A); return -1; }
+  A->d_long_col = lcol_d;
   A->h_nz_slot.resize(nu);
   if (nu > 0) {
     HIPC(hipMemcpyAsync(A->h_nz_slot.data(), nzs, nu * 8, hipMemcpyDeviceToHost, st));
@@ -1158,7 +1277,7 @@ int pa_mat_set_values(pa_mat* A, const void* nzval) {
   CHECK_ARG((int64_t)A->h_nz_slot.size() == A->csc_nnz, "matrix was not built from a CSC pattern");
   HIPC(hipSetDevice(A->ctx->device));
   const size_t S = dtype_size(A->dtype);
-  const int64_t nv = A->slots + A->n_gnz;
+  const int64_t nv = nvals(A);
   std::vector<unsigned char> hval(nv * S, 0);
   for (int64_t p = 0; p < A->csc_nnz; ++p)
     std::memcpy(&hval[nz_index(A, p) * S], (const unsigned char*)nzval + p * S, S);
@@ -1174,7 +1293,7 @@ int pa_mat_get_values(const pa_mat* A, void* nzval) {
   CHECK_ARG((int64_t)A->h_nz_slot.size() == A->csc_nnz, "matrix was not built from a CSC pattern");
   HIPC(hipSetDevice(A->ctx->device));
   const size_t S = dtype_size(A->dtype);
-  const int64_t nv = A->slots + A->n_gnz;
+  const int64_t nv = nvals(A);
   std::vector<unsigned char> hval(nv * S, 0);
   HIPC(hipStreamSynchronize(A->ctx->s_comm));
   HIPC(hipStreamSynchronize(A->ctx->s_main));
@@ -1191,7 +1310,7 @@ int pa_mat_xchg_create(pa_mat* A, int32_t n_rcv, const int32_t* parts_rcv, const
                        const int64_t* k_snd, pa_xchg** out) {
   CHECK_ARG(A && out, "null argument");
   CHECK_ARG((int64_t)A->h_nz_slot.size() == A->csc_nnz, "matrix was not built from a CSC pattern");
-  CHECK_ARG(A->slots + A->n_gnz < ((int64_t)1 << 31), "matrix exchanger: value index exceeds int32");
+  CHECK_ARG(nvals(A) < ((int64_t)1 << 31), "matrix exchanger: value index exceeds int32");
   CHECK_ARG(n_rcv >= 0 && n_snd >= 0, "negative neighbour count");
   auto conv = [&](int32_t n, const int32_t* ptrs, const int64_t* k, std::vector<int32_t>& o) -> int {
     const int64_t m = n > 0 ? (int64_t)ptrs[n] - 1 : 0;
@@ -1220,7 +1339,7 @@ int pa_mat_exchange_all(int n, pa_mat* const A[], pa_xchg* const xg[], int op, i
     CHECK_ARG(A[i] && xg[i] && A[i]->ctx == xg[i]->ctx, "exchange!(A): matrix and exchanger of different parts");
     vs[i].ctx = A[i]->ctx;
     vs[i].dtype = A[i]->dtype;
-    vs[i].n = A[i]->slots + A[i]->n_gnz;
+    vs[i].n = nvals(A[i]);
     vs[i].d = A[i]->d_val;
     vp[i] = &vs[i];
   }
@@ -1252,7 +1371,9 @@ int pa_mat_destroy(pa_mat* A) {
   for (void* p : {(void*)A->d_kind, (void*)A->d_plen, (void*)A->d_pat, (void*)A->d_mask,
                   (void*)A->d_pint_list, (void*)A->d_pbnd_list, (void*)A->d_xint_list,
                   (void*)A->d_xbnd_list, (void*)A->d_s_off, (void*)A->d_s_len,
-                  (void*)A->d_s_col, A->d_s_val, (void*)A->d_s_rowmap, (void*)A->d_s_rowlen, A->d_dotp})
+                  (void*)A->d_s_col, A->d_s_val, (void*)A->d_s_rowmap, (void*)A->d_s_rowlen, A->d_dotp,
+                  (void*)A->d_long_row, (void*)A->d_long_ptr, (void*)A->d_long_col, (void*)A->d_sflags,
+                  (void*)A->d_lmask, (void*)A->d_lchunk_start, (void*)A->d_lrow_chunk, A->d_lpart})
     dev_free(p);
   delete A;
   return 0;
@@ -1265,6 +1386,13 @@ int pa_mat_format_info(const pa_mat* A, int64_t* pattern_slices, int64_t* regula
   if (regular_rows) *regular_rows = A->nregular_rows;
   if (side_rows) *side_rows = A->s_nrows;
   if (side_slots) *side_slots = A->s_slots;
+  return 0;
+}
+
+int pa_mat_long_rows(const pa_mat* A, int64_t* n_long, int64_t* n_long_nnz) {
+  CHECK_ARG(A, "null matrix");
+  if (n_long) *n_long = A->n_long;
+  if (n_long_nnz) *n_long_nnz = A->n_lnz;
   return 0;
 }
 
@@ -1295,7 +1423,7 @@ static int spmv_impl(int n, pa_mat* const A[], pa_vec* const y[], const pa_index
       CHECK_ARG(x_idx && x_idx[i] && x_idx[i]->own_contig, "fused dot needs b with contiguous owned lids");
       if (!A[i]->d_dotp) {
         HIPC(hipSetDevice(A[i]->ctx->device));
-        HIPC(hipMalloc(&A[i]->d_dotp, std::max<int64_t>(A[i]->nslices + A[i]->s_nslices, 1) * 16));
+        HIPC(hipMalloc(&A[i]->d_dotp, std::max<int64_t>(A[i]->nslices + A[i]->s_nslices + A[i]->n_long, 1) * 16));
       }
       dotp[i] = A[i]->d_dotp;
     }
@@ -1369,10 +1497,13 @@ static int spmv_impl(int n, pa_mat* const A[], pa_vec* const y[], const pa_index
       launch_spmv_part(1, A[i]->nslices - A[i]->nslices_int, A[i]->d_bnd_list, A[i], x[i]->d, y[i]->d, ymap,
                        has_alpha, bmode, alpha, beta, dotp[i], c->s_main);
     }
-    if (want_dot) {  // fold the slice partials (main, then side in pattern mode) in order
-      const bool pat = g_spmv_format == 1 && A[i]->has_pat;
+    // long rows (after the halo: they may read ghost columns)
+    const bool pat = g_spmv_format == 1 && A[i]->has_pat;
+    const int64_t long_base = A[i]->nslices + (pat ? A[i]->s_nslices : 0);
+    launch_spmv_long(A[i], x[i]->d, y[i]->d, ymap, has_alpha, bmode, alpha, beta, dotp[i], long_base, c->s_main);
+    if (want_dot) {  // fold the partials (main slices, side slices, long rows) in order
       const bool cplx = dt == PA_C64 || dt == PA_C128;
-      launch_fold(cplx, (int)(A[i]->nslices + (pat ? A[i]->s_nslices : 0)), A[i]->d_dotp, c->d_fold, c->d_result, c->s_main);
+      launch_fold(cplx, (int)(long_base + A[i]->n_long), A[i]->d_dotp, c->d_fold, c->d_result, c->s_main);
     }
     if (c->timing) HIPC(hipEventRecord(c->ev_t[3], c->s_main));
   }

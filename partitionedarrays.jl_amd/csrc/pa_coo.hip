@@ -111,11 +111,13 @@ __global__ void k_rowptr(int64_t nrows, int64_t nnz, const uint64_t* __restrict_
 // last entry, ghost columns sorting after owned ones)
 __global__ void k_slice_len(int64_t ns, int64_t nrows, int H, const int64_t* __restrict__ rowptr,
                             const uint64_t* __restrict__ key2, int64_t ncols, int64_t noids_c,
-                            int32_t* __restrict__ slen, int32_t* __restrict__ sghost) {
+                            const int32_t* __restrict__ lidx, int32_t* __restrict__ slen,
+                            int32_t* __restrict__ sghost) {
   for (int64_t s = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; s < ns; s += (int64_t)gridDim.x * blockDim.x) {
     const int64_t r0 = s * H, r1 = (r0 + H < nrows) ? r0 + H : nrows;
     int32_t L = 0, g = 0;
     for (int64_t r = r0; r < r1; ++r) {
+      if (lidx && lidx[r] >= 0) continue;  // long rows leave the SELL
       const int64_t a = rowptr[r], b = rowptr[r + 1];
       if (b - a > L) L = (int32_t)(b - a);
       if (b > a && (int64_t)(key2[b - 1] % (uint64_t)ncols) >= noids_c) g = 1;
@@ -125,14 +127,26 @@ __global__ void k_slice_len(int64_t ns, int64_t nrows, int H, const int64_t* __r
   }
 }
 
+// lidx[r] >= 0: long row r, its entries go to the long CSR at lptr[lidx[r]]
+// (values at val[long_off + ..], nz_slot = -(ngh + pos + 1))
 template <typename T>
 __global__ void k_fill_slots(int64_t nnz, const uint64_t* __restrict__ key2, const int64_t* __restrict__ idx2,
                              const int64_t* __restrict__ rowptr, const int64_t* __restrict__ soff, int H, int R,
                              int64_t ncols, const int32_t* __restrict__ ccol, const T* __restrict__ cval,
-                             int32_t* __restrict__ col, T* __restrict__ val, int64_t* __restrict__ nz_slot) {
+                             int32_t* __restrict__ col, T* __restrict__ val, int64_t* __restrict__ nz_slot,
+                             const int32_t* __restrict__ lidx, const int64_t* __restrict__ lptr,
+                             int32_t* __restrict__ lcol, int64_t long_off, int64_t ngh) {
   for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < nnz; t += (int64_t)gridDim.x * blockDim.x) {
     const int64_t r = (int64_t)(key2[t] / (uint64_t)ncols);
     const int64_t k = t - rowptr[r];
+    if (lidx && lidx[r] >= 0) {
+      const int64_t pos = lptr[lidx[r]] + k;
+      const int64_t p = idx2[t];
+      lcol[pos] = ccol[p];
+      val[long_off + pos] = cval[p];
+      nz_slot[p] = -(ngh + pos + 1);
+      continue;
+    }
     const int64_t s = r / H, w = r - s * H;
     const int64_t slot = soff[s] + (k * 64 + w / R) * R + (w % R);
     const int64_t p = idx2[t];
@@ -340,9 +354,6 @@ int coo_row_order(int64_t nu, const int32_t* crow, const int32_t* ccol, const in
     PA_HIP_TRY(sort_pairs(*key2, *idx2, nu, ngh ? 64 : bits_for(maxk), st));
   }
   hipLaunchKernelGGL(k_rowptr, grid1(nrows + 1), dim3(256), 0, st, nrows, nnz, *key2, ncols, *rowptr);
-  if (ns > 0)
-    hipLaunchKernelGGL(k_slice_len, grid1(ns), dim3(256), 0, st, ns, nrows, H, *rowptr, *key2, ncols, noids_c, *slen,
-                       *sghost);
   PA_HIP_TRY(hipGetLastError());
   PA_HIP_TRY(hipStreamSynchronize(st));
 done:
@@ -360,14 +371,23 @@ done:
 
 // Phase B, second half: scatter into the SELL slots (col pre-filled with -1,
 // val zeroed by the caller) and the ghost-row values after them.
+// per-slice max row length and ghost flag of the SELL rows (long rows skipped)
+void coo_slices(int64_t ns, int64_t nrows, int H, const int64_t* rowptr, const uint64_t* key2, int64_t ncols,
+                int64_t noids_c, const int32_t* lidx, int32_t* slen, int32_t* sghost, hipStream_t st) {
+  if (ns > 0)
+    hipLaunchKernelGGL(k_slice_len, grid1(ns), dim3(256), 0, st, ns, nrows, H, rowptr, key2, ncols, noids_c, lidx,
+                       slen, sghost);
+}
+
 void coo_fill(int dtype, int64_t nnz, int64_t nu, const uint64_t* key2, const int64_t* idx2, const int64_t* rowptr,
               const int64_t* soff, int H, int R, int64_t ncols, const int32_t* ccol, const void* cval,
               const int64_t* gflag, const int64_t* grank, int64_t slots, int32_t* col, void* val, int64_t* nz_slot,
-              hipStream_t st) {
+              const int32_t* lidx, const int64_t* lptr, int32_t* lcol, int64_t long_off, hipStream_t st) {
+  const int64_t ngh = long_off - slots;
 #define PA_FILL(T)                                                                                             \
   if (nnz > 0)                                                                                                 \
     hipLaunchKernelGGL(k_fill_slots<T>, grid1(nnz), dim3(256), 0, st, nnz, key2, idx2, rowptr, soff, H, R,     \
-                       ncols, ccol, (const T*)cval, col, (T*)val, nz_slot);                                     \
+                       ncols, ccol, (const T*)cval, col, (T*)val, nz_slot, lidx, lptr, lcol, long_off, ngh);   \
   if (nu > 0)                                                                                                  \
     hipLaunchKernelGGL(k_fill_ghost<T>, grid1(nu), dim3(256), 0, st, nu, gflag, grank, (const T*)cval, slots, \
                        (T*)val, nz_slot);

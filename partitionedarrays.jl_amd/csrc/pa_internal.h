@@ -209,6 +209,22 @@ struct pa_mat {
   std::vector<int64_t> h_nz_slot;
   int64_t csc_nnz = 0;
   int64_t n_gnz = 0;
+  // long rows (row-length histogram): their own CSR, values in d_val at
+  // long_off = slots + n_gnz; CSC nz of a long row: h_nz_slot = -(n_gnz+t+1)
+  int64_t n_long = 0, n_lnz = 0, long_off = 0;
+  int32_t* d_long_row = nullptr;     // oids, ascending
+  int64_t* d_long_ptr = nullptr;     // n_long+1
+  int32_t* d_long_col = nullptr;     // x lids, reference order per row
+  int32_t* d_sflags = nullptr;       // per slice: 1 if it holds long rows (int32 path skips them)
+  uint64_t* d_lmask = nullptr;       // nslices*(H/64) bits: long rows
+  std::vector<int32_t> h_long_rows;  // sorted oids (excluded from the side SELL)
+  // chunks of the long rows (long_rows_exact = 0): chunk c covers long-CSR
+  // entries [lchunk_start[c], lchunk_start[c+1]); row i owns chunks
+  // [lrow_chunk[i], lrow_chunk[i+1]); one partial per chunk in d_lpart
+  int64_t n_lchunks = 0;
+  int64_t* d_lchunk_start = nullptr;
+  int64_t* d_lrow_chunk = nullptr;
+  void* d_lpart = nullptr;
 
   // Pattern slices (implied columns): in a pattern slice the
   // rows whose column sequence is `row + pat[k]` (k < plen) are "regular"

@@ -88,6 +88,10 @@ struct SpmvArgs {
   const T* dotu;
   void* dotp;
   int64_t dot_base;
+  // long rows (k_spmv_long) inside int32-column slices: slices with
+  // sflags[s] != 0 skip the rows whose lmask bit is set (null: none)
+  const int32_t* sflags;
+  const uint64_t* lmask;
 };
 
 template <typename T> struct DAcc { using type = double; };
@@ -250,6 +254,11 @@ __global__ __launch_bounds__(256) void k_spmv_sell(SpmvArgs<T> a) {
   } else {
 #pragma unroll
     for (int r = 0; r < R; ++r) ok[r] = row0 + r < a.nrows;
+    if (a.sflags && a.sflags[s]) {  // rows handed to the long-row kernel
+      const uint64_t m = a.lmask[s * (H / 64) + (lane * R) / 64];
+#pragma unroll
+      for (int r = 0; r < R; ++r) ok[r] = ok[r] && !((m >> ((lane * R + r) & 63)) & 1ull);
+    }
   }
   int64_t orow[R];
 #pragma unroll
@@ -371,8 +380,202 @@ static void launch_which(int which, int64_t nwork, const int32_t* list, const pa
       a.slen = A->d_slice_len;
     }
   }
+  if (which == 1) {
+    a.sflags = A->d_sflags;
+    a.lmask = A->d_lmask;
+  }
   if (which == 0) launch_ab<T, R, true>(a, has_alpha, bmode, st);
   else launch_ab<T, R, false>(a, has_alpha, bmode, st);
+}
+
+// ---------------------------------------------------------------------------
+// Long rows (row-length histogram): rows far longer than the
+// rest leave the SELL (whose slices would pad every row to their length)
+// and run one wave per row over their own CSR, entries in the reference's
+// order.  EXACT: the wave adds the 64 products of each chunk one after the
+// other (readlane), so the row is summed exactly as SparseUtils.jl:176-185
+// sums it; otherwise each lane keeps a strided partial sum and the wave
+// folds them in a fixed tree (deterministic, within 1e-12 of the reference).
+
+template <typename T> struct LaneOf;
+template <> struct LaneOf<float> { static __device__ float get(float v, int j) { return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), j)); } };
+template <> struct LaneOf<double> {
+  static __device__ double get(double v, int j) {
+    const long long b = __builtin_bit_cast(long long, v);
+    const int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffffll), j);
+    const int hi = __builtin_amdgcn_readlane((int)(b >> 32), j);
+    return __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned int)lo);
+  }
+};
+template <> struct LaneOf<c64> { static __device__ c64 get(c64 v, int j) { return c64{LaneOf<float>::get(v.re, j), LaneOf<float>::get(v.im, j)}; } };
+template <> struct LaneOf<c128> { static __device__ c128 get(c128 v, int j) { return c128{LaneOf<double>::get(v.re, j), LaneOf<double>::get(v.im, j)}; } };
+
+__device__ inline float shfl_xor_t(float v, int m) { return __shfl_xor(v, m, 64); }
+__device__ inline double shfl_xor_t(double v, int m) { return __shfl_xor(v, m, 64); }
+__device__ inline c64 shfl_xor_t(c64 v, int m) { return c64{__shfl_xor(v.re, m, 64), __shfl_xor(v.im, m, 64)}; }
+__device__ inline c128 shfl_xor_t(c128 v, int m) { return c128{__shfl_xor(v.re, m, 64), __shfl_xor(v.im, m, 64)}; }
+
+// EXACT: one wave (one 64-thread block) per long row.  The wave computes
+// the products of 512 entries at a time (8 per lane, the next 512 loading
+// while the current ones are summed), stages them in LDS and every lane adds
+// them one after the other: the reference's summation chain.
+template <typename T, bool ALPHA, int BMODE>
+__global__ __launch_bounds__(64) void k_spmv_long_exact(int64_t nlong, const int32_t* __restrict__ lrow,
+                                                        const int64_t* __restrict__ lptr,
+                                                        const int32_t* __restrict__ lcol, const T* __restrict__ lval,
+                                                        const T* __restrict__ x, T* __restrict__ y,
+                                                        const int32_t* __restrict__ ymap, T alpha, T beta,
+                                                        const T* __restrict__ dotu, void* dotp, int64_t dot_base) {
+  constexpr int U = 8, B = U * 64;
+  __shared__ T buf[B];
+  const int lane = threadIdx.x;
+  const int64_t w = blockIdx.x;
+  if (w >= nlong) return;
+  const int64_t r = lrow[w];
+  const int64_t yl = ymap ? (int64_t)ymap[r] : r;
+  T acc;
+  if (BMODE == 0) acc = zero_of<T>();
+  else acc = (BMODE == 2) ? y[yl] * beta : y[yl];
+  const int64_t b0 = lptr[w], b1 = lptr[w + 1];
+  T p[U];
+  auto load = [&](int64_t b) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t k = b + u * 64 + lane;
+      T q = zero_of<T>();
+      if (k < b1) {
+        T xx = x[lcol[k]];
+        if (ALPHA) xx = xx * alpha;
+        q = lval[k] * xx;
+      }
+      p[u] = q;
+    }
+  };
+  if (b0 < b1) load(b0);
+  for (int64_t b = b0; b < b1; b += B) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) buf[u * 64 + lane] = p[u];
+    __syncthreads();
+    if (b + B < b1) load(b + B);  // in flight while the chain below runs
+    const int cnt = (int)((b1 - b) < B ? (b1 - b) : B);
+    int t = 0;
+    for (; t + 16 <= cnt; t += 16) {  // reads ahead of the dependent adds
+      T v[16];
+#pragma unroll
+      for (int i = 0; i < 16; ++i) v[i] = buf[t + i];
+#pragma unroll
+      for (int i = 0; i < 16; ++i) acc = acc + v[i];
+    }
+    for (; t < cnt; ++t) acc = acc + buf[t];
+    __syncthreads();
+  }
+  if (lane == 0) {
+    y[yl] = acc;
+    if (dotp) {
+      using DA = typename DAcc<T>::type;
+      reinterpret_cast<DA*>(dotp)[dot_base + w] = dacc(cdot(dotu[r], acc));
+    }
+  }
+}
+
+// Fast (long_rows_exact = 0): the long rows are cut into chunks of
+// kLongChunk entries, one wave per chunk (lane-strided partial sums, then a
+// fixed xor tree); k_spmv_long_fold adds each row's chunk partials in chunk
+// order after the β-init.  Deterministic, within 1e-12 of the reference.
+template <typename T, bool ALPHA>
+__global__ __launch_bounds__(256) void k_spmv_long_chunks(int64_t nchunks, const int64_t* __restrict__ cstart,
+                                                          const int64_t* __restrict__ cend,
+                                                          const int32_t* __restrict__ lcol,
+                                                          const T* __restrict__ lval, const T* __restrict__ x,
+                                                          T alpha, T* __restrict__ part) {
+  constexpr int U = 8;
+  const int lane = threadIdx.x & 63;
+  const int64_t c = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (c >= nchunks) return;
+  const int64_t b1 = cend[c];
+  T s = zero_of<T>();
+  for (int64_t b = cstart[c]; b < b1; b += U * 64) {
+    T q[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t k = b + u * 64 + lane;
+      q[u] = zero_of<T>();
+      if (k < b1) {
+        T xx = x[lcol[k]];
+        if (ALPHA) xx = xx * alpha;
+        q[u] = lval[k] * xx;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) s = s + q[u];
+  }
+#pragma unroll
+  for (int m = 1; m < 64; m <<= 1) s = s + shfl_xor_t(s, m);
+  if (lane == 0) part[c] = s;
+}
+
+template <typename T, int BMODE>
+__global__ void k_spmv_long_fold(int64_t nlong, const int32_t* __restrict__ lrow, const int64_t* __restrict__ cptr,
+                                 const T* __restrict__ part, T* __restrict__ y, const int32_t* __restrict__ ymap,
+                                 T beta, const T* __restrict__ dotu, void* dotp, int64_t dot_base) {
+  const int64_t w = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (w >= nlong) return;
+  const int64_t r = lrow[w];
+  const int64_t yl = ymap ? (int64_t)ymap[r] : r;
+  T acc;
+  if (BMODE == 0) acc = zero_of<T>();
+  else acc = (BMODE == 2) ? y[yl] * beta : y[yl];
+  for (int64_t c = cptr[w]; c < cptr[w + 1]; ++c) acc = acc + part[c];
+  y[yl] = acc;
+  if (dotp) {
+    using DA = typename DAcc<T>::type;
+    reinterpret_cast<DA*>(dotp)[dot_base + w] = dacc(cdot(dotu[r], acc));
+  }
+}
+
+int g_long_exact = 1;  // pa_tune("long_rows_exact")
+
+template <typename T, bool ALPHA, int BMODE>
+static void long_t(const pa_mat* A, const void* x, void* y, const int32_t* ymap, const void* alpha, const void* beta,
+                   void* dotp, int64_t dot_base, hipStream_t st) {
+  const T* val = (const T*)A->d_val + A->long_off;
+  const T al = *(const T*)alpha, be = *(const T*)beta;
+  if (g_long_exact) {
+    hipLaunchKernelGGL((k_spmv_long_exact<T, ALPHA, BMODE>), dim3((unsigned)A->n_long), dim3(64), 0, st, A->n_long,
+                       A->d_long_row, A->d_long_ptr, A->d_long_col, val, (const T*)x, (T*)y, ymap, al, be,
+                       (const T*)x, dotp, dot_base);
+  } else {
+    hipLaunchKernelGGL((k_spmv_long_chunks<T, ALPHA>), dim3((unsigned)((A->n_lchunks + 3) / 4)), dim3(256), 0, st,
+                       A->n_lchunks, A->d_lchunk_start, A->d_lchunk_start + 1, A->d_long_col, val, (const T*)x, al,
+                       (T*)A->d_lpart);
+    hipLaunchKernelGGL((k_spmv_long_fold<T, BMODE>), dim3((unsigned)((A->n_long + 63) / 64)), dim3(64), 0, st,
+                       A->n_long, A->d_long_row, A->d_lrow_chunk, (const T*)A->d_lpart, (T*)y, ymap, be,
+                       (const T*)x, dotp, dot_base);
+  }
+}
+
+template <typename T>
+static void long_ab(const pa_mat* A, const void* x, void* y, const int32_t* ymap, bool has_alpha, int bmode,
+                    const void* alpha, const void* beta, void* dotp, int64_t dot_base, hipStream_t st) {
+#define PA_L(AL, BM) long_t<T, AL, BM>(A, x, y, ymap, alpha, beta, dotp, dot_base, st)
+  if (!has_alpha) {
+    if (bmode == 0) PA_L(false, 0); else if (bmode == 1) PA_L(false, 1); else PA_L(false, 2);
+  } else {
+    if (bmode == 0) PA_L(true, 0); else if (bmode == 1) PA_L(true, 1); else PA_L(true, 2);
+  }
+#undef PA_L
+}
+
+// dotp: partial of long row w at dotp[dot_base + w] (the fused CG dot)
+void launch_spmv_long(const pa_mat* A, const void* x, void* y, const int32_t* ymap, bool has_alpha, int bmode,
+                      const void* alpha, const void* beta, void* dotp, int64_t dot_base, hipStream_t st) {
+  if (A->n_long <= 0) return;
+  switch (A->dtype) {
+    case PA_F32: long_ab<float>(A, x, y, ymap, has_alpha, bmode, alpha, beta, dotp, dot_base, st); break;
+    case PA_F64: long_ab<double>(A, x, y, ymap, has_alpha, bmode, alpha, beta, dotp, dot_base, st); break;
+    case PA_C64: long_ab<c64>(A, x, y, ymap, has_alpha, bmode, alpha, beta, dotp, dot_base, st); break;
+    case PA_C128: long_ab<c128>(A, x, y, ymap, has_alpha, bmode, alpha, beta, dotp, dot_base, st); break;
+  }
 }
 
 void launch_spmv_part(int which, int64_t nwork, const int32_t* list, const pa_mat* A, const void* x,

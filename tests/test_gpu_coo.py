@@ -171,3 +171,119 @@ def test_device_to_lids_unknown_gid(be, pamd):
     with pytest.raises(pamd.PAError, match="KeyError"):
         pamd.DeviceMatrix.from_coo(ctx, I, I, np.ones(3), pamd.device.device_index_gids(ctx, s),
                                    pamd.device.device_index_gids(ctx, s), 10, 10, ids_global=True)
+
+
+def _long_row_coo(rng, part, p, dtype, long_lens):
+    """owned rows with ~9 entries, a few rows with long_lens entries (over all
+    local columns, ghosts included), in random order with duplicates."""
+    s = part.partition.local(p)
+    own = s.oid_to_lid
+    I, J = [], []
+    longs = rng.choice(own, size=min(len(long_lens), len(own)), replace=False)
+    for li in own:
+        k = 9
+        if li in longs:
+            k = long_lens[list(longs).index(li)]
+        I += [li] * k
+        J += list(rng.integers(1, s.num_lids + 1, size=k))
+    I, J = np.array(I), np.array(J)
+    o = rng.permutation(len(I))
+    V = rng.uniform(-1, 1, len(I))
+    if np.dtype(dtype).kind == "c":
+        V = V + 1j * rng.uniform(-1, 1, len(I))
+    return I[o], J[o], V[o].astype(dtype), sorted(int(v) for v in longs)
+
+
+def _ref_spmv(H, s, xl, yl, alpha, beta, dtype):
+    """SparseUtils.jl:157-187 on the host CSC: rmul!(c, β) (or fill!(c, 0)),
+    then the column loop over owned columns (oid order), then ghost columns."""
+    want = (yl * dtype(beta)) if beta != 0 else np.zeros_like(yl)
+    if beta == 1:
+        want = yl.copy()
+    l2o = np.zeros(s.num_lids, dtype=bool)
+    l2o[s.oid_to_lid - 1] = True
+    for j in list(s.oid_to_lid - 1) + list(s.hid_to_lid - 1):
+        axj = xl[j] * dtype(alpha) if alpha != 1 else xl[j]
+        for q in range(H.colptr[j] - 1, H.colptr[j + 1] - 1):
+            i = H.rowval[q] - 1
+            if l2o[i]:
+                want[i] = want[i] + H.nzval[q] * axj
+    return want
+
+
+@pytest.mark.parametrize("dtype", [np.float64, np.complex128, np.float32])
+@pytest.mark.parametrize("build", ["coo", "csc"])
+def test_long_rows_bitexact(be, pamd, dtype, build):
+    """Rows far longer than the rest (row-length histogram) run in the
+    long-row kernel: mul! with α/β, both column encodings, the halo, and
+    set_values all stay bit-exact against the reference's loop."""
+    parts = be.get_part_ids((2, 2, 1))
+    _, part = pamd.drivers.stencil_partition(parts, (20, 18, 16), 27)
+    rng = np.random.default_rng(23)
+    coo = {p: _long_row_coo(rng, part, p, dtype, [600, 1000, 4000, 70]) for p in parts.part_ids}
+    mk = lambda k: pamd.PData(parts.backend, parts.part_ids, [coo[p][k] for p in parts.part_ids], parts.shape)
+    if build == "coo":
+        A = pamd.PSparseMatrix.from_coo(mk(0), mk(1), mk(2), part, part, ids="local")
+    else:
+        csc = pamd.map_parts(lambda i, j, v, s: pamd.compresscoo(i, j, v, s.num_lids, s.num_lids),
+                             mk(0), mk(1), mk(2), part.partition)
+        A = pamd.PSparseMatrix.from_csc(csc, part, part)
+    for p in parts.part_ids:
+        assert A.values.local(p).info()["long_rows"] == 3  # 600, 1000, 4000 (less duplicates) > max(256, 8*p90)
+    xs = {p: (rng.uniform(-1, 1, part.partition.local(p).num_lids) + (1j * rng.uniform(-1, 1, part.partition.local(p).num_lids) if np.dtype(dtype).kind == "c" else 0)).astype(dtype) for p in parts.part_ids}
+    ys = {p: rng.uniform(-1, 1, part.partition.local(p).num_lids).astype(dtype) for p in parts.part_ids}
+    Hs = {p: pamd.compresscoo(*coo[p][:3], part.partition.local(p).num_lids, part.partition.local(p).num_lids)
+          for p in parts.part_ids}
+    x = pamd.PVector.from_host(pamd.map_parts(lambda s: xs[s.part], part.partition), part)
+    for fmt in (1, 0):
+        prev = pamd._lib.tune("spmv_format", fmt)
+        try:
+            for alpha, beta in ((1.0, 0.0), (2.5, 0.5), (1.0, 1.0)):
+                y = pamd.PVector.from_host(pamd.map_parts(lambda s: ys[s.part], part.partition), part)
+                pamd.mul_(y, A, x, alpha, beta)
+                xh = x.to_host()
+                for p in parts.part_ids:
+                    s = part.partition.local(p)
+                    want = _ref_spmv(Hs[p], s, xh.local(p), ys[p], alpha, beta, np.dtype(dtype).type)
+                    own = s.oid_to_lid - 1
+                    assert np.array_equal(y.to_host().local(p)[own], want[own]), (fmt, alpha, beta, p)
+        finally:
+            pamd._lib.tune("spmv_format", prev)
+    # new values into the same pattern (long-row values included)
+    for p in parts.part_ids:
+        M = A.values.local(p)
+        v2 = (M.get_values() * dtype(0.5)).astype(dtype)
+        M.set_values(v2)
+        assert np.array_equal(M.get_values(), v2)
+        Hs[p].nzval = v2
+    y = pamd.PVector.undef(part, dtype)
+    pamd.mul_(y, A, x)
+    for p in parts.part_ids:
+        s = part.partition.local(p)
+        want = _ref_spmv(Hs[p], s, x.to_host().local(p), np.zeros(s.num_lids, dtype), 1.0, 0.0, np.dtype(dtype).type)
+        own = s.oid_to_lid - 1
+        assert np.array_equal(y.to_host().local(p)[own], want[own])
+
+
+def test_long_rows_fast_mode_and_fused_dot(be, pamd):
+    """long_rows_exact = 0 (lane-strided tree) stays within 1e-12 of the
+    exact order; the fused SpMV+dot includes the long rows."""
+    parts = be.get_part_ids((2, 1, 1))
+    _, part = pamd.drivers.stencil_partition(parts, (20, 18, 16), 27)
+    rng = np.random.default_rng(5)
+    coo = {p: _long_row_coo(rng, part, p, np.float64, [5000, 2000]) for p in parts.part_ids}
+    mk = lambda k: pamd.PData(parts.backend, parts.part_ids, [coo[p][k] for p in parts.part_ids], parts.shape)
+    A = pamd.PSparseMatrix.from_coo(mk(0), mk(1), mk(2), part, part, ids="local")
+    x = pamd.PVector.from_host(pamd.map_parts(lambda s: rng.uniform(-1, 1, s.num_lids), part.partition), part)
+    y1, y2, y3 = (pamd.PVector.undef(part) for _ in range(3))
+    pamd.mul_(y1, A, x)
+    prev = pamd._lib.tune("long_rows_exact", 0)
+    try:
+        pamd.mul_(y2, A, x)
+    finally:
+        pamd._lib.tune("long_rows_exact", prev)
+    for p in parts.part_ids:
+        a, b = y1.to_host().local(p), y2.to_host().local(p)
+        assert np.allclose(a, b, rtol=1e-12, atol=1e-12 * np.abs(a).max())
+    d = pamd.mul_dot_(y3, A, x)
+    assert abs(d - pamd.dot(x, y1)) <= 1e-12 * abs(d)
