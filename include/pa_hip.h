@@ -40,6 +40,7 @@ typedef struct pa_index pa_index;
 typedef struct pa_xchg pa_xchg;
 typedef struct pa_vec pa_vec;
 typedef struct pa_mat pa_mat;
+typedef struct pa_graph pa_graph;
 
 /* ---- errors / library info ------------------------------------------- */
 const char* pa_last_error(void);
@@ -65,6 +66,10 @@ int pa_tune(const char* key, int value, int* previous);
  * Replaces the part slot of `get_part_ids(b::AbstractBackend, nparts)`
  * (Interfaces.jl:24) — part is 1-based, 1 <= part <= nparts.          */
 int pa_ctx_create(int device, int part, int nparts, pa_ctx** out);
+/* A context for another part on `with`'s device that shares its stream
+ * pair: several parts of one process on one GPU then form a single
+ * in-order chain (no cross-stream events between them).                 */
+int pa_ctx_create_shared(int part, int nparts, pa_ctx* with, pa_ctx** out);
 int pa_ctx_destroy(pa_ctx* ctx);
 int pa_ctx_sync(pa_ctx* ctx);
 
@@ -213,6 +218,19 @@ int pa_spmv_all(int n, pa_mat* const A[], pa_vec* const y[],
                 const pa_index* const y_idx[],
                 pa_vec* const x[], const pa_index* const x_idx[],
                 pa_xchg* const xg[], const void* alpha, const void* beta);
+
+/* The same mul! captured once as a HIP graph (every part of the call on one
+ * device, halo neighbours in this process) and replayed with one launch:
+ * for many small parts in one process, where host launch cost dominates.
+ * Replays use the handles and scalars given at capture; a replay is ordered
+ * after work already queued on the parts' streams and before later work.  */
+int pa_spmv_graph_create(int n, pa_mat* const A[], pa_vec* const y[],
+                         const pa_index* const y_idx[],
+                         pa_vec* const x[], const pa_index* const x_idx[],
+                         pa_xchg* const xg[], const void* alpha,
+                         const void* beta, pa_graph** out);
+int pa_graph_launch(pa_graph* g);
+int pa_graph_destroy(pa_graph* g);
 
 /* CG fusions (the caller of the hot path, IterativeSolvers.cg! at
  * test_fdm.jl:115 / test_fem_sa.jl:135):

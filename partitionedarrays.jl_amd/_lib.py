@@ -36,6 +36,7 @@ _SIGS = {
     "pa_device_count": [C.POINTER(C.c_int)],
     "pa_tune": [C.c_char_p, C.c_int, C.POINTER(C.c_int)],
     "pa_ctx_create": [C.c_int, C.c_int, C.c_int, C.POINTER(_p)],
+    "pa_ctx_create_shared": [C.c_int, C.c_int, _p, C.POINTER(_p)],
     "pa_ctx_destroy": [_p],
     "pa_ctx_sync": [_p],
     "pa_comm_unique_id": [C.c_char_p],
@@ -66,6 +67,10 @@ _SIGS = {
     "pa_mat_long_rows": [_p, _i64p, _i64p],
     "pa_mat_stencil": [_p, C.c_int, C.c_int, _i64p, _i64p, _i64p, C.c_int64, _i32p, C.POINTER(C.c_double), C.c_int, C.POINTER(_p)],
     "pa_spmv_all": [C.c_int, C.POINTER(_p), C.POINTER(_p), C.POINTER(_p), C.POINTER(_p), C.POINTER(_p), C.POINTER(_p), _p, _p],
+    "pa_spmv_graph_create": [C.c_int, C.POINTER(_p), C.POINTER(_p), C.POINTER(_p), C.POINTER(_p), C.POINTER(_p),
+                             C.POINTER(_p), _p, _p, C.POINTER(_p)],
+    "pa_graph_launch": [_p],
+    "pa_graph_destroy": [_p],
     "pa_spmv_dot_all": [C.c_int, C.POINTER(_p), C.POINTER(_p), C.POINTER(_p), C.POINTER(_p), C.POINTER(_p), C.POINTER(_p), _p, _p, _p],
     "pa_cg_update_all": [C.c_int, C.POINTER(_p), C.POINTER(_p), C.POINTER(_p), C.POINTER(_p), C.POINTER(_p), _p, C.POINTER(C.c_double)],
     "pa_cg_solve_all": [C.c_int, C.POINTER(_p), C.POINTER(_p), C.POINTER(_p), C.POINTER(_p), C.POINTER(_p),

@@ -7,6 +7,8 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <numeric>
 #include <string>
@@ -354,6 +356,13 @@ LocalSet local_set(int n, H* const* hs) {
   return L;
 }
 
+// During graph capture every part's work goes to one stream (a linear chain
+// of kernels; multi-stream captures with cross-stream events are not used).
+hipStream_t g_capture_stream = nullptr;
+inline hipStream_t SM(const pa_ctx* c) { return g_capture_stream ? g_capture_stream : c->s_main; }
+inline hipStream_t SC(const pa_ctx* c) { return g_capture_stream ? g_capture_stream : c->s_comm; }
+#define EV(expr) do { if (!g_capture_stream) HIPC(expr); } while (0)
+
 // Pull table of receiver i for direction dir (see pa_pull): built once per
 // set of local senders; ok = false when a sender's device is not reachable
 // by peer access (then the staging copies below are used).
@@ -446,11 +455,11 @@ int transport(int n, pa_xchg* const xg[], int dtype, int dir, int op, pa_vec* co
     pa_xchg* X = xg[i];
     pa_ctx* c = X->ctx;
     HIPC(hipSetDevice(c->device));
-    HIPC(hipStreamWaitEvent(c->s_comm, c->ev_packed, 0));
+    EV(hipStreamWaitEvent(SC(c), c->ev_packed, 0));
     const auto& prcv = dir == 0 ? X->parts_rcv : X->parts_snd;
     for (int32_t q : prcv) {
       const int j = L.find(q);
-      if (j >= 0) HIPC(hipStreamWaitEvent(c->s_comm, xg[j]->ctx->ev_packed, 0));
+      if (j >= 0) EV(hipStreamWaitEvent(SC(c), xg[j]->ctx->ev_packed, 0));
       else remote = true;
     }
     const auto& psnd = dir == 0 ? X->parts_snd : X->parts_rcv;
@@ -475,14 +484,14 @@ int transport(int n, pa_xchg* const xg[], int dtype, int dir, int op, pa_vec* co
         if (L.find(psnd[k]) >= 0) continue;
         const size_t cnt = (size_t)(osnd[k + 1] - osnd[k]) * S;
         if (cnt == 0) continue;  // the peer's matching segment is empty too (SequentialBackend.jl:187)
-        ncclResult_t r = ncclSend(bsnd + osnd[k] * S, cnt, ncclUint8, psnd[k] - 1, comm, c->s_comm);
+        ncclResult_t r = ncclSend(bsnd + osnd[k] * S, cnt, ncclUint8, psnd[k] - 1, comm, SC(c));
         if (r != ncclSuccess) { ncclGroupEnd(); PA_FAIL(std::string("ncclSend: ") + ncclGetErrorString(r)); }
       }
       for (size_t k = 0; k < prcv.size(); ++k) {
         if (L.find(prcv[k]) >= 0) continue;
         const size_t cnt = (size_t)(orcv[k + 1] - orcv[k]) * S;
         if (cnt == 0) continue;
-        ncclResult_t r = ncclRecv(brcv + orcv[k] * S, cnt, ncclUint8, prcv[k] - 1, comm, c->s_comm);
+        ncclResult_t r = ncclRecv(brcv + orcv[k] * S, cnt, ncclUint8, prcv[k] - 1, comm, SC(c));
         if (r != ncclSuccess) { ncclGroupEnd(); PA_FAIL(std::string("ncclRecv: ") + ncclGetErrorString(r)); }
       }
     }
@@ -496,10 +505,10 @@ int transport(int n, pa_xchg* const xg[], int dtype, int dir, int op, pa_vec* co
       const pa_pull& P = X->pull[dir];
       if (dir == 0)
         launch_pull(dtype, X->n_rcv_data, X->d_lids_rcv, X->plan_fwd, op, P.d_bid, P.d_elem,
-                    (const void* const*)P.d_bases, v[i]->d, c->s_comm);
+                    (const void* const*)P.d_bases, v[i]->d, SC(c));
       else
         launch_pull(dtype, X->n_snd_data, X->d_lids_snd, X->plan_rev, op, P.d_bid, P.d_elem,
-                    (const void* const*)P.d_bases, v[i]->d, c->s_comm);
+                    (const void* const*)P.d_bases, v[i]->d, SC(c));
     } else {
       // staging copies: receiver r, segment k from sender q (local), which
       // holds the matching segment at the position of r in its send list
@@ -520,10 +529,10 @@ int transport(int n, pa_xchg* const xg[], int dtype, int dir, int op, pa_vec* co
         const int64_t cnt = orcv[k + 1] - orcv[k];
         CHECK_ARG(cnt == qo[m + 1] - qo[m], "exchanger mismatch: segment lengths differ (SequentialBackend.jl:187)");
         if (cnt > 0)
-          HIPC(hipMemcpyAsync(brcv + orcv[k] * S, bq + qo[m] * S, (size_t)cnt * S, hipMemcpyDefault, c->s_comm));
+          HIPC(hipMemcpyAsync(brcv + orcv[k] * S, bq + qo[m] * S, (size_t)cnt * S, hipMemcpyDefault, SC(c)));
       }
     }
-    HIPC(hipEventRecord(c->ev_recvd, c->s_comm));
+    EV(hipEventRecord(c->ev_recvd, SC(c)));
   }
   HIPC(hipGetLastError());
   *unpacked = pull;
@@ -538,7 +547,10 @@ int check_lids(const pa_xchg* X, const pa_vec* v) {
 // Before packing into the send buffers again, wait for the copies that read
 // them in the previous exchange (local receivers record ev_recvd after their
 // copies; for RCCL sends the part's own ev_recvd covers them).
+bool g_capturing = false;  // inside pa_spmv_graph_create: one replay never overlaps the next
+
 int pre_pack_wait(int n, pa_xchg* const xg[]) {
+  if (g_capturing) return 0;
   LocalSet L = local_set(n, xg);
   for (int i = 0; i < n; ++i) {
     pa_ctx* c = xg[i]->ctx;
@@ -602,6 +614,18 @@ int pa_device_count(int* count) {
   return 0;
 }
 
+static int ctx_scratch(pa_ctx* c) {
+  HIPC(hipMalloc(&c->d_partials, 8192 * 16));  // block partials (reductions, CG update)
+  HIPC(hipMalloc(&c->d_fold, 256 * 16));
+  HIPC(hipMalloc(&c->d_result, 16));
+  HIPC(hipMalloc(&c->d_gather, (size_t)c->nparts * 16));
+  HIPC(hipHostMalloc(&c->h_pinned, std::max<size_t>((size_t)(c->nparts + 1) * 16, 256)));  // gathered partials / CG state
+  HIPC(hipEventCreateWithFlags(&c->ev_packed, hipEventDisableTiming));
+  HIPC(hipEventCreateWithFlags(&c->ev_recvd, hipEventDisableTiming));
+  for (auto& e : c->ev_t) HIPC(hipEventCreate(&e));
+  return 0;
+}
+
 int pa_ctx_create(int device, int part, int nparts, pa_ctx** out) {
   CHECK_ARG(out, "null out");
   CHECK_ARG(nparts >= 1 && part >= 1 && part <= nparts, "part must satisfy 1 <= part <= nparts");
@@ -635,14 +659,25 @@ int pa_ctx_create(int device, int part, int nparts, pa_ctx** out) {
     HIPC(hipStreamCreateWithFlags(&c->s_main, hipStreamNonBlocking));
     HIPC(hipStreamCreateWithPriority(&c->s_comm, hipStreamNonBlocking, greatest));
   }
-  HIPC(hipMalloc(&c->d_partials, 8192 * 16));  // block partials (reductions, CG update)
-  HIPC(hipMalloc(&c->d_fold, 256 * 16));
-  HIPC(hipMalloc(&c->d_result, 16));
-  HIPC(hipMalloc(&c->d_gather, (size_t)nparts * 16));
-  HIPC(hipHostMalloc(&c->h_pinned, std::max<size_t>((size_t)(nparts + 1) * 16, 256)));  // gathered partials / CG state
-  HIPC(hipEventCreateWithFlags(&c->ev_packed, hipEventDisableTiming));
-  HIPC(hipEventCreateWithFlags(&c->ev_recvd, hipEventDisableTiming));
-  for (auto& e : c->ev_t) HIPC(hipEventCreate(&e));
+  c->stream_refs = new pa_ctx::StreamRefs();
+  if (ctx_scratch(c)) return -1;
+  *out = c;
+  return 0;
+}
+
+int pa_ctx_create_shared(int part, int nparts, pa_ctx* with, pa_ctx** out) {
+  CHECK_ARG(out && with, "null argument");
+  CHECK_ARG(nparts == with->nparts && part >= 1 && part <= nparts, "part must satisfy 1 <= part <= nparts");
+  HIPC(hipSetDevice(with->device));
+  pa_ctx* c = new pa_ctx();
+  c->device = with->device;
+  c->part = part;
+  c->nparts = nparts;
+  c->s_main = with->s_main;
+  c->s_comm = with->s_comm;
+  c->stream_refs = with->stream_refs;
+  ++c->stream_refs->n;
+  if (ctx_scratch(c)) return -1;
   *out = c;
   return 0;
 }
@@ -661,8 +696,11 @@ int pa_ctx_destroy(pa_ctx* c) {
   (void)hipEventDestroy(c->ev_packed);
   (void)hipEventDestroy(c->ev_recvd);
   for (auto& e : c->ev_t) (void)hipEventDestroy(e);
-  (void)hipStreamDestroy(c->s_main);
-  (void)hipStreamDestroy(c->s_comm);
+  if (c->stream_refs && --c->stream_refs->n == 0) {
+    (void)hipStreamDestroy(c->s_main);
+    (void)hipStreamDestroy(c->s_comm);
+    delete c->stream_refs;
+  }
   delete c;
   return 0;
 }
@@ -1454,8 +1492,8 @@ static int spmv_impl(int n, pa_mat* const A[], pa_vec* const y[], const pa_index
     for (int i = 0; i < n; ++i) {
       pa_ctx* c = xg[i]->ctx;
       HIPC(hipSetDevice(c->device));
-      launch_pack(dt, xg[i]->n_snd_data, xg[i]->d_lids_snd, x[i]->d, xg[i]->d_buf_snd, c->s_main);
-      HIPC(hipEventRecord(c->ev_packed, c->s_main));
+      launch_pack(dt, xg[i]->n_snd_data, xg[i]->d_lids_snd, x[i]->d, xg[i]->d_buf_snd, SM(c));
+      EV(hipEventRecord(c->ev_packed, SM(c)));
     }
     if (transport(n, xg, dt, 0, PA_REPLACE, x, &pulled)) return -1;
   }
@@ -1463,49 +1501,49 @@ static int spmv_impl(int n, pa_mat* const A[], pa_vec* const y[], const pa_index
     pa_ctx* c = A[i]->ctx;
     HIPC(hipSetDevice(c->device));
     const int32_t* ymap = y_idx[i]->own_contig ? nullptr : y_idx[i]->d_oid_to_lid;
-    if (c->timing) HIPC(hipEventRecord(c->ev_t[0], c->s_main));
+    if (c->timing) EV(hipEventRecord(c->ev_t[0], SM(c)));
     // interior slices (no ghost column): overlap with the halo transport
     if (g_spmv_format == 1 && A[i]->has_pat) {
-      launch_spmv_part(0, A[i]->np_int, A[i]->d_pint_list, A[i], x[i]->d, y[i]->d, ymap, has_alpha, bmode, alpha, beta, dotp[i], c->s_main);
-      launch_spmv_part(1, A[i]->nx_int, A[i]->d_xint_list, A[i], x[i]->d, y[i]->d, ymap, has_alpha, bmode, alpha, beta, dotp[i], c->s_main);
+      launch_spmv_part(0, A[i]->np_int, A[i]->d_pint_list, A[i], x[i]->d, y[i]->d, ymap, has_alpha, bmode, alpha, beta, dotp[i], SM(c));
+      launch_spmv_part(1, A[i]->nx_int, A[i]->d_xint_list, A[i], x[i]->d, y[i]->d, ymap, has_alpha, bmode, alpha, beta, dotp[i], SM(c));
     } else if (A[i]->d_bnd_list) {  // split layout (the interior list may be empty)
       if (A[i]->nslices_int > 0)
-        launch_spmv_part(1, A[i]->nslices_int, A[i]->d_int_list, A[i], x[i]->d, y[i]->d, ymap, has_alpha, bmode, alpha, beta, dotp[i], c->s_main);
+        launch_spmv_part(1, A[i]->nslices_int, A[i]->d_int_list, A[i], x[i]->d, y[i]->d, ymap, has_alpha, bmode, alpha, beta, dotp[i], SM(c));
     } else {
-      launch_spmv_part(1, A[i]->nslices, nullptr, A[i], x[i]->d, y[i]->d, ymap, has_alpha, bmode, alpha, beta, dotp[i], c->s_main);
+      launch_spmv_part(1, A[i]->nslices, nullptr, A[i], x[i]->d, y[i]->d, ymap, has_alpha, bmode, alpha, beta, dotp[i], SM(c));
     }
-    if (c->timing) HIPC(hipEventRecord(c->ev_t[1], c->s_main));
+    if (c->timing) EV(hipEventRecord(c->ev_t[1], SM(c)));
   }
   HIPC(hipGetLastError());
   for (int i = 0; i < n; ++i) {
     pa_ctx* c = A[i]->ctx;
     HIPC(hipSetDevice(c->device));
     if (any_x) {
-      HIPC(hipStreamWaitEvent(c->s_main, c->ev_recvd, 0));
+      EV(hipStreamWaitEvent(SM(c), c->ev_recvd, 0));
       if (!pulled)
         launch_unpack(dt, xg[i]->n_rcv_data, xg[i]->d_lids_rcv, xg[i]->plan_fwd, PA_REPLACE,
-                      xg[i]->d_buf_rcv, x[i]->d, c->s_main);
+                      xg[i]->d_buf_rcv, x[i]->d, SM(c));
     }
-    if (c->timing) HIPC(hipEventRecord(c->ev_t[2], c->s_main));
+    if (c->timing) EV(hipEventRecord(c->ev_t[2], SM(c)));
     const int32_t* ymap = y_idx[i]->own_contig ? nullptr : y_idx[i]->d_oid_to_lid;
     if (g_spmv_format == 1 && A[i]->has_pat) {
       // pattern slices reading ghosts, then the side rows (after the halo)
-      launch_spmv_part(0, A[i]->np_bnd, A[i]->d_pbnd_list, A[i], x[i]->d, y[i]->d, ymap, has_alpha, bmode, alpha, beta, dotp[i], c->s_main);
-      launch_spmv_part(1, A[i]->nx_bnd, A[i]->d_xbnd_list, A[i], x[i]->d, y[i]->d, ymap, has_alpha, bmode, alpha, beta, dotp[i], c->s_main);
-      launch_spmv_part(2, A[i]->s_nslices, nullptr, A[i], x[i]->d, y[i]->d, ymap, has_alpha, bmode, alpha, beta, dotp[i], c->s_main);
+      launch_spmv_part(0, A[i]->np_bnd, A[i]->d_pbnd_list, A[i], x[i]->d, y[i]->d, ymap, has_alpha, bmode, alpha, beta, dotp[i], SM(c));
+      launch_spmv_part(1, A[i]->nx_bnd, A[i]->d_xbnd_list, A[i], x[i]->d, y[i]->d, ymap, has_alpha, bmode, alpha, beta, dotp[i], SM(c));
+      launch_spmv_part(2, A[i]->s_nslices, nullptr, A[i], x[i]->d, y[i]->d, ymap, has_alpha, bmode, alpha, beta, dotp[i], SM(c));
     } else if (A[i]->d_bnd_list) {
       launch_spmv_part(1, A[i]->nslices - A[i]->nslices_int, A[i]->d_bnd_list, A[i], x[i]->d, y[i]->d, ymap,
-                       has_alpha, bmode, alpha, beta, dotp[i], c->s_main);
+                       has_alpha, bmode, alpha, beta, dotp[i], SM(c));
     }
     // long rows (after the halo: they may read ghost columns)
     const bool pat = g_spmv_format == 1 && A[i]->has_pat;
     const int64_t long_base = A[i]->nslices + (pat ? A[i]->s_nslices : 0);
-    launch_spmv_long(A[i], x[i]->d, y[i]->d, ymap, has_alpha, bmode, alpha, beta, dotp[i], long_base, c->s_main);
+    launch_spmv_long(A[i], x[i]->d, y[i]->d, ymap, has_alpha, bmode, alpha, beta, dotp[i], long_base, SM(c));
     if (want_dot) {  // fold the partials (main slices, side slices, long rows) in order
       const bool cplx = dt == PA_C64 || dt == PA_C128;
-      launch_fold(cplx, (int)(long_base + A[i]->n_long), A[i]->d_dotp, c->d_fold, c->d_result, c->s_main);
+      launch_fold(cplx, (int)(long_base + A[i]->n_long), A[i]->d_dotp, c->d_fold, c->d_result, SM(c));
     }
-    if (c->timing) HIPC(hipEventRecord(c->ev_t[3], c->s_main));
+    if (c->timing) EV(hipEventRecord(c->ev_t[3], SM(c)));
   }
   HIPC(hipGetLastError());
   for (int i = 0; i < n; ++i) {
@@ -1516,6 +1554,114 @@ static int spmv_impl(int n, pa_mat* const A[], pa_vec* const y[], const pa_index
       HIPC(hipEventElapsedTime(&c->last_bnd_ms, c->ev_t[2], c->ev_t[3]));
     }
   }
+  return 0;
+}
+
+// ---------------------------------------------------------------------------
+// HIP graph of one mul! over the parts of this process (all on one device,
+// neighbours local): pack, pull-unpack, interior and boundary slices, long
+// rows — captured once from the parts' streams, replayed with one launch.
+struct pa_graph {
+  int device = 0;
+  hipStream_t origin = nullptr;
+  std::vector<hipStream_t> others;
+  std::vector<hipEvent_t> ev_pre;   // per other stream: its queued work, before a replay
+  hipEvent_t ev_done = nullptr;
+  hipGraph_t graph = nullptr;
+  hipGraphExec_t exec = nullptr;
+};
+
+int pa_graph_destroy(pa_graph* G) {
+  if (!G) return 0;
+  (void)hipSetDevice(G->device);
+  (void)hipStreamSynchronize(G->origin);
+  if (G->exec) (void)hipGraphExecDestroy(G->exec);
+  if (G->graph) (void)hipGraphDestroy(G->graph);
+  for (auto e : G->ev_pre) if (e) (void)hipEventDestroy(e);
+  if (G->ev_done) (void)hipEventDestroy(G->ev_done);
+  delete G;
+  return 0;
+}
+
+int pa_spmv_graph_create(int n, pa_mat* const A[], pa_vec* const y[], const pa_index* const y_idx[],
+                         pa_vec* const x[], const pa_index* const x_idx[], pa_xchg* const xg[],
+                         const void* alpha, const void* beta, pa_graph** out) {
+  CHECK_ARG(n >= 1 && A && y && x && out, "null argument");
+  const int dev = A[0]->ctx->device;
+  std::vector<pa_ctx*> ctxs(n);
+  for (int i = 0; i < n; ++i) {
+    CHECK_ARG(A[i], "null handle");
+    ctxs[i] = A[i]->ctx;
+    CHECK_ARG(ctxs[i]->device == dev, "graph capture: every part of the call on one device");
+  }
+  if (xg) {
+    LocalSet L = local_set(n, xg);
+    for (int i = 0; i < n; ++i) {
+      CHECK_ARG(xg[i], "null exchanger");
+      for (const auto* lst : {&xg[i]->parts_snd, &xg[i]->parts_rcv})
+        for (int32_t q : *lst) CHECK_ARG(L.find(q) >= 0, "graph capture: halo neighbours in other processes (RCCL) are not captured");
+    }
+  }
+  HIPC(hipSetDevice(dev));
+  if (xg && g_halo_pull) {  // lazily built device tables must exist before the capture
+    LocalSet L = local_set(n, xg);
+    for (int i = 0; i < n; ++i)
+      if (build_pull(i, n, xg, L, A[0]->dtype, 0)) return -1;
+  }
+  HIPC(hipSetDevice(dev));
+  for (pa_ctx* c : ctxs) {
+    HIPC(hipStreamSynchronize(SM(c)));
+    HIPC(hipStreamSynchronize(SC(c)));
+  }
+  pa_graph* G = new pa_graph();
+  G->device = dev;
+  G->origin = ctxs[0]->s_main;
+  for (int i = 0; i < n; ++i)
+    for (hipStream_t s : {ctxs[i]->s_main, ctxs[i]->s_comm})
+      if (s != G->origin && std::find(G->others.begin(), G->others.end(), s) == G->others.end())
+        G->others.push_back(s);
+  auto mk = [](hipEvent_t* e) { return hipEventCreateWithFlags(e, hipEventDisableTiming); };
+  if (mk(&G->ev_done) != hipSuccess) { pa_graph_destroy(G); PA_FAIL("graph: event creation failed"); }
+  G->ev_pre.resize(G->others.size(), nullptr);
+  for (size_t k = 0; k < G->others.size(); ++k)
+    if (mk(&G->ev_pre[k]) != hipSuccess) { pa_graph_destroy(G); PA_FAIL("graph: event creation failed"); }
+  std::vector<bool> timing(n);
+  for (int i = 0; i < n; ++i) { timing[i] = ctxs[i]->timing; ctxs[i]->timing = false; }
+  hipError_t e = hipStreamBeginCapture(G->origin, hipStreamCaptureModeRelaxed);
+  int rc = -1;
+  if (e == hipSuccess) {
+    g_capturing = true;
+    g_capture_stream = G->origin;  // the parts' kernels as one chain
+    rc = spmv_impl(n, A, y, y_idx, x, x_idx, xg, alpha, beta, false);
+    g_capture_stream = nullptr;
+    g_capturing = false;
+    hipError_t e2 = hipStreamEndCapture(G->origin, &G->graph);
+    if (e == hipSuccess) e = e2;
+  }
+  for (int i = 0; i < n; ++i) ctxs[i]->timing = timing[i];
+  if (e != hipSuccess || rc != 0) {
+    const std::string why = rc != 0 ? pa_last_error() : std::string(hipGetErrorString(e));
+    pa_graph_destroy(G);
+    PA_FAIL("graph capture of mul! failed: " + why);
+  }
+  e = hipGraphInstantiate(&G->exec, G->graph, nullptr, nullptr, 0);
+  if (e != hipSuccess) { pa_graph_destroy(G); PA_FAIL(std::string("hipGraphInstantiate: ") + hipGetErrorString(e)); }
+  *out = G;
+  return 0;
+}
+
+// one replay, ordered after the work already queued on every part stream,
+// and before whatever is queued on them next
+int pa_graph_launch(pa_graph* G) {
+  CHECK_ARG(G && G->exec, "null graph");
+  HIPC(hipSetDevice(G->device));
+  for (size_t k = 0; k < G->others.size(); ++k) {
+    HIPC(hipEventRecord(G->ev_pre[k], G->others[k]));
+    HIPC(hipStreamWaitEvent(G->origin, G->ev_pre[k], 0));
+  }
+  HIPC(hipGraphLaunch(G->exec, G->origin));
+  HIPC(hipEventRecord(G->ev_done, G->origin));
+  for (hipStream_t s : G->others) HIPC(hipStreamWaitEvent(s, G->ev_done, 0));
   return 0;
 }
 

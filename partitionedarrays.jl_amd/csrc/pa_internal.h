@@ -101,6 +101,10 @@ struct StencilGeom {
 // ---------------------------------------------------------------------------
 // Opaque handle definitions.
 struct pa_ctx {
+  // parts of one process on the same device may share one stream pair
+  // (pa_ctx_create_shared): their work then forms one in-order chain
+  struct StreamRefs { int n = 1; };
+  StreamRefs* stream_refs = nullptr;
   int device = 0;
   int part = 1;    // 1-based
   int nparts = 1;

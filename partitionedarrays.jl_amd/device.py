@@ -18,9 +18,12 @@ from .backends import DistributedBackend, PData, SequentialBackend
 class PartContext:
     """pa_ctx: device, streams and scratch of one part."""
 
-    def __init__(self, device: int, part: int, nparts: int):
+    def __init__(self, device: int, part: int, nparts: int, share_with=None):
         h = C.c_void_p()
-        _lib.call("pa_ctx_create", device, part, nparts, C.byref(h))
+        if share_with is not None:  # same device: one stream pair for both parts
+            _lib.call("pa_ctx_create_shared", part, nparts, share_with.h, C.byref(h))
+        else:
+            _lib.call("pa_ctx_create", device, part, nparts, C.byref(h))
         self.h = h
         self.device = device
         self.part = part
@@ -48,17 +51,30 @@ class HIPBackend(SequentialBackend):
     """All parts in this process, part p on device devices[(p-1) % len(devices)]
     (SequentialBackend semantics, HIP parts)."""
 
-    def __init__(self, devices=None):
+    def __init__(self, devices=None, share_streams=False):
         ndev = _lib.device_count()
         if ndev == 0:
             raise _lib.PAError("HIPBackend: no HIP device visible")
         self.devices = list(devices) if devices is not None else list(range(ndev))
+        self.share_streams = share_streams
         self.ctx = {}
 
     def get_part_ids(self, nparts):
+        """With share_streams, parts on the same device share one stream pair:
+        their kernels form one in-order chain instead of cross-stream event
+        waits.  Off by default: small parts fill the GPU better from separate
+        streams (C5, 8 parts of 128³/8 on one GPU: 0.48 vs 1.05 ms per mul!);
+        large parts gain from the chain (eight 256³ parts: 0.82 vs 0.91 ms
+        per part, tools/weak_sim.py)."""
         ids = super().get_part_ids(nparts)
         n = ids.num_parts
-        self.ctx = {p: PartContext(self.devices[(p - 1) % len(self.devices)], p, n) for p in ids.part_ids}
+        first = {}
+        self.ctx = {}
+        for p in ids.part_ids:
+            d = self.devices[(p - 1) % len(self.devices)]
+            share = first.get(d) if self.share_streams else None
+            self.ctx[p] = PartContext(d, p, n, share_with=share)
+            first.setdefault(d, self.ctx[p])
         return ids
 
     def context(self, part) -> PartContext:

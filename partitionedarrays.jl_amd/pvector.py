@@ -368,6 +368,30 @@ def mul_(c: PVector, a: PSparseMatrix, b: PVector, alpha=1.0, beta=0.0) -> PVect
     return c
 
 
+class SpMVGraph:
+    """mul!(c, a, b, α, β) captured once as a HIP graph (pa_spmv_graph_create)
+    and replayed by calling it: one launch instead of the per-part kernels,
+    copies and event waits of the eager path.  All parts on one device."""
+
+    def __init__(self, c: PVector, a: PSparseMatrix, b: PVector, alpha=1.0, beta=0.0):
+        args = _spmv_args(c, a, b, alpha, beta)
+        self._keep = (c, a, b, args)
+        h = C.c_void_p()
+        _lib.call("pa_spmv_graph_create", *args, C.byref(h))
+        self.h = h
+
+    def __call__(self):
+        _lib.call("pa_graph_launch", self.h)
+        return self._keep[0]
+
+    def __del__(self):
+        try:
+            if getattr(self, "h", None) and _lib._lib is not None:
+                _lib._lib.pa_graph_destroy(self.h)
+        except Exception:
+            pass
+
+
 def mul_dot_(c: PVector, a: PSparseMatrix, b: PVector, alpha=1.0, beta=0.0):
     """mul!(c, a, b, α, β) then dot(b, c), the dot accumulated by the SpMV
     kernel (pa_spmv_dot_all).  Returns the dot."""
@@ -377,6 +401,14 @@ def mul_dot_(c: PVector, a: PSparseMatrix, b: PVector, alpha=1.0, beta=0.0):
 
 
 def _spmv(c, a, b, alpha, beta, dot_out):
+    args = _spmv_args(c, a, b, alpha, beta)
+    if dot_out is None:
+        _lib.call("pa_spmv_all", *args)
+    else:
+        _lib.call("pa_spmv_dot_all", *args, dot_out.ctypes.data_as(C.c_void_p))
+
+
+def _spmv_args(c, a, b, alpha, beta):
     if not (c.rows is a.rows or oids_are_equal(c.rows, a.rows)):
         raise AssertionError("mul!: c.rows and a.rows own different ids")
     if not (b.rows is a.cols or (oids_are_equal(a.cols, b.rows) and hids_are_equal(a.cols, b.rows))):
@@ -392,12 +424,9 @@ def _spmv(c, a, b, alpha, beta, dot_out):
     xg = [device_exchanger(cx, ex, p) for cx, p in zip(ctxs, b.values.part_ids)] if has_x else None
     al, alp = _lib.scalar_buf(alpha, a.dtype)
     be, bep = _lib.scalar_buf(beta, a.dtype)
-    args = (n, _hs(a.values.parts), _hs(c.values.parts), _lib.ptr_array(_idx(c)),
+    # the scalar buffers ride along (the C side reads them during the call)
+    return (n, _hs(a.values.parts), _hs(c.values.parts), _lib.ptr_array(_idx(c)),
             _hs(b.values.parts), _lib.ptr_array(_idx(b)), _hs(xg) if xg else None, alp, bep)
-    if dot_out is None:
-        _lib.call("pa_spmv_all", *args)
-    else:
-        _lib.call("pa_spmv_dot_all", *args, dot_out.ctypes.data_as(C.c_void_p))
 
 
 def cg_update_(x: PVector, r: PVector, u: PVector, c: PVector, alpha) -> float:

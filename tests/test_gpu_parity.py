@@ -216,3 +216,57 @@ def test_large_fe27_vs_c_oracle(be, pamd, O, fmt, tmp_path):
     y = pamd.PVector.undef(A.rows)
     pamd.mul_(y, A, x)
     assert np.array_equal(y.to_host().local(1), yref)
+
+
+@pytest.mark.parametrize("shape,N", [((2, 2, 2), (12, 11, 10)), ((1, 1, 1), (9, 8, 7))])
+def test_spmv_graph_replay(be, pamd, O, fmt, shape, N):
+    """mul! captured as a HIP graph and replayed equals the eager mul!
+    bit for bit, follows new values of x uploaded between replays, and
+    orders correctly with eager work on the parts' streams."""
+    parts = be.get_part_ids(shape)
+    A = pamd.drivers.stencil_operator(parts, N, 27)
+    rng = np.random.default_rng(SEED + 9)
+    x = pamd.PVector.from_host(pamd.map_parts(lambda s: rng.uniform(-1, 1, s.num_lids), A.cols.partition), A.cols)
+    y_g = pamd.PVector.undef(A.rows)
+    y_e = pamd.PVector.undef(A.rows)
+    G = pamd.SpMVGraph(y_g, A, x, 2.0, 0.0)
+    for it in range(3):
+        vals = {p: rng.uniform(-1, 1, A.cols.partition.local(p).num_lids) for p in parts.part_ids}
+        for dv, p in zip(x.values.parts, x.values.part_ids):
+            dv.upload(vals[p])
+        G()
+        pamd.mul_(y_e, A, x, 2.0, 0.0)
+        for p in parts.part_ids:
+            assert np.array_equal(y_g.to_host().local(p), y_e.to_host().local(p)), (it, p)
+
+
+def test_shared_stream_parts(pamd, O):
+    """HIPBackend(share_streams=True): the parts on one device share one
+    stream pair; mul!, exchange!/assemble!, the graph replay and the device
+    CG give the same bits as with a stream pair per part."""
+    shape, N = (2, 2, 1), (12, 10, 9)
+    out = {}
+    for share in (False, True):
+        be = pamd.HIPBackend(devices=[0], share_streams=share)
+        parts = be.get_part_ids(shape)
+        A = pamd.drivers.stencil_operator(parts, N, 27)
+        rng = np.random.default_rng(SEED + 4)
+        x = pamd.PVector.from_host(pamd.map_parts(lambda s: rng.uniform(-1, 1, s.num_lids), A.cols.partition), A.cols)
+        y = pamd.PVector.undef(A.rows)
+        pamd.mul_(y, A, x)
+        w = x.copy()
+        pamd.assemble_(w)
+        g = pamd.PVector.undef(A.rows)
+        pamd.SpMVGraph(g, A, x)()
+        b = x.copy()
+        xs = pamd.PVector.undef(A.cols).fill_(0)
+        h = []
+        pamd.cg_(xs, A, b, reltol=0.0, maxiter=15, history=h, device=True)
+        out[share] = ([v.copy() for v in y.to_host().parts], [v.copy() for v in w.to_host().parts],
+                      [v.copy() for v in g.to_host().parts], [v.copy() for v in xs.to_host().parts], h)
+    for k in range(4):
+        for a, b in zip(out[False][k], out[True][k]):
+            assert np.array_equal(a, b), k
+    assert out[False][4] == out[True][4]
+    for a, b in zip(out[True][0], out[True][2]):
+        assert np.array_equal(a, b)
