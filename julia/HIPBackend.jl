@@ -211,15 +211,15 @@ end
 # sparse(I,J,V,m,n,+) on the device; the CSC pattern comes back for the
 # host-side matrix_exchanger (2300-2372).
 function pa_mat_coo(ctx::PartCtx, I::Vector{Int64}, J::Vector{Int64}, V::Vector{Tv},
-                    m::Integer, n::Integer, rows_h, cols_h) where Tv
+                    m::Integer, n::Integer, rows_h, cols_h; ids::Symbol=:local) where Tv
   out = Ref{Ptr{Cvoid}}(C_NULL)
   nnz = Ref{Int64}(0)
   colptr = Vector{Int64}(undef, n + 1)
   rowval = Vector{Int64}(undef, length(I))
   check(ccall((:pa_mat_from_coo, libpa), Cint,
-              (Ptr{Cvoid}, Cint, Cint, Int64, Int64, Int64, Ptr{Int64}, Ptr{Int64}, Ptr{Tv},
+              (Ptr{Cvoid}, Cint, Cint, Cint, Int64, Int64, Int64, Ptr{Int64}, Ptr{Int64}, Ptr{Tv},
                Ptr{Cvoid}, Ptr{Cvoid}, Ref{Int64}, Ptr{Int64}, Ptr{Int64}, Ref{Ptr{Cvoid}}),
-              ctx.h, dtype_code(Tv), 8, m, n, length(I), I, J, V, rows_h, cols_h,
+              ctx.h, dtype_code(Tv), 8, ids === :global ? 1 : 0, m, n, length(I), I, J, V, rows_h, cols_h,
               nnz, colptr, rowval, out))
   out[], colptr, resize!(rowval, nnz[])
 end

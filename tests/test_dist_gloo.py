@@ -149,27 +149,24 @@ def test_ptimer_and_prun_abort(fail_part):
     (MPIBackend.jl:21-36, test_exception.jl)."""
     world = 4
     ctx = mp.get_context("spawn")
-    q = ctx.Queue()
+    # SimpleQueue: put() writes to the pipe before returning, so a rank that
+    # aborts (os._exit) right after sending still delivers its message
+    q = ctx.SimpleQueue()
     port = _free_port()
     ps = [ctx.Process(target=_worker_timer_abort, args=(r, world, port, fail_part, q)) for r in range(world)]
     for p in ps:
         p.start()
     msgs = []
-    import queue
     import time
     t_end = time.time() + 120
     while time.time() < t_end and any(p.is_alive() for p in ps):
-        try:
-            msgs.append(q.get(timeout=0.5))
-        except queue.Empty:
-            pass
+        while not q.empty():
+            msgs.append(q.get())
+        time.sleep(0.1)
     for p in ps:
         p.join(timeout=10)
-    while True:
-        try:
-            msgs.append(q.get(timeout=0.5))
-        except queue.Empty:
-            break
+    while not q.empty():
+        msgs.append(q.get())
     assert all(p.exitcode is not None for p in ps), "a rank hung"
     timers = {r: d for r, k, d in msgs if k == "timer"}
     assert set(timers) == set(range(world))
