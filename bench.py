@@ -9,6 +9,7 @@ time of K steps (max over ranks) → GB/s.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--n 256] [--kind 27]
     torchrun --nproc-per-node N bench.py --gpus N ...   (one part per GPU)
+    ... --strong    256³ nodes in total split over the N parts (config 3)
 """
 from __future__ import annotations
 
@@ -175,7 +176,9 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--n", type=int, default=256, help="nodes per dim per GPU")
+    ap.add_argument("--n", type=int, default=256, help="nodes per dim per GPU (global with --strong)")
+    ap.add_argument("--strong", action="store_true",
+                    help="strong scaling (BASELINE config 3): --n^3 nodes in total, split over the parts")
     ap.add_argument("--kind", type=int, default=27, choices=[7, 27])
     ap.add_argument("--dtype", default="f64", choices=list(DTYPES))
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
@@ -204,7 +207,7 @@ def main():
     if ngpu not in PART_SHAPES:
         raise SystemExit(f"--gpus must be one of {sorted(PART_SHAPES)}")
     shape = PART_SHAPES[ngpu]
-    N = tuple(args.n * s for s in shape)
+    N = (args.n,) * 3 if args.strong else tuple(args.n * s for s in shape)
     dtype = DTYPES[args.dtype]
     S = np.dtype(dtype).itemsize
 
@@ -325,13 +328,13 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(ms_per_step, 4),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if args.strong else "weak",
         "vs_baseline": None,
         "dtype": {"f64": "f64", "f32": "f32", "c128": "c128", "c64": "c64"}[args.dtype],
         "data": "synthetic (seeded uniform x; operator generated on device)",
         "config": {
             "workload": f"mul!(y,A,x) incl. halo, {args.kind}-pt {'FE (test_fem_sa.jl pattern)' if args.kind == 27 else 'FD (test_fdm.jl)'} "
-                        f"operator, {args.n}^3 nodes per GPU, Cartesian parts {shape}",
+                        f"operator, {args.n}^3 nodes {'in total' if args.strong else 'per GPU'}, Cartesian parts {shape}",
             "global_nodes": list(N),
             "parts": list(shape),
             "nnz_per_part": info["nnz"],

@@ -30,10 +30,14 @@ void launch_pattern_detect(pa_mat* A, int64_t noids, int32_t* kind, int32_t* ple
 void launch_side_len(pa_mat* A, int64_t n, const int32_t* rows, int32_t* len, int64_t noids,
                      int32_t* sghost, hipStream_t st);
 void launch_side_fill(pa_mat* A, const int32_t* rows, const int32_t* len, hipStream_t st);
-void launch_fold(int cplx, int nb, const void* in, void* scratch, void* out, hipStream_t st);
+void launch_fold(int cplx, int nb, const void* in, void* scratch, void* out, unsigned* ticket, hipStream_t st);
+void launch_fold_cg_alpha(int dtype, int nb, const void* in, void* scratch, void* out, unsigned* ticket,
+                          CGState* cst, hipStream_t st);
+void launch_fold_cg_step(int nb, const void* in, void* scratch, void* out, unsigned* ticket, CGState* cst,
+                         double* history, hipStream_t st);
 void launch_cg_xr(int dtype, int64_t n, int64_t noids, const int32_t* own, void* x, void* r, const void* u,
                   const void* c, const void* alpha, const CGState* cst, double* part, int nb, hipStream_t st);
-void launch_cg_xpby(int dtype, int64_t n, void* u, const void* r, const CGState* cst, hipStream_t st);
+void launch_cg_xu(int dtype, int64_t n, void* x, void* u, const void* r, const CGState* cst, hipStream_t st);
 void launch_cg_alpha(int dtype, int P, const void* gathered, CGState* cst, hipStream_t st);
 void launch_cg_step(int P, const double* gathered, CGState* cst, double* history, hipStream_t st);
 void launch_gather_ptrs(int P, const void* const* srcs, int accsz, void* out, hipStream_t st);
@@ -75,7 +79,7 @@ void launch_axpby(int dtype, int64_t n, const int32_t* map, void* y, const void*
                   int mode, hipStream_t st);
 void launch_reduce(int dtype, int kind, int64_t n, const int32_t* ma, const void* a,
                    const int32_t* mb, const void* b, void* partials, void* result,
-                   hipStream_t st);
+                   unsigned* ticket, hipStream_t st);
 void launch_stencil_count(const StencilGeom& g, const int32_t* shell, const double* coef,
                           int64_t nrows, int noids, int H, int32_t* slen, int32_t* sghost,
                           int32_t* err, hipStream_t st);
@@ -619,6 +623,8 @@ static int ctx_scratch(pa_ctx* c) {
   HIPC(hipMalloc(&c->d_fold, 256 * 16));
   HIPC(hipMalloc(&c->d_result, 16));
   HIPC(hipMalloc(&c->d_gather, (size_t)c->nparts * 16));
+  HIPC(hipMalloc((void**)&c->d_ticket, 16));
+  HIPC(hipMemset(c->d_ticket, 0, 16));
   HIPC(hipHostMalloc(&c->h_pinned, std::max<size_t>((size_t)(c->nparts + 1) * 16, 256)));  // gathered partials / CG state
   HIPC(hipEventCreateWithFlags(&c->ev_packed, hipEventDisableTiming));
   HIPC(hipEventCreateWithFlags(&c->ev_recvd, hipEventDisableTiming));
@@ -692,6 +698,7 @@ int pa_ctx_destroy(pa_ctx* c) {
   dev_free(c->d_fold);
   dev_free(c->d_result);
   dev_free(c->d_gather);
+  dev_free(c->d_ticket);
   if (c->h_pinned) (void)hipHostFree(c->h_pinned);
   (void)hipEventDestroy(c->ev_packed);
   (void)hipEventDestroy(c->ev_recvd);
@@ -1451,7 +1458,7 @@ int pa_mat_info(const pa_mat* A, int64_t* nrows, int64_t* nnz, int64_t* slots, i
 // A->d_dotp, folded by fold_dot) — the CG's `dot(u, c)` after `mul!(c, A, u)`.
 static int spmv_impl(int n, pa_mat* const A[], pa_vec* const y[], const pa_index* const y_idx[],
                      pa_vec* const x[], const pa_index* const x_idx[], pa_xchg* const xg[],
-                     const void* alpha, const void* beta, bool want_dot) {
+                     const void* alpha, const void* beta, bool want_dot, CGState* const* dot_tail = nullptr) {
   CHECK_ARG(n >= 1 && A && y && x && alpha && beta, "null argument");
   const int dt = A[0]->dtype;
   bool any_x = false;
@@ -1541,7 +1548,11 @@ static int spmv_impl(int n, pa_mat* const A[], pa_vec* const y[], const pa_index
     launch_spmv_long(A[i], x[i]->d, y[i]->d, ymap, has_alpha, bmode, alpha, beta, dotp[i], long_base, SM(c));
     if (want_dot) {  // fold the partials (main slices, side slices, long rows) in order
       const bool cplx = dt == PA_C64 || dt == PA_C128;
-      launch_fold(cplx, (int)(long_base + A[i]->n_long), A[i]->d_dotp, c->d_fold, c->d_result, SM(c));
+      const int nbp = (int)(long_base + A[i]->n_long);
+      if (dot_tail)  // one part per process: the fold ends in the CG's α
+        launch_fold_cg_alpha(dt, nbp, A[i]->d_dotp, c->d_fold, c->d_result, c->d_ticket, dot_tail[i], SM(c));
+      else
+        launch_fold(cplx, nbp, A[i]->d_dotp, c->d_fold, c->d_result, c->d_ticket, SM(c));
     }
     if (c->timing) EV(hipEventRecord(c->ev_t[3], SM(c)));
   }
@@ -1771,7 +1782,7 @@ int reduce_all(int n, const pa_vec* const a[], const pa_index* const ia[], const
     HIPC(hipSetDevice(c->device));
     launch_reduce(dt, kind, ia[i]->noids, ia[i]->d_oid_to_lid, a[i]->d,
                   kind == 0 ? ib[i]->d_oid_to_lid : nullptr, kind == 0 ? b[i]->d : nullptr,
-                  c->d_partials, c->d_result, c->s_main);
+                  c->d_partials, c->d_result, c->d_ticket, c->s_main);
   }
   HIPC(hipGetLastError());
   std::vector<pa_ctx*> ctxs(n);
@@ -1831,12 +1842,12 @@ int pa_cg_update_all(int n, pa_vec* const x[], pa_vec* const r[], const pa_vec* 
       const int nb = (int)std::min<int64_t>(8192, std::max<int64_t>(1, (m + 255) / 256));
       launch_cg_xr(dt, m, idx[i]->noids, nullptr, x[i]->d, r[i]->d, u[i]->d, c[i]->d, alpha, nullptr,
                    (double*)cx->d_partials, nb, cx->s_main);
-      launch_fold(0, nb, cx->d_partials, cx->d_fold, cx->d_result, cx->s_main);
+      launch_fold(0, nb, cx->d_partials, cx->d_fold, cx->d_result, cx->d_ticket, cx->s_main);
     } else {  // unfused: two broadcasts and the norm reduction
       launch_axpby(dt, m, nullptr, x[i]->d, u[i]->d, alpha, 1, cx->s_main);
       launch_axpby(dt, m, nullptr, r[i]->d, c[i]->d, alpha, 2, cx->s_main);
       launch_reduce(dt, 1, idx[i]->noids, idx[i]->d_oid_to_lid, r[i]->d, nullptr, nullptr, cx->d_partials,
-                    cx->d_result, cx->s_main);
+                    cx->d_result, cx->d_ticket, cx->s_main);
     }
   }
   HIPC(hipGetLastError());
@@ -2004,35 +2015,46 @@ int pa_cg_solve_all(int n, pa_mat* const A[], pa_vec* const x[], const pa_vec* c
     HIPC(hipStreamSynchronize(R.ctxs[i]->s_main));
   }
   const size_t accsz = cplx ? 16 : 8;
+  // one part in this process and no other process: the folds end in the
+  // scalar updates themselves (no gather, no scalar kernels)
+  const bool tail = !R.remote && R.P == 1;
   int64_t enqueued = 0;
   bool done = h.done != 0;
   while (!done && enqueued < maxiter) {
     const int64_t k = std::min<int64_t>(batch, maxiter - enqueued);  // the same on every rank
     for (int64_t t = 0; t < k; ++t) {
-      for (int i = 0; i < n; ++i) {  // u .= r .+ β.*u
+      for (int i = 0; i < n; ++i) {  // (x .+= α.*u of the previous iteration); u .= r .+ β.*u
         HIPC(hipSetDevice(R.ctxs[i]->device));
-        launch_cg_xpby(dt, u[i]->n, u[i]->d, r[i]->d, R.st[i], R.ctxs[i]->s_main);
+        launch_cg_xu(dt, u[i]->n, x[i]->d, u[i]->d, r[i]->d, R.st[i], R.ctxs[i]->s_main);
       }
-      // mul!(c, A, u) with dot(u, c) accumulated by the SpMV
-      if (spmv_impl(n, A, c, idx, u, idx, xg, one, zero, true)) return -1;
-      if (cg_gather(R, accsz)) return -1;
-      for (int i = 0; i < n; ++i) {  // α = residual² / dot(u, c)
-        HIPC(hipSetDevice(R.ctxs[i]->device));
-        launch_cg_alpha(dt, R.P, R.ctxs[i]->d_gather, R.st[i], R.ctxs[i]->s_main);
+      // mul!(c, A, u) with dot(u, c) accumulated by the SpMV; α = residual² / dot(u, c)
+      if (spmv_impl(n, A, c, idx, u, idx, xg, one, zero, true, tail ? R.st.data() : nullptr)) return -1;
+      if (!tail) {
+        if (cg_gather(R, accsz)) return -1;
+        for (int i = 0; i < n; ++i) {
+          HIPC(hipSetDevice(R.ctxs[i]->device));
+          launch_cg_alpha(dt, R.P, R.ctxs[i]->d_gather, R.st[i], R.ctxs[i]->s_main);
+        }
       }
-      for (int i = 0; i < n; ++i) {  // x .+= α.*u; r .-= α.*c; Σ|r|²
+      for (int i = 0; i < n; ++i) {  // r .-= α.*c; Σ|r|²
         pa_ctx* cx = R.ctxs[i];
         HIPC(hipSetDevice(cx->device));
         const int64_t m = x[i]->n;
         const int nbk = (int)std::min<int64_t>(8192, std::max<int64_t>(1, (m + 255) / 256));
         launch_cg_xr(dt, m, idx[i]->noids, nullptr, x[i]->d, r[i]->d, u[i]->d, c[i]->d, nullptr, R.st[i],
                      (double*)cx->d_partials, nbk, cx->s_main);
-        launch_fold(0, nbk, cx->d_partials, cx->d_fold, cx->d_result, cx->s_main);
+        if (tail)  // prev = residual; residual = norm(r); it += 1; done?
+          launch_fold_cg_step(nbk, cx->d_partials, cx->d_fold, cx->d_result, cx->d_ticket, R.st[i], R.hist[i],
+                              cx->s_main);
+        else
+          launch_fold(0, nbk, cx->d_partials, cx->d_fold, cx->d_result, cx->d_ticket, cx->s_main);
       }
-      if (cg_gather(R, 8)) return -1;
-      for (int i = 0; i < n; ++i) {  // prev = residual; residual = norm(r); it += 1; done?
-        HIPC(hipSetDevice(R.ctxs[i]->device));
-        launch_cg_step(R.P, (const double*)R.ctxs[i]->d_gather, R.st[i], R.hist[i], R.ctxs[i]->s_main);
+      if (!tail) {
+        if (cg_gather(R, 8)) return -1;
+        for (int i = 0; i < n; ++i) {  // prev = residual; residual = norm(r); it += 1; done?
+          HIPC(hipSetDevice(R.ctxs[i]->device));
+          launch_cg_step(R.P, (const double*)R.ctxs[i]->d_gather, R.st[i], R.hist[i], R.ctxs[i]->s_main);
+        }
       }
       HIPC(hipGetLastError());
     }
@@ -2047,6 +2069,16 @@ int pa_cg_solve_all(int n, pa_mat* const A[], pa_vec* const x[], const pa_vec* c
     }
     std::memcpy(&h, c0->h_pinned, sizeof(CGState));
     done = h.done != 0;
+  }
+  if (h.it > h.xit) {  // the last iteration's deferred x .+= α.*u (u untouched: done)
+    for (int i = 0; i < n; ++i) {
+      HIPC(hipSetDevice(R.ctxs[i]->device));
+      launch_cg_xu(dt, u[i]->n, x[i]->d, u[i]->d, r[i]->d, R.st[i], R.ctxs[i]->s_main);
+    }
+    for (int i = 0; i < n; ++i) {
+      HIPC(hipSetDevice(R.ctxs[i]->device));
+      HIPC(hipStreamSynchronize(R.ctxs[i]->s_main));
+    }
   }
   *iterations = h.it;
   *residual = h.res;

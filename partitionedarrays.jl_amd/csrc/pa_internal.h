@@ -51,6 +51,115 @@ __host__ __device__ inline double abs2(double a) { return a * a; }
 __host__ __device__ inline float abs2(c64 a) { return a.re * a.re + a.im * a.im; }
 __host__ __device__ inline double abs2(c128 a) { return a.re * a.re + a.im * a.im; }
 
+// ---- deterministic block reductions (shared by the .hip files) -----------
+template <typename A>
+__device__ inline A shfl_down64(A v, int d) {
+  return __shfl_down(v, d, 64);
+}
+template <>
+__device__ inline c128 shfl_down64<c128>(c128 v, int d) {
+  return c128{__shfl_down(v.re, d, 64), __shfl_down(v.im, d, 64)};
+}
+
+// 256-thread block sum in a fixed order (wave tree, then waves 0..3); the
+// result is valid on thread 0
+template <typename A>
+__device__ inline A block_reduce(A v) {
+  __shared__ A sm[4];
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) v = v + shfl_down64(v, d);
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) sm[w] = v;
+  __syncthreads();
+  A r = zero_of<A>();
+  if (threadIdx.x == 0) {
+    r = sm[0];
+    for (int i = 1; i < (int)(blockDim.x >> 6); ++i) r = r + sm[i];
+  }
+  return r;
+}
+
+// In-launch hand-off of one value per block (cdna_hip_programming.md §6
+// Guideline 16, R1 with a ticket counter): lane 0 stores its value
+// write-through (sc1), drains, then takes a ticket; the block whose ticket
+// is the last one reads every value with sc1 loads.  The ticket is zeroed at
+// allocation and reset by the last block, so it is 0 between launches.
+typedef __attribute__((address_space(1))) unsigned long long pa_gu64;
+typedef __attribute__((address_space(1))) unsigned int pa_gu32;
+
+__device__ inline void st_wt(double* p, double v) {
+  __hip_atomic_store((pa_gu64*)p, (unsigned long long)__double_as_longlong(v), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ inline void st_wt(c128* p, c128 v) {
+  st_wt(reinterpret_cast<double*>(p), v.re);
+  st_wt(reinterpret_cast<double*>(p) + 1, v.im);
+}
+__device__ inline double ld_wt(const double* p) {
+  return __longlong_as_double((long long)__hip_atomic_load((pa_gu64*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+__device__ inline c128 ld_wt(const c128* p) {
+  const double* q = reinterpret_cast<const double*>(p);
+  return c128{ld_wt(q), ld_wt(q + 1)};
+}
+
+// every thread of the block gets: did this block arrive last?
+template <typename A>
+__device__ inline bool publish_arrive(A* slots, A v, unsigned* ticket) {
+  __shared__ int last;
+  if (threadIdx.x == 0) {
+    st_wt(&slots[blockIdx.x], v);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned t = __hip_atomic_fetch_add((pa_gu32*)ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last = t == gridDim.x - 1;
+    if (last) __hip_atomic_store((pa_gu32*)ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  return last != 0;
+}
+
+struct NoTail {
+  __device__ void operator()(const void*) const {}
+};
+
+constexpr int kFoldBlocks = 256;  // first-level blocks of a long fold (scratch: kFoldBlocks accumulators)
+
+// Fold nb partials into out[0] in ONE launch, in the order of the two-level
+// fold it replaces (k_fold_chunks + k_reduce_final): with g > 1 blocks,
+// block b sums chunk [b*chunk, (b+1)*chunk) and hands it over; the last
+// block sums the g chunk sums in block order.  tail(out) then runs on
+// thread 0 of the finishing block (e.g. the CG scalar update).
+template <typename A, typename Tail>
+__global__ __launch_bounds__(256) void k_fold(int nb, int chunk, const A* __restrict__ in, A* scratch,
+                                              A* __restrict__ out, unsigned* ticket, Tail tail) {
+  const bool one = gridDim.x == 1;
+  const int lo = one ? 0 : (int)blockIdx.x * chunk;
+  const int hi = one ? nb : min(nb, lo + chunk);
+  A s = zero_of<A>();
+  for (int i = lo + (int)threadIdx.x; i < hi; i += blockDim.x) s = s + in[i];
+  A r = block_reduce(s);
+  if (!one) {
+    if (!publish_arrive(scratch, r, ticket)) return;
+    A s2 = zero_of<A>();
+    for (int i = threadIdx.x; i < (int)gridDim.x; i += blockDim.x) s2 = s2 + ld_wt(&scratch[i]);
+    r = block_reduce(s2);
+  }
+  if (threadIdx.x == 0) {
+    out[0] = r;
+    tail(out);
+  }
+}
+
+template <typename A, typename Tail>
+inline void fold_launch(int nb, const A* in, A* scratch, A* out, unsigned* ticket, Tail tail, hipStream_t st) {
+  int g = 1, chunk = nb;
+  if (nb > 2 * kFoldBlocks && scratch) {  // one block over 10^5 partials is ~150 us
+    chunk = (nb + kFoldBlocks - 1) / kFoldBlocks;
+    g = (nb + chunk - 1) / chunk;
+  }
+  hipLaunchKernelGGL((k_fold<A, Tail>), dim3(g), dim3(256), 0, st, nb, chunk, in, scratch, out, ticket, tail);
+}
+
 inline size_t dtype_size(int dt) {
   switch (dt) {
     case PA_F32: return 4;
@@ -86,6 +195,7 @@ struct CGState {
   int32_t done;      // it >= maxiter || res <= tol
   int32_t pad;
   c128 alpha;        // α in the vectors' element type (first sizeof(T) bytes)
+  int64_t xit;       // iterations whose x .+= α.*u is applied (deferred into the next u update)
 };
 
 // Cartesian part box of a synthetic stencil operator (pa_mat_stencil).
@@ -116,6 +226,7 @@ struct pa_ctx {
   void* d_fold = nullptr;         // 256*16 B first-level fold of long partial lists
   void* d_result = nullptr;       // 16 B final per-part value
   void* d_gather = nullptr;       // nparts*16 B gathered partials (RCCL mode)
+  unsigned* d_ticket = nullptr;   // arrival counter of the one-launch folds (0 between launches)
   void* h_pinned = nullptr;       // pinned host staging (>= nparts*16 B)
   // timing
   bool timing = false;

@@ -272,33 +272,9 @@ void launch_axpby(int dtype, int64_t n, const int32_t* map, void* y, const void*
 
 // ---------------------------------------------------------------------------
 // Deterministic reductions: fixed grid, per-block tree in a fixed order,
-// then one block folds the block partials in order.  Accumulator type:
-// double (F32, F64) / c128 (C64, C128).
-
-template <typename A>
-__device__ inline A shfl_down64(A v, int d) {
-  return __shfl_down(v, d, 64);
-}
-template <>
-__device__ inline c128 shfl_down64<c128>(c128 v, int d) {
-  return c128{__shfl_down(v.re, d, 64), __shfl_down(v.im, d, 64)};
-}
-
-template <typename A>
-__device__ inline A block_reduce(A v) {
-  __shared__ A sm[4];
-#pragma unroll
-  for (int d = 32; d >= 1; d >>= 1) v = v + shfl_down64(v, d);
-  const int w = threadIdx.x >> 6;
-  if ((threadIdx.x & 63) == 0) sm[w] = v;
-  __syncthreads();
-  A r = zero_of<A>();
-  if (threadIdx.x == 0) {
-    r = sm[0];
-    for (int i = 1; i < (int)(blockDim.x >> 6); ++i) r = r + sm[i];
-  }
-  return r;
-}
+// then the last block to finish folds the block partials in order (one
+// launch; block_reduce / publish_arrive / k_fold in pa_internal.h).
+// Accumulator type: double (F32, F64) / c128 (C64, C128).
 
 template <typename T> struct acc_of { using type = double; };
 template <> struct acc_of<c64> { using type = c128; };
@@ -312,13 +288,16 @@ template <typename A> __device__ inline A acc_real(double v);
 template <> __device__ inline double acc_real<double>(double v) { return v; }
 template <> __device__ inline c128 acc_real<c128>(double v) { return c128{v, 0.0}; }
 
-// KIND 0: dot(a,b) (conj(a)·b); 1: Σ|a|²; 2: Σ a
+// KIND 0: dot(a,b) (conj(a)·b); 1: Σ|a|²; 2: Σ a.  Block partials go to
+// out[blockIdx]; the last block folds them (block order) into result[0].
 template <typename T, int KIND>
 __global__ __launch_bounds__(256) void k_reduce_partial(int64_t n, const int32_t* __restrict__ ma,
                                                         const T* __restrict__ a,
                                                         const int32_t* __restrict__ mb,
                                                         const T* __restrict__ b,
-                                                        typename acc_of<T>::type* __restrict__ out) {
+                                                        typename acc_of<T>::type* out,
+                                                        typename acc_of<T>::type* __restrict__ result,
+                                                        unsigned* ticket) {
   using A = typename acc_of<T>::type;
   A s = zero_of<A>();
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
@@ -334,73 +313,39 @@ __global__ __launch_bounds__(256) void k_reduce_partial(int64_t n, const int32_t
     }
   }
   A r = block_reduce(s);
-  if (threadIdx.x == 0) out[blockIdx.x] = r;
-}
-
-template <typename A>
-__global__ __launch_bounds__(256) void k_reduce_final(int nb, const A* __restrict__ in,
-                                                      A* __restrict__ out) {
-  A s = zero_of<A>();
-  for (int i = threadIdx.x; i < nb; i += blockDim.x) s = s + in[i];
-  A r = block_reduce(s);
-  if (threadIdx.x == 0) out[0] = r;
+  if (!publish_arrive(out, r, ticket)) return;
+  A f = zero_of<A>();
+  for (int i = threadIdx.x; i < (int)gridDim.x; i += blockDim.x) f = f + ld_wt(&out[i]);
+  f = block_reduce(f);
+  if (threadIdx.x == 0) result[0] = f;
 }
 
 constexpr int kReduceBlocks = 1024;
-constexpr int kFoldBlocks = 256;  // == PA_FOLD_SCRATCH / 16
 
 template <typename T, int KIND>
 static void reduce_t(int64_t n, const int32_t* ma, const void* a, const int32_t* mb,
-                     const void* b, void* partials, void* result, hipStream_t st) {
+                     const void* b, void* partials, void* result, unsigned* ticket, hipStream_t st) {
   using A = typename acc_of<T>::type;
   int nb = grid_for(n, 256, kReduceBlocks);
   hipLaunchKernelGGL((k_reduce_partial<T, KIND>), dim3(nb), dim3(256), 0, st, n, ma, (const T*)a,
-                     mb, (const T*)b, (A*)partials);
-  hipLaunchKernelGGL((k_reduce_final<A>), dim3(1), dim3(256), 0, st, nb, (const A*)partials,
-                     (A*)result);
-}
-
-// block b folds the contiguous chunk [b*chunk, min(nb, (b+1)*chunk))
-template <typename A>
-__global__ __launch_bounds__(256) void k_fold_chunks(int nb, int chunk, const A* __restrict__ in,
-                                                     A* __restrict__ out) {
-  const int lo = blockIdx.x * chunk;
-  const int hi = min(nb, lo + chunk);
-  A s = zero_of<A>();
-  for (int i = lo + threadIdx.x; i < hi; i += blockDim.x) s = s + in[i];
-  A r = block_reduce(s);
-  if (threadIdx.x == 0) out[blockIdx.x] = r;
-}
-
-template <typename A>
-static void fold_t(int nb, const A* in, A* scratch, A* out, hipStream_t st) {
-  if (nb <= 2 * kFoldBlocks || !scratch) {
-    hipLaunchKernelGGL((k_reduce_final<A>), dim3(1), dim3(256), 0, st, nb, in, out);
-    return;
-  }
-  // two levels (one block over 10^5 partials is ~150 us): the chunking
-  // depends only on nb, so the result stays run-to-run deterministic
-  const int chunk = (nb + kFoldBlocks - 1) / kFoldBlocks;
-  const int g = (nb + chunk - 1) / chunk;
-  hipLaunchKernelGGL((k_fold_chunks<A>), dim3(g), dim3(256), 0, st, nb, chunk, in, scratch);
-  hipLaunchKernelGGL((k_reduce_final<A>), dim3(1), dim3(256), 0, st, g, (const A*)scratch, out);
+                     mb, (const T*)b, (A*)partials, (A*)result, ticket);
 }
 
 // fold nb partials (double, or c128 when cplx) in a fixed order into out[0];
 // scratch holds kFoldBlocks accumulators
-void launch_fold(int cplx, int nb, const void* in, void* scratch, void* out, hipStream_t st) {
-  if (cplx) fold_t<c128>(nb, (const c128*)in, (c128*)scratch, (c128*)out, st);
-  else fold_t<double>(nb, (const double*)in, (double*)scratch, (double*)out, st);
+void launch_fold(int cplx, int nb, const void* in, void* scratch, void* out, unsigned* ticket, hipStream_t st) {
+  if (cplx) fold_launch<c128>(nb, (const c128*)in, (c128*)scratch, (c128*)out, ticket, NoTail{}, st);
+  else fold_launch<double>(nb, (const double*)in, (double*)scratch, (double*)out, ticket, NoTail{}, st);
 }
 
 // result: device accumulator (double or c128) of the part's local value
 void launch_reduce(int dtype, int kind, int64_t n, const int32_t* ma, const void* a,
                    const int32_t* mb, const void* b, void* partials, void* result,
-                   hipStream_t st) {
-#define PA_RED(T)                                                                   \
-  if (kind == 0) reduce_t<T, 0>(n, ma, a, mb, b, partials, result, st);             \
-  else if (kind == 1) reduce_t<T, 1>(n, ma, a, mb, b, partials, result, st);        \
-  else reduce_t<T, 2>(n, ma, a, mb, b, partials, result, st);
+                   unsigned* ticket, hipStream_t st) {
+#define PA_RED(T)                                                                           \
+  if (kind == 0) reduce_t<T, 0>(n, ma, a, mb, b, partials, result, ticket, st);             \
+  else if (kind == 1) reduce_t<T, 1>(n, ma, a, mb, b, partials, result, ticket, st);        \
+  else reduce_t<T, 2>(n, ma, a, mb, b, partials, result, ticket, st);
   switch (dtype) {
     case PA_F32: { PA_RED(float) } break;
     case PA_F64: { PA_RED(double) } break;

@@ -593,7 +593,9 @@ void launch_spmv_part(int which, int64_t nwork, const int32_t* list, const pa_ma
 // Σ|r|² of norm(r) (1767-1772) in one pass (contiguous owned lids
 // 0..noids-1); per-block partials, folded in block order afterwards.
 // V elements per 16 B access (V = 1: unaligned fallback).  DEV: α comes from
-// the device CG state (pa_cg_solve_all) and a finished solve is a no-op.
+// the device CG state (pa_cg_solve_all), x is left alone (its update is
+// deferred into the next k_cg_xu, which reads u anyway) and a finished solve
+// is a no-op.
 template <typename T, int V, bool DEV>
 __global__ __launch_bounds__(256) void k_cg_xr(int64_t n, int64_t noids, T* __restrict__ x, T* __restrict__ r,
                                                const T* __restrict__ u, const T* __restrict__ c, T alpha,
@@ -608,21 +610,24 @@ __global__ __launch_bounds__(256) void k_cg_xr(int64_t n, int64_t noids, T* __re
   const int64_t nv = n / V;
   double s = 0.0;
   for (int64_t j = t; j < nv; j += stride) {
-    P xv = reinterpret_cast<const P*>(x)[j];
+    if (!DEV) {
+      P xv = reinterpret_cast<const P*>(x)[j];
+      const P uv = reinterpret_cast<const P*>(u)[j];
+#pragma unroll
+      for (int e = 0; e < V; ++e) xv.v[e] = xv.v[e] + alpha * uv.v[e];
+      reinterpret_cast<P*>(x)[j] = xv;
+    }
     P rv = reinterpret_cast<const P*>(r)[j];
-    const P uv = reinterpret_cast<const P*>(u)[j];
     const P cv = reinterpret_cast<const P*>(c)[j];
 #pragma unroll
     for (int e = 0; e < V; ++e) {
-      xv.v[e] = xv.v[e] + alpha * uv.v[e];
       rv.v[e] = rv.v[e] - alpha * cv.v[e];
       if (j * V + e < noids) s = s + (double)abs2(rv.v[e]);
     }
-    reinterpret_cast<P*>(x)[j] = xv;
     reinterpret_cast<P*>(r)[j] = rv;
   }
   for (int64_t i = nv * V + t; i < n; i += stride) {
-    x[i] = x[i] + alpha * u[i];
+    if (!DEV) x[i] = x[i] + alpha * u[i];
     const T ri = r[i] - alpha * c[i];
     r[i] = ri;
     if (i < noids) s = s + (double)abs2(ri);
@@ -674,22 +679,52 @@ template <> __device__ inline c64 real_scalar<c64>(double v) { return c64{(float
 template <> __device__ inline c128 real_scalar<c128>(double v) { return c128{v, 0.0}; }
 
 // u .= r .+ β.*u over all lids, β = residual²/prev_residual² (IterativeSolvers
-// 0.9 cg iterate); a finished solve is a no-op
-template <typename T>
-__global__ __launch_bounds__(256) void k_cg_xpby(int64_t n, T* __restrict__ u, const T* __restrict__ r,
-                                                 const CGState* __restrict__ st) {
-  if (st->done) return;
-  const double b = (st->res * st->res) / (st->prev * st->prev);
-  const T a = real_scalar<T>(b);
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
-    u[i] = r[i] + a * u[i];
+// 0.9 cg iterate), preceded per element by the previous iteration's deferred
+// x .+= α.*u (while it > xit: α is still that iteration's, u not yet
+// overwritten).  Same arithmetic per element as the host-driven loop.  V
+// elements per 16 B access (V = 1: unaligned fallback).
+template <typename T, int V>
+__global__ __launch_bounds__(256) void k_cg_xu(int64_t n, T* __restrict__ x, T* __restrict__ u,
+                                               const T* __restrict__ r, const CGState* __restrict__ st) {
+  const bool xpend = st->it > st->xit;
+  const bool upd = !st->done;
+  if (!xpend && !upd) return;
+  const T a = *reinterpret_cast<const T*>(&st->alpha);
+  const T b = real_scalar<T>((st->res * st->res) / (st->prev * st->prev));
+  using P = Pack<T, V>;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  const int64_t nv = n / V;
+  for (int64_t j = t; j < nv; j += stride) {
+    P uv = reinterpret_cast<const P*>(u)[j];
+    if (xpend) {
+      P xv = reinterpret_cast<const P*>(x)[j];
+#pragma unroll
+      for (int e = 0; e < V; ++e) xv.v[e] = xv.v[e] + a * uv.v[e];
+      reinterpret_cast<P*>(x)[j] = xv;
+    }
+    if (upd) {
+      const P rv = reinterpret_cast<const P*>(r)[j];
+#pragma unroll
+      for (int e = 0; e < V; ++e) uv.v[e] = rv.v[e] + b * uv.v[e];
+      reinterpret_cast<P*>(u)[j] = uv;
+    }
+  }
+  for (int64_t i = nv * V + t; i < n; i += stride) {
+    const T ui = u[i];
+    if (xpend) x[i] = x[i] + a * ui;
+    if (upd) u[i] = r[i] + b * ui;
+  }
 }
 
 // the dot partials of the P parts (accumulators, part order) →
-// dot = reduce(+; init=0) narrowed to T → α = residual² / dot
+// dot = reduce(+; init=0) narrowed to T → α = residual² / dot.  It also
+// records that the previous iteration's x update has been applied (k_cg_xu
+// ran before this iteration's SpMV).
 template <typename T>
-__global__ void k_cg_alpha(int P, const void* __restrict__ gathered, CGState* __restrict__ st) {
-  if (threadIdx.x != 0 || blockIdx.x != 0 || st->done) return;
+__device__ inline void cg_alpha(int P, const void* __restrict__ gathered, CGState* __restrict__ st) {
+  st->xit = st->it;
+  if (st->done) return;
   const double res2 = st->res * st->res;
   T* out = reinterpret_cast<T*>(&st->alpha);
   if constexpr (std::is_same<T, float>::value || std::is_same<T, double>::value) {
@@ -734,11 +769,17 @@ __global__ void k_cg_alpha(int P, const void* __restrict__ gathered, CGState* __
   }
 }
 
+template <typename T>
+__global__ void k_cg_alpha(int P, const void* __restrict__ gathered, CGState* __restrict__ st) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  cg_alpha<T>(P, gathered, st);
+}
+
 // Σ|r|² partials of the P parts → prev = residual; residual = sqrt(Σ);
 // it += 1; history[it] = residual; done = it >= maxiter || residual <= tol
-__global__ void k_cg_step(int P, const double* __restrict__ gathered, CGState* __restrict__ st,
-                          double* __restrict__ history) {
-  if (threadIdx.x != 0 || blockIdx.x != 0 || st->done) return;
+__device__ inline void cg_step(int P, const double* __restrict__ gathered, CGState* __restrict__ st,
+                               double* __restrict__ history) {
+  if (st->done) return;
   double s = 0.0;
   for (int p = 0; p < P; ++p) s = s + gathered[p];
   const double res = sqrt(s);
@@ -749,6 +790,25 @@ __global__ void k_cg_step(int P, const double* __restrict__ gathered, CGState* _
   if (history) history[it - 1] = res;
   st->done = (it >= st->maxiter || res <= st->tol) ? 1 : 0;
 }
+
+__global__ void k_cg_step(int P, const double* __restrict__ gathered, CGState* __restrict__ st,
+                          double* __restrict__ history) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  cg_step(P, gathered, st, history);
+}
+
+// One part in one process: the fold of the part's partials ends in the
+// scalar update itself (no gather, no extra launch).
+template <typename T>
+struct AlphaTail {
+  CGState* st;
+  __device__ void operator()(const void* out) const { cg_alpha<T>(1, out, st); }
+};
+struct StepTail {
+  CGState* st;
+  double* hist;
+  __device__ void operator()(const void* out) const { cg_step(1, (const double*)out, st, hist); }
+};
 
 // gathered[p] = *srcs[p] (accsz bytes each): the part values of the parts
 // held by this process, read straight from their devices
@@ -761,13 +821,22 @@ __global__ void k_gather_ptrs(int P, const void* const* __restrict__ srcs, int a
   if (accsz == 16) d[1] = s[1];
 }
 
-void launch_cg_xpby(int dtype, int64_t n, void* u, const void* r, const CGState* st, hipStream_t s) {
-  const int nb = (int)std::min<int64_t>(8192, std::max<int64_t>(1, (n + 255) / 256));
+template <typename T>
+static void cg_xu_t(int64_t n, void* x, void* u, const void* r, const CGState* st, hipStream_t s) {
+  constexpr int V = 16 / sizeof(T);
+  const bool aligned = ((uintptr_t)x | (uintptr_t)u | (uintptr_t)r) % 16 == 0;
+  const int64_t nw = aligned ? (n + V - 1) / V : n;
+  const int nb = (int)std::min<int64_t>(8192, std::max<int64_t>(1, (nw + 255) / 256));
+  if (aligned) hipLaunchKernelGGL((k_cg_xu<T, V>), dim3(nb), dim3(256), 0, s, n, (T*)x, (T*)u, (const T*)r, st);
+  else hipLaunchKernelGGL((k_cg_xu<T, 1>), dim3(nb), dim3(256), 0, s, n, (T*)x, (T*)u, (const T*)r, st);
+}
+
+void launch_cg_xu(int dtype, int64_t n, void* x, void* u, const void* r, const CGState* st, hipStream_t s) {
   switch (dtype) {
-    case PA_F32: hipLaunchKernelGGL(k_cg_xpby<float>, dim3(nb), dim3(256), 0, s, n, (float*)u, (const float*)r, st); break;
-    case PA_F64: hipLaunchKernelGGL(k_cg_xpby<double>, dim3(nb), dim3(256), 0, s, n, (double*)u, (const double*)r, st); break;
-    case PA_C64: hipLaunchKernelGGL(k_cg_xpby<c64>, dim3(nb), dim3(256), 0, s, n, (c64*)u, (const c64*)r, st); break;
-    case PA_C128: hipLaunchKernelGGL(k_cg_xpby<c128>, dim3(nb), dim3(256), 0, s, n, (c128*)u, (const c128*)r, st); break;
+    case PA_F32: cg_xu_t<float>(n, x, u, r, st, s); break;
+    case PA_F64: cg_xu_t<double>(n, x, u, r, st, s); break;
+    case PA_C64: cg_xu_t<c64>(n, x, u, r, st, s); break;
+    case PA_C128: cg_xu_t<c128>(n, x, u, r, st, s); break;
   }
 }
 
@@ -782,6 +851,31 @@ void launch_cg_alpha(int dtype, int P, const void* gathered, CGState* st, hipStr
 
 void launch_cg_step(int P, const double* gathered, CGState* st, double* history, hipStream_t s) {
   hipLaunchKernelGGL(k_cg_step, dim3(1), dim3(64), 0, s, P, gathered, st, history);
+}
+
+// fold the SpMV's dot partials into out, then α (one part per process)
+void launch_fold_cg_alpha(int dtype, int nb, const void* in, void* scratch, void* out, unsigned* ticket,
+                          CGState* st, hipStream_t s) {
+  switch (dtype) {
+    case PA_F32:
+      fold_launch<double>(nb, (const double*)in, (double*)scratch, (double*)out, ticket, AlphaTail<float>{st}, s);
+      break;
+    case PA_F64:
+      fold_launch<double>(nb, (const double*)in, (double*)scratch, (double*)out, ticket, AlphaTail<double>{st}, s);
+      break;
+    case PA_C64:
+      fold_launch<c128>(nb, (const c128*)in, (c128*)scratch, (c128*)out, ticket, AlphaTail<c64>{st}, s);
+      break;
+    case PA_C128:
+      fold_launch<c128>(nb, (const c128*)in, (c128*)scratch, (c128*)out, ticket, AlphaTail<c128>{st}, s);
+      break;
+  }
+}
+
+// fold the Σ|r|² partials into out, then the residual step
+void launch_fold_cg_step(int nb, const void* in, void* scratch, void* out, unsigned* ticket, CGState* st,
+                         double* history, hipStream_t s) {
+  fold_launch<double>(nb, (const double*)in, (double*)scratch, (double*)out, ticket, StepTail{st, history}, s);
 }
 
 void launch_gather_ptrs(int P, const void* const* srcs, int accsz, void* out, hipStream_t s) {
