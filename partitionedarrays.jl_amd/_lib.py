@@ -12,7 +12,8 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libpa_hip.so")
+# PA_HIP_LIB: another build of the same library (A/B tooling only)
+LIB_PATH = os.environ.get("PA_HIP_LIB") or os.path.join(_HERE, "libpa_hip.so")
 
 PA_F32, PA_F64, PA_C64, PA_C128 = 0, 1, 2, 3
 PA_REPLACE, PA_ADD = 0, 1
