@@ -37,12 +37,13 @@ __device__ inline int64_t xcd_remap(int64_t b, int64_t G) {
   return x * q + (x < r ? x : r) + i;
 }
 
-enum { SPMV_NT = 1, SPMV_XCD = 2, SPMV_XPAIR = 4 };
+enum { SPMV_NT = 1, SPMV_XCD = 2, SPMV_XPAIR = 4, SPMV_TAILB = 8 };
 // Process-wide knobs (pa_tune).  Defaults from the A/Bs in
 // profiles/r01_ab_spmv.txt and profiles/r01/ab_xpair.txt: non-temporal
 // streams on, XCD remap off, U = 8, 16 B x runs on (FE27 256³: F64 −9 %,
-// F32 −33 %, C64 −5 % kernel time).
-int g_spmv_flags = SPMV_NT | SPMV_XPAIR;
+// F32 −33 %, C64 −5 % kernel time), predicated tail batch on
+// (profiles/r01/ab_tail.txt: FD7 256³ F64 −31 %, F32 −42 %; FE27 −1…−3 %).
+int g_spmv_flags = SPMV_NT | SPMV_XPAIR | SPMV_TAILB;
 int g_spmv_unroll = 8;
 // dynamic LDS per SpMV block (unused by the kernel): caps the blocks per CU,
 // i.e. the waves streaming at once (160 KB LDS per CU)
@@ -115,10 +116,12 @@ __device__ __forceinline__ c64 pick(bool c, c64 a, c64 b) { return c64{c ? a.re 
 __device__ __forceinline__ c128 pick(bool c, c128 a, c128 b) { return c128{c ? a.re : b.re, c ? a.im : b.im}; }
 
 // int32-column rows: c < 0 is padding (skipped: never multiplied)
+// TB: the entries past the last full U batch run as one masked batch
+// (entries >= len re-read entry len-1 and are never accumulated)
 template <typename T, int R, bool ALPHA, bool NT, int U>
 __device__ __forceinline__ void rows_int32(T (&acc)[R], const IPack<R>* __restrict__ cp,
                                            const Pack<T, R>* __restrict__ vp, int len,
-                                           const T* __restrict__ x, T alpha) {
+                                           const T* __restrict__ x, T alpha, bool TB) {
   int k = 0;
   for (; k + U <= len; k += U) {
     IPack<R> c[U];
@@ -144,6 +147,37 @@ __device__ __forceinline__ void rows_int32(T (&acc)[R], const IPack<R>* __restri
         const T t = acc[r] + v[u].v[r] * xx;
         acc[r] = pick(c[u].c[r] >= 0, t, acc[r]);
       }
+  }
+  if (TB && k < len) {  // the last len % U entries as one masked batch (loads issued together)
+    IPack<R> c[U];
+    Pack<T, R> v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (k + u < len) c[u] = ld<NT>(&cp[(k + u) * 64]);
+      else for (int r = 0; r < R; ++r) c[u].c[r] = -1;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (k + u < len) v[u] = ld<NT>(&vp[(k + u) * 64]);
+    T xv[U][R];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (k + u < len)
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          const int32_t cc = c[u].c[r];
+          xv[u][r] = x[cc >= 0 ? cc : 0];
+        }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        T xx = xv[u][r];
+        if (ALPHA) xx = xx * alpha;
+        const T t = acc[r] + v[u].v[r] * xx;
+        acc[r] = pick(k + u < len && c[u].c[r] >= 0, t, acc[r]);
+      }
+    k = len;
   }
   for (; k < len; ++k) {
     const IPack<R> c = ld<NT>(&cp[k * 64]);
@@ -179,7 +213,7 @@ template <typename T, int R, bool ALPHA, bool NT, int U, bool XP>
 __device__ __forceinline__ void rows_pattern(T (&acc)[R], const int32_t* __restrict__ pat,
                                              const Pack<T, R>* __restrict__ vp, int len,
                                              const T* __restrict__ x, int64_t rbase,
-                                             const bool (&ok)[R], T alpha) {
+                                             const bool (&ok)[R], T alpha, bool TB) {
   int64_t xb[R];
   bool any = false;
 #pragma unroll
@@ -217,6 +251,42 @@ __device__ __forceinline__ void rows_pattern(T (&acc)[R], const int32_t* __restr
         if (ALPHA) xx = xx * alpha;
         acc[r] = acc[r] + v[u].v[r] * xx;
       }
+  }
+  if (TB && k < len) {  // masked tail batch, as in rows_int32
+    int32_t o[U];
+    Pack<T, R> v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) o[u] = pat[min(k + u, len - 1)];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (k + u < len) v[u] = ld<NT>(&vp[(k + u) * 64]);
+    T xv[U][R];
+    if constexpr (XP && R > 1) {
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        if (k + u < len) {
+          const Pack<T, R> xr = ld_xrun<T, R>(x + (any ? rbase + o[u] : 0));
+#pragma unroll
+          for (int r = 0; r < R; ++r) xv[u][r] = xr.v[r];
+        }
+    } else {
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        if (k + u < len)
+#pragma unroll
+          for (int r = 0; r < R; ++r) xv[u][r] = x[xb[r] >= 0 ? xb[r] + o[u] : 0];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (k + u < len) {
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          T xx = xv[u][r];
+          if (ALPHA) xx = xx * alpha;
+          acc[r] = acc[r] + v[u].v[r] * xx;
+        }
+      }
+    k = len;
   }
   for (; k < len; ++k) {
     const int32_t o = pat[k];
@@ -277,19 +347,20 @@ __global__ __launch_bounds__(256) void k_spmv_sell(SpmvArgs<T> a) {
   }
 
   const Pack<T, R>* __restrict__ vp = reinterpret_cast<const Pack<T, R>*>(a.val + off) + lane;
+  const bool tb = (a.flags & SPMV_TAILB) != 0;
   if (PAT) {
     const int32_t* pat = a.pat + s * a.kmax;
     if (a.flags & SPMV_XPAIR) {
-      if (a.flags & SPMV_NT) rows_pattern<T, R, ALPHA, true, U, true>(acc, pat, vp, len, a.x, row0, ok, a.alpha);
-      else rows_pattern<T, R, ALPHA, false, U, true>(acc, pat, vp, len, a.x, row0, ok, a.alpha);
+      if (a.flags & SPMV_NT) rows_pattern<T, R, ALPHA, true, U, true>(acc, pat, vp, len, a.x, row0, ok, a.alpha, tb);
+      else rows_pattern<T, R, ALPHA, false, U, true>(acc, pat, vp, len, a.x, row0, ok, a.alpha, tb);
     } else {
-      if (a.flags & SPMV_NT) rows_pattern<T, R, ALPHA, true, U, false>(acc, pat, vp, len, a.x, row0, ok, a.alpha);
-      else rows_pattern<T, R, ALPHA, false, U, false>(acc, pat, vp, len, a.x, row0, ok, a.alpha);
+      if (a.flags & SPMV_NT) rows_pattern<T, R, ALPHA, true, U, false>(acc, pat, vp, len, a.x, row0, ok, a.alpha, tb);
+      else rows_pattern<T, R, ALPHA, false, U, false>(acc, pat, vp, len, a.x, row0, ok, a.alpha, tb);
     }
   } else {
     const IPack<R>* __restrict__ cp = reinterpret_cast<const IPack<R>*>(a.col + off) + lane;
-    if (a.flags & SPMV_NT) rows_int32<T, R, ALPHA, true, U>(acc, cp, vp, len, a.x, a.alpha);
-    else rows_int32<T, R, ALPHA, false, U>(acc, cp, vp, len, a.x, a.alpha);
+    if (a.flags & SPMV_NT) rows_int32<T, R, ALPHA, true, U>(acc, cp, vp, len, a.x, a.alpha, tb);
+    else rows_int32<T, R, ALPHA, false, U>(acc, cp, vp, len, a.x, a.alpha, tb);
   }
 
   if (a.dotp) {  // fused dot(u, c): Σ conj(u_i)·c_i over this slice's rows
