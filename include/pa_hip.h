@@ -55,6 +55,12 @@ int pa_device_count(int* count);
  * "spmv_unroll" 4 or 8 entries in flight per lane (default 8);
  * "spmv_format" 1: pattern slices where the matrix has them (default),
  *               0: int32 column ids everywhere;
+ * "spmv_patterns" 1..4 offset patterns per slice for matrices built
+ *               afterwards (default 1: single-pattern slices; >1:
+ *               multi-pattern slices where they save bytes);
+ * "spmv_pattern_rule" 1: each slice takes the encoding that streams the
+ *               fewest bytes, 0: a pattern slice whenever half its rows
+ *               follow the pattern (default; matrices built afterwards);
  * "long_rows_exact" 1: long rows summed in the reference's order (default),
  *               0: lane-strided partial sums + tree (within 1e-12);
  * "halo_pull"   1: parts of one process read their neighbours' packed
@@ -201,6 +207,11 @@ int pa_mat_info(const pa_mat* A, int64_t* nrows_owned, int64_t* nnz_owned,
 int pa_mat_format_info(const pa_mat* A, int64_t* pattern_slices,
                        int64_t* regular_rows, int64_t* side_rows,
                        int64_t* side_slots);
+/* Of those pattern slices, the ones holding several offset patterns (one
+ * chosen per 64-lane group of rows; irregular partitions whose runs of
+ * consecutive rows are shorter than a slice); 0 unless
+ * pa_tune("spmv_patterns", n > 1) preceded the build.                     */
+int pa_mat_multipattern_info(const pa_mat* A, int64_t* multi_slices);
 
 /* Long rows (row-length histogram): rows with more than max(256, 8 × the
  * 90th-percentile row length) entries leave the SELL and run one wave per

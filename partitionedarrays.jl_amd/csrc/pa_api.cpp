@@ -26,7 +26,7 @@ void launch_spmv_part(int which, int64_t nwork, const int32_t* list, const pa_ma
                       void* y, const int32_t* ymap, bool has_alpha, int bmode, const void* alpha,
                       const void* beta, void* dotp, hipStream_t st);
 void launch_pattern_detect(pa_mat* A, int64_t noids, int32_t* kind, int32_t* plen, int32_t* pat,
-                           uint64_t* mask, int32_t* pghost, int32_t* nirreg, hipStream_t st);
+                           uint64_t* mask, int32_t* pghost, int32_t* nirreg, int NP, int rule, hipStream_t st);
 void launch_side_len(pa_mat* A, int64_t n, const int32_t* rows, int32_t* len, int64_t noids,
                      int32_t* sghost, hipStream_t st);
 void launch_side_fill(pa_mat* A, const int32_t* rows, const int32_t* len, hipStream_t st);
@@ -42,6 +42,8 @@ void launch_cg_alpha(int dtype, int P, const void* gathered, CGState* cst, hipSt
 void launch_cg_step(int P, const double* gathered, CGState* cst, double* history, hipStream_t st);
 void launch_gather_ptrs(int P, const void* const* srcs, int accsz, void* out, hipStream_t st);
 extern int g_spmv_format;
+extern int g_spmv_pattern_rule;
+extern int g_spmv_patterns;  // patterns per slice at build time (1: single-pattern slices only)
 int g_halo_pull = 1;  // pa_tune("halo_pull"): pull-unpack between parts of one process
 int g_comm_cus = 0;   // pa_tune("comm_cus"): CUs reserved for the comm stream (0: priority stream instead)
 // COO → CSC → SELL on the device (pa_coo.hip)
@@ -278,7 +280,15 @@ int finalize_pattern(pa_mat* A, int kmax, int64_t noids) {
   HIPC(hipMalloc((void**)&d_pghost, ns * 4));
   HIPC(hipMalloc((void**)&d_nirreg, ns * 4));
   HIPC(hipMemsetAsync(A->d_mask, 0, ns * W * 8, st));
-  launch_pattern_detect(A, noids, A->d_kind, A->d_plen, A->d_pat, A->d_mask, d_pghost, d_nirreg, st);
+  const int NP = g_spmv_patterns;
+  if (NP > 1) {  // multi-pattern candidates (kept only if some slice takes them)
+    A->kmp = std::min(PA_MP_K, (A->kmax + 3) / 4 * 4);
+    HIPC(hipMalloc((void**)&A->d_mpat, ns * PA_MP_NP * A->kmp * 4));
+    HIPC(hipMalloc((void**)&A->d_psel, ns * 64));
+    HIPC(hipMemsetAsync(A->d_mpat, 0, ns * PA_MP_NP * A->kmp * 4, st));
+    HIPC(hipMemsetAsync(A->d_psel, 0, ns * 64, st));
+  }
+  launch_pattern_detect(A, noids, A->d_kind, A->d_plen, A->d_pat, A->d_mask, d_pghost, d_nirreg, NP, g_spmv_pattern_rule, st);
   HIPC(hipGetLastError());
   std::vector<int32_t> kind(ns), pghost(ns), nirreg(ns);
   std::vector<uint64_t> mask(ns * W);
@@ -289,9 +299,10 @@ int finalize_pattern(pa_mat* A, int kmax, int64_t noids) {
   HIPC(hipStreamSynchronize(st));
   dev_free(d_pghost);
   dev_free(d_nirreg);
-  std::vector<int32_t> pint, pbnd, xint, xbnd, side;
+  std::vector<int32_t> pint, pbnd, xint, xbnd, mint, mbnd, side;
   for (int64_t s = 0; s < ns; ++s) {
-    if (kind[s]) (pghost[s] ? pbnd : pint).push_back((int32_t)s);
+    if (kind[s] == 1) (pghost[s] ? pbnd : pint).push_back((int32_t)s);
+    else if (kind[s] == 2) (pghost[s] ? mbnd : mint).push_back((int32_t)s);
     else (pghost[s] ? xbnd : xint).push_back((int32_t)s);
     if (kind[s]) {
       ++A->npattern_slices;
@@ -306,9 +317,18 @@ int finalize_pattern(pa_mat* A, int kmax, int64_t noids) {
   A->np_bnd = (int64_t)pbnd.size();
   A->nx_int = (int64_t)xint.size();
   A->nx_bnd = (int64_t)xbnd.size();
+  A->nm_int = (int64_t)mint.size();
+  A->nm_bnd = (int64_t)mbnd.size();
   if (dev_upload(&A->d_pint_list, pint) || dev_upload(&A->d_pbnd_list, pbnd) ||
-      dev_upload(&A->d_xint_list, xint) || dev_upload(&A->d_xbnd_list, xbnd))
+      dev_upload(&A->d_xint_list, xint) || dev_upload(&A->d_xbnd_list, xbnd) ||
+      dev_upload(&A->d_mint_list, mint) || dev_upload(&A->d_mbnd_list, mbnd))
     return -1;
+  if (mint.empty() && mbnd.empty()) {  // no slice took several patterns
+    dev_free(A->d_mpat);
+    dev_free(A->d_psel);
+    A->d_mpat = nullptr;
+    A->d_psel = nullptr;
+  }
   // side SELL
   A->s_nrows = (int64_t)side.size();
   if (A->s_nrows > 0) {
@@ -603,6 +623,14 @@ int pa_tune(const char* key, int value, int* previous) {
   } else if (!std::strcmp(key, "spmv_format")) {
     CHECK_ARG(value == 0 || value == 1, "spmv_format: 0 = int32 columns, 1 = pattern slices");
     slot = &g_spmv_format;
+  } else if (!std::strcmp(key, "spmv_patterns")) {
+    CHECK_ARG(value >= 1 && value <= PA_MP_NP,
+              "spmv_patterns: offset patterns per slice for matrices built afterwards (1..4; 1 = single-pattern slices)");
+    slot = &g_spmv_patterns;
+  } else if (!std::strcmp(key, "spmv_pattern_rule")) {
+    CHECK_ARG(value == 0 || value == 1,
+              "spmv_pattern_rule: 1 = slice encoding by streamed bytes, 0 = pattern slice when half its rows follow one");
+    slot = &g_spmv_pattern_rule;
   } else {
     PA_FAIL(std::string("pa_tune: unknown key ") + key);
   }
@@ -1414,7 +1442,8 @@ int pa_mat_destroy(pa_mat* A) {
   dev_free(A->d_bnd_list);
   dev_free(A->d_col);
   dev_free(A->d_val);
-  for (void* p : {(void*)A->d_kind, (void*)A->d_plen, (void*)A->d_pat, (void*)A->d_mask,
+  for (void* p : {(void*)A->d_kind, (void*)A->d_plen, (void*)A->d_pat, (void*)A->d_mask, (void*)A->d_mpat,
+                  (void*)A->d_psel, (void*)A->d_mint_list, (void*)A->d_mbnd_list,
                   (void*)A->d_pint_list, (void*)A->d_pbnd_list, (void*)A->d_xint_list,
                   (void*)A->d_xbnd_list, (void*)A->d_s_off, (void*)A->d_s_len,
                   (void*)A->d_s_col, A->d_s_val, (void*)A->d_s_rowmap, (void*)A->d_s_rowlen, A->d_dotp,
@@ -1432,6 +1461,12 @@ int pa_mat_format_info(const pa_mat* A, int64_t* pattern_slices, int64_t* regula
   if (regular_rows) *regular_rows = A->nregular_rows;
   if (side_rows) *side_rows = A->s_nrows;
   if (side_slots) *side_slots = A->s_slots;
+  return 0;
+}
+
+int pa_mat_multipattern_info(const pa_mat* A, int64_t* multi_slices) {
+  CHECK_ARG(A, "null matrix");
+  if (multi_slices) *multi_slices = A->nm_int + A->nm_bnd;
   return 0;
 }
 
@@ -1513,6 +1548,7 @@ static int spmv_impl(int n, pa_mat* const A[], pa_vec* const y[], const pa_index
     // interior slices (no ghost column): overlap with the halo transport
     if (g_spmv_format == 1 && A[i]->has_pat) {
       launch_spmv_part(0, A[i]->np_int, A[i]->d_pint_list, A[i], x[i]->d, y[i]->d, ymap, has_alpha, bmode, alpha, beta, dotp[i], SM(c));
+      launch_spmv_part(3, A[i]->nm_int, A[i]->d_mint_list, A[i], x[i]->d, y[i]->d, ymap, has_alpha, bmode, alpha, beta, dotp[i], SM(c));
       launch_spmv_part(1, A[i]->nx_int, A[i]->d_xint_list, A[i], x[i]->d, y[i]->d, ymap, has_alpha, bmode, alpha, beta, dotp[i], SM(c));
     } else if (A[i]->d_bnd_list) {  // split layout (the interior list may be empty)
       if (A[i]->nslices_int > 0)
@@ -1537,6 +1573,7 @@ static int spmv_impl(int n, pa_mat* const A[], pa_vec* const y[], const pa_index
     if (g_spmv_format == 1 && A[i]->has_pat) {
       // pattern slices reading ghosts, then the side rows (after the halo)
       launch_spmv_part(0, A[i]->np_bnd, A[i]->d_pbnd_list, A[i], x[i]->d, y[i]->d, ymap, has_alpha, bmode, alpha, beta, dotp[i], SM(c));
+      launch_spmv_part(3, A[i]->nm_bnd, A[i]->d_mbnd_list, A[i], x[i]->d, y[i]->d, ymap, has_alpha, bmode, alpha, beta, dotp[i], SM(c));
       launch_spmv_part(1, A[i]->nx_bnd, A[i]->d_xbnd_list, A[i], x[i]->d, y[i]->d, ymap, has_alpha, bmode, alpha, beta, dotp[i], SM(c));
       launch_spmv_part(2, A[i]->s_nslices, nullptr, A[i], x[i]->d, y[i]->d, ymap, has_alpha, bmode, alpha, beta, dotp[i], SM(c));
     } else if (A[i]->d_bnd_list) {

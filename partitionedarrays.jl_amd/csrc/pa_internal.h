@@ -290,6 +290,8 @@ struct pa_xchg {
   pa_combine_plan plan_rev;   // unpack targets = lids_snd (reverse/assemble)
 };
 
+constexpr int PA_MP_NP = 4;   // offset patterns per multi-pattern slice
+constexpr int PA_MP_K = 64;   // longest pattern a multi-pattern slice takes
 constexpr size_t kVecPad = 64;  // bytes before and after a vector's values (pa_vec_create)
 
 struct pa_vec {
@@ -358,6 +360,15 @@ struct pa_mat {
   int32_t* d_xbnd_list = nullptr;    // pattern mode: int32-column slices with ghost columns
   int64_t nx_int = 0, nx_bnd = 0;
   int64_t npattern_slices = 0, nregular_rows = 0;
+  // multi-pattern slices (kind 2): up to PA_MP_NP offset patterns per slice,
+  // one chosen per lane (d_psel); for irregular partitions whose x-runs are
+  // shorter than a slice (C5).  Patterns of at most PA_MP_K entries.
+  int32_t* d_mpat = nullptr;         // nslices*PA_MP_NP*kmp offsets
+  uint8_t* d_psel = nullptr;         // nslices*64 pattern index per lane
+  int kmp = 0;                       // pattern stride (<= PA_MP_K)
+  int32_t* d_mint_list = nullptr;    // multi-pattern slices without ghost reads
+  int32_t* d_mbnd_list = nullptr;    // multi-pattern slices reading ghosts
+  int64_t nm_int = 0, nm_bnd = 0;
   // side SELL: the irregular rows of pattern slices (row map → oid)
   int64_t s_nrows = 0, s_nslices = 0, s_slots = 0;
   int64_t* d_s_off = nullptr;

@@ -49,6 +49,13 @@ int g_spmv_unroll = 8;
 // i.e. the waves streaming at once (160 KB LDS per CU)
 int g_spmv_lds = 0;
 int g_spmv_format = 1;  // 1: pattern slices where built, 0: int32 columns only
+// Build-time encoding knobs.  Defaults from profiles/r01/multipattern/README.md
+// (C5 Voronoi parts): multi-pattern slices stream up to 12 % fewer bytes but
+// add a launch per phase and per-lane LDS offset reads; kernel time is flat
+// to +25 % except F32 at 256³ on 8 parts (-9 %), so they stay opt-in, and
+// the byte-cost rule moves kernel time by ±4 % either way.
+int g_spmv_patterns = 1;         // patterns per slice (multi-pattern slices when > 1)
+int g_spmv_pattern_rule = 0;     // 1: slice encoding by streamed bytes, 0: pattern slice when half the rows follow it
 
 template <int BYTES> struct RawOf;
 template <> struct RawOf<4> { typedef unsigned int type; };
@@ -74,9 +81,10 @@ struct SpmvArgs {
   const int32_t* slen;      // entries per row of the slice
   const int32_t* col;
   const T* val;
-  const int32_t* pat;       // kmax offsets per slice
+  const int32_t* pat;       // kmax offsets per slice (multi-pattern: PA_MP_NP*kmax)
   const uint64_t* mask;     // H/64 words per slice
   int kmax;
+  const uint8_t* psel;      // multi-pattern: pattern of each lane (64 per slice)
   const int32_t* rowmap;    // structure row → oid (side SELL), null: identity
   int64_t nrows;            // rows of this structure
   const T* x;
@@ -302,11 +310,13 @@ __device__ __forceinline__ void rows_pattern(T (&acc)[R], const int32_t* __restr
 
 // BMODE: 0 → acc = 0 (β == 0: fill!(co,0)), 1 → acc = y (β == 1),
 //        2 → acc = y*β (rmul!(co,β)).  Interfaces.jl:2262-2263.
-// PAT: the launch's slices are pattern slices (implied columns for the rows
-// of their mask) or int32-column slices; one kernel per kind keeps the hot
-// loop free of the other's code and registers.
-template <typename T, int R, bool ALPHA, int BMODE, int U, bool PAT>
+// PK: the launch's slices are int32-column slices (0), pattern slices (1:
+// implied columns for the rows of their mask) or multi-pattern slices (2:
+// the same with one of PA_MP_NP patterns per lane, staged in LDS); one
+// kernel per kind keeps the hot loop free of the others' code and registers.
+template <typename T, int R, bool ALPHA, int BMODE, int U, int PK>
 __global__ __launch_bounds__(256) void k_spmv_sell(SpmvArgs<T> a) {
+  constexpr bool PAT = PK != 0;
   constexpr int H = 64 * R;
   const int lane = threadIdx.x & 63;
   const int64_t blk = (a.flags & SPMV_XCD) ? xcd_remap(blockIdx.x, gridDim.x) : (int64_t)blockIdx.x;
@@ -348,7 +358,24 @@ __global__ __launch_bounds__(256) void k_spmv_sell(SpmvArgs<T> a) {
 
   const Pack<T, R>* __restrict__ vp = reinterpret_cast<const Pack<T, R>*>(a.val + off) + lane;
   const bool tb = (a.flags & SPMV_TAILB) != 0;
-  if (PAT) {
+  if constexpr (PK == 2) {
+    // this wave's patterns → LDS; each lane reads its own pattern's offsets
+    __shared__ int32_t spat[4][PA_MP_NP * PA_MP_K];
+    int32_t* wp = spat[threadIdx.x >> 6];
+    const int np = PA_MP_NP * a.kmax;
+    for (int i = lane; i < np; i += 64) wp[i] = a.pat[s * np + i];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const int32_t* pat = wp + (int)a.psel[s * 64 + lane] * a.kmax;
+    if (a.flags & SPMV_XPAIR) {
+      if (a.flags & SPMV_NT) rows_pattern<T, R, ALPHA, true, U, true>(acc, pat, vp, len, a.x, row0, ok, a.alpha, tb);
+      else rows_pattern<T, R, ALPHA, false, U, true>(acc, pat, vp, len, a.x, row0, ok, a.alpha, tb);
+    } else {
+      if (a.flags & SPMV_NT) rows_pattern<T, R, ALPHA, true, U, false>(acc, pat, vp, len, a.x, row0, ok, a.alpha, tb);
+      else rows_pattern<T, R, ALPHA, false, U, false>(acc, pat, vp, len, a.x, row0, ok, a.alpha, tb);
+    }
+  } else if constexpr (PK == 1) {
     const int32_t* pat = a.pat + s * a.kmax;
     if (a.flags & SPMV_XPAIR) {
       if (a.flags & SPMV_NT) rows_pattern<T, R, ALPHA, true, U, true>(acc, pat, vp, len, a.x, row0, ok, a.alpha, tb);
@@ -389,7 +416,7 @@ __global__ __launch_bounds__(256) void k_spmv_sell(SpmvArgs<T> a) {
   }
 }
 
-template <typename T, int R, bool ALPHA, int BMODE, bool PAT>
+template <typename T, int R, bool ALPHA, int BMODE, int PAT>
 static void launch_t(const SpmvArgs<T>& a, hipStream_t st) {
   const int64_t blocks = (a.nwork + 3) / 4;
   if (blocks == 0) return;
@@ -399,7 +426,7 @@ static void launch_t(const SpmvArgs<T>& a, hipStream_t st) {
     hipLaunchKernelGGL((k_spmv_sell<T, R, ALPHA, BMODE, 8, PAT>), dim3(blocks), dim3(256), g_spmv_lds, st, a);
 }
 
-template <typename T, int R, bool PAT>
+template <typename T, int R, int PAT>
 static void launch_ab(const SpmvArgs<T>& a, bool has_alpha, int bmode, hipStream_t st) {
   if (!has_alpha) {
     if (bmode == 0) launch_t<T, R, false, 0, PAT>(a, st);
@@ -413,7 +440,8 @@ static void launch_ab(const SpmvArgs<T>& a, bool has_alpha, int bmode, hipStream
 }
 
 // which = 0: pattern slices of the main structure; 1: int32-column slices
-// of the main structure; 2: side SELL.  list/nwork select the slices.
+// of the main structure; 2: side SELL; 3: multi-pattern slices of the main
+// structure.  list/nwork select the slices.
 template <typename T, int R>
 static void launch_which(int which, int64_t nwork, const int32_t* list, const pa_mat* A, const void* x,
                          void* y, const int32_t* ymap, bool has_alpha, int bmode, const void* alpha,
@@ -447,6 +475,12 @@ static void launch_which(int which, int64_t nwork, const int32_t* list, const pa
       a.pat = A->d_pat;
       a.mask = A->d_mask;
       a.kmax = A->kmax;
+    } else if (which == 3) {
+      a.slen = A->d_plen;
+      a.pat = A->d_mpat;
+      a.mask = A->d_mask;
+      a.kmax = A->kmp;
+      a.psel = A->d_psel;
     } else {
       a.slen = A->d_slice_len;
     }
@@ -455,8 +489,9 @@ static void launch_which(int which, int64_t nwork, const int32_t* list, const pa
     a.sflags = A->d_sflags;
     a.lmask = A->d_lmask;
   }
-  if (which == 0) launch_ab<T, R, true>(a, has_alpha, bmode, st);
-  else launch_ab<T, R, false>(a, has_alpha, bmode, st);
+  if (which == 0) launch_ab<T, R, 1>(a, has_alpha, bmode, st);
+  else if (which == 3) launch_ab<T, R, 2>(a, has_alpha, bmode, st);
+  else launch_ab<T, R, 0>(a, has_alpha, bmode, st);
 }
 
 // ---------------------------------------------------------------------------
@@ -954,22 +989,31 @@ void launch_gather_ptrs(int P, const void* const* srcs, int accsz, void* out, hi
 }
 
 // ---------------------------------------------------------------------------
-// Pattern detection (one wave per slice).  Candidate: the middle valid row
-// of the slice; its offsets pat[k] = col_k - row.  A row is regular when its
-// column sequence is exactly row + pat[k] (same length).  A slice becomes a
-// pattern slice when at least half of its valid rows are regular.
+// Pattern detection (one wave per slice).  Candidate 0: the middle valid row
+// of the slice; its offsets pat[k] = col_k - row.  A row is regular for a
+// candidate when its column sequence is exactly row + pat[k] (same length).
+// Multi-pattern (NP > 1): while lanes are left without a pattern, the first
+// such lane's first full-length row becomes the next candidate; each lane
+// takes the first candidate that one of its rows follows, and its rows that
+// follow it are regular.  The slice keeps the cheapest encoding by streamed
+// bytes: int32 (S+4 per slot), single pattern or multi-pattern (S per slot
+// plus S+4 again for every side row's entry); multi-pattern must save more
+// than 1/16 of the int32 cost over the next best to be taken.
 
 template <int R>
 __global__ __launch_bounds__(256) void k_pattern_detect(int64_t nrows, int64_t nslices,
                                                         const int64_t* __restrict__ soff,
                                                         const int32_t* __restrict__ slen,
                                                         const int32_t* __restrict__ col, int64_t noids,
-                                                        int kmax, int32_t* __restrict__ kind,
+                                                        int kmax, int S, int NP, int kmp, int rule,
+                                                        int32_t* __restrict__ kind,
                                                         int32_t* __restrict__ plen,
                                                         int32_t* __restrict__ pat,
                                                         uint64_t* __restrict__ mask,
                                                         int32_t* __restrict__ pghost,
-                                                        int32_t* __restrict__ nirreg) {
+                                                        int32_t* __restrict__ nirreg,
+                                                        int32_t* __restrict__ mpat,
+                                                        uint8_t* __restrict__ psel) {
   constexpr int H = 64 * R;
   const int lane = threadIdx.x & 63;
   const int64_t s = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -979,66 +1023,129 @@ __global__ __launch_bounds__(256) void k_pattern_detect(int64_t nrows, int64_t n
   const int64_t rem = nrows - s * H;
   const int nvalid = (int)(rem < H ? rem : H);
   const int m = nvalid / 2;
-  const int64_t mrow = s * H + m;
   const int mlane = m / R, mr = m % R;
   int Lp = 0;
   for (int k = 0; k < L; ++k) {
     if (col[off + ((int64_t)k * 64 + mlane) * R + mr] < 0) break;
     ++Lp;
   }
-  int nreg = 0;
-  bool ghost_reg = false, ghost_any = false;
-  uint64_t bits[(R + 63) / 64 + 1] = {0};
-  (void)bits;
+  // row lengths (entries before the first padding slot) and ghost columns
+  int rlen[R];
+  bool ghost_any = false;
+#pragma unroll
   for (int r = 0; r < R; ++r) {
     const int i = lane * R + r;
-    const int64_t row = s * H + i;
     const bool valid = i < nvalid;
-    bool reg = valid && Lp > 0;
-    bool g = false;
+    int l = 0;
+    bool pad = false;
     for (int k = 0; k < L; ++k) {
       const int32_t c = col[off + ((int64_t)k * 64 + lane) * R + r];
+      if (c < 0) pad = true;
+      else if (pad) l = -(1 << 30);  // a column after padding: never regular
+      else ++l;
       if (valid && c >= noids) ghost_any = true;
-      if (k < Lp) {
-        const int32_t cm = col[off + ((int64_t)k * 64 + mlane) * R + mr];
-        const int64_t e = row + (int64_t)(cm - mrow);
+    }
+    rlen[r] = valid ? l : -1;
+  }
+  // rows of this lane regular for candidate (clane, cr): bit r; g = reads a ghost
+  auto follow = [&](int clane, int cr, bool& g) -> unsigned {
+    const int64_t crow = s * H + clane * R + cr;
+    unsigned bits = 0;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const int64_t row = s * H + lane * R + r;
+      bool reg = Lp > 0 && rlen[r] == Lp;
+      bool gr = false;
+      for (int k = 0; k < Lp; ++k) {
+        const int32_t cm = col[off + ((int64_t)k * 64 + clane) * R + cr];
+        const int32_t c = col[off + ((int64_t)k * 64 + lane) * R + r];
+        const int64_t e = row + (int64_t)(cm - crow);
         if ((int64_t)c != e) reg = false;
-        if (e >= noids) g = true;
-      } else if (c != -1) {
-        reg = false;
+        if (e >= noids) gr = true;
+      }
+      if (reg) {
+        bits |= 1u << r;
+        g = g || gr;
       }
     }
-    if (reg) {
-      ++nreg;
-      ghost_reg = ghost_reg || g;
-      atomicOr((unsigned long long*)&mask[s * (H / 64) + i / 64], 1ull << (i & 63));
-    }
-  }
-  // wave sums
-  int tot = nreg;
-  for (int d = 32; d >= 1; d >>= 1) tot += __shfl_xor(tot, d, 64);
-  const bool gr = __any(ghost_reg);
-  const bool ga = __any(ghost_any);
-  const bool is_pat = Lp > 0 && 2 * tot >= nvalid;
-  if (lane == 0) {
-    kind[s] = is_pat ? 1 : 0;
-    plen[s] = is_pat ? Lp : L;
-    pghost[s] = is_pat ? (gr ? 1 : 0) : (ga ? 1 : 0);
-    nirreg[s] = is_pat ? nvalid - tot : 0;
-  }
-  if (is_pat)
+    return bits;
+  };
+  auto wave_count = [&](unsigned bits) {
+    int t = __popc(bits);
+    for (int d = 32; d >= 1; d >>= 1) t += __shfl_xor(t, d, 64);
+    return t;
+  };
+  auto store_pat = [&](int32_t* dst, int clane, int cr) {
+    const int64_t crow = s * H + clane * R + cr;
     for (int k = lane; k < Lp; k += 64)
-      pat[s * kmax + k] = col[off + ((int64_t)k * 64 + mlane) * R + mr] - (int32_t)mrow;
+      dst[k] = col[off + ((int64_t)k * 64 + clane) * R + cr] - (int32_t)crow;
+  };
+  bool g1 = false;
+  const unsigned bits1 = follow(mlane, mr, g1);
+  const int tot1 = wave_count(bits1);
+  // multi-pattern passes
+  const bool mp = NP > 1 && Lp > 0 && Lp <= kmp && tot1 < nvalid;
+  unsigned bitsM = bits1;
+  int sel = bits1 ? 0 : -1;
+  bool gM = g1;
+  int totM = tot1;
+  if (mp) {
+    store_pat(mpat + (s * PA_MP_NP) * kmp, mlane, mr);
+    for (int p = 1; p < NP; ++p) {
+      int myr = -1;
+      if (sel < 0)
+        for (int r = R - 1; r >= 0; --r)
+          if (rlen[r] == Lp) myr = r;
+      const uint64_t b = __ballot(myr >= 0);
+      if (b == 0) break;
+      const int cl = __ffsll((unsigned long long)b) - 1;
+      const int cr = __shfl(myr, cl, 64);
+      bool g = false;
+      const unsigned bits = follow(cl, cr, g);
+      if (sel < 0 && bits) {
+        sel = p;
+        bitsM |= bits;
+        gM = gM || g;
+      }
+      store_pat(mpat + (s * PA_MP_NP + p) * kmp, cl, cr);
+    }
+    totM = wave_count(bitsM);
+  }
+  const int64_t SI = S + 4;
+  const int64_t c_int = SI * nvalid;
+  const int64_t c_one = (int64_t)S * nvalid + SI * (nvalid - tot1);
+  const int64_t c_mp = (int64_t)S * nvalid + SI * (nvalid - totM);
+  int best = 0;
+  int64_t bc = c_int;
+  if (Lp > 0 && (rule ? c_one < bc : 2 * tot1 >= nvalid)) { best = 1; bc = c_one; }
+  if (mp && c_mp + c_int / 16 < bc) { best = 2; bc = c_mp; }
+  const bool gr = __any(best == 1 ? g1 : gM);
+  const bool ga = __any(ghost_any);
+  const int tot = best == 1 ? tot1 : totM;
+  if (lane == 0) {
+    kind[s] = best;
+    plen[s] = best ? Lp : L;
+    pghost[s] = best ? (gr ? 1 : 0) : (ga ? 1 : 0);
+    nirreg[s] = best ? nvalid - tot : 0;
+  }
+  const unsigned bits = best == 1 ? bits1 : (best == 2 ? bitsM : 0u);
+  if (bits) {
+    const int i0 = lane * R;
+    atomicOr((unsigned long long*)&mask[s * (H / 64) + i0 / 64], (unsigned long long)bits << (i0 & 63));
+  }
+  if (psel && mp) psel[s * 64 + lane] = (uint8_t)(best == 2 && sel > 0 ? sel : 0);
+  if (best == 1) store_pat(pat + s * kmax, mlane, mr);
 }
 
 void launch_pattern_detect(pa_mat* A, int64_t noids, int32_t* kind, int32_t* plen, int32_t* pat,
-                           uint64_t* mask, int32_t* pghost, int32_t* nirreg, hipStream_t st) {
+                           uint64_t* mask, int32_t* pghost, int32_t* nirreg, int NP, int rule, hipStream_t st) {
   const int64_t blocks = (A->nslices + 3) / 4;
   if (blocks == 0) return;
-#define PA_DET(RR)                                                                                   \
-  hipLaunchKernelGGL(k_pattern_detect<RR>, dim3(blocks), dim3(256), 0, st, A->nrows, A->nslices,     \
-                     A->d_slice_off, A->d_slice_len, A->d_col, noids, A->kmax, kind, plen, pat, mask, \
-                     pghost, nirreg)
+  const int S = (int)dtype_size(A->dtype);
+#define PA_DET(RR)                                                                                      \
+  hipLaunchKernelGGL(k_pattern_detect<RR>, dim3(blocks), dim3(256), 0, st, A->nrows, A->nslices,        \
+                     A->d_slice_off, A->d_slice_len, A->d_col, noids, A->kmax, S, NP, A->kmp, rule, kind, plen, \
+                     pat, mask, pghost, nirreg, A->d_mpat, A->d_psel)
   switch (A->R) {
     case 1: PA_DET(1); break;
     case 2: PA_DET(2); break;

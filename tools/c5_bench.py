@@ -2,8 +2,11 @@
 all parts on device 0, F64/F32/C128/C64.  Reports mul! time (halo included:
 device copies between the parts), algorithmic GB/s over all parts, and the
 column-encoding coverage (pattern slices / regular rows) of the parts.
+--patterns A/Bs the offset patterns per slice (pa_tune("spmv_patterns"),
+1 = single-pattern slices); each build also reports the parts' SpMV kernel
+time (HIP events on the parts' streams, summed over the parts).
 
-    python tools/c5_bench.py [--n 128] [--parts 8] [--dtypes f64,f32,c128,c64]
+    python tools/c5_bench.py [--n 128] [--parts 8] [--dtypes f64,f32,c128,c64] [--patterns 1,4] [--share]
 """
 import argparse
 import json
@@ -22,14 +25,20 @@ ap.add_argument("--n", type=int, default=128)
 ap.add_argument("--parts", type=int, default=8)
 ap.add_argument("--dtypes", default="f64,f32,c128,c64")
 ap.add_argument("--steps", type=int, default=20)
+ap.add_argument("--patterns", default="4")
+ap.add_argument("--rules", default="1", help="pa_tune spmv_pattern_rule values to A/B")
+ap.add_argument("--share", action="store_true", help="parts as one in-order chain (share_streams)")
 a = ap.parse_args()
 DT = {"f64": np.float64, "f32": np.float32, "c128": np.complex128, "c64": np.complex64}
-be = pamd.HIPBackend(devices=[0])
+be = pamd.HIPBackend(devices=[0], share_streams=a.share)
 parts = be.get_part_ids(a.parts)
 N = (a.n,) * 3
 owners = pamd.drivers.voronoi_owners(N, a.parts)
-for name in a.dtypes.split(","):
+for name, npat, rule in [(d, int(q), int(r)) for d in a.dtypes.split(",") for q in a.patterns.split(",")
+                         for r in a.rules.split(",")]:
     dtype = DT[name]
+    pamd._lib.tune("spmv_patterns", npat)
+    pamd._lib.tune("spmv_pattern_rule", rule)
     t0 = time.perf_counter()
     A = pamd.drivers.irregular_problem(parts, N, 27, dtype, owners=owners)
     setup = time.perf_counter() - t0
@@ -45,7 +54,7 @@ for name in a.dtypes.split(","):
         ex = A.cols.exchanger
         B += (f["nnz"] * (S + 4) + (f["nrows"] + 1) * 4 + (f["nrows"] + s.num_hids) * S + f["nrows"] * S
               + (len(ex.lids_snd.local(p).data) + len(ex.lids_rcv.local(p).data)) * (4 + 2 * S))
-        for k in ("nslices", "pattern_slices", "nrows", "regular_rows", "side_rows"):
+        for k in ("nslices", "pattern_slices", "multi_pattern_slices", "nrows", "regular_rows", "side_rows"):
             info[k] = info.get(k, 0) + f[k]
     for _ in range(3):
         pamd.mul_(y, A, x)
@@ -57,6 +66,19 @@ for name in a.dtypes.split(","):
     for p in parts.part_ids:
         be.context(p).sync()
     t = (time.perf_counter() - t0) / a.steps
+    ctxs = [be.context(p) for p in parts.part_ids]
+    for c in ctxs:
+        c.set_timing(True)
+    kms = []
+    for _ in range(5):
+        pamd.mul_(y, A, x)
+        kms.append(sum(sum(c.last_kernel_ms()) for c in ctxs))
+    for c in ctxs:
+        c.set_timing(False)
+        c.sync()
+    km = float(np.median(kms))
     print(json.dumps({"config": f"C5 FE27 {a.n}^3 Voronoi {a.parts} parts on 1 GPU", "dtype": name,
+                      "spmv_patterns": npat, "spmv_pattern_rule": rule, "share_streams": a.share,
                       "ms_per_mul": round(1e3 * t, 4), "gbs_algorithmic_all_parts": round(B / t / 1e9, 1),
+                      "kernel_ms_sum_over_parts": round(km, 4), "gbs_algorithmic_kernels": round(B / km / 1e6, 1),
                       "setup_s": round(setup, 2), "format": info}), flush=True)
