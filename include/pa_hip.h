@@ -51,7 +51,8 @@ int pa_device_count(int* count);
  * "spmv_flags"  bit 0: non-temporal value/column streams, bit 1: XCD-aware
  *               slice mapping, bit 2: pattern rows fetch x as 16 B runs,
  *               bit 3: the last len % U entries of a slice as one
- *               predicated batch (default 13);
+ *               predicated batch, bit 4: a slice list covering the whole
+ *               structure is launched without the list (default 29);
  * "spmv_unroll" 4 or 8 entries in flight per lane (default 8);
  * "spmv_format" 1: pattern slices where the matrix has them (default),
  *               0: int32 column ids everywhere;

@@ -37,13 +37,14 @@ __device__ inline int64_t xcd_remap(int64_t b, int64_t G) {
   return x * q + (x < r ? x : r) + i;
 }
 
-enum { SPMV_NT = 1, SPMV_XCD = 2, SPMV_XPAIR = 4, SPMV_TAILB = 8 };
+enum { SPMV_NT = 1, SPMV_XCD = 2, SPMV_XPAIR = 4, SPMV_TAILB = 8, SPMV_IDLIST = 16 };
 // Process-wide knobs (pa_tune).  Defaults from the A/Bs in
 // profiles/r01_ab_spmv.txt and profiles/r01/ab_xpair.txt: non-temporal
 // streams on, XCD remap off, U = 8, 16 B x runs on (FE27 256³: F64 −9 %,
 // F32 −33 %, C64 −5 % kernel time), predicated tail batch on
-// (profiles/r01/ab_tail.txt: FD7 256³ F64 −31 %, F32 −42 %; FE27 −1…−3 %).
-int g_spmv_flags = SPMV_NT | SPMV_XPAIR | SPMV_TAILB;
+// (profiles/r01/ab_tail.txt: FD7 256³ F64 −31 %, F32 −42 %; FE27 −1…−3 %),
+// identity slice lists dropped (profiles/r01/ab_idlist.txt: FD7 −0.9 %, FE27 ±0).
+int g_spmv_flags = SPMV_NT | SPMV_XPAIR | SPMV_TAILB | SPMV_IDLIST;
 int g_spmv_unroll = 8;
 // dynamic LDS per SpMV block (unused by the kernel): caps the blocks per CU,
 // i.e. the waves streaming at once (160 KB LDS per CU)
@@ -687,6 +688,9 @@ void launch_spmv_long(const pa_mat* A, const void* x, void* y, const int32_t* ym
 void launch_spmv_part(int which, int64_t nwork, const int32_t* list, const pa_mat* A, const void* x,
                       void* y, const int32_t* ymap, bool has_alpha, int bmode, const void* alpha,
                       const void* beta, void* dotp, hipStream_t st) {
+  // a slice list as long as the structure is 0..nslices-1 (lists are
+  // ascending subsets): launch without it, one dependent load less per wave
+  if ((g_spmv_flags & SPMV_IDLIST) && list && which != 2 && nwork == A->nslices) list = nullptr;
   switch (A->dtype) {
     case PA_F32: launch_which<float, 4>(which, nwork, list, A, x, y, ymap, has_alpha, bmode, alpha, beta, dotp, st); break;
     case PA_F64: launch_which<double, 2>(which, nwork, list, A, x, y, ymap, has_alpha, bmode, alpha, beta, dotp, st); break;
