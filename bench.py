@@ -105,6 +105,16 @@ def pmc_traffic(args, steps=5):
                      f"FETCH_SIZE {tot['FETCH_SIZE']:.0f} KB x2 (gfx950) + WRITE_SIZE {tot['WRITE_SIZE']:.0f} KB per step")
 
 
+def box_hbm_gbs(pamd, nbytes, reps=10):
+    """Attainable HBM rates of this box (pa_hbm_probe: 16 B non-temporal
+    read-only and copy sweeps of an `nbytes` buffer, best of three grid
+    sizes).  A calibration beside the roofline, not the metric."""
+    try:
+        return pamd._lib.hbm_probe(0, nbytes, reps)
+    except pamd._lib.PAError:
+        return None
+
+
 def child_pmc(args):
     """the profiled child of pmc_traffic: build the operator, run warmup+steps."""
     import pamd
@@ -315,6 +325,7 @@ def main():
     prev = pamd._lib.tune("spmv_format", 0)
     kernel_ms_int32 = kernel_time(reps)
     pamd._lib.tune("spmv_format", prev)
+    box = box_hbm_gbs(pamd, spmv_bytes // 2) if world == 1 and ngpu == 1 else None
     traffic, traffic_note = (None, "skipped (--no-pmc)")
     if rank == 0 and ngpu == 1 and not args.no_pmc:
         traffic, traffic_note = pmc_traffic(args)
@@ -366,6 +377,13 @@ def main():
                               f"regular rows {info['regular_rows']}/{info['nrows']}, side rows {info['side_rows']}"),
             "int32_columns_kernel_ms": round(kernel_ms_int32, 4),
             "int32_columns_achieved": round(spmv_bytes / (kernel_ms_int32 * 1e-3) / 1e9, 1),
+            "box_read_gbs": None if box is None else round(box[0], 1),
+            "box_copy_gbs": None if box is None else round(box[1], 1),
+            "actual_vs_box_read": (None if box is None or traffic is None
+                                   else round(traffic / (kernel_ms * 1e-3) / 1e9 / box[0], 4)),
+            "box_note": ("pa_hbm_probe on the same box and run: best read-only / copy rate of 16 B "
+                         "non-temporal sweeps over a buffer of about the SpMV's traffic; the attainable "
+                         "rate the kernel's PMC-measured rate compares with (boxes differ by up to ~20 %)"),
         },
     }
     if rank == 0 and ngpu == 1 and not args.no_cpu_baseline:

@@ -68,6 +68,12 @@ int pa_device_count(int* count);
  *               buffers directly (default), 0: staging copies;
  * "spmv_lds", "comm_cus": occupancy / CU-mask experiments (default 0).    */
 int pa_tune(const char* key, int value, int* previous);
+/* HBM calibration of `device` (not the hot path): best read-only and copy
+ * rates (GB/s, read+write bytes for the copy; best of 4/8 loads in flight
+ * per lane and four grid sizes) over `reps` sweeps of a
+ * `bytes` buffer with the SpMV's 16 B non-temporal loads.  bench.py reports
+ * the SpMV's PMC-measured rate against it, since boxes differ.           */
+int pa_hbm_probe(int device, int64_t bytes, int reps, double* read_gbs, double* copy_gbs);
 
 /* ---- part context ------------------------------------------------------
  * One context per part: its device, its streams, its scratch.

@@ -36,6 +36,7 @@ _SIGS = {
     "pa_version": [],
     "pa_device_count": [C.POINTER(C.c_int)],
     "pa_tune": [C.c_char_p, C.c_int, C.POINTER(C.c_int)],
+    "pa_hbm_probe": [C.c_int, C.c_int64, C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_double)],
     "pa_ctx_create": [C.c_int, C.c_int, C.c_int, C.POINTER(_p)],
     "pa_ctx_create_shared": [C.c_int, C.c_int, _p, C.POINTER(_p)],
     "pa_ctx_destroy": [_p],
@@ -139,6 +140,13 @@ def tune(key: str, value: int) -> int:
     prev = C.c_int(0)
     call("pa_tune", key.encode(), int(value), C.byref(prev))
     return prev.value
+
+
+def hbm_probe(device: int = 0, nbytes: int = 2 << 30, reps: int = 10):
+    """pa_hbm_probe: (read GB/s, copy GB/s) attainable on `device` (calibration)."""
+    r, c = C.c_double(), C.c_double()
+    call("pa_hbm_probe", int(device), int(nbytes), int(reps), C.byref(r), C.byref(c))
+    return r.value, c.value
 
 
 def i32(a):

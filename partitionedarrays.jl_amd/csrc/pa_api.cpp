@@ -87,6 +87,7 @@ void launch_stencil_count(const StencilGeom& g, const int32_t* shell, const doub
                           int32_t* err, hipStream_t st);
 void launch_stencil_fill(const StencilGeom& g, const int32_t* shell, const double* coef,
                          int64_t nrows, int noids, pa_mat* A, int32_t* err, hipStream_t st);
+void launch_probe(int copy, int unroll, int64_t n16, const void* a, void* b, int blocks, hipStream_t st);
 extern int g_spmv_flags;
 extern int g_spmv_unroll;
 extern int g_spmv_lds;
@@ -644,6 +645,48 @@ int pa_device_count(int* count) {
   hipError_t e = hipGetDeviceCount(&c);
   if (e != hipSuccess) c = 0;
   *count = c;
+  return 0;
+}
+
+int pa_hbm_probe(int device, int64_t bytes, int reps, double* read_gbs, double* copy_gbs) {
+  CHECK_ARG(bytes >= (1 << 20) && reps > 0 && read_gbs && copy_gbs, "pa_hbm_probe: bytes >= 1 MiB, reps > 0");
+  HIPC(hipSetDevice(device));
+  const int64_t n16 = bytes / 16;
+  void *a = nullptr, *b = nullptr;
+  hipStream_t st = nullptr;
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  auto cleanup = [&]() {
+    if (a) (void)hipFree(a);
+    if (b) (void)hipFree(b);
+    if (e0) (void)hipEventDestroy(e0);
+    if (e1) (void)hipEventDestroy(e1);
+    if (st) (void)hipStreamDestroy(st);
+  };
+#define PROBE_CALL(expr) do { if ((expr) != hipSuccess) { cleanup(); PA_FAIL(std::string("pa_hbm_probe: ") + #expr); } } while (0)
+  PROBE_CALL(hipMalloc(&a, (size_t)n16 * 16));
+  PROBE_CALL(hipMalloc(&b, (size_t)n16 * 16));
+  PROBE_CALL(hipMemset(a, 0x5a, (size_t)n16 * 16));
+  PROBE_CALL(hipStreamCreate(&st));
+  PROBE_CALL(hipEventCreate(&e0));
+  PROBE_CALL(hipEventCreate(&e1));
+  double best[2] = {0.0, 0.0};
+  for (int copy = 0; copy < 2; ++copy)
+    for (int unroll : {4, 8})
+    for (int blocks : {2048, 4096, 8192, 16384}) {
+      launch_probe(copy, unroll, n16, a, b, blocks, st);  // warm
+      PROBE_CALL(hipEventRecord(e0, st));
+      for (int r = 0; r < reps; ++r) launch_probe(copy, unroll, n16, a, b, blocks, st);
+      PROBE_CALL(hipEventRecord(e1, st));
+      PROBE_CALL(hipEventSynchronize(e1));
+      float ms = 0.f;
+      PROBE_CALL(hipEventElapsedTime(&ms, e0, e1));
+      const double gbs = (double)n16 * 16 * (copy ? 2 : 1) * reps / (ms * 1e-3) / 1e9;
+      best[copy] = std::max(best[copy], gbs);
+    }
+#undef PROBE_CALL
+  cleanup();
+  *read_gbs = best[0];
+  *copy_gbs = best[1];
   return 0;
 }
 

@@ -583,4 +583,55 @@ void launch_stencil_fill(const StencilGeom& g, const int32_t* shell, const doubl
   }
 }
 
+// ---------------------------------------------------------------------------
+// HBM calibration (pa_hbm_probe): the attainable read and copy rates of the
+// box, measured with the SpMV's own load idiom (16 B non-temporal vector
+// loads, 4 or 8 in flight per lane, grid-stride).  Not on the hot path.
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+template <int U>
+__global__ __launch_bounds__(256) void k_probe_read(int64_t n16, const u32x4* __restrict__ a,
+                                                    u32x4* __restrict__ out) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  uint32_t acc = 0;
+  int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  for (; i + (U - 1) * stride < n16; i += U * stride) {
+    u32x4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) v[u] = __builtin_nontemporal_load(a + i + u * stride);
+#pragma unroll
+    for (int u = 0; u < U; ++u) acc ^= v[u].x ^ v[u].y ^ v[u].z ^ v[u].w;
+  }
+  for (; i < n16; i += stride) {
+    const u32x4 v = __builtin_nontemporal_load(a + i);
+    acc ^= v.x ^ v.y ^ v.z ^ v.w;
+  }
+  if (acc == 0x9e3779b9u) out[threadIdx.x] = u32x4{acc, 0u, 0u, 0u};  // keeps the loads live
+}
+
+template <int U>
+__global__ __launch_bounds__(256) void k_probe_copy(int64_t n16, const u32x4* __restrict__ a,
+                                                    u32x4* __restrict__ b) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  for (; i + (U - 1) * stride < n16; i += U * stride) {
+    u32x4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) v[u] = __builtin_nontemporal_load(a + i + u * stride);
+#pragma unroll
+    for (int u = 0; u < U; ++u) __builtin_nontemporal_store(v[u], b + i + u * stride);
+  }
+  for (; i < n16; i += stride) __builtin_nontemporal_store(__builtin_nontemporal_load(a + i), b + i);
+}
+
+void launch_probe(int copy, int unroll, int64_t n16, const void* a, void* b, int blocks, hipStream_t st) {
+  const u32x4* ia = (const u32x4*)a;
+  u32x4* ob = (u32x4*)b;
+  if (copy && unroll == 8) hipLaunchKernelGGL(k_probe_copy<8>, dim3(blocks), dim3(256), 0, st, n16, ia, ob);
+  else if (copy) hipLaunchKernelGGL(k_probe_copy<4>, dim3(blocks), dim3(256), 0, st, n16, ia, ob);
+  else if (unroll == 8) hipLaunchKernelGGL(k_probe_read<8>, dim3(blocks), dim3(256), 0, st, n16, ia, ob);
+  else hipLaunchKernelGGL(k_probe_read<4>, dim3(blocks), dim3(256), 0, st, n16, ia, ob);
+}
+
 }  // namespace pa

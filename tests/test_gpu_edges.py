@@ -106,3 +106,12 @@ def test_single_part_no_halo_and_empty_matrix(be, pamd):
     assert np.all(y.to_host().local(1) == 0.0)
     pamd.mul_(y, A, x, 2.0, 1.0)
     assert np.all(y.to_host().local(1) == 0.0)
+
+
+def test_hbm_probe_rates_and_arguments(be, pamd):
+    """pa_hbm_probe (bench.py's HBM calibration): plausible read/copy rates on
+    a 256 MiB buffer, and its argument check fails loudly."""
+    r, c = pamd._lib.hbm_probe(0, 256 << 20, 3)
+    assert 500.0 < r < 20000.0 and 500.0 < c < 20000.0
+    with pytest.raises(pamd._lib.PAError, match="pa_hbm_probe"):
+        pamd._lib.hbm_probe(0, 1024, 1)
