@@ -51,12 +51,20 @@ class HIPBackend(SequentialBackend):
     """All parts in this process, part p on device devices[(p-1) % len(devices)]
     (SequentialBackend semantics, HIP parts)."""
 
-    def __init__(self, devices=None, share_streams=False):
+    def __init__(self, devices=None, share_streams=False, graph_mul=False):
+        """graph_mul: mul!(c, a, b, α, β) captures a HIP graph the first time
+        it sees (c, a, b, α, β) and replays it afterwards (pamd.SpMVGraph; at
+        most 16 cached, least recently used evicted; a structure that cannot
+        be captured, e.g. parts on several devices, stays eager).  Off by
+        default.  With share_streams on one device it is the fast path for
+        many small parts (C5, 8 Voronoi parts of 128³: 0.36 ms per mul!
+        against 0.5-1.6 ms eager, tools/c5_bench.py)."""
         ndev = _lib.device_count()
         if ndev == 0:
             raise _lib.PAError("HIPBackend: no HIP device visible")
         self.devices = list(devices) if devices is not None else list(range(ndev))
         self.share_streams = share_streams
+        self.graph_mul = graph_mul
         self.ctx = {}
 
     def get_part_ids(self, nparts):

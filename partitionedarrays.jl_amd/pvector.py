@@ -8,6 +8,7 @@ the caller asks for them (`to_host`).
 from __future__ import annotations
 
 import ctypes as C
+from collections import OrderedDict
 import math
 
 import numpy as np
@@ -363,9 +364,51 @@ def _mat_exchange(A: "PSparseMatrix", op, reverse, zero_sent):
 
 def mul_(c: PVector, a: PSparseMatrix, b: PVector, alpha=1.0, beta=0.0) -> PVector:
     """mul!(c, a, b, α, β) (Interfaces.jl:2246-2275): halo exchange of b
-    overlapped with the interior slices, then the slices reading ghosts."""
+    overlapped with the interior slices, then the slices reading ghosts.
+    With HIPBackend(graph_mul=True): a cached HIP-graph replay of the same."""
+    g = _cached_graph(c, a, b, alpha, beta)
+    if g:
+        g()
+        return c
     _spmv(c, a, b, alpha, beta, None)
     return c
+
+
+_GRAPH_CACHE_MAX = 16
+
+
+def _cached_graph(c, a, b, alpha, beta):
+    """HIPBackend(graph_mul=True): the SpMVGraph of (c, a, b, α, β), captured
+    on first use.  The entry holds c, a and b, so their ids stay unique while
+    cached.  Falsy: graphs off, or this structure is not capturable (eager)."""
+    be = getattr(a.values, "backend", None)
+    if not getattr(be, "graph_mul", False):
+        return None
+    cache = be.__dict__.setdefault("_graphs", OrderedDict())
+    key = (id(c), id(a), id(b), complex(alpha), complex(beta))
+    if key in cache:
+        cache.move_to_end(key)
+        return cache[key]
+    try:
+        g = SpMVGraph(c, a, b, alpha, beta)
+    except _lib.PAError as e:
+        if "graph capture" not in str(e):
+            raise
+        g = _Uncapturable((c, a, b))
+    cache[key] = g
+    while len(cache) > _GRAPH_CACHE_MAX:
+        cache.popitem(last=False)
+    return g
+
+
+class _Uncapturable:
+    """cache entry of a structure that stays eager (keeps its ids unique)"""
+
+    def __init__(self, keep):
+        self._keep = keep
+
+    def __bool__(self):
+        return False
 
 
 class SpMVGraph:

@@ -28,6 +28,7 @@ ap.add_argument("--steps", type=int, default=20)
 ap.add_argument("--patterns", default="4")
 ap.add_argument("--rules", default="1", help="pa_tune spmv_pattern_rule values to A/B")
 ap.add_argument("--share", action="store_true", help="parts as one in-order chain (share_streams)")
+ap.add_argument("--graph", action="store_true", help="also time the HIP-graph replay (pamd.SpMVGraph)")
 a = ap.parse_args()
 DT = {"f64": np.float64, "f32": np.float32, "c128": np.complex128, "c64": np.complex64}
 be = pamd.HIPBackend(devices=[0], share_streams=a.share)
@@ -77,8 +78,28 @@ for name, npat, rule in [(d, int(q), int(r)) for d in a.dtypes.split(",") for q 
         c.set_timing(False)
         c.sync()
     km = float(np.median(kms))
+    t_graph = None
+    if a.graph:
+        ref = y.to_host()
+        g = pamd.SpMVGraph(y, A, x)
+        for _ in range(3):
+            g()
+        for p in parts.part_ids:
+            be.context(p).sync()
+        t0 = time.perf_counter()
+        for _ in range(a.steps):
+            g()
+        for p in parts.part_ids:
+            be.context(p).sync()
+        t_graph = (time.perf_counter() - t0) / a.steps
+        got = y.to_host()
+        for p in parts.part_ids:
+            own = A.rows.partition.local(p).oid_to_lid - 1
+            assert np.array_equal(got.local(p)[own], ref.local(p)[own]), "graph replay differs from eager mul!"
+        del g
     print(json.dumps({"config": f"C5 FE27 {a.n}^3 Voronoi {a.parts} parts on 1 GPU", "dtype": name,
                       "spmv_patterns": npat, "spmv_pattern_rule": rule, "share_streams": a.share,
-                      "ms_per_mul": round(1e3 * t, 4), "gbs_algorithmic_all_parts": round(B / t / 1e9, 1),
+                      "ms_per_mul": round(1e3 * t, 4),
+                      "ms_per_mul_graph": None if t_graph is None else round(1e3 * t_graph, 4), "gbs_algorithmic_all_parts": round(B / t / 1e9, 1),
                       "kernel_ms_sum_over_parts": round(km, 4), "gbs_algorithmic_kernels": round(B / km / 1e6, 1),
                       "setup_s": round(setup, 2), "format": info}), flush=True)
