@@ -135,10 +135,15 @@ def device_count() -> int:
     return n.value
 
 
+tune_generation = 0  # bumped by every tune(): cached mul! graphs captured under older knobs are stale
+
+
 def tune(key: str, value: int) -> int:
     """pa_tune: set a process-wide kernel knob, return the previous value."""
+    global tune_generation
     prev = C.c_int(0)
     call("pa_tune", key.encode(), int(value), C.byref(prev))
+    tune_generation += 1
     return prev.value
 
 

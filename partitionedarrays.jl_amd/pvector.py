@@ -380,12 +380,13 @@ _GRAPH_CACHE_MAX = 16
 def _cached_graph(c, a, b, alpha, beta):
     """HIPBackend(graph_mul=True): the SpMVGraph of (c, a, b, α, β), captured
     on first use.  The entry holds c, a and b, so their ids stay unique while
-    cached.  Falsy: graphs off, or this structure is not capturable (eager)."""
+    cached; a pa_tune call since the capture makes the entry stale (the graph
+    froze the kernel choice).  Replays do not feed pa_ctx_last_kernel_ms.  Falsy: graphs off, or this structure is not capturable (eager)."""
     be = getattr(a.values, "backend", None)
     if not getattr(be, "graph_mul", False):
         return None
     cache = be.__dict__.setdefault("_graphs", OrderedDict())
-    key = (id(c), id(a), id(b), complex(alpha), complex(beta))
+    key = (id(c), id(a), id(b), complex(alpha), complex(beta), _lib.tune_generation)
     if key in cache:
         cache.move_to_end(key)
         return cache[key]

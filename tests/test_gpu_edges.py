@@ -143,6 +143,11 @@ def test_graph_mul_cache_matches_eager(pamd, share):
         out[name] = (parts, A, res)
         if flag:
             assert len(be._graphs) == 2 and all(bool(g) for g in be._graphs.values())
+            prev = pamd._lib.tune("spmv_format", 0)  # knob change: the next call captures afresh
+            pamd._lib.tune("spmv_format", prev)
+            pamd.mul_(y, A, x, 1.0, 0.0)
+            assert len(be._graphs) == 3
+            assert np.array_equal(y.to_host().local(1), res[-1].local(1))
     parts, A, _ = out["eager"]
     for r_e, r_g in zip(out["eager"][2], out["graph"][2]):
         for p in parts.part_ids:
