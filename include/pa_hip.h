@@ -52,7 +52,8 @@ int pa_device_count(int* count);
  *               slice mapping, bit 2: pattern rows fetch x as 16 B runs,
  *               bit 3: the last len % U entries of a slice as one
  *               predicated batch, bit 4: a slice list covering the whole
- *               structure is launched without the list (default 29);
+ *               structure is launched without the list, bit 5: y written
+ *               with non-temporal stores (default 29);
  * "spmv_unroll" 4 or 8 entries in flight per lane (default 8);
  * "spmv_format" 1: pattern slices where the matrix has them (default),
  *               0: int32 column ids everywhere;

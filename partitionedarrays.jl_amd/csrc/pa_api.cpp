@@ -602,9 +602,9 @@ int pa_tune(const char* key, int value, int* previous) {
   CHECK_ARG(key, "null key");
   int* slot = nullptr;
   if (!std::strcmp(key, "spmv_flags")) {
-    CHECK_ARG(value >= 0 && value <= 31,
+    CHECK_ARG(value >= 0 && value <= 63,
               "spmv_flags: bit 0 = non-temporal streams, bit 1 = XCD mapping, bit 2 = 16 B x runs (pattern rows), "
-              "bit 3 = masked tail batch, bit 4 = identity slice lists dropped");
+              "bit 3 = masked tail batch, bit 4 = identity slice lists dropped, bit 5 = non-temporal y stores");
     slot = &g_spmv_flags;
   } else if (!std::strcmp(key, "spmv_lds")) {
     CHECK_ARG(value >= 0 && value <= 160 * 1024, "spmv_lds: bytes of LDS per SpMV block (occupancy cap)");

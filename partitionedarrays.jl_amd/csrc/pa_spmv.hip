@@ -37,7 +37,8 @@ __device__ inline int64_t xcd_remap(int64_t b, int64_t G) {
   return x * q + (x < r ? x : r) + i;
 }
 
-enum { SPMV_NT = 1, SPMV_XCD = 2, SPMV_XPAIR = 4, SPMV_TAILB = 8, SPMV_IDLIST = 16 };
+enum { SPMV_NT = 1, SPMV_XCD = 2, SPMV_XPAIR = 4, SPMV_TAILB = 8, SPMV_IDLIST = 16, SPMV_YNT = 32 };
+typedef unsigned int spmv_u32x4 __attribute__((ext_vector_type(4)));
 // Process-wide knobs (pa_tune).  Defaults from the A/Bs in
 // profiles/r01_ab_spmv.txt and profiles/r01/ab_xpair.txt: non-temporal
 // streams on, XCD remap off, U = 8, 16 B x runs on (FE27 256³: F64 −9 %,
@@ -409,7 +410,17 @@ __global__ __launch_bounds__(256) void k_spmv_sell(SpmvArgs<T> a) {
     Pack<T, R> o;
 #pragma unroll
     for (int r = 0; r < R; ++r) o.v[r] = acc[r];
-    *reinterpret_cast<Pack<T, R>*>(a.y + row0) = o;
+    if constexpr (sizeof(Pack<T, R>) == 16) {
+      if (a.flags & SPMV_YNT) {  // y as a non-temporal 16 B store per lane
+        spmv_u32x4 w;
+        __builtin_memcpy(&w, &o, 16);
+        __builtin_nontemporal_store(w, reinterpret_cast<spmv_u32x4*>(a.y + row0));
+      } else {
+        *reinterpret_cast<Pack<T, R>*>(a.y + row0) = o;
+      }
+    } else {
+      *reinterpret_cast<Pack<T, R>*>(a.y + row0) = o;
+    }
   } else {
 #pragma unroll
     for (int r = 0; r < R; ++r)
