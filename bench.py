@@ -4,8 +4,11 @@ per GPU, weak scaling over Cartesian parts (1 → (1,1,1), 2 → (2,1,1),
 4 → (2,2,1), 8 → (2,2,2)).
 
 A step = one mul! (halo exchange of x + SpMV of every owned row) with A and x
-resident in HBM.  value = algorithmic bytes of all parts /
-time of K steps (max over ranks) → GB/s.
+resident in HBM.  value = the bytes one mul! of every part must move in the
+layout it runs on (matrix values with padding, column ids and slice metadata
+as the kernels load them, pa_mat_traffic; x read once, y written once; pack +
+unpack of the halo) / time of K steps (max over ranks) → GB/s.  The format-
+independent CSR count of SURVEY.md §8d rides along as csr_equivalent_gbs.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--n 256] [--kind 27]
     torchrun --nproc-per-node N bench.py --gpus N ...   (one part per GPU)
@@ -30,10 +33,21 @@ PART_SHAPES = {1: (1, 1, 1), 2: (2, 1, 1), 4: (2, 2, 1), 8: (2, 2, 2)}
 DTYPES = {"f64": np.float64, "f32": np.float32, "c128": np.complex128, "c64": np.complex64}
 
 
-def algorithmic_bytes(nnz, n_own, n_ghost, n_snd, n_rcv, S, I=4):
-    """nnz·(S+I) + (n_own+1)·I + (n_own+n_ghost)·S + n_own·S
-    + (n_snd+n_rcv)·(I+2S)."""
+def csr_bytes(nnz, n_own, n_ghost, n_snd, n_rcv, S, I=4):
+    """SURVEY.md §8d (format-independent CSR count): nnz·(S+I) + (n_own+1)·I
+    + (n_own+n_ghost)·S + n_own·S + (n_snd+n_rcv)·(I+2S)."""
     return nnz * (S + I) + (n_own + 1) * I + (n_own + n_ghost) * S + n_own * S + (n_snd + n_rcv) * (I + 2 * S)
+
+
+def format_bytes(info, n_ghost, n_snd, n_rcv, S, I=4):
+    """Bytes one mul! of a part must move in the layout it runs on: the
+    matrix streams as its kernels load them (pa_mat_traffic: values incl.
+    padding, column ids, slice metadata), x read once (owned + ghost), y
+    written once, and the halo (pack: lid + value read + buffer write;
+    unpack: lid + buffer read + value write per halo value)."""
+    n_own = info["nrows"]
+    matrix = info["value_bytes"] + info["index_bytes"] + info["meta_bytes"]
+    return matrix + (n_own + n_ghost) * S + n_own * S + (n_snd + n_rcv) * (I + 2 * S)
 
 
 def host_cores():
@@ -45,35 +59,46 @@ def host_cores():
     return max(1, min(16, n))
 
 
-def cpu_baseline(kind, seconds=15.0, n=128):
+def cpu_baseline(kind, n, seconds=12.0):
     """oracle/build/spmv_ref: the reference's CSC column loop
     (SparseUtils.jl:157-187) restated in C ("port"), run as MPIBackend would
     run it on this host: one rank per core (--ranks), each with the CSC of
-    its block of rows, a barrier per SpMV.  A short 1-core run rides along."""
+    its block of rows of the SAME operator as the GPU line (n^3 nodes), a
+    barrier per SpMV.  Reported in the GPU line's CSR-equivalent GB/s
+    (SURVEY.md §8d bytes) and ms per SpMV; a 1-rank run on 128^3 rides along."""
     exe = os.path.join(ROOT, "oracle", "build", "spmv_ref")
     if not os.path.exists(exe):
         subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle")], check=True)
 
-    def run(ranks, secs):
-        out = subprocess.run([exe, "--kind", str(kind), "--n", str(n), "--seconds", str(secs), "--ranks", str(ranks)],
-                             check=True, capture_output=True, text=True).stdout
+    def run(ranks, nn, secs):
+        out = subprocess.run([exe, "--kind", str(kind), "--n", str(nn), "--seconds", str(secs), "--ranks",
+                              str(ranks)], check=True, capture_output=True, text=True, timeout=600).stdout
         return json.loads(out.strip().splitlines()[-1])
     cores = host_cores()
-    r = run(cores, 0.7 * seconds)
-    r1 = run(1, 0.3 * seconds)
-    return {"value": round(r["gbps"], 3), "unit": "GB/s", "cores": cores, "kind": "port",
-            "sample": f"{kind}-pt operator {n}^3 nodes ({r['nnz']} nnz), {r['reps']} SpMVs in ~{0.7 * seconds:.0f} s, "
-                      f"Int64 CSC column loop (SparseUtils.jl:157-187) in C, {cores} MPIBackend-like ranks "
-                      f"(threads, row blocks of PRange(parts, n), barrier per SpMV)",
-            "single_core_gbps": round(r1["gbps"], 3)}
+    r = run(cores, n, seconds)
+    r1 = run(1, 128, 3.0)
+    return {"value": round(r["gbps"], 3), "unit": "GB/s (SURVEY.md 8d CSR bytes, like csr_equivalent_gbs)",
+            "ms_per_spmv": round(1e3 * r["sec_per_spmv"], 3), "cores": cores, "kind": "port",
+            "sample": f"the benched operator ({kind}-pt, {n}^3 nodes, {r['nnz']} nnz), {r['reps']} SpMVs in "
+                      f"~{seconds:.0f} s, Int64 CSC column loop (SparseUtils.jl:157-187) in C, {cores} "
+                      f"MPIBackend-like ranks (threads, row blocks of PRange(parts, n), barrier per SpMV)",
+            "single_core_gbps_128": round(r1["gbps"], 3)}
+
+
+PROBE_BYTES = 1 << 30
 
 
 def pmc_traffic(args, steps=5):
     """HBM bytes per mul! step from rocprofv3 PMC counters, one counter per
-    pass (MI355X_MICROARCH.md §HBM / §rocprofv3): FETCH_SIZE (KB, x2 for the
-    gfx950 wide-stream under-count) + WRITE_SIZE (KB), summed over the SpMV
-    kernels of the profiled steps / steps.  Runs this script as the profiled
-    child (`--child-pmc`)."""
+    pass (MI355X_MICROARCH.md §HBM / §rocprofv3): FETCH_SIZE (KB) and
+    WRITE_SIZE (KB) summed over the SpMV kernels of the profiled steps /
+    steps.  FETCH_SIZE under-counts wide coalesced streaming reads on gfx950
+    (MI355X_MICROARCH.md: by 1/2); the factor is calibrated in the same
+    profiled process on k_probe_read launches that read a known 1 GiB with
+    the SpMV's own 16 B-per-lane non-temporal loads, and applied to the
+    SpMV's fetches (its loads are 16 B per lane: values, pattern rows' x
+    runs; the side rows' 4-8 B gathers are split out in the note).  Runs
+    this script as the profiled child (`--child-pmc`)."""
     import csv
     import shutil
     import signal
@@ -96,13 +121,22 @@ def pmc_traffic(args, steps=5):
         files = [os.path.join(r, f) for r, _, fs in os.walk(d) for f in fs if f.endswith("counter_collection.csv")]
         if p.returncode != 0 or not files:
             return None, f"rocprofv3 --pmc {ctr} failed (rc {p.returncode})"
-        vals = [float(r["Counter_Value"]) for r in csv.DictReader(open(files[0]))
+        rows = list(csv.DictReader(open(files[0])))
+        vals = [float(r["Counter_Value"]) for r in rows
                 if "k_spmv_sell" in r["Kernel_Name"] and r["Counter_Name"] == ctr]
         tot[ctr] = sum(vals) / (steps + 1)  # warmup step + steps
+        if ctr == "FETCH_SIZE":
+            probe = [float(r["Counter_Value"]) for r in rows
+                     if "k_probe_read" in r["Kernel_Name"] and r["Counter_Name"] == ctr]
+            tot["probe_kb"] = float(np.median(probe)) if probe else None
         shutil.rmtree(d, ignore_errors=True)
-    traffic = tot["FETCH_SIZE"] * 1024 * 2 + tot["WRITE_SIZE"] * 1024
-    return traffic, (f"rocprofv3 --pmc FETCH_SIZE | WRITE_SIZE passes over {steps + 1} mul! steps: "
-                     f"FETCH_SIZE {tot['FETCH_SIZE']:.0f} KB x2 (gfx950) + WRITE_SIZE {tot['WRITE_SIZE']:.0f} KB per step")
+    factor = PROBE_BYTES / (tot["probe_kb"] * 1024) if tot.get("probe_kb") else 2.0
+    traffic = tot["FETCH_SIZE"] * 1024 * factor + tot["WRITE_SIZE"] * 1024
+    return traffic, {"fetch_kb": round(tot["FETCH_SIZE"]), "write_kb": round(tot["WRITE_SIZE"]),
+                     "fetch_factor": round(factor, 4),
+                     "note": (f"rocprofv3 --pmc FETCH_SIZE | WRITE_SIZE passes over {steps + 1} mul! steps; "
+                              f"FETCH_SIZE x {factor:.3f}, the factor measured on k_probe_read launches "
+                              f"reading a known 1 GiB with 16 B/lane loads in the same process, + WRITE_SIZE")}
 
 
 def box_hbm_gbs(pamd, nbytes, reps=10):
@@ -129,6 +163,8 @@ def child_pmc(args):
     for _ in range(args.steps + 1):
         pamd.mul_(y, A, x)
     be.context(1).sync()
+    # FETCH_SIZE calibration: read sweeps of a known PROBE_BYTES
+    pamd._lib.hbm_probe(0, PROBE_BYTES, 1)
 
 
 def cg_mode(args, pamd, backend, parts, A, ngpu, world, sync):
@@ -164,7 +200,11 @@ def cg_mode(args, pamd, backend, parts, A, ngpu, world, sync):
     info = A.values.local(p0).info()
     S = np.dtype(dtype).itemsize
     n = info["nrows"]
-    it_bytes = (info["nnz"] * (S + 4) + (n + 1) * 4 + 2 * n * S) + 12 * n * S  # SpMV + dot 2 + norm 1 + 3 axpy x3
+    s0 = cols.partition.local(p0)
+    ns, nr = len(cols.exchanger.lids_snd.local(p0).data), len(cols.exchanger.lids_rcv.local(p0).data)
+    # per iteration of the device recurrence: mul! (format bytes, halo included)
+    # + k_cg_xu (x, u read+write, r read) + the fused dot's u re-read + k_cg_xr (r read+write, c read)
+    it_bytes = format_bytes(info, s0.num_hids, ns, nr, S) + 9 * s0.num_lids * S
     rows_all = n * ngpu
     line = {"metric": "CG iteration time (weak scaling, BASELINE config 4)",
             "value": round(out["device"][0], 4), "unit": "ms/iteration", "higher_is_better": False,
@@ -191,7 +231,7 @@ def main():
                     help="strong scaling (BASELINE config 3): --n^3 nodes in total, split over the parts")
     ap.add_argument("--kind", type=int, default=27, choices=[7, 27])
     ap.add_argument("--dtype", default="f64", choices=list(DTYPES))
-    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 HBM-traffic passes")
     ap.add_argument("--child-pmc", action="store_true", help=argparse.SUPPRESS)
@@ -238,21 +278,23 @@ def main():
     sync()
     t_setup = time.perf_counter() - t_setup
 
-    # algorithmic bytes of the local parts
+    # bytes of the local parts: in the layout they run on, and SURVEY.md §8d's CSR count
     ex = cols.exchanger
-    B_local, infos = 0, {}
+    B_local = C_local = 0
+    infos = {}
     for p in parts.part_ids:
         info = A.values.local(p).info()
         s = cols.partition.local(p)
         n_snd = len(ex.lids_snd.local(p).data)
         n_rcv = len(ex.lids_rcv.local(p).data)
-        infos[p] = (info, s.num_hids)
-        B_local += algorithmic_bytes(info["nnz"], info["nrows"], s.num_hids, n_snd, n_rcv, S)
-    B_all = B_local
+        infos[p] = (info, s.num_hids, n_snd, n_rcv)
+        B_local += format_bytes(info, s.num_hids, n_snd, n_rcv, S)
+        C_local += csr_bytes(info["nnz"], info["nrows"], s.num_hids, n_snd, n_rcv, S)
+    B_all, C_all = B_local, C_local
     if world > 1:
-        t = torch.tensor([float(B_local)], dtype=torch.float64)
+        t = torch.tensor([float(B_local), float(C_local)], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.SUM)
-        B_all = float(t.item())
+        B_all, C_all = float(t[0].item()), float(t[1].item())
 
     def barrier():
         if world > 1:
@@ -300,36 +342,46 @@ def main():
     ms_per_step = 1e3 * elapsed / args.steps
     value = B_all / (elapsed / args.steps) / 1e9
 
-    # roofline of the first local part: device time of its SpMV kernels, HIP
-    # events on the stream they run on (pa_ctx_last_kernel_ms), mean of K launches
-    p0 = parts.part_ids[0]
-    info, s_nhids = infos[p0]
-    ctx = backend.context(p0)
+    # device time of every local part's mul! phases: HIP events on the stream
+    # the kernels run on, recorded over `reps` untimed calls and read after
+    # the last one (no synchronisation per call): interior slices, halo
+    # completion after them (transport wait + unpack), boundary slices
+    reps = max(5, min(args.steps, 50))
 
-    def kernel_time(reps):
-        ctx.set_timing(True)
-        kms = []
+    def phase_times():
+        for c in ctxs:
+            c.set_timing(True)
         for i in range(reps):
             Ai, xi, yi = sets[i % ncopies]
             pamd.mul_(yi, Ai, xi)
-            a_ms, b_ms = ctx.last_kernel_ms()
-            kms.append(a_ms + b_ms)
-        ctx.set_timing(False)
         sync()
-        return float(np.mean(kms))
-    reps = max(5, min(args.steps, 50))
-    kernel_ms = kernel_time(reps)
-    spmv_bytes = info["nnz"] * (S + 4) + (info["nrows"] + 1) * 4 + (info["nrows"] + s_nhids) * S + info["nrows"] * S
+        return {p: c.kernel_times() for p, c in zip(parts.part_ids, ctxs)}
+    phases = phase_times()
+    per_part = {p: {k: round(v, 4) if isinstance(v, float) else v for k, v in t.items()} for p, t in phases.items()}
+    if world > 1:
+        allp = [None] * world
+        dist.all_gather_object(allp, per_part)
+        per_part = {k: v for d in allp for k, v in d.items()}
+    p0 = parts.part_ids[0]
+    info, s_nhids, n_snd0, n_rcv0 = infos[p0]
+    kernel_ms = phases[p0]["interior_ms"] + phases[p0]["boundary_ms"]
+    part_bytes = format_bytes(info, s_nhids, n_snd0, n_rcv0, S)
+    spmv_bytes = part_bytes - (n_snd0 + n_rcv0) * (4 + 2 * S)  # the SpMV kernels' share (no pack/unpack)
     achieved = spmv_bytes / (kernel_ms * 1e-3) / 1e9
     # the same kernels with int32 column ids everywhere (pa_tune spmv_format=0), for reference
     prev = pamd._lib.tune("spmv_format", 0)
-    kernel_ms_int32 = kernel_time(reps)
+    ph32 = phase_times()[p0]
+    info32 = A.values.local(p0).traffic()
     pamd._lib.tune("spmv_format", prev)
+    kernel_ms_int32 = ph32["interior_ms"] + ph32["boundary_ms"]
+    bytes_int32 = spmv_bytes - (info["value_bytes"] + info["index_bytes"] + info["meta_bytes"]) + sum(info32.values())
     box = box_hbm_gbs(pamd, spmv_bytes // 2) if world == 1 and ngpu == 1 else None
-    traffic, traffic_note = (None, "skipped (--no-pmc)")
+    traffic, tnote = (None, {"note": "skipped (--no-pmc)"})
     if rank == 0 and ngpu == 1 and not args.no_pmc:
-        traffic, traffic_note = pmc_traffic(args)
-
+        traffic, tnote = pmc_traffic(args)
+        if traffic is None:
+            tnote = {"note": tnote}
+    halo = s_nhids > 0
     line = {
         "metric": "SpMV+halo GB/s (frac of HBM peak), 3D Poisson 27-pt, 1/2/4/8 MI355X",
         "value": round(value, 2),
@@ -344,18 +396,25 @@ def main():
         "dtype": {"f64": "f64", "f32": "f32", "c128": "c128", "c64": "c64"}[args.dtype],
         "data": "synthetic (seeded uniform x; operator generated on device)",
         "config": {
-            "workload": f"mul!(y,A,x) incl. halo, {args.kind}-pt {'FE (test_fem_sa.jl pattern)' if args.kind == 27 else 'FD (test_fdm.jl)'} "
-                        f"operator, {args.n}^3 nodes {'in total' if args.strong else 'per GPU'}, Cartesian parts {shape}",
+            "workload": (f"mul!(y,A,x), {args.kind}-pt {'FE (test_fem_sa.jl pattern)' if args.kind == 27 else 'FD (test_fdm.jl)'} "
+                         f"operator, {args.n}^3 nodes {'in total' if args.strong else 'per GPU'}, Cartesian parts {shape}"
+                         + (", halo exchange of x between parts" if halo else ", one part: no halo to exchange")),
             "global_nodes": list(N),
             "parts": list(shape),
             "nnz_per_part": info["nnz"],
             "rows_per_part": info["nrows"],
             "ghosts_per_part": s_nhids,
             "process_model": "one part per process (RCCL halo)" if world > 1 else f"{ngpu} part(s) in one process",
-            "bytes_per_step_all_parts": B_all,
+            "bytes_per_step_all_parts": int(B_all),
+            "bytes_definition": ("per part: matrix streams as loaded (values incl. padding, column ids, slice "
+                                 "metadata; pa_mat_traffic) + x read once (owned+ghost) + y written once "
+                                 "+ halo pack/unpack (4+2S per value each side)"),
             "frac_of_hbm_peak": round(value / (HBM_PEAK_GBS * ngpu), 4),
+            "csr_equivalent_gbs": round(C_all / (elapsed / args.steps) / 1e9, 2),
+            "csr_bytes_per_step_all_parts": int(C_all),
             "setup_s": round(t_setup, 2),
             "operator_copies_rotated": ncopies,
+            "per_part_ms": per_part,
         },
         "roofline": {
             "bound": "hbm",
@@ -364,30 +423,32 @@ def main():
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4),
             "traffic": None if traffic is None else int(traffic),
-            "traffic_note": traffic_note,
-            "kernel": "k_spmv_sell (all SpMV kernels of one mul! step: pattern + side slices)",
+            "traffic_detail": tnote,
+            "kernel": "k_spmv_sell (all SpMV kernels of one mul! step of part %d: pattern + side slices)" % p0,
             "kernel_ms": round(kernel_ms, 4),
-            "algorithmic_bytes_per_launch": spmv_bytes,
+            "algorithmic_bytes_per_launch": int(spmv_bytes),
+            "bytes_split": {"values": info["value_bytes"], "column_ids": info["index_bytes"],
+                            "slice_metadata": info["meta_bytes"],
+                            "x_y": int((info["nrows"] + s_nhids) * S + info["nrows"] * S)},
+            "csr_equivalent_achieved": round(csr_bytes(info["nnz"], info["nrows"], s_nhids, 0, 0, S)
+                                             / (kernel_ms * 1e-3) / 1e9, 1),
             "actual_hbm_gbs": None if traffic is None else round(traffic / (kernel_ms * 1e-3) / 1e9, 1),
             "actual_frac": None if traffic is None else round(traffic / (kernel_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-            "bytes_note": ("achieved/frac count SURVEY.md 8d's format-independent CSR bytes (nnz*(S+4) + ...); "
-                           "pattern slices read no column ids for their regular rows, so frac can exceed 1. "
-                           "actual_frac = PMC traffic / kernel time / peak is the HBM utilisation."),
+            "traffic_over_bytes": None if traffic is None else round(traffic / spmv_bytes, 4),
             "column_format": (f"pattern slices {info['pattern_slices']}/{info['nslices']}, "
                               f"regular rows {info['regular_rows']}/{info['nrows']}, side rows {info['side_rows']}"),
             "int32_columns_kernel_ms": round(kernel_ms_int32, 4),
-            "int32_columns_achieved": round(spmv_bytes / (kernel_ms_int32 * 1e-3) / 1e9, 1),
+            "int32_columns_achieved": round(bytes_int32 / (kernel_ms_int32 * 1e-3) / 1e9, 1),
             "box_read_gbs": None if box is None else round(box[0], 1),
             "box_copy_gbs": None if box is None else round(box[1], 1),
-            "actual_vs_box_read": (None if box is None or traffic is None
-                                   else round(traffic / (kernel_ms * 1e-3) / 1e9 / box[0], 4)),
+            "achieved_vs_box_read": None if box is None else round(achieved / box[0], 4),
             "box_note": ("pa_hbm_probe on the same box and run: best read-only / copy rate of 16 B "
-                         "non-temporal sweeps over a buffer of about the SpMV's traffic; the attainable "
-                         "rate the kernel's PMC-measured rate compares with (boxes differ by up to ~20 %)"),
+                         "non-temporal sweeps over a buffer of about the SpMV's size; the attainable "
+                         "rate next to the 8 TB/s spec (boxes differ by up to ~20 %)"),
         },
     }
     if rank == 0 and ngpu == 1 and not args.no_cpu_baseline:
-        line["cpu_baseline"] = cpu_baseline(args.kind, args.cpu_seconds)
+        line["cpu_baseline"] = cpu_baseline(args.kind, args.n, args.cpu_seconds)
     if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:

@@ -67,6 +67,11 @@ int pa_device_count(int* count);
  *               0: lane-strided partial sums + tree (within 1e-12);
  * "halo_pull"   1: parts of one process read their neighbours' packed
  *               buffers directly (default), 0: staging copies;
+ * "halo_transport" 0: parts of one process exchange by device reads/copies
+ *               (default), 1: RCCL send/recv for every part that has a
+ *               communicator (pa_comm_init_all / pa_comm_init_rank);
+ * "spmv_group"  1: the parts of one process sharing a stream pair run each
+ *               mul! phase as one launch (default), 0: launches per part;
  * "spmv_lds", "comm_cus": occupancy / CU-mask experiments (default 0).    */
 int pa_tune(const char* key, int value, int* previous);
 /* HBM calibration of `device` (not the hot path): best read-only and copy
@@ -94,6 +99,12 @@ int pa_ctx_sync(pa_ctx* ctx);
  * rank = part-1 and nranks = nparts.                                    */
 int pa_comm_unique_id(unsigned char id[128]);
 int pa_comm_init_rank(pa_ctx* ctx, const unsigned char id[128]);
+/* RCCL between the parts of one process, one part per device
+ * (ncclCommInitAll over ctx[0..n-1] = parts 1..nparts, in order).  With
+ * pa_tune("halo_transport", 1) every halo segment then moves by the same
+ * grouped ncclSend/ncclRecv as across processes (MPIBackend.jl:261-309);
+ * with 0 (default) parts of one process read each other's buffers.      */
+int pa_comm_init_all(int n, pa_ctx* const ctx[]);
 
 /* ---- index sets --------------------------------------------------------
  * Device copy of an AbstractIndexSet's oid_to_lid / hid_to_lid
@@ -221,6 +232,14 @@ int pa_mat_format_info(const pa_mat* A, int64_t* pattern_slices,
  * pa_tune("spmv_patterns", n > 1) preceded the build.                     */
 int pa_mat_multipattern_info(const pa_mat* A, int64_t* multi_slices);
 
+/* Bytes one mul! streams from this matrix in its current encoding
+ * (pa_tune("spmv_format")), as its kernels load them: values (padding
+ * included), column ids (int32 slices, side rows, long rows) and slice
+ * metadata (offsets, lengths, lists, patterns, masks, row maps).  The
+ * bench's roofline adds x (read once), y and the halo to these.          */
+int pa_mat_traffic(const pa_mat* A, int64_t* value_bytes, int64_t* index_bytes,
+                   int64_t* meta_bytes);
+
 /* Long rows (row-length histogram): rows with more than max(256, 8 × the
  * 90th-percentile row length) entries leave the SELL and run one wave per
  * row over their own CSR (in the reference's summation order unless
@@ -327,11 +346,18 @@ int pa_mat_stencil(pa_ctx* ctx, int dtype, int kind, const int64_t gdims[3],
                    const double* coeffs, int ncoeffs, pa_mat** out);
 
 /* ---- timing (PTimer analogue, PTimers.jl) -------------------------------
- * Average device time of the last `pa_spmv_all` kernels of this context,
- * measured with HIP events on the stream they ran on.                    */
+ * pa_ctx_set_timing(ctx, 1) starts recording the mul! calls of this context
+ * with HIP events on the stream they run on (no synchronisation inside the
+ * calls).  pa_ctx_kernel_times returns the means over the recorded calls of
+ * the interior slices, the halo completion seen by the compute stream (wait
+ * for the transport + unpack, after the interior slices) and the boundary
+ * slices (+ long rows, fused-dot fold), and the number of calls; it clears
+ * the record.  pa_ctx_last_kernel_ms: the interior and boundary means.    */
+int pa_ctx_set_timing(pa_ctx* ctx, int enable);
+int pa_ctx_kernel_times(pa_ctx* ctx, float* interior_ms, float* halo_ms,
+                        float* boundary_ms, int* count);
 int pa_ctx_last_kernel_ms(pa_ctx* ctx, float* spmv_interior_ms,
                           float* spmv_boundary_ms);
-int pa_ctx_set_timing(pa_ctx* ctx, int enable);
 
 #ifdef __cplusplus
 }

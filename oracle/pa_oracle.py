@@ -1003,8 +1003,10 @@ def csc_mul_sub_(C, A: CSC, rows_inv, cols_list, rflag, cflag, B, alpha, beta):
     C, B: list-like of scalars (numpy scalar or Cx); cols_list = A.indices[2]
     (1-based parent col ids, in view order); rows_inv = invrows (lid_to_ohid)."""
     if not (beta == 1):
+        # β != 0 ? rmul!(C, β) : fill!(C, zero(eltype(C)))  (SparseUtils.jl:167-168):
+        # β = 0 overwrites, so NaN/Inf or a negative value in C does not leak
         for i in range(len(C)):
-            C[i] = C[i] * beta if beta != 0 else C[i] * 0
+            C[i] = C[i] * beta if beta != 0 else _zero_elem(C[i])
     nzv = A.nzval
     for j, Jc in enumerate(cols_list, start=1):
         axj = B[j - 1] * alpha if not _is_one(alpha) else B[j - 1]
@@ -1014,6 +1016,13 @@ def csc_mul_sub_(C, A: CSC, rows_inv, cols_list, rflag, cflag, B, alpha, beta):
             if i > 0:
                 C[i - 1] = C[i - 1] + _get(nzv, p) * axj
     return C
+
+
+def _zero_elem(v):
+    """zero(eltype(C)) for one element (numpy scalar or Cx)"""
+    if isinstance(v, Cx):
+        return Cx(type(v.re)(0), type(v.im)(0))
+    return type(v)(0)
 
 
 def _is_one(a):
@@ -1122,8 +1131,8 @@ def _spmv_part_vec(cv, A, bv, rows, acols, bcols, crows, alpha, beta):
 
     def init(vals):
         y = vals[ylid]
-        if beta == 0:
-            return y * 0 if not cx else y * 0
+        if beta == 0:  # fill!(co, zero(eltype(co))) (Interfaces.jl:2262-2263), not y*0
+            return np.zeros_like(y)
         return y if beta == 1 else y * beta
     if cx:
         acc = Cx(init(cv.re), init(cv.im))

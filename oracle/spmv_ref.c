@@ -1,33 +1,61 @@
 /*
  * spmv_ref.c — TEST INFRASTRUCTURE (oracle).  Plain-C restatement of the
- * reference's CPU hot path, used as the CPU baseline of bench.py
- * (cpu_baseline.kind = "port") and as a checker at sizes where the Python
- * oracle is slow.  Never linked into the product.
+ * reference's CPU hot path, used as bench.py's CPU baseline
+ * (cpu_baseline.kind = "port") and as the checker at BASELINE sizes, where
+ * the Python oracle is too slow.  Never linked into the product.
  *
  * Restated (reference paths relative to /root/reference):
  *  - the local kernel mul!(C, A::SubSparseMatrix{SparseMatrixCSC}, B, α, β)
- *    SparseUtils.jl:157-187: column loop over the owned columns, Int64
- *    colptr/rowval, `i = invrows[I]*rflag; if i>0: C[i] += nzv[p]*αxj`,
- *    after `fill!(C, 0)` for β = 0 (Interfaces.jl:2261-2266);
- *  - the single-part operator of the benchmark: the 27-point Q1-hex FE
- *    operator of test_fem_sa.jl's pattern in 3D (Dirichlet rows keep their
- *    diagonal, one per touching cell; entries summed over the cells holding
- *    both nodes in ascending cell order), or test_fdm.jl's 7-point operator,
- *    assembled as `sparse` does (CSC, rows ascending in each column).
+ *    SparseUtils.jl:157-187: column loop, Int64 colptr/rowval,
+ *    `i = invrows[I]*rflag; if i>0: C[i] += nzv[p]*αxj`, after
+ *    `fill!(C, 0)` for β = 0 (SparseUtils.jl:167-168, Interfaces.jl:2261-2266);
+ *  - mul!(c::PVector, a::PSparseMatrix, b::PVector) (Interfaces.jl:2246-2275)
+ *    on Cartesian parts: the owned_owned block (columns by oid), then the
+ *    owned_ghost block (columns by hid) after the exchange;
+ *  - the partition of the benchmark driver (partitionedarrays.jl_amd/
+ *    drivers.py stencil_partition): rows = PRange(parts, (N,N,N)) (Cartesian,
+ *    Interfaces.jl:1114-1137, _oid_to_gid 1307-1319), cols = rows + the ghosts
+ *    that add_gids!(rows, J) (Interfaces.jl:579-603, 1515-1533) appends in
+ *    first-touch order of the row-wise COO (owned rows by oid, neighbours in
+ *    (dz,dy,dx) lexicographic order);
+ *  - the operators: the 27-point Q1-hex FE operator of test_fem_sa.jl's
+ *    pattern in 3D (Dirichlet rows keep their diagonal, one 1.0 per touching
+ *    cell; entries summed over the cells holding both nodes in ascending cell
+ *    order), or test_fdm.jl's 7-point operator (Dirichlet rows: identity),
+ *    assembled as `sparse` does (CSC, rows ascending in each column);
+ *  - IterativeSolvers.cg! v0.9 (not vendored; SURVEY.md §3.5, called at
+ *    test_fdm.jl:115): u = 0; r = b; c = A*x; r .-= c; residual = norm(r);
+ *    tol = max(reltol*norm(b), abstol); prev = 1; per iteration
+ *    β = res²/prev²; u .= r .+ β.*u; mul!(c,A,u); α = res²/dot(u,c);
+ *    x .+= α.*u; r .-= α.*c; prev = res; res = norm(r).  dot and norm fold
+ *    the parts' owned partials in part order (reduce(+; init=0),
+ *    Interfaces.jl:221-238, 1767-1772, 1985-1992); the local sums run over
+ *    the owned values in oid order (the reference's BLAS internals are
+ *    unpinned).
  *
- * Usage: spmv_ref --kind 27|7 --n N [--seconds S] [--reps R] [--ranks P]
- *                 [--xin file --yout file]   (raw float64 in/out, length N^3)
- * --ranks P (P > 1) restates MPIBackend with P ranks on P host threads: the
- * rows are split into P contiguous blocks (PRange(parts, n), Interfaces.jl:
- * 1014-1030); each rank holds the CSC of its owned rows over its local
- * columns (owned + ghost, ghosts appended) and runs the same column loop on
- * its own copy of x, then all ranks meet at a barrier (the halo exchange and
- * the max-over-ranks timing of PTimer).
- * Prints one JSON line {"rows","nnz","reps","sec_per_spmv","gbps",...}.
- * Bytes per SpMV use the same algorithmic formula as bench.py (SURVEY.md
- * §8d, Int32 index width): nnz*(8+4) + (n+1)*4 + n*8 (x) + n*8 (y).
+ * Modes (F64; x fastest; gids 0-based in the files):
+ *  spmv_ref --kind 27|7 --n N [--reps R] [--xin f --yout f]
+ *      one part, literal CSC column loop over the whole operator
+ *  spmv_ref ... --parts PX PY PZ [--threads T] [--literal] --xin f --yout f
+ *      partitioned mul!: each owned row summed in the reference's order
+ *      (owned columns by oid, then ghost columns by hid).  Row-wise by
+ *      default (the per-row sequence of the column loop); --literal builds
+ *      each part's local CSC and runs the column loop itself over the
+ *      owned_owned then owned_ghost views (small sizes: the cross-check).
+ *  spmv_ref ... [--parts ...] --cg K --bin f [--xin f] [--hist f] [--xout f]
+ *      [--reltol r] [--abstol a] [--dot seq|pairwise]
+ *      cg! with maxiter = K (x0 = 0 without --xin); --dot: the local
+ *      summation order of dot/norm (below)
+ *  spmv_ref --kind 27|7 --n N --seconds S --ranks P
+ *      CPU baseline: MPIBackend with P ranks on P host threads; the rows
+ *      split into P contiguous blocks (PRange(parts, n), Interfaces.jl:
+ *      1014-1030), each rank holding the CSC of its owned rows over its local
+ *      columns and running the column loop on its own copy of x, then a
+ *      barrier (the halo exchange and PTimer's max-over-ranks).
+ * Every mode prints one JSON line.
  */
 #define _POSIX_C_SOURCE 200809L
+#include <math.h>
 #include <pthread.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -41,7 +69,20 @@ static double now(void) {
   return t.tv_sec + 1e-9 * t.tv_nsec;
 }
 
+static void* xmalloc(size_t n) {
+  void* p = malloc(n ? n : 1);
+  if (!p) { fprintf(stderr, "out of memory (%zu bytes)\n", n); exit(1); }
+  return p;
+}
+
+/* ---- the operators ------------------------------------------------------ */
 static double Ke[64];
+static int64_t N;
+static int kind;
+static double fd_diag, fd_off;
+static int K;                 /* stencil points */
+static int off_d[27][3];      /* (dx,dy,dz) in (dz,dy,dx) lexicographic order */
+static double interior_val[27];
 
 static void q1_hex_ke(double h) {
   const double K1[2][2] = {{1.0, -1.0}, {-1.0, 1.0}};
@@ -57,14 +98,12 @@ static void q1_hex_ke(double h) {
     }
 }
 
-static int64_t N;
-static int kind;
-static double fd_diag, fd_off;
-
 static int dirichlet(int64_t x, int64_t y, int64_t z) {
   return x == 0 || y == 0 || z == 0 || x == N - 1 || y == N - 1 || z == N - 1;
 }
 
+/* entry (row node g, column node g+d): Ke summed over the cells holding both,
+ * in ascending cell order (the cell loop's COO order, combined by sparse) */
 static double fe_value(int64_t gx, int64_t gy, int64_t gz, int dx, int dy, int dz) {
   double acc = 0.0;
   int first = 1;
@@ -107,34 +146,325 @@ static double ncells(int64_t gx, int64_t gy, int64_t gz) {
   return acc;
 }
 
-/* row r's entries (ascending column) */
-static int row_entries(int64_t r, int64_t* cols, double* vals) {
-  int64_t x = r % N, y = (r / N) % N, z = r / (N * N);
-  if (dirichlet(x, y, z)) {
-    cols[0] = r;
-    vals[0] = kind == 7 ? 1.0 : ncells(x, y, z);
-    return 1;
-  }
-  int k = 0;
+static double dirichlet_val(int64_t x, int64_t y, int64_t z) { return kind == 7 ? 1.0 : ncells(x, y, z); }
+
+static void setup_operator(void) {
+  const double h = 2.0 / (double)(N - 1);
+  q1_hex_ke(h);
+  fd_diag = -((-6.0) / (h * h));
+  fd_off = -(1.0 / (h * h));
+  K = 0;
   for (int dz = -1; dz <= 1; ++dz)
     for (int dy = -1; dy <= 1; ++dy)
       for (int dx = -1; dx <= 1; ++dx) {
         int nz = (dx != 0) + (dy != 0) + (dz != 0);
         if (kind == 7 && nz > 1) continue;
-        cols[k] = (x + dx) + N * ((y + dy) + N * (z + dz));
-        vals[k] = kind == 7 ? (nz == 0 ? fd_diag : fd_off) : fe_value(x, y, z, dx, dy, dz);
-        ++k;
+        off_d[K][0] = dx; off_d[K][1] = dy; off_d[K][2] = dz;
+        /* every non-Dirichlet node has all 8 cells: the same values as node (1,1,1) */
+        interior_val[K] = kind == 7 ? (nz == 0 ? fd_diag : fd_off) : (N >= 3 ? fe_value(1, 1, 1, dx, dy, dz) : 0.0);
+        ++K;
       }
-  return k;
 }
 
-/* ---- MPIBackend-like ranks on threads -------------------------------- */
+/* row r's entries (ascending column = lexicographic neighbour order) */
+static int row_entries(int64_t r, int64_t* cols, double* vals) {
+  int64_t x = r % N, y = (r / N) % N, z = r / (N * N);
+  if (dirichlet(x, y, z)) {
+    cols[0] = r;
+    vals[0] = dirichlet_val(x, y, z);
+    return 1;
+  }
+  for (int k = 0; k < K; ++k) {
+    cols[k] = (x + off_d[k][0]) + N * ((y + off_d[k][1]) + N * (z + off_d[k][2]));
+    vals[k] = interior_val[k]; /* == fe_value at every non-Dirichlet node (checked by --literal) */
+  }
+  return K;
+}
+
+/* ---- a tiny thread pool: parallel_for over [0, n) in chunks ------------- */
+typedef void (*range_fn)(void* ctx, int64_t lo, int64_t hi);
+typedef struct { range_fn fn; void* ctx; int64_t n; int t, T; } PFArg;
+static int g_threads = 1;
+
+static void* pf_run(void* a) {
+  PFArg* p = (PFArg*)a;
+  const int64_t lo = p->n * p->t / p->T, hi = p->n * (p->t + 1) / p->T;
+  if (lo < hi) p->fn(p->ctx, lo, hi);
+  return NULL;
+}
+
+static void parallel_for(int64_t n, range_fn fn, void* ctx) {
+  int T = g_threads;
+  if (T > n) T = (int)(n > 0 ? n : 1);
+  if (T <= 1) { if (n > 0) fn(ctx, 0, n); return; }
+  pthread_t th[256];
+  PFArg args[256];
+  if (T > 256) T = 256;
+  for (int t = 0; t < T; ++t) {
+    args[t] = (PFArg){fn, ctx, n, t, T};
+    pthread_create(&th[t], NULL, pf_run, &args[t]);
+  }
+  for (int t = 0; t < T; ++t) pthread_join(th[t], NULL);
+}
+
+/* ---- Cartesian parts ---------------------------------------------------- */
+/* _oid_to_gid (Interfaces.jl:1307-1319), 0-based first and length */
+static void oid_range(int64_t ng, int np, int p, int64_t* first, int64_t* len) {
+  const int64_t ol = ng / np, off = ol * (p - 1), rem = ng % np;
+  if (rem < (np - p + 1)) { *first = off; *len = ol; }
+  else { *first = off + p - (np - rem) - 1; *len = ol + 1; }
+}
+
+typedef struct {
+  int64_t lo[3], n[3];      /* owned box, 0-based global origin */
+  int64_t nown, nghost;
+  int32_t* shell;           /* (n+2)^3 extended box → hid (0-based) or -1 */
+} Part;
+
+static int P3[3] = {1, 1, 1};
+static int nparts = 1;
+static Part* parts;
+
+static inline int64_t shell_idx(const Part* q, int64_t ex, int64_t ey, int64_t ez) {
+  return ex + (q->n[0] + 2) * (ey + (q->n[1] + 2) * ez);
+}
+
+/* add_gids!(rows, J) over the row-wise COO: ghosts in first-touch order */
+static void build_part(Part* q, int part) {
+  int c[3] = {(part - 1) % P3[0], ((part - 1) / P3[0]) % P3[1], (part - 1) / (P3[0] * P3[1])};
+  for (int d = 0; d < 3; ++d) oid_range(N, P3[d], c[d] + 1, &q->lo[d], &q->n[d]);
+  q->nown = q->n[0] * q->n[1] * q->n[2];
+  const int64_t ext = (q->n[0] + 2) * (q->n[1] + 2) * (q->n[2] + 2);
+  q->shell = xmalloc((size_t)ext * sizeof(int32_t));
+  for (int64_t i = 0; i < ext; ++i) q->shell[i] = -1;
+  int64_t nh = 0;
+  for (int64_t lz = 0; lz < q->n[2]; ++lz)
+    for (int64_t ly = 0; ly < q->n[1]; ++ly)
+      for (int64_t lx = 0; lx < q->n[0]; ++lx) {
+        const int face = lx == 0 || ly == 0 || lz == 0 || lx == q->n[0] - 1 || ly == q->n[1] - 1 || lz == q->n[2] - 1;
+        if (!face) continue;  /* no neighbour outside the box */
+        const int64_t gx = q->lo[0] + lx, gy = q->lo[1] + ly, gz = q->lo[2] + lz;
+        if (dirichlet(gx, gy, gz)) continue;  /* its only column is itself */
+        for (int k = 0; k < K; ++k) {
+          const int64_t ex = lx + off_d[k][0], ey = ly + off_d[k][1], ez = lz + off_d[k][2];
+          if (ex >= 0 && ey >= 0 && ez >= 0 && ex < q->n[0] && ey < q->n[1] && ez < q->n[2]) continue;
+          const int64_t s = shell_idx(q, ex + 1, ey + 1, ez + 1);
+          if (q->shell[s] < 0) q->shell[s] = (int32_t)nh++;
+        }
+      }
+  q->nghost = nh;
+}
+
+static inline int64_t gid3(int64_t x, int64_t y, int64_t z) { return x + N * (y + N * z); }
+
+/* y[owned row] of one part, in the reference's order: the owned_owned
+ * block's columns by oid, then the owned_ghost block's by hid */
+static inline double row_apply(const Part* q, int64_t lx, int64_t ly, int64_t lz, const double* x) {
+  const int64_t gx = q->lo[0] + lx, gy = q->lo[1] + ly, gz = q->lo[2] + lz;
+  double acc = 0.0; /* fill!(co, 0) */
+  if (dirichlet(gx, gy, gz)) return acc + dirichlet_val(gx, gy, gz) * x[gid3(gx, gy, gz)];
+  int64_t key[27];
+  double v[27], xv[27];
+  int m = 0;
+  for (int k = 0; k < K; ++k) {
+    const int64_t ex = lx + off_d[k][0], ey = ly + off_d[k][1], ez = lz + off_d[k][2];
+    int64_t kk;
+    if (ex >= 0 && ey >= 0 && ez >= 0 && ex < q->n[0] && ey < q->n[1] && ez < q->n[2])
+      kk = ex + q->n[0] * (ey + q->n[1] * ez);                        /* oid - 1 */
+    else
+      kk = q->nown + q->shell[shell_idx(q, ex + 1, ey + 1, ez + 1)];  /* nown + hid - 1 */
+    /* insertion by key: owned (ascending oid) before ghosts (ascending hid) */
+    int t = m++;
+    while (t > 0 && key[t - 1] > kk) { key[t] = key[t - 1]; v[t] = v[t - 1]; xv[t] = xv[t - 1]; --t; }
+    key[t] = kk;
+    v[t] = interior_val[k];
+    xv[t] = x[gid3(gx + off_d[k][0], gy + off_d[k][1], gz + off_d[k][2])];
+  }
+  for (int t = 0; t < m; ++t) acc += v[t] * xv[t]; /* C[i] += nzv[p]*αxj, α = 1 */
+  return acc;
+}
+
+typedef struct { const double* x; double* y; } SpmvCtx;
+
+/* work item = (part, z-plane) */
+static void spmv_range(void* vctx, int64_t lo, int64_t hi) {
+  SpmvCtx* c = (SpmvCtx*)vctx;
+  for (int64_t w = lo; w < hi; ++w) {
+    int64_t acc = 0;
+    int p = 0;
+    while (w >= acc + parts[p].n[2]) { acc += parts[p].n[2]; ++p; }
+    const Part* q = &parts[p];
+    const int64_t lz = w - acc;
+    for (int64_t ly = 0; ly < q->n[1]; ++ly)
+      for (int64_t lx = 0; lx < q->n[0]; ++lx)
+        c->y[gid3(q->lo[0] + lx, q->lo[1] + ly, q->lo[2] + lz)] = row_apply(q, lx, ly, lz, c->x);
+  }
+}
+
+static int64_t total_planes(void) {
+  int64_t s = 0;
+  for (int p = 0; p < nparts; ++p) s += parts[p].n[2];
+  return s;
+}
+
+static void spmv_parts(const double* x, double* y) {
+  SpmvCtx c = {x, y};
+  parallel_for(total_planes(), spmv_range, &c);
+}
+
+/* --literal: each part's local CSC (rows: owned lids; columns: owned oids,
+ * then ghosts by hid) and the column loop of SparseUtils.jl:176-185 over the
+ * owned_owned view (flag (1,1)), then the owned_ghost view (flag (1,-1)) */
+static void spmv_parts_literal(const double* x, double* y) {
+  for (int p = 0; p < nparts; ++p) {
+    const Part* q = &parts[p];
+    const int64_t nl = q->nown + q->nghost;
+    int64_t* colptr = calloc((size_t)nl + 1, sizeof(int64_t));
+    int64_t* lid_gid = xmalloc((size_t)nl * sizeof(int64_t));
+    for (int64_t lz = 0; lz < q->n[2]; ++lz)
+      for (int64_t ly = 0; ly < q->n[1]; ++ly)
+        for (int64_t lx = 0; lx < q->n[0]; ++lx)
+          lid_gid[lx + q->n[0] * (ly + q->n[1] * lz)] = gid3(q->lo[0] + lx, q->lo[1] + ly, q->lo[2] + lz);
+    for (int64_t ez = 0; ez < q->n[2] + 2; ++ez)
+      for (int64_t ey = 0; ey < q->n[1] + 2; ++ey)
+        for (int64_t ex = 0; ex < q->n[0] + 2; ++ex) {
+          const int32_t h = q->shell[shell_idx(q, ex, ey, ez)];
+          if (h >= 0) lid_gid[q->nown + h] = gid3(q->lo[0] + ex - 1, q->lo[1] + ey - 1, q->lo[2] + ez - 1);
+        }
+    /* entries (row lid, col lid, value) of the owned rows */
+    int64_t cap = q->nown * K, ne = 0;
+    int64_t* er = xmalloc((size_t)cap * sizeof(int64_t));
+    int64_t* ec = xmalloc((size_t)cap * sizeof(int64_t));
+    double* ev = xmalloc((size_t)cap * sizeof(double));
+    for (int64_t lz = 0; lz < q->n[2]; ++lz)
+      for (int64_t ly = 0; ly < q->n[1]; ++ly)
+        for (int64_t lx = 0; lx < q->n[0]; ++lx) {
+          const int64_t gx = q->lo[0] + lx, gy = q->lo[1] + ly, gz = q->lo[2] + lz;
+          const int64_t row = lx + q->n[0] * (ly + q->n[1] * lz);
+          if (dirichlet(gx, gy, gz)) {
+            er[ne] = row; ec[ne] = row; ev[ne] = dirichlet_val(gx, gy, gz); ++ne;
+            continue;
+          }
+          for (int k = 0; k < K; ++k) {
+            const int64_t ex = lx + off_d[k][0], ey = ly + off_d[k][1], ez = lz + off_d[k][2];
+            int64_t cl;
+            if (ex >= 0 && ey >= 0 && ez >= 0 && ex < q->n[0] && ey < q->n[1] && ez < q->n[2])
+              cl = ex + q->n[0] * (ey + q->n[1] * ez);
+            else
+              cl = q->nown + q->shell[shell_idx(q, ex + 1, ey + 1, ez + 1)];
+            er[ne] = row; ec[ne] = cl;
+            ev[ne] = kind == 7 ? interior_val[k] : fe_value(gx, gy, gz, off_d[k][0], off_d[k][1], off_d[k][2]);
+            ++ne;
+          }
+        }
+    for (int64_t e = 0; e < ne; ++e) colptr[ec[e] + 1]++;
+    for (int64_t j = 0; j < nl; ++j) colptr[j + 1] += colptr[j];
+    int64_t* rowval = xmalloc((size_t)ne * sizeof(int64_t));
+    double* nzval = xmalloc((size_t)ne * sizeof(double));
+    int64_t* cur = xmalloc((size_t)nl * sizeof(int64_t));
+    memcpy(cur, colptr, (size_t)nl * sizeof(int64_t));
+    for (int64_t e = 0; e < ne; ++e) { /* entries by ascending row → rows ascending per column */
+      const int64_t pp = cur[ec[e]]++;
+      rowval[pp] = er[e] + 1;
+      nzval[pp] = ev[e];
+    }
+    for (int64_t j = 0; j <= nl; ++j) colptr[j] += 1;
+    double* C = xmalloc((size_t)q->nown * sizeof(double));
+    for (int64_t i = 0; i < q->nown; ++i) C[i] = 0.0; /* fill!(co, 0) */
+    for (int blk = 0; blk < 2; ++blk) {  /* owned_owned, then owned_ghost */
+      const int64_t j0 = blk == 0 ? 0 : q->nown, j1 = blk == 0 ? q->nown : nl;
+      for (int64_t J = j0; J < j1; ++J) {
+        const double axj = x[lid_gid[J]] * 1.0;
+        for (int64_t pp = colptr[J] - 1; pp < colptr[J + 1] - 1; ++pp) {
+          const int64_t i = rowval[pp]; /* invrows: owned row lids are their oids */
+          if (i > 0) C[i - 1] += nzval[pp] * axj;
+        }
+      }
+    }
+    for (int64_t i = 0; i < q->nown; ++i) y[lid_gid[i]] = C[i];
+    free(C); free(cur); free(rowval); free(nzval); free(er); free(ec); free(ev); free(colptr); free(lid_gid);
+  }
+}
+
+/* ---- reductions over parts (owned values, oid order, folded in part order)
+ * The local sum of a part runs over its owned values in oid order:
+ * sequentially (default), or pairwise (--dot pairwise: halves down to 128
+ * values, as blocked BLAS kernels do).  The reference's local dot/nrm2 is
+ * BLAS, whose order is unpinned; the two orders bound the
+ * rounding spread a CG trajectory inherits from that choice.              */
+static int g_pairwise = 0;
+
+static double pair_sum(const double* a, const double* b, const int64_t* idx, int64_t n) {
+  if (n <= 128) {
+    double s = 0.0;
+    for (int64_t i = 0; i < n; ++i) s += a[idx[i]] * b[idx[i]];
+    return s;
+  }
+  const int64_t h = n / 2;
+  return pair_sum(a, b, idx, h) + pair_sum(a, b, idx + h, n - h);
+}
+
+typedef struct { const double* a; const double* b; double* part_sum; } DotCtx;
+static void dot_range(void* vctx, int64_t lo, int64_t hi) {
+  DotCtx* c = (DotCtx*)vctx;
+  for (int64_t p = lo; p < hi; ++p) {
+    const Part* q = &parts[p];
+    double s = 0.0;
+    if (g_pairwise) {
+      int64_t* idx = xmalloc((size_t)q->nown * sizeof(int64_t));
+      int64_t k = 0;
+      for (int64_t lz = 0; lz < q->n[2]; ++lz)
+        for (int64_t ly = 0; ly < q->n[1]; ++ly)
+          for (int64_t lx = 0; lx < q->n[0]; ++lx) idx[k++] = gid3(q->lo[0] + lx, q->lo[1] + ly, q->lo[2] + lz);
+      s = pair_sum(c->a, c->b, idx, q->nown);
+      free(idx);
+    } else {
+      for (int64_t lz = 0; lz < q->n[2]; ++lz)
+        for (int64_t ly = 0; ly < q->n[1]; ++ly) {
+          const int64_t g = gid3(q->lo[0], q->lo[1] + ly, q->lo[2] + lz);
+          for (int64_t lx = 0; lx < q->n[0]; ++lx) s += c->a[g + lx] * c->b[g + lx];
+        }
+    }
+    c->part_sum[p] = s;
+  }
+}
+static double pdot(const double* a, const double* b) {
+  double* ps = xmalloc((size_t)nparts * sizeof(double));
+  DotCtx c = {a, b, ps};
+  parallel_for(nparts, dot_range, &c);
+  double s = 0.0; /* reduce(+, …; init=0) in part order */
+  for (int p = 0; p < nparts; ++p) s = s + ps[p];
+  free(ps);
+  return s;
+}
+static double pnorm(const double* a) { return sqrt(pdot(a, a)); }
+
+typedef struct { double* y; const double* x; double a; int mode; int64_t n; } AxCtx;
+static void ax_range(void* vctx, int64_t lo, int64_t hi) {
+  AxCtx* c = (AxCtx*)vctx;
+  for (int64_t i = lo; i < hi; ++i) {
+    switch (c->mode) {
+      case 0: c->y[i] = c->x[i] + c->a * c->y[i]; break; /* u .= r .+ β.*u */
+      case 1: c->y[i] = c->y[i] + c->a * c->x[i]; break; /* x .+= α.*u */
+      case 2: c->y[i] = c->y[i] - c->a * c->x[i]; break; /* r .-= α.*c */
+      case 3: c->y[i] = c->y[i] - c->x[i]; break;        /* r .-= c */
+    }
+  }
+}
+static void axpby(double* y, const double* x, double a, int mode, int64_t n) {
+  AxCtx c = {y, x, a, mode, n};
+  parallel_for(n, ax_range, &c);
+}
+
+/* ---- the MPIBackend-like CPU baseline (ranks on threads) ---------------- */
 typedef struct {
   int64_t r0, r1;          /* owned global rows [r0, r1) */
   int64_t c0, nc;          /* local columns: global c0 .. c0+nc-1 (owned + ghosts) */
   int64_t *colptr, *rowval;
   double *nzval, *x, *y;
   int32_t* invrows;        /* local row lid → ohid (all owned here) */
+  int64_t nnz;
+  const double* B;
 } Rank;
 
 static pthread_barrier_t g_bar;
@@ -143,7 +473,8 @@ static int g_reps_target;
 static double g_seconds;
 static int g_done;
 
-static void rank_build(Rank* R, const double* B) {
+static void* rank_build(void* arg) {
+  Rank* R = (Rank*)arg;
   const int64_t nrow = R->r1 - R->r0;
   int64_t cols[27];
   double vals[27];
@@ -164,10 +495,11 @@ static void rank_build(Rank* R, const double* B) {
     for (int t = 0; t < k; ++t) R->colptr[cols[t] - lo + 1]++;
     nnz += k;
   }
+  R->nnz = nnz;
   for (int64_t j = 0; j < R->nc; ++j) R->colptr[j + 1] += R->colptr[j];
-  R->rowval = malloc((size_t)(nnz > 0 ? nnz : 1) * sizeof(int64_t));
-  R->nzval = malloc((size_t)(nnz > 0 ? nnz : 1) * sizeof(double));
-  int64_t* cur = malloc((size_t)R->nc * sizeof(int64_t));
+  R->rowval = xmalloc((size_t)nnz * sizeof(int64_t));
+  R->nzval = xmalloc((size_t)nnz * sizeof(double));
+  int64_t* cur = xmalloc((size_t)R->nc * sizeof(int64_t));
   memcpy(cur, R->colptr, (size_t)R->nc * sizeof(int64_t));
   for (int64_t r = R->r0; r < R->r1; ++r) {
     int k = row_entries(r, cols, vals);
@@ -179,11 +511,12 @@ static void rank_build(Rank* R, const double* B) {
   }
   free(cur);
   for (int64_t j = 0; j <= R->nc; ++j) R->colptr[j] += 1;
-  R->invrows = malloc((size_t)(nrow > 0 ? nrow : 1) * sizeof(int32_t));
+  R->invrows = xmalloc((size_t)nrow * sizeof(int32_t));
   for (int64_t i = 0; i < nrow; ++i) R->invrows[i] = (int32_t)(i + 1);
-  R->x = malloc((size_t)R->nc * sizeof(double));
-  memcpy(R->x, B + lo, (size_t)R->nc * sizeof(double));
-  R->y = malloc((size_t)(nrow > 0 ? nrow : 1) * sizeof(double));
+  R->x = xmalloc((size_t)R->nc * sizeof(double));
+  memcpy(R->x, R->B + lo, (size_t)R->nc * sizeof(double));
+  R->y = xmalloc((size_t)nrow * sizeof(double));
+  return NULL;
 }
 
 static void* rank_run(void* arg) {
@@ -211,30 +544,158 @@ static void* rank_run(void* arg) {
   return NULL;
 }
 
+static double* read_vec(const char* path, int64_t n) {
+  double* v = xmalloc((size_t)n * sizeof(double));
+  FILE* f = fopen(path, "rb");
+  if (!f || fread(v, sizeof(double), (size_t)n, f) != (size_t)n) { fprintf(stderr, "bad input file %s\n", path); exit(1); }
+  fclose(f);
+  return v;
+}
+
+static void write_vec(const char* path, const double* v, int64_t n) {
+  FILE* f = fopen(path, "wb");
+  if (!f || fwrite(v, sizeof(double), (size_t)n, f) != (size_t)n) { fprintf(stderr, "cannot write %s\n", path); exit(1); }
+  fclose(f);
+}
+
+static void seeded_vec(double* B, int64_t n) {
+  uint64_t s = 20250114u;
+  for (int64_t i = 0; i < n; ++i) {
+    s = s * 6364136223846793005ull + 1442695040888963407ull;
+    B[i] = ((double)(s >> 11) / 9007199254740992.0) * 2.0 - 1.0;
+  }
+}
+
+static int run_ranks(int ranks, int reps, double seconds, const double* B, int64_t n) {
+  Rank* Rk = calloc((size_t)ranks, sizeof(Rank));
+  pthread_t* th = xmalloc((size_t)ranks * sizeof(pthread_t));
+  for (int q = 0; q < ranks; ++q) { /* _oid_to_gid (Interfaces.jl:1307-1319), 0-based */
+    int64_t off, len;
+    oid_range(n, ranks, q + 1, &off, &len);
+    Rk[q].r0 = off;
+    Rk[q].r1 = off + len;
+    Rk[q].B = B;
+    pthread_create(&th[q], NULL, rank_build, &Rk[q]); /* each rank assembles its own CSC */
+  }
+  int64_t nnz = 0;
+  for (int q = 0; q < ranks; ++q) { pthread_join(th[q], NULL); nnz += Rk[q].nnz; }
+  pthread_barrier_init(&g_bar, NULL, (unsigned)ranks);
+  g_reps_target = reps;
+  g_seconds = seconds;
+  double t0 = now();
+  for (int q = 0; q < ranks; ++q) pthread_create(&th[q], NULL, rank_run, &Rk[q]);
+  for (int q = 0; q < ranks; ++q) pthread_join(th[q], NULL);
+  double t1 = now();
+  const double per = (t1 - t0) / g_done;
+  const double bytes = (double)nnz * 12.0 + (double)(n + 1) * 4.0 + (double)n * 16.0;
+  double cs = 0.0;
+  for (int q = 0; q < ranks; ++q)
+    for (int64_t i = 0; i < Rk[q].r1 - Rk[q].r0; ++i) cs += Rk[q].y[i];
+  printf("{\"kind\": %d, \"n_per_dim\": %lld, \"rows\": %lld, \"nnz\": %lld, \"ranks\": %d, \"reps\": %d, "
+         "\"sec_per_spmv\": %.9g, \"gbps\": %.6g, \"bytes_per_spmv\": %.0f, \"checksum\": %.17g}\n",
+         kind, (long long)N, (long long)n, (long long)nnz, ranks, g_done, per, bytes / per / 1e9, bytes, cs);
+  return 0;
+}
+
 int main(int argc, char** argv) {
   N = 64;
   kind = 27;
-  double seconds = 10.0;
-  int reps = 0, ranks = 1;
-  const char *xin = NULL, *yout = NULL;
+  double seconds = 10.0, reltol = 0.0, abstol = 0.0;
+  int reps = 0, ranks = 1, literal = 0, have_parts = 0, cg = 0;
+  const char *xin = NULL, *yout = NULL, *bin = NULL, *hist = NULL, *xout = NULL;
   for (int i = 1; i < argc; ++i) {
     if (!strcmp(argv[i], "--n") && i + 1 < argc) N = atoll(argv[++i]);
     else if (!strcmp(argv[i], "--kind") && i + 1 < argc) kind = atoi(argv[++i]);
     else if (!strcmp(argv[i], "--seconds") && i + 1 < argc) seconds = atof(argv[++i]);
     else if (!strcmp(argv[i], "--reps") && i + 1 < argc) reps = atoi(argv[++i]);
     else if (!strcmp(argv[i], "--ranks") && i + 1 < argc) ranks = atoi(argv[++i]);
+    else if (!strcmp(argv[i], "--threads") && i + 1 < argc) g_threads = atoi(argv[++i]);
+    else if (!strcmp(argv[i], "--parts") && i + 3 < argc) {
+      for (int d = 0; d < 3; ++d) P3[d] = atoi(argv[++i]);
+      have_parts = 1;
+    }
+    else if (!strcmp(argv[i], "--literal")) literal = 1;
+    else if (!strcmp(argv[i], "--dot") && i + 1 < argc) g_pairwise = !strcmp(argv[++i], "pairwise");
+    else if (!strcmp(argv[i], "--cg") && i + 1 < argc) cg = atoi(argv[++i]);
+    else if (!strcmp(argv[i], "--reltol") && i + 1 < argc) reltol = atof(argv[++i]);
+    else if (!strcmp(argv[i], "--abstol") && i + 1 < argc) abstol = atof(argv[++i]);
     else if (!strcmp(argv[i], "--xin") && i + 1 < argc) xin = argv[++i];
     else if (!strcmp(argv[i], "--yout") && i + 1 < argc) yout = argv[++i];
+    else if (!strcmp(argv[i], "--bin") && i + 1 < argc) bin = argv[++i];
+    else if (!strcmp(argv[i], "--hist") && i + 1 < argc) hist = argv[++i];
+    else if (!strcmp(argv[i], "--xout") && i + 1 < argc) xout = argv[++i];
     else { fprintf(stderr, "unknown argument %s\n", argv[i]); return 2; }
   }
   if (kind != 7 && kind != 27) { fprintf(stderr, "kind must be 7 or 27\n"); return 2; }
-  const double h = 2.0 / (double)(N - 1);
-  q1_hex_ke(h);
-  fd_diag = -((-6.0) / (h * h));
-  fd_off = -(1.0 / (h * h));
+  if (N < 3) { fprintf(stderr, "n must be >= 3\n"); return 2; }
+  if (g_threads < 1) g_threads = 1;
+  setup_operator();
   const int64_t n = N * N * N;
-  const int maxk = kind;
-  /* CSC via a counting transpose of the row lists (sparse(): rows ascending) */
+
+  if (ranks > 1) {
+    double* B = xmalloc((size_t)n * sizeof(double));
+    if (xin) { free(B); B = read_vec(xin, n); } else seeded_vec(B, n);
+    return run_ranks(ranks, reps, seconds, B, n);
+  }
+
+  if (have_parts || cg) {
+    nparts = P3[0] * P3[1] * P3[2];
+    if (nparts < 1) { fprintf(stderr, "bad --parts\n"); return 2; }
+    for (int d = 0; d < 3; ++d)
+      if (P3[d] > N) { fprintf(stderr, "more parts than nodes\n"); return 2; }
+    parts = calloc((size_t)nparts, sizeof(Part));
+    int64_t nghost = 0;
+    for (int p = 0; p < nparts; ++p) { build_part(&parts[p], p + 1); nghost += parts[p].nghost; }
+    void (*spmv)(const double*, double*) = literal ? spmv_parts_literal : spmv_parts;
+    double t0 = now();
+    if (!cg) {
+      if (!xin || !yout) { fprintf(stderr, "--parts needs --xin and --yout\n"); return 2; }
+      double* x = read_vec(xin, n);
+      double* y = xmalloc((size_t)n * sizeof(double));
+      spmv(x, y);
+      write_vec(yout, y, n);
+      double cs = 0.0;
+      for (int64_t i = 0; i < n; ++i) cs += y[i];
+      printf("{\"mode\": \"spmv\", \"kind\": %d, \"n_per_dim\": %lld, \"parts\": [%d, %d, %d], \"ghosts\": %lld, "
+             "\"literal\": %d, \"seconds\": %.3f, \"checksum\": %.17g}\n",
+             kind, (long long)N, P3[0], P3[1], P3[2], (long long)nghost, literal, now() - t0, cs);
+      return 0;
+    }
+    if (!bin) { fprintf(stderr, "--cg needs --bin\n"); return 2; }
+    double* b = read_vec(bin, n);
+    double* x = xin ? read_vec(xin, n) : calloc((size_t)n, sizeof(double));
+    double* u = calloc((size_t)n, sizeof(double));
+    double* r = xmalloc((size_t)n * sizeof(double));
+    double* c = xmalloc((size_t)n * sizeof(double));
+    double* h = xmalloc((size_t)(cg > 0 ? cg : 1) * sizeof(double));
+    memcpy(r, b, (size_t)n * sizeof(double));      /* copyto!(r, b) */
+    spmv(x, c);                                   /* mul!(c, A, x) */
+    axpby(r, c, 0.0, 3, n);                       /* r .-= c */
+    double residual = pnorm(r);
+    const double nb = pnorm(b);
+    const double tol = fmax(reltol * nb, abstol);
+    double prev = 1.0;
+    int it = 0;
+    while (!(it >= cg || residual <= tol)) {
+      const double beta = (residual * residual) / (prev * prev);
+      axpby(u, r, beta, 0, n);                    /* u .= r .+ β.*u */
+      spmv(u, c);                                 /* mul!(c, A, u) */
+      const double alpha = (residual * residual) / pdot(u, c);
+      axpby(x, u, alpha, 1, n);                   /* x .+= α.*u */
+      axpby(r, c, alpha, 2, n);                   /* r .-= α.*c */
+      prev = residual;
+      residual = pnorm(r);
+      h[it++] = residual;
+    }
+    if (hist) write_vec(hist, h, it);
+    if (xout) write_vec(xout, x, n);
+    printf("{\"mode\": \"cg\", \"kind\": %d, \"n_per_dim\": %lld, \"parts\": [%d, %d, %d], \"iterations\": %d, "
+           "\"residual0_norm_b\": %.17g, \"residual\": %.17g, \"seconds\": %.3f}\n",
+           kind, (long long)N, P3[0], P3[1], P3[2], it, nb, residual, now() - t0);
+    return 0;
+  }
+
+  /* one part, the literal CSC column loop over the whole operator */
   int64_t* colptr = calloc((size_t)n + 1, sizeof(int64_t));
   int64_t cols[27];
   double vals[27];
@@ -245,9 +706,9 @@ int main(int argc, char** argv) {
     nnz += k;
   }
   for (int64_t j = 0; j < n; ++j) colptr[j + 1] += colptr[j];
-  int64_t* rowval = malloc((size_t)nnz * sizeof(int64_t));
-  double* nzval = malloc((size_t)nnz * sizeof(double));
-  int64_t* cur = malloc((size_t)n * sizeof(int64_t));
+  int64_t* rowval = xmalloc((size_t)nnz * sizeof(int64_t));
+  double* nzval = xmalloc((size_t)nnz * sizeof(double));
+  int64_t* cur = xmalloc((size_t)n * sizeof(int64_t));
   memcpy(cur, colptr, (size_t)n * sizeof(int64_t));
   for (int64_t r = 0; r < n; ++r) { /* rows visited ascending → rows ascending per column */
     int k = row_entries(r, cols, vals);
@@ -257,60 +718,13 @@ int main(int argc, char** argv) {
       nzval[p] = vals[t];
     }
   }
+  free(cur);
   for (int64_t j = 0; j <= n; ++j) colptr[j] += 1;
-  (void)maxk;
-  int32_t* invrows = malloc((size_t)n * sizeof(int32_t)); /* lid_to_ohid: owned rows 1..n */
+  int32_t* invrows = xmalloc((size_t)n * sizeof(int32_t)); /* lid_to_ohid: owned rows 1..n */
   for (int64_t i = 0; i < n; ++i) invrows[i] = (int32_t)(i + 1);
-  double* B = malloc((size_t)n * sizeof(double));
-  double* Cv = malloc((size_t)n * sizeof(double));
-  if (xin) {
-    FILE* f = fopen(xin, "rb");
-    if (!f || fread(B, sizeof(double), (size_t)n, f) != (size_t)n) { fprintf(stderr, "bad --xin\n"); return 1; }
-    fclose(f);
-  } else {
-    uint64_t s = 20250114u;
-    for (int64_t i = 0; i < n; ++i) {
-      s = s * 6364136223846793005ull + 1442695040888963407ull;
-      B[i] = ((double)(s >> 11) / 9007199254740992.0) * 2.0 - 1.0;
-    }
-  }
-  if (ranks > 1) {
-    Rank* Rk = calloc((size_t)ranks, sizeof(Rank));
-    pthread_t* th = malloc((size_t)ranks * sizeof(pthread_t));
-    for (int q = 0; q < ranks; ++q) { /* _oid_to_gid (Interfaces.jl:1307-1319), 0-based */
-      const int64_t ol = n / ranks, rem = n % ranks;
-      const int p = q + 1;
-      int64_t len = ol, off = ol * (p - 1);
-      if (!(rem < (ranks - p + 1))) { len = ol + 1; off = ol * (p - 1) + p - (ranks - rem) - 1; }
-      Rk[q].r0 = off;
-      Rk[q].r1 = off + len;
-      rank_build(&Rk[q], B);
-    }
-    pthread_barrier_init(&g_bar, NULL, (unsigned)ranks);
-    g_reps_target = reps;
-    g_seconds = seconds;
-    double t0 = now();
-    for (int q = 0; q < ranks; ++q) pthread_create(&th[q], NULL, rank_run, &Rk[q]);
-    for (int q = 0; q < ranks; ++q) pthread_join(th[q], NULL);
-    double t1 = now();
-    const double per = (t1 - t0) / g_done;
-    const double bytes = (double)nnz * 12.0 + (double)(n + 1) * 4.0 + (double)n * 16.0;
-    double cs = 0.0;
-    for (int q = 0; q < ranks; ++q)
-      for (int64_t i = 0; i < Rk[q].r1 - Rk[q].r0; ++i) {
-        cs += Rk[q].y[i];
-        Cv[Rk[q].r0 + i] = Rk[q].y[i];
-      }
-    if (yout) {
-      FILE* f = fopen(yout, "wb");
-      fwrite(Cv, sizeof(double), (size_t)n, f);
-      fclose(f);
-    }
-    printf("{\"kind\": %d, \"n_per_dim\": %lld, \"rows\": %lld, \"nnz\": %lld, \"ranks\": %d, \"reps\": %d, "
-           "\"sec_per_spmv\": %.9g, \"gbps\": %.6g, \"bytes_per_spmv\": %.0f, \"checksum\": %.17g}\n",
-           kind, (long long)N, (long long)n, (long long)nnz, ranks, g_done, per, bytes / per / 1e9, bytes, cs);
-    return 0;
-  }
+  double* B = xin ? read_vec(xin, n) : xmalloc((size_t)n * sizeof(double));
+  if (!xin) seeded_vec(B, n);
+  double* Cv = xmalloc((size_t)n * sizeof(double));
   const double alpha = 1.0;
   const int rflag = 1;
   int done = 0;
@@ -331,11 +745,7 @@ int main(int argc, char** argv) {
   } while (reps > 0 ? done < reps : (t1 - t0) < seconds);
   const double per = (t1 - t0) / done;
   const double bytes = (double)nnz * 12.0 + (double)(n + 1) * 4.0 + (double)n * 16.0;
-  if (yout) {
-    FILE* f = fopen(yout, "wb");
-    fwrite(Cv, sizeof(double), (size_t)n, f);
-    fclose(f);
-  }
+  if (yout) write_vec(yout, Cv, n);
   double cs = 0.0;
   for (int64_t i = 0; i < n; ++i) cs += Cv[i];
   printf("{\"kind\": %d, \"n_per_dim\": %lld, \"rows\": %lld, \"nnz\": %lld, \"ranks\": 1, \"reps\": %d, "

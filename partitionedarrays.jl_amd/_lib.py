@@ -43,6 +43,7 @@ _SIGS = {
     "pa_ctx_sync": [_p],
     "pa_comm_unique_id": [C.c_char_p],
     "pa_comm_init_rank": [_p, C.c_char_p],
+    "pa_comm_init_all": [C.c_int, C.POINTER(_p)],
     "pa_index_create": [_p, C.c_int64, C.c_int64, _i32p, C.c_int64, _i32p, C.POINTER(_p)],
     "pa_index_destroy": [_p],
     "pa_xchg_create": [_p, C.c_int32, _i32p, _i32p, _i32p, C.c_int32, _i32p, _i32p, _i32p, C.POINTER(_p)],
@@ -84,6 +85,9 @@ _SIGS = {
     "pa_norm2_all": [C.c_int, C.POINTER(_p), C.POINTER(_p), _p],
     "pa_sum_all": [C.c_int, C.POINTER(_p), C.POINTER(_p), _p],
     "pa_ctx_last_kernel_ms": [_p, C.POINTER(C.c_float), C.POINTER(C.c_float)],
+    "pa_ctx_kernel_times": [_p, C.POINTER(C.c_float), C.POINTER(C.c_float), C.POINTER(C.c_float),
+                            C.POINTER(C.c_int)],
+    "pa_mat_traffic": [_p, _i64p, _i64p, _i64p],
     "pa_ctx_set_timing": [_p, C.c_int],
 }
 

@@ -45,6 +45,8 @@ extern int g_spmv_format;
 extern int g_spmv_pattern_rule;
 extern int g_spmv_patterns;  // patterns per slice at build time (1: single-pattern slices only)
 int g_halo_pull = 1;  // pa_tune("halo_pull"): pull-unpack between parts of one process
+int g_spmv_group = 1; // pa_tune("spmv_group"): one launch per phase for the parts sharing a stream pair
+int g_halo_transport = 0;  // pa_tune("halo_transport"): 0 parts of this process by device reads, 1 RCCL for all
 int g_comm_cus = 0;   // pa_tune("comm_cus"): CUs reserved for the comm stream (0: priority stream instead)
 // COO → CSC → SELL on the device (pa_coo.hip)
 int coo_compress(int dtype, int index_bytes, int64_t m, int64_t ncols, int64_t n, const void* dI, const void* dJ,
@@ -75,6 +77,10 @@ void launch_pull(int dtype, int64_t n, const int32_t* lids, const pa_combine_pla
                  const int64_t* elem, const void* const* bases, void* v, hipStream_t st);
 void launch_fill(int dtype, int64_t n, int64_t base, const int32_t* map, void* v, const void* s,
                  hipStream_t st);
+void launch_spmv_group(int which, int np, const SpmvPart* parts, bool has_alpha, int bmode, const void* alpha,
+                       const void* beta, hipStream_t st);
+void launch_pack_group(int dtype, const PackGroup& g, hipStream_t st);
+void launch_pull_group(int dtype, const PullGroup& g, hipStream_t st);
 void launch_copy(int dtype, int64_t n, const int32_t* dmap, void* d, const int32_t* smap,
                  const void* s, hipStream_t st);
 void launch_axpby(int dtype, int64_t n, const int32_t* map, void* y, const void* x, const void* a,
@@ -252,6 +258,7 @@ int finish_sell_layout(pa_mat* A, const std::vector<int32_t>& slen, const std::v
   }
   A->slots = acc;
   A->nslices = ns;
+  A->h_slen = slen;
   std::vector<int32_t> ilist, blist;
   for (int64_t s = 0; s < ns; ++s) (sghost[s] ? blist : ilist).push_back((int32_t)s);
   A->nslices_int = (int64_t)ilist.size();
@@ -293,6 +300,8 @@ int finalize_pattern(pa_mat* A, int kmax, int64_t noids) {
   HIPC(hipGetLastError());
   std::vector<int32_t> kind(ns), pghost(ns), nirreg(ns);
   std::vector<uint64_t> mask(ns * W);
+  A->h_plen.resize(ns);
+  HIPC(hipMemcpyAsync(A->h_plen.data(), A->d_plen, ns * 4, hipMemcpyDeviceToHost, st));
   HIPC(hipMemcpyAsync(kind.data(), A->d_kind, ns * 4, hipMemcpyDeviceToHost, st));
   HIPC(hipMemcpyAsync(pghost.data(), d_pghost, ns * 4, hipMemcpyDeviceToHost, st));
   HIPC(hipMemcpyAsync(nirreg.data(), d_nirreg, ns * 4, hipMemcpyDeviceToHost, st));
@@ -314,6 +323,7 @@ int finalize_pattern(pa_mat* A, int kmax, int64_t noids) {
       }
     }
   }
+  A->h_kind = kind;
   A->np_int = (int64_t)pint.size();
   A->np_bnd = (int64_t)pbnd.size();
   A->nx_int = (int64_t)xint.size();
@@ -371,12 +381,21 @@ struct LocalSet {
   }
 };
 
+// The parts whose halo segments move by device copies / pull reads in this
+// call.  With pa_tune("halo_transport", 1) and an RCCL communicator on every
+// part (pa_comm_init_all: one part per device in this process), none: every
+// segment goes through the grouped ncclSend/ncclRecv, as across processes.
 template <typename H>
 LocalSet local_set(int n, H* const* hs) {
   LocalSet L;
   int maxp = 0;
-  for (int i = 0; i < n; ++i) maxp = std::max(maxp, hs[i]->ctx->nparts);
+  bool all_comm = true;
+  for (int i = 0; i < n; ++i) {
+    maxp = std::max(maxp, hs[i]->ctx->nparts);
+    all_comm = all_comm && hs[i]->ctx->comm != nullptr;
+  }
   L.pos_of_part.assign(maxp + 1, -1);
+  if (g_halo_transport == 1 && all_comm) return L;
   for (int i = 0; i < n; ++i) L.pos_of_part[hs[i]->ctx->part] = i;
   return L;
 }
@@ -621,6 +640,14 @@ int pa_tune(const char* key, int value, int* previous) {
   } else if (!std::strcmp(key, "halo_pull")) {
     CHECK_ARG(value == 0 || value == 1, "halo_pull: 1 = receivers read the senders' buffers (one kernel), 0 = staging copies");
     slot = &g_halo_pull;
+  } else if (!std::strcmp(key, "halo_transport")) {
+    CHECK_ARG(value == 0 || value == 1,
+              "halo_transport: 0 = parts of this process by device reads/copies, 1 = RCCL send/recv for every part "
+              "with a communicator (pa_comm_init_all)");
+    slot = &g_halo_transport;
+  } else if (!std::strcmp(key, "spmv_group")) {
+    CHECK_ARG(value == 0 || value == 1, "spmv_group: 1 = one launch per phase for parts sharing a stream pair, 0 = per part");
+    slot = &g_spmv_group;
   } else if (!std::strcmp(key, "spmv_format")) {
     CHECK_ARG(value == 0 || value == 1, "spmv_format: 0 = int32 columns, 1 = pattern slices");
     slot = &g_spmv_format;
@@ -690,7 +717,7 @@ int pa_hbm_probe(int device, int64_t bytes, int reps, double* read_gbs, double* 
   return 0;
 }
 
-static int ctx_scratch(pa_ctx* c) {
+static int ctx_scratch(pa_ctx* c, const pa_ctx* share_events = nullptr) {
   HIPC(hipMalloc(&c->d_partials, 8192 * 16));  // block partials (reductions, CG update)
   HIPC(hipMalloc(&c->d_fold, 256 * 16));
   HIPC(hipMalloc(&c->d_result, 16));
@@ -698,9 +725,13 @@ static int ctx_scratch(pa_ctx* c) {
   HIPC(hipMalloc((void**)&c->d_ticket, 16));
   HIPC(hipMemset(c->d_ticket, 0, 16));
   HIPC(hipHostMalloc(&c->h_pinned, std::max<size_t>((size_t)(c->nparts + 1) * 16, 256)));  // gathered partials / CG state
+  if (share_events) {  // one stream pair, one pair of pipeline events
+    c->ev_packed = share_events->ev_packed;
+    c->ev_recvd = share_events->ev_recvd;
+    return 0;
+  }
   HIPC(hipEventCreateWithFlags(&c->ev_packed, hipEventDisableTiming));
   HIPC(hipEventCreateWithFlags(&c->ev_recvd, hipEventDisableTiming));
-  for (auto& e : c->ev_t) HIPC(hipEventCreate(&e));
   return 0;
 }
 
@@ -755,7 +786,7 @@ int pa_ctx_create_shared(int part, int nparts, pa_ctx* with, pa_ctx** out) {
   c->s_comm = with->s_comm;
   c->stream_refs = with->stream_refs;
   ++c->stream_refs->n;
-  if (ctx_scratch(c)) return -1;
+  if (ctx_scratch(c, with)) return -1;
   *out = c;
   return 0;
 }
@@ -772,10 +803,10 @@ int pa_ctx_destroy(pa_ctx* c) {
   dev_free(c->d_gather);
   dev_free(c->d_ticket);
   if (c->h_pinned) (void)hipHostFree(c->h_pinned);
-  (void)hipEventDestroy(c->ev_packed);
-  (void)hipEventDestroy(c->ev_recvd);
-  for (auto& e : c->ev_t) (void)hipEventDestroy(e);
-  if (c->stream_refs && --c->stream_refs->n == 0) {
+  for (auto& e : c->tev) (void)hipEventDestroy(e);
+  if (c->stream_refs && --c->stream_refs->n == 0) {  // the last context of a shared stream pair
+    (void)hipEventDestroy(c->ev_packed);
+    (void)hipEventDestroy(c->ev_recvd);
     (void)hipStreamDestroy(c->s_main);
     (void)hipStreamDestroy(c->s_comm);
     delete c->stream_refs;
@@ -811,17 +842,64 @@ int pa_comm_init_rank(pa_ctx* c, const unsigned char id[128]) {
   return 0;
 }
 
+// RCCL for the parts of ONE process, one part per device (ncclCommInitAll):
+// the MPIBackend transport (MPIBackend.jl:261-309) without processes; used
+// for every halo segment with pa_tune("halo_transport", 1).  ctx[i] must be
+// part i+1 of n = nparts, each on its own device (RCCL rejects two ranks on
+// one GPU).
+int pa_comm_init_all(int n, pa_ctx* const ctx[]) {
+  CHECK_ARG(n >= 1 && ctx, "null argument");
+  std::vector<int> devs(n);
+  for (int i = 0; i < n; ++i) {
+    CHECK_ARG(ctx[i], "null ctx");
+    CHECK_ARG(ctx[i]->part == i + 1 && ctx[i]->nparts == n, "pa_comm_init_all: pass the contexts of parts 1..nparts in order");
+    CHECK_ARG(!ctx[i]->comm, "pa_comm_init_all: a communicator is already attached");
+    devs[i] = ctx[i]->device;
+    for (int j = 0; j < i; ++j)
+      CHECK_ARG(devs[j] != devs[i], "pa_comm_init_all: one part per device (RCCL rejects two ranks on one GPU)");
+  }
+  std::vector<ncclComm_t> comms(n);
+  NCCLC(ncclCommInitAll(comms.data(), n, devs.data()));
+  for (int i = 0; i < n; ++i) ctx[i]->comm = comms[i];
+  return 0;
+}
+
 int pa_ctx_set_timing(pa_ctx* c, int enable) {
   CHECK_ARG(c, "null ctx");
   c->timing = enable != 0;
+  c->tn = 0;
+  return 0;
+}
+
+// Means over the mul! calls recorded since timing was enabled (events read
+// after the last one completes: no synchronisation inside the timed calls);
+// the record is then cleared.
+int pa_ctx_kernel_times(pa_ctx* c, float* int_ms, float* halo_ms, float* bnd_ms, int* count) {
+  CHECK_ARG(c, "null ctx");
+  float a = 0.f, h = 0.f, b = 0.f;
+  const int n = c->tn;
+  if (n > 0) {
+    HIPC(hipSetDevice(c->device));
+    HIPC(hipEventSynchronize(c->tev[4 * (n - 1) + 3]));
+    for (int k = 0; k < n; ++k) {
+      float t01 = 0.f, t12 = 0.f, t23 = 0.f;
+      HIPC(hipEventElapsedTime(&t01, c->tev[4 * k], c->tev[4 * k + 1]));
+      HIPC(hipEventElapsedTime(&t12, c->tev[4 * k + 1], c->tev[4 * k + 2]));
+      HIPC(hipEventElapsedTime(&t23, c->tev[4 * k + 2], c->tev[4 * k + 3]));
+      a += t01; h += t12; b += t23;
+    }
+    a /= n; h /= n; b /= n;
+  }
+  if (int_ms) *int_ms = a;
+  if (halo_ms) *halo_ms = h;
+  if (bnd_ms) *bnd_ms = b;
+  if (count) *count = n;
+  c->tn = 0;
   return 0;
 }
 
 int pa_ctx_last_kernel_ms(pa_ctx* c, float* int_ms, float* bnd_ms) {
-  CHECK_ARG(c, "null ctx");
-  *int_ms = c->last_int_ms;
-  *bnd_ms = c->last_bnd_ms;
-  return 0;
+  return pa_ctx_kernel_times(c, int_ms, nullptr, bnd_ms, nullptr);
 }
 
 // ---------------------------------------------------------------------------
@@ -1520,6 +1598,43 @@ int pa_mat_long_rows(const pa_mat* A, int64_t* n_long, int64_t* n_long_nnz) {
   return 0;
 }
 
+// Bytes one mul! streams from the matrix in its current encoding (the
+// kernels' own loads, padding included): values, column ids, and the slice
+// metadata (offsets, lengths, lists, patterns, masks, side-row maps).
+int pa_mat_traffic(const pa_mat* A, int64_t* value_bytes, int64_t* index_bytes, int64_t* meta_bytes) {
+  CHECK_ARG(A, "null matrix");
+  const int64_t S = (int64_t)dtype_size(A->dtype), H = A->H, W = H / 64;
+  const bool pat = g_spmv_format == 1 && A->has_pat;
+  const bool split = A->d_bnd_list != nullptr;
+  int64_t v = 0, ix = 0, m = 0;
+  for (int64_t s = 0; s < A->nslices; ++s) {
+    const int kd = pat ? A->h_kind[s] : 0;
+    if (kd == 1) {
+      v += (int64_t)A->h_plen[s] * H * S;
+      m += (int64_t)A->kmax * 4 + W * 8 + 8 + 4 + 4;  // pattern, mask, offset, length, list entry
+    } else if (kd == 2) {
+      v += (int64_t)A->h_plen[s] * H * S;
+      m += (int64_t)PA_MP_NP * A->kmp * 4 + 64 + W * 8 + 8 + 4 + 4;
+    } else {
+      v += (int64_t)A->h_slen[s] * H * S;
+      ix += (int64_t)A->h_slen[s] * H * 4;
+      m += 8 + 4 + ((pat || split) ? 4 : 0);
+    }
+  }
+  if (pat) {
+    v += A->s_slots * S;
+    ix += A->s_slots * 4 + A->s_nrows * 4;  // column ids, row map
+    m += A->s_nslices * 12;
+  }
+  v += A->n_lnz * S;
+  ix += A->n_lnz * 4;
+  m += A->n_long * 16;
+  if (value_bytes) *value_bytes = v;
+  if (index_bytes) *index_bytes = ix;
+  if (meta_bytes) *meta_bytes = m;
+  return 0;
+}
+
 int pa_mat_info(const pa_mat* A, int64_t* nrows, int64_t* nnz, int64_t* slots, int64_t* nslices,
                 int64_t* nslices_int) {
   CHECK_ARG(A, "null matrix");
@@ -1535,6 +1650,147 @@ int pa_mat_info(const pa_mat* A, int64_t* nrows, int64_t* nnz, int64_t* slots, i
 // mul! for the n local parts; with want_dot each part's dot(x, y) over its
 // owned rows is accumulated by the SpMV kernel itself (per-slice partials in
 // A->d_dotp, folded by fold_dot) — the CG's `dot(u, c)` after `mul!(c, A, u)`.
+constexpr int kMaxTimed = 1024;  // mul! calls recorded per context between reads
+
+// The grouped path applies when every part of the call shares one stream
+// pair (pa_ctx_create_shared: same device, one in-order chain) and every
+// halo neighbour is a part of this call served by the pull-unpack.
+static bool group_ok(int n, pa_mat* const A[], pa_xchg* const xg[], bool any_x, int dt) {
+  if (!g_spmv_group || n < 2) return false;
+  const pa_ctx* c0 = A[0]->ctx;
+  for (int i = 0; i < n; ++i)
+    if (A[i]->ctx->s_main != c0->s_main || A[i]->ctx->s_comm != c0->s_comm) return false;
+  if (!any_x) return true;
+  if (!g_halo_pull) return false;
+  LocalSet L = local_set(n, xg);
+  for (int i = 0; i < n; ++i) {
+    for (const auto* lst : {&xg[i]->parts_snd, &xg[i]->parts_rcv})
+      for (int32_t q : *lst)
+        if (L.find(q) < 0) return false;
+    if (build_pull(i, n, xg, L, dt, 0)) return false;
+    if (!xg[i]->pull[0].ok || !xg[i]->plan_fwd.unique) return false;
+  }
+  return true;
+}
+
+// mul! over parts sharing a stream pair: one pack, one pull-unpack and one
+// launch per slice kind and phase for all parts (kernel-argument tables),
+// instead of the same sequence per part.  Every slice is computed by the
+// same wave code as in the per-part launches: results are identical.
+static int spmv_grouped(int n, pa_mat* const A[], pa_vec* const y[], const pa_index* const y_idx[],
+                        pa_vec* const x[], pa_xchg* const xg[], bool any_x, bool has_alpha, int bmode,
+                        const void* alpha, const void* beta, const std::vector<void*>& dotp, bool want_dot,
+                        CGState* const* dot_tail, const std::vector<hipEvent_t*>& tslot, int dt) {
+  pa_ctx* c0 = A[0]->ctx;
+  HIPC(hipSetDevice(c0->device));
+  const hipStream_t sm = SM(c0), sc = SC(c0);
+  auto mark = [&](int k) -> int {
+    for (int i = 0; i < n; ++i)
+      if (tslot[i]) HIPC(hipEventRecord(tslot[i][k], sm));
+    return 0;
+  };
+  if (any_x) {
+    // the previous exchange's pulls read the send buffers: pack after them
+    if (!g_capturing) HIPC(hipStreamWaitEvent(c0->s_main, c0->ev_recvd, 0));
+    PackGroup pg{};
+    PullGroup qg{};
+    for (int i0 = 0; i0 < n; i0 += PA_GROUP_MAX) {
+      pg.np = qg.np = 0;
+      for (int i = i0; i < n && i < i0 + PA_GROUP_MAX; ++i) {
+        pa_xchg* X = xg[i];
+        const int k = pg.np++;
+        pg.n[k] = X->n_snd_data;
+        pg.lids[k] = X->d_lids_snd;
+        pg.v[k] = x[i]->d;
+        pg.buf[k] = X->d_buf_snd;
+      }
+      launch_pack_group(dt, pg, sm);
+    }
+    EV(hipEventRecord(c0->ev_packed, sm));
+    EV(hipStreamWaitEvent(sc, c0->ev_packed, 0));
+    for (int i0 = 0; i0 < n; i0 += PA_GROUP_MAX) {
+      qg.np = 0;
+      for (int i = i0; i < n && i < i0 + PA_GROUP_MAX; ++i) {
+        pa_xchg* X = xg[i];
+        const pa_pull& P = X->pull[0];
+        const int k = qg.np++;
+        qg.n[k] = X->n_rcv_data;
+        qg.lids[k] = X->d_lids_rcv;
+        qg.bid[k] = P.d_bid;
+        qg.elem[k] = P.d_elem;
+        qg.bases[k] = (const void* const*)P.d_bases;
+        qg.v[k] = x[i]->d;
+      }
+      launch_pull_group(dt, qg, sc);
+    }
+    EV(hipEventRecord(c0->ev_recvd, sc));
+  }
+  HIPC(hipGetLastError());
+  std::vector<SpmvPart> P0, P1, P3;
+  auto part = [&](int i, int64_t nwork, const int32_t* list) {
+    const int32_t* ymap = y_idx[i]->own_contig ? nullptr : y_idx[i]->d_oid_to_lid;
+    return SpmvPart{nwork, list, A[i], x[i]->d, y[i]->d, ymap, dotp[i]};
+  };
+  auto launch_all = [&](int which, const std::vector<SpmvPart>& v) {
+    if (!v.empty()) launch_spmv_group(which, (int)v.size(), v.data(), has_alpha, bmode, alpha, beta, sm);
+  };
+  if (mark(0)) return -1;
+  // interior slices (no ghost column): overlap with the pulls on the comm stream
+  for (int i = 0; i < n; ++i) {
+    if (g_spmv_format == 1 && A[i]->has_pat) {
+      P0.push_back(part(i, A[i]->np_int, A[i]->d_pint_list));
+      P3.push_back(part(i, A[i]->nm_int, A[i]->d_mint_list));
+      P1.push_back(part(i, A[i]->nx_int, A[i]->d_xint_list));
+    } else if (A[i]->d_bnd_list) {
+      P1.push_back(part(i, A[i]->nslices_int, A[i]->d_int_list));
+    } else {
+      P1.push_back(part(i, A[i]->nslices, nullptr));
+    }
+  }
+  launch_all(0, P0);
+  launch_all(3, P3);
+  launch_all(1, P1);
+  if (mark(1)) return -1;
+  if (any_x) EV(hipStreamWaitEvent(sm, c0->ev_recvd, 0));
+  if (mark(2)) return -1;
+  P0.clear(); P1.clear(); P3.clear();
+  std::vector<SpmvPart> P2;
+  for (int i = 0; i < n; ++i) {
+    if (g_spmv_format == 1 && A[i]->has_pat) {
+      P0.push_back(part(i, A[i]->np_bnd, A[i]->d_pbnd_list));
+      P3.push_back(part(i, A[i]->nm_bnd, A[i]->d_mbnd_list));
+      P1.push_back(part(i, A[i]->nx_bnd, A[i]->d_xbnd_list));
+      P2.push_back(part(i, A[i]->s_nslices, nullptr));
+    } else if (A[i]->d_bnd_list) {
+      P1.push_back(part(i, A[i]->nslices - A[i]->nslices_int, A[i]->d_bnd_list));
+    }
+  }
+  launch_all(0, P0);
+  launch_all(3, P3);
+  launch_all(1, P1);
+  launch_all(2, P2);
+  for (int i = 0; i < n; ++i) {
+    const int32_t* ymap = y_idx[i]->own_contig ? nullptr : y_idx[i]->d_oid_to_lid;
+    const bool pat = g_spmv_format == 1 && A[i]->has_pat;
+    const int64_t long_base = A[i]->nslices + (pat ? A[i]->s_nslices : 0);
+    launch_spmv_long(A[i], x[i]->d, y[i]->d, ymap, has_alpha, bmode, alpha, beta, dotp[i], long_base, sm);
+    if (want_dot) {
+      pa_ctx* c = A[i]->ctx;
+      const bool cplx = dt == PA_C64 || dt == PA_C128;
+      const int nbp = (int)(long_base + A[i]->n_long);
+      if (dot_tail)
+        launch_fold_cg_alpha(dt, nbp, A[i]->d_dotp, c->d_fold, c->d_result, c->d_ticket, dot_tail[i], sm);
+      else
+        launch_fold(cplx, nbp, A[i]->d_dotp, c->d_fold, c->d_result, c->d_ticket, sm);
+    }
+  }
+  if (mark(3)) return -1;
+  HIPC(hipGetLastError());
+  for (int i = 0; i < n; ++i)
+    if (tslot[i]) ++A[i]->ctx->tn;
+  return 0;
+}
+
 static int spmv_impl(int n, pa_mat* const A[], pa_vec* const y[], const pa_index* const y_idx[],
                      pa_vec* const x[], const pa_index* const x_idx[], pa_xchg* const xg[],
                      const void* alpha, const void* beta, bool want_dot, CGState* const* dot_tail = nullptr) {
@@ -1568,6 +1824,30 @@ static int spmv_impl(int n, pa_mat* const A[], pa_vec* const y[], const pa_index
   const bool has_alpha = !scalar_is(dt, alpha, 1.0);
   const int bmode = scalar_is(dt, beta, 0.0) ? 0 : (scalar_is(dt, beta, 1.0) ? 1 : 2);
   bool pulled = false;
+  // timing: the events of this call (slot tn of each timed context)
+  std::vector<hipEvent_t*> tslot(n, nullptr);
+  for (int i = 0; i < n; ++i) {
+    pa_ctx* c = A[i]->ctx;
+    if (!c->timing || g_capture_stream || c->tn >= kMaxTimed) continue;
+    if ((int)c->tev.size() < 4 * (c->tn + 1)) {
+      HIPC(hipSetDevice(c->device));
+      for (int k = 0; k < 4; ++k) {
+        hipEvent_t e;
+        HIPC(hipEventCreate(&e));
+        c->tev.push_back(e);
+      }
+    }
+    tslot[i] = &c->tev[4 * c->tn];
+  }
+  if (group_ok(n, A, xg, any_x, dt)) {
+    if (any_x)
+      for (int i = 0; i < n; ++i) {
+        CHECK_ARG(xg[i] && xg[i]->ctx == x[i]->ctx, "mul!: exchanger missing for some parts");
+        if (check_lids(xg[i], x[i])) return -1;
+      }
+    return spmv_grouped(n, A, y, y_idx, x, xg, any_x, has_alpha, bmode, alpha, beta, dotp, want_dot, dot_tail,
+                        tslot, dt);
+  }
 
   if (any_x) {
     for (int i = 0; i < n; ++i) {
@@ -1587,7 +1867,7 @@ static int spmv_impl(int n, pa_mat* const A[], pa_vec* const y[], const pa_index
     pa_ctx* c = A[i]->ctx;
     HIPC(hipSetDevice(c->device));
     const int32_t* ymap = y_idx[i]->own_contig ? nullptr : y_idx[i]->d_oid_to_lid;
-    if (c->timing) EV(hipEventRecord(c->ev_t[0], SM(c)));
+    if (tslot[i]) HIPC(hipEventRecord(tslot[i][0], SM(c)));
     // interior slices (no ghost column): overlap with the halo transport
     if (g_spmv_format == 1 && A[i]->has_pat) {
       launch_spmv_part(0, A[i]->np_int, A[i]->d_pint_list, A[i], x[i]->d, y[i]->d, ymap, has_alpha, bmode, alpha, beta, dotp[i], SM(c));
@@ -1599,7 +1879,7 @@ static int spmv_impl(int n, pa_mat* const A[], pa_vec* const y[], const pa_index
     } else {
       launch_spmv_part(1, A[i]->nslices, nullptr, A[i], x[i]->d, y[i]->d, ymap, has_alpha, bmode, alpha, beta, dotp[i], SM(c));
     }
-    if (c->timing) EV(hipEventRecord(c->ev_t[1], SM(c)));
+    if (tslot[i]) HIPC(hipEventRecord(tslot[i][1], SM(c)));
   }
   HIPC(hipGetLastError());
   for (int i = 0; i < n; ++i) {
@@ -1611,7 +1891,7 @@ static int spmv_impl(int n, pa_mat* const A[], pa_vec* const y[], const pa_index
         launch_unpack(dt, xg[i]->n_rcv_data, xg[i]->d_lids_rcv, xg[i]->plan_fwd, PA_REPLACE,
                       xg[i]->d_buf_rcv, x[i]->d, SM(c));
     }
-    if (c->timing) EV(hipEventRecord(c->ev_t[2], SM(c)));
+    if (tslot[i]) HIPC(hipEventRecord(tslot[i][2], SM(c)));
     const int32_t* ymap = y_idx[i]->own_contig ? nullptr : y_idx[i]->d_oid_to_lid;
     if (g_spmv_format == 1 && A[i]->has_pat) {
       // pattern slices reading ghosts, then the side rows (after the halo)
@@ -1635,17 +1915,11 @@ static int spmv_impl(int n, pa_mat* const A[], pa_vec* const y[], const pa_index
       else
         launch_fold(cplx, nbp, A[i]->d_dotp, c->d_fold, c->d_result, c->d_ticket, SM(c));
     }
-    if (c->timing) EV(hipEventRecord(c->ev_t[3], SM(c)));
+    if (tslot[i]) HIPC(hipEventRecord(tslot[i][3], SM(c)));
   }
   HIPC(hipGetLastError());
-  for (int i = 0; i < n; ++i) {
-    pa_ctx* c = A[i]->ctx;
-    if (c->timing) {
-      HIPC(hipEventSynchronize(c->ev_t[3]));
-      HIPC(hipEventElapsedTime(&c->last_int_ms, c->ev_t[0], c->ev_t[1]));
-      HIPC(hipEventElapsedTime(&c->last_bnd_ms, c->ev_t[2], c->ev_t[3]));
-    }
-  }
+  for (int i = 0; i < n; ++i)
+    if (tslot[i]) ++A[i]->ctx->tn;
   return 0;
 }
 

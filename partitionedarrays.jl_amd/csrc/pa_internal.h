@@ -198,6 +198,36 @@ struct CGState {
   int64_t xit;       // iterations whose x .+= α.*u is applied (deferred into the next u update)
 };
 
+// Grouped launches (parts of one process sharing a stream pair): one launch
+// per phase covers up to PA_GROUP_MAX parts (kernel-argument tables).
+constexpr int PA_GROUP_MAX = 8;
+struct SpmvPart {
+  int64_t nwork;          // slices of this part in the launch
+  const int32_t* list;    // slice ids (null: 0..nwork-1)
+  const pa_mat* A;
+  const void* x;
+  void* y;
+  const int32_t* ymap;
+  void* dotp;
+};
+
+struct PackGroup {
+  int np;
+  int64_t n[PA_GROUP_MAX];
+  const int32_t* lids[PA_GROUP_MAX];
+  const void* v[PA_GROUP_MAX];
+  void* buf[PA_GROUP_MAX];
+};
+struct PullGroup {
+  int np;
+  int64_t n[PA_GROUP_MAX];
+  const int32_t* lids[PA_GROUP_MAX];
+  const int32_t* bid[PA_GROUP_MAX];
+  const int64_t* elem[PA_GROUP_MAX];
+  const void* const* bases[PA_GROUP_MAX];
+  void* v[PA_GROUP_MAX];
+};
+
 // Cartesian part box of a synthetic stencil operator (pa_mat_stencil).
 struct StencilGeom {
   int64_t N[3];   // global nodes per dim
@@ -228,10 +258,12 @@ struct pa_ctx {
   void* d_gather = nullptr;       // nparts*16 B gathered partials (RCCL mode)
   unsigned* d_ticket = nullptr;   // arrival counter of the one-launch folds (0 between launches)
   void* h_pinned = nullptr;       // pinned host staging (>= nparts*16 B)
-  // timing
+  // timing (pa_ctx_set_timing): four events per recorded mul! — before the
+  // interior slices, after them, after the halo wait (+unpack), after the
+  // boundary slices — read back only by pa_ctx_kernel_times (no sync per call)
   bool timing = false;
-  hipEvent_t ev_t[4] = {nullptr, nullptr, nullptr, nullptr};
-  float last_int_ms = 0.f, last_bnd_ms = 0.f;
+  std::vector<hipEvent_t> tev;
+  int tn = 0;                     // mul! calls recorded since timing was enabled
   // events for the exchange pipeline
   hipEvent_t ev_packed = nullptr;
   hipEvent_t ev_recvd = nullptr;
@@ -313,6 +345,9 @@ struct pa_mat {
   int64_t slots = 0;         // SELL slots incl. padding
   int64_t nslices = 0;
   int64_t nslices_int = 0;   // slices without ghost-column entries
+  std::vector<int32_t> h_slen;      // host copies for pa_mat_traffic: int32-layout slice lengths,
+  std::vector<int32_t> h_kind;      // pattern-layout slice kinds (0 int32, 1 pattern, 2 multi-pattern)
+  std::vector<int32_t> h_plen;      // and entries per row of each pattern-layout slice
   int64_t* d_slice_off = nullptr;   // nslices (slot offset of each slice)
   int32_t* d_slice_len = nullptr;   // nslices (entries per row, max over slice)
   int32_t* d_int_list = nullptr;    // interior slice ids (null: all interior 0..n-1)

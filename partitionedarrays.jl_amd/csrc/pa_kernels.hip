@@ -177,6 +177,64 @@ void launch_unpack(int dtype, int64_t n, const int32_t* lids, const pa_combine_p
 }
 
 // ---------------------------------------------------------------------------
+// Grouped pack / pull for the parts of one process that share a stream pair
+// (pa_spmv_all's grouped path): one launch for all parts, blockIdx.y = part,
+// so the per-part pointers are wave-uniform kernel arguments.
+
+template <typename T>
+__global__ void k_pack_group(const PackGroup g) {
+  const int p = blockIdx.y;
+  const int64_t n = g.n[p];
+  const int32_t* __restrict__ lids = g.lids[p];
+  const T* __restrict__ v = (const T*)g.v[p];
+  T* __restrict__ buf = (T*)g.buf[p];
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    buf[i] = v[lids[i]];
+}
+
+// forward halo (every ghost lid received once): v[lids[i]] = bases[bid[i]][elem[i]]
+template <typename T>
+__global__ void k_pull_group(const PullGroup g) {
+  const int p = blockIdx.y;
+  const int64_t n = g.n[p];
+  const int32_t* __restrict__ lids = g.lids[p];
+  const int32_t* __restrict__ bid = g.bid[p];
+  const int64_t* __restrict__ elem = g.elem[p];
+  const T* const* __restrict__ bases = (const T* const*)g.bases[p];
+  T* __restrict__ v = (T*)g.v[p];
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    v[lids[i]] = bases[bid[i]][elem[i]];
+}
+
+static inline dim3 group_grid(const int64_t* n, int np) {
+  int64_t m = 1;
+  for (int i = 0; i < np; ++i) m = n[i] > m ? n[i] : m;
+  return dim3((unsigned)grid_for(m, 256, 1024), (unsigned)np);
+}
+
+void launch_pack_group(int dtype, const PackGroup& g, hipStream_t st) {
+  if (g.np <= 0) return;
+  const dim3 grid = group_grid(g.n, g.np);
+  switch (dtype) {
+    case PA_F32: hipLaunchKernelGGL(k_pack_group<float>, grid, dim3(256), 0, st, g); break;
+    case PA_F64: hipLaunchKernelGGL(k_pack_group<double>, grid, dim3(256), 0, st, g); break;
+    case PA_C64: hipLaunchKernelGGL(k_pack_group<c64>, grid, dim3(256), 0, st, g); break;
+    case PA_C128: hipLaunchKernelGGL(k_pack_group<c128>, grid, dim3(256), 0, st, g); break;
+  }
+}
+
+void launch_pull_group(int dtype, const PullGroup& g, hipStream_t st) {
+  if (g.np <= 0) return;
+  const dim3 grid = group_grid(g.n, g.np);
+  switch (dtype) {
+    case PA_F32: hipLaunchKernelGGL(k_pull_group<float>, grid, dim3(256), 0, st, g); break;
+    case PA_F64: hipLaunchKernelGGL(k_pull_group<double>, grid, dim3(256), 0, st, g); break;
+    case PA_C64: hipLaunchKernelGGL(k_pull_group<c64>, grid, dim3(256), 0, st, g); break;
+    case PA_C128: hipLaunchKernelGGL(k_pull_group<c128>, grid, dim3(256), 0, st, g); break;
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Elementwise vector kernels.  Index maps: null → identity over [0,n) (plus
 // base offset), else lid = map[i].
 

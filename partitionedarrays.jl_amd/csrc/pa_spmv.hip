@@ -316,14 +316,12 @@ __device__ __forceinline__ void rows_pattern(T (&acc)[R], const int32_t* __restr
 // implied columns for the rows of their mask) or multi-pattern slices (2:
 // the same with one of PA_MP_NP patterns per lane, staged in LDS); one
 // kernel per kind keeps the hot loop free of the others' code and registers.
+// One wave computes work item w (slice a.list[w], or w) of the structure a.
 template <typename T, int R, bool ALPHA, int BMODE, int U, int PK>
-__global__ __launch_bounds__(256) void k_spmv_sell(SpmvArgs<T> a) {
+__device__ __forceinline__ void spmv_wave(const SpmvArgs<T>& a, const int64_t w) {
   constexpr bool PAT = PK != 0;
   constexpr int H = 64 * R;
   const int lane = threadIdx.x & 63;
-  const int64_t blk = (a.flags & SPMV_XCD) ? xcd_remap(blockIdx.x, gridDim.x) : (int64_t)blockIdx.x;
-  const int64_t w = blk * 4 + (threadIdx.x >> 6);
-  if (w >= a.nwork) return;
   const int64_t s = a.list ? (int64_t)a.list[w] : w;
   const int64_t off = a.soff[s];
   const int len = a.slen[s];
@@ -428,6 +426,60 @@ __global__ __launch_bounds__(256) void k_spmv_sell(SpmvArgs<T> a) {
   }
 }
 
+template <typename T, int R, bool ALPHA, int BMODE, int U, int PK>
+__global__ __launch_bounds__(256) void k_spmv_sell(SpmvArgs<T> a) {
+  const int64_t blk = (a.flags & SPMV_XCD) ? xcd_remap(blockIdx.x, gridDim.x) : (int64_t)blockIdx.x;
+  const int64_t w = blk * 4 + (threadIdx.x >> 6);
+  if (w >= a.nwork) return;
+  spmv_wave<T, R, ALPHA, BMODE, U, PK>(a, w);
+}
+
+// Several parts of one device in ONE launch (parts sharing a stream pair):
+// the work items of part p are [start[p], start[p+1]) of the grid's waves,
+// so a mul! over P small parts fills the GPU once instead of P times and
+// costs one launch per phase instead of P.  Each wave computes exactly what
+// the per-part launch computes (same slice, same order).
+template <typename T>
+struct SpmvGroup {
+  int np;
+  int64_t start[PA_GROUP_MAX + 1];
+  SpmvArgs<T> a[PA_GROUP_MAX];
+};
+
+template <typename T, int R, bool ALPHA, int BMODE, int U, int PK>
+__global__ __launch_bounds__(256) void k_spmv_sell_group(const SpmvGroup<T> g) {
+  // wave-uniform: the part's arguments are read with scalar loads
+  const int64_t w = (int64_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  if (w >= g.start[g.np]) return;
+  int p = 0;
+  while (p + 1 < g.np && w >= g.start[p + 1]) ++p;
+  p = __builtin_amdgcn_readfirstlane(p);
+  spmv_wave<T, R, ALPHA, BMODE, U, PK>(g.a[p], w - g.start[p]);
+}
+
+template <typename T, int R, bool ALPHA, int BMODE, int PAT>
+static void launch_group_t(const SpmvGroup<T>& g, hipStream_t st) {
+  const int64_t blocks = (g.start[g.np] + 3) / 4;
+  if (blocks == 0) return;
+  if (g_spmv_unroll == 4)
+    hipLaunchKernelGGL((k_spmv_sell_group<T, R, ALPHA, BMODE, 4, PAT>), dim3(blocks), dim3(256), g_spmv_lds, st, g);
+  else
+    hipLaunchKernelGGL((k_spmv_sell_group<T, R, ALPHA, BMODE, 8, PAT>), dim3(blocks), dim3(256), g_spmv_lds, st, g);
+}
+
+template <typename T, int R, int PAT>
+static void launch_group_ab(const SpmvGroup<T>& g, bool has_alpha, int bmode, hipStream_t st) {
+  if (!has_alpha) {
+    if (bmode == 0) launch_group_t<T, R, false, 0, PAT>(g, st);
+    else if (bmode == 1) launch_group_t<T, R, false, 1, PAT>(g, st);
+    else launch_group_t<T, R, false, 2, PAT>(g, st);
+  } else {
+    if (bmode == 0) launch_group_t<T, R, true, 0, PAT>(g, st);
+    else if (bmode == 1) launch_group_t<T, R, true, 1, PAT>(g, st);
+    else launch_group_t<T, R, true, 2, PAT>(g, st);
+  }
+}
+
 template <typename T, int R, bool ALPHA, int BMODE, int PAT>
 static void launch_t(const SpmvArgs<T>& a, hipStream_t st) {
   const int64_t blocks = (a.nwork + 3) / 4;
@@ -454,10 +506,9 @@ static void launch_ab(const SpmvArgs<T>& a, bool has_alpha, int bmode, hipStream
 // which = 0: pattern slices of the main structure; 1: int32-column slices
 // of the main structure; 2: side SELL; 3: multi-pattern slices of the main
 // structure.  list/nwork select the slices.
-template <typename T, int R>
-static void launch_which(int which, int64_t nwork, const int32_t* list, const pa_mat* A, const void* x,
-                         void* y, const int32_t* ymap, bool has_alpha, int bmode, const void* alpha,
-                         const void* beta, void* dotp, hipStream_t st) {
+template <typename T>
+static SpmvArgs<T> make_args(int which, int64_t nwork, const int32_t* list, const pa_mat* A, const void* x,
+                             void* y, const int32_t* ymap, const void* alpha, const void* beta, void* dotp) {
   SpmvArgs<T> a{};
   a.dotu = (const T*)x;
   a.dotp = dotp;
@@ -501,9 +552,52 @@ static void launch_which(int which, int64_t nwork, const int32_t* list, const pa
     a.sflags = A->d_sflags;
     a.lmask = A->d_lmask;
   }
+  return a;
+}
+
+template <typename T, int R>
+static void launch_which(int which, int64_t nwork, const int32_t* list, const pa_mat* A, const void* x,
+                         void* y, const int32_t* ymap, bool has_alpha, int bmode, const void* alpha,
+                         const void* beta, void* dotp, hipStream_t st) {
+  const SpmvArgs<T> a = make_args<T>(which, nwork, list, A, x, y, ymap, alpha, beta, dotp);
   if (which == 0) launch_ab<T, R, 1>(a, has_alpha, bmode, st);
   else if (which == 3) launch_ab<T, R, 2>(a, has_alpha, bmode, st);
   else launch_ab<T, R, 0>(a, has_alpha, bmode, st);
+}
+
+// the same slices of np parts as one launch per PA_GROUP_MAX parts
+template <typename T, int R>
+static void group_which(int which, int np, const SpmvPart* parts, bool has_alpha, int bmode, const void* alpha,
+                        const void* beta, hipStream_t st) {
+  SpmvGroup<T> g{};
+  auto flush = [&]() {
+    if (g.np == 0) return;
+    if (which == 0) launch_group_ab<T, R, 1>(g, has_alpha, bmode, st);
+    else if (which == 3) launch_group_ab<T, R, 2>(g, has_alpha, bmode, st);
+    else launch_group_ab<T, R, 0>(g, has_alpha, bmode, st);
+    g = SpmvGroup<T>{};
+  };
+  for (int i = 0; i < np; ++i) {
+    const SpmvPart& q = parts[i];
+    if (q.nwork <= 0) continue;
+    const int32_t* list = q.list;
+    if ((g_spmv_flags & SPMV_IDLIST) && list && which != 2 && q.nwork == q.A->nslices) list = nullptr;
+    g.a[g.np] = make_args<T>(which, q.nwork, list, q.A, q.x, q.y, q.ymap, alpha, beta, q.dotp);
+    g.start[g.np + 1] = g.start[g.np] + q.nwork;
+    if (++g.np == PA_GROUP_MAX) flush();
+  }
+  flush();
+}
+
+void launch_spmv_group(int which, int np, const SpmvPart* parts, bool has_alpha, int bmode, const void* alpha,
+                       const void* beta, hipStream_t st) {
+  if (np <= 0) return;
+  switch (parts[0].A->dtype) {
+    case PA_F32: group_which<float, 4>(which, np, parts, has_alpha, bmode, alpha, beta, st); break;
+    case PA_F64: group_which<double, 2>(which, np, parts, has_alpha, bmode, alpha, beta, st); break;
+    case PA_C64: group_which<c64, 2>(which, np, parts, has_alpha, bmode, alpha, beta, st); break;
+    case PA_C128: group_which<c128, 1>(which, np, parts, has_alpha, bmode, alpha, beta, st); break;
+  }
 }
 
 // ---------------------------------------------------------------------------

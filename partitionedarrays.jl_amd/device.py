@@ -36,9 +36,17 @@ class PartContext:
         _lib.call("pa_ctx_set_timing", self.h, 1 if on else 0)
 
     def last_kernel_ms(self):
+        """(interior, boundary) ms, means over the mul! calls since set_timing(True)"""
         a, b = C.c_float(), C.c_float()
         _lib.call("pa_ctx_last_kernel_ms", self.h, C.byref(a), C.byref(b))
         return a.value, b.value
+
+    def kernel_times(self):
+        """dict of mean interior / halo (wait + unpack) / boundary ms and the
+        number of mul! calls recorded since set_timing(True); clears the record"""
+        a, h, b, n = C.c_float(), C.c_float(), C.c_float(), C.c_int()
+        _lib.call("pa_ctx_kernel_times", self.h, C.byref(a), C.byref(h), C.byref(b), C.byref(n))
+        return {"interior_ms": a.value, "halo_wait_ms": h.value, "boundary_ms": b.value, "calls": n.value}
 
     def close(self):
         """pa_ctx_destroy; every vector/matrix of the part must be gone."""
@@ -51,29 +59,34 @@ class HIPBackend(SequentialBackend):
     """All parts in this process, part p on device devices[(p-1) % len(devices)]
     (SequentialBackend semantics, HIP parts)."""
 
-    def __init__(self, devices=None, share_streams=False, graph_mul=False):
-        """graph_mul: mul!(c, a, b, α, β) captures a HIP graph the first time
+    def __init__(self, devices=None, share_streams=True, graph_mul=False, rccl=False):
+        """share_streams (default): parts on the same device share one stream
+        pair, and mul! runs them as one grouped launch per phase (pack,
+        pull-unpack, interior and boundary slices of every part together;
+        pa_tune("spmv_group")).  False: a stream pair per part and per-part
+        launches.
+        graph_mul: mul!(c, a, b, α, β) captures a HIP graph the first time
         it sees (c, a, b, α, β) and replays it afterwards (pamd.SpMVGraph; at
         most 16 cached, least recently used evicted; a structure that cannot
         be captured, e.g. parts on several devices, stays eager).  Off by
-        default.  With share_streams on one device it is the fast path for
-        many small parts (C5, 8 Voronoi parts of 128³: 0.36 ms per mul!
-        against 0.5-1.6 ms eager, tools/c5_bench.py)."""
+        default.
+        rccl: one part per device; the halo moves by RCCL grouped
+        ncclSend/ncclRecv between the parts of this process (pa_comm_init_all
+        + pa_tune("halo_transport", 1)), the MPIBackend transport without
+        processes.  Default: the parts read each other's packed buffers."""
         ndev = _lib.device_count()
         if ndev == 0:
             raise _lib.PAError("HIPBackend: no HIP device visible")
         self.devices = list(devices) if devices is not None else list(range(ndev))
         self.share_streams = share_streams
         self.graph_mul = graph_mul
+        self.rccl = rccl
         self.ctx = {}
 
     def get_part_ids(self, nparts):
-        """With share_streams, parts on the same device share one stream pair:
-        their kernels form one in-order chain instead of cross-stream event
-        waits.  Off by default: small parts fill the GPU better from separate
-        streams (C5, 8 parts of 128³/8 on one GPU: 0.48 vs 1.05 ms per mul!);
-        large parts gain from the chain (eight 256³ parts: 0.82 vs 0.91 ms
-        per part, tools/weak_sim.py)."""
+        """With share_streams, parts on the same device share one stream pair
+        (pa_ctx_create_shared): one in-order chain, and mul! launches each
+        phase once for all of them (the grouped path of pa_spmv_all)."""
         ids = super().get_part_ids(nparts)
         n = ids.num_parts
         first = {}
@@ -83,6 +96,11 @@ class HIPBackend(SequentialBackend):
             share = first.get(d) if self.share_streams else None
             self.ctx[p] = PartContext(d, p, n, share_with=share)
             first.setdefault(d, self.ctx[p])
+        if self.rccl and n > 1:
+            if len({c.device for c in self.ctx.values()}) != n:
+                raise _lib.PAError("HIPBackend(rccl=True): one part per device (RCCL rejects two ranks on one GPU)")
+            _lib.call("pa_comm_init_all", n, _lib.ptr_array([self.ctx[p].h for p in ids.part_ids]))
+            _lib.tune("halo_transport", 1)
         return ids
 
     def context(self, part) -> PartContext:
@@ -335,7 +353,14 @@ class DeviceMatrix:
         lr = [C.c_int64() for _ in range(2)]
         _lib.call("pa_mat_long_rows", self.h, *[C.byref(x) for x in lr])
         d.update(zip(["long_rows", "long_nnz"], [x.value for x in lr]))
+        d.update(self.traffic())
         return d
+
+    def traffic(self):
+        """bytes one mul! streams from the matrix (current encoding)"""
+        t = [C.c_int64() for _ in range(3)]
+        _lib.call("pa_mat_traffic", self.h, *[C.byref(x) for x in t])
+        return dict(zip(["value_bytes", "index_bytes", "meta_bytes"], [x.value for x in t]))
 
     def __del__(self):
         try:

@@ -189,3 +189,82 @@ def test_ptimer_sequential(pamd):
     d = t.data
     assert set(d) == {"a", "b"} and all(v["min"] == v["max"] == v["avg"] for v in d.values())
     assert "Section" in t.report()
+
+
+def _worker_segments(rank, world, port, shape, N, kind, q):
+    """one part per process: the halo messages its RCCL group would post
+    (pa_api.cpp transport(): forward = exchange!, reverse = assemble!), as
+    (peer part, element count, gids in buffer order) per send and receive"""
+    try:
+        sys.path.insert(0, ROOT)
+        os.environ["MASTER_ADDR"] = "127.0.0.1"
+        os.environ["MASTER_PORT"] = str(port)
+        import torch.distributed as dist
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        import pamd
+        be = pamd.DistributedBackend()
+        parts = be.get_part_ids(shape)
+        _, cols = pamd.drivers.stencil_partition(parts, N, kind)
+        p = parts.part_ids[0]
+        s = cols.partition.local(p)
+        ex = cols.exchanger
+
+        def segs(part_list, table):
+            out = []
+            for k, peer in enumerate(part_list.local(p)):
+                lids = table.local(p)[k + 1]  # Table segment k (1-based), Helpers.jl:63-94
+                out.append((int(peer), len(lids), s.lid_to_gid[np.asarray(lids) - 1].tolist()))
+            return out
+        fwd_snd, fwd_rcv = segs(ex.parts_snd, ex.lids_snd), segs(ex.parts_rcv, ex.lids_rcv)
+        # reverse(exchanger) (Interfaces.jl:796-798): rcv and snd swap
+        msgs = {"fwd": (fwd_snd, fwd_rcv), "rev": (fwd_rcv, fwd_snd)}
+        allm = [None] * world
+        dist.all_gather_object(allm, (p, msgs))
+        dist.barrier()
+        dist.destroy_process_group()
+        q.put((rank, allm))
+    except Exception as e:  # pragma: no cover - surfaced by the parent
+        import traceback
+        q.put((rank, {"error": repr(e) + traceback.format_exc()}))
+
+
+@pytest.mark.parametrize("world,shape", [(2, (2, 1, 1)), (4, (2, 2, 1)), (8, (2, 2, 2))])
+def test_rccl_segment_pairing(world, shape):
+    """The grouped ncclSend/ncclRecv of the halo (pa_api.cpp transport(),
+    MPIBackend.jl:261-309) relies on every message being posted on both
+    sides with the same length — SequentialBackend.jl:187's check — and on
+    the sender's packed values being the receiver's ghosts in the same
+    order.  Every ordered pair of ranks of the (2,1,1), (2,2,1), (2,2,2)
+    partitions, forward (exchange!) and reverse (assemble!), over gloo."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    N, kind = (11, 9, 8), 27
+    ps = [ctx.Process(target=_worker_segments, args=(r, world, port, shape, N, kind, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = {}
+    for _ in range(world):
+        r, out = q.get(timeout=300)
+        res[r] = out
+    for p in ps:
+        p.join(timeout=60)
+    for r, out in res.items():
+        assert not isinstance(out, dict), out.get("error")
+    allm = dict(res[0])  # part -> messages, identical on every rank
+    assert all(dict(res[r]) == allm for r in res)
+    npairs = 0
+    for direction in ("fwd", "rev"):
+        for a, msgs in allm.items():
+            for peer, cnt, gids in msgs[direction][0]:
+                rcv_b = [m for m in allm[peer][direction][1] if m[0] == a]
+                assert len(rcv_b) == 1, f"{direction}: part {peer} posts {len(rcv_b)} receives from part {a}"
+                _, cnt_b, gids_b = rcv_b[0]
+                assert cnt == cnt_b, f"{direction}: {a}->{peer} sends {cnt}, receiver expects {cnt_b}"
+                assert gids == gids_b, f"{direction}: {a}->{peer} packs other gids than the receiver unpacks"
+                npairs += cnt > 0
+        for b, msgs in allm.items():  # no receive without its send
+            for peer, cnt, _ in msgs[direction][1]:
+                assert any(m[0] == b for m in allm[peer][direction][0]), f"{direction}: {b} waits on {peer}"
+    n_nbrs = {2: 1, 4: 3, 8: 7}[world]
+    assert npairs == 2 * world * n_nbrs  # every part talks to all others, both directions

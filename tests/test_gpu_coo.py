@@ -37,9 +37,27 @@ def _random_coo(rng, rows, cols, p, n_per_row, dtype, dup=3, ghost_rows=True):
     return I, J, V.astype(dtype)
 
 
+def _csc_equal(O, got_colptr, got_rowval, got_nzval, ref):
+    """device CSC pattern/values == the oracle's sparse(I, J, V) (SparseUtils.jl:80-94)"""
+    if not (np.array_equal(got_colptr, ref.colptr) and np.array_equal(got_rowval, ref.rowval)):
+        return False
+    if isinstance(ref.nzval, O.Cx):
+        return np.array_equal(got_nzval.real, ref.nzval.re) and np.array_equal(got_nzval.imag, ref.nzval.im)
+    return np.array_equal(got_nzval, ref.nzval)
+
+
+def _oracle_coo(O, I, J, V):
+    if np.iscomplexobj(V):
+        return I.copy(), J.copy(), O.Cx(V.real.copy(), V.imag.copy())
+    return I.copy(), J.copy(), V.copy()
+
+
 @pytest.mark.parametrize("dtype", [np.float64, np.float32, np.complex128, np.complex64])
 @pytest.mark.parametrize("shape,N", [((2, 2, 1), (12, 10, 9)), ((1, 1, 1), (9, 8, 7))])
-def test_device_sparse_equals_host(be, pamd, shape, N, dtype):
+def test_device_sparse_equals_oracle(be, pamd, O, shape, N, dtype):
+    """pa_mat_from_coo (rocPRIM sorts, duplicates summed in input order) ==
+    the oracle's sparse_csc: the CSC pattern and nonzeros(A) bit for bit; the
+    host compresscoo → pa_mat_from_csc path builds the same device layout."""
     parts = be.get_part_ids(shape)
     _, part = pamd.drivers.stencil_partition(parts, N, 27)
     rows = cols = part  # ghost lids as rows too: stored ghost rows (FE assembly)
@@ -50,11 +68,12 @@ def test_device_sparse_equals_host(be, pamd, shape, N, dtype):
         ctx = be.context(p)
         ri, ci = pamd.device_index(ctx, r), pamd.device_index(ctx, s)
         M, colptr, rowval = pamd.DeviceMatrix.from_coo(ctx, I, J, V, ri, ci, r.num_lids, s.num_lids)
+        ref = O.sparse_csc(*_oracle_coo(O, I, J, V), r.num_lids, s.num_lids)
+        assert _csc_equal(O, colptr, rowval, M.get_values(), ref)
         H = pamd.compresscoo(I, J, V, r.num_lids, s.num_lids)
-        assert np.array_equal(colptr, H.colptr) and np.array_equal(rowval, H.rowval)
-        assert np.array_equal(M.get_values(), H.nzval)
         M2 = pamd.DeviceMatrix.from_csc(ctx, H, ri, ci, r.num_lids, s.num_lids)
         assert M.info() == M2.info()
+        assert np.array_equal(M2.get_values(), M.get_values())
 
 
 @pytest.mark.parametrize("dtype", [np.float64, np.complex128])
@@ -64,32 +83,43 @@ def test_device_sparse_spmv(be, pamd, O, dtype):
     parts = be.get_part_ids((2, 2, 1))
     N = (11, 9, 8)
     _, part = pamd.drivers.stencil_partition(parts, N, 27)
+    OA = O.stencil_problem(O.get_part_ids((2, 2, 1)), N, 27)
+    opart = OA.cols  # the same lids, ghosts and Exchanger as `part`
     rng = np.random.default_rng(17)
     # no ghost-row entries: a random ghost layer is not a consistent pattern for matrix_exchanger
     coo = {p: _random_coo(rng, part, part, p, 7, dtype, ghost_rows=False) for p in parts.part_ids}
     mk = lambda k: pamd.PData(parts.backend, parts.part_ids, [coo[p][k] for p in parts.part_ids], parts.shape)
     A = pamd.PSparseMatrix.from_coo(mk(0), mk(1), mk(2), part, part, ids="local")
-    xs = {p: rng.uniform(-1, 1, part.partition.local(p).num_lids).astype(dtype) for p in parts.part_ids}
+    oc = {p: _oracle_coo(O, *coo[p]) for p in parts.part_ids}
+    omk = lambda k: O.PData([oc[p][k] for p in parts.part_ids], (2, 2, 1))
+    OM = O.psparse_from_coo(omk(0), omk(1), omk(2), opart, opart, ids="local")
+    xs = {p: _rand_vec(rng, part.partition.local(p).num_lids, dtype) for p in parts.part_ids}
     x = pamd.PVector.from_host(pamd.map_parts(lambda s: xs[s.part], part.partition), part)
     y = pamd.PVector.undef(part, dtype)
     pamd.mul_(y, A, x)
+    ox = O.PVector(O.map_parts(lambda s: _oracle_vec(O, xs[s.part]), opart.partition), opart)
+    oy = O.pvector_undef(opart, dtype)
+    O.mul_(oy, OM, ox)
+    got = y.to_host()
     for p in parts.part_ids:
-        s = part.partition.local(p)
-        H = pamd.compresscoo(*coo[p], s.num_lids, s.num_lids)
-        # the reference's local loop (SparseUtils.jl:157-187) on the host CSC, owned rows
-        xl = x.to_host().local(p)
-        want = np.zeros(s.num_lids, dtype=dtype)
-        l2o = np.zeros(s.num_lids, dtype=np.int64)
-        l2o[s.oid_to_lid - 1] = 1
-        order = list(s.oid_to_lid - 1) + list(s.hid_to_lid - 1)
-        for j in order:
-            for q in range(H.colptr[j] - 1, H.colptr[j + 1] - 1):
-                i = H.rowval[q] - 1
-                if l2o[i]:
-                    want[i] = want[i] + H.nzval[q] * xl[j]
-        got = y.to_host().local(p)
-        own = s.oid_to_lid - 1
-        assert np.array_equal(got[own], want[own])
+        own = part.partition.local(p).oid_to_lid - 1
+        ref = oy.values[p]
+        g = got.local(p)[own]
+        if isinstance(ref, O.Cx):
+            assert np.array_equal(g.real, ref.re[own]) and np.array_equal(g.imag, ref.im[own])
+        else:
+            assert np.array_equal(g, ref[own])
+
+
+def _rand_vec(rng, n, dtype):
+    v = rng.uniform(-1, 1, n)
+    if np.dtype(dtype).kind == "c":
+        v = v + 1j * rng.uniform(-1, 1, n)
+    return v.astype(dtype)
+
+
+def _oracle_vec(O, a):
+    return O.Cx(a.real.copy(), a.imag.copy()) if np.iscomplexobj(a) else a.copy()
 
 
 def test_device_sparse_int32_and_bounds(be, pamd):
@@ -133,35 +163,30 @@ def test_device_sparse_int32_and_bounds(be, pamd):
 
 
 @pytest.mark.parametrize("N,nparts", [((24, 22, 20), 8), ((13, 11, 9), 3)])
-def test_device_add_gids_and_to_lids(be, pamd, N, nparts):
+def test_device_add_gids_and_to_lids(be, pamd, O, N, nparts):
     """add_gids!(rows, J) with the first-touch discovery on the device
-    (pa_add_gids) gives the same ghost layer (gids, owners, order) and
-    Exchanger as the host restatement; PSparseMatrix(...; ids=:global) with
-    to_lids! on the device equals the host-mapped build."""
+    (pa_add_gids) gives the oracle's ghost layer (gids, owners, order) and
+    Exchanger (irregular_problem: add_gids!, Exchanger(ids),
+    Interfaces.jl:579-627, 723-786); PSparseMatrix(...; ids=:global) with
+    to_lids! on the device holds the oracle's nonzeros(A) in CSC order."""
     drv = pamd.drivers
     owners = drv.voronoi_owners(N, nparts)
-    parts_h = pamd.sequential.get_part_ids(nparts)
-    rows_h, cols_h, I_h, J_h, V_h = drv.irregular_partition(parts_h, N, 27, owners)
     parts = be.get_part_ids(nparts)
     rows, cols, I, J, V = drv.irregular_partition(parts, N, 27, owners)
-    for p in parts.part_ids:
-        a, b = cols.partition.local(p), cols_h.partition.local(p)
-        assert np.array_equal(a.lid_to_gid, b.lid_to_gid) and np.array_equal(a.lid_to_part, b.lid_to_part)
-        assert np.array_equal(a.hid_to_lid, b.hid_to_lid)
+    OA = O.irregular_problem(O.get_part_ids(nparts), N, 27, np.float64, owners)
+    for i, p in enumerate(parts.part_ids):
+        a, b = cols.partition.local(p), OA.cols.partition.parts[i]
+        assert np.array_equal(a.lid_to_gid, np.asarray(b.lid_to_gid))
+        assert np.array_equal(a.lid_to_part, np.asarray(b.lid_to_part))
+        assert np.array_equal(a.hid_to_lid, np.asarray(b.hid_to_lid))
         for t in ("lids_rcv", "lids_snd"):
-            ta, tb = getattr(cols.exchanger, t).local(p), getattr(cols_h.exchanger, t).local(p)
-            assert np.array_equal(ta.data, tb.data) and np.array_equal(ta.ptrs, tb.ptrs)
-        assert np.array_equal(cols.exchanger.parts_rcv.local(p), cols_h.exchanger.parts_rcv.local(p))
-        assert np.array_equal(cols.exchanger.parts_snd.local(p), cols_h.exchanger.parts_snd.local(p))
+            ta, tb = getattr(cols.exchanger, t).local(p), getattr(OA.cols.exchanger, t).parts[i]
+            assert np.array_equal(ta.data, np.asarray(tb.data)) and np.array_equal(ta.ptrs, np.asarray(tb.ptrs))
+        assert list(cols.exchanger.parts_rcv.local(p)) == list(OA.cols.exchanger.parts_rcv.parts[i])
+        assert list(cols.exchanger.parts_snd.local(p)) == list(OA.cols.exchanger.parts_snd.parts[i])
     A = pamd.PSparseMatrix.from_coo(I, J, V, rows, cols, ids="global")
-    Il = pamd.map_parts(lambda i, s: s.to_lids(i), I, rows.partition)
-    Jl = pamd.map_parts(lambda j, s: s.to_lids(j), J, cols.partition)
-    B = pamd.PSparseMatrix.from_coo(Il, Jl, V, rows, cols, ids="local")
-    for p in parts.part_ids:
-        assert np.array_equal(A.values.local(p).get_values(), B.values.local(p).get_values())
-        assert A.values.local(p).info() == B.values.local(p).info()
-
-
+    for i, p in enumerate(parts.part_ids):
+        assert np.array_equal(A.values.local(p).get_values(), OA.values.parts[i].nzval)
 def test_device_to_lids_unknown_gid(be, pamd):
     parts = be.get_part_ids(1)
     rows = pamd.prange_linear(parts, 10)

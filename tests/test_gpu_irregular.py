@@ -52,7 +52,9 @@ def _eq(O, got, ref):
 @pytest.mark.parametrize("N,nparts,dtype,fmt", [
     (BIG[0], BIG[1], np.float64, 1), (BIG[0], BIG[1], np.float64, 0),
     (BIG[0], BIG[1], np.float32, 1), (BIG[0], BIG[1], np.complex128, 1),
-    ((24, 22, 20), 8, np.complex64, 1), ((24, 22, 20), 8, np.float64, 0)])
+    ((24, 22, 20), 8, np.complex64, 1), ((24, 22, 20), 8, np.float64, 0),
+    (BIG[0], 8, np.float64, 1), (BIG[0], 8, np.float32, 1),       # C5 as benched: 8 parts of one device
+    ((24, 22, 20), 12, np.float64, 1), ((24, 22, 20), 12, np.complex128, 0)])  # > PA_GROUP_MAX parts
 def test_irregular_spmv_bitexact(be, pamd, O, N, nparts, dtype, fmt):
     prev = pamd._lib.tune("spmv_format", fmt)
     try:
@@ -145,3 +147,35 @@ def test_irregular_multipattern_bitexact(be, pamd, O, N, nparts, dtype, npat):
             assert nmulti > 0, "no slice took several patterns on the Voronoi partition"
     finally:
         pamd._lib.tune("spmv_patterns", prev)
+
+
+@pytest.mark.parametrize("dtype,fmt", [(np.float64, 1), (np.float64, 0), (np.complex128, 1), (np.float32, 1)])
+def test_grouped_launches_equal_per_part(be, pamd, dtype, fmt):
+    """pa_tune("spmv_group"): the parts sharing a stream pair as one launch
+    per phase (default) give the same bits as the per-part launches, the
+    fused SpMV+dot included (C5: 8 Voronoi parts of 128³)."""
+    N, nparts = BIG[0], 8
+    prev = pamd._lib.tune("spmv_format", fmt)
+    try:
+        parts = be.get_part_ids(nparts)
+        A = pamd.drivers.irregular_problem(parts, N, 27, dtype)
+        rng = np.random.default_rng(SEED + 3)
+        xs = {p: _rand(rng, A.cols.partition.local(p).num_lids, dtype) for p in parts.part_ids}
+        out = {}
+        for grp in (1, 0):
+            g0 = pamd._lib.tune("spmv_group", grp)
+            try:
+                x = pamd.PVector.from_host(pamd.map_parts(lambda s: xs[s.part], A.cols.partition), A.cols)
+                y = pamd.PVector.undef(A.rows, dtype)
+                pamd.mul_(y, A, x, 2.0, 0.0)
+                d = pamd.mul_dot_(y, A, x)
+                out[grp] = ([v.copy() for v in y.to_host().parts], [v.copy() for v in x.to_host().parts], d)
+            finally:
+                pamd._lib.tune("spmv_group", g0)
+        for a, b in zip(out[0][0], out[1][0]):
+            assert np.array_equal(a, b)
+        for a, b in zip(out[0][1], out[1][1]):
+            assert np.array_equal(a, b)
+        assert out[0][2] == out[1][2]
+    finally:
+        pamd._lib.tune("spmv_format", prev)

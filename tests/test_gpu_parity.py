@@ -270,3 +270,53 @@ def test_shared_stream_parts(pamd, O):
     assert out[False][4] == out[True][4]
     for a, b in zip(out[True][0], out[True][2]):
         assert np.array_equal(a, b)
+
+
+@pytest.mark.parametrize("alpha", [1.0, -2.5])
+def test_beta_zero_overwrites_nan_inf(be, pamd, O, fmt, alpha):
+    """β = 0 is fill!(c, 0), not c*0 (SparseUtils.jl:167-168, Interfaces.jl:
+    2262-2263): NaN / ±Inf in the prior c do not leak, and rows without
+    entries become +0.0 even where c held a negative value (c*0 = -0.0).
+    Bitwise against the oracle (literal and vectorised), both encodings."""
+    shape, N = (2, 1, 1), (9, 8, 7)
+    parts = be.get_part_ids(shape)
+    _, part = pamd.drivers.stencil_partition(parts, N, 27)
+    OA = O.stencil_problem(O.get_part_ids(shape), N, 27)
+    opart = OA.cols
+    coo, empty = {}, {}
+    for i, p in enumerate(parts.part_ids):
+        M = OA.values.parts[i]
+        s = part.partition.local(p)
+        cols_of = np.repeat(np.arange(1, M.n + 1), np.diff(M.colptr))
+        oid = np.zeros(s.num_lids, np.int64)
+        oid[s.oid_to_lid - 1] = np.arange(1, s.num_oids + 1)
+        keep = (oid[M.rowval - 1] % 5) != 0  # every 5th owned row (and all ghost rows) left empty
+        coo[p] = (M.rowval[keep].copy(), cols_of[keep].copy(), np.asarray(M.nzval)[keep].copy())
+        empty[p] = s.oid_to_lid[np.arange(1, s.num_oids + 1) % 5 == 0] - 1
+    mk = lambda k: pamd.PData(parts.backend, parts.part_ids, [coo[p][k] for p in parts.part_ids], parts.shape)
+    A = pamd.PSparseMatrix.from_coo(mk(0), mk(1), mk(2), part, part, ids="local")
+    omk = lambda k: O.PData([coo[p][k].copy() for p in parts.part_ids], shape)
+    OM = O.psparse_from_coo(omk(0), omk(1), omk(2), opart, opart, ids="local")
+    rng = np.random.default_rng(SEED + 9)
+    xs = {p: rng.uniform(-1, 1, part.partition.local(p).num_lids) for p in parts.part_ids}
+    ys = {}
+    for p in parts.part_ids:
+        v = rng.uniform(-1, 1, part.partition.local(p).num_lids)
+        v[0::4], v[1::4], v[2::4] = np.nan, np.inf, -np.inf
+        v[empty[p]] = -1.0
+        ys[p] = v
+    x = pamd.PVector.from_host(pamd.map_parts(lambda s: xs[s.part], part.partition), part)
+    y = pamd.PVector.from_host(pamd.map_parts(lambda s: ys[s.part], part.partition), part)
+    pamd.mul_(y, A, x, alpha, 0.0)
+    got = y.to_host()
+    for literal in (True, False):
+        ox = O.PVector(O.map_parts(lambda s: xs[s.part].copy(), opart.partition), opart)
+        oy = O.PVector(O.map_parts(lambda s: ys[s.part].copy(), opart.partition), opart)
+        O.mul_(oy, OM, ox, alpha, 0.0, literal=literal)
+        for p in parts.part_ids:
+            own = part.partition.local(p).oid_to_lid - 1
+            g, r = got.local(p)[own], oy.values[p][own]
+            assert np.isfinite(g).all(), f"part {p}: NaN/Inf of the prior c leaked through β = 0"
+            assert np.array_equal(g.view(np.uint64), r.view(np.uint64)), (p, literal)
+            e = got.local(p)[empty[p]]
+            assert np.array_equal(e.view(np.uint64), np.zeros(len(e), np.uint64)), "empty rows must be +0.0"

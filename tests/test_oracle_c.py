@@ -1,0 +1,92 @@
+"""The C restatement (oracle/build/spmv_ref, test infrastructure) against the
+Python oracle, which the reference's own KATs pin (test_oracle_kats.py).
+
+The C oracle is the checker of the BASELINE-size GPU tests (C2, C3, C4,
+tests/test_gpu_fullsize.py), where the Python oracle is too slow:
+* its partitioned mul! (Cartesian parts, ghosts in add_gids! first-touch
+  order, owned-then-ghost summation) equals the Python oracle's mul! bit for
+  bit, and its row-wise form equals its literal column loop over each part's
+  local CSC (SparseUtils.jl:176-185) bit for bit;
+* its cg! (IterativeSolvers 0.9 recurrence) follows the Python oracle's
+  residual history (the two sum the owned partials of dot/norm in different
+  orders: 1e-12 relative)."""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REF = os.path.join(ROOT, "oracle", "build", "spmv_ref")
+
+
+@pytest.fixture(scope="module")
+def ref():
+    subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle")], check=True)
+    return REF
+
+
+def _global_from_parts(O, pv, n):
+    out = np.zeros(n)
+    for s, v in zip(pv.rows.partition.parts, pv.values.parts):
+        own = np.asarray(s.oid_to_lid) - 1
+        out[np.asarray(s.lid_to_gid)[own] - 1] = v[own]
+    return out
+
+
+def _run(ref, *args):
+    return subprocess.run([ref, *map(str, args)], check=True, capture_output=True, text=True).stdout
+
+
+@pytest.mark.parametrize("kind", [7, 27])
+@pytest.mark.parametrize("shape", [(1, 1, 1), (2, 1, 1), (2, 2, 1), (2, 2, 2), (3, 2, 1)])
+def test_partitioned_spmv_equals_python_oracle(O, ref, tmp_path, kind, shape):
+    N = 9
+    n = N ** 3
+    x = np.random.default_rng(5 + kind).uniform(-1, 1, n)
+    x.tofile(tmp_path / "x.bin")
+    _run(ref, "--kind", kind, "--n", N, "--parts", *shape, "--xin", tmp_path / "x.bin", "--yout",
+         tmp_path / "y.bin", "--threads", 3)
+    _run(ref, "--kind", kind, "--n", N, "--parts", *shape, "--xin", tmp_path / "x.bin", "--yout",
+         tmp_path / "yl.bin", "--literal")
+    y, yl = np.fromfile(tmp_path / "y.bin"), np.fromfile(tmp_path / "yl.bin")
+    assert np.array_equal(y, yl), "row-wise form differs from the literal column loop"
+    parts = O.get_part_ids(shape)
+    A = O.stencil_problem(parts, (N,) * 3, kind)
+    ox = O.PVector(O.map_parts(lambda s: x[np.asarray(s.lid_to_gid) - 1].copy(), A.cols.partition), A.cols)
+    oy = O.pvector_undef(A.rows)
+    O.mul_(oy, A, ox)
+    got = _global_from_parts(O, oy, n)
+    bad = np.flatnonzero(got != y)
+    assert bad.size == 0, f"{bad.size} rows differ from the Python oracle (first gid {bad[:1] + 1})"
+
+
+def test_one_part_literal_equals_partitioned(ref, tmp_path):
+    """the one-part literal CSC mode (the headline checker) == --parts 1 1 1"""
+    N = 12
+    x = np.random.default_rng(3).uniform(-1, 1, N ** 3)
+    x.tofile(tmp_path / "x.bin")
+    _run(ref, "--kind", 27, "--n", N, "--reps", 1, "--xin", tmp_path / "x.bin", "--yout", tmp_path / "a.bin")
+    _run(ref, "--kind", 27, "--n", N, "--parts", 1, 1, 1, "--xin", tmp_path / "x.bin", "--yout", tmp_path / "b.bin")
+    assert np.array_equal(np.fromfile(tmp_path / "a.bin"), np.fromfile(tmp_path / "b.bin"))
+
+
+@pytest.mark.parametrize("kind,shape", [(7, (2, 2, 2)), (27, (2, 2, 1)), (27, (1, 1, 1))])
+def test_cg_history_equals_python_oracle(O, ref, tmp_path, kind, shape):
+    N, K = 9, 12
+    n = N ** 3
+    b = np.random.default_rng(11).uniform(-1, 1, n)
+    b.tofile(tmp_path / "b.bin")
+    out = _run(ref, "--kind", kind, "--n", N, "--parts", *shape, "--cg", K, "--bin", tmp_path / "b.bin",
+               "--hist", tmp_path / "h.bin", "--xout", tmp_path / "x.bin", "--threads", 2)
+    h = np.fromfile(tmp_path / "h.bin")
+    assert len(h) == K, out
+    parts = O.get_part_ids(shape)
+    A = O.stencil_problem(parts, (N,) * 3, kind)
+    ob = O.PVector(O.map_parts(lambda s: b[np.asarray(s.lid_to_gid) - 1].copy(), A.cols.partition), A.cols)
+    ox = O.pvector_undef(A.cols)
+    hist = []
+    O.cg_(ox, A, ob, reltol=0.0, maxiter=K, log=hist)
+    assert len(hist) == K
+    np.testing.assert_allclose(h, hist, rtol=1e-12, atol=0)
+    np.testing.assert_allclose(np.fromfile(tmp_path / "x.bin"), _global_from_parts(O, ox, n), rtol=1e-10, atol=1e-12)

@@ -6,7 +6,8 @@ column-encoding coverage (pattern slices / regular rows) of the parts.
 1 = single-pattern slices); each build also reports the parts' SpMV kernel
 time (HIP events on the parts' streams, summed over the parts).
 
-    python tools/c5_bench.py [--n 128] [--parts 8] [--dtypes f64,f32,c128,c64] [--patterns 1,4] [--share]
+    python tools/c5_bench.py [--n 128] [--parts 8] [--dtypes f64,f32,c128,c64] [--patterns 1,4]
+                             [--own-streams] [--group 0|1] [--graph]
 """
 import argparse
 import json
@@ -27,11 +28,13 @@ ap.add_argument("--dtypes", default="f64,f32,c128,c64")
 ap.add_argument("--steps", type=int, default=20)
 ap.add_argument("--patterns", default="4")
 ap.add_argument("--rules", default="1", help="pa_tune spmv_pattern_rule values to A/B")
-ap.add_argument("--share", action="store_true", help="parts as one in-order chain (share_streams)")
+ap.add_argument("--own-streams", action="store_true", help="a stream pair per part (share_streams=False)")
+ap.add_argument("--group", type=int, default=1, help="pa_tune spmv_group: 1 grouped launches (default), 0 per part")
 ap.add_argument("--graph", action="store_true", help="also time the HIP-graph replay (pamd.SpMVGraph)")
 a = ap.parse_args()
 DT = {"f64": np.float64, "f32": np.float32, "c128": np.complex128, "c64": np.complex64}
-be = pamd.HIPBackend(devices=[0], share_streams=a.share)
+be = pamd.HIPBackend(devices=[0], share_streams=not a.own_streams)
+pamd._lib.tune("spmv_group", a.group)
 parts = be.get_part_ids(a.parts)
 N = (a.n,) * 3
 owners = pamd.drivers.voronoi_owners(N, a.parts)
@@ -55,6 +58,9 @@ for name, npat, rule in [(d, int(q), int(r)) for d in a.dtypes.split(",") for q 
         ex = A.cols.exchanger
         B += (f["nnz"] * (S + 4) + (f["nrows"] + 1) * 4 + (f["nrows"] + s.num_hids) * S + f["nrows"] * S
               + (len(ex.lids_snd.local(p).data) + len(ex.lids_rcv.local(p).data)) * (4 + 2 * S))
+        Bf = f["value_bytes"] + f["index_bytes"] + f["meta_bytes"] + (f["nrows"] + s.num_hids) * S + f["nrows"] * S \
+            + (len(ex.lids_snd.local(p).data) + len(ex.lids_rcv.local(p).data)) * (4 + 2 * S)
+        info["format_bytes"] = info.get("format_bytes", 0) + Bf
         for k in ("nslices", "pattern_slices", "multi_pattern_slices", "nrows", "regular_rows", "side_rows"):
             info[k] = info.get(k, 0) + f[k]
     for _ in range(3):
@@ -70,14 +76,17 @@ for name, npat, rule in [(d, int(q), int(r)) for d in a.dtypes.split(",") for q 
     ctxs = [be.context(p) for p in parts.part_ids]
     for c in ctxs:
         c.set_timing(True)
-    kms = []
-    for _ in range(5):
+    for _ in range(10):
         pamd.mul_(y, A, x)
-        kms.append(sum(sum(c.last_kernel_ms()) for c in ctxs))
+    kt = [c.kernel_times() for c in ctxs]
     for c in ctxs:
         c.set_timing(False)
         c.sync()
-    km = float(np.median(kms))
+    # shared stream pair: every part's events bracket the same grouped launches
+    if not a.own_streams and a.group:
+        km = kt[0]["interior_ms"] + kt[0]["boundary_ms"]
+    else:
+        km = sum(t["interior_ms"] + t["boundary_ms"] for t in kt)
     t_graph = None
     if a.graph:
         ref = y.to_host()
@@ -98,7 +107,9 @@ for name, npat, rule in [(d, int(q), int(r)) for d in a.dtypes.split(",") for q 
             assert np.array_equal(got.local(p)[own], ref.local(p)[own]), "graph replay differs from eager mul!"
         del g
     print(json.dumps({"config": f"C5 FE27 {a.n}^3 Voronoi {a.parts} parts on 1 GPU", "dtype": name,
-                      "spmv_patterns": npat, "spmv_pattern_rule": rule, "share_streams": a.share,
+                      "spmv_patterns": npat, "spmv_pattern_rule": rule, "share_streams": not a.own_streams,
+                      "spmv_group": a.group, "format_gbs_all_parts": round(info["format_bytes"] / t / 1e9, 1),
+                      "format_gbs_kernels": round(info["format_bytes"] / km / 1e6, 1),
                       "ms_per_mul": round(1e3 * t, 4),
                       "ms_per_mul_graph": None if t_graph is None else round(1e3 * t_graph, 4), "gbs_algorithmic_all_parts": round(B / t / 1e9, 1),
                       "kernel_ms_sum_over_parts": round(km, 4), "gbs_algorithmic_kernels": round(B / km / 1e6, 1),
