@@ -327,13 +327,17 @@ def main():
     sync()
     barrier()
     sync()
+    c0 = ctxs[0]
     t0 = time.perf_counter()
+    c0.span_start()  # HIP events on part 1's compute stream, over the timed region
     for i in range(args.steps):
         Ai, xi, yi = sets[i % ncopies]
         pamd.mul_(yi, Ai, xi)
+    c0.span_stop()
     sync()
     t1 = time.perf_counter()
     barrier()
+    span_ms = c0.span_ms() / args.steps
     elapsed = t1 - t0
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64)
@@ -342,10 +346,11 @@ def main():
     ms_per_step = 1e3 * elapsed / args.steps
     value = B_all / (elapsed / args.steps) / 1e9
 
-    # device time of every local part's mul! phases: HIP events on the stream
-    # the kernels run on, recorded over `reps` untimed calls and read after
-    # the last one (no synchronisation per call): interior slices, halo
-    # completion after them (transport wait + unpack), boundary slices
+    # attribution (untimed calls): every local part's mul! phases, HIP events
+    # on the stream the kernels run on, read after the last call (no
+    # synchronisation per call): interior slices, halo completion after them
+    # (transport wait + unpack), boundary slices (parts grouped on one stream
+    # pair report on their first part)
     reps = max(5, min(args.steps, 50))
 
     def phase_times():
@@ -364,17 +369,28 @@ def main():
         per_part = {k: v for d in allp for k, v in d.items()}
     p0 = parts.part_ids[0]
     info, s_nhids, n_snd0, n_rcv0 = infos[p0]
-    kernel_ms = phases[p0]["interior_ms"] + phases[p0]["boundary_ms"]
-    part_bytes = format_bytes(info, s_nhids, n_snd0, n_rcv0, S)
-    spmv_bytes = part_bytes - (n_snd0 + n_rcv0) * (4 + 2 * S)  # the SpMV kernels' share (no pack/unpack)
+    # the dominant kernels' device time per step: the HIP-event span of the
+    # timed region on part 1's compute stream / K; with several parts on one
+    # stream pair (grouped launches) the span covers all of them
+    grouped_here = (len(ctxs) > 1 and len({c.device for c in ctxs}) == 1
+                    and getattr(backend, "share_streams", False))
+    kernel_ms = span_ms
+    spmv_bytes = B_local if grouped_here else format_bytes(info, s_nhids, n_snd0, n_rcv0, S)
     achieved = spmv_bytes / (kernel_ms * 1e-3) / 1e9
     # the same kernels with int32 column ids everywhere (pa_tune spmv_format=0), for reference
     prev = pamd._lib.tune("spmv_format", 0)
-    ph32 = phase_times()[p0]
-    info32 = A.values.local(p0).traffic()
+    sync()
+    c0.span_start()
+    for i in range(reps):
+        Ai, xi, yi = sets[i % ncopies]
+        pamd.mul_(yi, Ai, xi)
+    c0.span_stop()
+    kernel_ms_int32 = c0.span_ms() / reps
+    bytes_int32 = 0
+    for p in (parts.part_ids if grouped_here else [p0]):
+        inf, nh, ns_, nr_ = infos[p]
+        bytes_int32 += format_bytes(dict(inf, **A.values.local(p).traffic()), nh, ns_, nr_, S)
     pamd._lib.tune("spmv_format", prev)
-    kernel_ms_int32 = ph32["interior_ms"] + ph32["boundary_ms"]
-    bytes_int32 = spmv_bytes - (info["value_bytes"] + info["index_bytes"] + info["meta_bytes"]) + sum(info32.values())
     box = box_hbm_gbs(pamd, spmv_bytes // 2) if world == 1 and ngpu == 1 else None
     traffic, tnote = (None, {"note": "skipped (--no-pmc)"})
     if rank == 0 and ngpu == 1 and not args.no_pmc:
@@ -424,13 +440,17 @@ def main():
             "frac": round(achieved / HBM_PEAK_GBS, 4),
             "traffic": None if traffic is None else int(traffic),
             "traffic_detail": tnote,
-            "kernel": "k_spmv_sell (all SpMV kernels of one mul! step of part %d: pattern + side slices)" % p0,
+            "kernel": ("k_spmv_sell (all SpMV kernels of one mul! step: pattern + side slices"
+                       + (", halo pack/pull" if halo else "") + ")"),
             "kernel_ms": round(kernel_ms, 4),
+            "kernel_ms_note": ("HIP events on part %d's compute stream around the K timed steps, / K" % p0
+                               + ("; all parts of this process (grouped launches)" if grouped_here else "")),
             "algorithmic_bytes_per_launch": int(spmv_bytes),
             "bytes_split": {"values": info["value_bytes"], "column_ids": info["index_bytes"],
                             "slice_metadata": info["meta_bytes"],
                             "x_y": int((info["nrows"] + s_nhids) * S + info["nrows"] * S)},
-            "csr_equivalent_achieved": round(csr_bytes(info["nnz"], info["nrows"], s_nhids, 0, 0, S)
+            "csr_equivalent_achieved": round((C_local if grouped_here else
+                                              csr_bytes(info["nnz"], info["nrows"], s_nhids, n_snd0, n_rcv0, S))
                                              / (kernel_ms * 1e-3) / 1e9, 1),
             "actual_hbm_gbs": None if traffic is None else round(traffic / (kernel_ms * 1e-3) / 1e9, 1),
             "actual_frac": None if traffic is None else round(traffic / (kernel_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),

@@ -53,7 +53,9 @@ int pa_device_count(int* count);
  *               bit 3: the last len % U entries of a slice as one
  *               predicated batch, bit 4: a slice list covering the whole
  *               structure is launched without the list, bit 5: y written
- *               with non-temporal stores (default 29);
+ *               with non-temporal stores, bit 6: launches whose rows have
+ *               at most 8 entries use the short-row kernels (one predicated
+ *               batch, no loop: fewer registers) (default 93);
  * "spmv_unroll" 4 or 8 entries in flight per lane (default 8);
  * "spmv_format" 1: pattern slices where the matrix has them (default),
  *               0: int32 column ids everywhere;
@@ -358,6 +360,13 @@ int pa_ctx_kernel_times(pa_ctx* ctx, float* interior_ms, float* halo_ms,
                         float* boundary_ms, int* count);
 int pa_ctx_last_kernel_ms(pa_ctx* ctx, float* spmv_interior_ms,
                           float* spmv_boundary_ms);
+/* Device time of a region on the compute stream: pa_ctx_span(ctx, 0) before
+ * it, pa_ctx_span(ctx, 1) after it (event records, no synchronisation);
+ * pa_ctx_span_ms waits for the end and returns the elapsed ms.  Parts whose
+ * mul! runs grouped (shared stream pair) record their phase times on the
+ * first part of the call only (pa_ctx_kernel_times: count 0 for the rest). */
+int pa_ctx_span(pa_ctx* ctx, int stop);
+int pa_ctx_span_ms(pa_ctx* ctx, float* ms);
 
 #ifdef __cplusplus
 }

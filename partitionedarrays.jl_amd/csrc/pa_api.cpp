@@ -259,6 +259,8 @@ int finish_sell_layout(pa_mat* A, const std::vector<int32_t>& slen, const std::v
   A->slots = acc;
   A->nslices = ns;
   A->h_slen = slen;
+  A->maxlen_all = 0;
+  for (int32_t l : slen) A->maxlen_all = std::max(A->maxlen_all, (int)l);
   std::vector<int32_t> ilist, blist;
   for (int64_t s = 0; s < ns; ++s) (sghost[s] ? blist : ilist).push_back((int32_t)s);
   A->nslices_int = (int64_t)ilist.size();
@@ -324,6 +326,11 @@ int finalize_pattern(pa_mat* A, int kmax, int64_t noids) {
     }
   }
   A->h_kind = kind;
+  A->maxlen_pat = A->maxlen_pm_int = 0;
+  for (int64_t s = 0; s < ns; ++s) {
+    if (kind[s] == 1) A->maxlen_pat = std::max(A->maxlen_pat, (int)A->h_plen[s]);
+    else if (kind[s] == 0) A->maxlen_pm_int = std::max(A->maxlen_pm_int, (int)A->h_slen[s]);
+  }
   A->np_int = (int64_t)pint.size();
   A->np_bnd = (int64_t)pbnd.size();
   A->nx_int = (int64_t)xint.size();
@@ -358,6 +365,8 @@ int finalize_pattern(pa_mat* A, int kmax, int64_t noids) {
     std::vector<int32_t> slen(A->s_nslices, 0);
     std::vector<int64_t> soff(A->s_nslices);
     for (int64_t i = 0; i < A->s_nrows; ++i) slen[i / A->H] = std::max(slen[i / A->H], rl[i]);
+    A->maxlen_side = 0;
+    for (int32_t l : slen) A->maxlen_side = std::max(A->maxlen_side, (int)l);
     int64_t acc = 0;
     for (int64_t s = 0; s < A->s_nslices; ++s) { soff[s] = acc; acc += (int64_t)slen[s] * A->H; }
     A->s_slots = acc;
@@ -621,9 +630,10 @@ int pa_tune(const char* key, int value, int* previous) {
   CHECK_ARG(key, "null key");
   int* slot = nullptr;
   if (!std::strcmp(key, "spmv_flags")) {
-    CHECK_ARG(value >= 0 && value <= 63,
+    CHECK_ARG(value >= 0 && value <= 127,
               "spmv_flags: bit 0 = non-temporal streams, bit 1 = XCD mapping, bit 2 = 16 B x runs (pattern rows), "
-              "bit 3 = masked tail batch, bit 4 = identity slice lists dropped, bit 5 = non-temporal y stores");
+              "bit 3 = masked tail batch, bit 4 = identity slice lists dropped, bit 5 = non-temporal y stores, "
+              "bit 6 = short-row kernels (launches whose rows have <= 8 entries)");
     slot = &g_spmv_flags;
   } else if (!std::strcmp(key, "spmv_lds")) {
     CHECK_ARG(value >= 0 && value <= 160 * 1024, "spmv_lds: bytes of LDS per SpMV block (occupancy cap)");
@@ -804,6 +814,8 @@ int pa_ctx_destroy(pa_ctx* c) {
   dev_free(c->d_ticket);
   if (c->h_pinned) (void)hipHostFree(c->h_pinned);
   for (auto& e : c->tev) (void)hipEventDestroy(e);
+  for (auto& e : c->span_ev)
+    if (e) (void)hipEventDestroy(e);
   if (c->stream_refs && --c->stream_refs->n == 0) {  // the last context of a shared stream pair
     (void)hipEventDestroy(c->ev_packed);
     (void)hipEventDestroy(c->ev_recvd);
@@ -895,6 +907,25 @@ int pa_ctx_kernel_times(pa_ctx* c, float* int_ms, float* halo_ms, float* bnd_ms,
   if (bnd_ms) *bnd_ms = b;
   if (count) *count = n;
   c->tn = 0;
+  return 0;
+}
+
+// Device time of a region of work on the compute stream: stop = 0 records
+// the start, stop = 1 the end (no synchronisation); pa_ctx_span_ms waits for
+// the end and returns the elapsed time.
+int pa_ctx_span(pa_ctx* c, int stop) {
+  CHECK_ARG(c && (stop == 0 || stop == 1), "pa_ctx_span: stop is 0 or 1");
+  HIPC(hipSetDevice(c->device));
+  if (!c->span_ev[stop]) HIPC(hipEventCreate(&c->span_ev[stop]));
+  HIPC(hipEventRecord(c->span_ev[stop], c->s_main));
+  return 0;
+}
+
+int pa_ctx_span_ms(pa_ctx* c, float* ms) {
+  CHECK_ARG(c && ms && c->span_ev[0] && c->span_ev[1], "pa_ctx_span_ms: record a start and an end first");
+  HIPC(hipSetDevice(c->device));
+  HIPC(hipEventSynchronize(c->span_ev[1]));
+  HIPC(hipEventElapsedTime(ms, c->span_ev[0], c->span_ev[1]));
   return 0;
 }
 
@@ -1824,11 +1855,14 @@ static int spmv_impl(int n, pa_mat* const A[], pa_vec* const y[], const pa_index
   const bool has_alpha = !scalar_is(dt, alpha, 1.0);
   const int bmode = scalar_is(dt, beta, 0.0) ? 0 : (scalar_is(dt, beta, 1.0) ? 1 : 2);
   bool pulled = false;
-  // timing: the events of this call (slot tn of each timed context)
+  // timing: the events of this call (slot tn of each timed context); the
+  // grouped path brackets all parts with the same launches: part 1 of the
+  // call records them once
+  const bool grouped = group_ok(n, A, xg, any_x, dt);
   std::vector<hipEvent_t*> tslot(n, nullptr);
   for (int i = 0; i < n; ++i) {
     pa_ctx* c = A[i]->ctx;
-    if (!c->timing || g_capture_stream || c->tn >= kMaxTimed) continue;
+    if (!c->timing || g_capture_stream || c->tn >= kMaxTimed || (grouped && i > 0)) continue;
     if ((int)c->tev.size() < 4 * (c->tn + 1)) {
       HIPC(hipSetDevice(c->device));
       for (int k = 0; k < 4; ++k) {
@@ -1839,7 +1873,7 @@ static int spmv_impl(int n, pa_mat* const A[], pa_vec* const y[], const pa_index
     }
     tslot[i] = &c->tev[4 * c->tn];
   }
-  if (group_ok(n, A, xg, any_x, dt)) {
+  if (grouped) {
     if (any_x)
       for (int i = 0; i < n; ++i) {
         CHECK_ARG(xg[i] && xg[i]->ctx == x[i]->ctx, "mul!: exchanger missing for some parts");

@@ -264,6 +264,7 @@ struct pa_ctx {
   bool timing = false;
   std::vector<hipEvent_t> tev;
   int tn = 0;                     // mul! calls recorded since timing was enabled
+  hipEvent_t span_ev[2] = {nullptr, nullptr};  // pa_ctx_span: start / end of a region
   // events for the exchange pipeline
   hipEvent_t ev_packed = nullptr;
   hipEvent_t ev_recvd = nullptr;
@@ -348,6 +349,9 @@ struct pa_mat {
   std::vector<int32_t> h_slen;      // host copies for pa_mat_traffic: int32-layout slice lengths,
   std::vector<int32_t> h_kind;      // pattern-layout slice kinds (0 int32, 1 pattern, 2 multi-pattern)
   std::vector<int32_t> h_plen;      // and entries per row of each pattern-layout slice
+  // longest row of each launch kind (SH kernels when <= 8): pattern slices,
+  // int32 slices (of the current encoding), side SELL
+  int maxlen_all = INT32_MAX, maxlen_pm_int = INT32_MAX, maxlen_pat = INT32_MAX, maxlen_side = INT32_MAX;
   int64_t* d_slice_off = nullptr;   // nslices (slot offset of each slice)
   int32_t* d_slice_len = nullptr;   // nslices (entries per row, max over slice)
   int32_t* d_int_list = nullptr;    // interior slice ids (null: all interior 0..n-1)

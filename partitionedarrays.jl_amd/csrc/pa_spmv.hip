@@ -37,7 +37,7 @@ __device__ inline int64_t xcd_remap(int64_t b, int64_t G) {
   return x * q + (x < r ? x : r) + i;
 }
 
-enum { SPMV_NT = 1, SPMV_XCD = 2, SPMV_XPAIR = 4, SPMV_TAILB = 8, SPMV_IDLIST = 16, SPMV_YNT = 32 };
+enum { SPMV_NT = 1, SPMV_XCD = 2, SPMV_XPAIR = 4, SPMV_TAILB = 8, SPMV_IDLIST = 16, SPMV_YNT = 32, SPMV_SHORT = 64 };
 typedef unsigned int spmv_u32x4 __attribute__((ext_vector_type(4)));
 // Process-wide knobs (pa_tune).  Defaults from the A/Bs in
 // profiles/r01_ab_spmv.txt and profiles/r01/ab_xpair.txt: non-temporal
@@ -45,7 +45,7 @@ typedef unsigned int spmv_u32x4 __attribute__((ext_vector_type(4)));
 // F32 −33 %, C64 −5 % kernel time), predicated tail batch on
 // (profiles/r01/ab_tail.txt: FD7 256³ F64 −31 %, F32 −42 %; FE27 −1…−3 %),
 // identity slice lists dropped (profiles/r01/ab_idlist.txt: FD7 −0.9 %, FE27 ±0).
-int g_spmv_flags = SPMV_NT | SPMV_XPAIR | SPMV_TAILB | SPMV_IDLIST;
+int g_spmv_flags = SPMV_NT | SPMV_XPAIR | SPMV_TAILB | SPMV_IDLIST | SPMV_SHORT;
 int g_spmv_unroll = 8;
 // dynamic LDS per SpMV block (unused by the kernel): caps the blocks per CU,
 // i.e. the waves streaming at once (160 KB LDS per CU)
@@ -103,6 +103,7 @@ struct SpmvArgs {
   // sflags[s] != 0 skip the rows whose lmask bit is set (null: none)
   const int32_t* sflags;
   const uint64_t* lmask;
+  int maxlen;               // longest row (entries) of the launch's slices: <= U selects the SH kernels
 };
 
 template <typename T> struct DAcc { using type = double; };
@@ -128,12 +129,13 @@ __device__ __forceinline__ c128 pick(bool c, c128 a, c128 b) { return c128{c ? a
 // int32-column rows: c < 0 is padding (skipped: never multiplied)
 // TB: the entries past the last full U batch run as one masked batch
 // (entries >= len re-read entry len-1 and are never accumulated)
-template <typename T, int R, bool ALPHA, bool NT, int U>
+template <typename T, int R, bool ALPHA, bool NT, int U, bool SH = false>
 __device__ __forceinline__ void rows_int32(T (&acc)[R], const IPack<R>* __restrict__ cp,
                                            const Pack<T, R>* __restrict__ vp, int len,
                                            const T* __restrict__ x, T alpha, bool TB) {
   int k = 0;
-  for (; k + U <= len; k += U) {
+  if (SH) TB = true;  // short rows (len <= U): the one masked batch is the whole row
+  for (; !SH && k + U <= len; k += U) {
     IPack<R> c[U];
     Pack<T, R> v[U];
 #pragma unroll
@@ -189,7 +191,7 @@ __device__ __forceinline__ void rows_int32(T (&acc)[R], const IPack<R>* __restri
       }
     k = len;
   }
-  for (; k < len; ++k) {
+  for (; !SH && k < len; ++k) {
     const IPack<R> c = ld<NT>(&cp[k * 64]);
     const Pack<T, R> v = ld<NT>(&vp[k * 64]);
 #pragma unroll
@@ -219,11 +221,12 @@ __device__ __forceinline__ Pack<T, R> ld_xrun(const T* p) {
 // pattern rows: column of row `rbase + r` at entry k is rbase + r + pat[k].
 // XP: the lane's R rows read R consecutive x values per entry, fetched as
 // one 16 B run (rows that are not regular get values they never use).
-template <typename T, int R, bool ALPHA, bool NT, int U, bool XP>
+template <typename T, int R, bool ALPHA, bool NT, int U, bool XP, bool SH = false>
 __device__ __forceinline__ void rows_pattern(T (&acc)[R], const int32_t* __restrict__ pat,
                                              const Pack<T, R>* __restrict__ vp, int len,
                                              const T* __restrict__ x, int64_t rbase,
                                              const bool (&ok)[R], T alpha, bool TB) {
+  if (SH) TB = true;  // short rows (len <= U): the one masked batch is the whole row
   int64_t xb[R];
   bool any = false;
 #pragma unroll
@@ -232,7 +235,7 @@ __device__ __forceinline__ void rows_pattern(T (&acc)[R], const int32_t* __restr
     any = any || ok[r];
   }
   int k = 0;
-  for (; k + U <= len; k += U) {
+  for (; !SH && k + U <= len; k += U) {
     int32_t o[U];
     Pack<T, R> v[U];
 #pragma unroll
@@ -298,7 +301,7 @@ __device__ __forceinline__ void rows_pattern(T (&acc)[R], const int32_t* __restr
       }
     k = len;
   }
-  for (; k < len; ++k) {
+  for (; !SH && k < len; ++k) {
     const int32_t o = pat[k];
     const Pack<T, R> v = ld<NT>(&vp[k * 64]);
 #pragma unroll
@@ -317,7 +320,9 @@ __device__ __forceinline__ void rows_pattern(T (&acc)[R], const int32_t* __restr
 // the same with one of PA_MP_NP patterns per lane, staged in LDS); one
 // kernel per kind keeps the hot loop free of the others' code and registers.
 // One wave computes work item w (slice a.list[w], or w) of the structure a.
-template <typename T, int R, bool ALPHA, int BMODE, int U, int PK>
+// SH: every row of the launch has at most U entries (FD7: 7) — the masked
+// batch alone, no loop code (fewer registers, more waves per SIMD).
+template <typename T, int R, bool ALPHA, int BMODE, int U, int PK, bool SH = false>
 __device__ __forceinline__ void spmv_wave(const SpmvArgs<T>& a, const int64_t w) {
   constexpr bool PAT = PK != 0;
   constexpr int H = 64 * R;
@@ -369,25 +374,25 @@ __device__ __forceinline__ void spmv_wave(const SpmvArgs<T>& a, const int64_t w)
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     const int32_t* pat = wp + (int)a.psel[s * 64 + lane] * a.kmax;
     if (a.flags & SPMV_XPAIR) {
-      if (a.flags & SPMV_NT) rows_pattern<T, R, ALPHA, true, U, true>(acc, pat, vp, len, a.x, row0, ok, a.alpha, tb);
-      else rows_pattern<T, R, ALPHA, false, U, true>(acc, pat, vp, len, a.x, row0, ok, a.alpha, tb);
+      if (a.flags & SPMV_NT) rows_pattern<T, R, ALPHA, true, U, true, SH>(acc, pat, vp, len, a.x, row0, ok, a.alpha, tb);
+      else rows_pattern<T, R, ALPHA, false, U, true, SH>(acc, pat, vp, len, a.x, row0, ok, a.alpha, tb);
     } else {
-      if (a.flags & SPMV_NT) rows_pattern<T, R, ALPHA, true, U, false>(acc, pat, vp, len, a.x, row0, ok, a.alpha, tb);
-      else rows_pattern<T, R, ALPHA, false, U, false>(acc, pat, vp, len, a.x, row0, ok, a.alpha, tb);
+      if (a.flags & SPMV_NT) rows_pattern<T, R, ALPHA, true, U, false, SH>(acc, pat, vp, len, a.x, row0, ok, a.alpha, tb);
+      else rows_pattern<T, R, ALPHA, false, U, false, SH>(acc, pat, vp, len, a.x, row0, ok, a.alpha, tb);
     }
   } else if constexpr (PK == 1) {
     const int32_t* pat = a.pat + s * a.kmax;
     if (a.flags & SPMV_XPAIR) {
-      if (a.flags & SPMV_NT) rows_pattern<T, R, ALPHA, true, U, true>(acc, pat, vp, len, a.x, row0, ok, a.alpha, tb);
-      else rows_pattern<T, R, ALPHA, false, U, true>(acc, pat, vp, len, a.x, row0, ok, a.alpha, tb);
+      if (a.flags & SPMV_NT) rows_pattern<T, R, ALPHA, true, U, true, SH>(acc, pat, vp, len, a.x, row0, ok, a.alpha, tb);
+      else rows_pattern<T, R, ALPHA, false, U, true, SH>(acc, pat, vp, len, a.x, row0, ok, a.alpha, tb);
     } else {
-      if (a.flags & SPMV_NT) rows_pattern<T, R, ALPHA, true, U, false>(acc, pat, vp, len, a.x, row0, ok, a.alpha, tb);
-      else rows_pattern<T, R, ALPHA, false, U, false>(acc, pat, vp, len, a.x, row0, ok, a.alpha, tb);
+      if (a.flags & SPMV_NT) rows_pattern<T, R, ALPHA, true, U, false, SH>(acc, pat, vp, len, a.x, row0, ok, a.alpha, tb);
+      else rows_pattern<T, R, ALPHA, false, U, false, SH>(acc, pat, vp, len, a.x, row0, ok, a.alpha, tb);
     }
   } else {
     const IPack<R>* __restrict__ cp = reinterpret_cast<const IPack<R>*>(a.col + off) + lane;
-    if (a.flags & SPMV_NT) rows_int32<T, R, ALPHA, true, U>(acc, cp, vp, len, a.x, a.alpha, tb);
-    else rows_int32<T, R, ALPHA, false, U>(acc, cp, vp, len, a.x, a.alpha, tb);
+    if (a.flags & SPMV_NT) rows_int32<T, R, ALPHA, true, U, SH>(acc, cp, vp, len, a.x, a.alpha, tb);
+    else rows_int32<T, R, ALPHA, false, U, SH>(acc, cp, vp, len, a.x, a.alpha, tb);
   }
 
   if (a.dotp) {  // fused dot(u, c): Σ conj(u_i)·c_i over this slice's rows
@@ -426,12 +431,12 @@ __device__ __forceinline__ void spmv_wave(const SpmvArgs<T>& a, const int64_t w)
   }
 }
 
-template <typename T, int R, bool ALPHA, int BMODE, int U, int PK>
+template <typename T, int R, bool ALPHA, int BMODE, int U, int PK, bool SH = false>
 __global__ __launch_bounds__(256) void k_spmv_sell(SpmvArgs<T> a) {
   const int64_t blk = (a.flags & SPMV_XCD) ? xcd_remap(blockIdx.x, gridDim.x) : (int64_t)blockIdx.x;
   const int64_t w = blk * 4 + (threadIdx.x >> 6);
   if (w >= a.nwork) return;
-  spmv_wave<T, R, ALPHA, BMODE, U, PK>(a, w);
+  spmv_wave<T, R, ALPHA, BMODE, U, PK, SH>(a, w);
 }
 
 // Several parts of one device in ONE launch (parts sharing a stream pair):
@@ -446,7 +451,7 @@ struct SpmvGroup {
   SpmvArgs<T> a[PA_GROUP_MAX];
 };
 
-template <typename T, int R, bool ALPHA, int BMODE, int U, int PK>
+template <typename T, int R, bool ALPHA, int BMODE, int U, int PK, bool SH = false>
 __global__ __launch_bounds__(256) void k_spmv_sell_group(const SpmvGroup<T> g) {
   // wave-uniform: the part's arguments are read with scalar loads
   const int64_t w = (int64_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
@@ -454,14 +459,18 @@ __global__ __launch_bounds__(256) void k_spmv_sell_group(const SpmvGroup<T> g) {
   int p = 0;
   while (p + 1 < g.np && w >= g.start[p + 1]) ++p;
   p = __builtin_amdgcn_readfirstlane(p);
-  spmv_wave<T, R, ALPHA, BMODE, U, PK>(g.a[p], w - g.start[p]);
+  spmv_wave<T, R, ALPHA, BMODE, U, PK, SH>(g.a[p], w - g.start[p]);
 }
 
 template <typename T, int R, bool ALPHA, int BMODE, int PAT>
 static void launch_group_t(const SpmvGroup<T>& g, hipStream_t st) {
   const int64_t blocks = (g.start[g.np] + 3) / 4;
   if (blocks == 0) return;
-  if (g_spmv_unroll == 4)
+  bool sh = PAT != 2 && (g_spmv_flags & SPMV_SHORT);
+  for (int i = 0; i < g.np; ++i) sh = sh && g.a[i].maxlen <= 8;
+  if (sh)
+    hipLaunchKernelGGL((k_spmv_sell_group<T, R, ALPHA, BMODE, 8, PAT, true>), dim3(blocks), dim3(256), g_spmv_lds, st, g);
+  else if (g_spmv_unroll == 4)
     hipLaunchKernelGGL((k_spmv_sell_group<T, R, ALPHA, BMODE, 4, PAT>), dim3(blocks), dim3(256), g_spmv_lds, st, g);
   else
     hipLaunchKernelGGL((k_spmv_sell_group<T, R, ALPHA, BMODE, 8, PAT>), dim3(blocks), dim3(256), g_spmv_lds, st, g);
@@ -484,7 +493,9 @@ template <typename T, int R, bool ALPHA, int BMODE, int PAT>
 static void launch_t(const SpmvArgs<T>& a, hipStream_t st) {
   const int64_t blocks = (a.nwork + 3) / 4;
   if (blocks == 0) return;
-  if (g_spmv_unroll == 4)
+  if (PAT != 2 && (g_spmv_flags & SPMV_SHORT) && a.maxlen <= 8)
+    hipLaunchKernelGGL((k_spmv_sell<T, R, ALPHA, BMODE, 8, PAT, true>), dim3(blocks), dim3(256), g_spmv_lds, st, a);
+  else if (g_spmv_unroll == 4)
     hipLaunchKernelGGL((k_spmv_sell<T, R, ALPHA, BMODE, 4, PAT>), dim3(blocks), dim3(256), g_spmv_lds, st, a);
   else
     hipLaunchKernelGGL((k_spmv_sell<T, R, ALPHA, BMODE, 8, PAT>), dim3(blocks), dim3(256), g_spmv_lds, st, a);
@@ -521,6 +532,10 @@ static SpmvArgs<T> make_args(int which, int64_t nwork, const int32_t* list, cons
   a.alpha = *(const T*)alpha;
   a.beta = *(const T*)beta;
   a.flags = g_spmv_flags;
+  a.maxlen = which == 0   ? A->maxlen_pat
+             : which == 2 ? A->maxlen_side
+             : which == 1 ? ((g_spmv_format == 1 && A->has_pat) ? A->maxlen_pm_int : A->maxlen_all)
+                          : INT32_MAX;
   if (which == 2) {
     a.soff = A->d_s_off;
     a.slen = A->d_s_len;

@@ -41,6 +41,19 @@ class PartContext:
         _lib.call("pa_ctx_last_kernel_ms", self.h, C.byref(a), C.byref(b))
         return a.value, b.value
 
+    def span_start(self):
+        """pa_ctx_span(0): mark the start of a region on the compute stream"""
+        _lib.call("pa_ctx_span", self.h, 0)
+
+    def span_stop(self):
+        _lib.call("pa_ctx_span", self.h, 1)
+
+    def span_ms(self):
+        """device ms between span_start() and span_stop() (waits for the end)"""
+        v = C.c_float()
+        _lib.call("pa_ctx_span_ms", self.h, C.byref(v))
+        return v.value
+
     def kernel_times(self):
         """dict of mean interior / halo (wait + unpack) / boundary ms and the
         number of mul! calls recorded since set_timing(True); clears the record"""
