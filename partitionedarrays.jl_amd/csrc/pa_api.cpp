@@ -6,6 +6,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -1278,6 +1279,7 @@ int pa_mat_from_csc(pa_ctx* c, int dtype, int index_bytes, int64_t nrows_lids, i
   std::vector<unsigned char> lval(A->n_lnz * S);
   std::vector<int64_t> lpos(csc_nnz, -1);  // CSC nz → position in the long CSR
   A->h_nz_slot.assign(csc_nnz, -1);
+  A->nz_map = true;
   std::vector<int32_t> cur(nr, 0);
   const int R = A->R;
   visit([&](int64_t r, int64_t J, int64_t p, bool) {
@@ -1328,6 +1330,21 @@ int pa_mat_from_csc(pa_ctx* c, int dtype, int index_bytes, int64_t nrows_lids, i
 // sparse(I, J, V, m, n, +) (SparseUtils.jl:80-94) and the SELL build on the
 // device (pa_coo.hip); same layout and nz_slot map as pa_mat_from_csc.
 namespace {
+// PA_TRACE_SETUP=1: phase times of the device matrix build on stderr (each
+// mark synchronises the stream, so the phases are attributed, not overlapped)
+struct SetupTrace {
+  bool on = std::getenv("PA_TRACE_SETUP") != nullptr;
+  hipStream_t st;
+  std::chrono::steady_clock::time_point t;
+  explicit SetupTrace(hipStream_t s) : st(s), t(std::chrono::steady_clock::now()) {}
+  void mark(const char* what) {
+    if (!on) return;
+    (void)hipStreamSynchronize(st);
+    const auto n = std::chrono::steady_clock::now();
+    std::fprintf(stderr, "[pa setup] %-28s %8.2f ms\n", what, std::chrono::duration<double, std::milli>(n - t).count());
+    t = n;
+  }
+};
 struct DevBufs {
   std::vector<void*> p;
   ~DevBufs() { for (void* q : p) dev_free(q); }
@@ -1349,6 +1366,7 @@ int pa_mat_from_coo(pa_ctx* c, int dtype, int index_bytes, int ids_global, int64
   HIPC(hipSetDevice(c->device));
   hipStream_t st = c->s_main;
   const size_t S = dtype_size(dtype);
+  SetupTrace tr(st);
   DevBufs tmp, inp;
   void *dI = nullptr, *dJ = nullptr, *dV = nullptr;
   if (ncoo > 0) {
@@ -1364,10 +1382,12 @@ int pa_mat_from_coo(pa_ctx* c, int dtype, int index_bytes, int ids_global, int64
     if (ids_global) {  // to_lids!(I, rows); to_lids!(J, cols) (Interfaces.jl:2206-2209, 1541-1543)
       const int r1 = gids_to_lids(ncoo, (int64_t*)dI, rows->d_sgid, rows->d_slid, rows->nlids, st);
       const int r2 = r1 ? r1 : gids_to_lids(ncoo, (int64_t*)dJ, cols->d_sgid, cols->d_slid, cols->nlids, st);
+      tr.mark("upload + to_lids!");
       CHECK_ARG(r1 >= 0 && r2 >= 0, "to_lids!: device pass failed");
       CHECK_ARG(r1 == 0 && r2 == 0, "to_lids!: a global id is not a local id of the part (KeyError)");
     }
   }
+  tr.mark("upload / to_lids!");
   int64_t nu = 0;
   int32_t *crow = nullptr, *ccol = nullptr;
   void* cval = nullptr;
@@ -1379,6 +1399,7 @@ int pa_mat_from_coo(pa_ctx* c, int dtype, int index_bytes, int ids_global, int64
   CHECK_ARG(rc == 0, "sparse: COO index out of range (BoundsError)");
   tmp.add(crow); tmp.add(ccol); tmp.add(cval); tmp.add(dcolptr);
   for (void*& q : inp.p) { dev_free(q); q = nullptr; }  // the COO input is no longer needed
+  tr.mark("sparse (sort, combine)");
   *csc_nnz = nu;
   if (colptr_out) {
     HIPC(hipMemcpy(colptr_out, dcolptr, (ncols_lids + 1) * 8, hipMemcpyDeviceToHost));
@@ -1389,6 +1410,7 @@ int pa_mat_from_coo(pa_ctx* c, int dtype, int index_bytes, int ids_global, int64
     HIPC(hipMemcpy(rv.data(), crow, nu * 4, hipMemcpyDeviceToHost));
     for (int64_t p = 0; p < nu; ++p) rowval_out[p] = (int64_t)rv[p] + 1;
   }
+  tr.mark("CSC pattern to host");
   int32_t *rl2o = nullptr, *cl2o = nullptr;
   if (dev_upload(&rl2o, rows->h_lid_to_ohid) || dev_upload(&cl2o, cols->h_lid_to_ohid)) return -1;
   tmp.add(rl2o); tmp.add(cl2o);
@@ -1411,6 +1433,7 @@ int pa_mat_from_coo(pa_ctx* c, int dtype, int index_bytes, int ids_global, int64
     HIPC(e);
   }
   tmp.add(key2); tmp.add(idx2); tmp.add(rowptr); tmp.add(gflag); tmp.add(grank); tmp.add(slen_d); tmp.add(sghost_d);
+  tr.mark("row order");
   A->nnz = nnz;
   const int64_t ns = (A->nrows + A->H - 1) / A->H;
   // row-length histogram → long rows (they leave the SELL, see long_threshold)
@@ -1460,26 +1483,40 @@ int pa_mat_from_coo(pa_ctx* c, int dtype, int index_bytes, int ids_global, int64
     HIPC(hipMalloc(&A->d_val, nvals(A) * S));
     HIPC(hipMemsetAsync(A->d_val, 0, nvals(A) * S, st));
   }
-  if (nu > 0) {
-    HIPC(hipMalloc((void**)&nzs, nu * 8));
-    tmp.add(nzs);
-  }
+  if (nu > 0) HIPC(hipMalloc((void**)&nzs, nu * 8));
+  A->d_nz_slot = nzs;  // downloaded on first use (load_nz_map)
+  A->nz_map = true;
+  tr.mark("slices");
   coo_fill(dtype, nnz, nu, key2, idx2, rowptr, A->d_slice_off, A->H, A->R, ncols_lids, ccol, cval, gflag, grank,
            A->slots, A->d_col, A->d_val, nzs, lidx_d, lptr_d, lcol_d, A->long_off, st);
   HIPC(hipGetLastError());
+  tr.mark("SELL fill");
   if (upload_long(A, lrows, lptr, {})) { pa_mat_destroy(A); return -1; }
   A->d_long_col = lcol_d;
-  A->h_nz_slot.resize(nu);
-  if (nu > 0) {
-    HIPC(hipMemcpyAsync(A->h_nz_slot.data(), nzs, nu * 8, hipMemcpyDeviceToHost, st));
-  }
   HIPC(hipStreamSynchronize(st));
+  tr.mark("long rows");
   if (cols->own_contig && cols->ghost_contig) {
     int kmax = 0;
     for (int32_t l : slen) kmax = std::max(kmax, l);
     if (finalize_pattern(A, kmax, cols->noids)) { pa_mat_destroy(A); return -1; }
   }
+  tr.mark("pattern slices");
   *out = A;
+  return 0;
+}
+
+// the CSC nz → value map on the host (built on the device by pa_mat_from_coo)
+static int load_nz_map(const pa_mat* cA) {
+  CHECK_ARG(cA->nz_map, "matrix was not built from a CSC pattern");
+  pa_mat* A = const_cast<pa_mat*>(cA);
+  if (A->d_nz_slot) {
+    HIPC(hipSetDevice(A->ctx->device));
+    HIPC(hipStreamSynchronize(A->ctx->s_main));
+    A->h_nz_slot.resize(A->csc_nnz);
+    HIPC(hipMemcpy(A->h_nz_slot.data(), A->d_nz_slot, A->csc_nnz * 8, hipMemcpyDeviceToHost));
+    dev_free(A->d_nz_slot);
+    A->d_nz_slot = nullptr;
+  }
   return 0;
 }
 
@@ -1500,7 +1537,7 @@ static int refresh_side(pa_mat* A, hipStream_t st) {
 
 int pa_mat_set_values(pa_mat* A, const void* nzval) {
   CHECK_ARG(A && nzval, "null argument");
-  CHECK_ARG((int64_t)A->h_nz_slot.size() == A->csc_nnz, "matrix was not built from a CSC pattern");
+  if (load_nz_map(A)) return -1;
   HIPC(hipSetDevice(A->ctx->device));
   const size_t S = dtype_size(A->dtype);
   const int64_t nv = nvals(A);
@@ -1516,7 +1553,7 @@ int pa_mat_set_values(pa_mat* A, const void* nzval) {
 
 int pa_mat_get_values(const pa_mat* A, void* nzval) {
   CHECK_ARG(A && nzval, "null argument");
-  CHECK_ARG((int64_t)A->h_nz_slot.size() == A->csc_nnz, "matrix was not built from a CSC pattern");
+  if (load_nz_map(A)) return -1;
   HIPC(hipSetDevice(A->ctx->device));
   const size_t S = dtype_size(A->dtype);
   const int64_t nv = nvals(A);
@@ -1535,7 +1572,7 @@ int pa_mat_xchg_create(pa_mat* A, int32_t n_rcv, const int32_t* parts_rcv, const
                        const int64_t* k_rcv, int32_t n_snd, const int32_t* parts_snd, const int32_t* ptrs_snd,
                        const int64_t* k_snd, pa_xchg** out) {
   CHECK_ARG(A && out, "null argument");
-  CHECK_ARG((int64_t)A->h_nz_slot.size() == A->csc_nnz, "matrix was not built from a CSC pattern");
+  if (load_nz_map(A)) return -1;
   CHECK_ARG(nvals(A) < ((int64_t)1 << 31), "matrix exchanger: value index exceeds int32");
   CHECK_ARG(n_rcv >= 0 && n_snd >= 0, "negative neighbour count");
   auto conv = [&](int32_t n, const int32_t* ptrs, const int64_t* k, std::vector<int32_t>& o) -> int {
@@ -1594,6 +1631,7 @@ int pa_mat_destroy(pa_mat* A) {
   dev_free(A->d_bnd_list);
   dev_free(A->d_col);
   dev_free(A->d_val);
+  dev_free(A->d_nz_slot);
   for (void* p : {(void*)A->d_kind, (void*)A->d_plen, (void*)A->d_pat, (void*)A->d_mask, (void*)A->d_mpat,
                   (void*)A->d_psel, (void*)A->d_mint_list, (void*)A->d_mbnd_list,
                   (void*)A->d_pint_list, (void*)A->d_pbnd_list, (void*)A->d_xint_list,

@@ -362,7 +362,11 @@ struct pa_mat {
   // The ghost rows' nonzeros (stored by FE assembly, never multiplied) sit
   // after the SELL slots in d_val: the nz exchange/assemble (matrix
   // exchanger, Interfaces.jl:2312-2404) addresses both through one index.
+  // Built by pa_mat_from_coo, the map stays on the device (d_nz_slot) until
+  // a call that needs it on the host (set/get values, matrix exchanger).
   std::vector<int64_t> h_nz_slot;
+  int64_t* d_nz_slot = nullptr;
+  bool nz_map = false;              // built from a CSC pattern
   int64_t csc_nnz = 0;
   int64_t n_gnz = 0;
   // long rows (row-length histogram): their own CSR, values in d_val at

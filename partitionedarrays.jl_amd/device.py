@@ -316,28 +316,40 @@ class DeviceMatrix:
 
     @staticmethod
     def from_coo(ctx: PartContext, I, J, V, rows_idx: DeviceIndex, cols_idx: DeviceIndex, nrows_lids, ncols_lids,
-                 ids_global=False):
+                 ids_global=False, pattern=True):
         """sparse(I, J, V, m, n, +) and the SELL build on the device
         (pa_mat_from_coo; ids_global: I, J are gids mapped by to_lids! on the
         device, the indices need their gid tables).  Returns (matrix, colptr,
         rowval): the CSC pattern (1-based lids) for the host setup that needs
-        it (matrix_exchanger)."""
-        I = np.ascontiguousarray(I, dtype=np.int64).ravel()
-        J = np.ascontiguousarray(J, dtype=np.int64).ravel()
+        it (matrix_exchanger); pattern=False returns (matrix, None, None) and
+        downloads nothing.  Local ids cross PCIe as Int32 when they fit."""
         V = np.ascontiguousarray(V).ravel()
+        ib = 4 if not ids_global and max(nrows_lids, ncols_lids) < 2 ** 31 - 1 else 8
+        idt = np.int32 if ib == 4 else np.int64
+        I = np.asarray(I).ravel()
+        J = np.asarray(J).ravel()
+        if ib == 4 and len(I) and I.dtype != np.int32:
+            # out-of-range lids must still raise BoundsError, not wrap around
+            if min(I.min(), J.min()) < 1 or max(I.max(), J.max()) > 2 ** 31 - 1:
+                ib, idt = 8, np.int64
+        I = np.ascontiguousarray(I, dtype=idt)
+        J = np.ascontiguousarray(J, dtype=idt)
         if not (len(I) == len(J) == len(V)):
             raise ValueError("sparse: I, J and V must have the same length")
-        colptr = np.empty(ncols_lids + 1, dtype=np.int64)
-        rowval = np.empty(max(1, len(I)), dtype=np.int64)
+        colptr = np.empty(ncols_lids + 1, dtype=np.int64) if pattern else None
+        rowval = np.empty(max(1, len(I)), dtype=np.int64) if pattern else None
         nnz = C.c_int64(0)
         h = C.c_void_p()
-        _lib.call("pa_mat_from_coo", ctx.h, _lib.DTYPES[V.dtype], 8, 1 if ids_global else 0, nrows_lids, ncols_lids,
+        _lib.call("pa_mat_from_coo", ctx.h, _lib.DTYPES[V.dtype], ib, 1 if ids_global else 0, nrows_lids, ncols_lids,
                   len(I),
                   I.ctypes.data_as(C.c_void_p), J.ctypes.data_as(C.c_void_p), V.ctypes.data_as(C.c_void_p),
-                  rows_idx.h, cols_idx.h, C.byref(nnz), colptr.ctypes.data_as(C.POINTER(C.c_int64)),
-                  rowval.ctypes.data_as(C.POINTER(C.c_int64)), C.byref(h))
+                  rows_idx.h, cols_idx.h, C.byref(nnz),
+                  colptr.ctypes.data_as(C.POINTER(C.c_int64)) if pattern else None,
+                  rowval.ctypes.data_as(C.POINTER(C.c_int64)) if pattern else None, C.byref(h))
         M = DeviceMatrix(h, ctx, V.dtype)
         M.csc_nnz = nnz.value
+        if not pattern:
+            return M, None, None
         return M, colptr, rowval[:nnz.value].copy()
 
     def set_values(self, nzval):

@@ -55,3 +55,18 @@ def counts_to_ptrs(counts):
 def ptrs_to_counts(ptrs):
     """Helpers.jl:143-149"""
     return np.diff(np.asarray(ptrs, dtype=np.int64))
+
+
+def trace_setup():
+    """PA_TRACE_SETUP=1: phase times of the matrix setup on stderr"""
+    import os
+    import sys
+    import time
+    on = bool(os.environ.get("PA_TRACE_SETUP"))
+
+    def mark(what=None, t0=None):
+        t = time.perf_counter()
+        if on and what is not None:
+            print(f"[pa setup] {what:28s} {1e3 * (t - t0):8.2f} ms", file=sys.stderr, flush=True)
+        return t
+    return mark

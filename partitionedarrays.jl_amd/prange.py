@@ -11,7 +11,7 @@ import numpy as np
 
 from .backends import (MAIN, PData, exchange, gather, map_parts, preduce, scatter, unzip,
                        xscan_all)
-from .helpers import Table, counts_to_ptrs
+from .helpers import Table, counts_to_ptrs, trace_setup
 
 
 # ---------------------------------------------------------------------------
@@ -390,6 +390,8 @@ def prange_cartesian(parts: PData, ngids: tuple) -> PRange:
 
 def add_gids_(a: PRange, gids: PData, i_to_part: PData = None, neighbors=None) -> PRange:
     """add_gids!(a::PRange, gids[, i_to_part]) Interfaces.jl:1501-1533"""
+    trace = trace_setup()
+    t0 = trace()
     if i_to_part is not None:
         map_parts(lambda s, g, p: s.add_gids_parts(g, p), a.partition, gids, i_to_part)
     else:
@@ -407,7 +409,9 @@ def add_gids_(a: PRange, gids: PData, i_to_part: PData = None, neighbors=None) -
             map_parts(dev, a.gid_to_part, a.partition, gids)
         else:
             map_parts(lambda f, s, g: s.add_gids_owner(f, g), a.gid_to_part, a.partition, gids)
+    t1 = trace("add_gids! first touch", t0)
     a.exchanger = exchanger_from_ids(a.partition, neighbors)
+    trace("exchanger_from_ids", t1)
     a.ghost = True
     return a
 

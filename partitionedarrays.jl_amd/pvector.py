@@ -17,7 +17,7 @@ from . import _lib
 from .backends import PData, exchange, map_parts, unzip
 from .device import (DeviceMatrix, DeviceMatrixExchanger, DeviceVector, contexts, device_exchanger,
                      device_index, device_index_gids)
-from .helpers import Table, counts_to_ptrs
+from .helpers import Table, counts_to_ptrs, trace_setup
 from .prange import Exchanger, PRange, empty_exchanger, hids_are_equal, oids_are_equal
 
 
@@ -290,13 +290,21 @@ class PSparseMatrix:
         idx = device_index_gids if glob else device_index
         ctxs = contexts(rows.partition)
         mats, pats = [], []
+        # the host needs the CSC pattern only for matrix_exchanger, i.e. when
+        # rows have ghosts (stored ghost rows of FE assembly)
+        want_pattern = bool(rows.ghost)
+        trace = trace_setup()
+        t0 = trace()
         for c, i, j, v, r, s in zip(ctxs, I.parts, J.parts, V.parts, rows.partition.parts, cols.partition.parts):
             M, colptr, rowval = DeviceMatrix.from_coo(c, i, j, v, idx(c, r), idx(c, s), r.num_lids, s.num_lids,
-                                                      ids_global=glob)
+                                                      ids_global=glob, pattern=want_pattern)
             mats.append(M)
-            pats.append(CSC(r.num_lids, s.num_lids, colptr, rowval, np.zeros(0)))
+            pats.append(CSC(r.num_lids, s.num_lids, colptr, rowval, np.zeros(0)) if want_pattern else None)
+        t1 = trace("device sparse + SELL, all parts", t0)
         backend, pids, shape = rows.partition.backend, rows.partition.part_ids, rows.partition.shape
-        ex = matrix_exchanger(PData(backend, pids, pats, shape), rows, cols)
+        ex = (matrix_exchanger(PData(backend, pids, pats, shape), rows, cols) if want_pattern
+              else empty_exchanger(rows.partition))
+        trace("matrix_exchanger", t1)
         return PSparseMatrix(PData(backend, pids, mats, shape), rows, cols, ex)
 
     def info(self):

@@ -31,8 +31,15 @@ def test_library_exports_every_declared_symbol(pamd):
 def test_library_is_gfx950_code_object(pamd):
     # the HIP fat binary embeds the offload target id (amdgcn-amd-amdhsa--gfx950)
     data = open(pamd.LIB_PATH, "rb").read()
-    assert b"gfx950" in data
-    assert subprocess.run(["true"]).returncode == 0
+    assert b"amdgcn-amd-amdhsa--gfx950" in data
+    # and only that target: no code objects for other GPUs
+    targets = set(re.findall(rb"amdgcn-amd-amdhsa--(gfx\w+)", data))
+    assert targets == {b"gfx950"}, targets
+    # the library links RCCL (the MPIBackend-role transport) and exports C symbols
+    out = subprocess.run(["nm", "-D", "--defined-only", pamd.LIB_PATH], capture_output=True, text=True).stdout
+    assert " T pa_spmv_all" in out and " T pa_comm_init_all" in out
+    deps = subprocess.run(["ldd", pamd.LIB_PATH], capture_output=True, text=True).stdout
+    assert "librccl" in deps
 
 
 def test_error_reporting_without_gpu(pamd):
