@@ -142,6 +142,12 @@ int pa_xchg_destroy(pa_xchg* xg);
 int pa_index_set_gids(pa_index* idx, const int64_t* lid_to_gid);
 int pa_add_gids(pa_index* idx, int64_t n, const int64_t* gids, int64_t cap,
                 int64_t* new_gids, int64_t* n_new);
+/* to_lids!(ids, a) (Interfaces.jl:1541-1543, IndexSets.jl gid_to_lid): the
+ * n 1-based gids in ids become 1-based lids, in place, through the device
+ * gid table; a gid that is not a local id fails (KeyError).  Exchanger
+ * (Interfaces.jl:723-786) uses it for lids_snd of the gids its receivers
+ * asked for.                                                              */
+int pa_index_to_lids(pa_index* idx, int64_t n, int64_t* ids);
 
 /* ---- vectors (the values of one part of a PVector) --------------------- */
 int pa_vec_create(pa_ctx* ctx, int dtype, int64_t n, pa_vec** out);

@@ -60,6 +60,7 @@ _SIGS = {
                         _i64p, _i64p, C.POINTER(_p)],
     "pa_index_set_gids": [_p, _i64p],
     "pa_add_gids": [_p, C.c_int64, _i64p, C.c_int64, _i64p, _i64p],
+    "pa_index_to_lids": [_p, C.c_int64, _i64p],
     "pa_mat_set_values": [_p, _p],
     "pa_mat_get_values": [_p, _p],
     "pa_mat_xchg_create": [_p, C.c_int32, _i32p, _i32p, _i64p, C.c_int32, _i32p, _i32p, _i64p, C.POINTER(_p)],

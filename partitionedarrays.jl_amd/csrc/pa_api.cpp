@@ -1034,6 +1034,24 @@ int pa_add_gids(pa_index* I, int64_t n, const int64_t* gids, int64_t cap, int64_
   return 0;
 }
 
+int pa_index_to_lids(pa_index* I, int64_t n, int64_t* ids) {
+  CHECK_ARG(I && (n == 0 || ids), "null argument");
+  CHECK_ARG(I->has_gids, "pa_index_to_lids: call pa_index_set_gids first");
+  pa_ctx* c = I->ctx;
+  HIPC(hipSetDevice(c->device));
+  if (n == 0) return 0;
+  int64_t* d = nullptr;
+  HIPC(hipMalloc((void**)&d, n * 8));
+  hipError_t e = hipMemcpy(d, ids, n * 8, hipMemcpyHostToDevice);
+  const int rc = e == hipSuccess ? gids_to_lids(n, d, I->d_sgid, I->d_slid, I->nlids, c->s_main) : -1;
+  if (rc == 0) e = hipMemcpy(ids, d, n * 8, hipMemcpyDeviceToHost);
+  dev_free(d);
+  HIPC(e);
+  CHECK_ARG(rc >= 0, "pa_index_to_lids: device pass failed");
+  CHECK_ARG(rc == 0, "to_lids!: a global id is not a local id of the part (KeyError)");
+  return 0;
+}
+
 // ---------------------------------------------------------------------------
 int pa_xchg_create(pa_ctx* c, int32_t n_rcv, const int32_t* parts_rcv, const int32_t* ptrs_rcv,
                    const int32_t* lids_rcv, int32_t n_snd, const int32_t* parts_snd,

@@ -212,6 +212,14 @@ def device_first_touch(ctx: PartContext, s, gids):
         raise _lib.PAError(f"pa_add_gids: {L.pa_last_error().decode(errors='replace')}")
 
 
+def device_to_lids(ctx: PartContext, s, gids):
+    """to_lids!(gids, s) through the device gid table (pa_index_to_lids)."""
+    d = device_index_gids(ctx, s)
+    ids = np.array(gids, dtype=np.int64).ravel()
+    _lib.call("pa_index_to_lids", d.h, len(ids), ids.ctypes.data_as(C.POINTER(C.c_int64)))
+    return ids
+
+
 class DeviceExchanger:
     def __init__(self, ctx: PartContext, parts_rcv, lids_rcv, parts_snd, lids_snd):
         pr, prp = _lib.i32(parts_rcv)

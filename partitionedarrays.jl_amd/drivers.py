@@ -21,7 +21,7 @@ from . import _lib
 from .backends import PData, map_parts, unzip
 from .device import DeviceMatrix, contexts
 from .prange import (PRange, add_gids, box_of_part, cartesian_gid_to_part, exchanger_from_ids,
-                     linear_index, prange_cartesian, prange_linear, to_lids_)
+                     grid_neighbors_if_superset, linear_index, prange_cartesian, prange_linear, to_lids_)
 from .pvector import PSparseMatrix, PVector
 
 
@@ -267,7 +267,7 @@ def stencil_partition(parts: PData, N: tuple, kind: int):
         s._append_ghosts(gh, g2p(gh))
         return s
     map_parts(add, cols.partition)
-    cols.exchanger = exchanger_from_ids(cols.partition)
+    cols.exchanger = exchanger_from_ids(cols.partition, grid_neighbors_if_superset(cols.partition, parts.shape))
     cols.ghost = True
     return rows, cols
 

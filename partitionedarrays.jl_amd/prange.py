@@ -9,7 +9,7 @@ from __future__ import annotations
 
 import numpy as np
 
-from .backends import (MAIN, PData, exchange, gather, map_parts, preduce, scatter, unzip,
+from .backends import (MAIN, PData, exchange, gather, map_parts, preduce, reduce_all, scatter, unzip,
                        xscan_all)
 from .helpers import Table, counts_to_ptrs, trace_setup
 
@@ -280,6 +280,33 @@ def discover_parts_snd(parts_rcv: PData, neighbors=None) -> PData:
     return map_parts(lambda d: np.array([x for x in d if x > 0], dtype=np.int32), got)
 
 
+def grid_neighbors(part_shape, part):
+    """The parts of a Cartesian part grid within one step of `part` in every
+    direction (3^d - 1 at most), ascending: the neighbour superset of a
+    one-layer ghost (IndexSets.jl:195-213 geometry)."""
+    cp = [int(c) for c in cartesian_index(part_shape, part)]
+    rng = [range(max(1, c - 1), min(n, c + 1) + 1) for c, n in zip(cp, part_shape)]
+    mesh = np.meshgrid(*[np.array(list(r)) for r in rng], indexing="ij")
+    nb = np.sort(linear_index(part_shape, [m.ravel() for m in mesh]))
+    return nb[nb != part].astype(np.int32)
+
+
+def grid_neighbors_if_superset(ids: PData, part_shape):
+    """Neighbours for discover_parts_snd(parts_rcv, neighbors)
+    (Interfaces.jl:471-496) when every part's ghost owners are grid
+    neighbours: the grid relation is symmetric, so it is then a superset of
+    both the receivers and the senders.  Each part checks its own ghosts; one
+    reduce_all AND decides for all (None: the caller falls back to the
+    gather-based discovery, Interfaces.jl:515-521)."""
+    nbrs = map_parts(lambda s: grid_neighbors(part_shape, s.part), ids)
+
+    def ok(s, nb):
+        ghost = s.lid_to_part[s.lid_to_part != s.part]
+        return bool(np.all(np.isin(ghost, nb)))
+    good = reduce_all(lambda a, b: a and b, map_parts(ok, ids, nbrs), True)
+    return nbrs if all(good.parts) else None
+
+
 def exchanger_from_ids(ids: PData, neighbors=None, reuse_parts_rcv=False) -> Exchanger:
     """Exchanger(ids; reuse_parts_rcv) Interfaces.jl:723-786, vectorised."""
     def rcv(s: IndexSet):
@@ -300,10 +327,17 @@ def exchanger_from_ids(ids: PData, neighbors=None, reuse_parts_rcv=False) -> Exc
     segs = map_parts(lambda t: [t[i] for i in range(1, len(t) + 1)], gids_rcv)
     got = exchange(segs, parts_snd, parts_rcv)
 
+    backend = ids.backend
+    if hasattr(backend, "context"):  # HIP parts: to_lids! through the device gid table
+        from .device import device_to_lids
+        to_lids = lambda s, g: device_to_lids(backend.context(s.part), s, g)
+    else:
+        to_lids = lambda s, g: s.to_lids(g)
+
     def snd(s: IndexSet, g):
         ptrs = counts_to_ptrs([len(x) for x in g])
         data = np.concatenate(g).astype(np.int64) if g else np.zeros(0, np.int64)
-        return Table(s.to_lids(data).astype(np.int32), ptrs)
+        return Table(to_lids(s, data).astype(np.int32), ptrs)
     lids_snd = map_parts(snd, ids, got)
     parts_rcv = map_parts(lambda p: np.asarray(p, np.int32), parts_rcv)
     parts_snd = map_parts(lambda p: np.asarray(p, np.int32), parts_snd)
@@ -323,12 +357,16 @@ def empty_exchanger(a: PData) -> Exchanger:
 class PRange:
     """Partitioned range of global ids (Interfaces.jl:964-987)."""
 
-    def __init__(self, ngids, partition: PData, exchanger: Exchanger, gid_to_part=None, ghost=True):
+    def __init__(self, ngids, partition: PData, exchanger: Exchanger, gid_to_part=None, ghost=True,
+                 part_shape=None):
         self.ngids = int(ngids)
         self.partition = partition
         self.exchanger = exchanger
         self.gid_to_part = gid_to_part
         self.ghost = ghost
+        # Cartesian part grid (prange_cartesian): lets add_gids! discover
+        # parts_snd from grid neighbours instead of a gather on MAIN
+        self.part_shape = part_shape
 
     def __len__(self):
         return self.ngids
@@ -339,7 +377,7 @@ class PRange:
 
     def copy(self):
         part = map_parts(lambda s: s.copy(), self.partition)
-        return PRange(self.ngids, part, self.exchanger, self.gid_to_part, self.ghost)
+        return PRange(self.ngids, part, self.exchanger, self.gid_to_part, self.ghost, self.part_shape)
 
 
 def prange_from_partition(ngids, partition: PData, gid_to_part=None, ghost=True) -> PRange:
@@ -385,7 +423,7 @@ def prange_cartesian(parts: PData, ngids: tuple) -> PRange:
                         np.zeros(0, np.int32), owned_lookup=box_lookup(ngids, lo, n))
     partition = map_parts(mk, parts)
     g2p = map_parts(lambda _: cartesian_gid_to_part(ngids, np_), parts)
-    return PRange(int(np.prod(ngids)), partition, empty_exchanger(partition), g2p, False)
+    return PRange(int(np.prod(ngids)), partition, empty_exchanger(partition), g2p, False, tuple(np_))
 
 
 def add_gids_(a: PRange, gids: PData, i_to_part: PData = None, neighbors=None) -> PRange:
@@ -410,6 +448,8 @@ def add_gids_(a: PRange, gids: PData, i_to_part: PData = None, neighbors=None) -
         else:
             map_parts(lambda f, s, g: s.add_gids_owner(f, g), a.gid_to_part, a.partition, gids)
     t1 = trace("add_gids! first touch", t0)
+    if neighbors is None and a.part_shape is not None:
+        neighbors = grid_neighbors_if_superset(a.partition, a.part_shape)
     a.exchanger = exchanger_from_ids(a.partition, neighbors)
     trace("exchanger_from_ids", t1)
     a.ghost = True

@@ -135,19 +135,25 @@ def test_device_sparse_int32_and_bounds(be, pamd):
     I = rng.integers(1, s.num_lids + 1, 200)
     J = rng.integers(1, s.num_lids + 1, 200)
     V = rng.uniform(-1, 1, 200)
-    M8, cp8, rv8 = pamd.DeviceMatrix.from_coo(ctx, I, J, V, idx, idx, s.num_lids, s.num_lids)
-    I4, J4 = I.astype(np.int32), J.astype(np.int32)
+    # from_coo sends local ids as Int32 (index_bytes 4); the Int64 call must agree
+    M4, cp4, rv4 = pamd.DeviceMatrix.from_coo(ctx, I, J, V, idx, idx, s.num_lids, s.num_lids)
+    I8, J8 = I.astype(np.int64), J.astype(np.int64)
     colptr = np.empty(s.num_lids + 1, np.int64)
     rowval = np.empty(200, np.int64)
     nnz = C.c_int64()
     h = C.c_void_p()
-    L.call("pa_mat_from_coo", ctx.h, L.PA_F64, 4, 0, s.num_lids, s.num_lids, 200, I4.ctypes.data_as(C.c_void_p),
-           J4.ctypes.data_as(C.c_void_p), V.ctypes.data_as(C.c_void_p), idx.h, idx.h, C.byref(nnz),
+    L.call("pa_mat_from_coo", ctx.h, L.PA_F64, 8, 0, s.num_lids, s.num_lids, 200, I8.ctypes.data_as(C.c_void_p),
+           J8.ctypes.data_as(C.c_void_p), V.ctypes.data_as(C.c_void_p), idx.h, idx.h, C.byref(nnz),
            colptr.ctypes.data_as(C.POINTER(C.c_int64)), rowval.ctypes.data_as(C.POINTER(C.c_int64)), C.byref(h))
-    M4 = pamd.DeviceMatrix(h, ctx, np.float64)
-    M4.csc_nnz = nnz.value
-    assert np.array_equal(colptr, cp8) and np.array_equal(rowval[:nnz.value], rv8)
+    M8 = pamd.DeviceMatrix(h, ctx, np.float64)
+    M8.csc_nnz = nnz.value
+    assert np.array_equal(colptr, cp4) and np.array_equal(rowval[:nnz.value], rv4)
     assert np.array_equal(M4.get_values(), M8.get_values())
+    # a lid beyond Int32 in an Int64 array still fails as BoundsError (no wrap-around)
+    Iw = I.copy()
+    Iw[3] = 2 ** 32 + 1
+    with pytest.raises(L.PAError, match="BoundsError"):
+        pamd.DeviceMatrix.from_coo(ctx, Iw, J, V, idx, idx, s.num_lids, s.num_lids)
     Ib = I.copy()
     Ib[7] = s.num_lids + 1
     with pytest.raises(L.PAError, match="BoundsError"):
@@ -187,6 +193,25 @@ def test_device_add_gids_and_to_lids(be, pamd, O, N, nparts):
     A = pamd.PSparseMatrix.from_coo(I, J, V, rows, cols, ids="global")
     for i, p in enumerate(parts.part_ids):
         assert np.array_equal(A.values.local(p).get_values(), OA.values.parts[i].nzval)
+
+
+def test_device_index_to_lids(be, pamd):
+    """pa_index_to_lids (to_lids!, the Exchanger's lids_snd) equals the host
+    IndexSet lookup on owned and ghost gids, and an absent gid is a KeyError."""
+    parts = be.get_part_ids(3)
+    rows, cols, _, _, _ = pamd.drivers.irregular_partition(parts, (9, 8, 7), 27)
+    rng = np.random.default_rng(3)
+    for p in parts.part_ids:
+        s = cols.partition.local(p)
+        g = rng.choice(s.lid_to_gid, size=min(500, s.num_lids))
+        got = pamd.device.device_to_lids(be.context(p), s, g)
+        assert np.array_equal(got, s.to_lids(g))
+        missing = np.setdiff1d(np.arange(1, rows.ngids + 1), s.lid_to_gid)
+        if len(missing):
+            with pytest.raises(pamd.PAError, match="KeyError"):
+                pamd.device.device_to_lids(be.context(p), s, np.append(g, missing[:1]))
+
+
 def test_device_to_lids_unknown_gid(be, pamd):
     parts = be.get_part_ids(1)
     rows = pamd.prange_linear(parts, 10)

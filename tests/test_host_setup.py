@@ -256,3 +256,42 @@ def test_matrix_exchanger_inconsistent_pattern(pamd):
     csc = pamd.PData(parts.backend, parts.part_ids, [c1, c2], parts.shape)
     with pytest.raises(AssertionError):
         pamd.pvector.matrix_exchanger(csc, rows, cols)
+
+
+@pytest.mark.parametrize("shape,N,kind", [((2, 2, 2), (9, 8, 7), 27), ((3, 2, 1), (10, 9, 4), 7),
+                                          ((4, 1, 1), (12, 5, 5), 27)])
+def test_grid_neighbor_discovery(pamd, O, shape, N, kind, monkeypatch):
+    """Cartesian add_gids! discovers parts_snd from the grid neighbours
+    (Interfaces.jl:471-496) — no gather on MAIN — and yields the oracle's
+    Exchanger (gather-based, Interfaces.jl:515-521); a ghost owned by a part
+    outside the grid neighbourhood falls back to the gather."""
+    P = pamd.prange
+    parts = pamd.sequential.get_part_ids(shape)
+    rows = pamd.prange_cartesian(parts, N)
+    _, J, _ = pamd.backends.unzip(pamd.map_parts(
+        lambda s: pamd.drivers.stencil_entries(kind, N, s.lid_to_gid[s.oid_to_lid - 1]), rows.partition), 3)
+    orows = O.prange_cartesian(O.get_part_ids(shape), N)
+    ocols = O.add_gids(orows, O.PData([list(map(int, J.local(p))) for p in parts.part_ids]))
+
+    def no_gather(*a, **k):
+        raise AssertionError("gather-based discover_parts_snd used")
+    monkeypatch.setattr(P, "gather", no_gather)
+    cols = pamd.add_gids(rows, J)
+    oex = ocols.exchanger
+    for p in parts.part_ids:
+        assert list(cols.exchanger.parts_snd.local(p)) == list(oex.parts_snd[p])
+        assert cols.exchanger.lids_snd.local(p).tolist() == oex.lids_snd[p].tolist()
+        assert cols.exchanger.lids_rcv.local(p).tolist() == oex.lids_rcv[p].tolist()
+    # a far ghost (part 1 touches the last gid, owned by the last part)
+    far = pamd.map_parts(lambda s, j: np.append(j, rows.ngids) if s.part == 1 else j, rows.partition, J)
+    nbr_last = pamd.prange.grid_neighbors(shape, parts.num_parts)
+    if 1 in nbr_last:
+        return
+    with pytest.raises(AssertionError, match="gather-based"):
+        pamd.add_gids(rows, far)
+    monkeypatch.undo()
+    cols = pamd.add_gids(rows, far)
+    ocols = O.add_gids(orows, O.PData([list(map(int, far.local(p))) for p in parts.part_ids]))
+    for p in parts.part_ids:
+        assert list(cols.exchanger.parts_snd.local(p)) == list(ocols.exchanger.parts_snd[p])
+        assert cols.exchanger.lids_snd.local(p).tolist() == ocols.exchanger.lids_snd[p].tolist()
