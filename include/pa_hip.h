@@ -101,12 +101,19 @@ int pa_ctx_sync(pa_ctx* ctx);
  * rank = part-1 and nranks = nparts.                                    */
 int pa_comm_unique_id(unsigned char id[128]);
 int pa_comm_init_rank(pa_ctx* ctx, const unsigned char id[128]);
-/* RCCL between the parts of one process, one part per device
- * (ncclCommInitAll over ctx[0..n-1] = parts 1..nparts, in order).  With
- * pa_tune("halo_transport", 1) every halo segment then moves by the same
- * grouped ncclSend/ncclRecv as across processes (MPIBackend.jl:261-309);
+/* RCCL between the parts of one process (ncclCommInitAll over the distinct
+ * devices of ctx[0..n-1] = parts 1..nparts, in order: one rank per device,
+ * in order of first appearance; parts of one device share its rank, and
+ * must share their stream pair, so a segment between them is a send to
+ * self).  With pa_tune("halo_transport", 1) every halo segment then moves by
+ * the same grouped ncclSend/ncclRecv as across processes
+ * (MPIBackend.jl:261-309), posted in (sender part, receiver part) order;
  * with 0 (default) parts of one process read each other's buffers.      */
 int pa_comm_init_all(int n, pa_ctx* const ctx[]);
+/* Halo bytes this part has posted to RCCL sends / receives so far (what the
+ * grouped ncclSend/ncclRecv carried for it; 0 when every segment moved by
+ * device reads).                                                          */
+int pa_comm_stats(pa_ctx* ctx, int64_t* bytes_sent, int64_t* bytes_recv);
 
 /* ---- index sets --------------------------------------------------------
  * Device copy of an AbstractIndexSet's oid_to_lid / hid_to_lid

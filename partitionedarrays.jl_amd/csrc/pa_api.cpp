@@ -393,7 +393,7 @@ struct LocalSet {
 
 // The parts whose halo segments move by device copies / pull reads in this
 // call.  With pa_tune("halo_transport", 1) and an RCCL communicator on every
-// part (pa_comm_init_all: one part per device in this process), none: every
+// part (pa_comm_init_all: one rank per device of this process), none: every
 // segment goes through the grouped ncclSend/ncclRecv, as across processes.
 template <typename H>
 LocalSet local_set(int n, H* const* hs) {
@@ -523,7 +523,13 @@ int transport(int n, pa_xchg* const xg[], int dtype, int dir, int op, pa_vec* co
   if (remote) {
     for (int i = 0; i < n; ++i)
       CHECK_ARG(xg[i]->ctx->comm, "halo neighbour is not held by this process and no RCCL communicator was initialised (pa_comm_init_rank)");
-    NCCLC(ncclGroupStart());
+    // Every (sender part, receiver part) segment through the group.  Sends
+    // to one peer rank are matched with that rank's receives in posting
+    // order, and a rank may hold several parts (pa_comm_init_all: the parts
+    // of a device; a segment between two of them is a send to self), so both
+    // sides post in (sender part, receiver part) order.
+    struct P2P { int src, dst; bool send; char* buf; size_t cnt; int peer; ncclComm_t comm; hipStream_t s; };
+    std::vector<P2P> ops;
     for (int i = 0; i < n; ++i) {
       pa_xchg* X = xg[i];
       pa_ctx* c = X->ctx;
@@ -535,18 +541,34 @@ int transport(int n, pa_xchg* const xg[], int dtype, int dir, int op, pa_vec* co
       const auto& orcv = dir == 0 ? X->ptrs_rcv : X->ptrs_snd;
       char* brcv = (char*)(dir == 0 ? X->d_buf_rcv : X->d_buf_snd);
       for (size_t k = 0; k < psnd.size(); ++k) {
-        if (L.find(psnd[k]) >= 0) continue;
         const size_t cnt = (size_t)(osnd[k + 1] - osnd[k]) * S;
-        if (cnt == 0) continue;  // the peer's matching segment is empty too (SequentialBackend.jl:187)
-        ncclResult_t r = ncclSend(bsnd + osnd[k] * S, cnt, ncclUint8, psnd[k] - 1, comm, SC(c));
-        if (r != ncclSuccess) { ncclGroupEnd(); PA_FAIL(std::string("ncclSend: ") + ncclGetErrorString(r)); }
+        // an empty segment: the peer's matching one is empty too (SequentialBackend.jl:187)
+        if (L.find(psnd[k]) >= 0 || cnt == 0) continue;
+        ops.push_back({c->part, psnd[k], true, bsnd + osnd[k] * S, cnt, c->peer_rank(psnd[k]), comm, SC(c)});
       }
       for (size_t k = 0; k < prcv.size(); ++k) {
-        if (L.find(prcv[k]) >= 0) continue;
         const size_t cnt = (size_t)(orcv[k + 1] - orcv[k]) * S;
-        if (cnt == 0) continue;
-        ncclResult_t r = ncclRecv(brcv + orcv[k] * S, cnt, ncclUint8, prcv[k] - 1, comm, SC(c));
-        if (r != ncclSuccess) { ncclGroupEnd(); PA_FAIL(std::string("ncclRecv: ") + ncclGetErrorString(r)); }
+        if (L.find(prcv[k]) >= 0 || cnt == 0) continue;
+        ops.push_back({prcv[k], c->part, false, brcv + orcv[k] * S, cnt, c->peer_rank(prcv[k]), comm, SC(c)});
+      }
+    }
+    std::stable_sort(ops.begin(), ops.end(), [](const P2P& a, const P2P& b) {
+      return a.src != b.src ? a.src < b.src : a.dst < b.dst;
+    });
+    for (int i = 0; i < n; ++i) {
+      pa_ctx* c = xg[i]->ctx;
+      for (const P2P& o : ops) {
+        if (o.send && o.src == c->part) c->rccl_bytes_sent += (int64_t)o.cnt;
+        if (!o.send && o.dst == c->part) c->rccl_bytes_recv += (int64_t)o.cnt;
+      }
+    }
+    NCCLC(ncclGroupStart());
+    for (const P2P& o : ops) {
+      ncclResult_t r = o.send ? ncclSend(o.buf, o.cnt, ncclUint8, o.peer, o.comm, o.s)
+                              : ncclRecv(o.buf, o.cnt, ncclUint8, o.peer, o.comm, o.s);
+      if (r != ncclSuccess) {
+        ncclGroupEnd();
+        PA_FAIL(std::string(o.send ? "ncclSend: " : "ncclRecv: ") + ncclGetErrorString(r));
       }
     }
     NCCLC(ncclGroupEnd());
@@ -622,6 +644,11 @@ int pre_pack_wait(int n, pa_xchg* const xg[]) {
 }  // namespace
 
 // ===========================================================================
+// the communicator of a part, destroyed with the last part holding it
+static std::shared_ptr<void> own_comm(ncclComm_t comm) {
+  return std::shared_ptr<void>((void*)comm, [](void* p) { (void)ncclCommDestroy((ncclComm_t)p); });
+}
+
 extern "C" {
 
 const char* pa_last_error(void) { return g_err.c_str(); }
@@ -807,7 +834,8 @@ int pa_ctx_destroy(pa_ctx* c) {
   (void)hipSetDevice(c->device);
   (void)hipStreamSynchronize(c->s_main);
   (void)hipStreamSynchronize(c->s_comm);
-  if (c->comm) ncclCommDestroy((ncclComm_t)c->comm);
+  c->comm = nullptr;
+  c->comm_owner.reset();  // ncclCommDestroy with the last part of the communicator
   dev_free(c->d_partials);
   dev_free(c->d_fold);
   dev_free(c->d_result);
@@ -849,31 +877,56 @@ int pa_comm_init_rank(pa_ctx* c, const unsigned char id[128]) {
   HIPC(hipSetDevice(c->device));
   ncclUniqueId u;
   std::memcpy(&u, id, 128);
+  CHECK_ARG(!c->comm, "pa_comm_init_rank: a communicator is already attached");
   ncclComm_t comm;
   NCCLC(ncclCommInitRank(&comm, c->nparts, u, c->part - 1));
   c->comm = comm;
+  c->comm_owner = own_comm(comm);
+  c->rank_of_part = nullptr;  // rank = part - 1
   return 0;
 }
 
-// RCCL for the parts of ONE process, one part per device (ncclCommInitAll):
-// the MPIBackend transport (MPIBackend.jl:261-309) without processes; used
-// for every halo segment with pa_tune("halo_transport", 1).  ctx[i] must be
-// part i+1 of n = nparts, each on its own device (RCCL rejects two ranks on
-// one GPU).
+// RCCL for the parts of ONE process (ncclCommInitAll): one rank per distinct
+// device, in order of first appearance among parts 1..nparts; the parts of a
+// device share its communicator and their stream pair (pa_ctx_create_shared),
+// so a segment between two parts of one device is an RCCL send to self.  The
+// MPIBackend transport (MPIBackend.jl:261-309) without processes; used for
+// every halo segment with pa_tune("halo_transport", 1).
 int pa_comm_init_all(int n, pa_ctx* const ctx[]) {
   CHECK_ARG(n >= 1 && ctx, "null argument");
-  std::vector<int> devs(n);
+  std::vector<int> devs, first;  // rank -> device, rank -> position of its first part
+  auto rank_of = std::make_shared<std::vector<int>>(n);
   for (int i = 0; i < n; ++i) {
     CHECK_ARG(ctx[i], "null ctx");
     CHECK_ARG(ctx[i]->part == i + 1 && ctx[i]->nparts == n, "pa_comm_init_all: pass the contexts of parts 1..nparts in order");
     CHECK_ARG(!ctx[i]->comm, "pa_comm_init_all: a communicator is already attached");
-    devs[i] = ctx[i]->device;
-    for (int j = 0; j < i; ++j)
-      CHECK_ARG(devs[j] != devs[i], "pa_comm_init_all: one part per device (RCCL rejects two ranks on one GPU)");
+    int r = (int)(std::find(devs.begin(), devs.end(), ctx[i]->device) - devs.begin());
+    if (r == (int)devs.size()) {
+      devs.push_back(ctx[i]->device);
+      first.push_back(i);
+    } else {
+      CHECK_ARG(ctx[i]->s_comm == ctx[first[r]]->s_comm,
+                "pa_comm_init_all: parts of one device must share their stream pair (pa_ctx_create_shared)");
+    }
+    (*rank_of)[i] = r;
   }
-  std::vector<ncclComm_t> comms(n);
-  NCCLC(ncclCommInitAll(comms.data(), n, devs.data()));
-  for (int i = 0; i < n; ++i) ctx[i]->comm = comms[i];
+  std::vector<ncclComm_t> comms(devs.size());
+  NCCLC(ncclCommInitAll(comms.data(), (int)devs.size(), devs.data()));
+  std::vector<std::shared_ptr<void>> owners;
+  for (ncclComm_t cm : comms) owners.push_back(own_comm(cm));
+  for (int i = 0; i < n; ++i) {
+    const int r = (*rank_of)[i];
+    ctx[i]->comm = comms[r];
+    ctx[i]->comm_owner = owners[r];
+    ctx[i]->rank_of_part = rank_of;
+  }
+  return 0;
+}
+
+int pa_comm_stats(pa_ctx* c, int64_t* bytes_sent, int64_t* bytes_recv) {
+  CHECK_ARG(c && bytes_sent && bytes_recv, "null argument");
+  *bytes_sent = c->rccl_bytes_sent;
+  *bytes_recv = c->rccl_bytes_recv;
   return 0;
 }
 

@@ -7,6 +7,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <cstdint>
+#include <memory>
 #include <string>
 #include <vector>
 
@@ -251,6 +252,13 @@ struct pa_ctx {
   hipStream_t s_main = nullptr;   // compute stream
   hipStream_t s_comm = nullptr;   // halo transport stream (high priority)
   void* comm = nullptr;           // ncclComm_t (null: no remote transport)
+  // the communicator is destroyed with the last part using it; parts of one
+  // device share their device's rank (pa_comm_init_all), so the peer of a
+  // halo segment from/to part q is rank_of_part[q-1] (null: rank = q-1)
+  std::shared_ptr<void> comm_owner;
+  std::shared_ptr<const std::vector<int>> rank_of_part;
+  int peer_rank(int q) const { return rank_of_part ? (*rank_of_part)[q - 1] : q - 1; }
+  int64_t rccl_bytes_sent = 0, rccl_bytes_recv = 0;  // halo bytes this part posted to RCCL (pa_comm_stats)
   // reduction scratch
   void* d_partials = nullptr;     // per-block partials (max 16 B each)
   void* d_fold = nullptr;         // 256*16 B first-level fold of long partial lists

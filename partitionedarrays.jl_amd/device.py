@@ -32,6 +32,12 @@ class PartContext:
     def sync(self):
         _lib.call("pa_ctx_sync", self.h)
 
+    def comm_stats(self):
+        """(bytes sent, bytes received) this part has posted to RCCL so far"""
+        a, b = C.c_int64(), C.c_int64()
+        _lib.call("pa_comm_stats", self.h, C.byref(a), C.byref(b))
+        return a.value, b.value
+
     def set_timing(self, on: bool):
         _lib.call("pa_ctx_set_timing", self.h, 1 if on else 0)
 
@@ -83,10 +89,11 @@ class HIPBackend(SequentialBackend):
         most 16 cached, least recently used evicted; a structure that cannot
         be captured, e.g. parts on several devices, stays eager).  Off by
         default.
-        rccl: one part per device; the halo moves by RCCL grouped
-        ncclSend/ncclRecv between the parts of this process (pa_comm_init_all
-        + pa_tune("halo_transport", 1)), the MPIBackend transport without
-        processes.  Default: the parts read each other's packed buffers."""
+        rccl: the halo moves by RCCL grouped ncclSend/ncclRecv between the
+        parts of this process (pa_comm_init_all + pa_tune("halo_transport",
+        1)), the MPIBackend transport without processes: one RCCL rank per
+        device, parts of one device send to self.  Default: the parts read
+        each other's packed buffers."""
         ndev = _lib.device_count()
         if ndev == 0:
             raise _lib.PAError("HIPBackend: no HIP device visible")
@@ -110,8 +117,9 @@ class HIPBackend(SequentialBackend):
             self.ctx[p] = PartContext(d, p, n, share_with=share)
             first.setdefault(d, self.ctx[p])
         if self.rccl and n > 1:
-            if len({c.device for c in self.ctx.values()}) != n:
-                raise _lib.PAError("HIPBackend(rccl=True): one part per device (RCCL rejects two ranks on one GPU)")
+            if not self.share_streams and len({c.device for c in self.ctx.values()}) != n:
+                raise _lib.PAError("HIPBackend(rccl=True): parts of one device share one RCCL rank and "
+                                   "must share their stream pair (share_streams=True)")
             _lib.call("pa_comm_init_all", n, _lib.ptr_array([self.ctx[p].h for p in ids.part_ids]))
             _lib.tune("halo_transport", 1)
         return ids
