@@ -2229,7 +2229,9 @@ int gather_results(int n, pa_ctx* const* ctxs, bool cplx, std::vector<c128>* val
   const int P = ctxs[0]->nparts;
   vals->assign(P, c128{0.0, 0.0});
   std::vector<char> have(P, 0);
-  const bool remote_mode = ctxs[0]->comm && n == 1 && P > 1;
+  // one part per process (pa_comm_init_rank): the part values of every rank
+  // come by RCCL all-gather (with one process too: a one-rank gather)
+  const bool remote_mode = ctxs[0]->comm && !ctxs[0]->rank_of_part && n == 1;
   const size_t accsz = cplx ? 16 : 8;
   if (remote_mode) {
     pa_ctx* c = ctxs[0];
@@ -2449,7 +2451,7 @@ int pa_cg_solve_all(int n, pa_mat* const A[], pa_vec* const x[], const pa_vec* c
     CHECK_ARG(A[i]->ctx->nparts == R.P, "cg!: parts of different partitions");
     R.ctxs.push_back(A[i]->ctx);
   }
-  R.remote = R.ctxs[0]->comm && n == 1 && R.P > 1;
+  R.remote = R.ctxs[0]->comm && !R.ctxs[0]->rank_of_part && n == 1;  // one part per process
   CHECK_ARG(R.remote || n == R.P, "cg!: pass every part held by this process, or use one part per process with RCCL");
   std::vector<int> part_pos(R.P + 1, -1);
   for (int i = 0; i < n; ++i) part_pos[R.ctxs[i]->part] = i;

@@ -146,13 +146,14 @@ class HIPDistributedBackend(DistributedBackend):
         n = ids.num_parts
         part = ids.part_ids[0]
         c = PartContext(self.device, part, n)
-        if n > 1:
-            buf = C.create_string_buffer(128)
-            if part == 1:
-                _lib.call("pa_comm_unique_id", buf)
-            obj = [bytes(buf.raw) if part == 1 else None]
-            self.dist.broadcast_object_list(obj, src=0, group=self.group)
-            _lib.call("pa_comm_init_rank", c.h, C.c_char_p(obj[0]))
+        # RCCL for every world size (with one process, its reductions take the
+        # same one-rank all-gather path as with eight)
+        buf = C.create_string_buffer(128)
+        if part == 1:
+            _lib.call("pa_comm_unique_id", buf)
+        obj = [bytes(buf.raw) if part == 1 else None]
+        self.dist.broadcast_object_list(obj, src=0, group=self.group)
+        _lib.call("pa_comm_init_rank", c.h, C.c_char_p(obj[0]))
         self.ctx = {part: c}
         return ids
 

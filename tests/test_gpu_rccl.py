@@ -182,3 +182,36 @@ def test_rccl_needs_shared_streams(pamd):
     b = pamd.HIPBackend(devices=[0], share_streams=False, rccl=True)
     with pytest.raises(pamd.PAError):
         b.get_part_ids((2, 1, 1))
+
+
+def test_one_part_per_process_rccl_reductions(be_pull, pamd):
+    """HIPDistributedBackend (one part per process, pa_comm_init_rank) in a
+    one-process world: dot/norm and the device CG take the RCCL all-gather
+    path of the multi-process mode, and must equal HIPBackend's local fold
+    bit for bit."""
+    import socket
+    import torch.distributed as dist
+    own = not dist.is_initialized()
+    if own:
+        with socket.socket() as s:
+            s.bind(("127.0.0.1", 0))
+            port = s.getsockname()[1]
+        dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
+    try:
+        res = []
+        for b in (pamd.HIPDistributedBackend(device=0), be_pull):
+            parts = b.get_part_ids(1)
+            A, rhs, x0, _ = pamd.drivers.fdm_problem(parts, 14)
+            x = x0.copy()
+            h = []
+            pamd.cg_(x, A, rhs, reltol=0.0, maxiter=10, history=h, fused=True, device=True)
+            h2 = []
+            x2 = x0.copy()
+            pamd.cg_(x2, A, rhs, reltol=0.0, maxiter=6, history=h2, fused=True)
+            res.append((h, h2, pamd.dot(rhs, x), pamd.norm(x), x.to_host().local(1)))
+        (a1, a2, d1, n1, x1), (b1, b2, d2, n2, xx) = res
+        assert a1 == b1 and a2 == b2 and d1 == d2 and n1 == n2
+        assert np.array_equal(x1, xx)
+    finally:
+        if own:
+            dist.destroy_process_group()
