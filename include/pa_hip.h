@@ -41,6 +41,7 @@ typedef struct pa_xchg pa_xchg;
 typedef struct pa_vec pa_vec;
 typedef struct pa_mat pa_mat;
 typedef struct pa_graph pa_graph;
+typedef struct pa_coo pa_coo;
 
 /* ---- errors / library info ------------------------------------------- */
 const char* pa_last_error(void);
@@ -210,6 +211,31 @@ int pa_mat_from_coo(pa_ctx* ctx, int dtype, int index_bytes, int ids_global,
                     const pa_index* rows, const pa_index* cols,
                     int64_t* csc_nnz, int64_t* colptr_out,
                     int64_t* rowval_out, pa_mat** out);
+/* COO triplets of one part on the device: I, J global ids (Int64, 1-based),
+ * V of dtype — the (I, J, V) of PSparseMatrix(I, J, V, rows, cols;
+ * ids=:global), test_fem_sa.jl:60-131.                                  */
+int pa_coo_create(pa_ctx* ctx, int dtype, int64_t n, const int64_t* I,
+                  const int64_t* J, const void* V, pa_coo** out);
+int pa_coo_destroy(pa_coo* coo);
+int pa_coo_size(const pa_coo* coo, int64_t* n);
+int pa_coo_download(const pa_coo* coo, int64_t* I, int64_t* J, void* V);
+/* async_assemble!(I, J, V, rows) + wait (Interfaces.jl:2406-2492) over the
+ * n parts of this process: each triplet whose row (a gid of rows, which
+ * needs pa_index_set_gids) is owned by another part is sent to that owner —
+ * segments in rows.exchanger.parts_rcv order, input order inside — and its
+ * local value becomes zero (the entry stays); every part appends what it
+ * receives in parts_snd order.  I and J stay global.  Parts of this process
+ * exchange by device copies, other processes' parts by RCCL (counts first,
+ * then I, J, V per segment).  A row gid that is not a local id of rows is
+ * a KeyError (to_lids!, Interfaces.jl:2420).                              */
+int pa_coo_assemble_all(int n, pa_coo* const coo[], const pa_index* const rows[],
+                        pa_xchg* const rows_xchg[]);
+/* pa_mat_from_coo over a device COO (index_bytes 8): ids_global = 1 maps
+ * I, J through rows' and cols' gid tables; the COO is left unchanged.    */
+int pa_mat_from_dcoo(const pa_coo* coo, int ids_global, int64_t nrows_lids,
+                     int64_t ncols_lids, const pa_index* rows,
+                     const pa_index* cols, int64_t* csc_nnz,
+                     int64_t* colptr_out, int64_t* rowval_out, pa_mat** out);
 /* Replace the stored values keeping the pattern (same CSC nz order),
  * e.g. after fillstored!/re-assembly (Interfaces.jl:2127-2132).          */
 int pa_mat_set_values(pa_mat* A, const void* nzval);

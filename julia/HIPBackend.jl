@@ -15,9 +15,10 @@
 #     mul! (Interfaces.jl:2246), exchange!/assemble! of vectors (2071-2106)
 #     and matrices (2375-2404), dot/norm/sum (1767, 1973-1992), copyto!/
 #     copy!/fill!/rmul! (1649-1680, 1966), the CG broadcasts (1688-1765) and
-#     IterativeSolvers.cg! (v0.9, test_fdm.jl:115);
-#   * everything else (PRange, Exchanger, add_gids!, COO assembly, gather/
-#     scatter setup collectives) runs unchanged on the host parts.
+#     IterativeSolvers.cg! (v0.9, test_fdm.jl:115), and the COO triplet
+#     exchange assemble!(I, J, V, rows) (2406-2492);
+#   * everything else (PRange, Exchanger, add_gids!, gather/scatter setup
+#     collectives) runs unchanged on the host parts.
 #
 # Not executed in this repository (no Julia on the build image); the Python
 # host package partitionedarrays.jl_amd/ drives the same C-ABI with ctypes and
@@ -206,6 +207,7 @@ const VEC_MIRRORS = Dict{UInt,Tuple{WeakRef,VecMirror}}()  # host part Vector â†
 const MAT_MIRRORS = Dict{UInt,Tuple{WeakRef,MatMirror}}()  # host part SparseMatrixCSC â†’ its pa_mat
 const IDX_CACHE = IdDict{Any,Ptr{Cvoid}}()          # (index set, part, nlids) â†’ pa_index
 const XCHG_CACHE = IdDict{Any,Ptr{Cvoid}}()         # (exchanger, part) â†’ pa_xchg
+const GIDS_SET = Dict{Ptr{Cvoid},Bool}()          # pa_index handles with their gid table attached
 const MXCHG_CACHE = IdDict{Any,Vector{Ptr{Cvoid}}}()  # (matrix exchanger, matrix values) â†’ nz pa_xchg per part
 
 function _mirror(tab, x)
@@ -460,6 +462,53 @@ function async_assemble!(::typeof(+), a::HIPMatrix{T}, t0::AbstractPData=Partiti
 end
 async_assemble!(a::HIPMatrix{T}, t0::AbstractPData=PartitionedArrays._empty_tasks(a.exchanger.parts_rcv)) where {T<:DeviceEltype} =
   async_assemble!(+, a, t0)
+
+# ---- assemble!(I, J, V, rows) (Interfaces.jl:2406-2492) --------------------
+# the triplets go to the device (pa_coo), the ghost rows' triplets move to
+# their owners there (pa_coo_assemble_all: device copies / RCCL), and the
+# assembled lists come back into I, J, V (resize!, as the reference does)
+function _idx_gids_handle(ctx::PartCtx, ids)
+  h = _idx_handle(ctx, ids)
+  get!(GIDS_SET, h) do
+    g = Int64.(collect(ids.lid_to_gid))
+    check(ccall((:pa_index_set_gids, libpa), Cint, (Ptr{Cvoid}, Ptr{Int64}), h, g))
+    true
+  end
+  h
+end
+function async_assemble!(I::HIPData{<:Vector{<:Integer}}, J::HIPData{<:Vector{<:Integer}},
+                         V::HIPData{<:Vector{T}}, rows::PRange,
+                         t0::AbstractPData=PartitionedArrays._empty_tasks(rows.exchanger.parts_rcv)) where {T<:DeviceEltype}
+  _wait_all(t0)
+  n = length(I.parts)
+  coo = Vector{Ptr{Cvoid}}(undef, n)
+  for i in 1:n
+    out = Ref{Ptr{Cvoid}}(C_NULL)
+    gi = Int64.(I.parts[i]); gj = Int64.(J.parts[i])
+    check(ccall((:pa_coo_create, libpa), Cint,
+                (Ptr{Cvoid}, Cint, Int64, Ptr{Int64}, Ptr{Int64}, Ptr{T}, Ref{Ptr{Cvoid}}),
+                I.ctxs[i].h, dtype_code(T), length(gi), gi, gj, V.parts[i], out))
+    coo[i] = out[]
+  end
+  try
+    ri = [_idx_gids_handle(rows.partition.ctxs[i], rows.partition.parts[i]) for i in 1:n]
+    check(ccall((:pa_coo_assemble_all, libpa), Cint,
+                (Cint, Ptr{Ptr{Cvoid}}, Ptr{Ptr{Cvoid}}, Ptr{Ptr{Cvoid}}), n, coo, ri, dev_xchg(rows)))
+    for i in 1:n
+      m = Ref{Int64}(0)
+      check(ccall((:pa_coo_size, libpa), Cint, (Ptr{Cvoid}, Ref{Int64}), coo[i], m))
+      gi = Vector{Int64}(undef, m[]); gj = Vector{Int64}(undef, m[])
+      resize!(V.parts[i], m[])
+      check(ccall((:pa_coo_download, libpa), Cint, (Ptr{Cvoid}, Ptr{Int64}, Ptr{Int64}, Ptr{T}),
+                  coo[i], gi, gj, V.parts[i]))
+      resize!(I.parts[i], m[]); I.parts[i] .= gi
+      resize!(J.parts[i], m[]); J.parts[i] .= gj
+    end
+  finally
+    foreach(h -> ccall((:pa_coo_destroy, libpa), Cint, (Ptr{Cvoid},), h), coo)
+  end
+  _done_tasks(I)
+end
 
 # ---- reductions (Interfaces.jl:221-238, 1767-1772, 1973-1992) -------------
 function LinearAlgebra.dot(a::HIPVector{T}, b::HIPVector{T}) where {T<:DeviceEltype}

@@ -1303,6 +1303,9 @@ def assemble_coo_(I: PData, J: PData, V: PData, rows: PRange):
     to_lids_pr_(I, rows)
     parts = get_part_ids(rows.partition.shape if len(rows.partition.shape) > 1 else num_parts(rows.partition))
 
+    vdt = np.asarray(V.parts[0] if V.parts else []).dtype
+    vdt = vdt if vdt.kind in "fc" else np.dtype(np.float64)
+
     def setup_rcv(part, prcv, s, i, j, v):
         owner_to_i = {o: k for k, o in enumerate(prcv)}
         segs = [[[], [], []] for _ in prcv]
@@ -1314,20 +1317,20 @@ def assemble_coo_(I: PData, J: PData, V: PData, rows: PRange):
                 seg[0].append(s.lid_to_gid[li - 1])
                 seg[1].append(j[k])
                 seg[2].append(v[k])
-                v[k] = v[k] * 0
+                v[k] = vdt.type(0)  # k_v[k] = zero(v) (2446): not v*0, a NaN/Inf does not stay
         return segs
     segs = map_parts(setup_rcv, parts, rows.exchanger.parts_rcv, rows.partition, I, J, V)
     ex = rows.exchanger
     got = []
     for t in range(3):
-        data = map_parts(lambda sg: table_from([x[t] for x in sg], dtype=np.float64 if t == 2 else np.int64), segs)
+        data = map_parts(lambda sg: table_from([x[t] for x in sg], dtype=vdt if t == 2 else np.int64), segs)
         got.append(exchange_tables(data, ex.parts_snd, ex.parts_rcv))
 
     def setup_snd(s, i, j, v, gi, gj, gv):
         to_gids_(i, s)
         i.extend(int(x) for x in gi.data)
         j.extend(int(x) for x in gj.data)
-        return np.concatenate([np.asarray(v, dtype=np.float64), gv.data.astype(np.float64)])
+        return np.concatenate([np.asarray(v, dtype=vdt), gv.data.astype(vdt)])
     V2 = map_parts(setup_snd, rows.partition, I, J, V, *got)
     return I, J, V2
 

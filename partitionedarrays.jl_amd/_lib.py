@@ -57,6 +57,12 @@ _SIGS = {
     "pa_vec_copy": [_p, _p, _p, _p, C.c_int],
     "pa_vec_axpby": [_p, _p, _p, _p, C.c_int, C.c_int],
     "pa_mat_from_csc": [_p, C.c_int, C.c_int, C.c_int64, C.c_int64, _p, _p, _p, _p, _p, C.POINTER(_p)],
+    "pa_coo_create": [_p, C.c_int, C.c_int64, _i64p, _i64p, _p, C.POINTER(_p)],
+    "pa_coo_destroy": [_p],
+    "pa_coo_size": [_p, _i64p],
+    "pa_coo_download": [_p, _i64p, _i64p, _p],
+    "pa_coo_assemble_all": [C.c_int, C.POINTER(_p), C.POINTER(_p), C.POINTER(_p)],
+    "pa_mat_from_dcoo": [_p, C.c_int, C.c_int64, C.c_int64, _p, _p, _i64p, _i64p, _i64p, C.POINTER(_p)],
     "pa_mat_from_coo": [_p, C.c_int, C.c_int, C.c_int, C.c_int64, C.c_int64, C.c_int64, _p, _p, _p, _p, _p, _i64p,
                         _i64p, _i64p, C.POINTER(_p)],
     "pa_index_set_gids": [_p, _i64p],

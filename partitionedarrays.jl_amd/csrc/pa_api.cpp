@@ -11,6 +11,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <memory>
 #include <numeric>
 #include <string>
 #include <vector>
@@ -68,6 +69,10 @@ void launch_spmv_long(const pa_mat* A, const void* x, void* y, const int32_t* ym
                       const void* alpha, const void* beta, void* dotp, int64_t dot_base, hipStream_t st);
 int gid_table(int64_t n, const int64_t* d_lid_to_gid, uint64_t** sgid, int64_t** slid, hipStream_t st);
 int gids_to_lids(int64_t n, int64_t* ids, const uint64_t* sgid, const int64_t* slid, int64_t nl, hipStream_t st);
+int coo_assemble_pack(int dtype, int64_t n, const int64_t* I, const int64_t* J, void* V, const uint64_t* sgid,
+                      const int64_t* slid, int64_t nl, int nseg, const int32_t* d_lids_rcv,
+                      const std::vector<int64_t>& ptrs_rcv, int64_t** sI, int64_t** sJ, void** sV,
+                      std::vector<int64_t>* cnt, hipStream_t st);
 int gids_first_touch(int64_t n, const int64_t* gids, const uint64_t* sgid, const int64_t* slid, int64_t nl,
                      int64_t** out, int64_t* m_out, hipStream_t st);
 void launch_pack(int dtype, int64_t n, const int32_t* lids, const void* v, void* buf,
@@ -485,6 +490,39 @@ int build_pull(int i, int n, pa_xchg* const xg[], const LocalSet& L, int dtype, 
   return 0;
 }
 
+// One RCCL group of point-to-point byte transfers (segment src part → dst
+// part).  Sends to one peer rank are matched with that rank's receives in
+// posting order, and a rank may hold several parts (pa_comm_init_all: the
+// parts of a device; a segment between two of them is a send to self), so
+// every rank posts in (sender part, receiver part) order; transfers of one
+// pair keep the order they were listed in.
+struct P2P {
+  int src, dst;
+  bool send;
+  char* buf;
+  size_t cnt;
+  int peer;
+  ncclComm_t comm;
+  hipStream_t s;
+};
+
+int rccl_group(std::vector<P2P>& ops) {
+  std::stable_sort(ops.begin(), ops.end(), [](const P2P& a, const P2P& b) {
+    return a.src != b.src ? a.src < b.src : a.dst < b.dst;
+  });
+  NCCLC(ncclGroupStart());
+  for (const P2P& o : ops) {
+    ncclResult_t r = o.send ? ncclSend(o.buf, o.cnt, ncclUint8, o.peer, o.comm, o.s)
+                            : ncclRecv(o.buf, o.cnt, ncclUint8, o.peer, o.comm, o.s);
+    if (r != ncclSuccess) {
+      ncclGroupEnd();
+      PA_FAIL(std::string(o.send ? "ncclSend: " : "ncclRecv: ") + ncclGetErrorString(r));
+    }
+  }
+  NCCLC(ncclGroupEnd());
+  return 0;
+}
+
 // Halo transport for n local parts.  dir 0 (forward): send A-layout buffers
 // (ptrs_snd) to parts_snd, receive B-layout (ptrs_rcv) from parts_rcv;
 // dir 1 (reverse): the opposite.  Each part's s_comm first waits for the
@@ -523,12 +561,7 @@ int transport(int n, pa_xchg* const xg[], int dtype, int dir, int op, pa_vec* co
   if (remote) {
     for (int i = 0; i < n; ++i)
       CHECK_ARG(xg[i]->ctx->comm, "halo neighbour is not held by this process and no RCCL communicator was initialised (pa_comm_init_rank)");
-    // Every (sender part, receiver part) segment through the group.  Sends
-    // to one peer rank are matched with that rank's receives in posting
-    // order, and a rank may hold several parts (pa_comm_init_all: the parts
-    // of a device; a segment between two of them is a send to self), so both
-    // sides post in (sender part, receiver part) order.
-    struct P2P { int src, dst; bool send; char* buf; size_t cnt; int peer; ncclComm_t comm; hipStream_t s; };
+    // every (sender part, receiver part) segment through one group
     std::vector<P2P> ops;
     for (int i = 0; i < n; ++i) {
       pa_xchg* X = xg[i];
@@ -552,9 +585,6 @@ int transport(int n, pa_xchg* const xg[], int dtype, int dir, int op, pa_vec* co
         ops.push_back({prcv[k], c->part, false, brcv + orcv[k] * S, cnt, c->peer_rank(prcv[k]), comm, SC(c)});
       }
     }
-    std::stable_sort(ops.begin(), ops.end(), [](const P2P& a, const P2P& b) {
-      return a.src != b.src ? a.src < b.src : a.dst < b.dst;
-    });
     for (int i = 0; i < n; ++i) {
       pa_ctx* c = xg[i]->ctx;
       for (const P2P& o : ops) {
@@ -562,16 +592,7 @@ int transport(int n, pa_xchg* const xg[], int dtype, int dir, int op, pa_vec* co
         if (!o.send && o.dst == c->part) c->rccl_bytes_recv += (int64_t)o.cnt;
       }
     }
-    NCCLC(ncclGroupStart());
-    for (const P2P& o : ops) {
-      ncclResult_t r = o.send ? ncclSend(o.buf, o.cnt, ncclUint8, o.peer, o.comm, o.s)
-                              : ncclRecv(o.buf, o.cnt, ncclUint8, o.peer, o.comm, o.s);
-      if (r != ncclSuccess) {
-        ncclGroupEnd();
-        PA_FAIL(std::string(o.send ? "ncclSend: " : "ncclRecv: ") + ncclGetErrorString(r));
-      }
-    }
-    NCCLC(ncclGroupEnd());
+    if (rccl_group(ops)) return -1;
   }
   for (int i = 0; i < n; ++i) {
     pa_xchg* X = xg[i];
@@ -1423,9 +1444,37 @@ struct DevBufs {
 };
 }  // namespace
 
+namespace {
+// I, J, V: host arrays (kind H2D) or device arrays (D2D, pa_mat_from_dcoo);
+// either way they are copied first (to_lids! works in place).
+int mat_from_coo_impl(pa_ctx* c, int dtype, int index_bytes, int ids_global, int64_t nrows_lids,
+                      int64_t ncols_lids, int64_t ncoo, const void* I, const void* J, const void* V,
+                      hipMemcpyKind kind, const pa_index* rows, const pa_index* cols, int64_t* csc_nnz,
+                      int64_t* colptr_out, int64_t* rowval_out, pa_mat** out);
+}  // namespace
+
 int pa_mat_from_coo(pa_ctx* c, int dtype, int index_bytes, int ids_global, int64_t nrows_lids, int64_t ncols_lids,
                     int64_t ncoo, const void* I, const void* J, const void* V, const pa_index* rows,
                     const pa_index* cols, int64_t* csc_nnz, int64_t* colptr_out, int64_t* rowval_out, pa_mat** out) {
+  return mat_from_coo_impl(c, dtype, index_bytes, ids_global, nrows_lids, ncols_lids, ncoo, I, J, V,
+                           hipMemcpyHostToDevice, rows, cols, csc_nnz, colptr_out, rowval_out, out);
+}
+
+int pa_mat_from_dcoo(const pa_coo* coo, int ids_global, int64_t nrows_lids, int64_t ncols_lids, const pa_index* rows,
+                     const pa_index* cols, int64_t* csc_nnz, int64_t* colptr_out, int64_t* rowval_out, pa_mat** out) {
+  CHECK_ARG(coo, "null argument");
+  CHECK_ARG(rows && rows->ctx == coo->ctx && cols && cols->ctx == coo->ctx, "COO and index sets of different parts");
+  return mat_from_coo_impl(coo->ctx, coo->dtype, 8, ids_global, nrows_lids, ncols_lids, coo->n, coo->d_I, coo->d_J,
+                           coo->d_V, hipMemcpyDeviceToDevice, rows, cols, csc_nnz, colptr_out, rowval_out, out);
+}
+
+}  // extern "C"
+
+namespace {
+int mat_from_coo_impl(pa_ctx* c, int dtype, int index_bytes, int ids_global, int64_t nrows_lids,
+                      int64_t ncols_lids, int64_t ncoo, const void* I, const void* J, const void* V,
+                      hipMemcpyKind kind, const pa_index* rows, const pa_index* cols, int64_t* csc_nnz,
+                      int64_t* colptr_out, int64_t* rowval_out, pa_mat** out) {
   CHECK_ARG(c && out && rows && cols && csc_nnz, "null argument");
   CHECK_ARG(!ids_global || (index_bytes == 8 && rows->has_gids && cols->has_gids),
             "ids=:global needs Int64 ids and pa_index_set_gids on rows and cols");
@@ -1447,9 +1496,9 @@ int pa_mat_from_coo(pa_ctx* c, int dtype, int index_bytes, int ids_global, int64
     inp.add(dJ);
     HIPC(hipMalloc(&dV, ncoo * S));
     inp.add(dV);
-    HIPC(hipMemcpy(dI, I, ncoo * index_bytes, hipMemcpyHostToDevice));
-    HIPC(hipMemcpy(dJ, J, ncoo * index_bytes, hipMemcpyHostToDevice));
-    HIPC(hipMemcpy(dV, V, ncoo * S, hipMemcpyHostToDevice));
+    HIPC(hipMemcpy(dI, I, ncoo * index_bytes, kind));
+    HIPC(hipMemcpy(dJ, J, ncoo * index_bytes, kind));
+    HIPC(hipMemcpy(dV, V, ncoo * S, kind));
     if (ids_global) {  // to_lids!(I, rows); to_lids!(J, cols) (Interfaces.jl:2206-2209, 1541-1543)
       const int r1 = gids_to_lids(ncoo, (int64_t*)dI, rows->d_sgid, rows->d_slid, rows->nlids, st);
       const int r2 = r1 ? r1 : gids_to_lids(ncoo, (int64_t*)dJ, cols->d_sgid, cols->d_slid, cols->nlids, st);
@@ -1573,6 +1622,265 @@ int pa_mat_from_coo(pa_ctx* c, int dtype, int index_bytes, int ids_global, int64
   }
   tr.mark("pattern slices");
   *out = A;
+  return 0;
+}
+}  // namespace
+
+extern "C" {
+
+// ---------------------------------------------------------------------------
+// COO triplets on the device and async_assemble!(I, J, V, rows)
+// (Interfaces.jl:2406-2492)
+
+int pa_coo_create(pa_ctx* c, int dtype, int64_t n, const int64_t* I, const int64_t* J, const void* V, pa_coo** out) {
+  CHECK_ARG(c && out, "null argument");
+  CHECK_ARG(valid_dtype(dtype), "invalid dtype");
+  CHECK_ARG(n >= 0 && (n == 0 || (I && J && V)), "null COO arrays");
+  HIPC(hipSetDevice(c->device));
+  auto C = std::make_unique<pa_coo>();
+  C->ctx = c;
+  C->dtype = dtype;
+  C->n = n;
+  if (n > 0) {
+    const size_t S = dtype_size(dtype);
+    hipError_t e = hipMalloc((void**)&C->d_I, n * 8);
+    if (e == hipSuccess) e = hipMalloc((void**)&C->d_J, n * 8);
+    if (e == hipSuccess) e = hipMalloc(&C->d_V, n * S);
+    if (e == hipSuccess) e = hipMemcpy(C->d_I, I, n * 8, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(C->d_J, J, n * 8, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(C->d_V, V, n * S, hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+      pa_coo_destroy(C.release());
+      HIPC(e);
+    }
+  }
+  *out = C.release();
+  return 0;
+}
+
+int pa_coo_destroy(pa_coo* C) {
+  if (!C) return 0;
+  (void)hipSetDevice(C->ctx->device);
+  (void)hipStreamSynchronize(C->ctx->s_main);
+  dev_free(C->d_I);
+  dev_free(C->d_J);
+  dev_free(C->d_V);
+  delete C;
+  return 0;
+}
+
+int pa_coo_size(const pa_coo* C, int64_t* n) {
+  CHECK_ARG(C && n, "null argument");
+  *n = C->n;
+  return 0;
+}
+
+int pa_coo_download(const pa_coo* C, int64_t* I, int64_t* J, void* V) {
+  CHECK_ARG(C && (C->n == 0 || (I && J && V)), "null argument");
+  if (C->n == 0) return 0;
+  HIPC(hipSetDevice(C->ctx->device));
+  HIPC(hipStreamSynchronize(C->ctx->s_main));
+  HIPC(hipMemcpy(I, C->d_I, C->n * 8, hipMemcpyDeviceToHost));
+  HIPC(hipMemcpy(J, C->d_J, C->n * 8, hipMemcpyDeviceToHost));
+  HIPC(hipMemcpy(V, C->d_V, C->n * dtype_size(C->dtype), hipMemcpyDeviceToHost));
+  return 0;
+}
+
+int pa_coo_assemble_all(int n, pa_coo* const coo[], const pa_index* const rows[], pa_xchg* const xg[]) {
+  CHECK_ARG(n >= 1 && coo && rows && xg, "null argument");
+  const int dt = coo[0]->dtype;
+  const size_t S = dtype_size(dt);
+  for (int i = 0; i < n; ++i) {
+    CHECK_ARG(coo[i] && rows[i] && xg[i], "null handle");
+    CHECK_ARG(coo[i]->dtype == dt, "assemble!: element types differ across parts");
+    CHECK_ARG(coo[i]->ctx == rows[i]->ctx && xg[i]->ctx == rows[i]->ctx, "assemble!: COO, rows and exchanger of different parts");
+    CHECK_ARG(rows[i]->has_gids, "assemble!(I,J,V,rows): rows needs its global ids on the device (pa_index_set_gids)");
+    CHECK_ARG(xg[i]->max_lid < rows[i]->nlids, "assemble!: the exchanger's lids exceed rows' local ids");
+  }
+  // per part: the sent triplets (segments in parts_rcv order), counts and
+  // offsets; the received counts (parts_snd order); the new arrays
+  struct Side {
+    int64_t *sI = nullptr, *sJ = nullptr;
+    void* sV = nullptr;
+    std::vector<int64_t> cnt, off, rcnt, roff;
+    int64_t *nI = nullptr, *nJ = nullptr;
+    void* nV = nullptr;
+    int64_t nn = 0;
+  };
+  std::vector<Side> sd(n);
+  auto free_all = [&]() {
+    for (int i = 0; i < n; ++i) {
+      (void)hipSetDevice(coo[i]->ctx->device);
+      for (void* p : {(void*)sd[i].sI, (void*)sd[i].sJ, sd[i].sV, (void*)sd[i].nI, (void*)sd[i].nJ, sd[i].nV})
+        if (p) (void)hipFree(p);
+      sd[i] = Side{};
+    }
+  };
+  // 1. group the triplets of rows owned elsewhere by owner, zero them locally
+  for (int i = 0; i < n; ++i) {
+    pa_coo* C = coo[i];
+    pa_xchg* X = xg[i];
+    const pa_index* R = rows[i];
+    HIPC(hipSetDevice(C->ctx->device));
+    const int rc = coo_assemble_pack(dt, C->n, C->d_I, C->d_J, C->d_V, R->d_sgid, R->d_slid, R->nlids,
+                                     (int)X->parts_rcv.size(), X->d_lids_rcv, X->ptrs_rcv, &sd[i].sI, &sd[i].sJ,
+                                     &sd[i].sV, &sd[i].cnt, C->ctx->s_main);
+    if (rc) {
+      free_all();
+      if (rc < 0) PA_FAIL("assemble!(I,J,V,rows): device pass failed");
+      PA_FAIL("to_lids!: a row global id is not a local id of rows (KeyError)");
+    }
+    sd[i].off.assign(sd[i].cnt.size() + 1, 0);
+    for (size_t k = 0; k < sd[i].cnt.size(); ++k) sd[i].off[k + 1] = sd[i].off[k] + sd[i].cnt[k];
+  }
+  // 2. the counts each part receives, per entry of its parts_snd
+  LocalSet L = local_set(n, xg);
+  bool remote = false;
+  for (int i = 0; i < n; ++i) {
+    pa_xchg* X = xg[i];
+    sd[i].rcnt.assign(X->parts_snd.size(), 0);
+    for (size_t j = 0; j < X->parts_snd.size(); ++j) {
+      const int jj = L.find(X->parts_snd[j]);
+      if (jj < 0) { remote = true; continue; }
+      const auto& q = xg[jj]->parts_rcv;
+      const auto it = std::find(q.begin(), q.end(), X->ctx->part);
+      if (it == q.end()) { free_all(); PA_FAIL("assemble!: exchanger mismatch (a part in parts_snd does not list this part in parts_rcv)"); }
+      sd[i].rcnt[j] = sd[jj].cnt[it - q.begin()];
+    }
+    for (int32_t q : X->parts_rcv)
+      if (L.find(q) < 0) remote = true;
+  }
+  if (remote) {  // counts of the other processes' parts: one RCCL group of 8 B messages
+    std::vector<int64_t*> dsc(n, nullptr), drc(n, nullptr);
+    auto free_cnt = [&]() {
+      for (int i = 0; i < n; ++i) { (void)hipSetDevice(coo[i]->ctx->device); dev_free(dsc[i]); dev_free(drc[i]); }
+    };
+    std::vector<P2P> ops;
+    for (int i = 0; i < n; ++i) {
+      pa_xchg* X = xg[i];
+      pa_ctx* c = X->ctx;
+      if (!c->comm) { free_cnt(); free_all(); PA_FAIL("assemble!: a neighbour is not held by this process and no RCCL communicator was initialised"); }
+      HIPC(hipSetDevice(c->device));
+      if (dev_upload(&dsc[i], sd[i].cnt)) { free_cnt(); free_all(); return -1; }
+      if (!X->parts_snd.empty()) HIPC(hipMalloc((void**)&drc[i], X->parts_snd.size() * 8));
+      for (size_t k = 0; k < X->parts_rcv.size(); ++k)
+        if (L.find(X->parts_rcv[k]) < 0)
+          ops.push_back({c->part, X->parts_rcv[k], true, (char*)(dsc[i] + k), 8, c->peer_rank(X->parts_rcv[k]),
+                         (ncclComm_t)c->comm, c->s_main});
+      for (size_t j = 0; j < X->parts_snd.size(); ++j)
+        if (L.find(X->parts_snd[j]) < 0)
+          ops.push_back({X->parts_snd[j], c->part, false, (char*)(drc[i] + j), 8, c->peer_rank(X->parts_snd[j]),
+                         (ncclComm_t)c->comm, c->s_main});
+    }
+    if (rccl_group(ops)) { free_cnt(); free_all(); return -1; }
+    for (int i = 0; i < n; ++i) {
+      pa_xchg* X = xg[i];
+      HIPC(hipSetDevice(X->ctx->device));
+      HIPC(hipStreamSynchronize(X->ctx->s_main));
+      std::vector<int64_t> got(X->parts_snd.size());
+      if (!got.empty()) HIPC(hipMemcpy(got.data(), drc[i], got.size() * 8, hipMemcpyDeviceToHost));
+      for (size_t j = 0; j < X->parts_snd.size(); ++j)
+        if (L.find(X->parts_snd[j]) < 0) sd[i].rcnt[j] = got[j];
+    }
+    free_cnt();
+  }
+  // 3. the new lists: the local triplets (sent ones now zero), then the
+  // received segments in parts_snd order (Interfaces.jl:2470-2486)
+  for (int i = 0; i < n; ++i) {
+    pa_coo* C = coo[i];
+    Side& d = sd[i];
+    d.roff.assign(d.rcnt.size() + 1, 0);
+    for (size_t j = 0; j < d.rcnt.size(); ++j) d.roff[j + 1] = d.roff[j] + d.rcnt[j];
+    d.nn = C->n + d.roff.back();
+    HIPC(hipSetDevice(C->ctx->device));
+    if (d.nn > 0) {
+      hipError_t e = hipMalloc((void**)&d.nI, d.nn * 8);
+      if (e == hipSuccess) e = hipMalloc((void**)&d.nJ, d.nn * 8);
+      if (e == hipSuccess) e = hipMalloc(&d.nV, d.nn * S);
+      if (e != hipSuccess) { free_all(); HIPC(e); }
+    }
+    if (C->n > 0) {
+      hipStream_t st = C->ctx->s_main;
+      HIPC(hipMemcpyAsync(d.nI, C->d_I, C->n * 8, hipMemcpyDeviceToDevice, st));
+      HIPC(hipMemcpyAsync(d.nJ, C->d_J, C->n * 8, hipMemcpyDeviceToDevice, st));
+      HIPC(hipMemcpyAsync(d.nV, C->d_V, C->n * S, hipMemcpyDeviceToDevice, st));
+    }
+  }
+  for (int i = 0; i < n; ++i) {  // every pack has finished before any part reads it
+    HIPC(hipSetDevice(coo[i]->ctx->device));
+    HIPC(hipStreamSynchronize(coo[i]->ctx->s_main));
+  }
+  // 4. the segments: device copies between the parts of this process, one
+  // RCCL group (I, J, V per segment) for the others
+  std::vector<P2P> ops;
+  for (int i = 0; i < n; ++i) {
+    pa_xchg* X = xg[i];
+    pa_ctx* c = X->ctx;
+    Side& d = sd[i];
+    HIPC(hipSetDevice(c->device));
+    for (size_t j = 0; j < X->parts_snd.size(); ++j) {
+      const int64_t m = d.rcnt[j];
+      if (m == 0) continue;
+      const int64_t at = coo[i]->n + d.roff[j];
+      const int jj = L.find(X->parts_snd[j]);
+      if (jj < 0) {
+        const int q = X->parts_snd[j], pr = c->peer_rank(q);
+        ncclComm_t cm = (ncclComm_t)c->comm;
+        ops.push_back({q, c->part, false, (char*)(d.nI + at), (size_t)m * 8, pr, cm, c->s_main});
+        ops.push_back({q, c->part, false, (char*)(d.nJ + at), (size_t)m * 8, pr, cm, c->s_main});
+        ops.push_back({q, c->part, false, (char*)d.nV + at * S, (size_t)m * S, pr, cm, c->s_main});
+        continue;
+      }
+      const auto& qr = xg[jj]->parts_rcv;
+      const int64_t k = std::find(qr.begin(), qr.end(), c->part) - qr.begin();
+      const Side& src = sd[jj];
+      const int64_t from = src.off[k];
+      const int sdev = xg[jj]->ctx->device;
+      if (sdev == c->device) {
+        HIPC(hipMemcpyAsync(d.nI + at, src.sI + from, m * 8, hipMemcpyDeviceToDevice, c->s_main));
+        HIPC(hipMemcpyAsync(d.nJ + at, src.sJ + from, m * 8, hipMemcpyDeviceToDevice, c->s_main));
+        HIPC(hipMemcpyAsync((char*)d.nV + at * S, (const char*)src.sV + from * S, m * S, hipMemcpyDeviceToDevice,
+                            c->s_main));
+      } else {
+        HIPC(hipMemcpyPeerAsync(d.nI + at, c->device, src.sI + from, sdev, m * 8, c->s_main));
+        HIPC(hipMemcpyPeerAsync(d.nJ + at, c->device, src.sJ + from, sdev, m * 8, c->s_main));
+        HIPC(hipMemcpyPeerAsync((char*)d.nV + at * S, c->device, (const char*)src.sV + from * S, sdev, m * S,
+                                c->s_main));
+      }
+    }
+    for (size_t k = 0; k < X->parts_rcv.size(); ++k) {
+      const int64_t m = d.cnt[k];
+      const int q = X->parts_rcv[k];
+      if (m == 0 || L.find(q) >= 0) continue;
+      const int pr = c->peer_rank(q);
+      ncclComm_t cm = (ncclComm_t)c->comm;
+      ops.push_back({c->part, q, true, (char*)(d.sI + d.off[k]), (size_t)m * 8, pr, cm, c->s_main});
+      ops.push_back({c->part, q, true, (char*)(d.sJ + d.off[k]), (size_t)m * 8, pr, cm, c->s_main});
+      ops.push_back({c->part, q, true, (char*)d.sV + d.off[k] * S, (size_t)m * S, pr, cm, c->s_main});
+    }
+  }
+  if (!ops.empty() && rccl_group(ops)) { free_all(); return -1; }
+  for (int i = 0; i < n; ++i) {
+    HIPC(hipSetDevice(coo[i]->ctx->device));
+    HIPC(hipStreamSynchronize(coo[i]->ctx->s_main));
+  }
+  // 5. swap in the new lists
+  for (int i = 0; i < n; ++i) {
+    pa_coo* C = coo[i];
+    Side& d = sd[i];
+    HIPC(hipSetDevice(C->ctx->device));
+    dev_free(C->d_I);
+    dev_free(C->d_J);
+    dev_free(C->d_V);
+    C->d_I = d.nI;
+    C->d_J = d.nJ;
+    C->d_V = d.nV;
+    C->n = d.nn;
+    d.nI = nullptr;
+    d.nJ = nullptr;
+    d.nV = nullptr;
+  }
+  free_all();
   return 0;
 }
 

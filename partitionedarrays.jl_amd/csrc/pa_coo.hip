@@ -572,4 +572,140 @@ fail:
   return e == hipSuccess ? 0 : -1;
 }
 
+// ---------------------------------------------------------------------------
+// async_assemble!(I, J, V, rows) (Interfaces.jl:2406-2492) on the device: the
+// triplets whose row is owned by another part are grouped by owner (segments
+// in rows.exchanger.parts_rcv order, input order inside each), copied out
+// and their local value set to zero; the host side (pa_api.cpp) moves the
+// segments to the owners, which append them in parts_snd order.
+
+// seg_of_lid[lids_rcv[t]] = the segment of slot t (every ghost lid is in
+// exactly one receive segment: the one of its owner, Interfaces.jl:740-762)
+__global__ void k_seg_of_lid(int64_t nslots, const int32_t* __restrict__ lids_rcv, const int64_t* __restrict__ ptrs,
+                             int nseg, int32_t* __restrict__ seg_of_lid) {
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < nslots; t += (int64_t)gridDim.x * blockDim.x) {
+    int lo = 0, hi = nseg;  // last segment whose start <= t
+    while (hi - lo > 1) {
+      const int mid = (lo + hi) >> 1;
+      if (ptrs[mid] <= t) lo = mid; else hi = mid;
+    }
+    seg_of_lid[lids_rcv[t]] = lo;
+  }
+}
+
+// key[k] = 0 for a row owned here, 1 + segment of the row's owner otherwise
+// (rows' gid table: an absent gid is the KeyError of to_lids!)
+__global__ void k_coo_seg(int64_t n, const int64_t* __restrict__ I, const uint64_t* __restrict__ sgid,
+                          const int64_t* __restrict__ slid, int64_t nl, const int32_t* __restrict__ seg_of_lid,
+                          uint64_t* __restrict__ key, int64_t* __restrict__ idx, int* __restrict__ bad) {
+  for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < n; k += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t l = gid_lookup(I[k], sgid, slid, nl);
+    if (l < 0) *bad = 1;
+    key[k] = l < 0 ? 0 : (uint64_t)(seg_of_lid[l] + 1);
+    idx[k] = k;
+  }
+}
+
+// first[key] = the first position of each key of the sorted keys
+__global__ void k_key_first(int64_t n, const uint64_t* __restrict__ key, int64_t* __restrict__ first) {
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < n; t += (int64_t)gridDim.x * blockDim.x)
+    if (t == 0 || key[t] != key[t - 1]) first[key[t]] = t;
+}
+
+// the nr sent triplets in segment order: sI/sJ/sV[t] = I/J/V[idx[t]], and
+// the local value becomes zero(v) (the entry stays in the local list)
+template <typename T>
+__global__ void k_coo_pack(int64_t nr, const int64_t* __restrict__ idx, const int64_t* __restrict__ I,
+                           const int64_t* __restrict__ J, T* __restrict__ V, int64_t* __restrict__ sI,
+                           int64_t* __restrict__ sJ, T* __restrict__ sV) {
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < nr; t += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t k = idx[t];
+    sI[t] = I[k];
+    sJ[t] = J[k];
+    sV[t] = V[k];
+    V[k] = zero_of<T>();
+  }
+}
+
+// One part's send side.  Outputs (device, owned by the caller): *sI, *sJ,
+// *sV (the sent triplets, segment after segment) and cnt[0..nseg) on the
+// host.  Returns 1 when a row gid is not a local id of rows (KeyError).
+int coo_assemble_pack(int dtype, int64_t n, const int64_t* I, const int64_t* J, void* V, const uint64_t* sgid,
+                      const int64_t* slid, int64_t nl, int nseg, const int32_t* d_lids_rcv,
+                      const std::vector<int64_t>& ptrs_rcv, int64_t** sI, int64_t** sJ, void** sV,
+                      std::vector<int64_t>* cnt, hipStream_t st) {
+  const size_t S = dtype_size(dtype);
+  *sI = nullptr; *sJ = nullptr; *sV = nullptr;
+  cnt->assign(nseg, 0);
+  if (n <= 0) return 0;
+  hipError_t e = hipSuccess;
+  int32_t* sol = nullptr;
+  int64_t *dptrs = nullptr, *idx = nullptr, *first = nullptr;
+  uint64_t* key = nullptr;
+  int* bad = nullptr;
+  int hbad = 0, rc = 0;
+  std::vector<int64_t> hfirst(nseg + 2, -1);
+  const int64_t nslots = ptrs_rcv.empty() ? 0 : ptrs_rcv.back();
+  int64_t nloc = n;
+  e = hipMalloc((void**)&sol, (nl > 0 ? nl : 1) * 4);
+  if (e == hipSuccess) e = hipMemsetAsync(sol, 0xff, (nl > 0 ? nl : 1) * 4, st);  // -1: owned lid
+  if (e == hipSuccess && nslots > 0) e = hipMalloc((void**)&dptrs, ptrs_rcv.size() * 8);
+  if (e == hipSuccess && nslots > 0)
+    e = hipMemcpyAsync(dptrs, ptrs_rcv.data(), ptrs_rcv.size() * 8, hipMemcpyHostToDevice, st);
+  if (e != hipSuccess) goto done;
+  if (nslots > 0) hipLaunchKernelGGL(k_seg_of_lid, grid1(nslots), dim3(256), 0, st, nslots, d_lids_rcv, dptrs, nseg, sol);
+  e = hipMalloc((void**)&key, n * 8);
+  if (e == hipSuccess) e = hipMalloc((void**)&idx, n * 8);
+  if (e == hipSuccess) e = hipMalloc((void**)&bad, sizeof(int));
+  if (e == hipSuccess) e = hipMemsetAsync(bad, 0, sizeof(int), st);
+  if (e != hipSuccess) goto done;
+  hipLaunchKernelGGL(k_coo_seg, grid1(n), dim3(256), 0, st, n, I, sgid, slid, nl, sol, key, idx, bad);
+  e = hipMemcpyAsync(&hbad, bad, sizeof(int), hipMemcpyDeviceToHost, st);
+  if (e == hipSuccess) e = hipStreamSynchronize(st);
+  if (e != hipSuccess) goto done;
+  if (hbad) { rc = 1; goto done; }
+  e = sort_pairs(key, idx, n, bits_for((uint64_t)nseg + 1), st);  // stable: input order inside a segment
+  if (e == hipSuccess) e = hipMalloc((void**)&first, (nseg + 2) * 8);
+  if (e == hipSuccess) e = hipMemsetAsync(first, 0xff, (nseg + 2) * 8, st);
+  if (e != hipSuccess) goto done;
+  hipLaunchKernelGGL(k_key_first, grid1(n), dim3(256), 0, st, n, key, first);
+  e = hipMemcpyAsync(hfirst.data(), first, (nseg + 1) * 8, hipMemcpyDeviceToHost, st);
+  if (e == hipSuccess) e = hipStreamSynchronize(st);
+  if (e != hipSuccess) goto done;
+  {
+    // end of key q = start of the next present key, or n
+    hfirst[nseg + 1] = n;
+    std::vector<int64_t> start(nseg + 2, n);
+    for (int q = nseg; q >= 0; --q) start[q] = hfirst[q] >= 0 ? hfirst[q] : start[q + 1];
+    nloc = start[1];
+    for (int q = 0; q < nseg; ++q) (*cnt)[q] = start[q + 2] - start[q + 1];
+  }
+  if (n - nloc > 0) {
+    const int64_t nr = n - nloc;
+    e = hipMalloc((void**)sI, nr * 8);
+    if (e == hipSuccess) e = hipMalloc((void**)sJ, nr * 8);
+    if (e == hipSuccess) e = hipMalloc(sV, nr * S);
+    if (e != hipSuccess) goto done;
+#define PA_PK(T) hipLaunchKernelGGL(k_coo_pack<T>, grid1(nr), dim3(256), 0, st, nr, idx + nloc, I, J, (T*)V, *sI, *sJ, (T*)*sV)
+    switch (dtype) {
+      case PA_F32: PA_PK(float); break;
+      case PA_F64: PA_PK(double); break;
+      case PA_C64: PA_PK(c64); break;
+      case PA_C128: PA_PK(c128); break;
+    }
+#undef PA_PK
+    e = hipGetLastError();
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+  }
+done:
+  for (void* p : {(void*)sol, (void*)dptrs, (void*)idx, (void*)first, (void*)key, (void*)bad})
+    if (p) (void)hipFree(p);
+  if (e != hipSuccess || rc) {
+    for (void** p : {(void**)sI, (void**)sJ, sV})
+      if (*p) { (void)hipFree(*p); *p = nullptr; }
+    return e != hipSuccess ? -1 : rc;
+  }
+  return 0;
+}
+
 }  // namespace pa

@@ -335,6 +335,17 @@ constexpr int PA_MP_NP = 4;   // offset patterns per multi-pattern slice
 constexpr int PA_MP_K = 64;   // longest pattern a multi-pattern slice takes
 constexpr size_t kVecPad = 64;  // bytes before and after a vector's values (pa_vec_create)
 
+// COO triplets of one part on the device (global row/column ids, Int64),
+// the input of async_assemble!(I, J, V, rows) and PSparseMatrix(I, J, V, …)
+struct pa_coo {
+  pa_ctx* ctx = nullptr;
+  int dtype = PA_F64;
+  int64_t n = 0;
+  int64_t* d_I = nullptr;
+  int64_t* d_J = nullptr;
+  void* d_V = nullptr;
+};
+
 struct pa_vec {
   pa_ctx* ctx = nullptr;
   int dtype = PA_F64;

@@ -310,6 +310,43 @@ class DeviceVector:
             pass
 
 
+class DeviceCOO:
+    """pa_coo: the COO triplets (I, J global ids, V) of one part in HBM."""
+
+    def __init__(self, ctx: PartContext, I, J, V):
+        V = np.ascontiguousarray(V).ravel()
+        I = np.ascontiguousarray(I, dtype=np.int64).ravel()
+        J = np.ascontiguousarray(J, dtype=np.int64).ravel()
+        if not (len(I) == len(J) == len(V)):
+            raise ValueError("COO: I, J and V must have the same length")
+        self.ctx = ctx
+        self.dtype = V.dtype
+        h = C.c_void_p()
+        _lib.call("pa_coo_create", ctx.h, _lib.DTYPES[V.dtype], len(I), I.ctypes.data_as(C.POINTER(C.c_int64)),
+                  J.ctypes.data_as(C.POINTER(C.c_int64)), V.ctypes.data_as(C.c_void_p), C.byref(h))
+        self.h = h
+
+    def __len__(self):
+        n = C.c_int64()
+        _lib.call("pa_coo_size", self.h, C.byref(n))
+        return n.value
+
+    def download(self):
+        n = len(self)
+        I, J = np.empty(n, np.int64), np.empty(n, np.int64)
+        V = np.empty(n, self.dtype)
+        _lib.call("pa_coo_download", self.h, I.ctypes.data_as(C.POINTER(C.c_int64)),
+                  J.ctypes.data_as(C.POINTER(C.c_int64)), V.ctypes.data_as(C.c_void_p))
+        return I, J, V
+
+    def __del__(self):
+        try:
+            if getattr(self, "h", None) and _lib._lib is not None and not sys.is_finalizing():
+                _lib._lib.pa_coo_destroy(self.h)
+        except Exception:
+            pass
+
+
 class DeviceMatrix:
     """pa_mat: one part of a PSparseMatrix in the owned-row SELL layout."""
 
@@ -364,6 +401,24 @@ class DeviceMatrix:
                   colptr.ctypes.data_as(C.POINTER(C.c_int64)) if pattern else None,
                   rowval.ctypes.data_as(C.POINTER(C.c_int64)) if pattern else None, C.byref(h))
         M = DeviceMatrix(h, ctx, V.dtype)
+        M.csc_nnz = nnz.value
+        if not pattern:
+            return M, None, None
+        return M, colptr, rowval[:nnz.value].copy()
+
+    @staticmethod
+    def from_dcoo(coo: DeviceCOO, rows_idx: DeviceIndex, cols_idx: DeviceIndex, nrows_lids, ncols_lids,
+                  ids_global=True, pattern=True):
+        """DeviceMatrix.from_coo over device triplets (pa_mat_from_dcoo)."""
+        n = len(coo)
+        colptr = np.empty(ncols_lids + 1, dtype=np.int64) if pattern else None
+        rowval = np.empty(max(1, n), dtype=np.int64) if pattern else None
+        nnz = C.c_int64(0)
+        h = C.c_void_p()
+        _lib.call("pa_mat_from_dcoo", coo.h, 1 if ids_global else 0, nrows_lids, ncols_lids, rows_idx.h, cols_idx.h,
+                  C.byref(nnz), colptr.ctypes.data_as(C.POINTER(C.c_int64)) if pattern else None,
+                  rowval.ctypes.data_as(C.POINTER(C.c_int64)) if pattern else None, C.byref(h))
+        M = DeviceMatrix(h, coo.ctx, coo.dtype)
         M.csc_nnz = nnz.value
         if not pattern:
             return M, None, None

@@ -97,13 +97,13 @@ def fdm_host(parts: PData, nx=10):
 # ---------------------------------------------------------------------------
 # test_fem_sa.jl
 
-def fem_sa_host(parts: PData, nx=10):
-    """Host setup of test_fem_sa.jl:7-132 (2D Q1 FE, u = 1): cells, COO of
-    the owned cells, add_gids!(rows, I), async_assemble!(I, J, V, rows), the
-    rhs b filled through global ids (ghost rows included, before assemble!),
-    add_gids!(cols, J).  Returns rows, cols, I, J, V (global ids), b (host,
-    not yet assembled), x0 and x̂ (host, on cols)."""
-    from .prange import add_gids_, assemble_coo_, prange_cartesian, prange_linear
+def fem_sa_cells(parts: PData, nx=10):
+    """test_fem_sa.jl:7-103 (2D Q1 FE, u = 1) up to the COO assembly: cells,
+    COO of the owned cells (I, J global ids), add_gids!(rows, I), the rhs b
+    filled through global ids (ghost rows included, before assemble!).
+    Returns rows, cols (no ghosts yet), I, J, V, b (host, not yet assembled)
+    and init(cols) → (x0, x̂) host values."""
+    from .prange import add_gids_, prange_cartesian, prange_linear
     lx = 2.0
     ns = (nx, nx)
     h = lx / nx
@@ -140,7 +140,6 @@ def fem_sa_host(parts: PData, nx=10):
     mk = (lambda: prange_cartesian(parts, nsn)) if cart else (lambda: prange_linear(parts, nsn[0] * nsn[1]))
     rows, cols = mk(), mk()
     add_gids_(rows, I)
-    I, J, V = assemble_coo_(I, J, V, rows)
 
     def fill_b(s, sc):
         bv = np.zeros(s.num_lids)
@@ -150,24 +149,45 @@ def fem_sa_host(parts: PData, nx=10):
                     bv[s.to_lids([node_gid(*nr)])[0] - 1] += 1.0  # u(x) = 1
         return bv
     bh = map_parts(fill_b, rows.partition, cells.partition)
-    add_gids_(cols, J)
 
-    def init(s):
-        g = s.lid_to_gid - 1
-        bnd = (g % nsn[0] == 0) | (g % nsn[0] == nx) | (g // nsn[0] == 0) | (g // nsn[0] == nx)
-        own = s.lid_to_part == s.part
-        return np.where(own & bnd, 1.0, 0.0), np.where(own, 1.0, 0.0)
-    x0h, xh = unzip(map_parts(init, cols.partition), 2)
+    def init(cols):
+        def f(s):
+            g = s.lid_to_gid - 1
+            bnd = (g % nsn[0] == 0) | (g % nsn[0] == nx) | (g // nsn[0] == 0) | (g // nsn[0] == nx)
+            own = s.lid_to_part == s.part
+            return np.where(own & bnd, 1.0, 0.0), np.where(own, 1.0, 0.0)
+        return unzip(map_parts(f, cols.partition), 2)
+    return rows, cols, I, J, V, bh, init
+
+
+def fem_sa_host(parts: PData, nx=10):
+    """fem_sa_cells + async_assemble!(I, J, V, rows) restated on the host
+    (prange.assemble_coo_; CPU setup tests only — the product path,
+    fem_sa_problem, assembles on the device) + add_gids!(cols, J).  Returns
+    rows, cols, I, J, V (global ids), b (host, not yet assembled), x0, x̂."""
+    from .prange import add_gids_, assemble_coo_
+    rows, cols, I, J, V, bh, init = fem_sa_cells(parts, nx)
+    I, J, V = assemble_coo_(I, J, V, rows)
+    add_gids_(cols, J)
+    x0h, xh = init(cols)
     return rows, cols, I, J, V, bh, x0h, xh
 
 
 def fem_sa_problem(parts: PData, nx=10):
-    """test_fem_sa.jl on HIP parts: the PSparseMatrix from the assembled COO
-    (ids=:global) and b assembled on the device (assemble!, Interfaces.jl:2101)."""
-    rows, cols, I, J, V, bh, x0h, xh = fem_sa_host(parts, nx)
-    A = PSparseMatrix.from_coo(I, J, V, rows, cols, ids="global")
+    """test_fem_sa.jl on HIP parts: the COO triplets go to the device,
+    assemble!(I, J, V, rows) moves the ghost rows' triplets to their owners
+    there (pa_coo_assemble_all), add_gids!(cols, J), then the PSparseMatrix
+    from the device COO (ids=:global) and b assembled on the device
+    (assemble!, Interfaces.jl:2101)."""
+    from .prange import add_gids_
+    from .pvector import COO, assemble_
+    rows, cols, I, J, V, bh, init = fem_sa_cells(parts, nx)
+    coo = COO.from_host(I, J, V, rows)
+    assemble_(coo, rows)
+    add_gids_(cols, coo.global_cols())
+    x0h, xh = init(cols)
+    A = PSparseMatrix.from_coo(coo, None, None, rows, cols, ids="global")
     b = PVector.from_host(bh, rows)
-    from .pvector import assemble_
     assemble_(b)
     return A, b, PVector.from_host(x0h, cols), PVector.from_host(xh, cols)
 

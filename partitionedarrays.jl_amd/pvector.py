@@ -15,7 +15,7 @@ import numpy as np
 
 from . import _lib
 from .backends import PData, exchange, map_parts, unzip
-from .device import (DeviceMatrix, DeviceMatrixExchanger, DeviceVector, contexts, device_exchanger,
+from .device import (DeviceCOO, DeviceMatrix, DeviceMatrixExchanger, DeviceVector, contexts, device_exchanger,
                      device_index, device_index_gids)
 from .helpers import Table, counts_to_ptrs, trace_setup
 from .prange import Exchanger, PRange, empty_exchanger, hids_are_equal, oids_are_equal
@@ -200,11 +200,53 @@ def exchange_(v):
     return v
 
 
-def assemble_(v):
+class COO:
+    """The (I, J, V) triplets of a PSparseMatrix before `sparse`, on the
+    device: one pa_coo per part, I and J global ids (test_fem_sa.jl:60-131,
+    ids=:global)."""
+
+    def __init__(self, values: PData):
+        self.values = values
+
+    @staticmethod
+    def from_host(I: PData, J: PData, V: PData, rows: PRange) -> "COO":
+        ctxs = contexts(rows.partition)
+        parts = [DeviceCOO(c, i, j, v) for c, i, j, v in zip(ctxs, I.parts, J.parts, V.parts)]
+        p = rows.partition
+        return COO(PData(p.backend, p.part_ids, parts, p.shape))
+
+    def to_host(self):
+        """(I, J, V) as PData of host arrays"""
+        return unzip(map_parts(lambda c: c.download(), self.values), 3)
+
+    def global_cols(self) -> PData:
+        """J of every part (host), e.g. for add_gids!(cols, J)"""
+        return map_parts(lambda c: c.download()[1], self.values)
+
+
+def _assemble_coo(coo: COO, rows: PRange) -> COO:
+    """async_assemble!(I, J, V, rows) + wait (Interfaces.jl:2406-2492) on the
+    device (pa_coo_assemble_all): triplets of rows owned elsewhere go to the
+    owner (local value set to zero, entry kept), received ones are appended
+    in rows.exchanger.parts_snd order."""
+    ctxs = contexts(rows.partition)
+    pids = rows.partition.part_ids
+    idx = [device_index_gids(c, rows.partition.local(p)) for c, p in zip(ctxs, pids)]
+    xg = [device_exchanger(c, rows.exchanger, p) for c, p in zip(ctxs, pids)]
+    _lib.call("pa_coo_assemble_all", len(ctxs), _hs(coo.values.parts), _hs(idx), _hs(xg))
+    return coo
+
+
+def assemble_(v, rows: PRange = None):
     """assemble!(v) (Interfaces.jl:2084-2106): ghost values added to their
     owners (reverse exchanger, `+`), then ghost values set to zero.  For a
     PSparseMatrix: assemble!(A) (2383-2404), the ghost rows' nonzeros added
-    to the owners' and then zeroed."""
+    to the owners' and then zeroed.  For a COO and its rows:
+    assemble!(I, J, V, rows) (2406-2492) on the device."""
+    if isinstance(v, COO):
+        if rows is None:
+            raise TypeError("assemble!(I, J, V, rows): the rows PRange is required")
+        return _assemble_coo(v, rows)
     if isinstance(v, PSparseMatrix):
         return _mat_exchange(v, _lib.PA_ADD, 1, 1)
     ctxs = contexts(v.values)
@@ -281,14 +323,19 @@ class PSparseMatrix:
                                    rows.partition.shape), rows, cols, ex)
 
     @staticmethod
-    def from_coo(I: PData, J: PData, V: PData, rows: PRange, cols: PRange, ids="local"):
-        """PSparseMatrix(I, J, V, rows, cols; ids) (Interfaces.jl:2194-2215, sparse init)"""
+    def from_coo(I, J, V, rows: PRange, cols: PRange, ids="local"):
+        """PSparseMatrix(I, J, V, rows, cols; ids) (Interfaces.jl:2194-2215,
+        sparse init).  I, J, V: PData of host arrays, or I a device COO (then
+        J and V are None)."""
         # to_lids! (ids=:global) and sparse(I, J, V) on the device
         # (pa_mat_from_coo); the host keeps the CSC pattern only, for
         # matrix_exchanger
         glob = ids == "global"
         idx = device_index_gids if glob else device_index
         ctxs = contexts(rows.partition)
+        dev = isinstance(I, COO)  # device triplets: from_coo(coo, None, None, rows, cols; ids)
+        if dev:
+            I, J, V = I.values, I.values, I.values
         mats, pats = [], []
         # the host needs the CSC pattern only for matrix_exchanger, i.e. when
         # rows have ghosts (stored ghost rows of FE assembly)
@@ -296,8 +343,12 @@ class PSparseMatrix:
         trace = trace_setup()
         t0 = trace()
         for c, i, j, v, r, s in zip(ctxs, I.parts, J.parts, V.parts, rows.partition.parts, cols.partition.parts):
-            M, colptr, rowval = DeviceMatrix.from_coo(c, i, j, v, idx(c, r), idx(c, s), r.num_lids, s.num_lids,
-                                                      ids_global=glob, pattern=want_pattern)
+            if dev:
+                M, colptr, rowval = DeviceMatrix.from_dcoo(i, idx(c, r), idx(c, s), r.num_lids, s.num_lids,
+                                                           ids_global=glob, pattern=want_pattern)
+            else:
+                M, colptr, rowval = DeviceMatrix.from_coo(c, i, j, v, idx(c, r), idx(c, s), r.num_lids,
+                                                          s.num_lids, ids_global=glob, pattern=want_pattern)
             mats.append(M)
             pats.append(CSC(r.num_lids, s.num_lids, colptr, rowval, np.zeros(0)) if want_pattern else None)
         t1 = trace("device sparse + SELL, all parts", t0)

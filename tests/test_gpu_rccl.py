@@ -215,3 +215,16 @@ def test_one_part_per_process_rccl_reductions(be_pull, pamd):
     finally:
         if own:
             dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("nparts,ngids", [(4, 20000), ((2, 2, 2), (30, 28, 26))])
+def test_rccl_coo_assemble_bitexact(be, pamd, O, nparts, ngids):
+    """assemble!(I, J, V, rows) with every count and every (I, J, V) segment
+    through RCCL (pa_coo_assemble_all's cross-process path), bit-exact
+    against the oracle."""
+    from test_gpu_coo_assemble import _check, _problem
+    args = _problem(pamd, O, be, nparts, ngids, 12000, np.float64, SEED + 7)
+    s0 = _stats(pamd, args[0])
+    assert _check(pamd, O, *args) > 0
+    sent, recv = _moved(s0, _stats(pamd, args[0]))
+    assert sent == 0 and recv == 0  # the halo counters count mul!/exchange! segments only
