@@ -176,7 +176,15 @@ int pa_vec_copy(pa_vec* dst, const pa_index* idx_dst,
  *   mode 3: y[i] = y[i] - x[i]       (r .-= c)
  *   mode 4: y[i] = a*y[i]            (rmul!, Interfaces.jl:1675)
  * over all lids when all_lids != 0 (same partition: ghosts too), else over
- * the owned values through idx (which must describe both vectors).       */
+ * the owned values through idx (which must describe both vectors).
+ * The scalar a is of the element type, or — mode | PA_BCAST_F64 — a
+ * Float64 (double), or — mode | PA_BCAST_C128 — a ComplexF64 (complex
+ * vectors only): then each element is evaluated in Float64 / ComplexF64
+ * (Real * Complex componentwise) and rounded to the element type once,
+ * Julia's promotion for e.g. IterativeSolvers' Float64 α, β with Float32
+ * vectors.                                                                */
+#define PA_BCAST_F64 8
+#define PA_BCAST_C128 16
 int pa_vec_axpby(pa_vec* y, const pa_vec* x, const pa_index* idx,
                  const void* a, int mode, int all_lids);
 
@@ -317,7 +325,13 @@ int pa_graph_destroy(pa_graph* g);
  * pa_spmv_dot_all = mul!(c, A, u) followed by dot(u, c), the dot being
  * accumulated by the SpMV kernel over the owned rows it writes (u = x must
  * have contiguous owned lids); pa_cg_update_all = x .+= α.*u; r .-= α.*c
- * (all lids; the four vectors share one partition) and returns norm(r). */
+ * (all lids; the four vectors share one partition) and returns norm(r).
+ * alpha is a Float64 (double) for real vectors, a ComplexF64 for complex
+ * ones — IterativeSolvers' α = residual²/dot with a Float64 residual — and
+ * each element is evaluated in that type and rounded once (PA_BCAST_*).
+ * Reductions (dot, sum, norm) round each part's value to the element type
+ * and add the parts in that type, as Julia's reduce over the parts' T
+ * values does; norm's ^(1/2) is Float64.                                  */
 int pa_spmv_dot_all(int n, pa_mat* const A[], pa_vec* const y[],
                     const pa_index* const y_idx[],
                     pa_vec* const x[], const pa_index* const x_idx[],

@@ -928,7 +928,18 @@ def dot(a: PVector, b: PVector):
             return complex(re, im)
         return float(np.sum(xo.astype(np.float64) * yo.astype(np.float64)))
     c = map_parts(local, a.values, b.values, a.rows.partition, b.rows.partition)
+    if _is_single(a):  # the local dot returns T; sum(c) adds the T values in T
+        if isinstance(c.parts[0], complex):
+            re = _julia_reduce(lambda x, y: x + y, [np.float32(v.real) for v in c.parts], np.float32(0))
+            im = _julia_reduce(lambda x, y: x + y, [np.float32(v.imag) for v in c.parts], np.float32(0))
+            return complex(float(re), float(im))
+        return _julia_reduce(lambda x, y: x + y, [np.float32(v) for v in c.parts], np.float32(0))
     return _julia_reduce(lambda x, y: x + y, c.parts, 0.0)
+
+
+def _is_single(a: PVector):
+    v = a.values.parts[0]
+    return (v.re.dtype if isinstance(v, Cx) else np.asarray(v).dtype) == np.float32
 
 
 def norm(a: PVector, p=2):
@@ -939,6 +950,9 @@ def norm(a: PVector, p=2):
             return float(np.sum(xo.re.astype(np.float64) ** 2 + xo.im.astype(np.float64) ** 2))
         return float(np.sum(xo.astype(np.float64) ** 2))
     c = map_parts(local, a.values, a.rows.partition)
+    if _is_single(a):  # norm(v)^p is a Float32, reduced in Float32, then ^(1/p) in Float64
+        s = _julia_reduce(lambda x, y: x + y, [np.float32(v) for v in c.parts], np.float32(0))
+        return float(s) ** (1.0 / p)
     return _julia_reduce(lambda x, y: x + y, c.parts, 0.0) ** (1.0 / p)
 
 
@@ -1216,8 +1230,8 @@ def cg_(x: PVector, A: PSparseMatrix, b: PVector, reltol=None, abstol=0.0, maxit
     loop: β = res²/prev²; u .= r .+ β.*u; mul!(c,A,u); α = res²/dot(u,c);
     x .+= α.*u; r .-= α.*c; prev = res; res = norm(r)."""
     dt = x.values.parts[0].dtype
-    if reltol is None:
-        reltol = math.sqrt(np.finfo(dt).eps)
+    if reltol is None:  # sqrt(eps(T)) in T
+        reltol = float(np.sqrt(np.finfo(dt).eps))
     if maxiter is None:
         maxiter = A.cols.ngids
     mk = lambda: PVector(map_parts(lambda v: np.zeros_like(v), x.values), x.rows)
@@ -1231,10 +1245,13 @@ def cg_(x: PVector, A: PSparseMatrix, b: PVector, reltol=None, abstol=0.0, maxit
     it = 0
     hist = []
     while not (it >= maxiter or residual <= tol):
-        beta = residual ** 2 / prev ** 2
+        # residual is a Float64 (norm of a PVector), so are β and α; the
+        # broadcasts evaluate in Float64 and round to T (np.float64 scalars
+        # are strong under NumPy's promotion)
+        beta = np.float64(residual * residual / (prev * prev))
         bcast_(u, r, beta, 0)
         mul_(c, A, u)
-        alpha = residual ** 2 / dot(u, c)
+        alpha = np.float64(residual * residual / float(dot(u, c)))
         bcast_(x, u, alpha, 1)
         bcast_(r, c, alpha, 2)
         prev = residual

@@ -17,6 +17,7 @@ LIB_PATH = os.environ.get("PA_HIP_LIB") or os.path.join(_HERE, "libpa_hip.so")
 
 PA_F32, PA_F64, PA_C64, PA_C128 = 0, 1, 2, 3
 PA_REPLACE, PA_ADD = 0, 1
+PA_BCAST_F64, PA_BCAST_C128 = 8, 16  # pa_vec_axpby scalar kinds (Float64 / ComplexF64 scalars)
 
 DTYPES = {
     np.dtype(np.float32): PA_F32,

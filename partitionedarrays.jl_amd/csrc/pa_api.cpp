@@ -35,13 +35,13 @@ void launch_side_fill(pa_mat* A, const int32_t* rows, const int32_t* len, hipStr
 void launch_fold(int cplx, int nb, const void* in, void* scratch, void* out, unsigned* ticket, hipStream_t st);
 void launch_fold_cg_alpha(int dtype, int nb, const void* in, void* scratch, void* out, unsigned* ticket,
                           CGState* cst, hipStream_t st);
-void launch_fold_cg_step(int nb, const void* in, void* scratch, void* out, unsigned* ticket, CGState* cst,
-                         double* history, hipStream_t st);
+void launch_fold_cg_step(int dtype, int nb, const void* in, void* scratch, void* out, unsigned* ticket,
+                         CGState* cst, double* history, hipStream_t st);
 void launch_cg_xr(int dtype, int64_t n, int64_t noids, const int32_t* own, void* x, void* r, const void* u,
                   const void* c, const void* alpha, const CGState* cst, double* part, int nb, hipStream_t st);
 void launch_cg_xu(int dtype, int64_t n, void* x, void* u, const void* r, const CGState* cst, hipStream_t st);
 void launch_cg_alpha(int dtype, int P, const void* gathered, CGState* cst, hipStream_t st);
-void launch_cg_step(int P, const double* gathered, CGState* cst, double* history, hipStream_t st);
+void launch_cg_step(int dtype, int P, const double* gathered, CGState* cst, double* history, hipStream_t st);
 void launch_gather_ptrs(int P, const void* const* srcs, int accsz, void* out, hipStream_t st);
 extern int g_spmv_format;
 extern int g_spmv_pattern_rule;
@@ -90,7 +90,7 @@ void launch_pull_group(int dtype, const PullGroup& g, hipStream_t st);
 void launch_copy(int dtype, int64_t n, const int32_t* dmap, void* d, const int32_t* smap,
                  const void* s, hipStream_t st);
 void launch_axpby(int dtype, int64_t n, const int32_t* map, void* y, const void* x, const void* a,
-                  int mode, hipStream_t st);
+                  int mode, hipStream_t st, int sk = 0);
 void launch_reduce(int dtype, int kind, int64_t n, const int32_t* ma, const void* a,
                    const int32_t* mb, const void* b, void* partials, void* result,
                    unsigned* ticket, hipStream_t st);
@@ -1270,14 +1270,19 @@ int pa_vec_copy(pa_vec* d, const pa_index* id, const pa_vec* s, const pa_index* 
 
 int pa_vec_axpby(pa_vec* y, const pa_vec* x, const pa_index* idx, const void* a, int mode, int all_lids) {
   CHECK_ARG(y && a, "null argument");
+  const int sk = (mode & PA_BCAST_F64) ? 1 : (mode & PA_BCAST_C128) ? 2 : 0;
+  CHECK_ARG(!((mode & PA_BCAST_F64) && (mode & PA_BCAST_C128)), "axpby: one scalar kind");
+  CHECK_ARG(sk != 2 || y->dtype == PA_C64 || y->dtype == PA_C128,
+            "axpby: a ComplexF64 scalar into a real vector (InexactError)");
+  mode &= ~(PA_BCAST_F64 | PA_BCAST_C128);
   CHECK_ARG(mode >= 0 && mode <= 4, "invalid axpby mode");
   CHECK_ARG(mode == 4 || (x && x->dtype == y->dtype && x->n == y->n), "axpby: x must match y");
   HIPC(hipSetDevice(y->ctx->device));
   if (all_lids) {
-    launch_axpby(y->dtype, y->n, nullptr, y->d, x ? x->d : nullptr, a, mode, y->ctx->s_main);
+    launch_axpby(y->dtype, y->n, nullptr, y->d, x ? x->d : nullptr, a, mode, y->ctx->s_main, sk);
   } else {
     CHECK_ARG(idx && idx->nlids == y->n, "axpby over owned values needs the vector's index set");
-    launch_axpby(y->dtype, idx->noids, idx->d_oid_to_lid, y->d, x ? x->d : nullptr, a, mode, y->ctx->s_main);
+    launch_axpby(y->dtype, idx->noids, idx->d_oid_to_lid, y->d, x ? x->d : nullptr, a, mode, y->ctx->s_main, sk);
   }
   HIPC(hipGetLastError());
   return 0;
@@ -2598,6 +2603,23 @@ int reduce_all(int n, const pa_vec* const a[], const pa_index* const ia[], const
   return gather_results(n, ctxs.data(), cplx, vals);
 }
 
+// reduce(+, c; init=zero(T)) over the part values in part order
+// (Interfaces.jl:221-238), in T: each part's value is rounded to T first
+// (Julia's local dot / sum / norm^2 return T), Float32 parts add in Float32
+c128 fold_parts(int dt, const std::vector<c128>& vals, bool real_only) {
+  if (dt == PA_F32 || dt == PA_C64) {
+    float re = 0.f, im = 0.f;
+    for (const auto& v : vals) {
+      re = re + (float)v.re;
+      if (!real_only) im = im + (float)v.im;
+    }
+    return c128{(double)re, (double)im};
+  }
+  c128 s{0.0, 0.0};
+  for (const auto& v : vals) s = s + (real_only ? c128{v.re, 0.0} : v);
+  return s;
+}
+
 void store_scalar(int dt, c128 s, void* result) {
   switch (dt) {
     case PA_F32: *(float*)result = (float)s.re; break;
@@ -2625,9 +2647,7 @@ int pa_spmv_dot_all(int n, pa_mat* const A[], pa_vec* const y[], const pa_index*
   const int dt = A[0]->dtype;
   std::vector<c128> vals;
   if (gather_results(n, ctxs.data(), dt == PA_C64 || dt == PA_C128, &vals)) return -1;
-  c128 s{0.0, 0.0};
-  for (const auto& v : vals) s = s + v;  // reduce(+; init=0) in part order
-  store_scalar(dt, s, dot_result);
+  store_scalar(dt, fold_parts(dt, vals, false), dot_result);
   return 0;
 }
 
@@ -2652,8 +2672,9 @@ int pa_cg_update_all(int n, pa_vec* const x[], pa_vec* const r[], const pa_vec* 
                    (double*)cx->d_partials, nb, cx->s_main);
       launch_fold(0, nb, cx->d_partials, cx->d_fold, cx->d_result, cx->d_ticket, cx->s_main);
     } else {  // unfused: two broadcasts and the norm reduction
-      launch_axpby(dt, m, nullptr, x[i]->d, u[i]->d, alpha, 1, cx->s_main);
-      launch_axpby(dt, m, nullptr, r[i]->d, c[i]->d, alpha, 2, cx->s_main);
+      const int sk = (dt == PA_C64 || dt == PA_C128) ? 2 : 1;  // α: Float64 / ComplexF64
+      launch_axpby(dt, m, nullptr, x[i]->d, u[i]->d, alpha, 1, cx->s_main, sk);
+      launch_axpby(dt, m, nullptr, r[i]->d, c[i]->d, alpha, 2, cx->s_main, sk);
       launch_reduce(dt, 1, idx[i]->noids, idx[i]->d_oid_to_lid, r[i]->d, nullptr, nullptr, cx->d_partials,
                     cx->d_result, cx->d_ticket, cx->s_main);
     }
@@ -2661,9 +2682,7 @@ int pa_cg_update_all(int n, pa_vec* const x[], pa_vec* const r[], const pa_vec* 
   HIPC(hipGetLastError());
   std::vector<c128> vals;
   if (gather_results(n, ctxs.data(), false, &vals)) return -1;
-  double s = 0.0;
-  for (const auto& v : vals) s = s + v.re;
-  *rnorm = std::sqrt(s);  // (…)^(1/2), correctly rounded
+  *rnorm = std::sqrt(fold_parts(dt, vals, true).re);  // (…)^(1/2) in Float64, correctly rounded
   return 0;
 }
 
@@ -2852,7 +2871,7 @@ int pa_cg_solve_all(int n, pa_mat* const A[], pa_vec* const x[], const pa_vec* c
         launch_cg_xr(dt, m, idx[i]->noids, nullptr, x[i]->d, r[i]->d, u[i]->d, c[i]->d, nullptr, R.st[i],
                      (double*)cx->d_partials, nbk, cx->s_main);
         if (tail)  // prev = residual; residual = norm(r); it += 1; done?
-          launch_fold_cg_step(nbk, cx->d_partials, cx->d_fold, cx->d_result, cx->d_ticket, R.st[i], R.hist[i],
+          launch_fold_cg_step(dt, nbk, cx->d_partials, cx->d_fold, cx->d_result, cx->d_ticket, R.st[i], R.hist[i],
                               cx->s_main);
         else
           launch_fold(0, nbk, cx->d_partials, cx->d_fold, cx->d_result, cx->d_ticket, cx->s_main);
@@ -2861,7 +2880,7 @@ int pa_cg_solve_all(int n, pa_mat* const A[], pa_vec* const x[], const pa_vec* c
         if (cg_gather(R, 8)) return -1;
         for (int i = 0; i < n; ++i) {  // prev = residual; residual = norm(r); it += 1; done?
           HIPC(hipSetDevice(R.ctxs[i]->device));
-          launch_cg_step(R.P, (const double*)R.ctxs[i]->d_gather, R.st[i], R.hist[i], R.ctxs[i]->s_main);
+          launch_cg_step(dt, R.P, (const double*)R.ctxs[i]->d_gather, R.st[i], R.hist[i], R.ctxs[i]->s_main);
         }
       }
       HIPC(hipGetLastError());
@@ -2902,15 +2921,7 @@ int pa_dot_all(int n, const pa_vec* const a[], const pa_index* const ia[], const
   CHECK_ARG(result, "null result");
   std::vector<c128> vals;
   if (reduce_all(n, a, ia, b, ib, 0, &vals)) return -1;
-  // reduce(+, c; init=zero) folded in part order (Interfaces.jl:221-238)
-  c128 s{0.0, 0.0};
-  for (const auto& v : vals) s = s + v;
-  switch (a[0]->dtype) {
-    case PA_F32: *(float*)result = (float)s.re; break;
-    case PA_F64: *(double*)result = s.re; break;
-    case PA_C64: ((float*)result)[0] = (float)s.re; ((float*)result)[1] = (float)s.im; break;
-    case PA_C128: ((double*)result)[0] = s.re; ((double*)result)[1] = s.im; break;
-  }
+  store_scalar(a[0]->dtype, fold_parts(a[0]->dtype, vals, false), result);
   return 0;
 }
 
@@ -2918,11 +2929,9 @@ int pa_norm2_all(int n, const pa_vec* const a[], const pa_index* const ia[], voi
   CHECK_ARG(result, "null result");
   std::vector<c128> vals;
   if (reduce_all(n, a, ia, nullptr, nullptr, 1, &vals)) return -1;
-  double s = 0.0;
-  for (const auto& v : vals) s = s + v.re;
   // (…)^(1/p) with p = 2 (Interfaces.jl:1771); Julia promotes to Float64.
   // x^0.5 correctly rounded is sqrt(x) (the device CG uses the same)
-  *(double*)result = std::sqrt(s);
+  *(double*)result = std::sqrt(fold_parts(a[0]->dtype, vals, true).re);
   return 0;
 }
 
@@ -2930,14 +2939,7 @@ int pa_sum_all(int n, const pa_vec* const a[], const pa_index* const ia[], void*
   CHECK_ARG(result, "null result");
   std::vector<c128> vals;
   if (reduce_all(n, a, ia, nullptr, nullptr, 2, &vals)) return -1;
-  c128 s{0.0, 0.0};
-  for (const auto& v : vals) s = s + v;
-  switch (a[0]->dtype) {
-    case PA_F32: *(float*)result = (float)s.re; break;
-    case PA_F64: *(double*)result = s.re; break;
-    case PA_C64: ((float*)result)[0] = (float)s.re; ((float*)result)[1] = (float)s.im; break;
-    case PA_C128: ((double*)result)[0] = s.re; ((double*)result)[1] = s.im; break;
-  }
+  store_scalar(a[0]->dtype, fold_parts(a[0]->dtype, vals, false), result);
   return 0;
 }
 

@@ -37,6 +37,24 @@ template <typename T> struct real_of { using type = T; };
 template <> struct real_of<c64> { using type = float; };
 template <> struct real_of<c128> { using type = double; };
 
+// The wide type of Julia's mixed broadcasts with a Float64 / ComplexF64
+// scalar (IterativeSolvers' α, β are Float64 even for Float32 vectors: norm
+// of a PVector returns Float64, Interfaces.jl:1771): `r .+ β.*u` evaluates
+// in W and rounds to T once on the store.
+template <typename T> struct wide_of { using type = T; };
+template <> struct wide_of<float> { using type = double; };
+template <> struct wide_of<c64> { using type = c128; };
+__host__ __device__ inline double widen(float v) { return (double)v; }
+__host__ __device__ inline double widen(double v) { return v; }
+__host__ __device__ inline c128 widen(c64 v) { return c128{(double)v.re, (double)v.im}; }
+__host__ __device__ inline c128 widen(c128 v) { return v; }
+template <typename T> __host__ __device__ inline T narrow(typename wide_of<T>::type v) { return (T)v; }
+template <> __host__ __device__ inline c64 narrow<c64>(c128 v) { return c64{(float)v.re, (float)v.im}; }
+template <> __host__ __device__ inline c128 narrow<c128>(c128 v) { return v; }
+// Real * Complex is componentwise in Julia (base/complex.jl: x*real(z), x*imag(z))
+__host__ __device__ inline double rscale(double a, double x) { return a * x; }
+__host__ __device__ inline c128 rscale(double a, c128 z) { return c128{a * z.re, a * z.im}; }
+
 template <typename T> __host__ __device__ inline T zero_of() { return T(0); }
 template <> __host__ __device__ inline c64 zero_of<c64>() { return {0.f, 0.f}; }
 template <> __host__ __device__ inline c128 zero_of<c128>() { return {0.0, 0.0}; }
@@ -195,7 +213,7 @@ struct CGState {
   int64_t maxiter;
   int32_t done;      // it >= maxiter || res <= tol
   int32_t pad;
-  c128 alpha;        // α in the vectors' element type (first sizeof(T) bytes)
+  c128 alpha;        // α in the wide type: Float64 (.re) for real T, ComplexF64 for complex T
   int64_t xit;       // iterations whose x .+= α.*u is applied (deferred into the next u update)
 };
 

@@ -253,20 +253,40 @@ __global__ void k_copy_map(int64_t n, const int32_t* __restrict__ dmap, T* __res
     d[dmap ? (int64_t)dmap[i] : i] = s[smap ? (int64_t)smap[i] : i];
 }
 
-template <typename T, int MODE>
+// The scalar of a broadcast and the type its elements are evaluated in:
+// SK 0 a scalar of the element type T (arithmetic in T); SK 1 a Float64
+// (Real * element componentwise, arithmetic in Float64 / ComplexF64, one
+// rounding to T on the store); SK 2 a ComplexF64 (complex T only).  Julia's
+// promotion rules for `y .= x .+ a.*y` with those scalars.
+template <typename T, int SK> struct BcastScalar { using A = T; using W = T; };
+template <typename T> struct BcastScalar<T, 1> { using A = double; using W = typename wide_of<T>::type; };
+template <typename T> struct BcastScalar<T, 2> { using A = c128; using W = c128; };
+
+template <typename W, typename T> __device__ inline W to_w(T v) {
+  if constexpr (std::is_same<W, T>::value) return v; else return widen(v);
+}
+template <typename T, typename W> __device__ inline T from_w(W v) {
+  if constexpr (std::is_same<W, T>::value) return v; else return narrow<T>(v);
+}
+template <typename A, typename W> __device__ inline W scale(A a, W v) {
+  if constexpr (std::is_same<A, double>::value) return rscale(a, v); else return a * v;
+}
+
+template <typename T, int MODE, int SK>
 __global__ void k_axpby(int64_t n, const int32_t* __restrict__ map, T* __restrict__ y,
-                        const T* __restrict__ x, T a) {
+                        const T* __restrict__ x, typename BcastScalar<T, SK>::A a) {
+  using W = typename BcastScalar<T, SK>::W;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x) {
     const int64_t l = map ? (int64_t)map[i] : i;
-    const T yi = y[l];
-    T r;
-    if (MODE == 0) r = x[l] + a * yi;        // u .= r .+ β.*u
-    else if (MODE == 1) r = yi + a * x[l];   // x .+= α.*u
-    else if (MODE == 2) r = yi - a * x[l];   // r .-= α.*c
-    else if (MODE == 3) r = yi - x[l];       // r .-= c
-    else r = yi * a;                         // rmul!(y, a)
-    y[l] = r;
+    const W yi = to_w<W>(y[l]);
+    W r;
+    if (MODE == 0) r = to_w<W>(x[l]) + scale(a, yi);        // u .= r .+ β.*u
+    else if (MODE == 1) r = yi + scale(a, to_w<W>(x[l]));   // x .+= α.*u
+    else if (MODE == 2) r = yi - scale(a, to_w<W>(x[l]));   // r .-= α.*c
+    else if (MODE == 3) r = yi - to_w<W>(x[l]);             // r .-= c
+    else r = scale(a, yi);                                  // rmul!(y, a): a * y[i]
+    y[l] = from_w<T>(r);
   }
 }
 
@@ -304,27 +324,42 @@ void launch_copy(int dtype, int64_t n, const int32_t* dmap, void* d, const int32
   }
 }
 
-template <typename T>
+template <typename T, int SK>
 static void axpby_t(int64_t n, const int32_t* map, void* y, const void* x, const void* a, int mode,
                     hipStream_t st) {
   if (n <= 0) return;
-  const T av = *(const T*)a;
+  using A = typename BcastScalar<T, SK>::A;
+  const A av = *(const A*)a;
   const dim3 g(grid_for(n, 256, 8192)), b(256);
   switch (mode) {
-    case 0: hipLaunchKernelGGL((k_axpby<T, 0>), g, b, 0, st, n, map, (T*)y, (const T*)x, av); break;
-    case 1: hipLaunchKernelGGL((k_axpby<T, 1>), g, b, 0, st, n, map, (T*)y, (const T*)x, av); break;
-    case 2: hipLaunchKernelGGL((k_axpby<T, 2>), g, b, 0, st, n, map, (T*)y, (const T*)x, av); break;
-    case 3: hipLaunchKernelGGL((k_axpby<T, 3>), g, b, 0, st, n, map, (T*)y, (const T*)x, av); break;
-    default: hipLaunchKernelGGL((k_axpby<T, 4>), g, b, 0, st, n, map, (T*)y, (const T*)x, av); break;
+    case 0: hipLaunchKernelGGL((k_axpby<T, 0, SK>), g, b, 0, st, n, map, (T*)y, (const T*)x, av); break;
+    case 1: hipLaunchKernelGGL((k_axpby<T, 1, SK>), g, b, 0, st, n, map, (T*)y, (const T*)x, av); break;
+    case 2: hipLaunchKernelGGL((k_axpby<T, 2, SK>), g, b, 0, st, n, map, (T*)y, (const T*)x, av); break;
+    case 3: hipLaunchKernelGGL((k_axpby<T, 3, SK>), g, b, 0, st, n, map, (T*)y, (const T*)x, av); break;
+    default: hipLaunchKernelGGL((k_axpby<T, 4, SK>), g, b, 0, st, n, map, (T*)y, (const T*)x, av); break;
   }
 }
+template <typename T>
+static void axpby_sk(int64_t n, const int32_t* map, void* y, const void* x, const void* a, int mode, int sk,
+                     hipStream_t st) {
+  constexpr bool cplx = std::is_same<T, c64>::value || std::is_same<T, c128>::value;
+  if (sk == 1) {
+    axpby_t<T, 1>(n, map, y, x, a, mode, st);
+  } else if (sk == 2) {
+    if constexpr (cplx) axpby_t<T, 2>(n, map, y, x, a, mode, st);
+  } else {
+    axpby_t<T, 0>(n, map, y, x, a, mode, st);
+  }
+}
+// mode 0..4 (pa_vec_axpby); scalar kind sk (BcastScalar): 0 element type,
+// 1 Float64, 2 ComplexF64 (complex vectors only)
 void launch_axpby(int dtype, int64_t n, const int32_t* map, void* y, const void* x, const void* a,
-                  int mode, hipStream_t st) {
+                  int mode, hipStream_t st, int sk) {
   switch (dtype) {
-    case PA_F32: axpby_t<float>(n, map, y, x, a, mode, st); break;
-    case PA_F64: axpby_t<double>(n, map, y, x, a, mode, st); break;
-    case PA_C64: axpby_t<c64>(n, map, y, x, a, mode, st); break;
-    case PA_C128: axpby_t<c128>(n, map, y, x, a, mode, st); break;
+    case PA_F32: axpby_sk<float>(n, map, y, x, a, mode, sk == 2 ? 0 : sk, st); break;
+    case PA_F64: axpby_sk<double>(n, map, y, x, a, mode, sk == 2 ? 0 : sk, st); break;
+    case PA_C64: axpby_sk<c64>(n, map, y, x, a, mode, sk, st); break;
+    case PA_C128: axpby_sk<c128>(n, map, y, x, a, mode, sk, st); break;
   }
 }
 

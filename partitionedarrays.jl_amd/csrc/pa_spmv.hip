@@ -819,20 +819,28 @@ void launch_spmv_part(int which, int64_t nwork, const int32_t* list, const pa_ma
   }
 }
 
+// α of the device CG state in the wide type W (Float64 / ComplexF64)
+template <typename W> __device__ inline W cg_alpha_of(const CGState* st);
+template <> __device__ inline double cg_alpha_of<double>(const CGState* st) { return st->alpha.re; }
+template <> __device__ inline c128 cg_alpha_of<c128>(const CGState* st) { return st->alpha; }
+
 // x .+= α.*u; r .-= α.*c (all lids, Interfaces.jl:1710-1737) and the owned
 // Σ|r|² of norm(r) (1767-1772) in one pass (contiguous owned lids
-// 0..noids-1); per-block partials, folded in block order afterwards.
-// V elements per 16 B access (V = 1: unaligned fallback).  DEV: α comes from
-// the device CG state (pa_cg_solve_all), x is left alone (its update is
-// deferred into the next k_cg_xu, which reads u anyway) and a finished solve
-// is a no-op.
+// 0..noids-1); per-block partials, folded in block order afterwards.  α is
+// Float64 (ComplexF64 for complex T) as in IterativeSolvers: each element
+// is evaluated in that wide type and rounded to T once.  V elements per
+// 16 B access (V = 1: unaligned fallback).  DEV: α comes from the device CG
+// state (pa_cg_solve_all), x is left alone (its update is deferred into the
+// next k_cg_xu, which reads u anyway) and a finished solve is a no-op.
 template <typename T, int V, bool DEV>
 __global__ __launch_bounds__(256) void k_cg_xr(int64_t n, int64_t noids, T* __restrict__ x, T* __restrict__ r,
-                                               const T* __restrict__ u, const T* __restrict__ c, T alpha,
-                                               const CGState* __restrict__ st, double* __restrict__ part) {
+                                               const T* __restrict__ u, const T* __restrict__ c,
+                                               typename wide_of<T>::type alpha, const CGState* __restrict__ st,
+                                               double* __restrict__ part) {
+  using W = typename wide_of<T>::type;
   if (DEV) {
     if (st->done) return;
-    alpha = *reinterpret_cast<const T*>(&st->alpha);
+    alpha = cg_alpha_of<W>(st);
   }
   using P = Pack<T, V>;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
@@ -844,21 +852,21 @@ __global__ __launch_bounds__(256) void k_cg_xr(int64_t n, int64_t noids, T* __re
       P xv = reinterpret_cast<const P*>(x)[j];
       const P uv = reinterpret_cast<const P*>(u)[j];
 #pragma unroll
-      for (int e = 0; e < V; ++e) xv.v[e] = xv.v[e] + alpha * uv.v[e];
+      for (int e = 0; e < V; ++e) xv.v[e] = narrow<T>(widen(xv.v[e]) + alpha * widen(uv.v[e]));
       reinterpret_cast<P*>(x)[j] = xv;
     }
     P rv = reinterpret_cast<const P*>(r)[j];
     const P cv = reinterpret_cast<const P*>(c)[j];
 #pragma unroll
     for (int e = 0; e < V; ++e) {
-      rv.v[e] = rv.v[e] - alpha * cv.v[e];
+      rv.v[e] = narrow<T>(widen(rv.v[e]) - alpha * widen(cv.v[e]));
       if (j * V + e < noids) s = s + (double)abs2(rv.v[e]);
     }
     reinterpret_cast<P*>(r)[j] = rv;
   }
   for (int64_t i = nv * V + t; i < n; i += stride) {
-    if (!DEV) x[i] = x[i] + alpha * u[i];
-    const T ri = r[i] - alpha * c[i];
+    if (!DEV) x[i] = narrow<T>(widen(x[i]) + alpha * widen(u[i]));
+    const T ri = narrow<T>(widen(r[i]) - alpha * widen(c[i]));
     r[i] = ri;
     if (i < noids) s = s + (double)abs2(ri);
   }
@@ -872,9 +880,10 @@ __global__ __launch_bounds__(256) void k_cg_xr(int64_t n, int64_t noids, T* __re
 template <typename T>
 static void cg_xr_t(int64_t n, int64_t noids, void* x, void* r, const void* u, const void* c,
                     const void* alpha, const CGState* st, double* part, int nb, hipStream_t st_) {
+  using W = typename wide_of<T>::type;
   constexpr int V = 16 / sizeof(T);
   const bool aligned = ((uintptr_t)x | (uintptr_t)r | (uintptr_t)u | (uintptr_t)c) % 16 == 0;
-  const T a = alpha ? *(const T*)alpha : zero_of<T>();
+  const W a = alpha ? *(const W*)alpha : zero_of<W>();
 #define PA_XR(VV, DD)                                                                                  \
   hipLaunchKernelGGL((k_cg_xr<T, VV, DD>), dim3(nb), dim3(256), 0, st_, n, noids, (T*)x, (T*)r,      \
                      (const T*)u, (const T*)c, a, st, part)
@@ -886,7 +895,7 @@ static void cg_xr_t(int64_t n, int64_t noids, void* x, void* r, const void* u, c
 #undef PA_XR
 }
 
-// alpha: host scalar (st == nullptr) or read from the device CG state
+// alpha: host scalar in the wide type (st == nullptr) or read from the device CG state
 void launch_cg_xr(int dtype, int64_t n, int64_t noids, const int32_t* own, void* x, void* r, const void* u,
                   const void* c, const void* alpha, const CGState* st, double* part, int nb, hipStream_t s) {
   (void)own;  // owned lids are 0..noids-1 (checked by the caller)
@@ -899,28 +908,25 @@ void launch_cg_xr(int dtype, int64_t n, int64_t noids, const int32_t* own, void*
 }
 
 // ---------------------------------------------------------------------------
-// Device-driven CG scalars (pa_cg_solve_all).  The host driver folds the
-// part values in part order in double / c128 and hands scalars over as
-// the vectors' element type; these kernels repeat exactly that arithmetic
-// on one thread so the device recurrence equals the host-driven one.
+// Device-driven CG scalars (pa_cg_solve_all).  The same arithmetic as the
+// host-driven loop (pvector.cg_ over pa_spmv_dot_all / pa_cg_update_all),
+// on one thread, so the device recurrence equals it bit for bit.
 
-template <typename T> __device__ inline T real_scalar(double v) { return (T)v; }
-template <> __device__ inline c64 real_scalar<c64>(double v) { return c64{(float)v, 0.f}; }
-template <> __device__ inline c128 real_scalar<c128>(double v) { return c128{v, 0.0}; }
-
-// u .= r .+ β.*u over all lids, β = residual²/prev_residual² (IterativeSolvers
-// 0.9 cg iterate), preceded per element by the previous iteration's deferred
-// x .+= α.*u (while it > xit: α is still that iteration's, u not yet
-// overwritten).  Same arithmetic per element as the host-driven loop.  V
-// elements per 16 B access (V = 1: unaligned fallback).
+// u .= r .+ β.*u over all lids, β = residual²/prev_residual² (Float64,
+// IterativeSolvers 0.9 cg iterate; Real * Complex componentwise), preceded
+// per element by the previous iteration's deferred x .+= α.*u (while it >
+// xit: α is still that iteration's, u not yet overwritten).  Each element in
+// the wide type, rounded to T once.  V elements per 16 B access (V = 1:
+// unaligned fallback).
 template <typename T, int V>
 __global__ __launch_bounds__(256) void k_cg_xu(int64_t n, T* __restrict__ x, T* __restrict__ u,
                                                const T* __restrict__ r, const CGState* __restrict__ st) {
+  using W = typename wide_of<T>::type;
   const bool xpend = st->it > st->xit;
   const bool upd = !st->done;
   if (!xpend && !upd) return;
-  const T a = *reinterpret_cast<const T*>(&st->alpha);
-  const T b = real_scalar<T>((st->res * st->res) / (st->prev * st->prev));
+  const W a = cg_alpha_of<W>(st);
+  const double b = (st->res * st->res) / (st->prev * st->prev);
   using P = Pack<T, V>;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
@@ -930,72 +936,71 @@ __global__ __launch_bounds__(256) void k_cg_xu(int64_t n, T* __restrict__ x, T* 
     if (xpend) {
       P xv = reinterpret_cast<const P*>(x)[j];
 #pragma unroll
-      for (int e = 0; e < V; ++e) xv.v[e] = xv.v[e] + a * uv.v[e];
+      for (int e = 0; e < V; ++e) xv.v[e] = narrow<T>(widen(xv.v[e]) + a * widen(uv.v[e]));
       reinterpret_cast<P*>(x)[j] = xv;
     }
     if (upd) {
       const P rv = reinterpret_cast<const P*>(r)[j];
 #pragma unroll
-      for (int e = 0; e < V; ++e) uv.v[e] = rv.v[e] + b * uv.v[e];
+      for (int e = 0; e < V; ++e) uv.v[e] = narrow<T>(widen(rv.v[e]) + rscale(b, widen(uv.v[e])));
       reinterpret_cast<P*>(u)[j] = uv;
     }
   }
   for (int64_t i = nv * V + t; i < n; i += stride) {
     const T ui = u[i];
-    if (xpend) x[i] = x[i] + a * ui;
-    if (upd) u[i] = r[i] + b * ui;
+    if (xpend) x[i] = narrow<T>(widen(x[i]) + a * widen(ui));
+    if (upd) u[i] = narrow<T>(widen(r[i]) + rscale(b, widen(ui)));
   }
 }
 
-// the dot partials of the P parts (accumulators, part order) →
-// dot = reduce(+; init=0) narrowed to T → α = residual² / dot.  It also
-// records that the previous iteration's x update has been applied (k_cg_xu
-// ran before this iteration's SpMV).
+// Julia's inv(::ComplexF64) (base/complex.jl, the scaled Smith algorithm):
+// Float64 / ComplexF64 is a * inv(z), componentwise.
+__host__ __device__ inline c128 julia_inv(c128 w) {
+  double c = w.re, d = w.im;
+  if (isinf(c) || isinf(d)) return c128{copysign(0.0, c), signbit(d) ? 0.0 : -0.0};  // flipsign(-0.0, d)
+  const double half = 0.5, two = 2.0;
+  const double cd = fmax(fabs(c), fabs(d));
+  const double ov = 1.7976931348623157e308, un = 2.2250738585072014e-308, eps = 2.220446049250313e-16;
+  const double bs = two / (eps * eps);
+  double s = 1.0;
+  if (cd >= half * ov) { c = half * c; d = half * d; s = s * half; }
+  if (cd <= un * two / eps) { c = c * bs; d = d * bs; s = s * bs; }
+  double p, q;
+  if (fabs(d) <= fabs(c)) {
+    const double r = d / c;
+    const double t = 1.0 / (c + d * r);
+    p = t;
+    q = -r * t;
+  } else {
+    const double c2 = d, d2 = c;
+    const double r = d2 / c2;
+    const double t = 1.0 / (c2 + d2 * r);
+    p = r * t;
+    q = -t;
+  }
+  return c128{p * s, q * s};
+}
+
+// the dot partials of the P parts (accumulators, part order) → dot =
+// reduce(+; init=0) over the part values in T (each part's value rounded to
+// T: Julia's local dot returns T) → α = residual² / dot in Float64 /
+// ComplexF64.  It also records that the previous iteration's x update has
+// been applied (k_cg_xu ran before this iteration's SpMV).
 template <typename T>
 __device__ inline void cg_alpha(int P, const void* __restrict__ gathered, CGState* __restrict__ st) {
   st->xit = st->it;
   if (st->done) return;
   const double res2 = st->res * st->res;
-  T* out = reinterpret_cast<T*>(&st->alpha);
   if constexpr (std::is_same<T, float>::value || std::is_same<T, double>::value) {
     const double* g = (const double*)gathered;
-    double s = 0.0;
-    for (int p = 0; p < P; ++p) s = s + g[p];
-    const double d = (double)(T)s;
-    *out = (T)(res2 / d);
+    T s = (T)0;
+    for (int p = 0; p < P; ++p) s = s + (T)g[p];
+    st->alpha = c128{res2 / (double)s, 0.0};
   } else {
     const c128* g = (const c128*)gathered;
-    c128 s{0.0, 0.0};
-    for (int p = 0; p < P; ++p) s = s + g[p];
-    double br, bi;
-    if constexpr (std::is_same<T, c64>::value) {
-      br = (double)(float)s.re;
-      bi = (double)(float)s.im;
-    } else {
-      br = s.re;
-      bi = s.im;
-    }
-    // res2 / complex(br, bi), Smith's division as the host driver computes it
-    // (CPython _Py_c_quot with a = res2 + 0im)
-    double qr, qi;
-    const double abr = br < 0 ? -br : br, abi = bi < 0 ? -bi : bi;
-    if (abr >= abi) {
-      if (abr == 0.0) {
-        qr = qi = 0.0;
-      } else {
-        const double ratio = bi / br;
-        const double denom = br + bi * ratio;
-        qr = (res2 + 0.0 * ratio) / denom;
-        qi = (0.0 - res2 * ratio) / denom;
-      }
-    } else {
-      const double ratio = br / bi;
-      const double denom = br * ratio + bi;
-      qr = (res2 * ratio + 0.0) / denom;
-      qi = (0.0 * ratio - res2) / denom;
-    }
-    if constexpr (std::is_same<T, c64>::value) *out = c64{(float)qr, (float)qi};
-    else *out = c128{qr, qi};
+    T s = zero_of<T>();
+    for (int p = 0; p < P; ++p) s = s + narrow<T>(g[p]);
+    st->alpha = rscale(res2, julia_inv(widen(s)));
   }
 }
 
@@ -1006,12 +1011,23 @@ __global__ void k_cg_alpha(int P, const void* __restrict__ gathered, CGState* __
 }
 
 // Σ|r|² partials of the P parts → prev = residual; residual = sqrt(Σ);
-// it += 1; history[it] = residual; done = it >= maxiter || residual <= tol
+// it += 1; history[it] = residual; done = it >= maxiter || residual <= tol.
+// F32 (Float32 / ComplexF32 vectors): each part's norm(r)^2 is a Float32 and
+// their reduce(+) runs in Float32 before the Float64 ^(1/2) (Interfaces.jl:
+// 1767-1772).
+template <bool F32>
 __device__ inline void cg_step(int P, const double* __restrict__ gathered, CGState* __restrict__ st,
                                double* __restrict__ history) {
   if (st->done) return;
-  double s = 0.0;
-  for (int p = 0; p < P; ++p) s = s + gathered[p];
+  double s;
+  if (F32) {
+    float f = 0.f;
+    for (int p = 0; p < P; ++p) f = f + (float)gathered[p];
+    s = (double)f;
+  } else {
+    s = 0.0;
+    for (int p = 0; p < P; ++p) s = s + gathered[p];
+  }
   const double res = sqrt(s);
   st->prev = st->res;
   st->res = res;
@@ -1021,10 +1037,11 @@ __device__ inline void cg_step(int P, const double* __restrict__ gathered, CGSta
   st->done = (it >= st->maxiter || res <= st->tol) ? 1 : 0;
 }
 
+template <bool F32>
 __global__ void k_cg_step(int P, const double* __restrict__ gathered, CGState* __restrict__ st,
                           double* __restrict__ history) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
-  cg_step(P, gathered, st, history);
+  cg_step<F32>(P, gathered, st, history);
 }
 
 // One part in one process: the fold of the part's partials ends in the
@@ -1034,10 +1051,11 @@ struct AlphaTail {
   CGState* st;
   __device__ void operator()(const void* out) const { cg_alpha<T>(1, out, st); }
 };
+template <bool F32>
 struct StepTail {
   CGState* st;
   double* hist;
-  __device__ void operator()(const void* out) const { cg_step(1, (const double*)out, st, hist); }
+  __device__ void operator()(const void* out) const { cg_step<F32>(1, (const double*)out, st, hist); }
 };
 
 // gathered[p] = *srcs[p] (accsz bytes each): the part values of the parts
@@ -1079,8 +1097,11 @@ void launch_cg_alpha(int dtype, int P, const void* gathered, CGState* st, hipStr
   }
 }
 
-void launch_cg_step(int P, const double* gathered, CGState* st, double* history, hipStream_t s) {
-  hipLaunchKernelGGL(k_cg_step, dim3(1), dim3(64), 0, s, P, gathered, st, history);
+void launch_cg_step(int dtype, int P, const double* gathered, CGState* st, double* history, hipStream_t s) {
+  if (dtype == PA_F32 || dtype == PA_C64)
+    hipLaunchKernelGGL(k_cg_step<true>, dim3(1), dim3(64), 0, s, P, gathered, st, history);
+  else
+    hipLaunchKernelGGL(k_cg_step<false>, dim3(1), dim3(64), 0, s, P, gathered, st, history);
 }
 
 // fold the SpMV's dot partials into out, then α (one part per process)
@@ -1103,9 +1124,12 @@ void launch_fold_cg_alpha(int dtype, int nb, const void* in, void* scratch, void
 }
 
 // fold the Σ|r|² partials into out, then the residual step
-void launch_fold_cg_step(int nb, const void* in, void* scratch, void* out, unsigned* ticket, CGState* st,
-                         double* history, hipStream_t s) {
-  fold_launch<double>(nb, (const double*)in, (double*)scratch, (double*)out, ticket, StepTail{st, history}, s);
+void launch_fold_cg_step(int dtype, int nb, const void* in, void* scratch, void* out, unsigned* ticket,
+                         CGState* st, double* history, hipStream_t s) {
+  if (dtype == PA_F32 || dtype == PA_C64)
+    fold_launch<double>(nb, (const double*)in, (double*)scratch, (double*)out, ticket, StepTail<true>{st, history}, s);
+  else
+    fold_launch<double>(nb, (const double*)in, (double*)scratch, (double*)out, ticket, StepTail<false>{st, history}, s);
 }
 
 void launch_gather_ptrs(int P, const void* const* srcs, int accsz, void* out, hipStream_t s) {

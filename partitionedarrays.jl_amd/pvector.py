@@ -10,6 +10,7 @@ from __future__ import annotations
 import ctypes as C
 from collections import OrderedDict
 import math
+import sys
 
 import numpy as np
 
@@ -146,12 +147,32 @@ def copyto_(a: PVector, b: PVector) -> PVector:
     return a
 
 
+def _scalar_kind(a, dtype):
+    """the scalar of a broadcast as Julia types it: a Python float is a
+    Float64 and a Python complex a ComplexF64 (np.float64 / np.complex128
+    likewise) — the elements are then evaluated in Float64 / ComplexF64 and
+    rounded once (pa_vec_axpby PA_BCAST_*); ints and scalars of narrower or
+    equal type are converted to the element type."""
+    cplx = np.dtype(dtype).kind == "c"
+    if isinstance(a, (complex, np.complex128)) and not isinstance(a, (float, np.floating)):
+        if not cplx:
+            if complex(a).imag != 0:
+                raise TypeError("broadcast: a complex scalar into a real vector (InexactError)")
+            return np.float64(complex(a).real), _lib.PA_BCAST_F64
+        return np.complex128(a), _lib.PA_BCAST_C128
+    if isinstance(a, (float, np.float64)):
+        return np.float64(a), _lib.PA_BCAST_F64
+    return a, 0
+
+
 def _bcast(y: PVector, x: PVector, a, mode):
     all_lids = 1 if (x is None or y.rows is x.rows) else 0
     if x is not None and not all_lids and not oids_are_equal(y.rows, x.rows):
         raise AssertionError("broadcast: owned ids differ")
     iy = _idx(y)
-    buf, bp = _lib.scalar_buf(a if a is not None else 0, y.dtype)
+    a, kind = _scalar_kind(a if a is not None else 0, y.dtype)
+    mode |= kind
+    buf, bp = _lib.scalar_buf(a, a.dtype if kind else y.dtype)
     xs = x.values.parts if x is not None else [None] * len(y.values.parts)
     for dy, dx, i in zip(y.values.parts, xs, iy):
         _lib.call("pa_vec_axpby", dy.h, dx.h if dx is not None else None, i, bp, mode, all_lids)
@@ -533,14 +554,51 @@ def _spmv_args(c, a, b, alpha, beta):
 
 
 def cg_update_(x: PVector, r: PVector, u: PVector, c: PVector, alpha) -> float:
-    """x .+= α.*u; r .-= α.*c; norm(r) in one pass (pa_cg_update_all)."""
+    """x .+= α.*u; r .-= α.*c; norm(r) in one pass (pa_cg_update_all); α is
+    a Float64 (ComplexF64 for complex vectors) as in IterativeSolvers."""
     if not (x.rows is r.rows is u.rows is c.rows):
         raise ValueError("cg_update_: the four vectors must share one PRange")
-    al, alp = _lib.scalar_buf(alpha, x.dtype)
+    al, alp = _lib.scalar_buf(alpha, np.complex128 if np.dtype(x.dtype).kind == "c" else np.float64)
     out = C.c_double(0.0)
     _lib.call("pa_cg_update_all", len(x.values.parts), _hs(x.values.parts), _hs(r.values.parts),
               _hs(u.values.parts), _hs(c.values.parts), _lib.ptr_array(_idx(x)), alp, C.byref(out))
     return out.value
+
+
+def _julia_inv(w: complex) -> complex:
+    """Julia's inv(::ComplexF64) (base/complex.jl, scaled Smith): Float64 /
+    ComplexF64 is a * inv(z) componentwise (Julia Base arithmetic, restated;
+    the device CG's julia_inv is the same)."""
+    c, d = w.real, w.imag
+    if math.isinf(c) or math.isinf(d):
+        return complex(math.copysign(0.0, c), 0.0 if math.copysign(1.0, d) < 0 else -0.0)
+    half, two = 0.5, 2.0
+    cd = max(abs(c), abs(d))
+    ov, un, eps = sys.float_info.max, sys.float_info.min, sys.float_info.epsilon
+    bs = two / (eps * eps)
+    s = 1.0
+    if cd >= half * ov:
+        c, d, s = half * c, half * d, s * half
+    if cd <= un * two / eps:
+        c, d, s = c * bs, d * bs, s * bs
+    if abs(d) <= abs(c):
+        r = d / c
+        t = 1.0 / (c + d * r)
+        p, q = t, -r * t
+    else:
+        c, d = d, c
+        r = d / c
+        t = 1.0 / (c + d * r)
+        p, q = r * t, -t
+    return complex(p * s, q * s)
+
+
+def _rdiv(a: float, z):
+    """a::Float64 / z::T (Julia: Float64 for real T, a*inv(ComplexF64(z)) for complex)"""
+    if isinstance(z, complex):
+        w = _julia_inv(z)
+        return complex(a * w.real, a * w.imag)
+    return a / float(z)
 
 
 def matvec(a: PSparseMatrix, b: PVector) -> PVector:
@@ -567,8 +625,8 @@ def cg_(x: PVector, A: PSparseMatrix, b: PVector, reltol=None, abstol=0.0, maxit
     (pa_cg_solve_all): the host enqueues `batch` iterations between reads of
     the done flag; results equal the host-driven fused loop bit for bit."""
     real = np.float32 if x.dtype in (np.float32, np.complex64) else np.float64
-    if reltol is None:
-        reltol = math.sqrt(np.finfo(real).eps)
+    if reltol is None:  # sqrt(eps(real(eltype(b)))), in that type
+        reltol = float(np.sqrt(np.finfo(real).eps))
     if maxiter is None:
         maxiter = len(A.cols)
     if device:
@@ -591,11 +649,11 @@ def cg_(x: PVector, A: PSparseMatrix, b: PVector, reltol=None, abstol=0.0, maxit
         beta = (residual * residual) / (prev * prev)  # residual^2 (literal_pow: x*x)
         xpby_(u, r, beta)
         if fuse:
-            alpha = (residual * residual) / mul_dot_(c, A, u)
+            alpha = _rdiv(residual * residual, mul_dot_(c, A, u))
             new = cg_update_(x, r, u, c, alpha)
         else:
             mul_(c, A, u)
-            alpha = (residual * residual) / dot(u, c)
+            alpha = _rdiv(residual * residual, dot(u, c))
             axpy_(x, alpha, u)
             axmy_(r, alpha, c)
             new = norm(r)

@@ -282,3 +282,35 @@ def test_device_cg_fem_sa(be, pamd, O):
     O.cg_(ox, OA, ob, log=ohist)
     assert len(hist) == len(ohist)
     np.testing.assert_allclose(hist, ohist, rtol=1e-8)
+
+
+@pytest.mark.parametrize("device", [False, True])
+def test_fdm_cg_float32_julia_scalars(be, pamd, O, device):
+    """test_fdm.jl in Float32: IterativeSolvers' residual, β and α are
+    Float64 (norm of a PVector is Float64, Interfaces.jl:1771), so the
+    broadcasts evaluate in Float64 and round to Float32, and dot/norm add the
+    parts' Float32 values in Float32.  The device CG (host-driven and device
+    recurrence) follows the oracle's Float32 cg! with those semantics: the
+    first three residuals bit for bit (Float32 scalars would differ from the
+    first iteration on: tools/cg32_probe.py), then within 5e-6 relative (the
+    local dot/norm summation order is BLAS's in the reference: unpinned),
+    same iteration count."""
+    shape = (2, 2, 2)
+    parts = be.get_part_ids(shape)
+    A, b, x0, _ = pamd.drivers.fdm_problem(parts, 10, np.float32)
+    x = x0.copy()
+    hist = []
+    pamd.cg_(x, A, b, history=hist, device=device)
+    OA, ob, ox0, _ = O.fdm_problem(O.get_part_ids(shape), 10)
+    vals = O.map_parts(lambda M: O.CSC(M.m, M.n, M.colptr, M.rowval, O._convert_values(M.nzval, np.float32)),
+                       OA.values)
+    OA32 = O.PSparseMatrix(vals, OA.rows, OA.cols)
+    ob32 = O.PVector(O.map_parts(lambda v: np.asarray(v, np.float32).copy(), ob.values), ob.rows)
+    ox = O.PVector(O.map_parts(lambda v: np.asarray(v, np.float32).copy(), ox0.values), ox0.rows)
+    ohist = []
+    O.cg_(ox, OA32, ob32, log=ohist)
+    assert len(hist) == len(ohist) and len(hist) > 5
+    rel = max(abs(a - b) / abs(b) for a, b in zip(hist, ohist))
+    print(f"Float32 CG: {len(hist)} iterations, max relative history difference {rel:.3e}")
+    assert hist[:3] == ohist[:3]
+    assert rel <= 5e-6
