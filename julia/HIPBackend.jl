@@ -574,14 +574,23 @@ function Base.copyto!(a::HIPVector{T}, b::HIPVector{T}) where {T<:DeviceEltype}
 end
 Base.copy!(a::HIPVector{T}, b::HIPVector{T}) where {T<:DeviceEltype} = copyto!(a, b)
 
+# the scalar as Julia's broadcast types it: a Float64 (Real * Complex
+# componentwise) or a ComplexF64 that widens T is passed as such and the
+# elements are evaluated in Float64 / ComplexF64 (PA_BCAST_F64 / _C128);
+# anything else is converted to T
+const PA_BCAST_F64, PA_BCAST_C128 = Cint(8), Cint(16)
+_bcast_scalar(::Type{T}, a::Float64) where {T} = (Ref{Float64}(a), PA_BCAST_F64)
+_bcast_scalar(::Type{T}, a::ComplexF64) where {T<:Complex} = (Ref{ComplexF64}(a), PA_BCAST_C128)
+_bcast_scalar(::Type{T}, a) where {T} = (Ref{T}(T(a)), Cint(0))
+
 function _axpby!(y::HIPVector{T}, x::Union{Nothing,HIPVector{T}}, a, mode::Integer) where {T<:DeviceEltype}
   all_lids = x === nothing || y.rows === x.rows
   x === nothing || all_lids || @assert oids_are_equal(y.rows, x.rows)
-  s = Ref{T}(T(a))
+  s, kind = _bcast_scalar(T, a)
   yv, xv, iy = dev_vec(y), (x === nothing ? fill(C_NULL, num_parts(y.values)) : dev_vec(x)), dev_idx(y.rows)
   for i in eachindex(yv)
-    check(ccall((:pa_vec_axpby, libpa), Cint, (Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Ref{T}, Cint, Cint),
-                yv[i], xv[i], iy[i], s, mode, all_lids ? 1 : 0))
+    check(ccall((:pa_vec_axpby, libpa), Cint, (Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Cint, Cint),
+                yv[i], xv[i], iy[i], s, Cint(mode) | kind, all_lids ? 1 : 0))
   end
   mark_device_newer!(y)
 end
