@@ -70,6 +70,10 @@ int pa_device_count(int* count);
  *               0: lane-strided partial sums + tree (within 1e-12);
  * "halo_pull"   1: parts of one process read their neighbours' packed
  *               buffers directly (default), 0: staging copies;
+ * "halo_direct" 1: mul! over parts sharing a stream pair reads every ghost
+ *               straight from its owner's x on the compute stream (no
+ *               pack, no cross-stream event; default), 0: pack + pull on
+ *               the comm stream overlapped with the interior slices;
  * "halo_transport" 0: parts of one process exchange by device reads/copies
  *               (default), 1: RCCL send/recv for every part that has a
  *               communicator (pa_comm_init_all / pa_comm_init_rank);

@@ -48,6 +48,7 @@ extern int g_spmv_pattern_rule;
 extern int g_spmv_patterns;  // patterns per slice at build time (1: single-pattern slices only)
 int g_halo_pull = 1;  // pa_tune("halo_pull"): pull-unpack between parts of one process
 int g_spmv_group = 1; // pa_tune("spmv_group"): one launch per phase for the parts sharing a stream pair
+int g_halo_direct = 1;     // pa_tune("halo_direct"): grouped mul! pulls ghosts straight from the owners' x
 int g_halo_transport = 0;  // pa_tune("halo_transport"): 0 parts of this process by device reads, 1 RCCL for all
 int g_comm_cus = 0;   // pa_tune("comm_cus"): CUs reserved for the comm stream (0: priority stream instead)
 // COO → CSC → SELL on the device (pa_coo.hip)
@@ -490,6 +491,69 @@ int build_pull(int i, int n, pa_xchg* const xg[], const LocalSet& L, int dtype, 
   return 0;
 }
 
+// Direct pull table of receiver i for a grouped mul! over the n parts of
+// the call (all local, one device): receive slot p of segment k (sender q at
+// call position j) reads x_j at the lid q lists for this part in its
+// lids_snd.  ok = false when a sender is not in the call.
+int build_direct(int i, int n, pa_xchg* const xg[], const LocalSet& L) {
+  pa_xchg* X = xg[i];
+  pa_pull& P = X->direct;
+  std::vector<const void*> key(xg, xg + n);
+  if (P.built && P.key == key) return 0;
+  dev_free(P.d_bid);
+  dev_free(P.d_elem);
+  dev_free(P.d_bases);
+  P = pa_pull{};
+  P.built = true;
+  P.key = key;
+  const int64_t nslots = X->n_rcv_data;
+  std::vector<int32_t> bid(nslots);
+  std::vector<int64_t> elem(nslots);
+  for (size_t k = 0; k < X->parts_rcv.size(); ++k) {
+    const int j = L.find(X->parts_rcv[k]);
+    if (j < 0) return 0;
+    const pa_xchg* Q = xg[j];
+    if ((int64_t)Q->h_lids_snd.size() != Q->n_snd_data) return 0;
+    int m = -1;
+    for (size_t t = 0; t < Q->parts_snd.size(); ++t)
+      if (Q->parts_snd[t] == X->ctx->part) { m = (int)t; break; }
+    CHECK_ARG(m >= 0, "exchanger mismatch: a receiver lists a sender that does not send to it");
+    const int64_t cnt = X->ptrs_rcv[k + 1] - X->ptrs_rcv[k];
+    CHECK_ARG(cnt == Q->ptrs_snd[m + 1] - Q->ptrs_snd[m],
+              "exchanger mismatch: segment lengths differ (SequentialBackend.jl:187)");
+    for (int64_t t = 0; t < cnt; ++t) {
+      bid[X->ptrs_rcv[k] + t] = j;
+      elem[X->ptrs_rcv[k] + t] = Q->h_lids_snd[Q->ptrs_snd[m] + t];
+    }
+  }
+  HIPC(hipSetDevice(X->ctx->device));
+  if (dev_upload(&P.d_bid, bid) || dev_upload(&P.d_elem, elem)) return -1;
+  P.ok = true;
+  return 0;
+}
+
+// device array of the call's x pointers (the direct pull's bases), cached on
+// the leading context; a new set of vectors uploads once
+void** direct_bases(pa_ctx* c0, int n, pa_vec* const x[]) {
+  std::vector<void*> key(n);
+  for (int i = 0; i < n; ++i) key[i] = x[i]->d;
+  auto& C = c0->bases_cache;
+  for (size_t k = 0; k < C.size(); ++k)
+    if (C[k].first == key) {
+      if (k) std::swap(C[k], C[0]);
+      return C[0].second;
+    }
+  void** d = nullptr;
+  if (dev_upload(&d, key)) return nullptr;
+  if (C.size() >= 16) {
+    (void)hipStreamSynchronize(c0->s_main);  // the evicted array may still be read
+    dev_free(C.back().second);
+    C.pop_back();
+  }
+  C.insert(C.begin(), {key, d});
+  return d;
+}
+
 // One RCCL group of point-to-point byte transfers (segment src part → dst
 // part).  Sends to one peer rank are matched with that rank's receives in
 // posting order, and a rank may hold several parts (pa_comm_init_all: the
@@ -699,6 +763,11 @@ int pa_tune(const char* key, int value, int* previous) {
   } else if (!std::strcmp(key, "halo_pull")) {
     CHECK_ARG(value == 0 || value == 1, "halo_pull: 1 = receivers read the senders' buffers (one kernel), 0 = staging copies");
     slot = &g_halo_pull;
+  } else if (!std::strcmp(key, "halo_direct")) {
+    CHECK_ARG(value == 0 || value == 1,
+              "halo_direct: 1 = mul! over parts sharing a stream pair reads the ghosts straight from the owners' x "
+              "on the compute stream (default), 0 = pack + pull on the comm stream");
+    slot = &g_halo_direct;
   } else if (!std::strcmp(key, "halo_transport")) {
     CHECK_ARG(value == 0 || value == 1,
               "halo_transport: 0 = parts of this process by device reads/copies, 1 = RCCL send/recv for every part "
@@ -862,6 +931,7 @@ int pa_ctx_destroy(pa_ctx* c) {
   dev_free(c->d_result);
   dev_free(c->d_gather);
   dev_free(c->d_ticket);
+  for (auto& b : c->bases_cache) dev_free(b.second);
   if (c->h_pinned) (void)hipHostFree(c->h_pinned);
   for (auto& e : c->tev) (void)hipEventDestroy(e);
   for (auto& e : c->span_ev)
@@ -1163,6 +1233,7 @@ int pa_xchg_create(pa_ctx* c, int32_t n_rcv, const int32_t* parts_rcv, const int
   X->n_rcv_data = (int64_t)hr.size();
   X->n_snd_data = (int64_t)hs.size();
   if (dev_upload(&X->d_lids_rcv, hr) || dev_upload(&X->d_lids_snd, hs)) { delete X; return -1; }
+  X->h_lids_snd = hs;
   if (X->n_rcv_data) HIPC(hipMalloc(&X->d_buf_rcv, X->n_rcv_data * 16));
   if (X->n_snd_data) HIPC(hipMalloc(&X->d_buf_snd, X->n_snd_data * 16));
   if (build_plan(hr, &X->plan_fwd) || build_plan(hs, &X->plan_rev)) { delete X; return -1; }
@@ -1179,10 +1250,10 @@ int pa_xchg_destroy(pa_xchg* X) {
   dev_free(X->d_buf_snd);
   free_plan(X->plan_fwd);
   free_plan(X->plan_rev);
-  for (auto& t : X->pull) {
-    dev_free(t.d_bid);
-    dev_free(t.d_elem);
-    dev_free(t.d_bases);
+  for (pa_pull* t : {&X->pull[0], &X->pull[1], &X->direct}) {
+    dev_free(t->d_bid);
+    dev_free(t->d_elem);
+    dev_free(t->d_bases);
   }
   delete X;
   return 0;
@@ -2108,22 +2179,37 @@ constexpr int kMaxTimed = 1024;  // mul! calls recorded per context between read
 // The grouped path applies when every part of the call shares one stream
 // pair (pa_ctx_create_shared: same device, one in-order chain) and every
 // halo neighbour is a part of this call served by the pull-unpack.
-static bool group_ok(int n, pa_mat* const A[], pa_xchg* const xg[], bool any_x, int dt) {
-  if (!g_spmv_group || n < 2) return false;
+// Returns 0 (per-part launches), 1 (grouped: pack + pull on the comm
+// stream, overlapped with the interior slices) or 2 (grouped, direct pull:
+// the ghosts read straight from the owners' x on the compute stream, one
+// in-order chain without cross-stream events, pa_tune("halo_direct")).
+static int group_ok(int n, pa_mat* const A[], pa_xchg* const xg[], bool any_x, int dt) {
+  if (!g_spmv_group || n < 2) return 0;
   const pa_ctx* c0 = A[0]->ctx;
   for (int i = 0; i < n; ++i)
-    if (A[i]->ctx->s_main != c0->s_main || A[i]->ctx->s_comm != c0->s_comm) return false;
-  if (!any_x) return true;
-  if (!g_halo_pull) return false;
+    if (A[i]->ctx->s_main != c0->s_main || A[i]->ctx->s_comm != c0->s_comm) return 0;
+  if (!any_x) return 1;
+  if (!g_halo_pull) return 0;
   LocalSet L = local_set(n, xg);
-  for (int i = 0; i < n; ++i) {
+  for (int i = 0; i < n; ++i)
     for (const auto* lst : {&xg[i]->parts_snd, &xg[i]->parts_rcv})
       for (int32_t q : *lst)
-        if (L.find(q) < 0) return false;
-    if (build_pull(i, n, xg, L, dt, 0)) return false;
-    if (!xg[i]->pull[0].ok || !xg[i]->plan_fwd.unique) return false;
+        if (L.find(q) < 0) return 0;
+  for (int i = 0; i < n; ++i)
+    if (!xg[i]->plan_fwd.unique) return 0;
+  if (g_halo_direct) {
+    bool ok = true;
+    for (int i = 0; i < n && ok; ++i) {
+      if (build_direct(i, n, xg, L)) return 0;
+      ok = xg[i]->direct.ok;
+    }
+    if (ok) return 2;
   }
-  return true;
+  for (int i = 0; i < n; ++i) {
+    if (build_pull(i, n, xg, L, dt, 0)) return 0;
+    if (!xg[i]->pull[0].ok) return 0;
+  }
+  return 1;
 }
 
 // mul! over parts sharing a stream pair: one pack, one pull-unpack and one
@@ -2133,7 +2219,7 @@ static bool group_ok(int n, pa_mat* const A[], pa_xchg* const xg[], bool any_x, 
 static int spmv_grouped(int n, pa_mat* const A[], pa_vec* const y[], const pa_index* const y_idx[],
                         pa_vec* const x[], pa_xchg* const xg[], bool any_x, bool has_alpha, int bmode,
                         const void* alpha, const void* beta, const std::vector<void*>& dotp, bool want_dot,
-                        CGState* const* dot_tail, const std::vector<hipEvent_t*>& tslot, int dt) {
+                        CGState* const* dot_tail, const std::vector<hipEvent_t*>& tslot, int dt, bool direct) {
   pa_ctx* c0 = A[0]->ctx;
   HIPC(hipSetDevice(c0->device));
   const hipStream_t sm = SM(c0), sc = SC(c0);
@@ -2142,7 +2228,27 @@ static int spmv_grouped(int n, pa_mat* const A[], pa_vec* const y[], const pa_in
       if (tslot[i]) HIPC(hipEventRecord(tslot[i][k], sm));
     return 0;
   };
-  if (any_x) {
+  if (any_x && direct) {
+    // every ghost of x straight from its owner's x, in stream order before
+    // the slices (owned values are only read, ghosts only written)
+    void** bases = direct_bases(c0, n, x);
+    if (!bases) return -1;
+    PullGroup qg{};
+    for (int i0 = 0; i0 < n; i0 += PA_GROUP_MAX) {
+      qg.np = 0;
+      for (int i = i0; i < n && i < i0 + PA_GROUP_MAX; ++i) {
+        pa_xchg* X = xg[i];
+        const int k = qg.np++;
+        qg.n[k] = X->n_rcv_data;
+        qg.lids[k] = X->d_lids_rcv;
+        qg.bid[k] = X->direct.d_bid;
+        qg.elem[k] = X->direct.d_elem;
+        qg.bases[k] = (const void* const*)bases;
+        qg.v[k] = x[i]->d;
+      }
+      launch_pull_group(dt, qg, sm);
+    }
+  } else if (any_x) {
     // the previous exchange's pulls read the send buffers: pack after them
     if (!g_capturing) HIPC(hipStreamWaitEvent(c0->s_main, c0->ev_recvd, 0));
     PackGroup pg{};
@@ -2204,7 +2310,7 @@ static int spmv_grouped(int n, pa_mat* const A[], pa_vec* const y[], const pa_in
   launch_all(3, P3);
   launch_all(1, P1);
   if (mark(1)) return -1;
-  if (any_x) EV(hipStreamWaitEvent(sm, c0->ev_recvd, 0));
+  if (any_x && !direct) EV(hipStreamWaitEvent(sm, c0->ev_recvd, 0));
   if (mark(2)) return -1;
   P0.clear(); P1.clear(); P3.clear();
   std::vector<SpmvPart> P2;
@@ -2280,7 +2386,8 @@ static int spmv_impl(int n, pa_mat* const A[], pa_vec* const y[], const pa_index
   // timing: the events of this call (slot tn of each timed context); the
   // grouped path brackets all parts with the same launches: part 1 of the
   // call records them once
-  const bool grouped = group_ok(n, A, xg, any_x, dt);
+  const int gmode = group_ok(n, A, xg, any_x, dt);
+  const bool grouped = gmode != 0;
   std::vector<hipEvent_t*> tslot(n, nullptr);
   for (int i = 0; i < n; ++i) {
     pa_ctx* c = A[i]->ctx;
@@ -2302,7 +2409,7 @@ static int spmv_impl(int n, pa_mat* const A[], pa_vec* const y[], const pa_index
         if (check_lids(xg[i], x[i])) return -1;
       }
     return spmv_grouped(n, A, y, y_idx, x, xg, any_x, has_alpha, bmode, alpha, beta, dotp, want_dot, dot_tail,
-                        tslot, dt);
+                        tslot, dt, gmode == 2);
   }
 
   if (any_x) {
@@ -2429,6 +2536,11 @@ int pa_spmv_graph_create(int n, pa_mat* const A[], pa_vec* const y[], const pa_i
     LocalSet L = local_set(n, xg);
     for (int i = 0; i < n; ++i)
       if (build_pull(i, n, xg, L, A[0]->dtype, 0)) return -1;
+    if (g_halo_direct) {
+      for (int i = 0; i < n; ++i)
+        if (build_direct(i, n, xg, L)) return -1;
+      if (!direct_bases(A[0]->ctx, n, x)) return -1;
+    }
   }
   HIPC(hipSetDevice(dev));
   for (pa_ctx* c : ctxs) {

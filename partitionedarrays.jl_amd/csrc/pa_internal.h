@@ -294,6 +294,9 @@ struct pa_ctx {
   // events for the exchange pipeline
   hipEvent_t ev_packed = nullptr;
   hipEvent_t ev_recvd = nullptr;
+  // device arrays of the x pointers of grouped mul! calls led by this part
+  // (the direct pull's bases), most recent first
+  std::vector<std::pair<std::vector<void*>, void**>> bases_cache;
 };
 
 struct pa_index {
@@ -337,6 +340,11 @@ struct pa_pull {
 struct pa_xchg {
   pa_ctx* ctx = nullptr;
   pa_pull pull[2];                             // [0] forward, [1] reverse
+  // direct pull of mul! over parts sharing one stream pair (spmv_grouped):
+  // receive slot p reads x of the call's part bid[p] at lid elem[p] (the
+  // sender's lids_snd entry), no pack, no send buffer, no cross-stream event
+  pa_pull direct;
+  std::vector<int32_t> h_lids_snd;             // 0-based host copy (vector exchangers)
   std::vector<int32_t> parts_rcv, parts_snd;   // 1-based
   std::vector<int64_t> ptrs_rcv, ptrs_snd;     // 0-based offsets, size n+1
   int64_t n_rcv_data = 0, n_snd_data = 0;

@@ -32,7 +32,11 @@ ap.add_argument("--own-streams", action="store_true", help="a stream pair per pa
 ap.add_argument("--group", type=int, default=1, help="pa_tune spmv_group: 1 grouped launches (default), 0 per part")
 ap.add_argument("--graph", action="store_true", help="also time the HIP-graph replay (pamd.SpMVGraph)")
 ap.add_argument("--rccl", action="store_true", help="halo over RCCL grouped send/recv (HIPBackend(rccl=True))")
+ap.add_argument("--tune", default="", help="extra pa_tune knobs, key=value[,key=value]")
 a = ap.parse_args()
+for kv in filter(None, a.tune.split(",")):
+    k, v = kv.split("=")
+    pamd._lib.tune(k, int(v))
 DT = {"f64": np.float64, "f32": np.float32, "c128": np.complex128, "c64": np.complex64}
 be = pamd.HIPBackend(devices=[0], share_streams=not a.own_streams, rccl=a.rccl)
 pamd._lib.tune("spmv_group", a.group)
@@ -107,7 +111,7 @@ for name, npat, rule in [(d, int(q), int(r)) for d in a.dtypes.split(",") for q 
             own = A.rows.partition.local(p).oid_to_lid - 1
             assert np.array_equal(got.local(p)[own], ref.local(p)[own]), "graph replay differs from eager mul!"
         del g
-    print(json.dumps({"config": f"C5 FE27 {a.n}^3 Voronoi {a.parts} parts on 1 GPU", "dtype": name, "halo": "rccl" if a.rccl else "device reads",
+    print(json.dumps({"config": f"C5 FE27 {a.n}^3 Voronoi {a.parts} parts on 1 GPU", "dtype": name, "halo": "rccl" if a.rccl else "device reads", "tune": a.tune,
                       "spmv_patterns": npat, "spmv_pattern_rule": rule, "share_streams": not a.own_streams,
                       "spmv_group": a.group, "format_gbs_all_parts": round(info["format_bytes"] / t / 1e9, 1),
                       "format_gbs_kernels": round(info["format_bytes"] / km / 1e6, 1),
