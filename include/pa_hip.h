@@ -70,6 +70,8 @@ int pa_device_count(int* count);
  *               0: lane-strided partial sums + tree (within 1e-12);
  * "halo_pull"   1: parts of one process read their neighbours' packed
  *               buffers directly (default), 0: staging copies;
+ * "spmv_delta16" 1: int32-column slices whose columns fit 16-bit codes
+ *               store those (matrices built afterwards; default), 0: off;
  * "halo_direct" 1: mul! over parts sharing a stream pair reads every ghost
  *               straight from its owner's x on the compute stream (no
  *               pack, no cross-stream event; default), 0: pack + pull on
@@ -284,6 +286,11 @@ int pa_mat_format_info(const pa_mat* A, int64_t* pattern_slices,
  * consecutive rows are shorter than a slice); 0 unless
  * pa_tune("spmv_patterns", n > 1) preceded the build.                     */
 int pa_mat_multipattern_info(const pa_mat* A, int64_t* multi_slices);
+/* delta16 slices (pa_tune "spmv_delta16", default on): int32-column slices
+ * whose columns all fit 16-bit codes — an owned column as the row + a
+ * signed 15-bit delta, a ghost column as the slice's smallest ghost column
+ * + 15 bits — stream 2 B of column id per slot instead of 4.              */
+int pa_mat_delta16_info(const pa_mat* A, int64_t* delta16_slices);
 
 /* Bytes one mul! streams from this matrix in its current encoding
  * (pa_tune("spmv_format")), as its kernels load them: values (padding

@@ -27,6 +27,7 @@ void set_error(const std::string& msg) { g_err = msg; }
 void launch_spmv_part(int which, int64_t nwork, const int32_t* list, const pa_mat* A, const void* x,
                       void* y, const int32_t* ymap, bool has_alpha, int bmode, const void* alpha,
                       const void* beta, void* dotp, hipStream_t st);
+void launch_delta16(pa_mat* A, int64_t noids, const int32_t* kind, int32_t* ok, hipStream_t st);
 void launch_pattern_detect(pa_mat* A, int64_t noids, int32_t* kind, int32_t* plen, int32_t* pat,
                            uint64_t* mask, int32_t* pghost, int32_t* nirreg, int NP, int rule, hipStream_t st);
 void launch_side_len(pa_mat* A, int64_t n, const int32_t* rows, int32_t* len, int64_t noids,
@@ -48,6 +49,7 @@ extern int g_spmv_pattern_rule;
 extern int g_spmv_patterns;  // patterns per slice at build time (1: single-pattern slices only)
 int g_halo_pull = 1;  // pa_tune("halo_pull"): pull-unpack between parts of one process
 int g_spmv_group = 1; // pa_tune("spmv_group"): one launch per phase for the parts sharing a stream pair
+int g_spmv_delta16 = 1;   // pa_tune("spmv_delta16"): int32-column slices with 16-bit column codes where they fit
 int g_halo_direct = 1;     // pa_tune("halo_direct"): grouped mul! pulls ghosts straight from the owners' x
 int g_halo_transport = 0;  // pa_tune("halo_transport"): 0 parts of this process by device reads, 1 RCCL for all
 int g_comm_cus = 0;   // pa_tune("comm_cus"): CUs reserved for the comm stream (0: priority stream instead)
@@ -318,12 +320,34 @@ int finalize_pattern(pa_mat* A, int kmax, int64_t noids) {
   HIPC(hipStreamSynchronize(st));
   dev_free(d_pghost);
   dev_free(d_nirreg);
-  std::vector<int32_t> pint, pbnd, xint, xbnd, mint, mbnd, side;
+  if (g_spmv_delta16) {  // int32-column slices whose columns fit 16-bit codes (kind 3)
+    int32_t* d_ok = nullptr;
+    HIPC(hipMalloc((void**)&A->d_col16, std::max<int64_t>(A->slots, 1) * 2));
+    HIPC(hipMalloc((void**)&A->d_gbase, ns * 4));
+    HIPC(hipMalloc((void**)&d_ok, ns * 4));
+    launch_delta16(A, noids, A->d_kind, d_ok, st);
+    HIPC(hipGetLastError());
+    std::vector<int32_t> ok(ns);
+    HIPC(hipMemcpyAsync(ok.data(), d_ok, ns * 4, hipMemcpyDeviceToHost, st));
+    HIPC(hipStreamSynchronize(st));
+    dev_free(d_ok);
+    int64_t nd = 0;
+    for (int64_t s = 0; s < ns; ++s)
+      if (ok[s]) { kind[s] = 3; ++nd; }
+    if (nd == 0) {
+      dev_free(A->d_col16);
+      dev_free(A->d_gbase);
+      A->d_col16 = nullptr;
+      A->d_gbase = nullptr;
+    }
+  }
+  std::vector<int32_t> pint, pbnd, xint, xbnd, mint, mbnd, dint, dbnd, side;
   for (int64_t s = 0; s < ns; ++s) {
     if (kind[s] == 1) (pghost[s] ? pbnd : pint).push_back((int32_t)s);
     else if (kind[s] == 2) (pghost[s] ? mbnd : mint).push_back((int32_t)s);
+    else if (kind[s] == 3) (pghost[s] ? dbnd : dint).push_back((int32_t)s);
     else (pghost[s] ? xbnd : xint).push_back((int32_t)s);
-    if (kind[s]) {
+    if (kind[s] == 1 || kind[s] == 2) {
       ++A->npattern_slices;
       const int64_t nvalid = std::min<int64_t>(A->H, A->nrows - s * A->H);
       for (int64_t i = 0; i < nvalid; ++i) {
@@ -333,10 +357,11 @@ int finalize_pattern(pa_mat* A, int kmax, int64_t noids) {
     }
   }
   A->h_kind = kind;
-  A->maxlen_pat = A->maxlen_pm_int = 0;
+  A->maxlen_pat = A->maxlen_pm_int = A->maxlen_d16 = 0;
   for (int64_t s = 0; s < ns; ++s) {
     if (kind[s] == 1) A->maxlen_pat = std::max(A->maxlen_pat, (int)A->h_plen[s]);
     else if (kind[s] == 0) A->maxlen_pm_int = std::max(A->maxlen_pm_int, (int)A->h_slen[s]);
+    else if (kind[s] == 3) A->maxlen_d16 = std::max(A->maxlen_d16, (int)A->h_slen[s]);
   }
   A->np_int = (int64_t)pint.size();
   A->np_bnd = (int64_t)pbnd.size();
@@ -344,9 +369,12 @@ int finalize_pattern(pa_mat* A, int kmax, int64_t noids) {
   A->nx_bnd = (int64_t)xbnd.size();
   A->nm_int = (int64_t)mint.size();
   A->nm_bnd = (int64_t)mbnd.size();
+  A->nd_int = (int64_t)dint.size();
+  A->nd_bnd = (int64_t)dbnd.size();
   if (dev_upload(&A->d_pint_list, pint) || dev_upload(&A->d_pbnd_list, pbnd) ||
       dev_upload(&A->d_xint_list, xint) || dev_upload(&A->d_xbnd_list, xbnd) ||
-      dev_upload(&A->d_mint_list, mint) || dev_upload(&A->d_mbnd_list, mbnd))
+      dev_upload(&A->d_mint_list, mint) || dev_upload(&A->d_mbnd_list, mbnd) ||
+      dev_upload(&A->d_dint_list, dint) || dev_upload(&A->d_dbnd_list, dbnd))
     return -1;
   if (mint.empty() && mbnd.empty()) {  // no slice took several patterns
     dev_free(A->d_mpat);
@@ -763,6 +791,11 @@ int pa_tune(const char* key, int value, int* previous) {
   } else if (!std::strcmp(key, "halo_pull")) {
     CHECK_ARG(value == 0 || value == 1, "halo_pull: 1 = receivers read the senders' buffers (one kernel), 0 = staging copies");
     slot = &g_halo_pull;
+  } else if (!std::strcmp(key, "spmv_delta16")) {
+    CHECK_ARG(value == 0 || value == 1,
+              "spmv_delta16: 1 = int32-column slices whose columns fit 16-bit codes store those (matrices built "
+              "afterwards; default), 0 = int32 column ids");
+    slot = &g_spmv_delta16;
   } else if (!std::strcmp(key, "halo_direct")) {
     CHECK_ARG(value == 0 || value == 1,
               "halo_direct: 1 = mul! over parts sharing a stream pair reads the ghosts straight from the owners' x "
@@ -2093,7 +2126,8 @@ int pa_mat_destroy(pa_mat* A) {
                   (void*)A->d_xbnd_list, (void*)A->d_s_off, (void*)A->d_s_len,
                   (void*)A->d_s_col, A->d_s_val, (void*)A->d_s_rowmap, (void*)A->d_s_rowlen, A->d_dotp,
                   (void*)A->d_long_row, (void*)A->d_long_ptr, (void*)A->d_long_col, (void*)A->d_sflags,
-                  (void*)A->d_lmask, (void*)A->d_lchunk_start, (void*)A->d_lrow_chunk, A->d_lpart})
+                  (void*)A->d_lmask, (void*)A->d_lchunk_start, (void*)A->d_lrow_chunk, A->d_lpart,
+                  (void*)A->d_col16, (void*)A->d_gbase, (void*)A->d_dint_list, (void*)A->d_dbnd_list})
     dev_free(p);
   delete A;
   return 0;
@@ -2112,6 +2146,12 @@ int pa_mat_format_info(const pa_mat* A, int64_t* pattern_slices, int64_t* regula
 int pa_mat_multipattern_info(const pa_mat* A, int64_t* multi_slices) {
   CHECK_ARG(A, "null matrix");
   if (multi_slices) *multi_slices = A->nm_int + A->nm_bnd;
+  return 0;
+}
+
+int pa_mat_delta16_info(const pa_mat* A, int64_t* delta16_slices) {
+  CHECK_ARG(A, "null matrix");
+  if (delta16_slices) *delta16_slices = A->nd_int + A->nd_bnd;
   return 0;
 }
 
@@ -2139,6 +2179,10 @@ int pa_mat_traffic(const pa_mat* A, int64_t* value_bytes, int64_t* index_bytes, 
     } else if (kd == 2) {
       v += (int64_t)A->h_plen[s] * H * S;
       m += (int64_t)PA_MP_NP * A->kmp * 4 + 64 + W * 8 + 8 + 4 + 4;
+    } else if (kd == 3) {
+      v += (int64_t)A->h_slen[s] * H * S;
+      ix += (int64_t)A->h_slen[s] * H * 2;
+      m += 8 + 4 + 4 + 4;  // offset, length, list entry, ghost base
     } else {
       v += (int64_t)A->h_slen[s] * H * S;
       ix += (int64_t)A->h_slen[s] * H * 4;
@@ -2285,7 +2329,7 @@ static int spmv_grouped(int n, pa_mat* const A[], pa_vec* const y[], const pa_in
     EV(hipEventRecord(c0->ev_recvd, sc));
   }
   HIPC(hipGetLastError());
-  std::vector<SpmvPart> P0, P1, P3;
+  std::vector<SpmvPart> P0, P1, P3, P4;
   auto part = [&](int i, int64_t nwork, const int32_t* list) {
     const int32_t* ymap = y_idx[i]->own_contig ? nullptr : y_idx[i]->d_oid_to_lid;
     return SpmvPart{nwork, list, A[i], x[i]->d, y[i]->d, ymap, dotp[i]};
@@ -2300,6 +2344,7 @@ static int spmv_grouped(int n, pa_mat* const A[], pa_vec* const y[], const pa_in
       P0.push_back(part(i, A[i]->np_int, A[i]->d_pint_list));
       P3.push_back(part(i, A[i]->nm_int, A[i]->d_mint_list));
       P1.push_back(part(i, A[i]->nx_int, A[i]->d_xint_list));
+      P4.push_back(part(i, A[i]->nd_int, A[i]->d_dint_list));
     } else if (A[i]->d_bnd_list) {
       P1.push_back(part(i, A[i]->nslices_int, A[i]->d_int_list));
     } else {
@@ -2308,16 +2353,18 @@ static int spmv_grouped(int n, pa_mat* const A[], pa_vec* const y[], const pa_in
   }
   launch_all(0, P0);
   launch_all(3, P3);
+  launch_all(4, P4);
   launch_all(1, P1);
   if (mark(1)) return -1;
   if (any_x && !direct) EV(hipStreamWaitEvent(sm, c0->ev_recvd, 0));
   if (mark(2)) return -1;
-  P0.clear(); P1.clear(); P3.clear();
+  P0.clear(); P1.clear(); P3.clear(); P4.clear();
   std::vector<SpmvPart> P2;
   for (int i = 0; i < n; ++i) {
     if (g_spmv_format == 1 && A[i]->has_pat) {
       P0.push_back(part(i, A[i]->np_bnd, A[i]->d_pbnd_list));
       P3.push_back(part(i, A[i]->nm_bnd, A[i]->d_mbnd_list));
+      P4.push_back(part(i, A[i]->nd_bnd, A[i]->d_dbnd_list));
       P1.push_back(part(i, A[i]->nx_bnd, A[i]->d_xbnd_list));
       P2.push_back(part(i, A[i]->s_nslices, nullptr));
     } else if (A[i]->d_bnd_list) {
@@ -2326,6 +2373,7 @@ static int spmv_grouped(int n, pa_mat* const A[], pa_vec* const y[], const pa_in
   }
   launch_all(0, P0);
   launch_all(3, P3);
+  launch_all(4, P4);
   launch_all(1, P1);
   launch_all(2, P2);
   for (int i = 0; i < n; ++i) {
@@ -2435,6 +2483,7 @@ static int spmv_impl(int n, pa_mat* const A[], pa_vec* const y[], const pa_index
     if (g_spmv_format == 1 && A[i]->has_pat) {
       launch_spmv_part(0, A[i]->np_int, A[i]->d_pint_list, A[i], x[i]->d, y[i]->d, ymap, has_alpha, bmode, alpha, beta, dotp[i], SM(c));
       launch_spmv_part(3, A[i]->nm_int, A[i]->d_mint_list, A[i], x[i]->d, y[i]->d, ymap, has_alpha, bmode, alpha, beta, dotp[i], SM(c));
+      launch_spmv_part(4, A[i]->nd_int, A[i]->d_dint_list, A[i], x[i]->d, y[i]->d, ymap, has_alpha, bmode, alpha, beta, dotp[i], SM(c));
       launch_spmv_part(1, A[i]->nx_int, A[i]->d_xint_list, A[i], x[i]->d, y[i]->d, ymap, has_alpha, bmode, alpha, beta, dotp[i], SM(c));
     } else if (A[i]->d_bnd_list) {  // split layout (the interior list may be empty)
       if (A[i]->nslices_int > 0)
@@ -2460,6 +2509,7 @@ static int spmv_impl(int n, pa_mat* const A[], pa_vec* const y[], const pa_index
       // pattern slices reading ghosts, then the side rows (after the halo)
       launch_spmv_part(0, A[i]->np_bnd, A[i]->d_pbnd_list, A[i], x[i]->d, y[i]->d, ymap, has_alpha, bmode, alpha, beta, dotp[i], SM(c));
       launch_spmv_part(3, A[i]->nm_bnd, A[i]->d_mbnd_list, A[i], x[i]->d, y[i]->d, ymap, has_alpha, bmode, alpha, beta, dotp[i], SM(c));
+      launch_spmv_part(4, A[i]->nd_bnd, A[i]->d_dbnd_list, A[i], x[i]->d, y[i]->d, ymap, has_alpha, bmode, alpha, beta, dotp[i], SM(c));
       launch_spmv_part(1, A[i]->nx_bnd, A[i]->d_xbnd_list, A[i], x[i]->d, y[i]->d, ymap, has_alpha, bmode, alpha, beta, dotp[i], SM(c));
       launch_spmv_part(2, A[i]->s_nslices, nullptr, A[i], x[i]->d, y[i]->d, ymap, has_alpha, bmode, alpha, beta, dotp[i], SM(c));
     } else if (A[i]->d_bnd_list) {

@@ -454,6 +454,16 @@ struct pa_mat {
   int32_t* d_mpat = nullptr;         // nslices*PA_MP_NP*kmp offsets
   uint8_t* d_psel = nullptr;         // nslices*64 pattern index per lane
   int kmp = 0;                       // pattern stride (<= PA_MP_K)
+  // delta16 slices (kind 3): int32-column slices whose columns all fit a
+  // 16-bit code (pa_tune "spmv_delta16"): an owned column c of row r as
+  // c - r in 15 signed bits, a ghost column as the slice's ghost base +
+  // 15 unsigned bits (bit 15 set), 0xFFFF padding — 2 B per slot instead of 4
+  uint16_t* d_col16 = nullptr;       // slots (codes of the delta16 slices)
+  int32_t* d_gbase = nullptr;        // per slice: smallest ghost column
+  int32_t* d_dint_list = nullptr;    // delta16 slices without ghost columns
+  int32_t* d_dbnd_list = nullptr;    // delta16 slices with ghost columns
+  int64_t nd_int = 0, nd_bnd = 0;
+  int maxlen_d16 = INT32_MAX;
   int32_t* d_mint_list = nullptr;    // multi-pattern slices without ghost reads
   int32_t* d_mbnd_list = nullptr;    // multi-pattern slices reading ghosts
   int64_t nm_int = 0, nm_bnd = 0;

@@ -29,6 +29,10 @@ template <int R>
 struct alignas(4 * R) IPack {
   int32_t c[R];
 };
+template <int R>
+struct alignas(2 * R) S16Pack {
+  uint16_t c[R];
+};
 
 // XCD-aware block remap (cdna_hip_programming.md §5.5 T1, bijective variant).
 __device__ inline int64_t xcd_remap(int64_t b, int64_t G) {
@@ -60,6 +64,7 @@ int g_spmv_patterns = 1;         // patterns per slice (multi-pattern slices whe
 int g_spmv_pattern_rule = 0;     // 1: slice encoding by streamed bytes, 0: pattern slice when half the rows follow it
 
 template <int BYTES> struct RawOf;
+template <> struct RawOf<2> { typedef unsigned short type; };
 template <> struct RawOf<4> { typedef unsigned int type; };
 template <> struct RawOf<8> { typedef unsigned int type __attribute__((ext_vector_type(2))); };
 template <> struct RawOf<16> { typedef unsigned int type __attribute__((ext_vector_type(4))); };
@@ -104,6 +109,9 @@ struct SpmvArgs {
   const int32_t* sflags;
   const uint64_t* lmask;
   int maxlen;               // longest row (entries) of the launch's slices: <= U selects the SH kernels
+  // delta16 slices: 16-bit column codes and the per-slice ghost base
+  const uint16_t* col16;
+  const int32_t* gbase;
 };
 
 template <typename T> struct DAcc { using type = double; };
@@ -197,6 +205,92 @@ __device__ __forceinline__ void rows_int32(T (&acc)[R], const IPack<R>* __restri
 #pragma unroll
     for (int r = 0; r < R; ++r) {
       const int32_t cc = c.c[r];
+      T xx = x[cc >= 0 ? cc : 0];
+      if (ALPHA) xx = xx * alpha;
+      const T t = acc[r] + v.v[r] * xx;
+      acc[r] = pick(cc >= 0, t, acc[r]);
+    }
+  }
+}
+
+// delta16 code → x lid (-1: padding): bit 15 clear = owned column, row +
+// the signed 15-bit delta; set = ghost column, the slice's ghost base + the
+// 15-bit offset; 0xFFFF = padding
+__device__ __forceinline__ int32_t d16_col(uint32_t q, int32_t row, int32_t gb) {
+  if (q == 0xFFFFu) return -1;
+  return (q & 0x8000u) ? gb + (int32_t)(q & 0x7FFFu) : row + (((int32_t)(q << 17)) >> 17);
+}
+
+// delta16 rows: rows_int32 with the column ids decoded from 2 B codes
+template <typename T, int R, bool ALPHA, bool NT, int U, bool SH = false>
+__device__ __forceinline__ void rows_d16(T (&acc)[R], const S16Pack<R>* __restrict__ cp,
+                                         const Pack<T, R>* __restrict__ vp, int len,
+                                         const T* __restrict__ x, T alpha, bool TB, int32_t row0, int32_t gb) {
+  int k = 0;
+  if (SH) TB = true;
+  for (; !SH && k + U <= len; k += U) {
+    S16Pack<R> q[U];
+    Pack<T, R> v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) q[u] = ld<NT>(&cp[(k + u) * 64]);
+#pragma unroll
+    for (int u = 0; u < U; ++u) v[u] = ld<NT>(&vp[(k + u) * 64]);
+    int32_t c[U][R];
+    T xv[U][R];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        c[u][r] = d16_col(q[u].c[r], row0 + r, gb);
+        xv[u][r] = x[c[u][r] >= 0 ? c[u][r] : 0];
+      }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        T xx = xv[u][r];
+        if (ALPHA) xx = xx * alpha;
+        const T t = acc[r] + v[u].v[r] * xx;
+        acc[r] = pick(c[u][r] >= 0, t, acc[r]);
+      }
+  }
+  if (TB && k < len) {  // the last len % U entries as one masked batch
+    S16Pack<R> q[U];
+    Pack<T, R> v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (k + u < len) q[u] = ld<NT>(&cp[(k + u) * 64]);
+      else for (int r = 0; r < R; ++r) q[u].c[r] = 0xFFFFu;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (k + u < len) v[u] = ld<NT>(&vp[(k + u) * 64]);
+    int32_t c[U][R];
+    T xv[U][R];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        c[u][r] = d16_col(q[u].c[r], row0 + r, gb);
+        if (k + u < len) xv[u][r] = x[c[u][r] >= 0 ? c[u][r] : 0];
+      }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        T xx = xv[u][r];
+        if (ALPHA) xx = xx * alpha;
+        const T t = acc[r] + v[u].v[r] * xx;
+        acc[r] = pick(k + u < len && c[u][r] >= 0, t, acc[r]);
+      }
+    k = len;
+  }
+  for (; !SH && k < len; ++k) {
+    const S16Pack<R> q = ld<NT>(&cp[k * 64]);
+    const Pack<T, R> v = ld<NT>(&vp[k * 64]);
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const int32_t cc = d16_col(q.c[r], row0 + r, gb);
       T xx = x[cc >= 0 ? cc : 0];
       if (ALPHA) xx = xx * alpha;
       const T t = acc[r] + v.v[r] * xx;
@@ -316,8 +410,9 @@ __device__ __forceinline__ void rows_pattern(T (&acc)[R], const int32_t* __restr
 // BMODE: 0 → acc = 0 (β == 0: fill!(co,0)), 1 → acc = y (β == 1),
 //        2 → acc = y*β (rmul!(co,β)).  Interfaces.jl:2262-2263.
 // PK: the launch's slices are int32-column slices (0), pattern slices (1:
-// implied columns for the rows of their mask) or multi-pattern slices (2:
-// the same with one of PA_MP_NP patterns per lane, staged in LDS); one
+// implied columns for the rows of their mask), multi-pattern slices (2:
+// the same with one of PA_MP_NP patterns per lane, staged in LDS) or
+// delta16 slices (3: 2 B column codes decoded against the row); one
 // kernel per kind keeps the hot loop free of the others' code and registers.
 // One wave computes work item w (slice a.list[w], or w) of the structure a.
 // SH: every row of the launch has at most U entries (FD7: 7) — the masked
@@ -389,6 +484,11 @@ __device__ __forceinline__ void spmv_wave(const SpmvArgs<T>& a, const int64_t w)
       if (a.flags & SPMV_NT) rows_pattern<T, R, ALPHA, true, U, false, SH>(acc, pat, vp, len, a.x, row0, ok, a.alpha, tb);
       else rows_pattern<T, R, ALPHA, false, U, false, SH>(acc, pat, vp, len, a.x, row0, ok, a.alpha, tb);
     }
+  } else if constexpr (PK == 3) {
+    const S16Pack<R>* __restrict__ cp = reinterpret_cast<const S16Pack<R>*>(a.col16 + off) + lane;
+    const int32_t gb = a.gbase[s];
+    if (a.flags & SPMV_NT) rows_d16<T, R, ALPHA, true, U, SH>(acc, cp, vp, len, a.x, a.alpha, tb, (int32_t)row0, gb);
+    else rows_d16<T, R, ALPHA, false, U, SH>(acc, cp, vp, len, a.x, a.alpha, tb, (int32_t)row0, gb);
   } else {
     const IPack<R>* __restrict__ cp = reinterpret_cast<const IPack<R>*>(a.col + off) + lane;
     if (a.flags & SPMV_NT) rows_int32<T, R, ALPHA, true, U, SH>(acc, cp, vp, len, a.x, a.alpha, tb);
@@ -516,7 +616,8 @@ static void launch_ab(const SpmvArgs<T>& a, bool has_alpha, int bmode, hipStream
 
 // which = 0: pattern slices of the main structure; 1: int32-column slices
 // of the main structure; 2: side SELL; 3: multi-pattern slices of the main
-// structure.  list/nwork select the slices.
+// structure; 4: delta16 slices of the main structure.  list/nwork select the
+// slices.
 template <typename T>
 static SpmvArgs<T> make_args(int which, int64_t nwork, const int32_t* list, const pa_mat* A, const void* x,
                              void* y, const int32_t* ymap, const void* alpha, const void* beta, void* dotp) {
@@ -535,6 +636,7 @@ static SpmvArgs<T> make_args(int which, int64_t nwork, const int32_t* list, cons
   a.maxlen = which == 0   ? A->maxlen_pat
              : which == 2 ? A->maxlen_side
              : which == 1 ? ((g_spmv_format == 1 && A->has_pat) ? A->maxlen_pm_int : A->maxlen_all)
+             : which == 4 ? A->maxlen_d16
                           : INT32_MAX;
   if (which == 2) {
     a.soff = A->d_s_off;
@@ -561,6 +663,10 @@ static SpmvArgs<T> make_args(int which, int64_t nwork, const int32_t* list, cons
       a.psel = A->d_psel;
     } else {
       a.slen = A->d_slice_len;
+      if (which == 4) {
+        a.col16 = A->d_col16;
+        a.gbase = A->d_gbase;
+      }
     }
   }
   if (which == 1) {
@@ -577,6 +683,7 @@ static void launch_which(int which, int64_t nwork, const int32_t* list, const pa
   const SpmvArgs<T> a = make_args<T>(which, nwork, list, A, x, y, ymap, alpha, beta, dotp);
   if (which == 0) launch_ab<T, R, 1>(a, has_alpha, bmode, st);
   else if (which == 3) launch_ab<T, R, 2>(a, has_alpha, bmode, st);
+  else if (which == 4) launch_ab<T, R, 3>(a, has_alpha, bmode, st);
   else launch_ab<T, R, 0>(a, has_alpha, bmode, st);
 }
 
@@ -589,6 +696,7 @@ static void group_which(int which, int np, const SpmvPart* parts, bool has_alpha
     if (g.np == 0) return;
     if (which == 0) launch_group_ab<T, R, 1>(g, has_alpha, bmode, st);
     else if (which == 3) launch_group_ab<T, R, 2>(g, has_alpha, bmode, st);
+    else if (which == 4) launch_group_ab<T, R, 3>(g, has_alpha, bmode, st);
     else launch_group_ab<T, R, 0>(g, has_alpha, bmode, st);
     g = SpmvGroup<T>{};
   };
@@ -1283,6 +1391,78 @@ __global__ __launch_bounds__(256) void k_pattern_detect(int64_t nrows, int64_t n
   }
   if (psel && mp) psel[s * 64 + lane] = (uint8_t)(best == 2 && sel > 0 ? sel : 0);
   if (best == 1) store_pat(pat + s * kmax, mlane, mr);
+}
+
+// delta16 eligibility and codes, one wave per slice: an int32-column slice
+// (kind 0, no long rows) becomes delta16 when every owned column is within
+// ±16383 of its row and every ghost column within 32766 of the slice's
+// smallest ghost column; its codes are then written to col16 (same slots).
+template <int R>
+__global__ __launch_bounds__(256) void k_delta16(int64_t nslices, const int64_t* __restrict__ soff,
+                                                 const int32_t* __restrict__ slen, const int32_t* __restrict__ col,
+                                                 const int32_t* __restrict__ kind, const int32_t* __restrict__ sflags,
+                                                 int64_t noids, uint16_t* __restrict__ col16,
+                                                 int32_t* __restrict__ gbase, int32_t* __restrict__ ok) {
+  constexpr int H = 64 * R;
+  const int64_t s = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (s >= nslices) return;
+  const int lane = threadIdx.x & 63;
+  if (kind[s] != 0 || (sflags && sflags[s])) {
+    if (lane == 0) { ok[s] = 0; gbase[s] = 0; }
+    return;
+  }
+  const int64_t off = soff[s];
+  const int len = slen[s];
+  const int64_t row0 = s * H + (int64_t)lane * R;
+  int32_t gmin = INT32_MAX;
+  for (int k = 0; k < len; ++k)
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const int32_t c = col[off + ((int64_t)k * 64 + lane) * R + r];
+      if (c >= noids) gmin = min(gmin, c);
+    }
+  for (int d = 32; d >= 1; d >>= 1) gmin = min(gmin, __shfl_xor(gmin, d, 64));
+  bool fit = true;
+  for (int k = 0; k < len; ++k)
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const int32_t c = col[off + ((int64_t)k * 64 + lane) * R + r];
+      if (c < 0) continue;
+      if (c < noids) {
+        const int64_t dlt = (int64_t)c - (row0 + r);
+        fit = fit && dlt >= -16384 && dlt <= 16383;
+      } else {
+        fit = fit && (int64_t)c - gmin <= 32766;
+      }
+    }
+  const bool all = __all(fit);
+  if (lane == 0) { ok[s] = all ? 1 : 0; gbase[s] = gmin == INT32_MAX ? 0 : gmin; }
+  if (!all) return;
+  for (int k = 0; k < len; ++k)
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const int64_t slot = off + ((int64_t)k * 64 + lane) * R + r;
+      const int32_t c = col[slot];
+      uint16_t q;
+      if (c < 0) q = 0xFFFFu;
+      else if (c < noids) q = (uint16_t)((uint32_t)(c - (int32_t)(row0 + r)) & 0x7FFFu);
+      else q = (uint16_t)(0x8000u | (uint32_t)(c - gmin));
+      col16[slot] = q;
+    }
+}
+
+void launch_delta16(pa_mat* A, int64_t noids, const int32_t* kind, int32_t* ok, hipStream_t st) {
+  const int64_t blocks = (A->nslices + 3) / 4;
+  if (blocks == 0) return;
+#define PA_D16(RR)                                                                                          \
+  hipLaunchKernelGGL(k_delta16<RR>, dim3(blocks), dim3(256), 0, st, A->nslices, A->d_slice_off,              \
+                     A->d_slice_len, A->d_col, kind, A->d_sflags, noids, A->d_col16, A->d_gbase, ok)
+  switch (A->R) {
+    case 1: PA_D16(1); break;
+    case 2: PA_D16(2); break;
+    case 4: PA_D16(4); break;
+  }
+#undef PA_D16
 }
 
 void launch_pattern_detect(pa_mat* A, int64_t noids, int32_t* kind, int32_t* plen, int32_t* pat,

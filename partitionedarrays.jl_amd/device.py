@@ -447,6 +447,9 @@ class DeviceMatrix:
         mp = C.c_int64()
         _lib.call("pa_mat_multipattern_info", self.h, C.byref(mp))
         d["multi_pattern_slices"] = mp.value
+        dd = C.c_int64()
+        _lib.call("pa_mat_delta16_info", self.h, C.byref(dd))
+        d["delta16_slices"] = dd.value
         lr = [C.c_int64() for _ in range(2)]
         _lib.call("pa_mat_long_rows", self.h, *[C.byref(x) for x in lr])
         d.update(zip(["long_rows", "long_nnz"], [x.value for x in lr]))

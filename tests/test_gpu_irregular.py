@@ -179,3 +179,35 @@ def test_grouped_launches_equal_per_part(be, pamd, dtype, fmt):
         assert out[0][2] == out[1][2]
     finally:
         pamd._lib.tune("spmv_format", prev)
+
+
+@pytest.mark.parametrize("dtype", [np.float64, np.float32, np.complex128, np.complex64])
+def test_delta16_slices_equal_int32(be, pamd, O, dtype):
+    """C5 Voronoi parts: most int32-column slices become delta16 slices (2 B
+    column codes, pa_tune spmv_delta16); mul! is bit-identical with and
+    without them and equals the oracle."""
+    N, nparts = (40, 36, 32), 8
+    parts = be.get_part_ids(nparts)
+    OA = _oracle(O, N, nparts, dtype)
+    rng = np.random.default_rng(SEED + 11)
+    out = []
+    for d16 in (1, 0):
+        prev = pamd._lib.tune("spmv_delta16", d16)
+        try:
+            A = pamd.drivers.irregular_problem(parts, N, 27, dtype)
+        finally:
+            pamd._lib.tune("spmv_delta16", prev)
+        nd = sum(i["delta16_slices"] for i in A.info().parts)
+        assert (nd > 0) == bool(d16)
+        if d16:
+            xs = {p: _rand(rng, A.cols.partition.local(p).num_lids, dtype) for p in parts.part_ids}
+        x = pamd.PVector.from_host(pamd.map_parts(lambda s: xs[s.part], A.cols.partition), A.cols)
+        y = pamd.PVector.undef(A.rows, dtype)
+        pamd.mul_(y, A, x)
+        out.append(y.to_host())
+    ox = O.PVector(O.map_parts(lambda s: _ox(O, xs[s.part]), OA.cols.partition), OA.cols)
+    oy = O.pvector_undef(OA.rows, dtype)
+    O.mul_(oy, OA, ox)
+    for p in parts.part_ids:
+        assert _eq(O, out[0].local(p), oy.values[p]), f"part {p}: delta16 SpMV differs from the oracle"
+        assert _eq(O, out[1].local(p), oy.values[p]), f"part {p}: int32 SpMV differs from the oracle"
