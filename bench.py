@@ -456,6 +456,7 @@ def main():
             "actual_frac": None if traffic is None else round(traffic / (kernel_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
             "traffic_over_bytes": None if traffic is None else round(traffic / spmv_bytes, 4),
             "column_format": (f"pattern slices {info['pattern_slices']}/{info['nslices']}, "
+                              f"delta16 slices {info.get('delta16_slices', 0)}, "
                               f"regular rows {info['regular_rows']}/{info['nrows']}, side rows {info['side_rows']}"),
             "int32_columns_kernel_ms": round(kernel_ms_int32, 4),
             "int32_columns_achieved": round(bytes_int32 / (kernel_ms_int32 * 1e-3) / 1e9, 1),

@@ -419,7 +419,7 @@ __device__ __forceinline__ void rows_pattern(T (&acc)[R], const int32_t* __restr
 // batch alone, no loop code (fewer registers, more waves per SIMD).
 template <typename T, int R, bool ALPHA, int BMODE, int U, int PK, bool SH = false>
 __device__ __forceinline__ void spmv_wave(const SpmvArgs<T>& a, const int64_t w) {
-  constexpr bool PAT = PK != 0;
+  constexpr bool PAT = PK == 1 || PK == 2;  // implied columns (mask of regular rows)
   constexpr int H = 64 * R;
   const int lane = threadIdx.x & 63;
   const int64_t s = a.list ? (int64_t)a.list[w] : w;
