@@ -50,6 +50,7 @@ extern int g_spmv_patterns;  // patterns per slice at build time (1: single-patt
 int g_halo_pull = 1;  // pa_tune("halo_pull"): pull-unpack between parts of one process
 int g_spmv_group = 1; // pa_tune("spmv_group"): one launch per phase for the parts sharing a stream pair
 int g_spmv_delta16 = 1;   // pa_tune("spmv_delta16"): int32-column slices with 16-bit column codes where they fit
+int g_spmv_merge = 1;     // pa_tune("spmv_merge"): one launch for every slice kind of every part when no halo is in flight
 int g_halo_direct = 1;     // pa_tune("halo_direct"): grouped mul! pulls ghosts straight from the owners' x
 int g_halo_transport = 0;  // pa_tune("halo_transport"): 0 parts of this process by device reads, 1 RCCL for all
 int g_comm_cus = 0;   // pa_tune("comm_cus"): CUs reserved for the comm stream (0: priority stream instead)
@@ -86,6 +87,8 @@ void launch_pull(int dtype, int64_t n, const int32_t* lids, const pa_combine_pla
                  const int64_t* elem, const void* const* bases, void* v, hipStream_t st);
 void launch_fill(int dtype, int64_t n, int64_t base, const int32_t* map, void* v, const void* s,
                  hipStream_t st);
+int launch_spmv_merged(int n, const int* which, const SpmvPart* parts, bool has_alpha, int bmode,
+                       const void* alpha, const void* beta, pa_ctx* owner, hipStream_t st);
 void launch_spmv_group(int which, int np, const SpmvPart* parts, bool has_alpha, int bmode, const void* alpha,
                        const void* beta, hipStream_t st);
 void launch_pack_group(int dtype, const PackGroup& g, hipStream_t st);
@@ -796,6 +799,11 @@ int pa_tune(const char* key, int value, int* previous) {
               "spmv_delta16: 1 = int32-column slices whose columns fit 16-bit codes store those (matrices built "
               "afterwards; default), 0 = int32 column ids");
     slot = &g_spmv_delta16;
+  } else if (!std::strcmp(key, "spmv_merge")) {
+    CHECK_ARG(value == 0 || value == 1,
+              "spmv_merge: 1 = mul! without a halo in flight (one part, or parts of one stream pair with the direct "
+              "pull) runs every slice kind of every part as one launch (default), 0 = one launch per kind");
+    slot = &g_spmv_merge;
   } else if (!std::strcmp(key, "halo_direct")) {
     CHECK_ARG(value == 0 || value == 1,
               "halo_direct: 1 = mul! over parts sharing a stream pair reads the ghosts straight from the owners' x "
@@ -965,6 +973,7 @@ int pa_ctx_destroy(pa_ctx* c) {
   dev_free(c->d_gather);
   dev_free(c->d_ticket);
   for (auto& b : c->bases_cache) dev_free(b.second);
+  for (auto& b : c->merged_cache) dev_free(b.second);
   if (c->h_pinned) (void)hipHostFree(c->h_pinned);
   for (auto& e : c->tev) (void)hipEventDestroy(e);
   for (auto& e : c->span_ev)
@@ -2228,7 +2237,7 @@ constexpr int kMaxTimed = 1024;  // mul! calls recorded per context between read
 // the ghosts read straight from the owners' x on the compute stream, one
 // in-order chain without cross-stream events, pa_tune("halo_direct")).
 static int group_ok(int n, pa_mat* const A[], pa_xchg* const xg[], bool any_x, int dt) {
-  if (!g_spmv_group || n < 2) return 0;
+  if (!g_spmv_group || (n < 2 && any_x)) return 0;  // one part without a halo: the merged launch
   const pa_ctx* c0 = A[0]->ctx;
   for (int i = 0; i < n; ++i)
     if (A[i]->ctx->s_main != c0->s_main || A[i]->ctx->s_comm != c0->s_comm) return 0;
@@ -2338,6 +2347,51 @@ static int spmv_grouped(int n, pa_mat* const A[], pa_vec* const y[], const pa_in
     if (!v.empty()) launch_spmv_group(which, (int)v.size(), v.data(), has_alpha, bmode, alpha, beta, sm);
   };
   if (mark(0)) return -1;
+  // no halo in flight (none, or pulled already on this stream): every slice
+  // kind of every part in one launch — side rows and int32 slices first, so
+  // their few long waves start early, then delta16, multi-pattern, pattern
+  int merged = 1;
+  if (g_spmv_merge && !g_capture_stream && (!any_x || direct)) {
+    std::vector<SpmvPart> E;
+    std::vector<int> W;
+    auto add = [&](int which, int i, int64_t nwork, const int32_t* list) {
+      if (nwork <= 0) return;
+      E.push_back(part(i, nwork, list));
+      W.push_back(which);
+    };
+    for (int i = 0; i < n; ++i)
+      if (g_spmv_format == 1 && A[i]->has_pat) add(2, i, A[i]->s_nslices, nullptr);
+    for (int i = 0; i < n; ++i) {
+      if (g_spmv_format == 1 && A[i]->has_pat) {
+        add(1, i, A[i]->nx_int, A[i]->d_xint_list);
+        add(1, i, A[i]->nx_bnd, A[i]->d_xbnd_list);
+      } else if (A[i]->d_bnd_list) {
+        add(1, i, A[i]->nslices_int, A[i]->d_int_list);
+        add(1, i, A[i]->nslices - A[i]->nslices_int, A[i]->d_bnd_list);
+      } else {
+        add(1, i, A[i]->nslices, nullptr);
+      }
+    }
+    for (int i = 0; i < n; ++i)
+      if (g_spmv_format == 1 && A[i]->has_pat) {
+        add(4, i, A[i]->nd_int, A[i]->d_dint_list);
+        add(4, i, A[i]->nd_bnd, A[i]->d_dbnd_list);
+      }
+    for (int i = 0; i < n; ++i)
+      if (g_spmv_format == 1 && A[i]->has_pat) {
+        add(3, i, A[i]->nm_int, A[i]->d_mint_list);
+        add(3, i, A[i]->nm_bnd, A[i]->d_mbnd_list);
+      }
+    for (int i = 0; i < n; ++i)
+      if (g_spmv_format == 1 && A[i]->has_pat) {
+        add(0, i, A[i]->np_int, A[i]->d_pint_list);
+        add(0, i, A[i]->np_bnd, A[i]->d_pbnd_list);
+      }
+    merged = launch_spmv_merged((int)E.size(), W.data(), E.data(), has_alpha, bmode, alpha, beta, c0, sm);
+    if (merged < 0) PA_FAIL("mul!: merged launch table (device allocation or copy) failed");
+    if (merged == 0 && (mark(1) || mark(2))) return -1;
+  }
+  if (merged) {
   // interior slices (no ghost column): overlap with the pulls on the comm stream
   for (int i = 0; i < n; ++i) {
     if (g_spmv_format == 1 && A[i]->has_pat) {
@@ -2376,6 +2430,7 @@ static int spmv_grouped(int n, pa_mat* const A[], pa_vec* const y[], const pa_in
   launch_all(4, P4);
   launch_all(1, P1);
   launch_all(2, P2);
+  }  // per-kind launches
   for (int i = 0; i < n; ++i) {
     const int32_t* ymap = y_idx[i]->own_contig ? nullptr : y_idx[i]->d_oid_to_lid;
     const bool pat = g_spmv_format == 1 && A[i]->has_pat;

@@ -297,6 +297,8 @@ struct pa_ctx {
   // device arrays of the x pointers of grouped mul! calls led by this part
   // (the direct pull's bases), most recent first
   std::vector<std::pair<std::vector<void*>, void**>> bases_cache;
+  // device copies of the merged-launch tables of calls led by this part
+  std::vector<std::pair<std::vector<char>, void*>> merged_cache;
 };
 
 struct pa_index {

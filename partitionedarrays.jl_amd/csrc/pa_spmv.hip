@@ -17,6 +17,7 @@
 #include "pa_internal.h"
 
 #include <algorithm>
+#include <cstring>
 #include <type_traits>
 
 namespace pa {
@@ -721,6 +722,127 @@ void launch_spmv_group(int which, int np, const SpmvPart* parts, bool has_alpha,
     case PA_C64: group_which<c64, 2>(which, np, parts, has_alpha, bmode, alpha, beta, st); break;
     case PA_C128: group_which<c128, 1>(which, np, parts, has_alpha, bmode, alpha, beta, st); break;
   }
+}
+
+// ---------------------------------------------------------------------------
+// Merged launch: every slice kind of every part of the call in ONE launch
+// (when no halo is in flight: the ghosts are already in x), instead of one
+// launch per kind and phase.  Each entry of the table is (kind, the
+// arguments of one part's launch of that kind); waves pick their entry with
+// a wave-uniform search and run exactly the per-kind wave code, so results
+// equal the separate launches bit for bit.  The small latency-bound launches
+// (side rows, the few int32 slices) then overlap the big ones instead of
+// each adding its own tail.  The table lives in device memory (too large for
+// kernel arguments), one cached copy per distinct call.
+constexpr int kMergeMax = 48;
+
+template <typename T>
+struct SpmvTable {
+  int n;
+  int pk[kMergeMax];
+  int64_t start[kMergeMax + 1];
+  SpmvArgs<T> a[kMergeMax];
+};
+
+template <typename T, int R, bool ALPHA, int BMODE, int U, bool SH>
+__global__ __launch_bounds__(256) void k_spmv_merged(const SpmvTable<T>* __restrict__ tab) {
+  const int64_t w = (int64_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const int n = tab->n;
+  if (w >= tab->start[n]) return;
+  int lo = 0, hi = n;  // last entry whose start <= w
+  while (hi - lo > 1) {
+    const int mid = (lo + hi) >> 1;
+    if (tab->start[mid] <= w) lo = mid; else hi = mid;
+  }
+  const int p = __builtin_amdgcn_readfirstlane(lo);
+  const int pk = __builtin_amdgcn_readfirstlane(tab->pk[p]);
+  const int64_t lw = w - tab->start[p];
+  const SpmvArgs<T>& a = tab->a[p];
+  if (pk == 1) spmv_wave<T, R, ALPHA, BMODE, U, 1, SH>(a, lw);
+  else if (pk == 3) spmv_wave<T, R, ALPHA, BMODE, U, 3, SH>(a, lw);
+  else if (pk == 0) spmv_wave<T, R, ALPHA, BMODE, U, 0, SH>(a, lw);
+  else if constexpr (!SH) spmv_wave<T, R, ALPHA, BMODE, U, 2, false>(a, lw);
+}
+
+template <typename T, int R, bool ALPHA, int BMODE>
+static void launch_merged_t(const SpmvTable<T>* d, int64_t waves, bool sh, hipStream_t st) {
+  const int64_t blocks = (waves + 3) / 4;
+  if (blocks == 0) return;
+  if (sh)
+    hipLaunchKernelGGL((k_spmv_merged<T, R, ALPHA, BMODE, 8, true>), dim3(blocks), dim3(256), g_spmv_lds, st, d);
+  else if (g_spmv_unroll == 4)
+    hipLaunchKernelGGL((k_spmv_merged<T, R, ALPHA, BMODE, 4, false>), dim3(blocks), dim3(256), g_spmv_lds, st, d);
+  else
+    hipLaunchKernelGGL((k_spmv_merged<T, R, ALPHA, BMODE, 8, false>), dim3(blocks), dim3(256), g_spmv_lds, st, d);
+}
+
+static int pk_of(int which) { return which == 0 ? 1 : which == 3 ? 2 : which == 4 ? 3 : 0; }
+
+template <typename T, int R>
+static int merged_t(int n, const int* which, const SpmvPart* parts, bool has_alpha, int bmode, const void* alpha,
+                    const void* beta, pa_ctx* owner, hipStream_t st) {
+  SpmvTable<T> h;
+  std::memset(&h, 0, sizeof(h));  // the table's bytes are its cache key
+  bool sh = (g_spmv_flags & SPMV_SHORT) != 0;
+  for (int i = 0; i < n; ++i) {
+    const SpmvPart& q = parts[i];
+    if (q.nwork <= 0) continue;
+    if (h.n == kMergeMax) return 1;
+    const int32_t* list = q.list;
+    if ((g_spmv_flags & SPMV_IDLIST) && list && which[i] != 2 && q.nwork == q.A->nslices) list = nullptr;
+    h.a[h.n] = make_args<T>(which[i], q.nwork, list, q.A, q.x, q.y, q.ymap, alpha, beta, q.dotp);
+    h.pk[h.n] = pk_of(which[i]);
+    sh = sh && h.pk[h.n] != 2 && h.a[h.n].maxlen <= 8;
+    h.start[h.n + 1] = h.start[h.n] + q.nwork;
+    ++h.n;
+  }
+  if (h.n == 0) return 0;
+  // cached device copy of this exact table (most recent first)
+  auto& C = owner->merged_cache;
+  const char* hb = reinterpret_cast<const char*>(&h);
+  void* d = nullptr;
+  for (size_t k = 0; k < C.size(); ++k)
+    if (C[k].first.size() == sizeof(h) && std::memcmp(C[k].first.data(), hb, sizeof(h)) == 0) {
+      if (k) std::swap(C[k], C[0]);
+      d = C[0].second;
+      break;
+    }
+  if (!d) {
+    if (hipMalloc(&d, sizeof(h)) != hipSuccess) return -1;
+    if (hipMemcpy(d, &h, sizeof(h), hipMemcpyHostToDevice) != hipSuccess) { (void)hipFree(d); return -1; }
+    if (C.size() >= 16) {
+      (void)hipStreamSynchronize(st);  // the evicted table may still be read
+      (void)hipFree(C.back().second);
+      C.pop_back();
+    }
+    C.insert(C.begin(), {std::vector<char>(hb, hb + sizeof(h)), d});
+  }
+  const SpmvTable<T>* dt = (const SpmvTable<T>*)d;
+  const int64_t waves = h.start[h.n];
+  if (!has_alpha) {
+    if (bmode == 0) launch_merged_t<T, R, false, 0>(dt, waves, sh, st);
+    else if (bmode == 1) launch_merged_t<T, R, false, 1>(dt, waves, sh, st);
+    else launch_merged_t<T, R, false, 2>(dt, waves, sh, st);
+  } else {
+    if (bmode == 0) launch_merged_t<T, R, true, 0>(dt, waves, sh, st);
+    else if (bmode == 1) launch_merged_t<T, R, true, 1>(dt, waves, sh, st);
+    else launch_merged_t<T, R, true, 2>(dt, waves, sh, st);
+  }
+  return 0;
+}
+
+// n (which, part) entries as one launch; returns 1 when they do not fit one
+// table (the caller launches per kind), -1 on an allocation/copy error
+int launch_spmv_merged(int n, const int* which, const SpmvPart* parts, bool has_alpha, int bmode,
+                       const void* alpha, const void* beta, pa_ctx* owner, hipStream_t st) {
+  if (n <= 0) return 0;
+  switch (parts[0].A->dtype) {
+    case PA_F32: return merged_t<float, 4>(n, which, parts, has_alpha, bmode, alpha, beta, owner, st);
+    case PA_F64: return merged_t<double, 2>(n, which, parts, has_alpha, bmode, alpha, beta, owner, st);
+    case PA_C64: return merged_t<c64, 2>(n, which, parts, has_alpha, bmode, alpha, beta, owner, st);
+    case PA_C128: return merged_t<c128, 1>(n, which, parts, has_alpha, bmode, alpha, beta, owner, st);
+  }
+  return 0;
 }
 
 // ---------------------------------------------------------------------------
