@@ -123,7 +123,8 @@ def pmc_traffic(args, steps=5):
             return None, f"rocprofv3 --pmc {ctr} failed (rc {p.returncode})"
         rows = list(csv.DictReader(open(files[0])))
         vals = [float(r["Counter_Value"]) for r in rows
-                if "k_spmv_sell" in r["Kernel_Name"] and r["Counter_Name"] == ctr]
+                if ("k_spmv_sell" in r["Kernel_Name"] or "k_spmv_merged" in r["Kernel_Name"])
+                and r["Counter_Name"] == ctr]
         tot[ctr] = sum(vals) / (steps + 1)  # warmup step + steps
         if ctr == "FETCH_SIZE":
             probe = [float(r["Counter_Value"]) for r in rows
@@ -440,7 +441,7 @@ def main():
             "frac": round(achieved / HBM_PEAK_GBS, 4),
             "traffic": None if traffic is None else int(traffic),
             "traffic_detail": tnote,
-            "kernel": ("k_spmv_sell (all SpMV kernels of one mul! step: pattern + side slices"
+            "kernel": ("k_spmv_merged / k_spmv_sell (all SpMV kernels of one mul! step: pattern + side slices"
                        + (", halo pack/pull" if halo else "") + ")"),
             "kernel_ms": round(kernel_ms, 4),
             "kernel_ms_note": ("HIP events on part %d's compute stream around the K timed steps, / K" % p0

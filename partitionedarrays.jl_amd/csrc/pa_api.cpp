@@ -2453,6 +2453,48 @@ static int spmv_grouped(int n, pa_mat* const A[], pa_vec* const y[], const pa_in
   return 0;
 }
 
+// One phase of one part's slices (0: interior, before the halo; 1: boundary
+// slices and side rows, after it): one merged launch (pa_tune spmv_merge)
+// or one launch per slice kind.
+static int launch_phase(int phase, pa_mat* A, const void* x, void* y, const int32_t* ymap, bool has_alpha,
+                        int bmode, const void* alpha, const void* beta, void* dotp, hipStream_t st) {
+  std::vector<SpmvPart> E;
+  std::vector<int> W;
+  auto add = [&](int which, int64_t nwork, const int32_t* list) {
+    if (nwork <= 0) return;
+    E.push_back(SpmvPart{nwork, list, A, x, y, ymap, dotp});
+    W.push_back(which);
+  };
+  if (g_spmv_format == 1 && A->has_pat) {
+    if (phase == 0) {
+      add(1, A->nx_int, A->d_xint_list);
+      add(4, A->nd_int, A->d_dint_list);
+      add(3, A->nm_int, A->d_mint_list);
+      add(0, A->np_int, A->d_pint_list);
+    } else {
+      add(2, A->s_nslices, nullptr);
+      add(1, A->nx_bnd, A->d_xbnd_list);
+      add(4, A->nd_bnd, A->d_dbnd_list);
+      add(3, A->nm_bnd, A->d_mbnd_list);
+      add(0, A->np_bnd, A->d_pbnd_list);
+    }
+  } else if (A->d_bnd_list) {  // split layout (the interior list may be empty)
+    if (phase == 0) add(1, A->nslices_int, A->d_int_list);
+    else add(1, A->nslices - A->nslices_int, A->d_bnd_list);
+  } else if (phase == 0) {
+    add(1, A->nslices, nullptr);
+  }
+  if (E.empty()) return 0;
+  if (E.size() > 1 && g_spmv_merge && !g_capture_stream) {
+    const int rc = launch_spmv_merged((int)E.size(), W.data(), E.data(), has_alpha, bmode, alpha, beta, A->ctx, st);
+    if (rc < 0) PA_FAIL("mul!: merged launch table (device allocation or copy) failed");
+    if (rc == 0) return 0;
+  }
+  for (size_t k = 0; k < E.size(); ++k)
+    launch_spmv_part(W[k], E[k].nwork, E[k].list, A, x, y, ymap, has_alpha, bmode, alpha, beta, dotp, st);
+  return 0;
+}
+
 static int spmv_impl(int n, pa_mat* const A[], pa_vec* const y[], const pa_index* const y_idx[],
                      pa_vec* const x[], const pa_index* const x_idx[], pa_xchg* const xg[],
                      const void* alpha, const void* beta, bool want_dot, CGState* const* dot_tail = nullptr) {
@@ -2535,17 +2577,7 @@ static int spmv_impl(int n, pa_mat* const A[], pa_vec* const y[], const pa_index
     const int32_t* ymap = y_idx[i]->own_contig ? nullptr : y_idx[i]->d_oid_to_lid;
     if (tslot[i]) HIPC(hipEventRecord(tslot[i][0], SM(c)));
     // interior slices (no ghost column): overlap with the halo transport
-    if (g_spmv_format == 1 && A[i]->has_pat) {
-      launch_spmv_part(0, A[i]->np_int, A[i]->d_pint_list, A[i], x[i]->d, y[i]->d, ymap, has_alpha, bmode, alpha, beta, dotp[i], SM(c));
-      launch_spmv_part(3, A[i]->nm_int, A[i]->d_mint_list, A[i], x[i]->d, y[i]->d, ymap, has_alpha, bmode, alpha, beta, dotp[i], SM(c));
-      launch_spmv_part(4, A[i]->nd_int, A[i]->d_dint_list, A[i], x[i]->d, y[i]->d, ymap, has_alpha, bmode, alpha, beta, dotp[i], SM(c));
-      launch_spmv_part(1, A[i]->nx_int, A[i]->d_xint_list, A[i], x[i]->d, y[i]->d, ymap, has_alpha, bmode, alpha, beta, dotp[i], SM(c));
-    } else if (A[i]->d_bnd_list) {  // split layout (the interior list may be empty)
-      if (A[i]->nslices_int > 0)
-        launch_spmv_part(1, A[i]->nslices_int, A[i]->d_int_list, A[i], x[i]->d, y[i]->d, ymap, has_alpha, bmode, alpha, beta, dotp[i], SM(c));
-    } else {
-      launch_spmv_part(1, A[i]->nslices, nullptr, A[i], x[i]->d, y[i]->d, ymap, has_alpha, bmode, alpha, beta, dotp[i], SM(c));
-    }
+    if (launch_phase(0, A[i], x[i]->d, y[i]->d, ymap, has_alpha, bmode, alpha, beta, dotp[i], SM(c))) return -1;
     if (tslot[i]) HIPC(hipEventRecord(tslot[i][1], SM(c)));
   }
   HIPC(hipGetLastError());
@@ -2560,17 +2592,8 @@ static int spmv_impl(int n, pa_mat* const A[], pa_vec* const y[], const pa_index
     }
     if (tslot[i]) HIPC(hipEventRecord(tslot[i][2], SM(c)));
     const int32_t* ymap = y_idx[i]->own_contig ? nullptr : y_idx[i]->d_oid_to_lid;
-    if (g_spmv_format == 1 && A[i]->has_pat) {
-      // pattern slices reading ghosts, then the side rows (after the halo)
-      launch_spmv_part(0, A[i]->np_bnd, A[i]->d_pbnd_list, A[i], x[i]->d, y[i]->d, ymap, has_alpha, bmode, alpha, beta, dotp[i], SM(c));
-      launch_spmv_part(3, A[i]->nm_bnd, A[i]->d_mbnd_list, A[i], x[i]->d, y[i]->d, ymap, has_alpha, bmode, alpha, beta, dotp[i], SM(c));
-      launch_spmv_part(4, A[i]->nd_bnd, A[i]->d_dbnd_list, A[i], x[i]->d, y[i]->d, ymap, has_alpha, bmode, alpha, beta, dotp[i], SM(c));
-      launch_spmv_part(1, A[i]->nx_bnd, A[i]->d_xbnd_list, A[i], x[i]->d, y[i]->d, ymap, has_alpha, bmode, alpha, beta, dotp[i], SM(c));
-      launch_spmv_part(2, A[i]->s_nslices, nullptr, A[i], x[i]->d, y[i]->d, ymap, has_alpha, bmode, alpha, beta, dotp[i], SM(c));
-    } else if (A[i]->d_bnd_list) {
-      launch_spmv_part(1, A[i]->nslices - A[i]->nslices_int, A[i]->d_bnd_list, A[i], x[i]->d, y[i]->d, ymap,
-                       has_alpha, bmode, alpha, beta, dotp[i], SM(c));
-    }
+    // slices reading ghosts and the side rows (after the halo)
+    if (launch_phase(1, A[i], x[i]->d, y[i]->d, ymap, has_alpha, bmode, alpha, beta, dotp[i], SM(c))) return -1;
     // long rows (after the halo: they may read ghost columns)
     const bool pat = g_spmv_format == 1 && A[i]->has_pat;
     const int64_t long_base = A[i]->nslices + (pat ? A[i]->s_nslices : 0);

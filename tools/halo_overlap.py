@@ -5,12 +5,17 @@
     python tools/halo_overlap.py analyze DIR/.../ov_kernel_trace.csv
 
 `run`: the (2,2,2) weak-scaling partition (n^3 nodes per part) with all parts
-in this process on device 0, mul! repeated `steps` times.  The parts share
-one stream pair, so each mul! is: pack (all parts, compute stream) → pull-
-unpack (all parts, comm stream) ‖ interior slices (all parts, compute
-stream) → boundary slices.  `analyze`: per mul!, the interval of the pull
-kernel and of the interior SpMV kernel(s) launched after the same pack, and
-how much of the pull ran while an interior kernel was running."""
+in this process on device 0, mul! repeated `steps` times.
+  --mode pull: the parts share one stream pair and the grouped mul! packs
+    (compute stream), pulls (comm stream) ‖ interior slices, then boundary
+    slices (pa_tune halo_direct = 0; the default direct pull has no transport
+    to overlap);
+  --mode rccl: the multi-GPU path — per part: pack, the halo as one RCCL
+    group of ncclSend/ncclRecv on the comm stream (here to self, one GPU)
+    ‖ interior slices, then unpack and the boundary slices.
+`analyze`: per mul!, the interval of the transport kernel(s) (pull or RCCL)
+and of the interior SpMV kernels launched after the packs, and how much of
+the transport ran while an interior kernel was running."""
 import csv
 import json
 import os
@@ -28,9 +33,12 @@ def run(argv):
     ap.add_argument("--n", type=int, default=128)
     ap.add_argument("--shape", default="2,2,2")
     ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--mode", default="pull", choices=["pull", "rccl"])
     a = ap.parse_args(argv)
     shape = tuple(int(v) for v in a.shape.split(","))
-    be = pamd.HIPBackend(devices=[0])
+    if a.mode == "pull":
+        pamd._lib.tune("halo_direct", 0)
+    be = pamd.HIPBackend(devices=[0], rccl=a.mode == "rccl")
     parts = be.get_part_ids(shape)
     N = tuple(a.n * s for s in shape)
     A = pamd.drivers.stencil_operator(parts, N, 27)
@@ -53,34 +61,46 @@ def analyze(path):
     ks = sorted(((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]) for r in rows),
                 key=lambda t: t[0])
     steps = []
+    is_pack = lambda n: "k_pack" in n
+    is_xport = lambda n: "k_pull_group" in n or "nccl" in n.lower()
+    is_spmv = lambda n: "k_spmv" in n
     i = 0
     while i < len(ks):
-        if "k_pack_group" not in ks[i][2]:
+        if not is_pack(ks[i][2]):
             i += 1
             continue
-        pack = ks[i]
-        j = i + 1
-        pull, interior = None, []
-        while j < len(ks) and "k_pack_group" not in ks[j][2]:
+        j = i
+        packs = []
+        while j < len(ks) and is_pack(ks[j][2]):
+            packs.append(ks[j])
+            j += 1
+        xport, interior = [], []
+        while j < len(ks) and not is_pack(ks[j][2]):
             k = ks[j]
-            if "k_pull_group" in k[2] and pull is None:
-                pull = k
-            elif "k_spmv_sell_group" in k[2] and (pull is None or k[0] < pull[1]):
+            if is_xport(k[2]):
+                xport.append(k)
+            elif is_spmv(k[2]):
                 interior.append(k)
             j += 1
-        if pull is not None and interior:
-            lo = max(pull[0], min(k[0] for k in interior))
-            hi = min(pull[1], max(k[1] for k in interior))
-            steps.append({"pack_us": (pack[1] - pack[0]) / 1e3, "pull_us": (pull[1] - pull[0]) / 1e3,
+        if xport and interior:
+            t0, t1 = min(k[0] for k in xport), max(k[1] for k in xport)
+            interior = [k for k in interior if k[0] < t1]  # launched before the transport ended
+        if xport and interior:
+            lo = max(t0, min(k[0] for k in interior))
+            hi = min(t1, max(k[1] for k in interior))
+            steps.append({"pack_us": (packs[-1][1] - packs[0][0]) / 1e3, "pull_us": (t1 - t0) / 1e3,
                           "interior_us": (max(k[1] for k in interior) - min(k[0] for k in interior)) / 1e3,
-                          "pull_hidden_frac": max(0, hi - lo) / max(1, pull[1] - pull[0]),
-                          "pull_start_after_interior_start_us": (pull[0] - min(k[0] for k in interior)) / 1e3})
+                          "pull_hidden_frac": max(0, hi - lo) / max(1, t1 - t0),
+                          "pull_start_after_interior_start_us": (t0 - min(k[0] for k in interior)) / 1e3,
+                          "transport": "rccl" if any("nccl" in k[2].lower() for k in xport) else "pull"})
         i = j
     if not steps:
         print(json.dumps({"error": "no pack → pull ‖ interior sequence found"}))
         return
     med = lambda key: sorted(s[key] for s in steps)[len(steps) // 2]
-    print(json.dumps({"steps": len(steps), "median": {k: round(med(k), 3) for k in steps[0]},
+    num = [k for k in steps[0] if k != "transport"]
+    print(json.dumps({"steps": len(steps), "transport": steps[0]["transport"],
+                      "median": {k: round(med(k), 3) for k in num},
                       "min_hidden_frac": round(min(s["pull_hidden_frac"] for s in steps), 3),
                       "per_step": steps}, indent=1))
 
