@@ -211,3 +211,34 @@ def test_delta16_slices_equal_int32(be, pamd, O, dtype):
     for p in parts.part_ids:
         assert _eq(O, out[0].local(p), oy.values[p]), f"part {p}: delta16 SpMV differs from the oracle"
         assert _eq(O, out[1].local(p), oy.values[p]), f"part {p}: int32 SpMV differs from the oracle"
+
+
+@pytest.mark.parametrize("merge,direct,d16", [(1, 1, 1), (0, 1, 1), (1, 0, 1), (0, 0, 0), (1, 1, 0)])
+def test_launch_paths_equal_oracle(be, pamd, O, merge, direct, d16):
+    """Every launch path of mul! over the parts of one GPU gives the oracle's
+    bits: merged launch or one launch per slice kind (spmv_merge), direct
+    pull or pack + pull on the comm stream (halo_direct), delta16 or int32
+    column ids (spmv_delta16); Voronoi parts, F64, 8 parts."""
+    N, nparts = (30, 28, 26), 8
+    knobs = {"spmv_merge": merge, "halo_direct": direct, "spmv_delta16": d16}
+    prev = {k: pamd._lib.tune(k, v) for k, v in knobs.items()}
+    try:
+        parts = be.get_part_ids(nparts)
+        A = pamd.drivers.irregular_problem(parts, N, 27, np.float64)
+        OA = _oracle(O, N, nparts, np.float64)
+        rng = np.random.default_rng(SEED + 21)
+        xs = {p: rng.uniform(-1, 1, A.cols.partition.local(p).num_lids) for p in parts.part_ids}
+        x = pamd.PVector.from_host(pamd.map_parts(lambda s: xs[s.part], A.cols.partition), A.cols)
+        y = pamd.PVector.undef(A.rows)
+        for _ in range(2):  # the second call reuses the cached tables
+            pamd.mul_(y, A, x)
+        ox = O.PVector(O.map_parts(lambda s: xs[s.part].copy(), OA.cols.partition), OA.cols)
+        oy = O.pvector_undef(OA.rows)
+        O.mul_(oy, OA, ox)
+        got, gx = y.to_host(), x.to_host()
+        for p in parts.part_ids:
+            assert np.array_equal(got.local(p), oy.values[p]), f"part {p}: SpMV differs"
+            assert np.array_equal(gx.local(p), ox.values[p]), f"part {p}: ghost values of x differ"
+    finally:
+        for k, v in prev.items():
+            pamd._lib.tune(k, v)
