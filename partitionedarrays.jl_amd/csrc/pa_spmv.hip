@@ -746,7 +746,10 @@ struct SpmvTable {
 
 template <typename T, int R, bool ALPHA, int BMODE, int U, bool SH>
 __global__ __launch_bounds__(256) void k_spmv_merged(const SpmvTable<T>* __restrict__ tab) {
-  const int64_t w = (int64_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  // SPMV_XCD: consecutive blocks on one XCD (each XCD sweeps its own row
+  // range, so the x window of its waves stays in its L2)
+  const int64_t blk = (tab->a[0].flags & SPMV_XCD) ? xcd_remap(blockIdx.x, gridDim.x) : (int64_t)blockIdx.x;
+  const int64_t w = blk * 4 + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   const int n = tab->n;
   if (w >= tab->start[n]) return;
   int lo = 0, hi = n;  // last entry whose start <= w
