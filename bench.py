@@ -168,7 +168,7 @@ def child_pmc(args):
     pamd._lib.hbm_probe(0, PROBE_BYTES, 1)
 
 
-def cg_mode(args, pamd, backend, parts, A, ngpu, world, sync):
+def cg_mode(args, pamd, backend, parts, A, ngpu, use_dist, sync):
     """--cg K: IterativeSolvers.cg! iterations (BASELINE config 4) on the same
     operator: per iteration 1 mul! (+halo), dot, norm, 3 broadcasts.  Prints
     its own JSON line (not the headline metric)."""
@@ -184,7 +184,7 @@ def cg_mode(args, pamd, backend, parts, A, ngpu, world, sync):
         x = pamd.PVector.undef(cols, dtype).fill_(0)
         pamd.cg_(x, A, b, reltol=0.0, maxiter=args.warmup, **kw)
         sync()
-        if world > 1:
+        if use_dist:
             dist.barrier()
         x = pamd.PVector.undef(cols, dtype).fill_(0)
         t0 = time.perf_counter()
@@ -192,7 +192,7 @@ def cg_mode(args, pamd, backend, parts, A, ngpu, world, sync):
         pamd.cg_(x, A, b, reltol=0.0, maxiter=args.cg, history=hist, **kw)
         sync()
         el = time.perf_counter() - t0
-        if world > 1:
+        if use_dist:
             t = torch.tensor([el], dtype=torch.float64)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             el = float(t.item())
@@ -237,6 +237,9 @@ def main():
     ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 HBM-traffic passes")
     ap.add_argument("--child-pmc", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--cg", type=int, default=0, help="time K CG iterations instead (own JSON line)")
+    ap.add_argument("--distributed", action="store_true",
+                    help="one part per process (HIPDistributedBackend, RCCL) even for one process: "
+                         "rehearses the torchrun path of --gpus N > 1 on a single GPU")
     args = ap.parse_args()
     if args.child_pmc:
         return child_pmc(args)
@@ -247,8 +250,12 @@ def main():
     import torch.distributed as dist
     import pamd
 
-    if world > 1:
+    use_dist = world > 1 or args.distributed
+    if use_dist:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29511")
+        os.environ.setdefault("RANK", "0")
+        os.environ.setdefault("WORLD_SIZE", "1")
         dist.init_process_group("gloo")
         backend = pamd.HIPDistributedBackend()      # one part per process, halo over RCCL
         ngpu = world
@@ -292,20 +299,20 @@ def main():
         B_local += format_bytes(info, s.num_hids, n_snd, n_rcv, S)
         C_local += csr_bytes(info["nnz"], info["nrows"], s.num_hids, n_snd, n_rcv, S)
     B_all, C_all = B_local, C_local
-    if world > 1:
+    if use_dist:
         t = torch.tensor([float(B_local), float(C_local)], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.SUM)
         B_all, C_all = float(t[0].item()), float(t[1].item())
 
     def barrier():
-        if world > 1:
+        if use_dist:
             dist.barrier()
 
     if args.cg > 0:
-        line = cg_mode(args, pamd, backend, parts, A, ngpu, world, sync)
+        line = cg_mode(args, pamd, backend, parts, A, ngpu, use_dist, sync)
         if rank == 0:
             print(json.dumps(line), flush=True)
-        if world > 1:
+        if use_dist:
             dist.destroy_process_group()
         return
 
@@ -340,7 +347,7 @@ def main():
     barrier()
     span_ms = c0.span_ms() / args.steps
     elapsed = t1 - t0
-    if world > 1:
+    if use_dist:
         t = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
@@ -364,7 +371,7 @@ def main():
         return {p: c.kernel_times() for p, c in zip(parts.part_ids, ctxs)}
     phases = phase_times()
     per_part = {p: {k: round(v, 4) if isinstance(v, float) else v for k, v in t.items()} for p, t in phases.items()}
-    if world > 1:
+    if use_dist:
         allp = [None] * world
         dist.all_gather_object(allp, per_part)
         per_part = {k: v for d in allp for k, v in d.items()}
@@ -421,7 +428,7 @@ def main():
             "nnz_per_part": info["nnz"],
             "rows_per_part": info["nrows"],
             "ghosts_per_part": s_nhids,
-            "process_model": "one part per process (RCCL halo)" if world > 1 else f"{ngpu} part(s) in one process",
+            "process_model": "one part per process (RCCL halo)" if use_dist else f"{ngpu} part(s) in one process",
             "bytes_per_step_all_parts": int(B_all),
             "bytes_definition": ("per part: matrix streams as loaded (values incl. padding, column ids, slice "
                                  "metadata; pa_mat_traffic) + x read once (owned+ghost) + y written once "
@@ -473,7 +480,7 @@ def main():
         line["cpu_baseline"] = cpu_baseline(args.kind, args.n, args.cpu_seconds)
     if rank == 0:
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if use_dist:
         dist.destroy_process_group()
 
 
