@@ -88,7 +88,9 @@ void launch_pull(int dtype, int64_t n, const int32_t* lids, const pa_combine_pla
 void launch_fill(int dtype, int64_t n, int64_t base, const int32_t* map, void* v, const void* s,
                  hipStream_t st);
 int launch_spmv_merged(int n, const int* which, const SpmvPart* parts, bool has_alpha, int bmode,
-                       const void* alpha, const void* beta, pa_ctx* owner, hipStream_t st);
+                       const void* alpha, const void* beta, pa_ctx* owner, std::vector<void*>* pinned,
+                       hipStream_t st);
+extern std::vector<std::pair<void*, std::vector<char>>> g_capture_uploads;
 void launch_spmv_group(int which, int np, const SpmvPart* parts, bool has_alpha, int bmode, const void* alpha,
                        const void* beta, hipStream_t st);
 void launch_pack_group(int dtype, const PackGroup& g, hipStream_t st);
@@ -740,6 +742,7 @@ int check_lids(const pa_xchg* X, const pa_vec* v) {
 // them in the previous exchange (local receivers record ev_recvd after their
 // copies; for RCCL sends the part's own ev_recvd covers them).
 bool g_capturing = false;  // inside pa_spmv_graph_create: one replay never overlaps the next
+std::vector<void*>* g_capture_tables = nullptr;  // merged-launch tables the graph being captured owns
 
 int pre_pack_wait(int n, pa_xchg* const xg[]) {
   if (g_capturing) return 0;
@@ -2351,7 +2354,7 @@ static int spmv_grouped(int n, pa_mat* const A[], pa_vec* const y[], const pa_in
   // kind of every part in one launch — side rows and int32 slices first, so
   // their few long waves start early, then delta16, multi-pattern, pattern
   int merged = 1;
-  if (g_spmv_merge && !g_capture_stream && (!any_x || direct)) {
+  if (g_spmv_merge && (!any_x || direct)) {
     std::vector<SpmvPart> E;
     std::vector<int> W;
     auto add = [&](int which, int i, int64_t nwork, const int32_t* list) {
@@ -2387,7 +2390,8 @@ static int spmv_grouped(int n, pa_mat* const A[], pa_vec* const y[], const pa_in
         add(0, i, A[i]->np_int, A[i]->d_pint_list);
         add(0, i, A[i]->np_bnd, A[i]->d_pbnd_list);
       }
-    merged = launch_spmv_merged((int)E.size(), W.data(), E.data(), has_alpha, bmode, alpha, beta, c0, sm);
+    merged = launch_spmv_merged((int)E.size(), W.data(), E.data(), has_alpha, bmode, alpha, beta, c0,
+                                g_capture_tables, sm);
     if (merged < 0) PA_FAIL("mul!: merged launch table (device allocation or copy) failed");
     if (merged == 0 && (mark(1) || mark(2))) return -1;
   }
@@ -2485,8 +2489,9 @@ static int launch_phase(int phase, pa_mat* A, const void* x, void* y, const int3
     add(1, A->nslices, nullptr);
   }
   if (E.empty()) return 0;
-  if (E.size() > 1 && g_spmv_merge && !g_capture_stream) {
-    const int rc = launch_spmv_merged((int)E.size(), W.data(), E.data(), has_alpha, bmode, alpha, beta, A->ctx, st);
+  if (E.size() > 1 && g_spmv_merge) {
+    const int rc = launch_spmv_merged((int)E.size(), W.data(), E.data(), has_alpha, bmode, alpha, beta, A->ctx,
+                                      g_capture_tables, st);
     if (rc < 0) PA_FAIL("mul!: merged launch table (device allocation or copy) failed");
     if (rc == 0) return 0;
   }
@@ -2620,6 +2625,7 @@ static int spmv_impl(int n, pa_mat* const A[], pa_vec* const y[], const pa_index
 // rows — captured once from the parts' streams, replayed with one launch.
 struct pa_graph {
   int device = 0;
+  std::vector<void*> tables;        // merged-launch argument tables the graph's kernels read
   hipStream_t origin = nullptr;
   std::vector<hipStream_t> others;
   std::vector<hipEvent_t> ev_pre;   // per other stream: its queued work, before a replay
@@ -2636,6 +2642,7 @@ int pa_graph_destroy(pa_graph* G) {
   if (G->graph) (void)hipGraphDestroy(G->graph);
   for (auto e : G->ev_pre) if (e) (void)hipEventDestroy(e);
   if (G->ev_done) (void)hipEventDestroy(G->ev_done);
+  for (void* t : G->tables) dev_free(t);
   delete G;
   return 0;
 }
@@ -2694,13 +2701,21 @@ int pa_spmv_graph_create(int n, pa_mat* const A[], pa_vec* const y[], const pa_i
   if (e == hipSuccess) {
     g_capturing = true;
     g_capture_stream = G->origin;  // the parts' kernels as one chain
+    g_capture_tables = &G->tables;
+    g_capture_uploads.clear();
     rc = spmv_impl(n, A, y, y_idx, x, x_idx, xg, alpha, beta, false);
+    g_capture_tables = nullptr;
     g_capture_stream = nullptr;
     g_capturing = false;
     hipError_t e2 = hipStreamEndCapture(G->origin, &G->graph);
     if (e == hipSuccess) e = e2;
   }
   for (int i = 0; i < n; ++i) ctxs[i]->timing = timing[i];
+  // the merged-launch tables the captured kernels read (allocated during the
+  // capture, owned by the graph)
+  for (auto& u : g_capture_uploads)
+    if (e == hipSuccess && rc == 0) e = hipMemcpy(u.first, u.second.data(), u.second.size(), hipMemcpyHostToDevice);
+  g_capture_uploads.clear();
   if (e != hipSuccess || rc != 0) {
     const std::string why = rc != 0 ? pa_last_error() : std::string(hipGetErrorString(e));
     pa_graph_destroy(G);

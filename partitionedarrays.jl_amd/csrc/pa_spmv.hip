@@ -63,6 +63,9 @@ int g_spmv_format = 1;  // 1: pattern slices where built, 0: int32 columns only
 // the byte-cost rule moves kernel time by ±4 % either way.
 int g_spmv_patterns = 1;         // patterns per slice (multi-pattern slices when > 1)
 int g_spmv_pattern_rule = 0;     // 1: slice encoding by streamed bytes, 0: pattern slice when half the rows follow it
+// merged-launch tables allocated during a graph capture, copied after it ends
+// (no copies while a stream is being captured)
+std::vector<std::pair<void*, std::vector<char>>> g_capture_uploads;
 
 template <int BYTES> struct RawOf;
 template <> struct RawOf<2> { typedef unsigned short type; };
@@ -783,7 +786,7 @@ static int pk_of(int which) { return which == 0 ? 1 : which == 3 ? 2 : which == 
 
 template <typename T, int R>
 static int merged_t(int n, const int* which, const SpmvPart* parts, bool has_alpha, int bmode, const void* alpha,
-                    const void* beta, pa_ctx* owner, hipStream_t st) {
+                    const void* beta, pa_ctx* owner, std::vector<void*>* pinned, hipStream_t st) {
   SpmvTable<T> h;
   std::memset(&h, 0, sizeof(h));  // the table's bytes are its cache key
   bool sh = (g_spmv_flags & SPMV_SHORT) != 0;
@@ -800,11 +803,20 @@ static int merged_t(int n, const int* which, const SpmvPart* parts, bool has_alp
     ++h.n;
   }
   if (h.n == 0) return 0;
-  // cached device copy of this exact table (most recent first)
+  // cached device copy of this exact table (most recent first); a graph
+  // capture (pinned) gets its own copy, owned by the graph
   auto& C = owner->merged_cache;
   const char* hb = reinterpret_cast<const char*>(&h);
   void* d = nullptr;
-  for (size_t k = 0; k < C.size(); ++k)
+  if (pinned) {  // during a capture: device memory now, its contents after the capture ends
+    if (hipMalloc(&d, sizeof(h)) != hipSuccess) {
+      (void)hipGetLastError();
+      return 1;  // the caller launches per kind
+    }
+    pinned->push_back(d);
+    g_capture_uploads.push_back({d, std::vector<char>(hb, hb + sizeof(h))});
+  }
+  for (size_t k = 0; !d && k < C.size(); ++k)
     if (C[k].first.size() == sizeof(h) && std::memcmp(C[k].first.data(), hb, sizeof(h)) == 0) {
       if (k) std::swap(C[k], C[0]);
       d = C[0].second;
@@ -837,13 +849,14 @@ static int merged_t(int n, const int* which, const SpmvPart* parts, bool has_alp
 // n (which, part) entries as one launch; returns 1 when they do not fit one
 // table (the caller launches per kind), -1 on an allocation/copy error
 int launch_spmv_merged(int n, const int* which, const SpmvPart* parts, bool has_alpha, int bmode,
-                       const void* alpha, const void* beta, pa_ctx* owner, hipStream_t st) {
+                       const void* alpha, const void* beta, pa_ctx* owner, std::vector<void*>* pinned,
+                       hipStream_t st) {
   if (n <= 0) return 0;
   switch (parts[0].A->dtype) {
-    case PA_F32: return merged_t<float, 4>(n, which, parts, has_alpha, bmode, alpha, beta, owner, st);
-    case PA_F64: return merged_t<double, 2>(n, which, parts, has_alpha, bmode, alpha, beta, owner, st);
-    case PA_C64: return merged_t<c64, 2>(n, which, parts, has_alpha, bmode, alpha, beta, owner, st);
-    case PA_C128: return merged_t<c128, 1>(n, which, parts, has_alpha, bmode, alpha, beta, owner, st);
+    case PA_F32: return merged_t<float, 4>(n, which, parts, has_alpha, bmode, alpha, beta, owner, pinned, st);
+    case PA_F64: return merged_t<double, 2>(n, which, parts, has_alpha, bmode, alpha, beta, owner, pinned, st);
+    case PA_C64: return merged_t<c64, 2>(n, which, parts, has_alpha, bmode, alpha, beta, owner, pinned, st);
+    case PA_C128: return merged_t<c128, 1>(n, which, parts, has_alpha, bmode, alpha, beta, owner, pinned, st);
   }
   return 0;
 }
