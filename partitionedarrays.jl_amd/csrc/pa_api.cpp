@@ -777,10 +777,11 @@ int pa_tune(const char* key, int value, int* previous) {
   CHECK_ARG(key, "null key");
   int* slot = nullptr;
   if (!std::strcmp(key, "spmv_flags")) {
-    CHECK_ARG(value >= 0 && value <= 127,
+    CHECK_ARG(value >= 0 && value <= 255,
               "spmv_flags: bit 0 = non-temporal streams, bit 1 = XCD mapping, bit 2 = 16 B x runs (pattern rows), "
               "bit 3 = masked tail batch, bit 4 = identity slice lists dropped, bit 5 = non-temporal y stores, "
-              "bit 6 = short-row kernels (launches whose rows have <= 8 entries)");
+              "bit 6 = short-row kernels (launches whose rows have <= 8 entries), bit 7 = 16 B x runs in "
+              "int32/delta16 slices where a lane's rows read consecutive columns");
     slot = &g_spmv_flags;
   } else if (!std::strcmp(key, "spmv_lds")) {
     CHECK_ARG(value >= 0 && value <= 160 * 1024, "spmv_lds: bytes of LDS per SpMV block (occupancy cap)");

@@ -42,7 +42,8 @@ __device__ inline int64_t xcd_remap(int64_t b, int64_t G) {
   return x * q + (x < r ? x : r) + i;
 }
 
-enum { SPMV_NT = 1, SPMV_XCD = 2, SPMV_XPAIR = 4, SPMV_TAILB = 8, SPMV_IDLIST = 16, SPMV_YNT = 32, SPMV_SHORT = 64 };
+enum { SPMV_NT = 1, SPMV_XCD = 2, SPMV_XPAIR = 4, SPMV_TAILB = 8, SPMV_IDLIST = 16, SPMV_YNT = 32, SPMV_SHORT = 64,
+       SPMV_XRUN = 128 };
 typedef unsigned int spmv_u32x4 __attribute__((ext_vector_type(4)));
 // Process-wide knobs (pa_tune).  Defaults from the A/Bs in
 // profiles/r01_ab_spmv.txt and profiles/r01/ab_xpair.txt: non-temporal
@@ -138,13 +139,46 @@ __device__ __forceinline__ double pick(bool c, double a, double b) { return c ? 
 __device__ __forceinline__ c64 pick(bool c, c64 a, c64 b) { return c64{c ? a.re : b.re, c ? a.im : b.im}; }
 __device__ __forceinline__ c128 pick(bool c, c128 a, c128 b) { return c128{c ? a.re : b.re, c ? a.im : b.im}; }
 
+// the R consecutive x values x[i .. i+R-1] as one 16 B load (i only
+// dword-aligned: global loads need 4 B alignment); pa_vec pads 64 B on both
+// sides, so i in [-(R-1), n-1] stays inside the allocation
+typedef unsigned int u4a __attribute__((ext_vector_type(4))) __attribute__((aligned(4)));
+template <typename T, int R>
+__device__ __forceinline__ Pack<T, R> ld_xrun(const T* p) {
+  static_assert(sizeof(Pack<T, R>) == 16, "16 B runs");
+  const u4a r = *reinterpret_cast<const u4a*>(p);
+  Pack<T, R> v;
+  __builtin_memcpy(&v, &r, 16);
+  return v;
+}
+
+// the x values of a lane's R rows at one entry: one 16 B run when their
+// columns are consecutive (rows of a structured block, SPMV_XRUN), else R
+// gathers (c < 0: padding, read x[0], never used)
+template <typename T, int R>
+__device__ __forceinline__ void gather_x(T (&xv)[R], const int32_t (&c)[R], const T* __restrict__ x, bool xrun) {
+  if constexpr (R > 1 && sizeof(Pack<T, R>) == 16) {
+    bool run = xrun && c[0] >= 0;
+#pragma unroll
+    for (int r = 1; r < R; ++r) run = run && c[r] == c[0] + r;
+    if (run) {
+      const Pack<T, R> p = ld_xrun<T, R>(x + c[0]);
+#pragma unroll
+      for (int r = 0; r < R; ++r) xv[r] = p.v[r];
+      return;
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < R; ++r) xv[r] = x[c[r] >= 0 ? c[r] : 0];
+}
+
 // int32-column rows: c < 0 is padding (skipped: never multiplied)
 // TB: the entries past the last full U batch run as one masked batch
 // (entries >= len re-read entry len-1 and are never accumulated)
 template <typename T, int R, bool ALPHA, bool NT, int U, bool SH = false>
 __device__ __forceinline__ void rows_int32(T (&acc)[R], const IPack<R>* __restrict__ cp,
                                            const Pack<T, R>* __restrict__ vp, int len,
-                                           const T* __restrict__ x, T alpha, bool TB) {
+                                           const T* __restrict__ x, T alpha, bool TB, bool xrun) {
   int k = 0;
   if (SH) TB = true;  // short rows (len <= U): the one masked batch is the whole row
   for (; !SH && k + U <= len; k += U) {
@@ -156,12 +190,7 @@ __device__ __forceinline__ void rows_int32(T (&acc)[R], const IPack<R>* __restri
     for (int u = 0; u < U; ++u) v[u] = ld<NT>(&vp[(k + u) * 64]);
     T xv[U][R];
 #pragma unroll
-    for (int u = 0; u < U; ++u)
-#pragma unroll
-      for (int r = 0; r < R; ++r) {
-        const int32_t cc = c[u].c[r];
-        xv[u][r] = x[cc >= 0 ? cc : 0];
-      }
+    for (int u = 0; u < U; ++u) gather_x<T, R>(xv[u], c[u].c, x, xrun);
 #pragma unroll
     for (int u = 0; u < U; ++u)
 #pragma unroll
@@ -186,12 +215,7 @@ __device__ __forceinline__ void rows_int32(T (&acc)[R], const IPack<R>* __restri
     T xv[U][R];
 #pragma unroll
     for (int u = 0; u < U; ++u)
-      if (k + u < len)
-#pragma unroll
-        for (int r = 0; r < R; ++r) {
-          const int32_t cc = c[u].c[r];
-          xv[u][r] = x[cc >= 0 ? cc : 0];
-        }
+      if (k + u < len) gather_x<T, R>(xv[u], c[u].c, x, xrun);
 #pragma unroll
     for (int u = 0; u < U; ++u)
 #pragma unroll
@@ -229,7 +253,8 @@ __device__ __forceinline__ int32_t d16_col(uint32_t q, int32_t row, int32_t gb) 
 template <typename T, int R, bool ALPHA, bool NT, int U, bool SH = false>
 __device__ __forceinline__ void rows_d16(T (&acc)[R], const S16Pack<R>* __restrict__ cp,
                                          const Pack<T, R>* __restrict__ vp, int len,
-                                         const T* __restrict__ x, T alpha, bool TB, int32_t row0, int32_t gb) {
+                                         const T* __restrict__ x, T alpha, bool TB, int32_t row0, int32_t gb,
+                                         bool xrun) {
   int k = 0;
   if (SH) TB = true;
   for (; !SH && k + U <= len; k += U) {
@@ -242,12 +267,11 @@ __device__ __forceinline__ void rows_d16(T (&acc)[R], const S16Pack<R>* __restri
     int32_t c[U][R];
     T xv[U][R];
 #pragma unroll
-    for (int u = 0; u < U; ++u)
+    for (int u = 0; u < U; ++u) {
 #pragma unroll
-      for (int r = 0; r < R; ++r) {
-        c[u][r] = d16_col(q[u].c[r], row0 + r, gb);
-        xv[u][r] = x[c[u][r] >= 0 ? c[u][r] : 0];
-      }
+      for (int r = 0; r < R; ++r) c[u][r] = d16_col(q[u].c[r], row0 + r, gb);
+      gather_x<T, R>(xv[u], c[u], x, xrun);
+    }
 #pragma unroll
     for (int u = 0; u < U; ++u)
 #pragma unroll
@@ -272,12 +296,11 @@ __device__ __forceinline__ void rows_d16(T (&acc)[R], const S16Pack<R>* __restri
     int32_t c[U][R];
     T xv[U][R];
 #pragma unroll
-    for (int u = 0; u < U; ++u)
+    for (int u = 0; u < U; ++u) {
 #pragma unroll
-      for (int r = 0; r < R; ++r) {
-        c[u][r] = d16_col(q[u].c[r], row0 + r, gb);
-        if (k + u < len) xv[u][r] = x[c[u][r] >= 0 ? c[u][r] : 0];
-      }
+      for (int r = 0; r < R; ++r) c[u][r] = d16_col(q[u].c[r], row0 + r, gb);
+      if (k + u < len) gather_x<T, R>(xv[u], c[u], x, xrun);
+    }
 #pragma unroll
     for (int u = 0; u < U; ++u)
 #pragma unroll
@@ -301,19 +324,6 @@ __device__ __forceinline__ void rows_d16(T (&acc)[R], const S16Pack<R>* __restri
       acc[r] = pick(cc >= 0, t, acc[r]);
     }
   }
-}
-
-// the R consecutive x values x[i .. i+R-1] as one 16 B load (i only
-// dword-aligned: global loads need 4 B alignment); pa_vec pads 64 B on both
-// sides, so i in [-(R-1), n-1] stays inside the allocation
-typedef unsigned int u4a __attribute__((ext_vector_type(4))) __attribute__((aligned(4)));
-template <typename T, int R>
-__device__ __forceinline__ Pack<T, R> ld_xrun(const T* p) {
-  static_assert(sizeof(Pack<T, R>) == 16, "16 B runs");
-  const u4a r = *reinterpret_cast<const u4a*>(p);
-  Pack<T, R> v;
-  __builtin_memcpy(&v, &r, 16);
-  return v;
 }
 
 // pattern rows: column of row `rbase + r` at entry k is rbase + r + pat[k].
@@ -491,12 +501,14 @@ __device__ __forceinline__ void spmv_wave(const SpmvArgs<T>& a, const int64_t w)
   } else if constexpr (PK == 3) {
     const S16Pack<R>* __restrict__ cp = reinterpret_cast<const S16Pack<R>*>(a.col16 + off) + lane;
     const int32_t gb = a.gbase[s];
-    if (a.flags & SPMV_NT) rows_d16<T, R, ALPHA, true, U, SH>(acc, cp, vp, len, a.x, a.alpha, tb, (int32_t)row0, gb);
-    else rows_d16<T, R, ALPHA, false, U, SH>(acc, cp, vp, len, a.x, a.alpha, tb, (int32_t)row0, gb);
+    const bool xrun = (a.flags & SPMV_XRUN) != 0;
+    if (a.flags & SPMV_NT) rows_d16<T, R, ALPHA, true, U, SH>(acc, cp, vp, len, a.x, a.alpha, tb, (int32_t)row0, gb, xrun);
+    else rows_d16<T, R, ALPHA, false, U, SH>(acc, cp, vp, len, a.x, a.alpha, tb, (int32_t)row0, gb, xrun);
   } else {
     const IPack<R>* __restrict__ cp = reinterpret_cast<const IPack<R>*>(a.col + off) + lane;
-    if (a.flags & SPMV_NT) rows_int32<T, R, ALPHA, true, U, SH>(acc, cp, vp, len, a.x, a.alpha, tb);
-    else rows_int32<T, R, ALPHA, false, U, SH>(acc, cp, vp, len, a.x, a.alpha, tb);
+    const bool xrun = (a.flags & SPMV_XRUN) != 0;
+    if (a.flags & SPMV_NT) rows_int32<T, R, ALPHA, true, U, SH>(acc, cp, vp, len, a.x, a.alpha, tb, xrun);
+    else rows_int32<T, R, ALPHA, false, U, SH>(acc, cp, vp, len, a.x, a.alpha, tb, xrun);
   }
 
   if (a.dotp) {  // fused dot(u, c): Σ conj(u_i)·c_i over this slice's rows
