@@ -409,11 +409,55 @@ def prange_noids(parts: PData, noids: PData, ngids=None) -> PRange:
     return PRange(ngids, partition, empty_exchanger(partition), g2p, False)
 
 
-def prange_cartesian(parts: PData, ngids: tuple) -> PRange:
-    """PRange(parts, ngids::NTuple) Interfaces.jl:1114-1137 (no ghost layer)."""
+def _lids_1d(ngids, np_, p, periodic):
+    """One dimension of a Cartesian part with its ghost layer (Interfaces.jl:
+    1321-1335 / 1353-1373 and 1375-1411): the gids of the local ids and the
+    part coordinate owning each — the owned range, one ghost id before it
+    (from part p-1, or wrapped around from the last part when periodic) and
+    one after it (part p+1, or wrapped to the first); a single part in the
+    dimension has no ghost layer there."""
+    a, b = oid_range(ngids, np_, p)
+    g = np.arange(a, b + 1, dtype=np.int64)
+    c = np.full(len(g), p, dtype=np.int64)
+    if np_ == 1:
+        return g, c
+    if p > 1 or periodic:
+        g = np.concatenate([[a - 1 if p > 1 else ngids], g])
+        c = np.concatenate([[p - 1 if p > 1 else np_], c])
+    if p < np_ or periodic:
+        g = np.concatenate([g, [b + 1 if p < np_ else 1]])
+        c = np.concatenate([c, [p + 1 if p < np_ else 1]])
+    return g, c
+
+
+def _tensor(axes, shape):
+    """_id_tensor_product (Interfaces.jl:1473-1491): linear ids in `shape` of
+    the per-dimension ids, first dimension fastest."""
+    grids = np.meshgrid(*[np.asarray(a) for a in axes[::-1]], indexing="ij")[::-1]
+    return linear_index(shape, [g.ravel() for g in grids])
+
+
+def prange_cartesian(parts: PData, ngids: tuple, with_ghost=False, isperiodic=None) -> PRange:
+    """PRange(parts, ngids::NTuple) Interfaces.jl:1114-1137 (no ghost layer);
+    with_ghost (1166-1193): every part also holds the one-wide layer of its
+    neighbours' ids, in the local Cartesian order, so owned and ghost lids
+    interleave (oid_to_lid / hid_to_lid = findall of the owner), and the
+    Exchanger reuses parts_rcv as parts_snd; isperiodic (1195-1223) wraps the
+    layer around the global boundary."""
     np_ = parts.shape
     if len(np_) != len(ngids):
         raise ValueError("Cartesian PRange needs len(parts.shape) == len(ngids)")
+    if with_ghost:
+        per = tuple(isperiodic) if isperiodic is not None else (False,) * len(ngids)
+
+        def mk_ghost(part):
+            cp = [int(c) for c in cartesian_index(np_, part)]
+            gs, cs = zip(*[_lids_1d(ngids[d], np_[d], cp[d], per[d]) for d in range(len(ngids))])
+            return IndexSet(part, _tensor(gs, ngids), _tensor(cs, np_))  # oid/hid = findall (IndexSets.jl:267-280)
+        partition = map_parts(mk_ghost, parts)
+        g2p = map_parts(lambda _: cartesian_gid_to_part(ngids, np_), parts)
+        ex = exchanger_from_ids(partition, reuse_parts_rcv=True)
+        return PRange(int(np.prod(ngids)), partition, ex, g2p, True, tuple(np_))
 
     def mk(part):
         lo, n = box_of_part(ngids, np_, part)

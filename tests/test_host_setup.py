@@ -295,3 +295,25 @@ def test_grid_neighbor_discovery(pamd, O, shape, N, kind, monkeypatch):
     for p in parts.part_ids:
         assert list(cols.exchanger.parts_snd.local(p)) == list(ocols.exchanger.parts_snd[p])
         assert cols.exchanger.lids_snd.local(p).tolist() == ocols.exchanger.lids_snd[p].tolist()
+
+
+@pytest.mark.parametrize("shape,ngids,periodic", [((2, 2), (5, 4), None), ((2, 2), (4, 4), (True, True)),
+                                                   ((2, 2), (4, 4), (False, True)), ((3, 1, 2), (7, 3, 5), None),
+                                                   ((2, 3, 2), (6, 7, 5), (True, False, True)), ((4,), (11,), (True,))])
+def test_prange_with_ghost_matches_oracle(pamd, O, shape, ngids, periodic):
+    """PRange(parts, ngids, with_ghost[, isperiodic]) (Interfaces.jl:1166-1223):
+    interleaved owned/ghost lids, owners, and the reuse_parts_rcv Exchanger
+    equal the oracle's (pinned by test_interfaces.jl:383-497)."""
+    parts = pamd.sequential.get_part_ids(shape)
+    r = pamd.prange_cartesian(parts, ngids, with_ghost=True, isperiodic=periodic)
+    o = O.prange_cartesian(O.get_part_ids(shape), ngids, with_ghost=True, isperiodic=periodic)
+    for p in parts.part_ids:
+        s, os_ = r.partition.local(p), o.partition[p]
+        assert s.lid_to_gid.tolist() == list(os_.lid_to_gid)
+        assert s.lid_to_part.tolist() == list(os_.lid_to_part)
+        assert s.oid_to_lid.tolist() == list(os_.oid_to_lid) and s.hid_to_lid.tolist() == list(os_.hid_to_lid)
+        ex, oex = r.exchanger, o.exchanger
+        assert list(ex.parts_rcv.local(p)) == list(oex.parts_rcv[p])
+        assert list(ex.parts_snd.local(p)) == list(oex.parts_snd[p])
+        assert ex.lids_rcv.local(p).tolist() == oex.lids_rcv[p].tolist()
+        assert ex.lids_snd.local(p).tolist() == oex.lids_snd[p].tolist()
