@@ -102,30 +102,40 @@ class HIPBackend(SequentialBackend):
         self.graph_mul = graph_mul
         self.rccl = rccl
         self.ctx = {}
+        self._sets = {}  # number of parts -> {part: PartContext}
 
     def get_part_ids(self, nparts):
         """With share_streams, parts on the same device share one stream pair
         (pa_ctx_create_shared): one in-order chain, and mul! launches each
-        phase once for all of them (the grouped path of pa_spmv_all)."""
+        phase once for all of them (the grouped path of pa_spmv_all).
+        The contexts of a number of parts are created once per backend and
+        reused by later calls (streams and RCCL communicators are not
+        re-created; objects built on an earlier call stay on their streams)."""
         ids = super().get_part_ids(nparts)
         n = ids.num_parts
+        if n in self._sets:
+            self.ctx = self._sets[n]
+            return ids
         first = {}
-        self.ctx = {}
+        ctx = {}
         for p in ids.part_ids:
             d = self.devices[(p - 1) % len(self.devices)]
             share = first.get(d) if self.share_streams else None
-            self.ctx[p] = PartContext(d, p, n, share_with=share)
-            first.setdefault(d, self.ctx[p])
+            ctx[p] = PartContext(d, p, n, share_with=share)
+            first.setdefault(d, ctx[p])
         if self.rccl and n > 1:
-            if not self.share_streams and len({c.device for c in self.ctx.values()}) != n:
+            if not self.share_streams and len({c.device for c in ctx.values()}) != n:
                 raise _lib.PAError("HIPBackend(rccl=True): parts of one device share one RCCL rank and "
                                    "must share their stream pair (share_streams=True)")
-            _lib.call("pa_comm_init_all", n, _lib.ptr_array([self.ctx[p].h for p in ids.part_ids]))
+            _lib.call("pa_comm_init_all", n, _lib.ptr_array([ctx[p].h for p in ids.part_ids]))
             _lib.tune("halo_transport", 1)
+        self._sets[n] = self.ctx = ctx
         return ids
 
-    def context(self, part) -> PartContext:
-        return self.ctx[part]
+    def context(self, part, nparts=None) -> PartContext:
+        """the context of `part` in the partition into `nparts` parts (default:
+        the latest get_part_ids)"""
+        return (self._sets[nparts] if nparts in self._sets else self.ctx)[part]
 
 
 class HIPDistributedBackend(DistributedBackend):
@@ -145,6 +155,8 @@ class HIPDistributedBackend(DistributedBackend):
         ids = super().get_part_ids(nparts)
         n = ids.num_parts
         part = ids.part_ids[0]
+        if part in self.ctx:  # created by an earlier call (RCCL communicator included)
+            return ids
         c = PartContext(self.device, part, n)
         # RCCL for every world size (with one process, its reductions take the
         # same one-rank all-gather path as with eight)
@@ -157,12 +169,12 @@ class HIPDistributedBackend(DistributedBackend):
         self.ctx = {part: c}
         return ids
 
-    def context(self, part) -> PartContext:
+    def context(self, part, nparts=None) -> PartContext:
         return self.ctx[part]
 
 
 def contexts(a: PData):
-    return [a.backend.context(p) for p in a.part_ids]
+    return [a.backend.context(p, a.num_parts) for p in a.part_ids]
 
 
 class DeviceIndex:
