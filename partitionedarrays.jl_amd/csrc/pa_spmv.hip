@@ -1396,7 +1396,8 @@ void launch_gather_ptrs(int P, const void* const* srcs, int accsz, void* out, hi
 
 // ---------------------------------------------------------------------------
 // Pattern detection (one wave per slice).  Candidate 0: the middle valid row
-// of the slice; its offsets pat[k] = col_k - row.  A row is regular for a
+// of the slice (or the row at 1/4 or 3/4 when more rows follow that one); its
+// offsets pat[k] = col_k - row.  A row is regular for a
 // candidate when its column sequence is exactly row + pat[k] (same length).
 // Multi-pattern (NP > 1): while lanes are left without a pattern, the first
 // such lane's first full-length row becomes the next candidate; each lane
@@ -1428,13 +1429,17 @@ __global__ __launch_bounds__(256) void k_pattern_detect(int64_t nrows, int64_t n
   const int L = slen[s];
   const int64_t rem = nrows - s * H;
   const int nvalid = (int)(rem < H ? rem : H);
-  const int m = nvalid / 2;
-  const int mlane = m / R, mr = m % R;
-  int Lp = 0;
-  for (int k = 0; k < L; ++k) {
-    if (col[off + ((int64_t)k * 64 + mlane) * R + mr] < 0) break;
-    ++Lp;
-  }
+  // candidate row length (entries before its first padding slot)
+  auto cand_len = [&](int clane, int cr) {
+    int l = 0;
+    for (int k = 0; k < L; ++k) {
+      if (col[off + ((int64_t)k * 64 + clane) * R + cr] < 0) break;
+      ++l;
+    }
+    return l;
+  };
+  int mlane = (nvalid / 2) / R, mr = (nvalid / 2) % R;
+  int Lp = cand_len(mlane, mr);
   // row lengths (entries before the first padding slot) and ghost columns
   int rlen[R];
   bool ghost_any = false;
@@ -1487,8 +1492,27 @@ __global__ __launch_bounds__(256) void k_pattern_detect(int64_t nrows, int64_t n
       dst[k] = col[off + ((int64_t)k * 64 + clane) * R + cr] - (int32_t)crow;
   };
   bool g1 = false;
-  const unsigned bits1 = follow(mlane, mr, g1);
-  const int tot1 = wave_count(bits1);
+  unsigned bits1 = follow(mlane, mr, g1);
+  int tot1 = wave_count(bits1);
+  // the middle row may be an exception (a slice of several grid lines: the
+  // first row of the second line); the rows at 1/4 and 3/4 are candidates too,
+  // the one most rows follow wins (ties keep the earlier)
+  if (tot1 < nvalid && nvalid >= 4) {
+    for (int q = 1; q <= 3; q += 2) {
+      const int m = q * nvalid / 4;
+      const int cl = m / R, cr = m % R;
+      const int keepL = Lp;
+      Lp = cand_len(cl, cr);
+      bool g = false;
+      const unsigned b = follow(cl, cr, g);
+      const int t = wave_count(b);
+      if (t > tot1) {
+        mlane = cl; mr = cr; bits1 = b; tot1 = t; g1 = g;
+      } else {
+        Lp = keepL;
+      }
+    }
+  }
   // multi-pattern passes
   const bool mp = NP > 1 && Lp > 0 && Lp <= kmp && tot1 < nvalid;
   unsigned bitsM = bits1;
