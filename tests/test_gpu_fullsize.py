@@ -97,6 +97,33 @@ def test_c2_fd7_128_one_part_bitexact(be, pamd, tmp_path, fmt):
     assert info["nnz"] == 14099408  # SURVEY.md §8 size table
 
 
+def test_c2_fd7_128_f32_all_pattern_slices(be, pamd):
+    """F32 slices are 256 rows (two x-lines of 128): the middle row of a slice
+    is an x = 0 boundary row, so the pattern candidate must come from another
+    row (1/4 or 3/4).  Every slice is a pattern slice, and y equals the int32
+    encoding's bit for bit (that encoding is pinned to the oracle at small
+    sizes, test_gpu_parity.py; the C oracle is F64 only)."""
+    n = 128
+    parts = be.get_part_ids((1, 1, 1))
+    x_ = np.random.default_rng(SEED + 3).uniform(-1, 1, n ** 3).astype(np.float32)
+    ys = []
+    for fmt in (1, 0):
+        prev = pamd._lib.tune("spmv_format", fmt)
+        try:
+            A = pamd.drivers.stencil_operator(parts, (n,) * 3, 7, np.float32)
+            x = pamd.PVector.from_host(pamd.map_parts(lambda s: x_, A.cols.partition), A.cols)
+            y = pamd.PVector.undef(A.rows, np.float32)
+            pamd.mul_(y, A, x)
+            ys.append(y.to_host().local(1))
+            if fmt == 1:
+                info = A.values.local(1).info()
+                assert info["pattern_slices"] == info["nslices"] == 8192
+        finally:
+            pamd._lib.tune("spmv_format", prev)
+    bad = np.flatnonzero(ys[0] != ys[1])
+    assert bad.size == 0, f"{bad.size} rows differ between the encodings, first at gid {bad[0] + 1}"
+
+
 @pytest.mark.parametrize("fmt", [1, 0], ids=["pattern", "int32"])
 def test_fe27_256_one_part_bitexact(be, pamd, ref256, fmt):
     x_, yref, _ = ref256
