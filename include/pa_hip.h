@@ -21,7 +21,11 @@
  *    by RCCL point-to-point over xGMI (after pa_comm_init_rank);
  *  - dtype codes: PA_F32, PA_F64, PA_C64 (ComplexF32), PA_C128 (ComplexF64).
  *    Scalars (alpha, beta, results) are passed as pointers to host values of
- *    the vector's element type.
+ *    the vector's element type;
+ *  - threading: one host thread drives the library per process (the
+ *    reference's tasks run on the main Julia task too).  pa_tune knobs, the
+ *    graph-capture state and the per-context caches are process-wide and
+ *    unsynchronised; only pa_last_error is per thread.
  */
 #ifndef PA_HIP_H
 #define PA_HIP_H
