@@ -760,7 +760,7 @@ struct SpmvTable {
 };
 
 template <typename T, int R, bool ALPHA, int BMODE, int U, bool SH>
-__global__ __launch_bounds__(256) void k_spmv_merged(const SpmvTable<T>* __restrict__ tab) {
+__device__ __forceinline__ void merged_wave(const SpmvTable<T>* __restrict__ tab) {
   // SPMV_XCD: consecutive blocks on one XCD (each XCD sweeps its own row
   // range, so the x window of its waves stays in its L2)
   const int64_t blk = (tab->a[0].flags & SPMV_XCD) ? xcd_remap(blockIdx.x, gridDim.x) : (int64_t)blockIdx.x;
@@ -782,11 +782,28 @@ __global__ __launch_bounds__(256) void k_spmv_merged(const SpmvTable<T>* __restr
   else if constexpr (!SH) spmv_wave<T, R, ALPHA, BMODE, U, 2, false>(a, lw);
 }
 
+template <typename T, int R, bool ALPHA, int BMODE, int U, bool SH>
+__global__ __launch_bounds__(256) void k_spmv_merged(const SpmvTable<T>* __restrict__ tab) {
+  merged_wave<T, R, ALPHA, BMODE, U, SH>(tab);
+}
+
+// F64 short rows (FD7): 5 waves per SIMD instead of 4 (96 VGPRs instead of
+// 102; the pattern path keeps its registers, a few int32-path values spill).
+// C2 FD7 128^3: 0.0312-0.0317 -> 0.0303 ms (profiles/r02/waves/).  Not for
+// F32/C64 (R = 4 / complex: ~200 spills) nor for longer rows (FE27: -10 %).
+template <typename T, int R, bool ALPHA, int BMODE>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k_spmv_merged_short(
+    const SpmvTable<T>* __restrict__ tab) {
+  merged_wave<T, R, ALPHA, BMODE, 8, true>(tab);
+}
+
 template <typename T, int R, bool ALPHA, int BMODE>
 static void launch_merged_t(const SpmvTable<T>* d, int64_t waves, bool sh, hipStream_t st) {
   const int64_t blocks = (waves + 3) / 4;
   if (blocks == 0) return;
-  if (sh)
+  if (sh && std::is_same<T, double>::value)
+    hipLaunchKernelGGL((k_spmv_merged_short<T, R, ALPHA, BMODE>), dim3(blocks), dim3(256), g_spmv_lds, st, d);
+  else if (sh)
     hipLaunchKernelGGL((k_spmv_merged<T, R, ALPHA, BMODE, 8, true>), dim3(blocks), dim3(256), g_spmv_lds, st, d);
   else if (g_spmv_unroll == 4)
     hipLaunchKernelGGL((k_spmv_merged<T, R, ALPHA, BMODE, 4, false>), dim3(blocks), dim3(256), g_spmv_lds, st, d);
