@@ -1,0 +1,194 @@
+// Stream probe (standalone, not part of the library): where does the headline
+// SpMV's value stream lose rate against a plain read sweep on the same box?
+// Same 3.57 GB of values (131,072 FE27 slices × 27 entries × 1 KB), variants:
+//   lin_ro     grid-stride read sweep, no writes (pa_hbm_probe's idiom)
+//   lin_w      the same + 1 KB of y per slice written after the sweep
+//   slice_ro   wave w streams its own contiguous 27 KB slice, no y write
+//   slice_w    the same + its 1 KB of y (the SELL kernel's traffic shape)
+//   slice_wnt  the same with a non-temporal y store
+//   slice_b64  slice_w launched as one wave per workgroup
+//   slice_2    slice_w with two slices per wave (grid halved)
+//   (with a 3rd argument) write-only sweeps of y / of 3.57 GB, memset, and
+//   slice_w with y folded into a 1 / 16 / 64 MB ring
+// hipcc --offload-arch=gfx950 -O3 tools/probe_stream.hip -o probe_stream
+#include <hip/hip_runtime.h>
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+#define CK(x)                                                                \
+  do {                                                                       \
+    hipError_t e = (x);                                                      \
+    if (e != hipSuccess) {                                                   \
+      std::fprintf(stderr, "%s failed: %s\n", #x, hipGetErrorString(e));     \
+      std::exit(1);                                                          \
+    }                                                                        \
+  } while (0)
+
+constexpr int L = 27;  // entries per slice (FE27)
+constexpr int U = 8;   // loads in flight per lane
+constexpr unsigned MAGIC = 0x9e3779b9u;
+
+__device__ __forceinline__ u32x4 ldnt(const u32x4* p) { return __builtin_nontemporal_load(p); }
+
+__device__ __forceinline__ u32x4 stream_slice(const u32x4* __restrict__ v, int64_t s, int lane) {
+  const int64_t base = s * L * 64;
+  u32x4 acc = {0, 0, 0, 0};
+  int k = 0;
+  for (; k + U <= L; k += U) {
+    u32x4 t[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) t[u] = ldnt(v + base + (k + u) * 64 + lane);
+#pragma unroll
+    for (int u = 0; u < U; ++u) acc ^= t[u];
+  }
+  for (; k < L; ++k) acc ^= ldnt(v + base + k * 64 + lane);
+  return acc;
+}
+
+// WMODE 0: no write (kept live by a never-true test), 1: plain store, 2: non-temporal store
+template <int WMODE, int WPB, int SPW>
+__global__ __launch_bounds__(64 * WPB) void k_slice(const u32x4* __restrict__ v, u32x4* __restrict__ y,
+                                                   int64_t nslices) {
+  const int lane = threadIdx.x & 63;
+  const int64_t w = (int64_t)blockIdx.x * WPB + (threadIdx.x >> 6);
+#pragma unroll
+  for (int j = 0; j < SPW; ++j) {
+    const int64_t s = w * SPW + j;
+    if (s >= nslices) return;
+    const u32x4 acc = stream_slice(v, s, lane);
+    if (WMODE == 0) {
+      if (acc.x == MAGIC) y[s * 64 + lane] = acc;
+    } else if (WMODE == 1) {
+      y[s * 64 + lane] = acc;
+    } else {
+      __builtin_nontemporal_store(acc, y + s * 64 + lane);
+    }
+  }
+}
+
+// write-only sweep of n16 16 B values (NT: non-temporal stores)
+template <bool NT>
+__global__ __launch_bounds__(256) void k_wonly(u32x4* __restrict__ y, int64_t n16) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const u32x4 v = {1u, 2u, 3u, (unsigned)threadIdx.x};
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n16; i += stride) {
+    if (NT) __builtin_nontemporal_store(v, y + i);
+    else y[i] = v;
+  }
+}
+
+// slice_w with the y store folded into a small ring (RING 16 B slots): same
+// store instructions, but the bytes stay in L2
+template <int RINGLOG>
+__global__ __launch_bounds__(256) void k_slice_ring(const u32x4* __restrict__ v, u32x4* __restrict__ y,
+                                                    int64_t nslices) {
+  const int lane = threadIdx.x & 63;
+  const int64_t s = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (s >= nslices) return;
+  const u32x4 acc = stream_slice(v, s, lane);
+  y[(s * 64 + lane) & ((1ll << RINGLOG) - 1)] = acc;
+}
+
+template <int WRITE>
+__global__ __launch_bounds__(256) void k_linear(const u32x4* __restrict__ v, u32x4* __restrict__ y,
+                                                int64_t n16, int64_t nslices) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  u32x4 acc = {0, 0, 0, 0};
+  int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  for (; i + (U - 1) * stride < n16; i += U * stride) {
+    u32x4 t[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) t[u] = ldnt(v + i + u * stride);
+#pragma unroll
+    for (int u = 0; u < U; ++u) acc ^= t[u];
+  }
+  for (; i < n16; i += stride) acc ^= ldnt(v + i);
+  if (WRITE) {
+    for (int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; j < nslices * 64; j += stride) y[j] = acc;
+  } else if (acc.x == MAGIC) {
+    y[threadIdx.x] = acc;
+  }
+}
+
+int main(int argc, char** argv) {
+  const int64_t nslices = argc > 1 ? std::atoll(argv[1]) : 131072;
+  const int reps = argc > 2 ? std::atoi(argv[2]) : 10;
+  const int64_t n16 = nslices * L * 64;
+  const size_t vbytes = (size_t)n16 * 16, ybytes = (size_t)nslices * 1024;
+  u32x4 *v, *y;
+  CK(hipMalloc(&v, vbytes));
+  CK(hipMalloc(&y, ybytes));
+  CK(hipMemset(v, 0x5a, vbytes));
+  CK(hipMemset(y, 0, ybytes));
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  auto run = [&](const char* name, bool writes, auto launch) {
+    launch();
+    CK(hipDeviceSynchronize());
+    std::vector<float> ms;
+    for (int r = 0; r < reps; ++r) {
+      CK(hipEventRecord(e0, 0));
+      launch();
+      CK(hipEventRecord(e1, 0));
+      CK(hipEventSynchronize(e1));
+      float t;
+      CK(hipEventElapsedTime(&t, e0, e1));
+      ms.push_back(t);
+    }
+    std::sort(ms.begin(), ms.end());
+    const double bytes = (double)vbytes + (writes ? (double)ybytes : 0.0);
+    std::printf("{\"variant\": \"%s\", \"median_ms\": %.4f, \"min_ms\": %.4f, \"gbs_median\": %.1f}\n", name,
+                ms[ms.size() / 2], ms[0], bytes / (ms[ms.size() / 2] * 1e-3) / 1e9);
+    std::fflush(stdout);
+  };
+  if (argc > 3) {  // write-side variants only
+    const int64_t yn16 = (int64_t)ybytes / 16;
+    u32x4* big;
+    CK(hipMalloc(&big, vbytes));
+    for (int round = 0; round < 2; ++round) {
+      for (int blocks : {4096, 16384}) {
+        char nm[48];
+        std::snprintf(nm, sizeof nm, "wonly_y_%d", blocks);
+        run(nm, false, [&] { hipLaunchKernelGGL(k_wonly<false>, dim3(blocks), dim3(256), 0, 0, y, yn16); });
+        std::snprintf(nm, sizeof nm, "wonly_y_nt_%d", blocks);
+        run(nm, false, [&] { hipLaunchKernelGGL(k_wonly<true>, dim3(blocks), dim3(256), 0, 0, y, yn16); });
+        std::snprintf(nm, sizeof nm, "wonly_big_%d", blocks);
+        run(nm, false, [&] { hipLaunchKernelGGL(k_wonly<false>, dim3(blocks), dim3(256), 0, 0, big, n16); });
+        std::snprintf(nm, sizeof nm, "wonly_big_nt_%d", blocks);
+        run(nm, false, [&] { hipLaunchKernelGGL(k_wonly<true>, dim3(blocks), dim3(256), 0, 0, big, n16); });
+      }
+      run("memset_y", false, [&] { CK(hipMemsetAsync(y, round, ybytes, 0)); });
+      const int64_t b4 = (nslices + 3) / 4;
+      run("slice_ro", false, [&] { hipLaunchKernelGGL((k_slice<0, 4, 1>), dim3(b4), dim3(256), 0, 0, v, y, nslices); });
+      run("slice_w", true, [&] { hipLaunchKernelGGL((k_slice<1, 4, 1>), dim3(b4), dim3(256), 0, 0, v, y, nslices); });
+      run("slice_ring1MB", true, [&] { hipLaunchKernelGGL((k_slice_ring<16>), dim3(b4), dim3(256), 0, 0, v, y, nslices); });
+      run("slice_ring16MB", true, [&] { hipLaunchKernelGGL((k_slice_ring<20>), dim3(b4), dim3(256), 0, 0, v, y, nslices); });
+      run("slice_ring64MB", true, [&] { hipLaunchKernelGGL((k_slice_ring<22>), dim3(b4), dim3(256), 0, 0, v, y, nslices); });
+    }
+    CK(hipFree(big));
+    return 0;
+  }
+  for (int round = 0; round < 2; ++round) {
+    for (int blocks : {4096, 16384}) {
+      char nm[32];
+      std::snprintf(nm, sizeof nm, "lin_ro_%d", blocks);
+      run(nm, false, [&] { hipLaunchKernelGGL(k_linear<0>, dim3(blocks), dim3(256), 0, 0, v, y, n16, nslices); });
+      std::snprintf(nm, sizeof nm, "lin_w_%d", blocks);
+      run(nm, true, [&] { hipLaunchKernelGGL(k_linear<1>, dim3(blocks), dim3(256), 0, 0, v, y, n16, nslices); });
+    }
+    const int64_t b4 = (nslices + 3) / 4;
+    run("slice_ro", false, [&] { hipLaunchKernelGGL((k_slice<0, 4, 1>), dim3(b4), dim3(256), 0, 0, v, y, nslices); });
+    run("slice_w", true, [&] { hipLaunchKernelGGL((k_slice<1, 4, 1>), dim3(b4), dim3(256), 0, 0, v, y, nslices); });
+    run("slice_wnt", true, [&] { hipLaunchKernelGGL((k_slice<2, 4, 1>), dim3(b4), dim3(256), 0, 0, v, y, nslices); });
+    run("slice_b64", true, [&] { hipLaunchKernelGGL((k_slice<1, 1, 1>), dim3(nslices), dim3(64), 0, 0, v, y, nslices); });
+    run("slice_2", true, [&] { hipLaunchKernelGGL((k_slice<1, 4, 2>), dim3((nslices + 7) / 8), dim3(256), 0, 0, v, y, nslices); });
+  }
+  CK(hipFree(v));
+  CK(hipFree(y));
+  return 0;
+}
