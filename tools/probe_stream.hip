@@ -10,6 +10,8 @@
 //   slice_2    slice_w with two slices per wave (grid halved)
 //   (with a 3rd argument) write-only sweeps of y / of 3.57 GB, memset, and
 //   slice_w with y folded into a 1 / 16 / 64 MB ring
+//   (3rd argument "e") persistent blocks staging y in LDS per epoch of C
+//   slices and writing it in one burst, with or without a grid barrier
 // hipcc --offload-arch=gfx950 -O3 tools/probe_stream.hip -o probe_stream
 #include <hip/hip_runtime.h>
 #include <algorithm>
@@ -93,6 +95,43 @@ __global__ __launch_bounds__(256) void k_slice_ring(const u32x4* __restrict__ v,
   y[(s * 64 + lane) & ((1ll << RINGLOG) - 1)] = acc;
 }
 
+// Persistent blocks of 16 waves (one per CU): epoch e of block b streams the
+// C consecutive slices [(e*nb + b)*C, +C), stages their y (1 KB each) in LDS
+// and writes the C KB at once after the block's waves finish the epoch.
+// SYNC: all blocks meet at a grid barrier before the write burst, so the
+// whole GPU reads, then writes (the barrier gives up after 2^18 polls:
+// never a hang, only a wrong time).
+__device__ unsigned g_bar[2];
+template <int C, bool SYNC>
+__global__ __launch_bounds__(1024) void k_slice_epoch(const u32x4* __restrict__ v, u32x4* __restrict__ y,
+                                                      int64_t nslices) {
+  __shared__ u32x4 sy[C * 64];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int64_t nb = gridDim.x;
+  const int64_t nep = (nslices + nb * C - 1) / (nb * C);
+  for (int64_t e = 0; e < nep; ++e) {
+    const int64_t s0 = (e * nb + blockIdx.x) * C;
+    for (int j = wv; j < C; j += 16)
+      if (s0 + j < nslices) sy[j * 64 + lane] = stream_slice(v, s0 + j, lane);
+    __syncthreads();
+    if (SYNC) {
+      if (threadIdx.x == 0) {
+        __threadfence();
+        const unsigned target = (unsigned)((e + 1) * nb);
+        atomicAdd(&g_bar[0], 1u);
+        for (int it = 0; it < (1 << 18); ++it)
+          if (__hip_atomic_load(&g_bar[0], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) >= target) break;
+      }
+      __syncthreads();
+    }
+    for (int i = threadIdx.x; i < C * 64; i += 1024)
+      if (s0 + i / 64 < nslices) y[s0 * 64 + i] = sy[i];
+    __syncthreads();
+  }
+}
+
+__global__ void k_bar_reset() { g_bar[0] = 0; g_bar[1] = 0; }
+
 template <int WRITE>
 __global__ __launch_bounds__(256) void k_linear(const u32x4* __restrict__ v, u32x4* __restrict__ y,
                                                 int64_t n16, int64_t nslices) {
@@ -146,6 +185,27 @@ int main(int argc, char** argv) {
                 ms[ms.size() / 2], ms[0], bytes / (ms[ms.size() / 2] * 1e-3) / 1e9);
     std::fflush(stdout);
   };
+  if (argc > 3 && argv[3][0] == 'e') {  // epoch-staged y variants
+    int ncu = 256;
+    {
+      hipDeviceProp_t pr;
+      CK(hipGetDeviceProperties(&pr, 0));
+      ncu = pr.multiProcessorCount;
+    }
+    const int64_t b4 = (nslices + 3) / 4;
+    for (int round = 0; round < 2; ++round) {
+      run("slice_ro", false, [&] { hipLaunchKernelGGL((k_slice<0, 4, 1>), dim3(b4), dim3(256), 0, 0, v, y, nslices); });
+      run("slice_w", true, [&] { hipLaunchKernelGGL((k_slice<1, 4, 1>), dim3(b4), dim3(256), 0, 0, v, y, nslices); });
+      run("epoch128_nosync", true, [&] { hipLaunchKernelGGL((k_slice_epoch<128, false>), dim3(ncu), dim3(1024), 0, 0, v, y, nslices); });
+      run("epoch32_nosync", true, [&] { hipLaunchKernelGGL((k_slice_epoch<32, false>), dim3(ncu), dim3(1024), 0, 0, v, y, nslices); });
+      run("epoch128_sync", true, [&] {
+        hipLaunchKernelGGL(k_bar_reset, dim3(1), dim3(1), 0, 0);
+        void* args[] = {(void*)&v, (void*)&y, (void*)&nslices};
+        CK(hipLaunchCooperativeKernel((const void*)k_slice_epoch<128, true>, dim3(ncu), dim3(1024), args, 0, 0));
+      });
+    }
+    return 0;
+  }
   if (argc > 3) {  // write-side variants only
     const int64_t yn16 = (int64_t)ybytes / 16;
     u32x4* big;
