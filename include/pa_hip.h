@@ -211,6 +211,22 @@ int pa_mat_from_csc(pa_ctx* ctx, int dtype, int index_bytes,
                     const void* colptr, const void* rowval, const void* nzval,
                     const pa_index* rows, const pa_index* cols,
                     pa_mat** out);
+/* From the local SparseMatrixCSR{Bi} of one part (SparseUtils.jl:189-252;
+ * PSparseMatrix(sparsecsr, I, J, V, rows, cols; ids), Interfaces.jl:
+ * 2194-2215 with a CSR init): rowptr (nrows_lids+1) and colval hold
+ * Bi-based indices (Bi = 0 or 1, index_bytes 4 or 8), nzval in storage
+ * order.  Same SELL layout as pa_mat_from_csc; each owned row keeps its
+ * owned-column entries in storage order, then its ghost-column entries in
+ * storage order (the owned_owned then owned_ghost passes of
+ * SparseUtils.jl:242-250), and mul! with α != 1 scales each product,
+ * (v*x)*α, as SparseUtils.jl:247 does (a CSC parent scales x, :177).
+ * pa_mat_set_values / pa_mat_get_values / pa_mat_xchg_create index the CSR
+ * nonzeros.                                                             */
+int pa_mat_from_csr(pa_ctx* ctx, int dtype, int index_bytes, int Bi,
+                    int64_t nrows_lids, int64_t ncols_lids,
+                    const void* rowptr, const void* colval, const void* nzval,
+                    const pa_index* rows, const pa_index* cols,
+                    pa_mat** out);
 /* From COO triplets: PSparseMatrix(I, J, V, rows, cols; ids=:local)
  * (Interfaces.jl:2194-2244) → sparse(I, J, V, m, n, +) (SparseUtils.jl:
  * 80-94) on the device (stable radix sort, duplicates summed in input

@@ -1032,6 +1032,61 @@ def csc_mul_sub_(C, A: CSC, rows_inv, cols_list, rflag, cflag, B, alpha, beta):
     return C
 
 
+@dataclass
+class CSR:
+    """SparseMatrixCSR{Bi} (SparseMatricesCSR.jl, a dependency not vendored
+    in /root/reference): rowptr and colval hold Bi-based indices (Bi = 0 or
+    1), getoffset(A) = 1 - Bi (SparseUtils.jl:212), nzval in row order."""
+    Bi: int
+    m: int
+    n: int
+    rowptr: np.ndarray
+    colval: np.ndarray
+    nzval: object
+
+
+def sparse_csr(Bi, I, J, V, m, n) -> CSR:
+    """compresscoo(SparseMatrixCSR{Bi}, I, J, V, m, n) SparseUtils.jl:193-208
+    → sparsecsr(Val(Bi), I, J, V, m, n, +).  SparseMatricesCSR's published
+    algorithm: the CSC of the transpose, sparse(J, I, V, n, m, +), read as
+    rows — duplicates combined with + in input order, columns sorted within
+    each row — with its 1-based indices shifted to base Bi.  Pinned by
+    SparseUtilsTests.jl:62-65 (compresscoo(T,…) == sparse(I,J,V), nziterator
+    order = findnz order, nzindex, the sub-matrix mul! against the dense
+    product)."""
+    assert Bi in (0, 1)
+    t = sparse_csc(J, I, V, n, m)
+    return CSR(Bi, m, n, (t.colptr - 1 + Bi).astype(np.int64), (t.rowval - 1 + Bi).astype(np.int64), t.nzval)
+
+
+def csr_nzrange(A: CSR, I):
+    """nzrange(A, I) for SparseMatrixCSR{Bi}: rowptr[I]+o : rowptr[I+1]-Bi
+    (1-based positions; SparseUtils.jl:214-215)"""
+    o = 1 - A.Bi
+    return range(int(A.rowptr[I - 1]) + o, int(A.rowptr[I]) - A.Bi + 1)
+
+
+def csr_mul_sub_(C, A: CSR, rows_list, cols_inv, rflag, cflag, B, alpha, beta):
+    """mul!(C, A::SubSparseMatrix{<:SparseMatrixCSR}, B, α, β)
+    SparseUtils.jl:222-252, literally: rows in view order, each row's entries
+    in storage order, `C[i] += nzv[p]*B[j]*α` — the product first, then α
+    (the CSC twin scales x first, :177).  rows_list = A.indices[1] (1-based
+    parent row ids), cols_inv = invcols (lid_to_ohid)."""
+    if not (beta == 1):
+        for i in range(len(C)):
+            C[i] = C[i] * beta if beta != 0 else _zero_elem(C[i])
+    nzv = A.nzval
+    o = 1 - A.Bi
+    for i, Ir in enumerate(rows_list, start=1):
+        for p in csr_nzrange(A, Ir):
+            Jc = int(A.colval[p - 1]) + o
+            j = cols_inv[Jc - 1] * cflag
+            if j > 0:
+                t = _get(nzv, p - 1) * B[j - 1]
+                C[i - 1] = C[i - 1] + (t if _is_one(alpha) else t * alpha)
+    return C
+
+
 def _zero_elem(v):
     """zero(eltype(C)) for one element (numpy scalar or Cx)"""
     if isinstance(v, Cx):
@@ -1051,13 +1106,15 @@ class PSparseMatrix:
     exchanger: Exchanger = None
 
 
-def psparse_from_coo(I: PData, J: PData, V: PData, rows: PRange, cols: PRange, ids="local"):
-    """PSparseMatrix(I,J,V,rows,cols; ids) Interfaces.jl:2194-2215 with
-    init = sparse (2237-2244)."""
+def psparse_from_coo(I: PData, J: PData, V: PData, rows: PRange, cols: PRange, ids="local", init=None):
+    """PSparseMatrix(init,I,J,V,rows,cols; ids) Interfaces.jl:2194-2215;
+    init = sparse by default (2237-2244), or e.g.
+    `lambda i, j, v, m, n: sparse_csr(Bi, i, j, v, m, n)` (sparsecsr)."""
     if ids == "global":
         to_lids_pr_(I, rows)
         to_lids_pr_(J, cols)
-    vals = map_parts(lambda i, j, v, r, c: sparse_csc(i, j, v, r.num_lids, c.num_lids), I, J, V,
+    init = init or sparse_csc
+    vals = map_parts(lambda i, j, v, r, c: init(i, j, v, r.num_lids, c.num_lids), I, J, V,
                      rows.partition, cols.partition)
     return PSparseMatrix(vals, rows, cols, matrix_exchanger(vals, rows, cols))  # Interfaces.jl:2117
 
@@ -1071,6 +1128,10 @@ def mul_(c: PVector, a: PSparseMatrix, b: PVector, alpha=1.0, beta=0.0, literal=
     if literal:
         def part(cv, A, bv, r, ac, bc, cr):
             C = _OwnedView(cv, cr.oid_to_lid)
+            if isinstance(A, CSR):  # owned_owned then owned_ghost views (Interfaces.jl:2142-2156)
+                csr_mul_sub_(C, A, r.oid_to_lid, ac.lid_to_ohid, 1, 1, _OwnedView(bv, bc.oid_to_lid), alpha, beta)
+                csr_mul_sub_(C, A, r.oid_to_lid, ac.lid_to_ohid, 1, -1, _OwnedView(bv, bc.hid_to_lid), alpha, 1)
+                return
             csc_mul_sub_(C, A, r.lid_to_ohid, ac.oid_to_lid, 1, 1, _OwnedView(bv, bc.oid_to_lid), alpha, beta)
             csc_mul_sub_(C, A, r.lid_to_ohid, ac.hid_to_lid, 1, -1, _OwnedView(bv, bc.hid_to_lid), alpha, 1)
         map_parts(part, c.values, a.values, b.values, a.rows.partition, a.cols.partition,
@@ -1096,11 +1157,33 @@ class _OwnedView:
         return len(self.lids)
 
 
+def split_rows_csr(A: CSR, rows: IndexSet, cols: IndexSet):
+    """split_rows for a CSR parent (SparseUtils.jl:242-250 over owned_owned,
+    then owned_ghost): each owned row's owned-column entries in storage
+    order, then its ghost-column entries in storage order."""
+    oid = np.asarray(rows.oid_to_lid, dtype=np.int64)
+    if len(oid) == 0:
+        z = np.zeros(0, np.int64)
+        return z, z, z
+    o = 1 - A.Bi
+    starts = A.rowptr[oid - 1] + o - 1          # 0-based first position of each owned row
+    cnt = A.rowptr[oid] - A.Bi - (A.rowptr[oid - 1] + o) + 1
+    rep = np.repeat(np.arange(len(oid)), cnt)
+    pos = np.repeat(starts, cnt) + (np.arange(cnt.sum()) - np.repeat(np.cumsum(cnt) - cnt, cnt))
+    lid = A.colval[pos] + o
+    ohid = np.asarray(cols.lid_to_ohid, dtype=np.int64)[lid - 1]
+    ghost = (ohid < 0).astype(np.int64)
+    k = np.lexsort((np.arange(len(pos)), ghost, rep))
+    return (rep + 1)[k], lid[k], pos[k]
+
+
 def split_rows(A: CSC, rows: IndexSet, cols: IndexSet):
     """Owned rows of the local CSC as per-row entry lists in the reference's
     summation order (SparseUtils.jl:176-185 applied to owned_owned then
     owned_ghost, Interfaces.jl:2142-2156): returns (row_oid, col_lid, nz_pos)
     sorted by (row, order) where order = own cols by oid, then ghost cols by hid."""
+    if isinstance(A, CSR):
+        return split_rows_csr(A, rows, cols)
     row_ohid = np.asarray(rows.lid_to_ohid, dtype=np.int64)
     cols_seq = [(cols.oid_to_lid, 0), (cols.hid_to_lid, len(cols.oid_to_lid))]
     R, Cc, P, K = [], [], [], []
@@ -1149,19 +1232,35 @@ def _spmv_part_vec(cv, A, bv, rows, acols, bcols, crows, alpha, beta):
             return np.zeros_like(y)
         return y if beta == 1 else y * beta
     if cx:
-        acc = Cx(init(cv.re), init(cv.im))
+        if isinstance(beta, Cx):  # a complex β: rmul!(co, β) with Julia's complex product
+            yr, yi = cv.re[ylid], cv.im[ylid]
+            if beta.re == 0 and beta.im == 0:
+                acc = Cx(np.zeros_like(yr), np.zeros_like(yi))
+            elif beta.re == 1 and beta.im == 0:
+                acc = Cx(yr, yi)
+            else:
+                acc = Cx(yr * beta.re - yi * beta.im, yr * beta.im + yi * beta.re)
+        else:
+            acc = Cx(init(cv.re), init(cv.im))
         xr, xi = bv.re[xl], bv.im[xl]
+        csr = isinstance(A, CSR)  # CSR: (v*x)*α (SparseUtils.jl:247); CSC: v*(x*α) (:177, 182)
         if not _is_one(alpha):
             a = alpha if isinstance(alpha, Cx) else Cx(alpha, 0 * alpha)
-            xr, xi = xr * a.re - xi * a.im, xr * a.im + xi * a.re
+            if not csr:
+                xr, xi = xr * a.re - xi * a.im, xr * a.im + xi * a.re
         vr, vi = A.nzval.re[pos], A.nzval.im[pos]
         pr, pi = vr * xr - vi * xi, vr * xi + vi * xr
+        if csr and not _is_one(alpha):
+            pr, pi = pr * a.re - pi * a.im, pr * a.im + pi * a.re
     else:
         acc = init(cv)
         xv = bv[xl]
-        if not _is_one(alpha):
+        csr = isinstance(A, CSR)
+        if not _is_one(alpha) and not csr:
             xv = xv * alpha
         pr = A.nzval[pos] * xv
+        if not _is_one(alpha) and csr:
+            pr = pr * alpha
     maxlen = int(counts.max()) if nrows and len(r_oid) else 0
     for t in range(maxlen):
         sel = np.flatnonzero(counts > t)
@@ -1352,8 +1451,9 @@ def assemble_coo_(I: PData, J: PData, V: PData, rows: PRange):
     return I, J, V2
 
 
-def fem_sa_problem(parts: PData, nx=10):
-    """test_fem_sa.jl:7-132 (2D Q1 FE, Dirichlet u = 1): returns (A, b, x0, x̂)."""
+def fem_sa_problem(parts: PData, nx=10, init=None):
+    """test_fem_sa.jl:7-132 (2D Q1 FE, Dirichlet u = 1): returns (A, b, x0, x̂).
+    init: the local matrix constructor (sparse by default, or sparse_csr)."""
     lx = 2.0
     ns = (nx, nx)
     h = lx / nx
@@ -1397,7 +1497,7 @@ def fem_sa_problem(parts: PData, nx=10):
                     bv[lid - 1] += 1.0
     map_parts(fill_b, b.values, rows.partition, cells.partition)
     add_gids_(cols, J)
-    A = psparse_from_coo(I, J, V, rows, cols, ids="global")
+    A = psparse_from_coo(I, J, V, rows, cols, ids="global", init=init)
     assemble_(b)
     x0 = pvector_undef(cols)
     xh = pvector_undef(cols)
@@ -1497,7 +1597,7 @@ def stencil_row_entries(kind, N, g, coef):
     return out
 
 
-def stencil_problem(parts: PData, N: tuple, kind: int, dtype=np.float64):
+def stencil_problem(parts: PData, N: tuple, kind: int, dtype=np.float64, init=None):
     """Row-wise assembly of the Cartesian stencil operator (FD7 or FE27) on a
     Cartesian PRange (test_fdm.jl's driver structure: each part pushes the
     COO entries of its owned rows, J in row order then stencil order; cols =
@@ -1520,7 +1620,7 @@ def stencil_problem(parts: PData, N: tuple, kind: int, dtype=np.float64):
     cols = add_gids(rows, J)
     to_lids_pr_(J, cols)
     V = map_parts(lambda v: _convert_values(v, dtype), V)
-    A = psparse_from_coo(I, J, V, rows, cols, ids="local")
+    A = psparse_from_coo(I, J, V, rows, cols, ids="local", init=init)
     return A
 
 
@@ -1615,7 +1715,7 @@ def to_lids_vec(ids, a: IndexSet):
     return o[i] + 1
 
 
-def irregular_problem(parts: PData, N: tuple, kind=27, dtype=np.float64, owners=None):
+def irregular_problem(parts: PData, N: tuple, kind=27, dtype=np.float64, owners=None, init=None):
     """C5 on the oracle: rows = IndexSets of the owned gids in gid order
     (IndexSets.jl:215-291), gid_to_part = owner map; COO of owned rows with
     global ids; cols = add_gids(rows, J) (first touch); psparse with
@@ -1644,14 +1744,29 @@ def irregular_problem(parts: PData, N: tuple, kind=27, dtype=np.float64, owners=
     Il = map_parts(to_lids_vec, I, rows.partition)
     Jl = map_parts(to_lids_vec, J, cols.partition)
     V = map_parts(lambda v: _convert_values(v, dtype), V)
-    return psparse_from_coo(Il, Jl, V, rows, cols, ids="local")
+    return psparse_from_coo(Il, Jl, V, rows, cols, ids="local", init=init)
 
 
 # ---------------------------------------------------------------------------
 # Matrix nonzero exchange
 
-def nzindex(A: CSC, i0, i1):
-    """nzindex(A::SparseMatrixCSC, i0, i1) SparseUtils.jl:96-104 (-1 if absent)"""
+def nzindex(A, i0, i1):
+    """nzindex(A::SparseMatrixCSC, i0, i1) SparseUtils.jl:96-104 (-1 if absent);
+    for a CSR parent SparseUtils.jl:210-220"""
+    if isinstance(A, CSR):
+        o = 1 - A.Bi
+        r1, r2 = int(A.rowptr[i0 - 1]) + o, int(A.rowptr[i0]) - A.Bi
+        if r1 > r2:
+            return -1
+        key = i1 - o
+        lo, hi = r1, r2 + 1  # searchsortedfirst(colvals(A), i1-o, r1, r2)
+        while lo < hi:
+            mid = (lo + hi) // 2
+            if A.colval[mid - 1] < key:
+                lo = mid + 1
+            else:
+                hi = mid
+        return lo if lo <= r2 and A.colval[lo - 1] == key else -1
     r1, r2 = int(A.colptr[i1 - 1]), int(A.colptr[i1]) - 1
     if r1 > r2:
         return -1
@@ -1665,9 +1780,15 @@ def nzindex(A: CSC, i0, i1):
     return lo if lo <= r2 and A.rowval[lo - 1] == i0 else -1
 
 
-def nz_entries(A: CSC):
-    """nziterator(A) for CSC (SparseUtils.jl:106-150): (k, li, lj) in storage order"""
+def nz_entries(A):
+    """nziterator(A) for CSC (SparseUtils.jl:106-150), or for CSR
+    (SparseUtils.jl:254-300, row by row): (k, li, lj) in storage order"""
     out = []
+    if isinstance(A, CSR):
+        for i in range(1, A.m + 1):
+            for k in csr_nzrange(A, i):
+                out.append((k, i, int(A.colval[k - 1]) + 1 - A.Bi))
+        return out
     for j in range(1, A.n + 1):
         for k in range(int(A.colptr[j - 1]), int(A.colptr[j])):
             out.append((k, int(A.rowval[k - 1]), j))

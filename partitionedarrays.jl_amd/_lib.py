@@ -58,6 +58,7 @@ _SIGS = {
     "pa_vec_copy": [_p, _p, _p, _p, C.c_int],
     "pa_vec_axpby": [_p, _p, _p, _p, C.c_int, C.c_int],
     "pa_mat_from_csc": [_p, C.c_int, C.c_int, C.c_int64, C.c_int64, _p, _p, _p, _p, _p, C.POINTER(_p)],
+    "pa_mat_from_csr": [_p, C.c_int, C.c_int, C.c_int, C.c_int64, C.c_int64, _p, _p, _p, _p, _p, C.POINTER(_p)],
     "pa_coo_create": [_p, C.c_int, C.c_int64, _i64p, _i64p, _p, C.POINTER(_p)],
     "pa_coo_destroy": [_p],
     "pa_coo_size": [_p, _i64p],

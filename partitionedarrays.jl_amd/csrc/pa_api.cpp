@@ -1406,62 +1406,35 @@ int pa_vec_axpby(pa_vec* y, const pa_vec* x, const pa_index* idx, const void* a,
 }
 
 // ---------------------------------------------------------------------------
-// CSC → owned-row SELL (one time, host side).  Loop order is the reference's
-// (SparseUtils.jl:176-185 over owned_owned then owned_ghost): columns in oid
-// order, then in hid order; each row's entries are appended in that order.
-int pa_mat_from_csc(pa_ctx* c, int dtype, int index_bytes, int64_t nrows_lids, int64_t ncols_lids,
-                    const void* colptr, const void* rowval, const void* nzval, const pa_index* rows,
-                    const pa_index* cols, pa_mat** out) {
-  CHECK_ARG(c && out && rows && cols, "null argument");
-  CHECK_ARG(valid_dtype(dtype), "invalid dtype");
-  CHECK_ARG(index_bytes == 4 || index_bytes == 8, "index_bytes must be 4 or 8");
-  CHECK_ARG(rows->nlids == nrows_lids && cols->nlids == ncols_lids,
-            "matrix size must be num_lids(rows) x num_lids(cols) (DimensionMismatch)");
-  HIPC(hipSetDevice(c->device));
-  auto cp = [&](int64_t j) -> int64_t {
-    return index_bytes == 8 ? ((const int64_t*)colptr)[j] : ((const int32_t*)colptr)[j];
-  };
-  auto rv = [&](int64_t p) -> int64_t {
-    return index_bytes == 8 ? ((const int64_t*)rowval)[p] : ((const int32_t*)rowval)[p];
-  };
-  const int64_t csc_nnz = ncols_lids > 0 ? cp(ncols_lids) - 1 : 0;
-  CHECK_ARG(csc_nnz >= 0, "colptr[end] must be >= 1");
+// Local matrix → owned-row SELL (one time, host side).  `visit(f)` calls
+// f(row oid (0-based), x lid (0-based), input nz position, ghost column?)
+// for every owned-row entry, each row's entries in the reference's
+// summation order (owned columns, then ghost columns; SparseUtils.jl:176-185
+// for a CSC parent, 242-250 for a CSR parent), and returns -1 on an index
+// out of range.  The input's other nonzeros (stored ghost rows) are kept
+// after the slots for exchange!/assemble!(A); nz positions index nzval.
+extern "C++" {
+namespace {
+template <class Visit>
+int mat_from_visit(pa_ctx* c, int dtype, int64_t nrows_lids, int64_t ncols_lids, int64_t in_nnz,
+                   const void* nzval, const pa_index* rows, const pa_index* cols, Visit&& visit,
+                   const char* range_error, bool csr, pa_mat** out) {
   const size_t S = dtype_size(dtype);
   pa_mat* A = new pa_mat();
+  A->csr = csr;
   A->ctx = c;
   A->dtype = dtype;
   A->R = sell_rows_per_lane(dtype);
   A->H = 64 * A->R;
   A->nrows = rows->noids;
   A->ncols_lids = ncols_lids;
-  A->csc_nnz = csc_nnz;
+  A->csc_nnz = in_nnz;
   const int64_t nr = A->nrows;
   std::vector<int32_t> len(nr, 0);
   std::vector<char> has_ghost(nr, 0);
-  auto visit = [&](auto&& f) -> int {
-    for (int64_t j = 0; j < cols->noids; ++j) {
-      const int64_t J = cols->h_oid_to_lid[j];
-      for (int64_t p = cp(J) - 1; p < cp(J + 1) - 1; ++p) {
-        const int64_t I = rv(p) - 1;
-        if (I < 0 || I >= nrows_lids) return -1;
-        const int32_t o = rows->h_lid_to_ohid[I];
-        if (o > 0) f(o - 1, J, p, false);
-      }
-    }
-    for (int64_t h = 0; h < cols->nhids; ++h) {
-      const int64_t J = cols->h_hid_to_lid[h];
-      for (int64_t p = cp(J) - 1; p < cp(J + 1) - 1; ++p) {
-        const int64_t I = rv(p) - 1;
-        if (I < 0 || I >= nrows_lids) return -1;
-        const int32_t o = rows->h_lid_to_ohid[I];
-        if (o > 0) f(o - 1, J, p, true);
-      }
-    }
-    return 0;
-  };
   if (visit([&](int64_t r, int64_t, int64_t, bool g) { ++len[r]; if (g) has_ghost[r] = 1; })) {
     delete A;
-    PA_FAIL("CSC rowval out of range");
+    PA_FAIL(range_error);
   }
   const int64_t ns = (nr + A->H - 1) / A->H;
   // long rows (row-length histogram) leave the SELL
@@ -1491,8 +1464,8 @@ int pa_mat_from_csc(pa_ctx* c, int dtype, int index_bytes, int64_t nrows_lids, i
   std::vector<unsigned char> hval(A->slots * S, 0);
   std::vector<int32_t> lcol(A->n_lnz);
   std::vector<unsigned char> lval(A->n_lnz * S);
-  std::vector<int64_t> lpos(csc_nnz, -1);  // CSC nz → position in the long CSR
-  A->h_nz_slot.assign(csc_nnz, -1);
+  std::vector<int64_t> lpos(in_nnz, -1);  // input nz → position in the long CSR
+  A->h_nz_slot.assign(in_nnz, -1);
   A->nz_map = true;
   std::vector<int32_t> cur(nr, 0);
   const int R = A->R;
@@ -1515,13 +1488,13 @@ int pa_mat_from_csc(pa_ctx* c, int dtype, int index_bytes, int64_t nrows_lids, i
   });
   // ghost-row nonzeros (dropped by the SpMV, kept for exchange!/assemble!(A)),
   // then the long rows' values: both after the SELL slots in d_val
-  for (int64_t p = 0; p < csc_nnz; ++p)
+  for (int64_t p = 0; p < in_nnz; ++p)
     if (A->h_nz_slot[p] < 0 && lpos[p] < 0) A->h_nz_slot[p] = -(++A->n_gnz);
   A->long_off = A->slots + A->n_gnz;
-  for (int64_t p = 0; p < csc_nnz; ++p)
+  for (int64_t p = 0; p < in_nnz; ++p)
     if (lpos[p] >= 0) A->h_nz_slot[p] = -(A->n_gnz + lpos[p] + 1);
   hval.resize(nvals(A) * S);
-  for (int64_t p = 0; p < csc_nnz; ++p)
+  for (int64_t p = 0; p < in_nnz; ++p)
     if (A->h_nz_slot[p] < 0 && lpos[p] < 0)
       std::memcpy(&hval[(A->slots - A->h_nz_slot[p] - 1) * S], (const unsigned char*)nzval + p * S, S);
   if (A->n_lnz) std::memcpy(&hval[A->long_off * S], lval.data(), A->n_lnz * S);
@@ -1539,6 +1512,94 @@ int pa_mat_from_csc(pa_ctx* c, int dtype, int index_bytes, int64_t nrows_lids, i
   }
   *out = A;
   return 0;
+}
+
+}  // namespace
+}  // extern "C++"
+
+// CSC parent: columns in oid order, then in hid order; each row's entries
+// are appended in that order.
+int pa_mat_from_csc(pa_ctx* c, int dtype, int index_bytes, int64_t nrows_lids, int64_t ncols_lids,
+                    const void* colptr, const void* rowval, const void* nzval, const pa_index* rows,
+                    const pa_index* cols, pa_mat** out) {
+  CHECK_ARG(c && out && rows && cols, "null argument");
+  CHECK_ARG(valid_dtype(dtype), "invalid dtype");
+  CHECK_ARG(index_bytes == 4 || index_bytes == 8, "index_bytes must be 4 or 8");
+  CHECK_ARG(rows->nlids == nrows_lids && cols->nlids == ncols_lids,
+            "matrix size must be num_lids(rows) x num_lids(cols) (DimensionMismatch)");
+  HIPC(hipSetDevice(c->device));
+  auto cp = [&](int64_t j) -> int64_t {
+    return index_bytes == 8 ? ((const int64_t*)colptr)[j] : ((const int32_t*)colptr)[j];
+  };
+  auto rv = [&](int64_t p) -> int64_t {
+    return index_bytes == 8 ? ((const int64_t*)rowval)[p] : ((const int32_t*)rowval)[p];
+  };
+  const int64_t csc_nnz = ncols_lids > 0 ? cp(ncols_lids) - 1 : 0;
+  CHECK_ARG(csc_nnz >= 0, "colptr[end] must be >= 1");
+  auto visit = [&](auto&& f) -> int {
+    for (int64_t j = 0; j < cols->noids; ++j) {
+      const int64_t J = cols->h_oid_to_lid[j];
+      for (int64_t p = cp(J) - 1; p < cp(J + 1) - 1; ++p) {
+        const int64_t I = rv(p) - 1;
+        if (I < 0 || I >= nrows_lids) return -1;
+        const int32_t o = rows->h_lid_to_ohid[I];
+        if (o > 0) f(o - 1, J, p, false);
+      }
+    }
+    for (int64_t h = 0; h < cols->nhids; ++h) {
+      const int64_t J = cols->h_hid_to_lid[h];
+      for (int64_t p = cp(J) - 1; p < cp(J + 1) - 1; ++p) {
+        const int64_t I = rv(p) - 1;
+        if (I < 0 || I >= nrows_lids) return -1;
+        const int32_t o = rows->h_lid_to_ohid[I];
+        if (o > 0) f(o - 1, J, p, true);
+      }
+    }
+    return 0;
+  };
+  return mat_from_visit(c, dtype, nrows_lids, ncols_lids, csc_nnz, nzval, rows, cols, visit,
+                        "CSC rowval out of range", false, out);
+}
+
+// CSR parent (SparseMatrixCSR{Bi}): rows in oid order; each row's owned
+// columns in storage order, then its ghost columns in storage order
+// (SparseUtils.jl:242-250 over owned_owned, then owned_ghost).
+int pa_mat_from_csr(pa_ctx* c, int dtype, int index_bytes, int Bi, int64_t nrows_lids, int64_t ncols_lids,
+                    const void* rowptr, const void* colval, const void* nzval, const pa_index* rows,
+                    const pa_index* cols, pa_mat** out) {
+  CHECK_ARG(c && out && rows && cols, "null argument");
+  CHECK_ARG(valid_dtype(dtype), "invalid dtype");
+  CHECK_ARG(index_bytes == 4 || index_bytes == 8, "index_bytes must be 4 or 8");
+  CHECK_ARG(Bi == 0 || Bi == 1, "Bi (index base) must be 0 or 1");
+  CHECK_ARG(rows->nlids == nrows_lids && cols->nlids == ncols_lids,
+            "matrix size must be num_lids(rows) x num_lids(cols) (DimensionMismatch)");
+  HIPC(hipSetDevice(c->device));
+  auto rp = [&](int64_t i) -> int64_t {
+    return (index_bytes == 8 ? ((const int64_t*)rowptr)[i] : ((const int32_t*)rowptr)[i]) - Bi;
+  };
+  auto cv = [&](int64_t p) -> int64_t {
+    return (index_bytes == 8 ? ((const int64_t*)colval)[p] : ((const int32_t*)colval)[p]) - Bi;
+  };
+  CHECK_ARG(nrows_lids == 0 || rp(0) == 0, "rowptr[1] must equal Bi");
+  const int64_t csr_nnz = nrows_lids > 0 ? rp(nrows_lids) : 0;
+  CHECK_ARG(csr_nnz >= 0, "rowptr[end] must be >= Bi");
+  for (int64_t i = 0; i < nrows_lids; ++i)
+    CHECK_ARG(rp(i) <= rp(i + 1), "rowptr must be nondecreasing");
+  auto visit = [&](auto&& f) -> int {
+    for (int pass = 0; pass < 2; ++pass)
+      for (int64_t o = 0; o < rows->noids; ++o) {
+        const int64_t I = rows->h_oid_to_lid[o];
+        for (int64_t p = rp(I); p < rp(I + 1); ++p) {
+          const int64_t J = cv(p);
+          if (J < 0 || J >= ncols_lids) return -1;
+          const int32_t oh = cols->h_lid_to_ohid[J];
+          if (pass == 0 ? oh > 0 : oh < 0) f(o, J, p, pass == 1);
+        }
+      }
+    return 0;
+  };
+  return mat_from_visit(c, dtype, nrows_lids, ncols_lids, csr_nnz, nzval, rows, cols, visit,
+                        "CSR colval out of range", true, out);
 }
 
 // sparse(I, J, V, m, n, +) (SparseUtils.jl:80-94) and the SELL build on the

@@ -393,6 +393,7 @@ struct pa_mat {
   int64_t slots = 0;         // SELL slots incl. padding
   int64_t nslices = 0;
   int64_t nslices_int = 0;   // slices without ghost-column entries
+  bool csr = false;          // built from a SparseMatrixCSR: α scales each product, (v*x)*α (SparseUtils.jl:247)
   std::vector<int32_t> h_slen;      // host copies for pa_mat_traffic: int32-layout slice lengths,
   std::vector<int32_t> h_kind;      // pattern-layout slice kinds (0 int32, 1 pattern, 2 multi-pattern)
   std::vector<int32_t> h_plen;      // and entries per row of each pattern-layout slice

@@ -43,7 +43,7 @@ __device__ inline int64_t xcd_remap(int64_t b, int64_t G) {
 }
 
 enum { SPMV_NT = 1, SPMV_XCD = 2, SPMV_XPAIR = 4, SPMV_TAILB = 8, SPMV_IDLIST = 16, SPMV_YNT = 32, SPMV_SHORT = 64,
-       SPMV_XRUN = 128 };
+       SPMV_XRUN = 128, SPMV_PRODA = 256 /* per matrix: CSR parent, α scales the product */ };
 typedef unsigned int spmv_u32x4 __attribute__((ext_vector_type(4)));
 // Process-wide knobs (pa_tune).  Defaults from the A/Bs in
 // profiles/r01_ab_spmv.txt and profiles/r01/ab_xpair.txt: non-temporal
@@ -172,13 +172,23 @@ __device__ __forceinline__ void gather_x(T (&xv)[R], const int32_t (&c)[R], cons
   for (int r = 0; r < R; ++r) xv[r] = x[c[r] >= 0 ? c[r] : 0];
 }
 
+// One term of a row's sum.  A CSC parent scales x first, v*(x*α)
+// (SparseUtils.jl:177, 182); a CSR parent scales the product, (v*x)*α
+// (SparseUtils.jl:247: nzv[p]*B[j]*α).  ALPHA false (α == 1): v*x either way.
+template <bool ALPHA, typename T>
+__device__ __forceinline__ T term(T v, T x, T alpha, bool pf) {
+  if (!ALPHA) return v * x;
+  if (pf) return (v * x) * alpha;
+  return v * (x * alpha);
+}
+
 // int32-column rows: c < 0 is padding (skipped: never multiplied)
 // TB: the entries past the last full U batch run as one masked batch
 // (entries >= len re-read entry len-1 and are never accumulated)
 template <typename T, int R, bool ALPHA, bool NT, int U, bool SH = false>
 __device__ __forceinline__ void rows_int32(T (&acc)[R], const IPack<R>* __restrict__ cp,
                                            const Pack<T, R>* __restrict__ vp, int len,
-                                           const T* __restrict__ x, T alpha, bool TB, bool xrun) {
+                                           const T* __restrict__ x, T alpha, bool pf, bool TB, bool xrun) {
   int k = 0;
   if (SH) TB = true;  // short rows (len <= U): the one masked batch is the whole row
   for (; !SH && k + U <= len; k += U) {
@@ -195,9 +205,7 @@ __device__ __forceinline__ void rows_int32(T (&acc)[R], const IPack<R>* __restri
     for (int u = 0; u < U; ++u)
 #pragma unroll
       for (int r = 0; r < R; ++r) {
-        T xx = xv[u][r];
-        if (ALPHA) xx = xx * alpha;
-        const T t = acc[r] + v[u].v[r] * xx;
+        const T t = acc[r] + term<ALPHA>(v[u].v[r], xv[u][r], alpha, pf);
         acc[r] = pick(c[u].c[r] >= 0, t, acc[r]);
       }
   }
@@ -220,9 +228,7 @@ __device__ __forceinline__ void rows_int32(T (&acc)[R], const IPack<R>* __restri
     for (int u = 0; u < U; ++u)
 #pragma unroll
       for (int r = 0; r < R; ++r) {
-        T xx = xv[u][r];
-        if (ALPHA) xx = xx * alpha;
-        const T t = acc[r] + v[u].v[r] * xx;
+        const T t = acc[r] + term<ALPHA>(v[u].v[r], xv[u][r], alpha, pf);
         acc[r] = pick(k + u < len && c[u].c[r] >= 0, t, acc[r]);
       }
     k = len;
@@ -233,9 +239,7 @@ __device__ __forceinline__ void rows_int32(T (&acc)[R], const IPack<R>* __restri
 #pragma unroll
     for (int r = 0; r < R; ++r) {
       const int32_t cc = c.c[r];
-      T xx = x[cc >= 0 ? cc : 0];
-      if (ALPHA) xx = xx * alpha;
-      const T t = acc[r] + v.v[r] * xx;
+      const T t = acc[r] + term<ALPHA>(v.v[r], x[cc >= 0 ? cc : 0], alpha, pf);
       acc[r] = pick(cc >= 0, t, acc[r]);
     }
   }
@@ -253,7 +257,7 @@ __device__ __forceinline__ int32_t d16_col(uint32_t q, int32_t row, int32_t gb) 
 template <typename T, int R, bool ALPHA, bool NT, int U, bool SH = false>
 __device__ __forceinline__ void rows_d16(T (&acc)[R], const S16Pack<R>* __restrict__ cp,
                                          const Pack<T, R>* __restrict__ vp, int len,
-                                         const T* __restrict__ x, T alpha, bool TB, int32_t row0, int32_t gb,
+                                         const T* __restrict__ x, T alpha, bool pf, bool TB, int32_t row0, int32_t gb,
                                          bool xrun) {
   int k = 0;
   if (SH) TB = true;
@@ -276,9 +280,7 @@ __device__ __forceinline__ void rows_d16(T (&acc)[R], const S16Pack<R>* __restri
     for (int u = 0; u < U; ++u)
 #pragma unroll
       for (int r = 0; r < R; ++r) {
-        T xx = xv[u][r];
-        if (ALPHA) xx = xx * alpha;
-        const T t = acc[r] + v[u].v[r] * xx;
+        const T t = acc[r] + term<ALPHA>(v[u].v[r], xv[u][r], alpha, pf);
         acc[r] = pick(c[u][r] >= 0, t, acc[r]);
       }
   }
@@ -305,9 +307,7 @@ __device__ __forceinline__ void rows_d16(T (&acc)[R], const S16Pack<R>* __restri
     for (int u = 0; u < U; ++u)
 #pragma unroll
       for (int r = 0; r < R; ++r) {
-        T xx = xv[u][r];
-        if (ALPHA) xx = xx * alpha;
-        const T t = acc[r] + v[u].v[r] * xx;
+        const T t = acc[r] + term<ALPHA>(v[u].v[r], xv[u][r], alpha, pf);
         acc[r] = pick(k + u < len && c[u][r] >= 0, t, acc[r]);
       }
     k = len;
@@ -318,9 +318,7 @@ __device__ __forceinline__ void rows_d16(T (&acc)[R], const S16Pack<R>* __restri
 #pragma unroll
     for (int r = 0; r < R; ++r) {
       const int32_t cc = d16_col(q.c[r], row0 + r, gb);
-      T xx = x[cc >= 0 ? cc : 0];
-      if (ALPHA) xx = xx * alpha;
-      const T t = acc[r] + v.v[r] * xx;
+      const T t = acc[r] + term<ALPHA>(v.v[r], x[cc >= 0 ? cc : 0], alpha, pf);
       acc[r] = pick(cc >= 0, t, acc[r]);
     }
   }
@@ -333,7 +331,7 @@ template <typename T, int R, bool ALPHA, bool NT, int U, bool XP, bool SH = fals
 __device__ __forceinline__ void rows_pattern(T (&acc)[R], const int32_t* __restrict__ pat,
                                              const Pack<T, R>* __restrict__ vp, int len,
                                              const T* __restrict__ x, int64_t rbase,
-                                             const bool (&ok)[R], T alpha, bool TB) {
+                                             const bool (&ok)[R], T alpha, bool pf, bool TB) {
   if (SH) TB = true;  // short rows (len <= U): the one masked batch is the whole row
   int64_t xb[R];
   bool any = false;
@@ -368,9 +366,7 @@ __device__ __forceinline__ void rows_pattern(T (&acc)[R], const int32_t* __restr
     for (int u = 0; u < U; ++u)
 #pragma unroll
       for (int r = 0; r < R; ++r) {
-        T xx = xv[u][r];
-        if (ALPHA) xx = xx * alpha;
-        acc[r] = acc[r] + v[u].v[r] * xx;
+        acc[r] = acc[r] + term<ALPHA>(v[u].v[r], xv[u][r], alpha, pf);
       }
   }
   if (TB && k < len) {  // masked tail batch, as in rows_int32
@@ -402,9 +398,7 @@ __device__ __forceinline__ void rows_pattern(T (&acc)[R], const int32_t* __restr
       if (k + u < len) {
 #pragma unroll
         for (int r = 0; r < R; ++r) {
-          T xx = xv[u][r];
-          if (ALPHA) xx = xx * alpha;
-          acc[r] = acc[r] + v[u].v[r] * xx;
+          acc[r] = acc[r] + term<ALPHA>(v[u].v[r], xv[u][r], alpha, pf);
         }
       }
     k = len;
@@ -414,9 +408,7 @@ __device__ __forceinline__ void rows_pattern(T (&acc)[R], const int32_t* __restr
     const Pack<T, R> v = ld<NT>(&vp[k * 64]);
 #pragma unroll
     for (int r = 0; r < R; ++r) {
-      T xx = x[xb[r] >= 0 ? xb[r] + o : 0];
-      if (ALPHA) xx = xx * alpha;
-      acc[r] = acc[r] + v.v[r] * xx;
+      acc[r] = acc[r] + term<ALPHA>(v.v[r], x[xb[r] >= 0 ? xb[r] + o : 0], alpha, pf);
     }
   }
 }
@@ -472,6 +464,7 @@ __device__ __forceinline__ void spmv_wave(const SpmvArgs<T>& a, const int64_t w)
 
   const Pack<T, R>* __restrict__ vp = reinterpret_cast<const Pack<T, R>*>(a.val + off) + lane;
   const bool tb = (a.flags & SPMV_TAILB) != 0;
+  const bool pf = (a.flags & SPMV_PRODA) != 0;
   if constexpr (PK == 2) {
     // this wave's patterns → LDS; each lane reads its own pattern's offsets
     __shared__ int32_t spat[4][PA_MP_NP * PA_MP_K];
@@ -483,32 +476,32 @@ __device__ __forceinline__ void spmv_wave(const SpmvArgs<T>& a, const int64_t w)
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     const int32_t* pat = wp + (int)a.psel[s * 64 + lane] * a.kmax;
     if (a.flags & SPMV_XPAIR) {
-      if (a.flags & SPMV_NT) rows_pattern<T, R, ALPHA, true, U, true, SH>(acc, pat, vp, len, a.x, row0, ok, a.alpha, tb);
-      else rows_pattern<T, R, ALPHA, false, U, true, SH>(acc, pat, vp, len, a.x, row0, ok, a.alpha, tb);
+      if (a.flags & SPMV_NT) rows_pattern<T, R, ALPHA, true, U, true, SH>(acc, pat, vp, len, a.x, row0, ok, a.alpha, pf, tb);
+      else rows_pattern<T, R, ALPHA, false, U, true, SH>(acc, pat, vp, len, a.x, row0, ok, a.alpha, pf, tb);
     } else {
-      if (a.flags & SPMV_NT) rows_pattern<T, R, ALPHA, true, U, false, SH>(acc, pat, vp, len, a.x, row0, ok, a.alpha, tb);
-      else rows_pattern<T, R, ALPHA, false, U, false, SH>(acc, pat, vp, len, a.x, row0, ok, a.alpha, tb);
+      if (a.flags & SPMV_NT) rows_pattern<T, R, ALPHA, true, U, false, SH>(acc, pat, vp, len, a.x, row0, ok, a.alpha, pf, tb);
+      else rows_pattern<T, R, ALPHA, false, U, false, SH>(acc, pat, vp, len, a.x, row0, ok, a.alpha, pf, tb);
     }
   } else if constexpr (PK == 1) {
     const int32_t* pat = a.pat + s * a.kmax;
     if (a.flags & SPMV_XPAIR) {
-      if (a.flags & SPMV_NT) rows_pattern<T, R, ALPHA, true, U, true, SH>(acc, pat, vp, len, a.x, row0, ok, a.alpha, tb);
-      else rows_pattern<T, R, ALPHA, false, U, true, SH>(acc, pat, vp, len, a.x, row0, ok, a.alpha, tb);
+      if (a.flags & SPMV_NT) rows_pattern<T, R, ALPHA, true, U, true, SH>(acc, pat, vp, len, a.x, row0, ok, a.alpha, pf, tb);
+      else rows_pattern<T, R, ALPHA, false, U, true, SH>(acc, pat, vp, len, a.x, row0, ok, a.alpha, pf, tb);
     } else {
-      if (a.flags & SPMV_NT) rows_pattern<T, R, ALPHA, true, U, false, SH>(acc, pat, vp, len, a.x, row0, ok, a.alpha, tb);
-      else rows_pattern<T, R, ALPHA, false, U, false, SH>(acc, pat, vp, len, a.x, row0, ok, a.alpha, tb);
+      if (a.flags & SPMV_NT) rows_pattern<T, R, ALPHA, true, U, false, SH>(acc, pat, vp, len, a.x, row0, ok, a.alpha, pf, tb);
+      else rows_pattern<T, R, ALPHA, false, U, false, SH>(acc, pat, vp, len, a.x, row0, ok, a.alpha, pf, tb);
     }
   } else if constexpr (PK == 3) {
     const S16Pack<R>* __restrict__ cp = reinterpret_cast<const S16Pack<R>*>(a.col16 + off) + lane;
     const int32_t gb = a.gbase[s];
     const bool xrun = (a.flags & SPMV_XRUN) != 0;
-    if (a.flags & SPMV_NT) rows_d16<T, R, ALPHA, true, U, SH>(acc, cp, vp, len, a.x, a.alpha, tb, (int32_t)row0, gb, xrun);
-    else rows_d16<T, R, ALPHA, false, U, SH>(acc, cp, vp, len, a.x, a.alpha, tb, (int32_t)row0, gb, xrun);
+    if (a.flags & SPMV_NT) rows_d16<T, R, ALPHA, true, U, SH>(acc, cp, vp, len, a.x, a.alpha, pf, tb, (int32_t)row0, gb, xrun);
+    else rows_d16<T, R, ALPHA, false, U, SH>(acc, cp, vp, len, a.x, a.alpha, pf, tb, (int32_t)row0, gb, xrun);
   } else {
     const IPack<R>* __restrict__ cp = reinterpret_cast<const IPack<R>*>(a.col + off) + lane;
     const bool xrun = (a.flags & SPMV_XRUN) != 0;
-    if (a.flags & SPMV_NT) rows_int32<T, R, ALPHA, true, U, SH>(acc, cp, vp, len, a.x, a.alpha, tb, xrun);
-    else rows_int32<T, R, ALPHA, false, U, SH>(acc, cp, vp, len, a.x, a.alpha, tb, xrun);
+    if (a.flags & SPMV_NT) rows_int32<T, R, ALPHA, true, U, SH>(acc, cp, vp, len, a.x, a.alpha, pf, tb, xrun);
+    else rows_int32<T, R, ALPHA, false, U, SH>(acc, cp, vp, len, a.x, a.alpha, pf, tb, xrun);
   }
 
   if (a.dotp) {  // fused dot(u, c): Σ conj(u_i)·c_i over this slice's rows
@@ -648,7 +641,7 @@ static SpmvArgs<T> make_args(int which, int64_t nwork, const int32_t* list, cons
   a.ymap = ymap;
   a.alpha = *(const T*)alpha;
   a.beta = *(const T*)beta;
-  a.flags = g_spmv_flags;
+  a.flags = g_spmv_flags | (A->csr ? SPMV_PRODA : 0);
   a.maxlen = which == 0   ? A->maxlen_pat
              : which == 2 ? A->maxlen_side
              : which == 1 ? ((g_spmv_format == 1 && A->has_pat) ? A->maxlen_pm_int : A->maxlen_all)
@@ -926,7 +919,7 @@ __global__ __launch_bounds__(64) void k_spmv_long_exact(int64_t nlong, const int
                                                         const int64_t* __restrict__ lptr,
                                                         const int32_t* __restrict__ lcol, const T* __restrict__ lval,
                                                         const T* __restrict__ x, T* __restrict__ y,
-                                                        const int32_t* __restrict__ ymap, T alpha, T beta,
+                                                        const int32_t* __restrict__ ymap, T alpha, bool pf, T beta,
                                                         const T* __restrict__ dotu, void* dotp, int64_t dot_base) {
   constexpr int U = 8, B = U * 64;
   __shared__ T buf[B];
@@ -946,9 +939,7 @@ __global__ __launch_bounds__(64) void k_spmv_long_exact(int64_t nlong, const int
       const int64_t k = b + u * 64 + lane;
       T q = zero_of<T>();
       if (k < b1) {
-        T xx = x[lcol[k]];
-        if (ALPHA) xx = xx * alpha;
-        q = lval[k] * xx;
+        q = term<ALPHA>(lval[k], x[lcol[k]], alpha, pf);
       }
       p[u] = q;
     }
@@ -989,7 +980,7 @@ __global__ __launch_bounds__(256) void k_spmv_long_chunks(int64_t nchunks, const
                                                           const int64_t* __restrict__ cend,
                                                           const int32_t* __restrict__ lcol,
                                                           const T* __restrict__ lval, const T* __restrict__ x,
-                                                          T alpha, T* __restrict__ part) {
+                                                          T alpha, bool pf, T* __restrict__ part) {
   constexpr int U = 8;
   const int lane = threadIdx.x & 63;
   const int64_t c = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -1003,9 +994,7 @@ __global__ __launch_bounds__(256) void k_spmv_long_chunks(int64_t nchunks, const
       const int64_t k = b + u * 64 + lane;
       q[u] = zero_of<T>();
       if (k < b1) {
-        T xx = x[lcol[k]];
-        if (ALPHA) xx = xx * alpha;
-        q[u] = lval[k] * xx;
+        q[u] = term<ALPHA>(lval[k], x[lcol[k]], alpha, pf);
       }
     }
 #pragma unroll
@@ -1044,12 +1033,12 @@ static void long_t(const pa_mat* A, const void* x, void* y, const int32_t* ymap,
   const T al = *(const T*)alpha, be = *(const T*)beta;
   if (g_long_exact) {
     hipLaunchKernelGGL((k_spmv_long_exact<T, ALPHA, BMODE>), dim3((unsigned)A->n_long), dim3(64), 0, st, A->n_long,
-                       A->d_long_row, A->d_long_ptr, A->d_long_col, val, (const T*)x, (T*)y, ymap, al, be,
+                       A->d_long_row, A->d_long_ptr, A->d_long_col, val, (const T*)x, (T*)y, ymap, al, A->csr, be,
                        (const T*)x, dotp, dot_base);
   } else {
     hipLaunchKernelGGL((k_spmv_long_chunks<T, ALPHA>), dim3((unsigned)((A->n_lchunks + 3) / 4)), dim3(256), 0, st,
                        A->n_lchunks, A->d_lchunk_start, A->d_lchunk_start + 1, A->d_long_col, val, (const T*)x, al,
-                       (T*)A->d_lpart);
+                       A->csr, (T*)A->d_lpart);
     hipLaunchKernelGGL((k_spmv_long_fold<T, BMODE>), dim3((unsigned)((A->n_long + 63) / 64)), dim3(64), 0, st,
                        A->n_long, A->d_long_row, A->d_lrow_chunk, (const T*)A->d_lpart, (T*)y, ymap, be,
                        (const T*)x, dotp, dot_base);

@@ -381,6 +381,21 @@ class DeviceMatrix:
         return M
 
     @staticmethod
+    def from_csr(ctx: PartContext, csr, rows_idx: DeviceIndex, cols_idx: DeviceIndex, nrows_lids, ncols_lids):
+        """From a local SparseMatrixCSR{Bi} (pa_mat_from_csr): its nonzero
+        order (set/get values, nz exchange) is the CSR storage order."""
+        rowptr = np.ascontiguousarray(csr.rowptr, dtype=np.int64)
+        colval = np.ascontiguousarray(csr.colval, dtype=np.int64)
+        nzval = np.ascontiguousarray(csr.nzval)
+        h = C.c_void_p()
+        _lib.call("pa_mat_from_csr", ctx.h, _lib.DTYPES[nzval.dtype], 8, int(csr.Bi), nrows_lids, ncols_lids,
+                  rowptr.ctypes.data_as(C.c_void_p), colval.ctypes.data_as(C.c_void_p),
+                  nzval.ctypes.data_as(C.c_void_p), rows_idx.h, cols_idx.h, C.byref(h))
+        M = DeviceMatrix(h, ctx, nzval.dtype)
+        M.csc_nnz = len(nzval)
+        return M
+
+    @staticmethod
     def from_coo(ctx: PartContext, I, J, V, rows_idx: DeviceIndex, cols_idx: DeviceIndex, nrows_lids, ncols_lids,
                  ids_global=False, pattern=True):
         """sparse(I, J, V, m, n, +) and the SELL build on the device

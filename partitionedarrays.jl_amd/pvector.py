@@ -63,6 +63,37 @@ def compresscoo(I, J, V, m, n) -> CSC:
     return CSC(m, n, colptr, Is[starts], acc)
 
 
+class CSR:
+    """SparseMatrixCSR{Bi,T,Int64} (SparseUtils.jl:189-300): rowptr and
+    colval hold Bi-based indices (Bi = 0 or 1), nzval in row order."""
+
+    def __init__(self, Bi, m, n, rowptr, colval, nzval):
+        if Bi not in (0, 1):
+            raise ValueError("SparseMatrixCSR: Bi must be 0 or 1")
+        self.Bi, self.m, self.n = int(Bi), int(m), int(n)
+        self.rowptr = np.asarray(rowptr, dtype=np.int64)
+        self.colval = np.asarray(colval, dtype=np.int64)
+        self.nzval = np.asarray(nzval)
+
+    @property
+    def nnz(self):
+        return int(self.rowptr[-1] - self.Bi)
+
+
+def sparsecsr(Bi, I, J, V, m, n) -> CSR:
+    """compresscoo(SparseMatrixCSR{Bi}, I, J, V, m, n) (SparseUtils.jl:
+    193-208) → sparsecsr(Val(Bi), I, J, V, m, n, +): the CSC of the
+    transposed triplets read as rows (duplicates combined with + in input
+    order, columns ascending within rows), indices shifted to base Bi."""
+    t = compresscoo(J, I, V, n, m)
+    return CSR(Bi, m, n, t.colptr - 1 + Bi, t.rowval - 1 + Bi, t.nzval)
+
+
+def csr_init(Bi):
+    """init for PSparseMatrix.from_coo: sparsecsr with index base Bi"""
+    return lambda I, J, V, m, n: sparsecsr(Bi, I, J, V, m, n)
+
+
 # ---------------------------------------------------------------------------
 # PVector
 
@@ -344,10 +375,38 @@ class PSparseMatrix:
                                    rows.partition.shape), rows, cols, ex)
 
     @staticmethod
-    def from_coo(I, J, V, rows: PRange, cols: PRange, ids="local"):
-        """PSparseMatrix(I, J, V, rows, cols; ids) (Interfaces.jl:2194-2215,
-        sparse init).  I, J, V: PData of host arrays, or I a device COO (then
-        J and V are None)."""
+    def from_csr(csr: PData, rows: PRange, cols: PRange) -> "PSparseMatrix":
+        """From each part's local SparseMatrixCSR{Bi} (num_lids(rows) ×
+        num_lids(cols)); mul! then follows SparseUtils.jl:222-252."""
+        ctxs = contexts(rows.partition)
+        mats = []
+        for c, A, r, s in zip(ctxs, csr.parts, rows.partition.parts, cols.partition.parts):
+            mats.append(DeviceMatrix.from_csr(c, A, device_index(c, r), device_index(c, s),
+                                              r.num_lids, s.num_lids))
+        ex = matrix_exchanger(csr, rows, cols)
+        return PSparseMatrix(PData(rows.partition.backend, rows.partition.part_ids, mats,
+                                   rows.partition.shape), rows, cols, ex)
+
+    @staticmethod
+    def from_coo(I, J, V, rows: PRange, cols: PRange, ids="local", init=None):
+        """PSparseMatrix(init, I, J, V, rows, cols; ids) (Interfaces.jl:
+        2194-2215).  init None = sparse (2237-2244), on the device; I, J, V:
+        PData of host arrays, or I a device COO (then J and V are None).
+        Another init (e.g. csr_init(Bi), sparsecsr) compresses each part's
+        host triplets with it and uploads the result."""
+        if init is not None:
+            if isinstance(I, COO):
+                raise NotImplementedError("from_coo: a custom init needs host triplets")
+            if ids == "global":
+                I = map_parts(lambda i, r: r.to_lids(np.asarray(i, dtype=np.int64)), I, rows.partition)
+                J = map_parts(lambda j, c: c.to_lids(np.asarray(j, dtype=np.int64)), J, cols.partition)
+            loc = map_parts(lambda i, j, v, r, c: init(i, j, v, r.num_lids, c.num_lids), I, J, V,
+                            rows.partition, cols.partition)
+            if all(isinstance(m, CSR) for m in loc.parts):
+                return PSparseMatrix.from_csr(loc, rows, cols)
+            if all(isinstance(m, CSC) for m in loc.parts):
+                return PSparseMatrix.from_csc(loc, rows, cols)
+            raise TypeError("from_coo: init must return CSC or CSR local matrices")
         # to_lids! (ids=:global) and sparse(I, J, V) on the device
         # (pa_mat_from_coo); the host keeps the CSC pattern only, for
         # matrix_exchanger
@@ -393,10 +452,16 @@ def matrix_exchanger(values: PData, rows: PRange, cols: PRange) -> Exchanger:
     parts_rcv = rows.exchanger.parts_rcv
     parts_snd = rows.exchanger.parts_snd
 
+    def nz_lids(A):
+        """0-based (row, col) lids of the nonzeros in storage order
+        (nziterator, SparseUtils.jl:106-150 for CSC, 254-300 for CSR)"""
+        if isinstance(A, CSR):
+            return np.repeat(np.arange(A.m), np.diff(A.rowptr)), A.colval - A.Bi
+        return A.rowval - 1, np.repeat(np.arange(A.n), np.diff(A.colptr))
+
     def setup_rcv(prcv, r, c, A):
         prcv = np.asarray(prcv, dtype=np.int64)
-        li = A.rowval - 1
-        lj = np.repeat(np.arange(A.n), np.diff(A.colptr))
+        li, lj = nz_lids(A)
         owner = r.lid_to_part[li].astype(np.int64)
         k = np.flatnonzero(owner != r.part)
         seg = np.searchsorted(prcv, owner[k])
@@ -419,9 +484,13 @@ def matrix_exchanger(values: PData, rows: PRange, cols: PRange) -> Exchanger:
         gj = np.concatenate(gj).astype(np.int64) if gj else np.zeros(0, np.int64)
         li = r.to_lids(gi) - 1
         lj = c.to_lids(gj) - 1
-        # nzindex(A, li, lj) (SparseUtils.jl:96-104): CSC order is sorted by (col, row)
-        key = np.repeat(np.arange(A.n, dtype=np.int64), np.diff(A.colptr)) * A.m + (A.rowval - 1)
-        q = lj * A.m + li
+        # nzindex(A, li, lj): CSC order is sorted by (col, row) (SparseUtils.jl:
+        # 96-104), CSR order by (row, col) (210-220)
+        ri, rj = nz_lids(A)
+        if isinstance(A, CSR):
+            key, q = ri.astype(np.int64) * A.n + rj, li * A.n + lj
+        else:
+            key, q = rj.astype(np.int64) * A.m + ri, lj * A.m + li
         pos = np.searchsorted(key, q)
         ok = (pos < len(key)) & (key[np.minimum(pos, max(len(key) - 1, 0))] == q) if len(key) else pos < 0
         if not np.all(ok):

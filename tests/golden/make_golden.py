@@ -109,6 +109,15 @@ K["sparse_utils"] = {
     "rows": [4, 2, 3], "cols": [6, 2, 5, 1],
     "dense_nonzeros": {"1,3": 9, "2,6": 5, "5,1": 3, "4,1": 2},
 }
+# SparseUtilsTests.jl:62-65: the same test_mat for SparseMatrixCSR{1} and
+# {0} (Float64/Int, Float32/Int32): compresscoo(T, I, J, V, m, n) == A, the
+# nziterator order equals findnz's (row by row for CSR: the sparsity of A
+# above listed row-major), nzindex(B, i, j) == k, the sub-matrix mul! ≈ dense
+K["sparse_utils_csr"] = {
+    "src": "test/SparseUtilsTests.jl:9-65 (test_mat on SparseMatrixCSR{Bi})",
+    "types": [[1, "f64", "i64"], [1, "f32", "i32"], [0, "f64", "i64"], [0, "f32", "i32"]],
+    "findnz_order": [[1, 3, 9], [2, 6, 5], [4, 1, 2], [5, 1, 3]],
+}
 # test_fdm.jl:118 / test_fem_sa.jl:137
 K["solvers"] = {"src": "test/test_fdm.jl:118, test/test_fem_sa.jl:137", "err_tol": 1e-5,
                 "fdm_nx": 10, "fdm_nnz": 4072}

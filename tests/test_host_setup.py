@@ -317,3 +317,48 @@ def test_prange_with_ghost_matches_oracle(pamd, O, shape, ngids, periodic):
         assert list(ex.parts_snd.local(p)) == list(oex.parts_snd[p])
         assert ex.lids_rcv.local(p).tolist() == oex.lids_rcv[p].tolist()
         assert ex.lids_snd.local(p).tolist() == oex.lids_snd[p].tolist()
+
+
+@pytest.mark.parametrize("Bi", [0, 1])
+@pytest.mark.parametrize("dtype", [np.float64, np.float32, np.complex128])
+def test_sparsecsr_matches_oracle(pamd, O, Bi, dtype):
+    """sparsecsr(Val(Bi), I, J, V, m, n, +) (SparseUtils.jl:193-208): the
+    host compress equals the oracle's (duplicates in input order, columns
+    ascending in each row, indices in base Bi)."""
+    rng = np.random.default_rng(17)
+    m, n, k = 40, 33, 600
+    I, J = rng.integers(1, m + 1, k), rng.integers(1, n + 1, k)
+    V = rng.uniform(-1, 1, k) + (1j * rng.uniform(-1, 1, k) if np.dtype(dtype).kind == "c" else 0)
+    V = V.astype(dtype)
+    M = pamd.sparsecsr(Bi, I, J, V, m, n)
+    OV = O.Cx(V.real.copy(), V.imag.copy()) if np.iscomplexobj(V) else V.copy()
+    OM = O.sparse_csr(Bi, I, J, OV, m, n)
+    assert M.Bi == Bi and M.rowptr[0] == Bi
+    assert np.array_equal(M.rowptr, OM.rowptr) and np.array_equal(M.colval, OM.colval)
+    if np.iscomplexobj(V):
+        assert np.array_equal(M.nzval.real, OM.nzval.re) and np.array_equal(M.nzval.imag, OM.nzval.im)
+    else:
+        assert np.array_equal(M.nzval, OM.nzval)
+
+
+@pytest.mark.parametrize("Bi", [0, 1])
+@pytest.mark.parametrize("nparts", [4, (2, 2)])
+def test_matrix_exchanger_csr_matches_oracle(pamd, O, nparts, Bi):
+    """matrix_exchanger over SparseMatrixCSR parts (nzindex of
+    SparseUtils.jl:210-220, CSR storage order): equals the oracle's literal
+    matrix_exchanger on the same CSRs."""
+    parts = pamd.sequential.get_part_ids(nparts)
+    rows, cols, I, J, V, _, _, _ = pamd.drivers.fem_sa_host(parts, 10)
+    csr = pamd.map_parts(lambda i, j, v, r, c: pamd.sparsecsr(Bi, r.to_lids(i), c.to_lids(j), v, r.num_lids,
+                                                              c.num_lids), I, J, V, rows.partition, cols.partition)
+    ex = pamd.pvector.matrix_exchanger(csr, rows, cols)
+    OA, _, _, _ = O.fem_sa_problem(O.get_part_ids(nparts), 10, init=lambda i, j, v, m, n: O.sparse_csr(Bi, i, j, v, m, n))
+    oex = OA.exchanger
+    assert sum(len(oex.lids_rcv[p].data) for p in parts.part_ids) > 0
+    for p in parts.part_ids:
+        M, OM = csr.local(p), OA.values[p]
+        assert np.array_equal(M.rowptr, OM.rowptr) and np.array_equal(M.colval, OM.colval)
+        assert list(ex.parts_rcv.local(p)) == list(oex.parts_rcv[p])
+        assert list(ex.parts_snd.local(p)) == list(oex.parts_snd[p])
+        for a, b in ((ex.lids_rcv.local(p), oex.lids_rcv[p]), (ex.lids_snd.local(p), oex.lids_snd[p])):
+            assert a.data.tolist() == list(b.data) and a.ptrs.tolist() == list(b.ptrs)

@@ -260,3 +260,57 @@ def test_mul_literal_equals_vectorised(O):
                 assert np.array_equal(a.re, b.re) and np.array_equal(a.im, b.im)
             else:
                 assert np.array_equal(a, b)
+
+
+@pytest.mark.parametrize("Bi,tv", [(1, np.float64), (1, np.float32), (0, np.float64), (0, np.float32)])
+def test_sparse_utils_csr_kat(O, Bi, tv):
+    """SparseUtilsTests.jl:62-65: test_mat(SparseMatrixCSR{Bi,Tv,Ti})"""
+    k = GOLD["sparse_utils"]
+    kc = GOLD["sparse_utils_csr"]
+    B = O.sparse_csr(Bi, k["I"], k["J"], np.array(k["V"], dtype=tv), k["m"], k["n"])
+    assert B.nzval.dtype == tv
+    ents = O.nz_entries(B)
+    assert [[i, j, float(B.nzval[p - 1])] for p, i, j in ents] == kc["findnz_order"]
+    for p, i, j in ents:
+        assert O.nzindex(B, i, j) == p
+    assert O.nzindex(B, 3, 3) == -1 and O.nzindex(B, 1, 6) == -1
+    D = np.zeros((k["m"], k["n"]), dtype=tv)
+    for i, j, v in kc["findnz_order"]:
+        D[i - 1, j - 1] = v
+    rows, cols = k["rows"], k["cols"]
+    inv_cols = [0] * k["n"]
+    for j, c in enumerate(cols):
+        inv_cols[c - 1] = j + 1
+    x = np.random.default_rng(0).uniform(size=len(cols)).astype(tv)
+    y = np.zeros(len(rows), dtype=tv)
+    O.csr_mul_sub_(y, B, rows, inv_cols, 1, 1, x, tv(1), tv(0))
+    np.testing.assert_allclose(y, D[np.array(rows) - 1][:, np.array(cols) - 1] @ x, rtol=1e-6)
+
+
+def test_csr_partitioned_mul_literal_equals_vectorised(O):
+    """PSparseMatrix(sparsecsr, I, J, V, rows, cols): the vectorised mul!
+    equals the literal SparseUtils.jl:222-252 loop bit for bit, α = 1 equals
+    the CSC parent's result, α != 1 scales the product (SparseUtils.jl:247)."""
+    rng = np.random.default_rng(5)
+    for Bi in (0, 1):
+        for alpha, beta in ((1.0, 0.0), (0.7, 0.0), (-1.3, 0.5)):
+            outs = {}
+            for fmt in ("csc", "csr", "csr_lit"):
+                parts = O.get_part_ids((2, 2, 1))
+                init = None if fmt == "csc" else (lambda i, j, v, m, n: O.sparse_csr(Bi, i, j, v, m, n))
+                A = O.stencil_problem(parts, (7, 6, 5), 27, init=init)
+                xs = O.PVector(O.map_parts(lambda s: np.random.default_rng(s.part).uniform(-1, 1, s.num_lids),
+                                           A.cols.partition), A.cols)
+                y = O.PVector(O.map_parts(lambda s: np.random.default_rng(9 + s.part).uniform(-1, 1, s.num_lids),
+                                          A.rows.partition), A.rows)
+                O.mul_(y, A, xs, alpha, beta, literal=fmt == "csr_lit")
+                outs[fmt] = [v[np.asarray(s.oid_to_lid) - 1] for v, s in zip(y.values.parts, y.rows.partition.parts)]
+            for a, b in zip(outs["csr"], outs["csr_lit"]):
+                assert np.array_equal(a, b)
+            if alpha == 1.0:
+                for a, b in zip(outs["csr"], outs["csc"]):
+                    assert np.array_equal(a, b)
+            else:
+                for a, b in zip(outs["csr"], outs["csc"]):
+                    np.testing.assert_allclose(a, b, rtol=1e-12, atol=1e-12)
+    del rng
