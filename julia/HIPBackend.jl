@@ -31,6 +31,7 @@ module HIPBackends
 using PartitionedArrays
 using LinearAlgebra
 using SparseArrays
+using SparseMatricesCSR
 import IterativeSolvers
 import PartitionedArrays: get_part_ids, map_parts, i_am_main, get_backend, get_part, gather!,
   gather_all!, scatter, async_exchange!, async_assemble!, num_parts, prun_debug, PVector,
@@ -259,6 +260,19 @@ function mark_host_newer!(A::SparseMatrixCSC)
   m === nothing || (m.state = :host)
   nothing
 end
+function sync_host!(A::SparseMatrixCSR)
+  m = _mirror(MAT_MIRRORS, A)
+  if m !== nothing && m.state === :device
+    check(ccall((:pa_mat_get_values, libpa), Cint, (Ptr{Cvoid}, Ptr{Cvoid}), m.h, nonzeros(A)))
+    m.state = :both
+  end
+  nothing
+end
+function mark_host_newer!(A::SparseMatrixCSR)
+  m = _mirror(MAT_MIRRORS, A)
+  m === nothing || (m.state = :host)
+  nothing
+end
 sync_host!(A::PartitionedArrays.SubSparseMatrix) = sync_host!(A.parent)
 mark_host_newer!(A::PartitionedArrays.SubSparseMatrix) = mark_host_newer!(A.parent)
 
@@ -344,8 +358,33 @@ function _mat_handle(ctx::PartCtx, A::SparseMatrixCSC{Tv}, rows_h::Ptr{Cvoid}, c
   m.h
 end
 
+# a SparseMatrixCSR{Bi} part (SparseUtils.jl:189-300): pa_mat_from_csr keeps
+# the CSR's per-row order and scales each product by α, (v*x)*α (:247)
+function _mat_handle(ctx::PartCtx, A::SparseMatrixCSR{Bi,Tv}, rows_h::Ptr{Cvoid}, cols_h::Ptr{Cvoid}) where {Bi,Tv<:DeviceEltype}
+  m = _mirror(MAT_MIRRORS, A)
+  if m !== nothing && m.nnz != nnz(A)  # new pattern: rebuild
+    _free_mat(m)
+    m = nothing
+  end
+  if m === nothing
+    rowptr = Vector{Int64}(A.rowptr); colval = Vector{Int64}(A.colval)
+    out = Ref{Ptr{Cvoid}}(C_NULL)
+    check(ccall((:pa_mat_from_csr, libpa), Cint,
+                (Ptr{Cvoid}, Cint, Cint, Cint, Int64, Int64, Ptr{Int64}, Ptr{Int64}, Ptr{Cvoid},
+                 Ptr{Cvoid}, Ptr{Cvoid}, Ref{Ptr{Cvoid}}),
+                ctx.h, dtype_code(Tv), 8, Bi, size(A, 1), size(A, 2), rowptr, colval, nonzeros(A),
+                rows_h, cols_h, out))
+    m = _set_mirror!(MAT_MIRRORS, A, MatMirror(out[], nnz(A), :both), _free_mat)
+  elseif m.state === :host
+    check(ccall((:pa_mat_set_values, libpa), Cint, (Ptr{Cvoid}, Ptr{Cvoid}), m.h, nonzeros(A)))
+    m.state = :both
+  end
+  m.h
+end
+
 """pa_mat handles of the parts of `a` (owned-row SELL, built once from the
-local SparseMatrixCSC; values re-uploaded when the host copy is newer)."""
+local SparseMatrixCSC or SparseMatrixCSR; values re-uploaded when the host
+copy is newer)."""
 function dev_mat(a::PSparseMatrix)
   rh, ch = dev_idx(a.rows), dev_idx(a.cols)
   [_mat_handle(a.values.ctxs[i], a.values.parts[i], rh[i], ch[i]) for i in eachindex(a.values.parts)]
