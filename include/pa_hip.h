@@ -245,6 +245,24 @@ int pa_mat_from_coo(pa_ctx* ctx, int dtype, int index_bytes, int ids_global,
                     const pa_index* rows, const pa_index* cols,
                     int64_t* csc_nnz, int64_t* colptr_out,
                     int64_t* rowval_out, pa_mat** out);
+/* PSparseMatrix(sparsecsr, I, J, V, rows, cols; ids) with the compress on
+ * the device: pa_mat_from_coo / pa_mat_from_dcoo with a SparseMatrixCSR{Bi}
+ * parent — sparsecsr(Val(Bi), I, J, V, m, n, +) (SparseUtils.jl:193-208:
+ * duplicates combined with + in input order, columns ascending in each
+ * row), the matrix's nonzeros in CSR order and mul! with α applied to each
+ * product (SparseUtils.jl:247), as pa_mat_from_csr.  *nnz = nonzeros;
+ * rowptr_out (nrows_lids+1) / colval_out (>= ncoo), when non-NULL, receive
+ * the CSR pattern in base Bi.  Needs ascending oid_to_lid / hid_to_lid in
+ * cols (every PRange the reference builds).                              */
+int pa_mat_from_coo_csr(pa_ctx* ctx, int dtype, int index_bytes, int ids_global, int Bi,
+                        int64_t nrows_lids, int64_t ncols_lids, int64_t ncoo,
+                        const void* I, const void* J, const void* V,
+                        const pa_index* rows, const pa_index* cols, int64_t* nnz,
+                        int64_t* rowptr_out, int64_t* colval_out, pa_mat** out);
+int pa_mat_from_dcoo_csr(const pa_coo* coo, int ids_global, int Bi, int64_t nrows_lids,
+                         int64_t ncols_lids, const pa_index* rows, const pa_index* cols,
+                         int64_t* nnz, int64_t* rowptr_out, int64_t* colval_out,
+                         pa_mat** out);
 /* COO triplets of one part on the device: I, J global ids (Int64, 1-based),
  * V of dtype — the (I, J, V) of PSparseMatrix(I, J, V, rows, cols;
  * ids=:global), test_fem_sa.jl:60-131.                                  */

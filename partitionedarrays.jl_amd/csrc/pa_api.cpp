@@ -56,8 +56,8 @@ int g_halo_transport = 0;  // pa_tune("halo_transport"): 0 parts of this process
 int g_comm_cus = 0;   // pa_tune("comm_cus"): CUs reserved for the comm stream (0: priority stream instead)
 // COO → CSC → SELL on the device (pa_coo.hip)
 int coo_compress(int dtype, int index_bytes, int64_t m, int64_t ncols, int64_t n, const void* dI, const void* dJ,
-                 const void* dV, int64_t* nu_out, int32_t** crow, int32_t** ccol, void** cval, int64_t** colptr,
-                 hipStream_t st, hipError_t* err_out);
+                 const void* dV, int csr, int64_t* nu_out, int32_t** crow, int32_t** ccol, void** cval,
+                 int64_t** colptr, hipStream_t st, hipError_t* err_out);
 int coo_row_order(int64_t nu, const int32_t* crow, const int32_t* ccol, const int32_t* rl2o, const int32_t* cl2o,
                   int64_t nrows, int64_t noids_c, int64_t ncols, int H, uint64_t** key2, int64_t** idx2,
                   int64_t** rowptr, int64_t** gflag, int64_t** grank, int32_t** slen, int32_t** sghost,
@@ -108,6 +108,7 @@ void launch_stencil_count(const StencilGeom& g, const int32_t* shell, const doub
 void launch_stencil_fill(const StencilGeom& g, const int32_t* shell, const double* coef,
                          int64_t nrows, int noids, pa_mat* A, int32_t* err, hipStream_t st);
 void launch_probe(int copy, int unroll, int64_t n16, const void* a, void* b, int blocks, hipStream_t st);
+void launch_pattern_triples(const pa_mat* A, uint8_t* tri, hipStream_t st);
 extern int g_spmv_flags;
 extern int g_spmv_unroll;
 extern int g_spmv_lds;
@@ -362,6 +363,11 @@ int finalize_pattern(pa_mat* A, int kmax, int64_t noids) {
     }
   }
   A->h_kind = kind;
+  if (A->npattern_slices) {  // pattern slices of consecutive triples (lane-shared x runs)
+    HIPC(hipMalloc((void**)&A->d_ptri, ns));
+    launch_pattern_triples(A, A->d_ptri, st);
+    HIPC(hipGetLastError());
+  }
   A->maxlen_pat = A->maxlen_pm_int = A->maxlen_d16 = 0;
   for (int64_t s = 0; s < ns; ++s) {
     if (kind[s] == 1) A->maxlen_pat = std::max(A->maxlen_pat, (int)A->h_plen[s]);
@@ -777,11 +783,12 @@ int pa_tune(const char* key, int value, int* previous) {
   CHECK_ARG(key, "null key");
   int* slot = nullptr;
   if (!std::strcmp(key, "spmv_flags")) {
-    CHECK_ARG(value >= 0 && value <= 255,
+    CHECK_ARG(value >= 0 && (value & ~0x2ff) == 0,
               "spmv_flags: bit 0 = non-temporal streams, bit 1 = XCD mapping, bit 2 = 16 B x runs (pattern rows), "
               "bit 3 = masked tail batch, bit 4 = identity slice lists dropped, bit 5 = non-temporal y stores, "
               "bit 6 = short-row kernels (launches whose rows have <= 8 entries), bit 7 = 16 B x runs in "
-              "int32/delta16 slices where a lane's rows read consecutive columns");
+              "int32/delta16 slices where a lane's rows read consecutive columns, bit 9 = triple-pattern slices "
+              "share x runs between lanes (bit 8 is per matrix: CSR parent)");
     slot = &g_spmv_flags;
   } else if (!std::strcmp(key, "spmv_lds")) {
     CHECK_ARG(value >= 0 && value <= 160 * 1024, "spmv_lds: bytes of LDS per SpMV block (occupancy cap)");
@@ -1630,9 +1637,11 @@ struct DevBufs {
 namespace {
 // I, J, V: host arrays (kind H2D) or device arrays (D2D, pa_mat_from_dcoo);
 // either way they are copied first (to_lids! works in place).
+// csr_bi: -1 = sparse (CSC parent); 0 / 1 = sparsecsr with index base Bi
+// (the pattern returned is then rowptr / colval in base Bi)
 int mat_from_coo_impl(pa_ctx* c, int dtype, int index_bytes, int ids_global, int64_t nrows_lids,
                       int64_t ncols_lids, int64_t ncoo, const void* I, const void* J, const void* V,
-                      hipMemcpyKind kind, const pa_index* rows, const pa_index* cols, int64_t* csc_nnz,
+                      hipMemcpyKind kind, const pa_index* rows, const pa_index* cols, int csr_bi, int64_t* csc_nnz,
                       int64_t* colptr_out, int64_t* rowval_out, pa_mat** out);
 }  // namespace
 
@@ -1640,7 +1649,7 @@ int pa_mat_from_coo(pa_ctx* c, int dtype, int index_bytes, int ids_global, int64
                     int64_t ncoo, const void* I, const void* J, const void* V, const pa_index* rows,
                     const pa_index* cols, int64_t* csc_nnz, int64_t* colptr_out, int64_t* rowval_out, pa_mat** out) {
   return mat_from_coo_impl(c, dtype, index_bytes, ids_global, nrows_lids, ncols_lids, ncoo, I, J, V,
-                           hipMemcpyHostToDevice, rows, cols, csc_nnz, colptr_out, rowval_out, out);
+                           hipMemcpyHostToDevice, rows, cols, -1, csc_nnz, colptr_out, rowval_out, out);
 }
 
 int pa_mat_from_dcoo(const pa_coo* coo, int ids_global, int64_t nrows_lids, int64_t ncols_lids, const pa_index* rows,
@@ -1648,7 +1657,26 @@ int pa_mat_from_dcoo(const pa_coo* coo, int ids_global, int64_t nrows_lids, int6
   CHECK_ARG(coo, "null argument");
   CHECK_ARG(rows && rows->ctx == coo->ctx && cols && cols->ctx == coo->ctx, "COO and index sets of different parts");
   return mat_from_coo_impl(coo->ctx, coo->dtype, 8, ids_global, nrows_lids, ncols_lids, coo->n, coo->d_I, coo->d_J,
-                           coo->d_V, hipMemcpyDeviceToDevice, rows, cols, csc_nnz, colptr_out, rowval_out, out);
+                           coo->d_V, hipMemcpyDeviceToDevice, rows, cols, -1, csc_nnz, colptr_out, rowval_out, out);
+}
+
+int pa_mat_from_coo_csr(pa_ctx* c, int dtype, int index_bytes, int ids_global, int Bi, int64_t nrows_lids,
+                        int64_t ncols_lids, int64_t ncoo, const void* I, const void* J, const void* V,
+                        const pa_index* rows, const pa_index* cols, int64_t* nnz, int64_t* rowptr_out,
+                        int64_t* colval_out, pa_mat** out) {
+  CHECK_ARG(Bi == 0 || Bi == 1, "Bi (index base) must be 0 or 1");
+  return mat_from_coo_impl(c, dtype, index_bytes, ids_global, nrows_lids, ncols_lids, ncoo, I, J, V,
+                           hipMemcpyHostToDevice, rows, cols, Bi, nnz, rowptr_out, colval_out, out);
+}
+
+int pa_mat_from_dcoo_csr(const pa_coo* coo, int ids_global, int Bi, int64_t nrows_lids, int64_t ncols_lids,
+                         const pa_index* rows, const pa_index* cols, int64_t* nnz, int64_t* rowptr_out,
+                         int64_t* colval_out, pa_mat** out) {
+  CHECK_ARG(coo, "null argument");
+  CHECK_ARG(Bi == 0 || Bi == 1, "Bi (index base) must be 0 or 1");
+  CHECK_ARG(rows && rows->ctx == coo->ctx && cols && cols->ctx == coo->ctx, "COO and index sets of different parts");
+  return mat_from_coo_impl(coo->ctx, coo->dtype, 8, ids_global, nrows_lids, ncols_lids, coo->n, coo->d_I, coo->d_J,
+                           coo->d_V, hipMemcpyDeviceToDevice, rows, cols, Bi, nnz, rowptr_out, colval_out, out);
 }
 
 }  // extern "C"
@@ -1656,9 +1684,16 @@ int pa_mat_from_dcoo(const pa_coo* coo, int ids_global, int64_t nrows_lids, int6
 namespace {
 int mat_from_coo_impl(pa_ctx* c, int dtype, int index_bytes, int ids_global, int64_t nrows_lids,
                       int64_t ncols_lids, int64_t ncoo, const void* I, const void* J, const void* V,
-                      hipMemcpyKind kind, const pa_index* rows, const pa_index* cols, int64_t* csc_nnz,
+                      hipMemcpyKind kind, const pa_index* rows, const pa_index* cols, int csr_bi, int64_t* csc_nnz,
                       int64_t* colptr_out, int64_t* rowval_out, pa_mat** out) {
   CHECK_ARG(c && out && rows && cols && csc_nnz, "null argument");
+  const bool csr = csr_bi >= 0;
+  if (csr) {  // the row order below (owned columns by oid, ghosts by hid) is the CSR storage order
+    bool inc = true;  // when oid_to_lid and hid_to_lid ascend (every PRange / IndexSet the reference builds)
+    for (size_t k = 1; inc && k < cols->h_oid_to_lid.size(); ++k) inc = cols->h_oid_to_lid[k] > cols->h_oid_to_lid[k - 1];
+    for (size_t k = 1; inc && k < cols->h_hid_to_lid.size(); ++k) inc = cols->h_hid_to_lid[k] > cols->h_hid_to_lid[k - 1];
+    CHECK_ARG(inc, "sparsecsr on the device needs ascending oid_to_lid / hid_to_lid of cols (use pa_mat_from_csr)");
+  }
   CHECK_ARG(!ids_global || (index_bytes == 8 && rows->has_gids && cols->has_gids),
             "ids=:global needs Int64 ids and pa_index_set_gids on rows and cols");
   CHECK_ARG(ncoo >= 0 && (ncoo == 0 || (I && J && V)), "null COO arrays");
@@ -1696,22 +1731,24 @@ int mat_from_coo_impl(pa_ctx* c, int dtype, int index_bytes, int ids_global, int
   void* cval = nullptr;
   int64_t* dcolptr = nullptr;
   hipError_t e = hipSuccess;
-  const int rc = coo_compress(dtype, index_bytes, nrows_lids, ncols_lids, ncoo, dI, dJ, dV, &nu, &crow, &ccol,
-                              &cval, &dcolptr, st, &e);
+  const int rc = coo_compress(dtype, index_bytes, nrows_lids, ncols_lids, ncoo, dI, dJ, dV, csr ? 1 : 0, &nu, &crow,
+                              &ccol, &cval, &dcolptr, st, &e);
   if (rc < 0) HIPC(e);
   CHECK_ARG(rc == 0, "sparse: COO index out of range (BoundsError)");
   tmp.add(crow); tmp.add(ccol); tmp.add(cval); tmp.add(dcolptr);
   for (void*& q : inp.p) { dev_free(q); q = nullptr; }  // the COO input is no longer needed
   tr.mark("sparse (sort, combine)");
   *csc_nnz = nu;
-  if (colptr_out) {
-    HIPC(hipMemcpy(colptr_out, dcolptr, (ncols_lids + 1) * 8, hipMemcpyDeviceToHost));
-    for (int64_t j = 0; j <= ncols_lids; ++j) colptr_out[j] += 1;
+  const int64_t nptr = csr ? nrows_lids : ncols_lids;
+  const int64_t base = csr ? csr_bi : 1;
+  if (colptr_out) {  // colptr (CSC, 1-based) or rowptr (CSR, base Bi)
+    HIPC(hipMemcpy(colptr_out, dcolptr, (nptr + 1) * 8, hipMemcpyDeviceToHost));
+    for (int64_t j = 0; j <= nptr; ++j) colptr_out[j] += base;
   }
-  if (rowval_out && nu > 0) {
+  if (rowval_out && nu > 0) {  // rowval (CSC) or colval (CSR)
     std::vector<int32_t> rv(nu);
-    HIPC(hipMemcpy(rv.data(), crow, nu * 4, hipMemcpyDeviceToHost));
-    for (int64_t p = 0; p < nu; ++p) rowval_out[p] = (int64_t)rv[p] + 1;
+    HIPC(hipMemcpy(rv.data(), csr ? ccol : crow, nu * 4, hipMemcpyDeviceToHost));
+    for (int64_t p = 0; p < nu; ++p) rowval_out[p] = (int64_t)rv[p] + base;
   }
   tr.mark("CSC pattern to host");
   int32_t *rl2o = nullptr, *cl2o = nullptr;
@@ -1721,6 +1758,7 @@ int mat_from_coo_impl(pa_ctx* c, int dtype, int index_bytes, int ids_global, int
   pa_mat* A = new pa_mat();
   A->ctx = c;
   A->dtype = dtype;
+  A->csr = csr;
   A->R = sell_rows_per_lane(dtype);
   A->H = 64 * A->R;
   A->nrows = rows->noids;
@@ -2194,7 +2232,7 @@ int pa_mat_destroy(pa_mat* A) {
   dev_free(A->d_col);
   dev_free(A->d_val);
   dev_free(A->d_nz_slot);
-  for (void* p : {(void*)A->d_kind, (void*)A->d_plen, (void*)A->d_pat, (void*)A->d_mask, (void*)A->d_mpat,
+  for (void* p : {(void*)A->d_kind, (void*)A->d_plen, (void*)A->d_pat, (void*)A->d_ptri, (void*)A->d_mask, (void*)A->d_mpat,
                   (void*)A->d_psel, (void*)A->d_mint_list, (void*)A->d_mbnd_list,
                   (void*)A->d_pint_list, (void*)A->d_pbnd_list, (void*)A->d_xint_list,
                   (void*)A->d_xbnd_list, (void*)A->d_s_off, (void*)A->d_s_len,
@@ -2249,7 +2287,7 @@ int pa_mat_traffic(const pa_mat* A, int64_t* value_bytes, int64_t* index_bytes, 
     const int kd = pat ? A->h_kind[s] : 0;
     if (kd == 1) {
       v += (int64_t)A->h_plen[s] * H * S;
-      m += (int64_t)A->kmax * 4 + W * 8 + 8 + 4 + 4;  // pattern, mask, offset, length, list entry
+      m += (int64_t)A->kmax * 4 + W * 8 + 8 + 4 + 4 + (A->d_ptri ? 1 : 0);  // pattern, mask, offset, length, list entry, triple flag
     } else if (kd == 2) {
       v += (int64_t)A->h_plen[s] * H * S;
       m += (int64_t)PA_MP_NP * A->kmp * 4 + 64 + W * 8 + 8 + 4 + 4;

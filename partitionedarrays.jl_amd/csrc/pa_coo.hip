@@ -19,10 +19,11 @@
 
 namespace pa {
 
-// key = (J-1)*m + (I-1) (column-major = CSC order), payload = input position
+// key = (J-1)*m + (I-1) (column-major = CSC order), or (I-1)*ncols + (J-1)
+// (row-major = CSR order, sparsecsr), payload = input position
 template <typename IT>
 __global__ void k_coo_keys(int64_t n, const IT* __restrict__ I, const IT* __restrict__ J, int64_t m,
-                           int64_t ncols, uint64_t* __restrict__ key, int64_t* __restrict__ idx,
+                           int64_t ncols, int csr, uint64_t* __restrict__ key, int64_t* __restrict__ idx,
                            int* __restrict__ bad) {
   for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < n; k += (int64_t)gridDim.x * blockDim.x) {
     const int64_t i = (int64_t)I[k] - 1, j = (int64_t)J[k] - 1;
@@ -30,7 +31,7 @@ __global__ void k_coo_keys(int64_t n, const IT* __restrict__ I, const IT* __rest
       *bad = 1;
       key[k] = 0;
     } else {
-      key[k] = (uint64_t)j * (uint64_t)m + (uint64_t)i;
+      key[k] = csr ? (uint64_t)i * (uint64_t)ncols + (uint64_t)j : (uint64_t)j * (uint64_t)m + (uint64_t)i;
     }
     idx[k] = k;
   }
@@ -52,20 +53,21 @@ __global__ void k_seg_start(int64_t n, const int64_t* __restrict__ head, const i
 // input order (the sort is stable)
 template <typename T>
 __global__ void k_seg_sum(int64_t nu, int64_t n, const int64_t* __restrict__ start, const uint64_t* __restrict__ key,
-                          const int64_t* __restrict__ idx, const T* __restrict__ V, int64_t m,
+                          const int64_t* __restrict__ idx, const T* __restrict__ V, int64_t m, int64_t ncols, int csr,
                           int32_t* __restrict__ crow, int32_t* __restrict__ ccol, T* __restrict__ cval) {
   for (int64_t s = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; s < nu; s += (int64_t)gridDim.x * blockDim.x) {
     const int64_t a = start[s], b = (s + 1 < nu) ? start[s + 1] : n;
     T acc = V[idx[a]];
     for (int64_t k = a + 1; k < b; ++k) acc = acc + V[idx[k]];
     const uint64_t kk = key[a];
-    crow[s] = (int32_t)(kk % (uint64_t)m);
-    ccol[s] = (int32_t)(kk / (uint64_t)m);
+    crow[s] = (int32_t)(csr ? kk / (uint64_t)ncols : kk % (uint64_t)m);
+    ccol[s] = (int32_t)(csr ? kk % (uint64_t)ncols : kk / (uint64_t)m);
     cval[s] = acc;
   }
 }
 
-// colptr[j] = first nz of column j (lower bound in the column-sorted list)
+// colptr[j] = first nz of column j (lower bound in the column-sorted list);
+// for a CSR the same over the rows (ccol = the row of each nz)
 __global__ void k_colptr(int64_t ncols, int64_t nu, const int32_t* __restrict__ ccol, int64_t* __restrict__ colptr) {
   for (int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; j <= ncols; j += (int64_t)gridDim.x * blockDim.x) {
     int64_t lo = 0, hi = nu;
@@ -237,9 +239,10 @@ hipError_t exclusive_sum(const int64_t* in, int64_t* out, int64_t n, hipStream_t
 
 template <typename T>
 void seg_sum_t(int64_t nu, int64_t n, const int64_t* start, const uint64_t* key, const int64_t* idx,
-               const void* V, int64_t m, int32_t* crow, int32_t* ccol, void* cval, hipStream_t st) {
-  hipLaunchKernelGGL(k_seg_sum<T>, grid1(nu), dim3(256), 0, st, nu, n, start, key, idx, (const T*)V, m, crow,
-                     ccol, (T*)cval);
+               const void* V, int64_t m, int64_t ncols, int csr, int32_t* crow, int32_t* ccol, void* cval,
+               hipStream_t st) {
+  hipLaunchKernelGGL(k_seg_sum<T>, grid1(nu), dim3(256), 0, st, nu, n, start, key, idx, (const T*)V, m, ncols, csr,
+                     crow, ccol, (T*)cval);
 }
 
 }  // namespace
@@ -257,9 +260,11 @@ void seg_sum_t(int64_t nu, int64_t n, const int64_t* start, const uint64_t* key,
 // values combined).  I, J: 1-based device arrays (index_bytes 4 or 8).
 // On success the caller owns *crow, *ccol, *cval (nu entries) and *colptr
 // (ncols+1, 0-based offsets).  Returns 1 on an out-of-range index.
+// csr: sparsecsr instead — the nonzeros in row-major (CSR) order and
+// *colptr the row pointers (m+1).
 int coo_compress(int dtype, int index_bytes, int64_t m, int64_t ncols, int64_t n, const void* dI, const void* dJ,
-                 const void* dV, int64_t* nu_out, int32_t** crow, int32_t** ccol, void** cval, int64_t** colptr,
-                 hipStream_t st, hipError_t* err_out) {
+                 const void* dV, int csr, int64_t* nu_out, int32_t** crow, int32_t** ccol, void** cval,
+                 int64_t** colptr, hipStream_t st, hipError_t* err_out) {
   hipError_t err = hipSuccess;
   const size_t S = dtype_size(dtype);
   uint64_t* key = nullptr;
@@ -272,7 +277,8 @@ int coo_compress(int dtype, int index_bytes, int64_t m, int64_t ncols, int64_t n
   *cval = nullptr;
   *colptr = nullptr;
   int rc = 0;
-  PA_HIP_TRY(hipMalloc((void**)colptr, (ncols + 1) * 8));
+  const int64_t nptr = csr ? m : ncols;  // columns (CSC) or rows (CSR) of the compressed axis
+  PA_HIP_TRY(hipMalloc((void**)colptr, (nptr + 1) * 8));
   if (n > 0) {
     PA_HIP_TRY(hipMalloc((void**)&key, n * 8));
     PA_HIP_TRY(hipMalloc((void**)&idx, n * 8));
@@ -280,10 +286,10 @@ int coo_compress(int dtype, int index_bytes, int64_t m, int64_t ncols, int64_t n
     PA_HIP_TRY(hipMemsetAsync(bad, 0, sizeof(int), st));
     if (index_bytes == 8)
       hipLaunchKernelGGL(k_coo_keys<int64_t>, grid1(n), dim3(256), 0, st, n, (const int64_t*)dI, (const int64_t*)dJ,
-                         m, ncols, key, idx, bad);
+                         m, ncols, csr, key, idx, bad);
     else
       hipLaunchKernelGGL(k_coo_keys<int32_t>, grid1(n), dim3(256), 0, st, n, (const int32_t*)dI, (const int32_t*)dJ,
-                         m, ncols, key, idx, bad);
+                         m, ncols, csr, key, idx, bad);
     PA_HIP_TRY(hipMemcpyAsync(&hbad, bad, sizeof(int), hipMemcpyDeviceToHost, st));
     PA_HIP_TRY(hipStreamSynchronize(st));
     if (hbad) { rc = 1; goto done; }
@@ -299,13 +305,13 @@ int coo_compress(int dtype, int index_bytes, int64_t m, int64_t ncols, int64_t n
     PA_HIP_TRY(hipMalloc((void**)ccol, nu * 4));
     PA_HIP_TRY(hipMalloc(cval, nu * S));
     switch (dtype) {
-      case PA_F32: seg_sum_t<float>(nu, n, start, key, idx, dV, m, *crow, *ccol, *cval, st); break;
-      case PA_F64: seg_sum_t<double>(nu, n, start, key, idx, dV, m, *crow, *ccol, *cval, st); break;
-      case PA_C64: seg_sum_t<c64>(nu, n, start, key, idx, dV, m, *crow, *ccol, *cval, st); break;
-      case PA_C128: seg_sum_t<c128>(nu, n, start, key, idx, dV, m, *crow, *ccol, *cval, st); break;
+      case PA_F32: seg_sum_t<float>(nu, n, start, key, idx, dV, m, ncols, csr, *crow, *ccol, *cval, st); break;
+      case PA_F64: seg_sum_t<double>(nu, n, start, key, idx, dV, m, ncols, csr, *crow, *ccol, *cval, st); break;
+      case PA_C64: seg_sum_t<c64>(nu, n, start, key, idx, dV, m, ncols, csr, *crow, *ccol, *cval, st); break;
+      case PA_C128: seg_sum_t<c128>(nu, n, start, key, idx, dV, m, ncols, csr, *crow, *ccol, *cval, st); break;
     }
   }
-  hipLaunchKernelGGL(k_colptr, grid1(ncols + 1), dim3(256), 0, st, ncols, nu, *ccol, *colptr);
+  hipLaunchKernelGGL(k_colptr, grid1(nptr + 1), dim3(256), 0, st, nptr, nu, csr ? *crow : *ccol, *colptr);
   PA_HIP_TRY(hipGetLastError());
   PA_HIP_TRY(hipStreamSynchronize(st));
 done:

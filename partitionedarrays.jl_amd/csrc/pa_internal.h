@@ -443,6 +443,7 @@ struct pa_mat {
   int32_t* d_kind = nullptr;         // per slice: 1 pattern, 0 int32 columns
   int32_t* d_plen = nullptr;         // per slice: entries per row (pattern len or int32 len)
   int32_t* d_pat = nullptr;          // nslices*kmax offsets
+  uint8_t* d_ptri = nullptr;         // per slice: 1 if its pattern is consecutive triples (x runs shared by lanes)
   uint64_t* d_mask = nullptr;        // nslices*(H/64) regular-row bits
   int32_t* d_pint_list = nullptr;    // pattern mode: pattern slices without ghost reads
   int32_t* d_pbnd_list = nullptr;    // pattern mode: pattern slices reading ghosts

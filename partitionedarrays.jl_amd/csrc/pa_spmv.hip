@@ -43,7 +43,8 @@ __device__ inline int64_t xcd_remap(int64_t b, int64_t G) {
 }
 
 enum { SPMV_NT = 1, SPMV_XCD = 2, SPMV_XPAIR = 4, SPMV_TAILB = 8, SPMV_IDLIST = 16, SPMV_YNT = 32, SPMV_SHORT = 64,
-       SPMV_XRUN = 128, SPMV_PRODA = 256 /* per matrix: CSR parent, α scales the product */ };
+       SPMV_XRUN = 128, SPMV_PRODA = 256 /* per matrix: CSR parent, α scales the product */,
+       SPMV_XTRI = 512 /* triple-pattern slices share x runs between lanes */ };
 typedef unsigned int spmv_u32x4 __attribute__((ext_vector_type(4)));
 // Process-wide knobs (pa_tune).  Defaults from the A/Bs in
 // profiles/r01_ab_spmv.txt and profiles/r01/ab_xpair.txt: non-temporal
@@ -51,6 +52,10 @@ typedef unsigned int spmv_u32x4 __attribute__((ext_vector_type(4)));
 // F32 −33 %, C64 −5 % kernel time), predicated tail batch on
 // (profiles/r01/ab_tail.txt: FD7 256³ F64 −31 %, F32 −42 %; FE27 −1…−3 %),
 // identity slice lists dropped (profiles/r01/ab_idlist.txt: FD7 −0.9 %, FE27 ±0).
+// Lane-shared x runs for triple-pattern slices (SPMV_XTRI) stay opt-in:
+// interleaved A/B on FE27 256³ (profiles/r02/stream/ab_xtri.txt): F64 −0.2 %,
+// C128 −0.9 %, C64 +0.4 %, F32 +3 % kernel time — the x loads are not what
+// bounds the SpMV (their 6 % in the probe is hidden in the full kernel).
 int g_spmv_flags = SPMV_NT | SPMV_XPAIR | SPMV_TAILB | SPMV_IDLIST | SPMV_SHORT;
 int g_spmv_unroll = 8;
 // dynamic LDS per SpMV block (unused by the kernel): caps the blocks per CU,
@@ -67,6 +72,16 @@ int g_spmv_pattern_rule = 0;     // 1: slice encoding by streamed bytes, 0: patt
 // merged-launch tables allocated during a graph capture, copied after it ends
 // (no copies while a stream is being captured)
 std::vector<std::pair<void*, std::vector<char>>> g_capture_uploads;
+
+// SpmvArgs' pointers are global memory.  The merged launch reads them from a
+// device-resident table, where the compiler cannot see their address space:
+// typed global in device code, its loads are global_load (scalar s_load for
+// the wave-uniform ones: patterns, slice offsets) instead of flat_load.
+#if defined(__HIP_DEVICE_COMPILE__)
+#define PA_GLB __attribute__((address_space(1)))
+#else
+#define PA_GLB
+#endif
 
 template <int BYTES> struct RawOf;
 template <> struct RawOf<2> { typedef unsigned short type; };
@@ -88,35 +103,37 @@ __device__ __forceinline__ V ld(const V* p) {
 template <typename T>
 struct SpmvArgs {
   int64_t nwork;            // slices of this launch
-  const int32_t* list;      // slice ids (null: 0..nwork-1)
-  const int64_t* soff;
-  const int32_t* slen;      // entries per row of the slice
-  const int32_t* col;
-  const T* val;
-  const int32_t* pat;       // kmax offsets per slice (multi-pattern: PA_MP_NP*kmax)
-  const uint64_t* mask;     // H/64 words per slice
+  const PA_GLB int32_t* list;      // slice ids (null: 0..nwork-1)
+  const PA_GLB int64_t* soff;
+  const PA_GLB int32_t* slen;      // entries per row of the slice
+  const PA_GLB int32_t* col;
+  const PA_GLB T* val;
+  const PA_GLB int32_t* pat;       // kmax offsets per slice (multi-pattern: PA_MP_NP*kmax)
+  const PA_GLB uint8_t* ptri;      // pattern slices: 1 if the pattern is consecutive triples (null: none)
+  const PA_GLB uint64_t* mask;     // H/64 words per slice
   int kmax;
-  const uint8_t* psel;      // multi-pattern: pattern of each lane (64 per slice)
-  const int32_t* rowmap;    // structure row → oid (side SELL), null: identity
+  const PA_GLB uint8_t* psel;      // multi-pattern: pattern of each lane (64 per slice)
+  const PA_GLB int32_t* rowmap;    // structure row → oid (side SELL), null: identity
   int64_t nrows;            // rows of this structure
-  const T* x;
-  T* y;
-  const int32_t* ymap;      // oid → y lid, null: identity
+  const PA_GLB T* x;
+  int64_t nx;               // x length (lids)
+  PA_GLB T* y;
+  const PA_GLB int32_t* ymap;      // oid → y lid, null: identity
   T alpha, beta;
   int flags;
   // fused dot(u, c) (CG): u = x indexed by oid (contiguous own layout);
   // one partial per slice at dotp[dot_base + s] (deterministic fold later)
-  const T* dotu;
+  const PA_GLB T* dotu;
   void* dotp;
   int64_t dot_base;
   // long rows (k_spmv_long) inside int32-column slices: slices with
   // sflags[s] != 0 skip the rows whose lmask bit is set (null: none)
-  const int32_t* sflags;
-  const uint64_t* lmask;
+  const PA_GLB int32_t* sflags;
+  const PA_GLB uint64_t* lmask;
   int maxlen;               // longest row (entries) of the launch's slices: <= U selects the SH kernels
   // delta16 slices: 16-bit column codes and the per-slice ghost base
-  const uint16_t* col16;
-  const int32_t* gbase;
+  const PA_GLB uint16_t* col16;
+  const PA_GLB int32_t* gbase;
 };
 
 template <typename T> struct DAcc { using type = double; };
@@ -413,6 +430,111 @@ __device__ __forceinline__ void rows_pattern(T (&acc)[R], const int32_t* __restr
   }
 }
 
+// One T from the neighbouring lane by a DPP wave shift (GFX9 wave_shr:1 /
+// wave_shl:1, no LDS): lane l gets lane l-1's (SHR) or l+1's (SHL) value;
+// lane 0 (SHR) and lane 63 (SHL) get 0, for the caller to patch.  Every lane
+// of the wave must be active.
+constexpr int kDppWaveShr1 = 0x138, kDppWaveShl1 = 0x130;
+template <int CTRL, typename T>
+__device__ __forceinline__ T lane_shift(T v) {
+  static_assert(sizeof(T) % 4 == 0, "dword values");
+  uint32_t w[sizeof(T) / 4];
+  __builtin_memcpy(w, &v, sizeof(T));
+#pragma unroll
+  for (int i = 0; i < (int)(sizeof(T) / 4); ++i)
+    w[i] = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)w[i], CTRL, 0xf, 0xf, false);
+  T o;
+  __builtin_memcpy(&o, w, sizeof(T));
+  return o;
+}
+
+// Per pattern slice (build time): does its pattern consist of consecutive
+// triples (o-1, o, o+1)?  (FE27: its 9 x-lines.)  Checking in the SpMV
+// itself costs a chain of dependent scalar loads per wave before its first
+// value load (+8 % on FE27 256³), so it is one byte per slice.
+__global__ void k_pattern_triples(int64_t ns, int kmax, const int32_t* __restrict__ kind,
+                                  const int32_t* __restrict__ plen, const int32_t* __restrict__ pat,
+                                  uint8_t* __restrict__ tri) {
+  const int64_t s = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (s >= ns) return;
+  const int len = plen[s];
+  bool ok = kind[s] == 1 && len >= 3 && len % 3 == 0;
+  const int32_t* p = pat + s * kmax;
+  for (int t = 0; ok && t < len; t += 3) ok = p[t + 1] == p[t] + 1 && p[t + 2] == p[t] + 2;
+  tri[s] = ok ? 1 : 0;
+}
+
+void launch_pattern_triples(const pa_mat* A, uint8_t* tri, hipStream_t st) {
+  const int64_t ns = A->nslices;
+  if (ns == 0) return;
+  hipLaunchKernelGGL(k_pattern_triples, dim3((unsigned)((ns + 255) / 256)), dim3(256), 0, st, ns, A->kmax, A->d_kind,
+                     A->d_plen, A->d_pat, tri);
+}
+
+// Triple-pattern rows: per triple (o-1, o, o+1) ONE 16 B x run per lane, at
+// the centre offset o; the dx = -1 / +1 runs are the same values moved by
+// one row, taken from the neighbouring lanes (lane_shift) — lanes 0 and 63
+// fetch the one value past the slice's edge.  A third of rows_pattern's x
+// loads (the x loads cost the headline 6 % even as L2 hits,
+// profiles/r02/stream/).  Same terms in the same order: entries 3t, 3t+1,
+// 3t+2 of each row in turn.  Lanes load at their natural rows whether or
+// not their rows are regular (a regular neighbour may need the value),
+// clamped into the 64 B padding of x when far out of range (then no regular
+// row reads it).  nx: x length.
+template <typename T, int R, bool ALPHA, bool NT>
+__device__ __forceinline__ void rows_pattern3(T (&acc)[R], const int32_t* __restrict__ pat,
+                                              const Pack<T, R>* __restrict__ vp, int len,
+                                              const T* __restrict__ x, int64_t row0, int64_t srow0, int64_t nx,
+                                              T alpha, bool pf) {
+  constexpr int H = 64 * R;
+  const int lane = threadIdx.x & 63;
+  const int nt = len / 3;
+  auto center = [&](int o, Pack<T, R>& c, T& e) {
+    int64_t i = row0 + o;
+    i = i < -(int64_t)R ? -(int64_t)R : (i > nx ? nx : i);
+    c = ld_xrun<T, R>(x + i);
+    e = zero_of<T>();
+    if (lane == 0 || lane == 63) {
+      int64_t j = lane == 0 ? srow0 + o - 1 : srow0 + H + o;
+      j = j < -1 ? -1 : (j > nx ? nx : j);
+      e = x[j];
+    }
+  };
+  auto triple = [&](const Pack<T, R>* v, const Pack<T, R>& c, T e) {
+    T lo = lane_shift<kDppWaveShr1>(c.v[R - 1]);
+    T hi = lane_shift<kDppWaveShl1>(c.v[0]);
+    if (lane == 0) lo = e;
+    if (lane == 63) hi = e;
+#pragma unroll
+    for (int r = 0; r < R; ++r) acc[r] = acc[r] + term<ALPHA>(v[0].v[r], r == 0 ? lo : c.v[r - 1], alpha, pf);
+#pragma unroll
+    for (int r = 0; r < R; ++r) acc[r] = acc[r] + term<ALPHA>(v[1].v[r], c.v[r], alpha, pf);
+#pragma unroll
+    for (int r = 0; r < R; ++r) acc[r] = acc[r] + term<ALPHA>(v[2].v[r], r == R - 1 ? hi : c.v[r + 1], alpha, pf);
+  };
+  int t = 0;
+  for (; t + 3 <= nt; t += 3) {  // 3 triples (9 entries) in flight
+    Pack<T, R> v[9];
+#pragma unroll
+    for (int u = 0; u < 9; ++u) v[u] = ld<NT>(&vp[(3 * t + u) * 64]);
+    Pack<T, R> c[3];
+    T e[3];
+#pragma unroll
+    for (int q = 0; q < 3; ++q) center(pat[3 * (t + q) + 1], c[q], e[q]);
+#pragma unroll
+    for (int q = 0; q < 3; ++q) triple(&v[3 * q], c[q], e[q]);
+  }
+  for (; t < nt; ++t) {
+    Pack<T, R> v[3];
+#pragma unroll
+    for (int u = 0; u < 3; ++u) v[u] = ld<NT>(&vp[(3 * t + u) * 64]);
+    Pack<T, R> c;
+    T e;
+    center(pat[3 * t + 1], c, e);
+    triple(v, c, e);
+  }
+}
+
 // BMODE: 0 → acc = 0 (β == 0: fill!(co,0)), 1 → acc = y (β == 1),
 //        2 → acc = y*β (rmul!(co,β)).  Interfaces.jl:2262-2263.
 // PK: the launch's slices are int32-column slices (0), pattern slices (1:
@@ -484,7 +606,15 @@ __device__ __forceinline__ void spmv_wave(const SpmvArgs<T>& a, const int64_t w)
     }
   } else if constexpr (PK == 1) {
     const int32_t* pat = a.pat + s * a.kmax;
-    if (a.flags & SPMV_XPAIR) {
+    bool tri = false;
+    if constexpr (!SH && sizeof(Pack<T, R>) == 16)
+      tri = (a.flags & SPMV_XPAIR) && (a.flags & SPMV_XTRI) && a.ptri && a.ptri[s];
+    if (tri) {
+      if constexpr (!SH && sizeof(Pack<T, R>) == 16) {
+        if (a.flags & SPMV_NT) rows_pattern3<T, R, ALPHA, true>(acc, pat, vp, len, a.x, row0, s * H, a.nx, a.alpha, pf);
+        else rows_pattern3<T, R, ALPHA, false>(acc, pat, vp, len, a.x, row0, s * H, a.nx, a.alpha, pf);
+      }
+    } else if (a.flags & SPMV_XPAIR) {
       if (a.flags & SPMV_NT) rows_pattern<T, R, ALPHA, true, U, true, SH>(acc, pat, vp, len, a.x, row0, ok, a.alpha, pf, tb);
       else rows_pattern<T, R, ALPHA, false, U, true, SH>(acc, pat, vp, len, a.x, row0, ok, a.alpha, pf, tb);
     } else {
@@ -631,14 +761,15 @@ template <typename T>
 static SpmvArgs<T> make_args(int which, int64_t nwork, const int32_t* list, const pa_mat* A, const void* x,
                              void* y, const int32_t* ymap, const void* alpha, const void* beta, void* dotp) {
   SpmvArgs<T> a{};
-  a.dotu = (const T*)x;
+  a.dotu = (decltype(a.dotu))((const T*)x);
   a.dotp = dotp;
   a.dot_base = which == 2 ? A->nslices : 0;
   a.nwork = nwork;
-  a.list = list;
-  a.x = (const T*)x;
-  a.y = (T*)y;
-  a.ymap = ymap;
+  a.list = (decltype(a.list))(list);
+  a.x = (decltype(a.x))((const T*)x);
+  a.nx = A->ncols_lids;
+  a.y = (decltype(a.y))((T*)y);
+  a.ymap = (decltype(a.ymap))(ymap);
   a.alpha = *(const T*)alpha;
   a.beta = *(const T*)beta;
   a.flags = g_spmv_flags | (A->csr ? SPMV_PRODA : 0);
@@ -648,39 +779,40 @@ static SpmvArgs<T> make_args(int which, int64_t nwork, const int32_t* list, cons
              : which == 4 ? A->maxlen_d16
                           : INT32_MAX;
   if (which == 2) {
-    a.soff = A->d_s_off;
-    a.slen = A->d_s_len;
-    a.col = A->d_s_col;
-    a.val = (const T*)A->d_s_val;
-    a.rowmap = A->d_s_rowmap;
+    a.soff = (decltype(a.soff))(A->d_s_off);
+    a.slen = (decltype(a.slen))(A->d_s_len);
+    a.col = (decltype(a.col))(A->d_s_col);
+    a.val = (decltype(a.val))((const T*)A->d_s_val);
+    a.rowmap = (decltype(a.rowmap))(A->d_s_rowmap);
     a.nrows = A->s_nrows;
   } else {
-    a.soff = A->d_slice_off;
-    a.col = A->d_col;
-    a.val = (const T*)A->d_val;
+    a.soff = (decltype(a.soff))(A->d_slice_off);
+    a.col = (decltype(a.col))(A->d_col);
+    a.val = (decltype(a.val))((const T*)A->d_val);
     a.nrows = A->nrows;
     if (which == 0) {
-      a.slen = A->d_plen;
-      a.pat = A->d_pat;
-      a.mask = A->d_mask;
+      a.slen = (decltype(a.slen))(A->d_plen);
+      a.pat = (decltype(a.pat))(A->d_pat);
+      a.ptri = (decltype(a.ptri))(A->d_ptri);
+      a.mask = (decltype(a.mask))(A->d_mask);
       a.kmax = A->kmax;
     } else if (which == 3) {
-      a.slen = A->d_plen;
-      a.pat = A->d_mpat;
-      a.mask = A->d_mask;
+      a.slen = (decltype(a.slen))(A->d_plen);
+      a.pat = (decltype(a.pat))(A->d_mpat);
+      a.mask = (decltype(a.mask))(A->d_mask);
       a.kmax = A->kmp;
-      a.psel = A->d_psel;
+      a.psel = (decltype(a.psel))(A->d_psel);
     } else {
-      a.slen = A->d_slice_len;
+      a.slen = (decltype(a.slen))(A->d_slice_len);
       if (which == 4) {
-        a.col16 = A->d_col16;
-        a.gbase = A->d_gbase;
+        a.col16 = (decltype(a.col16))(A->d_col16);
+        a.gbase = (decltype(a.gbase))(A->d_gbase);
       }
     }
   }
   if (which == 1) {
-    a.sflags = A->d_sflags;
-    a.lmask = A->d_lmask;
+    a.sflags = (decltype(a.sflags))(A->d_sflags);
+    a.lmask = (decltype(a.lmask))(A->d_lmask);
   }
   return a;
 }

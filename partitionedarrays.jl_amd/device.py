@@ -397,13 +397,15 @@ class DeviceMatrix:
 
     @staticmethod
     def from_coo(ctx: PartContext, I, J, V, rows_idx: DeviceIndex, cols_idx: DeviceIndex, nrows_lids, ncols_lids,
-                 ids_global=False, pattern=True):
+                 ids_global=False, pattern=True, csr_bi=None):
         """sparse(I, J, V, m, n, +) and the SELL build on the device
         (pa_mat_from_coo; ids_global: I, J are gids mapped by to_lids! on the
         device, the indices need their gid tables).  Returns (matrix, colptr,
         rowval): the CSC pattern (1-based lids) for the host setup that needs
         it (matrix_exchanger); pattern=False returns (matrix, None, None) and
-        downloads nothing.  Local ids cross PCIe as Int32 when they fit."""
+        downloads nothing.  Local ids cross PCIe as Int32 when they fit.
+        csr_bi = 0 / 1: sparsecsr instead (pa_mat_from_coo_csr); the pattern
+        returned is then (rowptr, colval) in base Bi."""
         V = np.ascontiguousarray(V).ravel()
         ib = 4 if not ids_global and max(nrows_lids, ncols_lids) < 2 ** 31 - 1 else 8
         idt = np.int32 if ib == 4 else np.int64
@@ -417,16 +419,20 @@ class DeviceMatrix:
         J = np.ascontiguousarray(J, dtype=idt)
         if not (len(I) == len(J) == len(V)):
             raise ValueError("sparse: I, J and V must have the same length")
-        colptr = np.empty(ncols_lids + 1, dtype=np.int64) if pattern else None
+        colptr = np.empty((nrows_lids if csr_bi is not None else ncols_lids) + 1, dtype=np.int64) if pattern else None
         rowval = np.empty(max(1, len(I)), dtype=np.int64) if pattern else None
         nnz = C.c_int64(0)
         h = C.c_void_p()
-        _lib.call("pa_mat_from_coo", ctx.h, _lib.DTYPES[V.dtype], ib, 1 if ids_global else 0, nrows_lids, ncols_lids,
-                  len(I),
-                  I.ctypes.data_as(C.c_void_p), J.ctypes.data_as(C.c_void_p), V.ctypes.data_as(C.c_void_p),
-                  rows_idx.h, cols_idx.h, C.byref(nnz),
-                  colptr.ctypes.data_as(C.POINTER(C.c_int64)) if pattern else None,
-                  rowval.ctypes.data_as(C.POINTER(C.c_int64)) if pattern else None, C.byref(h))
+        ptrs = (colptr.ctypes.data_as(C.POINTER(C.c_int64)) if pattern else None,
+                rowval.ctypes.data_as(C.POINTER(C.c_int64)) if pattern else None)
+        if csr_bi is None:
+            _lib.call("pa_mat_from_coo", ctx.h, _lib.DTYPES[V.dtype], ib, 1 if ids_global else 0, nrows_lids,
+                      ncols_lids, len(I), I.ctypes.data_as(C.c_void_p), J.ctypes.data_as(C.c_void_p),
+                      V.ctypes.data_as(C.c_void_p), rows_idx.h, cols_idx.h, C.byref(nnz), *ptrs, C.byref(h))
+        else:
+            _lib.call("pa_mat_from_coo_csr", ctx.h, _lib.DTYPES[V.dtype], ib, 1 if ids_global else 0, int(csr_bi),
+                      nrows_lids, ncols_lids, len(I), I.ctypes.data_as(C.c_void_p), J.ctypes.data_as(C.c_void_p),
+                      V.ctypes.data_as(C.c_void_p), rows_idx.h, cols_idx.h, C.byref(nnz), *ptrs, C.byref(h))
         M = DeviceMatrix(h, ctx, V.dtype)
         M.csc_nnz = nnz.value
         if not pattern:
@@ -435,16 +441,22 @@ class DeviceMatrix:
 
     @staticmethod
     def from_dcoo(coo: DeviceCOO, rows_idx: DeviceIndex, cols_idx: DeviceIndex, nrows_lids, ncols_lids,
-                  ids_global=True, pattern=True):
-        """DeviceMatrix.from_coo over device triplets (pa_mat_from_dcoo)."""
+                  ids_global=True, pattern=True, csr_bi=None):
+        """DeviceMatrix.from_coo over device triplets (pa_mat_from_dcoo, or
+        pa_mat_from_dcoo_csr with csr_bi = 0 / 1)."""
         n = len(coo)
-        colptr = np.empty(ncols_lids + 1, dtype=np.int64) if pattern else None
+        colptr = np.empty((nrows_lids if csr_bi is not None else ncols_lids) + 1, dtype=np.int64) if pattern else None
         rowval = np.empty(max(1, n), dtype=np.int64) if pattern else None
         nnz = C.c_int64(0)
         h = C.c_void_p()
-        _lib.call("pa_mat_from_dcoo", coo.h, 1 if ids_global else 0, nrows_lids, ncols_lids, rows_idx.h, cols_idx.h,
-                  C.byref(nnz), colptr.ctypes.data_as(C.POINTER(C.c_int64)) if pattern else None,
-                  rowval.ctypes.data_as(C.POINTER(C.c_int64)) if pattern else None, C.byref(h))
+        ptrs = (colptr.ctypes.data_as(C.POINTER(C.c_int64)) if pattern else None,
+                rowval.ctypes.data_as(C.POINTER(C.c_int64)) if pattern else None)
+        if csr_bi is None:
+            _lib.call("pa_mat_from_dcoo", coo.h, 1 if ids_global else 0, nrows_lids, ncols_lids, rows_idx.h,
+                      cols_idx.h, C.byref(nnz), *ptrs, C.byref(h))
+        else:
+            _lib.call("pa_mat_from_dcoo_csr", coo.h, 1 if ids_global else 0, int(csr_bi), nrows_lids, ncols_lids,
+                      rows_idx.h, cols_idx.h, C.byref(nnz), *ptrs, C.byref(h))
         M = DeviceMatrix(h, coo.ctx, coo.dtype)
         M.csc_nnz = nnz.value
         if not pattern:
@@ -456,7 +468,8 @@ class DeviceMatrix:
         _lib.call("pa_mat_set_values", self.h, nzval.ctypes.data_as(C.c_void_p))
 
     def get_values(self):
-        """nonzeros(A) in CSC order, ghost rows included."""
+        """nonzeros(A) in the parent's order (CSC, or CSR for a SparseMatrixCSR
+        parent), ghost rows included."""
         n = getattr(self, "csc_nnz", None)
         if n is None:
             raise _lib.PAError("matrix was not built from a CSC pattern")

@@ -173,20 +173,22 @@ def fem_sa_host(parts: PData, nx=10):
     return rows, cols, I, J, V, bh, x0h, xh
 
 
-def fem_sa_problem(parts: PData, nx=10):
+def fem_sa_problem(parts: PData, nx=10, init=None):
     """test_fem_sa.jl on HIP parts: the COO triplets go to the device,
     assemble!(I, J, V, rows) moves the ghost rows' triplets to their owners
     there (pa_coo_assemble_all), add_gids!(cols, J), then the PSparseMatrix
-    from the device COO (ids=:global) and b assembled on the device
-    (assemble!, Interfaces.jl:2101)."""
+    from the device COO (ids=:global; init = csr_init(Bi) for
+    SparseMatrixCSR{Bi} parents) and b assembled on the device (assemble!,
+    Interfaces.jl:2101)."""
     from .prange import add_gids_
     from .pvector import COO, assemble_
+    mat_init = init  # the local matrix constructor (fem_sa_cells returns the x0/x̂ initializer as `init`)
     rows, cols, I, J, V, bh, init = fem_sa_cells(parts, nx)
     coo = COO.from_host(I, J, V, rows)
     assemble_(coo, rows)
     add_gids_(cols, coo.global_cols())
     x0h, xh = init(cols)
-    A = PSparseMatrix.from_coo(coo, None, None, rows, cols, ids="global")
+    A = PSparseMatrix.from_coo(coo, None, None, rows, cols, ids="global", init=mat_init)
     b = PVector.from_host(bh, rows)
     assemble_(b)
     return A, b, PVector.from_host(x0h, cols), PVector.from_host(xh, cols)

@@ -89,9 +89,18 @@ def sparsecsr(Bi, I, J, V, m, n) -> CSR:
     return CSR(Bi, m, n, t.colptr - 1 + Bi, t.rowval - 1 + Bi, t.nzval)
 
 
-def csr_init(Bi):
-    """init for PSparseMatrix.from_coo: sparsecsr with index base Bi"""
-    return lambda I, J, V, m, n: sparsecsr(Bi, I, J, V, m, n)
+class csr_init:
+    """init for PSparseMatrix.from_coo: sparsecsr with index base Bi (the
+    compress then runs on the device, pa_mat_from_coo_csr); called as
+    init(I, J, V, m, n) it is the host sparsecsr."""
+
+    def __init__(self, Bi):
+        if Bi not in (0, 1):
+            raise ValueError("SparseMatrixCSR: Bi must be 0 or 1")
+        self.Bi = int(Bi)
+
+    def __call__(self, I, J, V, m, n):
+        return sparsecsr(self.Bi, I, J, V, m, n)
 
 
 # ---------------------------------------------------------------------------
@@ -392,8 +401,12 @@ class PSparseMatrix:
         """PSparseMatrix(init, I, J, V, rows, cols; ids) (Interfaces.jl:
         2194-2215).  init None = sparse (2237-2244), on the device; I, J, V:
         PData of host arrays, or I a device COO (then J and V are None).
-        Another init (e.g. csr_init(Bi), sparsecsr) compresses each part's
-        host triplets with it and uploads the result."""
+        init = csr_init(Bi) (sparsecsr): the same compress on the device into
+        SparseMatrixCSR{Bi} parents (pa_mat_from_coo_csr).  Another callable
+        init compresses each part's host triplets and uploads the result
+        (pa_mat_from_csc / pa_mat_from_csr)."""
+        if isinstance(init, csr_init):  # sparsecsr on the device
+            return PSparseMatrix._from_coo_device(I, J, V, rows, cols, ids, csr_bi=init.Bi)
         if init is not None:
             if isinstance(I, COO):
                 raise NotImplementedError("from_coo: a custom init needs host triplets")
@@ -407,8 +420,12 @@ class PSparseMatrix:
             if all(isinstance(m, CSC) for m in loc.parts):
                 return PSparseMatrix.from_csc(loc, rows, cols)
             raise TypeError("from_coo: init must return CSC or CSR local matrices")
-        # to_lids! (ids=:global) and sparse(I, J, V) on the device
-        # (pa_mat_from_coo); the host keeps the CSC pattern only, for
+        return PSparseMatrix._from_coo_device(I, J, V, rows, cols, ids)
+
+    @staticmethod
+    def _from_coo_device(I, J, V, rows: PRange, cols: PRange, ids="local", csr_bi=None):
+        # to_lids! (ids=:global) and sparse(I, J, V) (or sparsecsr) on the
+        # device (pa_mat_from_coo[_csr]); the host keeps the pattern only, for
         # matrix_exchanger
         glob = ids == "global"
         idx = device_index_gids if glob else device_index
@@ -425,12 +442,18 @@ class PSparseMatrix:
         for c, i, j, v, r, s in zip(ctxs, I.parts, J.parts, V.parts, rows.partition.parts, cols.partition.parts):
             if dev:
                 M, colptr, rowval = DeviceMatrix.from_dcoo(i, idx(c, r), idx(c, s), r.num_lids, s.num_lids,
-                                                           ids_global=glob, pattern=want_pattern)
+                                                           ids_global=glob, pattern=want_pattern, csr_bi=csr_bi)
             else:
                 M, colptr, rowval = DeviceMatrix.from_coo(c, i, j, v, idx(c, r), idx(c, s), r.num_lids,
-                                                          s.num_lids, ids_global=glob, pattern=want_pattern)
+                                                          s.num_lids, ids_global=glob, pattern=want_pattern,
+                                                          csr_bi=csr_bi)
             mats.append(M)
-            pats.append(CSC(r.num_lids, s.num_lids, colptr, rowval, np.zeros(0)) if want_pattern else None)
+            if not want_pattern:
+                pats.append(None)
+            elif csr_bi is None:
+                pats.append(CSC(r.num_lids, s.num_lids, colptr, rowval, np.zeros(0)))
+            else:
+                pats.append(CSR(csr_bi, r.num_lids, s.num_lids, colptr, rowval, np.zeros(0)))
         t1 = trace("device sparse + SELL, all parts", t0)
         backend, pids, shape = rows.partition.backend, rows.partition.part_ids, rows.partition.shape
         ex = (matrix_exchanger(PData(backend, pids, pats, shape), rows, cols) if want_pattern

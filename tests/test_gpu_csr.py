@@ -247,3 +247,87 @@ def test_csr_long_rows_alpha(be, pamd, exact):
             assert np.array_equal(got, want[own])
         else:
             np.testing.assert_allclose(got, want[own], rtol=1e-12, atol=1e-12 * np.abs(want).max())
+
+
+@pytest.mark.parametrize("Bi", [0, 1])
+@pytest.mark.parametrize("nparts", [4, (2, 2)])
+def test_csr_fem_sa_device_cg(be, pamd, O, nparts, Bi):
+    """test_fem_sa.jl with SparseMatrixCSR{Bi} parents, assembled on the
+    device end to end (device COO → assemble!(I,J,V,rows) → sparsecsr on the
+    device, pa_mat_from_dcoo_csr): nonzeros(A) == the oracle's CSR, equal to
+    the host-compressed build, and the CG history follows the oracle's."""
+    parts = be.get_part_ids(nparts)
+    A, b, x0, xh = pamd.drivers.fem_sa_problem(parts, 10, init=pamd.csr_init(Bi))
+    OA, ob, ox0, oxh = O.fem_sa_problem(O.get_part_ids(nparts), 10, init=_csr_init(O, Bi))
+    for M, OM in zip(A.values.parts, OA.values.parts):
+        assert np.array_equal(M.get_values(), OM.nzval)
+    rows, cols, I, J, V, _, _, _ = pamd.drivers.fem_sa_host(parts, 10)
+    H = pamd.PSparseMatrix.from_csr(
+        pamd.map_parts(lambda i, j, v, r, c: pamd.sparsecsr(Bi, r.to_lids(i), c.to_lids(j), v, r.num_lids, c.num_lids),
+                       I, J, V, rows.partition, cols.partition), rows, cols)
+    for M, MH in zip(A.values.parts, H.values.parts):
+        assert np.array_equal(M.get_values(), MH.get_values())
+    x = x0.copy()
+    hist = []
+    pamd.cg_(x, A, b, history=hist)
+    ox = O.PVector(O.map_parts(lambda v: v.copy(), ox0.values), ox0.rows)
+    ohist = []
+    O.cg_(ox, OA, ob, log=ohist)
+    assert len(hist) == len(ohist)
+    np.testing.assert_allclose(hist, ohist, rtol=1e-8)
+
+
+@pytest.mark.parametrize("dtype", [np.float64, np.complex128, np.float32])
+def test_csr_device_compress_duplicates_bitexact(be, pamd, O, dtype):
+    """sparsecsr on the device (pa_mat_from_coo_csr) of shuffled triplets with
+    many duplicates == the oracle's sparse_csr (input-order sums), and mul!
+    with α != 1 == the oracle's CSR mul!."""
+    parts = be.get_part_ids((2, 1, 1))
+    _, part = pamd.drivers.stencil_partition(parts, (12, 10, 9), 27)
+    rng = np.random.default_rng(41)
+    trip = {}
+    for p in parts.part_ids:
+        s = part.partition.local(p)
+        n = 40 * len(s.oid_to_lid)
+        I = rng.choice(s.oid_to_lid, size=n)
+        J = rng.integers(1, s.num_lids + 1, size=n)
+        V = _rand(rng, n, dtype)
+        trip[p] = (I, J, V)
+    mk = lambda k: pamd.PData(parts.backend, parts.part_ids, [trip[p][k] for p in parts.part_ids], parts.shape)
+    A = pamd.PSparseMatrix.from_coo(mk(0), mk(1), mk(2), part, part, ids="local", init=pamd.csr_init(0))
+    xs = {p: _rand(rng, part.partition.local(p).num_lids, dtype) for p in parts.part_ids}
+    x = pamd.PVector.from_host(pamd.map_parts(lambda s: xs[s.part], part.partition), part)
+    y = pamd.PVector.undef(part, dtype)
+    alpha = 0.37
+    pamd.mul_(y, A, x, alpha, 0.0)
+    for p in parts.part_ids:
+        s = part.partition.local(p)
+        I, J, V = trip[p]
+        OM = O.sparse_csr(0, I, J, _ox(O, V), s.num_lids, s.num_lids)
+        got = A.values.local(p).get_values()
+        assert _eq(O, got, OM.nzval)
+    # mul! of each part: SparseUtils.jl:242-250 over its owned rows (owned
+    # columns, then ghost columns, storage order), α on each product
+    got = y.to_host()
+    for p in parts.part_ids:
+        s = part.partition.local(p)
+        I, J, V = trip[p]
+        M = pamd.sparsecsr(0, I, J, V, s.num_lids, s.num_lids)
+        xl = x.to_host().local(p)
+        l2o = np.asarray(s.lid_to_ohid)
+        want = np.zeros(s.num_lids, dtype)
+        a = np.dtype(dtype).type(alpha)
+        for li in s.oid_to_lid - 1:
+            acc = np.dtype(dtype).type(0)
+            for ghost in (False, True):
+                for q in range(M.rowptr[li], M.rowptr[li + 1]):
+                    j = M.colval[q]
+                    if (l2o[j] < 0) == ghost:
+                        acc = acc + (M.nzval[q] * xl[j]) * a
+            want[li] = acc
+        own = s.oid_to_lid - 1
+        if np.dtype(dtype).kind == "c":
+            # Julia's complex product, not numpy's (which may fuse differently): compare to 1 ulp-ish
+            np.testing.assert_allclose(got.local(p)[own], want[own], rtol=1e-13)
+        else:
+            assert np.array_equal(got.local(p)[own], want[own])

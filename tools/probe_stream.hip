@@ -10,6 +10,12 @@
 //   slice_2    slice_w with two slices per wave (grid halved)
 //   (with a 3rd argument) write-only sweeps of y / of 3.57 GB, memset, and
 //   slice_w with y folded into a 1 / 16 / 64 MB ring
+//   (3rd argument "x") slice_w plus the FE27 pattern kernel's x reads (16 B
+//   runs at row + 27 stencil offsets of a 256³ x), or the same folded into
+//   a 1 MB window (L2 hits), or with each dx triple's x shared between
+//   neighbouring lanes (one 16 B run per lane per triple; __shfl or DPP)
+//   (3rd argument "c") slice_w behind a list → offset load chain, with 1,
+//   2, 4 or 8 slices per wave, the next slice's metadata prefetched or not
 //   (3rd argument "e") persistent blocks staging y in LDS per epoch of C
 //   slices and writing it in one burst, with or without a grid barrier
 // hipcc --offload-arch=gfx950 -O3 tools/probe_stream.hip -o probe_stream
@@ -36,23 +42,24 @@ constexpr unsigned MAGIC = 0x9e3779b9u;
 
 __device__ __forceinline__ u32x4 ldnt(const u32x4* p) { return __builtin_nontemporal_load(p); }
 
+template <int UU = U>
 __device__ __forceinline__ u32x4 stream_slice(const u32x4* __restrict__ v, int64_t s, int lane) {
   const int64_t base = s * L * 64;
   u32x4 acc = {0, 0, 0, 0};
   int k = 0;
-  for (; k + U <= L; k += U) {
-    u32x4 t[U];
+  for (; k + UU <= L; k += UU) {
+    u32x4 t[UU];
 #pragma unroll
-    for (int u = 0; u < U; ++u) t[u] = ldnt(v + base + (k + u) * 64 + lane);
+    for (int u = 0; u < UU; ++u) t[u] = ldnt(v + base + (k + u) * 64 + lane);
 #pragma unroll
-    for (int u = 0; u < U; ++u) acc ^= t[u];
+    for (int u = 0; u < UU; ++u) acc ^= t[u];
   }
   for (; k < L; ++k) acc ^= ldnt(v + base + k * 64 + lane);
   return acc;
 }
 
 // WMODE 0: no write (kept live by a never-true test), 1: plain store, 2: non-temporal store
-template <int WMODE, int WPB, int SPW>
+template <int WMODE, int WPB, int SPW, int UU = U>
 __global__ __launch_bounds__(64 * WPB) void k_slice(const u32x4* __restrict__ v, u32x4* __restrict__ y,
                                                    int64_t nslices) {
   const int lane = threadIdx.x & 63;
@@ -61,13 +68,165 @@ __global__ __launch_bounds__(64 * WPB) void k_slice(const u32x4* __restrict__ v,
   for (int j = 0; j < SPW; ++j) {
     const int64_t s = w * SPW + j;
     if (s >= nslices) return;
-    const u32x4 acc = stream_slice(v, s, lane);
+    const u32x4 acc = stream_slice<UU>(v, s, lane);
     if (WMODE == 0) {
       if (acc.x == MAGIC) y[s * 64 + lane] = acc;
     } else if (WMODE == 1) {
       y[s * 64 + lane] = acc;
     } else {
       __builtin_nontemporal_store(acc, y + s * 64 + lane);
+    }
+  }
+}
+
+// slice_w + the x reads of the FE27 pattern kernel: entry k of lane l's two
+// rows (r0 = slice*128 + 2l) reads x[r0 + off[k]] as one 16 B run, off = the
+// 27 offsets {dz*N² + dy*N + dx}, N = 256 (x: N³ doubles).  XWIN: x indices
+// folded into a 1 MB window (always L2 hits) instead of the real 134 MB x.
+__constant__ int c_off[L];
+template <bool XWIN>
+__global__ __launch_bounds__(256) void k_slice_x(const u32x4* __restrict__ v, const double* __restrict__ x,
+                                                 u32x4* __restrict__ y, int64_t nslices, int64_t nx) {
+  const int lane = threadIdx.x & 63;
+  const int64_t s = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (s >= nslices) return;
+  const int64_t base = s * L * 64;
+  const int64_t r0 = s * 128 + 2 * lane;
+  u32x4 acc = {0, 0, 0, 0};
+  double xa = 0.0;
+  int k = 0;
+  for (; k + U <= L; k += U) {
+    u32x4 t[U];
+    double2 xr[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) t[u] = ldnt(v + base + (k + u) * 64 + lane);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      int64_t i = r0 + c_off[k + u];
+      i = i < 0 ? 0 : (i >= nx - 1 ? nx - 2 : i);
+      if (XWIN) i &= (1 << 17) - 2;
+      xr[u] = *reinterpret_cast<const double2*>(x + i);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      acc ^= t[u];
+      xa = xa + xr[u].x * xr[u].y;
+    }
+  }
+  for (; k < L; ++k) {
+    acc ^= ldnt(v + base + k * 64 + lane);
+    int64_t i = r0 + c_off[k];
+    i = i < 0 ? 0 : (i >= nx - 1 ? nx - 2 : i);
+    if (XWIN) i &= (1 << 17) - 2;
+    xa = xa + x[i];
+  }
+  acc.x ^= (unsigned)(xa != 0.5);
+  y[s * 64 + lane] = acc;
+}
+
+// slice_wx with the x of each (dx = -1, 0, +1) triple shared between
+// neighbouring lanes: one 16 B run per lane at dx = 0, the dx = ±1 runs
+// assembled from the neighbours' values (DPP wave shift, or __shfl when
+// DPP is 0), lanes 0 and 63 fetch the one value past the slice's edge
+template <int DPP>
+__device__ __forceinline__ double shift_from_lower(double v) {  // lane l gets lane l-1's v
+  if (DPP) {
+    const long long b = __builtin_bit_cast(long long, v);
+    const int lo = __builtin_amdgcn_update_dpp(0, (int)(b & 0xffffffffll), 0x138, 0xf, 0xf, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), 0x138, 0xf, 0xf, false);
+    return __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned int)lo);
+  }
+  return __shfl_up(v, 1, 64);
+}
+template <int DPP>
+__device__ __forceinline__ double shift_from_upper(double v) {  // lane l gets lane l+1's v
+  if (DPP) {
+    const long long b = __builtin_bit_cast(long long, v);
+    const int lo = __builtin_amdgcn_update_dpp(0, (int)(b & 0xffffffffll), 0x130, 0xf, 0xf, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), 0x130, 0xf, 0xf, false);
+    return __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned int)lo);
+  }
+  return __shfl_down(v, 1, 64);
+}
+template <int DPP, bool ROLL = false>
+__global__ __launch_bounds__(256) void k_slice_x3(const u32x4* __restrict__ v, const double* __restrict__ x,
+                                                  u32x4* __restrict__ y, int64_t nslices, int64_t nx) {
+  const int lane = threadIdx.x & 63;
+  const int64_t s = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (s >= nslices) return;
+  const int64_t base = s * L * 64;
+  const int64_t r0 = s * 128 + 2 * lane;
+  u32x4 acc = {0, 0, 0, 0};
+  double xa = 0.0;
+  // 27 entries = 9 triples; 3 triples (9 entries) per batch
+#pragma unroll(ROLL ? 1 : 3)
+  for (int g = 0; g < 9; g += 3) {
+    u32x4 t[9];
+#pragma unroll
+    for (int u = 0; u < 9; ++u) t[u] = ldnt(v + base + (3 * g + u) * 64 + lane);
+    double2 c[3];
+    double e[3];
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      int64_t i = r0 + c_off[3 * (g + q) + 1];
+      i = i < 2 ? 2 : (i >= nx - 3 ? nx - 4 : i);
+      c[q] = *reinterpret_cast<const double2*>(x + i);
+      e[q] = 0.0;
+      if (lane == 0 || lane == 63) e[q] = x[lane == 0 ? i - 1 : i + 2];
+    }
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      double lo = shift_from_lower<DPP>(c[q].y);
+      double hi = shift_from_upper<DPP>(c[q].x);
+      if (lane == 0) lo = e[q];
+      if (lane == 63) hi = e[q];
+      acc ^= t[3 * q] ^ t[3 * q + 1] ^ t[3 * q + 2];
+      xa = xa + lo * c[q].x + c[q].x * c[q].y + c[q].y * hi;
+    }
+  }
+  acc.x ^= (unsigned)(xa != 0.5);
+  y[s * 64 + lane] = acc;
+}
+
+// slice_w behind the SpMV's metadata chain: the slice's offset comes from
+// soff[list[w]] (two dependent loads) before its first value load; CHAIN 2:
+// each wave streams SPW slices and loads the next slice's metadata while
+// the current one streams (software-pipelined across slices)
+template <int SPW, bool PREF>
+__global__ __launch_bounds__(256) void k_slice_chain(const u32x4* __restrict__ v, u32x4* __restrict__ y,
+                                                     const int32_t* __restrict__ list, const int64_t* __restrict__ soff,
+                                                     int64_t nslices) {
+  const int lane = threadIdx.x & 63;
+  const int64_t w = (int64_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const int64_t w0 = w * SPW;
+  if (w0 >= nslices) return;
+  int64_t s = list[w0];
+  int64_t off = soff[s];
+  for (int j = 0; j < SPW; ++j) {
+    int64_t s_next = 0, off_next = 0;
+    const bool more = j + 1 < SPW && w0 + j + 1 < nslices;
+    if (PREF && more) {
+      s_next = list[w0 + j + 1];
+      off_next = soff[s_next];
+    }
+    u32x4 acc = {0, 0, 0, 0};
+    int k = 0;
+    for (; k + U <= L; k += U) {
+      u32x4 t[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) t[u] = ldnt(v + off + (k + u) * 64 + lane);
+#pragma unroll
+      for (int u = 0; u < U; ++u) acc ^= t[u];
+    }
+    for (; k < L; ++k) acc ^= ldnt(v + off + k * 64 + lane);
+    y[s * 64 + lane] = acc;
+    if (!more) break;
+    if (PREF) {
+      s = s_next;
+      off = off_next;
+    } else {
+      s = list[w0 + j + 1];
+      off = soff[s];
     }
   }
 }
@@ -185,6 +344,53 @@ int main(int argc, char** argv) {
                 ms[ms.size() / 2], ms[0], bytes / (ms[ms.size() / 2] * 1e-3) / 1e9);
     std::fflush(stdout);
   };
+  if (argc > 3 && argv[3][0] == 'c') {  // metadata-chain variants
+    std::vector<int32_t> hl(nslices);
+    std::vector<int64_t> ho(nslices);
+    for (int64_t i = 0; i < nslices; ++i) { hl[i] = (int32_t)i; ho[i] = i * L * 64; }
+    int32_t* dl;
+    int64_t* dof;
+    CK(hipMalloc(&dl, nslices * 4));
+    CK(hipMalloc(&dof, nslices * 8));
+    CK(hipMemcpy(dl, hl.data(), nslices * 4, hipMemcpyHostToDevice));
+    CK(hipMemcpy(dof, ho.data(), nslices * 8, hipMemcpyHostToDevice));
+    const int64_t b4 = (nslices + 3) / 4;
+    for (int round = 0; round < 2; ++round) {
+      run("slice_w", true, [&] { hipLaunchKernelGGL((k_slice<1, 4, 1>), dim3(b4), dim3(256), 0, 0, v, y, nslices); });
+      run("chain1", true, [&] { hipLaunchKernelGGL((k_slice_chain<1, false>), dim3(b4), dim3(256), 0, 0, v, y, dl, dof, nslices); });
+      run("chain2", true, [&] { hipLaunchKernelGGL((k_slice_chain<2, false>), dim3((nslices + 7) / 8), dim3(256), 0, 0, v, y, dl, dof, nslices); });
+      run("chain2_pref", true, [&] { hipLaunchKernelGGL((k_slice_chain<2, true>), dim3((nslices + 7) / 8), dim3(256), 0, 0, v, y, dl, dof, nslices); });
+      run("chain4_pref", true, [&] { hipLaunchKernelGGL((k_slice_chain<4, true>), dim3((nslices + 15) / 16), dim3(256), 0, 0, v, y, dl, dof, nslices); });
+      run("chain8_pref", true, [&] { hipLaunchKernelGGL((k_slice_chain<8, true>), dim3((nslices + 31) / 32), dim3(256), 0, 0, v, y, dl, dof, nslices); });
+    }
+    CK(hipFree(dl));
+    CK(hipFree(dof));
+    return 0;
+  }
+  if (argc > 3 && argv[3][0] == 'x') {  // x-read variants
+    const int64_t N = 256, nx = N * N * N;
+    double* x;
+    CK(hipMalloc(&x, (size_t)nx * 8));
+    CK(hipMemset(x, 0, (size_t)nx * 8));
+    int off[L], t = 0;
+    for (int dz = -1; dz <= 1; ++dz)
+      for (int dy = -1; dy <= 1; ++dy)
+        for (int dx = -1; dx <= 1; ++dx) off[t++] = (int)(dz * N * N + dy * N + dx);
+    CK(hipMemcpyToSymbol(HIP_SYMBOL(c_off), off, sizeof off));
+    const int64_t b4 = (nslices + 3) / 4;
+    for (int round = 0; round < 2; ++round) {
+      run("slice_w", true, [&] { hipLaunchKernelGGL((k_slice<1, 4, 1>), dim3(b4), dim3(256), 0, 0, v, y, nslices); });
+      run("slice_wx", true, [&] { hipLaunchKernelGGL(k_slice_x<false>, dim3(b4), dim3(256), 0, 0, v, x, y, nslices, nx); });
+      run("slice_wx_l2", true, [&] { hipLaunchKernelGGL(k_slice_x<true>, dim3(b4), dim3(256), 0, 0, v, x, y, nslices, nx); });
+      run("slice_wx3_shfl", true, [&] { hipLaunchKernelGGL(k_slice_x3<0>, dim3(b4), dim3(256), 0, 0, v, x, y, nslices, nx); });
+      run("slice_wx3_dpp", true, [&] { hipLaunchKernelGGL(k_slice_x3<1>, dim3(b4), dim3(256), 0, 0, v, x, y, nslices, nx); });
+      run("slice_wx3_dpp_rolled", true, [&] { hipLaunchKernelGGL((k_slice_x3<1, true>), dim3(b4), dim3(256), 0, 0, v, x, y, nslices, nx); });
+      run("slice_w_u9", true, [&] { hipLaunchKernelGGL((k_slice<1, 4, 1, 9>), dim3(b4), dim3(256), 0, 0, v, y, nslices); });
+      run("slice_w_u27", true, [&] { hipLaunchKernelGGL((k_slice<1, 4, 1, 27>), dim3(b4), dim3(256), 0, 0, v, y, nslices); });
+    }
+    CK(hipFree(x));
+    return 0;
+  }
   if (argc > 3 && argv[3][0] == 'e') {  // epoch-staged y variants
     int ncu = 256;
     {
