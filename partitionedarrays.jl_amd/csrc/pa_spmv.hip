@@ -907,6 +907,9 @@ __device__ __forceinline__ void merged_wave(const SpmvTable<T>* __restrict__ tab
   else if constexpr (!SH) spmv_wave<T, R, ALPHA, BMODE, U, 2, false>(a, lw);
 }
 
+// No occupancy cap: amdgpu_waves_per_eu(4) (F32 134 -> 128 VGPRs, a small
+// spill) lost in a same-box A/B: C5 F32 +4.5 %, FE27 F64 +0.4 %, F32 +0.6 %
+// (profiles/r02/stream/ab_waves4.txt).
 template <typename T, int R, bool ALPHA, int BMODE, int U, bool SH>
 __global__ __launch_bounds__(256) void k_spmv_merged(const SpmvTable<T>* __restrict__ tab) {
   merged_wave<T, R, ALPHA, BMODE, U, SH>(tab);
