@@ -291,6 +291,10 @@ int pa_mat_from_dcoo(const pa_coo* coo, int ids_global, int64_t nrows_lids,
 /* Replace the stored values keeping the pattern (same CSC nz order),
  * e.g. after fillstored!/re-assembly (Interfaces.jl:2127-2132).          */
 int pa_mat_set_values(pa_mat* A, const void* nzval);
+/* fillstored!(A, v) (Interfaces.jl:2127-2132): every stored value of the
+ * part (ghost rows included) becomes the scalar *v of the matrix's dtype,
+ * on the device, stream-ordered with the part's other work.              */
+int pa_mat_fillstored(pa_mat* A, const void* v);
 /* nonzeros(A) in CSC nz order, ghost rows included (the device keeps the
  * ghost rows' values beside the SELL slots for exchange!/assemble!(A)).  */
 int pa_mat_get_values(const pa_mat* A, void* nzval);

@@ -502,6 +502,18 @@ end
 async_assemble!(a::HIPMatrix{T}, t0::AbstractPData=PartitionedArrays._empty_tasks(a.exchanger.parts_rcv)) where {T<:DeviceEltype} =
   async_assemble!(+, a, t0)
 
+# fillstored!(a, v) (Interfaces.jl:2127-2132) on the device copies; the host
+# parts are refreshed on their next generic use (sync_host!)
+function LinearAlgebra.fillstored!(a::HIPMatrix{T}, v) where {T<:DeviceEltype}
+  A = dev_mat(a)
+  s = Ref{T}(convert(T, v))
+  for h in A
+    check(ccall((:pa_mat_fillstored, libpa), Cint, (Ptr{Cvoid}, Ptr{T}), h, s))
+  end
+  mark_device_newer!(a)
+  a
+end
+
 # ---- assemble!(I, J, V, rows) (Interfaces.jl:2406-2492) --------------------
 # the triplets go to the device (pa_coo), the ghost rows' triplets move to
 # their owners there (pa_coo_assemble_all: device copies / RCCL), and the

@@ -19,7 +19,7 @@ from .prange import (Exchanger, IndexSet, PRange, add_gids, add_gids_, discover_
                      prange_linear, prange_noids, to_lids_)
 from .device import DeviceMatrix, HIPBackend, HIPDistributedBackend, device_index  # noqa: F401
 from .pvector import (COO, CSC, CSR, PSparseMatrix, PVector, SpMVGraph, assemble_, axmy_, axpy_, cg_, cg_update_,  # noqa: F401
-                      compresscoo, copyto_, csr_init, sparsecsr, dot, exchange_, matvec, mul_, mul_dot_, norm, psum, rmul_,
+                      compresscoo, copyto_, csr_init, sparsecsr, fillstored_, dot, exchange_, matvec, mul_, mul_dot_, norm, psum, rmul_,
                       sub_, xpby_)
 from .ptimers import PTimer  # noqa: F401
 from . import drivers  # noqa: F401

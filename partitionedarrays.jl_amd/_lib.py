@@ -71,6 +71,7 @@ _SIGS = {
                             _p, _i64p, _i64p, _i64p, C.POINTER(_p)],
     "pa_mat_from_dcoo_csr": [_p, C.c_int, C.c_int, C.c_int64, C.c_int64, _p, _p, _i64p, _i64p, _i64p,
                              C.POINTER(_p)],
+    "pa_mat_fillstored": [_p, _p],
     "pa_index_set_gids": [_p, _i64p],
     "pa_add_gids": [_p, C.c_int64, _i64p, C.c_int64, _i64p, _i64p],
     "pa_index_to_lids": [_p, C.c_int64, _i64p],

@@ -2151,6 +2151,19 @@ int pa_mat_set_values(pa_mat* A, const void* nzval) {
   return 0;
 }
 
+// fillstored!(A, v) (Interfaces.jl:2127-2132 → SparseArrays.fillstored!):
+// every stored value of the part becomes v, on the device.  The padding
+// slots take v too (never multiplied: masked or column -1 / 0xFFFF).
+int pa_mat_fillstored(pa_mat* A, const void* v) {
+  CHECK_ARG(A && v, "null argument");
+  HIPC(hipSetDevice(A->ctx->device));
+  const int64_t nv = nvals(A);
+  if (nv) launch_fill(A->dtype, nv, 0, nullptr, A->d_val, v, A->ctx->s_main);
+  HIPC(hipGetLastError());
+  if (refresh_side(A, A->ctx->s_main)) return -1;
+  return 0;
+}
+
 int pa_mat_get_values(const pa_mat* A, void* nzval) {
   CHECK_ARG(A && nzval, "null argument");
   if (load_nz_map(A)) return -1;

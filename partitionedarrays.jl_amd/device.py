@@ -467,6 +467,12 @@ class DeviceMatrix:
         nzval = np.ascontiguousarray(nzval, dtype=self.dtype)
         _lib.call("pa_mat_set_values", self.h, nzval.ctypes.data_as(C.c_void_p))
 
+    def fillstored(self, v):
+        """fillstored!(A, v) on the device (pa_mat_fillstored)."""
+        buf, ptr = _lib.scalar_buf(v, self.dtype)
+        _lib.call("pa_mat_fillstored", self.h, ptr)
+        del buf
+
     def get_values(self):
         """nonzeros(A) in the parent's order (CSC, or CSR for a SparseMatrixCSR
         parent), ghost rows included."""

@@ -465,6 +465,14 @@ class PSparseMatrix:
         return map_parts(lambda m: m.info(), self.values)
 
 
+def fillstored_(a: "PSparseMatrix", v) -> "PSparseMatrix":
+    """LinearAlgebra.fillstored!(a, v) (Interfaces.jl:2127-2132): every
+    stored value of every part becomes v (on the device)."""
+    for M in a.values.parts:
+        M.fillstored(v)
+    return a
+
+
 def matrix_exchanger(values: PData, rows: PRange, cols: PRange) -> Exchanger:
     """matrix_exchanger(values, rows, cols) (Interfaces.jl:2300-2372),
     vectorised: the nonzeros of ghost rows (CSC order k) grouped by the row

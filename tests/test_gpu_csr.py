@@ -331,3 +331,37 @@ def test_csr_device_compress_duplicates_bitexact(be, pamd, O, dtype):
             np.testing.assert_allclose(got.local(p)[own], want[own], rtol=1e-13)
         else:
             assert np.array_equal(got.local(p)[own], want[own])
+
+
+@pytest.mark.parametrize("fmt", [1, 0], ids=["pattern", "int32"])
+@pytest.mark.parametrize("parent", ["csc", "csr"])
+def test_fillstored_on_device(be, pamd, O, fmt, parent):
+    """fillstored!(A, v) (Interfaces.jl:2127-2132) on the device
+    (pa_mat_fillstored): nonzeros(A) all v (ghost rows included), and mul!
+    then equals the oracle's mul! with every stored value = v; test_fem_sa's
+    matrix (stored ghost rows, side rows)."""
+    prev = pamd._lib.tune("spmv_format", fmt)
+    try:
+        parts = be.get_part_ids((2, 2))
+        init = pamd.csr_init(1) if parent == "csr" else None
+        A, _, _, _ = pamd.drivers.fem_sa_problem(parts, 10, init=init)
+        OA, _, _, _ = O.fem_sa_problem(O.get_part_ids((2, 2)), 10,
+                                       init=_csr_init(O, 1) if parent == "csr" else None)
+        v = -0.625
+        pamd.fillstored_(A, v)
+        for M, OM in zip(A.values.parts, OA.values.parts):
+            got = M.get_values()
+            assert got.shape == OM.nzval.shape and np.all(got == v)
+            OM.nzval[:] = v
+        rng = np.random.default_rng(8)
+        x = pamd.PVector.from_host(pamd.map_parts(lambda s: rng.uniform(-1, 1, s.num_lids), A.cols.partition), A.cols)
+        ox = O.PVector(O.PData([t.copy() for t in x.to_host().parts], OA.cols.partition.shape), OA.cols)
+        y = pamd.PVector.undef(A.rows)
+        oy = O.pvector_undef(OA.rows)
+        pamd.mul_(y, A, x)
+        O.mul_(oy, OA, ox)
+        for p in parts.part_ids:
+            own = A.rows.partition.local(p).oid_to_lid - 1
+            assert np.array_equal(y.to_host().local(p)[own], oy.values[p][own])
+    finally:
+        pamd._lib.tune("spmv_format", prev)
