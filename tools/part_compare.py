@@ -15,7 +15,12 @@ import pamd  # noqa: E402
 ap = argparse.ArgumentParser()
 ap.add_argument("--reps", type=int, default=30)
 ap.add_argument("--n", type=int, default=256)
+ap.add_argument("--merge", type=int, default=1, help="pa_tune spmv_merge (0: one launch per slice kind)")
+ap.add_argument("--idlist", type=int, default=1, help="0: keep identity slice lists (spmv_flags bit 4 off)")
 a = ap.parse_args()
+pamd._lib.tune("spmv_merge", a.merge)
+if not a.idlist:
+    pamd._lib.tune("spmv_flags", pamd._lib.tune("spmv_flags", 0) & ~16)
 be = pamd.HIPBackend(devices=[0])
 
 
