@@ -19,7 +19,7 @@ from .backends import PData, exchange, map_parts, unzip
 from .device import (DeviceCOO, DeviceMatrix, DeviceMatrixExchanger, DeviceVector, contexts, device_exchanger,
                      device_index, device_index_gids)
 from .helpers import Table, counts_to_ptrs, trace_setup
-from .prange import Exchanger, PRange, empty_exchanger, hids_are_equal, oids_are_equal
+from .prange import Exchanger, PRange, _cached_eq, empty_exchanger, hids_are_equal, oids_are_equal
 
 
 # ---------------------------------------------------------------------------
@@ -637,10 +637,10 @@ def _spmv_args(c, a, b, alpha, beta):
         raise AssertionError("mul!: c.rows and a.rows own different ids")
     if not (b.rows is a.cols or (oids_are_equal(a.cols, b.rows) and hids_are_equal(a.cols, b.rows))):
         raise AssertionError("mul!: b.rows differs from a.cols")
-    if b.rows is not a.cols:
-        for s, t in zip(a.cols.partition.parts, b.rows.partition.parts):
-            if not (np.array_equal(s.oid_to_lid, t.oid_to_lid) and np.array_equal(s.hid_to_lid, t.hid_to_lid)):
-                raise NotImplementedError("mul!: b.rows must have a.cols' local layout")
+    if b.rows is not a.cols and not _cached_eq(
+            "layout", a.cols, b.rows,
+            lambda s, t: bool(np.array_equal(s.oid_to_lid, t.oid_to_lid) and np.array_equal(s.hid_to_lid, t.hid_to_lid))):
+        raise NotImplementedError("mul!: b.rows must have a.cols' local layout")
     ctxs = contexts(a.values)
     n = len(ctxs)
     ex = b.rows.exchanger

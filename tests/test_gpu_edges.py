@@ -153,3 +153,28 @@ def test_graph_mul_cache_matches_eager(pamd, share):
         for p in parts.part_ids:
             own = A.rows.partition.local(p).oid_to_lid - 1
             assert np.array_equal(r_e.local(p)[own], r_g.local(p)[own])
+
+
+def test_mul_with_equal_copies_of_the_ranges(be, pamd, O):
+    """mul!(c, a, b) with c.rows / b.rows equal copies (not the same objects)
+    of a.rows / a.cols (Interfaces.jl:2253-2255 @checks pass on equal ids):
+    the result equals the oracle's, and the checks are answered from the
+    per-pair cache after the first call (no per-call O(n) host compare)."""
+    import time
+    shape, N = (2, 2, 1), (12, 10, 9)
+    parts = be.get_part_ids(shape)
+    A = pamd.drivers.stencil_operator(parts, N, 27)
+    rows2, cols2 = A.rows.copy(), A.cols.copy()
+    rng = np.random.default_rng(12)
+    xs = {p: rng.uniform(-1, 1, A.cols.partition.local(p).num_lids) for p in parts.part_ids}
+    x = pamd.PVector.from_host(pamd.map_parts(lambda s: xs[s.part], cols2.partition), cols2)
+    y = pamd.PVector.undef(rows2)
+    pamd.mul_(y, A, x)
+    OA = O.stencil_problem(O.get_part_ids(shape), N, 27)
+    ox = O.PVector(O.map_parts(lambda s: xs[s.part].copy(), OA.cols.partition), OA.cols)
+    oy = O.pvector_undef(OA.rows)
+    O.mul_(oy, OA, ox)
+    for p in parts.part_ids:
+        own = A.rows.partition.local(p).oid_to_lid - 1
+        assert np.array_equal(y.to_host().local(p)[own], oy.values[p][own])
+    assert "_eq_cache" in A.cols.__dict__ and any(k[0] == "layout" for k in A.cols._eq_cache)
