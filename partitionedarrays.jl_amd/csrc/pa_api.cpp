@@ -51,6 +51,12 @@ int g_halo_pull = 1;  // pa_tune("halo_pull"): pull-unpack between parts of one 
 int g_spmv_group = 1; // pa_tune("spmv_group"): one launch per phase for the parts sharing a stream pair
 int g_spmv_delta16 = 1;   // pa_tune("spmv_delta16"): int32-column slices with 16-bit column codes where they fit
 int g_spmv_merge = 1;     // pa_tune("spmv_merge"): one launch for every slice kind of every part when no halo is in flight
+// pa_tune("spmv_merge_max"): ... unless one part alone has more slices than
+// this: such a part fills the GPU many times over, and one launch per kind
+// (the kind's own kernel, fewer registers) is faster — FE27 256³ F64 −1.0 %,
+// F32 −2.8 %; C2 (16 k slices) and C5 stay merged (−10 % / −15 %).
+// profiles/r02/open/ab_merge.jsonl.  0: no limit.
+int64_t g_spmv_merge_max = 65536;
 int g_halo_direct = 1;     // pa_tune("halo_direct"): grouped mul! pulls ghosts straight from the owners' x
 int g_halo_transport = 0;  // pa_tune("halo_transport"): 0 parts of this process by device reads, 1 RCCL for all
 int g_comm_cus = 0;   // pa_tune("comm_cus"): CUs reserved for the comm stream (0: priority stream instead)
@@ -815,6 +821,12 @@ int pa_tune(const char* key, int value, int* previous) {
               "spmv_merge: 1 = mul! without a halo in flight (one part, or parts of one stream pair with the direct "
               "pull) runs every slice kind of every part as one launch (default), 0 = one launch per kind");
     slot = &g_spmv_merge;
+  } else if (!std::strcmp(key, "spmv_merge_max")) {
+    CHECK_ARG(value >= 0, "spmv_merge_max: one part with more slices than this runs one launch per kind (0: always merge)");
+    const int prev = (int)std::min<int64_t>(g_spmv_merge_max, INT32_MAX);
+    g_spmv_merge_max = value;
+    if (previous) *previous = prev;
+    return 0;
   } else if (!std::strcmp(key, "halo_direct")) {
     CHECK_ARG(value == 0 || value == 1,
               "halo_direct: 1 = mul! over parts sharing a stream pair reads the ghosts straight from the owners' x "
@@ -2467,7 +2479,9 @@ static int spmv_grouped(int n, pa_mat* const A[], pa_vec* const y[], const pa_in
   // kind of every part in one launch — side rows and int32 slices first, so
   // their few long waves start early, then delta16, multi-pattern, pattern
   int merged = 1;
-  if (g_spmv_merge && (!any_x || direct)) {
+  bool big_part = false;  // one part alone fills the GPU many times: per-kind launches (g_spmv_merge_max)
+  if (g_spmv_merge_max > 0 && n == 1) big_part = A[0]->nslices > g_spmv_merge_max;
+  if (g_spmv_merge && !big_part && (!any_x || direct)) {
     std::vector<SpmvPart> E;
     std::vector<int> W;
     auto add = [&](int which, int i, int64_t nwork, const int32_t* list) {
@@ -2602,7 +2616,7 @@ static int launch_phase(int phase, pa_mat* A, const void* x, void* y, const int3
     add(1, A->nslices, nullptr);
   }
   if (E.empty()) return 0;
-  if (E.size() > 1 && g_spmv_merge) {
+  if (E.size() > 1 && g_spmv_merge && !(g_spmv_merge_max > 0 && A->nslices > g_spmv_merge_max)) {
     const int rc = launch_spmv_merged((int)E.size(), W.data(), E.data(), has_alpha, bmode, alpha, beta, A->ctx,
                                       g_capture_tables, st);
     if (rc < 0) PA_FAIL("mul!: merged launch table (device allocation or copy) failed");
