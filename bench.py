@@ -243,6 +243,14 @@ def main():
     args = ap.parse_args()
     if args.child_pmc:
         return child_pmc(args)
+    # stdout carries exactly one JSON line (rank 0): native libraries print
+    # banners to fd 1 during init (RCCL's version block, gloo's connection
+    # line), so fd 1 points at stderr until the line is written
+    out_fd = os.dup(1)
+    os.dup2(2, 1)
+
+    def emit(line):
+        os.write(out_fd, (json.dumps(line) + "\n").encode())
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -311,7 +319,7 @@ def main():
     if args.cg > 0:
         line = cg_mode(args, pamd, backend, parts, A, ngpu, use_dist, sync)
         if rank == 0:
-            print(json.dumps(line), flush=True)
+            emit(line)
         if use_dist:
             dist.destroy_process_group()
         return
@@ -479,7 +487,7 @@ def main():
     if rank == 0 and ngpu == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(args.kind, args.n, args.cpu_seconds)
     if rank == 0:
-        print(json.dumps(line), flush=True)
+        emit(line)
     if use_dist:
         dist.destroy_process_group()
 
