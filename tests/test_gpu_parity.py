@@ -320,3 +320,34 @@ def test_beta_zero_overwrites_nan_inf(be, pamd, O, fmt, alpha):
             assert np.array_equal(g.view(np.uint64), r.view(np.uint64)), (p, literal)
             e = got.local(p)[empty[p]]
             assert np.array_equal(e.view(np.uint64), np.zeros(len(e), np.uint64)), "empty rows must be +0.0"
+
+
+@pytest.mark.parametrize("dtype", [np.float64, np.float32, np.complex128, np.complex64])
+def test_lane_shared_x_runs_bitexact(be, pamd, O, dtype):
+    """spmv_flags bit 9 (opt-in): triple-pattern slices read one x run per
+    stencil triple and take the dx = ±1 runs from the neighbouring lanes
+    (DPP wave shifts) — the same terms in the same order, so bit-exact
+    against the oracle, α ≠ 1 included."""
+    prev = pamd._lib.tune("spmv_flags", 0)
+    pamd._lib.tune("spmv_flags", prev | 512)
+    try:
+        shape, N = (2, 1, 2), (13, 9, 10)
+        parts = be.get_part_ids(shape)
+        A = pamd.drivers.stencil_operator(parts, N, 27, dtype)
+        rng = np.random.default_rng(SEED + 9)
+        xs = {p: _rand(rng, A.cols.partition.local(p).num_lids, dtype) for p in parts.part_ids}
+        x = pamd.PVector.from_host(pamd.map_parts(lambda s: xs[s.part], A.cols.partition), A.cols)
+        OA = O.stencil_problem(O.get_part_ids(shape), N, 27, dtype)
+        for alpha in (1.0, 0.75):
+            y = pamd.PVector.undef(A.rows, dtype)
+            pamd.mul_(y, A, x, alpha, 0.0)
+            ox = O.PVector(O.map_parts(lambda s: _to_oracle(O, xs[s.part]), OA.cols.partition), OA.cols)
+            oy = O.pvector_undef(OA.rows, dtype)
+            oa = np.float32(alpha) if np.dtype(dtype) in (np.float32, np.complex64) else alpha
+            O.mul_(oy, OA, ox, oa, 0.0)
+            got = y.to_host()
+            for p in parts.part_ids:
+                own = A.rows.partition.local(p).oid_to_lid - 1
+                assert _eq(O, got.local(p)[own], _sel(O, oy.values[p], own)), (alpha, p)
+    finally:
+        pamd._lib.tune("spmv_flags", prev)
