@@ -55,3 +55,31 @@ def test_error_reporting_without_gpu(pamd):
         import pytest
         with pytest.raises(pamd.PAError):
             pamd.HIPBackend()
+
+
+def test_tune_knobs_round_trip_and_reject_bad_values(pamd):
+    """pa_tune (no device needed): every knob returns its previous value and
+    refuses out-of-range values with a PAError; spmv_flags keeps bit 8 (the
+    per-matrix CSR flag) out of the user's reach."""
+    knobs = {"spmv_merge": 0, "spmv_merge_max": 1024, "spmv_group": 0, "spmv_unroll": 4, "spmv_delta16": 0,
+             "long_rows_exact": 0, "halo_direct": 0}
+    for k, v in knobs.items():
+        prev = pamd._lib.tune(k, v)
+        assert pamd._lib.tune(k, prev) == v, k
+    prev = pamd._lib.tune("spmv_flags", 0)
+    try:
+        assert pamd._lib.tune("spmv_flags", prev | 512) == 0
+        for bad in (256, 1024, -1):
+            try:
+                pamd._lib.tune("spmv_flags", bad)
+                raise AssertionError(f"spmv_flags accepted {bad}")
+            except pamd.PAError:
+                pass
+    finally:
+        pamd._lib.tune("spmv_flags", prev)
+    for k, bad in (("spmv_merge", 2), ("spmv_merge_max", -1), ("spmv_unroll", 3)):
+        try:
+            pamd._lib.tune(k, bad)
+            raise AssertionError(f"{k} accepted {bad}")
+        except pamd.PAError:
+            pass
