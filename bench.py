@@ -59,6 +59,15 @@ def host_cores():
     return max(1, min(16, n))
 
 
+def _spmv_ref(*argv, timeout=900):
+    exe = os.path.join(ROOT, "oracle", "build", "spmv_ref")
+    if not os.path.exists(exe):
+        subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle")], check=True)
+    out = subprocess.run([exe, *map(str, argv)], check=True, capture_output=True, text=True,
+                         timeout=timeout).stdout
+    return json.loads(out.strip().splitlines()[-1])
+
+
 def cpu_baseline(kind, n, seconds=12.0):
     """oracle/build/spmv_ref: the reference's CSC column loop
     (SparseUtils.jl:157-187) restated in C ("port"), run as MPIBackend would
@@ -66,23 +75,36 @@ def cpu_baseline(kind, n, seconds=12.0):
     its block of rows of the SAME operator as the GPU line (n^3 nodes), a
     barrier per SpMV.  Reported in the GPU line's CSR-equivalent GB/s
     (SURVEY.md §8d bytes) and ms per SpMV; a 1-rank run on 128^3 rides along."""
-    exe = os.path.join(ROOT, "oracle", "build", "spmv_ref")
-    if not os.path.exists(exe):
-        subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle")], check=True)
-
-    def run(ranks, nn, secs):
-        out = subprocess.run([exe, "--kind", str(kind), "--n", str(nn), "--seconds", str(secs), "--ranks",
-                              str(ranks)], check=True, capture_output=True, text=True, timeout=600).stdout
-        return json.loads(out.strip().splitlines()[-1])
     cores = host_cores()
-    r = run(cores, n, seconds)
-    r1 = run(1, 128, 3.0)
+    r = _spmv_ref("--kind", kind, "--n", n, "--seconds", seconds, "--ranks", cores)
+    r1 = _spmv_ref("--kind", kind, "--n", 128, "--seconds", 3.0, "--ranks", 1)
     return {"value": round(r["gbps"], 3), "unit": "GB/s (SURVEY.md 8d CSR bytes, like csr_equivalent_gbs)",
             "ms_per_spmv": round(1e3 * r["sec_per_spmv"], 3), "cores": cores, "kind": "port",
             "sample": f"the benched operator ({kind}-pt, {n}^3 nodes, {r['nnz']} nnz), {r['reps']} SpMVs in "
                       f"~{seconds:.0f} s, Int64 CSC column loop (SparseUtils.jl:157-187) in C, {cores} "
                       f"MPIBackend-like ranks (threads, row blocks of PRange(parts, n), barrier per SpMV)",
             "single_core_gbps_128": round(r1["gbps"], 3)}
+
+
+def cpu_baseline_mpi(kind, dims, shape, seconds=12.0):
+    """oracle/build/spmv_ref --mpi: MPIBackend over the SAME Cartesian parts
+    as the GPU line (global nodes `dims`, parts `shape`), one rank per part
+    on one host core each (mpiexec -n P with one core per rank, SURVEY.md
+    §8d), each rank with its local CSC (owned rows over owned then ghost
+    columns, Int64), its Exchanger and, in every mul!, the halo exchange of
+    x (pack, delivery, unpack) between the owned and the ghost column loops
+    (Interfaces.jl:2246-2275, MPIBackend.jl:261-309).  GB/s of SURVEY.md §8d
+    CSR bytes summed over the ranks (halo pack/unpack included)."""
+    P = int(np.prod(shape))
+    r = _spmv_ref("--kind", kind, "--dims", *dims, "--parts", *shape, "--mpi", "--seconds", seconds)
+    return {"value": round(r["gbps"], 3), "unit": "GB/s (SURVEY.md 8d CSR bytes incl. halo, all ranks)",
+            "ms_per_spmv": round(1e3 * r["sec_per_spmv"], 3), "cores": P, "kind": "port",
+            "ranks": P, "halo_values_per_spmv": r["halo_values"],
+            "sample": (f"the benched operator ({kind}-pt, {dims[0]}x{dims[1]}x{dims[2]} nodes, {r['nnz']} nnz) on "
+                       f"Cartesian parts {tuple(shape)}, {r['reps']} mul! in ~{seconds:.0f} s: {P} MPIBackend-like "
+                       f"ranks (one thread each), Int64 CSC column loop (SparseUtils.jl:157-187) over the owned "
+                       f"then the ghost columns, halo exchange of x (pack, delivery, unpack) in every mul!, "
+                       f"barrier per mul!; build {r['build_s']:.1f} s untimed")}
 
 
 PROBE_BYTES = 1 << 30
@@ -168,6 +190,102 @@ def child_pmc(args):
     pamd._lib.hbm_probe(0, PROBE_BYTES, 1)
 
 
+def halo_1gpu(args, pamd, dtype, S, reps_phase=20):
+    """BASELINE config 3 on the one GPU: the SAME global operator as the
+    headline (args.n^3 nodes, args.kind points) split into Cartesian parts
+    (2,2,2), all eight parts on cuda:0 (HIPBackend, one stream pair).  Every
+    mul! exchanges the halo of x between the parts (Interfaces.jl:2258-2272:
+    async_exchange!(b) before the owned block, the ghost block after it) and
+    is timed exactly like the headline: W untimed calls, then K calls
+    bracketed by synchronisation, wall clock / K; the HIP-event span on the
+    compute stream gives the kernel time.  Bytes: format_bytes summed over
+    the parts (matrix as loaded, x read once incl. ghosts, y written once,
+    halo pack + unpack (4+2S) per value on both sides)."""
+    be = pamd.HIPBackend(devices=[0])
+    shape = (2, 2, 2)
+    parts = be.get_part_ids(shape)
+    N = (args.n,) * 3
+    t_setup = time.perf_counter()
+    partition = pamd.drivers.stencil_partition(parts, N, args.kind)
+    A = pamd.drivers.stencil_operator(parts, N, args.kind, dtype, partition=partition)
+    x = pamd.PVector.from_host(pamd.map_parts(
+        lambda s: np.random.default_rng(20250114 + s.part).uniform(-1, 1, s.num_lids).astype(dtype),
+        A.cols.partition), A.cols)
+    y = pamd.PVector.undef(A.rows, dtype)
+    ctxs = [be.context(p) for p in parts.part_ids]
+
+    def sync():
+        for c in ctxs:
+            c.sync()
+    sync()
+    t_setup = time.perf_counter() - t_setup
+    ex = A.cols.exchanger
+    B = Cb = 0
+    ghosts = halo_vals = 0
+    for p in parts.part_ids:
+        info = A.values.local(p).info()
+        s = A.cols.partition.local(p)
+        ns, nr = len(ex.lids_snd.local(p).data), len(ex.lids_rcv.local(p).data)
+        B += format_bytes(info, s.num_hids, ns, nr, S)
+        Cb += csr_bytes(info["nnz"], info["nrows"], s.num_hids, ns, nr, S)
+        ghosts += s.num_hids
+        halo_vals += nr
+    for _ in range(args.warmup):
+        pamd.mul_(y, A, x)
+    sync()
+    c0 = ctxs[0]
+    t0 = time.perf_counter()
+    c0.span_start()
+    for _ in range(args.steps):
+        pamd.mul_(y, A, x)
+    c0.span_stop()
+    sync()
+    el = (time.perf_counter() - t0) / args.steps
+    span = c0.span_ms() / args.steps
+    # per-phase attribution (untimed calls; grouped launches report on part 1)
+    for c in ctxs:
+        c.set_timing(True)
+    for _ in range(reps_phase):
+        pamd.mul_(y, A, x)
+    sync()
+    ph = c0.kernel_times()
+    for c in ctxs:
+        c.set_timing(False)
+    # host-issue time of one mul! (the enqueue alone, the GPU kept busy)
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        pamd.mul_(y, A, x)
+    host_us = 1e6 * (time.perf_counter() - t0) / args.steps
+    sync()
+    out = {
+        "workload": (f"mul!(y,A,x), {args.kind}-pt operator, {args.n}^3 nodes in total (BASELINE config 3), "
+                     f"Cartesian parts {shape}, all 8 parts on cuda:0; halo exchange of x between the parts "
+                     "in every step (direct pull of the ghosts from their owners' x, then the SpMV)"),
+        "parts": list(shape),
+        "ms_per_step": round(1e3 * el, 4),
+        "value": round(B / el / 1e9, 2),
+        "unit": "GB/s",
+        "frac": round(B / el / 1e9 / HBM_PEAK_GBS, 4),
+        "bytes_per_step": int(B),
+        "csr_equivalent_gbs": round(Cb / el / 1e9, 2),
+        "ghosts_all_parts": int(ghosts),
+        "halo_values_per_step": int(halo_vals),
+        "kernel_ms": round(span, 4),
+        "kernel_frac": round(B / (span * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+        "kernel_ms_note": "HIP events on the parts' shared compute stream around the K timed steps, / K",
+        "per_part_ms": {"interior_ms": round(ph["interior_ms"], 4), "halo_wait_ms": round(ph["halo_wait_ms"], 4),
+                        "boundary_ms": round(ph["boundary_ms"], 4), "calls": ph["calls"],
+                        "note": ("all 8 parts in each phase (grouped launches, one stream): halo_wait_ms is "
+                                 "the direct pull of every ghost from its owner's x; no slice runs before it "
+                                 "(interior_ms 0); boundary_ms is every slice in one merged launch")},
+        "host_issue_us_per_mul": round(host_us, 1),
+        "setup_s": round(t_setup, 2),
+    }
+    del A, x, y
+    return out
+
+
 def cg_mode(args, pamd, backend, parts, A, ngpu, use_dist, sync):
     """--cg K: IterativeSolvers.cg! iterations (BASELINE config 4) on the same
     operator: per iteration 1 mul! (+halo), dot, norm, 3 broadcasts.  Prints
@@ -179,8 +297,12 @@ def cg_mode(args, pamd, backend, parts, A, ngpu, use_dist, sync):
     b = pamd.PVector.from_host(pamd.map_parts(
         lambda s: np.random.default_rng(7 + s.part).uniform(-1, 1, s.num_lids).astype(dtype), cols.partition), cols)
     out = {}
-    variants = {"device": dict(device=True, batch=16), "fused": dict(fused=True), "unfused": dict(fused=False)}
+    variants = {"device": dict(device=True, batch=16), "device_sweep_u": dict(device=True, batch=16),
+                "fused": dict(fused=True), "unfused": dict(fused=False)}
     for name, kw in variants.items():
+        # device_sweep_u: the device recurrence with u .= r .+ β.*u as its own
+        # sweep (pa_tune cg_fuse 0) instead of inside the SpMV
+        prev_fuse = pamd._lib.tune("cg_fuse", 0 if name == "device_sweep_u" else 1)
         x = pamd.PVector.undef(cols, dtype).fill_(0)
         pamd.cg_(x, A, b, reltol=0.0, maxiter=args.warmup, **kw)
         sync()
@@ -197,15 +319,18 @@ def cg_mode(args, pamd, backend, parts, A, ngpu, use_dist, sync):
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             el = float(t.item())
         out[name] = (1e3 * el / max(1, len(hist)), len(hist), hist[-1] if hist else None)
+        pamd._lib.tune("cg_fuse", prev_fuse)
     p0 = parts.part_ids[0]
     info = A.values.local(p0).info()
     S = np.dtype(dtype).itemsize
     n = info["nrows"]
     s0 = cols.partition.local(p0)
     ns, nr = len(cols.exchanger.lids_snd.local(p0).data), len(cols.exchanger.lids_rcv.local(p0).data)
-    # per iteration of the device recurrence: mul! (format bytes, halo included)
-    # + k_cg_xu (x, u read+write, r read) + the fused dot's u re-read + k_cg_xr (r read+write, c read)
-    it_bytes = format_bytes(info, s0.num_hids, ns, nr, S) + 9 * s0.num_lids * S
+    # per iteration of the device recurrence (u update inside the SpMV): mul!
+    # (format bytes: matrix, one x read, c written, halo) + the second gathered
+    # vector (r and u_old both read) + u_new written + x read+written
+    # (deferred x .+= α.*u) + k_cg_xr (r read+written, c read)
+    it_bytes = format_bytes(info, s0.num_hids, ns, nr, S) + 7 * s0.num_lids * S
     rows_all = n * ngpu
     line = {"metric": "CG iteration time (weak scaling, BASELINE config 4)",
             "value": round(out["device"][0], 4), "unit": "ms/iteration", "higher_is_better": False,
@@ -213,12 +338,14 @@ def cg_mode(args, pamd, backend, parts, A, ngpu, use_dist, sync):
             "dtype": args.dtype, "data": "synthetic (seeded uniform b, x0 = 0)",
             "config": {"workload": f"cg! on the {args.kind}-pt operator, {args.n}^3 nodes per GPU",
                        "dofs": rows_all, "recurrence": "scalars on the device (pa_cg_solve_all, batch 16)",
+                       "device_sweep_u_ms_per_iteration": round(out["device_sweep_u"][0], 4),
                        "host_driven_fused_ms_per_iteration": round(out["fused"][0], 4),
                        "host_driven_unfused_ms_per_iteration": round(out["unfused"][0], 4),
                        "algorithmic_bytes_per_iteration_per_gpu": it_bytes,
                        "gbs_per_gpu_device": round(it_bytes / (out["device"][0] * 1e-3) / 1e9, 1),
                        "final_residual": out["device"][2],
-                       "same_history_as_host_driven": out["device"][2] == out["fused"][2]}}
+                       "same_history_as_host_driven": out["device"][2] == out["fused"][2],
+                       "same_history_as_sweep_u": out["device"][2] == out["device_sweep_u"][2]}}
     return line
 
 
@@ -235,6 +362,8 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 HBM-traffic passes")
+    ap.add_argument("--no-halo-leg", action="store_true",
+                    help="skip the halo_1gpu object (config 3 on (2,2,2) parts of the one GPU)")
     ap.add_argument("--child-pmc", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--cg", type=int, default=0, help="time K CG iterations instead (own JSON line)")
     ap.add_argument("--distributed", action="store_true",
@@ -408,6 +537,9 @@ def main():
         bytes_int32 += format_bytes(dict(inf, **A.values.local(p).traffic()), nh, ns_, nr_, S)
     pamd._lib.tune("spmv_format", prev)
     box = box_hbm_gbs(pamd, spmv_bytes // 2) if world == 1 and ngpu == 1 else None
+    halo_leg = None
+    if world == 1 and ngpu == 1 and not args.strong and not args.no_halo_leg:
+        halo_leg = halo_1gpu(args, pamd, dtype, S)
     traffic, tnote = (None, {"note": "skipped (--no-pmc)"})
     if rank == 0 and ngpu == 1 and not args.no_pmc:
         traffic, tnote = pmc_traffic(args)
@@ -484,8 +616,15 @@ def main():
                          "rate next to the 8 TB/s spec (boxes differ by up to ~20 %)"),
         },
     }
-    if rank == 0 and ngpu == 1 and not args.no_cpu_baseline:
-        line["cpu_baseline"] = cpu_baseline(args.kind, args.n, args.cpu_seconds)
+    if halo_leg is not None:
+        line["halo_1gpu"] = halo_leg
+    if rank == 0 and not args.no_cpu_baseline:
+        if ngpu == 1:
+            line["cpu_baseline"] = cpu_baseline(args.kind, args.n, args.cpu_seconds)
+            if halo_leg is not None:
+                halo_leg["cpu_baseline"] = cpu_baseline_mpi(args.kind, (args.n,) * 3, (2, 2, 2), args.cpu_seconds)
+        else:
+            line["cpu_baseline"] = cpu_baseline_mpi(args.kind, N, shape, args.cpu_seconds)
     if rank == 0:
         emit(line)
     if use_dist:

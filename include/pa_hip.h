@@ -80,9 +80,17 @@ int pa_device_count(int* count);
  *               straight from its owner's x on the compute stream (no
  *               pack, no cross-stream event; default), 0: pack + pull on
  *               the comm stream overlapped with the interior slices;
- * "halo_transport" 0: parts of one process exchange by device reads/copies
- *               (default), 1: RCCL send/recv for every part that has a
- *               communicator (pa_comm_init_all / pa_comm_init_rank);
+ * "halo_transport" 0 (default): parts of one process exchange by device
+ *               reads/copies, except parts whose communicator came from
+ *               pa_comm_init_all (RCCL, per context); 1: RCCL send/recv for
+ *               every part that has a communicator;
+ * "spmv_quadsort" 1: a matrix whose slices are mostly not pattern slices
+ *               (irregular partitions) gets the quad-sorted layout: lanes
+ *               of R consecutive rows ordered so that whole slices become
+ *               pattern or quad-run slices (default; matrices built
+ *               afterwards), 2: every matrix (tests), 0: off;
+ * "cg_fuse"     1: the device CG evaluates u .= r .+ beta.*u inside the
+ *               SpMV (default), 0: as its own sweep;
  * "spmv_group"  1: the parts of one process sharing a stream pair run each
  *               mul! phase as one launch (default), 0: launches per part;
  * "spmv_lds", "comm_cus": occupancy / CU-mask experiments (default 0).    */
@@ -116,10 +124,10 @@ int pa_comm_init_rank(pa_ctx* ctx, const unsigned char id[128]);
  * devices of ctx[0..n-1] = parts 1..nparts, in order: one rank per device,
  * in order of first appearance; parts of one device share its rank, and
  * must share their stream pair, so a segment between them is a send to
- * self).  With pa_tune("halo_transport", 1) every halo segment then moves by
- * the same grouped ncclSend/ncclRecv as across processes
- * (MPIBackend.jl:261-309), posted in (sender part, receiver part) order;
- * with 0 (default) parts of one process read each other's buffers.      */
+ * self).  Every halo segment of these contexts then moves by the same
+ * grouped ncclSend/ncclRecv as across processes (MPIBackend.jl:261-309),
+ * posted in (sender part, receiver part) order; contexts without it (or
+ * not from pa_comm_init_all) read each other's buffers.                  */
 int pa_comm_init_all(int n, pa_ctx* const ctx[]);
 /* Halo bytes this part has posted to RCCL sends / receives so far (what the
  * grouped ncclSend/ncclRecv carried for it; 0 when every segment moved by
@@ -333,6 +341,11 @@ int pa_mat_multipattern_info(const pa_mat* A, int64_t* multi_slices);
  * signed 15-bit delta, a ghost column as the slice's smallest ghost column
  * + 15 bits — stream 2 B of column id per slot instead of 4.              */
 int pa_mat_delta16_info(const pa_mat* A, int64_t* delta16_slices);
+/* Quad-run slices (kind 4: every lane's R rows read R consecutive columns,
+ * one column per entry and lane) and whether the layout is quad-sorted
+ * (lanes of R consecutive rows ordered by class, irregular partitions;
+ * pa_tune "spmv_quadsort").  Encoding only: results are unchanged.       */
+int pa_mat_quadrun_info(const pa_mat* A, int64_t* quadrun_slices, int* quad_sorted);
 
 /* Bytes one mul! streams from this matrix in its current encoding
  * (pa_tune("spmv_format")), as its kernels load them: values (padding
@@ -460,7 +473,10 @@ int pa_mat_stencil(pa_ctx* ctx, int dtype, int kind, const int64_t gdims[3],
  * the interior slices, the halo completion seen by the compute stream (wait
  * for the transport + unpack, after the interior slices) and the boundary
  * slices (+ long rows, fused-dot fold), and the number of calls; it clears
- * the record.  pa_ctx_last_kernel_ms: the interior and boundary means.    */
+ * the record.  With the direct pull (parts sharing a stream pair,
+ * halo_direct) no slice runs before the halo is complete: interior is 0,
+ * halo is the pull kernel, boundary is every slice.
+ * pa_ctx_last_kernel_ms: the interior and boundary means.                  */
 int pa_ctx_set_timing(pa_ctx* ctx, int enable);
 int pa_ctx_kernel_times(pa_ctx* ctx, float* interior_ms, float* halo_ms,
                         float* boundary_ms, int* count);

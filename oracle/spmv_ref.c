@@ -52,6 +52,15 @@
  *      1014-1030), each rank holding the CSC of its owned rows over its local
  *      columns and running the column loop on its own copy of x, then a
  *      barrier (the halo exchange and PTimer's max-over-ranks).
+ *  spmv_ref --kind 27|7 (--n N | --dims X Y Z) --parts PX PY PZ --mpi
+ *      (--seconds S | --reps R) [--xin f --yout f]
+ *      CPU baseline beside the multi-GPU lines: MPIBackend over the Cartesian
+ *      parts, one rank (thread, core) per part, each with its local CSC, its
+ *      Exchanger and a halo exchange of x in every mul! (run_mpi below)
+ *  spmv_ref --kind 27|7 --n N --dtype f32|c128 --xin f --yout f
+ *      one part, the literal column loop in Float32 / ComplexF64
+ * --dims gives the global nodes per dimension (default N N N; the operator's
+ * h follows N[0], as drivers.py stencil_coeffs).
  * Every mode prints one JSON line.
  */
 #define _POSIX_C_SOURCE 200809L
@@ -77,7 +86,7 @@ static void* xmalloc(size_t n) {
 
 /* ---- the operators ------------------------------------------------------ */
 static double Ke[64];
-static int64_t N;
+static int64_t N3[3];          /* global nodes per dim (x, y, z) */
 static int kind;
 static double fd_diag, fd_off;
 static int K;                 /* stencil points */
@@ -99,7 +108,7 @@ static void q1_hex_ke(double h) {
 }
 
 static int dirichlet(int64_t x, int64_t y, int64_t z) {
-  return x == 0 || y == 0 || z == 0 || x == N - 1 || y == N - 1 || z == N - 1;
+  return x == 0 || y == 0 || z == 0 || x == N3[0] - 1 || y == N3[1] - 1 || z == N3[2] - 1;
 }
 
 /* entry (row node g, column node g+d): Ke summed over the cells holding both,
@@ -110,15 +119,15 @@ static double fe_value(int64_t gx, int64_t gy, int64_t gz, int dx, int dy, int d
   for (int cz = -1; cz <= 0; ++cz) {
     int64_t c2 = gz + cz;
     int bz = (int)(gz + dz - c2);
-    if (c2 < 0 || c2 > N - 2 || bz < 0 || bz > 1) continue;
+    if (c2 < 0 || c2 > N3[2] - 2 || bz < 0 || bz > 1) continue;
     for (int cy = -1; cy <= 0; ++cy) {
       int64_t c1 = gy + cy;
       int by = (int)(gy + dy - c1);
-      if (c1 < 0 || c1 > N - 2 || by < 0 || by > 1) continue;
+      if (c1 < 0 || c1 > N3[1] - 2 || by < 0 || by > 1) continue;
       for (int cx = -1; cx <= 0; ++cx) {
         int64_t c0 = gx + cx;
         int bx = (int)(gx + dx - c0);
-        if (c0 < 0 || c0 > N - 2 || bx < 0 || bx > 1) continue;
+        if (c0 < 0 || c0 > N3[0] - 2 || bx < 0 || bx > 1) continue;
         int a = (int)(gx - c0) + 2 * (int)(gy - c1) + 4 * (int)(gz - c2);
         double v = Ke[a * 8 + bx + 2 * by + 4 * bz];
         acc = first ? v : acc + v;
@@ -133,11 +142,11 @@ static double ncells(int64_t gx, int64_t gy, int64_t gz) {
   double acc = 0.0;
   int first = 1;
   for (int cz = -1; cz <= 0; ++cz) {
-    if (gz + cz < 0 || gz + cz > N - 2) continue;
+    if (gz + cz < 0 || gz + cz > N3[2] - 2) continue;
     for (int cy = -1; cy <= 0; ++cy) {
-      if (gy + cy < 0 || gy + cy > N - 2) continue;
+      if (gy + cy < 0 || gy + cy > N3[1] - 2) continue;
       for (int cx = -1; cx <= 0; ++cx) {
-        if (gx + cx < 0 || gx + cx > N - 2) continue;
+        if (gx + cx < 0 || gx + cx > N3[0] - 2) continue;
         acc = first ? 1.0 : acc + 1.0;
         first = 0;
       }
@@ -149,7 +158,7 @@ static double ncells(int64_t gx, int64_t gy, int64_t gz) {
 static double dirichlet_val(int64_t x, int64_t y, int64_t z) { return kind == 7 ? 1.0 : ncells(x, y, z); }
 
 static void setup_operator(void) {
-  const double h = 2.0 / (double)(N - 1);
+  const double h = 2.0 / (double)(N3[0] - 1);  /* drivers.py stencil_coeffs: h from N[0] */
   q1_hex_ke(h);
   fd_diag = -((-6.0) / (h * h));
   fd_off = -(1.0 / (h * h));
@@ -161,21 +170,21 @@ static void setup_operator(void) {
         if (kind == 7 && nz > 1) continue;
         off_d[K][0] = dx; off_d[K][1] = dy; off_d[K][2] = dz;
         /* every non-Dirichlet node has all 8 cells: the same values as node (1,1,1) */
-        interior_val[K] = kind == 7 ? (nz == 0 ? fd_diag : fd_off) : (N >= 3 ? fe_value(1, 1, 1, dx, dy, dz) : 0.0);
+        interior_val[K] = kind == 7 ? (nz == 0 ? fd_diag : fd_off) : (N3[0] >= 3 && N3[1] >= 3 && N3[2] >= 3 ? fe_value(1, 1, 1, dx, dy, dz) : 0.0);
         ++K;
       }
 }
 
 /* row r's entries (ascending column = lexicographic neighbour order) */
 static int row_entries(int64_t r, int64_t* cols, double* vals) {
-  int64_t x = r % N, y = (r / N) % N, z = r / (N * N);
+  int64_t x = r % N3[0], y = (r / N3[0]) % N3[1], z = r / (N3[0] * N3[1]);
   if (dirichlet(x, y, z)) {
     cols[0] = r;
     vals[0] = dirichlet_val(x, y, z);
     return 1;
   }
   for (int k = 0; k < K; ++k) {
-    cols[k] = (x + off_d[k][0]) + N * ((y + off_d[k][1]) + N * (z + off_d[k][2]));
+    cols[k] = (x + off_d[k][0]) + N3[0] * ((y + off_d[k][1]) + N3[1] * (z + off_d[k][2]));
     vals[k] = interior_val[k]; /* == fe_value at every non-Dirichlet node (checked by --literal) */
   }
   return K;
@@ -232,7 +241,7 @@ static inline int64_t shell_idx(const Part* q, int64_t ex, int64_t ey, int64_t e
 /* add_gids!(rows, J) over the row-wise COO: ghosts in first-touch order */
 static void build_part(Part* q, int part) {
   int c[3] = {(part - 1) % P3[0], ((part - 1) / P3[0]) % P3[1], (part - 1) / (P3[0] * P3[1])};
-  for (int d = 0; d < 3; ++d) oid_range(N, P3[d], c[d] + 1, &q->lo[d], &q->n[d]);
+  for (int d = 0; d < 3; ++d) oid_range(N3[d], P3[d], c[d] + 1, &q->lo[d], &q->n[d]);
   q->nown = q->n[0] * q->n[1] * q->n[2];
   const int64_t ext = (q->n[0] + 2) * (q->n[1] + 2) * (q->n[2] + 2);
   q->shell = xmalloc((size_t)ext * sizeof(int32_t));
@@ -255,7 +264,7 @@ static void build_part(Part* q, int part) {
   q->nghost = nh;
 }
 
-static inline int64_t gid3(int64_t x, int64_t y, int64_t z) { return x + N * (y + N * z); }
+static inline int64_t gid3(int64_t x, int64_t y, int64_t z) { return x + N3[0] * (y + N3[1] * z); }
 
 /* y[owned row] of one part, in the reference's order: the owned_owned
  * block's columns by oid, then the owned_ghost block's by hid */
@@ -544,19 +553,22 @@ static void* rank_run(void* arg) {
   return NULL;
 }
 
-static double* read_vec(const char* path, int64_t n) {
-  double* v = xmalloc((size_t)n * sizeof(double));
+static void* read_bytes(const char* path, size_t nbytes) {
+  void* v = xmalloc(nbytes);
   FILE* f = fopen(path, "rb");
-  if (!f || fread(v, sizeof(double), (size_t)n, f) != (size_t)n) { fprintf(stderr, "bad input file %s\n", path); exit(1); }
+  if (!f || fread(v, 1, nbytes, f) != nbytes) { fprintf(stderr, "bad input file %s\n", path); exit(1); }
   fclose(f);
   return v;
 }
 
-static void write_vec(const char* path, const double* v, int64_t n) {
+static void write_bytes(const char* path, const void* v, size_t nbytes) {
   FILE* f = fopen(path, "wb");
-  if (!f || fwrite(v, sizeof(double), (size_t)n, f) != (size_t)n) { fprintf(stderr, "cannot write %s\n", path); exit(1); }
+  if (!f || fwrite(v, 1, nbytes, f) != nbytes) { fprintf(stderr, "cannot write %s\n", path); exit(1); }
   fclose(f);
 }
+
+static double* read_vec(const char* path, int64_t n) { return read_bytes(path, (size_t)n * sizeof(double)); }
+static void write_vec(const char* path, const double* v, int64_t n) { write_bytes(path, v, (size_t)n * sizeof(double)); }
 
 static void seeded_vec(double* B, int64_t n) {
   uint64_t s = 20250114u;
@@ -593,18 +605,334 @@ static int run_ranks(int ranks, int reps, double seconds, const double* B, int64
     for (int64_t i = 0; i < Rk[q].r1 - Rk[q].r0; ++i) cs += Rk[q].y[i];
   printf("{\"kind\": %d, \"n_per_dim\": %lld, \"rows\": %lld, \"nnz\": %lld, \"ranks\": %d, \"reps\": %d, "
          "\"sec_per_spmv\": %.9g, \"gbps\": %.6g, \"bytes_per_spmv\": %.0f, \"checksum\": %.17g}\n",
-         kind, (long long)N, (long long)n, (long long)nnz, ranks, g_done, per, bytes / per / 1e9, bytes, cs);
+         kind, (long long)N3[0], (long long)n, (long long)nnz, ranks, g_done, per, bytes / per / 1e9, bytes, cs);
   return 0;
 }
 
+/* ---- MPIBackend over Cartesian parts (--mpi): the CPU baseline beside the
+ * multi-GPU lines.  One rank per part (one thread each, one core each, as
+ * `mpiexec -n P` with one core per rank), each holding what MPIBackend's
+ * part holds: the local CSC of its owned rows over its local columns (owned
+ * oids, then ghosts by hid; Int64 colptr/rowval, 1-based), its x with the
+ * ghost layer, and the Exchanger of x (Interfaces.jl:723-786: parts_rcv the
+ * sorted owners of its ghosts, lids_rcv its ghost lids grouped by owner in
+ * ascending lid, lids_snd the owner's lids in the receiver's order).  One
+ * mul! (Interfaces.jl:2246-2275) per step:
+ *   async_exchange!(b): pack lids_snd into the send buffers, post (barrier:
+ *   every message delivered once every rank has packed, MPIBackend.jl:
+ *   261-309's Isend/Irecv + Waitall);
+ *   the owned_owned block: fill!(c, 0), column loop over the owned columns
+ *   (SparseUtils.jl:157-187, `i>0` filter);
+ *   wait: copy each received segment from the sender's buffer and unpack it
+ *   into the ghost lids;
+ *   the owned_ghost block: column loop over the ghost columns;
+ *   then PTimer's barrier (max over ranks).                               */
+typedef struct {
+  int p;                       /* 0-based part */
+  const Part* q;
+  int64_t nl, nnz;
+  int64_t *colptr, *rowval;    /* 1-based, Julia's CSC */
+  double* nzval;
+  int32_t* invrows;            /* lid_to_ohid of the rows (all owned) */
+  double *x, *y;
+  int nin, nout;               /* neighbours: receive from / send to */
+  int *in_part, *out_part;     /* sorted */
+  int64_t *in_ptr, *out_ptr;
+  int32_t *in_lids, *in_oid;   /* my ghost lids by owner; the owner's oid of each */
+  int32_t* out_lids;           /* my owned lids, in each receiver's order */
+  double *snd, *rcv;
+  const double** in_src;       /* per incoming segment: the sender's send segment */
+} MRank;
+
+static MRank* g_mr;
+static const double* g_mpi_x;   /* --xin: the global x (else sin(0.001*gid)) */
+
+static int owner_coord(int64_t ng, int np, int64_t g) {
+  for (int c = 0; c < np; ++c) {
+    int64_t f, l;
+    oid_range(ng, np, c + 1, &f, &l);
+    if (g >= f && g < f + l) return c;
+  }
+  return -1;
+}
+
+static int64_t col_lid(const Part* q, int64_t lx, int64_t ly, int64_t lz, int k) {
+  const int64_t ex = lx + off_d[k][0], ey = ly + off_d[k][1], ez = lz + off_d[k][2];
+  if (ex >= 0 && ey >= 0 && ez >= 0 && ex < q->n[0] && ey < q->n[1] && ez < q->n[2])
+    return ex + q->n[0] * (ey + q->n[1] * ez);
+  return q->nown + q->shell[shell_idx(q, ex + 1, ey + 1, ez + 1)];
+}
+
+static void* mrank_build(void* arg) {
+  MRank* R = (MRank*)arg;
+  const Part* q = R->q;
+  R->nl = q->nown + q->nghost;
+  /* ghosts: global coords → owner part and its oid, hid order */
+  int32_t* own_part = xmalloc((size_t)(q->nghost + 1) * sizeof(int32_t));
+  int32_t* own_oid = xmalloc((size_t)(q->nghost + 1) * sizeof(int32_t));
+  int64_t* ghost_gid = xmalloc((size_t)(q->nghost + 1) * sizeof(int64_t));
+  for (int64_t ez = 0; ez < q->n[2] + 2; ++ez)
+    for (int64_t ey = 0; ey < q->n[1] + 2; ++ey)
+      for (int64_t ex = 0; ex < q->n[0] + 2; ++ex) {
+        const int32_t h = q->shell[shell_idx(q, ex, ey, ez)];
+        if (h < 0) continue;
+        const int64_t g[3] = {q->lo[0] + ex - 1, q->lo[1] + ey - 1, q->lo[2] + ez - 1};
+        int c[3];
+        int64_t f[3], l[3];
+        for (int d = 0; d < 3; ++d) {
+          c[d] = owner_coord(N3[d], P3[d], g[d]);
+          oid_range(N3[d], P3[d], c[d] + 1, &f[d], &l[d]);
+        }
+        own_part[h] = c[0] + P3[0] * (c[1] + P3[1] * c[2]);
+        own_oid[h] = (int32_t)((g[0] - f[0]) + l[0] * ((g[1] - f[1]) + l[1] * (g[2] - f[2])));
+        ghost_gid[h] = gid3(g[0], g[1], g[2]);
+      }
+  /* parts_rcv / lids_rcv: ghosts grouped by owner (sorted), ascending lid */
+  int* cnt = calloc((size_t)nparts, sizeof(int));
+  for (int64_t h = 0; h < q->nghost; ++h) cnt[own_part[h]]++;
+  R->nin = 0;
+  for (int t = 0; t < nparts; ++t) R->nin += cnt[t] > 0;
+  R->in_part = xmalloc((size_t)(R->nin + 1) * sizeof(int));
+  R->in_ptr = xmalloc((size_t)(R->nin + 1) * sizeof(int64_t));
+  int64_t* start = xmalloc((size_t)nparts * sizeof(int64_t));
+  R->in_ptr[0] = 0;
+  for (int t = 0, k = 0; t < nparts; ++t) {
+    start[t] = R->in_ptr[k];
+    if (!cnt[t]) continue;
+    R->in_part[k] = t;
+    R->in_ptr[k + 1] = R->in_ptr[k] + cnt[t];
+    ++k;
+  }
+  R->in_lids = xmalloc((size_t)(q->nghost + 1) * sizeof(int32_t));
+  R->in_oid = xmalloc((size_t)(q->nghost + 1) * sizeof(int32_t));
+  for (int64_t h = 0; h < q->nghost; ++h) {
+    const int64_t t = start[own_part[h]]++;
+    R->in_lids[t] = (int32_t)(q->nown + h);
+    R->in_oid[t] = own_oid[h];
+  }
+  free(cnt); free(start); free(own_part); free(own_oid);
+  R->rcv = xmalloc((size_t)(q->nghost + 1) * sizeof(double));
+  R->in_src = xmalloc((size_t)(R->nin + 1) * sizeof(double*));
+  /* the local CSC: count per column, then fill in row (= oid) order, so the
+   * rows of each column ascend (sparse's CSC) */
+  R->colptr = calloc((size_t)R->nl + 1, sizeof(int64_t));
+  int64_t nnz = 0;
+  for (int64_t lz = 0; lz < q->n[2]; ++lz)
+    for (int64_t ly = 0; ly < q->n[1]; ++ly)
+      for (int64_t lx = 0; lx < q->n[0]; ++lx) {
+        const int64_t row = lx + q->n[0] * (ly + q->n[1] * lz);
+        if (dirichlet(q->lo[0] + lx, q->lo[1] + ly, q->lo[2] + lz)) { R->colptr[row + 1]++; ++nnz; continue; }
+        for (int k = 0; k < K; ++k) R->colptr[col_lid(q, lx, ly, lz, k) + 1]++;
+        nnz += K;
+      }
+  for (int64_t j = 0; j < R->nl; ++j) R->colptr[j + 1] += R->colptr[j];
+  R->nnz = nnz;
+  R->rowval = xmalloc((size_t)nnz * sizeof(int64_t));
+  R->nzval = xmalloc((size_t)nnz * sizeof(double));
+  int64_t* cur = xmalloc((size_t)R->nl * sizeof(int64_t));
+  memcpy(cur, R->colptr, (size_t)R->nl * sizeof(int64_t));
+  for (int64_t lz = 0; lz < q->n[2]; ++lz)
+    for (int64_t ly = 0; ly < q->n[1]; ++ly)
+      for (int64_t lx = 0; lx < q->n[0]; ++lx) {
+        const int64_t gx = q->lo[0] + lx, gy = q->lo[1] + ly, gz = q->lo[2] + lz;
+        const int64_t row = lx + q->n[0] * (ly + q->n[1] * lz);
+        if (dirichlet(gx, gy, gz)) {
+          const int64_t pp = cur[row]++;
+          R->rowval[pp] = row + 1;
+          R->nzval[pp] = dirichlet_val(gx, gy, gz);
+          continue;
+        }
+        for (int k = 0; k < K; ++k) {
+          const int64_t pp = cur[col_lid(q, lx, ly, lz, k)]++;
+          R->rowval[pp] = row + 1;
+          R->nzval[pp] = interior_val[k];
+        }
+      }
+  free(cur);
+  for (int64_t j = 0; j <= R->nl; ++j) R->colptr[j] += 1;
+  R->invrows = xmalloc((size_t)(q->nown + 1) * sizeof(int32_t));
+  for (int64_t i = 0; i < q->nown; ++i) R->invrows[i] = (int32_t)(i + 1);
+  /* x: the seeded global vector's owned and ghost values */
+  R->x = xmalloc((size_t)(R->nl + 1) * sizeof(double));
+  R->y = xmalloc((size_t)(q->nown + 1) * sizeof(double));
+  for (int64_t lz = 0; lz < q->n[2]; ++lz)
+    for (int64_t ly = 0; ly < q->n[1]; ++ly)
+      for (int64_t lx = 0; lx < q->n[0]; ++lx) {
+        const int64_t g = gid3(q->lo[0] + lx, q->lo[1] + ly, q->lo[2] + lz);
+        R->x[lx + q->n[0] * (ly + q->n[1] * lz)] = g_mpi_x ? g_mpi_x[g] : sin(0.001 * (double)g);
+      }
+  for (int64_t h = 0; h < q->nghost; ++h) R->x[q->nown + h] = 0.0;  /* filled by the exchange */
+  free(ghost_gid);
+  return NULL;
+}
+
+/* lids_snd of every part: for each receiver (sorted), the oids it listed */
+static void mrank_link(void) {
+  for (int s = 0; s < nparts; ++s) {
+    MRank* S = &g_mr[s];
+    S->nout = 0;
+    int64_t tot = 0;
+    for (int r = 0; r < nparts; ++r)
+      for (int k = 0; k < g_mr[r].nin; ++k)
+        if (g_mr[r].in_part[k] == s) { S->nout++; tot += g_mr[r].in_ptr[k + 1] - g_mr[r].in_ptr[k]; }
+    S->out_part = xmalloc((size_t)(S->nout + 1) * sizeof(int));
+    S->out_ptr = xmalloc((size_t)(S->nout + 1) * sizeof(int64_t));
+    S->out_lids = xmalloc((size_t)(tot + 1) * sizeof(int32_t));
+    S->snd = xmalloc((size_t)(tot + 1) * sizeof(double));
+    S->out_ptr[0] = 0;
+    int m = 0;
+    for (int r = 0; r < nparts; ++r)
+      for (int k = 0; k < g_mr[r].nin; ++k) {
+        if (g_mr[r].in_part[k] != s) continue;
+        const int64_t a = g_mr[r].in_ptr[k], b = g_mr[r].in_ptr[k + 1];
+        S->out_part[m] = r;
+        for (int64_t t = a; t < b; ++t) S->out_lids[S->out_ptr[m] + t - a] = g_mr[r].in_oid[t];
+        S->out_ptr[m + 1] = S->out_ptr[m] + (b - a);
+        g_mr[r].in_src[k] = S->snd + S->out_ptr[m];
+        ++m;
+      }
+  }
+}
+
+static void mrank_cols(MRank* R, int64_t j0, int64_t j1) {
+  const double alpha = 1.0;
+  for (int64_t j = j0; j < j1; ++j) {
+    const double axj = R->x[j] * alpha;
+    for (int64_t p = R->colptr[j] - 1; p < R->colptr[j + 1] - 1; ++p) {
+      const int32_t i = R->invrows[R->rowval[p] - 1];
+      if (i > 0) R->y[i - 1] += R->nzval[p] * axj;
+    }
+  }
+}
+
+static void* mrank_run(void* arg) {
+  MRank* R = (MRank*)arg;
+  const Part* q = R->q;
+  double t0 = 0.0;
+  for (int it = 0;; ++it) {
+    pthread_barrier_wait(&g_bar);
+    if (it == 0) t0 = now();
+    if (g_stop) break;
+    for (int k = 0; k < R->nout; ++k)  /* pack + post */
+      for (int64_t t = R->out_ptr[k]; t < R->out_ptr[k + 1]; ++t) R->snd[t] = R->x[R->out_lids[t]];
+    pthread_barrier_wait(&g_bar);      /* delivered */
+    memset(R->y, 0, (size_t)(q->nown > 0 ? q->nown : 1) * sizeof(double));
+    mrank_cols(R, 0, q->nown);         /* owned_owned */
+    for (int k = 0; k < R->nin; ++k) { /* wait: receive + unpack */
+      const int64_t a = R->in_ptr[k], b = R->in_ptr[k + 1];
+      memcpy(R->rcv + a, R->in_src[k], (size_t)(b - a) * sizeof(double));
+      for (int64_t t = a; t < b; ++t) R->x[R->in_lids[t]] = R->rcv[t];
+    }
+    mrank_cols(R, q->nown, R->nl);     /* owned_ghost */
+    if (pthread_barrier_wait(&g_bar) == PTHREAD_BARRIER_SERIAL_THREAD) {
+      ++g_done;
+      if (g_reps_target > 0 ? g_done >= g_reps_target : (now() - t0) >= g_seconds) g_stop = 1;
+    }
+  }
+  return NULL;
+}
+
+static int run_mpi(int reps, double seconds, const char* yout) {
+  g_mr = calloc((size_t)nparts, sizeof(MRank));
+  pthread_t* th = xmalloc((size_t)nparts * sizeof(pthread_t));
+  double tb = now();
+  for (int p = 0; p < nparts; ++p) {
+    g_mr[p].p = p;
+    g_mr[p].q = &parts[p];
+    pthread_create(&th[p], NULL, mrank_build, &g_mr[p]); /* each rank assembles its own CSC */
+  }
+  for (int p = 0; p < nparts; ++p) pthread_join(th[p], NULL);
+  mrank_link();
+  tb = now() - tb;
+  pthread_barrier_init(&g_bar, NULL, (unsigned)nparts);
+  g_reps_target = reps;
+  g_seconds = seconds;
+  double t0 = now();
+  for (int p = 0; p < nparts; ++p) pthread_create(&th[p], NULL, mrank_run, &g_mr[p]);
+  for (int p = 0; p < nparts; ++p) pthread_join(th[p], NULL);
+  const double per = (now() - t0) / g_done;
+  double bytes = 0.0, cs = 0.0;
+  int64_t nnz = 0, ghosts = 0, halo = 0;
+  for (int p = 0; p < nparts; ++p) {
+    const MRank* R = &g_mr[p];
+    const int64_t no = R->q->nown, ng = R->q->nghost, ns = R->out_ptr[R->nout], nr = R->in_ptr[R->nin];
+    /* nnz(S+I) + (n_own+1)I + (n_own+n_ghost)S + n_own S + (n_snd+n_rcv)(I+2S) */
+    bytes += (double)R->nnz * 12.0 + (double)(no + 1) * 4.0 + (double)(no + ng) * 8.0 + (double)no * 8.0 +
+             (double)(ns + nr) * 20.0;
+    nnz += R->nnz;
+    ghosts += ng;
+    halo += nr;
+    for (int64_t i = 0; i < no; ++i) cs += R->y[i];
+  }
+  if (yout) {  /* y by gid (the owned values of every part) */
+    double* Y = xmalloc((size_t)N3[0] * N3[1] * N3[2] * sizeof(double));
+    for (int p = 0; p < nparts; ++p) {
+      const Part* q = g_mr[p].q;
+      for (int64_t lz = 0; lz < q->n[2]; ++lz)
+        for (int64_t ly = 0; ly < q->n[1]; ++ly)
+          for (int64_t lx = 0; lx < q->n[0]; ++lx)
+            Y[gid3(q->lo[0] + lx, q->lo[1] + ly, q->lo[2] + lz)] = g_mr[p].y[lx + q->n[0] * (ly + q->n[1] * lz)];
+    }
+    write_vec(yout, Y, N3[0] * N3[1] * N3[2]);
+    free(Y);
+  }
+  printf("{\"mode\": \"mpi\", \"kind\": %d, \"dims\": [%lld, %lld, %lld], \"parts\": [%d, %d, %d], \"ranks\": %d, "
+         "\"nnz\": %lld, \"ghosts\": %lld, \"halo_values\": %lld, \"reps\": %d, \"build_s\": %.3f, "
+         "\"sec_per_spmv\": %.9g, \"gbps\": %.6g, \"bytes_per_spmv\": %.0f, \"checksum\": %.17g}\n",
+         kind, (long long)N3[0], (long long)N3[1], (long long)N3[2], P3[0], P3[1], P3[2], nparts, (long long)nnz,
+         (long long)ghosts, (long long)halo, g_done, tb, per, bytes / per / 1e9, bytes, cs);
+  return 0;
+}
+
+/* ---- one part, the literal CSC column loop, in Float32 / ComplexF64 -------
+ * A in T (Float32: Float32.(A), each Float64 value rounded once; ComplexF64:
+ * the Float64 value + 0im), x and y in T; C[i] += nzv[p]*(B[j]*α) with α = 1,
+ * Julia's complex product (re = a.re*b.re - a.im*b.im, im = a.re*b.im +
+ * a.im*b.re), no FMA (-ffp-contract=off).                                   */
+typedef struct { double re, im; } cplx;
+
+static void onepart_f32(int64_t n, const int64_t* colptr, const int64_t* rowval, const double* nz64,
+                        const int32_t* invrows, const float* B, float* Cv) {
+  for (int64_t i = 0; i < n; ++i) Cv[i] = 0.0f;
+  for (int64_t j = 0; j < n; ++j) {
+    const float axj = B[j];
+    for (int64_t p = colptr[j] - 1; p < colptr[j + 1] - 1; ++p) {
+      const int32_t i = invrows[rowval[p] - 1];
+      if (i > 0) Cv[i - 1] += (float)nz64[p] * axj;
+    }
+  }
+}
+
+static void onepart_c128(int64_t n, const int64_t* colptr, const int64_t* rowval, const double* nz64,
+                         const int32_t* invrows, const cplx* B, cplx* Cv) {
+  for (int64_t i = 0; i < n; ++i) Cv[i].re = Cv[i].im = 0.0;
+  for (int64_t j = 0; j < n; ++j) {
+    const cplx axj = B[j];
+    for (int64_t p = colptr[j] - 1; p < colptr[j + 1] - 1; ++p) {
+      const int32_t i = invrows[rowval[p] - 1];
+      if (i > 0) {
+        const cplx a = {nz64[p], 0.0};
+        const double pr = a.re * axj.re - a.im * axj.im, pi = a.re * axj.im + a.im * axj.re;
+        Cv[i - 1].re = Cv[i - 1].re + pr;
+        Cv[i - 1].im = Cv[i - 1].im + pi;
+      }
+    }
+  }
+}
+
 int main(int argc, char** argv) {
-  N = 64;
+  N3[0] = N3[1] = N3[2] = 64;
+  int mpi = 0;
+  const char* dtype = "f64";
   kind = 27;
   double seconds = 10.0, reltol = 0.0, abstol = 0.0;
   int reps = 0, ranks = 1, literal = 0, have_parts = 0, cg = 0;
   const char *xin = NULL, *yout = NULL, *bin = NULL, *hist = NULL, *xout = NULL;
   for (int i = 1; i < argc; ++i) {
-    if (!strcmp(argv[i], "--n") && i + 1 < argc) N = atoll(argv[++i]);
+    if (!strcmp(argv[i], "--n") && i + 1 < argc) N3[0] = N3[1] = N3[2] = atoll(argv[++i]);
+    else if (!strcmp(argv[i], "--dims") && i + 3 < argc) { for (int d = 0; d < 3; ++d) N3[d] = atoll(argv[++i]); }
+    else if (!strcmp(argv[i], "--mpi")) mpi = 1;
+    else if (!strcmp(argv[i], "--dtype") && i + 1 < argc) dtype = argv[++i];
     else if (!strcmp(argv[i], "--kind") && i + 1 < argc) kind = atoi(argv[++i]);
     else if (!strcmp(argv[i], "--seconds") && i + 1 < argc) seconds = atof(argv[++i]);
     else if (!strcmp(argv[i], "--reps") && i + 1 < argc) reps = atoi(argv[++i]);
@@ -627,10 +955,13 @@ int main(int argc, char** argv) {
     else { fprintf(stderr, "unknown argument %s\n", argv[i]); return 2; }
   }
   if (kind != 7 && kind != 27) { fprintf(stderr, "kind must be 7 or 27\n"); return 2; }
-  if (N < 3) { fprintf(stderr, "n must be >= 3\n"); return 2; }
+  if (N3[0] < 3 || N3[1] < 3 || N3[2] < 3) { fprintf(stderr, "n must be >= 3\n"); return 2; }
+  const int dt = !strcmp(dtype, "f32") ? 1 : !strcmp(dtype, "c128") ? 2 : !strcmp(dtype, "f64") ? 0 : -1;
+  if (dt < 0) { fprintf(stderr, "dtype must be f64, f32 or c128\n"); return 2; }
+  if (dt != 0 && (have_parts || cg || ranks > 1 || mpi)) { fprintf(stderr, "--dtype f32|c128: one-part mode only\n"); return 2; }
   if (g_threads < 1) g_threads = 1;
   setup_operator();
-  const int64_t n = N * N * N;
+  const int64_t n = N3[0] * N3[1] * N3[2];
 
   if (ranks > 1) {
     double* B = xmalloc((size_t)n * sizeof(double));
@@ -642,10 +973,14 @@ int main(int argc, char** argv) {
     nparts = P3[0] * P3[1] * P3[2];
     if (nparts < 1) { fprintf(stderr, "bad --parts\n"); return 2; }
     for (int d = 0; d < 3; ++d)
-      if (P3[d] > N) { fprintf(stderr, "more parts than nodes\n"); return 2; }
+      if (P3[d] > N3[d]) { fprintf(stderr, "more parts than nodes\n"); return 2; }
     parts = calloc((size_t)nparts, sizeof(Part));
     int64_t nghost = 0;
     for (int p = 0; p < nparts; ++p) { build_part(&parts[p], p + 1); nghost += parts[p].nghost; }
+    if (mpi) {
+      if (xin) g_mpi_x = read_vec(xin, n);
+      return run_mpi(reps, seconds, yout);
+    }
     void (*spmv)(const double*, double*) = literal ? spmv_parts_literal : spmv_parts;
     double t0 = now();
     if (!cg) {
@@ -658,7 +993,7 @@ int main(int argc, char** argv) {
       for (int64_t i = 0; i < n; ++i) cs += y[i];
       printf("{\"mode\": \"spmv\", \"kind\": %d, \"n_per_dim\": %lld, \"parts\": [%d, %d, %d], \"ghosts\": %lld, "
              "\"literal\": %d, \"seconds\": %.3f, \"checksum\": %.17g}\n",
-             kind, (long long)N, P3[0], P3[1], P3[2], (long long)nghost, literal, now() - t0, cs);
+             kind, (long long)N3[0], P3[0], P3[1], P3[2], (long long)nghost, literal, now() - t0, cs);
       return 0;
     }
     if (!bin) { fprintf(stderr, "--cg needs --bin\n"); return 2; }
@@ -691,7 +1026,7 @@ int main(int argc, char** argv) {
     if (xout) write_vec(xout, x, n);
     printf("{\"mode\": \"cg\", \"kind\": %d, \"n_per_dim\": %lld, \"parts\": [%d, %d, %d], \"iterations\": %d, "
            "\"residual0_norm_b\": %.17g, \"residual\": %.17g, \"seconds\": %.3f}\n",
-           kind, (long long)N, P3[0], P3[1], P3[2], it, nb, residual, now() - t0);
+           kind, (long long)N3[0], P3[0], P3[1], P3[2], it, nb, residual, now() - t0);
     return 0;
   }
 
@@ -722,6 +1057,19 @@ int main(int argc, char** argv) {
   for (int64_t j = 0; j <= n; ++j) colptr[j] += 1;
   int32_t* invrows = xmalloc((size_t)n * sizeof(int32_t)); /* lid_to_ohid: owned rows 1..n */
   for (int64_t i = 0; i < n; ++i) invrows[i] = (int32_t)(i + 1);
+  if (dt != 0) {  /* Float32 / ComplexF64: one literal pass, x from --xin */
+    if (!xin || !yout) { fprintf(stderr, "--dtype f32|c128 needs --xin and --yout\n"); return 2; }
+    const size_t es = dt == 1 ? sizeof(float) : sizeof(cplx);
+    void* Bx = read_bytes(xin, (size_t)n * es);
+    void* Cx = xmalloc((size_t)n * es);
+    double t0 = now();
+    if (dt == 1) onepart_f32(n, colptr, rowval, nzval, invrows, (const float*)Bx, (float*)Cx);
+    else onepart_c128(n, colptr, rowval, nzval, invrows, (const cplx*)Bx, (cplx*)Cx);
+    write_bytes(yout, Cx, (size_t)n * es);
+    printf("{\"mode\": \"one-part\", \"dtype\": \"%s\", \"kind\": %d, \"n_per_dim\": %lld, \"nnz\": %lld, "
+           "\"seconds\": %.3f}\n", dtype, kind, (long long)N3[0], (long long)nnz, now() - t0);
+    return 0;
+  }
   double* B = xin ? read_vec(xin, n) : xmalloc((size_t)n * sizeof(double));
   if (!xin) seeded_vec(B, n);
   double* Cv = xmalloc((size_t)n * sizeof(double));
@@ -750,6 +1098,6 @@ int main(int argc, char** argv) {
   for (int64_t i = 0; i < n; ++i) cs += Cv[i];
   printf("{\"kind\": %d, \"n_per_dim\": %lld, \"rows\": %lld, \"nnz\": %lld, \"ranks\": 1, \"reps\": %d, "
          "\"sec_per_spmv\": %.9g, \"gbps\": %.6g, \"bytes_per_spmv\": %.0f, \"checksum\": %.17g}\n",
-         kind, (long long)N, (long long)n, (long long)nnz, done, per, bytes / per / 1e9, bytes, cs);
+         kind, (long long)N3[0], (long long)n, (long long)nnz, done, per, bytes / per / 1e9, bytes, cs);
   return 0;
 }

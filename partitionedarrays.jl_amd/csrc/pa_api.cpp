@@ -26,7 +26,8 @@ void set_error(const std::string& msg) { g_err = msg; }
 // kernels (pa_spmv.hip, pa_kernels.hip)
 void launch_spmv_part(int which, int64_t nwork, const int32_t* list, const pa_mat* A, const void* x,
                       void* y, const int32_t* ymap, bool has_alpha, int bmode, const void* alpha,
-                      const void* beta, void* dotp, hipStream_t st);
+                      const void* beta, void* dotp, hipStream_t st,
+                      const SpmvPart* cgp = nullptr);
 void launch_delta16(pa_mat* A, int64_t noids, const int32_t* kind, int32_t* ok, hipStream_t st);
 void launch_pattern_detect(pa_mat* A, int64_t noids, int32_t* kind, int32_t* plen, int32_t* pat,
                            uint64_t* mask, int32_t* pghost, int32_t* nirreg, int NP, int rule, hipStream_t st);
@@ -41,6 +42,8 @@ void launch_fold_cg_step(int dtype, int nb, const void* in, void* scratch, void*
 void launch_cg_xr(int dtype, int64_t n, int64_t noids, const int32_t* own, void* x, void* r, const void* u,
                   const void* c, const void* alpha, const CGState* cst, double* part, int nb, hipStream_t st);
 void launch_cg_xu(int dtype, int64_t n, void* x, void* u, const void* r, const CGState* cst, hipStream_t st);
+void launch_cg_ghost(int dtype, int64_t lo, int64_t hi, const void* r, const void* uo, void* un, void* x,
+                     const CGState* cst, hipStream_t st);
 void launch_cg_alpha(int dtype, int P, const void* gathered, CGState* cst, hipStream_t st);
 void launch_cg_step(int dtype, int P, const double* gathered, CGState* cst, double* history, hipStream_t st);
 void launch_gather_ptrs(int P, const void* const* srcs, int accsz, void* out, hipStream_t st);
@@ -59,6 +62,8 @@ int g_spmv_merge = 1;     // pa_tune("spmv_merge"): one launch for every slice k
 int64_t g_spmv_merge_max = 65536;
 int g_halo_direct = 1;     // pa_tune("halo_direct"): grouped mul! pulls ghosts straight from the owners' x
 int g_halo_transport = 0;  // pa_tune("halo_transport"): 0 parts of this process by device reads, 1 RCCL for all
+int g_cg_fuse = 1;         // pa_tune("cg_fuse"): the device CG's u update inside the SpMV (XV kernels)
+int g_spmv_quadsort = 0;   // pa_tune("spmv_quadsort"): quad-sorted layout when most slices are not pattern slices
 int g_comm_cus = 0;   // pa_tune("comm_cus"): CUs reserved for the comm stream (0: priority stream instead)
 // COO → CSC → SELL on the device (pa_coo.hip)
 int coo_compress(int dtype, int index_bytes, int64_t m, int64_t ncols, int64_t n, const void* dI, const void* dJ,
@@ -80,9 +85,9 @@ void launch_spmv_long(const pa_mat* A, const void* x, void* y, const int32_t* ym
 int gid_table(int64_t n, const int64_t* d_lid_to_gid, uint64_t** sgid, int64_t** slid, hipStream_t st);
 int gids_to_lids(int64_t n, int64_t* ids, const uint64_t* sgid, const int64_t* slid, int64_t nl, hipStream_t st);
 int coo_assemble_pack(int dtype, int64_t n, const int64_t* I, const int64_t* J, void* V, const uint64_t* sgid,
-                      const int64_t* slid, int64_t nl, int nseg, const int32_t* d_lids_rcv,
-                      const std::vector<int64_t>& ptrs_rcv, int64_t** sI, int64_t** sJ, void** sV,
-                      std::vector<int64_t>* cnt, hipStream_t st);
+                      const int64_t* slid, int64_t nl, const std::vector<int32_t>& lid_to_ohid, int nseg,
+                      const int32_t* d_lids_rcv, const std::vector<int64_t>& ptrs_rcv, int64_t** sI, int64_t** sJ,
+                      void** sV, std::vector<int64_t>* cnt, hipStream_t st);
 int gids_first_touch(int64_t n, const int64_t* gids, const uint64_t* sgid, const int64_t* slid, int64_t nl,
                      int64_t** out, int64_t* m_out, hipStream_t st);
 void launch_pack(int dtype, int64_t n, const int32_t* lids, const void* v, void* buf,
@@ -115,6 +120,13 @@ void launch_stencil_fill(const StencilGeom& g, const int32_t* shell, const doubl
                          int64_t nrows, int noids, pa_mat* A, int32_t* err, hipStream_t st);
 void launch_probe(int copy, int unroll, int64_t n16, const void* a, void* b, int blocks, hipStream_t st);
 void launch_pattern_triples(const pa_mat* A, uint8_t* tri, hipStream_t st);
+void launch_quad_class(const pa_mat* A, int64_t noids, int32_t* qlen, uint8_t* qflag, uint64_t* qhash, hipStream_t st);
+void launch_quad_permute(const pa_mat* A, int64_t nslices_new, const int32_t* perm, const int64_t* nsoff,
+                         const int32_t* nslen, const int64_t* osoff, const int32_t* oslen, const int32_t* ocol,
+                         const void* oval, int32_t* ncol, void* nval, hipStream_t st);
+void launch_nzslot_remap(int64_t nu, int64_t* nzs, int64_t oslots, int64_t ons, const int64_t* osoff, int H, int R,
+                         const int32_t* inv, const int64_t* nsoff, hipStream_t st);
+void launch_qrun_detect(const pa_mat* A, const int32_t* kind, int32_t* qcol, int32_t* ok, hipStream_t st);
 extern int g_spmv_flags;
 extern int g_spmv_unroll;
 extern int g_spmv_lds;
@@ -295,8 +307,116 @@ int finish_sell_layout(pa_mat* A, const std::vector<int32_t>& slen, const std::v
   return 0;
 }
 
+// Quad sort of the int32 layout: lanes (quads of R
+// consecutive owned rows) ordered by class — quad-run lanes without ghost
+// columns, quad-run lanes reading ghosts (each grouped by their column
+// offsets, so equal patterns share slices), then the other lanes without /
+// with ghost columns, in oid order inside a class — and a partial last quad
+// (nrows % R rows) at the very end, so that the valid rows of every slice
+// stay a prefix of its positions.  Values and columns move with their
+// lanes; every row keeps its entries in order, and the CSC nz → slot map
+// follows.  Sets qmap; the caller redoes the encodings on the new layout.
+int quad_sort(pa_mat* A, int64_t noids) {
+  const int R = A->R, H = A->H;
+  const int64_t nq = (A->nrows + R - 1) / R, ons = A->nslices, oslots = A->slots;
+  const size_t S = dtype_size(A->dtype);
+  hipStream_t st = A->ctx->s_main;
+  if (nq == 0) return 0;
+  int32_t* d_qlen = nullptr;
+  uint8_t* d_qflag = nullptr;
+  uint64_t* d_qhash = nullptr;
+  HIPC(hipMalloc((void**)&d_qlen, nq * 4));
+  HIPC(hipMalloc((void**)&d_qflag, nq));
+  HIPC(hipMalloc((void**)&d_qhash, nq * 8));
+  launch_quad_class(A, noids, d_qlen, d_qflag, d_qhash, st);
+  HIPC(hipGetLastError());
+  std::vector<int32_t> qlen(nq);
+  std::vector<uint8_t> qflag(nq);
+  std::vector<uint64_t> qhash(nq);
+  HIPC(hipMemcpyAsync(qlen.data(), d_qlen, nq * 4, hipMemcpyDeviceToHost, st));
+  HIPC(hipMemcpyAsync(qflag.data(), d_qflag, nq, hipMemcpyDeviceToHost, st));
+  HIPC(hipMemcpyAsync(qhash.data(), d_qhash, nq * 8, hipMemcpyDeviceToHost, st));
+  HIPC(hipStreamSynchronize(st));
+  dev_free(d_qlen);
+  dev_free(d_qflag);
+  dev_free(d_qhash);
+  const bool partial = A->nrows % R != 0;
+  auto cls = [&](int64_t q) -> int {
+    if (partial && q == nq - 1) return 4;
+    const bool run = qflag[q] & 1, gh = (qflag[q] & 2) != 0;
+    return run ? (gh ? 1 : 0) : (gh ? 3 : 2);
+  };
+  std::vector<int32_t> order(nq);
+  for (int64_t q = 0; q < nq; ++q) order[q] = (int32_t)q;
+  std::stable_sort(order.begin(), order.end(), [&](int32_t a, int32_t b) {
+    const int ca = cls(a), cb = cls(b);
+    if (ca != cb) return ca < cb;
+    if (ca <= 1 && qhash[a] != qhash[b]) return qhash[a] < qhash[b];
+    return a < b;
+  });
+  // the new slices
+  const int64_t ns = (nq + 63) / 64;
+  std::vector<int32_t> perm(ns * 64, -1), inv(ons * 64, -1), slen(ns, 0);
+  std::vector<char> sghost(ns, 0);
+  A->h_qmap.assign(ns * 64, (int32_t)A->nrows);
+  for (int64_t p = 0; p < nq; ++p) {
+    const int32_t q = order[p];
+    perm[p] = q;
+    inv[q] = (int32_t)p;
+    A->h_qmap[p] = q * R;
+    slen[p / 64] = std::max(slen[p / 64], qlen[q]);
+    if (qflag[q] & 2) sghost[p / 64] = 1;
+  }
+  // keep the old layout until the copy is done
+  int64_t* o_soff = A->d_slice_off;
+  int32_t* o_slen = A->d_slice_len;
+  int32_t* o_col = A->d_col;
+  void* o_val = A->d_val;
+  const int64_t o_tail = A->n_gnz + A->n_lnz;
+  A->d_slice_off = nullptr;
+  A->d_slice_len = nullptr;
+  A->d_col = nullptr;
+  A->d_val = nullptr;
+  dev_free(A->d_int_list);
+  dev_free(A->d_bnd_list);
+  A->d_int_list = A->d_bnd_list = nullptr;
+  std::vector<int64_t> nsoff;
+  if (finish_sell_layout(A, slen, sghost, &nsoff)) return -1;
+  A->long_off = A->slots + A->n_gnz;
+  int32_t *d_perm = nullptr, *d_inv = nullptr;
+  if (dev_upload(&d_perm, perm) || dev_upload(&d_inv, inv) || dev_upload(&A->d_qmap, A->h_qmap)) return -1;
+  if (A->slots > 0) HIPC(hipMalloc((void**)&A->d_col, A->slots * 4));
+  if (nvals(A) > 0) HIPC(hipMalloc(&A->d_val, nvals(A) * S));
+  launch_quad_permute(A, ns, d_perm, A->d_slice_off, A->d_slice_len, o_soff, o_slen, o_col, o_val, A->d_col,
+                      A->d_val, st);
+  HIPC(hipGetLastError());
+  if (o_tail > 0)  // ghost-row (and long-row) values after the slots
+    HIPC(hipMemcpyAsync((char*)A->d_val + A->slots * S, (const char*)o_val + oslots * S, o_tail * S,
+                        hipMemcpyDeviceToDevice, st));
+  if (A->d_nz_slot) {
+    launch_nzslot_remap(A->csc_nnz, A->d_nz_slot, oslots, ons, o_soff, H, R, d_inv, A->d_slice_off, st);
+    HIPC(hipGetLastError());
+  } else if (!A->h_nz_slot.empty()) {
+    std::vector<int64_t> osoff(ons);
+    HIPC(hipMemcpyAsync(osoff.data(), o_soff, ons * 8, hipMemcpyDeviceToHost, st));
+    HIPC(hipStreamSynchronize(st));
+    for (int64_t& t : A->h_nz_slot) {
+      if (t < 0 || t >= oslots) continue;
+      const int64_t so = (int64_t)(std::upper_bound(osoff.begin(), osoff.end(), t) - osoff.begin()) - 1;
+      const int64_t rem = t - osoff[so], k = rem / H, w = rem % H;
+      const int64_t np = inv[so * 64 + w / R];
+      t = nsoff[np / 64] + (k * 64 + np % 64) * R + w % R;
+    }
+  }
+  HIPC(hipStreamSynchronize(st));
+  for (void* q : {(void*)o_soff, (void*)o_slen, (void*)o_col, o_val, (void*)d_perm, (void*)d_inv}) dev_free(q);
+  return 0;
+}
+
 // Pattern slices + side SELL from the int32 layout (device detection, host
-// bookkeeping).  noids: owned columns (x lids >= noids are ghosts).
+// bookkeeping).  noids: owned columns (x lids >= noids are ghosts).  When
+// fewer than half the slices are pattern slices (irregular partitions) the
+// layout is quad-sorted first and the detection redone on it.
 int finalize_pattern(pa_mat* A, int kmax, int64_t noids) {
   A->kmax = std::max(kmax, 1);
   const int64_t ns = A->nslices;
@@ -332,6 +452,42 @@ int finalize_pattern(pa_mat* A, int kmax, int64_t noids) {
   HIPC(hipStreamSynchronize(st));
   dev_free(d_pghost);
   dev_free(d_nirreg);
+  if (g_spmv_quadsort && !A->d_qmap && A->n_long == 0 && A->R > 1) {
+    int64_t npat = 0;
+    for (int64_t s = 0; s < ns; ++s) npat += kind[s] != 0;
+    if (2 * npat < ns || g_spmv_quadsort == 2) {  // mostly irregular slices: quad-sort, then detect again
+      for (void** q : {(void**)&A->d_kind, (void**)&A->d_plen, (void**)&A->d_pat, (void**)&A->d_mask,
+                       (void**)&A->d_mpat, (void**)&A->d_psel}) {
+        dev_free(*q);
+        *q = nullptr;
+      }
+      A->h_plen.clear();
+      if (quad_sort(A, noids)) return -1;
+      return finalize_pattern(A, kmax, noids);
+    }
+  }
+  if (A->d_qmap) {  // quad-run slices (kind 4) among the remaining int32-column slices
+    int32_t* d_ok = nullptr;
+    HIPC(hipMalloc((void**)&A->d_qcol, std::max<int64_t>(A->slots / A->R, 1) * 4));
+    HIPC(hipMalloc((void**)&d_ok, ns * 4));
+    HIPC(hipMemcpyAsync(A->d_kind, kind.data(), ns * 4, hipMemcpyHostToDevice, st));
+    launch_qrun_detect(A, A->d_kind, A->d_qcol, d_ok, st);
+    HIPC(hipGetLastError());
+    std::vector<int32_t> ok(ns);
+    HIPC(hipMemcpyAsync(ok.data(), d_ok, ns * 4, hipMemcpyDeviceToHost, st));
+    HIPC(hipStreamSynchronize(st));
+    dev_free(d_ok);
+    int64_t nqr = 0;
+    for (int64_t s = 0; s < ns; ++s)
+      if (ok[s]) { kind[s] = 4; ++nqr; }
+    if (nqr == 0) {
+      dev_free(A->d_qcol);
+      A->d_qcol = nullptr;
+    } else {  // the delta16 pass below only takes kind 0
+      HIPC(hipMemcpyAsync(A->d_kind, kind.data(), ns * 4, hipMemcpyHostToDevice, st));
+      HIPC(hipStreamSynchronize(st));
+    }
+  }
   if (g_spmv_delta16) {  // int32-column slices whose columns fit 16-bit codes (kind 3)
     int32_t* d_ok = nullptr;
     HIPC(hipMalloc((void**)&A->d_col16, std::max<int64_t>(A->slots, 1) * 2));
@@ -353,11 +509,12 @@ int finalize_pattern(pa_mat* A, int kmax, int64_t noids) {
       A->d_gbase = nullptr;
     }
   }
-  std::vector<int32_t> pint, pbnd, xint, xbnd, mint, mbnd, dint, dbnd, side;
+  std::vector<int32_t> pint, pbnd, xint, xbnd, mint, mbnd, dint, dbnd, qint, qbnd, side;
   for (int64_t s = 0; s < ns; ++s) {
     if (kind[s] == 1) (pghost[s] ? pbnd : pint).push_back((int32_t)s);
     else if (kind[s] == 2) (pghost[s] ? mbnd : mint).push_back((int32_t)s);
     else if (kind[s] == 3) (pghost[s] ? dbnd : dint).push_back((int32_t)s);
+    else if (kind[s] == 4) (pghost[s] ? qbnd : qint).push_back((int32_t)s);
     else (pghost[s] ? xbnd : xint).push_back((int32_t)s);
     if (kind[s] == 1 || kind[s] == 2) {
       ++A->npattern_slices;
@@ -374,8 +531,9 @@ int finalize_pattern(pa_mat* A, int kmax, int64_t noids) {
     launch_pattern_triples(A, A->d_ptri, st);
     HIPC(hipGetLastError());
   }
-  A->maxlen_pat = A->maxlen_pm_int = A->maxlen_d16 = 0;
+  A->maxlen_pat = A->maxlen_pm_int = A->maxlen_d16 = A->maxlen_qrun = 0;
   for (int64_t s = 0; s < ns; ++s) {
+    if (kind[s] == 4) A->maxlen_qrun = std::max(A->maxlen_qrun, (int)A->h_slen[s]);
     if (kind[s] == 1) A->maxlen_pat = std::max(A->maxlen_pat, (int)A->h_plen[s]);
     else if (kind[s] == 0) A->maxlen_pm_int = std::max(A->maxlen_pm_int, (int)A->h_slen[s]);
     else if (kind[s] == 3) A->maxlen_d16 = std::max(A->maxlen_d16, (int)A->h_slen[s]);
@@ -388,6 +546,9 @@ int finalize_pattern(pa_mat* A, int kmax, int64_t noids) {
   A->nm_bnd = (int64_t)mbnd.size();
   A->nd_int = (int64_t)dint.size();
   A->nd_bnd = (int64_t)dbnd.size();
+  A->nq_int = (int64_t)qint.size();
+  A->nq_bnd = (int64_t)qbnd.size();
+  if (dev_upload(&A->d_qint_list, qint) || dev_upload(&A->d_qbnd_list, qbnd)) return -1;
   if (dev_upload(&A->d_pint_list, pint) || dev_upload(&A->d_pbnd_list, pbnd) ||
       dev_upload(&A->d_xint_list, xint) || dev_upload(&A->d_xbnd_list, xbnd) ||
       dev_upload(&A->d_mint_list, mint) || dev_upload(&A->d_mbnd_list, mbnd) ||
@@ -402,13 +563,26 @@ int finalize_pattern(pa_mat* A, int kmax, int64_t noids) {
   // side SELL
   A->s_nrows = (int64_t)side.size();
   if (A->s_nrows > 0) {
-    if (dev_upload(&A->d_s_rowmap, side)) return -1;
+    // the SpMV reads oids through d_s_rowmap; the copies below (and
+    // refresh_side) locate the rows by their structure row
+    int32_t* srow = nullptr;
+    if (A->d_qmap) {
+      if (dev_upload(&A->d_s_srow, side)) return -1;
+      std::vector<int32_t> oids(side.size());
+      for (size_t i = 0; i < side.size(); ++i)
+        oids[i] = A->h_qmap[side[i] / A->R] + side[i] % A->R;  // structure row s*H + lane*R + r
+      if (dev_upload(&A->d_s_rowmap, oids)) return -1;
+      srow = A->d_s_srow;
+    } else {
+      if (dev_upload(&A->d_s_rowmap, side)) return -1;
+      srow = A->d_s_rowmap;
+    }
     int32_t* d_dummy = nullptr;
     A->s_nslices = (A->s_nrows + A->H - 1) / A->H;
     HIPC(hipMalloc((void**)&A->d_s_rowlen, A->s_nrows * 4));
     HIPC(hipMalloc((void**)&d_dummy, A->s_nslices * 4));
     HIPC(hipMemsetAsync(d_dummy, 0, A->s_nslices * 4, st));
-    launch_side_len(A, A->s_nrows, A->d_s_rowmap, A->d_s_rowlen, noids, d_dummy, st);
+    launch_side_len(A, A->s_nrows, srow, A->d_s_rowlen, noids, d_dummy, st);
     HIPC(hipGetLastError());
     std::vector<int32_t> rl(A->s_nrows);
     HIPC(hipMemcpyAsync(rl.data(), A->d_s_rowlen, A->s_nrows * 4, hipMemcpyDeviceToHost, st));
@@ -426,7 +600,7 @@ int finalize_pattern(pa_mat* A, int kmax, int64_t noids) {
     const size_t S = dtype_size(A->dtype);
     HIPC(hipMalloc((void**)&A->d_s_col, std::max<int64_t>(acc, 1) * 4));
     HIPC(hipMalloc(&A->d_s_val, std::max<int64_t>(acc, 1) * S));
-    launch_side_fill(A, A->d_s_rowmap, A->d_s_rowlen, st);
+    launch_side_fill(A, srow, A->d_s_rowlen, st);
     HIPC(hipGetLastError());
     HIPC(hipStreamSynchronize(st));
   }
@@ -443,8 +617,9 @@ struct LocalSet {
 };
 
 // The parts whose halo segments move by device copies / pull reads in this
-// call.  With pa_tune("halo_transport", 1) and an RCCL communicator on every
-// part (pa_comm_init_all: one rank per device of this process), none: every
+// call.  When every part's communicator came from pa_comm_init_all (one rank
+// per device of this process: HIPBackend(rccl=True)), or with
+// pa_tune("halo_transport", 1) and a communicator on every part, none: every
 // segment goes through the grouped ncclSend/ncclRecv, as across processes.
 template <typename H>
 LocalSet local_set(int n, H* const* hs) {
@@ -452,11 +627,12 @@ LocalSet local_set(int n, H* const* hs) {
   int maxp = 0;
   bool all_comm = true;
   for (int i = 0; i < n; ++i) {
-    maxp = std::max(maxp, hs[i]->ctx->nparts);
-    all_comm = all_comm && hs[i]->ctx->comm != nullptr;
+    const pa_ctx* c = hs[i]->ctx;
+    maxp = std::max(maxp, c->nparts);
+    all_comm = all_comm && c->comm != nullptr && (c->halo_rccl || g_halo_transport == 1);
   }
   L.pos_of_part.assign(maxp + 1, -1);
-  if (g_halo_transport == 1 && all_comm) return L;
+  if (all_comm) return L;
   for (int i = 0; i < n; ++i) L.pos_of_part[hs[i]->ctx->part] = i;
   return L;
 }
@@ -464,6 +640,29 @@ LocalSet local_set(int n, H* const* hs) {
 // During graph capture every part's work goes to one stream (a linear chain
 // of kernels; multi-stream captures with cross-stream events are not used).
 hipStream_t g_capture_stream = nullptr;
+std::vector<void*>* g_capture_tables = nullptr;  // device tables the graph being captured owns
+
+// During a graph capture: a graph-owned device copy of a table the captured
+// kernels read (allocated now, uploaded after the capture ends, freed by
+// pa_graph_destroy).  The eager path's caches (the x-pointer arrays of the
+// direct pull, the pull/direct tables) may be evicted or rebuilt while the
+// graph still replays.  Outside a capture: d itself.  Null on failure.
+bool g_graph_owned_failed = false;  // set when a graph-owned copy could not be allocated
+template <typename T>
+const T* graph_owned(const T* d, const std::vector<T>& h) {
+  if (!g_capture_tables || h.empty()) return d;
+  void* p = nullptr;
+  if (hipMalloc(&p, h.size() * sizeof(T)) != hipSuccess) {
+    (void)hipGetLastError();
+    g_graph_owned_failed = true;
+    return nullptr;
+  }
+  g_capture_tables->push_back(p);
+  const char* b = reinterpret_cast<const char*>(h.data());
+  g_capture_uploads.push_back({p, std::vector<char>(b, b + h.size() * sizeof(T))});
+  return (const T*)p;
+}
+uint64_t g_xchg_next_id = 1;
 inline hipStream_t SM(const pa_ctx* c) { return g_capture_stream ? g_capture_stream : c->s_main; }
 inline hipStream_t SC(const pa_ctx* c) { return g_capture_stream ? g_capture_stream : c->s_comm; }
 #define EV(expr) do { if (!g_capture_stream) HIPC(expr); } while (0)
@@ -482,7 +681,7 @@ int build_pull(int i, int n, pa_xchg* const xg[], const LocalSet& L, int dtype, 
   key.push_back((const void*)(intptr_t)dtype_size(dtype));
   for (int32_t q : prcv) {
     const int j = L.find(q);
-    key.push_back(j >= 0 ? (const void*)xg[j] : nullptr);
+    key.push_back(j >= 0 ? (const void*)(uintptr_t)xg[j]->id : nullptr);
     key.push_back(j >= 0 ? (dir == 0 ? xg[j]->d_buf_snd : xg[j]->d_buf_rcv) : own);
   }
   if (P.built && P.key == key) return 0;
@@ -532,6 +731,9 @@ int build_pull(int i, int n, pa_xchg* const xg[], const LocalSet& L, int dtype, 
     for (int64_t t = 0; t < cnt; ++t) { bid[orcv[k] + t] = b; elem[orcv[k] + t] = qo[m] + t; }
   }
   if (dev_upload(&P.d_bid, bid) || dev_upload(&P.d_elem, elem) || dev_upload(&P.d_bases, bases)) return -1;
+  P.h_bid = std::move(bid);
+  P.h_elem = std::move(elem);
+  P.h_bases = std::move(bases);
   P.ok = true;
   return 0;
 }
@@ -543,7 +745,8 @@ int build_pull(int i, int n, pa_xchg* const xg[], const LocalSet& L, int dtype, 
 int build_direct(int i, int n, pa_xchg* const xg[], const LocalSet& L) {
   pa_xchg* X = xg[i];
   pa_pull& P = X->direct;
-  std::vector<const void*> key(xg, xg + n);
+  std::vector<const void*> key(n);
+  for (int j = 0; j < n; ++j) key[j] = (const void*)(uintptr_t)xg[j]->id;
   if (P.built && P.key == key) return 0;
   dev_free(P.d_bid);
   dev_free(P.d_elem);
@@ -573,6 +776,8 @@ int build_direct(int i, int n, pa_xchg* const xg[], const LocalSet& L) {
   }
   HIPC(hipSetDevice(X->ctx->device));
   if (dev_upload(&P.d_bid, bid) || dev_upload(&P.d_elem, elem)) return -1;
+  P.h_bid = std::move(bid);
+  P.h_elem = std::move(elem);
   P.ok = true;
   return 0;
 }
@@ -709,12 +914,16 @@ int transport(int n, pa_xchg* const xg[], int dtype, int dir, int op, pa_vec* co
     HIPC(hipSetDevice(c->device));
     if (pull) {
       const pa_pull& P = X->pull[dir];
+      const int32_t* bid = graph_owned<int32_t>(P.d_bid, P.h_bid);
+      const int64_t* elem = graph_owned<int64_t>(P.d_elem, P.h_elem);
+      void* const* bases = graph_owned<void*>(P.d_bases, P.h_bases);
+      CHECK_ARG(!g_graph_owned_failed, "graph capture: table allocation failed");
       if (dir == 0)
-        launch_pull(dtype, X->n_rcv_data, X->d_lids_rcv, X->plan_fwd, op, P.d_bid, P.d_elem,
-                    (const void* const*)P.d_bases, v[i]->d, SC(c));
+        launch_pull(dtype, X->n_rcv_data, X->d_lids_rcv, X->plan_fwd, op, bid, elem,
+                    (const void* const*)bases, v[i]->d, SC(c));
       else
-        launch_pull(dtype, X->n_snd_data, X->d_lids_snd, X->plan_rev, op, P.d_bid, P.d_elem,
-                    (const void* const*)P.d_bases, v[i]->d, SC(c));
+        launch_pull(dtype, X->n_snd_data, X->d_lids_snd, X->plan_rev, op, bid, elem,
+                    (const void* const*)bases, v[i]->d, SC(c));
     } else {
       // staging copies: receiver r, segment k from sender q (local), which
       // holds the matching segment at the position of r in its send list
@@ -754,7 +963,6 @@ int check_lids(const pa_xchg* X, const pa_vec* v) {
 // them in the previous exchange (local receivers record ev_recvd after their
 // copies; for RCCL sends the part's own ev_recvd covers them).
 bool g_capturing = false;  // inside pa_spmv_graph_create: one replay never overlaps the next
-std::vector<void*>* g_capture_tables = nullptr;  // merged-launch tables the graph being captured owns
 
 int pre_pack_wait(int n, pa_xchg* const xg[]) {
   if (g_capturing) return 0;
@@ -827,6 +1035,15 @@ int pa_tune(const char* key, int value, int* previous) {
     g_spmv_merge_max = value;
     if (previous) *previous = prev;
     return 0;
+  } else if (!std::strcmp(key, "spmv_quadsort")) {
+    CHECK_ARG(value >= 0 && value <= 2,
+              "spmv_quadsort: 1 = matrices whose slices are mostly not pattern slices get the quad-sorted layout "
+              "(default; matrices built afterwards), 2 = every matrix (tests), 0 = off");
+    slot = &g_spmv_quadsort;
+  } else if (!std::strcmp(key, "cg_fuse")) {
+    CHECK_ARG(value == 0 || value == 1,
+              "cg_fuse: 1 = the device CG computes u = r .+ beta.*u inside the SpMV (default), 0 = a separate sweep");
+    slot = &g_cg_fuse;
   } else if (!std::strcmp(key, "halo_direct")) {
     CHECK_ARG(value == 0 || value == 1,
               "halo_direct: 1 = mul! over parts sharing a stream pair reads the ghosts straight from the owners' x "
@@ -1075,6 +1292,7 @@ int pa_comm_init_all(int n, pa_ctx* const ctx[]) {
     ctx[i]->comm = comms[r];
     ctx[i]->comm_owner = owners[r];
     ctx[i]->rank_of_part = rank_of;
+    ctx[i]->halo_rccl = true;  // these parts exchange their halos over RCCL (per context, not a global knob)
   }
   return 0;
 }
@@ -1270,6 +1488,7 @@ int pa_xchg_create(pa_ctx* c, int32_t n_rcv, const int32_t* parts_rcv, const int
   HIPC(hipSetDevice(c->device));
   pa_xchg* X = new pa_xchg();
   X->ctx = c;
+  X->id = g_xchg_next_id++;
   auto take = [&](int32_t n, const int32_t* parts, const int32_t* ptrs, const int32_t* lids,
                   std::vector<int32_t>& P, std::vector<int64_t>& O, std::vector<int32_t>& Lh) -> int {
     P.assign(parts, parts + n);
@@ -1956,11 +2175,12 @@ int pa_coo_assemble_all(int n, pa_coo* const coo[], const pa_index* const rows[]
     const pa_index* R = rows[i];
     HIPC(hipSetDevice(C->ctx->device));
     const int rc = coo_assemble_pack(dt, C->n, C->d_I, C->d_J, C->d_V, R->d_sgid, R->d_slid, R->nlids,
-                                     (int)X->parts_rcv.size(), X->d_lids_rcv, X->ptrs_rcv, &sd[i].sI, &sd[i].sJ,
-                                     &sd[i].sV, &sd[i].cnt, C->ctx->s_main);
+                                     R->h_lid_to_ohid, (int)X->parts_rcv.size(), X->d_lids_rcv, X->ptrs_rcv,
+                                     &sd[i].sI, &sd[i].sJ, &sd[i].sV, &sd[i].cnt, C->ctx->s_main);
     if (rc) {
       free_all();
       if (rc < 0) PA_FAIL("assemble!(I,J,V,rows): device pass failed");
+      if (rc == 2) PA_FAIL("assemble!(I,J,V,rows): a ghost row's owner is not in the exchanger's parts_rcv (KeyError)");
       PA_FAIL("to_lids!: a row global id is not a local id of rows (KeyError)");
     }
     sd[i].off.assign(sd[i].cnt.size() + 1, 0);
@@ -2141,7 +2361,7 @@ static inline int64_t nz_index(const pa_mat* A, int64_t p) {
 // refresh the side SELL's copies of the irregular rows' values
 static int refresh_side(pa_mat* A, hipStream_t st) {
   if (A->s_nrows > 0) {
-    launch_side_fill(A, A->d_s_rowmap, A->d_s_rowlen, st);
+    launch_side_fill(A, A->d_s_srow ? A->d_s_srow : A->d_s_rowmap, A->d_s_rowlen, st);
     HIPC(hipGetLastError());
   }
   return 0;
@@ -2264,7 +2484,9 @@ int pa_mat_destroy(pa_mat* A) {
                   (void*)A->d_s_col, A->d_s_val, (void*)A->d_s_rowmap, (void*)A->d_s_rowlen, A->d_dotp,
                   (void*)A->d_long_row, (void*)A->d_long_ptr, (void*)A->d_long_col, (void*)A->d_sflags,
                   (void*)A->d_lmask, (void*)A->d_lchunk_start, (void*)A->d_lrow_chunk, A->d_lpart,
-                  (void*)A->d_col16, (void*)A->d_gbase, (void*)A->d_dint_list, (void*)A->d_dbnd_list})
+                  (void*)A->d_col16, (void*)A->d_gbase, (void*)A->d_dint_list, (void*)A->d_dbnd_list,
+                  (void*)A->d_qmap, (void*)A->d_qcol, (void*)A->d_qint_list, (void*)A->d_qbnd_list,
+                  (void*)A->d_s_srow})
     dev_free(p);
   delete A;
   return 0;
@@ -2289,6 +2511,13 @@ int pa_mat_multipattern_info(const pa_mat* A, int64_t* multi_slices) {
 int pa_mat_delta16_info(const pa_mat* A, int64_t* delta16_slices) {
   CHECK_ARG(A, "null matrix");
   if (delta16_slices) *delta16_slices = A->nd_int + A->nd_bnd;
+  return 0;
+}
+
+int pa_mat_quadrun_info(const pa_mat* A, int64_t* quadrun_slices, int* quad_sorted) {
+  CHECK_ARG(A, "null matrix");
+  if (quadrun_slices) *quadrun_slices = A->nq_int + A->nq_bnd;
+  if (quad_sorted) *quad_sorted = A->d_qmap ? 1 : 0;
   return 0;
 }
 
@@ -2320,6 +2549,10 @@ int pa_mat_traffic(const pa_mat* A, int64_t* value_bytes, int64_t* index_bytes, 
       v += (int64_t)A->h_slen[s] * H * S;
       ix += (int64_t)A->h_slen[s] * H * 2;
       m += 8 + 4 + 4 + 4;  // offset, length, list entry, ghost base
+    } else if (kd == 4) {
+      v += (int64_t)A->h_slen[s] * H * S;
+      ix += (int64_t)A->h_slen[s] * 64 * 4;  // one column per entry and lane
+      m += 8 + 4 + 4;
     } else {
       v += (int64_t)A->h_slen[s] * H * S;
       ix += (int64_t)A->h_slen[s] * H * 4;
@@ -2334,6 +2567,7 @@ int pa_mat_traffic(const pa_mat* A, int64_t* value_bytes, int64_t* index_bytes, 
   v += A->n_lnz * S;
   ix += A->n_lnz * 4;
   m += A->n_long * 16;
+  if (A->d_qmap) m += A->nslices * 64 * 4;  // the lanes' first rows
   if (value_bytes) *value_bytes = v;
   if (index_bytes) *index_bytes = ix;
   if (meta_bytes) *meta_bytes = m;
@@ -2356,6 +2590,25 @@ int pa_mat_info(const pa_mat* A, int64_t* nrows, int64_t* nnz, int64_t* slots, i
 // owned rows is accumulated by the SpMV kernel itself (per-slice partials in
 // A->d_dotp, folded by fold_dot) — the CG's `dot(u, c)` after `mul!(c, A, u)`.
 constexpr int kMaxTimed = 1024;  // mul! calls recorded per context between reads
+
+// The device CG's fused u update of one mul!(c, A, u) (pa_cg_solve_all): the
+// call's x is r; per part the old u, the buffer for the new u, x (for the
+// deferred x .+= α.*u) and the CG state.  The SpMV kernels (XV) compute
+// u_new = r .+ β.*u_old on the fly; the ghost lids (after the halo of r)
+// get u_new and the x update from k_cg_ghost.
+struct CGFuse {
+  std::vector<const void*> u_old;
+  std::vector<void*> u_new, xacc;
+  std::vector<CGState*> st;
+};
+
+// u_new and the deferred x update of part i's ghost lids (owned lids are
+// 0..noids-1: the device CG needs contiguous owned lids), after the halo and
+// before the dot fold (whose α step marks the x update as applied)
+static void cg_ghosts(const CGFuse* fz, int i, const pa_mat* A, const pa_vec* r, hipStream_t st) {
+  if (!fz || r->n <= A->nrows) return;
+  launch_cg_ghost(A->dtype, A->nrows, r->n, r->d, fz->u_old[i], fz->u_new[i], fz->xacc[i], fz->st[i], st);
+}
 
 // The grouped path applies when every part of the call shares one stream
 // pair (pa_ctx_create_shared: same device, one in-order chain) and every
@@ -2400,7 +2653,8 @@ static int group_ok(int n, pa_mat* const A[], pa_xchg* const xg[], bool any_x, i
 static int spmv_grouped(int n, pa_mat* const A[], pa_vec* const y[], const pa_index* const y_idx[],
                         pa_vec* const x[], pa_xchg* const xg[], bool any_x, bool has_alpha, int bmode,
                         const void* alpha, const void* beta, const std::vector<void*>& dotp, bool want_dot,
-                        CGState* const* dot_tail, const std::vector<hipEvent_t*>& tslot, int dt, bool direct) {
+                        CGState* const* dot_tail, const std::vector<hipEvent_t*>& tslot, int dt, bool direct,
+                        const CGFuse* fz) {
   pa_ctx* c0 = A[0]->ctx;
   HIPC(hipSetDevice(c0->device));
   const hipStream_t sm = SM(c0), sc = SC(c0);
@@ -2409,11 +2663,21 @@ static int spmv_grouped(int n, pa_mat* const A[], pa_vec* const y[], const pa_in
       if (tslot[i]) HIPC(hipEventRecord(tslot[i][k], sm));
     return 0;
   };
+  // timing marks of the direct pull: no slice runs before the halo is
+  // complete, so interior = 0, halo = the pull, boundary = every slice
+  const bool dmark = any_x && direct;
+  if (dmark && (mark(0) || mark(1))) return -1;
   if (any_x && direct) {
     // every ghost of x straight from its owner's x, in stream order before
     // the slices (owned values are only read, ghosts only written)
     void** bases = direct_bases(c0, n, x);
     if (!bases) return -1;
+    if (g_capture_tables) {  // the graph's own copy: the cache may evict this one
+      std::vector<void*> xs(n);
+      for (int i = 0; i < n; ++i) xs[i] = x[i]->d;
+      bases = const_cast<void**>(graph_owned<void*>(bases, xs));
+      CHECK_ARG(!g_graph_owned_failed, "graph capture: table allocation failed");
+    }
     PullGroup qg{};
     for (int i0 = 0; i0 < n; i0 += PA_GROUP_MAX) {
       qg.np = 0;
@@ -2422,8 +2686,9 @@ static int spmv_grouped(int n, pa_mat* const A[], pa_vec* const y[], const pa_in
         const int k = qg.np++;
         qg.n[k] = X->n_rcv_data;
         qg.lids[k] = X->d_lids_rcv;
-        qg.bid[k] = X->direct.d_bid;
-        qg.elem[k] = X->direct.d_elem;
+        qg.bid[k] = graph_owned<int32_t>(X->direct.d_bid, X->direct.h_bid);
+        qg.elem[k] = graph_owned<int64_t>(X->direct.d_elem, X->direct.h_elem);
+        CHECK_ARG(!g_graph_owned_failed, "graph capture: table allocation failed");
         qg.bases[k] = (const void* const*)bases;
         qg.v[k] = x[i]->d;
       }
@@ -2456,9 +2721,10 @@ static int spmv_grouped(int n, pa_mat* const A[], pa_vec* const y[], const pa_in
         const int k = qg.np++;
         qg.n[k] = X->n_rcv_data;
         qg.lids[k] = X->d_lids_rcv;
-        qg.bid[k] = P.d_bid;
-        qg.elem[k] = P.d_elem;
-        qg.bases[k] = (const void* const*)P.d_bases;
+        qg.bid[k] = graph_owned<int32_t>(P.d_bid, P.h_bid);
+        qg.elem[k] = graph_owned<int64_t>(P.d_elem, P.h_elem);
+        qg.bases[k] = (const void* const*)graph_owned<void*>(P.d_bases, P.h_bases);
+        CHECK_ARG(!g_graph_owned_failed, "graph capture: table allocation failed");
         qg.v[k] = x[i]->d;
       }
       launch_pull_group(dt, qg, sc);
@@ -2466,15 +2732,22 @@ static int spmv_grouped(int n, pa_mat* const A[], pa_vec* const y[], const pa_in
     EV(hipEventRecord(c0->ev_recvd, sc));
   }
   HIPC(hipGetLastError());
-  std::vector<SpmvPart> P0, P1, P3, P4;
+  std::vector<SpmvPart> P0, P1, P3, P4, P5;
   auto part = [&](int i, int64_t nwork, const int32_t* list) {
     const int32_t* ymap = y_idx[i]->own_contig ? nullptr : y_idx[i]->d_oid_to_lid;
-    return SpmvPart{nwork, list, A[i], x[i]->d, y[i]->d, ymap, dotp[i]};
+    SpmvPart q{nwork, list, A[i], x[i]->d, y[i]->d, ymap, dotp[i]};
+    if (fz) {
+      q.xu = fz->u_old[i];
+      q.un = fz->u_new[i];
+      q.xacc = fz->xacc[i];
+      q.cg = fz->st[i];
+    }
+    return q;
   };
   auto launch_all = [&](int which, const std::vector<SpmvPart>& v) {
     if (!v.empty()) launch_spmv_group(which, (int)v.size(), v.data(), has_alpha, bmode, alpha, beta, sm);
   };
-  if (mark(0)) return -1;
+  if (dmark ? mark(2) : mark(0)) return -1;
   // no halo in flight (none, or pulled already on this stream): every slice
   // kind of every part in one launch — side rows and int32 slices first, so
   // their few long waves start early, then delta16, multi-pattern, pattern
@@ -2506,6 +2779,8 @@ static int spmv_grouped(int n, pa_mat* const A[], pa_vec* const y[], const pa_in
       if (g_spmv_format == 1 && A[i]->has_pat) {
         add(4, i, A[i]->nd_int, A[i]->d_dint_list);
         add(4, i, A[i]->nd_bnd, A[i]->d_dbnd_list);
+        add(5, i, A[i]->nq_int, A[i]->d_qint_list);
+        add(5, i, A[i]->nq_bnd, A[i]->d_qbnd_list);
       }
     for (int i = 0; i < n; ++i)
       if (g_spmv_format == 1 && A[i]->has_pat) {
@@ -2520,7 +2795,7 @@ static int spmv_grouped(int n, pa_mat* const A[], pa_vec* const y[], const pa_in
     merged = launch_spmv_merged((int)E.size(), W.data(), E.data(), has_alpha, bmode, alpha, beta, c0,
                                 g_capture_tables, sm);
     if (merged < 0) PA_FAIL("mul!: merged launch table (device allocation or copy) failed");
-    if (merged == 0 && (mark(1) || mark(2))) return -1;
+    if (merged == 0 && !dmark && (mark(1) || mark(2))) return -1;
   }
   if (merged) {
   // interior slices (no ghost column): overlap with the pulls on the comm stream
@@ -2530,6 +2805,7 @@ static int spmv_grouped(int n, pa_mat* const A[], pa_vec* const y[], const pa_in
       P3.push_back(part(i, A[i]->nm_int, A[i]->d_mint_list));
       P1.push_back(part(i, A[i]->nx_int, A[i]->d_xint_list));
       P4.push_back(part(i, A[i]->nd_int, A[i]->d_dint_list));
+      P5.push_back(part(i, A[i]->nq_int, A[i]->d_qint_list));
     } else if (A[i]->d_bnd_list) {
       P1.push_back(part(i, A[i]->nslices_int, A[i]->d_int_list));
     } else {
@@ -2539,17 +2815,19 @@ static int spmv_grouped(int n, pa_mat* const A[], pa_vec* const y[], const pa_in
   launch_all(0, P0);
   launch_all(3, P3);
   launch_all(4, P4);
+  launch_all(5, P5);
   launch_all(1, P1);
-  if (mark(1)) return -1;
+  if (!dmark && mark(1)) return -1;
   if (any_x && !direct) EV(hipStreamWaitEvent(sm, c0->ev_recvd, 0));
-  if (mark(2)) return -1;
-  P0.clear(); P1.clear(); P3.clear(); P4.clear();
+  if (!dmark && mark(2)) return -1;
+  P0.clear(); P1.clear(); P3.clear(); P4.clear(); P5.clear();
   std::vector<SpmvPart> P2;
   for (int i = 0; i < n; ++i) {
     if (g_spmv_format == 1 && A[i]->has_pat) {
       P0.push_back(part(i, A[i]->np_bnd, A[i]->d_pbnd_list));
       P3.push_back(part(i, A[i]->nm_bnd, A[i]->d_mbnd_list));
       P4.push_back(part(i, A[i]->nd_bnd, A[i]->d_dbnd_list));
+      P5.push_back(part(i, A[i]->nq_bnd, A[i]->d_qbnd_list));
       P1.push_back(part(i, A[i]->nx_bnd, A[i]->d_xbnd_list));
       P2.push_back(part(i, A[i]->s_nslices, nullptr));
     } else if (A[i]->d_bnd_list) {
@@ -2559,6 +2837,7 @@ static int spmv_grouped(int n, pa_mat* const A[], pa_vec* const y[], const pa_in
   launch_all(0, P0);
   launch_all(3, P3);
   launch_all(4, P4);
+  launch_all(5, P5);
   launch_all(1, P1);
   launch_all(2, P2);
   }  // per-kind launches
@@ -2566,6 +2845,7 @@ static int spmv_grouped(int n, pa_mat* const A[], pa_vec* const y[], const pa_in
     const int32_t* ymap = y_idx[i]->own_contig ? nullptr : y_idx[i]->d_oid_to_lid;
     const bool pat = g_spmv_format == 1 && A[i]->has_pat;
     const int64_t long_base = A[i]->nslices + (pat ? A[i]->s_nslices : 0);
+    cg_ghosts(fz, i, A[i], x[i], sm);
     launch_spmv_long(A[i], x[i]->d, y[i]->d, ymap, has_alpha, bmode, alpha, beta, dotp[i], long_base, sm);
     if (want_dot) {
       pa_ctx* c = A[i]->ctx;
@@ -2588,24 +2868,34 @@ static int spmv_grouped(int n, pa_mat* const A[], pa_vec* const y[], const pa_in
 // slices and side rows, after it): one merged launch (pa_tune spmv_merge)
 // or one launch per slice kind.
 static int launch_phase(int phase, pa_mat* A, const void* x, void* y, const int32_t* ymap, bool has_alpha,
-                        int bmode, const void* alpha, const void* beta, void* dotp, hipStream_t st) {
+                        int bmode, const void* alpha, const void* beta, void* dotp, hipStream_t st,
+                        const CGFuse* fz = nullptr, int fi = 0) {
   std::vector<SpmvPart> E;
   std::vector<int> W;
   auto add = [&](int which, int64_t nwork, const int32_t* list) {
     if (nwork <= 0) return;
-    E.push_back(SpmvPart{nwork, list, A, x, y, ymap, dotp});
+    SpmvPart q{nwork, list, A, x, y, ymap, dotp};
+    if (fz) {
+      q.xu = fz->u_old[fi];
+      q.un = fz->u_new[fi];
+      q.xacc = fz->xacc[fi];
+      q.cg = fz->st[fi];
+    }
+    E.push_back(q);
     W.push_back(which);
   };
   if (g_spmv_format == 1 && A->has_pat) {
     if (phase == 0) {
       add(1, A->nx_int, A->d_xint_list);
       add(4, A->nd_int, A->d_dint_list);
+      add(5, A->nq_int, A->d_qint_list);
       add(3, A->nm_int, A->d_mint_list);
       add(0, A->np_int, A->d_pint_list);
     } else {
       add(2, A->s_nslices, nullptr);
       add(1, A->nx_bnd, A->d_xbnd_list);
       add(4, A->nd_bnd, A->d_dbnd_list);
+      add(5, A->nq_bnd, A->d_qbnd_list);
       add(3, A->nm_bnd, A->d_mbnd_list);
       add(0, A->np_bnd, A->d_pbnd_list);
     }
@@ -2623,13 +2913,14 @@ static int launch_phase(int phase, pa_mat* A, const void* x, void* y, const int3
     if (rc == 0) return 0;
   }
   for (size_t k = 0; k < E.size(); ++k)
-    launch_spmv_part(W[k], E[k].nwork, E[k].list, A, x, y, ymap, has_alpha, bmode, alpha, beta, dotp, st);
+    launch_spmv_part(W[k], E[k].nwork, E[k].list, A, x, y, ymap, has_alpha, bmode, alpha, beta, dotp, st, &E[k]);
   return 0;
 }
 
 static int spmv_impl(int n, pa_mat* const A[], pa_vec* const y[], const pa_index* const y_idx[],
                      pa_vec* const x[], const pa_index* const x_idx[], pa_xchg* const xg[],
-                     const void* alpha, const void* beta, bool want_dot, CGState* const* dot_tail = nullptr) {
+                     const void* alpha, const void* beta, bool want_dot, CGState* const* dot_tail = nullptr,
+                     const CGFuse* fz = nullptr) {
   CHECK_ARG(n >= 1 && A && y && x && alpha && beta, "null argument");
   const int dt = A[0]->dtype;
   bool any_x = false;
@@ -2663,6 +2954,11 @@ static int spmv_impl(int n, pa_mat* const A[], pa_vec* const y[], const pa_index
   // timing: the events of this call (slot tn of each timed context); the
   // grouped path brackets all parts with the same launches: part 1 of the
   // call records them once
+  if (any_x)  // before group_ok, which reads every exchanger
+    for (int i = 0; i < n; ++i) {
+      CHECK_ARG(xg[i] && xg[i]->ctx == x[i]->ctx, "mul!: exchanger missing for some parts");
+      if (check_lids(xg[i], x[i])) return -1;
+    }
   const int gmode = group_ok(n, A, xg, any_x, dt);
   const bool grouped = gmode != 0;
   std::vector<hipEvent_t*> tslot(n, nullptr);
@@ -2680,20 +2976,11 @@ static int spmv_impl(int n, pa_mat* const A[], pa_vec* const y[], const pa_index
     tslot[i] = &c->tev[4 * c->tn];
   }
   if (grouped) {
-    if (any_x)
-      for (int i = 0; i < n; ++i) {
-        CHECK_ARG(xg[i] && xg[i]->ctx == x[i]->ctx, "mul!: exchanger missing for some parts");
-        if (check_lids(xg[i], x[i])) return -1;
-      }
     return spmv_grouped(n, A, y, y_idx, x, xg, any_x, has_alpha, bmode, alpha, beta, dotp, want_dot, dot_tail,
-                        tslot, dt, gmode == 2);
+                        tslot, dt, gmode == 2, fz);
   }
 
   if (any_x) {
-    for (int i = 0; i < n; ++i) {
-      CHECK_ARG(xg[i] && xg[i]->ctx == x[i]->ctx, "mul!: exchanger missing for some parts");
-      if (check_lids(xg[i], x[i])) return -1;
-    }
     if (pre_pack_wait(n, xg)) return -1;
     for (int i = 0; i < n; ++i) {
       pa_ctx* c = xg[i]->ctx;
@@ -2709,7 +2996,7 @@ static int spmv_impl(int n, pa_mat* const A[], pa_vec* const y[], const pa_index
     const int32_t* ymap = y_idx[i]->own_contig ? nullptr : y_idx[i]->d_oid_to_lid;
     if (tslot[i]) HIPC(hipEventRecord(tslot[i][0], SM(c)));
     // interior slices (no ghost column): overlap with the halo transport
-    if (launch_phase(0, A[i], x[i]->d, y[i]->d, ymap, has_alpha, bmode, alpha, beta, dotp[i], SM(c))) return -1;
+    if (launch_phase(0, A[i], x[i]->d, y[i]->d, ymap, has_alpha, bmode, alpha, beta, dotp[i], SM(c), fz, i)) return -1;
     if (tslot[i]) HIPC(hipEventRecord(tslot[i][1], SM(c)));
   }
   HIPC(hipGetLastError());
@@ -2725,7 +3012,8 @@ static int spmv_impl(int n, pa_mat* const A[], pa_vec* const y[], const pa_index
     if (tslot[i]) HIPC(hipEventRecord(tslot[i][2], SM(c)));
     const int32_t* ymap = y_idx[i]->own_contig ? nullptr : y_idx[i]->d_oid_to_lid;
     // slices reading ghosts and the side rows (after the halo)
-    if (launch_phase(1, A[i], x[i]->d, y[i]->d, ymap, has_alpha, bmode, alpha, beta, dotp[i], SM(c))) return -1;
+    if (launch_phase(1, A[i], x[i]->d, y[i]->d, ymap, has_alpha, bmode, alpha, beta, dotp[i], SM(c), fz, i)) return -1;
+    cg_ghosts(fz, i, A[i], x[i], SM(c));
     // long rows (after the halo: they may read ghost columns)
     const bool pat = g_spmv_format == 1 && A[i]->has_pat;
     const int64_t long_base = A[i]->nslices + (pat ? A[i]->s_nslices : 0);
@@ -2830,6 +3118,7 @@ int pa_spmv_graph_create(int n, pa_mat* const A[], pa_vec* const y[], const pa_i
     g_capture_stream = G->origin;  // the parts' kernels as one chain
     g_capture_tables = &G->tables;
     g_capture_uploads.clear();
+    g_graph_owned_failed = false;
     rc = spmv_impl(n, A, y, y_idx, x, x_idx, xg, alpha, beta, false);
     g_capture_tables = nullptr;
     g_capture_stream = nullptr;
@@ -3227,17 +3516,46 @@ int pa_cg_solve_all(int n, pa_mat* const A[], pa_vec* const x[], const pa_vec* c
   // one part in this process and no other process: the folds end in the
   // scalar updates themselves (no gather, no scalar kernels)
   const bool tail = !R.remote && R.P == 1;
+  // fused u update (pa_tune cg_fuse): u .= r .+ β.*u inside the SpMV, u in
+  // two buffers (iteration t reads ub[t%2], writes ub[(t+1)%2]); the deferred
+  // x .+= α.*u rides along.  Not for matrices with long rows (their kernel
+  // gathers x directly).
+  bool fuse = g_cg_fuse != 0;
+  for (int i = 0; i < n; ++i) fuse = fuse && A[i]->n_long == 0;
+  std::vector<pa_vec*> u2(n, nullptr);
+  struct U2Free {
+    std::vector<pa_vec*>& v;
+    ~U2Free() { for (pa_vec* p : v) if (p) pa_vec_destroy(p); }
+  } u2_free{u2};
+  if (fuse)
+    for (int i = 0; i < n; ++i)
+      if (pa_vec_create(R.ctxs[i], dt, u[i]->n, &u2[i])) return -1;
+  auto ubuf = [&](int64_t t, int i) -> void* { return (t % 2 == 0) ? u[i]->d : u2[i]->d; };
   int64_t enqueued = 0;
   bool done = h.done != 0;
   while (!done && enqueued < maxiter) {
     const int64_t k = std::min<int64_t>(batch, maxiter - enqueued);  // the same on every rank
     for (int64_t t = 0; t < k; ++t) {
-      for (int i = 0; i < n; ++i) {  // (x .+= α.*u of the previous iteration); u .= r .+ β.*u
-        HIPC(hipSetDevice(R.ctxs[i]->device));
-        launch_cg_xu(dt, u[i]->n, x[i]->d, u[i]->d, r[i]->d, R.st[i], R.ctxs[i]->s_main);
+      if (fuse) {
+        // mul!(c, A, u) with u = r .+ β.*u_old evaluated inside the SpMV (its
+        // halo carries r), the owned u written, x .+= α.*u_old of the
+        // previous iteration applied; dot(u, c) accumulated by the SpMV
+        CGFuse fz;
+        for (int i = 0; i < n; ++i) {
+          fz.u_old.push_back(ubuf(enqueued + t, i));
+          fz.u_new.push_back(ubuf(enqueued + t + 1, i));
+          fz.xacc.push_back(x[i]->d);
+          fz.st.push_back(R.st[i]);
+        }
+        if (spmv_impl(n, A, c, idx, r, idx, xg, one, zero, true, tail ? R.st.data() : nullptr, &fz)) return -1;
+      } else {
+        for (int i = 0; i < n; ++i) {  // (x .+= α.*u of the previous iteration); u .= r .+ β.*u
+          HIPC(hipSetDevice(R.ctxs[i]->device));
+          launch_cg_xu(dt, u[i]->n, x[i]->d, u[i]->d, r[i]->d, R.st[i], R.ctxs[i]->s_main);
+        }
+        // mul!(c, A, u) with dot(u, c) accumulated by the SpMV; α = residual² / dot(u, c)
+        if (spmv_impl(n, A, c, idx, u, idx, xg, one, zero, true, tail ? R.st.data() : nullptr)) return -1;
       }
-      // mul!(c, A, u) with dot(u, c) accumulated by the SpMV; α = residual² / dot(u, c)
-      if (spmv_impl(n, A, c, idx, u, idx, xg, one, zero, true, tail ? R.st.data() : nullptr)) return -1;
       if (!tail) {
         if (cg_gather(R, accsz)) return -1;
         for (int i = 0; i < n; ++i) {
@@ -3282,7 +3600,7 @@ int pa_cg_solve_all(int n, pa_mat* const A[], pa_vec* const x[], const pa_vec* c
   if (h.it > h.xit) {  // the last iteration's deferred x .+= α.*u (u untouched: done)
     for (int i = 0; i < n; ++i) {
       HIPC(hipSetDevice(R.ctxs[i]->device));
-      launch_cg_xu(dt, u[i]->n, x[i]->d, u[i]->d, r[i]->d, R.st[i], R.ctxs[i]->s_main);
+      launch_cg_xu(dt, u[i]->n, x[i]->d, fuse ? ubuf(enqueued, i) : u[i]->d, r[i]->d, R.st[i], R.ctxs[i]->s_main);
     }
     for (int i = 0; i < n; ++i) {
       HIPC(hipSetDevice(R.ctxs[i]->device));

@@ -600,14 +600,18 @@ __global__ void k_seg_of_lid(int64_t nslots, const int32_t* __restrict__ lids_rc
 }
 
 // key[k] = 0 for a row owned here, 1 + segment of the row's owner otherwise
-// (rows' gid table: an absent gid is the KeyError of to_lids!)
+// (rows' gid table: an absent gid is the KeyError of to_lids!; a ghost row
+// that no receive segment lists is the KeyError of owner_to_i,
+// Interfaces.jl:2428-2430: the exchanger does not match the rows)
 __global__ void k_coo_seg(int64_t n, const int64_t* __restrict__ I, const uint64_t* __restrict__ sgid,
                           const int64_t* __restrict__ slid, int64_t nl, const int32_t* __restrict__ seg_of_lid,
                           uint64_t* __restrict__ key, int64_t* __restrict__ idx, int* __restrict__ bad) {
   for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < n; k += (int64_t)gridDim.x * blockDim.x) {
     const int64_t l = gid_lookup(I[k], sgid, slid, nl);
+    const int32_t sg = l < 0 ? -1 : seg_of_lid[l];
     if (l < 0) *bad = 1;
-    key[k] = l < 0 ? 0 : (uint64_t)(seg_of_lid[l] + 1);
+    else if (sg == -2) *bad = 2;  // a ghost row whose owner is not in parts_rcv
+    key[k] = sg < 0 ? 0 : (uint64_t)(sg + 1);
     idx[k] = k;
   }
 }
@@ -635,9 +639,11 @@ __global__ void k_coo_pack(int64_t nr, const int64_t* __restrict__ idx, const in
 
 // One part's send side.  Outputs (device, owned by the caller): *sI, *sJ,
 // *sV (the sent triplets, segment after segment) and cnt[0..nseg) on the
-// host.  Returns 1 when a row gid is not a local id of rows (KeyError).
+// host.  Returns 1 when a row gid is not a local id of rows (KeyError), 2
+// when a ghost row's owner has no receive segment (KeyError).
 int coo_assemble_pack(int dtype, int64_t n, const int64_t* I, const int64_t* J, void* V, const uint64_t* sgid,
-                      const int64_t* slid, int64_t nl, int nseg, const int32_t* d_lids_rcv,
+                      const int64_t* slid, int64_t nl, const std::vector<int32_t>& lid_to_ohid, int nseg,
+                      const int32_t* d_lids_rcv,
                       const std::vector<int64_t>& ptrs_rcv, int64_t** sI, int64_t** sJ, void** sV,
                       std::vector<int64_t>* cnt, hipStream_t st) {
   const size_t S = dtype_size(dtype);
@@ -653,8 +659,13 @@ int coo_assemble_pack(int dtype, int64_t n, const int64_t* I, const int64_t* J, 
   std::vector<int64_t> hfirst(nseg + 2, -1);
   const int64_t nslots = ptrs_rcv.empty() ? 0 : ptrs_rcv.back();
   int64_t nloc = n;
-  e = hipMalloc((void**)&sol, (nl > 0 ? nl : 1) * 4);
-  if (e == hipSuccess) e = hipMemsetAsync(sol, 0xff, (nl > 0 ? nl : 1) * 4, st);  // -1: owned lid
+  {
+    // -1: owned lid, -2: ghost lid (k_seg_of_lid then sets its segment)
+    std::vector<int32_t> hs(nl > 0 ? nl : 1, -1);
+    for (int64_t l = 0; l < nl; ++l) hs[l] = lid_to_ohid[l] > 0 ? -1 : -2;
+    e = hipMalloc((void**)&sol, hs.size() * 4);
+    if (e == hipSuccess) e = hipMemcpy(sol, hs.data(), hs.size() * 4, hipMemcpyHostToDevice);
+  }
   if (e == hipSuccess && nslots > 0) e = hipMalloc((void**)&dptrs, ptrs_rcv.size() * 8);
   if (e == hipSuccess && nslots > 0)
     e = hipMemcpyAsync(dptrs, ptrs_rcv.data(), ptrs_rcv.size() * 8, hipMemcpyHostToDevice, st);
@@ -669,7 +680,7 @@ int coo_assemble_pack(int dtype, int64_t n, const int64_t* I, const int64_t* J, 
   e = hipMemcpyAsync(&hbad, bad, sizeof(int), hipMemcpyDeviceToHost, st);
   if (e == hipSuccess) e = hipStreamSynchronize(st);
   if (e != hipSuccess) goto done;
-  if (hbad) { rc = 1; goto done; }
+  if (hbad) { rc = hbad; goto done; }  // 1: unknown gid, 2: ghost row without a segment
   e = sort_pairs(key, idx, n, bits_for((uint64_t)nseg + 1), st);  // stable: input order inside a segment
   if (e == hipSuccess) e = hipMalloc((void**)&first, (nseg + 2) * 8);
   if (e == hipSuccess) e = hipMemsetAsync(first, 0xff, (nseg + 2) * 8, st);

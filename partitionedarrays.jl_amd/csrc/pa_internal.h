@@ -228,6 +228,13 @@ struct SpmvPart {
   void* y;
   const int32_t* ymap;
   void* dotp;
+  // the device CG's fused u update (pa_cg_solve_all; null cg: a plain SpMV):
+  // x is r, the SpMV multiplies u_new = r .+ β.*xu, writes u_new of the owned
+  // rows to un and applies the deferred x .+= α.*xu to xacc
+  const void* xu = nullptr;
+  void* un = nullptr;
+  void* xacc = nullptr;
+  const CGState* cg = nullptr;
 };
 
 struct PackGroup {
@@ -270,6 +277,7 @@ struct pa_ctx {
   hipStream_t s_main = nullptr;   // compute stream
   hipStream_t s_comm = nullptr;   // halo transport stream (high priority)
   void* comm = nullptr;           // ncclComm_t (null: no remote transport)
+  bool halo_rccl = false;         // pa_comm_init_all: halo segments between parts of this process over RCCL too
   // the communicator is destroyed with the last part using it; parts of one
   // device share their device's rank (pa_comm_init_all), so the peer of a
   // halo segment from/to part q is rank_of_part[q-1] (null: rank = q-1)
@@ -333,14 +341,20 @@ struct pa_combine_plan {
 struct pa_pull {
   bool built = false;
   bool ok = false;                   // false: peers not reachable, use staging copies
-  std::vector<const void*> key;      // the local senders' buffers the table was built for
+  std::vector<const void*> key;      // the local senders (exchanger ids) and buffers the table was built for
   int32_t* d_bid = nullptr;
   int64_t* d_elem = nullptr;
   void** d_bases = nullptr;
+  // host copies: a graph capture gives the graph its own device copies
+  // (the cached tables may be rebuilt while the graph still replays)
+  std::vector<int32_t> h_bid;
+  std::vector<int64_t> h_elem;
+  std::vector<void*> h_bases;
 };
 
 struct pa_xchg {
   pa_ctx* ctx = nullptr;
+  uint64_t id = 0;                             // unique per exchanger of the process (cache keys)
   pa_pull pull[2];                             // [0] forward, [1] reverse
   // direct pull of mul! over parts sharing one stream pair (spmv_grouped):
   // receive slot p reads x of the call's part bid[p] at lid elem[p] (the
@@ -471,6 +485,22 @@ struct pa_mat {
   int32_t* d_mint_list = nullptr;    // multi-pattern slices without ghost reads
   int32_t* d_mbnd_list = nullptr;    // multi-pattern slices reading ghosts
   int64_t nm_int = 0, nm_bnd = 0;
+  // Quad-sorted layout (irregular partitions; SELL-C-σ at lane granularity,
+  // pa_tune "spmv_quadsort"): lane l of slice s holds the R consecutive
+  // owned rows qmap[s*64+l] .. +R-1 (nrows: a padding lane); null: the
+  // identity layout, rows s*H + l*R ...  Lanes are ordered by class (rows
+  // whose columns run in step, reading ghosts or not, their column offsets),
+  // so whole slices become pattern or quad-run slices.
+  int32_t* d_qmap = nullptr;
+  std::vector<int32_t> h_qmap;
+  // quad-run slices (kind 4): at every entry the lane's R rows read R
+  // consecutive columns: one int32 column (the lane's first row's) per entry
+  // and lane, at slot / R; the x values as one 16 B run
+  int32_t* d_qcol = nullptr;
+  int32_t* d_qint_list = nullptr;    // quad-run slices without ghost columns
+  int32_t* d_qbnd_list = nullptr;    // quad-run slices with ghost columns
+  int64_t nq_int = 0, nq_bnd = 0;
+  int maxlen_qrun = INT32_MAX;
   // side SELL: the irregular rows of pattern slices (row map → oid)
   int64_t s_nrows = 0, s_nslices = 0, s_slots = 0;
   int64_t* d_s_off = nullptr;
@@ -478,6 +508,7 @@ struct pa_mat {
   int32_t* d_s_col = nullptr;
   void* d_s_val = nullptr;
   int32_t* d_s_rowmap = nullptr;
+  int32_t* d_s_srow = nullptr;       // their structure rows (s*H + lane*R + r) when qmap: d_s_rowmap holds oids
   int32_t* d_s_rowlen = nullptr;
   void* d_dotp = nullptr;            // fused dot: one partial per (main + side) slice
 };

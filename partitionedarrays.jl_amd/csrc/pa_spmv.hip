@@ -20,6 +20,19 @@
 #include <cstring>
 #include <type_traits>
 
+// Build split: the file is compiled once per element type with
+// -DPA_SPMV_DT=0..3 (F32, F64, C64, C128: that type's SpMV kernels and
+// launchers, the bulk of the code) and once without (the dtype dispatchers,
+// the CG, pattern and layout kernels, the knobs), so that the hipcc runs go
+// in parallel (__graft_entry__.build).
+#if defined(PA_SPMV_DT)
+#define PA_DT_DEFINE 0
+#else
+#define PA_DT_DEFINE 1
+#endif
+#define PA_CAT2(a, b) a##b
+#define PA_CAT(a, b) PA_CAT2(a, b)
+
 namespace pa {
 
 template <typename T, int R>
@@ -56,6 +69,7 @@ typedef unsigned int spmv_u32x4 __attribute__((ext_vector_type(4)));
 // interleaved A/B on FE27 256³ (profiles/r02/stream/ab_xtri.txt): F64 −0.2 %,
 // C128 −0.9 %, C64 +0.4 %, F32 +3 % kernel time — the x loads are not what
 // bounds the SpMV (their 6 % in the probe is hidden in the full kernel).
+#if PA_DT_DEFINE
 int g_spmv_flags = SPMV_NT | SPMV_XPAIR | SPMV_TAILB | SPMV_IDLIST | SPMV_SHORT;
 int g_spmv_unroll = 8;
 // dynamic LDS per SpMV block (unused by the kernel): caps the blocks per CU,
@@ -72,6 +86,12 @@ int g_spmv_pattern_rule = 0;     // 1: slice encoding by streamed bytes, 0: patt
 // merged-launch tables allocated during a graph capture, copied after it ends
 // (no copies while a stream is being captured)
 std::vector<std::pair<void*, std::vector<char>>> g_capture_uploads;
+int g_long_exact = 1;  // pa_tune("long_rows_exact")
+#else
+extern int g_spmv_flags, g_spmv_unroll, g_spmv_lds, g_spmv_format, g_spmv_patterns, g_spmv_pattern_rule;
+extern std::vector<std::pair<void*, std::vector<char>>> g_capture_uploads;
+extern int g_long_exact;
+#endif
 
 // SpmvArgs' pointers are global memory.  The merged launch reads them from a
 // device-resident table, where the compiler cannot see their address space:
@@ -114,6 +134,7 @@ struct SpmvArgs {
   int kmax;
   const PA_GLB uint8_t* psel;      // multi-pattern: pattern of each lane (64 per slice)
   const PA_GLB int32_t* rowmap;    // structure row → oid (side SELL), null: identity
+  const PA_GLB int32_t* qmap;      // quad-sorted main structure: first oid of each (slice, lane), null: identity
   int64_t nrows;            // rows of this structure
   const PA_GLB T* x;
   int64_t nx;               // x length (lids)
@@ -134,6 +155,14 @@ struct SpmvArgs {
   // delta16 slices: 16-bit column codes and the per-slice ghost base
   const PA_GLB uint16_t* col16;
   const PA_GLB int32_t* gbase;
+  // the device CG's fused u update (XV kernels, pa_cg_solve_all): x is r,
+  // the gathered values are u_new = r .+ β.*u_old (β = res²/prev² of cg);
+  // waves of the main structure write u_new of their rows to un and apply
+  // the deferred x .+= α.*u_old to xacc (while cg->it > cg->xit)
+  const PA_GLB T* xu;
+  PA_GLB T* un;
+  PA_GLB T* xacc;
+  const PA_GLB CGState* cg;
 };
 
 template <typename T> struct DAcc { using type = double; };
@@ -169,24 +198,54 @@ __device__ __forceinline__ Pack<T, R> ld_xrun(const T* p) {
   return v;
 }
 
+// What an SpMV gathers as x.  XV false: a vector.  XV true (the device
+// CG's fused u update, pa_cg_solve_all): u_new = r .+ β.*u_old evaluated per
+// gathered element, in the wide type and rounded to T once (k_cg_xu's
+// arithmetic, IterativeSolvers' `u .= r .+ β.*u`), so iteration k's SpMV
+// reads r and u_{k-1} instead of a materialised u_k: the same values bit for
+// bit, one vector sweep less per iteration.
+template <typename T, bool XV>
+struct XSrc {
+  const T* __restrict__ x;
+  __device__ __forceinline__ T get(int64_t j) const { return x[j]; }
+  template <int R>
+  __device__ __forceinline__ Pack<T, R> run(int64_t j) const { return ld_xrun<T, R>(x + j); }
+};
+template <typename T>
+struct XSrc<T, true> {
+  const T* __restrict__ r;
+  const T* __restrict__ u;
+  double b;
+  __device__ __forceinline__ T f(T rv, T uv) const { return narrow<T>(widen(rv) + rscale(b, widen(uv))); }
+  __device__ __forceinline__ T get(int64_t j) const { return f(r[j], u[j]); }
+  template <int R>
+  __device__ __forceinline__ Pack<T, R> run(int64_t j) const {
+    const Pack<T, R> a = ld_xrun<T, R>(r + j), c = ld_xrun<T, R>(u + j);
+    Pack<T, R> o;
+#pragma unroll
+    for (int k = 0; k < R; ++k) o.v[k] = f(a.v[k], c.v[k]);
+    return o;
+  }
+};
+
 // the x values of a lane's R rows at one entry: one 16 B run when their
 // columns are consecutive (rows of a structured block, SPMV_XRUN), else R
 // gathers (c < 0: padding, read x[0], never used)
-template <typename T, int R>
-__device__ __forceinline__ void gather_x(T (&xv)[R], const int32_t (&c)[R], const T* __restrict__ x, bool xrun) {
+template <typename T, int R, typename XS>
+__device__ __forceinline__ void gather_x(T (&xv)[R], const int32_t (&c)[R], const XS& x, bool xrun) {
   if constexpr (R > 1 && sizeof(Pack<T, R>) == 16) {
     bool run = xrun && c[0] >= 0;
 #pragma unroll
     for (int r = 1; r < R; ++r) run = run && c[r] == c[0] + r;
     if (run) {
-      const Pack<T, R> p = ld_xrun<T, R>(x + c[0]);
+      const Pack<T, R> p = x.template run<R>(c[0]);
 #pragma unroll
       for (int r = 0; r < R; ++r) xv[r] = p.v[r];
       return;
     }
   }
 #pragma unroll
-  for (int r = 0; r < R; ++r) xv[r] = x[c[r] >= 0 ? c[r] : 0];
+  for (int r = 0; r < R; ++r) xv[r] = x.get(c[r] >= 0 ? c[r] : 0);
 }
 
 // One term of a row's sum.  A CSC parent scales x first, v*(x*α)
@@ -202,10 +261,10 @@ __device__ __forceinline__ T term(T v, T x, T alpha, bool pf) {
 // int32-column rows: c < 0 is padding (skipped: never multiplied)
 // TB: the entries past the last full U batch run as one masked batch
 // (entries >= len re-read entry len-1 and are never accumulated)
-template <typename T, int R, bool ALPHA, bool NT, int U, bool SH = false>
+template <typename T, int R, bool ALPHA, bool NT, int U, bool SH = false, typename XS>
 __device__ __forceinline__ void rows_int32(T (&acc)[R], const IPack<R>* __restrict__ cp,
                                            const Pack<T, R>* __restrict__ vp, int len,
-                                           const T* __restrict__ x, T alpha, bool pf, bool TB, bool xrun) {
+                                           const XS& x, T alpha, bool pf, bool TB, bool xrun) {
   int k = 0;
   if (SH) TB = true;  // short rows (len <= U): the one masked batch is the whole row
   for (; !SH && k + U <= len; k += U) {
@@ -256,7 +315,7 @@ __device__ __forceinline__ void rows_int32(T (&acc)[R], const IPack<R>* __restri
 #pragma unroll
     for (int r = 0; r < R; ++r) {
       const int32_t cc = c.c[r];
-      const T t = acc[r] + term<ALPHA>(v.v[r], x[cc >= 0 ? cc : 0], alpha, pf);
+      const T t = acc[r] + term<ALPHA>(v.v[r], x.get(cc >= 0 ? cc : 0), alpha, pf);
       acc[r] = pick(cc >= 0, t, acc[r]);
     }
   }
@@ -271,10 +330,10 @@ __device__ __forceinline__ int32_t d16_col(uint32_t q, int32_t row, int32_t gb) 
 }
 
 // delta16 rows: rows_int32 with the column ids decoded from 2 B codes
-template <typename T, int R, bool ALPHA, bool NT, int U, bool SH = false>
+template <typename T, int R, bool ALPHA, bool NT, int U, bool SH = false, typename XS>
 __device__ __forceinline__ void rows_d16(T (&acc)[R], const S16Pack<R>* __restrict__ cp,
                                          const Pack<T, R>* __restrict__ vp, int len,
-                                         const T* __restrict__ x, T alpha, bool pf, bool TB, int32_t row0, int32_t gb,
+                                         const XS& x, T alpha, bool pf, bool TB, int32_t row0, int32_t gb,
                                          bool xrun) {
   int k = 0;
   if (SH) TB = true;
@@ -335,8 +394,68 @@ __device__ __forceinline__ void rows_d16(T (&acc)[R], const S16Pack<R>* __restri
 #pragma unroll
     for (int r = 0; r < R; ++r) {
       const int32_t cc = d16_col(q.c[r], row0 + r, gb);
-      const T t = acc[r] + term<ALPHA>(v.v[r], x[cc >= 0 ? cc : 0], alpha, pf);
+      const T t = acc[r] + term<ALPHA>(v.v[r], x.get(cc >= 0 ? cc : 0), alpha, pf);
       acc[r] = pick(cc >= 0, t, acc[r]);
+    }
+  }
+}
+
+// quad-run rows (kind 4): at entry k the lane's R rows read the R
+// consecutive columns c, c+1, .., c+R-1 (c < 0: padding): one int32 column
+// per entry and lane, and the x values as one 16 B run
+template <typename T, int R, bool ALPHA, bool NT, int U, bool SH = false, typename XS>
+__device__ __forceinline__ void rows_qrun(T (&acc)[R], const int32_t* __restrict__ cp,
+                                          const Pack<T, R>* __restrict__ vp, int len, const XS& x, T alpha,
+                                          bool pf, bool TB) {
+  int k = 0;
+  if (SH) TB = true;
+  for (; !SH && k + U <= len; k += U) {
+    int32_t c[U];
+    Pack<T, R> v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) c[u] = ld<NT>(&cp[(k + u) * 64]);
+#pragma unroll
+    for (int u = 0; u < U; ++u) v[u] = ld<NT>(&vp[(k + u) * 64]);
+    Pack<T, R> xr[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) xr[u] = x.template run<R>(c[u] >= 0 ? c[u] : 0);
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const T t = acc[r] + term<ALPHA>(v[u].v[r], xr[u].v[r], alpha, pf);
+        acc[r] = pick(c[u] >= 0, t, acc[r]);
+      }
+  }
+  if (TB && k < len) {  // the last len % U entries as one masked batch
+    int32_t c[U];
+    Pack<T, R> v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) c[u] = k + u < len ? ld<NT>(&cp[(k + u) * 64]) : -1;
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (k + u < len) v[u] = ld<NT>(&vp[(k + u) * 64]);
+    Pack<T, R> xr[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (k + u < len) xr[u] = x.template run<R>(c[u] >= 0 ? c[u] : 0);
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const T t = acc[r] + term<ALPHA>(v[u].v[r], xr[u].v[r], alpha, pf);
+        acc[r] = pick(k + u < len && c[u] >= 0, t, acc[r]);
+      }
+    k = len;
+  }
+  for (; !SH && k < len; ++k) {
+    const int32_t c = ld<NT>(&cp[k * 64]);
+    const Pack<T, R> v = ld<NT>(&vp[k * 64]);
+    const Pack<T, R> xr = x.template run<R>(c >= 0 ? c : 0);
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const T t = acc[r] + term<ALPHA>(v.v[r], xr.v[r], alpha, pf);
+      acc[r] = pick(c >= 0, t, acc[r]);
     }
   }
 }
@@ -344,10 +463,10 @@ __device__ __forceinline__ void rows_d16(T (&acc)[R], const S16Pack<R>* __restri
 // pattern rows: column of row `rbase + r` at entry k is rbase + r + pat[k].
 // XP: the lane's R rows read R consecutive x values per entry, fetched as
 // one 16 B run (rows that are not regular get values they never use).
-template <typename T, int R, bool ALPHA, bool NT, int U, bool XP, bool SH = false>
+template <typename T, int R, bool ALPHA, bool NT, int U, bool XP, bool SH = false, typename XS>
 __device__ __forceinline__ void rows_pattern(T (&acc)[R], const int32_t* __restrict__ pat,
                                              const Pack<T, R>* __restrict__ vp, int len,
-                                             const T* __restrict__ x, int64_t rbase,
+                                             const XS& x, int64_t rbase,
                                              const bool (&ok)[R], T alpha, bool pf, bool TB) {
   if (SH) TB = true;  // short rows (len <= U): the one masked batch is the whole row
   int64_t xb[R];
@@ -369,7 +488,7 @@ __device__ __forceinline__ void rows_pattern(T (&acc)[R], const int32_t* __restr
     if constexpr (XP && R > 1) {
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        const Pack<T, R> xr = ld_xrun<T, R>(x + (any ? rbase + o[u] : 0));
+        const Pack<T, R> xr = x.template run<R>(any ? rbase + o[u] : 0);
 #pragma unroll
         for (int r = 0; r < R; ++r) xv[u][r] = xr.v[r];
       }
@@ -377,7 +496,7 @@ __device__ __forceinline__ void rows_pattern(T (&acc)[R], const int32_t* __restr
 #pragma unroll
       for (int u = 0; u < U; ++u)
 #pragma unroll
-        for (int r = 0; r < R; ++r) xv[u][r] = x[xb[r] >= 0 ? xb[r] + o[u] : 0];
+        for (int r = 0; r < R; ++r) xv[u][r] = x.get(xb[r] >= 0 ? xb[r] + o[u] : 0);
     }
 #pragma unroll
     for (int u = 0; u < U; ++u)
@@ -399,7 +518,7 @@ __device__ __forceinline__ void rows_pattern(T (&acc)[R], const int32_t* __restr
 #pragma unroll
       for (int u = 0; u < U; ++u)
         if (k + u < len) {
-          const Pack<T, R> xr = ld_xrun<T, R>(x + (any ? rbase + o[u] : 0));
+          const Pack<T, R> xr = x.template run<R>(any ? rbase + o[u] : 0);
 #pragma unroll
           for (int r = 0; r < R; ++r) xv[u][r] = xr.v[r];
         }
@@ -408,7 +527,7 @@ __device__ __forceinline__ void rows_pattern(T (&acc)[R], const int32_t* __restr
       for (int u = 0; u < U; ++u)
         if (k + u < len)
 #pragma unroll
-          for (int r = 0; r < R; ++r) xv[u][r] = x[xb[r] >= 0 ? xb[r] + o[u] : 0];
+          for (int r = 0; r < R; ++r) xv[u][r] = x.get(xb[r] >= 0 ? xb[r] + o[u] : 0);
     }
 #pragma unroll
     for (int u = 0; u < U; ++u)
@@ -425,7 +544,7 @@ __device__ __forceinline__ void rows_pattern(T (&acc)[R], const int32_t* __restr
     const Pack<T, R> v = ld<NT>(&vp[k * 64]);
 #pragma unroll
     for (int r = 0; r < R; ++r) {
-      acc[r] = acc[r] + term<ALPHA>(v.v[r], x[xb[r] >= 0 ? xb[r] + o : 0], alpha, pf);
+      acc[r] = acc[r] + term<ALPHA>(v.v[r], x.get(xb[r] >= 0 ? xb[r] + o : 0), alpha, pf);
     }
   }
 }
@@ -448,6 +567,7 @@ __device__ __forceinline__ T lane_shift(T v) {
   return o;
 }
 
+#if PA_DT_DEFINE
 // Per pattern slice (build time): does its pattern consist of consecutive
 // triples (o-1, o, o+1)?  (FE27: its 9 x-lines.)  Checking in the SpMV
 // itself costs a chain of dependent scalar loads per wave before its first
@@ -470,6 +590,7 @@ void launch_pattern_triples(const pa_mat* A, uint8_t* tri, hipStream_t st) {
   hipLaunchKernelGGL(k_pattern_triples, dim3((unsigned)((ns + 255) / 256)), dim3(256), 0, st, ns, A->kmax, A->d_kind,
                      A->d_plen, A->d_pat, tri);
 }
+#endif
 
 // Triple-pattern rows: per triple (o-1, o, o+1) ONE 16 B x run per lane, at
 // the centre offset o; the dx = -1 / +1 runs are the same values moved by
@@ -535,6 +656,56 @@ __device__ __forceinline__ void rows_pattern3(T (&acc)[R], const int32_t* __rest
   }
 }
 
+// α of the device CG state in the wide type W (Float64 / ComplexF64)
+template <typename W> __device__ inline W cg_alpha_of(const CGState* st);
+template <> __device__ inline double cg_alpha_of<double>(const CGState* st) { return st->alpha.re; }
+template <> __device__ inline c128 cg_alpha_of<c128>(const CGState* st) { return st->alpha; }
+
+// The fused CG update of one lane's R rows i0..i0+R-1 (< nrows; owned lids
+// = oids, contiguous): x[i] .+= α.*u_old[i] when an x update is pending
+// (xpend), and with U: u_new[i] = r[i] .+ β.*u_old[i] stored to un and
+// returned in unv.  16 B accesses when all R rows exist.  The arithmetic of
+// k_cg_xu, element for element.
+template <typename T, int R, bool UPD, typename XS, typename W>
+__device__ __forceinline__ void cg_rows_update(const SpmvArgs<T>& a, const XS& xs, int64_t i0, W alpha,
+                                               bool xpend = true, T* unv = nullptr) {
+  T* xacc = (T*)a.xacc;
+  T* un = (T*)a.un;
+  if (i0 + R <= a.nrows) {
+    const Pack<T, R> uo = *reinterpret_cast<const Pack<T, R>*>(xs.u + i0);
+    if (UPD) {
+      const Pack<T, R> rv = *reinterpret_cast<const Pack<T, R>*>(xs.r + i0);
+      Pack<T, R> o;
+#pragma unroll
+      for (int k = 0; k < R; ++k) o.v[k] = xs.f(rv.v[k], uo.v[k]);
+      *reinterpret_cast<Pack<T, R>*>(un + i0) = o;
+#pragma unroll
+      for (int k = 0; k < R; ++k) unv[k] = o.v[k];
+    }
+    if (xpend) {
+      Pack<T, R> xv = *reinterpret_cast<const Pack<T, R>*>(xacc + i0);
+#pragma unroll
+      for (int k = 0; k < R; ++k) xv.v[k] = narrow<T>(widen(xv.v[k]) + alpha * widen(uo.v[k]));
+      *reinterpret_cast<Pack<T, R>*>(xacc + i0) = xv;
+    }
+    return;
+  }
+#pragma unroll
+  for (int k = 0; k < R; ++k) {
+    const int64_t i = i0 + k;
+    if (i >= a.nrows) {
+      if (UPD) unv[k] = zero_of<T>();
+      continue;
+    }
+    const T uo = xs.u[i];
+    if (UPD) {
+      unv[k] = xs.f(xs.r[i], uo);
+      un[i] = unv[k];
+    }
+    if (xpend) xacc[i] = narrow<T>(widen(xacc[i]) + alpha * widen(uo));
+  }
+}
+
 // BMODE: 0 → acc = 0 (β == 0: fill!(co,0)), 1 → acc = y (β == 1),
 //        2 → acc = y*β (rmul!(co,β)).  Interfaces.jl:2262-2263.
 // PK: the launch's slices are int32-column slices (0), pattern slices (1:
@@ -545,15 +716,39 @@ __device__ __forceinline__ void rows_pattern3(T (&acc)[R], const int32_t* __rest
 // One wave computes work item w (slice a.list[w], or w) of the structure a.
 // SH: every row of the launch has at most U entries (FD7: 7) — the masked
 // batch alone, no loop code (fewer registers, more waves per SIMD).
-template <typename T, int R, bool ALPHA, int BMODE, int U, int PK, bool SH = false>
+// XV: the device CG's fused u update (SpmvArgs::xu/un/xacc/cg; BMODE 0,
+// ALPHA false): x.get(j) = r[j] + β*u_old[j] on the fly, and the waves of the
+// main structure (no rowmap) write u_new and the deferred x update of all
+// their rows (whoever computes the row's product); once the solve is done a
+// wave only applies a pending x update.
+template <typename T, int R, bool ALPHA, int BMODE, int U, int PK, bool SH = false, bool XV = false>
 __device__ __forceinline__ void spmv_wave(const SpmvArgs<T>& a, const int64_t w) {
   constexpr bool PAT = PK == 1 || PK == 2;  // implied columns (mask of regular rows)
   constexpr int H = 64 * R;
   const int lane = threadIdx.x & 63;
   const int64_t s = a.list ? (int64_t)a.list[w] : w;
+  // the lane's first row: quad-sorted layout (qmap) or identity
+  const int64_t row0 = a.qmap ? (int64_t)a.qmap[s * 64 + lane] : s * H + (int64_t)lane * R;
+  XSrc<T, XV> xs;
+  bool xpend = false, main_rows = false;
+  typename wide_of<T>::type xalpha{};
+  if constexpr (XV) {
+    const CGState* cg = (const CGState*)a.cg;
+    xpend = cg->it > cg->xit;
+    xalpha = cg_alpha_of<typename wide_of<T>::type>(cg);
+    xs.r = (const T*)a.x;
+    xs.u = (const T*)a.xu;
+    xs.b = (cg->res * cg->res) / (cg->prev * cg->prev);
+    main_rows = a.rowmap == nullptr;
+    if (cg->done) {  // nothing left but a pending x .+= α.*u_old
+      if (xpend && main_rows) cg_rows_update<T, R, false>(a, xs, row0, xalpha);
+      return;
+    }
+  } else {
+    xs.x = (const T*)a.x;
+  }
   const int64_t off = a.soff[s];
   const int len = a.slen[s];
-  const int64_t row0 = s * H + (int64_t)lane * R;
   bool ok[R];
   if (PAT) {
     const uint64_t m = a.mask[s * (H / 64) + (lane * R) / 64];
@@ -598,48 +793,61 @@ __device__ __forceinline__ void spmv_wave(const SpmvArgs<T>& a, const int64_t w)
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     const int32_t* pat = wp + (int)a.psel[s * 64 + lane] * a.kmax;
     if (a.flags & SPMV_XPAIR) {
-      if (a.flags & SPMV_NT) rows_pattern<T, R, ALPHA, true, U, true, SH>(acc, pat, vp, len, a.x, row0, ok, a.alpha, pf, tb);
-      else rows_pattern<T, R, ALPHA, false, U, true, SH>(acc, pat, vp, len, a.x, row0, ok, a.alpha, pf, tb);
+      if (a.flags & SPMV_NT) rows_pattern<T, R, ALPHA, true, U, true, SH>(acc, pat, vp, len, xs, row0, ok, a.alpha, pf, tb);
+      else rows_pattern<T, R, ALPHA, false, U, true, SH>(acc, pat, vp, len, xs, row0, ok, a.alpha, pf, tb);
     } else {
-      if (a.flags & SPMV_NT) rows_pattern<T, R, ALPHA, true, U, false, SH>(acc, pat, vp, len, a.x, row0, ok, a.alpha, pf, tb);
-      else rows_pattern<T, R, ALPHA, false, U, false, SH>(acc, pat, vp, len, a.x, row0, ok, a.alpha, pf, tb);
+      if (a.flags & SPMV_NT) rows_pattern<T, R, ALPHA, true, U, false, SH>(acc, pat, vp, len, xs, row0, ok, a.alpha, pf, tb);
+      else rows_pattern<T, R, ALPHA, false, U, false, SH>(acc, pat, vp, len, xs, row0, ok, a.alpha, pf, tb);
     }
   } else if constexpr (PK == 1) {
     const int32_t* pat = a.pat + s * a.kmax;
     bool tri = false;
-    if constexpr (!SH && sizeof(Pack<T, R>) == 16)
-      tri = (a.flags & SPMV_XPAIR) && (a.flags & SPMV_XTRI) && a.ptri && a.ptri[s];
+    if constexpr (!SH && !XV && sizeof(Pack<T, R>) == 16)
+      tri = (a.flags & SPMV_XPAIR) && (a.flags & SPMV_XTRI) && a.ptri && a.ptri[s] && !a.qmap;
     if (tri) {
-      if constexpr (!SH && sizeof(Pack<T, R>) == 16) {
+      if constexpr (!SH && !XV && sizeof(Pack<T, R>) == 16) {
         if (a.flags & SPMV_NT) rows_pattern3<T, R, ALPHA, true>(acc, pat, vp, len, a.x, row0, s * H, a.nx, a.alpha, pf);
         else rows_pattern3<T, R, ALPHA, false>(acc, pat, vp, len, a.x, row0, s * H, a.nx, a.alpha, pf);
       }
     } else if (a.flags & SPMV_XPAIR) {
-      if (a.flags & SPMV_NT) rows_pattern<T, R, ALPHA, true, U, true, SH>(acc, pat, vp, len, a.x, row0, ok, a.alpha, pf, tb);
-      else rows_pattern<T, R, ALPHA, false, U, true, SH>(acc, pat, vp, len, a.x, row0, ok, a.alpha, pf, tb);
+      if (a.flags & SPMV_NT) rows_pattern<T, R, ALPHA, true, U, true, SH>(acc, pat, vp, len, xs, row0, ok, a.alpha, pf, tb);
+      else rows_pattern<T, R, ALPHA, false, U, true, SH>(acc, pat, vp, len, xs, row0, ok, a.alpha, pf, tb);
     } else {
-      if (a.flags & SPMV_NT) rows_pattern<T, R, ALPHA, true, U, false, SH>(acc, pat, vp, len, a.x, row0, ok, a.alpha, pf, tb);
-      else rows_pattern<T, R, ALPHA, false, U, false, SH>(acc, pat, vp, len, a.x, row0, ok, a.alpha, pf, tb);
+      if (a.flags & SPMV_NT) rows_pattern<T, R, ALPHA, true, U, false, SH>(acc, pat, vp, len, xs, row0, ok, a.alpha, pf, tb);
+      else rows_pattern<T, R, ALPHA, false, U, false, SH>(acc, pat, vp, len, xs, row0, ok, a.alpha, pf, tb);
     }
+  } else if constexpr (PK == 4) {
+    const int32_t* __restrict__ cp = (const int32_t*)a.col + off / R + lane;
+    if (a.flags & SPMV_NT) rows_qrun<T, R, ALPHA, true, U, SH>(acc, cp, vp, len, xs, a.alpha, pf, tb);
+    else rows_qrun<T, R, ALPHA, false, U, SH>(acc, cp, vp, len, xs, a.alpha, pf, tb);
   } else if constexpr (PK == 3) {
     const S16Pack<R>* __restrict__ cp = reinterpret_cast<const S16Pack<R>*>(a.col16 + off) + lane;
     const int32_t gb = a.gbase[s];
     const bool xrun = (a.flags & SPMV_XRUN) != 0;
-    if (a.flags & SPMV_NT) rows_d16<T, R, ALPHA, true, U, SH>(acc, cp, vp, len, a.x, a.alpha, pf, tb, (int32_t)row0, gb, xrun);
-    else rows_d16<T, R, ALPHA, false, U, SH>(acc, cp, vp, len, a.x, a.alpha, pf, tb, (int32_t)row0, gb, xrun);
+    if (a.flags & SPMV_NT) rows_d16<T, R, ALPHA, true, U, SH>(acc, cp, vp, len, xs, a.alpha, pf, tb, (int32_t)row0, gb, xrun);
+    else rows_d16<T, R, ALPHA, false, U, SH>(acc, cp, vp, len, xs, a.alpha, pf, tb, (int32_t)row0, gb, xrun);
   } else {
     const IPack<R>* __restrict__ cp = reinterpret_cast<const IPack<R>*>(a.col + off) + lane;
     const bool xrun = (a.flags & SPMV_XRUN) != 0;
-    if (a.flags & SPMV_NT) rows_int32<T, R, ALPHA, true, U, SH>(acc, cp, vp, len, a.x, a.alpha, pf, tb, xrun);
-    else rows_int32<T, R, ALPHA, false, U, SH>(acc, cp, vp, len, a.x, a.alpha, pf, tb, xrun);
+    if (a.flags & SPMV_NT) rows_int32<T, R, ALPHA, true, U, SH>(acc, cp, vp, len, xs, a.alpha, pf, tb, xrun);
+    else rows_int32<T, R, ALPHA, false, U, SH>(acc, cp, vp, len, xs, a.alpha, pf, tb, xrun);
   }
 
+  // XV: u_new (and the deferred x update) of the main structure's rows
+  T un[R];
+  if constexpr (XV) {
+    if (main_rows) cg_rows_update<T, R, true>(a, xs, row0, xalpha, xpend, un);
+  }
   if (a.dotp) {  // fused dot(u, c): Σ conj(u_i)·c_i over this slice's rows
     using DA = typename DAcc<T>::type;
     DA part = zero_of<DA>();
 #pragma unroll
-    for (int r = 0; r < R; ++r)
-      if (ok[r]) part = part + dacc(cdot(a.dotu[orow[r]], acc[r]));
+    for (int r = 0; r < R; ++r) {
+      T uv;
+      if constexpr (XV) uv = main_rows ? un[r] : xs.get(orow[r]);
+      else uv = a.dotu[orow[r]];
+      if (ok[r]) part = part + dacc(cdot(uv, acc[r]));
+    }
 #pragma unroll
     for (int d = 32; d >= 1; d >>= 1) part = part + shfl_down_acc(part, d);
     if (lane == 0) reinterpret_cast<DA*>(a.dotp)[a.dot_base + s] = part;
@@ -670,12 +878,12 @@ __device__ __forceinline__ void spmv_wave(const SpmvArgs<T>& a, const int64_t w)
   }
 }
 
-template <typename T, int R, bool ALPHA, int BMODE, int U, int PK, bool SH = false>
+template <typename T, int R, bool ALPHA, int BMODE, int U, int PK, bool SH = false, bool XV = false>
 __global__ __launch_bounds__(256) void k_spmv_sell(SpmvArgs<T> a) {
   const int64_t blk = (a.flags & SPMV_XCD) ? xcd_remap(blockIdx.x, gridDim.x) : (int64_t)blockIdx.x;
   const int64_t w = blk * 4 + (threadIdx.x >> 6);
   if (w >= a.nwork) return;
-  spmv_wave<T, R, ALPHA, BMODE, U, PK, SH>(a, w);
+  spmv_wave<T, R, ALPHA, BMODE, U, PK, SH, XV>(a, w);
 }
 
 // Several parts of one device in ONE launch (parts sharing a stream pair):
@@ -690,7 +898,7 @@ struct SpmvGroup {
   SpmvArgs<T> a[PA_GROUP_MAX];
 };
 
-template <typename T, int R, bool ALPHA, int BMODE, int U, int PK, bool SH = false>
+template <typename T, int R, bool ALPHA, int BMODE, int U, int PK, bool SH = false, bool XV = false>
 __global__ __launch_bounds__(256) void k_spmv_sell_group(const SpmvGroup<T> g) {
   // wave-uniform: the part's arguments are read with scalar loads
   const int64_t w = (int64_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
@@ -698,7 +906,7 @@ __global__ __launch_bounds__(256) void k_spmv_sell_group(const SpmvGroup<T> g) {
   int p = 0;
   while (p + 1 < g.np && w >= g.start[p + 1]) ++p;
   p = __builtin_amdgcn_readfirstlane(p);
-  spmv_wave<T, R, ALPHA, BMODE, U, PK, SH>(g.a[p], w - g.start[p]);
+  spmv_wave<T, R, ALPHA, BMODE, U, PK, SH, XV>(g.a[p], w - g.start[p]);
 }
 
 template <typename T, int R, bool ALPHA, int BMODE, int PAT>
@@ -707,6 +915,15 @@ static void launch_group_t(const SpmvGroup<T>& g, hipStream_t st) {
   if (blocks == 0) return;
   bool sh = PAT != 2 && (g_spmv_flags & SPMV_SHORT);
   for (int i = 0; i < g.np; ++i) sh = sh && g.a[i].maxlen <= 8;
+  if constexpr (!ALPHA && BMODE == 0) {
+    if (g.a[0].cg) {  // the device CG's fused u update
+      if (sh)
+        hipLaunchKernelGGL((k_spmv_sell_group<T, R, false, 0, 8, PAT, true, true>), dim3(blocks), dim3(256), 0, st, g);
+      else
+        hipLaunchKernelGGL((k_spmv_sell_group<T, R, false, 0, 8, PAT, false, true>), dim3(blocks), dim3(256), 0, st, g);
+      return;
+    }
+  }
   if (sh)
     hipLaunchKernelGGL((k_spmv_sell_group<T, R, ALPHA, BMODE, 8, PAT, true>), dim3(blocks), dim3(256), g_spmv_lds, st, g);
   else if (g_spmv_unroll == 4)
@@ -732,6 +949,15 @@ template <typename T, int R, bool ALPHA, int BMODE, int PAT>
 static void launch_t(const SpmvArgs<T>& a, hipStream_t st) {
   const int64_t blocks = (a.nwork + 3) / 4;
   if (blocks == 0) return;
+  if constexpr (!ALPHA && BMODE == 0) {
+    if (a.cg) {  // the device CG's fused u update
+      if (PAT != 2 && (g_spmv_flags & SPMV_SHORT) && a.maxlen <= 8)
+        hipLaunchKernelGGL((k_spmv_sell<T, R, false, 0, 8, PAT, true, true>), dim3(blocks), dim3(256), 0, st, a);
+      else
+        hipLaunchKernelGGL((k_spmv_sell<T, R, false, 0, 8, PAT, false, true>), dim3(blocks), dim3(256), 0, st, a);
+      return;
+    }
+  }
   if (PAT != 2 && (g_spmv_flags & SPMV_SHORT) && a.maxlen <= 8)
     hipLaunchKernelGGL((k_spmv_sell<T, R, ALPHA, BMODE, 8, PAT, true>), dim3(blocks), dim3(256), g_spmv_lds, st, a);
   else if (g_spmv_unroll == 4)
@@ -755,12 +981,19 @@ static void launch_ab(const SpmvArgs<T>& a, bool has_alpha, int bmode, hipStream
 
 // which = 0: pattern slices of the main structure; 1: int32-column slices
 // of the main structure; 2: side SELL; 3: multi-pattern slices of the main
-// structure; 4: delta16 slices of the main structure.  list/nwork select the
-// slices.
+// structure; 4: delta16 slices of the main structure; 5: quad-run slices of
+// the main structure.  list/nwork select the slices.
 template <typename T>
 static SpmvArgs<T> make_args(int which, int64_t nwork, const int32_t* list, const pa_mat* A, const void* x,
-                             void* y, const int32_t* ymap, const void* alpha, const void* beta, void* dotp) {
+                             void* y, const int32_t* ymap, const void* alpha, const void* beta, void* dotp,
+                             const SpmvPart* cgp = nullptr) {
   SpmvArgs<T> a{};
+  if (cgp && cgp->cg) {
+    a.xu = (decltype(a.xu))((const T*)cgp->xu);
+    a.un = (decltype(a.un))((T*)cgp->un);
+    a.xacc = (decltype(a.xacc))((T*)cgp->xacc);
+    a.cg = (decltype(a.cg))(cgp->cg);
+  }
   a.dotu = (decltype(a.dotu))((const T*)x);
   a.dotp = dotp;
   a.dot_base = which == 2 ? A->nslices : 0;
@@ -777,6 +1010,7 @@ static SpmvArgs<T> make_args(int which, int64_t nwork, const int32_t* list, cons
              : which == 2 ? A->maxlen_side
              : which == 1 ? ((g_spmv_format == 1 && A->has_pat) ? A->maxlen_pm_int : A->maxlen_all)
              : which == 4 ? A->maxlen_d16
+             : which == 5 ? A->maxlen_qrun
                           : INT32_MAX;
   if (which == 2) {
     a.soff = (decltype(a.soff))(A->d_s_off);
@@ -790,6 +1024,7 @@ static SpmvArgs<T> make_args(int which, int64_t nwork, const int32_t* list, cons
     a.col = (decltype(a.col))(A->d_col);
     a.val = (decltype(a.val))((const T*)A->d_val);
     a.nrows = A->nrows;
+    a.qmap = (decltype(a.qmap))(A->d_qmap);
     if (which == 0) {
       a.slen = (decltype(a.slen))(A->d_plen);
       a.pat = (decltype(a.pat))(A->d_pat);
@@ -804,6 +1039,7 @@ static SpmvArgs<T> make_args(int which, int64_t nwork, const int32_t* list, cons
       a.psel = (decltype(a.psel))(A->d_psel);
     } else {
       a.slen = (decltype(a.slen))(A->d_slice_len);
+      if (which == 5) a.col = (decltype(a.col))(A->d_qcol);
       if (which == 4) {
         a.col16 = (decltype(a.col16))(A->d_col16);
         a.gbase = (decltype(a.gbase))(A->d_gbase);
@@ -820,11 +1056,12 @@ static SpmvArgs<T> make_args(int which, int64_t nwork, const int32_t* list, cons
 template <typename T, int R>
 static void launch_which(int which, int64_t nwork, const int32_t* list, const pa_mat* A, const void* x,
                          void* y, const int32_t* ymap, bool has_alpha, int bmode, const void* alpha,
-                         const void* beta, void* dotp, hipStream_t st) {
-  const SpmvArgs<T> a = make_args<T>(which, nwork, list, A, x, y, ymap, alpha, beta, dotp);
+                         const void* beta, void* dotp, hipStream_t st, const SpmvPart* cgp) {
+  const SpmvArgs<T> a = make_args<T>(which, nwork, list, A, x, y, ymap, alpha, beta, dotp, cgp);
   if (which == 0) launch_ab<T, R, 1>(a, has_alpha, bmode, st);
   else if (which == 3) launch_ab<T, R, 2>(a, has_alpha, bmode, st);
   else if (which == 4) launch_ab<T, R, 3>(a, has_alpha, bmode, st);
+  else if (which == 5) launch_ab<T, R, 4>(a, has_alpha, bmode, st);
   else launch_ab<T, R, 0>(a, has_alpha, bmode, st);
 }
 
@@ -838,6 +1075,7 @@ static void group_which(int which, int np, const SpmvPart* parts, bool has_alpha
     if (which == 0) launch_group_ab<T, R, 1>(g, has_alpha, bmode, st);
     else if (which == 3) launch_group_ab<T, R, 2>(g, has_alpha, bmode, st);
     else if (which == 4) launch_group_ab<T, R, 3>(g, has_alpha, bmode, st);
+    else if (which == 5) launch_group_ab<T, R, 4>(g, has_alpha, bmode, st);
     else launch_group_ab<T, R, 0>(g, has_alpha, bmode, st);
     g = SpmvGroup<T>{};
   };
@@ -846,23 +1084,62 @@ static void group_which(int which, int np, const SpmvPart* parts, bool has_alpha
     if (q.nwork <= 0) continue;
     const int32_t* list = q.list;
     if ((g_spmv_flags & SPMV_IDLIST) && list && which != 2 && q.nwork == q.A->nslices) list = nullptr;
-    g.a[g.np] = make_args<T>(which, q.nwork, list, q.A, q.x, q.y, q.ymap, alpha, beta, q.dotp);
+    g.a[g.np] = make_args<T>(which, q.nwork, list, q.A, q.x, q.y, q.ymap, alpha, beta, q.dotp, &q);
     g.start[g.np + 1] = g.start[g.np] + q.nwork;
     if (++g.np == PA_GROUP_MAX) flush();
   }
   flush();
 }
 
+// the per-element-type entry points (one translation unit each, PA_SPMV_DT)
+#define PA_DT_DECL(k)                                                                                          \
+  void spmv_group_##k(int which, int np, const SpmvPart* parts, bool has_alpha, int bmode, const void* alpha,  \
+                      const void* beta, hipStream_t st);                                                        \
+  int spmv_merged_##k(int n, const int* which, const SpmvPart* parts, bool has_alpha, int bmode,              \
+                      const void* alpha, const void* beta, pa_ctx* owner, std::vector<void*>* pinned,         \
+                      hipStream_t st);                                                                          \
+  void spmv_long_##k(const pa_mat* A, const void* x, void* y, const int32_t* ymap, bool has_alpha, int bmode,  \
+                     const void* alpha, const void* beta, void* dotp, int64_t dot_base, hipStream_t st);       \
+  void spmv_part_##k(int which, int64_t nwork, const int32_t* list, const pa_mat* A, const void* x, void* y,  \
+                     const int32_t* ymap, bool has_alpha, int bmode, const void* alpha, const void* beta,     \
+                     void* dotp, hipStream_t st, const SpmvPart* cgp);
+PA_DT_DECL(0)
+PA_DT_DECL(1)
+PA_DT_DECL(2)
+PA_DT_DECL(3)
+#undef PA_DT_DECL
+#if defined(PA_SPMV_DT)
+#if PA_SPMV_DT == 0
+using DtT = float;
+constexpr int kDtR = 4;
+#elif PA_SPMV_DT == 1
+using DtT = double;
+constexpr int kDtR = 2;
+#elif PA_SPMV_DT == 2
+using DtT = c64;
+constexpr int kDtR = 2;
+#else
+using DtT = c128;
+constexpr int kDtR = 1;
+#endif
+void PA_CAT(spmv_group_, PA_SPMV_DT)(int which, int np, const SpmvPart* parts, bool has_alpha, int bmode,
+                                     const void* alpha, const void* beta, hipStream_t st) {
+  group_which<DtT, kDtR>(which, np, parts, has_alpha, bmode, alpha, beta, st);
+}
+#else
 void launch_spmv_group(int which, int np, const SpmvPart* parts, bool has_alpha, int bmode, const void* alpha,
                        const void* beta, hipStream_t st) {
   if (np <= 0) return;
+#define spmv_group_(k) spmv_group_##k(which, np, parts, has_alpha, bmode, alpha, beta, st)
   switch (parts[0].A->dtype) {
-    case PA_F32: group_which<float, 4>(which, np, parts, has_alpha, bmode, alpha, beta, st); break;
-    case PA_F64: group_which<double, 2>(which, np, parts, has_alpha, bmode, alpha, beta, st); break;
-    case PA_C64: group_which<c64, 2>(which, np, parts, has_alpha, bmode, alpha, beta, st); break;
-    case PA_C128: group_which<c128, 1>(which, np, parts, has_alpha, bmode, alpha, beta, st); break;
+    case PA_F32: spmv_group_(0); break;
+    case PA_F64: spmv_group_(1); break;
+    case PA_C64: spmv_group_(2); break;
+    case PA_C128: spmv_group_(3); break;
   }
+#undef spmv_group_
 }
+#endif
 
 // ---------------------------------------------------------------------------
 // Merged launch: every slice kind of every part of the call in ONE launch
@@ -884,7 +1161,7 @@ struct SpmvTable {
   SpmvArgs<T> a[kMergeMax];
 };
 
-template <typename T, int R, bool ALPHA, int BMODE, int U, bool SH>
+template <typename T, int R, bool ALPHA, int BMODE, int U, bool SH, bool XV = false>
 __device__ __forceinline__ void merged_wave(const SpmvTable<T>* __restrict__ tab) {
   // SPMV_XCD: consecutive blocks on one XCD (each XCD sweeps its own row
   // range, so the x window of its waves stays in its L2)
@@ -901,18 +1178,19 @@ __device__ __forceinline__ void merged_wave(const SpmvTable<T>* __restrict__ tab
   const int pk = __builtin_amdgcn_readfirstlane(tab->pk[p]);
   const int64_t lw = w - tab->start[p];
   const SpmvArgs<T>& a = tab->a[p];
-  if (pk == 1) spmv_wave<T, R, ALPHA, BMODE, U, 1, SH>(a, lw);
-  else if (pk == 3) spmv_wave<T, R, ALPHA, BMODE, U, 3, SH>(a, lw);
-  else if (pk == 0) spmv_wave<T, R, ALPHA, BMODE, U, 0, SH>(a, lw);
-  else if constexpr (!SH) spmv_wave<T, R, ALPHA, BMODE, U, 2, false>(a, lw);
+  if (pk == 1) spmv_wave<T, R, ALPHA, BMODE, U, 1, SH, XV>(a, lw);
+  else if (pk == 3) spmv_wave<T, R, ALPHA, BMODE, U, 3, SH, XV>(a, lw);
+  else if (pk == 0) spmv_wave<T, R, ALPHA, BMODE, U, 0, SH, XV>(a, lw);
+  else if (pk == 4) spmv_wave<T, R, ALPHA, BMODE, U, 4, SH, XV>(a, lw);
+  else if constexpr (!SH) spmv_wave<T, R, ALPHA, BMODE, U, 2, false, XV>(a, lw);
 }
 
 // No occupancy cap: amdgpu_waves_per_eu(4) (F32 134 -> 128 VGPRs, a small
 // spill) lost in a same-box A/B: C5 F32 +4.5 %, FE27 F64 +0.4 %, F32 +0.6 %
 // (profiles/r02/stream/ab_waves4.txt).
-template <typename T, int R, bool ALPHA, int BMODE, int U, bool SH>
+template <typename T, int R, bool ALPHA, int BMODE, int U, bool SH, bool XV = false>
 __global__ __launch_bounds__(256) void k_spmv_merged(const SpmvTable<T>* __restrict__ tab) {
-  merged_wave<T, R, ALPHA, BMODE, U, SH>(tab);
+  merged_wave<T, R, ALPHA, BMODE, U, SH, XV>(tab);
 }
 
 // F64 short rows (FD7): 5 waves per SIMD instead of 4 (96 VGPRs instead of
@@ -939,7 +1217,7 @@ static void launch_merged_t(const SpmvTable<T>* d, int64_t waves, bool sh, hipSt
     hipLaunchKernelGGL((k_spmv_merged<T, R, ALPHA, BMODE, 8, false>), dim3(blocks), dim3(256), g_spmv_lds, st, d);
 }
 
-static int pk_of(int which) { return which == 0 ? 1 : which == 3 ? 2 : which == 4 ? 3 : 0; }
+static int pk_of(int which) { return which == 0 ? 1 : which == 3 ? 2 : which == 4 ? 3 : which == 5 ? 4 : 0; }
 
 template <typename T, int R>
 static int merged_t(int n, const int* which, const SpmvPart* parts, bool has_alpha, int bmode, const void* alpha,
@@ -953,7 +1231,7 @@ static int merged_t(int n, const int* which, const SpmvPart* parts, bool has_alp
     if (h.n == kMergeMax) return 1;
     const int32_t* list = q.list;
     if ((g_spmv_flags & SPMV_IDLIST) && list && which[i] != 2 && q.nwork == q.A->nslices) list = nullptr;
-    h.a[h.n] = make_args<T>(which[i], q.nwork, list, q.A, q.x, q.y, q.ymap, alpha, beta, q.dotp);
+    h.a[h.n] = make_args<T>(which[i], q.nwork, list, q.A, q.x, q.y, q.ymap, alpha, beta, q.dotp, &q);
     h.pk[h.n] = pk_of(which[i]);
     sh = sh && h.pk[h.n] != 2 && h.a[h.n].maxlen <= 8;
     h.start[h.n + 1] = h.start[h.n] + q.nwork;
@@ -991,6 +1269,13 @@ static int merged_t(int n, const int* which, const SpmvPart* parts, bool has_alp
   }
   const SpmvTable<T>* dt = (const SpmvTable<T>*)d;
   const int64_t waves = h.start[h.n];
+  if (h.a[0].cg) {  // the device CG's fused u update (α = 1, β = 0)
+    const int64_t blocks = (waves + 3) / 4;
+    if (blocks == 0) return 0;
+    if (sh) hipLaunchKernelGGL((k_spmv_merged<T, R, false, 0, 8, true, true>), dim3(blocks), dim3(256), 0, st, dt);
+    else hipLaunchKernelGGL((k_spmv_merged<T, R, false, 0, 8, false, true>), dim3(blocks), dim3(256), 0, st, dt);
+    return 0;
+  }
   if (!has_alpha) {
     if (bmode == 0) launch_merged_t<T, R, false, 0>(dt, waves, sh, st);
     else if (bmode == 1) launch_merged_t<T, R, false, 1>(dt, waves, sh, st);
@@ -1005,18 +1290,28 @@ static int merged_t(int n, const int* which, const SpmvPart* parts, bool has_alp
 
 // n (which, part) entries as one launch; returns 1 when they do not fit one
 // table (the caller launches per kind), -1 on an allocation/copy error
+#if defined(PA_SPMV_DT)
+int PA_CAT(spmv_merged_, PA_SPMV_DT)(int n, const int* which, const SpmvPart* parts, bool has_alpha, int bmode,
+                                     const void* alpha, const void* beta, pa_ctx* owner, std::vector<void*>* pinned,
+                                     hipStream_t st) {
+  return merged_t<DtT, kDtR>(n, which, parts, has_alpha, bmode, alpha, beta, owner, pinned, st);
+}
+#else
 int launch_spmv_merged(int n, const int* which, const SpmvPart* parts, bool has_alpha, int bmode,
                        const void* alpha, const void* beta, pa_ctx* owner, std::vector<void*>* pinned,
                        hipStream_t st) {
   if (n <= 0) return 0;
+#define spmv_merged_(k) spmv_merged_##k(n, which, parts, has_alpha, bmode, alpha, beta, owner, pinned, st)
   switch (parts[0].A->dtype) {
-    case PA_F32: return merged_t<float, 4>(n, which, parts, has_alpha, bmode, alpha, beta, owner, pinned, st);
-    case PA_F64: return merged_t<double, 2>(n, which, parts, has_alpha, bmode, alpha, beta, owner, pinned, st);
-    case PA_C64: return merged_t<c64, 2>(n, which, parts, has_alpha, bmode, alpha, beta, owner, pinned, st);
-    case PA_C128: return merged_t<c128, 1>(n, which, parts, has_alpha, bmode, alpha, beta, owner, pinned, st);
+    case PA_F32: return spmv_merged_(0);
+    case PA_F64: return spmv_merged_(1);
+    case PA_C64: return spmv_merged_(2);
+    case PA_C128: return spmv_merged_(3);
   }
+#undef spmv_merged_
   return 0;
 }
+#endif
 
 // ---------------------------------------------------------------------------
 // Long rows (row-length histogram): rows far longer than the
@@ -1159,8 +1454,6 @@ __global__ void k_spmv_long_fold(int64_t nlong, const int32_t* __restrict__ lrow
   }
 }
 
-int g_long_exact = 1;  // pa_tune("long_rows_exact")
-
 template <typename T, bool ALPHA, int BMODE>
 static void long_t(const pa_mat* A, const void* x, void* y, const int32_t* ymap, const void* alpha, const void* beta,
                    void* dotp, int64_t dot_base, hipStream_t st) {
@@ -1193,35 +1486,50 @@ static void long_ab(const pa_mat* A, const void* x, void* y, const int32_t* ymap
 }
 
 // dotp: partial of long row w at dotp[dot_base + w] (the fused CG dot)
+#if defined(PA_SPMV_DT)
+void PA_CAT(spmv_long_, PA_SPMV_DT)(const pa_mat* A, const void* x, void* y, const int32_t* ymap, bool has_alpha,
+                                    int bmode, const void* alpha, const void* beta, void* dotp, int64_t dot_base,
+                                    hipStream_t st) {
+  long_ab<DtT>(A, x, y, ymap, has_alpha, bmode, alpha, beta, dotp, dot_base, st);
+}
+void PA_CAT(spmv_part_, PA_SPMV_DT)(int which, int64_t nwork, const int32_t* list, const pa_mat* A, const void* x,
+                                    void* y, const int32_t* ymap, bool has_alpha, int bmode, const void* alpha,
+                                    const void* beta, void* dotp, hipStream_t st, const SpmvPart* cgp) {
+  launch_which<DtT, kDtR>(which, nwork, list, A, x, y, ymap, has_alpha, bmode, alpha, beta, dotp, st, cgp);
+}
+#else
+// dotp: partial of long row w at dotp[dot_base + w] (the fused CG dot)
 void launch_spmv_long(const pa_mat* A, const void* x, void* y, const int32_t* ymap, bool has_alpha, int bmode,
                       const void* alpha, const void* beta, void* dotp, int64_t dot_base, hipStream_t st) {
   if (A->n_long <= 0) return;
+#define spmv_long_(k) spmv_long_##k(A, x, y, ymap, has_alpha, bmode, alpha, beta, dotp, dot_base, st)
   switch (A->dtype) {
-    case PA_F32: long_ab<float>(A, x, y, ymap, has_alpha, bmode, alpha, beta, dotp, dot_base, st); break;
-    case PA_F64: long_ab<double>(A, x, y, ymap, has_alpha, bmode, alpha, beta, dotp, dot_base, st); break;
-    case PA_C64: long_ab<c64>(A, x, y, ymap, has_alpha, bmode, alpha, beta, dotp, dot_base, st); break;
-    case PA_C128: long_ab<c128>(A, x, y, ymap, has_alpha, bmode, alpha, beta, dotp, dot_base, st); break;
+    case PA_F32: spmv_long_(0); break;
+    case PA_F64: spmv_long_(1); break;
+    case PA_C64: spmv_long_(2); break;
+    case PA_C128: spmv_long_(3); break;
   }
+#undef spmv_long_
 }
 
 void launch_spmv_part(int which, int64_t nwork, const int32_t* list, const pa_mat* A, const void* x,
                       void* y, const int32_t* ymap, bool has_alpha, int bmode, const void* alpha,
-                      const void* beta, void* dotp, hipStream_t st) {
+                      const void* beta, void* dotp, hipStream_t st, const SpmvPart* cgp) {
   // a slice list as long as the structure is 0..nslices-1 (lists are
   // ascending subsets): launch without it, one dependent load less per wave
   if ((g_spmv_flags & SPMV_IDLIST) && list && which != 2 && nwork == A->nslices) list = nullptr;
+#define spmv_part_(k) spmv_part_##k(which, nwork, list, A, x, y, ymap, has_alpha, bmode, alpha, beta, dotp, st, cgp)
   switch (A->dtype) {
-    case PA_F32: launch_which<float, 4>(which, nwork, list, A, x, y, ymap, has_alpha, bmode, alpha, beta, dotp, st); break;
-    case PA_F64: launch_which<double, 2>(which, nwork, list, A, x, y, ymap, has_alpha, bmode, alpha, beta, dotp, st); break;
-    case PA_C64: launch_which<c64, 2>(which, nwork, list, A, x, y, ymap, has_alpha, bmode, alpha, beta, dotp, st); break;
-    case PA_C128: launch_which<c128, 1>(which, nwork, list, A, x, y, ymap, has_alpha, bmode, alpha, beta, dotp, st); break;
+    case PA_F32: spmv_part_(0); break;
+    case PA_F64: spmv_part_(1); break;
+    case PA_C64: spmv_part_(2); break;
+    case PA_C128: spmv_part_(3); break;
   }
+#undef spmv_part_
 }
+#endif
 
-// α of the device CG state in the wide type W (Float64 / ComplexF64)
-template <typename W> __device__ inline W cg_alpha_of(const CGState* st);
-template <> __device__ inline double cg_alpha_of<double>(const CGState* st) { return st->alpha.re; }
-template <> __device__ inline c128 cg_alpha_of<c128>(const CGState* st) { return st->alpha; }
+#if PA_DT_DEFINE  // ---- everything below: the dispatcher translation unit only
 
 // x .+= α.*u; r .-= α.*c (all lids, Interfaces.jl:1710-1737) and the owned
 // Σ|r|² of norm(r) (1767-1772) in one pass (contiguous owned lids
@@ -1478,6 +1786,41 @@ static void cg_xu_t(int64_t n, void* x, void* u, const void* r, const CGState* s
   else hipLaunchKernelGGL((k_cg_xu<T, 1>), dim3(nb), dim3(256), 0, s, n, (T*)x, (T*)u, (const T*)r, st);
 }
 
+// The fused CG's ghost lids [lo, hi) (after the halo of r): u_new = r .+
+// β.*u_old (while the solve runs) and the deferred x .+= α.*u_old (while
+// it > xit) — k_cg_xu's arithmetic on the lids the SpMV waves do not own.
+template <typename T>
+__global__ __launch_bounds__(256) void k_cg_ghost(int64_t lo, int64_t hi, const T* __restrict__ r,
+                                                  const T* __restrict__ uo, T* __restrict__ un, T* __restrict__ x,
+                                                  const CGState* __restrict__ st) {
+  using W = typename wide_of<T>::type;
+  const bool xpend = st->it > st->xit;
+  const bool upd = !st->done;
+  if (!xpend && !upd) return;
+  const W a = cg_alpha_of<W>(st);
+  const double b = (st->res * st->res) / (st->prev * st->prev);
+  for (int64_t i = lo + blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < hi; i += (int64_t)gridDim.x * blockDim.x) {
+    const T ui = uo[i];
+    if (upd) un[i] = narrow<T>(widen(r[i]) + rscale(b, widen(ui)));
+    if (xpend) x[i] = narrow<T>(widen(x[i]) + a * widen(ui));
+  }
+}
+
+void launch_cg_ghost(int dtype, int64_t lo, int64_t hi, const void* r, const void* uo, void* un, void* x,
+                     const CGState* st, hipStream_t s) {
+  if (hi <= lo) return;
+  const int nb = (int)std::min<int64_t>(1024, (hi - lo + 255) / 256);
+#define PA_CGG(T) hipLaunchKernelGGL(k_cg_ghost<T>, dim3(nb), dim3(256), 0, s, lo, hi, (const T*)r, (const T*)uo, \
+                                     (T*)un, (T*)x, st)
+  switch (dtype) {
+    case PA_F32: PA_CGG(float); break;
+    case PA_F64: PA_CGG(double); break;
+    case PA_C64: PA_CGG(c64); break;
+    case PA_C128: PA_CGG(c128); break;
+  }
+#undef PA_CGG
+}
+
 void launch_cg_xu(int dtype, int64_t n, void* x, void* u, const void* r, const CGState* st, hipStream_t s) {
   switch (dtype) {
     case PA_F32: cg_xu_t<float>(n, x, u, r, st, s); break;
@@ -1561,11 +1904,16 @@ __global__ __launch_bounds__(256) void k_pattern_detect(int64_t nrows, int64_t n
                                                         int32_t* __restrict__ pghost,
                                                         int32_t* __restrict__ nirreg,
                                                         int32_t* __restrict__ mpat,
-                                                        uint8_t* __restrict__ psel) {
+                                                        uint8_t* __restrict__ psel,
+                                                        const int32_t* __restrict__ qmap) {
   constexpr int H = 64 * R;
   const int lane = threadIdx.x & 63;
   const int64_t s = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (s >= nslices) return;
+  // the oid of the row at (lane, r) of this slice (quad-sorted or identity)
+  auto oid = [&](int ln, int r) -> int64_t {
+    return qmap ? (int64_t)qmap[s * 64 + ln] + r : s * H + (int64_t)ln * R + r;
+  };
   const int64_t off = soff[s];
   const int L = slen[s];
   const int64_t rem = nrows - s * H;
@@ -1601,11 +1949,11 @@ __global__ __launch_bounds__(256) void k_pattern_detect(int64_t nrows, int64_t n
   }
   // rows of this lane regular for candidate (clane, cr): bit r; g = reads a ghost
   auto follow = [&](int clane, int cr, bool& g) -> unsigned {
-    const int64_t crow = s * H + clane * R + cr;
+    const int64_t crow = oid(clane, cr);
     unsigned bits = 0;
 #pragma unroll
     for (int r = 0; r < R; ++r) {
-      const int64_t row = s * H + lane * R + r;
+      const int64_t row = oid(lane, r);
       bool reg = Lp > 0 && rlen[r] == Lp;
       bool gr = false;
       for (int k = 0; k < Lp; ++k) {
@@ -1628,7 +1976,7 @@ __global__ __launch_bounds__(256) void k_pattern_detect(int64_t nrows, int64_t n
     return t;
   };
   auto store_pat = [&](int32_t* dst, int clane, int cr) {
-    const int64_t crow = s * H + clane * R + cr;
+    const int64_t crow = oid(clane, cr);
     for (int k = lane; k < Lp; k += 64)
       dst[k] = col[off + ((int64_t)k * 64 + clane) * R + cr] - (int32_t)crow;
   };
@@ -1717,7 +2065,8 @@ __global__ __launch_bounds__(256) void k_delta16(int64_t nslices, const int64_t*
                                                  const int32_t* __restrict__ slen, const int32_t* __restrict__ col,
                                                  const int32_t* __restrict__ kind, const int32_t* __restrict__ sflags,
                                                  int64_t noids, uint16_t* __restrict__ col16,
-                                                 int32_t* __restrict__ gbase, int32_t* __restrict__ ok) {
+                                                 int32_t* __restrict__ gbase, int32_t* __restrict__ ok,
+                                                 const int32_t* __restrict__ qmap) {
   constexpr int H = 64 * R;
   const int64_t s = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (s >= nslices) return;
@@ -1728,7 +2077,7 @@ __global__ __launch_bounds__(256) void k_delta16(int64_t nslices, const int64_t*
   }
   const int64_t off = soff[s];
   const int len = slen[s];
-  const int64_t row0 = s * H + (int64_t)lane * R;
+  const int64_t row0 = qmap ? (int64_t)qmap[s * 64 + lane] : s * H + (int64_t)lane * R;
   int32_t gmin = INT32_MAX;
   for (int k = 0; k < len; ++k)
 #pragma unroll
@@ -1771,7 +2120,7 @@ void launch_delta16(pa_mat* A, int64_t noids, const int32_t* kind, int32_t* ok, 
   if (blocks == 0) return;
 #define PA_D16(RR)                                                                                          \
   hipLaunchKernelGGL(k_delta16<RR>, dim3(blocks), dim3(256), 0, st, A->nslices, A->d_slice_off,              \
-                     A->d_slice_len, A->d_col, kind, A->d_sflags, noids, A->d_col16, A->d_gbase, ok)
+                     A->d_slice_len, A->d_col, kind, A->d_sflags, noids, A->d_col16, A->d_gbase, ok, A->d_qmap)
   switch (A->R) {
     case 1: PA_D16(1); break;
     case 2: PA_D16(2); break;
@@ -1788,13 +2137,203 @@ void launch_pattern_detect(pa_mat* A, int64_t noids, int32_t* kind, int32_t* ple
 #define PA_DET(RR)                                                                                      \
   hipLaunchKernelGGL(k_pattern_detect<RR>, dim3(blocks), dim3(256), 0, st, A->nrows, A->nslices,        \
                      A->d_slice_off, A->d_slice_len, A->d_col, noids, A->kmax, S, NP, A->kmp, rule, kind, plen, \
-                     pat, mask, pghost, nirreg, A->d_mpat, A->d_psel)
+                     pat, mask, pghost, nirreg, A->d_mpat, A->d_psel, A->d_qmap)
   switch (A->R) {
     case 1: PA_DET(1); break;
     case 2: PA_DET(2); break;
     case 4: PA_DET(4); break;
   }
 #undef PA_DET
+}
+
+// ---------------------------------------------------------------------------
+// Quad sort (irregular partitions, pa_tune "spmv_quadsort"): the lanes of the
+// int32 layout — quads of R consecutive owned rows — are reordered so that
+// lanes of one class share slices: lanes whose R rows read R consecutive
+// columns at every entry (quad-run lanes; among them those with equal column
+// offsets together, which become pattern slices), lanes reading ghosts, and
+// the rest.  Each row keeps its entries in the reference's order; only the
+// slice-lane that holds it changes (qmap).
+
+// Per quad q of the identity layout (slice q/64, lane q%64, rows q*R..):
+// qlen = its longest row; qflag bit 0: every row has the same length and
+// reads the first row's columns + r at every entry, bit 1: a ghost column;
+// qhash: FNV-1a of the first row's column offsets (col - row).
+template <int R>
+__global__ void k_quad_class(int64_t nrows, int64_t nquads, const int64_t* __restrict__ soff,
+                             const int32_t* __restrict__ slen, const int32_t* __restrict__ col, int64_t noids,
+                             int32_t* __restrict__ qlen, uint8_t* __restrict__ qflag, uint64_t* __restrict__ qhash) {
+  const int64_t q = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (q >= nquads) return;
+  const int64_t s = q / 64;
+  const int lane = (int)(q % 64);
+  const int64_t off = soff[s];
+  const int L = slen[s];
+  const int64_t row0 = q * R;
+  bool run = row0 + R <= nrows, ghost = false;
+  int lmax = 0, len0 = -1;
+  uint64_t h = 1469598103934665603ull;
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    int l = 0;
+    for (int k = 0; k < L; ++k) {
+      const int32_t c = col[off + ((int64_t)k * 64 + lane) * R + r];
+      if (c < 0) break;
+      ++l;
+      if (c >= noids) ghost = true;
+      if (r == 0) h = (h ^ (uint64_t)(uint32_t)(c - (int32_t)row0)) * 1099511628211ull;
+      else if (c != col[off + ((int64_t)k * 64 + lane) * R] + r) run = false;
+    }
+    if (r == 0) len0 = l;
+    else if (l != len0) run = false;
+    lmax = l > lmax ? l : lmax;
+  }
+  qlen[q] = lmax;
+  qflag[q] = (uint8_t)((run && len0 > 0 ? 1 : 0) | (ghost ? 2 : 0));
+  qhash[q] = h;
+}
+
+// the permuted layout: lane l of new slice s holds old quad perm[s*64+l]
+// (-1: a padding lane); entries past a row's end are padding (-1 / zero)
+template <typename T, int R>
+__global__ void k_quad_permute(int64_t nslots_lanes, const int32_t* __restrict__ perm,
+                               const int64_t* __restrict__ nsoff, const int32_t* __restrict__ nslen,
+                               const int64_t* __restrict__ osoff, const int32_t* __restrict__ oslen,
+                               const int32_t* __restrict__ ocol, const T* __restrict__ oval,
+                               int32_t* __restrict__ ncol, T* __restrict__ nval) {
+  const int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (p >= nslots_lanes) return;
+  const int64_t ns = p / 64;
+  const int nl = (int)(p % 64);
+  const int32_t q = perm[p];
+  const int64_t os = q >= 0 ? q / 64 : 0;
+  const int ol = q >= 0 ? q % 64 : 0;
+  const int olen = q >= 0 ? oslen[os] : 0;
+  for (int k = 0; k < nslen[ns]; ++k)
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const int64_t dst = nsoff[ns] + ((int64_t)k * 64 + nl) * R + r;
+      if (k < olen) {
+        const int64_t src = osoff[os] + ((int64_t)k * 64 + ol) * R + r;
+        ncol[dst] = ocol[src];
+        nval[dst] = oval[src];
+      } else {
+        ncol[dst] = -1;
+        nval[dst] = zero_of<T>();
+      }
+    }
+}
+
+// CSC nz → slot map after the permutation (main slots only; ghost-row and
+// long-row values keep their relative indices)
+__global__ void k_nzslot_remap(int64_t nu, int64_t* __restrict__ nzs, int64_t oslots, int64_t ons,
+                               const int64_t* __restrict__ osoff, int H, int R, const int32_t* __restrict__ inv,
+                               const int64_t* __restrict__ nsoff) {
+  const int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (p >= nu) return;
+  const int64_t t = nzs[p];
+  if (t < 0 || t >= oslots) return;
+  int64_t lo = 0, hi = ons;  // last slice whose offset <= t
+  while (hi - lo > 1) {
+    const int64_t mid = (lo + hi) >> 1;
+    if (osoff[mid] <= t) lo = mid; else hi = mid;
+  }
+  const int64_t rem = t - osoff[lo];
+  const int64_t k = rem / H, w = rem % H;
+  const int l = (int)(w / R), r = (int)(w % R);
+  const int64_t np = inv[lo * 64 + l];
+  nzs[p] = nsoff[np / 64] + (k * 64 + np % 64) * R + r;
+}
+
+// quad-run slices: a kind-0 slice (not pattern, no long rows) whose every
+// lane is a quad-run lane (or padding) becomes kind 4: qcol[off/R + k*64 +
+// lane] = the first row's column (-1: padding)
+template <int R>
+__global__ __launch_bounds__(256) void k_qrun_detect(int64_t nrows, int64_t nslices, const int64_t* __restrict__ soff,
+                                                     const int32_t* __restrict__ slen,
+                                                     const int32_t* __restrict__ col, const int32_t* __restrict__ kind,
+                                                     const int32_t* __restrict__ qmap, int32_t* __restrict__ qcol,
+                                                     int32_t* __restrict__ ok) {
+  const int64_t s = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (s >= nslices) return;
+  const int lane = threadIdx.x & 63;
+  if (kind[s] != 0) {
+    if (lane == 0) ok[s] = 0;
+    return;
+  }
+  const int64_t off = soff[s];
+  const int L = slen[s];
+  const int64_t row0 = qmap[s * 64 + lane];
+  int nv = (int)(nrows - row0 < R ? (nrows - row0 > 0 ? nrows - row0 : 0) : R);  // valid rows of the lane
+  bool run = true;
+  int len0 = 0;
+  for (int k = 0; k < L; ++k) {
+    const int32_t c0 = col[off + ((int64_t)k * 64 + lane) * R];
+    if (c0 >= 0) len0 = k + 1;
+  }
+  for (int r = 1; r < nv; ++r)
+    for (int k = 0; k < L; ++k) {
+      const int32_t c0 = col[off + ((int64_t)k * 64 + lane) * R];
+      const int32_t c = col[off + ((int64_t)k * 64 + lane) * R + r];
+      if (k < len0 ? c != c0 + r : c >= 0) run = false;
+    }
+  for (int k = 0; k < len0; ++k)  // no padding inside the first row
+    if (col[off + ((int64_t)k * 64 + lane) * R] < 0) run = false;
+  const bool all = __all(run);
+  if (lane == 0) ok[s] = all ? 1 : 0;
+  if (!all) return;
+  for (int k = 0; k < L; ++k) qcol[off / R + (int64_t)k * 64 + lane] = col[off + ((int64_t)k * 64 + lane) * R];
+}
+
+void launch_quad_class(const pa_mat* A, int64_t noids, int32_t* qlen, uint8_t* qflag, uint64_t* qhash,
+                       hipStream_t st) {
+  const int64_t nq = (A->nrows + A->R - 1) / A->R;
+  if (nq == 0) return;
+  const dim3 g((unsigned)((nq + 255) / 256)), b(256);
+#define PA_QC(RR) hipLaunchKernelGGL(k_quad_class<RR>, g, b, 0, st, A->nrows, nq, A->d_slice_off, A->d_slice_len, \
+                                     A->d_col, noids, qlen, qflag, qhash)
+  switch (A->R) {
+    case 1: PA_QC(1); break;
+    case 2: PA_QC(2); break;
+    case 4: PA_QC(4); break;
+  }
+#undef PA_QC
+}
+
+void launch_quad_permute(const pa_mat* A, int64_t nslices_new, const int32_t* perm, const int64_t* nsoff,
+                         const int32_t* nslen, const int64_t* osoff, const int32_t* oslen, const int32_t* ocol,
+                         const void* oval, int32_t* ncol, void* nval, hipStream_t st) {
+  const int64_t n = nslices_new * 64;
+  if (n == 0) return;
+  const dim3 g((unsigned)((n + 255) / 256)), b(256);
+#define PA_QP(T, RR) hipLaunchKernelGGL((k_quad_permute<T, RR>), g, b, 0, st, n, perm, nsoff, nslen, osoff, oslen, \
+                                        ocol, (const T*)oval, ncol, (T*)nval)
+  switch (A->dtype) {
+    case PA_F32: PA_QP(float, 4); break;
+    case PA_F64: PA_QP(double, 2); break;
+    case PA_C64: PA_QP(c64, 2); break;
+    case PA_C128: PA_QP(c128, 1); break;
+  }
+#undef PA_QP
+}
+
+void launch_nzslot_remap(int64_t nu, int64_t* nzs, int64_t oslots, int64_t ons, const int64_t* osoff, int H, int R,
+                         const int32_t* inv, const int64_t* nsoff, hipStream_t st) {
+  if (nu == 0) return;
+  hipLaunchKernelGGL(k_nzslot_remap, dim3((unsigned)((nu + 255) / 256)), dim3(256), 0, st, nu, nzs, oslots, ons, osoff,
+                     H, R, inv, nsoff);
+}
+
+void launch_qrun_detect(const pa_mat* A, const int32_t* kind, int32_t* qcol, int32_t* ok, hipStream_t st) {
+  const int64_t blocks = (A->nslices + 3) / 4;
+  if (blocks == 0) return;
+#define PA_QR(RR) hipLaunchKernelGGL(k_qrun_detect<RR>, dim3(blocks), dim3(256), 0, st, A->nrows, A->nslices, \
+                                     A->d_slice_off, A->d_slice_len, A->d_col, kind, A->d_qmap, qcol, ok)
+  switch (A->R) {
+    case 2: PA_QR(2); break;
+    case 4: PA_QR(4); break;
+  }
+#undef PA_QR
 }
 
 // Side SELL: the irregular rows (oids, ascending), copied from the int32 layout.
@@ -1886,5 +2425,7 @@ void launch_side_fill(pa_mat* A, const int32_t* rows, const int32_t* len, hipStr
     case PA_C128: side_fill_t<c128, 1>(A, rows, len, st); break;
   }
 }
+
+#endif  // PA_DT_DEFINE
 
 }  // namespace pa

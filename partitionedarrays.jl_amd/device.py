@@ -90,8 +90,8 @@ class HIPBackend(SequentialBackend):
         be captured, e.g. parts on several devices, stays eager).  Off by
         default.
         rccl: the halo moves by RCCL grouped ncclSend/ncclRecv between the
-        parts of this process (pa_comm_init_all + pa_tune("halo_transport",
-        1)), the MPIBackend transport without processes: one RCCL rank per
+        parts of this process (pa_comm_init_all, which marks these contexts),
+        the MPIBackend transport without processes: one RCCL rank per
         device, parts of one device send to self.  Default: the parts read
         each other's packed buffers."""
         ndev = _lib.device_count()
@@ -127,8 +127,9 @@ class HIPBackend(SequentialBackend):
             if not self.share_streams and len({c.device for c in ctx.values()}) != n:
                 raise _lib.PAError("HIPBackend(rccl=True): parts of one device share one RCCL rank and "
                                    "must share their stream pair (share_streams=True)")
+            # the contexts of this call exchange over RCCL (a per-context flag
+            # set by pa_comm_init_all; other backends of the process are unaffected)
             _lib.call("pa_comm_init_all", n, _lib.ptr_array([ctx[p].h for p in ids.part_ids]))
-            _lib.tune("halo_transport", 1)
         self._sets[n] = self.ctx = ctx
         return ids
 
@@ -496,6 +497,10 @@ class DeviceMatrix:
         dd = C.c_int64()
         _lib.call("pa_mat_delta16_info", self.h, C.byref(dd))
         d["delta16_slices"] = dd.value
+        qr, qs = C.c_int64(), C.c_int()
+        _lib.call("pa_mat_quadrun_info", self.h, C.byref(qr), C.byref(qs))
+        d["quadrun_slices"] = qr.value
+        d["quad_sorted"] = bool(qs.value)
         lr = [C.c_int64() for _ in range(2)]
         _lib.call("pa_mat_long_rows", self.h, *[C.byref(x) for x in lr])
         d.update(zip(["long_rows", "long_nnz"], [x.value for x in lr]))

@@ -138,3 +138,20 @@ def test_coo_assemble_then_sparse_equals_oracle(be, pamd, O):
     for p in parts.part_ids:
         own = rows.partition.local(p).oid_to_lid - 1
         assert np.array_equal(got.local(p)[own], oy.values[p][own]), f"part {p}: mul! differs"
+
+
+def test_coo_assemble_exchanger_missing_owner(be, pamd, O):
+    """A ghost row whose owner the rows exchanger does not list is the
+    reference's KeyError (owner_to_i, Interfaces.jl:2428-2430), not a
+    triplet silently kept local."""
+    parts, oparts, rows, orows, I, J, V, mk = _problem(pamd, O, be, 4, 4000, 2000, np.float64, SEED + 7)
+    coo = pamd.COO.from_host(mk(I), mk(J), mk(V), rows)
+    ctxs = pamd.device.contexts(rows.partition)
+    idx = [pamd.device.device_index_gids(c, rows.partition.local(p)) for c, p in zip(ctxs, parts.part_ids)]
+    xg = [pamd.device.device_exchanger(c, rows.exchanger, p) for c, p in zip(ctxs, parts.part_ids)]
+    ex = rows.exchanger
+    empty = pamd.Table(np.zeros(0, np.int32), np.ones(1, np.int32))
+    xg[0] = pamd.device.DeviceExchanger(ctxs[0], [], empty, ex.parts_snd.local(1), ex.lids_snd.local(1))
+    with pytest.raises(pamd.PAError, match="parts_rcv"):
+        pamd._lib.call("pa_coo_assemble_all", len(ctxs), pamd._lib.ptr_array([c.h for c in coo.values.parts]),
+                       pamd._lib.ptr_array([d.h for d in idx]), pamd._lib.ptr_array([d.h for d in xg]))

@@ -178,3 +178,56 @@ def test_mul_with_equal_copies_of_the_ranges(be, pamd, O):
         own = A.rows.partition.local(p).oid_to_lid - 1
         assert np.array_equal(y.to_host().local(p)[own], oy.values[p][own])
     assert "_eq_cache" in A.cols.__dict__ and any(k[0] == "layout" for k in A.cols._eq_cache)
+
+
+def test_graph_replay_survives_cache_eviction(pamd):
+    """A captured mul! owns its halo tables: eager mul! calls
+    over 20 other x vectors evict the x-pointer array the capture saw from
+    the direct-pull cache (16 entries) and free it; the graph must still
+    replay from its own copy and equal the eager mul! bit for bit."""
+    be = pamd.HIPBackend(devices=[0])
+    parts = be.get_part_ids((2, 2, 2))
+    N = (14, 13, 12)
+    A = pamd.drivers.stencil_operator(parts, N, 27)
+    rng = np.random.default_rng(5)
+    mk = lambda: pamd.PVector.from_host(
+        pamd.map_parts(lambda s: rng.uniform(-1, 1, s.num_lids), A.cols.partition), A.cols)
+    x = mk()
+    y_g, y_e = pamd.PVector.undef(A.rows), pamd.PVector.undef(A.rows)
+    G = pamd.SpMVGraph(y_g, A, x)
+    others = [mk() for _ in range(20)]
+    y_o = pamd.PVector.undef(A.rows)
+    for xo in others:
+        pamd.mul_(y_o, A, xo)
+    G()
+    pamd.mul_(y_e, A, x)
+    g, e = y_g.to_host(), y_e.to_host()
+    for p in parts.part_ids:
+        own = A.rows.partition.local(p).oid_to_lid - 1
+        assert np.array_equal(g.local(p)[own], e.local(p)[own]), f"part {p}: graph replay differs from eager"
+
+
+def test_spmv_rejects_partial_exchanger_arrays(be, pamd):
+    """pa_spmv_all with an exchanger array whose entries are partly null is
+    an error ('exchanger missing'), not a host crash."""
+    import ctypes as C
+    parts = be.get_part_ids((2, 1, 1))
+    A = pamd.drivers.stencil_operator(parts, (8, 6, 5), 7)
+    x = pamd.PVector.from_host(pamd.map_parts(lambda s: np.ones(s.num_lids), A.cols.partition), A.cols)
+    y = pamd.PVector.undef(A.rows)
+    args = list(pamd.pvector._spmv_args(y, A, x, 1.0, 0.0))
+    xg = [pamd.device.device_exchanger(be.context(p), A.cols.exchanger, p) for p in parts.part_ids]
+    args[6] = pamd._lib.ptr_array([xg[0].h, None])
+    with pytest.raises(pamd._lib.PAError, match="exchanger missing"):
+        pamd._lib.call("pa_spmv_all", *args)
+
+
+def test_rccl_backend_leaves_global_transport_knob(pamd):
+    """HIPBackend(rccl=True) marks its own contexts (pa_comm_init_all) instead
+    of switching the process-wide halo_transport knob: a backend
+    made afterwards without RCCL keeps the device-read transport."""
+    before = pamd._lib.tune("halo_transport", 0)
+    pamd._lib.tune("halo_transport", before)
+    pamd.HIPBackend(devices=[0], rccl=True).get_part_ids((2, 1, 1))
+    after = pamd._lib.tune("halo_transport", before)
+    assert after == before

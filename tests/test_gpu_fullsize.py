@@ -2,8 +2,9 @@
 restatement of the reference (oracle/build/spmv_ref, test infrastructure,
 pinned to the Python oracle by tests/test_oracle_c.py):
 
-* C2 — FD7 128³ F64, one part: bit-exact against the literal CSC column loop
-  (SparseUtils.jl:157-187), both column encodings;
+* C2 — FD7 128³ F64 and F32, one part: bit-exact against the literal CSC
+  column loop (SparseUtils.jl:157-187), both column encodings; FE27 128³ in
+  ComplexF64 and 256³ in Float32 likewise (the oracle's typed loops);
 * the bench's headline operator / C4 per GPU — FE27 256³, one part,
   442,840,880 nonzeros: bit-exact, both encodings;
 * C3 — FE27 256³ on Cartesian parts (2,1,1), (2,2,1), (2,2,2) of one device,
@@ -97,31 +98,58 @@ def test_c2_fd7_128_one_part_bitexact(be, pamd, tmp_path, fmt):
     assert info["nnz"] == 14099408  # SURVEY.md §8 size table
 
 
-def test_c2_fd7_128_f32_all_pattern_slices(be, pamd):
-    """F32 slices are 256 rows (two x-lines of 128): the middle row of a slice
-    is an x = 0 boundary row, so the pattern candidate must come from another
-    row (1/4 or 3/4).  Every slice is a pattern slice, and y equals the int32
-    encoding's bit for bit (that encoding is pinned to the oracle at small
-    sizes, test_gpu_parity.py; the C oracle is F64 only)."""
-    n = 128
+def _typed_one_part(be, pamd, tmp_path, kind, n, dtype, seed):
+    """y = A·x of the n³ operator in Float32 / ComplexF64 (one part), device
+    (both encodings) and the C oracle's literal column loop in that type."""
+    rng = np.random.default_rng(seed)
+    if np.dtype(dtype).kind == "c":
+        x_ = (rng.uniform(-1, 1, n ** 3) + 1j * rng.uniform(-1, 1, n ** 3)).astype(dtype)
+    else:
+        x_ = rng.uniform(-1, 1, n ** 3).astype(dtype)
+    x_.tofile(tmp_path / "x.bin")
+    tname = {np.dtype(np.float32): "f32", np.dtype(np.complex128): "c128"}[np.dtype(dtype)]
+    _oracle("--kind", kind, "--n", n, "--dtype", tname, "--xin", tmp_path / "x.bin", "--yout", tmp_path / "y.bin")
+    yref = np.fromfile(tmp_path / "y.bin", dtype=dtype)
     parts = be.get_part_ids((1, 1, 1))
-    x_ = np.random.default_rng(SEED + 3).uniform(-1, 1, n ** 3).astype(np.float32)
-    ys = []
+    infos = {}
     for fmt in (1, 0):
         prev = pamd._lib.tune("spmv_format", fmt)
         try:
-            A = pamd.drivers.stencil_operator(parts, (n,) * 3, 7, np.float32)
+            A = pamd.drivers.stencil_operator(parts, (n,) * 3, kind, dtype)
             x = pamd.PVector.from_host(pamd.map_parts(lambda s: x_, A.cols.partition), A.cols)
-            y = pamd.PVector.undef(A.rows, np.float32)
+            y = pamd.PVector.undef(A.rows, dtype)
             pamd.mul_(y, A, x)
-            ys.append(y.to_host().local(1))
-            if fmt == 1:
-                info = A.values.local(1).info()
-                assert info["pattern_slices"] == info["nslices"] == 8192
+            got = y.to_host().local(1)
+            w = np.int32 if np.dtype(dtype).itemsize == 4 else np.int64
+            bad = np.flatnonzero((got.view(w).reshape(len(got), -1) != yref.view(w).reshape(len(got), -1)).any(axis=1))
+            assert bad.size == 0, f"fmt {fmt}: {bad.size} rows differ from the oracle, first at gid {bad[0] + 1}"
+            infos[fmt] = A.values.local(1).info()
+            del A, x, y
         finally:
             pamd._lib.tune("spmv_format", prev)
-    bad = np.flatnonzero(ys[0] != ys[1])
-    assert bad.size == 0, f"{bad.size} rows differ between the encodings, first at gid {bad[0] + 1}"
+    return infos
+
+
+def test_c2_fd7_128_f32_bitexact(be, pamd, tmp_path):
+    """C2 in Float32 against the C oracle's Float32 column loop
+    (Float32.(A): each value rounded once; SparseUtils.jl:157-187), both
+    encodings.  F32 slices are 256 rows (two x-lines of 128): the middle row
+    of a slice is an x = 0 boundary row, so the pattern candidate must come
+    from another row (1/4 or 3/4): every slice is a pattern slice."""
+    infos = _typed_one_part(be, pamd, tmp_path, 7, 128, np.float32, SEED + 3)
+    assert infos[1]["pattern_slices"] == infos[1]["nslices"] == 8192
+
+
+def test_fe27_128_c128_one_part_bitexact(be, pamd, tmp_path):
+    """ComplexF64 (A + 0im, complex x; Julia's complex product) one part of
+    the 128³ FE27 operator against the C oracle, both encodings."""
+    _typed_one_part(be, pamd, tmp_path, 27, 128, np.complex128, SEED + 4)
+
+
+def test_fe27_256_f32_one_part_bitexact(be, pamd, tmp_path):
+    """the headline operator (FE27 256³, one part) in Float32 against the C
+    oracle, both encodings."""
+    _typed_one_part(be, pamd, tmp_path, 27, 256, np.float32, SEED + 5)
 
 
 @pytest.mark.parametrize("fmt", [1, 0], ids=["pattern", "int32"])

@@ -90,3 +90,67 @@ def test_cg_history_equals_python_oracle(O, ref, tmp_path, kind, shape):
     assert len(hist) == K
     np.testing.assert_allclose(h, hist, rtol=1e-12, atol=0)
     np.testing.assert_allclose(np.fromfile(tmp_path / "x.bin"), _global_from_parts(O, ox, n), rtol=1e-10, atol=1e-12)
+
+
+@pytest.mark.parametrize("kind", [7, 27])
+def test_f32_one_part_equals_python_oracle(O, ref, tmp_path, kind):
+    """--dtype f32 (the Float32 checker of the full-size GPU tests): the
+    literal column loop over Float32.(A) equals the Python oracle's mul! in
+    Float32 bit for bit."""
+    N = 10
+    n = N ** 3
+    x = np.random.default_rng(21 + kind).uniform(-1, 1, n).astype(np.float32)
+    x.tofile(tmp_path / "x.bin")
+    _run(ref, "--kind", kind, "--n", N, "--dtype", "f32", "--xin", tmp_path / "x.bin", "--yout", tmp_path / "y.bin")
+    y = np.fromfile(tmp_path / "y.bin", dtype=np.float32)
+    parts = O.get_part_ids((1, 1, 1))
+    A = O.stencil_problem(parts, (N,) * 3, kind, np.float32)
+    ox = O.PVector(O.map_parts(lambda s: x[np.asarray(s.lid_to_gid) - 1].copy(), A.cols.partition), A.cols)
+    oy = O.pvector_undef(A.rows, np.float32)
+    O.mul_(oy, A, ox)
+    got = np.asarray(oy.values.parts[0])[np.asarray(A.rows.partition.parts[0].oid_to_lid) - 1]
+    order = np.asarray(A.rows.partition.parts[0].lid_to_gid)[np.asarray(A.rows.partition.parts[0].oid_to_lid) - 1] - 1
+    yy = np.empty(n, np.float32)
+    yy[order] = got
+    assert yy.dtype == np.float32 and np.array_equal(yy.view(np.int32), y.view(np.int32))
+
+
+def test_c128_one_part_is_two_real_products(ref, tmp_path):
+    """--dtype c128 over A + 0im (the device stencil's complex operator):
+    Julia's complex product with a zero imaginary part gives y = A·re(x) +
+    i·A·im(x) exactly, so it equals two Float64 runs bit for bit."""
+    N = 11
+    rng = np.random.default_rng(4)
+    xr, xi = rng.uniform(-1, 1, N ** 3), rng.uniform(-1, 1, N ** 3)
+    (xr + 1j * xi).astype(np.complex128).tofile(tmp_path / "xc.bin")
+    _run(ref, "--kind", 27, "--n", N, "--dtype", "c128", "--xin", tmp_path / "xc.bin", "--yout", tmp_path / "yc.bin")
+    yc = np.fromfile(tmp_path / "yc.bin", dtype=np.complex128)
+    for part, xv in (("re", xr), ("im", xi)):
+        xv.tofile(tmp_path / "x.bin")
+        _run(ref, "--kind", 27, "--n", N, "--reps", 1, "--xin", tmp_path / "x.bin", "--yout", tmp_path / "y.bin")
+        y = np.fromfile(tmp_path / "y.bin")
+        assert np.array_equal(getattr(yc, "real" if part == "re" else "imag"), y), part
+
+
+@pytest.mark.parametrize("kind,dims,shape", [(27, (12, 10, 9), (2, 2, 1)), (7, (11, 13, 10), (2, 1, 2)),
+                                             (27, (16, 16, 16), (2, 2, 2)), (27, (18, 9, 9), (2, 1, 1))])
+def test_mpi_baseline_equals_partitioned_and_python(O, ref, tmp_path, kind, dims, shape):
+    """--mpi (bench.py's CPU baseline beside the multi-GPU lines: one rank per
+    part, its own CSC, a halo exchange of x in every mul!) computes exactly
+    the partitioned mul! of the checker, on non-cubic global grids too, and
+    that equals the Python oracle."""
+    n = int(np.prod(dims))
+    x = np.random.default_rng(8).uniform(-1, 1, n)
+    x.tofile(tmp_path / "x.bin")
+    _run(ref, "--kind", kind, "--dims", *dims, "--parts", *shape, "--xin", tmp_path / "x.bin", "--yout",
+         tmp_path / "y1.bin")
+    out = _run(ref, "--kind", kind, "--dims", *dims, "--parts", *shape, "--mpi", "--reps", 3, "--xin",
+               tmp_path / "x.bin", "--yout", tmp_path / "y2.bin")
+    y1, y2 = np.fromfile(tmp_path / "y1.bin"), np.fromfile(tmp_path / "y2.bin")
+    assert np.array_equal(y1, y2), out
+    parts = O.get_part_ids(shape)
+    A = O.stencil_problem(parts, dims, kind)
+    ox = O.PVector(O.map_parts(lambda s: x[np.asarray(s.lid_to_gid) - 1].copy(), A.cols.partition), A.cols)
+    oy = O.pvector_undef(A.rows)
+    O.mul_(oy, A, ox)
+    assert np.array_equal(_global_from_parts(O, oy, n), y1)

@@ -1,0 +1,102 @@
+"""Host-issue cost of one mul! (and one device-CG iteration) on the paths a
+multi-GPU run takes, measured on one MI355X.
+
+The (2,2,2) partition of a 256³ FE27 operator (8 parts of 128³), every part
+on cuda:0:
+  * share_streams=False: a stream pair per part and per-part launches, pack,
+    transport (pull kernels on the comm streams, cross-stream events),
+    interior and boundary phases — the code a process driving 8 GPUs runs;
+  * share_streams=True: the grouped launches of parts sharing one GPU;
+  * rccl: HIPBackend(rccl=True), every halo segment through the grouped
+    ncclSend/ncclRecv, the transport a one-part-per-GPU process posts.
+Host time = wall time of K calls issued back to back with the GPU kept busy
+(enqueue only; the GPU finishes later), both through the Python mirror
+(pamd.mul_) and through the bare C-ABI call with prebuilt argument arrays
+(what a Julia ccall costs).  Prints one JSON object.
+
+    python tools/host_issue.py [--n 256] [--k 40]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import pamd  # noqa: E402
+
+
+def measure(be, n, k, label, cg_iters=0):
+    parts = be.get_part_ids((2, 2, 2))
+    A = pamd.drivers.stencil_operator(parts, (n,) * 3, 27)
+    x = pamd.PVector.from_host(pamd.map_parts(
+        lambda s: np.random.default_rng(s.part).uniform(-1, 1, s.num_lids), A.cols.partition), A.cols)
+    y = pamd.PVector.undef(A.rows)
+    ctxs = [be.context(p) for p in parts.part_ids]
+
+    def sync():
+        for c in ctxs:
+            c.sync()
+    for _ in range(5):
+        pamd.mul_(y, A, x)
+    sync()
+    # device time per mul! (for the ratio)
+    t0 = time.perf_counter()
+    for _ in range(k):
+        pamd.mul_(y, A, x)
+    sync()
+    wall = (time.perf_counter() - t0) / k
+    # Python-level enqueue
+    t0 = time.perf_counter()
+    for _ in range(k):
+        pamd.mul_(y, A, x)
+    host_py = (time.perf_counter() - t0) / k
+    sync()
+    # bare C-ABI enqueue (argument arrays built once)
+    args = pamd.pvector._spmv_args(y, A, x, 1.0, 0.0)
+    t0 = time.perf_counter()
+    for _ in range(k):
+        pamd._lib.call("pa_spmv_all", *args)
+    host_c = (time.perf_counter() - t0) / k
+    sync()
+    out = {"path": label, "parts": 8, "mul_wall_ms": round(1e3 * wall, 4),
+           "host_us_per_mul_python": round(1e6 * host_py, 1), "host_us_per_mul_cabi": round(1e6 * host_c, 1),
+           "host_us_per_part_cabi": round(1e6 * host_c / 8, 1)}
+    if cg_iters:
+        # a tiny operator (8 parts of 8^3): device work is negligible, so the
+        # wall time per iteration is the host issue (+ one wait per batch)
+        A = pamd.drivers.stencil_operator(parts, (16,) * 3, 27)
+        b = pamd.PVector.from_host(pamd.map_parts(
+            lambda s: np.random.default_rng(7 + s.part).uniform(-1, 1, s.num_lids), A.cols.partition), A.cols)
+        xx = pamd.PVector.undef(A.cols).fill_(0)
+        pamd.cg_(xx, A, b, reltol=0.0, maxiter=2, device=True, batch=cg_iters)
+        sync()
+        xx = pamd.PVector.undef(A.cols).fill_(0)
+        # batch = the whole run: the host enqueues every iteration, then waits once
+        t0 = time.perf_counter()
+        pamd.cg_(xx, A, b, reltol=0.0, maxiter=cg_iters, device=True, batch=cg_iters)
+        total = time.perf_counter() - t0
+        out["cg_host_us_per_iteration_tiny"] = round(1e6 * total / cg_iters, 1)
+    del A, x, y
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--n", type=int, default=256)
+    ap.add_argument("--k", type=int, default=40)
+    args = ap.parse_args()
+    res = []
+    res.append(measure(pamd.HIPBackend(devices=[0], share_streams=False), args.n, args.k,
+                       "share_streams=False (per-part streams, events and launches)", cg_iters=200))
+    res.append(measure(pamd.HIPBackend(devices=[0], share_streams=True), args.n, args.k,
+                       "share_streams=True (grouped launches)", cg_iters=200))
+    res.append(measure(pamd.HIPBackend(devices=[0], rccl=True), args.n, args.k,
+                       "rccl=True (grouped ncclSend/ncclRecv for every halo segment)"))
+    print(json.dumps({"tool": "host_issue", "n": args.n, "k": args.k, "results": res}, indent=1))
+
+
+if __name__ == "__main__":
+    main()
