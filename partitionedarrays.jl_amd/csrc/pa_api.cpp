@@ -131,6 +131,7 @@ extern int g_spmv_flags;
 extern int g_spmv_unroll;
 extern int g_spmv_lds;
 extern int g_long_exact;
+extern int g_spmv_short_occ;
 
 }  // namespace pa
 
@@ -1035,6 +1036,11 @@ int pa_tune(const char* key, int value, int* previous) {
     g_spmv_merge_max = value;
     if (previous) *previous = prev;
     return 0;
+  } else if (!std::strcmp(key, "spmv_short_occ")) {
+    CHECK_ARG(value >= 0 && value <= 3,
+              "spmv_short_occ: short-row F64 merged launch, 0 = one batch at 5 waves/SIMD (default), 1 = U 4 at 8, "
+              "2 = U 4 at 6, 3 = one batch at 6");
+    slot = &g_spmv_short_occ;
   } else if (!std::strcmp(key, "spmv_quadsort")) {
     CHECK_ARG(value >= 0 && value <= 2,
               "spmv_quadsort: 1 = matrices whose slices are mostly not pattern slices get the quad-sorted layout "

@@ -76,6 +76,7 @@ int g_spmv_unroll = 8;
 // i.e. the waves streaming at once (160 KB LDS per CU)
 int g_spmv_lds = 0;
 int g_spmv_format = 1;  // 1: pattern slices where built, 0: int32 columns only
+int g_spmv_short_occ = 0;  // short-row F64 merged launch: 0 one batch at 5 waves/SIMD, 1..3 occupancy variants
 // Build-time encoding knobs.  Defaults from profiles/r01/multipattern/README.md
 // (C5 Voronoi parts): multi-pattern slices stream up to 12 % fewer bytes but
 // add a launch per phase and per-lane LDS offset reads; kernel time is flat
@@ -88,7 +89,8 @@ int g_spmv_pattern_rule = 0;     // 1: slice encoding by streamed bytes, 0: patt
 std::vector<std::pair<void*, std::vector<char>>> g_capture_uploads;
 int g_long_exact = 1;  // pa_tune("long_rows_exact")
 #else
-extern int g_spmv_flags, g_spmv_unroll, g_spmv_lds, g_spmv_format, g_spmv_patterns, g_spmv_pattern_rule;
+extern int g_spmv_flags, g_spmv_unroll, g_spmv_lds, g_spmv_format, g_spmv_patterns, g_spmv_pattern_rule,
+    g_spmv_short_occ;
 extern std::vector<std::pair<void*, std::vector<char>>> g_capture_uploads;
 extern int g_long_exact;
 #endif
@@ -1203,11 +1205,38 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
   merged_wave<T, R, ALPHA, BMODE, 8, true>(tab);
 }
 
+// Occupancy variants of the short-row F64 launch (pa_tune "spmv_short_occ",
+// C2's FD7 operator: 16 K one-wave slices are 3.35 rounds of resident waves
+// at 5 per SIMD): 1 = U 4 at 8 waves per SIMD (2.1 rounds), 2 = U 4 at 6,
+// 3 = the one-batch kernel at 6.
+template <typename T, int R, bool ALPHA, int BMODE>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k_spmv_merged_u4w8(
+    const SpmvTable<T>* __restrict__ tab) {
+  merged_wave<T, R, ALPHA, BMODE, 4, false>(tab);
+}
+template <typename T, int R, bool ALPHA, int BMODE>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k_spmv_merged_u4w6(
+    const SpmvTable<T>* __restrict__ tab) {
+  merged_wave<T, R, ALPHA, BMODE, 4, false>(tab);
+}
+template <typename T, int R, bool ALPHA, int BMODE>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k_spmv_merged_shw6(
+    const SpmvTable<T>* __restrict__ tab) {
+  merged_wave<T, R, ALPHA, BMODE, 8, true>(tab);
+}
+
 template <typename T, int R, bool ALPHA, int BMODE>
 static void launch_merged_t(const SpmvTable<T>* d, int64_t waves, bool sh, hipStream_t st) {
   const int64_t blocks = (waves + 3) / 4;
   if (blocks == 0) return;
-  if (sh && std::is_same<T, double>::value)
+  if (sh && std::is_same<T, double>::value && g_spmv_short_occ) {
+    if (g_spmv_short_occ == 1)
+      hipLaunchKernelGGL((k_spmv_merged_u4w8<T, R, ALPHA, BMODE>), dim3(blocks), dim3(256), 0, st, d);
+    else if (g_spmv_short_occ == 2)
+      hipLaunchKernelGGL((k_spmv_merged_u4w6<T, R, ALPHA, BMODE>), dim3(blocks), dim3(256), 0, st, d);
+    else
+      hipLaunchKernelGGL((k_spmv_merged_shw6<T, R, ALPHA, BMODE>), dim3(blocks), dim3(256), 0, st, d);
+  } else if (sh && std::is_same<T, double>::value)
     hipLaunchKernelGGL((k_spmv_merged_short<T, R, ALPHA, BMODE>), dim3(blocks), dim3(256), g_spmv_lds, st, d);
   else if (sh)
     hipLaunchKernelGGL((k_spmv_merged<T, R, ALPHA, BMODE, 8, true>), dim3(blocks), dim3(256), g_spmv_lds, st, d);
