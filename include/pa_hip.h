@@ -61,7 +61,11 @@ int pa_device_count(int* count);
  *               with non-temporal stores, bit 6: launches whose rows have
  *               at most 8 entries use the short-row kernels (one predicated
  *               batch, no loop: fewer registers) (default 93);
- * "spmv_unroll" 4 or 8 entries in flight per lane (default 8);
+ * "spmv_unroll" 4 or 8 entries in flight per lane in the merged launch
+ *               (default 8; the per-kind launches use 8);
+ * "spmv_short_occ" short-row F64 merged launch: 0 one predicated batch at
+ *               5 waves/SIMD (default), 1 U = 4 at 8, 2 U = 4 at 6, 3 one
+ *               batch at 6;
  * "spmv_format" 1: pattern slices where the matrix has them (default),
  *               0: int32 column ids everywhere;
  * "spmv_patterns" 1..4 offset patterns per slice for matrices built

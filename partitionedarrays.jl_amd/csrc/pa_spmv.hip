@@ -926,10 +926,10 @@ static void launch_group_t(const SpmvGroup<T>& g, hipStream_t st) {
       return;
     }
   }
+  // (spmv_unroll 4 applies to the merged launch only: the per-kind
+  // launches keep U = 8, which keeps the library's code objects small)
   if (sh)
     hipLaunchKernelGGL((k_spmv_sell_group<T, R, ALPHA, BMODE, 8, PAT, true>), dim3(blocks), dim3(256), g_spmv_lds, st, g);
-  else if (g_spmv_unroll == 4)
-    hipLaunchKernelGGL((k_spmv_sell_group<T, R, ALPHA, BMODE, 4, PAT>), dim3(blocks), dim3(256), g_spmv_lds, st, g);
   else
     hipLaunchKernelGGL((k_spmv_sell_group<T, R, ALPHA, BMODE, 8, PAT>), dim3(blocks), dim3(256), g_spmv_lds, st, g);
 }
@@ -962,8 +962,6 @@ static void launch_t(const SpmvArgs<T>& a, hipStream_t st) {
   }
   if (PAT != 2 && (g_spmv_flags & SPMV_SHORT) && a.maxlen <= 8)
     hipLaunchKernelGGL((k_spmv_sell<T, R, ALPHA, BMODE, 8, PAT, true>), dim3(blocks), dim3(256), g_spmv_lds, st, a);
-  else if (g_spmv_unroll == 4)
-    hipLaunchKernelGGL((k_spmv_sell<T, R, ALPHA, BMODE, 4, PAT>), dim3(blocks), dim3(256), g_spmv_lds, st, a);
   else
     hipLaunchKernelGGL((k_spmv_sell<T, R, ALPHA, BMODE, 8, PAT>), dim3(blocks), dim3(256), g_spmv_lds, st, a);
 }
@@ -1229,16 +1227,22 @@ template <typename T, int R, bool ALPHA, int BMODE>
 static void launch_merged_t(const SpmvTable<T>* d, int64_t waves, bool sh, hipStream_t st) {
   const int64_t blocks = (waves + 3) / 4;
   if (blocks == 0) return;
-  if (sh && std::is_same<T, double>::value && g_spmv_short_occ) {
-    if (g_spmv_short_occ == 1)
-      hipLaunchKernelGGL((k_spmv_merged_u4w8<T, R, ALPHA, BMODE>), dim3(blocks), dim3(256), 0, st, d);
-    else if (g_spmv_short_occ == 2)
-      hipLaunchKernelGGL((k_spmv_merged_u4w6<T, R, ALPHA, BMODE>), dim3(blocks), dim3(256), 0, st, d);
-    else
-      hipLaunchKernelGGL((k_spmv_merged_shw6<T, R, ALPHA, BMODE>), dim3(blocks), dim3(256), 0, st, d);
-  } else if (sh && std::is_same<T, double>::value)
-    hipLaunchKernelGGL((k_spmv_merged_short<T, R, ALPHA, BMODE>), dim3(blocks), dim3(256), g_spmv_lds, st, d);
-  else if (sh)
+  if constexpr (std::is_same<T, double>::value) {
+    if (sh && g_spmv_short_occ) {
+      if (g_spmv_short_occ == 1)
+        hipLaunchKernelGGL((k_spmv_merged_u4w8<T, R, ALPHA, BMODE>), dim3(blocks), dim3(256), 0, st, d);
+      else if (g_spmv_short_occ == 2)
+        hipLaunchKernelGGL((k_spmv_merged_u4w6<T, R, ALPHA, BMODE>), dim3(blocks), dim3(256), 0, st, d);
+      else
+        hipLaunchKernelGGL((k_spmv_merged_shw6<T, R, ALPHA, BMODE>), dim3(blocks), dim3(256), 0, st, d);
+      return;
+    }
+    if (sh) {
+      hipLaunchKernelGGL((k_spmv_merged_short<T, R, ALPHA, BMODE>), dim3(blocks), dim3(256), g_spmv_lds, st, d);
+      return;
+    }
+  }
+  if (sh)
     hipLaunchKernelGGL((k_spmv_merged<T, R, ALPHA, BMODE, 8, true>), dim3(blocks), dim3(256), g_spmv_lds, st, d);
   else if (g_spmv_unroll == 4)
     hipLaunchKernelGGL((k_spmv_merged<T, R, ALPHA, BMODE, 4, false>), dim3(blocks), dim3(256), g_spmv_lds, st, d);

@@ -154,3 +154,17 @@ def test_mpi_baseline_equals_partitioned_and_python(O, ref, tmp_path, kind, dims
     oy = O.pvector_undef(A.rows)
     O.mul_(oy, A, ox)
     assert np.array_equal(_global_from_parts(O, oy, n), y1)
+
+
+@pytest.mark.parametrize("dims,shape", [((16, 16, 16), (2, 2, 2)), ((24, 12, 12), (2, 1, 1))])
+def test_bench_cpu_baseline_mpi_leg(ref, dims, shape):
+    """bench.py's CPU baseline beside the N > 1 lines and the halo leg: one
+    rank per part, halo values counted, a positive rate, cores = ranks."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(ROOT, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    r = bench.cpu_baseline_mpi(27, dims, shape, seconds=0.2)
+    P = int(np.prod(shape))
+    assert r["cores"] == r["ranks"] == P and r["kind"] == "port"
+    assert r["value"] > 0 and r["ms_per_spmv"] > 0 and r["halo_values_per_spmv"] > 0

@@ -7,6 +7,11 @@ extra work a part of the 8-GPU run does (boundary slices, side rows, pack/
 unpack) — the part of weak-scaling efficiency that is not RCCL latency.
 
     python tools/weak_sim.py [--n 256] [--reps 10]
+
+Each part alone is timed through the per-part launches (pa_tune spmv_group
+0), which split it into the interior phase (no ghost column: what overlaps
+the halo transport on 8 GPUs) and the boundary phase: the interior time is
+the per-part halo budget.
 """
 import argparse
 import json
@@ -68,13 +73,22 @@ for shape in ((1, 1, 1), (2, 2, 2)):
         args = (1, pamd._lib.ptr_array([A.values.local(p).h]), pamd._lib.ptr_array([y.values.local(p).h]),
                 pamd._lib.ptr_array([iy.h]), pamd._lib.ptr_array([x.values.local(p).h]), pamd._lib.ptr_array([ix.h]),
                 None, one[1], zero[1])
+        # per-part launches (spmv_group 0): the interior phase (slices
+        # without ghost columns: what runs while the halo is in flight on
+        # 8 GPUs) and the boundary phase (slices reading ghosts, side rows)
+        prev = pamd._lib.tune("spmv_group", 0)
         c.set_timing(True)
-        ks = []
+        ks, ki, kb = [], [], []
         for _ in range(a.reps + 2):
             pamd._lib.call("pa_spmv_all", *args)
-            ks.append(sum(c.last_kernel_ms()))
+            t = c.kernel_times()
+            ks.append(t["interior_ms"] + t["boundary_ms"])
+            ki.append(t["interior_ms"])
+            kb.append(t["boundary_ms"])
         c.set_timing(False)
-        alone[p] = round(float(np.median(ks[2:])), 4)
+        pamd._lib.tune("spmv_group", prev)
+        alone[p] = {"total_ms": round(float(np.median(ks[2:])), 4), "interior_ms": round(float(np.median(ki[2:])), 4),
+                    "boundary_ms": round(float(np.median(kb[2:])), 4)}
     infos = {p: A.values.local(p).info() for p in parts.part_ids}
     out[str(shape)] = {"wall_ms_per_mul_all_parts": round(1e3 * wall, 4),
                        "wall_ms_per_part": round(1e3 * wall / len(parts.part_ids), 4),
