@@ -88,7 +88,7 @@ int pa_device_count(int* count);
  *               reads/copies, except parts whose communicator came from
  *               pa_comm_init_all (RCCL, per context); 1: RCCL send/recv for
  *               every part that has a communicator;
- * "spmv_quadsort" 1: a matrix whose slices are mostly not pattern slices
+ * "spmv_quadsort" 1: a matrix with fewer than 90 % pattern slices
  *               (irregular partitions) gets the quad-sorted layout: lanes
  *               of R consecutive rows ordered so that whole slices become
  *               pattern or quad-run slices (default; matrices built

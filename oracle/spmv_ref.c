@@ -59,6 +59,7 @@
  *      Exchanger and a halo exchange of x in every mul! (run_mpi below)
  *  spmv_ref --kind 27|7 --n N --dtype f32|c128 --xin f --yout f
  *      one part, the literal column loop in Float32 / ComplexF64
+ *      (Float32.(A) / A .* (1+0.5im))
  * --dims gives the global nodes per dimension (default N N N; the operator's
  * h follows N[0], as drivers.py stencil_coeffs).
  * Every mode prints one JSON line.
@@ -886,7 +887,8 @@ static int run_mpi(int reps, double seconds, const char* yout) {
 
 /* ---- one part, the literal CSC column loop, in Float32 / ComplexF64 -------
  * A in T (Float32: Float32.(A), each Float64 value rounded once; ComplexF64:
- * the Float64 value + 0im), x and y in T; C[i] += nzv[p]*(B[j]*α) with α = 1,
+ * A .* (1+0.5im) entrywise, Complex(v*1, v*0.5), as BASELINE config 5 and
+ * the device stencil build it), x and y in T; C[i] += nzv[p]*(B[j]*α) with α = 1,
  * Julia's complex product (re = a.re*b.re - a.im*b.im, im = a.re*b.im +
  * a.im*b.re), no FMA (-ffp-contract=off).                                   */
 typedef struct { double re, im; } cplx;
@@ -911,7 +913,7 @@ static void onepart_c128(int64_t n, const int64_t* colptr, const int64_t* rowval
     for (int64_t p = colptr[j] - 1; p < colptr[j + 1] - 1; ++p) {
       const int32_t i = invrows[rowval[p] - 1];
       if (i > 0) {
-        const cplx a = {nz64[p], 0.0};
+        const cplx a = {nz64[p] * 1.0, nz64[p] * 0.5};  /* A .* (1+0.5im), BASELINE config 5 */
         const double pr = a.re * axj.re - a.im * axj.im, pi = a.re * axj.im + a.im * axj.re;
         Cv[i - 1].re = Cv[i - 1].re + pr;
         Cv[i - 1].im = Cv[i - 1].im + pi;

@@ -416,8 +416,9 @@ int quad_sort(pa_mat* A, int64_t noids) {
 
 // Pattern slices + side SELL from the int32 layout (device detection, host
 // bookkeeping).  noids: owned columns (x lids >= noids are ghosts).  When
-// fewer than half the slices are pattern slices (irregular partitions) the
-// layout is quad-sorted first and the detection redone on it.
+// fewer than 90 % of the slices are pattern slices (irregular partitions;
+// Cartesian parts have them all) the layout is quad-sorted first and the
+// detection redone on it.
 int finalize_pattern(pa_mat* A, int kmax, int64_t noids) {
   A->kmax = std::max(kmax, 1);
   const int64_t ns = A->nslices;
@@ -456,7 +457,7 @@ int finalize_pattern(pa_mat* A, int kmax, int64_t noids) {
   if (g_spmv_quadsort && !A->d_qmap && A->n_long == 0 && A->R > 1) {
     int64_t npat = 0;
     for (int64_t s = 0; s < ns; ++s) npat += kind[s] != 0;
-    if (2 * npat < ns || g_spmv_quadsort == 2) {  // mostly irregular slices: quad-sort, then detect again
+    if (10 * npat < 9 * ns || g_spmv_quadsort == 2) {  // irregular slices: quad-sort, then detect again
       for (void** q : {(void**)&A->d_kind, (void**)&A->d_plen, (void**)&A->d_pat, (void**)&A->d_mask,
                        (void**)&A->d_mpat, (void**)&A->d_psel}) {
         dev_free(*q);

