@@ -1246,6 +1246,8 @@ static void launch_merged_t(const SpmvTable<T>* d, int64_t waves, bool sh, hipSt
     hipLaunchKernelGGL((k_spmv_merged<T, R, ALPHA, BMODE, 8, true>), dim3(blocks), dim3(256), g_spmv_lds, st, d);
   else if (g_spmv_unroll == 4)
     hipLaunchKernelGGL((k_spmv_merged<T, R, ALPHA, BMODE, 4, false>), dim3(blocks), dim3(256), g_spmv_lds, st, d);
+  else if (!ALPHA && BMODE == 0 && g_spmv_unroll == 16)
+    hipLaunchKernelGGL((k_spmv_merged<T, R, false, 0, 16, false>), dim3(blocks), dim3(256), g_spmv_lds, st, d);
   else
     hipLaunchKernelGGL((k_spmv_merged<T, R, ALPHA, BMODE, 8, false>), dim3(blocks), dim3(256), g_spmv_lds, st, d);
 }

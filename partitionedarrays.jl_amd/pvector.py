@@ -11,6 +11,7 @@ import ctypes as C
 from collections import OrderedDict
 import math
 import sys
+import weakref
 
 import numpy as np
 
@@ -632,7 +633,36 @@ def _spmv(c, a, b, alpha, beta, dot_out):
         _lib.call("pa_spmv_dot_all", *args, dot_out.ctypes.data_as(C.c_void_p))
 
 
+_ARGS_CACHE_MAX = 8
+
+
 def _spmv_args(c, a, b, alpha, beta):
+    """The C-ABI arguments of mul!(c, a, b, α, β), cached on `a` per (c, b,
+    α, β): the layout checks and the handle arrays are built on the first
+    call only (the Python side of a mul! costs about as much as a small
+    SpMV's kernels otherwise).  An entry is reused only while c and b are the
+    same live objects with the same values and ranges (the entry holds no
+    strong reference to them: their device memory is freed as usual)."""
+    cache = a.__dict__.get("_args_cache")
+    if cache is None:
+        cache = a.__dict__["_args_cache"] = OrderedDict()
+    key = (id(c), id(b), type(alpha), alpha, type(beta), beta)
+    try:
+        e = cache.get(key)
+    except TypeError:  # unhashable scalars (0-d arrays): no caching
+        return _spmv_args_build(c, a, b, alpha, beta)
+    now = (id(c.values), id(b.values), id(c.rows), id(b.rows))
+    if e is not None and e[0]() is c and e[1]() is b and e[2] == now:
+        cache.move_to_end(key)
+        return e[3]
+    args = _spmv_args_build(c, a, b, alpha, beta)
+    cache[key] = (weakref.ref(c), weakref.ref(b), now, args)
+    while len(cache) > _ARGS_CACHE_MAX:
+        cache.popitem(last=False)
+    return args
+
+
+def _spmv_args_build(c, a, b, alpha, beta):
     if not (c.rows is a.rows or oids_are_equal(c.rows, a.rows)):
         raise AssertionError("mul!: c.rows and a.rows own different ids")
     if not (b.rows is a.cols or (oids_are_equal(a.cols, b.rows) and hids_are_equal(a.cols, b.rows))):

@@ -231,3 +231,34 @@ def test_rccl_backend_leaves_global_transport_knob(pamd):
     pamd.HIPBackend(devices=[0], rccl=True).get_part_ids((2, 1, 1))
     after = pamd._lib.tune("halo_transport", before)
     assert after == before
+
+
+def test_mul_argument_cache_follows_objects(be, pamd, O):
+    """mul_'s cached C-ABI arguments (per c, b, α, β on the matrix): repeated
+    calls, a new α, and a new y allocated after the old one died (possibly
+    at the same address) all give the oracle's values."""
+    import gc
+    nparts, n = 4, 37
+    parts = be.get_part_ids(nparts)
+    A, OA = _build(pamd, O, parts, n, nparts)
+    rng = np.random.default_rng(5)
+    xs = {p: rng.uniform(-1, 1, A.cols.partition.local(p).num_lids) for p in parts.part_ids}
+    x = pamd.PVector.from_host(pamd.map_parts(lambda s: xs[s.part], A.cols.partition), A.cols)
+    ox = O.PVector(O.map_parts(lambda s: xs[s.part].copy(), OA.cols.partition), OA.cols)
+
+    def check(y, alpha):
+        oy = O.pvector_undef(OA.rows)
+        O.mul_(oy, OA, ox, alpha, 0.0)
+        got = y.to_host()
+        for p in parts.part_ids:
+            own = A.rows.partition.local(p).oid_to_lid - 1
+            assert np.array_equal(got.local(p)[own], oy.values[p][own])
+
+    for alpha in (1.0, 1.0, 0.5, 1.0):
+        y = pamd.PVector.undef(A.rows)
+        pamd.mul_(y, A, x, alpha, 0.0)
+        pamd.mul_(y, A, x, alpha, 0.0)
+        check(y, alpha)
+        del y
+        gc.collect()
+    assert len(A.__dict__["_args_cache"]) <= 8

@@ -10,8 +10,10 @@
 #   smoke                 __graft_entry__.smoke()
 #   bench[:bench args]    python bench.py ARGS            > OUT/bench<i>.json
 #   kt[:bench args]       rocprofv3 --kernel-trace --stats  -d OUT/kt<i>
+#   ktpy:script args      rocprofv3 --kernel-trace --stats of python3 script args  -d OUT/kt<i>
 #   pmc:CTR[,CTR..][:bench args]  rocprofv3 --pmc CTR..     -d OUT/pmc<i>
 #   py:script args        python script args              > OUT/py<i>.log
+#   cmd:program args      a host program (no GPU), e.g. the C port   > OUT/cmd<i>.log
 # Profiled runs default to "--steps 10 --warmup 2 --no-cpu-baseline --no-pmc".
 set -o pipefail
 OUT=$1
@@ -42,6 +44,10 @@ for step in "$@"; do
       timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/kt$i" -o kt --output-format csv \
         -- python3 bench.py ${args:-$PROF_ARGS} > "$OUT/kt$i.log" 2>&1
       rc=$? ;;
+    ktpy)
+      timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/kt$i" -o kt --output-format csv \
+        -- python3 $args > "$OUT/kt$i.log" 2>&1
+      rc=$? ;;
     pmc)
       ctr=${args%%:*}
       bargs=""
@@ -52,6 +58,9 @@ for step in "$@"; do
     py)
       timeout -k 10 600 python -u $args > "$OUT/py$i.log" 2>&1
       rc=$?; tail -5 "$OUT/py$i.log" ;;
+    cmd)
+      timeout -k 10 600 $args > "$OUT/cmd$i.log" 2>&1
+      rc=$?; tail -c 600 "$OUT/cmd$i.log" ;;
     *)
       echo "unknown step $name"; exit 2 ;;
   esac
