@@ -184,6 +184,10 @@ int pa_vec_create(pa_ctx* ctx, int dtype, int64_t n, pa_vec** out);
 int pa_vec_destroy(pa_vec* v);
 int pa_vec_upload(pa_vec* v, const void* host, int64_t n);
 int pa_vec_download(const pa_vec* v, void* host, int64_t n);
+/* the device address of v's values (lid 1 at offset 0; valid until
+ * pa_vec_destroy): zero-copy interop, e.g. Julia's unsafe_wrap of a
+ * ROCArray over a part's values, and placement diagnostics              */
+int pa_vec_device_ptr(const pa_vec* v, void** out);
 /* fill!(v, s) (Interfaces.jl:1966-1971), all lids */
 int pa_vec_fill(pa_vec* v, const void* s);
 /* copyto!(dst, src): all lids when same_layout, owned values otherwise

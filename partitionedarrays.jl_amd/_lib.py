@@ -54,6 +54,7 @@ _SIGS = {
     "pa_vec_destroy": [_p],
     "pa_vec_upload": [_p, _p, C.c_int64],
     "pa_vec_download": [_p, _p, C.c_int64],
+    "pa_vec_device_ptr": [_p, _p],
     "pa_vec_fill": [_p, _p],
     "pa_vec_copy": [_p, _p, _p, _p, C.c_int],
     "pa_vec_axpby": [_p, _p, _p, _p, C.c_int, C.c_int],

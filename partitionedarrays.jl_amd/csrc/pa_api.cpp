@@ -1607,6 +1607,12 @@ int pa_vec_download(const pa_vec* v, void* host, int64_t n) {
   return 0;
 }
 
+int pa_vec_device_ptr(const pa_vec* v, void** out) {
+  CHECK_ARG(v && out, "null argument");
+  *out = v->d;
+  return 0;
+}
+
 int pa_vec_fill(pa_vec* v, const void* s) {
   CHECK_ARG(v && s, "null argument");
   HIPC(hipSetDevice(v->ctx->device));

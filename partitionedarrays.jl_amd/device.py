@@ -311,6 +311,12 @@ class DeviceVector:
         _lib.call("pa_vec_download", self.h, a.ctypes.data_as(C.c_void_p), self.n)
         return a
 
+    def device_ptr(self) -> int:
+        """device address of the values (pa_vec_device_ptr)"""
+        p = C.c_void_p()
+        _lib.call("pa_vec_device_ptr", self.h, C.byref(p))
+        return p.value or 0
+
     def fill(self, v):
         b, bp = _lib.scalar_buf(v, self.dtype)
         _lib.call("pa_vec_fill", self.h, bp)

@@ -8,6 +8,10 @@ checks that every variant gives the same bits.
 
     python tools/ab_knob.py --problem stencil --kind 7 --n 128 --variants "spmv_short_occ=0|spmv_short_occ=1"
     python tools/ab_knob.py --problem c5 --n 128 --parts 8 --dtype f32 --variants "spmv_quadsort=0|spmv_quadsort=1"
+
+With --shared (run-time knobs only) every variant runs on the same operator
+copies: separate copies differ in physical placement, which alone moves the
+time by up to ~15 % on some boxes (profiles/r03/f/).
 """
 import argparse
 import json
@@ -40,6 +44,9 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--label", default="")
+    ap.add_argument("--shared", action="store_true",
+                    help="run-time knobs only: every variant runs on the SAME operator copies (no allocation/"
+                         "placement difference between variants)")
     a = ap.parse_args()
     dtype = DT[a.dtype]
     S = np.dtype(dtype).itemsize
@@ -70,7 +77,10 @@ def main():
             pamd._lib.tune(k, x)
 
     sets, info = {}, {}
-    for v in variants:
+    for vi, v in enumerate(variants):
+        if a.shared and vi > 0:
+            sets[vi], info[vi] = sets[0], info[0]
+            continue
         prev = knobs(v)
         A = build()
         B = 0
@@ -89,18 +99,18 @@ def main():
                 lambda s: (np.random.default_rng(s.part).uniform(-1, 1, s.num_lids)).astype(dtype),
                 Ak.cols.partition), Ak.cols)
             xs.append((Ak, x, pamd.PVector.undef(Ak.rows, dtype)))
-        sets[v] = xs
+        sets[vi] = xs
         f0 = A.values.local(parts.part_ids[0]).info()
-        info[v] = {"bytes": B, "copies": ncopies,
+        info[vi] = {"bytes": B, "copies": ncopies,
                    "format": {k: f0[k] for k in ("nslices", "pattern_slices", "delta16_slices", "quadrun_slices",
                                                  "quad_sorted", "side_rows") if k in f0}}
         restore(prev)
-    times = {v: [] for v in variants}
+    times = {vi: [] for vi in range(len(variants))}
     out = {}
     for rnd in range(a.rounds):
-        for v in variants:
+        for vi, v in enumerate(variants):
             prev = knobs(v)
-            xs = sets[v]
+            xs = sets[vi]
             for i in range(3):
                 pamd.mul_(xs[i % len(xs)][2], xs[i % len(xs)][0], xs[i % len(xs)][1])
             sync()
@@ -109,19 +119,21 @@ def main():
                 Ak, x, y = xs[i % len(xs)]
                 pamd.mul_(y, Ak, x)
             sync()
-            times[v].append(1e3 * (time.perf_counter() - t0) / a.steps)
+            times[vi].append(1e3 * (time.perf_counter() - t0) / a.steps)
             if rnd == 0:
-                out[v] = [t.copy() for t in xs[0][2].to_host().parts]
+                out[vi] = [t.copy() for t in xs[0][2].to_host().parts]
             restore(prev)
-    ref = out[variants[0]]
-    same = {str(dict(v)): all(np.array_equal(p, q) for p, q in zip(out[v], ref)) for v in variants}
+    ref = out[0]
+    same = {f"{vi}:{dict(v)}": all(np.array_equal(p, q) for p, q in zip(out[vi], ref))
+            for vi, v in enumerate(variants)}
     res = []
-    for v in variants:
-        ms = float(np.median(times[v]))
-        res.append({"knobs": dict(v), "ms_median": round(ms, 5), "ms_all": [round(t, 5) for t in times[v]],
-                    "gbs": round(info[v]["bytes"] / (ms * 1e-3) / 1e9, 1),
-                    "frac": round(info[v]["bytes"] / (ms * 1e-3) / 1e9 / 8000.0, 4), **info[v]})
-    print(json.dumps({"tool": "ab_knob", "label": a.label, "problem": a.problem, "kind": a.kind, "n": a.n,
+    for vi, v in enumerate(variants):
+        ms = float(np.median(times[vi]))
+        res.append({"knobs": dict(v), "ms_median": round(ms, 5), "ms_all": [round(t, 5) for t in times[vi]],
+                    "gbs": round(info[vi]["bytes"] / (ms * 1e-3) / 1e9, 1),
+                    "frac": round(info[vi]["bytes"] / (ms * 1e-3) / 1e9 / 8000.0, 4), **info[vi]})
+    print(json.dumps({"tool": "ab_knob", "label": a.label, "shared": a.shared, "problem": a.problem,
+                      "kind": a.kind, "n": a.n,
                       "dtype": a.dtype, "shape": a.shape if a.problem == "stencil" else a.parts,
                       "same_bits": same, "results": res}))
 
