@@ -1010,9 +1010,12 @@ int pa_tune(const char* key, int value, int* previous) {
     CHECK_ARG(value >= 0 && value <= 160 * 1024, "spmv_lds: bytes of LDS per SpMV block (occupancy cap)");
     slot = &g_spmv_lds;
   } else if (!std::strcmp(key, "spmv_unroll")) {
-    CHECK_ARG(value == 4 || value == 8 || value == 9 || value == 12 || value == 14 || value == 16 || value == 28,
-              "spmv_unroll must be 4, 8, 9, 12, 14, 16 or 28 (16: merged launches with alpha 1, beta 0; "
-              "9/12/14/28: the same, F64 only)");
+    // (U = 9/12/14/16/28 were measured in r03 on one shared operator copy:
+    // FE27 256³ F64 U 12 = U 8 within 0.1 %, U 16 +1.7 %; C5 U 16 +5-10 %;
+    // profiles/r03/g/placement_and_shared_ab.jsonl — not kept; nor a
+    // prefetch of the next batch's delta16 codes: C5 F32/F64/C128 ±1 %,
+    // C64 +26 %, profiles/r03/m/)
+    CHECK_ARG(value == 4 || value == 8, "spmv_unroll must be 4 or 8");
     slot = &g_spmv_unroll;
   } else if (!std::strcmp(key, "long_rows_exact")) {
     CHECK_ARG(value == 0 || value == 1, "long_rows_exact: 1 = reference summation order, 0 = lane-strided tree (1e-12)");

@@ -1246,21 +1246,6 @@ static void launch_merged_t(const SpmvTable<T>* d, int64_t waves, bool sh, hipSt
     hipLaunchKernelGGL((k_spmv_merged<T, R, ALPHA, BMODE, 8, true>), dim3(blocks), dim3(256), g_spmv_lds, st, d);
   else if (g_spmv_unroll == 4)
     hipLaunchKernelGGL((k_spmv_merged<T, R, ALPHA, BMODE, 4, false>), dim3(blocks), dim3(256), g_spmv_lds, st, d);
-  else if (!ALPHA && BMODE == 0 && g_spmv_unroll == 16)
-    hipLaunchKernelGGL((k_spmv_merged<T, R, false, 0, 16, false>), dim3(blocks), dim3(256), g_spmv_lds, st, d);
-  else if (std::is_same<T, double>::value && !ALPHA && BMODE == 0 && g_spmv_unroll != 8) {
-    // entries in flight per lane, A/B variants (F64, α = 1, β = 0 only)
-    if constexpr (std::is_same<T, double>::value && !ALPHA && BMODE == 0) {
-      if (g_spmv_unroll == 9)
-        hipLaunchKernelGGL((k_spmv_merged<T, R, false, 0, 9, false>), dim3(blocks), dim3(256), g_spmv_lds, st, d);
-      else if (g_spmv_unroll == 12)
-        hipLaunchKernelGGL((k_spmv_merged<T, R, false, 0, 12, false>), dim3(blocks), dim3(256), g_spmv_lds, st, d);
-      else if (g_spmv_unroll == 14)
-        hipLaunchKernelGGL((k_spmv_merged<T, R, false, 0, 14, false>), dim3(blocks), dim3(256), g_spmv_lds, st, d);
-      else
-        hipLaunchKernelGGL((k_spmv_merged<T, R, false, 0, 28, false>), dim3(blocks), dim3(256), g_spmv_lds, st, d);
-    }
-  }
   else
     hipLaunchKernelGGL((k_spmv_merged<T, R, ALPHA, BMODE, 8, false>), dim3(blocks), dim3(256), g_spmv_lds, st, d);
 }
