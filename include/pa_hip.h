@@ -355,6 +355,11 @@ int pa_mat_delta16_info(const pa_mat* A, int64_t* delta16_slices);
  * pa_tune "spmv_quadsort").  Encoding only: results are unchanged.       */
 int pa_mat_quadrun_info(const pa_mat* A, int64_t* quadrun_slices, int* quad_sorted);
 
+/* device addresses of the matrix's main arrays, for placement diagnostics:
+ * out[0..7] = values, int32 columns, slice offsets, slice lengths (pattern),
+ * patterns, masks, side values, side columns (0 where absent)           */
+int pa_mat_device_ptrs(const pa_mat* A, uint64_t out[8]);
+
 /* Bytes one mul! streams from this matrix in its current encoding
  * (pa_tune("spmv_format")), as its kernels load them: values (padding
  * included), column ids (int32 slices, side rows, long rows) and slice

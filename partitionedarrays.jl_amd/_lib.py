@@ -106,6 +106,7 @@ _SIGS = {
     "pa_ctx_kernel_times": [_p, C.POINTER(C.c_float), C.POINTER(C.c_float), C.POINTER(C.c_float),
                             C.POINTER(C.c_int)],
     "pa_mat_traffic": [_p, _i64p, _i64p, _i64p],
+    "pa_mat_device_ptrs": [_p, _p],
     "pa_ctx_span": [_p, C.c_int],
     "pa_ctx_span_ms": [_p, C.POINTER(C.c_float)],
     "pa_ctx_set_timing": [_p, C.c_int],

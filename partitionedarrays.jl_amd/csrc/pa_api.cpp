@@ -2549,6 +2549,13 @@ int pa_mat_long_rows(const pa_mat* A, int64_t* n_long, int64_t* n_long_nnz) {
 // Bytes one mul! streams from the matrix in its current encoding (the
 // kernels' own loads, padding included): values, column ids, and the slice
 // metadata (offsets, lengths, lists, patterns, masks, side-row maps).
+int pa_mat_device_ptrs(const pa_mat* A, uint64_t out[8]) {
+  CHECK_ARG(A && out, "null argument");
+  const void* p[8] = {A->d_val, A->d_col, A->d_slice_off, A->d_plen, A->d_pat, A->d_mask, A->d_s_val, A->d_s_col};
+  for (int i = 0; i < 8; ++i) out[i] = (uint64_t)(uintptr_t)p[i];
+  return 0;
+}
+
 int pa_mat_traffic(const pa_mat* A, int64_t* value_bytes, int64_t* index_bytes, int64_t* meta_bytes) {
   CHECK_ARG(A, "null matrix");
   const int64_t S = (int64_t)dtype_size(A->dtype), H = A->H, W = H / 64;

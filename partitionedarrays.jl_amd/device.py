@@ -513,6 +513,12 @@ class DeviceMatrix:
         d.update(self.traffic())
         return d
 
+    def device_ptrs(self):
+        """pa_mat_device_ptrs: addresses of the main arrays (diagnostics)"""
+        out = (C.c_uint64 * 8)()
+        _lib.call("pa_mat_device_ptrs", self.h, out)
+        return dict(zip(["val", "col", "slice_off", "plen", "pat", "mask", "s_val", "s_col"], list(out)))
+
     def traffic(self):
         """bytes one mul! streams from the matrix (current encoding)"""
         t = [C.c_int64() for _ in range(3)]

@@ -65,8 +65,10 @@ def main():
                 pamd.mul_(y, Ai, x)
             ctx.span_stop()
             t[i].append(ctx.span_ms() / a.reps)
+    ptrs = [{k: hex(v) for k, v in Ai.values.local(1).device_ptrs().items()} for Ai in As]
     print(json.dumps({"tool": "first_alloc_probe", "prealloc_gb": a.prealloc_gb, "keep": a.keep,
-                      "swap": a.swap, "dummy_first": a.dummy_first,
+                      "swap": a.swap, "dummy_first": a.dummy_first, "mat_ptrs": ptrs,
+                      "x": hex(x.values.parts[0].device_ptr()), "y": hex(y.values.parts[0].device_ptr()),
                       "ms": [round(float(np.median(v)), 4) for v in t]}))
 
 
