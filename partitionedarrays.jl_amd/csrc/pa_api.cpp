@@ -177,6 +177,21 @@ int dev_upload(T** dptr, const std::vector<T>& h) {
   return 0;
 }
 
+// pa_tune("alloc_contiguous"): the large arrays (matrix values and column
+// ids, vectors) of matrices and vectors created afterwards are allocated in
+// physically contiguous device memory (hipDeviceMallocContiguous), falling
+// back to hipMalloc when that fails.  An experiment on the placement spread
+// of DESIGN.md §4.1: off by default.
+int g_alloc_contig = 0;
+hipError_t big_malloc(void** p, size_t bytes) {
+  if (g_alloc_contig && bytes >= ((size_t)64 << 20)) {
+    const hipError_t e = hipExtMallocWithFlags(p, bytes, hipDeviceMallocContiguous);
+    if (e == hipSuccess) return e;
+    (void)hipGetLastError();
+  }
+  return hipMalloc(p, bytes);
+}
+
 void dev_free(void* p) {
   if (p) (void)hipFree(p);
 }
@@ -386,8 +401,8 @@ int quad_sort(pa_mat* A, int64_t noids) {
   A->long_off = A->slots + A->n_gnz;
   int32_t *d_perm = nullptr, *d_inv = nullptr;
   if (dev_upload(&d_perm, perm) || dev_upload(&d_inv, inv) || dev_upload(&A->d_qmap, A->h_qmap)) return -1;
-  if (A->slots > 0) HIPC(hipMalloc((void**)&A->d_col, A->slots * 4));
-  if (nvals(A) > 0) HIPC(hipMalloc(&A->d_val, nvals(A) * S));
+  if (A->slots > 0) HIPC(big_malloc((void**)&A->d_col, A->slots * 4));
+  if (nvals(A) > 0) HIPC(big_malloc(&A->d_val, nvals(A) * S));
   launch_quad_permute(A, ns, d_perm, A->d_slice_off, A->d_slice_len, o_soff, o_slen, o_col, o_val, A->d_col,
                       A->d_val, st);
   HIPC(hipGetLastError());
@@ -492,7 +507,7 @@ int finalize_pattern(pa_mat* A, int kmax, int64_t noids) {
   }
   if (g_spmv_delta16) {  // int32-column slices whose columns fit 16-bit codes (kind 3)
     int32_t* d_ok = nullptr;
-    HIPC(hipMalloc((void**)&A->d_col16, std::max<int64_t>(A->slots, 1) * 2));
+    HIPC(big_malloc((void**)&A->d_col16, std::max<int64_t>(A->slots, 1) * 2));
     HIPC(hipMalloc((void**)&A->d_gbase, ns * 4));
     HIPC(hipMalloc((void**)&d_ok, ns * 4));
     launch_delta16(A, noids, A->d_kind, d_ok, st);
@@ -1047,6 +1062,10 @@ int pa_tune(const char* key, int value, int* previous) {
               "spmv_short_occ: short-row F64 merged launch, 0 = one batch at 5 waves/SIMD (default), 1 = U 4 at 8, "
               "2 = U 4 at 6, 3 = one batch at 6");
     slot = &g_spmv_short_occ;
+  } else if (!std::strcmp(key, "alloc_contiguous")) {
+    CHECK_ARG(value == 0 || value == 1, "alloc_contiguous: 1 = large arrays in physically contiguous device memory "
+                                        "(matrices and vectors created afterwards), 0 = hipMalloc (default)");
+    slot = &g_alloc_contig;
   } else if (!std::strcmp(key, "spmv_quadsort")) {
     CHECK_ARG(value >= 0 && value <= 2,
               "spmv_quadsort: 1 = matrices whose slices are mostly not pattern slices get the quad-sorted layout "
@@ -1569,7 +1588,7 @@ int pa_vec_create(pa_ctx* c, int dtype, int64_t n, pa_vec** out) {
     // kVecPad bytes on both sides: the SpMV's 16 B x runs may start up to
     // 3 elements before lid 0 or end up to 3 after the last lid
     const size_t bytes = (size_t)n * dtype_size(dtype) + 2 * kVecPad;
-    hipError_t e = hipMalloc(&v->base, bytes);
+    hipError_t e = big_malloc(&v->base, bytes);
     if (e != hipSuccess) { delete v; PA_FAIL(std::string("hipMalloc(vector) failed: ") + hipGetErrorString(e)); }
     v->d = (char*)v->base + kVecPad;
     HIPC(hipMemsetAsync(v->base, 0, bytes, c->s_main));
@@ -1756,7 +1775,7 @@ int mat_from_visit(pa_ctx* c, int dtype, int64_t nrows_lids, int64_t ncols_lids,
   if (A->n_lnz) std::memcpy(&hval[A->long_off * S], lval.data(), A->n_lnz * S);
   if (dev_upload(&A->d_col, hcol)) { pa_mat_destroy(A); return -1; }
   if (nvals(A)) {
-    HIPC(hipMalloc(&A->d_val, nvals(A) * S));
+    HIPC(big_malloc(&A->d_val, nvals(A) * S));
     HIPC(hipMemcpy(A->d_val, hval.data(), nvals(A) * S, hipMemcpyHostToDevice));
   }
   if (upload_long(A, lrows, lptr, lcol)) { pa_mat_destroy(A); return -1; }
@@ -2064,13 +2083,13 @@ int mat_from_coo_impl(pa_ctx* c, int dtype, int index_bytes, int ids_global, int
   for (int64_t s = 0; s < ns; ++s) sghost[s] = sg[s] ? 1 : 0;
   if (finish_sell_layout(A, slen, sghost, nullptr)) { pa_mat_destroy(A); return -1; }
   if (A->slots > 0) {
-    HIPC(hipMalloc((void**)&A->d_col, A->slots * 4));
+    HIPC(big_malloc((void**)&A->d_col, A->slots * 4));
     launch_fill_i32(A->slots, A->d_col, -1, st);
   }
   A->n_gnz = ngh;
   A->long_off = A->slots + ngh;
   if (nvals(A) > 0) {
-    HIPC(hipMalloc(&A->d_val, nvals(A) * S));
+    HIPC(big_malloc(&A->d_val, nvals(A) * S));
     HIPC(hipMemsetAsync(A->d_val, 0, nvals(A) * S, st));
   }
   if (nu > 0) HIPC(hipMalloc((void**)&nzs, nu * 8));
@@ -3728,8 +3747,8 @@ int pa_mat_stencil(pa_ctx* c, int dtype, int kind, const int64_t gdims[3], const
   const size_t S = dtype_size(dtype);
   int64_t nnz_owned = 0;
   (void)nnz_owned;
-  hipError_t e1 = hipMalloc((void**)&A->d_col, std::max<int64_t>(A->slots, 1) * 4);
-  hipError_t e2 = hipMalloc(&A->d_val, std::max<int64_t>(A->slots, 1) * S);
+  hipError_t e1 = big_malloc((void**)&A->d_col, std::max<int64_t>(A->slots, 1) * 4);
+  hipError_t e2 = big_malloc(&A->d_val, std::max<int64_t>(A->slots, 1) * S);
   if (e1 != hipSuccess || e2 != hipSuccess) { cleanup(); pa_mat_destroy(A); PA_FAIL("hipMalloc(matrix) failed: out of device memory"); }
   launch_stencil_fill(g, d_shell, d_coef, nrows, (int)nrows, A, d_err, c->s_main);
   HIPC(hipGetLastError());

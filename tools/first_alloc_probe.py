@@ -27,7 +27,11 @@ def main():
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--swap", action="store_true", help="free the first copy, then build one more")
     ap.add_argument("--dummy-first", type=int, default=0, help="build (and keep) an n^3 operator first")
+    ap.add_argument("--tune", default="", help="pa_tune knobs before anything is built: key=v[,key=v]")
     a = ap.parse_args()
+    for kv in filter(None, a.tune.split(",")):
+        k, v = kv.split("=")
+        pamd._lib.tune(k, int(v))
     be = pamd.HIPBackend(devices=[0])
     parts = be.get_part_ids((1, 1, 1))
     ctx = be.context(1)
@@ -66,7 +70,7 @@ def main():
             ctx.span_stop()
             t[i].append(ctx.span_ms() / a.reps)
     ptrs = [{k: hex(v) for k, v in Ai.values.local(1).device_ptrs().items()} for Ai in As]
-    print(json.dumps({"tool": "first_alloc_probe", "prealloc_gb": a.prealloc_gb, "keep": a.keep,
+    print(json.dumps({"tool": "first_alloc_probe", "tune": a.tune, "prealloc_gb": a.prealloc_gb, "keep": a.keep,
                       "swap": a.swap, "dummy_first": a.dummy_first, "mat_ptrs": ptrs,
                       "x": hex(x.values.parts[0].device_ptr()), "y": hex(y.values.parts[0].device_ptr()),
                       "ms": [round(float(np.median(v)), 4) for v in t]}))

@@ -24,7 +24,11 @@ def main():
     ap.add_argument("--rounds", type=int, default=4)
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--shape", default="1,1,1")
+    ap.add_argument("--tune", default="", help="pa_tune knobs before anything is built: key=v[,key=v]")
     a = ap.parse_args()
+    for kv in filter(None, a.tune.split(",")):
+        k, v = kv.split("=")
+        pamd._lib.tune(k, int(v))
     be = pamd.HIPBackend(devices=[0])
     shape = tuple(int(v) for v in a.shape.split(","))
     parts = be.get_part_ids(shape)
@@ -58,7 +62,7 @@ def main():
                 if ref is None:
                     ref = y.to_host().parts[0].copy()
     table = [[round(float(np.median(t[(i, j)])), 4) for j in range(a.k)] for i in range(a.k)]
-    print(json.dumps({"tool": "placement_matrix", "n": a.n, "shape": a.shape, "k": a.k,
+    print(json.dumps({"tool": "placement_matrix", "tune": a.tune, "n": a.n, "shape": a.shape, "k": a.k,
                       "ms_A_rows_x_cols": table,
                       "x_va": [hex(v.values.parts[0].device_ptr()) for v in xs],
                       "y_va": [hex(v.values.parts[0].device_ptr()) for v in ys]}))
