@@ -62,7 +62,12 @@ int g_spmv_merge = 1;     // pa_tune("spmv_merge"): one launch for every slice k
 int64_t g_spmv_merge_max = 65536;
 int g_halo_direct = 1;     // pa_tune("halo_direct"): grouped mul! pulls ghosts straight from the owners' x
 int g_halo_transport = 0;  // pa_tune("halo_transport"): 0 parts of this process by device reads, 1 RCCL for all
-int g_cg_fuse = 1;         // pa_tune("cg_fuse"): the device CG's u update inside the SpMV (XV kernels)
+// pa_tune("cg_fuse"): the device CG's u update inside the SpMV (XV kernels)
+// instead of its own sweep.  Off: steady-state iteration on FE27 256³, sweep
+// vs fused, on four boxes: 0.958 / 1.080, 0.947 / 0.973, 0.917 / 0.882,
+// whole call 1.043 / 1.075 ms (profiles/r03/s, final, f, d) — the fused
+// SpMV gathers two vectors (r and u_old) per x value.
+int g_cg_fuse = 0;
 int g_spmv_quadsort = 0;   // pa_tune("spmv_quadsort"): quad-sorted layout when most slices are not pattern slices
 int g_comm_cus = 0;   // pa_tune("comm_cus"): CUs reserved for the comm stream (0: priority stream instead)
 // COO → CSC → SELL on the device (pa_coo.hip)
@@ -1073,7 +1078,7 @@ int pa_tune(const char* key, int value, int* previous) {
     slot = &g_spmv_quadsort;
   } else if (!std::strcmp(key, "cg_fuse")) {
     CHECK_ARG(value == 0 || value == 1,
-              "cg_fuse: 1 = the device CG computes u = r .+ beta.*u inside the SpMV (default), 0 = a separate sweep");
+              "cg_fuse: 1 = the device CG computes u = r .+ beta.*u inside the SpMV, 0 = a separate sweep (default)");
     slot = &g_cg_fuse;
   } else if (!std::strcmp(key, "halo_direct")) {
     CHECK_ARG(value == 0 || value == 1,

@@ -214,6 +214,15 @@ def _stencil_rhs(pamd, A, dtype, seed):
     return pamd.PVector.from_host(pamd.map_parts(rnd, cols.partition), cols)
 
 
+@pytest.fixture(params=[0, 1], ids=["u_sweep", "u_in_spmv"])
+def cgfuse(request, pamd, be):
+    """Both device recurrences (pa_tune cg_fuse): u .= r .+ β.*u as its own
+    sweep (default) or evaluated inside the SpMV."""
+    prev = pamd._lib.tune("cg_fuse", request.param)
+    yield request.param
+    pamd._lib.tune("cg_fuse", prev)
+
+
 @pytest.mark.parametrize("shape,N,dtype,batch,maxiter", [
     ((2, 2, 1), (12, 10, 9), np.float64, 8, 40),    # 4 local parts: device gather kernel
     ((1, 1, 1), (9, 8, 7), np.float64, 3, 25),      # batch not dividing maxiter
@@ -221,7 +230,7 @@ def _stencil_rhs(pamd, A, dtype, seed):
     ((2, 1, 1), (9, 9, 9), np.float32, 4, 20),
     ((2, 2, 2), (8, 8, 8), np.complex64, 7, 20),
 ])
-def test_device_cg_equals_host_cg(be, pamd, O, shape, N, dtype, batch, maxiter):
+def test_device_cg_equals_host_cg(be, pamd, O, cgfuse, shape, N, dtype, batch, maxiter):
     """pa_cg_solve_all (scalars on the device, batched enqueue) reproduces the
     host-driven fused CG bit for bit: x, the residual history, and the
     iteration count (reltol = 0 → exactly maxiter iterations)."""
