@@ -492,6 +492,7 @@ def main():
     barrier()
     sync()
     c0 = ctxs[0]
+    comm0 = [c.comm_stats() for c in ctxs] if use_dist else None
     t0 = time.perf_counter()
     c0.span_start()  # HIP events on part 1's compute stream, over the timed region
     for i in range(args.steps):
@@ -509,6 +510,18 @@ def main():
         elapsed = float(t.item())
     ms_per_step = 1e3 * elapsed / args.steps
     value = B_all / (elapsed / args.steps) / 1e9
+    rccl = None
+    if use_dist:
+        # bytes this process posted to RCCL (ncclSend / ncclRecv of the halo
+        # segments) over the timed steps, summed over the ranks: the xGMI
+        # bytes of SURVEY.md §8d (n_rcv·S per GPU), reported beside `value`
+        sent = sum(c.comm_stats()[0] - a[0] for c, a in zip(ctxs, comm0))
+        recv = sum(c.comm_stats()[1] - a[1] for c, a in zip(ctxs, comm0))
+        t = torch.tensor([float(sent), float(recv)], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        rccl = {"bytes_sent_per_step_all_ranks": int(t[0].item()) // args.steps,
+                "bytes_recv_per_step_all_ranks": int(t[1].item()) // args.steps,
+                "gbs_all_ranks": round(float(t[1].item()) / elapsed / 1e9, 2)}
 
     # attribution (untimed calls): every local part's mul! phases, HIP events
     # on the stream the kernels run on, read after the last call (no
@@ -598,6 +611,7 @@ def main():
             "setup_s": round(t_setup, 2),
             "operator_copies_rotated": ncopies,
             "per_part_ms": per_part,
+            "rccl_halo": rccl,
         },
         "roofline": {
             "bound": "hbm",
