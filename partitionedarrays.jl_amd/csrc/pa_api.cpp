@@ -68,7 +68,6 @@ int g_halo_transport = 0;  // pa_tune("halo_transport"): 0 parts of this process
 // whole call 1.043 / 1.075 ms (profiles/r03/s, final, f, d) — the fused
 // SpMV gathers two vectors (r and u_old) per x value.
 int g_cg_fuse = 0;
-int g_f32_rows = 4;  // pa_tune("f32_rows_per_lane"): SELL rows per lane of Float32 matrices built afterwards
 int g_spmv_quadsort = 0;   // pa_tune("spmv_quadsort"): quad-sorted layout when most slices are not pattern slices
 int g_comm_cus = 0;   // pa_tune("comm_cus"): CUs reserved for the comm stream (0: priority stream instead)
 // COO → CSC → SELL on the device (pa_coo.hip)
@@ -1068,10 +1067,6 @@ int pa_tune(const char* key, int value, int* previous) {
               "spmv_short_occ: short-row F64 merged launch, 0 = one batch at 5 waves/SIMD (default), 1 = U 4 at 8, "
               "2 = U 4 at 6, 3 = one batch at 6");
     slot = &g_spmv_short_occ;
-  } else if (!std::strcmp(key, "f32_rows_per_lane")) {
-    CHECK_ARG(value == 2 || value == 4, "f32_rows_per_lane: 4 (16 B value loads, default) or 2 (8 B loads, twice "
-                                        "the waves) for Float32 matrices built afterwards");
-    slot = &g_f32_rows;
   } else if (!std::strcmp(key, "alloc_contiguous")) {
     CHECK_ARG(value == 0 || value == 1, "alloc_contiguous: 1 = large arrays in physically contiguous device memory "
                                         "(matrices and vectors created afterwards), 0 = hipMalloc (default)");

@@ -189,13 +189,10 @@ inline size_t dtype_size(int dt) {
   return 0;
 }
 
-// Rows per lane of the SELL layout so that one lane's value load is 16 B
-// (Float32: 4, or 2 with pa_tune("f32_rows_per_lane", 2): 8 B loads, half the
-// x gathers and registers per lane, twice the waves — for irregular parts).
-extern int g_f32_rows;
+// Rows per lane of the SELL layout so that one lane's value load is 16 B.
 inline int sell_rows_per_lane(int dt) {
   switch (dt) {
-    case PA_F32: return g_f32_rows;
+    case PA_F32: return 4;
     case PA_F64: return 2;
     case PA_C64: return 2;
     case PA_C128: return 1;

@@ -191,18 +191,12 @@ __device__ __forceinline__ c128 pick(bool c, c128 a, c128 b) { return c128{c ? a
 // dword-aligned: global loads need 4 B alignment); pa_vec pads 64 B on both
 // sides, so i in [-(R-1), n-1] stays inside the allocation
 typedef unsigned int u4a __attribute__((ext_vector_type(4))) __attribute__((aligned(4)));
-typedef unsigned int u2a __attribute__((ext_vector_type(2))) __attribute__((aligned(4)));
 template <typename T, int R>
 __device__ __forceinline__ Pack<T, R> ld_xrun(const T* p) {
-  static_assert(sizeof(Pack<T, R>) == 16 || sizeof(Pack<T, R>) == 8, "8 or 16 B runs");
+  static_assert(sizeof(Pack<T, R>) == 16, "16 B runs");
+  const u4a r = *reinterpret_cast<const u4a*>(p);
   Pack<T, R> v;
-  if constexpr (sizeof(Pack<T, R>) == 16) {
-    const u4a r = *reinterpret_cast<const u4a*>(p);
-    __builtin_memcpy(&v, &r, 16);
-  } else {  // Float32 with 2 rows per lane
-    const u2a r = *reinterpret_cast<const u2a*>(p);
-    __builtin_memcpy(&v, &r, 8);
-  }
+  __builtin_memcpy(&v, &r, 16);
   return v;
 }
 
@@ -1130,9 +1124,6 @@ constexpr int kDtR = 1;
 #endif
 void PA_CAT(spmv_group_, PA_SPMV_DT)(int which, int np, const SpmvPart* parts, bool has_alpha, int bmode,
                                      const void* alpha, const void* beta, hipStream_t st) {
-#if PA_SPMV_DT == 0
-  if (parts[0].A->R == 2) return group_which<float, 2>(which, np, parts, has_alpha, bmode, alpha, beta, st);
-#endif
   group_which<DtT, kDtR>(which, np, parts, has_alpha, bmode, alpha, beta, st);
 }
 #else
@@ -1336,9 +1327,6 @@ static int merged_t(int n, const int* which, const SpmvPart* parts, bool has_alp
 int PA_CAT(spmv_merged_, PA_SPMV_DT)(int n, const int* which, const SpmvPart* parts, bool has_alpha, int bmode,
                                      const void* alpha, const void* beta, pa_ctx* owner, std::vector<void*>* pinned,
                                      hipStream_t st) {
-#if PA_SPMV_DT == 0
-  if (parts[0].A->R == 2) return merged_t<float, 2>(n, which, parts, has_alpha, bmode, alpha, beta, owner, pinned, st);
-#endif
   return merged_t<DtT, kDtR>(n, which, parts, has_alpha, bmode, alpha, beta, owner, pinned, st);
 }
 #else
@@ -1540,9 +1528,6 @@ void PA_CAT(spmv_long_, PA_SPMV_DT)(const pa_mat* A, const void* x, void* y, con
 void PA_CAT(spmv_part_, PA_SPMV_DT)(int which, int64_t nwork, const int32_t* list, const pa_mat* A, const void* x,
                                     void* y, const int32_t* ymap, bool has_alpha, int bmode, const void* alpha,
                                     const void* beta, void* dotp, hipStream_t st, const SpmvPart* cgp) {
-#if PA_SPMV_DT == 0
-  if (A->R == 2) return launch_which<float, 2>(which, nwork, list, A, x, y, ymap, has_alpha, bmode, alpha, beta, dotp, st, cgp);
-#endif
   launch_which<DtT, kDtR>(which, nwork, list, A, x, y, ymap, has_alpha, bmode, alpha, beta, dotp, st, cgp);
 }
 #else
@@ -2357,7 +2342,7 @@ void launch_quad_permute(const pa_mat* A, int64_t nslices_new, const int32_t* pe
 #define PA_QP(T, RR) hipLaunchKernelGGL((k_quad_permute<T, RR>), g, b, 0, st, n, perm, nsoff, nslen, osoff, oslen, \
                                         ocol, (const T*)oval, ncol, (T*)nval)
   switch (A->dtype) {
-    case PA_F32: if (A->R == 2) PA_QP(float, 2); else PA_QP(float, 4); break;
+    case PA_F32: PA_QP(float, 4); break;
     case PA_F64: PA_QP(double, 2); break;
     case PA_C64: PA_QP(c64, 2); break;
     case PA_C128: PA_QP(c128, 1); break;
@@ -2467,10 +2452,7 @@ static void side_fill_t(pa_mat* A, const int32_t* rows, const int32_t* len, hipS
 
 void launch_side_fill(pa_mat* A, const int32_t* rows, const int32_t* len, hipStream_t st) {
   switch (A->dtype) {
-    case PA_F32:
-      if (A->R == 2) side_fill_t<float, 2>(A, rows, len, st);
-      else side_fill_t<float, 4>(A, rows, len, st);
-      break;
+    case PA_F32: side_fill_t<float, 4>(A, rows, len, st); break;
     case PA_F64: side_fill_t<double, 2>(A, rows, len, st); break;
     case PA_C64: side_fill_t<c64, 2>(A, rows, len, st); break;
     case PA_C128: side_fill_t<c128, 1>(A, rows, len, st); break;
