@@ -1077,8 +1077,9 @@ int pa_tune(const char* key, int value, int* previous) {
               "(default; matrices built afterwards), 2 = every matrix (tests), 0 = off");
     slot = &g_spmv_quadsort;
   } else if (!std::strcmp(key, "cg_fuse")) {
-    CHECK_ARG(value == 0 || value == 1,
-              "cg_fuse: 1 = the device CG computes u = r .+ beta.*u inside the SpMV, 0 = a separate sweep (default)");
+    CHECK_ARG(value >= 0 && value <= 2,
+              "cg_fuse: 1 = the device CG computes u = r .+ beta.*u inside the SpMV, 0 = a separate sweep (default), "
+              "2 = auto (one batch of each, then the faster; all parts in one process)");
     slot = &g_cg_fuse;
   } else if (!std::strcmp(key, "halo_direct")) {
     CHECK_ARG(value == 0 || value == 1,
@@ -3565,45 +3566,72 @@ int pa_cg_solve_all(int n, pa_mat* const A[], pa_vec* const x[], const pa_vec* c
   // one part in this process and no other process: the folds end in the
   // scalar updates themselves (no gather, no scalar kernels)
   const bool tail = !R.remote && R.P == 1;
-  // fused u update (pa_tune cg_fuse): u .= r .+ β.*u inside the SpMV, u in
-  // two buffers (iteration t reads ub[t%2], writes ub[(t+1)%2]); the deferred
-  // x .+= α.*u rides along.  Not for matrices with long rows (their kernel
-  // gathers x directly).
-  bool fuse = g_cg_fuse != 0;
-  for (int i = 0; i < n; ++i) fuse = fuse && A[i]->n_long == 0;
+  // The u update (pa_tune cg_fuse): 0 its own sweep, in place on u; 1 inside
+  // the SpMV, u = r .+ β.*u_old evaluated per gathered element (the halo
+  // carries r), u in two buffers (an iteration reads ucur, writes uoth, then
+  // they swap), the deferred x .+= α.*u riding along; 2 auto: with all parts
+  // in this process and at least three batches, the first batch runs the
+  // sweep, the second the fused update, the rest the faster of the two (HIP
+  // events on part 1's stream), remembered on the matrix.  The variants give
+  // the same values bit for bit, so switching between batches changes no
+  // result.  Fused: not for matrices with long rows (their kernel gathers x
+  // directly).
+  bool can_fuse = true;
+  for (int i = 0; i < n; ++i) can_fuse = can_fuse && A[i]->n_long == 0;
+  int mode = can_fuse ? g_cg_fuse : 0;
+  if (mode == 2 && (R.remote || maxiter < 3 * (int64_t)batch)) mode = A[0]->cg_fuse_choice >= 0 ? A[0]->cg_fuse_choice : 0;
+  if (mode == 2 && A[0]->cg_fuse_choice >= 0) mode = A[0]->cg_fuse_choice;
   std::vector<pa_vec*> u2(n, nullptr);
   struct U2Free {
     std::vector<pa_vec*>& v;
     ~U2Free() { for (pa_vec* p : v) if (p) pa_vec_destroy(p); }
   } u2_free{u2};
-  if (fuse)
+  if (mode != 0)
     for (int i = 0; i < n; ++i)
       if (pa_vec_create(R.ctxs[i], dt, u[i]->n, &u2[i])) return -1;
-  auto ubuf = [&](int64_t t, int i) -> void* { return (t % 2 == 0) ? u[i]->d : u2[i]->d; };
-  int64_t enqueued = 0;
+  std::vector<pa_vec*> ucur(u, u + n), uoth(u2);
+  hipEvent_t tev[2] = {nullptr, nullptr};
+  struct EvFree {
+    hipEvent_t* e;
+    ~EvFree() { for (int j = 0; j < 2; ++j) if (e[j]) (void)hipEventDestroy(e[j]); }
+  } ev_free{tev};
+  if (mode == 2) {
+    HIPC(hipSetDevice(R.ctxs[0]->device));
+    HIPC(hipEventCreate(&tev[0]));
+    HIPC(hipEventCreate(&tev[1]));
+  }
+  float batch_ms[2] = {0.f, 0.f};
+  int64_t enqueued = 0, nbatch = 0;
   bool done = h.done != 0;
   while (!done && enqueued < maxiter) {
     const int64_t k = std::min<int64_t>(batch, maxiter - enqueued);  // the same on every rank
+    const int variant = mode == 2 ? (nbatch < 2 ? (int)nbatch : A[0]->cg_fuse_choice) : mode;
+    const bool timed = mode == 2 && nbatch < 2;
+    if (timed) {
+      HIPC(hipSetDevice(R.ctxs[0]->device));
+      HIPC(hipEventRecord(tev[0], R.ctxs[0]->s_main));
+    }
     for (int64_t t = 0; t < k; ++t) {
-      if (fuse) {
+      if (variant == 1) {
         // mul!(c, A, u) with u = r .+ β.*u_old evaluated inside the SpMV (its
         // halo carries r), the owned u written, x .+= α.*u_old of the
         // previous iteration applied; dot(u, c) accumulated by the SpMV
         CGFuse fz;
         for (int i = 0; i < n; ++i) {
-          fz.u_old.push_back(ubuf(enqueued + t, i));
-          fz.u_new.push_back(ubuf(enqueued + t + 1, i));
+          fz.u_old.push_back(ucur[i]->d);
+          fz.u_new.push_back(uoth[i]->d);
           fz.xacc.push_back(x[i]->d);
           fz.st.push_back(R.st[i]);
         }
         if (spmv_impl(n, A, c, idx, r, idx, xg, one, zero, true, tail ? R.st.data() : nullptr, &fz)) return -1;
+        std::swap(ucur, uoth);
       } else {
         for (int i = 0; i < n; ++i) {  // (x .+= α.*u of the previous iteration); u .= r .+ β.*u
           HIPC(hipSetDevice(R.ctxs[i]->device));
-          launch_cg_xu(dt, u[i]->n, x[i]->d, u[i]->d, r[i]->d, R.st[i], R.ctxs[i]->s_main);
+          launch_cg_xu(dt, ucur[i]->n, x[i]->d, ucur[i]->d, r[i]->d, R.st[i], R.ctxs[i]->s_main);
         }
         // mul!(c, A, u) with dot(u, c) accumulated by the SpMV; α = residual² / dot(u, c)
-        if (spmv_impl(n, A, c, idx, u, idx, xg, one, zero, true, tail ? R.st.data() : nullptr)) return -1;
+        if (spmv_impl(n, A, c, idx, ucur.data(), idx, xg, one, zero, true, tail ? R.st.data() : nullptr)) return -1;
       }
       if (!tail) {
         if (cg_gather(R, accsz)) return -1;
@@ -3638,6 +3666,7 @@ int pa_cg_solve_all(int n, pa_mat* const A[], pa_vec* const x[], const pa_vec* c
     // every part holds the same state; read part 0's
     pa_ctx* c0 = R.ctxs[0];
     HIPC(hipSetDevice(c0->device));
+    if (timed) HIPC(hipEventRecord(tev[1], c0->s_main));
     HIPC(hipMemcpyAsync(c0->h_pinned, R.st[0], sizeof(CGState), hipMemcpyDeviceToHost, c0->s_main));
     for (int i = 0; i < n; ++i) {
       HIPC(hipSetDevice(R.ctxs[i]->device));
@@ -3645,11 +3674,18 @@ int pa_cg_solve_all(int n, pa_mat* const A[], pa_vec* const x[], const pa_vec* c
     }
     std::memcpy(&h, c0->h_pinned, sizeof(CGState));
     done = h.done != 0;
+    if (timed) {
+      float ms = 0.f;
+      HIPC(hipEventElapsedTime(&ms, tev[0], tev[1]));
+      batch_ms[nbatch] = ms / (float)k;
+      if (nbatch == 1) A[0]->cg_fuse_choice = batch_ms[1] < batch_ms[0] ? 1 : 0;
+    }
+    ++nbatch;
   }
   if (h.it > h.xit) {  // the last iteration's deferred x .+= α.*u (u untouched: done)
     for (int i = 0; i < n; ++i) {
       HIPC(hipSetDevice(R.ctxs[i]->device));
-      launch_cg_xu(dt, u[i]->n, x[i]->d, fuse ? ubuf(enqueued, i) : u[i]->d, r[i]->d, R.st[i], R.ctxs[i]->s_main);
+      launch_cg_xu(dt, ucur[i]->n, x[i]->d, ucur[i]->d, r[i]->d, R.st[i], R.ctxs[i]->s_main);
     }
     for (int i = 0; i < n; ++i) {
       HIPC(hipSetDevice(R.ctxs[i]->device));

@@ -399,6 +399,7 @@ struct pa_vec {
 struct pa_mat {
   pa_ctx* ctx = nullptr;
   int dtype = PA_F64;
+  int cg_fuse_choice = -1;   // device CG with cg_fuse 2 (auto): the faster u-update variant measured on this matrix
   int R = 2;                 // rows per lane
   int H = 128;               // rows per slice = 64*R
   int64_t nrows = 0;         // owned rows

@@ -214,10 +214,11 @@ def _stencil_rhs(pamd, A, dtype, seed):
     return pamd.PVector.from_host(pamd.map_parts(rnd, cols.partition), cols)
 
 
-@pytest.fixture(params=[0, 1], ids=["u_sweep", "u_in_spmv"])
+@pytest.fixture(params=[0, 1, 2], ids=["u_sweep", "u_in_spmv", "u_auto"])
 def cgfuse(request, pamd, be):
-    """Both device recurrences (pa_tune cg_fuse): u .= r .+ β.*u as its own
-    sweep (default) or evaluated inside the SpMV."""
+    """Every device recurrence (pa_tune cg_fuse): u .= r .+ β.*u as its own
+    sweep (default), evaluated inside the SpMV, or auto (one batch of each,
+    then the faster: the switch between batches changes no value)."""
     prev = pamd._lib.tune("cg_fuse", request.param)
     yield request.param
     pamd._lib.tune("cg_fuse", prev)
