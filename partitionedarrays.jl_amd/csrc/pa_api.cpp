@@ -66,8 +66,9 @@ int g_halo_transport = 0;  // pa_tune("halo_transport"): 0 parts of this process
 // instead of its own sweep.  Off: steady-state iteration on FE27 256³, sweep
 // vs fused, on four boxes: 0.958 / 1.080, 0.947 / 0.973, 0.917 / 0.882,
 // whole call 1.043 / 1.075 ms (profiles/r03/s, final, f, d) — the fused
-// SpMV gathers two vectors (r and u_old) per x value.
-int g_cg_fuse = 0;
+// SpMV gathers two vectors (r and u_old) per x value — so the default is 2:
+// measure one batch of each on this box and keep the faster (pa_cg_solve_all).
+int g_cg_fuse = 2;
 int g_spmv_quadsort = 0;   // pa_tune("spmv_quadsort"): quad-sorted layout when most slices are not pattern slices
 int g_comm_cus = 0;   // pa_tune("comm_cus"): CUs reserved for the comm stream (0: priority stream instead)
 // COO → CSC → SELL on the device (pa_coo.hip)
@@ -1078,8 +1079,8 @@ int pa_tune(const char* key, int value, int* previous) {
     slot = &g_spmv_quadsort;
   } else if (!std::strcmp(key, "cg_fuse")) {
     CHECK_ARG(value >= 0 && value <= 2,
-              "cg_fuse: 1 = the device CG computes u = r .+ beta.*u inside the SpMV, 0 = a separate sweep (default), "
-              "2 = auto (one batch of each, then the faster; all parts in one process)");
+              "cg_fuse: 1 = the device CG computes u = r .+ beta.*u inside the SpMV, 0 = a separate sweep, "
+              "2 = auto (default: one batch of each, then the faster; all parts in one process, else the sweep)");
     slot = &g_cg_fuse;
   } else if (!std::strcmp(key, "halo_direct")) {
     CHECK_ARG(value == 0 || value == 1,
