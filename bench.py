@@ -110,17 +110,23 @@ def cpu_baseline_mpi(kind, dims, shape, seconds=12.0):
 PROBE_BYTES = 1 << 30
 
 
-def pmc_traffic(args, steps=5):
+# the kernels of one mul! step (SpMV slices, halo pull / pack / unpack)
+PMC_KERNELS = ("k_spmv_sell", "k_spmv_merged", "k_pull_", "k_pack", "k_unpack")
+
+
+def pmc_traffic(args, steps=5, halo=False):
     """HBM bytes per mul! step from rocprofv3 PMC counters, one counter per
     pass (MI355X_MICROARCH.md §HBM / §rocprofv3): FETCH_SIZE (KB) and
-    WRITE_SIZE (KB) summed over the SpMV kernels of the profiled steps /
-    steps.  FETCH_SIZE under-counts wide coalesced streaming reads on gfx950
+    WRITE_SIZE (KB) summed over the kernels of the profiled steps (SpMV
+    slices, and with halo=True the halo leg's pulls) / steps.  FETCH_SIZE
+    under-counts wide coalesced streaming reads on gfx950
     (MI355X_MICROARCH.md: by 1/2); the factor is calibrated in the same
     profiled process on k_probe_read launches that read a known 1 GiB with
     the SpMV's own 16 B-per-lane non-temporal loads, and applied to the
     SpMV's fetches (its loads are 16 B per lane: values, pattern rows' x
     runs; the side rows' 4-8 B gathers are split out in the note).  Runs
-    this script as the profiled child (`--child-pmc`)."""
+    this script as the profiled child (`--child-pmc`, `--child-halo` for
+    the halo leg's (2,2,2) operator)."""
     import csv
     import shutil
     import signal
@@ -132,7 +138,7 @@ def pmc_traffic(args, steps=5):
         d = tempfile.mkdtemp(prefix="pa_pmc_", dir="/tmp")
         cmd = ["rocprofv3", "--pmc", ctr, "-d", d, "-o", "pmc", "--output-format", "csv", "--",
                sys.executable, os.path.abspath(__file__), "--child-pmc", "--steps", str(steps),
-               "--n", str(args.n), "--kind", str(args.kind), "--dtype", args.dtype]
+               "--n", str(args.n), "--kind", str(args.kind), "--dtype", args.dtype] + (["--child-halo"] if halo else [])
         p = subprocess.Popen(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL, start_new_session=True,
                              env=dict(os.environ, TMPDIR="/tmp"))
         try:
@@ -145,8 +151,7 @@ def pmc_traffic(args, steps=5):
             return None, f"rocprofv3 --pmc {ctr} failed (rc {p.returncode})"
         rows = list(csv.DictReader(open(files[0])))
         vals = [float(r["Counter_Value"]) for r in rows
-                if ("k_spmv_sell" in r["Kernel_Name"] or "k_spmv_merged" in r["Kernel_Name"])
-                and r["Counter_Name"] == ctr]
+                if any(k in r["Kernel_Name"] for k in PMC_KERNELS) and r["Counter_Name"] == ctr]
         tot[ctr] = sum(vals) / (steps + 1)  # warmup step + steps
         if ctr == "FETCH_SIZE":
             probe = [float(r["Counter_Value"]) for r in rows
@@ -173,10 +178,12 @@ def box_hbm_gbs(pamd, nbytes, reps=10):
 
 
 def child_pmc(args):
-    """the profiled child of pmc_traffic: build the operator, run warmup+steps."""
+    """the profiled child of pmc_traffic: build the operator (the headline's
+    one part, or with --child-halo the halo leg's (2,2,2) parts of the same
+    global operator on the one GPU), run warmup+steps."""
     import pamd
     be = pamd.HIPBackend(devices=[0])
-    parts = be.get_part_ids((1, 1, 1))
+    parts = be.get_part_ids((2, 2, 2) if args.child_halo else (1, 1, 1))
     dtype = DTYPES[args.dtype]
     A = pamd.drivers.stencil_operator(parts, (args.n,) * 3, args.kind, dtype)
     x = pamd.PVector.from_host(pamd.map_parts(
@@ -185,7 +192,8 @@ def child_pmc(args):
     y = pamd.PVector.undef(A.rows, dtype)
     for _ in range(args.steps + 1):
         pamd.mul_(y, A, x)
-    be.context(1).sync()
+    for p in parts.part_ids:
+        be.context(p).sync()
     # FETCH_SIZE calibration: read sweeps of a known PROBE_BYTES
     pamd._lib.hbm_probe(0, PROBE_BYTES, 1)
 
@@ -368,6 +376,20 @@ def cg_mode(args, pamd, backend, parts, A, ngpu, use_dist, sync):
     return line
 
 
+def launch_ranks(n):
+    """Run this script under torch.distributed.run with n ranks (one part and
+    one GPU per rank, HIPDistributedBackend) as a child process; rank 0
+    prints the JSON line to the inherited stdout."""
+    import socket
+    with socket.socket() as s:  # a free rendezvous port on the loopback
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", str(n),
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__), *sys.argv[1:]]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
+    return subprocess.run(cmd, env=env).returncode
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -384,6 +406,7 @@ def main():
     ap.add_argument("--no-halo-leg", action="store_true",
                     help="skip the halo_1gpu object (config 3 on (2,2,2) parts of the one GPU)")
     ap.add_argument("--child-pmc", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--child-halo", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--cg", type=int, default=0, help="time K CG iterations instead (own JSON line)")
     ap.add_argument("--distributed", action="store_true",
                     help="one part per process (HIPDistributedBackend, RCCL) even for one process: "
@@ -391,6 +414,13 @@ def main():
     args = ap.parse_args()
     if args.child_pmc:
         return child_pmc(args)
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # `python bench.py --gpus N` (no torchrun around it): start the N
+        # one-part-per-GPU ranks ourselves, as the driver's torchrun command
+        # does, before this process touches the GPU (no HIP call, no torch
+        # import above this line), and pass their exit status on.  One
+        # process per GPU keeps every rank's host issue to its own part.
+        return launch_ranks(args.gpus)
     # stdout carries exactly one JSON line (rank 0): native libraries print
     # banners to fd 1 during init (RCCL's version block, gloo's connection
     # line), so fd 1 points at stderr until the line is written
@@ -577,6 +607,22 @@ def main():
         traffic, tnote = pmc_traffic(args)
         if traffic is None:
             tnote = {"note": tnote}
+        if halo_leg is not None:
+            # the halo leg's HBM bytes from the same counters (all 8 parts'
+            # SpMV and pull kernels of a step), beside its format bytes
+            ht, hnote = pmc_traffic(args, halo=True)
+            hr = halo_leg["roofline"] = {"bound": "hbm", "achieved": halo_leg["value"], "peak": HBM_PEAK_GBS,
+                                         "unit": "GB/s", "frac": halo_leg["frac"],
+                                         "traffic": None if ht is None else int(ht),
+                                         "traffic_detail": hnote if ht is not None else {"note": hnote}}
+            if ht is not None:
+                k_s = halo_leg["kernel_ms"] * 1e-3
+                hr["actual_hbm_gbs"] = round(ht / k_s / 1e9, 1)
+                hr["actual_frac"] = round(ht / k_s / 1e9 / HBM_PEAK_GBS, 4)
+                hr["traffic_over_bytes"] = round(ht / halo_leg["bytes_per_step"], 4)
+                hr["note"] = ("format bytes count x once per part: with the parts' x and y (2 x 134 MB) "
+                              "partly held in the 256 MB MALL across steps, HBM traffic can sit below them; "
+                              "actual_frac is the counter-based fraction")
     halo = s_nhids > 0
     line = {
         "metric": "SpMV+halo GB/s (frac of HBM peak), 3D Poisson 27-pt, 1/2/4/8 MI355X",
@@ -665,4 +711,4 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main() or 0)

@@ -52,34 +52,27 @@ const char* pa_last_error(void);
 int pa_version(void);
 /* number of visible HIP devices (0 when no GPU). */
 int pa_device_count(int* count);
-/* Process-wide kernel tuning knobs (performance only, results unchanged):
- * "spmv_flags"  bit 0: non-temporal value/column streams, bit 1: XCD-aware
- *               slice mapping, bit 2: pattern rows fetch x as 16 B runs,
- *               bit 3: the last len % U entries of a slice as one
- *               predicated batch, bit 4: a slice list covering the whole
- *               structure is launched without the list, bit 5: y written
- *               with non-temporal stores, bit 6: launches whose rows have
- *               at most 8 entries use the short-row kernels (one predicated
- *               batch, no loop: fewer registers) (default 93);
- * "spmv_unroll" 4 or 8 entries in flight per lane in the merged launch
- *               (default 8; the per-kind launches use 8);
- * "spmv_short_occ" short-row F64 merged launch: 0 one predicated batch at
- *               5 waves/SIMD (default), 1 U = 4 at 8, 2 U = 4 at 6, 3 one
- *               batch at 6;
+/* Process-wide tuning knobs (performance only, results unchanged); each is
+ * an A/B lever kept because a configuration uses it or a test pins it:
+ * "spmv_flags"  bit 0: non-temporal value/column streams, bit 2: pattern
+ *               rows fetch x as 16 B runs, bit 3: the last len % U entries
+ *               of a slice as one predicated batch, bit 4: a slice list
+ *               covering the whole structure is launched without the list,
+ *               bit 5: y written with non-temporal stores, bit 6: launches
+ *               whose rows have at most 8 entries use the short-row kernels
+ *               (one predicated batch, no loop: fewer registers) (default 93);
  * "spmv_format" 1: pattern slices where the matrix has them (default),
  *               0: int32 column ids everywhere;
- * "spmv_patterns" 1..4 offset patterns per slice for matrices built
- *               afterwards (default 1: single-pattern slices; >1:
- *               multi-pattern slices where they save bytes);
- * "spmv_pattern_rule" 1: each slice takes the encoding that streams the
- *               fewest bytes, 0: a pattern slice whenever half its rows
- *               follow the pattern (default; matrices built afterwards);
  * "long_rows_exact" 1: long rows summed in the reference's order (default),
  *               0: lane-strided partial sums + tree (within 1e-12);
  * "halo_pull"   1: parts of one process read their neighbours' packed
  *               buffers directly (default), 0: staging copies;
  * "spmv_delta16" 1: int32-column slices whose columns fit 16-bit codes
  *               store those (matrices built afterwards; default), 0: off;
+ * "spmv_merge"  1: every slice kind of every part of a mul! without a halo
+ *               in flight as one launch (default), 0: one launch per kind;
+ * "spmv_merge_max" parts with more slices than this run one launch per
+ *               kind (default 65536; 0: no limit);
  * "halo_direct" 1: mul! over parts sharing a stream pair reads every ghost
  *               straight from its owner's x on the compute stream (no
  *               pack, no cross-stream event; default), 0: pack + pull on
@@ -88,16 +81,13 @@ int pa_device_count(int* count);
  *               reads/copies, except parts whose communicator came from
  *               pa_comm_init_all (RCCL, per context); 1: RCCL send/recv for
  *               every part that has a communicator;
- * "spmv_quadsort" 1: a matrix with fewer than 90 % pattern slices
- *               (irregular partitions) gets the quad-sorted layout: lanes
- *               of R consecutive rows ordered so that whole slices become
- *               pattern or quad-run slices (default; matrices built
- *               afterwards), 2: every matrix (tests), 0: off;
- * "cg_fuse"     1: the device CG evaluates u .= r .+ beta.*u inside the
- *               SpMV (default), 0: as its own sweep;
+ * "cg_fuse"     0: the device CG's u .= r .+ beta.*u as its own sweep,
+ *               1: inside the SpMV (XV kernels), 2 (default, auto): with
+ *               all parts in one process and at least three batches, one
+ *               batch of each, then the faster (remembered on the matrix);
+ *               otherwise the sweep or the matrix's earlier choice;
  * "spmv_group"  1: the parts of one process sharing a stream pair run each
- *               mul! phase as one launch (default), 0: launches per part;
- * "spmv_lds", "comm_cus": occupancy / CU-mask experiments (default 0).    */
+ *               mul! phase as one launch (default), 0: launches per part. */
 int pa_tune(const char* key, int value, int* previous);
 /* HBM calibration of `device` (not the hot path): best read-only and copy
  * rates (GB/s, read+write bytes for the copy; best of 4/8 loads in flight
@@ -339,21 +329,11 @@ int pa_mat_info(const pa_mat* A, int64_t* nrows_owned, int64_t* nnz_owned,
 int pa_mat_format_info(const pa_mat* A, int64_t* pattern_slices,
                        int64_t* regular_rows, int64_t* side_rows,
                        int64_t* side_slots);
-/* Of those pattern slices, the ones holding several offset patterns (one
- * chosen per 64-lane group of rows; irregular partitions whose runs of
- * consecutive rows are shorter than a slice); 0 unless
- * pa_tune("spmv_patterns", n > 1) preceded the build.                     */
-int pa_mat_multipattern_info(const pa_mat* A, int64_t* multi_slices);
 /* delta16 slices (pa_tune "spmv_delta16", default on): int32-column slices
  * whose columns all fit 16-bit codes — an owned column as the row + a
  * signed 15-bit delta, a ghost column as the slice's smallest ghost column
  * + 15 bits — stream 2 B of column id per slot instead of 4.              */
 int pa_mat_delta16_info(const pa_mat* A, int64_t* delta16_slices);
-/* Quad-run slices (kind 4: every lane's R rows read R consecutive columns,
- * one column per entry and lane) and whether the layout is quad-sorted
- * (lanes of R consecutive rows ordered by class, irregular partitions;
- * pa_tune "spmv_quadsort").  Encoding only: results are unchanged.       */
-int pa_mat_quadrun_info(const pa_mat* A, int64_t* quadrun_slices, int* quad_sorted);
 
 /* device addresses of the matrix's main arrays, for placement diagnostics:
  * out[0..7] = values, int32 columns, slice offsets, slice lengths (pattern),

@@ -30,7 +30,7 @@ void launch_spmv_part(int which, int64_t nwork, const int32_t* list, const pa_ma
                       const SpmvPart* cgp = nullptr);
 void launch_delta16(pa_mat* A, int64_t noids, const int32_t* kind, int32_t* ok, hipStream_t st);
 void launch_pattern_detect(pa_mat* A, int64_t noids, int32_t* kind, int32_t* plen, int32_t* pat,
-                           uint64_t* mask, int32_t* pghost, int32_t* nirreg, int NP, int rule, hipStream_t st);
+                           uint64_t* mask, int32_t* pghost, int32_t* nirreg, hipStream_t st);
 void launch_side_len(pa_mat* A, int64_t n, const int32_t* rows, int32_t* len, int64_t noids,
                      int32_t* sghost, hipStream_t st);
 void launch_side_fill(pa_mat* A, const int32_t* rows, const int32_t* len, hipStream_t st);
@@ -48,8 +48,6 @@ void launch_cg_alpha(int dtype, int P, const void* gathered, CGState* cst, hipSt
 void launch_cg_step(int dtype, int P, const double* gathered, CGState* cst, double* history, hipStream_t st);
 void launch_gather_ptrs(int P, const void* const* srcs, int accsz, void* out, hipStream_t st);
 extern int g_spmv_format;
-extern int g_spmv_pattern_rule;
-extern int g_spmv_patterns;  // patterns per slice at build time (1: single-pattern slices only)
 int g_halo_pull = 1;  // pa_tune("halo_pull"): pull-unpack between parts of one process
 int g_spmv_group = 1; // pa_tune("spmv_group"): one launch per phase for the parts sharing a stream pair
 int g_spmv_delta16 = 1;   // pa_tune("spmv_delta16"): int32-column slices with 16-bit column codes where they fit
@@ -69,8 +67,6 @@ int g_halo_transport = 0;  // pa_tune("halo_transport"): 0 parts of this process
 // SpMV gathers two vectors (r and u_old) per x value — so the default is 2:
 // measure one batch of each on this box and keep the faster (pa_cg_solve_all).
 int g_cg_fuse = 2;
-int g_spmv_quadsort = 0;   // pa_tune("spmv_quadsort"): quad-sorted layout when most slices are not pattern slices
-int g_comm_cus = 0;   // pa_tune("comm_cus"): CUs reserved for the comm stream (0: priority stream instead)
 // COO → CSC → SELL on the device (pa_coo.hip)
 int coo_compress(int dtype, int index_bytes, int64_t m, int64_t ncols, int64_t n, const void* dI, const void* dJ,
                  const void* dV, int csr, int64_t* nu_out, int32_t** crow, int32_t** ccol, void** cval,
@@ -125,19 +121,8 @@ void launch_stencil_count(const StencilGeom& g, const int32_t* shell, const doub
 void launch_stencil_fill(const StencilGeom& g, const int32_t* shell, const double* coef,
                          int64_t nrows, int noids, pa_mat* A, int32_t* err, hipStream_t st);
 void launch_probe(int copy, int unroll, int64_t n16, const void* a, void* b, int blocks, hipStream_t st);
-void launch_pattern_triples(const pa_mat* A, uint8_t* tri, hipStream_t st);
-void launch_quad_class(const pa_mat* A, int64_t noids, int32_t* qlen, uint8_t* qflag, uint64_t* qhash, hipStream_t st);
-void launch_quad_permute(const pa_mat* A, int64_t nslices_new, const int32_t* perm, const int64_t* nsoff,
-                         const int32_t* nslen, const int64_t* osoff, const int32_t* oslen, const int32_t* ocol,
-                         const void* oval, int32_t* ncol, void* nval, hipStream_t st);
-void launch_nzslot_remap(int64_t nu, int64_t* nzs, int64_t oslots, int64_t ons, const int64_t* osoff, int H, int R,
-                         const int32_t* inv, const int64_t* nsoff, hipStream_t st);
-void launch_qrun_detect(const pa_mat* A, const int32_t* kind, int32_t* qcol, int32_t* ok, hipStream_t st);
 extern int g_spmv_flags;
-extern int g_spmv_unroll;
-extern int g_spmv_lds;
 extern int g_long_exact;
-extern int g_spmv_short_occ;
 
 }  // namespace pa
 
@@ -181,21 +166,6 @@ int dev_upload(T** dptr, const std::vector<T>& h) {
   HIPC(hipMalloc((void**)dptr, h.size() * sizeof(T)));
   HIPC(hipMemcpy(*dptr, h.data(), h.size() * sizeof(T), hipMemcpyHostToDevice));
   return 0;
-}
-
-// pa_tune("alloc_contiguous"): the large arrays (matrix values and column
-// ids, vectors) of matrices and vectors created afterwards are allocated in
-// physically contiguous device memory (hipDeviceMallocContiguous), falling
-// back to hipMalloc when that fails.  An experiment on the placement spread
-// of DESIGN.md §4.1: off by default.
-int g_alloc_contig = 0;
-hipError_t big_malloc(void** p, size_t bytes) {
-  if (g_alloc_contig && bytes >= ((size_t)64 << 20)) {
-    const hipError_t e = hipExtMallocWithFlags(p, bytes, hipDeviceMallocContiguous);
-    if (e == hipSuccess) return e;
-    (void)hipGetLastError();
-  }
-  return hipMalloc(p, bytes);
 }
 
 void dev_free(void* p) {
@@ -329,117 +299,8 @@ int finish_sell_layout(pa_mat* A, const std::vector<int32_t>& slen, const std::v
   return 0;
 }
 
-// Quad sort of the int32 layout: lanes (quads of R
-// consecutive owned rows) ordered by class — quad-run lanes without ghost
-// columns, quad-run lanes reading ghosts (each grouped by their column
-// offsets, so equal patterns share slices), then the other lanes without /
-// with ghost columns, in oid order inside a class — and a partial last quad
-// (nrows % R rows) at the very end, so that the valid rows of every slice
-// stay a prefix of its positions.  Values and columns move with their
-// lanes; every row keeps its entries in order, and the CSC nz → slot map
-// follows.  Sets qmap; the caller redoes the encodings on the new layout.
-int quad_sort(pa_mat* A, int64_t noids) {
-  const int R = A->R, H = A->H;
-  const int64_t nq = (A->nrows + R - 1) / R, ons = A->nslices, oslots = A->slots;
-  const size_t S = dtype_size(A->dtype);
-  hipStream_t st = A->ctx->s_main;
-  if (nq == 0) return 0;
-  int32_t* d_qlen = nullptr;
-  uint8_t* d_qflag = nullptr;
-  uint64_t* d_qhash = nullptr;
-  HIPC(hipMalloc((void**)&d_qlen, nq * 4));
-  HIPC(hipMalloc((void**)&d_qflag, nq));
-  HIPC(hipMalloc((void**)&d_qhash, nq * 8));
-  launch_quad_class(A, noids, d_qlen, d_qflag, d_qhash, st);
-  HIPC(hipGetLastError());
-  std::vector<int32_t> qlen(nq);
-  std::vector<uint8_t> qflag(nq);
-  std::vector<uint64_t> qhash(nq);
-  HIPC(hipMemcpyAsync(qlen.data(), d_qlen, nq * 4, hipMemcpyDeviceToHost, st));
-  HIPC(hipMemcpyAsync(qflag.data(), d_qflag, nq, hipMemcpyDeviceToHost, st));
-  HIPC(hipMemcpyAsync(qhash.data(), d_qhash, nq * 8, hipMemcpyDeviceToHost, st));
-  HIPC(hipStreamSynchronize(st));
-  dev_free(d_qlen);
-  dev_free(d_qflag);
-  dev_free(d_qhash);
-  const bool partial = A->nrows % R != 0;
-  auto cls = [&](int64_t q) -> int {
-    if (partial && q == nq - 1) return 4;
-    const bool run = qflag[q] & 1, gh = (qflag[q] & 2) != 0;
-    return run ? (gh ? 1 : 0) : (gh ? 3 : 2);
-  };
-  std::vector<int32_t> order(nq);
-  for (int64_t q = 0; q < nq; ++q) order[q] = (int32_t)q;
-  std::stable_sort(order.begin(), order.end(), [&](int32_t a, int32_t b) {
-    const int ca = cls(a), cb = cls(b);
-    if (ca != cb) return ca < cb;
-    if (ca <= 1 && qhash[a] != qhash[b]) return qhash[a] < qhash[b];
-    return a < b;
-  });
-  // the new slices
-  const int64_t ns = (nq + 63) / 64;
-  std::vector<int32_t> perm(ns * 64, -1), inv(ons * 64, -1), slen(ns, 0);
-  std::vector<char> sghost(ns, 0);
-  A->h_qmap.assign(ns * 64, (int32_t)A->nrows);
-  for (int64_t p = 0; p < nq; ++p) {
-    const int32_t q = order[p];
-    perm[p] = q;
-    inv[q] = (int32_t)p;
-    A->h_qmap[p] = q * R;
-    slen[p / 64] = std::max(slen[p / 64], qlen[q]);
-    if (qflag[q] & 2) sghost[p / 64] = 1;
-  }
-  // keep the old layout until the copy is done
-  int64_t* o_soff = A->d_slice_off;
-  int32_t* o_slen = A->d_slice_len;
-  int32_t* o_col = A->d_col;
-  void* o_val = A->d_val;
-  const int64_t o_tail = A->n_gnz + A->n_lnz;
-  A->d_slice_off = nullptr;
-  A->d_slice_len = nullptr;
-  A->d_col = nullptr;
-  A->d_val = nullptr;
-  dev_free(A->d_int_list);
-  dev_free(A->d_bnd_list);
-  A->d_int_list = A->d_bnd_list = nullptr;
-  std::vector<int64_t> nsoff;
-  if (finish_sell_layout(A, slen, sghost, &nsoff)) return -1;
-  A->long_off = A->slots + A->n_gnz;
-  int32_t *d_perm = nullptr, *d_inv = nullptr;
-  if (dev_upload(&d_perm, perm) || dev_upload(&d_inv, inv) || dev_upload(&A->d_qmap, A->h_qmap)) return -1;
-  if (A->slots > 0) HIPC(big_malloc((void**)&A->d_col, A->slots * 4));
-  if (nvals(A) > 0) HIPC(big_malloc(&A->d_val, nvals(A) * S));
-  launch_quad_permute(A, ns, d_perm, A->d_slice_off, A->d_slice_len, o_soff, o_slen, o_col, o_val, A->d_col,
-                      A->d_val, st);
-  HIPC(hipGetLastError());
-  if (o_tail > 0)  // ghost-row (and long-row) values after the slots
-    HIPC(hipMemcpyAsync((char*)A->d_val + A->slots * S, (const char*)o_val + oslots * S, o_tail * S,
-                        hipMemcpyDeviceToDevice, st));
-  if (A->d_nz_slot) {
-    launch_nzslot_remap(A->csc_nnz, A->d_nz_slot, oslots, ons, o_soff, H, R, d_inv, A->d_slice_off, st);
-    HIPC(hipGetLastError());
-  } else if (!A->h_nz_slot.empty()) {
-    std::vector<int64_t> osoff(ons);
-    HIPC(hipMemcpyAsync(osoff.data(), o_soff, ons * 8, hipMemcpyDeviceToHost, st));
-    HIPC(hipStreamSynchronize(st));
-    for (int64_t& t : A->h_nz_slot) {
-      if (t < 0 || t >= oslots) continue;
-      const int64_t so = (int64_t)(std::upper_bound(osoff.begin(), osoff.end(), t) - osoff.begin()) - 1;
-      const int64_t rem = t - osoff[so], k = rem / H, w = rem % H;
-      const int64_t np = inv[so * 64 + w / R];
-      t = nsoff[np / 64] + (k * 64 + np % 64) * R + w % R;
-    }
-  }
-  HIPC(hipStreamSynchronize(st));
-  for (void* q : {(void*)o_soff, (void*)o_slen, (void*)o_col, o_val, (void*)d_perm, (void*)d_inv}) dev_free(q);
-  return 0;
-}
-
 // Pattern slices + side SELL from the int32 layout (device detection, host
-// bookkeeping).  noids: owned columns (x lids >= noids are ghosts).  When
-// fewer than 90 % of the slices are pattern slices (irregular partitions;
-// Cartesian parts have them all) the layout is quad-sorted first and the
-// detection redone on it.
+// bookkeeping).  noids: owned columns (x lids >= noids are ghosts).
 int finalize_pattern(pa_mat* A, int kmax, int64_t noids) {
   A->kmax = std::max(kmax, 1);
   const int64_t ns = A->nslices;
@@ -454,15 +315,7 @@ int finalize_pattern(pa_mat* A, int kmax, int64_t noids) {
   HIPC(hipMalloc((void**)&d_pghost, ns * 4));
   HIPC(hipMalloc((void**)&d_nirreg, ns * 4));
   HIPC(hipMemsetAsync(A->d_mask, 0, ns * W * 8, st));
-  const int NP = g_spmv_patterns;
-  if (NP > 1) {  // multi-pattern candidates (kept only if some slice takes them)
-    A->kmp = std::min(PA_MP_K, (A->kmax + 3) / 4 * 4);
-    HIPC(hipMalloc((void**)&A->d_mpat, ns * PA_MP_NP * A->kmp * 4));
-    HIPC(hipMalloc((void**)&A->d_psel, ns * 64));
-    HIPC(hipMemsetAsync(A->d_mpat, 0, ns * PA_MP_NP * A->kmp * 4, st));
-    HIPC(hipMemsetAsync(A->d_psel, 0, ns * 64, st));
-  }
-  launch_pattern_detect(A, noids, A->d_kind, A->d_plen, A->d_pat, A->d_mask, d_pghost, d_nirreg, NP, g_spmv_pattern_rule, st);
+  launch_pattern_detect(A, noids, A->d_kind, A->d_plen, A->d_pat, A->d_mask, d_pghost, d_nirreg, st);
   HIPC(hipGetLastError());
   std::vector<int32_t> kind(ns), pghost(ns), nirreg(ns);
   std::vector<uint64_t> mask(ns * W);
@@ -475,45 +328,9 @@ int finalize_pattern(pa_mat* A, int kmax, int64_t noids) {
   HIPC(hipStreamSynchronize(st));
   dev_free(d_pghost);
   dev_free(d_nirreg);
-  if (g_spmv_quadsort && !A->d_qmap && A->n_long == 0 && A->R > 1) {
-    int64_t npat = 0;
-    for (int64_t s = 0; s < ns; ++s) npat += kind[s] != 0;
-    if (10 * npat < 9 * ns || g_spmv_quadsort == 2) {  // irregular slices: quad-sort, then detect again
-      for (void** q : {(void**)&A->d_kind, (void**)&A->d_plen, (void**)&A->d_pat, (void**)&A->d_mask,
-                       (void**)&A->d_mpat, (void**)&A->d_psel}) {
-        dev_free(*q);
-        *q = nullptr;
-      }
-      A->h_plen.clear();
-      if (quad_sort(A, noids)) return -1;
-      return finalize_pattern(A, kmax, noids);
-    }
-  }
-  if (A->d_qmap) {  // quad-run slices (kind 4) among the remaining int32-column slices
-    int32_t* d_ok = nullptr;
-    HIPC(hipMalloc((void**)&A->d_qcol, std::max<int64_t>(A->slots / A->R, 1) * 4));
-    HIPC(hipMalloc((void**)&d_ok, ns * 4));
-    HIPC(hipMemcpyAsync(A->d_kind, kind.data(), ns * 4, hipMemcpyHostToDevice, st));
-    launch_qrun_detect(A, A->d_kind, A->d_qcol, d_ok, st);
-    HIPC(hipGetLastError());
-    std::vector<int32_t> ok(ns);
-    HIPC(hipMemcpyAsync(ok.data(), d_ok, ns * 4, hipMemcpyDeviceToHost, st));
-    HIPC(hipStreamSynchronize(st));
-    dev_free(d_ok);
-    int64_t nqr = 0;
-    for (int64_t s = 0; s < ns; ++s)
-      if (ok[s]) { kind[s] = 4; ++nqr; }
-    if (nqr == 0) {
-      dev_free(A->d_qcol);
-      A->d_qcol = nullptr;
-    } else {  // the delta16 pass below only takes kind 0
-      HIPC(hipMemcpyAsync(A->d_kind, kind.data(), ns * 4, hipMemcpyHostToDevice, st));
-      HIPC(hipStreamSynchronize(st));
-    }
-  }
   if (g_spmv_delta16) {  // int32-column slices whose columns fit 16-bit codes (kind 3)
     int32_t* d_ok = nullptr;
-    HIPC(big_malloc((void**)&A->d_col16, std::max<int64_t>(A->slots, 1) * 2));
+    HIPC(hipMalloc((void**)&A->d_col16, std::max<int64_t>(A->slots, 1) * 2));
     HIPC(hipMalloc((void**)&A->d_gbase, ns * 4));
     HIPC(hipMalloc((void**)&d_ok, ns * 4));
     launch_delta16(A, noids, A->d_kind, d_ok, st);
@@ -532,14 +349,12 @@ int finalize_pattern(pa_mat* A, int kmax, int64_t noids) {
       A->d_gbase = nullptr;
     }
   }
-  std::vector<int32_t> pint, pbnd, xint, xbnd, mint, mbnd, dint, dbnd, qint, qbnd, side;
+  std::vector<int32_t> pint, pbnd, xint, xbnd, dint, dbnd, side;
   for (int64_t s = 0; s < ns; ++s) {
     if (kind[s] == 1) (pghost[s] ? pbnd : pint).push_back((int32_t)s);
-    else if (kind[s] == 2) (pghost[s] ? mbnd : mint).push_back((int32_t)s);
     else if (kind[s] == 3) (pghost[s] ? dbnd : dint).push_back((int32_t)s);
-    else if (kind[s] == 4) (pghost[s] ? qbnd : qint).push_back((int32_t)s);
     else (pghost[s] ? xbnd : xint).push_back((int32_t)s);
-    if (kind[s] == 1 || kind[s] == 2) {
+    if (kind[s] == 1) {
       ++A->npattern_slices;
       const int64_t nvalid = std::min<int64_t>(A->H, A->nrows - s * A->H);
       for (int64_t i = 0; i < nvalid; ++i) {
@@ -549,14 +364,8 @@ int finalize_pattern(pa_mat* A, int kmax, int64_t noids) {
     }
   }
   A->h_kind = kind;
-  if (A->npattern_slices) {  // pattern slices of consecutive triples (lane-shared x runs)
-    HIPC(hipMalloc((void**)&A->d_ptri, ns));
-    launch_pattern_triples(A, A->d_ptri, st);
-    HIPC(hipGetLastError());
-  }
-  A->maxlen_pat = A->maxlen_pm_int = A->maxlen_d16 = A->maxlen_qrun = 0;
+  A->maxlen_pat = A->maxlen_pm_int = A->maxlen_d16 = 0;
   for (int64_t s = 0; s < ns; ++s) {
-    if (kind[s] == 4) A->maxlen_qrun = std::max(A->maxlen_qrun, (int)A->h_slen[s]);
     if (kind[s] == 1) A->maxlen_pat = std::max(A->maxlen_pat, (int)A->h_plen[s]);
     else if (kind[s] == 0) A->maxlen_pm_int = std::max(A->maxlen_pm_int, (int)A->h_slen[s]);
     else if (kind[s] == 3) A->maxlen_d16 = std::max(A->maxlen_d16, (int)A->h_slen[s]);
@@ -565,41 +374,18 @@ int finalize_pattern(pa_mat* A, int kmax, int64_t noids) {
   A->np_bnd = (int64_t)pbnd.size();
   A->nx_int = (int64_t)xint.size();
   A->nx_bnd = (int64_t)xbnd.size();
-  A->nm_int = (int64_t)mint.size();
-  A->nm_bnd = (int64_t)mbnd.size();
   A->nd_int = (int64_t)dint.size();
   A->nd_bnd = (int64_t)dbnd.size();
-  A->nq_int = (int64_t)qint.size();
-  A->nq_bnd = (int64_t)qbnd.size();
-  if (dev_upload(&A->d_qint_list, qint) || dev_upload(&A->d_qbnd_list, qbnd)) return -1;
   if (dev_upload(&A->d_pint_list, pint) || dev_upload(&A->d_pbnd_list, pbnd) ||
       dev_upload(&A->d_xint_list, xint) || dev_upload(&A->d_xbnd_list, xbnd) ||
-      dev_upload(&A->d_mint_list, mint) || dev_upload(&A->d_mbnd_list, mbnd) ||
       dev_upload(&A->d_dint_list, dint) || dev_upload(&A->d_dbnd_list, dbnd))
     return -1;
-  if (mint.empty() && mbnd.empty()) {  // no slice took several patterns
-    dev_free(A->d_mpat);
-    dev_free(A->d_psel);
-    A->d_mpat = nullptr;
-    A->d_psel = nullptr;
-  }
   // side SELL
   A->s_nrows = (int64_t)side.size();
   if (A->s_nrows > 0) {
-    // the SpMV reads oids through d_s_rowmap; the copies below (and
-    // refresh_side) locate the rows by their structure row
-    int32_t* srow = nullptr;
-    if (A->d_qmap) {
-      if (dev_upload(&A->d_s_srow, side)) return -1;
-      std::vector<int32_t> oids(side.size());
-      for (size_t i = 0; i < side.size(); ++i)
-        oids[i] = A->h_qmap[side[i] / A->R] + side[i] % A->R;  // structure row s*H + lane*R + r
-      if (dev_upload(&A->d_s_rowmap, oids)) return -1;
-      srow = A->d_s_srow;
-    } else {
-      if (dev_upload(&A->d_s_rowmap, side)) return -1;
-      srow = A->d_s_rowmap;
-    }
+    // the side rows (oids = structure rows) through d_s_rowmap
+    if (dev_upload(&A->d_s_rowmap, side)) return -1;
+    int32_t* srow = A->d_s_rowmap;
     int32_t* d_dummy = nullptr;
     A->s_nslices = (A->s_nrows + A->H - 1) / A->H;
     HIPC(hipMalloc((void**)&A->d_s_rowlen, A->s_nrows * 4));
@@ -675,7 +461,10 @@ template <typename T>
 const T* graph_owned(const T* d, const std::vector<T>& h) {
   if (!g_capture_tables || h.empty()) return d;
   void* p = nullptr;
-  if (hipMalloc(&p, h.size() * sizeof(T)) != hipSuccess) {
+  // PA_TEST_FAIL_GRAPH_ALLOC (tests only): the allocation fails, as on an
+  // out-of-memory device
+  const bool test_fail = std::getenv("PA_TEST_FAIL_GRAPH_ALLOC") != nullptr;
+  if (test_fail || hipMalloc(&p, h.size() * sizeof(T)) != hipSuccess) {
     (void)hipGetLastError();
     g_graph_owned_failed = true;
     return nullptr;
@@ -940,7 +729,7 @@ int transport(int n, pa_xchg* const xg[], int dtype, int dir, int op, pa_vec* co
       const int32_t* bid = graph_owned<int32_t>(P.d_bid, P.h_bid);
       const int64_t* elem = graph_owned<int64_t>(P.d_elem, P.h_elem);
       void* const* bases = graph_owned<void*>(P.d_bases, P.h_bases);
-      CHECK_ARG(!g_graph_owned_failed, "graph capture: table allocation failed");
+      CHECK_ARG(!(g_capture_tables && g_graph_owned_failed), "graph capture: table allocation failed");
       if (dir == 0)
         launch_pull(dtype, X->n_rcv_data, X->d_lids_rcv, X->plan_fwd, op, bid, elem,
                     (const void* const*)bases, v[i]->d, SC(c));
@@ -1020,30 +809,14 @@ int pa_tune(const char* key, int value, int* previous) {
   CHECK_ARG(key, "null key");
   int* slot = nullptr;
   if (!std::strcmp(key, "spmv_flags")) {
-    CHECK_ARG(value >= 0 && (value & ~0x2ff) == 0,
-              "spmv_flags: bit 0 = non-temporal streams, bit 1 = XCD mapping, bit 2 = 16 B x runs (pattern rows), "
+    CHECK_ARG(value >= 0 && (value & ~0x7d) == 0,
+              "spmv_flags: bit 0 = non-temporal streams, bit 2 = 16 B x runs (pattern rows), "
               "bit 3 = masked tail batch, bit 4 = identity slice lists dropped, bit 5 = non-temporal y stores, "
-              "bit 6 = short-row kernels (launches whose rows have <= 8 entries), bit 7 = 16 B x runs in "
-              "int32/delta16 slices where a lane's rows read consecutive columns, bit 9 = triple-pattern slices "
-              "share x runs between lanes (bit 8 is per matrix: CSR parent)");
+              "bit 6 = short-row kernels (launches whose rows have <= 8 entries)");
     slot = &g_spmv_flags;
-  } else if (!std::strcmp(key, "spmv_lds")) {
-    CHECK_ARG(value >= 0 && value <= 160 * 1024, "spmv_lds: bytes of LDS per SpMV block (occupancy cap)");
-    slot = &g_spmv_lds;
-  } else if (!std::strcmp(key, "spmv_unroll")) {
-    // (U = 9/12/14/16/28 were measured in r03 on one shared operator copy:
-    // FE27 256³ F64 U 12 = U 8 within 0.1 %, U 16 +1.7 %; C5 U 16 +5-10 %;
-    // profiles/r03/g/placement_and_shared_ab.jsonl — not kept; nor a
-    // prefetch of the next batch's delta16 codes: C5 F32/F64/C128 ±1 %,
-    // C64 +26 %, profiles/r03/m/)
-    CHECK_ARG(value == 4 || value == 8, "spmv_unroll must be 4 or 8");
-    slot = &g_spmv_unroll;
   } else if (!std::strcmp(key, "long_rows_exact")) {
     CHECK_ARG(value == 0 || value == 1, "long_rows_exact: 1 = reference summation order, 0 = lane-strided tree (1e-12)");
     slot = &g_long_exact;
-  } else if (!std::strcmp(key, "comm_cus")) {
-    CHECK_ARG(value >= 0 && value <= 64, "comm_cus: 0..64 CUs reserved for the halo stream (contexts created afterwards)");
-    slot = &g_comm_cus;
   } else if (!std::strcmp(key, "halo_pull")) {
     CHECK_ARG(value == 0 || value == 1, "halo_pull: 1 = receivers read the senders' buffers (one kernel), 0 = staging copies");
     slot = &g_halo_pull;
@@ -1063,20 +836,6 @@ int pa_tune(const char* key, int value, int* previous) {
     g_spmv_merge_max = value;
     if (previous) *previous = prev;
     return 0;
-  } else if (!std::strcmp(key, "spmv_short_occ")) {
-    CHECK_ARG(value >= 0 && value <= 3,
-              "spmv_short_occ: short-row F64 merged launch, 0 = one batch at 5 waves/SIMD (default), 1 = U 4 at 8, "
-              "2 = U 4 at 6, 3 = one batch at 6");
-    slot = &g_spmv_short_occ;
-  } else if (!std::strcmp(key, "alloc_contiguous")) {
-    CHECK_ARG(value == 0 || value == 1, "alloc_contiguous: 1 = large arrays in physically contiguous device memory "
-                                        "(matrices and vectors created afterwards), 0 = hipMalloc (default)");
-    slot = &g_alloc_contig;
-  } else if (!std::strcmp(key, "spmv_quadsort")) {
-    CHECK_ARG(value >= 0 && value <= 2,
-              "spmv_quadsort: 1 = matrices whose slices are mostly not pattern slices get the quad-sorted layout "
-              "(default; matrices built afterwards), 2 = every matrix (tests), 0 = off");
-    slot = &g_spmv_quadsort;
   } else if (!std::strcmp(key, "cg_fuse")) {
     CHECK_ARG(value >= 0 && value <= 2,
               "cg_fuse: 1 = the device CG computes u = r .+ beta.*u inside the SpMV, 0 = a separate sweep, "
@@ -1098,14 +857,6 @@ int pa_tune(const char* key, int value, int* previous) {
   } else if (!std::strcmp(key, "spmv_format")) {
     CHECK_ARG(value == 0 || value == 1, "spmv_format: 0 = int32 columns, 1 = pattern slices");
     slot = &g_spmv_format;
-  } else if (!std::strcmp(key, "spmv_patterns")) {
-    CHECK_ARG(value >= 1 && value <= PA_MP_NP,
-              "spmv_patterns: offset patterns per slice for matrices built afterwards (1..4; 1 = single-pattern slices)");
-    slot = &g_spmv_patterns;
-  } else if (!std::strcmp(key, "spmv_pattern_rule")) {
-    CHECK_ARG(value == 0 || value == 1,
-              "spmv_pattern_rule: 1 = slice encoding by streamed bytes, 0 = pattern slice when half its rows follow one");
-    slot = &g_spmv_pattern_rule;
   } else {
     PA_FAIL(std::string("pa_tune: unknown key ") + key);
   }
@@ -1195,26 +946,8 @@ int pa_ctx_create(int device, int part, int nparts, pa_ctx** out) {
   c->nparts = nparts;
   int least = 0, greatest = 0;
   HIPC(hipDeviceGetStreamPriorityRange(&least, &greatest));
-  int ncu = 0;
-  HIPC(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device));
-  if (g_comm_cus > 0 && g_comm_cus < ncu) {
-    // k CUs spread over the chip run the halo stream; the compute stream
-    // keeps the rest, so packs/RCCL/pull-unpack never queue behind a
-    // grid-filling SpMV
-    const int k = g_comm_cus, words = (ncu + 31) / 32;
-    std::vector<uint32_t> mm(words, 0), mc(words, 0);
-    for (int cu = 0; cu < ncu; ++cu) mm[cu / 32] |= 1u << (cu % 32);
-    for (int i = 0; i < k; ++i) {
-      const int cu = i * (ncu / k) + (ncu / k - 1);
-      mm[cu / 32] &= ~(1u << (cu % 32));
-      mc[cu / 32] |= 1u << (cu % 32);
-    }
-    HIPC(hipExtStreamCreateWithCUMask(&c->s_main, (uint32_t)words, mm.data()));
-    HIPC(hipExtStreamCreateWithCUMask(&c->s_comm, (uint32_t)words, mc.data()));
-  } else {
-    HIPC(hipStreamCreateWithFlags(&c->s_main, hipStreamNonBlocking));
-    HIPC(hipStreamCreateWithPriority(&c->s_comm, hipStreamNonBlocking, greatest));
-  }
+  HIPC(hipStreamCreateWithFlags(&c->s_main, hipStreamNonBlocking));
+  HIPC(hipStreamCreateWithPriority(&c->s_comm, hipStreamNonBlocking, greatest));
   c->stream_refs = new pa_ctx::StreamRefs();
   if (ctx_scratch(c)) return -1;
   *out = c;
@@ -1595,7 +1328,7 @@ int pa_vec_create(pa_ctx* c, int dtype, int64_t n, pa_vec** out) {
     // kVecPad bytes on both sides: the SpMV's 16 B x runs may start up to
     // 3 elements before lid 0 or end up to 3 after the last lid
     const size_t bytes = (size_t)n * dtype_size(dtype) + 2 * kVecPad;
-    hipError_t e = big_malloc(&v->base, bytes);
+    hipError_t e = hipMalloc(&v->base, bytes);
     if (e != hipSuccess) { delete v; PA_FAIL(std::string("hipMalloc(vector) failed: ") + hipGetErrorString(e)); }
     v->d = (char*)v->base + kVecPad;
     HIPC(hipMemsetAsync(v->base, 0, bytes, c->s_main));
@@ -1782,7 +1515,7 @@ int mat_from_visit(pa_ctx* c, int dtype, int64_t nrows_lids, int64_t ncols_lids,
   if (A->n_lnz) std::memcpy(&hval[A->long_off * S], lval.data(), A->n_lnz * S);
   if (dev_upload(&A->d_col, hcol)) { pa_mat_destroy(A); return -1; }
   if (nvals(A)) {
-    HIPC(big_malloc(&A->d_val, nvals(A) * S));
+    HIPC(hipMalloc(&A->d_val, nvals(A) * S));
     HIPC(hipMemcpy(A->d_val, hval.data(), nvals(A) * S, hipMemcpyHostToDevice));
   }
   if (upload_long(A, lrows, lptr, lcol)) { pa_mat_destroy(A); return -1; }
@@ -2090,13 +1823,13 @@ int mat_from_coo_impl(pa_ctx* c, int dtype, int index_bytes, int ids_global, int
   for (int64_t s = 0; s < ns; ++s) sghost[s] = sg[s] ? 1 : 0;
   if (finish_sell_layout(A, slen, sghost, nullptr)) { pa_mat_destroy(A); return -1; }
   if (A->slots > 0) {
-    HIPC(big_malloc((void**)&A->d_col, A->slots * 4));
+    HIPC(hipMalloc((void**)&A->d_col, A->slots * 4));
     launch_fill_i32(A->slots, A->d_col, -1, st);
   }
   A->n_gnz = ngh;
   A->long_off = A->slots + ngh;
   if (nvals(A) > 0) {
-    HIPC(big_malloc(&A->d_val, nvals(A) * S));
+    HIPC(hipMalloc(&A->d_val, nvals(A) * S));
     HIPC(hipMemsetAsync(A->d_val, 0, nvals(A) * S, st));
   }
   if (nu > 0) HIPC(hipMalloc((void**)&nzs, nu * 8));
@@ -2405,7 +2138,7 @@ static inline int64_t nz_index(const pa_mat* A, int64_t p) {
 // refresh the side SELL's copies of the irregular rows' values
 static int refresh_side(pa_mat* A, hipStream_t st) {
   if (A->s_nrows > 0) {
-    launch_side_fill(A, A->d_s_srow ? A->d_s_srow : A->d_s_rowmap, A->d_s_rowlen, st);
+    launch_side_fill(A, A->d_s_rowmap, A->d_s_rowlen, st);
     HIPC(hipGetLastError());
   }
   return 0;
@@ -2521,16 +2254,13 @@ int pa_mat_destroy(pa_mat* A) {
   dev_free(A->d_col);
   dev_free(A->d_val);
   dev_free(A->d_nz_slot);
-  for (void* p : {(void*)A->d_kind, (void*)A->d_plen, (void*)A->d_pat, (void*)A->d_ptri, (void*)A->d_mask, (void*)A->d_mpat,
-                  (void*)A->d_psel, (void*)A->d_mint_list, (void*)A->d_mbnd_list,
+  for (void* p : {(void*)A->d_kind, (void*)A->d_plen, (void*)A->d_pat, (void*)A->d_mask,
                   (void*)A->d_pint_list, (void*)A->d_pbnd_list, (void*)A->d_xint_list,
                   (void*)A->d_xbnd_list, (void*)A->d_s_off, (void*)A->d_s_len,
                   (void*)A->d_s_col, A->d_s_val, (void*)A->d_s_rowmap, (void*)A->d_s_rowlen, A->d_dotp,
                   (void*)A->d_long_row, (void*)A->d_long_ptr, (void*)A->d_long_col, (void*)A->d_sflags,
                   (void*)A->d_lmask, (void*)A->d_lchunk_start, (void*)A->d_lrow_chunk, A->d_lpart,
-                  (void*)A->d_col16, (void*)A->d_gbase, (void*)A->d_dint_list, (void*)A->d_dbnd_list,
-                  (void*)A->d_qmap, (void*)A->d_qcol, (void*)A->d_qint_list, (void*)A->d_qbnd_list,
-                  (void*)A->d_s_srow})
+                  (void*)A->d_col16, (void*)A->d_gbase, (void*)A->d_dint_list, (void*)A->d_dbnd_list})
     dev_free(p);
   delete A;
   return 0;
@@ -2546,22 +2276,9 @@ int pa_mat_format_info(const pa_mat* A, int64_t* pattern_slices, int64_t* regula
   return 0;
 }
 
-int pa_mat_multipattern_info(const pa_mat* A, int64_t* multi_slices) {
-  CHECK_ARG(A, "null matrix");
-  if (multi_slices) *multi_slices = A->nm_int + A->nm_bnd;
-  return 0;
-}
-
 int pa_mat_delta16_info(const pa_mat* A, int64_t* delta16_slices) {
   CHECK_ARG(A, "null matrix");
   if (delta16_slices) *delta16_slices = A->nd_int + A->nd_bnd;
-  return 0;
-}
-
-int pa_mat_quadrun_info(const pa_mat* A, int64_t* quadrun_slices, int* quad_sorted) {
-  CHECK_ARG(A, "null matrix");
-  if (quadrun_slices) *quadrun_slices = A->nq_int + A->nq_bnd;
-  if (quad_sorted) *quad_sorted = A->d_qmap ? 1 : 0;
   return 0;
 }
 
@@ -2592,18 +2309,11 @@ int pa_mat_traffic(const pa_mat* A, int64_t* value_bytes, int64_t* index_bytes, 
     const int kd = pat ? A->h_kind[s] : 0;
     if (kd == 1) {
       v += (int64_t)A->h_plen[s] * H * S;
-      m += (int64_t)A->kmax * 4 + W * 8 + 8 + 4 + 4 + (A->d_ptri ? 1 : 0);  // pattern, mask, offset, length, list entry, triple flag
-    } else if (kd == 2) {
-      v += (int64_t)A->h_plen[s] * H * S;
-      m += (int64_t)PA_MP_NP * A->kmp * 4 + 64 + W * 8 + 8 + 4 + 4;
+      m += (int64_t)A->kmax * 4 + W * 8 + 8 + 4 + 4;  // pattern, mask, offset, length, list entry
     } else if (kd == 3) {
       v += (int64_t)A->h_slen[s] * H * S;
       ix += (int64_t)A->h_slen[s] * H * 2;
       m += 8 + 4 + 4 + 4;  // offset, length, list entry, ghost base
-    } else if (kd == 4) {
-      v += (int64_t)A->h_slen[s] * H * S;
-      ix += (int64_t)A->h_slen[s] * 64 * 4;  // one column per entry and lane
-      m += 8 + 4 + 4;
     } else {
       v += (int64_t)A->h_slen[s] * H * S;
       ix += (int64_t)A->h_slen[s] * H * 4;
@@ -2618,7 +2328,6 @@ int pa_mat_traffic(const pa_mat* A, int64_t* value_bytes, int64_t* index_bytes, 
   v += A->n_lnz * S;
   ix += A->n_lnz * 4;
   m += A->n_long * 16;
-  if (A->d_qmap) m += A->nslices * 64 * 4;  // the lanes' first rows
   if (value_bytes) *value_bytes = v;
   if (index_bytes) *index_bytes = ix;
   if (meta_bytes) *meta_bytes = m;
@@ -2727,7 +2436,7 @@ static int spmv_grouped(int n, pa_mat* const A[], pa_vec* const y[], const pa_in
       std::vector<void*> xs(n);
       for (int i = 0; i < n; ++i) xs[i] = x[i]->d;
       bases = const_cast<void**>(graph_owned<void*>(bases, xs));
-      CHECK_ARG(!g_graph_owned_failed, "graph capture: table allocation failed");
+      CHECK_ARG(!(g_capture_tables && g_graph_owned_failed), "graph capture: table allocation failed");
     }
     PullGroup qg{};
     for (int i0 = 0; i0 < n; i0 += PA_GROUP_MAX) {
@@ -2739,7 +2448,7 @@ static int spmv_grouped(int n, pa_mat* const A[], pa_vec* const y[], const pa_in
         qg.lids[k] = X->d_lids_rcv;
         qg.bid[k] = graph_owned<int32_t>(X->direct.d_bid, X->direct.h_bid);
         qg.elem[k] = graph_owned<int64_t>(X->direct.d_elem, X->direct.h_elem);
-        CHECK_ARG(!g_graph_owned_failed, "graph capture: table allocation failed");
+        CHECK_ARG(!(g_capture_tables && g_graph_owned_failed), "graph capture: table allocation failed");
         qg.bases[k] = (const void* const*)bases;
         qg.v[k] = x[i]->d;
       }
@@ -2775,7 +2484,7 @@ static int spmv_grouped(int n, pa_mat* const A[], pa_vec* const y[], const pa_in
         qg.bid[k] = graph_owned<int32_t>(P.d_bid, P.h_bid);
         qg.elem[k] = graph_owned<int64_t>(P.d_elem, P.h_elem);
         qg.bases[k] = (const void* const*)graph_owned<void*>(P.d_bases, P.h_bases);
-        CHECK_ARG(!g_graph_owned_failed, "graph capture: table allocation failed");
+        CHECK_ARG(!(g_capture_tables && g_graph_owned_failed), "graph capture: table allocation failed");
         qg.v[k] = x[i]->d;
       }
       launch_pull_group(dt, qg, sc);
@@ -2783,7 +2492,7 @@ static int spmv_grouped(int n, pa_mat* const A[], pa_vec* const y[], const pa_in
     EV(hipEventRecord(c0->ev_recvd, sc));
   }
   HIPC(hipGetLastError());
-  std::vector<SpmvPart> P0, P1, P3, P4, P5;
+  std::vector<SpmvPart> P0, P1, P4;
   auto part = [&](int i, int64_t nwork, const int32_t* list) {
     const int32_t* ymap = y_idx[i]->own_contig ? nullptr : y_idx[i]->d_oid_to_lid;
     SpmvPart q{nwork, list, A[i], x[i]->d, y[i]->d, ymap, dotp[i]};
@@ -2830,13 +2539,6 @@ static int spmv_grouped(int n, pa_mat* const A[], pa_vec* const y[], const pa_in
       if (g_spmv_format == 1 && A[i]->has_pat) {
         add(4, i, A[i]->nd_int, A[i]->d_dint_list);
         add(4, i, A[i]->nd_bnd, A[i]->d_dbnd_list);
-        add(5, i, A[i]->nq_int, A[i]->d_qint_list);
-        add(5, i, A[i]->nq_bnd, A[i]->d_qbnd_list);
-      }
-    for (int i = 0; i < n; ++i)
-      if (g_spmv_format == 1 && A[i]->has_pat) {
-        add(3, i, A[i]->nm_int, A[i]->d_mint_list);
-        add(3, i, A[i]->nm_bnd, A[i]->d_mbnd_list);
       }
     for (int i = 0; i < n; ++i)
       if (g_spmv_format == 1 && A[i]->has_pat) {
@@ -2853,10 +2555,8 @@ static int spmv_grouped(int n, pa_mat* const A[], pa_vec* const y[], const pa_in
   for (int i = 0; i < n; ++i) {
     if (g_spmv_format == 1 && A[i]->has_pat) {
       P0.push_back(part(i, A[i]->np_int, A[i]->d_pint_list));
-      P3.push_back(part(i, A[i]->nm_int, A[i]->d_mint_list));
       P1.push_back(part(i, A[i]->nx_int, A[i]->d_xint_list));
       P4.push_back(part(i, A[i]->nd_int, A[i]->d_dint_list));
-      P5.push_back(part(i, A[i]->nq_int, A[i]->d_qint_list));
     } else if (A[i]->d_bnd_list) {
       P1.push_back(part(i, A[i]->nslices_int, A[i]->d_int_list));
     } else {
@@ -2864,21 +2564,17 @@ static int spmv_grouped(int n, pa_mat* const A[], pa_vec* const y[], const pa_in
     }
   }
   launch_all(0, P0);
-  launch_all(3, P3);
   launch_all(4, P4);
-  launch_all(5, P5);
   launch_all(1, P1);
   if (!dmark && mark(1)) return -1;
   if (any_x && !direct) EV(hipStreamWaitEvent(sm, c0->ev_recvd, 0));
   if (!dmark && mark(2)) return -1;
-  P0.clear(); P1.clear(); P3.clear(); P4.clear(); P5.clear();
+  P0.clear(); P1.clear(); P4.clear();
   std::vector<SpmvPart> P2;
   for (int i = 0; i < n; ++i) {
     if (g_spmv_format == 1 && A[i]->has_pat) {
       P0.push_back(part(i, A[i]->np_bnd, A[i]->d_pbnd_list));
-      P3.push_back(part(i, A[i]->nm_bnd, A[i]->d_mbnd_list));
       P4.push_back(part(i, A[i]->nd_bnd, A[i]->d_dbnd_list));
-      P5.push_back(part(i, A[i]->nq_bnd, A[i]->d_qbnd_list));
       P1.push_back(part(i, A[i]->nx_bnd, A[i]->d_xbnd_list));
       P2.push_back(part(i, A[i]->s_nslices, nullptr));
     } else if (A[i]->d_bnd_list) {
@@ -2886,9 +2582,7 @@ static int spmv_grouped(int n, pa_mat* const A[], pa_vec* const y[], const pa_in
     }
   }
   launch_all(0, P0);
-  launch_all(3, P3);
   launch_all(4, P4);
-  launch_all(5, P5);
   launch_all(1, P1);
   launch_all(2, P2);
   }  // per-kind launches
@@ -2939,15 +2633,11 @@ static int launch_phase(int phase, pa_mat* A, const void* x, void* y, const int3
     if (phase == 0) {
       add(1, A->nx_int, A->d_xint_list);
       add(4, A->nd_int, A->d_dint_list);
-      add(5, A->nq_int, A->d_qint_list);
-      add(3, A->nm_int, A->d_mint_list);
       add(0, A->np_int, A->d_pint_list);
     } else {
       add(2, A->s_nslices, nullptr);
       add(1, A->nx_bnd, A->d_xbnd_list);
       add(4, A->nd_bnd, A->d_dbnd_list);
-      add(5, A->nq_bnd, A->d_qbnd_list);
-      add(3, A->nm_bnd, A->d_mbnd_list);
       add(0, A->np_bnd, A->d_pbnd_list);
     }
   } else if (A->d_bnd_list) {  // split layout (the interior list may be empty)
@@ -3172,6 +2862,7 @@ int pa_spmv_graph_create(int n, pa_mat* const A[], pa_vec* const y[], const pa_i
     g_graph_owned_failed = false;
     rc = spmv_impl(n, A, y, y_idx, x, x_idx, xg, alpha, beta, false);
     g_capture_tables = nullptr;
+    g_graph_owned_failed = false;  // eager calls after a failed capture never see it
     g_capture_stream = nullptr;
     g_capturing = false;
     hipError_t e2 = hipStreamEndCapture(G->origin, &G->graph);
@@ -3606,13 +3297,16 @@ int pa_cg_solve_all(int n, pa_mat* const A[], pa_vec* const x[], const pa_vec* c
   bool done = h.done != 0;
   while (!done && enqueued < maxiter) {
     const int64_t k = std::min<int64_t>(batch, maxiter - enqueued);  // the same on every rank
-    const int variant = mode == 2 ? (nbatch < 2 ? (int)nbatch : A[0]->cg_fuse_choice) : mode;
-    const bool timed = mode == 2 && nbatch < 2;
-    if (timed) {
-      HIPC(hipSetDevice(R.ctxs[0]->device));
-      HIPC(hipEventRecord(tev[0], R.ctxs[0]->s_main));
-    }
+    // (a batch that ended the solve before the choice was made runs the sweep)
+    const int variant = mode == 2 ? (nbatch < 2 ? (int)nbatch : std::max(0, A[0]->cg_fuse_choice)) : mode;
+    // the timed batches start their clock after their first iteration (which
+    // builds the variant's launch tables) and need two iterations at least
+    const bool timed = mode == 2 && nbatch < 2 && k >= 2;
     for (int64_t t = 0; t < k; ++t) {
+      if (timed && t == 1) {
+        HIPC(hipSetDevice(R.ctxs[0]->device));
+        HIPC(hipEventRecord(tev[0], R.ctxs[0]->s_main));
+      }
       if (variant == 1) {
         // mul!(c, A, u) with u = r .+ β.*u_old evaluated inside the SpMV (its
         // halo carries r), the owned u written, x .+= α.*u_old of the
@@ -3675,11 +3369,13 @@ int pa_cg_solve_all(int n, pa_mat* const A[], pa_vec* const x[], const pa_vec* c
     }
     std::memcpy(&h, c0->h_pinned, sizeof(CGState));
     done = h.done != 0;
-    if (timed) {
+    if (timed && !done) {  // a batch that converged part-way is no measurement
       float ms = 0.f;
       HIPC(hipEventElapsedTime(&ms, tev[0], tev[1]));
-      batch_ms[nbatch] = ms / (float)k;
-      if (nbatch == 1) A[0]->cg_fuse_choice = batch_ms[1] < batch_ms[0] ? 1 : 0;
+      batch_ms[nbatch] = ms / (float)(k - 1);
+      if (nbatch == 1 && batch_ms[0] > 0.f) A[0]->cg_fuse_choice = batch_ms[1] < batch_ms[0] ? 1 : 0;
+    } else if (mode == 2 && nbatch < 2) {
+      mode = A[0]->cg_fuse_choice >= 0 ? A[0]->cg_fuse_choice : 0;  // no choice this solve: keep it unset
     }
     ++nbatch;
   }
@@ -3789,8 +3485,8 @@ int pa_mat_stencil(pa_ctx* c, int dtype, int kind, const int64_t gdims[3], const
   const size_t S = dtype_size(dtype);
   int64_t nnz_owned = 0;
   (void)nnz_owned;
-  hipError_t e1 = big_malloc((void**)&A->d_col, std::max<int64_t>(A->slots, 1) * 4);
-  hipError_t e2 = big_malloc(&A->d_val, std::max<int64_t>(A->slots, 1) * S);
+  hipError_t e1 = hipMalloc((void**)&A->d_col, std::max<int64_t>(A->slots, 1) * 4);
+  hipError_t e2 = hipMalloc(&A->d_val, std::max<int64_t>(A->slots, 1) * S);
   if (e1 != hipSuccess || e2 != hipSuccess) { cleanup(); pa_mat_destroy(A); PA_FAIL("hipMalloc(matrix) failed: out of device memory"); }
   launch_stencil_fill(g, d_shell, d_coef, nrows, (int)nrows, A, d_err, c->s_main);
   HIPC(hipGetLastError());

@@ -373,8 +373,6 @@ struct pa_xchg {
   pa_combine_plan plan_rev;   // unpack targets = lids_snd (reverse/assemble)
 };
 
-constexpr int PA_MP_NP = 4;   // offset patterns per multi-pattern slice
-constexpr int PA_MP_K = 64;   // longest pattern a multi-pattern slice takes
 constexpr size_t kVecPad = 64;  // bytes before and after a vector's values (pa_vec_create)
 
 // COO triplets of one part on the device (global row/column ids, Int64),
@@ -410,7 +408,7 @@ struct pa_mat {
   int64_t nslices_int = 0;   // slices without ghost-column entries
   bool csr = false;          // built from a SparseMatrixCSR: α scales each product, (v*x)*α (SparseUtils.jl:247)
   std::vector<int32_t> h_slen;      // host copies for pa_mat_traffic: int32-layout slice lengths,
-  std::vector<int32_t> h_kind;      // pattern-layout slice kinds (0 int32, 1 pattern, 2 multi-pattern)
+  std::vector<int32_t> h_kind;      // pattern-layout slice kinds (0 int32, 1 pattern, 3 delta16)
   std::vector<int32_t> h_plen;      // and entries per row of each pattern-layout slice
   // longest row of each launch kind (SH kernels when <= 8): pattern slices,
   // int32 slices (of the current encoding), side SELL
@@ -458,7 +456,6 @@ struct pa_mat {
   int32_t* d_kind = nullptr;         // per slice: 1 pattern, 0 int32 columns
   int32_t* d_plen = nullptr;         // per slice: entries per row (pattern len or int32 len)
   int32_t* d_pat = nullptr;          // nslices*kmax offsets
-  uint8_t* d_ptri = nullptr;         // per slice: 1 if its pattern is consecutive triples (x runs shared by lanes)
   uint64_t* d_mask = nullptr;        // nslices*(H/64) regular-row bits
   int32_t* d_pint_list = nullptr;    // pattern mode: pattern slices without ghost reads
   int32_t* d_pbnd_list = nullptr;    // pattern mode: pattern slices reading ghosts
@@ -467,12 +464,6 @@ struct pa_mat {
   int32_t* d_xbnd_list = nullptr;    // pattern mode: int32-column slices with ghost columns
   int64_t nx_int = 0, nx_bnd = 0;
   int64_t npattern_slices = 0, nregular_rows = 0;
-  // multi-pattern slices (kind 2): up to PA_MP_NP offset patterns per slice,
-  // one chosen per lane (d_psel); for irregular partitions whose x-runs are
-  // shorter than a slice (C5).  Patterns of at most PA_MP_K entries.
-  int32_t* d_mpat = nullptr;         // nslices*PA_MP_NP*kmp offsets
-  uint8_t* d_psel = nullptr;         // nslices*64 pattern index per lane
-  int kmp = 0;                       // pattern stride (<= PA_MP_K)
   // delta16 slices (kind 3): int32-column slices whose columns all fit a
   // 16-bit code (pa_tune "spmv_delta16"): an owned column c of row r as
   // c - r in 15 signed bits, a ghost column as the slice's ghost base +
@@ -483,25 +474,6 @@ struct pa_mat {
   int32_t* d_dbnd_list = nullptr;    // delta16 slices with ghost columns
   int64_t nd_int = 0, nd_bnd = 0;
   int maxlen_d16 = INT32_MAX;
-  int32_t* d_mint_list = nullptr;    // multi-pattern slices without ghost reads
-  int32_t* d_mbnd_list = nullptr;    // multi-pattern slices reading ghosts
-  int64_t nm_int = 0, nm_bnd = 0;
-  // Quad-sorted layout (irregular partitions; SELL-C-σ at lane granularity,
-  // pa_tune "spmv_quadsort"): lane l of slice s holds the R consecutive
-  // owned rows qmap[s*64+l] .. +R-1 (nrows: a padding lane); null: the
-  // identity layout, rows s*H + l*R ...  Lanes are ordered by class (rows
-  // whose columns run in step, reading ghosts or not, their column offsets),
-  // so whole slices become pattern or quad-run slices.
-  int32_t* d_qmap = nullptr;
-  std::vector<int32_t> h_qmap;
-  // quad-run slices (kind 4): at every entry the lane's R rows read R
-  // consecutive columns: one int32 column (the lane's first row's) per entry
-  // and lane, at slot / R; the x values as one 16 B run
-  int32_t* d_qcol = nullptr;
-  int32_t* d_qint_list = nullptr;    // quad-run slices without ghost columns
-  int32_t* d_qbnd_list = nullptr;    // quad-run slices with ghost columns
-  int64_t nq_int = 0, nq_bnd = 0;
-  int maxlen_qrun = INT32_MAX;
   // side SELL: the irregular rows of pattern slices (row map → oid)
   int64_t s_nrows = 0, s_nslices = 0, s_slots = 0;
   int64_t* d_s_off = nullptr;
@@ -509,7 +481,6 @@ struct pa_mat {
   int32_t* d_s_col = nullptr;
   void* d_s_val = nullptr;
   int32_t* d_s_rowmap = nullptr;
-  int32_t* d_s_srow = nullptr;       // their structure rows (s*H + lane*R + r) when qmap: d_s_rowmap holds oids
   int32_t* d_s_rowlen = nullptr;
   void* d_dotp = nullptr;            // fused dot: one partial per (main + side) slice
 };

@@ -48,49 +48,27 @@ struct alignas(2 * R) S16Pack {
   uint16_t c[R];
 };
 
-// XCD-aware block remap (cdna_hip_programming.md §5.5 T1, bijective variant).
-__device__ inline int64_t xcd_remap(int64_t b, int64_t G) {
-  const int64_t q = G >> 3, r = G & 7;
-  const int64_t x = b & 7, i = b >> 3;
-  return x * q + (x < r ? x : r) + i;
-}
+// Bit 1 (XCD remap), 7 (x runs in int32 slices) and 9 (lane-shared x runs)
+// were negative A/Bs of rounds 1-3 and are gone.
+enum { SPMV_NT = 1, SPMV_XPAIR = 4, SPMV_TAILB = 8, SPMV_IDLIST = 16, SPMV_YNT = 32, SPMV_SHORT = 64,
+       SPMV_PRODA = 256 /* per matrix: CSR parent, α scales the product */ };
 
-enum { SPMV_NT = 1, SPMV_XCD = 2, SPMV_XPAIR = 4, SPMV_TAILB = 8, SPMV_IDLIST = 16, SPMV_YNT = 32, SPMV_SHORT = 64,
-       SPMV_XRUN = 128, SPMV_PRODA = 256 /* per matrix: CSR parent, α scales the product */,
-       SPMV_XTRI = 512 /* triple-pattern slices share x runs between lanes */ };
 typedef unsigned int spmv_u32x4 __attribute__((ext_vector_type(4)));
 // Process-wide knobs (pa_tune).  Defaults from the A/Bs in
 // profiles/r01_ab_spmv.txt and profiles/r01/ab_xpair.txt: non-temporal
-// streams on, XCD remap off, U = 8, 16 B x runs on (FE27 256³: F64 −9 %,
+// streams on, U = 8, 16 B x runs on (FE27 256³: F64 −9 %,
 // F32 −33 %, C64 −5 % kernel time), predicated tail batch on
 // (profiles/r01/ab_tail.txt: FD7 256³ F64 −31 %, F32 −42 %; FE27 −1…−3 %),
 // identity slice lists dropped (profiles/r01/ab_idlist.txt: FD7 −0.9 %, FE27 ±0).
-// Lane-shared x runs for triple-pattern slices (SPMV_XTRI) stay opt-in:
-// interleaved A/B on FE27 256³ (profiles/r02/stream/ab_xtri.txt): F64 −0.2 %,
-// C128 −0.9 %, C64 +0.4 %, F32 +3 % kernel time — the x loads are not what
-// bounds the SpMV (their 6 % in the probe is hidden in the full kernel).
 #if PA_DT_DEFINE
 int g_spmv_flags = SPMV_NT | SPMV_XPAIR | SPMV_TAILB | SPMV_IDLIST | SPMV_SHORT;
-int g_spmv_unroll = 8;
-// dynamic LDS per SpMV block (unused by the kernel): caps the blocks per CU,
-// i.e. the waves streaming at once (160 KB LDS per CU)
-int g_spmv_lds = 0;
 int g_spmv_format = 1;  // 1: pattern slices where built, 0: int32 columns only
-int g_spmv_short_occ = 0;  // short-row F64 merged launch: 0 one batch at 5 waves/SIMD, 1..3 occupancy variants
-// Build-time encoding knobs.  Defaults from profiles/r01/multipattern/README.md
-// (C5 Voronoi parts): multi-pattern slices stream up to 12 % fewer bytes but
-// add a launch per phase and per-lane LDS offset reads; kernel time is flat
-// to +25 % except F32 at 256³ on 8 parts (-9 %), so they stay opt-in, and
-// the byte-cost rule moves kernel time by ±4 % either way.
-int g_spmv_patterns = 1;         // patterns per slice (multi-pattern slices when > 1)
-int g_spmv_pattern_rule = 0;     // 1: slice encoding by streamed bytes, 0: pattern slice when half the rows follow it
 // merged-launch tables allocated during a graph capture, copied after it ends
 // (no copies while a stream is being captured)
 std::vector<std::pair<void*, std::vector<char>>> g_capture_uploads;
 int g_long_exact = 1;  // pa_tune("long_rows_exact")
 #else
-extern int g_spmv_flags, g_spmv_unroll, g_spmv_lds, g_spmv_format, g_spmv_patterns, g_spmv_pattern_rule,
-    g_spmv_short_occ;
+extern int g_spmv_flags, g_spmv_format;
 extern std::vector<std::pair<void*, std::vector<char>>> g_capture_uploads;
 extern int g_long_exact;
 #endif
@@ -130,13 +108,10 @@ struct SpmvArgs {
   const PA_GLB int32_t* slen;      // entries per row of the slice
   const PA_GLB int32_t* col;
   const PA_GLB T* val;
-  const PA_GLB int32_t* pat;       // kmax offsets per slice (multi-pattern: PA_MP_NP*kmax)
-  const PA_GLB uint8_t* ptri;      // pattern slices: 1 if the pattern is consecutive triples (null: none)
+  const PA_GLB int32_t* pat;       // kmax offsets per slice
   const PA_GLB uint64_t* mask;     // H/64 words per slice
   int kmax;
-  const PA_GLB uint8_t* psel;      // multi-pattern: pattern of each lane (64 per slice)
   const PA_GLB int32_t* rowmap;    // structure row → oid (side SELL), null: identity
-  const PA_GLB int32_t* qmap;      // quad-sorted main structure: first oid of each (slice, lane), null: identity
   int64_t nrows;            // rows of this structure
   const PA_GLB T* x;
   int64_t nx;               // x length (lids)
@@ -230,22 +205,10 @@ struct XSrc<T, true> {
   }
 };
 
-// the x values of a lane's R rows at one entry: one 16 B run when their
-// columns are consecutive (rows of a structured block, SPMV_XRUN), else R
-// gathers (c < 0: padding, read x[0], never used)
+// the x values of a lane's R rows at one entry: R gathers (c < 0: padding,
+// read x[0], never used)
 template <typename T, int R, typename XS>
-__device__ __forceinline__ void gather_x(T (&xv)[R], const int32_t (&c)[R], const XS& x, bool xrun) {
-  if constexpr (R > 1 && sizeof(Pack<T, R>) == 16) {
-    bool run = xrun && c[0] >= 0;
-#pragma unroll
-    for (int r = 1; r < R; ++r) run = run && c[r] == c[0] + r;
-    if (run) {
-      const Pack<T, R> p = x.template run<R>(c[0]);
-#pragma unroll
-      for (int r = 0; r < R; ++r) xv[r] = p.v[r];
-      return;
-    }
-  }
+__device__ __forceinline__ void gather_x(T (&xv)[R], const int32_t (&c)[R], const XS& x) {
 #pragma unroll
   for (int r = 0; r < R; ++r) xv[r] = x.get(c[r] >= 0 ? c[r] : 0);
 }
@@ -266,7 +229,7 @@ __device__ __forceinline__ T term(T v, T x, T alpha, bool pf) {
 template <typename T, int R, bool ALPHA, bool NT, int U, bool SH = false, typename XS>
 __device__ __forceinline__ void rows_int32(T (&acc)[R], const IPack<R>* __restrict__ cp,
                                            const Pack<T, R>* __restrict__ vp, int len,
-                                           const XS& x, T alpha, bool pf, bool TB, bool xrun) {
+                                           const XS& x, T alpha, bool pf, bool TB) {
   int k = 0;
   if (SH) TB = true;  // short rows (len <= U): the one masked batch is the whole row
   for (; !SH && k + U <= len; k += U) {
@@ -278,7 +241,7 @@ __device__ __forceinline__ void rows_int32(T (&acc)[R], const IPack<R>* __restri
     for (int u = 0; u < U; ++u) v[u] = ld<NT>(&vp[(k + u) * 64]);
     T xv[U][R];
 #pragma unroll
-    for (int u = 0; u < U; ++u) gather_x<T, R>(xv[u], c[u].c, x, xrun);
+    for (int u = 0; u < U; ++u) gather_x<T, R>(xv[u], c[u].c, x);
 #pragma unroll
     for (int u = 0; u < U; ++u)
 #pragma unroll
@@ -301,7 +264,7 @@ __device__ __forceinline__ void rows_int32(T (&acc)[R], const IPack<R>* __restri
     T xv[U][R];
 #pragma unroll
     for (int u = 0; u < U; ++u)
-      if (k + u < len) gather_x<T, R>(xv[u], c[u].c, x, xrun);
+      if (k + u < len) gather_x<T, R>(xv[u], c[u].c, x);
 #pragma unroll
     for (int u = 0; u < U; ++u)
 #pragma unroll
@@ -335,8 +298,7 @@ __device__ __forceinline__ int32_t d16_col(uint32_t q, int32_t row, int32_t gb) 
 template <typename T, int R, bool ALPHA, bool NT, int U, bool SH = false, typename XS>
 __device__ __forceinline__ void rows_d16(T (&acc)[R], const S16Pack<R>* __restrict__ cp,
                                          const Pack<T, R>* __restrict__ vp, int len,
-                                         const XS& x, T alpha, bool pf, bool TB, int32_t row0, int32_t gb,
-                                         bool xrun) {
+                                         const XS& x, T alpha, bool pf, bool TB, int32_t row0, int32_t gb) {
   int k = 0;
   if (SH) TB = true;
   for (; !SH && k + U <= len; k += U) {
@@ -352,7 +314,7 @@ __device__ __forceinline__ void rows_d16(T (&acc)[R], const S16Pack<R>* __restri
     for (int u = 0; u < U; ++u) {
 #pragma unroll
       for (int r = 0; r < R; ++r) c[u][r] = d16_col(q[u].c[r], row0 + r, gb);
-      gather_x<T, R>(xv[u], c[u], x, xrun);
+      gather_x<T, R>(xv[u], c[u], x);
     }
 #pragma unroll
     for (int u = 0; u < U; ++u)
@@ -379,7 +341,7 @@ __device__ __forceinline__ void rows_d16(T (&acc)[R], const S16Pack<R>* __restri
     for (int u = 0; u < U; ++u) {
 #pragma unroll
       for (int r = 0; r < R; ++r) c[u][r] = d16_col(q[u].c[r], row0 + r, gb);
-      if (k + u < len) gather_x<T, R>(xv[u], c[u], x, xrun);
+      if (k + u < len) gather_x<T, R>(xv[u], c[u], x);
     }
 #pragma unroll
     for (int u = 0; u < U; ++u)
@@ -398,66 +360,6 @@ __device__ __forceinline__ void rows_d16(T (&acc)[R], const S16Pack<R>* __restri
       const int32_t cc = d16_col(q.c[r], row0 + r, gb);
       const T t = acc[r] + term<ALPHA>(v.v[r], x.get(cc >= 0 ? cc : 0), alpha, pf);
       acc[r] = pick(cc >= 0, t, acc[r]);
-    }
-  }
-}
-
-// quad-run rows (kind 4): at entry k the lane's R rows read the R
-// consecutive columns c, c+1, .., c+R-1 (c < 0: padding): one int32 column
-// per entry and lane, and the x values as one 16 B run
-template <typename T, int R, bool ALPHA, bool NT, int U, bool SH = false, typename XS>
-__device__ __forceinline__ void rows_qrun(T (&acc)[R], const int32_t* __restrict__ cp,
-                                          const Pack<T, R>* __restrict__ vp, int len, const XS& x, T alpha,
-                                          bool pf, bool TB) {
-  int k = 0;
-  if (SH) TB = true;
-  for (; !SH && k + U <= len; k += U) {
-    int32_t c[U];
-    Pack<T, R> v[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) c[u] = ld<NT>(&cp[(k + u) * 64]);
-#pragma unroll
-    for (int u = 0; u < U; ++u) v[u] = ld<NT>(&vp[(k + u) * 64]);
-    Pack<T, R> xr[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) xr[u] = x.template run<R>(c[u] >= 0 ? c[u] : 0);
-#pragma unroll
-    for (int u = 0; u < U; ++u)
-#pragma unroll
-      for (int r = 0; r < R; ++r) {
-        const T t = acc[r] + term<ALPHA>(v[u].v[r], xr[u].v[r], alpha, pf);
-        acc[r] = pick(c[u] >= 0, t, acc[r]);
-      }
-  }
-  if (TB && k < len) {  // the last len % U entries as one masked batch
-    int32_t c[U];
-    Pack<T, R> v[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) c[u] = k + u < len ? ld<NT>(&cp[(k + u) * 64]) : -1;
-#pragma unroll
-    for (int u = 0; u < U; ++u)
-      if (k + u < len) v[u] = ld<NT>(&vp[(k + u) * 64]);
-    Pack<T, R> xr[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u)
-      if (k + u < len) xr[u] = x.template run<R>(c[u] >= 0 ? c[u] : 0);
-#pragma unroll
-    for (int u = 0; u < U; ++u)
-#pragma unroll
-      for (int r = 0; r < R; ++r) {
-        const T t = acc[r] + term<ALPHA>(v[u].v[r], xr[u].v[r], alpha, pf);
-        acc[r] = pick(k + u < len && c[u] >= 0, t, acc[r]);
-      }
-    k = len;
-  }
-  for (; !SH && k < len; ++k) {
-    const int32_t c = ld<NT>(&cp[k * 64]);
-    const Pack<T, R> v = ld<NT>(&vp[k * 64]);
-    const Pack<T, R> xr = x.template run<R>(c >= 0 ? c : 0);
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-      const T t = acc[r] + term<ALPHA>(v.v[r], xr.v[r], alpha, pf);
-      acc[r] = pick(c >= 0, t, acc[r]);
     }
   }
 }
@@ -551,113 +453,6 @@ __device__ __forceinline__ void rows_pattern(T (&acc)[R], const int32_t* __restr
   }
 }
 
-// One T from the neighbouring lane by a DPP wave shift (GFX9 wave_shr:1 /
-// wave_shl:1, no LDS): lane l gets lane l-1's (SHR) or l+1's (SHL) value;
-// lane 0 (SHR) and lane 63 (SHL) get 0, for the caller to patch.  Every lane
-// of the wave must be active.
-constexpr int kDppWaveShr1 = 0x138, kDppWaveShl1 = 0x130;
-template <int CTRL, typename T>
-__device__ __forceinline__ T lane_shift(T v) {
-  static_assert(sizeof(T) % 4 == 0, "dword values");
-  uint32_t w[sizeof(T) / 4];
-  __builtin_memcpy(w, &v, sizeof(T));
-#pragma unroll
-  for (int i = 0; i < (int)(sizeof(T) / 4); ++i)
-    w[i] = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)w[i], CTRL, 0xf, 0xf, false);
-  T o;
-  __builtin_memcpy(&o, w, sizeof(T));
-  return o;
-}
-
-#if PA_DT_DEFINE
-// Per pattern slice (build time): does its pattern consist of consecutive
-// triples (o-1, o, o+1)?  (FE27: its 9 x-lines.)  Checking in the SpMV
-// itself costs a chain of dependent scalar loads per wave before its first
-// value load (+8 % on FE27 256³), so it is one byte per slice.
-__global__ void k_pattern_triples(int64_t ns, int kmax, const int32_t* __restrict__ kind,
-                                  const int32_t* __restrict__ plen, const int32_t* __restrict__ pat,
-                                  uint8_t* __restrict__ tri) {
-  const int64_t s = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  if (s >= ns) return;
-  const int len = plen[s];
-  bool ok = kind[s] == 1 && len >= 3 && len % 3 == 0;
-  const int32_t* p = pat + s * kmax;
-  for (int t = 0; ok && t < len; t += 3) ok = p[t + 1] == p[t] + 1 && p[t + 2] == p[t] + 2;
-  tri[s] = ok ? 1 : 0;
-}
-
-void launch_pattern_triples(const pa_mat* A, uint8_t* tri, hipStream_t st) {
-  const int64_t ns = A->nslices;
-  if (ns == 0) return;
-  hipLaunchKernelGGL(k_pattern_triples, dim3((unsigned)((ns + 255) / 256)), dim3(256), 0, st, ns, A->kmax, A->d_kind,
-                     A->d_plen, A->d_pat, tri);
-}
-#endif
-
-// Triple-pattern rows: per triple (o-1, o, o+1) ONE 16 B x run per lane, at
-// the centre offset o; the dx = -1 / +1 runs are the same values moved by
-// one row, taken from the neighbouring lanes (lane_shift) — lanes 0 and 63
-// fetch the one value past the slice's edge.  A third of rows_pattern's x
-// loads (the x loads cost the headline 6 % even as L2 hits,
-// profiles/r02/stream/).  Same terms in the same order: entries 3t, 3t+1,
-// 3t+2 of each row in turn.  Lanes load at their natural rows whether or
-// not their rows are regular (a regular neighbour may need the value),
-// clamped into the 64 B padding of x when far out of range (then no regular
-// row reads it).  nx: x length.
-template <typename T, int R, bool ALPHA, bool NT>
-__device__ __forceinline__ void rows_pattern3(T (&acc)[R], const int32_t* __restrict__ pat,
-                                              const Pack<T, R>* __restrict__ vp, int len,
-                                              const T* __restrict__ x, int64_t row0, int64_t srow0, int64_t nx,
-                                              T alpha, bool pf) {
-  constexpr int H = 64 * R;
-  const int lane = threadIdx.x & 63;
-  const int nt = len / 3;
-  auto center = [&](int o, Pack<T, R>& c, T& e) {
-    int64_t i = row0 + o;
-    i = i < -(int64_t)R ? -(int64_t)R : (i > nx ? nx : i);
-    c = ld_xrun<T, R>(x + i);
-    e = zero_of<T>();
-    if (lane == 0 || lane == 63) {
-      int64_t j = lane == 0 ? srow0 + o - 1 : srow0 + H + o;
-      j = j < -1 ? -1 : (j > nx ? nx : j);
-      e = x[j];
-    }
-  };
-  auto triple = [&](const Pack<T, R>* v, const Pack<T, R>& c, T e) {
-    T lo = lane_shift<kDppWaveShr1>(c.v[R - 1]);
-    T hi = lane_shift<kDppWaveShl1>(c.v[0]);
-    if (lane == 0) lo = e;
-    if (lane == 63) hi = e;
-#pragma unroll
-    for (int r = 0; r < R; ++r) acc[r] = acc[r] + term<ALPHA>(v[0].v[r], r == 0 ? lo : c.v[r - 1], alpha, pf);
-#pragma unroll
-    for (int r = 0; r < R; ++r) acc[r] = acc[r] + term<ALPHA>(v[1].v[r], c.v[r], alpha, pf);
-#pragma unroll
-    for (int r = 0; r < R; ++r) acc[r] = acc[r] + term<ALPHA>(v[2].v[r], r == R - 1 ? hi : c.v[r + 1], alpha, pf);
-  };
-  int t = 0;
-  for (; t + 3 <= nt; t += 3) {  // 3 triples (9 entries) in flight
-    Pack<T, R> v[9];
-#pragma unroll
-    for (int u = 0; u < 9; ++u) v[u] = ld<NT>(&vp[(3 * t + u) * 64]);
-    Pack<T, R> c[3];
-    T e[3];
-#pragma unroll
-    for (int q = 0; q < 3; ++q) center(pat[3 * (t + q) + 1], c[q], e[q]);
-#pragma unroll
-    for (int q = 0; q < 3; ++q) triple(&v[3 * q], c[q], e[q]);
-  }
-  for (; t < nt; ++t) {
-    Pack<T, R> v[3];
-#pragma unroll
-    for (int u = 0; u < 3; ++u) v[u] = ld<NT>(&vp[(3 * t + u) * 64]);
-    Pack<T, R> c;
-    T e;
-    center(pat[3 * t + 1], c, e);
-    triple(v, c, e);
-  }
-}
-
 // α of the device CG state in the wide type W (Float64 / ComplexF64)
 template <typename W> __device__ inline W cg_alpha_of(const CGState* st);
 template <> __device__ inline double cg_alpha_of<double>(const CGState* st) { return st->alpha.re; }
@@ -711,10 +506,9 @@ __device__ __forceinline__ void cg_rows_update(const SpmvArgs<T>& a, const XS& x
 // BMODE: 0 → acc = 0 (β == 0: fill!(co,0)), 1 → acc = y (β == 1),
 //        2 → acc = y*β (rmul!(co,β)).  Interfaces.jl:2262-2263.
 // PK: the launch's slices are int32-column slices (0), pattern slices (1:
-// implied columns for the rows of their mask), multi-pattern slices (2:
-// the same with one of PA_MP_NP patterns per lane, staged in LDS) or
-// delta16 slices (3: 2 B column codes decoded against the row); one
-// kernel per kind keeps the hot loop free of the others' code and registers.
+// implied columns for the rows of their mask) or delta16 slices (3: 2 B
+// column codes decoded against the row); one kernel per kind keeps the hot
+// loop free of the others' code and registers.
 // One wave computes work item w (slice a.list[w], or w) of the structure a.
 // SH: every row of the launch has at most U entries (FD7: 7) — the masked
 // batch alone, no loop code (fewer registers, more waves per SIMD).
@@ -725,12 +519,11 @@ __device__ __forceinline__ void cg_rows_update(const SpmvArgs<T>& a, const XS& x
 // wave only applies a pending x update.
 template <typename T, int R, bool ALPHA, int BMODE, int U, int PK, bool SH = false, bool XV = false>
 __device__ __forceinline__ void spmv_wave(const SpmvArgs<T>& a, const int64_t w) {
-  constexpr bool PAT = PK == 1 || PK == 2;  // implied columns (mask of regular rows)
+  constexpr bool PAT = PK == 1;  // implied columns (mask of regular rows)
   constexpr int H = 64 * R;
   const int lane = threadIdx.x & 63;
   const int64_t s = a.list ? (int64_t)a.list[w] : w;
-  // the lane's first row: quad-sorted layout (qmap) or identity
-  const int64_t row0 = a.qmap ? (int64_t)a.qmap[s * 64 + lane] : s * H + (int64_t)lane * R;
+  const int64_t row0 = s * H + (int64_t)lane * R;  // the lane's first row
   XSrc<T, XV> xs;
   bool xpend = false, main_rows = false;
   typename wide_of<T>::type xalpha{};
@@ -784,16 +577,8 @@ __device__ __forceinline__ void spmv_wave(const SpmvArgs<T>& a, const int64_t w)
   const Pack<T, R>* __restrict__ vp = reinterpret_cast<const Pack<T, R>*>(a.val + off) + lane;
   const bool tb = (a.flags & SPMV_TAILB) != 0;
   const bool pf = (a.flags & SPMV_PRODA) != 0;
-  if constexpr (PK == 2) {
-    // this wave's patterns → LDS; each lane reads its own pattern's offsets
-    __shared__ int32_t spat[4][PA_MP_NP * PA_MP_K];
-    int32_t* wp = spat[threadIdx.x >> 6];
-    const int np = PA_MP_NP * a.kmax;
-    for (int i = lane; i < np; i += 64) wp[i] = a.pat[s * np + i];
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    const int32_t* pat = wp + (int)a.psel[s * 64 + lane] * a.kmax;
+  if constexpr (PK == 1) {
+    const int32_t* pat = a.pat + s * a.kmax;
     if (a.flags & SPMV_XPAIR) {
       if (a.flags & SPMV_NT) rows_pattern<T, R, ALPHA, true, U, true, SH>(acc, pat, vp, len, xs, row0, ok, a.alpha, pf, tb);
       else rows_pattern<T, R, ALPHA, false, U, true, SH>(acc, pat, vp, len, xs, row0, ok, a.alpha, pf, tb);
@@ -801,38 +586,15 @@ __device__ __forceinline__ void spmv_wave(const SpmvArgs<T>& a, const int64_t w)
       if (a.flags & SPMV_NT) rows_pattern<T, R, ALPHA, true, U, false, SH>(acc, pat, vp, len, xs, row0, ok, a.alpha, pf, tb);
       else rows_pattern<T, R, ALPHA, false, U, false, SH>(acc, pat, vp, len, xs, row0, ok, a.alpha, pf, tb);
     }
-  } else if constexpr (PK == 1) {
-    const int32_t* pat = a.pat + s * a.kmax;
-    bool tri = false;
-    if constexpr (!SH && !XV && sizeof(Pack<T, R>) == 16)
-      tri = (a.flags & SPMV_XPAIR) && (a.flags & SPMV_XTRI) && a.ptri && a.ptri[s] && !a.qmap;
-    if (tri) {
-      if constexpr (!SH && !XV && sizeof(Pack<T, R>) == 16) {
-        if (a.flags & SPMV_NT) rows_pattern3<T, R, ALPHA, true>(acc, pat, vp, len, a.x, row0, s * H, a.nx, a.alpha, pf);
-        else rows_pattern3<T, R, ALPHA, false>(acc, pat, vp, len, a.x, row0, s * H, a.nx, a.alpha, pf);
-      }
-    } else if (a.flags & SPMV_XPAIR) {
-      if (a.flags & SPMV_NT) rows_pattern<T, R, ALPHA, true, U, true, SH>(acc, pat, vp, len, xs, row0, ok, a.alpha, pf, tb);
-      else rows_pattern<T, R, ALPHA, false, U, true, SH>(acc, pat, vp, len, xs, row0, ok, a.alpha, pf, tb);
-    } else {
-      if (a.flags & SPMV_NT) rows_pattern<T, R, ALPHA, true, U, false, SH>(acc, pat, vp, len, xs, row0, ok, a.alpha, pf, tb);
-      else rows_pattern<T, R, ALPHA, false, U, false, SH>(acc, pat, vp, len, xs, row0, ok, a.alpha, pf, tb);
-    }
-  } else if constexpr (PK == 4) {
-    const int32_t* __restrict__ cp = (const int32_t*)a.col + off / R + lane;
-    if (a.flags & SPMV_NT) rows_qrun<T, R, ALPHA, true, U, SH>(acc, cp, vp, len, xs, a.alpha, pf, tb);
-    else rows_qrun<T, R, ALPHA, false, U, SH>(acc, cp, vp, len, xs, a.alpha, pf, tb);
   } else if constexpr (PK == 3) {
     const S16Pack<R>* __restrict__ cp = reinterpret_cast<const S16Pack<R>*>(a.col16 + off) + lane;
     const int32_t gb = a.gbase[s];
-    const bool xrun = (a.flags & SPMV_XRUN) != 0;
-    if (a.flags & SPMV_NT) rows_d16<T, R, ALPHA, true, U, SH>(acc, cp, vp, len, xs, a.alpha, pf, tb, (int32_t)row0, gb, xrun);
-    else rows_d16<T, R, ALPHA, false, U, SH>(acc, cp, vp, len, xs, a.alpha, pf, tb, (int32_t)row0, gb, xrun);
+    if (a.flags & SPMV_NT) rows_d16<T, R, ALPHA, true, U, SH>(acc, cp, vp, len, xs, a.alpha, pf, tb, (int32_t)row0, gb);
+    else rows_d16<T, R, ALPHA, false, U, SH>(acc, cp, vp, len, xs, a.alpha, pf, tb, (int32_t)row0, gb);
   } else {
     const IPack<R>* __restrict__ cp = reinterpret_cast<const IPack<R>*>(a.col + off) + lane;
-    const bool xrun = (a.flags & SPMV_XRUN) != 0;
-    if (a.flags & SPMV_NT) rows_int32<T, R, ALPHA, true, U, SH>(acc, cp, vp, len, xs, a.alpha, pf, tb, xrun);
-    else rows_int32<T, R, ALPHA, false, U, SH>(acc, cp, vp, len, xs, a.alpha, pf, tb, xrun);
+    if (a.flags & SPMV_NT) rows_int32<T, R, ALPHA, true, U, SH>(acc, cp, vp, len, xs, a.alpha, pf, tb);
+    else rows_int32<T, R, ALPHA, false, U, SH>(acc, cp, vp, len, xs, a.alpha, pf, tb);
   }
 
   // XV: u_new (and the deferred x update) of the main structure's rows
@@ -882,8 +644,7 @@ __device__ __forceinline__ void spmv_wave(const SpmvArgs<T>& a, const int64_t w)
 
 template <typename T, int R, bool ALPHA, int BMODE, int U, int PK, bool SH = false, bool XV = false>
 __global__ __launch_bounds__(256) void k_spmv_sell(SpmvArgs<T> a) {
-  const int64_t blk = (a.flags & SPMV_XCD) ? xcd_remap(blockIdx.x, gridDim.x) : (int64_t)blockIdx.x;
-  const int64_t w = blk * 4 + (threadIdx.x >> 6);
+  const int64_t w = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (w >= a.nwork) return;
   spmv_wave<T, R, ALPHA, BMODE, U, PK, SH, XV>(a, w);
 }
@@ -915,7 +676,7 @@ template <typename T, int R, bool ALPHA, int BMODE, int PAT>
 static void launch_group_t(const SpmvGroup<T>& g, hipStream_t st) {
   const int64_t blocks = (g.start[g.np] + 3) / 4;
   if (blocks == 0) return;
-  bool sh = PAT != 2 && (g_spmv_flags & SPMV_SHORT);
+  bool sh = (g_spmv_flags & SPMV_SHORT) != 0;
   for (int i = 0; i < g.np; ++i) sh = sh && g.a[i].maxlen <= 8;
   if constexpr (!ALPHA && BMODE == 0) {
     if (g.a[0].cg) {  // the device CG's fused u update
@@ -926,12 +687,10 @@ static void launch_group_t(const SpmvGroup<T>& g, hipStream_t st) {
       return;
     }
   }
-  // (spmv_unroll 4 applies to the merged launch only: the per-kind
-  // launches keep U = 8, which keeps the library's code objects small)
   if (sh)
-    hipLaunchKernelGGL((k_spmv_sell_group<T, R, ALPHA, BMODE, 8, PAT, true>), dim3(blocks), dim3(256), g_spmv_lds, st, g);
+    hipLaunchKernelGGL((k_spmv_sell_group<T, R, ALPHA, BMODE, 8, PAT, true>), dim3(blocks), dim3(256), 0, st, g);
   else
-    hipLaunchKernelGGL((k_spmv_sell_group<T, R, ALPHA, BMODE, 8, PAT>), dim3(blocks), dim3(256), g_spmv_lds, st, g);
+    hipLaunchKernelGGL((k_spmv_sell_group<T, R, ALPHA, BMODE, 8, PAT>), dim3(blocks), dim3(256), 0, st, g);
 }
 
 template <typename T, int R, int PAT>
@@ -953,17 +712,17 @@ static void launch_t(const SpmvArgs<T>& a, hipStream_t st) {
   if (blocks == 0) return;
   if constexpr (!ALPHA && BMODE == 0) {
     if (a.cg) {  // the device CG's fused u update
-      if (PAT != 2 && (g_spmv_flags & SPMV_SHORT) && a.maxlen <= 8)
+      if ((g_spmv_flags & SPMV_SHORT) && a.maxlen <= 8)
         hipLaunchKernelGGL((k_spmv_sell<T, R, false, 0, 8, PAT, true, true>), dim3(blocks), dim3(256), 0, st, a);
       else
         hipLaunchKernelGGL((k_spmv_sell<T, R, false, 0, 8, PAT, false, true>), dim3(blocks), dim3(256), 0, st, a);
       return;
     }
   }
-  if (PAT != 2 && (g_spmv_flags & SPMV_SHORT) && a.maxlen <= 8)
-    hipLaunchKernelGGL((k_spmv_sell<T, R, ALPHA, BMODE, 8, PAT, true>), dim3(blocks), dim3(256), g_spmv_lds, st, a);
+  if ((g_spmv_flags & SPMV_SHORT) && a.maxlen <= 8)
+    hipLaunchKernelGGL((k_spmv_sell<T, R, ALPHA, BMODE, 8, PAT, true>), dim3(blocks), dim3(256), 0, st, a);
   else
-    hipLaunchKernelGGL((k_spmv_sell<T, R, ALPHA, BMODE, 8, PAT>), dim3(blocks), dim3(256), g_spmv_lds, st, a);
+    hipLaunchKernelGGL((k_spmv_sell<T, R, ALPHA, BMODE, 8, PAT>), dim3(blocks), dim3(256), 0, st, a);
 }
 
 template <typename T, int R, int PAT>
@@ -980,9 +739,8 @@ static void launch_ab(const SpmvArgs<T>& a, bool has_alpha, int bmode, hipStream
 }
 
 // which = 0: pattern slices of the main structure; 1: int32-column slices
-// of the main structure; 2: side SELL; 3: multi-pattern slices of the main
-// structure; 4: delta16 slices of the main structure; 5: quad-run slices of
-// the main structure.  list/nwork select the slices.
+// of the main structure; 2: side SELL; 4: delta16 slices of the main
+// structure.  list/nwork select the slices.
 template <typename T>
 static SpmvArgs<T> make_args(int which, int64_t nwork, const int32_t* list, const pa_mat* A, const void* x,
                              void* y, const int32_t* ymap, const void* alpha, const void* beta, void* dotp,
@@ -1010,7 +768,6 @@ static SpmvArgs<T> make_args(int which, int64_t nwork, const int32_t* list, cons
              : which == 2 ? A->maxlen_side
              : which == 1 ? ((g_spmv_format == 1 && A->has_pat) ? A->maxlen_pm_int : A->maxlen_all)
              : which == 4 ? A->maxlen_d16
-             : which == 5 ? A->maxlen_qrun
                           : INT32_MAX;
   if (which == 2) {
     a.soff = (decltype(a.soff))(A->d_s_off);
@@ -1024,22 +781,13 @@ static SpmvArgs<T> make_args(int which, int64_t nwork, const int32_t* list, cons
     a.col = (decltype(a.col))(A->d_col);
     a.val = (decltype(a.val))((const T*)A->d_val);
     a.nrows = A->nrows;
-    a.qmap = (decltype(a.qmap))(A->d_qmap);
     if (which == 0) {
       a.slen = (decltype(a.slen))(A->d_plen);
       a.pat = (decltype(a.pat))(A->d_pat);
-      a.ptri = (decltype(a.ptri))(A->d_ptri);
       a.mask = (decltype(a.mask))(A->d_mask);
       a.kmax = A->kmax;
-    } else if (which == 3) {
-      a.slen = (decltype(a.slen))(A->d_plen);
-      a.pat = (decltype(a.pat))(A->d_mpat);
-      a.mask = (decltype(a.mask))(A->d_mask);
-      a.kmax = A->kmp;
-      a.psel = (decltype(a.psel))(A->d_psel);
     } else {
       a.slen = (decltype(a.slen))(A->d_slice_len);
-      if (which == 5) a.col = (decltype(a.col))(A->d_qcol);
       if (which == 4) {
         a.col16 = (decltype(a.col16))(A->d_col16);
         a.gbase = (decltype(a.gbase))(A->d_gbase);
@@ -1059,9 +807,7 @@ static void launch_which(int which, int64_t nwork, const int32_t* list, const pa
                          const void* beta, void* dotp, hipStream_t st, const SpmvPart* cgp) {
   const SpmvArgs<T> a = make_args<T>(which, nwork, list, A, x, y, ymap, alpha, beta, dotp, cgp);
   if (which == 0) launch_ab<T, R, 1>(a, has_alpha, bmode, st);
-  else if (which == 3) launch_ab<T, R, 2>(a, has_alpha, bmode, st);
   else if (which == 4) launch_ab<T, R, 3>(a, has_alpha, bmode, st);
-  else if (which == 5) launch_ab<T, R, 4>(a, has_alpha, bmode, st);
   else launch_ab<T, R, 0>(a, has_alpha, bmode, st);
 }
 
@@ -1073,9 +819,7 @@ static void group_which(int which, int np, const SpmvPart* parts, bool has_alpha
   auto flush = [&]() {
     if (g.np == 0) return;
     if (which == 0) launch_group_ab<T, R, 1>(g, has_alpha, bmode, st);
-    else if (which == 3) launch_group_ab<T, R, 2>(g, has_alpha, bmode, st);
     else if (which == 4) launch_group_ab<T, R, 3>(g, has_alpha, bmode, st);
-    else if (which == 5) launch_group_ab<T, R, 4>(g, has_alpha, bmode, st);
     else launch_group_ab<T, R, 0>(g, has_alpha, bmode, st);
     g = SpmvGroup<T>{};
   };
@@ -1163,10 +907,7 @@ struct SpmvTable {
 
 template <typename T, int R, bool ALPHA, int BMODE, int U, bool SH, bool XV = false>
 __device__ __forceinline__ void merged_wave(const SpmvTable<T>* __restrict__ tab) {
-  // SPMV_XCD: consecutive blocks on one XCD (each XCD sweeps its own row
-  // range, so the x window of its waves stays in its L2)
-  const int64_t blk = (tab->a[0].flags & SPMV_XCD) ? xcd_remap(blockIdx.x, gridDim.x) : (int64_t)blockIdx.x;
-  const int64_t w = blk * 4 + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const int64_t w = (int64_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   const int n = tab->n;
   if (w >= tab->start[n]) return;
   int lo = 0, hi = n;  // last entry whose start <= w
@@ -1180,9 +921,7 @@ __device__ __forceinline__ void merged_wave(const SpmvTable<T>* __restrict__ tab
   const SpmvArgs<T>& a = tab->a[p];
   if (pk == 1) spmv_wave<T, R, ALPHA, BMODE, U, 1, SH, XV>(a, lw);
   else if (pk == 3) spmv_wave<T, R, ALPHA, BMODE, U, 3, SH, XV>(a, lw);
-  else if (pk == 0) spmv_wave<T, R, ALPHA, BMODE, U, 0, SH, XV>(a, lw);
-  else if (pk == 4) spmv_wave<T, R, ALPHA, BMODE, U, 4, SH, XV>(a, lw);
-  else if constexpr (!SH) spmv_wave<T, R, ALPHA, BMODE, U, 2, false, XV>(a, lw);
+  else spmv_wave<T, R, ALPHA, BMODE, U, 0, SH, XV>(a, lw);
 }
 
 // No occupancy cap: amdgpu_waves_per_eu(4) (F32 134 -> 128 VGPRs, a small
@@ -1203,54 +942,23 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
   merged_wave<T, R, ALPHA, BMODE, 8, true>(tab);
 }
 
-// Occupancy variants of the short-row F64 launch (pa_tune "spmv_short_occ",
-// C2's FD7 operator: 16 K one-wave slices are 3.35 rounds of resident waves
-// at 5 per SIMD): 1 = U 4 at 8 waves per SIMD (2.1 rounds), 2 = U 4 at 6,
-// 3 = the one-batch kernel at 6.
-template <typename T, int R, bool ALPHA, int BMODE>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k_spmv_merged_u4w8(
-    const SpmvTable<T>* __restrict__ tab) {
-  merged_wave<T, R, ALPHA, BMODE, 4, false>(tab);
-}
-template <typename T, int R, bool ALPHA, int BMODE>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k_spmv_merged_u4w6(
-    const SpmvTable<T>* __restrict__ tab) {
-  merged_wave<T, R, ALPHA, BMODE, 4, false>(tab);
-}
-template <typename T, int R, bool ALPHA, int BMODE>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k_spmv_merged_shw6(
-    const SpmvTable<T>* __restrict__ tab) {
-  merged_wave<T, R, ALPHA, BMODE, 8, true>(tab);
-}
-
 template <typename T, int R, bool ALPHA, int BMODE>
 static void launch_merged_t(const SpmvTable<T>* d, int64_t waves, bool sh, hipStream_t st) {
   const int64_t blocks = (waves + 3) / 4;
   if (blocks == 0) return;
   if constexpr (std::is_same<T, double>::value) {
-    if (sh && g_spmv_short_occ) {
-      if (g_spmv_short_occ == 1)
-        hipLaunchKernelGGL((k_spmv_merged_u4w8<T, R, ALPHA, BMODE>), dim3(blocks), dim3(256), 0, st, d);
-      else if (g_spmv_short_occ == 2)
-        hipLaunchKernelGGL((k_spmv_merged_u4w6<T, R, ALPHA, BMODE>), dim3(blocks), dim3(256), 0, st, d);
-      else
-        hipLaunchKernelGGL((k_spmv_merged_shw6<T, R, ALPHA, BMODE>), dim3(blocks), dim3(256), 0, st, d);
-      return;
-    }
     if (sh) {
-      hipLaunchKernelGGL((k_spmv_merged_short<T, R, ALPHA, BMODE>), dim3(blocks), dim3(256), g_spmv_lds, st, d);
+      hipLaunchKernelGGL((k_spmv_merged_short<T, R, ALPHA, BMODE>), dim3(blocks), dim3(256), 0, st, d);
       return;
     }
   }
   if (sh)
-    hipLaunchKernelGGL((k_spmv_merged<T, R, ALPHA, BMODE, 8, true>), dim3(blocks), dim3(256), g_spmv_lds, st, d);
-  else if (g_spmv_unroll == 4)
-    hipLaunchKernelGGL((k_spmv_merged<T, R, ALPHA, BMODE, 4, false>), dim3(blocks), dim3(256), g_spmv_lds, st, d);
+    hipLaunchKernelGGL((k_spmv_merged<T, R, ALPHA, BMODE, 8, true>), dim3(blocks), dim3(256), 0, st, d);
   else
-    hipLaunchKernelGGL((k_spmv_merged<T, R, ALPHA, BMODE, 8, false>), dim3(blocks), dim3(256), g_spmv_lds, st, d);
+    hipLaunchKernelGGL((k_spmv_merged<T, R, ALPHA, BMODE, 8, false>), dim3(blocks), dim3(256), 0, st, d);
 }
 
-static int pk_of(int which) { return which == 0 ? 1 : which == 3 ? 2 : which == 4 ? 3 : which == 5 ? 4 : 0; }
+static int pk_of(int which) { return which == 0 ? 1 : which == 4 ? 3 : 0; }
 
 template <typename T, int R>
 static int merged_t(int n, const int* which, const SpmvPart* parts, bool has_alpha, int bmode, const void* alpha,
@@ -1266,7 +974,7 @@ static int merged_t(int n, const int* which, const SpmvPart* parts, bool has_alp
     if ((g_spmv_flags & SPMV_IDLIST) && list && which[i] != 2 && q.nwork == q.A->nslices) list = nullptr;
     h.a[h.n] = make_args<T>(which[i], q.nwork, list, q.A, q.x, q.y, q.ymap, alpha, beta, q.dotp, &q);
     h.pk[h.n] = pk_of(which[i]);
-    sh = sh && h.pk[h.n] != 2 && h.a[h.n].maxlen <= 8;
+    sh = sh && h.a[h.n].maxlen <= 8;
     h.start[h.n + 1] = h.start[h.n] + q.nwork;
     ++h.n;
   }
@@ -1916,37 +1624,25 @@ void launch_gather_ptrs(int P, const void* const* srcs, int accsz, void* out, hi
 // of the slice (or the row at 1/4 or 3/4 when more rows follow that one); its
 // offsets pat[k] = col_k - row.  A row is regular for a
 // candidate when its column sequence is exactly row + pat[k] (same length).
-// Multi-pattern (NP > 1): while lanes are left without a pattern, the first
-// such lane's first full-length row becomes the next candidate; each lane
-// takes the first candidate that one of its rows follows, and its rows that
-// follow it are regular.  The slice keeps the cheapest encoding by streamed
-// bytes: int32 (S+4 per slot), single pattern or multi-pattern (S per slot
-// plus S+4 again for every side row's entry); multi-pattern must save more
-// than 1/16 of the int32 cost over the next best to be taken.
+// The slice becomes a pattern slice when at least half its rows are regular
+// (the others go to the side SELL).
 
 template <int R>
 __global__ __launch_bounds__(256) void k_pattern_detect(int64_t nrows, int64_t nslices,
                                                         const int64_t* __restrict__ soff,
                                                         const int32_t* __restrict__ slen,
-                                                        const int32_t* __restrict__ col, int64_t noids,
-                                                        int kmax, int S, int NP, int kmp, int rule,
+                                                        const int32_t* __restrict__ col, int64_t noids, int kmax,
                                                         int32_t* __restrict__ kind,
                                                         int32_t* __restrict__ plen,
                                                         int32_t* __restrict__ pat,
                                                         uint64_t* __restrict__ mask,
                                                         int32_t* __restrict__ pghost,
-                                                        int32_t* __restrict__ nirreg,
-                                                        int32_t* __restrict__ mpat,
-                                                        uint8_t* __restrict__ psel,
-                                                        const int32_t* __restrict__ qmap) {
+                                                        int32_t* __restrict__ nirreg) {
   constexpr int H = 64 * R;
   const int lane = threadIdx.x & 63;
   const int64_t s = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (s >= nslices) return;
-  // the oid of the row at (lane, r) of this slice (quad-sorted or identity)
-  auto oid = [&](int ln, int r) -> int64_t {
-    return qmap ? (int64_t)qmap[s * 64 + ln] + r : s * H + (int64_t)ln * R + r;
-  };
+  auto oid = [&](int ln, int r) -> int64_t { return s * H + (int64_t)ln * R + r; };
   const int64_t off = soff[s];
   const int L = slen[s];
   const int64_t rem = nrows - s * H;
@@ -2008,11 +1704,6 @@ __global__ __launch_bounds__(256) void k_pattern_detect(int64_t nrows, int64_t n
     for (int d = 32; d >= 1; d >>= 1) t += __shfl_xor(t, d, 64);
     return t;
   };
-  auto store_pat = [&](int32_t* dst, int clane, int cr) {
-    const int64_t crow = oid(clane, cr);
-    for (int k = lane; k < Lp; k += 64)
-      dst[k] = col[off + ((int64_t)k * 64 + clane) * R + cr] - (int32_t)crow;
-  };
   bool g1 = false;
   unsigned bits1 = follow(mlane, mr, g1);
   int tot1 = wave_count(bits1);
@@ -2035,58 +1726,24 @@ __global__ __launch_bounds__(256) void k_pattern_detect(int64_t nrows, int64_t n
       }
     }
   }
-  // multi-pattern passes
-  const bool mp = NP > 1 && Lp > 0 && Lp <= kmp && tot1 < nvalid;
-  unsigned bitsM = bits1;
-  int sel = bits1 ? 0 : -1;
-  bool gM = g1;
-  int totM = tot1;
-  if (mp) {
-    store_pat(mpat + (s * PA_MP_NP) * kmp, mlane, mr);
-    for (int p = 1; p < NP; ++p) {
-      int myr = -1;
-      if (sel < 0)
-        for (int r = R - 1; r >= 0; --r)
-          if (rlen[r] == Lp) myr = r;
-      const uint64_t b = __ballot(myr >= 0);
-      if (b == 0) break;
-      const int cl = __ffsll((unsigned long long)b) - 1;
-      const int cr = __shfl(myr, cl, 64);
-      bool g = false;
-      const unsigned bits = follow(cl, cr, g);
-      if (sel < 0 && bits) {
-        sel = p;
-        bitsM |= bits;
-        gM = gM || g;
-      }
-      store_pat(mpat + (s * PA_MP_NP + p) * kmp, cl, cr);
-    }
-    totM = wave_count(bitsM);
-  }
-  const int64_t SI = S + 4;
-  const int64_t c_int = SI * nvalid;
-  const int64_t c_one = (int64_t)S * nvalid + SI * (nvalid - tot1);
-  const int64_t c_mp = (int64_t)S * nvalid + SI * (nvalid - totM);
-  int best = 0;
-  int64_t bc = c_int;
-  if (Lp > 0 && (rule ? c_one < bc : 2 * tot1 >= nvalid)) { best = 1; bc = c_one; }
-  if (mp && c_mp + c_int / 16 < bc) { best = 2; bc = c_mp; }
-  const bool gr = __any(best == 1 ? g1 : gM);
+  // a pattern slice when at least half its rows follow the pattern
+  const bool best = Lp > 0 && 2 * tot1 >= nvalid;
+  const bool gr = __any(g1);
   const bool ga = __any(ghost_any);
-  const int tot = best == 1 ? tot1 : totM;
   if (lane == 0) {
-    kind[s] = best;
+    kind[s] = best ? 1 : 0;
     plen[s] = best ? Lp : L;
     pghost[s] = best ? (gr ? 1 : 0) : (ga ? 1 : 0);
-    nirreg[s] = best ? nvalid - tot : 0;
+    nirreg[s] = best ? nvalid - tot1 : 0;
   }
-  const unsigned bits = best == 1 ? bits1 : (best == 2 ? bitsM : 0u);
-  if (bits) {
+  if (best && bits1) {
     const int i0 = lane * R;
-    atomicOr((unsigned long long*)&mask[s * (H / 64) + i0 / 64], (unsigned long long)bits << (i0 & 63));
+    atomicOr((unsigned long long*)&mask[s * (H / 64) + i0 / 64], (unsigned long long)bits1 << (i0 & 63));
   }
-  if (psel && mp) psel[s * 64 + lane] = (uint8_t)(best == 2 && sel > 0 ? sel : 0);
-  if (best == 1) store_pat(pat + s * kmax, mlane, mr);
+  if (best) {
+    const int64_t crow = oid(mlane, mr);
+    for (int k = lane; k < Lp; k += 64) pat[s * kmax + k] = col[off + ((int64_t)k * 64 + mlane) * R + mr] - (int32_t)crow;
+  }
 }
 
 // delta16 eligibility and codes, one wave per slice: an int32-column slice
@@ -2098,8 +1755,7 @@ __global__ __launch_bounds__(256) void k_delta16(int64_t nslices, const int64_t*
                                                  const int32_t* __restrict__ slen, const int32_t* __restrict__ col,
                                                  const int32_t* __restrict__ kind, const int32_t* __restrict__ sflags,
                                                  int64_t noids, uint16_t* __restrict__ col16,
-                                                 int32_t* __restrict__ gbase, int32_t* __restrict__ ok,
-                                                 const int32_t* __restrict__ qmap) {
+                                                 int32_t* __restrict__ gbase, int32_t* __restrict__ ok) {
   constexpr int H = 64 * R;
   const int64_t s = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (s >= nslices) return;
@@ -2110,7 +1766,7 @@ __global__ __launch_bounds__(256) void k_delta16(int64_t nslices, const int64_t*
   }
   const int64_t off = soff[s];
   const int len = slen[s];
-  const int64_t row0 = qmap ? (int64_t)qmap[s * 64 + lane] : s * H + (int64_t)lane * R;
+  const int64_t row0 = s * H + (int64_t)lane * R;
   int32_t gmin = INT32_MAX;
   for (int k = 0; k < len; ++k)
 #pragma unroll
@@ -2153,7 +1809,7 @@ void launch_delta16(pa_mat* A, int64_t noids, const int32_t* kind, int32_t* ok, 
   if (blocks == 0) return;
 #define PA_D16(RR)                                                                                          \
   hipLaunchKernelGGL(k_delta16<RR>, dim3(blocks), dim3(256), 0, st, A->nslices, A->d_slice_off,              \
-                     A->d_slice_len, A->d_col, kind, A->d_sflags, noids, A->d_col16, A->d_gbase, ok, A->d_qmap)
+                     A->d_slice_len, A->d_col, kind, A->d_sflags, noids, A->d_col16, A->d_gbase, ok)
   switch (A->R) {
     case 1: PA_D16(1); break;
     case 2: PA_D16(2); break;
@@ -2163,210 +1819,19 @@ void launch_delta16(pa_mat* A, int64_t noids, const int32_t* kind, int32_t* ok, 
 }
 
 void launch_pattern_detect(pa_mat* A, int64_t noids, int32_t* kind, int32_t* plen, int32_t* pat,
-                           uint64_t* mask, int32_t* pghost, int32_t* nirreg, int NP, int rule, hipStream_t st) {
+                           uint64_t* mask, int32_t* pghost, int32_t* nirreg, hipStream_t st) {
   const int64_t blocks = (A->nslices + 3) / 4;
   if (blocks == 0) return;
-  const int S = (int)dtype_size(A->dtype);
 #define PA_DET(RR)                                                                                      \
   hipLaunchKernelGGL(k_pattern_detect<RR>, dim3(blocks), dim3(256), 0, st, A->nrows, A->nslices,        \
-                     A->d_slice_off, A->d_slice_len, A->d_col, noids, A->kmax, S, NP, A->kmp, rule, kind, plen, \
-                     pat, mask, pghost, nirreg, A->d_mpat, A->d_psel, A->d_qmap)
+                     A->d_slice_off, A->d_slice_len, A->d_col, noids, A->kmax, kind, plen, pat, mask,  \
+                     pghost, nirreg)
   switch (A->R) {
     case 1: PA_DET(1); break;
     case 2: PA_DET(2); break;
     case 4: PA_DET(4); break;
   }
 #undef PA_DET
-}
-
-// ---------------------------------------------------------------------------
-// Quad sort (irregular partitions, pa_tune "spmv_quadsort"): the lanes of the
-// int32 layout — quads of R consecutive owned rows — are reordered so that
-// lanes of one class share slices: lanes whose R rows read R consecutive
-// columns at every entry (quad-run lanes; among them those with equal column
-// offsets together, which become pattern slices), lanes reading ghosts, and
-// the rest.  Each row keeps its entries in the reference's order; only the
-// slice-lane that holds it changes (qmap).
-
-// Per quad q of the identity layout (slice q/64, lane q%64, rows q*R..):
-// qlen = its longest row; qflag bit 0: every row has the same length and
-// reads the first row's columns + r at every entry, bit 1: a ghost column;
-// qhash: FNV-1a of the first row's column offsets (col - row).
-template <int R>
-__global__ void k_quad_class(int64_t nrows, int64_t nquads, const int64_t* __restrict__ soff,
-                             const int32_t* __restrict__ slen, const int32_t* __restrict__ col, int64_t noids,
-                             int32_t* __restrict__ qlen, uint8_t* __restrict__ qflag, uint64_t* __restrict__ qhash) {
-  const int64_t q = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  if (q >= nquads) return;
-  const int64_t s = q / 64;
-  const int lane = (int)(q % 64);
-  const int64_t off = soff[s];
-  const int L = slen[s];
-  const int64_t row0 = q * R;
-  bool run = row0 + R <= nrows, ghost = false;
-  int lmax = 0, len0 = -1;
-  uint64_t h = 1469598103934665603ull;
-#pragma unroll
-  for (int r = 0; r < R; ++r) {
-    int l = 0;
-    for (int k = 0; k < L; ++k) {
-      const int32_t c = col[off + ((int64_t)k * 64 + lane) * R + r];
-      if (c < 0) break;
-      ++l;
-      if (c >= noids) ghost = true;
-      if (r == 0) h = (h ^ (uint64_t)(uint32_t)(c - (int32_t)row0)) * 1099511628211ull;
-      else if (c != col[off + ((int64_t)k * 64 + lane) * R] + r) run = false;
-    }
-    if (r == 0) len0 = l;
-    else if (l != len0) run = false;
-    lmax = l > lmax ? l : lmax;
-  }
-  qlen[q] = lmax;
-  qflag[q] = (uint8_t)((run && len0 > 0 ? 1 : 0) | (ghost ? 2 : 0));
-  qhash[q] = h;
-}
-
-// the permuted layout: lane l of new slice s holds old quad perm[s*64+l]
-// (-1: a padding lane); entries past a row's end are padding (-1 / zero)
-template <typename T, int R>
-__global__ void k_quad_permute(int64_t nslots_lanes, const int32_t* __restrict__ perm,
-                               const int64_t* __restrict__ nsoff, const int32_t* __restrict__ nslen,
-                               const int64_t* __restrict__ osoff, const int32_t* __restrict__ oslen,
-                               const int32_t* __restrict__ ocol, const T* __restrict__ oval,
-                               int32_t* __restrict__ ncol, T* __restrict__ nval) {
-  const int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  if (p >= nslots_lanes) return;
-  const int64_t ns = p / 64;
-  const int nl = (int)(p % 64);
-  const int32_t q = perm[p];
-  const int64_t os = q >= 0 ? q / 64 : 0;
-  const int ol = q >= 0 ? q % 64 : 0;
-  const int olen = q >= 0 ? oslen[os] : 0;
-  for (int k = 0; k < nslen[ns]; ++k)
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-      const int64_t dst = nsoff[ns] + ((int64_t)k * 64 + nl) * R + r;
-      if (k < olen) {
-        const int64_t src = osoff[os] + ((int64_t)k * 64 + ol) * R + r;
-        ncol[dst] = ocol[src];
-        nval[dst] = oval[src];
-      } else {
-        ncol[dst] = -1;
-        nval[dst] = zero_of<T>();
-      }
-    }
-}
-
-// CSC nz → slot map after the permutation (main slots only; ghost-row and
-// long-row values keep their relative indices)
-__global__ void k_nzslot_remap(int64_t nu, int64_t* __restrict__ nzs, int64_t oslots, int64_t ons,
-                               const int64_t* __restrict__ osoff, int H, int R, const int32_t* __restrict__ inv,
-                               const int64_t* __restrict__ nsoff) {
-  const int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  if (p >= nu) return;
-  const int64_t t = nzs[p];
-  if (t < 0 || t >= oslots) return;
-  int64_t lo = 0, hi = ons;  // last slice whose offset <= t
-  while (hi - lo > 1) {
-    const int64_t mid = (lo + hi) >> 1;
-    if (osoff[mid] <= t) lo = mid; else hi = mid;
-  }
-  const int64_t rem = t - osoff[lo];
-  const int64_t k = rem / H, w = rem % H;
-  const int l = (int)(w / R), r = (int)(w % R);
-  const int64_t np = inv[lo * 64 + l];
-  nzs[p] = nsoff[np / 64] + (k * 64 + np % 64) * R + r;
-}
-
-// quad-run slices: a kind-0 slice (not pattern, no long rows) whose every
-// lane is a quad-run lane (or padding) becomes kind 4: qcol[off/R + k*64 +
-// lane] = the first row's column (-1: padding)
-template <int R>
-__global__ __launch_bounds__(256) void k_qrun_detect(int64_t nrows, int64_t nslices, const int64_t* __restrict__ soff,
-                                                     const int32_t* __restrict__ slen,
-                                                     const int32_t* __restrict__ col, const int32_t* __restrict__ kind,
-                                                     const int32_t* __restrict__ qmap, int32_t* __restrict__ qcol,
-                                                     int32_t* __restrict__ ok) {
-  const int64_t s = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (s >= nslices) return;
-  const int lane = threadIdx.x & 63;
-  if (kind[s] != 0) {
-    if (lane == 0) ok[s] = 0;
-    return;
-  }
-  const int64_t off = soff[s];
-  const int L = slen[s];
-  const int64_t row0 = qmap[s * 64 + lane];
-  int nv = (int)(nrows - row0 < R ? (nrows - row0 > 0 ? nrows - row0 : 0) : R);  // valid rows of the lane
-  bool run = true;
-  int len0 = 0;
-  for (int k = 0; k < L; ++k) {
-    const int32_t c0 = col[off + ((int64_t)k * 64 + lane) * R];
-    if (c0 >= 0) len0 = k + 1;
-  }
-  for (int r = 1; r < nv; ++r)
-    for (int k = 0; k < L; ++k) {
-      const int32_t c0 = col[off + ((int64_t)k * 64 + lane) * R];
-      const int32_t c = col[off + ((int64_t)k * 64 + lane) * R + r];
-      if (k < len0 ? c != c0 + r : c >= 0) run = false;
-    }
-  for (int k = 0; k < len0; ++k)  // no padding inside the first row
-    if (col[off + ((int64_t)k * 64 + lane) * R] < 0) run = false;
-  const bool all = __all(run);
-  if (lane == 0) ok[s] = all ? 1 : 0;
-  if (!all) return;
-  for (int k = 0; k < L; ++k) qcol[off / R + (int64_t)k * 64 + lane] = col[off + ((int64_t)k * 64 + lane) * R];
-}
-
-void launch_quad_class(const pa_mat* A, int64_t noids, int32_t* qlen, uint8_t* qflag, uint64_t* qhash,
-                       hipStream_t st) {
-  const int64_t nq = (A->nrows + A->R - 1) / A->R;
-  if (nq == 0) return;
-  const dim3 g((unsigned)((nq + 255) / 256)), b(256);
-#define PA_QC(RR) hipLaunchKernelGGL(k_quad_class<RR>, g, b, 0, st, A->nrows, nq, A->d_slice_off, A->d_slice_len, \
-                                     A->d_col, noids, qlen, qflag, qhash)
-  switch (A->R) {
-    case 1: PA_QC(1); break;
-    case 2: PA_QC(2); break;
-    case 4: PA_QC(4); break;
-  }
-#undef PA_QC
-}
-
-void launch_quad_permute(const pa_mat* A, int64_t nslices_new, const int32_t* perm, const int64_t* nsoff,
-                         const int32_t* nslen, const int64_t* osoff, const int32_t* oslen, const int32_t* ocol,
-                         const void* oval, int32_t* ncol, void* nval, hipStream_t st) {
-  const int64_t n = nslices_new * 64;
-  if (n == 0) return;
-  const dim3 g((unsigned)((n + 255) / 256)), b(256);
-#define PA_QP(T, RR) hipLaunchKernelGGL((k_quad_permute<T, RR>), g, b, 0, st, n, perm, nsoff, nslen, osoff, oslen, \
-                                        ocol, (const T*)oval, ncol, (T*)nval)
-  switch (A->dtype) {
-    case PA_F32: PA_QP(float, 4); break;
-    case PA_F64: PA_QP(double, 2); break;
-    case PA_C64: PA_QP(c64, 2); break;
-    case PA_C128: PA_QP(c128, 1); break;
-  }
-#undef PA_QP
-}
-
-void launch_nzslot_remap(int64_t nu, int64_t* nzs, int64_t oslots, int64_t ons, const int64_t* osoff, int H, int R,
-                         const int32_t* inv, const int64_t* nsoff, hipStream_t st) {
-  if (nu == 0) return;
-  hipLaunchKernelGGL(k_nzslot_remap, dim3((unsigned)((nu + 255) / 256)), dim3(256), 0, st, nu, nzs, oslots, ons, osoff,
-                     H, R, inv, nsoff);
-}
-
-void launch_qrun_detect(const pa_mat* A, const int32_t* kind, int32_t* qcol, int32_t* ok, hipStream_t st) {
-  const int64_t blocks = (A->nslices + 3) / 4;
-  if (blocks == 0) return;
-#define PA_QR(RR) hipLaunchKernelGGL(k_qrun_detect<RR>, dim3(blocks), dim3(256), 0, st, A->nrows, A->nslices, \
-                                     A->d_slice_off, A->d_slice_len, A->d_col, kind, A->d_qmap, qcol, ok)
-  switch (A->R) {
-    case 2: PA_QR(2); break;
-    case 4: PA_QR(4); break;
-  }
-#undef PA_QR
 }
 
 // Side SELL: the irregular rows (oids, ascending), copied from the int32 layout.

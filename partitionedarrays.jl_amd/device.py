@@ -497,16 +497,9 @@ class DeviceMatrix:
         f = [C.c_int64() for _ in range(4)]
         _lib.call("pa_mat_format_info", self.h, *[C.byref(x) for x in f])
         d.update(zip(["pattern_slices", "regular_rows", "side_rows", "side_slots"], [x.value for x in f]))
-        mp = C.c_int64()
-        _lib.call("pa_mat_multipattern_info", self.h, C.byref(mp))
-        d["multi_pattern_slices"] = mp.value
         dd = C.c_int64()
         _lib.call("pa_mat_delta16_info", self.h, C.byref(dd))
         d["delta16_slices"] = dd.value
-        qr, qs = C.c_int64(), C.c_int()
-        _lib.call("pa_mat_quadrun_info", self.h, C.byref(qr), C.byref(qs))
-        d["quadrun_slices"] = qr.value
-        d["quad_sorted"] = bool(qs.value)
         lr = [C.c_int64() for _ in range(2)]
         _lib.call("pa_mat_long_rows", self.h, *[C.byref(x) for x in lr])
         d.update(zip(["long_rows", "long_nnz"], [x.value for x in lr]))

@@ -61,15 +61,15 @@ def test_tune_knobs_round_trip_and_reject_bad_values(pamd):
     """pa_tune (no device needed): every knob returns its previous value and
     refuses out-of-range values with a PAError; spmv_flags keeps bit 8 (the
     per-matrix CSR flag) out of the user's reach."""
-    knobs = {"spmv_merge": 0, "spmv_merge_max": 1024, "spmv_group": 0, "spmv_unroll": 4, "spmv_delta16": 0,
-             "long_rows_exact": 0, "halo_direct": 0}
+    knobs = {"spmv_merge": 0, "spmv_merge_max": 1024, "spmv_group": 0, "spmv_delta16": 0,
+             "long_rows_exact": 0, "halo_direct": 0, "cg_fuse": 1, "halo_pull": 0, "spmv_format": 0}
     for k, v in knobs.items():
         prev = pamd._lib.tune(k, v)
         assert pamd._lib.tune(k, prev) == v, k
     prev = pamd._lib.tune("spmv_flags", 0)
     try:
-        assert pamd._lib.tune("spmv_flags", prev | 512) == 0
-        for bad in (256, 1024, -1):
+        assert pamd._lib.tune("spmv_flags", prev | 32) == 0
+        for bad in (2, 128, 256, 512, 1024, -1):
             try:
                 pamd._lib.tune("spmv_flags", bad)
                 raise AssertionError(f"spmv_flags accepted {bad}")
@@ -77,9 +77,17 @@ def test_tune_knobs_round_trip_and_reject_bad_values(pamd):
                 pass
     finally:
         pamd._lib.tune("spmv_flags", prev)
-    for k, bad in (("spmv_merge", 2), ("spmv_merge_max", -1), ("spmv_unroll", 3)):
+    for k, bad in (("spmv_merge", 2), ("spmv_merge_max", -1), ("cg_fuse", 3)):
         try:
             pamd._lib.tune(k, bad)
             raise AssertionError(f"{k} accepted {bad}")
+        except pamd.PAError:
+            pass
+    # the knobs of rounds 1-3's negative A/Bs are gone
+    for k in ("spmv_quadsort", "spmv_patterns", "spmv_pattern_rule", "spmv_lds", "comm_cus", "spmv_short_occ",
+              "alloc_contiguous", "spmv_unroll"):
+        try:
+            pamd._lib.tune(k, 0)
+            raise AssertionError(f"{k} still accepted")
         except pamd.PAError:
             pass

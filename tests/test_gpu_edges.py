@@ -207,6 +207,32 @@ def test_graph_replay_survives_cache_eviction(pamd):
         assert np.array_equal(g.local(p)[own], e.local(p)[own]), f"part {p}: graph replay differs from eager"
 
 
+def test_eager_mul_after_failed_capture(pamd, monkeypatch):
+    """A graph capture whose table allocation fails (forced with
+    PA_TEST_FAIL_GRAPH_ALLOC, as on an out-of-memory device) raises, and
+    leaves no state behind: the eager mul! with a halo right
+    after it, and a later capture, both give the same bits as before."""
+    be = pamd.HIPBackend(devices=[0])
+    parts = be.get_part_ids((2, 2, 1))
+    A = pamd.drivers.stencil_operator(parts, (12, 11, 10), 27)
+    x = pamd.PVector.from_host(pamd.map_parts(
+        lambda s: np.random.default_rng(s.part).uniform(-1, 1, s.num_lids), A.cols.partition), A.cols)
+    y0, y1, y2 = (pamd.PVector.undef(A.rows) for _ in range(3))
+    pamd.mul_(y0, A, x)
+    monkeypatch.setenv("PA_TEST_FAIL_GRAPH_ALLOC", "1")
+    with pytest.raises(pamd._lib.PAError, match="graph capture"):
+        pamd.SpMVGraph(y1, A, x)
+    monkeypatch.delenv("PA_TEST_FAIL_GRAPH_ALLOC")
+    pamd.mul_(y1, A, x)
+    G = pamd.SpMVGraph(y2, A, x)
+    G()
+    h0, h1, h2 = y0.to_host(), y1.to_host(), y2.to_host()
+    for p in parts.part_ids:
+        own = A.rows.partition.local(p).oid_to_lid - 1
+        assert np.array_equal(h1.local(p)[own], h0.local(p)[own]), f"part {p}: eager mul! after the failed capture"
+        assert np.array_equal(h2.local(p)[own], h0.local(p)[own]), f"part {p}: graph after the failed capture"
+
+
 def test_spmv_rejects_partial_exchanger_arrays(be, pamd):
     """pa_spmv_all with an exchanger array whose entries are partly null is
     an error ('exchanger missing'), not a host crash."""

@@ -114,39 +114,27 @@ def _irregular_exchange_assemble_dot(be, pamd, O):
     assert abs(pamd.norm(w) - O.norm(ow)) <= 1e-12 * O.norm(ow)
 
 
-@pytest.mark.parametrize("N,nparts,dtype,npat", [
-    (BIG[0], BIG[1], np.float64, 4), (BIG[0], BIG[1], np.float64, 2), (BIG[0], BIG[1], np.float64, 1),
-    (BIG[0], BIG[1], np.float32, 4), (BIG[0], BIG[1], np.complex128, 4),
-    ((24, 22, 20), 8, np.complex64, 4), ((24, 22, 20), 8, np.float64, 3)])
-def test_irregular_multipattern_bitexact(be, pamd, O, N, nparts, dtype, npat):
-    """Multi-pattern slices (one of up to 4 offset patterns per 64-lane row
-    group, pa_tune("spmv_patterns")): Voronoi parts keep their rows in gid
-    order, so a slice spans several x-runs with different y/z offsets.  The
-    product stays bit-exact, and the build takes several patterns where the
-    partition calls for them."""
-    prev = pamd._lib.tune("spmv_patterns", npat)
-    try:
-        parts = be.get_part_ids(nparts)
-        A = pamd.drivers.irregular_problem(parts, N, 27, dtype)
-        OA = _oracle(O, N, nparts, dtype)
-        rng = np.random.default_rng(SEED + 7)
-        xs = {p: _rand(rng, A.cols.partition.local(p).num_lids, dtype) for p in parts.part_ids}
-        x = pamd.PVector.from_host(pamd.map_parts(lambda s: xs[s.part], A.cols.partition), A.cols)
-        y = pamd.PVector.undef(A.rows, dtype)
-        pamd.mul_(y, A, x)
-        ox = O.PVector(O.map_parts(lambda s: _ox(O, xs[s.part]), OA.cols.partition), OA.cols)
-        oy = O.pvector_undef(OA.rows, dtype)
-        O.mul_(oy, OA, ox)
-        got = y.to_host()
-        for p in parts.part_ids:
-            assert _eq(O, got.local(p), oy.values[p]), f"part {p}: SpMV differs (spmv_patterns={npat})"
-        nmulti = sum(i["multi_pattern_slices"] for i in A.info().parts)
-        if npat == 1:
-            assert nmulti == 0
-        elif N == BIG[0]:
-            assert nmulti > 0, "no slice took several patterns on the Voronoi partition"
-    finally:
-        pamd._lib.tune("spmv_patterns", prev)
+@pytest.mark.parametrize("N,nparts,dtype", [
+    (BIG[0], BIG[1], np.float64), (BIG[0], BIG[1], np.float32), (BIG[0], BIG[1], np.complex128),
+    ((24, 22, 20), 8, np.complex64), ((24, 22, 20), 8, np.float64)])
+def test_irregular_big_bitexact(be, pamd, O, N, nparts, dtype):
+    """Voronoi parts keep their rows in gid order, so a slice spans several
+    x-runs with different y/z offsets (pattern slices with side rows,
+    delta16 and int32 slices mixed): the product stays bit-exact."""
+    parts = be.get_part_ids(nparts)
+    A = pamd.drivers.irregular_problem(parts, N, 27, dtype)
+    OA = _oracle(O, N, nparts, dtype)
+    rng = np.random.default_rng(SEED + 7)
+    xs = {p: _rand(rng, A.cols.partition.local(p).num_lids, dtype) for p in parts.part_ids}
+    x = pamd.PVector.from_host(pamd.map_parts(lambda s: xs[s.part], A.cols.partition), A.cols)
+    y = pamd.PVector.undef(A.rows, dtype)
+    pamd.mul_(y, A, x)
+    ox = O.PVector(O.map_parts(lambda s: _ox(O, xs[s.part]), OA.cols.partition), OA.cols)
+    oy = O.pvector_undef(OA.rows, dtype)
+    O.mul_(oy, OA, ox)
+    got = y.to_host()
+    for p in parts.part_ids:
+        assert _eq(O, got.local(p), oy.values[p]), f"part {p}: SpMV differs"
 
 
 @pytest.mark.parametrize("dtype,fmt", [(np.float64, 1), (np.float64, 0), (np.complex128, 1), (np.float32, 1)])

@@ -1,13 +1,13 @@
 """Interleaved A/B of pa_tune settings on one problem, in one process
 (cdna_hip_programming.md §5.4 rule 24): every variant builds its own copies
-of the operator under its knobs (build-time knobs such as spmv_quadsort take
+of the operator under its knobs (build-time knobs such as spmv_delta16 take
 effect), then the variants' mul! loops alternate over several rounds.
 Reports per variant the median ms per mul! (wall clock over K calls, copies
 rotated so every call streams from HBM), the format bytes and GB/s, and
 checks that every variant gives the same bits.
 
-    python tools/ab_knob.py --problem stencil --kind 7 --n 128 --variants "spmv_short_occ=0|spmv_short_occ=1"
-    python tools/ab_knob.py --problem c5 --n 128 --parts 8 --dtype f32 --variants "spmv_quadsort=0|spmv_quadsort=1"
+    python tools/ab_knob.py --problem stencil --kind 7 --n 128 --variants "spmv_merge=0|spmv_merge=1"
+    python tools/ab_knob.py --problem c5 --n 128 --parts 8 --dtype f32 --variants "spmv_delta16=0|spmv_delta16=1"
 
 With --shared (run-time knobs only) every variant runs on the same operator
 copies: separate copies differ in physical placement, which alone moves the
@@ -102,8 +102,8 @@ def main():
         sets[vi] = xs
         f0 = A.values.local(parts.part_ids[0]).info()
         info[vi] = {"bytes": B, "copies": ncopies,
-                   "format": {k: f0[k] for k in ("nslices", "pattern_slices", "delta16_slices", "quadrun_slices",
-                                                 "quad_sorted", "side_rows") if k in f0}}
+                   "format": {k: f0[k] for k in ("nslices", "pattern_slices", "delta16_slices",
+                                                 "side_rows") if k in f0}}
         restore(prev)
     times = {vi: [] for vi in range(len(variants))}
     out = {}

@@ -1,12 +1,11 @@
 """BASELINE config 5 on one GPU: FE27 on a Voronoi ("METIS-like") partition,
 all parts on device 0, F64/F32/C128/C64.  Reports mul! time (halo included:
 device copies between the parts), algorithmic GB/s over all parts, and the
-column-encoding coverage (pattern slices / regular rows) of the parts.
---patterns A/Bs the offset patterns per slice (pa_tune("spmv_patterns"),
-1 = single-pattern slices); each build also reports the parts' SpMV kernel
-time (HIP events on the parts' streams, summed over the parts).
+column-encoding coverage (pattern slices / regular rows) of the parts; each
+build also reports the parts' SpMV kernel time (HIP events on the parts'
+streams, summed over the parts).
 
-    python tools/c5_bench.py [--n 128] [--parts 8] [--dtypes f64,f32,c128,c64] [--patterns 1,4]
+    python tools/c5_bench.py [--n 128] [--parts 8] [--dtypes f64,f32,c128,c64]
                              [--own-streams] [--group 0|1] [--graph]
 """
 import argparse
@@ -26,8 +25,6 @@ ap.add_argument("--n", type=int, default=128)
 ap.add_argument("--parts", type=int, default=8)
 ap.add_argument("--dtypes", default="f64,f32,c128,c64")
 ap.add_argument("--steps", type=int, default=20)
-ap.add_argument("--patterns", default="4")
-ap.add_argument("--rules", default="1", help="pa_tune spmv_pattern_rule values to A/B")
 ap.add_argument("--own-streams", action="store_true", help="a stream pair per part (share_streams=False)")
 ap.add_argument("--group", type=int, default=1, help="pa_tune spmv_group: 1 grouped launches (default), 0 per part")
 ap.add_argument("--graph", action="store_true", help="also time the HIP-graph replay (pamd.SpMVGraph)")
@@ -43,11 +40,8 @@ pamd._lib.tune("spmv_group", a.group)
 parts = be.get_part_ids(a.parts)
 N = (a.n,) * 3
 owners = pamd.drivers.voronoi_owners(N, a.parts)
-for name, npat, rule in [(d, int(q), int(r)) for d in a.dtypes.split(",") for q in a.patterns.split(",")
-                         for r in a.rules.split(",")]:
+for name in a.dtypes.split(","):
     dtype = DT[name]
-    pamd._lib.tune("spmv_patterns", npat)
-    pamd._lib.tune("spmv_pattern_rule", rule)
     t0 = time.perf_counter()
     A = pamd.drivers.irregular_problem(parts, N, 27, dtype, owners=owners)
     setup = time.perf_counter() - t0
@@ -66,7 +60,7 @@ for name, npat, rule in [(d, int(q), int(r)) for d in a.dtypes.split(",") for q 
         Bf = f["value_bytes"] + f["index_bytes"] + f["meta_bytes"] + (f["nrows"] + s.num_hids) * S + f["nrows"] * S \
             + (len(ex.lids_snd.local(p).data) + len(ex.lids_rcv.local(p).data)) * (4 + 2 * S)
         info["format_bytes"] = info.get("format_bytes", 0) + Bf
-        for k in ("nslices", "pattern_slices", "multi_pattern_slices", "nrows", "regular_rows", "side_rows"):
+        for k in ("nslices", "pattern_slices", "delta16_slices", "nrows", "regular_rows", "side_rows"):
             info[k] = info.get(k, 0) + f[k]
     for _ in range(3):
         pamd.mul_(y, A, x)
@@ -112,7 +106,7 @@ for name, npat, rule in [(d, int(q), int(r)) for d in a.dtypes.split(",") for q 
             assert np.array_equal(got.local(p)[own], ref.local(p)[own]), "graph replay differs from eager mul!"
         del g
     print(json.dumps({"config": f"C5 FE27 {a.n}^3 Voronoi {a.parts} parts on 1 GPU", "dtype": name, "halo": "rccl" if a.rccl else "device reads", "tune": a.tune,
-                      "spmv_patterns": npat, "spmv_pattern_rule": rule, "share_streams": not a.own_streams,
+                      "share_streams": not a.own_streams,
                       "spmv_group": a.group, "format_gbs_all_parts": round(info["format_bytes"] / t / 1e9, 1),
                       "format_gbs_kernels": round(info["format_bytes"] / km / 1e6, 1),
                       "ms_per_mul": round(1e3 * t, 4),

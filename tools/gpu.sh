@@ -12,7 +12,7 @@
 #   kt[:bench args]       rocprofv3 --kernel-trace --stats  -d OUT/kt<i>
 #   ktpy:script args      rocprofv3 --kernel-trace --stats of python3 script args  -d OUT/kt<i>
 #   pmc:CTR[,CTR..][:bench args]  rocprofv3 --pmc CTR..     -d OUT/pmc<i>
-#   pmcpy:CTR[,CTR..]:script args  rocprofv3 --pmc CTR.. of python3 script args
+#   pmcpy:CTR[,CTR..]:script args  rocprofv3 --kernel-trace --pmc CTR.. of python3 script args
 #   py:script args        python script args              > OUT/py<i>.log
 #   cmd:program args      a host program (no GPU), e.g. the C port   > OUT/cmd<i>.log
 # Profiled runs default to "--steps 10 --warmup 2 --no-cpu-baseline --no-pmc".
@@ -59,7 +59,7 @@ for step in "$@"; do
     pmcpy)
       ctr=${args%%:*}
       sargs=${args#*:}
-      timeout -s KILL 240 rocprofv3 --pmc ${ctr//,/ } -d "$OUT/pmc$i" -o pmc --output-format csv \
+      timeout -s KILL 240 rocprofv3 --kernel-trace --pmc ${ctr//,/ } -d "$OUT/pmc$i" -o pmc --output-format csv \
         -- python3 $sargs > "$OUT/pmc$i.log" 2>&1
       rc=$? ;;
     py)
