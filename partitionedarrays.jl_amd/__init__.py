@@ -9,7 +9,7 @@ identifier.
 """
 from ._lib import PAError, device_count, LIB_PATH  # noqa: F401
 from .backends import (MAIN, AbstractBackend, DistributedBackend, PData, SequentialBackend,  # noqa: F401
-                       emit, exchange, gather, gather_all, get_part_ids, i_am_main, map_parts,
+                       alltoall, emit, exchange, gather, gather_all, get_part_ids, i_am_main, map_parts,
                        num_parts, preduce, prun, psum as psum_parts, reduce_all, reduce_main,
                        scatter, sequential, xscan_all)
 from .helpers import Table, counts_to_ptrs, ptrs_to_counts  # noqa: F401

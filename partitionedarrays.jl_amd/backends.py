@@ -96,6 +96,12 @@ class AbstractBackend:
         to it (Interfaces.jl:377-450; delivery rule SequentialBackend.jl:126-200)."""
         raise NotImplementedError
 
+    def alltoall(self, snd: PData) -> PData:
+        """Part p holds one int per part (snd[p][q-1] is for part q); part q
+        receives the column [snd[p][q-1] for p = 1..P] (MPI_Alltoall of one
+        int: the scalable discovery of parts_snd, prange.discover_parts_snd)."""
+        raise NotImplementedError
+
     def i_am_main(self, a: PData) -> bool:
         return MAIN in a.part_ids
 
@@ -129,6 +135,14 @@ class SequentialBackend(AbstractBackend):
         if len(v) != snd.num_parts:
             raise ValueError("scatter: MAIN must hold one value per part")
         return PData(self, snd.part_ids, list(v), snd.shape)
+
+    def alltoall(self, snd):
+        P = snd.num_parts
+        rows = [np.asarray(snd.local(p), dtype=np.int64) for p in range(1, P + 1)]
+        if any(len(r) != P for r in rows):
+            raise ValueError("alltoall: every part must hold one value per part")
+        return PData(self, snd.part_ids, [np.array([r[q - 1] for r in rows], dtype=np.int64)
+                                          for q in snd.part_ids], snd.shape)
 
     def exchange(self, data_snd, parts_rcv, parts_snd):
         out = []
@@ -182,6 +196,15 @@ class DistributedBackend(AbstractBackend):
         objs = [v]
         self.dist.broadcast_object_list(objs, src=0, group=self.group)
         return PData(self, snd.part_ids, [objs[0][self.rank]], snd.shape)
+
+    def alltoall(self, snd):
+        import torch
+        v = np.asarray(snd.parts[0], dtype=np.int64)
+        if len(v) != self.size:
+            raise ValueError("alltoall: every part must hold one value per part")
+        out = torch.empty(self.size, dtype=torch.int64)
+        self.dist.all_to_all_single(out, torch.from_numpy(v.copy()), group=self.group)
+        return PData(self, snd.part_ids, [out.numpy().astype(np.int64)], snd.shape)
 
     def exchange(self, data_snd, parts_rcv, parts_snd):
         me = self.rank + 1
@@ -281,6 +304,10 @@ def xscan_all(op, a: PData, init) -> PData:
 
 def exchange(data_snd: PData, parts_rcv: PData, parts_snd: PData) -> PData:
     return data_snd.backend.exchange(data_snd, parts_rcv, parts_snd)
+
+
+def alltoall(a: PData) -> PData:
+    return a.backend.alltoall(a)
 
 
 def i_am_main(a: PData) -> bool:

@@ -336,7 +336,8 @@ def stencil_operator(parts: PData, N: tuple, kind: int, dtype=np.float64, partit
 # BASELINE config 5: the stencil operators on an irregular ("METIS-like")
 # partition — owners from the nearest of P seeded points,
 # rows in gid order, ghosts in first-touch order (add_gids!), the Exchanger
-# from the gather-based discover (Interfaces.jl:515-552, 723-786).
+# (Interfaces.jl:723-786) with parts_snd from a P-int all-to-all instead of
+# the gather on MAIN (Interfaces.jl:515-552).
 
 def _row_constants(kind, N):
     """Values of an interior row (all neighbours present), neighbour order
@@ -438,7 +439,8 @@ def irregular_partition(parts: PData, N: tuple, kind: int = 27, owners=None):
     """C5 setup on the host: rows = PRange(ngids, IndexSets of the owned gids
     in gid order, gid_to_part); each part's COO of its owned rows (global
     ids, Float64 values); cols = add_gids(rows, J) (first touch, Exchanger
-    by the gather-based discover).  Returns rows, cols, I, J, V."""
+    with parts_snd from the all-to-all discover, prange.discover_parts_snd).
+    Returns rows, cols, I, J, V."""
     from .prange import IndexSet, prange_from_partition
     if owners is None:
         owners = voronoi_owners(N, parts.num_parts)

@@ -9,7 +9,7 @@ from __future__ import annotations
 
 import numpy as np
 
-from .backends import (MAIN, PData, exchange, gather, map_parts, preduce, reduce_all, scatter, unzip,
+from .backends import (MAIN, PData, alltoall, exchange, gather, map_parts, preduce, reduce_all, scatter, unzip,
                        xscan_all)
 from .helpers import Table, counts_to_ptrs, trace_setup
 
@@ -263,13 +263,35 @@ def _parts_rcv_to_parts_snd(parts_rcv_all):
     return [np.array(sorted(s), dtype=np.int32) for s in snd]
 
 
-def discover_parts_snd(parts_rcv: PData, neighbors=None) -> PData:
-    """discover_parts_snd (Interfaces.jl:471-521): gather-based without
-    neighbours, neighbour-assisted otherwise."""
+def discover_parts_snd(parts_rcv: PData, neighbors=None, method="alltoall") -> PData:
+    """discover_parts_snd (Interfaces.jl:471-521).  With `neighbors` (a
+    superset of both the senders and the receivers): each part tells its
+    neighbours whether it receives from them (Interfaces.jl:471-496).
+    Without: method "alltoall" (default) — each part marks the parts it
+    receives from in a P-int vector and one all-to-all of those vectors
+    tells every part who receives from it (part q learns p iff p receives
+    from q; P ints per part, no part holds the whole graph); method
+    "gather" — the reference's fallback (Interfaces.jl:515-521, flagged
+    there as non-scalable, :500-510): gather the graph on MAIN, transpose
+    (:525-552), scatter.  All give parts_snd ascending."""
     if neighbors is None:
-        main = gather(parts_rcv)
-        snd = map_parts(lambda v: _parts_rcv_to_parts_snd(v) if len(v) else [], main)
-        return scatter(snd)
+        if method == "gather":
+            main = gather(parts_rcv)
+            snd = map_parts(lambda v: _parts_rcv_to_parts_snd(v) if len(v) else [], main)
+            return scatter(snd)
+        if method != "alltoall":
+            raise ValueError(f"discover_parts_snd: unknown method {method!r}")
+        P = parts_rcv.num_parts
+
+        def marks(prcv):
+            m = np.zeros(P, dtype=np.int64)
+            for q in prcv:
+                if not 1 <= int(q) <= P:
+                    raise ValueError(f"discover_parts_snd: part {int(q)} out of 1..{P}")
+                m[int(q) - 1] = 1
+            return m
+        col = alltoall(map_parts(marks, parts_rcv))
+        return map_parts(lambda c: (np.flatnonzero(c) + 1).astype(np.int32), col)
     parts = PData(parts_rcv.backend, parts_rcv.part_ids, parts_rcv.part_ids, parts_rcv.shape)
 
     def tell(part, nb, prcv):
@@ -307,8 +329,10 @@ def grid_neighbors_if_superset(ids: PData, part_shape):
     return nbrs if all(good.parts) else None
 
 
-def exchanger_from_ids(ids: PData, neighbors=None, reuse_parts_rcv=False) -> Exchanger:
-    """Exchanger(ids; reuse_parts_rcv) Interfaces.jl:723-786, vectorised."""
+def exchanger_from_ids(ids: PData, neighbors=None, reuse_parts_rcv=False, discover="alltoall") -> Exchanger:
+    """Exchanger(ids; reuse_parts_rcv) Interfaces.jl:723-786, vectorised
+    (parts_snd by discover_parts_snd(..., method=discover) without
+    neighbours)."""
     def rcv(s: IndexSet):
         ghost = np.flatnonzero(s.lid_to_part != s.part)
         owners = s.lid_to_part[ghost]
@@ -322,7 +346,7 @@ def exchanger_from_ids(ids: PData, neighbors=None, reuse_parts_rcv=False) -> Exc
     if reuse_parts_rcv:
         parts_snd = parts_rcv
     else:
-        parts_snd = discover_parts_snd(parts_rcv, neighbors)
+        parts_snd = discover_parts_snd(parts_rcv, neighbors, discover)
     # exchange(gids_rcv, parts_snd, parts_rcv): segment i goes to parts_rcv[i]
     segs = map_parts(lambda t: [t[i] for i in range(1, len(t) + 1)], gids_rcv)
     got = exchange(segs, parts_snd, parts_rcv)

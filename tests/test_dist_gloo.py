@@ -45,6 +45,7 @@ def _worker(rank, world, port, shape, N, kind, q):
             data = pamd.map_parts(lambda s: [10 * i for i in s], psnd)
             out["exchange"] = pamd.exchange(data, prcv, psnd).parts[0]
             out["discover"] = [int(v) for v in pamd.discover_parts_snd(prcv).parts[0]]
+            out["discover_gather"] = [int(v) for v in pamd.discover_parts_snd(prcv, method="gather").parts[0]]
         g = pamd.gather(pamd.map_parts(lambda p: 10 * p, parts))
         out["gather"] = g.parts[0]
         out["scatter"] = pamd.scatter(pamd.map_parts(lambda p: [p * 100 for p in range(1, world + 1)] if p == 1 else [], parts)).parts[0]
@@ -104,6 +105,7 @@ def test_distributed_setup_matches_sequential(pamd, O, world, shape, N, kind):
             assert out["xscan"] == GOLD["scan"]["xscan_init1"]
             assert out["exchange"] == GOLD["exchange_scalar"]["expected_rcv"][r]
             assert out["discover"] == GOLD["discover"]["expected_parts_snd"][r]
+            assert out["discover_gather"] == GOLD["discover"]["expected_parts_snd"][r]
         s = cols.partition.local(p)
         assert out["lid_to_gid"] == s.lid_to_gid.tolist() == OA.cols.partition[p].lid_to_gid
         assert out["parts_rcv"] == cols.exchanger.parts_rcv.local(p).tolist()

@@ -27,6 +27,53 @@ def test_sequential_exchange_kat(pamd):
     assert [list(x) for x in got.parts] == k["parts_snd"]
 
 
+def test_discover_alltoall_equals_gather(pamd):
+    """discover_parts_snd without neighbours: the default P-int all-to-all
+    (no part holds the whole graph) equals the reference's gather-based
+    fallback (Interfaces.jl:515-552) on the KAT and on random graphs."""
+    k = GOLD["exchange_scalar"]
+    parts = pamd.sequential.get_part_ids(4)
+    prcv = _pd(pamd, parts, k["parts_rcv"])
+    assert [list(x) for x in pamd.discover_parts_snd(prcv).parts] == k["parts_snd"]
+    assert [list(x) for x in pamd.discover_parts_snd(prcv, method="gather").parts] == k["parts_snd"]
+    rng = np.random.default_rng(11)
+    for P in (1, 2, 5, 9, 16):
+        parts = pamd.sequential.get_part_ids(P)
+        graph = [sorted(set(int(q) for q in rng.integers(1, P + 1, rng.integers(0, P + 1))) - {p})
+                 for p in range(1, P + 1)]
+        prcv = _pd(pamd, parts, graph)
+        a = pamd.discover_parts_snd(prcv)
+        g = pamd.discover_parts_snd(prcv, method="gather")
+        assert [list(x) for x in a.parts] == [list(x) for x in g.parts], P
+    with pytest.raises(ValueError):
+        pamd.discover_parts_snd(_pd(pamd, pamd.sequential.get_part_ids(2), [[3], []]))
+
+
+def test_irregular_setup_discovers_without_gather(pamd, O, monkeypatch):
+    """BASELINE config 5's Voronoi partition: add_gids! finds parts_snd by
+    the all-to-all (no gather on MAIN) and yields the
+    oracle's (gather-based) Exchanger."""
+    P = pamd.prange
+    N, nparts = (14, 12, 10), 6
+    parts = pamd.sequential.get_part_ids(nparts)
+    ref_cols = pamd.drivers.irregular_partition(parts, N, 27)[1]
+
+    def no_gather(*a, **k):
+        raise AssertionError("gather-based discover_parts_snd used")
+    monkeypatch.setattr(P, "gather", no_gather)
+    rows, cols = pamd.drivers.irregular_partition(parts, N, 27)[:2]
+    monkeypatch.undo()
+    gex = pamd.exchanger_from_ids(ref_cols.partition, discover="gather")
+    for p in parts.part_ids:
+        assert list(cols.exchanger.parts_snd.local(p)) == list(gex.parts_snd.local(p))
+        assert cols.exchanger.lids_snd.local(p).tolist() == gex.lids_snd.local(p).tolist()
+        assert cols.exchanger.lids_rcv.local(p).tolist() == gex.lids_rcv.local(p).tolist()
+    OA = O.irregular_problem(O.get_part_ids(nparts), N, 27)
+    for p in parts.part_ids:
+        assert list(cols.exchanger.parts_snd.local(p)) == list(OA.cols.exchanger.parts_snd[p])
+        assert cols.exchanger.lids_snd.local(p).tolist() == OA.cols.exchanger.lids_snd[p].tolist()
+
+
 def _kat_partition(pamd, parts):
     k = GOLD["exchanger"]
     return _pd(pamd, parts, [pamd.IndexSet(p + 1, k["lid_to_gid"][p], k["lid_to_part"][p]) for p in range(4)])
@@ -264,7 +311,7 @@ def test_grid_neighbor_discovery(pamd, O, shape, N, kind, monkeypatch):
     """Cartesian add_gids! discovers parts_snd from the grid neighbours
     (Interfaces.jl:471-496) — no gather on MAIN — and yields the oracle's
     Exchanger (gather-based, Interfaces.jl:515-521); a ghost owned by a part
-    outside the grid neighbourhood falls back to the gather."""
+    outside the grid neighbourhood falls back to the all-to-all discover."""
     P = pamd.prange
     parts = pamd.sequential.get_part_ids(shape)
     rows = pamd.prange_cartesian(parts, N)
@@ -287,10 +334,8 @@ def test_grid_neighbor_discovery(pamd, O, shape, N, kind, monkeypatch):
     nbr_last = pamd.prange.grid_neighbors(shape, parts.num_parts)
     if 1 in nbr_last:
         return
-    with pytest.raises(AssertionError, match="gather-based"):
-        pamd.add_gids(rows, far)
+    cols = pamd.add_gids(rows, far)  # outside the grid neighbourhood: the all-to-all discover, still no gather
     monkeypatch.undo()
-    cols = pamd.add_gids(rows, far)
     ocols = O.add_gids(orows, O.PData([list(map(int, far.local(p))) for p in parts.part_ids]))
     for p in parts.part_ids:
         assert list(cols.exchanger.parts_snd.local(p)) == list(ocols.exchanger.parts_snd[p])
