@@ -59,6 +59,7 @@ int g_spmv_merge = 1;     // pa_tune("spmv_merge"): one launch for every slice k
 // profiles/r02/open/ab_merge.jsonl.  0: no limit.
 int64_t g_spmv_merge_max = 65536;
 int g_halo_direct = 1;     // pa_tune("halo_direct"): grouped mul! pulls ghosts straight from the owners' x
+int g_halo_fuse = 1;       // pa_tune("halo_fuse"): ... inside the merged launch (boundary slices wait for it)
 int g_halo_transport = 0;  // pa_tune("halo_transport"): 0 parts of this process by device reads, 1 RCCL for all
 // pa_tune("cg_fuse"): the device CG's u update inside the SpMV (XV kernels)
 // instead of its own sweep.  Off: steady-state iteration on FE27 256³, sweep
@@ -809,8 +810,8 @@ int pa_tune(const char* key, int value, int* previous) {
   CHECK_ARG(key, "null key");
   int* slot = nullptr;
   if (!std::strcmp(key, "spmv_flags")) {
-    CHECK_ARG(value >= 0 && (value & ~0x7d) == 0,
-              "spmv_flags: bit 0 = non-temporal streams, bit 2 = 16 B x runs (pattern rows), "
+    CHECK_ARG(value >= 0 && (value & ~0x7f) == 0,
+              "spmv_flags: bit 0 = non-temporal streams, bit 1 = merged launch as one round of resident waves (A/B), bit 2 = 16 B x runs (pattern rows), "
               "bit 3 = masked tail batch, bit 4 = identity slice lists dropped, bit 5 = non-temporal y stores, "
               "bit 6 = short-row kernels (launches whose rows have <= 8 entries)");
     slot = &g_spmv_flags;
@@ -846,6 +847,11 @@ int pa_tune(const char* key, int value, int* previous) {
               "halo_direct: 1 = mul! over parts sharing a stream pair reads the ghosts straight from the owners' x "
               "on the compute stream (default), 0 = pack + pull on the comm stream");
     slot = &g_halo_direct;
+  } else if (!std::strcmp(key, "halo_fuse")) {
+    CHECK_ARG(value == 0 || value == 1,
+              "halo_fuse: 1 = the direct pull's waves lead the merged launch and its boundary slices wait for "
+              "them (default), 0 = a pull launch before the merged launch");
+    slot = &g_halo_fuse;
   } else if (!std::strcmp(key, "halo_transport")) {
     CHECK_ARG(value == 0 || value == 1,
               "halo_transport: 0 = parts of this process by device reads/copies, 1 = RCCL send/recv for every part "
@@ -922,6 +928,8 @@ static int ctx_scratch(pa_ctx* c, const pa_ctx* share_events = nullptr) {
   HIPC(hipMalloc(&c->d_gather, (size_t)c->nparts * 16));
   HIPC(hipMalloc((void**)&c->d_ticket, 16));
   HIPC(hipMemset(c->d_ticket, 0, 16));
+  HIPC(hipMalloc((void**)&c->d_pull_ticket, 8));
+  HIPC(hipMemset(c->d_pull_ticket, 0, 8));
   HIPC(hipHostMalloc(&c->h_pinned, std::max<size_t>((size_t)(c->nparts + 1) * 16, 256)));  // gathered partials / CG state
   if (share_events) {  // one stream pair, one pair of pipeline events
     c->ev_packed = share_events->ev_packed;
@@ -983,6 +991,7 @@ int pa_ctx_destroy(pa_ctx* c) {
   dev_free(c->d_result);
   dev_free(c->d_gather);
   dev_free(c->d_ticket);
+  dev_free(c->d_pull_ticket);
   for (auto& b : c->bases_cache) dev_free(b.second);
   for (auto& b : c->merged_cache) dev_free(b.second);
   if (c->h_pinned) (void)hipHostFree(c->h_pinned);
@@ -2427,11 +2436,22 @@ static int spmv_grouped(int n, pa_mat* const A[], pa_vec* const y[], const pa_in
   // complete, so interior = 0, halo = the pull, boundary = every slice
   const bool dmark = any_x && direct;
   if (dmark && (mark(0) || mark(1))) return -1;
+  bool big_part = false;  // one part alone fills the GPU many times: per-kind launches (g_spmv_merge_max)
+  if (g_spmv_merge_max > 0 && n == 1) big_part = A[0]->nslices > g_spmv_merge_max;
+  // the fused halo (pa_tune halo_fuse): the direct pull's waves lead the
+  // merged launch and its boundary slices wait for them (pa_spmv.hip,
+  // SpmvTable), instead of a pull launch ahead of it
+  const bool fuse = any_x && direct && g_halo_fuse && g_spmv_merge && !big_part && !g_capture_stream && !fz &&
+                    !has_alpha && bmode == 0;
+  void** dbases = nullptr;
   if (any_x && direct) {
-    // every ghost of x straight from its owner's x, in stream order before
-    // the slices (owned values are only read, ghosts only written)
-    void** bases = direct_bases(c0, n, x);
-    if (!bases) return -1;
+    dbases = direct_bases(c0, n, x);
+    if (!dbases) return -1;
+  }
+  // every ghost of x straight from its owner's x, in stream order before
+  // the slices (owned values are only read, ghosts only written)
+  auto direct_pull = [&]() -> int {
+    void** bases = dbases;
     if (g_capture_tables) {  // the graph's own copy: the cache may evict this one
       std::vector<void*> xs(n);
       for (int i = 0; i < n; ++i) xs[i] = x[i]->d;
@@ -2454,6 +2474,10 @@ static int spmv_grouped(int n, pa_mat* const A[], pa_vec* const y[], const pa_in
       }
       launch_pull_group(dt, qg, sm);
     }
+    return 0;
+  };
+  if (any_x && direct) {
+    if (!fuse && direct_pull()) return -1;  // (fused: the merged launch below pulls)
   } else if (any_x) {
     // the previous exchange's pulls read the send buffers: pack after them
     if (!g_capturing) HIPC(hipStreamWaitEvent(c0->s_main, c0->ev_recvd, 0));
@@ -2510,10 +2534,9 @@ static int spmv_grouped(int n, pa_mat* const A[], pa_vec* const y[], const pa_in
   if (dmark ? mark(2) : mark(0)) return -1;
   // no halo in flight (none, or pulled already on this stream): every slice
   // kind of every part in one launch — side rows and int32 slices first, so
-  // their few long waves start early, then delta16, multi-pattern, pattern
+  // their few long waves start early, then delta16, pattern.  Fused halo:
+  // the pulls first, then the interior slices, then the gated rest.
   int merged = 1;
-  bool big_part = false;  // one part alone fills the GPU many times: per-kind launches (g_spmv_merge_max)
-  if (g_spmv_merge_max > 0 && n == 1) big_part = A[0]->nslices > g_spmv_merge_max;
   if (g_spmv_merge && !big_part && (!any_x || direct)) {
     std::vector<SpmvPart> E;
     std::vector<int> W;
@@ -2522,6 +2545,50 @@ static int spmv_grouped(int n, pa_mat* const A[], pa_vec* const y[], const pa_in
       E.push_back(part(i, nwork, list));
       W.push_back(which);
     };
+    if (fuse) {
+      for (int i = 0; i < n; ++i) {
+        pa_xchg* X = xg[i];
+        if (X->n_rcv_data <= 0) continue;
+        SpmvPart q{};
+        q.nwork = (X->n_rcv_data + 64 * kPullPerLane - 1) / (64 * kPullPerLane);
+        q.list = X->d_lids_rcv;
+        q.A = A[i];
+        q.y = x[i]->d;
+        q.n_pull = X->n_rcv_data;
+        q.pbid = X->direct.d_bid;
+        q.pelem = X->direct.d_elem;
+        q.pbases = (const void* const*)dbases;
+        E.push_back(q);
+        W.push_back(5);
+      }
+      auto addg = [&](int which, int i, int64_t nwork, const int32_t* list) {
+        if (nwork <= 0) return;
+        E.push_back(part(i, nwork, list));
+        E.back().gate = true;
+        W.push_back(which);
+      };
+      for (int i = 0; i < n; ++i) {
+        if (g_spmv_format == 1 && A[i]->has_pat) {
+          add(1, i, A[i]->nx_int, A[i]->d_xint_list);
+          add(4, i, A[i]->nd_int, A[i]->d_dint_list);
+          add(0, i, A[i]->np_int, A[i]->d_pint_list);
+        } else if (A[i]->d_bnd_list) {
+          add(1, i, A[i]->nslices_int, A[i]->d_int_list);
+        }
+      }
+      for (int i = 0; i < n; ++i) {
+        if (g_spmv_format == 1 && A[i]->has_pat) {
+          addg(2, i, A[i]->s_nslices, nullptr);
+          addg(1, i, A[i]->nx_bnd, A[i]->d_xbnd_list);
+          addg(4, i, A[i]->nd_bnd, A[i]->d_dbnd_list);
+          addg(0, i, A[i]->np_bnd, A[i]->d_pbnd_list);
+        } else if (A[i]->d_bnd_list) {
+          addg(1, i, A[i]->nslices - A[i]->nslices_int, A[i]->d_bnd_list);
+        } else {
+          addg(1, i, A[i]->nslices, nullptr);
+        }
+      }
+    } else {
     for (int i = 0; i < n; ++i)
       if (g_spmv_format == 1 && A[i]->has_pat) add(2, i, A[i]->s_nslices, nullptr);
     for (int i = 0; i < n; ++i) {
@@ -2545,9 +2612,11 @@ static int spmv_grouped(int n, pa_mat* const A[], pa_vec* const y[], const pa_in
         add(0, i, A[i]->np_int, A[i]->d_pint_list);
         add(0, i, A[i]->np_bnd, A[i]->d_pbnd_list);
       }
+    }
     merged = launch_spmv_merged((int)E.size(), W.data(), E.data(), has_alpha, bmode, alpha, beta, c0,
                                 g_capture_tables, sm);
     if (merged < 0) PA_FAIL("mul!: merged launch table (device allocation or copy) failed");
+    if (merged && fuse && direct_pull()) return -1;  // too many entries for one table: pull, then per kind
     if (merged == 0 && !dmark && (mark(1) || mark(2))) return -1;
   }
   if (merged) {
