@@ -325,10 +325,13 @@ def cg_mode(args, pamd, backend, parts, A, ngpu, use_dist, sync):
             el = float(t.item())
         return el, hist
 
+    ctxs = [backend.context(p) for p in parts.part_ids]
     for name, kw in variants.items():
         # the device recurrence with u .= r .+ β.*u as its own sweep
-        # (pa_tune cg_fuse 0, the default) or inside the SpMV (cg_fuse 1)
-        prev_fuse = pamd._lib.tune("cg_fuse", 1 if name == "device_fused_u" else 0)
+        # (cg_fuse 0) or inside the SpMV (cg_fuse 1), set on this run's
+        # contexts (pa_ctx_tune; the process default is 2, auto)
+        for c in ctxs:
+            c.tune("cg_fuse", 1 if name == "device_fused_u" else 0)
         x = pamd.PVector.undef(cols, dtype).fill_(0)
         pamd.cg_(x, A, b, reltol=0.0, maxiter=args.warmup, **kw)
         sync()
@@ -339,7 +342,8 @@ def cg_mode(args, pamd, backend, parts, A, ngpu, use_dist, sync):
             # setup: cg_iterator!'s SpMV, norms and host syncs) over 2K
             el3, hist3 = timed(kw, 3 * args.cg)
             steady[name] = 1e3 * (el3 - el) / max(1, len(hist3) - len(hist))
-        pamd._lib.tune("cg_fuse", prev_fuse)
+        for c in ctxs:
+            c.tune("cg_fuse", -1)
     best = min(steady, key=steady.get)
     p0 = parts.part_ids[0]
     info = A.values.local(p0).info()
@@ -584,8 +588,10 @@ def main():
     kernel_ms = span_ms
     spmv_bytes = B_local if grouped_here else format_bytes(info, s_nhids, n_snd0, n_rcv0, S)
     achieved = spmv_bytes / (kernel_ms * 1e-3) / 1e9
-    # the same kernels with int32 column ids everywhere (pa_tune spmv_format=0), for reference
-    prev = pamd._lib.tune("spmv_format", 0)
+    # the same kernels with int32 column ids everywhere (spmv_format=0 on
+    # this run's contexts), for reference
+    for c in ctxs:
+        c.tune("spmv_format", 0)
     sync()
     c0.span_start()
     for i in range(reps):
@@ -597,7 +603,8 @@ def main():
     for p in (parts.part_ids if grouped_here else [p0]):
         inf, nh, ns_, nr_ = infos[p]
         bytes_int32 += format_bytes(dict(inf, **A.values.local(p).traffic()), nh, ns_, nr_, S)
-    pamd._lib.tune("spmv_format", prev)
+    for c in ctxs:
+        c.tune("spmv_format", -1)
     box = box_hbm_gbs(pamd, spmv_bytes // 2) if world == 1 and ngpu == 1 else None
     halo_leg = None
     if world == 1 and ngpu == 1 and not args.strong and not args.no_halo_leg:

@@ -89,6 +89,11 @@ int pa_device_count(int* count);
  * "spmv_group"  1: the parts of one process sharing a stream pair run each
  *               mul! phase as one launch (default), 0: launches per part. */
 int pa_tune(const char* key, int value, int* previous);
+/* The same knobs for one context: calls led by parts of `c` (their first
+ * part's context) run with this value instead of the process default, for
+ * the duration of the call; value -1 drops the override.  *previous gets
+ * the context's former override (-1: none).                             */
+int pa_ctx_tune(pa_ctx* c, const char* key, int value, int* previous);
 /* HBM calibration of `device` (not the hot path): best read-only and copy
  * rates (GB/s, read+write bytes for the copy; best of 4/8 loads in flight
  * per lane and four grid sizes) over `reps` sweeps of a

@@ -37,6 +37,7 @@ _SIGS = {
     "pa_version": [],
     "pa_device_count": [C.POINTER(C.c_int)],
     "pa_tune": [C.c_char_p, C.c_int, C.POINTER(C.c_int)],
+    "pa_ctx_tune": [_p, C.c_char_p, C.c_int, C.POINTER(C.c_int)],
     "pa_hbm_probe": [C.c_int, C.c_int64, C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_double)],
     "pa_ctx_create": [C.c_int, C.c_int, C.c_int, C.POINTER(_p)],
     "pa_ctx_create_shared": [C.c_int, C.c_int, _p, C.POINTER(_p)],
@@ -168,6 +169,12 @@ def tune(key: str, value: int) -> int:
     call("pa_tune", key.encode(), int(value), C.byref(prev))
     tune_generation += 1
     return prev.value
+
+
+def tune_generation_bump():
+    """a per-context knob changed (PartContext.tune): cached graphs are stale"""
+    global tune_generation
+    tune_generation += 1
 
 
 def hbm_probe(device: int = 0, nbytes: int = 2 << 30, reps: int = 10):

@@ -806,68 +806,116 @@ extern "C" {
 const char* pa_last_error(void) { return g_err.c_str(); }
 int pa_version(void) { return 1; }
 
+// The tuning knobs (performance only, results unchanged): the process
+// defaults (pa_tune) and per-context overrides (pa_ctx_tune).  A call
+// applies the overrides of its first part's context for its duration
+// (TuneScope), so parts of one stream group always run with one setting.
+}  // extern "C"
+namespace {
+struct Knob {
+  const char* key;
+  int* slot;           // process default (int knobs)
+  int64_t* slot64;     // ... or 64-bit
+  int64_t lo, hi;      // valid range
+  int64_t mask;        // spmv_flags: allowed bits (0: range only)
+  const char* help;
+};
+const Knob kKnobs[] = {
+    {"spmv_flags", &g_spmv_flags, nullptr, 0, 0x7f, 0x7f,
+     "spmv_flags: bit 0 = non-temporal streams, bit 1 = merged launch as one round of resident waves (A/B), "
+     "bit 2 = 16 B x runs (pattern rows), bit 3 = masked tail batch, bit 4 = identity slice lists dropped, "
+     "bit 5 = non-temporal y stores, bit 6 = short-row kernels (launches whose rows have <= 8 entries)"},
+    {"long_rows_exact", &g_long_exact, nullptr, 0, 1, 0,
+     "long_rows_exact: 1 = reference summation order, 0 = lane-strided tree (1e-12)"},
+    {"halo_pull", &g_halo_pull, nullptr, 0, 1, 0,
+     "halo_pull: 1 = receivers read the senders' buffers (one kernel), 0 = staging copies"},
+    {"spmv_delta16", &g_spmv_delta16, nullptr, 0, 1, 0,
+     "spmv_delta16: 1 = int32-column slices whose columns fit 16-bit codes store those (matrices built "
+     "afterwards; default), 0 = int32 column ids"},
+    {"spmv_merge", &g_spmv_merge, nullptr, 0, 1, 0,
+     "spmv_merge: 1 = mul! without a halo in flight (one part, or parts of one stream pair with the direct "
+     "pull) runs every slice kind of every part as one launch (default), 0 = one launch per kind"},
+    {"spmv_merge_max", nullptr, &g_spmv_merge_max, 0, INT32_MAX, 0,
+     "spmv_merge_max: one part with more slices than this runs one launch per kind (0: always merge)"},
+    {"cg_fuse", &g_cg_fuse, nullptr, 0, 2, 0,
+     "cg_fuse: 1 = the device CG computes u = r .+ beta.*u inside the SpMV, 0 = a separate sweep, "
+     "2 = auto (default: one batch of each, then the faster; all parts in one process, else the sweep)"},
+    {"halo_direct", &g_halo_direct, nullptr, 0, 1, 0,
+     "halo_direct: 1 = mul! over parts sharing a stream pair reads the ghosts straight from the owners' x "
+     "on the compute stream (default), 0 = pack + pull on the comm stream"},
+    {"halo_fuse", &g_halo_fuse, nullptr, 0, 1, 0,
+     "halo_fuse: 1 = the direct pull's waves lead the merged launch and its boundary slices wait for "
+     "them (default), 0 = a pull launch before the merged launch"},
+    {"halo_transport", &g_halo_transport, nullptr, 0, 1, 0,
+     "halo_transport: 0 = parts of this process by device reads/copies, 1 = RCCL send/recv for every part "
+     "with a communicator (pa_comm_init_all)"},
+    {"spmv_group", &g_spmv_group, nullptr, 0, 1, 0,
+     "spmv_group: 1 = one launch per phase for parts sharing a stream pair, 0 = per part"},
+    {"spmv_format", &g_spmv_format, nullptr, 0, 1, 0, "spmv_format: 0 = int32 columns, 1 = pattern slices"},
+};
+constexpr int kNumKnobs = (int)(sizeof(kKnobs) / sizeof(kKnobs[0]));
+static_assert(kNumKnobs <= pa_ctx::kMaxKnobs, "pa_ctx::over too small");
+
+// the knob's index (-1: unknown key), value checked (-2: out of range)
+int knob_find(const char* key) {
+  for (int i = 0; i < kNumKnobs; ++i)
+    if (!std::strcmp(key, kKnobs[i].key)) return i;
+  pa::set_error(std::string("pa_tune: unknown key ") + key);
+  return -1;
+}
+int knob_index(const char* key, int64_t value) {
+  const int i = knob_find(key);
+  if (i < 0) return -1;
+  const Knob& k = kKnobs[i];
+  if (value < k.lo || value > k.hi || (k.mask != 0 && (value & ~k.mask) != 0)) {
+    pa::set_error(k.help);
+    return -2;
+  }
+  return i;
+}
+int64_t knob_get(int i) { return kKnobs[i].slot ? (int64_t)*kKnobs[i].slot : *kKnobs[i].slot64; }
+void knob_set(int i, int64_t v) {
+  if (kKnobs[i].slot) *kKnobs[i].slot = (int)v;
+  else *kKnobs[i].slot64 = v;
+}
+}  // namespace
+
+// For the duration of a call: the knobs of the call's context (its
+// overrides over the process defaults), restored on exit.
+TuneScope::TuneScope(const pa_ctx* c) {
+  if (!c) return;
+  for (int i = 0; i < kNumKnobs; ++i)
+    if (c->has_over[i]) {
+      if (!active) saved.assign(kNumKnobs, 0), set.assign(kNumKnobs, false), active = true;
+      saved[i] = knob_get(i);
+      set[i] = true;
+      knob_set(i, c->over[i]);
+    }
+}
+TuneScope::~TuneScope() {
+  if (!active) return;
+  for (int i = 0; i < kNumKnobs; ++i)
+    if (set[i]) knob_set(i, saved[i]);
+}
+
+extern "C" {
+
 int pa_tune(const char* key, int value, int* previous) {
   CHECK_ARG(key, "null key");
-  int* slot = nullptr;
-  if (!std::strcmp(key, "spmv_flags")) {
-    CHECK_ARG(value >= 0 && (value & ~0x7f) == 0,
-              "spmv_flags: bit 0 = non-temporal streams, bit 1 = merged launch as one round of resident waves (A/B), bit 2 = 16 B x runs (pattern rows), "
-              "bit 3 = masked tail batch, bit 4 = identity slice lists dropped, bit 5 = non-temporal y stores, "
-              "bit 6 = short-row kernels (launches whose rows have <= 8 entries)");
-    slot = &g_spmv_flags;
-  } else if (!std::strcmp(key, "long_rows_exact")) {
-    CHECK_ARG(value == 0 || value == 1, "long_rows_exact: 1 = reference summation order, 0 = lane-strided tree (1e-12)");
-    slot = &g_long_exact;
-  } else if (!std::strcmp(key, "halo_pull")) {
-    CHECK_ARG(value == 0 || value == 1, "halo_pull: 1 = receivers read the senders' buffers (one kernel), 0 = staging copies");
-    slot = &g_halo_pull;
-  } else if (!std::strcmp(key, "spmv_delta16")) {
-    CHECK_ARG(value == 0 || value == 1,
-              "spmv_delta16: 1 = int32-column slices whose columns fit 16-bit codes store those (matrices built "
-              "afterwards; default), 0 = int32 column ids");
-    slot = &g_spmv_delta16;
-  } else if (!std::strcmp(key, "spmv_merge")) {
-    CHECK_ARG(value == 0 || value == 1,
-              "spmv_merge: 1 = mul! without a halo in flight (one part, or parts of one stream pair with the direct "
-              "pull) runs every slice kind of every part as one launch (default), 0 = one launch per kind");
-    slot = &g_spmv_merge;
-  } else if (!std::strcmp(key, "spmv_merge_max")) {
-    CHECK_ARG(value >= 0, "spmv_merge_max: one part with more slices than this runs one launch per kind (0: always merge)");
-    const int prev = (int)std::min<int64_t>(g_spmv_merge_max, INT32_MAX);
-    g_spmv_merge_max = value;
-    if (previous) *previous = prev;
-    return 0;
-  } else if (!std::strcmp(key, "cg_fuse")) {
-    CHECK_ARG(value >= 0 && value <= 2,
-              "cg_fuse: 1 = the device CG computes u = r .+ beta.*u inside the SpMV, 0 = a separate sweep, "
-              "2 = auto (default: one batch of each, then the faster; all parts in one process, else the sweep)");
-    slot = &g_cg_fuse;
-  } else if (!std::strcmp(key, "halo_direct")) {
-    CHECK_ARG(value == 0 || value == 1,
-              "halo_direct: 1 = mul! over parts sharing a stream pair reads the ghosts straight from the owners' x "
-              "on the compute stream (default), 0 = pack + pull on the comm stream");
-    slot = &g_halo_direct;
-  } else if (!std::strcmp(key, "halo_fuse")) {
-    CHECK_ARG(value == 0 || value == 1,
-              "halo_fuse: 1 = the direct pull's waves lead the merged launch and its boundary slices wait for "
-              "them (default), 0 = a pull launch before the merged launch");
-    slot = &g_halo_fuse;
-  } else if (!std::strcmp(key, "halo_transport")) {
-    CHECK_ARG(value == 0 || value == 1,
-              "halo_transport: 0 = parts of this process by device reads/copies, 1 = RCCL send/recv for every part "
-              "with a communicator (pa_comm_init_all)");
-    slot = &g_halo_transport;
-  } else if (!std::strcmp(key, "spmv_group")) {
-    CHECK_ARG(value == 0 || value == 1, "spmv_group: 1 = one launch per phase for parts sharing a stream pair, 0 = per part");
-    slot = &g_spmv_group;
-  } else if (!std::strcmp(key, "spmv_format")) {
-    CHECK_ARG(value == 0 || value == 1, "spmv_format: 0 = int32 columns, 1 = pattern slices");
-    slot = &g_spmv_format;
-  } else {
-    PA_FAIL(std::string("pa_tune: unknown key ") + key);
-  }
-  if (previous) *previous = *slot;
-  *slot = value;
+  const int i = knob_index(key, value);
+  if (i < 0) return -1;
+  if (previous) *previous = (int)std::min<int64_t>(knob_get(i), INT32_MAX);
+  knob_set(i, value);
+  return 0;
+}
+
+int pa_ctx_tune(pa_ctx* c, const char* key, int value, int* previous) {
+  CHECK_ARG(c && key, "null argument");
+  const int i = value == -1 ? knob_find(key) : knob_index(key, value);  // -1: drop the override
+  if (i < 0) return -1;
+  if (previous) *previous = c->has_over[i] ? (int)c->over[i] : -1;
+  c->has_over[i] = value != -1;
+  c->over[i] = value;
   return 0;
 }
 
@@ -1547,6 +1595,7 @@ int pa_mat_from_csc(pa_ctx* c, int dtype, int index_bytes, int64_t nrows_lids, i
                     const void* colptr, const void* rowval, const void* nzval, const pa_index* rows,
                     const pa_index* cols, pa_mat** out) {
   CHECK_ARG(c && out && rows && cols, "null argument");
+  TuneScope ts(c);
   CHECK_ARG(valid_dtype(dtype), "invalid dtype");
   CHECK_ARG(index_bytes == 4 || index_bytes == 8, "index_bytes must be 4 or 8");
   CHECK_ARG(rows->nlids == nrows_lids && cols->nlids == ncols_lids,
@@ -1592,6 +1641,7 @@ int pa_mat_from_csr(pa_ctx* c, int dtype, int index_bytes, int Bi, int64_t nrows
                     const void* rowptr, const void* colval, const void* nzval, const pa_index* rows,
                     const pa_index* cols, pa_mat** out) {
   CHECK_ARG(c && out && rows && cols, "null argument");
+  TuneScope ts(c);
   CHECK_ARG(valid_dtype(dtype), "invalid dtype");
   CHECK_ARG(index_bytes == 4 || index_bytes == 8, "index_bytes must be 4 or 8");
   CHECK_ARG(Bi == 0 || Bi == 1, "Bi (index base) must be 0 or 1");
@@ -1704,6 +1754,7 @@ int mat_from_coo_impl(pa_ctx* c, int dtype, int index_bytes, int ids_global, int
                       hipMemcpyKind kind, const pa_index* rows, const pa_index* cols, int csr_bi, int64_t* csc_nnz,
                       int64_t* colptr_out, int64_t* rowval_out, pa_mat** out) {
   CHECK_ARG(c && out && rows && cols && csc_nnz, "null argument");
+  TuneScope ts(c);
   const bool csr = csr_bi >= 0;
   if (csr) {  // the row order below (owned columns by oid, ghosts by hid) is the CSR storage order
     bool inc = true;  // when oid_to_lid and hid_to_lid ascend (every PRange / IndexSet the reference builds)
@@ -1925,7 +1976,8 @@ int pa_coo_download(const pa_coo* C, int64_t* I, int64_t* J, void* V) {
 }
 
 int pa_coo_assemble_all(int n, pa_coo* const coo[], const pa_index* const rows[], pa_xchg* const xg[]) {
-  CHECK_ARG(n >= 1 && coo && rows && xg, "null argument");
+  CHECK_ARG(n >= 1 && coo && rows && xg && coo[0], "null argument");
+  TuneScope ts(coo[0]->ctx);
   const int dt = coo[0]->dtype;
   const size_t S = dtype_size(dt);
   for (int i = 0; i < n; ++i) {
@@ -2226,7 +2278,8 @@ int pa_mat_xchg_create(pa_mat* A, int32_t n_rcv, const int32_t* parts_rcv, const
 // the vector exchange over nonzeros(A); assemble zeroes the sent ghost-row
 // values afterwards (2398) and refreshes the side SELL copies.
 int pa_mat_exchange_all(int n, pa_mat* const A[], pa_xchg* const xg[], int op, int reverse, int zero_sent) {
-  CHECK_ARG(n >= 1 && A && xg, "null argument");
+  CHECK_ARG(n >= 1 && A && xg && A[0], "null argument");
+  TuneScope ts(A[0]->ctx);
   std::vector<pa_vec> vs(n);
   std::vector<pa_vec*> vp(n);
   for (int i = 0; i < n; ++i) {
@@ -2310,6 +2363,7 @@ int pa_mat_device_ptrs(const pa_mat* A, uint64_t out[8]) {
 
 int pa_mat_traffic(const pa_mat* A, int64_t* value_bytes, int64_t* index_bytes, int64_t* meta_bytes) {
   CHECK_ARG(A, "null matrix");
+  TuneScope ts(A->ctx);
   const int64_t S = (int64_t)dtype_size(A->dtype), H = A->H, W = H / 64;
   const bool pat = g_spmv_format == 1 && A->has_pat;
   const bool split = A->d_bnd_list != nullptr;
@@ -2875,7 +2929,8 @@ int pa_graph_destroy(pa_graph* G) {
 int pa_spmv_graph_create(int n, pa_mat* const A[], pa_vec* const y[], const pa_index* const y_idx[],
                          pa_vec* const x[], const pa_index* const x_idx[], pa_xchg* const xg[],
                          const void* alpha, const void* beta, pa_graph** out) {
-  CHECK_ARG(n >= 1 && A && y && x && out, "null argument");
+  CHECK_ARG(n >= 1 && A && A[0] && y && x && out, "null argument");
+  TuneScope ts(A[0]->ctx);
   const int dev = A[0]->ctx->device;
   std::vector<pa_ctx*> ctxs(n);
   for (int i = 0; i < n; ++i) {
@@ -2971,8 +3026,9 @@ int pa_graph_launch(pa_graph* G) {
 
 int pa_exchange_all(int n, pa_vec* const v[], pa_xchg* const xg[], const pa_index* const idx[], int op,
                     int reverse, int zero_ghosts) {
-  CHECK_ARG(n >= 1 && v && xg, "null argument");
+  CHECK_ARG(n >= 1 && v && xg && v[0], "null argument");
   CHECK_ARG(op == PA_REPLACE || op == PA_ADD, "invalid combine op");
+  TuneScope ts(v[0]->ctx);
   const int dt = v[0]->dtype;
   for (int i = 0; i < n; ++i) {
     CHECK_ARG(v[i] && xg[i], "null handle");
@@ -3116,13 +3172,16 @@ void store_scalar(int dt, c128 s, void* result) {
 int pa_spmv_all(int n, pa_mat* const A[], pa_vec* const y[], const pa_index* const y_idx[],
                 pa_vec* const x[], const pa_index* const x_idx[], pa_xchg* const xg[],
                 const void* alpha, const void* beta) {
+  CHECK_ARG(n >= 1 && A && A[0], "null argument");
+  TuneScope ts(A[0]->ctx);
   return spmv_impl(n, A, y, y_idx, x, x_idx, xg, alpha, beta, false);
 }
 
 int pa_spmv_dot_all(int n, pa_mat* const A[], pa_vec* const y[], const pa_index* const y_idx[],
                     pa_vec* const x[], const pa_index* const x_idx[], pa_xchg* const xg[],
                     const void* alpha, const void* beta, void* dot_result) {
-  CHECK_ARG(dot_result, "null result");
+  CHECK_ARG(dot_result && n >= 1 && A && A[0], "null argument");
+  TuneScope ts(A[0]->ctx);
   if (spmv_impl(n, A, y, y_idx, x, x_idx, xg, alpha, beta, true)) return -1;
   std::vector<pa_ctx*> ctxs(n);
   for (int i = 0; i < n; ++i) ctxs[i] = A[i]->ctx;
@@ -3242,8 +3301,9 @@ int pa_cg_solve_all(int n, pa_mat* const A[], pa_vec* const x[], const pa_vec* c
                     pa_vec* const u[], pa_vec* const r[], pa_vec* const c[],
                     const pa_index* const idx[], pa_xchg* const xg[], double reltol, double abstol,
                     int64_t maxiter, int batch, int64_t* iterations, double* residual, double* history) {
-  CHECK_ARG(n >= 1 && A && x && b && u && r && c && idx && iterations && residual, "null argument");
+  CHECK_ARG(n >= 1 && A && A[0] && x && b && u && r && c && idx && iterations && residual, "null argument");
   CHECK_ARG(batch >= 1, "batch must be >= 1");
+  TuneScope ts(A[0]->ctx);
   const int dt = A[0]->dtype;
   const bool cplx = dt == PA_C64 || dt == PA_C128;
   CGRun R;
@@ -3502,6 +3562,7 @@ int pa_mat_stencil(pa_ctx* c, int dtype, int kind, const int64_t gdims[3], const
                    const int64_t box_n[3], int64_t nlids_cols, const int32_t* shell_lid,
                    const double* coeffs, int ncoeffs, pa_mat** out) {
   CHECK_ARG(c && out && gdims && box_lo && box_n && coeffs, "null argument");
+  TuneScope ts(c);
   CHECK_ARG(valid_dtype(dtype), "invalid dtype");
   CHECK_ARG(kind == 7 || kind == 27, "kind must be 7 or 27");
   CHECK_ARG((kind == 7 && ncoeffs == 2) || (kind == 27 && ncoeffs == 64), "coefficient count");

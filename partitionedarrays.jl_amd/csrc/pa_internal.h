@@ -322,6 +322,22 @@ struct pa_ctx {
   std::vector<std::pair<std::vector<void*>, void**>> bases_cache;
   // device copies of the merged-launch tables of calls led by this part
   std::vector<std::pair<std::vector<char>, void*>> merged_cache;
+  // pa_ctx_tune: this context's knob values over the process defaults,
+  // applied to the calls it leads (TuneScope)
+  static constexpr int kMaxKnobs = 16;
+  bool has_over[kMaxKnobs] = {};
+  int64_t over[kMaxKnobs] = {};
+};
+
+// the knobs of a call's (first part's) context for the call's duration
+struct TuneScope {
+  explicit TuneScope(const pa_ctx* c);
+  ~TuneScope();
+  TuneScope(const TuneScope&) = delete;
+  TuneScope& operator=(const TuneScope&) = delete;
+  bool active = false;
+  std::vector<int64_t> saved;
+  std::vector<bool> set;
 };
 
 struct pa_index {

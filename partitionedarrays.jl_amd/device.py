@@ -32,6 +32,15 @@ class PartContext:
     def sync(self):
         _lib.call("pa_ctx_sync", self.h)
 
+    def tune(self, key: str, value: int) -> int:
+        """pa_ctx_tune: this part's value of a knob for the calls it leads
+        (-1 drops it: the process default again); returns the former
+        override (-1: none)."""
+        prev = C.c_int(0)
+        _lib.call("pa_ctx_tune", self.h, key.encode(), int(value), C.byref(prev))
+        _lib.tune_generation_bump()
+        return prev.value
+
     def comm_stats(self):
         """(bytes sent, bytes received) this part has posted to RCCL so far"""
         a, b = C.c_int64(), C.c_int64()

@@ -288,3 +288,36 @@ def test_mul_argument_cache_follows_objects(be, pamd, O):
         del y
         gc.collect()
     assert len(A.__dict__["_args_cache"]) <= 8
+
+
+def test_context_knobs_override_process_defaults(pamd):
+    """pa_ctx_tune: a context's knob applies to the calls its parts lead and
+    to nothing else; -1 drops it.  spmv_format 0 on one backend's contexts
+    shows in its matrix's streamed bytes (int32 ids), not in another
+    backend's, and the products stay bit-identical."""
+    mk = lambda be: (be, be.get_part_ids((2, 1, 1)))
+    (b1, p1), (b2, p2) = mk(pamd.HIPBackend(devices=[0])), mk(pamd.HIPBackend(devices=[0]))
+    N = (16, 12, 10)
+    A1 = pamd.drivers.stencil_operator(p1, N, 27)
+    A2 = pamd.drivers.stencil_operator(p2, N, 27)
+    t1 = A1.values.local(1).traffic()["index_bytes"]
+    for p in p1.part_ids:
+        assert b1.context(p).tune("spmv_format", 0) == -1
+    assert A1.values.local(1).traffic()["index_bytes"] > t1, "override not applied to the context's calls"
+    assert A2.values.local(1).traffic()["index_bytes"] == t1, "override leaked to another context"
+    xs = {p: np.random.default_rng(p).uniform(-1, 1, A1.cols.partition.local(p).num_lids) for p in p1.part_ids}
+    x1 = pamd.PVector.from_host(pamd.map_parts(lambda s: xs[s.part], A1.cols.partition), A1.cols)
+    x2 = pamd.PVector.from_host(pamd.map_parts(lambda s: xs[s.part], A2.cols.partition), A2.cols)
+    y1, y2 = pamd.PVector.undef(A1.rows), pamd.PVector.undef(A2.rows)
+    pamd.mul_(y1, A1, x1)
+    pamd.mul_(y2, A2, x2)
+    h1, h2 = y1.to_host(), y2.to_host()
+    for p in p1.part_ids:
+        assert np.array_equal(h1.local(p), h2.local(p))
+    for p in p1.part_ids:
+        assert b1.context(p).tune("spmv_format", -1) == 0
+    assert A1.values.local(1).traffic()["index_bytes"] == t1
+    with pytest.raises(pamd._lib.PAError):
+        b1.context(1).tune("spmv_format", 5)
+    with pytest.raises(pamd._lib.PAError):
+        b1.context(1).tune("no_such_knob", 0)
