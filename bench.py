@@ -138,7 +138,8 @@ def pmc_traffic(args, steps=5, halo=False):
         d = tempfile.mkdtemp(prefix="pa_pmc_", dir="/tmp")
         cmd = ["rocprofv3", "--pmc", ctr, "-d", d, "-o", "pmc", "--output-format", "csv", "--",
                sys.executable, os.path.abspath(__file__), "--child-pmc", "--steps", str(steps),
-               "--n", str(args.n), "--kind", str(args.kind), "--dtype", args.dtype] + (["--child-halo"] if halo else [])
+               "--n", str(args.n), "--kind", str(args.kind), "--dtype", args.dtype, "--tune", args.tune] + \
+            (["--child-halo"] if halo else [])
         p = subprocess.Popen(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL, start_new_session=True,
                              env=dict(os.environ, TMPDIR="/tmp"))
         try:
@@ -412,11 +413,17 @@ def main():
     ap.add_argument("--child-pmc", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--child-halo", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--cg", type=int, default=0, help="time K CG iterations instead (own JSON line)")
+    ap.add_argument("--tune", default="", help="process-default knobs before anything is built (A/B runs): "
+                                                 "key=v[,key=v]")
     ap.add_argument("--distributed", action="store_true",
                     help="one part per process (HIPDistributedBackend, RCCL) even for one process: "
                          "rehearses the torchrun path of --gpus N > 1 on a single GPU")
     args = ap.parse_args()
     if args.child_pmc:
+        import pamd
+        for kv in filter(None, args.tune.split(",")):
+            k, v = kv.split("=")
+            pamd._lib.tune(k, int(v))
         return child_pmc(args)
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         # `python bench.py --gpus N` (no torchrun around it): start the N
@@ -439,6 +446,9 @@ def main():
     import torch
     import torch.distributed as dist
     import pamd
+    for kv in filter(None, args.tune.split(",")):
+        k, v = kv.split("=")
+        pamd._lib.tune(k, int(v))
 
     use_dist = world > 1 or args.distributed
     if use_dist:
@@ -665,6 +675,7 @@ def main():
             "operator_copies_rotated": ncopies,
             "per_part_ms": per_part,
             "rccl_halo": rccl,
+            "tune": args.tune or None,
         },
         "roofline": {
             "bound": "hbm",

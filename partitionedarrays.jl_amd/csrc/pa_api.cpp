@@ -59,7 +59,6 @@ int g_spmv_merge = 1;     // pa_tune("spmv_merge"): one launch for every slice k
 // profiles/r02/open/ab_merge.jsonl.  0: no limit.
 int64_t g_spmv_merge_max = 65536;
 int g_halo_direct = 1;     // pa_tune("halo_direct"): grouped mul! pulls ghosts straight from the owners' x
-int g_halo_fuse = 1;       // pa_tune("halo_fuse"): ... inside the merged launch (boundary slices wait for it)
 int g_halo_transport = 0;  // pa_tune("halo_transport"): 0 parts of this process by device reads, 1 RCCL for all
 // pa_tune("cg_fuse"): the device CG's u update inside the SpMV (XV kernels)
 // instead of its own sweep.  Off: steady-state iteration on FE27 256³, sweep
@@ -821,8 +820,8 @@ struct Knob {
   const char* help;
 };
 const Knob kKnobs[] = {
-    {"spmv_flags", &g_spmv_flags, nullptr, 0, 0x7f, 0x7f,
-     "spmv_flags: bit 0 = non-temporal streams, bit 1 = merged launch as one round of resident waves (A/B), "
+    {"spmv_flags", &g_spmv_flags, nullptr, 0, 0x7d, 0x7d,
+     "spmv_flags: bit 0 = non-temporal streams, "
      "bit 2 = 16 B x runs (pattern rows), bit 3 = masked tail batch, bit 4 = identity slice lists dropped, "
      "bit 5 = non-temporal y stores, bit 6 = short-row kernels (launches whose rows have <= 8 entries)"},
     {"long_rows_exact", &g_long_exact, nullptr, 0, 1, 0,
@@ -843,9 +842,6 @@ const Knob kKnobs[] = {
     {"halo_direct", &g_halo_direct, nullptr, 0, 1, 0,
      "halo_direct: 1 = mul! over parts sharing a stream pair reads the ghosts straight from the owners' x "
      "on the compute stream (default), 0 = pack + pull on the comm stream"},
-    {"halo_fuse", &g_halo_fuse, nullptr, 0, 1, 0,
-     "halo_fuse: 1 = the direct pull's waves lead the merged launch and its boundary slices wait for "
-     "them (default), 0 = a pull launch before the merged launch"},
     {"halo_transport", &g_halo_transport, nullptr, 0, 1, 0,
      "halo_transport: 0 = parts of this process by device reads/copies, 1 = RCCL send/recv for every part "
      "with a communicator (pa_comm_init_all)"},
@@ -976,8 +972,7 @@ static int ctx_scratch(pa_ctx* c, const pa_ctx* share_events = nullptr) {
   HIPC(hipMalloc(&c->d_gather, (size_t)c->nparts * 16));
   HIPC(hipMalloc((void**)&c->d_ticket, 16));
   HIPC(hipMemset(c->d_ticket, 0, 16));
-  HIPC(hipMalloc((void**)&c->d_pull_ticket, 8));
-  HIPC(hipMemset(c->d_pull_ticket, 0, 8));
+  HIPC(hipDeviceSynchronize());  // (the null-stream memset done before any stream of the context uses it)
   HIPC(hipHostMalloc(&c->h_pinned, std::max<size_t>((size_t)(c->nparts + 1) * 16, 256)));  // gathered partials / CG state
   if (share_events) {  // one stream pair, one pair of pipeline events
     c->ev_packed = share_events->ev_packed;
@@ -1039,7 +1034,6 @@ int pa_ctx_destroy(pa_ctx* c) {
   dev_free(c->d_result);
   dev_free(c->d_gather);
   dev_free(c->d_ticket);
-  dev_free(c->d_pull_ticket);
   for (auto& b : c->bases_cache) dev_free(b.second);
   for (auto& b : c->merged_cache) dev_free(b.second);
   if (c->h_pinned) (void)hipHostFree(c->h_pinned);
@@ -1282,7 +1276,8 @@ int pa_add_gids(pa_index* I, int64_t n, const int64_t* gids, int64_t cap, int64_
   *n_new = m;
   if (m > cap || (m > 0 && !new_gids)) { dev_free(out); PA_FAIL("pa_add_gids: new_gids buffer too small (see *n_new)"); }
   if (m > 0) {
-    e = hipMemcpy(new_gids, out, m * 8, hipMemcpyDeviceToHost);
+    e = hipStreamSynchronize(c->s_main);  // (hipMemcpy runs on the null stream)
+    if (e == hipSuccess) e = hipMemcpy(new_gids, out, m * 8, hipMemcpyDeviceToHost);
     dev_free(out);
     HIPC(e);
   }
@@ -1299,7 +1294,8 @@ int pa_index_to_lids(pa_index* I, int64_t n, int64_t* ids) {
   HIPC(hipMalloc((void**)&d, n * 8));
   hipError_t e = hipMemcpy(d, ids, n * 8, hipMemcpyHostToDevice);
   const int rc = e == hipSuccess ? gids_to_lids(n, d, I->d_sgid, I->d_slid, I->nlids, c->s_main) : -1;
-  if (rc == 0) e = hipMemcpy(ids, d, n * 8, hipMemcpyDeviceToHost);
+  if (rc == 0) e = hipStreamSynchronize(c->s_main);  // (hipMemcpy runs on the null stream)
+  if (rc == 0 && e == hipSuccess) e = hipMemcpy(ids, d, n * 8, hipMemcpyDeviceToHost);
   dev_free(d);
   HIPC(e);
   CHECK_ARG(rc >= 0, "pa_index_to_lids: device pass failed");
@@ -1810,6 +1806,7 @@ int mat_from_coo_impl(pa_ctx* c, int dtype, int index_bytes, int ids_global, int
   const int64_t nptr = csr ? nrows_lids : ncols_lids;
   const int64_t base = csr ? csr_bi : 1;
   if (colptr_out) {  // colptr (CSC, 1-based) or rowptr (CSR, base Bi)
+    HIPC(hipStreamSynchronize(st));  // (hipMemcpy runs on the null stream)
     HIPC(hipMemcpy(colptr_out, dcolptr, (nptr + 1) * 8, hipMemcpyDeviceToHost));
     for (int64_t j = 0; j <= nptr; ++j) colptr_out[j] += base;
   }
@@ -1852,6 +1849,7 @@ int mat_from_coo_impl(pa_ctx* c, int dtype, int index_bytes, int ids_global, int
   int64_t* lptr_d = nullptr;
   if (A->nrows > 0) {
     std::vector<int64_t> rp(A->nrows + 1);
+    HIPC(hipStreamSynchronize(st));  // (hipMemcpy runs on the null stream)
     HIPC(hipMemcpy(rp.data(), rowptr, (A->nrows + 1) * 8, hipMemcpyDeviceToHost));
     std::vector<int32_t> len(A->nrows);
     for (int64_t r = 0; r < A->nrows; ++r) len[r] = (int32_t)(rp[r + 1] - rp[r]);
@@ -2490,22 +2488,11 @@ static int spmv_grouped(int n, pa_mat* const A[], pa_vec* const y[], const pa_in
   // complete, so interior = 0, halo = the pull, boundary = every slice
   const bool dmark = any_x && direct;
   if (dmark && (mark(0) || mark(1))) return -1;
-  bool big_part = false;  // one part alone fills the GPU many times: per-kind launches (g_spmv_merge_max)
-  if (g_spmv_merge_max > 0 && n == 1) big_part = A[0]->nslices > g_spmv_merge_max;
-  // the fused halo (pa_tune halo_fuse): the direct pull's waves lead the
-  // merged launch and its boundary slices wait for them (pa_spmv.hip,
-  // SpmvTable), instead of a pull launch ahead of it
-  const bool fuse = any_x && direct && g_halo_fuse && g_spmv_merge && !big_part && !g_capture_stream && !fz &&
-                    !has_alpha && bmode == 0;
-  void** dbases = nullptr;
   if (any_x && direct) {
-    dbases = direct_bases(c0, n, x);
-    if (!dbases) return -1;
-  }
-  // every ghost of x straight from its owner's x, in stream order before
-  // the slices (owned values are only read, ghosts only written)
-  auto direct_pull = [&]() -> int {
-    void** bases = dbases;
+    // every ghost of x straight from its owner's x, in stream order before
+    // the slices (owned values are only read, ghosts only written)
+    void** bases = direct_bases(c0, n, x);
+    if (!bases) return -1;
     if (g_capture_tables) {  // the graph's own copy: the cache may evict this one
       std::vector<void*> xs(n);
       for (int i = 0; i < n; ++i) xs[i] = x[i]->d;
@@ -2528,10 +2515,6 @@ static int spmv_grouped(int n, pa_mat* const A[], pa_vec* const y[], const pa_in
       }
       launch_pull_group(dt, qg, sm);
     }
-    return 0;
-  };
-  if (any_x && direct) {
-    if (!fuse && direct_pull()) return -1;  // (fused: the merged launch below pulls)
   } else if (any_x) {
     // the previous exchange's pulls read the send buffers: pack after them
     if (!g_capturing) HIPC(hipStreamWaitEvent(c0->s_main, c0->ev_recvd, 0));
@@ -2588,9 +2571,10 @@ static int spmv_grouped(int n, pa_mat* const A[], pa_vec* const y[], const pa_in
   if (dmark ? mark(2) : mark(0)) return -1;
   // no halo in flight (none, or pulled already on this stream): every slice
   // kind of every part in one launch — side rows and int32 slices first, so
-  // their few long waves start early, then delta16, pattern.  Fused halo:
-  // the pulls first, then the interior slices, then the gated rest.
+  // their few long waves start early, then delta16, multi-pattern, pattern
   int merged = 1;
+  bool big_part = false;  // one part alone fills the GPU many times: per-kind launches (g_spmv_merge_max)
+  if (g_spmv_merge_max > 0 && n == 1) big_part = A[0]->nslices > g_spmv_merge_max;
   if (g_spmv_merge && !big_part && (!any_x || direct)) {
     std::vector<SpmvPart> E;
     std::vector<int> W;
@@ -2599,50 +2583,6 @@ static int spmv_grouped(int n, pa_mat* const A[], pa_vec* const y[], const pa_in
       E.push_back(part(i, nwork, list));
       W.push_back(which);
     };
-    if (fuse) {
-      for (int i = 0; i < n; ++i) {
-        pa_xchg* X = xg[i];
-        if (X->n_rcv_data <= 0) continue;
-        SpmvPart q{};
-        q.nwork = (X->n_rcv_data + 64 * kPullPerLane - 1) / (64 * kPullPerLane);
-        q.list = X->d_lids_rcv;
-        q.A = A[i];
-        q.y = x[i]->d;
-        q.n_pull = X->n_rcv_data;
-        q.pbid = X->direct.d_bid;
-        q.pelem = X->direct.d_elem;
-        q.pbases = (const void* const*)dbases;
-        E.push_back(q);
-        W.push_back(5);
-      }
-      auto addg = [&](int which, int i, int64_t nwork, const int32_t* list) {
-        if (nwork <= 0) return;
-        E.push_back(part(i, nwork, list));
-        E.back().gate = true;
-        W.push_back(which);
-      };
-      for (int i = 0; i < n; ++i) {
-        if (g_spmv_format == 1 && A[i]->has_pat) {
-          add(1, i, A[i]->nx_int, A[i]->d_xint_list);
-          add(4, i, A[i]->nd_int, A[i]->d_dint_list);
-          add(0, i, A[i]->np_int, A[i]->d_pint_list);
-        } else if (A[i]->d_bnd_list) {
-          add(1, i, A[i]->nslices_int, A[i]->d_int_list);
-        }
-      }
-      for (int i = 0; i < n; ++i) {
-        if (g_spmv_format == 1 && A[i]->has_pat) {
-          addg(2, i, A[i]->s_nslices, nullptr);
-          addg(1, i, A[i]->nx_bnd, A[i]->d_xbnd_list);
-          addg(4, i, A[i]->nd_bnd, A[i]->d_dbnd_list);
-          addg(0, i, A[i]->np_bnd, A[i]->d_pbnd_list);
-        } else if (A[i]->d_bnd_list) {
-          addg(1, i, A[i]->nslices - A[i]->nslices_int, A[i]->d_bnd_list);
-        } else {
-          addg(1, i, A[i]->nslices, nullptr);
-        }
-      }
-    } else {
     for (int i = 0; i < n; ++i)
       if (g_spmv_format == 1 && A[i]->has_pat) add(2, i, A[i]->s_nslices, nullptr);
     for (int i = 0; i < n; ++i) {
@@ -2666,11 +2606,9 @@ static int spmv_grouped(int n, pa_mat* const A[], pa_vec* const y[], const pa_in
         add(0, i, A[i]->np_int, A[i]->d_pint_list);
         add(0, i, A[i]->np_bnd, A[i]->d_pbnd_list);
       }
-    }
     merged = launch_spmv_merged((int)E.size(), W.data(), E.data(), has_alpha, bmode, alpha, beta, c0,
                                 g_capture_tables, sm);
     if (merged < 0) PA_FAIL("mul!: merged launch table (device allocation or copy) failed");
-    if (merged && fuse && direct_pull()) return -1;  // too many entries for one table: pull, then per kind
     if (merged == 0 && !dmark && (mark(1) || mark(2))) return -1;
   }
   if (merged) {
@@ -3597,9 +3535,11 @@ int pa_mat_stencil(pa_ctx* c, int dtype, int kind, const int64_t gdims[3], const
   HIPC(hipMalloc((void**)&d_slen, std::max<int64_t>(ns, 1) * 4));
   HIPC(hipMalloc((void**)&d_sg, std::max<int64_t>(ns, 1) * 4));
   HIPC(hipMalloc((void**)&d_err, 4));
-  HIPC(hipMemset(d_slen, 0, std::max<int64_t>(ns, 1) * 4));
-  HIPC(hipMemset(d_sg, 0, std::max<int64_t>(ns, 1) * 4));
-  HIPC(hipMemset(d_err, 0, 4));
+  // zeroed on the compute stream the kernels below run on (a hipMemset on
+  // the null stream is not ordered before work on a non-blocking stream)
+  HIPC(hipMemsetAsync(d_slen, 0, std::max<int64_t>(ns, 1) * 4, c->s_main));
+  HIPC(hipMemsetAsync(d_sg, 0, std::max<int64_t>(ns, 1) * 4, c->s_main));
+  HIPC(hipMemsetAsync(d_err, 0, 4, c->s_main));
   launch_stencil_count(g, d_shell, d_coef, nrows, (int)nrows, A->H, d_slen, d_sg, d_err, c->s_main);
   HIPC(hipGetLastError());
   HIPC(hipStreamSynchronize(c->s_main));

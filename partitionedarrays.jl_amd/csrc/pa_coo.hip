@@ -19,6 +19,16 @@
 
 namespace pa {
 
+// a blocking copy ordered after the work queued on stream st (a plain
+// hipMemcpy goes to the null stream, which a non-blocking stream's kernels
+// are not ordered against)
+static inline hipError_t copy_sync(void* dst, const void* src, size_t bytes, hipMemcpyKind kind, hipStream_t st) {
+  hipError_t e = hipMemcpyAsync(dst, src, bytes, kind, st);
+  if (e == hipSuccess) e = hipStreamSynchronize(st);
+  return e;
+}
+
+
 // key = (J-1)*m + (I-1) (column-major = CSC order), or (I-1)*ncols + (J-1)
 // (row-major = CSR order, sparsecsr), payload = input position
 template <typename IT>
@@ -298,7 +308,7 @@ int coo_compress(int dtype, int index_bytes, int64_t m, int64_t ncols, int64_t n
     PA_HIP_TRY(hipMalloc((void**)&segid, n * 8));
     hipLaunchKernelGGL(k_heads, grid1(n), dim3(256), 0, st, n, key, head);
     PA_HIP_TRY(inclusive_sum(head, segid, n, st));
-    PA_HIP_TRY(hipMemcpy(&nu, segid + n - 1, 8, hipMemcpyDeviceToHost));
+    PA_HIP_TRY(copy_sync(&nu, segid + n - 1, 8, hipMemcpyDeviceToHost, st));
     PA_HIP_TRY(hipMalloc((void**)&start, nu * 8));
     hipLaunchKernelGGL(k_seg_start, grid1(n), dim3(256), 0, st, n, head, segid, start);
     PA_HIP_TRY(hipMalloc((void**)crow, nu * 4));
@@ -351,8 +361,8 @@ int coo_row_order(int64_t nu, const int32_t* crow, const int32_t* ccol, const in
     hipLaunchKernelGGL(k_own_keys, grid1(nu), dim3(256), 0, st, nu, crow, ccol, rl2o, cl2o, noids_c, ncols, *key2,
                        *idx2, *gflag);
     PA_HIP_TRY(exclusive_sum(*gflag, *grank, nu, st));
-    PA_HIP_TRY(hipMemcpy(&last, *grank + nu - 1, 8, hipMemcpyDeviceToHost));
-    PA_HIP_TRY(hipMemcpy(&lastf, *gflag + nu - 1, 8, hipMemcpyDeviceToHost));
+    PA_HIP_TRY(copy_sync(&last, *grank + nu - 1, 8, hipMemcpyDeviceToHost, st));
+    PA_HIP_TRY(copy_sync(&lastf, *gflag + nu - 1, 8, hipMemcpyDeviceToHost, st));
     ngh = last + lastf;
     nnz = nu - ngh;
     // ghost rows carry key2 = ~0: sort all bits of the owned range + 1
@@ -530,8 +540,8 @@ int gids_first_touch(int64_t n, const int64_t* gids, const uint64_t* sgid, const
   if (e != hipSuccess) goto fail;
   hipLaunchKernelGGL(k_absent, grid1(n), dim3(256), 0, st, n, gids, sgid, slid, nl, flag);
   e = exclusive_sum(flag, pos, n, st);
-  if (e == hipSuccess) e = hipMemcpy(&m, pos + n - 1, 8, hipMemcpyDeviceToHost);
-  if (e == hipSuccess) e = hipMemcpy(&lastf, flag + n - 1, 8, hipMemcpyDeviceToHost);
+  if (e == hipSuccess) e = copy_sync(&m, pos + n - 1, 8, hipMemcpyDeviceToHost, st);
+  if (e == hipSuccess) e = copy_sync(&lastf, flag + n - 1, 8, hipMemcpyDeviceToHost, st);
   if (e != hipSuccess) goto fail;
   m += lastf;
   if (m > 0) {
@@ -561,7 +571,7 @@ int gids_first_touch(int64_t n, const int64_t* gids, const uint64_t* sgid, const
     if (e != hipSuccess) goto fail;
     hipLaunchKernelGGL(k_heads, grid1(m), dim3(256), 0, st, m, key, head);
     e = inclusive_sum(head, rank, m, st);
-    if (e == hipSuccess) e = hipMemcpy(&u, rank + m - 1, 8, hipMemcpyDeviceToHost);
+    if (e == hipSuccess) e = copy_sync(&u, rank + m - 1, 8, hipMemcpyDeviceToHost, st);
     if (e == hipSuccess) e = hipMalloc((void**)&key2, u * 8);
     if (e == hipSuccess) e = hipMalloc((void**)&val2, u * 8);
     if (e != hipSuccess) goto fail;
@@ -664,7 +674,7 @@ int coo_assemble_pack(int dtype, int64_t n, const int64_t* I, const int64_t* J, 
     std::vector<int32_t> hs(nl > 0 ? nl : 1, -1);
     for (int64_t l = 0; l < nl; ++l) hs[l] = lid_to_ohid[l] > 0 ? -1 : -2;
     e = hipMalloc((void**)&sol, hs.size() * 4);
-    if (e == hipSuccess) e = hipMemcpy(sol, hs.data(), hs.size() * 4, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = copy_sync(sol, hs.data(), hs.size() * 4, hipMemcpyHostToDevice, st);
   }
   if (e == hipSuccess && nslots > 0) e = hipMalloc((void**)&dptrs, ptrs_rcv.size() * 8);
   if (e == hipSuccess && nslots > 0)

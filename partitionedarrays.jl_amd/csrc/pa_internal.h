@@ -235,17 +235,7 @@ struct SpmvPart {
   void* un = nullptr;
   void* xacc = nullptr;
   const CGState* cg = nullptr;
-  // a pull entry of the merged launch (which 5, spmv_grouped's fused halo):
-  // nwork waves pull the part's n_pull ghosts x[lids[i]] = bases[bid[i]][elem[i]]
-  // (x is y here: the receiving part's vector), then publish their arrival
-  int64_t n_pull = 0;
-  const int32_t* pbid = nullptr;
-  const int64_t* pelem = nullptr;
-  const void* const* pbases = nullptr;
-  // the merged launch's boundary entries wait for the call's pulls
-  bool gate = false;
 };
-constexpr int kPullPerLane = 8;  // ghosts per lane of a fused pull wave
 
 struct PackGroup {
   int np;
@@ -301,11 +291,6 @@ struct pa_ctx {
   void* d_result = nullptr;       // 16 B final per-part value
   void* d_gather = nullptr;       // nparts*16 B gathered partials (RCCL mode)
   unsigned* d_ticket = nullptr;   // arrival counter of the one-launch folds (0 between launches)
-  // the fused halo's pull waves count their arrivals here (never reset); the
-  // launches that use it run in order on this context's compute stream, so
-  // at a launch's start it holds pull_issued, the pulls of earlier launches
-  unsigned long long* d_pull_ticket = nullptr;
-  uint64_t pull_issued = 0;
   void* h_pinned = nullptr;       // pinned host staging (>= nparts*16 B)
   // timing (pa_ctx_set_timing): four events per recorded mul! — before the
   // interior slices, after them, after the halo wait (+unpack), after the

@@ -48,11 +48,9 @@ struct alignas(2 * R) S16Pack {
   uint16_t c[R];
 };
 
-// Bits 7 (x runs in int32 slices) and 9 (lane-shared x runs) and the old
-// bit 1 (XCD remap) were negative A/Bs of rounds 1-3.
-// SPMV_PERSIST (bit 1, under A/B): the merged launch as a grid of at most
-// one round of resident waves, each looping over work items w, w + G, ...
-enum { SPMV_NT = 1, SPMV_PERSIST = 2, SPMV_XPAIR = 4, SPMV_TAILB = 8, SPMV_IDLIST = 16, SPMV_YNT = 32, SPMV_SHORT = 64,
+// Bit 1 (XCD remap), 7 (x runs in int32 slices) and 9 (lane-shared x runs)
+// were negative A/Bs of rounds 1-3 and are gone.
+enum { SPMV_NT = 1, SPMV_XPAIR = 4, SPMV_TAILB = 8, SPMV_IDLIST = 16, SPMV_YNT = 32, SPMV_SHORT = 64,
        SPMV_PRODA = 256 /* per matrix: CSR parent, α scales the product */ };
 
 typedef unsigned int spmv_u32x4 __attribute__((ext_vector_type(4)));
@@ -142,11 +140,6 @@ struct SpmvArgs {
   PA_GLB T* un;
   PA_GLB T* xacc;
   const PA_GLB CGState* cg;
-  // a pull entry (pk 5): ghost i of the part: y[list[i]] = pbases[pbid[i]][pelem[i]],
-  // i < nrows (y is the receiving part's x)
-  const PA_GLB int32_t* pbid;
-  const PA_GLB int64_t* pelem;
-  const PA_GLB uint64_t* pbases;   // the owners' x (device addresses)
 };
 
 template <typename T> struct DAcc { using type = double; };
@@ -775,15 +768,7 @@ static SpmvArgs<T> make_args(int which, int64_t nwork, const int32_t* list, cons
              : which == 2 ? A->maxlen_side
              : which == 1 ? ((g_spmv_format == 1 && A->has_pat) ? A->maxlen_pm_int : A->maxlen_all)
              : which == 4 ? A->maxlen_d16
-             : which == 5 ? 0
                           : INT32_MAX;
-  if (which == 5) {  // a pull entry: y is the receiving part's x, list its ghost lids
-    a.nrows = cgp->n_pull;
-    a.pbid = (decltype(a.pbid))(cgp->pbid);
-    a.pelem = (decltype(a.pelem))(cgp->pelem);
-    a.pbases = (decltype(a.pbases))((const uint64_t*)cgp->pbases);
-    return a;
-  }
   if (which == 2) {
     a.soff = (decltype(a.soff))(A->d_s_off);
     a.slen = (decltype(a.slen))(A->d_s_len);
@@ -910,77 +895,21 @@ void launch_spmv_group(int which, int np, const SpmvPart* parts, bool has_alpha,
 // (side rows, the few int32 slices) then overlap the big ones instead of
 // each adding its own tail.  The table lives in device memory (too large for
 // kernel arguments), one cached copy per distinct call.
-constexpr int kMergeMax = 72;
+constexpr int kMergeMax = 48;
 
-// The fused halo (spmv_grouped with the direct pull): the call's pulls are
-// the table's first entries (pk 5), its boundary entries (gate) wait until
-// every pull wave of the launch has arrived on `ticket` (>= the launch's
-// target): pull waves store the ghosts write-through and drain them before
-// their arrival (cdna_hip_programming.md Guideline 16, R1), a gated wave polls
-// the counter and takes an agent-scope acquire before its first x load.
-// Workgroups are dispatched in index order and the pulls come first, so
-// every pull wave is running or done when a gated wave waits.
 template <typename T>
 struct SpmvTable {
   int n;
   int pk[kMergeMax];
-  int gate[kMergeMax];
-  unsigned long long* ticket;
   int64_t start[kMergeMax + 1];
   SpmvArgs<T> a[kMergeMax];
 };
 
-typedef __attribute__((address_space(1))) unsigned long long pa_gull;
-
-// one pull wave: kPullPerLane ghosts per lane, stored write-through
-template <typename T>
-__device__ __forceinline__ void pull_wave(const SpmvArgs<T>& a, int64_t w, unsigned long long* ticket) {
-  const int lane = threadIdx.x & 63;
-  const int64_t n = a.nrows;
-  T v[kPullPerLane];
-  int32_t dst[kPullPerLane];
-#pragma unroll
-  for (int k = 0; k < kPullPerLane; ++k) {
-    const int64_t i = (w * kPullPerLane + k) * 64 + lane;
-    dst[k] = -1;
-    if (i < n) {
-      const T* src = (const T*)(uintptr_t)a.pbases[a.pbid[i]];
-      v[k] = src[a.pelem[i]];
-      dst[k] = a.list[i];
-    }
-  }
-#pragma unroll
-  for (int k = 0; k < kPullPerLane; ++k)
-    if (dst[k] >= 0) {
-      T* p = (T*)a.y + dst[k];
-      if constexpr (sizeof(T) == 4) {
-        __hip_atomic_store((pa_gu32*)p, __builtin_bit_cast(unsigned, v[k]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      } else if constexpr (sizeof(T) == 8) {
-        __hip_atomic_store((pa_gull*)p, __builtin_bit_cast(unsigned long long, v[k]), __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-      } else {
-        unsigned long long q[2];
-        __builtin_memcpy(q, &v[k], 16);
-        __hip_atomic_store((pa_gull*)p, q[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store((pa_gull*)p + 1, q[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-    }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every store of the wave done before its arrival
-  if (lane == 0) __hip_atomic_fetch_add((pa_gull*)ticket, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// a gated wave: every pull wave of the launch has arrived, then the acquire
-__device__ __forceinline__ void wait_pulls(unsigned long long* ticket, unsigned long long target) {
-  if ((threadIdx.x & 63) == 0)
-    while (__hip_atomic_load((pa_gull*)ticket, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target)
-      __builtin_amdgcn_s_sleep(2);
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-}
-
-template <typename T, int R, bool ALPHA, int BMODE, int U, bool SH, bool XV, bool HALO>
-__device__ __forceinline__ void merged_item(const SpmvTable<T>* __restrict__ tab, int64_t w,
-                                            unsigned long long target, bool& waited) {
+template <typename T, int R, bool ALPHA, int BMODE, int U, bool SH, bool XV = false>
+__device__ __forceinline__ void merged_wave(const SpmvTable<T>* __restrict__ tab) {
+  const int64_t w = (int64_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   const int n = tab->n;
+  if (w >= tab->start[n]) return;
   int lo = 0, hi = n;  // last entry whose start <= w
   while (hi - lo > 1) {
     const int mid = (lo + hi) >> 1;
@@ -990,126 +919,46 @@ __device__ __forceinline__ void merged_item(const SpmvTable<T>* __restrict__ tab
   const int pk = __builtin_amdgcn_readfirstlane(tab->pk[p]);
   const int64_t lw = w - tab->start[p];
   const SpmvArgs<T>& a = tab->a[p];
-  if constexpr (HALO) {
-    if (pk == 5) {
-      pull_wave<T>(a, lw, tab->ticket);
-      return;
-    }
-    if (!waited && __builtin_amdgcn_readfirstlane(tab->gate[p])) {
-      wait_pulls(tab->ticket, target);
-      waited = true;
-    }
-  }
   if (pk == 1) spmv_wave<T, R, ALPHA, BMODE, U, 1, SH, XV>(a, lw);
   else if (pk == 3) spmv_wave<T, R, ALPHA, BMODE, U, 3, SH, XV>(a, lw);
   else spmv_wave<T, R, ALPHA, BMODE, U, 0, SH, XV>(a, lw);
 }
 
-// one work item per wave, or (SPMV_PERSIST: the grid holds fewer waves than
-// items) items w, w + G, w + 2G, ... (G = the grid's waves), each computed
-// exactly as by its own wave
-template <typename T, int R, bool ALPHA, int BMODE, int U, bool SH, bool XV = false, bool HALO = false,
-          bool PERSIST = false>
-__device__ __forceinline__ void merged_wave(const SpmvTable<T>* __restrict__ tab, unsigned long long target) {
-  const int64_t total = tab->start[tab->n];
-  bool waited = false;
-  int64_t w = (int64_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-  if constexpr (PERSIST) {
-    const int64_t G = (int64_t)gridDim.x * 4;
-    for (; w < total; w += G) merged_item<T, R, ALPHA, BMODE, U, SH, XV, HALO>(tab, w, target, waited);
-  } else {
-    if (w < total) merged_item<T, R, ALPHA, BMODE, U, SH, XV, HALO>(tab, w, target, waited);
-  }
-}
-
 // No occupancy cap: amdgpu_waves_per_eu(4) (F32 134 -> 128 VGPRs, a small
 // spill) lost in a same-box A/B: C5 F32 +4.5 %, FE27 F64 +0.4 %, F32 +0.6 %
 // (profiles/r02/stream/ab_waves4.txt).
-// HALO: the fused halo's pull entries and gates; PERSIST: a grid of at most
-// one round of resident waves, each looping over its items (spmv_flags bit
-// 1, under A/B; the loop costs registers, so it is its own instantiation).
-// Both for y = A*x only (α = 1, β = 0).
-template <typename T, int R, bool ALPHA, int BMODE, int U, bool SH, bool XV = false, bool HALO = false,
-          bool PERSIST = false>
-__global__ __launch_bounds__(256) void k_spmv_merged(const SpmvTable<T>* __restrict__ tab,
-                                                     unsigned long long target) {
-  merged_wave<T, R, ALPHA, BMODE, U, SH, XV, HALO, PERSIST>(tab, target);
+template <typename T, int R, bool ALPHA, int BMODE, int U, bool SH, bool XV = false>
+__global__ __launch_bounds__(256) void k_spmv_merged(const SpmvTable<T>* __restrict__ tab) {
+  merged_wave<T, R, ALPHA, BMODE, U, SH, XV>(tab);
 }
 
 // F64 short rows (FD7): 5 waves per SIMD instead of 4 (96 VGPRs instead of
 // 102; the pattern path keeps its registers, a few int32-path values spill).
 // C2 FD7 128^3: 0.0312-0.0317 -> 0.0303 ms (profiles/r02/waves/).  Not for
 // F32/C64 (R = 4 / complex: ~200 spills) nor for longer rows (FE27: -10 %).
-template <typename T, int R, bool ALPHA, int BMODE, bool HALO = false, bool PERSIST = false>
+template <typename T, int R, bool ALPHA, int BMODE>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k_spmv_merged_short(
-    const SpmvTable<T>* __restrict__ tab, unsigned long long target) {
-  merged_wave<T, R, ALPHA, BMODE, 8, true, false, HALO, PERSIST>(tab, target);
-}
-
-// one block per 4 waves; a PERSIST kernel: capped at one round of the
-// kernel's resident blocks
-template <typename K>
-static int64_t merged_blocks(K kernel, int64_t waves, bool persist = false) {
-  const int64_t blocks = (waves + 3) / 4;
-  if (!persist || blocks == 0) return blocks;
-  int dev = 0, ncu = 0, per_cu = 0;
-  if (hipGetDevice(&dev) != hipSuccess ||
-      hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-      hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, 256, 0) != hipSuccess || per_cu <= 0) {
-    (void)hipGetLastError();
-    return blocks;
-  }
-  return std::min<int64_t>(blocks, (int64_t)ncu * per_cu);
+    const SpmvTable<T>* __restrict__ tab) {
+  merged_wave<T, R, ALPHA, BMODE, 8, true>(tab);
 }
 
 template <typename T, int R, bool ALPHA, int BMODE>
-static void launch_merged_t(const SpmvTable<T>* d, int64_t waves, bool sh, unsigned long long target,
-                            hipStream_t st) {
-  if (waves <= 0) return;
-  if constexpr (!ALPHA && BMODE == 0) {
-    if (!target && (g_spmv_flags & SPMV_PERSIST)) {
-      if constexpr (std::is_same<T, double>::value) {
-        if (sh) {
-          auto k = k_spmv_merged_short<T, R, false, 0, false, true>;
-          hipLaunchKernelGGL(k, dim3(merged_blocks(k, waves, true)), dim3(256), 0, st, d, target);
-          return;
-        }
-      }
-      auto k = sh ? k_spmv_merged<T, R, false, 0, 8, true, false, false, true>
-                  : k_spmv_merged<T, R, false, 0, 8, false, false, false, true>;
-      hipLaunchKernelGGL(k, dim3(merged_blocks(k, waves, true)), dim3(256), 0, st, d, target);
-      return;
-    }
-    if (target) {  // the fused halo
-      if constexpr (std::is_same<T, double>::value) {
-        if (sh) {
-          auto k = k_spmv_merged_short<T, R, false, 0, true>;
-          hipLaunchKernelGGL(k, dim3(merged_blocks(k, waves)), dim3(256), 0, st, d, target);
-          return;
-        }
-      }
-      auto k = sh ? k_spmv_merged<T, R, false, 0, 8, true, false, true> : k_spmv_merged<T, R, false, 0, 8, false, false, true>;
-      hipLaunchKernelGGL(k, dim3(merged_blocks(k, waves)), dim3(256), 0, st, d, target);
-      return;
-    }
-  }
+static void launch_merged_t(const SpmvTable<T>* d, int64_t waves, bool sh, hipStream_t st) {
+  const int64_t blocks = (waves + 3) / 4;
+  if (blocks == 0) return;
   if constexpr (std::is_same<T, double>::value) {
     if (sh) {
-      auto k = k_spmv_merged_short<T, R, ALPHA, BMODE>;
-      hipLaunchKernelGGL(k, dim3(merged_blocks(k, waves)), dim3(256), 0, st, d, target);
+      hipLaunchKernelGGL((k_spmv_merged_short<T, R, ALPHA, BMODE>), dim3(blocks), dim3(256), 0, st, d);
       return;
     }
   }
-  if (sh) {
-    auto k = k_spmv_merged<T, R, ALPHA, BMODE, 8, true>;
-    hipLaunchKernelGGL(k, dim3(merged_blocks(k, waves)), dim3(256), 0, st, d, target);
-  } else {
-    auto k = k_spmv_merged<T, R, ALPHA, BMODE, 8, false>;
-    hipLaunchKernelGGL(k, dim3(merged_blocks(k, waves)), dim3(256), 0, st, d, target);
-  }
+  if (sh)
+    hipLaunchKernelGGL((k_spmv_merged<T, R, ALPHA, BMODE, 8, true>), dim3(blocks), dim3(256), 0, st, d);
+  else
+    hipLaunchKernelGGL((k_spmv_merged<T, R, ALPHA, BMODE, 8, false>), dim3(blocks), dim3(256), 0, st, d);
 }
 
-static int pk_of(int which) { return which == 0 ? 1 : which == 4 ? 3 : which == 5 ? 5 : 0; }
+static int pk_of(int which) { return which == 0 ? 1 : which == 4 ? 3 : 0; }
 
 template <typename T, int R>
 static int merged_t(int n, const int* which, const SpmvPart* parts, bool has_alpha, int bmode, const void* alpha,
@@ -1117,31 +966,19 @@ static int merged_t(int n, const int* which, const SpmvPart* parts, bool has_alp
   SpmvTable<T> h;
   std::memset(&h, 0, sizeof(h));  // the table's bytes are its cache key
   bool sh = (g_spmv_flags & SPMV_SHORT) != 0;
-  int64_t npull = 0;
   for (int i = 0; i < n; ++i) {
     const SpmvPart& q = parts[i];
     if (q.nwork <= 0) continue;
     if (h.n == kMergeMax) return 1;
     const int32_t* list = q.list;
-    if ((g_spmv_flags & SPMV_IDLIST) && list && which[i] != 2 && which[i] != 5 && q.nwork == q.A->nslices)
-      list = nullptr;
+    if ((g_spmv_flags & SPMV_IDLIST) && list && which[i] != 2 && q.nwork == q.A->nslices) list = nullptr;
     h.a[h.n] = make_args<T>(which[i], q.nwork, list, q.A, q.x, q.y, q.ymap, alpha, beta, q.dotp, &q);
     h.pk[h.n] = pk_of(which[i]);
-    h.gate[h.n] = q.gate ? 1 : 0;
-    if (which[i] == 5) npull += q.nwork;
     sh = sh && h.a[h.n].maxlen <= 8;
     h.start[h.n + 1] = h.start[h.n] + q.nwork;
     ++h.n;
   }
   if (h.n == 0) return 0;
-  unsigned long long target = 0;
-  if (npull > 0) {  // pull waves arrive on the owner's ticket; gated waves wait for this launch's
-    // (a captured launch would replay one target: never fused under capture;
-    // the fused kernels are instantiated for y = A*x only)
-    if (pinned || has_alpha || bmode != 0 || h.a[0].cg) return 1;
-    h.ticket = owner->d_pull_ticket;
-    target = owner->pull_issued + (unsigned long long)npull;
-  }
   // cached device copy of this exact table (most recent first); a graph
   // capture (pinned) gets its own copy, owned by the graph
   auto& C = owner->merged_cache;
@@ -1176,21 +1013,19 @@ static int merged_t(int n, const int* which, const SpmvPart* parts, bool has_alp
   if (h.a[0].cg) {  // the device CG's fused u update (α = 1, β = 0)
     const int64_t blocks = (waves + 3) / 4;
     if (blocks == 0) return 0;
-    if (sh) hipLaunchKernelGGL((k_spmv_merged<T, R, false, 0, 8, true, true>), dim3(blocks), dim3(256), 0, st, dt, target);
-    else hipLaunchKernelGGL((k_spmv_merged<T, R, false, 0, 8, false, true>), dim3(blocks), dim3(256), 0, st, dt, target);
-    if (npull > 0) owner->pull_issued = target;
+    if (sh) hipLaunchKernelGGL((k_spmv_merged<T, R, false, 0, 8, true, true>), dim3(blocks), dim3(256), 0, st, dt);
+    else hipLaunchKernelGGL((k_spmv_merged<T, R, false, 0, 8, false, true>), dim3(blocks), dim3(256), 0, st, dt);
     return 0;
   }
   if (!has_alpha) {
-    if (bmode == 0) launch_merged_t<T, R, false, 0>(dt, waves, sh, target, st);
-    else if (bmode == 1) launch_merged_t<T, R, false, 1>(dt, waves, sh, target, st);
-    else launch_merged_t<T, R, false, 2>(dt, waves, sh, target, st);
+    if (bmode == 0) launch_merged_t<T, R, false, 0>(dt, waves, sh, st);
+    else if (bmode == 1) launch_merged_t<T, R, false, 1>(dt, waves, sh, st);
+    else launch_merged_t<T, R, false, 2>(dt, waves, sh, st);
   } else {
-    if (bmode == 0) launch_merged_t<T, R, true, 0>(dt, waves, sh, target, st);
-    else if (bmode == 1) launch_merged_t<T, R, true, 1>(dt, waves, sh, target, st);
-    else launch_merged_t<T, R, true, 2>(dt, waves, sh, target, st);
+    if (bmode == 0) launch_merged_t<T, R, true, 0>(dt, waves, sh, st);
+    else if (bmode == 1) launch_merged_t<T, R, true, 1>(dt, waves, sh, st);
+    else launch_merged_t<T, R, true, 2>(dt, waves, sh, st);
   }
-  if (npull > 0) owner->pull_issued = target;
   return 0;
 }
 

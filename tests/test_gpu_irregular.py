@@ -43,10 +43,6 @@ def _ox(O, a):
     return O.Cx(a.real.copy(), a.imag.copy()) if np.iscomplexobj(a) else a.copy()
 
 
-def _sel(O, ref, idx):
-    return O.Cx(ref.re[idx], ref.im[idx]) if isinstance(ref, O.Cx) else ref[idx]
-
-
 def _eq(O, got, ref):
     if isinstance(ref, O.Cx):
         return np.array_equal(got.real, ref.re) and np.array_equal(got.imag, ref.im)
@@ -234,43 +230,3 @@ def test_launch_paths_equal_oracle(be, pamd, O, merge, direct, d16):
     finally:
         for k, v in prev.items():
             pamd._lib.tune(k, v)
-
-
-@pytest.mark.parametrize("dtype", [np.float64, np.float32, np.complex128, np.complex64])
-@pytest.mark.parametrize("problem", ["voronoi", "cartesian"])
-def test_fused_halo_equals_pull_launch(be, pamd, O, dtype, problem):
-    """pa_tune("halo_fuse"): the direct pull's waves inside the merged launch,
-    the boundary slices waiting for them on a device ticket, give the bits
-    of the pull launch ahead of the merged launch and of the oracle, over
-    repeated calls (the ticket keeps counting) with x changed in between."""
-    if problem == "voronoi":
-        N, nparts = (30, 28, 26), 8
-        parts = be.get_part_ids(nparts)
-        A = pamd.drivers.irregular_problem(parts, N, 27, dtype)
-        OA = _oracle(O, N, nparts, dtype)
-    else:
-        N, shape = (26, 24, 22), (2, 2, 2)
-        parts = be.get_part_ids(shape)
-        A = pamd.drivers.stencil_operator(parts, N, 27, dtype)
-        OA = O.stencil_problem(O.get_part_ids(shape), N, 27, dtype)
-    rng = np.random.default_rng(SEED + 41)
-    for rep in range(3):
-        xs = {p: _rand(rng, A.cols.partition.local(p).num_lids, dtype) for p in parts.part_ids}
-        x = pamd.PVector.from_host(pamd.map_parts(lambda s: xs[s.part], A.cols.partition), A.cols)
-        got = []
-        for fuse in (1, 0):
-            prev = pamd._lib.tune("halo_fuse", fuse)
-            try:
-                y = pamd.PVector.undef(A.rows, dtype)
-                pamd.mul_(y, A, x)
-                got.append((y.to_host(), x.to_host()))
-            finally:
-                pamd._lib.tune("halo_fuse", prev)
-        ox = O.PVector(O.map_parts(lambda s: _ox(O, xs[s.part]), OA.cols.partition), OA.cols)
-        oy = O.pvector_undef(OA.rows, dtype)
-        O.mul_(oy, OA, ox)
-        for p in parts.part_ids:
-            own = A.rows.partition.local(p).oid_to_lid - 1
-            for (gy, gx), label in zip(got, ("fused", "pull launch")):
-                assert _eq(O, gy.local(p)[own], _sel(O, oy.values[p], own)), f"{label}: part {p} SpMV differs"
-                assert _eq(O, gx.local(p), ox.values[p]), f"{label}: part {p} ghost values differ"

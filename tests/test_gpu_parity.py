@@ -323,7 +323,7 @@ def test_beta_zero_overwrites_nan_inf(be, pamd, O, fmt, alpha):
 
 
 @pytest.mark.parametrize("dtype", [np.float64, np.float32, np.complex128, np.complex64])
-@pytest.mark.parametrize("flags", [1 | 8 | 16 | 32 | 64, 4 | 16, 1 | 4 | 8, 93 | 2])
+@pytest.mark.parametrize("flags", [1 | 8 | 16 | 32 | 64, 4 | 16, 1 | 4 | 8])
 def test_spmv_flag_variants_bitexact(be, pamd, O, dtype, flags):
     """spmv_flags variants (pattern rows' 16 B x runs off, non-temporal y
     stores on, tail batch / short-row kernels off): the same terms in the
@@ -350,30 +350,3 @@ def test_spmv_flag_variants_bitexact(be, pamd, O, dtype, flags):
                 assert _eq(O, got.local(p)[own], _sel(O, oy.values[p], own)), (alpha, p)
     finally:
         pamd._lib.tune("spmv_flags", prev)
-
-
-@pytest.mark.parametrize("kind,N,shape,dtype", [(7, (128, 128, 128), (1, 1, 1), np.float64),
-                                                (27, (96, 96, 96), (2, 2, 2), np.float32),
-                                                (27, (80, 80, 80), (1, 1, 1), np.complex128)])
-def test_persistent_merged_equals_default(be, pamd, kind, N, shape, dtype):
-    """spmv_flags bit 1: the merged launch as one round of resident waves,
-    each looping over its work items, at sizes with several rounds of waves
-    (the loop runs): the same bits as one wave per item."""
-    parts = be.get_part_ids(shape)
-    A = pamd.drivers.stencil_operator(parts, N, kind, dtype)
-    rng = np.random.default_rng(SEED + 31)
-    xs = {p: _rand(rng, A.cols.partition.local(p).num_lids, dtype) for p in parts.part_ids}
-    x = pamd.PVector.from_host(pamd.map_parts(lambda s: xs[s.part], A.cols.partition), A.cols)
-    out = []
-    for flags in (93, 95):
-        prev = pamd._lib.tune("spmv_flags", flags)
-        try:
-            y = pamd.PVector.undef(A.rows, dtype)
-            pamd.mul_(y, A, x)
-            out.append(y.to_host())
-        finally:
-            pamd._lib.tune("spmv_flags", prev)
-    for p in parts.part_ids:
-        own = A.rows.partition.local(p).oid_to_lid - 1
-        a, b = out[0].local(p)[own], out[1].local(p)[own]
-        assert np.array_equal(a.view(np.uint8), b.view(np.uint8)), f"part {p}: persistent launch differs"
