@@ -134,9 +134,15 @@ def pmc_traffic(args, steps=5, halo=False):
     if shutil.which("rocprofv3") is None:
         return None, "rocprofv3 not found"
     tot = {}
-    for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
+    # FETCH_SIZE and WRITE_SIZE (one pass each), then the UTCL1 translation
+    # counters of the same kernels (address translation beside the bytes:
+    # a placement-dependent rate shows here if it is the TLB)
+    passes = [("FETCH_SIZE",), ("WRITE_SIZE",),
+              ("TCP_UTCL1_REQUEST_sum", "TCP_UTCL1_TRANSLATION_MISS_sum", "TCP_UTCL1_TRANSLATION_HIT_sum")]
+    for ctrs in passes:
+        ctr = ctrs[0]
         d = tempfile.mkdtemp(prefix="pa_pmc_", dir="/tmp")
-        cmd = ["rocprofv3", "--pmc", ctr, "-d", d, "-o", "pmc", "--output-format", "csv", "--",
+        cmd = ["rocprofv3", "--pmc", *ctrs, "-d", d, "-o", "pmc", "--output-format", "csv", "--",
                sys.executable, os.path.abspath(__file__), "--child-pmc", "--steps", str(steps),
                "--n", str(args.n), "--kind", str(args.kind), "--dtype", args.dtype, "--tune", args.tune] + \
             (["--child-halo"] if halo else [])
@@ -146,14 +152,19 @@ def pmc_traffic(args, steps=5, halo=False):
             p.wait(timeout=240)
         except subprocess.TimeoutExpired:
             os.killpg(p.pid, signal.SIGKILL)
+            if ctr.startswith("TCP_"):
+                break  # the translation pass is extra: keep the byte counts
             return None, f"rocprofv3 --pmc {ctr} timed out"
         files = [os.path.join(r, f) for r, _, fs in os.walk(d) for f in fs if f.endswith("counter_collection.csv")]
         if p.returncode != 0 or not files:
+            if ctr.startswith("TCP_"):
+                break
             return None, f"rocprofv3 --pmc {ctr} failed (rc {p.returncode})"
         rows = list(csv.DictReader(open(files[0])))
-        vals = [float(r["Counter_Value"]) for r in rows
-                if any(k in r["Kernel_Name"] for k in PMC_KERNELS) and r["Counter_Name"] == ctr]
-        tot[ctr] = sum(vals) / (steps + 1)  # warmup step + steps
+        for c in ctrs:
+            vals = [float(r["Counter_Value"]) for r in rows
+                    if any(k in r["Kernel_Name"] for k in PMC_KERNELS) and r["Counter_Name"] == c]
+            tot[c] = sum(vals) / (steps + 1)  # warmup step + steps
         if ctr == "FETCH_SIZE":
             probe = [float(r["Counter_Value"]) for r in rows
                      if "k_probe_read" in r["Kernel_Name"] and r["Counter_Name"] == ctr]
@@ -161,8 +172,14 @@ def pmc_traffic(args, steps=5, halo=False):
         shutil.rmtree(d, ignore_errors=True)
     factor = PROBE_BYTES / (tot["probe_kb"] * 1024) if tot.get("probe_kb") else 2.0
     traffic = tot["FETCH_SIZE"] * 1024 * factor + tot["WRITE_SIZE"] * 1024
+    tlb = None
+    if tot.get("TCP_UTCL1_REQUEST_sum"):
+        tlb = {"utcl1_requests": round(tot["TCP_UTCL1_REQUEST_sum"]),
+               "utcl1_misses": round(tot["TCP_UTCL1_TRANSLATION_MISS_sum"]),
+               "utcl1_hits": round(tot["TCP_UTCL1_TRANSLATION_HIT_sum"]),
+               "utcl1_miss_rate": round(tot["TCP_UTCL1_TRANSLATION_MISS_sum"] / tot["TCP_UTCL1_REQUEST_sum"], 5)}
     return traffic, {"fetch_kb": round(tot["FETCH_SIZE"]), "write_kb": round(tot["WRITE_SIZE"]),
-                     "fetch_factor": round(factor, 4),
+                     "fetch_factor": round(factor, 4), "translation_per_step": tlb,
                      "note": (f"rocprofv3 --pmc FETCH_SIZE | WRITE_SIZE passes over {steps + 1} mul! steps; "
                               f"FETCH_SIZE x {factor:.3f}, the factor measured on k_probe_read launches "
                               f"reading a known 1 GiB with 16 B/lane loads in the same process, + WRITE_SIZE")}

@@ -14,6 +14,7 @@
 #include <memory>
 #include <numeric>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "pa_internal.h"
@@ -58,6 +59,7 @@ int g_spmv_merge = 1;     // pa_tune("spmv_merge"): one launch for every slice k
 // F32 −2.8 %; C2 (16 k slices) and C5 stay merged (−10 % / −15 %).
 // profiles/r02/open/ab_merge.jsonl.  0: no limit.
 int64_t g_spmv_merge_max = 65536;
+int g_pattern_dedup = 1;  // pa_tune("pattern_dedup") (A/B, build time): distinct-pattern table
 int g_halo_direct = 1;     // pa_tune("halo_direct"): grouped mul! pulls ghosts straight from the owners' x
 int g_halo_transport = 0;  // pa_tune("halo_transport"): 0 parts of this process by device reads, 1 RCCL for all
 // pa_tune("cg_fuse"): the device CG's u update inside the SpMV (XV kernels)
@@ -299,6 +301,48 @@ int finish_sell_layout(pa_mat* A, const std::vector<int32_t>& slen, const std::v
   return 0;
 }
 
+// The pattern slices' offset lists as a table of the distinct ones (a
+// Cartesian part has a handful: interior rows, the boundary planes' Dirichlet
+// rows): d_pat becomes that table and d_plen[s] of a pattern slice packs
+// its entries per row (low 8 bits, <= 255 by detection) with its table row
+// (bits 8-30).  A wave's pattern load then hits a small hot table instead of
+// one cold row per slice, and the slice metadata shrinks by kmax*4 B each.
+int dedup_patterns(pa_mat* A, const std::vector<int32_t>& kind) {
+  const int64_t ns = A->nslices, K = A->kmax;
+  hipStream_t st = A->ctx->s_main;
+  std::vector<int32_t> pat(ns * K);
+  HIPC(hipMemcpyAsync(pat.data(), A->d_pat, ns * K * 4, hipMemcpyDeviceToHost, st));
+  HIPC(hipStreamSynchronize(st));
+  std::vector<int32_t> table, packed(A->h_plen);
+  std::unordered_map<std::string, int32_t> ids;
+  for (int64_t s = 0; s < ns; ++s) {
+    if (kind[s] != 1) continue;
+    const int32_t len = A->h_plen[s];
+    CHECK_ARG(len >= 1 && len <= 255, "pattern slice with more than 255 entries per row");
+    std::string key(reinterpret_cast<const char*>(&pat[s * K]), (size_t)len * 4);
+    if (!g_pattern_dedup) key.append(reinterpret_cast<const char*>(&s), 8);  // A/B: one row per slice
+    auto it = ids.find(key);
+    int32_t id;
+    if (it == ids.end()) {
+      id = (int32_t)ids.size();
+      CHECK_ARG(id < (1 << 23), "more than 2^23 distinct slice patterns");
+      ids.emplace(std::move(key), id);
+      table.insert(table.end(), pat.begin() + s * K, pat.begin() + (s + 1) * K);
+    } else {
+      id = it->second;
+    }
+    packed[s] = len | (id << 8);
+  }
+  A->npatterns = (int64_t)ids.size();
+  dev_free(A->d_pat);
+  A->d_pat = nullptr;
+  if (table.empty()) table.assign(K, 0);
+  if (dev_upload(&A->d_pat, table)) return -1;
+  HIPC(hipMemcpyAsync(A->d_plen, packed.data(), ns * 4, hipMemcpyHostToDevice, st));
+  HIPC(hipStreamSynchronize(st));
+  return 0;
+}
+
 // Pattern slices + side SELL from the int32 layout (device detection, host
 // bookkeeping).  noids: owned columns (x lids >= noids are ghosts).
 int finalize_pattern(pa_mat* A, int kmax, int64_t noids) {
@@ -328,6 +372,7 @@ int finalize_pattern(pa_mat* A, int kmax, int64_t noids) {
   HIPC(hipStreamSynchronize(st));
   dev_free(d_pghost);
   dev_free(d_nirreg);
+  if (dedup_patterns(A, kind)) return -1;
   if (g_spmv_delta16) {  // int32-column slices whose columns fit 16-bit codes (kind 3)
     int32_t* d_ok = nullptr;
     HIPC(hipMalloc((void**)&A->d_col16, std::max<int64_t>(A->slots, 1) * 2));
@@ -848,6 +893,8 @@ const Knob kKnobs[] = {
     {"spmv_group", &g_spmv_group, nullptr, 0, 1, 0,
      "spmv_group: 1 = one launch per phase for parts sharing a stream pair, 0 = per part"},
     {"spmv_format", &g_spmv_format, nullptr, 0, 1, 0, "spmv_format: 0 = int32 columns, 1 = pattern slices"},
+    {"pattern_dedup", &g_pattern_dedup, nullptr, 0, 1, 0,
+     "pattern_dedup (A/B): 1 = pattern slices index a table of the distinct patterns, 0 = one row per slice"},
 };
 constexpr int kNumKnobs = (int)(sizeof(kKnobs) / sizeof(kKnobs[0]));
 static_assert(kNumKnobs <= pa_ctx::kMaxKnobs, "pa_ctx::over too small");
@@ -2370,7 +2417,7 @@ int pa_mat_traffic(const pa_mat* A, int64_t* value_bytes, int64_t* index_bytes, 
     const int kd = pat ? A->h_kind[s] : 0;
     if (kd == 1) {
       v += (int64_t)A->h_plen[s] * H * S;
-      m += (int64_t)A->kmax * 4 + W * 8 + 8 + 4 + 4;  // pattern, mask, offset, length, list entry
+      m += W * 8 + 8 + 4 + 4;  // mask, offset, length | pattern id, list entry
     } else if (kd == 3) {
       v += (int64_t)A->h_slen[s] * H * S;
       ix += (int64_t)A->h_slen[s] * H * 2;
@@ -2382,6 +2429,7 @@ int pa_mat_traffic(const pa_mat* A, int64_t* value_bytes, int64_t* index_bytes, 
     }
   }
   if (pat) {
+    m += A->npatterns * A->kmax * 4;  // the distinct patterns (read once; hot thereafter)
     v += A->s_slots * S;
     ix += A->s_slots * 4 + A->s_nrows * 4;  // column ids, row map
     m += A->s_nslices * 12;

@@ -470,8 +470,9 @@ struct pa_mat {
   bool has_pat = false;
   int kmax = 0;                      // pattern stride per slice
   int32_t* d_kind = nullptr;         // per slice: 1 pattern, 0 int32 columns
-  int32_t* d_plen = nullptr;         // per slice: entries per row (pattern len or int32 len)
-  int32_t* d_pat = nullptr;          // nslices*kmax offsets
+  int32_t* d_plen = nullptr;         // per slice: entries per row (int32 len; pattern slices: len | pattern id << 8)
+  int32_t* d_pat = nullptr;          // npatterns*kmax offsets: the distinct patterns (dedup_patterns)
+  int64_t npatterns = 0;
   uint64_t* d_mask = nullptr;        // nslices*(H/64) regular-row bits
   int32_t* d_pint_list = nullptr;    // pattern mode: pattern slices without ghost reads
   int32_t* d_pbnd_list = nullptr;    // pattern mode: pattern slices reading ghosts

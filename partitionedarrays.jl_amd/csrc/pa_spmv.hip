@@ -543,7 +543,8 @@ __device__ __forceinline__ void spmv_wave(const SpmvArgs<T>& a, const int64_t w)
     xs.x = (const T*)a.x;
   }
   const int64_t off = a.soff[s];
-  const int len = a.slen[s];
+  const int32_t lraw = a.slen[s];
+  const int len = PAT ? (lraw & 0xff) : lraw;  // pattern slices: len | pattern id << 8 (dedup_patterns)
   bool ok[R];
   if (PAT) {
     const uint64_t m = a.mask[s * (H / 64) + (lane * R) / 64];
@@ -578,7 +579,7 @@ __device__ __forceinline__ void spmv_wave(const SpmvArgs<T>& a, const int64_t w)
   const bool tb = (a.flags & SPMV_TAILB) != 0;
   const bool pf = (a.flags & SPMV_PRODA) != 0;
   if constexpr (PK == 1) {
-    const int32_t* pat = a.pat + s * a.kmax;
+    const int32_t* pat = a.pat + (int64_t)(lraw >> 8) * a.kmax;
     if (a.flags & SPMV_XPAIR) {
       if (a.flags & SPMV_NT) rows_pattern<T, R, ALPHA, true, U, true, SH>(acc, pat, vp, len, xs, row0, ok, a.alpha, pf, tb);
       else rows_pattern<T, R, ALPHA, false, U, true, SH>(acc, pat, vp, len, xs, row0, ok, a.alpha, pf, tb);
@@ -1726,8 +1727,9 @@ __global__ __launch_bounds__(256) void k_pattern_detect(int64_t nrows, int64_t n
       }
     }
   }
-  // a pattern slice when at least half its rows follow the pattern
-  const bool best = Lp > 0 && 2 * tot1 >= nvalid;
+  // a pattern slice when at least half its rows follow the pattern (and
+  // its rows have at most 255 entries: the length is packed in 8 bits)
+  const bool best = Lp > 0 && Lp <= 255 && 2 * tot1 >= nvalid;
   const bool gr = __any(g1);
   const bool ga = __any(ghost_any);
   if (lane == 0) {
