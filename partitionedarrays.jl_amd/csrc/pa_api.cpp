@@ -59,7 +59,6 @@ int g_spmv_merge = 1;     // pa_tune("spmv_merge"): one launch for every slice k
 // F32 −2.8 %; C2 (16 k slices) and C5 stay merged (−10 % / −15 %).
 // profiles/r02/open/ab_merge.jsonl.  0: no limit.
 int64_t g_spmv_merge_max = 65536;
-int g_pattern_dedup = 1;  // pa_tune("pattern_dedup") (A/B, build time): distinct-pattern table
 int g_halo_direct = 1;     // pa_tune("halo_direct"): grouped mul! pulls ghosts straight from the owners' x
 int g_halo_transport = 0;  // pa_tune("halo_transport"): 0 parts of this process by device reads, 1 RCCL for all
 // pa_tune("cg_fuse"): the device CG's u update inside the SpMV (XV kernels)
@@ -307,6 +306,8 @@ int finish_sell_layout(pa_mat* A, const std::vector<int32_t>& slen, const std::v
 // its entries per row (low 8 bits, <= 255 by detection) with its table row
 // (bits 8-30).  A wave's pattern load then hits a small hot table instead of
 // one cold row per slice, and the slice metadata shrinks by kmax*4 B each.
+// A/B (one row per slice vs the table, profiles/r04/g/ab_pattern_dedup.jsonl):
+// FE27 256³ 0.6539 -> 0.6407 ms, FD7 128³ 0.02865 -> 0.02833 ms.
 int dedup_patterns(pa_mat* A, const std::vector<int32_t>& kind) {
   const int64_t ns = A->nslices, K = A->kmax;
   hipStream_t st = A->ctx->s_main;
@@ -320,7 +321,6 @@ int dedup_patterns(pa_mat* A, const std::vector<int32_t>& kind) {
     const int32_t len = A->h_plen[s];
     CHECK_ARG(len >= 1 && len <= 255, "pattern slice with more than 255 entries per row");
     std::string key(reinterpret_cast<const char*>(&pat[s * K]), (size_t)len * 4);
-    if (!g_pattern_dedup) key.append(reinterpret_cast<const char*>(&s), 8);  // A/B: one row per slice
     auto it = ids.find(key);
     int32_t id;
     if (it == ids.end()) {
@@ -893,8 +893,6 @@ const Knob kKnobs[] = {
     {"spmv_group", &g_spmv_group, nullptr, 0, 1, 0,
      "spmv_group: 1 = one launch per phase for parts sharing a stream pair, 0 = per part"},
     {"spmv_format", &g_spmv_format, nullptr, 0, 1, 0, "spmv_format: 0 = int32 columns, 1 = pattern slices"},
-    {"pattern_dedup", &g_pattern_dedup, nullptr, 0, 1, 0,
-     "pattern_dedup (A/B): 1 = pattern slices index a table of the distinct patterns, 0 = one row per slice"},
 };
 constexpr int kNumKnobs = (int)(sizeof(kKnobs) / sizeof(kKnobs[0]));
 static_assert(kNumKnobs <= pa_ctx::kMaxKnobs, "pa_ctx::over too small");

@@ -25,8 +25,9 @@ def child(a):
     sys.path.insert(0, ROOT)
     import pamd
     be = pamd.HIPBackend(devices=[0])
-    parts = be.get_part_ids((1, 1, 1))
-    N = (a.n,) * 3
+    shape = tuple(int(v) for v in a.shape.split(","))
+    parts = be.get_part_ids(shape)
+    N = tuple(a.n * s for s in shape)
     partition = pamd.drivers.stencil_partition(parts, N, 27)
     ctx = be.context(1)
     As = [pamd.drivers.stencil_operator(parts, N, 27, np.float64, partition=partition) for _ in range(a.k)]
@@ -42,8 +43,20 @@ def child(a):
                 pamd.mul_(y, As[i], xs[j])
                 sched.append([i, j])
     ctx.sync()
+    # and without the profiler's serialisation: HIP-event time per pairing
+    ms = {}
+    for i in range(a.k):
+        for j in range(a.k):
+            pamd.mul_(y, As[i], xs[j])
+            ctx.sync()
+            ctx.span_start()
+            for _ in range(a.reps):
+                pamd.mul_(y, As[i], xs[j])
+            ctx.span_stop()
+            ms[f"A{i}x{j}"] = round(ctx.span_ms() / a.reps, 4)
     ptrs = [{k: hex(v) for k, v in Ai.values.local(1).device_ptrs().items()} for Ai in As]
-    print(json.dumps({"tool": "placement_pmc", "k": a.k, "reps": a.reps, "schedule": sched, "mat_ptrs": ptrs,
+    print(json.dumps({"tool": "placement_pmc", "k": a.k, "reps": a.reps, "shape": shape, "event_ms": ms,
+                      "schedule": sched, "mat_ptrs": ptrs,
                       "x": [hex(x.values.parts[0].device_ptr()) for x in xs]}), flush=True)
 
 
@@ -61,6 +74,8 @@ def analyze(dirs):
     for d in dirs:
         log = [json.loads(l) for l in open(d + ".log") if l.startswith("{\"tool\": \"placement_pmc\"")]
         sched = log[0]["schedule"]
+        for key, v in log[0].get("event_ms", {}).items():
+            out.setdefault(key, {}).setdefault("event_ms", []).append(v)
         trace = [r for r in _csv(d, "kernel_trace.csv") if any(k in r["Kernel_Name"] for k in SPMV)]
         # one mul! = the dispatches of the SpMV kernels; group consecutive dispatches per call
         per_call = len(trace) // len(sched)
@@ -96,6 +111,7 @@ if __name__ == "__main__":
     ap.add_argument("--n", type=int, default=256)
     ap.add_argument("--k", type=int, default=2)
     ap.add_argument("--reps", type=int, default=6)
+    ap.add_argument("--shape", default="1,1,1", help="Cartesian parts of one GPU (n^3 nodes each)")
     ap.add_argument("--analyze", nargs="+")
     a = ap.parse_args()
     if a.analyze:
