@@ -15,6 +15,11 @@
 #include <numeric>
 #include <string>
 #include <unordered_map>
+#include <atomic>
+#include <condition_variable>
+#include <functional>
+#include <mutex>
+#include <thread>
 #include <vector>
 
 #include "pa_internal.h"
@@ -59,6 +64,7 @@ int g_spmv_merge = 1;     // pa_tune("spmv_merge"): one launch for every slice k
 // F32 −2.8 %; C2 (16 k slices) and C5 stay merged (−10 % / −15 %).
 // profiles/r02/open/ab_merge.jsonl.  0: no limit.
 int64_t g_spmv_merge_max = 65536;
+int g_issue_threads = 1;   // pa_tune("issue_threads"): parts with their own streams issued from host threads
 int g_halo_direct = 1;     // pa_tune("halo_direct"): grouped mul! pulls ghosts straight from the owners' x
 int g_halo_transport = 0;  // pa_tune("halo_transport"): 0 parts of this process by device reads, 1 RCCL for all
 // pa_tune("cg_fuse"): the device CG's u update inside the SpMV (XV kernels)
@@ -704,110 +710,160 @@ int rccl_group(std::vector<P2P>& ops) {
 // that combines (op) the values straight from the senders' buffers into
 // v[i] (*unpacked = true; the caller must not unpack again); otherwise
 // device-to-device copies into the receive buffer.
-int transport(int n, pa_xchg* const xg[], int dtype, int dir, int op, pa_vec* const v[], bool* unpacked) {
-  const size_t S = dtype_size(dtype);
-  LocalSet L = local_set(n, xg);
+// The transport of one call, planned once (pull tables, RCCL or not), then
+// issued per part: transport_part(i) is what part i's streams get (the
+// waits for its senders' packs, the pull or the staging copies, ev_recvd),
+// so the parts can be issued from several host threads (IssuePool).
+struct TransportPlan {
+  LocalSet L;
   bool remote = false;
-  *unpacked = false;
-  bool pull = v != nullptr && g_halo_pull;
-  for (int i = 0; i < n && pull; ++i) {
-    if (build_pull(i, n, xg, L, dtype, dir)) return -1;
-    pull = xg[i]->pull[dir].ok;
+  bool pull = false;
+  size_t S = 0;
+  int dtype = 0, dir = 0, op = 0;
+};
+
+int transport_plan(int n, pa_xchg* const xg[], int dtype, int dir, int op, pa_vec* const v[], TransportPlan* T) {
+  T->S = dtype_size(dtype);
+  T->dtype = dtype;
+  T->dir = dir;
+  T->op = op;
+  T->L = local_set(n, xg);
+  T->pull = v != nullptr && g_halo_pull;
+  for (int i = 0; i < n && T->pull; ++i) {
+    if (build_pull(i, n, xg, T->L, dtype, dir)) return -1;
+    T->pull = xg[i]->pull[dir].ok;
   }
+  T->remote = false;
   for (int i = 0; i < n; ++i) {
-    pa_xchg* X = xg[i];
-    pa_ctx* c = X->ctx;
-    HIPC(hipSetDevice(c->device));
-    EV(hipStreamWaitEvent(SC(c), c->ev_packed, 0));
+    const pa_xchg* X = xg[i];
+    for (const auto* lst : {&X->parts_rcv, &X->parts_snd})
+      for (int32_t q : *lst)
+        if (T->L.find(q) < 0) T->remote = true;
+  }
+  return 0;
+}
+
+// part i's s_comm waits for the packs of every sender it reads from (and its own)
+int transport_wait(int i, pa_xchg* const xg[], const TransportPlan& T) {
+  pa_xchg* X = xg[i];
+  pa_ctx* c = X->ctx;
+  HIPC(hipSetDevice(c->device));
+  EV(hipStreamWaitEvent(SC(c), c->ev_packed, 0));
+  const auto& prcv = T.dir == 0 ? X->parts_rcv : X->parts_snd;
+  for (int32_t q : prcv) {
+    const int j = T.L.find(q);
+    if (j >= 0 && xg[j]->ctx->ev_packed != c->ev_packed) EV(hipStreamWaitEvent(SC(c), xg[j]->ctx->ev_packed, 0));
+  }
+  return 0;
+}
+
+// part i's local segments (pull kernel or staging copies), then ev_recvd
+int transport_local(int i, pa_xchg* const xg[], pa_vec* const v[], const TransportPlan& T) {
+  pa_xchg* X = xg[i];
+  pa_ctx* c = X->ctx;
+  const int dir = T.dir;
+  const size_t S = T.S;
+  HIPC(hipSetDevice(c->device));
+  if (T.pull) {
+    const pa_pull& P = X->pull[dir];
+    const int32_t* bid = graph_owned<int32_t>(P.d_bid, P.h_bid);
+    const int64_t* elem = graph_owned<int64_t>(P.d_elem, P.h_elem);
+    void* const* bases = graph_owned<void*>(P.d_bases, P.h_bases);
+    CHECK_ARG(!(g_capture_tables && g_graph_owned_failed), "graph capture: table allocation failed");
+    if (dir == 0)
+      launch_pull(T.dtype, X->n_rcv_data, X->d_lids_rcv, X->plan_fwd, T.op, bid, elem, (const void* const*)bases,
+                  v[i]->d, SC(c));
+    else
+      launch_pull(T.dtype, X->n_snd_data, X->d_lids_snd, X->plan_rev, T.op, bid, elem, (const void* const*)bases,
+                  v[i]->d, SC(c));
+  } else {
+    // staging copies: receiver r, segment k from sender q (local), which
+    // holds the matching segment at the position of r in its send list
     const auto& prcv = dir == 0 ? X->parts_rcv : X->parts_snd;
-    for (int32_t q : prcv) {
-      const int j = L.find(q);
-      if (j >= 0) EV(hipStreamWaitEvent(SC(c), xg[j]->ctx->ev_packed, 0));
-      else remote = true;
+    const auto& orcv = dir == 0 ? X->ptrs_rcv : X->ptrs_snd;
+    char* brcv = (char*)(dir == 0 ? X->d_buf_rcv : X->d_buf_snd);
+    for (size_t k = 0; k < prcv.size(); ++k) {
+      const int j = T.L.find(prcv[k]);
+      if (j < 0) continue;
+      pa_xchg* Q = xg[j];
+      const auto& qsnd = dir == 0 ? Q->parts_snd : Q->parts_rcv;
+      const auto& qo = dir == 0 ? Q->ptrs_snd : Q->ptrs_rcv;
+      const char* bq = (const char*)(dir == 0 ? Q->d_buf_snd : Q->d_buf_rcv);
+      int m = -1;
+      for (size_t t = 0; t < qsnd.size(); ++t)
+        if (qsnd[t] == c->part) { m = (int)t; break; }
+      CHECK_ARG(m >= 0, "exchanger mismatch: a receiver lists a sender that does not send to it");
+      const int64_t cnt = orcv[k + 1] - orcv[k];
+      CHECK_ARG(cnt == qo[m + 1] - qo[m], "exchanger mismatch: segment lengths differ (SequentialBackend.jl:187)");
+      if (cnt > 0)
+        HIPC(hipMemcpyAsync(brcv + orcv[k] * S, bq + qo[m] * S, (size_t)cnt * S, hipMemcpyDefault, SC(c)));
     }
-    const auto& psnd = dir == 0 ? X->parts_snd : X->parts_rcv;
-    for (int32_t q : psnd)
-      if (L.find(q) < 0) remote = true;
   }
-  if (remote) {
-    for (int i = 0; i < n; ++i)
-      CHECK_ARG(xg[i]->ctx->comm, "halo neighbour is not held by this process and no RCCL communicator was initialised (pa_comm_init_rank)");
-    // every (sender part, receiver part) segment through one group
-    std::vector<P2P> ops;
-    for (int i = 0; i < n; ++i) {
-      pa_xchg* X = xg[i];
-      pa_ctx* c = X->ctx;
-      ncclComm_t comm = (ncclComm_t)c->comm;
-      const auto& psnd = dir == 0 ? X->parts_snd : X->parts_rcv;
-      const auto& osnd = dir == 0 ? X->ptrs_snd : X->ptrs_rcv;
-      char* bsnd = (char*)(dir == 0 ? X->d_buf_snd : X->d_buf_rcv);
-      const auto& prcv = dir == 0 ? X->parts_rcv : X->parts_snd;
-      const auto& orcv = dir == 0 ? X->ptrs_rcv : X->ptrs_snd;
-      char* brcv = (char*)(dir == 0 ? X->d_buf_rcv : X->d_buf_snd);
-      for (size_t k = 0; k < psnd.size(); ++k) {
-        const size_t cnt = (size_t)(osnd[k + 1] - osnd[k]) * S;
-        // an empty segment: the peer's matching one is empty too (SequentialBackend.jl:187)
-        if (L.find(psnd[k]) >= 0 || cnt == 0) continue;
-        ops.push_back({c->part, psnd[k], true, bsnd + osnd[k] * S, cnt, c->peer_rank(psnd[k]), comm, SC(c)});
-      }
-      for (size_t k = 0; k < prcv.size(); ++k) {
-        const size_t cnt = (size_t)(orcv[k + 1] - orcv[k]) * S;
-        if (L.find(prcv[k]) >= 0 || cnt == 0) continue;
-        ops.push_back({prcv[k], c->part, false, brcv + orcv[k] * S, cnt, c->peer_rank(prcv[k]), comm, SC(c)});
-      }
-    }
-    for (int i = 0; i < n; ++i) {
-      pa_ctx* c = xg[i]->ctx;
-      for (const P2P& o : ops) {
-        if (o.send && o.src == c->part) c->rccl_bytes_sent += (int64_t)o.cnt;
-        if (!o.send && o.dst == c->part) c->rccl_bytes_recv += (int64_t)o.cnt;
-      }
-    }
-    if (rccl_group(ops)) return -1;
-  }
+  EV(hipEventRecord(c->ev_recvd, SC(c)));
+  return 0;
+}
+
+// every (sender part, receiver part) segment with a part of another process
+// through one RCCL group
+int transport_remote(int n, pa_xchg* const xg[], const TransportPlan& T) {
+  const int dir = T.dir;
+  const size_t S = T.S;
+  for (int i = 0; i < n; ++i)
+    CHECK_ARG(xg[i]->ctx->comm, "halo neighbour is not held by this process and no RCCL communicator was initialised (pa_comm_init_rank)");
+  std::vector<P2P> ops;
   for (int i = 0; i < n; ++i) {
     pa_xchg* X = xg[i];
     pa_ctx* c = X->ctx;
-    HIPC(hipSetDevice(c->device));
-    if (pull) {
-      const pa_pull& P = X->pull[dir];
-      const int32_t* bid = graph_owned<int32_t>(P.d_bid, P.h_bid);
-      const int64_t* elem = graph_owned<int64_t>(P.d_elem, P.h_elem);
-      void* const* bases = graph_owned<void*>(P.d_bases, P.h_bases);
-      CHECK_ARG(!(g_capture_tables && g_graph_owned_failed), "graph capture: table allocation failed");
-      if (dir == 0)
-        launch_pull(dtype, X->n_rcv_data, X->d_lids_rcv, X->plan_fwd, op, bid, elem,
-                    (const void* const*)bases, v[i]->d, SC(c));
-      else
-        launch_pull(dtype, X->n_snd_data, X->d_lids_snd, X->plan_rev, op, bid, elem,
-                    (const void* const*)bases, v[i]->d, SC(c));
-    } else {
-      // staging copies: receiver r, segment k from sender q (local), which
-      // holds the matching segment at the position of r in its send list
-      const auto& prcv = dir == 0 ? X->parts_rcv : X->parts_snd;
-      const auto& orcv = dir == 0 ? X->ptrs_rcv : X->ptrs_snd;
-      char* brcv = (char*)(dir == 0 ? X->d_buf_rcv : X->d_buf_snd);
-      for (size_t k = 0; k < prcv.size(); ++k) {
-        const int j = L.find(prcv[k]);
-        if (j < 0) continue;
-        pa_xchg* Q = xg[j];
-        const auto& qsnd = dir == 0 ? Q->parts_snd : Q->parts_rcv;
-        const auto& qo = dir == 0 ? Q->ptrs_snd : Q->ptrs_rcv;
-        const char* bq = (const char*)(dir == 0 ? Q->d_buf_snd : Q->d_buf_rcv);
-        int m = -1;
-        for (size_t t = 0; t < qsnd.size(); ++t)
-          if (qsnd[t] == c->part) { m = (int)t; break; }
-        CHECK_ARG(m >= 0, "exchanger mismatch: a receiver lists a sender that does not send to it");
-        const int64_t cnt = orcv[k + 1] - orcv[k];
-        CHECK_ARG(cnt == qo[m + 1] - qo[m], "exchanger mismatch: segment lengths differ (SequentialBackend.jl:187)");
-        if (cnt > 0)
-          HIPC(hipMemcpyAsync(brcv + orcv[k] * S, bq + qo[m] * S, (size_t)cnt * S, hipMemcpyDefault, SC(c)));
-      }
+    ncclComm_t comm = (ncclComm_t)c->comm;
+    const auto& psnd = dir == 0 ? X->parts_snd : X->parts_rcv;
+    const auto& osnd = dir == 0 ? X->ptrs_snd : X->ptrs_rcv;
+    char* bsnd = (char*)(dir == 0 ? X->d_buf_snd : X->d_buf_rcv);
+    const auto& prcv = dir == 0 ? X->parts_rcv : X->parts_snd;
+    const auto& orcv = dir == 0 ? X->ptrs_rcv : X->ptrs_snd;
+    char* brcv = (char*)(dir == 0 ? X->d_buf_rcv : X->d_buf_snd);
+    for (size_t k = 0; k < psnd.size(); ++k) {
+      const size_t cnt = (size_t)(osnd[k + 1] - osnd[k]) * S;
+      // an empty segment: the peer's matching one is empty too (SequentialBackend.jl:187)
+      if (T.L.find(psnd[k]) >= 0 || cnt == 0) continue;
+      ops.push_back({c->part, psnd[k], true, bsnd + osnd[k] * S, cnt, c->peer_rank(psnd[k]), comm, SC(c)});
     }
-    EV(hipEventRecord(c->ev_recvd, SC(c)));
+    for (size_t k = 0; k < prcv.size(); ++k) {
+      const size_t cnt = (size_t)(orcv[k + 1] - orcv[k]) * S;
+      if (T.L.find(prcv[k]) >= 0 || cnt == 0) continue;
+      ops.push_back({prcv[k], c->part, false, brcv + orcv[k] * S, cnt, c->peer_rank(prcv[k]), comm, SC(c)});
+    }
   }
+  for (int i = 0; i < n; ++i) {
+    pa_ctx* c = xg[i]->ctx;
+    for (const P2P& o : ops) {
+      if (o.send && o.src == c->part) c->rccl_bytes_sent += (int64_t)o.cnt;
+      if (!o.send && o.dst == c->part) c->rccl_bytes_recv += (int64_t)o.cnt;
+    }
+  }
+  return rccl_group(ops);
+}
+
+// Halo transport for n local parts.  dir 0 (forward): send A-layout buffers
+// (ptrs_snd) to parts_snd, receive B-layout (ptrs_rcv) from parts_rcv;
+// dir 1 (reverse): the opposite.  Each part's s_comm first waits for the
+// packs of every sender it reads from (ev_packed), then ev_recvd is recorded
+// on it.  Senders in other processes: RCCL into the receive buffer.
+// Senders in this process: when every part's pull table is usable and the
+// target vectors v are given, s_comm runs one pull-unpack kernel per part
+// that combines (op) the values straight from the senders' buffers into
+// v[i] (*unpacked = true; the caller must not unpack again); otherwise
+// device-to-device copies into the receive buffer.
+int transport(int n, pa_xchg* const xg[], int dtype, int dir, int op, pa_vec* const v[], bool* unpacked) {
+  TransportPlan T;
+  *unpacked = false;
+  if (transport_plan(n, xg, dtype, dir, op, v, &T)) return -1;
+  for (int i = 0; i < n; ++i)
+    if (transport_wait(i, xg, T)) return -1;
+  if (T.remote && transport_remote(n, xg, T)) return -1;
+  for (int i = 0; i < n; ++i)
+    if (transport_local(i, xg, v, T)) return -1;
   HIPC(hipGetLastError());
-  *unpacked = pull;
+  *unpacked = T.pull;
   return 0;
 }
 
@@ -821,21 +877,108 @@ int check_lids(const pa_xchg* X, const pa_vec* v) {
 // copies; for RCCL sends the part's own ev_recvd covers them).
 bool g_capturing = false;  // inside pa_spmv_graph_create: one replay never overlaps the next
 
+// before part i packs into its send buffer: the previous exchange's reads
+// of it (its own unpack and its receivers' pulls) are done
+int pre_pack_wait_part(int i, pa_xchg* const xg[], const LocalSet& L) {
+  if (g_capturing) return 0;
+  pa_ctx* c = xg[i]->ctx;
+  HIPC(hipSetDevice(c->device));
+  HIPC(hipStreamWaitEvent(c->s_main, c->ev_recvd, 0));
+  std::vector<hipEvent_t> seen{c->ev_recvd};
+  for (const auto* lst : {&xg[i]->parts_snd, &xg[i]->parts_rcv})
+    for (int32_t q : *lst) {
+      const int j = L.find(q);
+      if (j < 0 || j == i) continue;
+      const hipEvent_t e = xg[j]->ctx->ev_recvd;
+      if (std::find(seen.begin(), seen.end(), e) != seen.end()) continue;  // parts_snd and parts_rcv overlap
+      seen.push_back(e);
+      HIPC(hipStreamWaitEvent(c->s_main, e, 0));
+    }
+  return 0;
+}
+
 int pre_pack_wait(int n, pa_xchg* const xg[]) {
   if (g_capturing) return 0;
   LocalSet L = local_set(n, xg);
-  for (int i = 0; i < n; ++i) {
-    pa_ctx* c = xg[i]->ctx;
-    HIPC(hipSetDevice(c->device));
-    HIPC(hipStreamWaitEvent(c->s_main, c->ev_recvd, 0));
-    for (const auto* lst : {&xg[i]->parts_snd, &xg[i]->parts_rcv})
-      for (int32_t q : *lst) {
-        const int j = L.find(q);
-        if (j >= 0 && j != i) HIPC(hipStreamWaitEvent(c->s_main, xg[j]->ctx->ev_recvd, 0));
-      }
-  }
+  for (int i = 0; i < n; ++i)
+    if (pre_pack_wait_part(i, xg, L)) return -1;
   return 0;
 }
+
+// Host threads that issue the per-part work of one call in parallel (parts
+// with their own stream pairs, typically one per GPU: one thread driving 8
+// GPUs issues them one after the other, SURVEY.md §8(b)'s model).  run(n, f)
+// calls f(i) for i in [0, n) on the pool and the caller, returns the first
+// failure (its error text is carried over to the caller's thread).  Workers
+// spin briefly between calls, then sleep.
+class IssuePool {
+ public:
+  static IssuePool& get() {
+    static IssuePool* p = new IssuePool();  // never destroyed: workers may outlive static destruction
+    return *p;
+  }
+  int run(int n, const std::function<int(int)>& f) {
+    std::lock_guard<std::mutex> call_lock(call_mu_);
+    ensure_workers(std::min(n - 1, kMaxWorkers));
+    f_ = &f;
+    n_ = n;
+    next_.store(0);
+    failed_.store(false);
+    err_.clear();
+    done_.store(0);
+    const int nw = (int)workers_.size();
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      gen_.fetch_add(1);
+    }
+    cv_.notify_all();
+    work();
+    while (done_.load(std::memory_order_acquire) < nw) std::this_thread::yield();
+    f_ = nullptr;
+    if (failed_.load()) {
+      pa::set_error(err_);
+      return -1;
+    }
+    return 0;
+  }
+
+ private:
+  static constexpr int kMaxWorkers = 15;
+  void work() {
+    for (int i = next_.fetch_add(1); i < n_; i = next_.fetch_add(1)) {
+      if ((*f_)(i) != 0 && !failed_.exchange(true)) {
+        std::lock_guard<std::mutex> g(mu_);
+        err_ = pa_last_error();
+      }
+    }
+  }
+  void ensure_workers(int k) {
+    while ((int)workers_.size() < k) {
+      workers_.emplace_back([this, seen = gen_.load()]() mutable {
+        for (;;) {
+          for (int spin = 0; gen_.load(std::memory_order_acquire) == seen; ++spin) {
+            if (spin < 20000) continue;  // ~tens of µs busy, then sleep
+            std::unique_lock<std::mutex> g(mu_);
+            cv_.wait(g, [&] { return gen_.load() != seen; });
+          }
+          seen = gen_.load();
+          work();
+          done_.fetch_add(1, std::memory_order_release);
+        }
+      });
+      workers_.back().detach();
+    }
+  }
+  std::mutex call_mu_, mu_;
+  std::condition_variable cv_;
+  std::atomic<uint64_t> gen_{0};
+  std::atomic<int> next_{0}, done_{0};
+  std::atomic<bool> failed_{false};
+  std::string err_;
+  const std::function<int(int)>* f_ = nullptr;
+  int n_ = 0;
+  std::vector<std::thread> workers_;
+};
 
 }  // namespace
 
@@ -893,6 +1036,9 @@ const Knob kKnobs[] = {
     {"spmv_group", &g_spmv_group, nullptr, 0, 1, 0,
      "spmv_group: 1 = one launch per phase for parts sharing a stream pair, 0 = per part"},
     {"spmv_format", &g_spmv_format, nullptr, 0, 1, 0, "spmv_format: 0 = int32 columns, 1 = pattern slices"},
+    {"issue_threads", &g_issue_threads, nullptr, 0, 1, 0,
+     "issue_threads: 1 = a call over parts with their own stream pairs is issued from host threads (default), "
+     "0 = from the calling thread, one part after the other"},
 };
 constexpr int kNumKnobs = (int)(sizeof(kKnobs) / sizeof(kKnobs[0]));
 static_assert(kNumKnobs <= pa_ctx::kMaxKnobs, "pa_ctx::over too small");
@@ -2828,17 +2974,14 @@ static int spmv_impl(int n, pa_mat* const A[], pa_vec* const y[], const pa_index
                         tslot, dt, gmode == 2, fz);
   }
 
-  if (any_x) {
-    if (pre_pack_wait(n, xg)) return -1;
-    for (int i = 0; i < n; ++i) {
-      pa_ctx* c = xg[i]->ctx;
-      HIPC(hipSetDevice(c->device));
-      launch_pack(dt, xg[i]->n_snd_data, xg[i]->d_lids_snd, x[i]->d, xg[i]->d_buf_snd, SM(c));
-      EV(hipEventRecord(c->ev_packed, SM(c)));
-    }
-    if (transport(n, xg, dt, 0, PA_REPLACE, x, &pulled)) return -1;
-  }
-  for (int i = 0; i < n; ++i) {
+  auto pack = [&](int i) -> int {
+    pa_ctx* c = xg[i]->ctx;
+    HIPC(hipSetDevice(c->device));
+    launch_pack(dt, xg[i]->n_snd_data, xg[i]->d_lids_snd, x[i]->d, xg[i]->d_buf_snd, SM(c));
+    EV(hipEventRecord(c->ev_packed, SM(c)));
+    return 0;
+  };
+  auto interior = [&](int i) -> int {
     pa_ctx* c = A[i]->ctx;
     HIPC(hipSetDevice(c->device));
     const int32_t* ymap = y_idx[i]->own_contig ? nullptr : y_idx[i]->d_oid_to_lid;
@@ -2846,9 +2989,9 @@ static int spmv_impl(int n, pa_mat* const A[], pa_vec* const y[], const pa_index
     // interior slices (no ghost column): overlap with the halo transport
     if (launch_phase(0, A[i], x[i]->d, y[i]->d, ymap, has_alpha, bmode, alpha, beta, dotp[i], SM(c), fz, i)) return -1;
     if (tslot[i]) HIPC(hipEventRecord(tslot[i][1], SM(c)));
-  }
-  HIPC(hipGetLastError());
-  for (int i = 0; i < n; ++i) {
+    return 0;
+  };
+  auto boundary = [&](int i) -> int {
     pa_ctx* c = A[i]->ctx;
     HIPC(hipSetDevice(c->device));
     if (any_x) {
@@ -2875,6 +3018,48 @@ static int spmv_impl(int n, pa_mat* const A[], pa_vec* const y[], const pa_index
         launch_fold(cplx, nbp, A[i]->d_dotp, c->d_fold, c->d_result, c->d_ticket, SM(c));
     }
     if (tslot[i]) HIPC(hipEventRecord(tslot[i][3], SM(c)));
+    return 0;
+  };
+  // several parts, each with its own stream pair (one per GPU when one
+  // process drives several GPUs): the parts are issued from the IssuePool's
+  // host threads in two rounds — pre-pack waits + packs (every part's
+  // ev_packed recorded before any receiver waits on it), then per part its
+  // transport (waits, pull), interior and boundary phases; the RCCL
+  // transport (parts in other processes) stays on this thread
+  bool threads = g_issue_threads && n >= 2 && !g_capture_stream;
+  for (int i = 0; threads && i < n; ++i)
+    for (int j = 0; j < i; ++j)
+      if (A[i]->ctx->s_main == A[j]->ctx->s_main || A[i]->ctx->s_comm == A[j]->ctx->s_comm) threads = false;
+  TransportPlan T;
+  if (any_x && transport_plan(n, xg, dt, 0, PA_REPLACE, x, &T)) return -1;
+  if (threads && !(any_x && T.remote)) {
+    if (any_x) {
+      const LocalSet L = local_set(n, xg);
+      if (IssuePool::get().run(n, [&](int i) -> int { return pre_pack_wait_part(i, xg, L) || pack(i); })) return -1;
+    }
+    pulled = any_x && T.pull;
+    if (IssuePool::get().run(n, [&](int i) -> int {
+          if (any_x && (transport_wait(i, xg, T) || transport_local(i, xg, x, T))) return -1;
+          return interior(i) || boundary(i);
+        }))
+      return -1;
+  } else {
+    if (any_x) {
+      if (pre_pack_wait(n, xg)) return -1;
+      for (int i = 0; i < n; ++i)
+        if (pack(i)) return -1;
+      for (int i = 0; i < n; ++i)
+        if (transport_wait(i, xg, T)) return -1;
+      if (T.remote && transport_remote(n, xg, T)) return -1;
+      for (int i = 0; i < n; ++i)
+        if (transport_local(i, xg, x, T)) return -1;
+      pulled = T.pull;
+    }
+    for (int i = 0; i < n; ++i)
+      if (interior(i)) return -1;
+    HIPC(hipGetLastError());
+    for (int i = 0; i < n; ++i)
+      if (boundary(i)) return -1;
   }
   HIPC(hipGetLastError());
   for (int i = 0; i < n; ++i)

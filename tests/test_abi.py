@@ -62,7 +62,8 @@ def test_tune_knobs_round_trip_and_reject_bad_values(pamd):
     refuses out-of-range values with a PAError; spmv_flags keeps bit 8 (the
     per-matrix CSR flag) out of the user's reach."""
     knobs = {"spmv_merge": 0, "spmv_merge_max": 1024, "spmv_group": 0, "spmv_delta16": 0,
-             "long_rows_exact": 0, "halo_direct": 0, "cg_fuse": 1, "halo_pull": 0, "spmv_format": 0}
+             "long_rows_exact": 0, "halo_direct": 0, "cg_fuse": 1, "halo_pull": 0, "spmv_format": 0,
+             "issue_threads": 0}
     for k, v in knobs.items():
         prev = pamd._lib.tune(k, v)
         assert pamd._lib.tune(k, prev) == v, k

@@ -350,3 +350,50 @@ def test_spmv_flag_variants_bitexact(be, pamd, O, dtype, flags):
                 assert _eq(O, got.local(p)[own], _sel(O, oy.values[p], own)), (alpha, p)
     finally:
         pamd._lib.tune("spmv_flags", prev)
+
+
+def test_threaded_issue_matches_sequential(pamd, O):
+    """Parts with their own stream pairs are issued from host threads
+    (pa_tune issue_threads=1, the default): mul! with α/β, the fused mul!+dot
+    of the device CG and back-to-back calls on alternating x give the same
+    bits as issue_threads=0 (one part after the other) and as the oracle."""
+    shape, N = (2, 2, 2), (14, 11, 9)
+    rng = np.random.default_rng(SEED + 9)
+    vals = [rng.uniform(-1, 1, 3000) for _ in range(2)]
+    out = {}
+    for threads in (0, 1):
+        prev = pamd._lib.tune("issue_threads", threads)
+        try:
+            be = pamd.HIPBackend(devices=[0], share_streams=False)
+            parts = be.get_part_ids(shape)
+            A = pamd.drivers.stencil_operator(parts, N, 27)
+            xs = [pamd.PVector.from_host(pamd.map_parts(lambda s, v=v: v[:s.num_lids].copy(), A.cols.partition),
+                                         A.cols) for v in vals]
+            y = pamd.PVector.undef(A.rows).fill_(0.5)
+            res = []
+            for it in range(12):
+                pamd.mul_(y, A, xs[it % 2], 1.0 if it % 3 else -2.0, 0.0 if it % 4 else 0.75)
+                if it % 4 == 3:
+                    res.append([v.copy() for v in y.to_host().parts])
+            res.append([v.copy() for v in y.to_host().parts])
+            xc = pamd.PVector.undef(A.cols).fill_(0)
+            h = []
+            pamd.cg_(xc, A, xs[0], reltol=0.0, maxiter=12, history=h, device=True)
+            out[threads] = (res, [v.copy() for v in xc.to_host().parts], h)
+            if threads == 1:
+                y0 = pamd.PVector.undef(A.rows)
+                pamd.mul_(y0, A, xs[0])
+                OA = O.stencil_problem(O.get_part_ids(shape), N, 27)
+                ox = O.PVector(O.map_parts(lambda s: vals[0][:s.num_lids].copy(), OA.cols.partition), OA.cols)
+                oy = O.pvector_undef(OA.rows, np.float64)
+                O.mul_(oy, OA, ox)
+                for p in parts.part_ids:
+                    assert np.array_equal(y0.to_host().local(p), oy.values[p]), p
+        finally:
+            pamd._lib.tune("issue_threads", prev)
+    for r0, r1 in zip(out[0][0], out[1][0]):
+        for a, b in zip(r0, r1):
+            assert np.array_equal(a, b)
+    for a, b in zip(out[0][1], out[1][1]):
+        assert np.array_equal(a, b)
+    assert out[0][2] == out[1][2]

@@ -29,6 +29,8 @@ ap.add_argument("--own-streams", action="store_true", help="a stream pair per pa
 ap.add_argument("--group", type=int, default=1, help="pa_tune spmv_group: 1 grouped launches (default), 0 per part")
 ap.add_argument("--graph", action="store_true", help="also time the HIP-graph replay (pamd.SpMVGraph)")
 ap.add_argument("--rccl", action="store_true", help="halo over RCCL grouped send/recv (HIPBackend(rccl=True))")
+ap.add_argument("--probe", action="store_true",
+                help="also report pa_hbm_probe's read rate over the same bytes per launch as one mul!")
 ap.add_argument("--tune", default="", help="extra pa_tune knobs, key=value[,key=value]")
 a = ap.parse_args()
 for kv in filter(None, a.tune.split(",")):
@@ -105,6 +107,7 @@ for name in a.dtypes.split(","):
             own = A.rows.partition.local(p).oid_to_lid - 1
             assert np.array_equal(got.local(p)[own], ref.local(p)[own]), "graph replay differs from eager mul!"
         del g
+    probe = pamd._lib.hbm_probe(0, int(info["format_bytes"]), 20)[0] if a.probe else None
     print(json.dumps({"config": f"C5 FE27 {a.n}^3 Voronoi {a.parts} parts on 1 GPU", "dtype": name, "halo": "rccl" if a.rccl else "device reads", "tune": a.tune,
                       "share_streams": not a.own_streams,
                       "spmv_group": a.group, "format_gbs_all_parts": round(info["format_bytes"] / t / 1e9, 1),
@@ -112,4 +115,6 @@ for name in a.dtypes.split(","):
                       "ms_per_mul": round(1e3 * t, 4),
                       "ms_per_mul_graph": None if t_graph is None else round(1e3 * t_graph, 4), "gbs_algorithmic_all_parts": round(B / t / 1e9, 1),
                       "kernel_ms_sum_over_parts": round(km, 4), "gbs_algorithmic_kernels": round(B / km / 1e6, 1),
+                      "probe_read_gbs_same_bytes": None if probe is None else round(probe, 1),
+                      "kernels_of_probe": None if probe is None else round(info["format_bytes"] / km / 1e6 / probe, 4),
                       "setup_s": round(setup, 2), "format": info}), flush=True)

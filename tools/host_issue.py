@@ -6,6 +6,8 @@ on cuda:0:
   * share_streams=False: a stream pair per part and per-part launches, pack,
     transport (pull kernels on the comm streams, cross-stream events),
     interior and boundary phases — the code a process driving 8 GPUs runs;
+    issued from the IssuePool's host threads (default) and, for comparison,
+    with issue_threads=0 from the calling thread;
   * share_streams=True: the grouped launches of parts sharing one GPU;
   * rccl: HIPBackend(rccl=True), every halo segment through the grouped
     ncclSend/ncclRecv, the transport a one-part-per-GPU process posts.
@@ -90,7 +92,12 @@ def main():
     args = ap.parse_args()
     res = []
     res.append(measure(pamd.HIPBackend(devices=[0], share_streams=False), args.n, args.k,
-                       "share_streams=False (per-part streams, events and launches)", cg_iters=200))
+                       "share_streams=False (per-part streams, events and launches, issued from host threads)",
+                       cg_iters=200))
+    prev = pamd._lib.tune("issue_threads", 0)
+    res.append(measure(pamd.HIPBackend(devices=[0], share_streams=False), args.n, args.k,
+                       "share_streams=False, issue_threads=0 (one part after the other on the calling thread)"))
+    pamd._lib.tune("issue_threads", prev)
     res.append(measure(pamd.HIPBackend(devices=[0], share_streams=True), args.n, args.k,
                        "share_streams=True (grouped launches)", cg_iters=200))
     res.append(measure(pamd.HIPBackend(devices=[0], rccl=True), args.n, args.k,
