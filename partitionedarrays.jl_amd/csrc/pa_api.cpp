@@ -917,24 +917,32 @@ class IssuePool {
     static IssuePool* p = new IssuePool();  // never destroyed: workers may outlive static destruction
     return *p;
   }
+  // The call returns once its n items are done and no worker is inside it;
+  // a worker joins a call by reading the job under the lock, so the caller
+  // never waits for workers that are asleep, and a late one joins whichever
+  // call is current (or none).
   int run(int n, const std::function<int(int)>& f) {
     std::lock_guard<std::mutex> call_lock(call_mu_);
     ensure_workers(std::min(n - 1, kMaxWorkers));
-    f_ = &f;
-    n_ = n;
-    next_.store(0);
-    failed_.store(false);
-    err_.clear();
-    done_.store(0);
-    const int nw = (int)workers_.size();
     {
       std::lock_guard<std::mutex> g(mu_);
+      f_ = &f;
+      n_ = n;
+      next_.store(0);
+      finished_.store(0);
+      failed_.store(false);
+      err_.clear();
       gen_.fetch_add(1);
     }
     cv_.notify_all();
-    work();
-    while (done_.load(std::memory_order_acquire) < nw) std::this_thread::yield();
-    f_ = nullptr;
+    work(&f, n);
+    while (finished_.load(std::memory_order_acquire) < n) std::this_thread::yield();
+    {  // no worker joins after this; those that joined find no item left
+      std::lock_guard<std::mutex> g(mu_);
+      f_ = nullptr;
+      n_ = 0;
+    }
+    while (busy_.load(std::memory_order_acquire) > 0) std::this_thread::yield();
     if (failed_.load()) {
       pa::set_error(err_);
       return -1;
@@ -944,26 +952,37 @@ class IssuePool {
 
  private:
   static constexpr int kMaxWorkers = 15;
-  void work() {
-    for (int i = next_.fetch_add(1); i < n_; i = next_.fetch_add(1)) {
-      if ((*f_)(i) != 0 && !failed_.exchange(true)) {
+  void work(const std::function<int(int)>* f, int n) {
+    for (int i = next_.fetch_add(1); i < n; i = next_.fetch_add(1)) {
+      if ((*f)(i) != 0 && !failed_.exchange(true)) {
         std::lock_guard<std::mutex> g(mu_);
         err_ = pa_last_error();
       }
+      finished_.fetch_add(1, std::memory_order_release);
     }
   }
   void ensure_workers(int k) {
     while ((int)workers_.size() < k) {
-      workers_.emplace_back([this, seen = gen_.load()]() mutable {
+      workers_.emplace_back([this]() {
+        uint64_t seen = 0;
         for (;;) {
           for (int spin = 0; gen_.load(std::memory_order_acquire) == seen; ++spin) {
             if (spin < 20000) continue;  // ~tens of µs busy, then sleep
             std::unique_lock<std::mutex> g(mu_);
             cv_.wait(g, [&] { return gen_.load() != seen; });
           }
-          seen = gen_.load();
-          work();
-          done_.fetch_add(1, std::memory_order_release);
+          const std::function<int(int)>* f;
+          int n;
+          {
+            std::lock_guard<std::mutex> g(mu_);
+            seen = gen_.load();
+            f = f_;
+            n = n_;
+            if (f) busy_.fetch_add(1);
+          }
+          if (!f) continue;  // woke after the call ended: wait for the next
+          work(f, n);
+          busy_.fetch_sub(1, std::memory_order_release);
         }
       });
       workers_.back().detach();
@@ -972,10 +991,10 @@ class IssuePool {
   std::mutex call_mu_, mu_;
   std::condition_variable cv_;
   std::atomic<uint64_t> gen_{0};
-  std::atomic<int> next_{0}, done_{0};
+  std::atomic<int> next_{0}, finished_{0}, busy_{0};
   std::atomic<bool> failed_{false};
   std::string err_;
-  const std::function<int(int)>* f_ = nullptr;
+  const std::function<int(int)>* f_ = nullptr;  // the current call's job (under mu_)
   int n_ = 0;
   std::vector<std::thread> workers_;
 };
@@ -3022,10 +3041,11 @@ static int spmv_impl(int n, pa_mat* const A[], pa_vec* const y[], const pa_index
   };
   // several parts, each with its own stream pair (one per GPU when one
   // process drives several GPUs): the parts are issued from the IssuePool's
-  // host threads in two rounds — pre-pack waits + packs (every part's
-  // ev_packed recorded before any receiver waits on it), then per part its
-  // transport (waits, pull), interior and boundary phases; the RCCL
-  // transport (parts in other processes) stays on this thread
+  // host threads in three rounds — pre-pack waits + packs (every part's
+  // ev_packed recorded before any receiver waits on it), per part its
+  // transport (waits, pull) and interior phase, then the boundary phases;
+  // with an RCCL transport (parts in other processes) the call stays on
+  // this thread
   bool threads = g_issue_threads && n >= 2 && !g_capture_stream;
   for (int i = 0; threads && i < n; ++i)
     for (int j = 0; j < i; ++j)
@@ -3040,9 +3060,13 @@ static int spmv_impl(int n, pa_mat* const A[], pa_vec* const y[], const pa_index
     pulled = any_x && T.pull;
     if (IssuePool::get().run(n, [&](int i) -> int {
           if (any_x && (transport_wait(i, xg, T) || transport_local(i, xg, x, T))) return -1;
-          return interior(i) || boundary(i);
+          return interior(i);
         }))
       return -1;
+    // every interior enqueued before any boundary's wait for its halo: with
+    // several parts' streams sharing a hardware queue (one GPU), a wait
+    // enqueued early would hold back the other parts' interiors behind it
+    if (IssuePool::get().run(n, boundary)) return -1;
   } else {
     if (any_x) {
       if (pre_pack_wait(n, xg)) return -1;

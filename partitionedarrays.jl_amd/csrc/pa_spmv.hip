@@ -223,15 +223,78 @@ __device__ __forceinline__ T term(T v, T x, T alpha, bool pf) {
   return v * (x * alpha);
 }
 
+// Column ids one batch ahead (IPF in rows_int32 / rows_d16) for Float64:
+// same-copy A/B (profiles/r04/i/): C5 F64 0.1240 -> 0.1217 ms (-1.9 %), FE27
+// 256^3 F64 +-0; Float32 (R = 4, 134 -> 155 VGPRs) C5 0.0832 -> 0.0852 ms
+// (+2.4 %): off.
+template <typename T> constexpr bool kIdsAhead = std::is_same<T, double>::value;
+
 // int32-column rows: c < 0 is padding (skipped: never multiplied)
 // TB: the entries past the last full U batch run as one masked batch
 // (entries >= len re-read entry len-1 and are never accumulated)
-template <typename T, int R, bool ALPHA, bool NT, int U, bool SH = false, typename XS>
+template <typename T, int R, bool ALPHA, bool NT, int U, bool SH = false, bool IPF = false, typename XS>
 __device__ __forceinline__ void rows_int32(T (&acc)[R], const IPack<R>* __restrict__ cp,
                                            const Pack<T, R>* __restrict__ vp, int len,
                                            const XS& x, T alpha, bool pf, bool TB) {
   int k = 0;
   if (SH) TB = true;  // short rows (len <= U): the one masked batch is the whole row
+  if constexpr (IPF && !SH) {
+    // column ids one batch ahead: batch k+1's ids load while batch k's
+    // gathers are in flight, so a batch waits for one load latency (the
+    // gather), not two (ids, then gather)
+    if (U <= len) {
+      IPack<R> cn[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) cn[u] = ld<NT>(&cp[u * 64]);
+      for (; k + U <= len; k += U) {
+        IPack<R> c[U];
+        Pack<T, R> v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) c[u] = cn[u];
+#pragma unroll
+        for (int u = 0; u < U; ++u) v[u] = ld<NT>(&vp[(k + u) * 64]);
+        T xv[U][R];
+#pragma unroll
+        for (int u = 0; u < U; ++u) gather_x<T, R>(xv[u], c[u].c, x);
+        const int kn = k + U;
+        if (kn + U <= len) {
+#pragma unroll
+          for (int u = 0; u < U; ++u) cn[u] = ld<NT>(&cp[(kn + u) * 64]);
+        } else if (TB && kn < len) {
+#pragma unroll
+          for (int u = 0; u < U; ++u) {
+            if (kn + u < len) cn[u] = ld<NT>(&cp[(kn + u) * 64]);
+            else for (int r = 0; r < R; ++r) cn[u].c[r] = -1;
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+          for (int r = 0; r < R; ++r) {
+            const T t = acc[r] + term<ALPHA>(v[u].v[r], xv[u][r], alpha, pf);
+            acc[r] = pick(c[u].c[r] >= 0, t, acc[r]);
+          }
+      }
+      if (TB && k < len) {  // the masked tail batch, its ids already loaded
+        Pack<T, R> v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+          if (k + u < len) v[u] = ld<NT>(&vp[(k + u) * 64]);
+        T xv[U][R];
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+          if (k + u < len) gather_x<T, R>(xv[u], cn[u].c, x);
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+          for (int r = 0; r < R; ++r) {
+            const T t = acc[r] + term<ALPHA>(v[u].v[r], xv[u][r], alpha, pf);
+            acc[r] = pick(k + u < len && cn[u].c[r] >= 0, t, acc[r]);
+          }
+        k = len;
+      }
+    }
+  }
   for (; !SH && k + U <= len; k += U) {
     IPack<R> c[U];
     Pack<T, R> v[U];
@@ -295,12 +358,73 @@ __device__ __forceinline__ int32_t d16_col(uint32_t q, int32_t row, int32_t gb) 
 }
 
 // delta16 rows: rows_int32 with the column ids decoded from 2 B codes
-template <typename T, int R, bool ALPHA, bool NT, int U, bool SH = false, typename XS>
+template <typename T, int R, bool ALPHA, bool NT, int U, bool SH = false, bool IPF = false, typename XS>
 __device__ __forceinline__ void rows_d16(T (&acc)[R], const S16Pack<R>* __restrict__ cp,
                                          const Pack<T, R>* __restrict__ vp, int len,
                                          const XS& x, T alpha, bool pf, bool TB, int32_t row0, int32_t gb) {
   int k = 0;
   if (SH) TB = true;
+  if constexpr (IPF && !SH) {  // codes one batch ahead, as in rows_int32
+    if (U <= len) {
+      S16Pack<R> qn[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) qn[u] = ld<NT>(&cp[u * 64]);
+      for (; k + U <= len; k += U) {
+        int32_t c[U][R];
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+          for (int r = 0; r < R; ++r) c[u][r] = d16_col(qn[u].c[r], row0 + r, gb);
+        Pack<T, R> v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) v[u] = ld<NT>(&vp[(k + u) * 64]);
+        T xv[U][R];
+#pragma unroll
+        for (int u = 0; u < U; ++u) gather_x<T, R>(xv[u], c[u], x);
+        const int kn = k + U;
+        if (kn + U <= len) {
+#pragma unroll
+          for (int u = 0; u < U; ++u) qn[u] = ld<NT>(&cp[(kn + u) * 64]);
+        } else if (TB && kn < len) {
+#pragma unroll
+          for (int u = 0; u < U; ++u) {
+            if (kn + u < len) qn[u] = ld<NT>(&cp[(kn + u) * 64]);
+            else for (int r = 0; r < R; ++r) qn[u].c[r] = 0xFFFFu;
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+          for (int r = 0; r < R; ++r) {
+            const T t = acc[r] + term<ALPHA>(v[u].v[r], xv[u][r], alpha, pf);
+            acc[r] = pick(c[u][r] >= 0, t, acc[r]);
+          }
+      }
+      if (TB && k < len) {  // the masked tail batch, its codes already loaded
+        int32_t c[U][R];
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+          for (int r = 0; r < R; ++r) c[u][r] = d16_col(qn[u].c[r], row0 + r, gb);
+        Pack<T, R> v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+          if (k + u < len) v[u] = ld<NT>(&vp[(k + u) * 64]);
+        T xv[U][R];
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+          if (k + u < len) gather_x<T, R>(xv[u], c[u], x);
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+          for (int r = 0; r < R; ++r) {
+            const T t = acc[r] + term<ALPHA>(v[u].v[r], xv[u][r], alpha, pf);
+            acc[r] = pick(k + u < len && c[u][r] >= 0, t, acc[r]);
+          }
+        k = len;
+      }
+    }
+  }
   for (; !SH && k + U <= len; k += U) {
     S16Pack<R> q[U];
     Pack<T, R> v[U];
@@ -590,12 +714,12 @@ __device__ __forceinline__ void spmv_wave(const SpmvArgs<T>& a, const int64_t w)
   } else if constexpr (PK == 3) {
     const S16Pack<R>* __restrict__ cp = reinterpret_cast<const S16Pack<R>*>(a.col16 + off) + lane;
     const int32_t gb = a.gbase[s];
-    if (a.flags & SPMV_NT) rows_d16<T, R, ALPHA, true, U, SH>(acc, cp, vp, len, xs, a.alpha, pf, tb, (int32_t)row0, gb);
-    else rows_d16<T, R, ALPHA, false, U, SH>(acc, cp, vp, len, xs, a.alpha, pf, tb, (int32_t)row0, gb);
+    if (a.flags & SPMV_NT) rows_d16<T, R, ALPHA, true, U, SH, kIdsAhead<T>>(acc, cp, vp, len, xs, a.alpha, pf, tb, (int32_t)row0, gb);
+    else rows_d16<T, R, ALPHA, false, U, SH, kIdsAhead<T>>(acc, cp, vp, len, xs, a.alpha, pf, tb, (int32_t)row0, gb);
   } else {
     const IPack<R>* __restrict__ cp = reinterpret_cast<const IPack<R>*>(a.col + off) + lane;
-    if (a.flags & SPMV_NT) rows_int32<T, R, ALPHA, true, U, SH>(acc, cp, vp, len, xs, a.alpha, pf, tb);
-    else rows_int32<T, R, ALPHA, false, U, SH>(acc, cp, vp, len, xs, a.alpha, pf, tb);
+    if (a.flags & SPMV_NT) rows_int32<T, R, ALPHA, true, U, SH, kIdsAhead<T>>(acc, cp, vp, len, xs, a.alpha, pf, tb);
+    else rows_int32<T, R, ALPHA, false, U, SH, kIdsAhead<T>>(acc, cp, vp, len, xs, a.alpha, pf, tb);
   }
 
   // XV: u_new (and the deferred x update) of the main structure's rows

@@ -323,11 +323,12 @@ def test_beta_zero_overwrites_nan_inf(be, pamd, O, fmt, alpha):
 
 
 @pytest.mark.parametrize("dtype", [np.float64, np.float32, np.complex128, np.complex64])
-@pytest.mark.parametrize("flags", [1 | 8 | 16 | 32 | 64, 4 | 16, 1 | 4 | 8])
+@pytest.mark.parametrize("flags", [1 | 8 | 16 | 32 | 64, 4 | 16, 1 | 4 | 8, 1 | 4 | 16 | 64])
 def test_spmv_flag_variants_bitexact(be, pamd, O, dtype, flags):
     """spmv_flags variants (pattern rows' 16 B x runs off, non-temporal y
-    stores on, tail batch / short-row kernels off): the same terms in the
-    same order, so bit-exact against the oracle, alpha != 1 included."""
+    stores on, tail batch / short-row kernels off, the tail batch off under
+    Float64's ids-ahead loop): the same terms in the same order, so
+    bit-exact against the oracle, alpha != 1 included."""
     prev = pamd._lib.tune("spmv_flags", flags)
     try:
         shape, N = (2, 1, 2), (13, 9, 10)
