@@ -71,6 +71,7 @@ for step in "$@"; do
     *)
       echo "unknown step $name"; exit 2 ;;
   esac
+  case $name in kt|ktpy|pmc|pmcpy) python3 tools/prune_prof.py "$OUT/kt$i" "$OUT/pmc$i" ;; esac
   echo "   rc $rc, $(( $(date +%s) - t0 )) s" | tee -a "$OUT/steps.log"
   [ $rc -ne 0 ] && exit $rc
 done
