@@ -88,9 +88,10 @@ int pa_device_count(int* count);
  *               otherwise the sweep or the matrix's earlier choice;
  * "spmv_group"  1: the parts of one process sharing a stream pair run each
  *               mul! phase as one launch (default), 0: launches per part;
- * "issue_threads" 1: a mul! over several parts with their own stream pairs
- *               (e.g. one per GPU) is issued from host threads, one part per
- *               thread (default), 0: from the calling thread in turn. */
+ * "issue_threads" a mul! over several parts with their own stream pairs is
+ *               issued from host threads, one part per thread: 1 when the
+ *               parts span several devices (default), 2 always, 0 never
+ *               (the calling thread, one part after the other). */
 int pa_tune(const char* key, int value, int* previous);
 /* The same knobs for one context: calls led by parts of `c` (their first
  * part's context) run with this value instead of the process default, for

@@ -64,7 +64,7 @@ int g_spmv_merge = 1;     // pa_tune("spmv_merge"): one launch for every slice k
 // F32 −2.8 %; C2 (16 k slices) and C5 stay merged (−10 % / −15 %).
 // profiles/r02/open/ab_merge.jsonl.  0: no limit.
 int64_t g_spmv_merge_max = 65536;
-int g_issue_threads = 1;   // pa_tune("issue_threads"): parts with their own streams issued from host threads
+int g_issue_threads = 1;   // pa_tune("issue_threads"): 1 auto (several devices), 2 always, 0 never
 int g_halo_direct = 1;     // pa_tune("halo_direct"): grouped mul! pulls ghosts straight from the owners' x
 int g_halo_transport = 0;  // pa_tune("halo_transport"): 0 parts of this process by device reads, 1 RCCL for all
 // pa_tune("cg_fuse"): the device CG's u update inside the SpMV (XV kernels)
@@ -351,6 +351,31 @@ int dedup_patterns(pa_mat* A, const std::vector<int32_t>& kind) {
 
 // Pattern slices + side SELL from the int32 layout (device detection, host
 // bookkeeping).  noids: owned columns (x lids >= noids are ghosts).
+// The CSC nz → slot map (pa_mat_from_csc / _coo) after k_delta16 moved the
+// delta16 slices' values to the interleaved layout: a slot of such a slice
+// at (k, lane, r) held row w = lane*R + r, which now sits at (k, w % 64,
+// w / 64).  The map moves to the host here (as load_nz_map does).
+int remap_nz_interleaved(pa_mat* A, const std::vector<int32_t>& kind, hipStream_t st) {
+  HIPC(hipStreamSynchronize(st));
+  if (A->d_nz_slot) {
+    A->h_nz_slot.resize(A->csc_nnz);
+    HIPC(hipMemcpy(A->h_nz_slot.data(), A->d_nz_slot, A->csc_nnz * 8, hipMemcpyDeviceToHost));
+    dev_free(A->d_nz_slot);
+    A->d_nz_slot = nullptr;
+  }
+  const int64_t ns = A->nslices, R = A->R, H = A->H;
+  std::vector<int64_t> soff(ns);
+  HIPC(hipMemcpy(soff.data(), A->d_slice_off, ns * 8, hipMemcpyDeviceToHost));
+  for (int64_t& slot : A->h_nz_slot) {
+    if (slot < 0) continue;
+    const int64_t s = (int64_t)(std::upper_bound(soff.begin(), soff.end(), slot) - soff.begin()) - 1;
+    if (kind[s] != 3) continue;
+    const int64_t t = slot - soff[s], k = t / H, w = t % H;  // w = lane*R + r before the move
+    slot = soff[s] + (k * 64 + w % 64) * R + w / 64;
+  }
+  return 0;
+}
+
 int finalize_pattern(pa_mat* A, int kmax, int64_t noids) {
   A->kmax = std::max(kmax, 1);
   const int64_t ns = A->nslices;
@@ -398,6 +423,12 @@ int finalize_pattern(pa_mat* A, int kmax, int64_t noids) {
       dev_free(A->d_gbase);
       A->d_col16 = nullptr;
       A->d_gbase = nullptr;
+    } else {
+      // Float32 delta16 slices' rows are interleaved now (k_delta16): the
+      // int32 kernel of spmv_format 0 reads the layout per slice from d_kind
+      // (3), and the CSC nz → slot map follows the moved values
+      HIPC(hipMemcpyAsync(A->d_kind, kind.data(), ns * 4, hipMemcpyHostToDevice, st));
+      if (A->nz_map && A->R == 4 && remap_nz_interleaved(A, kind, st)) return -1;
     }
   }
   std::vector<int32_t> pint, pbnd, xint, xbnd, dint, dbnd, side;
@@ -1055,9 +1086,10 @@ const Knob kKnobs[] = {
     {"spmv_group", &g_spmv_group, nullptr, 0, 1, 0,
      "spmv_group: 1 = one launch per phase for parts sharing a stream pair, 0 = per part"},
     {"spmv_format", &g_spmv_format, nullptr, 0, 1, 0, "spmv_format: 0 = int32 columns, 1 = pattern slices"},
-    {"issue_threads", &g_issue_threads, nullptr, 0, 1, 0,
-     "issue_threads: 1 = a call over parts with their own stream pairs is issued from host threads (default), "
-     "0 = from the calling thread, one part after the other"},
+    {"issue_threads", &g_issue_threads, nullptr, 0, 2, 0,
+     "issue_threads: a call over parts with their own stream pairs is issued from host threads, one part "
+     "per thread: 1 = when the parts span several devices (default), 2 = always, 0 = never (the calling "
+     "thread, one part after the other)"},
 };
 constexpr int kNumKnobs = (int)(sizeof(kKnobs) / sizeof(kKnobs[0]));
 static_assert(kNumKnobs <= pa_ctx::kMaxKnobs, "pa_ctx::over too small");
@@ -3046,10 +3078,18 @@ static int spmv_impl(int n, pa_mat* const A[], pa_vec* const y[], const pa_index
   // transport (waits, pull) and interior phase, then the boundary phases;
   // with an RCCL transport (parts in other processes) the call stays on
   // this thread
+  // issue_threads 1 (auto): only when the parts span several devices; on
+  // one device the parts' streams share its hardware queues and the serial
+  // order keeps the device time lower (1.44 vs 1.70 ms for 8 parts of the
+  // 256³ (2,2,2) problem, profiles/r04/k/host_issue_3round.json); 2: always
   bool threads = g_issue_threads && n >= 2 && !g_capture_stream;
-  for (int i = 0; threads && i < n; ++i)
+  bool multi_dev = false;
+  for (int i = 0; threads && i < n; ++i) {
+    multi_dev = multi_dev || A[i]->ctx->device != A[0]->ctx->device;
     for (int j = 0; j < i; ++j)
       if (A[i]->ctx->s_main == A[j]->ctx->s_main || A[i]->ctx->s_comm == A[j]->ctx->s_comm) threads = false;
+  }
+  if (g_issue_threads == 1 && !multi_dev) threads = false;
   TransportPlan T;
   if (any_x && transport_plan(n, xg, dt, 0, PA_REPLACE, x, &T)) return -1;
   if (threads && !(any_x && T.remote)) {

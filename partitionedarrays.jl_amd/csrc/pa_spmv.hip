@@ -132,6 +132,9 @@ struct SpmvArgs {
   // delta16 slices: 16-bit column codes and the per-slice ghost base
   const PA_GLB uint16_t* col16;
   const PA_GLB int32_t* gbase;
+  // int32-column launches over delta16 slices (spmv_format 0): the slices'
+  // kinds; kind 3 = interleaved rows (null: every slice blocked)
+  const PA_GLB int32_t* ilv;
   // the device CG's fused u update (XV kernels, pa_cg_solve_all): x is r,
   // the gathered values are u_new = r .+ β.*u_old (β = res²/prev² of cg);
   // waves of the main structure write u_new of their rows to un and apply
@@ -357,7 +360,13 @@ __device__ __forceinline__ int32_t d16_col(uint32_t q, int32_t row, int32_t gb) 
   return (q & 0x8000u) ? gb + (int32_t)(q & 0x7FFFu) : row + (((int32_t)(q << 17)) >> 17);
 }
 
-// delta16 rows: rows_int32 with the column ids decoded from 2 B codes
+// delta16 rows: rows_int32 with the column ids decoded from 2 B codes.
+// Float32 (R = 4) delta16 slices have interleaved rows (k_delta16): row0 =
+// the slice's first row + lane, the lane's rows row0 + r*64.  Same-box A/B
+// (profiles/r04/l/): C5 F32 0.0855 -> 0.0757 ms (-11.5 %), F64 (R = 2)
+// 0.1191 -> 0.1232 (+3.4 %), so the other types keep blocked rows.
+template <int R> constexpr bool kInterleaveD16 = R == 4;
+template <int R> constexpr int kD16RowStride = kInterleaveD16<R> ? 64 : 1;
 template <typename T, int R, bool ALPHA, bool NT, int U, bool SH = false, bool IPF = false, typename XS>
 __device__ __forceinline__ void rows_d16(T (&acc)[R], const S16Pack<R>* __restrict__ cp,
                                          const Pack<T, R>* __restrict__ vp, int len,
@@ -374,7 +383,7 @@ __device__ __forceinline__ void rows_d16(T (&acc)[R], const S16Pack<R>* __restri
 #pragma unroll
         for (int u = 0; u < U; ++u)
 #pragma unroll
-          for (int r = 0; r < R; ++r) c[u][r] = d16_col(qn[u].c[r], row0 + r, gb);
+          for (int r = 0; r < R; ++r) c[u][r] = d16_col(qn[u].c[r], row0 + r * kD16RowStride<R>, gb);
         Pack<T, R> v[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) v[u] = ld<NT>(&vp[(k + u) * 64]);
@@ -405,7 +414,7 @@ __device__ __forceinline__ void rows_d16(T (&acc)[R], const S16Pack<R>* __restri
 #pragma unroll
         for (int u = 0; u < U; ++u)
 #pragma unroll
-          for (int r = 0; r < R; ++r) c[u][r] = d16_col(qn[u].c[r], row0 + r, gb);
+          for (int r = 0; r < R; ++r) c[u][r] = d16_col(qn[u].c[r], row0 + r * kD16RowStride<R>, gb);
         Pack<T, R> v[U];
 #pragma unroll
         for (int u = 0; u < U; ++u)
@@ -437,7 +446,7 @@ __device__ __forceinline__ void rows_d16(T (&acc)[R], const S16Pack<R>* __restri
 #pragma unroll
     for (int u = 0; u < U; ++u) {
 #pragma unroll
-      for (int r = 0; r < R; ++r) c[u][r] = d16_col(q[u].c[r], row0 + r, gb);
+      for (int r = 0; r < R; ++r) c[u][r] = d16_col(q[u].c[r], row0 + r * kD16RowStride<R>, gb);
       gather_x<T, R>(xv[u], c[u], x);
     }
 #pragma unroll
@@ -464,7 +473,7 @@ __device__ __forceinline__ void rows_d16(T (&acc)[R], const S16Pack<R>* __restri
 #pragma unroll
     for (int u = 0; u < U; ++u) {
 #pragma unroll
-      for (int r = 0; r < R; ++r) c[u][r] = d16_col(q[u].c[r], row0 + r, gb);
+      for (int r = 0; r < R; ++r) c[u][r] = d16_col(q[u].c[r], row0 + r * kD16RowStride<R>, gb);
       if (k + u < len) gather_x<T, R>(xv[u], c[u], x);
     }
 #pragma unroll
@@ -481,7 +490,7 @@ __device__ __forceinline__ void rows_d16(T (&acc)[R], const S16Pack<R>* __restri
     const Pack<T, R> v = ld<NT>(&vp[k * 64]);
 #pragma unroll
     for (int r = 0; r < R; ++r) {
-      const int32_t cc = d16_col(q.c[r], row0 + r, gb);
+      const int32_t cc = d16_col(q.c[r], row0 + r * kD16RowStride<R>, gb);
       const T t = acc[r] + term<ALPHA>(v.v[r], x.get(cc >= 0 ? cc : 0), alpha, pf);
       acc[r] = pick(cc >= 0, t, acc[r]);
     }
@@ -582,17 +591,17 @@ template <typename W> __device__ inline W cg_alpha_of(const CGState* st);
 template <> __device__ inline double cg_alpha_of<double>(const CGState* st) { return st->alpha.re; }
 template <> __device__ inline c128 cg_alpha_of<c128>(const CGState* st) { return st->alpha; }
 
-// The fused CG update of one lane's R rows i0..i0+R-1 (< nrows; owned lids
-// = oids, contiguous): x[i] .+= α.*u_old[i] when an x update is pending
+// The fused CG update of one lane's R rows i0 + k*rs (< nrows; owned lids
+// = oids, contiguous; rs = 1 blocked rows, 64 interleaved): x[i] .+= α.*u_old[i] when an x update is pending
 // (xpend), and with U: u_new[i] = r[i] .+ β.*u_old[i] stored to un and
 // returned in unv.  16 B accesses when all R rows exist.  The arithmetic of
 // k_cg_xu, element for element.
 template <typename T, int R, bool UPD, typename XS, typename W>
-__device__ __forceinline__ void cg_rows_update(const SpmvArgs<T>& a, const XS& xs, int64_t i0, W alpha,
+__device__ __forceinline__ void cg_rows_update(const SpmvArgs<T>& a, const XS& xs, int64_t i0, int rs, W alpha,
                                                bool xpend = true, T* unv = nullptr) {
   T* xacc = (T*)a.xacc;
   T* un = (T*)a.un;
-  if (i0 + R <= a.nrows) {
+  if (rs == 1 && i0 + R <= a.nrows) {
     const Pack<T, R> uo = *reinterpret_cast<const Pack<T, R>*>(xs.u + i0);
     if (UPD) {
       const Pack<T, R> rv = *reinterpret_cast<const Pack<T, R>*>(xs.r + i0);
@@ -613,7 +622,7 @@ __device__ __forceinline__ void cg_rows_update(const SpmvArgs<T>& a, const XS& x
   }
 #pragma unroll
   for (int k = 0; k < R; ++k) {
-    const int64_t i = i0 + k;
+    const int64_t i = i0 + (int64_t)k * rs;
     if (i >= a.nrows) {
       if (UPD) unv[k] = zero_of<T>();
       continue;
@@ -647,7 +656,13 @@ __device__ __forceinline__ void spmv_wave(const SpmvArgs<T>& a, const int64_t w)
   constexpr int H = 64 * R;
   const int lane = threadIdx.x & 63;
   const int64_t s = a.list ? (int64_t)a.list[w] : w;
-  const int64_t row0 = s * H + (int64_t)lane * R;  // the lane's first row
+  // the slice's row layout: blocked (the lane's rows lane*R + r) or, for
+  // delta16 slices, interleaved (rows r*64 + lane; k_delta16)
+  bool il = false;
+  if constexpr (PK == 3) il = kInterleaveD16<R>;
+  if constexpr (PK == 0 && kInterleaveD16<R>) il = a.ilv && a.ilv[s] == 3;
+  const int rs = il ? 64 : 1;
+  const int64_t row0 = s * H + (il ? (int64_t)lane : (int64_t)lane * R);  // the lane's first row
   XSrc<T, XV> xs;
   bool xpend = false, main_rows = false;
   typename wide_of<T>::type xalpha{};
@@ -660,7 +675,7 @@ __device__ __forceinline__ void spmv_wave(const SpmvArgs<T>& a, const int64_t w)
     xs.b = (cg->res * cg->res) / (cg->prev * cg->prev);
     main_rows = a.rowmap == nullptr;
     if (cg->done) {  // nothing left but a pending x .+= α.*u_old
-      if (xpend && main_rows) cg_rows_update<T, R, false>(a, xs, row0, xalpha);
+      if (xpend && main_rows) cg_rows_update<T, R, false>(a, xs, row0, rs, xalpha);
       return;
     }
   } else {
@@ -676,8 +691,8 @@ __device__ __forceinline__ void spmv_wave(const SpmvArgs<T>& a, const int64_t w)
     for (int r = 0; r < R; ++r) ok[r] = ((m >> ((lane * R + r) & 63)) & 1ull) && (row0 + r < a.nrows);
   } else {
 #pragma unroll
-    for (int r = 0; r < R; ++r) ok[r] = row0 + r < a.nrows;
-    if (a.sflags && a.sflags[s]) {  // rows handed to the long-row kernel
+    for (int r = 0; r < R; ++r) ok[r] = row0 + (int64_t)r * rs < a.nrows;
+    if (a.sflags && a.sflags[s]) {  // rows handed to the long-row kernel (blocked slices only)
       const uint64_t m = a.lmask[s * (H / 64) + (lane * R) / 64];
 #pragma unroll
       for (int r = 0; r < R; ++r) ok[r] = ok[r] && !((m >> ((lane * R + r) & 63)) & 1ull);
@@ -685,7 +700,10 @@ __device__ __forceinline__ void spmv_wave(const SpmvArgs<T>& a, const int64_t w)
   }
   int64_t orow[R];
 #pragma unroll
-  for (int r = 0; r < R; ++r) orow[r] = ok[r] ? (a.rowmap ? (int64_t)a.rowmap[row0 + r] : row0 + r) : 0;
+  for (int r = 0; r < R; ++r) {
+    const int64_t i = row0 + (int64_t)r * rs;
+    orow[r] = ok[r] ? (a.rowmap ? (int64_t)a.rowmap[i] : i) : 0;
+  }
 
   T acc[R];
 #pragma unroll
@@ -725,7 +743,7 @@ __device__ __forceinline__ void spmv_wave(const SpmvArgs<T>& a, const int64_t w)
   // XV: u_new (and the deferred x update) of the main structure's rows
   T un[R];
   if constexpr (XV) {
-    if (main_rows) cg_rows_update<T, R, true>(a, xs, row0, xalpha, xpend, un);
+    if (main_rows) cg_rows_update<T, R, true>(a, xs, row0, rs, xalpha, xpend, un);
   }
   if (a.dotp) {  // fused dot(u, c): Σ conj(u_i)·c_i over this slice's rows
     using DA = typename DAcc<T>::type;
@@ -745,7 +763,7 @@ __device__ __forceinline__ void spmv_wave(const SpmvArgs<T>& a, const int64_t w)
   bool all = true;
 #pragma unroll
   for (int r = 0; r < R; ++r) all = all && ok[r];
-  if (all && !a.ymap && !a.rowmap) {
+  if (all && !a.ymap && !a.rowmap && !il) {
     Pack<T, R> o;
 #pragma unroll
     for (int r = 0; r < R; ++r) o.v[r] = acc[r];
@@ -922,6 +940,8 @@ static SpmvArgs<T> make_args(int which, int64_t nwork, const int32_t* list, cons
   if (which == 1) {
     a.sflags = (decltype(a.sflags))(A->d_sflags);
     a.lmask = (decltype(a.lmask))(A->d_lmask);
+    // spmv_format 0 runs the delta16 slices (Float32: interleaved rows) as int32
+    if (A->d_col16 && A->R == 4 && !(g_spmv_format == 1 && A->has_pat)) a.ilv = (decltype(a.ilv))(A->d_kind);
   }
   return a;
 }
@@ -1875,13 +1895,20 @@ __global__ __launch_bounds__(256) void k_pattern_detect(int64_t nrows, int64_t n
 // delta16 eligibility and codes, one wave per slice: an int32-column slice
 // (kind 0, no long rows) becomes delta16 when every owned column is within
 // ±16383 of its row and every ghost column within 32766 of the slice's
-// smallest ghost column; its codes are then written to col16 (same slots).
+// smallest ghost column.  Float32 slices' rows are then re-laid out
+// interleaved (row w of the slice at lane w % 64, position w / 64, instead
+// of lane w / R, position w % R), values and int32 ids moved in place,
+// block k by block k; the codes go to col16 in the (new) slots: a gather
+// instruction then reads x for 64 consecutive rows (a coalesced span)
+// instead of 64 rows R apart.
 template <int R>
 __global__ __launch_bounds__(256) void k_delta16(int64_t nslices, const int64_t* __restrict__ soff,
-                                                 const int32_t* __restrict__ slen, const int32_t* __restrict__ col,
+                                                 const int32_t* __restrict__ slen, int32_t* __restrict__ col,
                                                  const int32_t* __restrict__ kind, const int32_t* __restrict__ sflags,
                                                  int64_t noids, uint16_t* __restrict__ col16,
-                                                 int32_t* __restrict__ gbase, int32_t* __restrict__ ok) {
+                                                 int32_t* __restrict__ gbase, int32_t* __restrict__ ok,
+                                                 unsigned char* __restrict__ val) {
+  typedef typename RawOf<16 / R>::type E;  // one value (R values = 16 B per lane)
   constexpr int H = 64 * R;
   const int64_t s = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (s >= nslices) return;
@@ -1917,17 +1944,35 @@ __global__ __launch_bounds__(256) void k_delta16(int64_t nslices, const int64_t*
   const bool all = __all(fit);
   if (lane == 0) { ok[s] = all ? 1 : 0; gbase[s] = gmin == INT32_MAX ? 0 : gmin; }
   if (!all) return;
-  for (int k = 0; k < len; ++k)
+  for (int k = 0; k < len; ++k) {
+    // block k (64*R slots) in registers first: every lane's loads of the
+    // block are issued before any lane stores into it
+    int32_t c[R];
+    E v[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) {
       const int64_t slot = off + ((int64_t)k * 64 + lane) * R + r;
-      const int32_t c = col[slot];
-      uint16_t q;
-      if (c < 0) q = 0xFFFFu;
-      else if (c < noids) q = (uint16_t)((uint32_t)(c - (int32_t)(row0 + r)) & 0x7FFFu);
-      else q = (uint16_t)(0x8000u | (uint32_t)(c - gmin));
-      col16[slot] = q;
+      c[r] = col[slot];
+      v[r] = reinterpret_cast<const E*>(val)[slot];
     }
+    __builtin_amdgcn_s_waitcnt(0);
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const int w = lane * R + r;  // the row within the slice
+      const int64_t slot = kInterleaveD16<R> ? off + ((int64_t)k * 64 + (w & 63)) * R + (w >> 6)
+                                             : off + ((int64_t)k * 64 + lane) * R + r;
+      uint16_t q;
+      if (c[r] < 0) q = 0xFFFFu;
+      else if (c[r] < noids) q = (uint16_t)((uint32_t)(c[r] - (int32_t)(row0 + r)) & 0x7FFFu);
+      else q = (uint16_t)(0x8000u | (uint32_t)(c[r] - gmin));
+      col16[slot] = q;
+      if (kInterleaveD16<R>) {
+        col[slot] = c[r];
+        reinterpret_cast<E*>(val)[slot] = v[r];
+      }
+    }
+  }
 }
 
 void launch_delta16(pa_mat* A, int64_t noids, const int32_t* kind, int32_t* ok, hipStream_t st) {
@@ -1935,7 +1980,8 @@ void launch_delta16(pa_mat* A, int64_t noids, const int32_t* kind, int32_t* ok, 
   if (blocks == 0) return;
 #define PA_D16(RR)                                                                                          \
   hipLaunchKernelGGL(k_delta16<RR>, dim3(blocks), dim3(256), 0, st, A->nslices, A->d_slice_off,              \
-                     A->d_slice_len, A->d_col, kind, A->d_sflags, noids, A->d_col16, A->d_gbase, ok)
+                     A->d_slice_len, A->d_col, kind, A->d_sflags, noids, A->d_col16, A->d_gbase, ok,  \
+                     (unsigned char*)A->d_val)
   switch (A->R) {
     case 1: PA_D16(1); break;
     case 2: PA_D16(2); break;

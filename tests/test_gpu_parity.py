@@ -354,15 +354,16 @@ def test_spmv_flag_variants_bitexact(be, pamd, O, dtype, flags):
 
 
 def test_threaded_issue_matches_sequential(pamd, O):
-    """Parts with their own stream pairs are issued from host threads
-    (pa_tune issue_threads=1, the default): mul! with α/β, the fused mul!+dot
-    of the device CG and back-to-back calls on alternating x give the same
-    bits as issue_threads=0 (one part after the other) and as the oracle."""
+    """Parts with their own stream pairs issued from host threads (pa_tune
+    issue_threads=2: always; the default 1 does so only across devices):
+    mul! with α/β, the fused mul!+dot of the device CG and back-to-back
+    calls on alternating x give the same bits as issue_threads=0 (one part
+    after the other) and as the oracle."""
     shape, N = (2, 2, 2), (14, 11, 9)
     rng = np.random.default_rng(SEED + 9)
     vals = [rng.uniform(-1, 1, 3000) for _ in range(2)]
     out = {}
-    for threads in (0, 1):
+    for threads in (0, 2):
         prev = pamd._lib.tune("issue_threads", threads)
         try:
             be = pamd.HIPBackend(devices=[0], share_streams=False)
@@ -381,7 +382,7 @@ def test_threaded_issue_matches_sequential(pamd, O):
             h = []
             pamd.cg_(xc, A, xs[0], reltol=0.0, maxiter=12, history=h, device=True)
             out[threads] = (res, [v.copy() for v in xc.to_host().parts], h)
-            if threads == 1:
+            if threads == 2:
                 y0 = pamd.PVector.undef(A.rows)
                 pamd.mul_(y0, A, xs[0])
                 OA = O.stencil_problem(O.get_part_ids(shape), N, 27)
@@ -392,9 +393,9 @@ def test_threaded_issue_matches_sequential(pamd, O):
                     assert np.array_equal(y0.to_host().local(p), oy.values[p]), p
         finally:
             pamd._lib.tune("issue_threads", prev)
-    for r0, r1 in zip(out[0][0], out[1][0]):
+    for r0, r1 in zip(out[0][0], out[2][0]):
         for a, b in zip(r0, r1):
             assert np.array_equal(a, b)
-    for a, b in zip(out[0][1], out[1][1]):
+    for a, b in zip(out[0][1], out[2][1]):
         assert np.array_equal(a, b)
-    assert out[0][2] == out[1][2]
+    assert out[0][2] == out[2][2]

@@ -92,9 +92,11 @@ def main():
     ap.add_argument("--k", type=int, default=40)
     args = ap.parse_args()
     res = []
+    prev = pamd._lib.tune("issue_threads", 2)  # the default (1) threads only across devices
     res.append(measure(pamd.HIPBackend(devices=[0], share_streams=False), args.n, args.k,
-                       "share_streams=False (per-part streams, events and launches, issued from host threads)",
-                       cg_iters=200))
+                       "share_streams=False, issue_threads=2 (per-part streams, events and launches, issued from "
+                       "host threads)", cg_iters=200))
+    pamd._lib.tune("issue_threads", prev)
     prev = pamd._lib.tune("issue_threads", 0)
     res.append(measure(pamd.HIPBackend(devices=[0], share_streams=False), args.n, args.k,
                        "share_streams=False, issue_threads=0 (one part after the other on the calling thread)",
