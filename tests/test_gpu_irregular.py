@@ -233,13 +233,14 @@ def test_launch_paths_equal_oracle(be, pamd, O, merge, direct, d16):
 
 
 
-@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+@pytest.mark.parametrize("dtype", [np.float64, np.float32, np.complex64, np.complex128])
 @pytest.mark.parametrize("d16", [1, 0])
 @pytest.mark.parametrize("tail", [8, 0])
 def test_voronoi_column_loops_equal_oracle(be, pamd, O, dtype, d16, tail):
     """The int32 / delta16 column loops (Float64: ids one batch ahead;
-    Float32: not), with and without the masked tail batch, α != 1: the
-    Voronoi parts' SpMV gives the oracle's bits for both column encodings."""
+    Float32: interleaved delta16 rows), with and without the masked tail
+    batch, α != 1: the Voronoi parts' SpMV gives the oracle's bits for both
+    column encodings and every element type."""
     N, nparts = (30, 28, 26), 8
     prev = {"spmv_delta16": pamd._lib.tune("spmv_delta16", d16),
             "spmv_flags": pamd._lib.tune("spmv_flags", 1 | 4 | 16 | 64 | tail)}
@@ -248,16 +249,17 @@ def test_voronoi_column_loops_equal_oracle(be, pamd, O, dtype, d16, tail):
         A = pamd.drivers.irregular_problem(parts, N, 27, dtype)
         OA = _oracle(O, N, nparts, dtype)
         rng = np.random.default_rng(SEED + 23)
-        xs = {p: rng.uniform(-1, 1, A.cols.partition.local(p).num_lids).astype(dtype) for p in parts.part_ids}
+        xs = {p: _rand(rng, A.cols.partition.local(p).num_lids, dtype) for p in parts.part_ids}
         x = pamd.PVector.from_host(pamd.map_parts(lambda s: xs[s.part], A.cols.partition), A.cols)
         y = pamd.PVector.undef(A.rows, dtype)
         pamd.mul_(y, A, x, 0.5, 0.0)
-        ox = O.PVector(O.map_parts(lambda s: xs[s.part].copy(), OA.cols.partition), OA.cols)
+        ox = O.PVector(O.map_parts(lambda s: _ox(O, xs[s.part]), OA.cols.partition), OA.cols)
         oy = O.pvector_undef(OA.rows, dtype)
-        O.mul_(oy, OA, ox, dtype(0.5), 0.0)
+        half = np.float32(0.5) if np.dtype(dtype) in (np.float32, np.complex64) else 0.5
+        O.mul_(oy, OA, ox, half, 0.0)
         got = y.to_host()
         for p in parts.part_ids:
-            assert np.array_equal(got.local(p), oy.values[p]), f"part {p}: SpMV differs"
+            assert _eq(O, got.local(p), oy.values[p]), f"part {p}: SpMV differs"
     finally:
         for k, v in prev.items():
             pamd._lib.tune(k, v)
