@@ -331,13 +331,19 @@ int dedup_patterns(pa_mat* A, const std::vector<int32_t>& kind) {
     int32_t id;
     if (it == ids.end()) {
       id = (int32_t)ids.size();
-      CHECK_ARG(id < (1 << 23), "more than 2^23 distinct slice patterns");
+      CHECK_ARG(id < (1 << 22), "more than 2^22 distinct slice patterns");
       ids.emplace(std::move(key), id);
       table.insert(table.end(), pat.begin() + s * K, pat.begin() + (s + 1) * K);
     } else {
       id = it->second;
     }
-    packed[s] = len | (id << 8);
+    // tri: the pattern is consecutive column triples (o, o+1, o+2) — every
+    // FE27 interior row — so a lane reads the three x runs of a triple with
+    // two 16 B loads (rows_pattern_tri)
+    bool tri = len % 3 == 0;
+    for (int32_t k = 0; tri && k < len; k += 3)
+      tri = pat[s * K + k + 1] == pat[s * K + k] + 1 && pat[s * K + k + 2] == pat[s * K + k] + 2;
+    packed[s] = len | ((tri ? 1 : 0) << 8) | (id << 9);
   }
   A->npatterns = (int64_t)ids.size();
   dev_free(A->d_pat);

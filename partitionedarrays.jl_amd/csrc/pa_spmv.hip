@@ -586,6 +586,65 @@ __device__ __forceinline__ void rows_pattern(T (&acc)[R], const int32_t* __restr
   }
 }
 
+// Pattern rows whose pattern is consecutive column triples (o, o+1, o+2),
+// tri bit of the slice's length word: the lane's R rows read the three x
+// runs x[rbase+o .. +R-1], x[rbase+o+1 .. +R], x[rbase+o+2 .. +R+1] as two
+// 16 B loads, A = x[rbase+o ..] and B = x[rbase+o+2 ..]: run 0 = A, run 2 =
+// B, run 1 = A[1..R-1] followed by B[R-2].  Three triples (9 entries) per
+// batch, then single triples; the terms and their order are those of
+// rows_pattern.  Library A/B on one box (profiles/r04/p/): FE27 256^3 one
+// part 0.6744 -> 0.6523 ms, the (2,2,2) halo leg 0.714 -> 0.688 ms, C5 F64
+// -1.0 %: one x load in three fewer relieves the per-CU memory pipeline.
+template <typename T, int R, bool ALPHA, bool NT, typename XS>
+__device__ __forceinline__ void rows_pattern_tri(T (&acc)[R], const int32_t* __restrict__ pat,
+                                                 const Pack<T, R>* __restrict__ vp, int len, const XS& x,
+                                                 int64_t rbase, const bool (&ok)[R], T alpha, bool pf) {
+  static_assert(R > 1, "runs of R > 1 values");
+  bool any = false;
+#pragma unroll
+  for (int r = 0; r < R; ++r) any = any || ok[r];
+  auto triple = [&](int32_t o, T (&xv)[3][R]) {
+    const Pack<T, R> A = x.template run<R>(any ? rbase + o : 0);
+    const Pack<T, R> B = x.template run<R>(any ? rbase + o + 2 : 0);
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      xv[0][r] = A.v[r];
+      xv[1][r] = r + 1 < R ? A.v[r + 1] : B.v[R - 2];
+      xv[2][r] = B.v[r];
+    }
+  };
+  int k = 0;
+  for (; k + 9 <= len; k += 9) {
+    int32_t o[3];
+#pragma unroll
+    for (int t = 0; t < 3; ++t) o[t] = pat[k + 3 * t];
+    Pack<T, R> v[9];
+#pragma unroll
+    for (int u = 0; u < 9; ++u) v[u] = ld<NT>(&vp[(k + u) * 64]);
+    T xv[3][3][R];
+#pragma unroll
+    for (int t = 0; t < 3; ++t) triple(o[t], xv[t]);
+#pragma unroll
+    for (int t = 0; t < 3; ++t)
+#pragma unroll
+      for (int j = 0; j < 3; ++j)
+#pragma unroll
+        for (int r = 0; r < R; ++r) acc[r] = acc[r] + term<ALPHA>(v[3 * t + j].v[r], xv[t][j][r], alpha, pf);
+  }
+  for (; k < len; k += 3) {
+    const int32_t o = pat[k];
+    Pack<T, R> v[3];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) v[j] = ld<NT>(&vp[(k + j) * 64]);
+    T xv[3][R];
+    triple(o, xv);
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+#pragma unroll
+      for (int r = 0; r < R; ++r) acc[r] = acc[r] + term<ALPHA>(v[j].v[r], xv[j][r], alpha, pf);
+  }
+}
+
 // α of the device CG state in the wide type W (Float64 / ComplexF64)
 template <typename W> __device__ inline W cg_alpha_of(const CGState* st);
 template <> __device__ inline double cg_alpha_of<double>(const CGState* st) { return st->alpha.re; }
@@ -683,7 +742,7 @@ __device__ __forceinline__ void spmv_wave(const SpmvArgs<T>& a, const int64_t w)
   }
   const int64_t off = a.soff[s];
   const int32_t lraw = a.slen[s];
-  const int len = PAT ? (lraw & 0xff) : lraw;  // pattern slices: len | pattern id << 8 (dedup_patterns)
+  const int len = PAT ? (lraw & 0xff) : lraw;  // pattern slices: len | tri << 8 | pattern id << 9 (dedup_patterns)
   bool ok[R];
   if (PAT) {
     const uint64_t m = a.mask[s * (H / 64) + (lane * R) / 64];
@@ -721,8 +780,17 @@ __device__ __forceinline__ void spmv_wave(const SpmvArgs<T>& a, const int64_t w)
   const bool tb = (a.flags & SPMV_TAILB) != 0;
   const bool pf = (a.flags & SPMV_PRODA) != 0;
   if constexpr (PK == 1) {
-    const int32_t* pat = a.pat + (int64_t)(lraw >> 8) * a.kmax;
-    if (a.flags & SPMV_XPAIR) {
+    const int32_t* pat = a.pat + (int64_t)(lraw >> 9) * a.kmax;
+    bool tri_done = false;
+    if constexpr (R > 1 && !SH) {
+      if ((lraw & 0x100) && (a.flags & SPMV_XPAIR)) {  // triples of consecutive columns
+        if (a.flags & SPMV_NT) rows_pattern_tri<T, R, ALPHA, true>(acc, pat, vp, len, xs, row0, ok, a.alpha, pf);
+        else rows_pattern_tri<T, R, ALPHA, false>(acc, pat, vp, len, xs, row0, ok, a.alpha, pf);
+        tri_done = true;
+      }
+    }
+    if (tri_done) {
+    } else if (a.flags & SPMV_XPAIR) {
       if (a.flags & SPMV_NT) rows_pattern<T, R, ALPHA, true, U, true, SH>(acc, pat, vp, len, xs, row0, ok, a.alpha, pf, tb);
       else rows_pattern<T, R, ALPHA, false, U, true, SH>(acc, pat, vp, len, xs, row0, ok, a.alpha, pf, tb);
     } else {
