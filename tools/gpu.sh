@@ -6,7 +6,7 @@
 # Steps run in order, each under its own time limit; the first failure ends
 # the call (no GPU step after a fault, a timeout or an abort).  A step is
 # "name" or "name:arguments":
-#   tests[:pytest args]   python -m pytest tests -m gpu (e.g. "tests:-k fullsize")
+#   tests[:pytest args]   python -m pytest tests -m gpu (e.g. "tests:-k fullsize", "tests:-k 'cg or dot'")
 #   smoke                 __graft_entry__.smoke()
 #   bench[:bench args]    python bench.py ARGS            > OUT/bench<i>.json
 #   kt[:bench args]       rocprofv3 --kernel-trace --stats  -d OUT/kt<i>
@@ -32,7 +32,8 @@ for step in "$@"; do
   t0=$(date +%s)
   case $name in
     tests)
-      timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread $args \
+      # eval: a quoted -k expression ("tests:-k 'cg or dot'") stays one argument
+      eval "timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread $args" \
         > "$OUT/tests$i.log" 2>&1
       rc=$?; tail -3 "$OUT/tests$i.log" ;;
     smoke)
