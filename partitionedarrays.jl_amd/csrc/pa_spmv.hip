@@ -1837,11 +1837,11 @@ void launch_gather_ptrs(int P, const void* const* srcs, int accsz, void* out, hi
 // of the slice (or the row at 1/4 or 3/4 when more rows follow that one); its
 // offsets pat[k] = col_k - row.  A row is regular for a
 // candidate when its column sequence is exactly row + pat[k] (same length).
-// The slice becomes a pattern slice when at least half its rows are regular
+// The slice becomes a pattern slice when at least pattern_min_regular % (70) of its rows are regular
 // (the others go to the side SELL).
 
 template <int R>
-__global__ __launch_bounds__(256) void k_pattern_detect(int64_t nrows, int64_t nslices,
+__global__ __launch_bounds__(256) void k_pattern_detect(int64_t nrows, int64_t nslices, int min_pct,
                                                         const int64_t* __restrict__ soff,
                                                         const int32_t* __restrict__ slen,
                                                         const int32_t* __restrict__ col, int64_t noids, int kmax,
@@ -1939,9 +1939,10 @@ __global__ __launch_bounds__(256) void k_pattern_detect(int64_t nrows, int64_t n
       }
     }
   }
-  // a pattern slice when at least half its rows follow the pattern (and
-  // its rows have at most 255 entries: the length is packed in 8 bits)
-  const bool best = Lp > 0 && Lp <= 255 && 2 * tot1 >= nvalid;
+  // a pattern slice when at least min_pct % of its rows follow the pattern
+  // (pa_tune pattern_min_regular, default 70; the others go to the side
+  // SELL) and its rows have at most 255 entries (the length has 8 bits)
+  const bool best = Lp > 0 && Lp <= 255 && 100 * tot1 >= min_pct * nvalid;
   const bool gr = __any(g1);
   const bool ga = __any(ghost_any);
   if (lane == 0) {
@@ -2058,12 +2059,12 @@ void launch_delta16(pa_mat* A, int64_t noids, const int32_t* kind, int32_t* ok, 
 #undef PA_D16
 }
 
-void launch_pattern_detect(pa_mat* A, int64_t noids, int32_t* kind, int32_t* plen, int32_t* pat,
+void launch_pattern_detect(pa_mat* A, int64_t noids, int min_pct, int32_t* kind, int32_t* plen, int32_t* pat,
                            uint64_t* mask, int32_t* pghost, int32_t* nirreg, hipStream_t st) {
   const int64_t blocks = (A->nslices + 3) / 4;
   if (blocks == 0) return;
 #define PA_DET(RR)                                                                                      \
-  hipLaunchKernelGGL(k_pattern_detect<RR>, dim3(blocks), dim3(256), 0, st, A->nrows, A->nslices,        \
+  hipLaunchKernelGGL(k_pattern_detect<RR>, dim3(blocks), dim3(256), 0, st, A->nrows, A->nslices, min_pct, \
                      A->d_slice_off, A->d_slice_len, A->d_col, noids, A->kmax, kind, plen, pat, mask,  \
                      pghost, nirreg)
   switch (A->R) {

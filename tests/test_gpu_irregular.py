@@ -57,6 +57,9 @@ def _eq(O, got, ref):
     ((24, 22, 20), 12, np.float64, 1), ((24, 22, 20), 12, np.complex128, 0)])  # > PA_GROUP_MAX parts
 def test_irregular_spmv_bitexact(be, pamd, O, N, nparts, dtype, fmt):
     prev = pamd._lib.tune("spmv_format", fmt)
+    # pattern slices from 40 % regular rows (default 70): the side SELL gets
+    # the rest, so both the pattern and the side-row paths run
+    prev_pct = pamd._lib.tune("pattern_min_regular", 40)
     try:
         parts = be.get_part_ids(nparts)
         A = pamd.drivers.irregular_problem(parts, N, 27, dtype)
@@ -79,6 +82,7 @@ def test_irregular_spmv_bitexact(be, pamd, O, N, nparts, dtype, fmt):
             assert any(i["side_rows"] > 0 for i in info.parts)
     finally:
         pamd._lib.tune("spmv_format", prev)
+        pamd._lib.tune("pattern_min_regular", prev_pct)
 
 
 @pytest.mark.parametrize("pull", [1, 0])
