@@ -89,8 +89,9 @@ int pa_device_count(int* count);
  * "spmv_group"  1: the parts of one process sharing a stream pair run each
  *               mul! phase as one launch (default), 0: launches per part;
  * "pattern_min_regular" a slice becomes a pattern slice when at least this
- *               percentage of its rows follow its pattern (1-100, default
- *               70; matrices built afterwards), the others go to the side SELL;
+ *               percentage of its rows follow its pattern (1-100; 0 = auto,
+ *               the default: 70, 50 for Float32's 256-row slices; matrices
+ *               built afterwards), the others go to the side SELL;
  * "issue_threads" a mul! over several parts with their own stream pairs is
  *               issued from host threads, one part per thread: 1 when the
  *               parts span several devices (default), 2 always, 0 never

@@ -65,12 +65,16 @@ int g_spmv_merge = 1;     // pa_tune("spmv_merge"): one launch for every slice k
 // profiles/r02/open/ab_merge.jsonl.  0: no limit.
 int64_t g_spmv_merge_max = 65536;
 // pa_tune("pattern_min_regular"): % of a slice's rows that must follow its
-// pattern for a pattern slice (the others become side rows).  A/B on C5
+// pattern for a pattern slice (the others become side rows); 0 = auto: 70 %
+// for slices of 128 rows, 50 % for Float32's 256-row slices.  A/B on C5
 // (profiles/r04/y/, copies per variant): F64 50 % 0.1195 ms, 70 % 0.1131,
 // 90 % 0.1124 (the side SELL's duplicate values and ids gone: 621 -> 589 MB
-// per mul!); F32 0.0737 / 0.0725 / 0.0742; 30 % +11 % / +6 %.  FE27, FD7
-// and Cartesian parts are >= 99 % regular either way.
-int g_pattern_min_pct = 70;
+// per mul!); F32 0.0737 / 0.0725 / 0.0742 (within noise); 30 % +11 % / +6 %.
+// A 256-row Float32 slice of a structured grid at 128³ spans two x-lines,
+// one of them on a domain face (its own pattern): 50 % keeps it a pattern
+// slice (FD7 128³: all 8192 slices).  FE27 / FD7 slices of one x-line and
+// Cartesian parts are >= 99 % regular either way.
+int g_pattern_min_pct = 0;
 int g_issue_threads = 1;   // pa_tune("issue_threads"): 1 auto (several devices), 2 always, 0 never
 int g_halo_direct = 1;     // pa_tune("halo_direct"): grouped mul! pulls ghosts straight from the owners' x
 int g_halo_transport = 0;  // pa_tune("halo_transport"): 0 parts of this process by device reads, 1 RCCL for all
@@ -403,8 +407,8 @@ int finalize_pattern(pa_mat* A, int kmax, int64_t noids) {
   HIPC(hipMalloc((void**)&d_pghost, ns * 4));
   HIPC(hipMalloc((void**)&d_nirreg, ns * 4));
   HIPC(hipMemsetAsync(A->d_mask, 0, ns * W * 8, st));
-  launch_pattern_detect(A, noids, g_pattern_min_pct, A->d_kind, A->d_plen, A->d_pat, A->d_mask, d_pghost, d_nirreg,
-                        st);
+  const int min_pct = g_pattern_min_pct ? g_pattern_min_pct : (A->R == 4 ? 50 : 70);
+  launch_pattern_detect(A, noids, min_pct, A->d_kind, A->d_plen, A->d_pat, A->d_mask, d_pghost, d_nirreg, st);
   HIPC(hipGetLastError());
   std::vector<int32_t> kind(ns), pghost(ns), nirreg(ns);
   std::vector<uint64_t> mask(ns * W);
@@ -1100,9 +1104,9 @@ const Knob kKnobs[] = {
     {"spmv_group", &g_spmv_group, nullptr, 0, 1, 0,
      "spmv_group: 1 = one launch per phase for parts sharing a stream pair, 0 = per part"},
     {"spmv_format", &g_spmv_format, nullptr, 0, 1, 0, "spmv_format: 0 = int32 columns, 1 = pattern slices"},
-    {"pattern_min_regular", &g_pattern_min_pct, nullptr, 1, 100, 0,
+    {"pattern_min_regular", &g_pattern_min_pct, nullptr, 0, 100, 0,
      "pattern_min_regular: a slice becomes a pattern slice when at least this % of its rows follow its pattern "
-     "(matrices built afterwards; default 70)"},
+     "(matrices built afterwards); 0 = auto (default): 70 for 128-row slices, 50 for Float32's 256-row slices"},
     {"issue_threads", &g_issue_threads, nullptr, 0, 2, 0,
      "issue_threads: a call over parts with their own stream pairs is issued from host threads, one part "
      "per thread: 1 = when the parts span several devices (default), 2 = always, 0 = never (the calling "

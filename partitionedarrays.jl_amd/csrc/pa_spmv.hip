@@ -1837,7 +1837,7 @@ void launch_gather_ptrs(int P, const void* const* srcs, int accsz, void* out, hi
 // of the slice (or the row at 1/4 or 3/4 when more rows follow that one); its
 // offsets pat[k] = col_k - row.  A row is regular for a
 // candidate when its column sequence is exactly row + pat[k] (same length).
-// The slice becomes a pattern slice when at least pattern_min_regular % (70) of its rows are regular
+// The slice becomes a pattern slice when at least pattern_min_regular % of its rows are regular
 // (the others go to the side SELL).
 
 template <int R>
@@ -1940,7 +1940,7 @@ __global__ __launch_bounds__(256) void k_pattern_detect(int64_t nrows, int64_t n
     }
   }
   // a pattern slice when at least min_pct % of its rows follow the pattern
-  // (pa_tune pattern_min_regular, default 70; the others go to the side
+  // (pa_tune pattern_min_regular, default 70 / 50 for Float32; the others go to the side
   // SELL) and its rows have at most 255 entries (the length has 8 bits)
   const bool best = Lp > 0 && Lp <= 255 && 100 * tot1 >= min_pct * nvalid;
   const bool gr = __any(g1);

@@ -78,7 +78,7 @@ def test_tune_knobs_round_trip_and_reject_bad_values(pamd):
                 pass
     finally:
         pamd._lib.tune("spmv_flags", prev)
-    for k, bad in (("spmv_merge", 2), ("spmv_merge_max", -1), ("cg_fuse", 3), ("pattern_min_regular", 0),
+    for k, bad in (("spmv_merge", 2), ("spmv_merge_max", -1), ("cg_fuse", 3), ("pattern_min_regular", -1),
                    ("pattern_min_regular", 101)):
         try:
             pamd._lib.tune(k, bad)
