@@ -671,11 +671,17 @@ __device__ __forceinline__ void cg_rows_update(const SpmvArgs<T>& a, const XS& x
 #pragma unroll
       for (int k = 0; k < R; ++k) unv[k] = o.v[k];
     }
-    if (xpend) {
-      Pack<T, R> xv = *reinterpret_cast<const Pack<T, R>*>(xacc + i0);
+    if (xpend) {  // x is next read one iteration later: non-temporal, as in k_cg_xu
+      Pack<T, R> xv = ld<true>(reinterpret_cast<const Pack<T, R>*>(xacc + i0));
 #pragma unroll
       for (int k = 0; k < R; ++k) xv.v[k] = narrow<T>(widen(xv.v[k]) + alpha * widen(uo.v[k]));
-      *reinterpret_cast<Pack<T, R>*>(xacc + i0) = xv;
+      if constexpr (sizeof(Pack<T, R>) == 16) {
+        spmv_u32x4 w;
+        __builtin_memcpy(&w, &xv, 16);
+        __builtin_nontemporal_store(w, reinterpret_cast<spmv_u32x4*>(xacc + i0));
+      } else {
+        *reinterpret_cast<Pack<T, R>*>(xacc + i0) = xv;
+      }
     }
     return;
   }
@@ -1594,11 +1600,17 @@ __global__ __launch_bounds__(256) void k_cg_xu(int64_t n, T* __restrict__ x, T* 
   const int64_t nv = n / V;
   for (int64_t j = t; j < nv; j += stride) {
     P uv = reinterpret_cast<const P*>(u)[j];
-    if (xpend) {
-      P xv = reinterpret_cast<const P*>(x)[j];
+    if (xpend) {  // x is next read one iteration later: non-temporal (CG 0.9234 -> 0.895 ms, profiles/r04/ab/)
+      P xv = ld<true>(&reinterpret_cast<const P*>(x)[j]);
 #pragma unroll
       for (int e = 0; e < V; ++e) xv.v[e] = narrow<T>(widen(xv.v[e]) + a * widen(uv.v[e]));
-      reinterpret_cast<P*>(x)[j] = xv;
+      if constexpr (sizeof(P) == 16) {
+        spmv_u32x4 w;
+        __builtin_memcpy(&w, &xv, 16);
+        __builtin_nontemporal_store(w, reinterpret_cast<spmv_u32x4*>(x) + j);
+      } else {
+        reinterpret_cast<P*>(x)[j] = xv;
+      }
     }
     if (upd) {
       const P rv = reinterpret_cast<const P*>(r)[j];

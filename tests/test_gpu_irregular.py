@@ -267,3 +267,39 @@ def test_voronoi_column_loops_equal_oracle(be, pamd, O, dtype, d16, tail):
     finally:
         for k, v in prev.items():
             pamd._lib.tune(k, v)
+
+
+@pytest.mark.parametrize("dtype", [np.float32, np.float64])
+def test_voronoi_values_round_trip_through_moved_slots(be, pamd, O, dtype):
+    """Float32 delta16 slices move their values to interleaved rows at
+    build time and the CSC nz → slot map follows: get_values returns the
+    oracle's nzval in CSC order, set_values writes new values to the right
+    slots (mul! with them equals the oracle's), for both element types."""
+    N, nparts = (30, 28, 26), 8
+    parts = be.get_part_ids(nparts)
+    A = pamd.drivers.irregular_problem(parts, N, 27, dtype)
+    OA = _oracle(O, N, nparts, dtype)
+    if np.dtype(dtype) == np.float32:
+        assert any(A.values.local(p).info()["delta16_slices"] > 0 for p in parts.part_ids)
+    for i, p in enumerate(parts.part_ids):
+        assert np.array_equal(A.values.local(p).get_values(), OA.values.parts[i].nzval), p
+    rng = np.random.default_rng(SEED + 31)
+    new = []
+    for i, p in enumerate(parts.part_ids):
+        v2 = rng.uniform(-1, 1, len(OA.values.parts[i].nzval)).astype(dtype)
+        A.values.local(p).set_values(v2)
+        assert np.array_equal(A.values.local(p).get_values(), v2)
+        new.append(v2)
+    it = iter(new)  # the oracle with the same new values (a copy: _oracle caches its matrices)
+    OA = O.PSparseMatrix(O.map_parts(lambda M: O.CSC(M.m, M.n, M.colptr, M.rowval, next(it).copy()), OA.values),
+                         OA.rows, OA.cols)
+    xs = {p: _rand(rng, A.cols.partition.local(p).num_lids, dtype) for p in parts.part_ids}
+    x = pamd.PVector.from_host(pamd.map_parts(lambda s: xs[s.part], A.cols.partition), A.cols)
+    y = pamd.PVector.undef(A.rows, dtype)
+    pamd.mul_(y, A, x)
+    ox = O.PVector(O.map_parts(lambda s: _ox(O, xs[s.part]), OA.cols.partition), OA.cols)
+    oy = O.pvector_undef(OA.rows, dtype)
+    O.mul_(oy, OA, ox)
+    got = y.to_host()
+    for p in parts.part_ids:
+        assert _eq(O, got.local(p), oy.values[p]), f"part {p}: SpMV with the new values differs"
