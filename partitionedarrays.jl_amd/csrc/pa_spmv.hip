@@ -595,6 +595,10 @@ __device__ __forceinline__ void rows_pattern(T (&acc)[R], const int32_t* __restr
 // rows_pattern.  Library A/B on one box (profiles/r04/p/): FE27 256^3 one
 // part 0.6744 -> 0.6523 ms, the (2,2,2) halo leg 0.714 -> 0.688 ms, C5 F64
 // -1.0 %: one x load in three fewer relieves the per-CU memory pipeline.
+// triples per batch: 12 entries in flight per lane (library A/B, profiles/r04/ag/: FE27
+// 256^3 2 triples 0.6590 ms, 3 0.6549-0.6554, 4 0.6500; the VGPR count is the
+// same, the loop is not the kernel's register maximum)
+constexpr int kTriBatch = 4;
 template <typename T, int R, bool ALPHA, bool NT, typename XS>
 __device__ __forceinline__ void rows_pattern_tri(T (&acc)[R], const int32_t* __restrict__ pat,
                                                  const Pack<T, R>* __restrict__ vp, int len, const XS& x,
@@ -614,18 +618,19 @@ __device__ __forceinline__ void rows_pattern_tri(T (&acc)[R], const int32_t* __r
     }
   };
   int k = 0;
-  for (; k + 9 <= len; k += 9) {
-    int32_t o[3];
+  constexpr int TB = kTriBatch;  // triples per batch
+  for (; k + 3 * TB <= len; k += 3 * TB) {
+    int32_t o[TB];
 #pragma unroll
-    for (int t = 0; t < 3; ++t) o[t] = pat[k + 3 * t];
-    Pack<T, R> v[9];
+    for (int t = 0; t < TB; ++t) o[t] = pat[k + 3 * t];
+    Pack<T, R> v[3 * TB];
 #pragma unroll
-    for (int u = 0; u < 9; ++u) v[u] = ld<NT>(&vp[(k + u) * 64]);
-    T xv[3][3][R];
+    for (int u = 0; u < 3 * TB; ++u) v[u] = ld<NT>(&vp[(k + u) * 64]);
+    T xv[TB][3][R];
 #pragma unroll
-    for (int t = 0; t < 3; ++t) triple(o[t], xv[t]);
+    for (int t = 0; t < TB; ++t) triple(o[t], xv[t]);
 #pragma unroll
-    for (int t = 0; t < 3; ++t)
+    for (int t = 0; t < TB; ++t)
 #pragma unroll
       for (int j = 0; j < 3; ++j)
 #pragma unroll
