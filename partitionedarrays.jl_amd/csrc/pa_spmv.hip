@@ -596,8 +596,8 @@ __device__ __forceinline__ void rows_pattern(T (&acc)[R], const int32_t* __restr
 // part 0.6744 -> 0.6523 ms, the (2,2,2) halo leg 0.714 -> 0.688 ms, C5 F64
 // -1.0 %: one x load in three fewer relieves the per-CU memory pipeline.
 // triples per batch: 12 entries in flight per lane (library A/B, profiles/r04/ag/: FE27
-// 256^3 2 triples 0.6590 ms, 3 0.6549-0.6554, 4 0.6500; the VGPR count is the
-// same, the loop is not the kernel's register maximum)
+// 256^3 2 triples 0.6590 ms, 3 0.6549-0.6554, 4 0.6500 at the same VGPR count;
+// 6: 0.6627, the merged kernel 122 -> 132 VGPRs, halo leg +12 %, r04/ai/)
 constexpr int kTriBatch = 4;
 template <typename T, int R, bool ALPHA, bool NT, typename XS>
 __device__ __forceinline__ void rows_pattern_tri(T (&acc)[R], const int32_t* __restrict__ pat,
