@@ -1130,10 +1130,11 @@ struct SpmvTable {
 };
 
 template <typename T, int R, bool ALPHA, int BMODE, int U, bool SH, bool XV = false>
-__device__ __forceinline__ void merged_wave(const SpmvTable<T>* __restrict__ tab) {
+__device__ __forceinline__ void merged_wave(const SpmvTable<T>* __restrict__ tab, int n, int64_t waves) {
+  // n and the wave count come as kernel arguments (with the kernarg load, not
+  // two dependent table loads ahead of the search)
   const int64_t w = (int64_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-  const int n = tab->n;
-  if (w >= tab->start[n]) return;
+  if (w >= waves) return;
   int lo = 0, hi = n;  // last entry whose start <= w
   while (hi - lo > 1) {
     const int mid = (lo + hi) >> 1;
@@ -1152,8 +1153,9 @@ __device__ __forceinline__ void merged_wave(const SpmvTable<T>* __restrict__ tab
 // spill) lost in a same-box A/B: C5 F32 +4.5 %, FE27 F64 +0.4 %, F32 +0.6 %
 // (profiles/r02/stream/ab_waves4.txt).
 template <typename T, int R, bool ALPHA, int BMODE, int U, bool SH, bool XV = false>
-__global__ __launch_bounds__(256) void k_spmv_merged(const SpmvTable<T>* __restrict__ tab) {
-  merged_wave<T, R, ALPHA, BMODE, U, SH, XV>(tab);
+__global__ __launch_bounds__(256) void k_spmv_merged(const SpmvTable<T>* __restrict__ tab, int n,
+                                                         int64_t waves) {
+  merged_wave<T, R, ALPHA, BMODE, U, SH, XV>(tab, n, waves);
 }
 
 // F64 short rows (FD7): 5 waves per SIMD instead of 4 (96 VGPRs instead of
@@ -1162,24 +1164,24 @@ __global__ __launch_bounds__(256) void k_spmv_merged(const SpmvTable<T>* __restr
 // F32/C64 (R = 4 / complex: ~200 spills) nor for longer rows (FE27: -10 %).
 template <typename T, int R, bool ALPHA, int BMODE>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k_spmv_merged_short(
-    const SpmvTable<T>* __restrict__ tab) {
-  merged_wave<T, R, ALPHA, BMODE, 8, true>(tab);
+    const SpmvTable<T>* __restrict__ tab, int n, int64_t waves) {
+  merged_wave<T, R, ALPHA, BMODE, 8, true>(tab, n, waves);
 }
 
 template <typename T, int R, bool ALPHA, int BMODE>
-static void launch_merged_t(const SpmvTable<T>* d, int64_t waves, bool sh, hipStream_t st) {
+static void launch_merged_t(const SpmvTable<T>* d, int n, int64_t waves, bool sh, hipStream_t st) {
   const int64_t blocks = (waves + 3) / 4;
   if (blocks == 0) return;
   if constexpr (std::is_same<T, double>::value) {
     if (sh) {
-      hipLaunchKernelGGL((k_spmv_merged_short<T, R, ALPHA, BMODE>), dim3(blocks), dim3(256), 0, st, d);
+      hipLaunchKernelGGL((k_spmv_merged_short<T, R, ALPHA, BMODE>), dim3(blocks), dim3(256), 0, st, d, n, waves);
       return;
     }
   }
   if (sh)
-    hipLaunchKernelGGL((k_spmv_merged<T, R, ALPHA, BMODE, 8, true>), dim3(blocks), dim3(256), 0, st, d);
+    hipLaunchKernelGGL((k_spmv_merged<T, R, ALPHA, BMODE, 8, true>), dim3(blocks), dim3(256), 0, st, d, n, waves);
   else
-    hipLaunchKernelGGL((k_spmv_merged<T, R, ALPHA, BMODE, 8, false>), dim3(blocks), dim3(256), 0, st, d);
+    hipLaunchKernelGGL((k_spmv_merged<T, R, ALPHA, BMODE, 8, false>), dim3(blocks), dim3(256), 0, st, d, n, waves);
 }
 
 static int pk_of(int which) { return which == 0 ? 1 : which == 4 ? 3 : 0; }
@@ -1237,18 +1239,18 @@ static int merged_t(int n, const int* which, const SpmvPart* parts, bool has_alp
   if (h.a[0].cg) {  // the device CG's fused u update (α = 1, β = 0)
     const int64_t blocks = (waves + 3) / 4;
     if (blocks == 0) return 0;
-    if (sh) hipLaunchKernelGGL((k_spmv_merged<T, R, false, 0, 8, true, true>), dim3(blocks), dim3(256), 0, st, dt);
-    else hipLaunchKernelGGL((k_spmv_merged<T, R, false, 0, 8, false, true>), dim3(blocks), dim3(256), 0, st, dt);
+    if (sh) hipLaunchKernelGGL((k_spmv_merged<T, R, false, 0, 8, true, true>), dim3(blocks), dim3(256), 0, st, dt, h.n, waves);
+    else hipLaunchKernelGGL((k_spmv_merged<T, R, false, 0, 8, false, true>), dim3(blocks), dim3(256), 0, st, dt, h.n, waves);
     return 0;
   }
   if (!has_alpha) {
-    if (bmode == 0) launch_merged_t<T, R, false, 0>(dt, waves, sh, st);
-    else if (bmode == 1) launch_merged_t<T, R, false, 1>(dt, waves, sh, st);
-    else launch_merged_t<T, R, false, 2>(dt, waves, sh, st);
+    if (bmode == 0) launch_merged_t<T, R, false, 0>(dt, h.n, waves, sh, st);
+    else if (bmode == 1) launch_merged_t<T, R, false, 1>(dt, h.n, waves, sh, st);
+    else launch_merged_t<T, R, false, 2>(dt, h.n, waves, sh, st);
   } else {
-    if (bmode == 0) launch_merged_t<T, R, true, 0>(dt, waves, sh, st);
-    else if (bmode == 1) launch_merged_t<T, R, true, 1>(dt, waves, sh, st);
-    else launch_merged_t<T, R, true, 2>(dt, waves, sh, st);
+    if (bmode == 0) launch_merged_t<T, R, true, 0>(dt, h.n, waves, sh, st);
+    else if (bmode == 1) launch_merged_t<T, R, true, 1>(dt, h.n, waves, sh, st);
+    else launch_merged_t<T, R, true, 2>(dt, h.n, waves, sh, st);
   }
   return 0;
 }
