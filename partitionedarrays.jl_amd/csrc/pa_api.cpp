@@ -62,7 +62,8 @@ int g_spmv_merge = 1;     // pa_tune("spmv_merge"): one launch for every slice k
 // this: such a part fills the GPU many times over, and one launch per kind
 // (the kind's own kernel, fewer registers) is faster — FE27 256³ F64 −1.0 %,
 // F32 −2.8 %; C2 (16 k slices) and C5 stay merged (−10 % / −15 %).
-// profiles/r02/open/ab_merge.jsonl.  0: no limit.
+// profiles/r02/open/ab_merge.jsonl; r04 again: F64 −0.6 %, F32 ±0
+// (profiles/r04/an/).  0: no limit.
 int64_t g_spmv_merge_max = 65536;
 // pa_tune("pattern_min_regular"): % of a slice's rows that must follow its
 // pattern for a pattern slice (the others become side rows); 0 = auto: 70 %
