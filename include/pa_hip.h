@@ -22,10 +22,15 @@
  *  - dtype codes: PA_F32, PA_F64, PA_C64 (ComplexF32), PA_C128 (ComplexF64).
  *    Scalars (alpha, beta, results) are passed as pointers to host values of
  *    the vector's element type;
- *  - threading: one host thread drives the library per process (the
- *    reference's tasks run on the main Julia task too).  pa_tune knobs, the
- *    graph-capture state and the per-context caches are process-wide and
- *    unsynchronised; only pa_last_error is per thread.
+ *  - threading: one host thread drives a set of parts (the reference's
+ *    tasks run on the main Julia task too); the library may issue a call's
+ *    per-part work from its own threads.  The tuning knobs are resolved per
+ *    call (the process defaults of pa_tune under the call's context
+ *    overrides, pa_ctx_tune) and never written while a call runs, so calls
+ *    on different parts from different host threads each run with their own
+ *    context's knobs (pa_knob_selftest).  The graph-capture state and the
+ *    per-context caches are not synchronised: concurrent calls must not
+ *    share a context.  pa_last_error is per thread.
  */
 #ifndef PA_HIP_H
 #define PA_HIP_H
@@ -102,6 +107,11 @@ int pa_tune(const char* key, int value, int* previous);
  * the duration of the call; value -1 drops the override.  *previous gets
  * the context's former override (-1: none).                             */
 int pa_ctx_tune(pa_ctx* c, const char* key, int value, int* previous);
+/* Test support (no device needed): `nthreads` host threads resolve calls'
+ * knobs with different context overrides, on their own threads and on the
+ * library's issue threads, while the process default changes; *mismatches
+ * counts resolutions that saw another call's value (0 expected).        */
+int pa_knob_selftest(int nthreads, int iters, int* mismatches);
 /* HBM calibration of `device` (not the hot path): best read-only and copy
  * rates (GB/s, read+write bytes for the copy; best of 4/8 loads in flight
  * per lane and four grid sizes) over `reps` sweeps of a

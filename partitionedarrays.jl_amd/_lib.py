@@ -38,6 +38,7 @@ _SIGS = {
     "pa_device_count": [C.POINTER(C.c_int)],
     "pa_tune": [C.c_char_p, C.c_int, C.POINTER(C.c_int)],
     "pa_ctx_tune": [_p, C.c_char_p, C.c_int, C.POINTER(C.c_int)],
+    "pa_knob_selftest": [C.c_int, C.c_int, C.POINTER(C.c_int)],
     "pa_hbm_probe": [C.c_int, C.c_int64, C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_double)],
     "pa_ctx_create": [C.c_int, C.c_int, C.c_int, C.POINTER(_p)],
     "pa_ctx_create_shared": [C.c_int, C.c_int, _p, C.POINTER(_p)],
@@ -177,6 +178,14 @@ def tune_generation_bump():
     """a per-context knob changed (PartContext.tune): cached graphs are stale"""
     global tune_generation
     tune_generation += 1
+
+
+def knob_selftest(nthreads: int = 4, iters: int = 2000) -> int:
+    """pa_knob_selftest: resolutions of concurrent calls' knobs that saw
+    another call's context value (0 expected; no device needed)."""
+    n = C.c_int(-1)
+    call("pa_knob_selftest", int(nthreads), int(iters), C.byref(n))
+    return n.value
 
 
 def hbm_probe(device: int = 0, nbytes: int = 2 << 30, reps: int = 10):

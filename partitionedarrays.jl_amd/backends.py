@@ -202,6 +202,13 @@ class DistributedBackend(AbstractBackend):
         v = np.asarray(snd.parts[0], dtype=np.int64)
         if len(v) != self.size:
             raise ValueError("alltoall: every part must hold one value per part")
+        if self.dist.get_backend(self.group) != "gloo":
+            # nccl (or another device backend) as the host group: CPU tensors
+            # cannot go through its all_to_all, so take the column from the
+            # object all-gather (P ints from each part)
+            allv = self._all_gather(v.tolist())
+            return PData(self, snd.part_ids, [np.array([r[self.rank] for r in allv], dtype=np.int64)],
+                         snd.shape)
         out = torch.empty(self.size, dtype=torch.int64)
         self.dist.all_to_all_single(out, torch.from_numpy(v.copy()), group=self.group)
         return PData(self, snd.part_ids, [out.numpy().astype(np.int64)], snd.shape)

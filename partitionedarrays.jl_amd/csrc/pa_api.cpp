@@ -53,39 +53,42 @@ void launch_cg_ghost(int dtype, int64_t lo, int64_t hi, const void* r, const voi
 void launch_cg_alpha(int dtype, int P, const void* gathered, CGState* cst, hipStream_t st);
 void launch_cg_step(int dtype, int P, const double* gathered, CGState* cst, double* history, hipStream_t st);
 void launch_gather_ptrs(int P, const void* const* srcs, int accsz, void* out, hipStream_t st);
-extern int g_spmv_format;
-int g_halo_pull = 1;  // pa_tune("halo_pull"): pull-unpack between parts of one process
-int g_spmv_group = 1; // pa_tune("spmv_group"): one launch per phase for the parts sharing a stream pair
-int g_spmv_delta16 = 1;   // pa_tune("spmv_delta16"): int32-column slices with 16-bit column codes where they fit
-int g_spmv_merge = 1;     // pa_tune("spmv_merge"): one launch for every slice kind of every part when no halo is in flight
-// pa_tune("spmv_merge_max"): ... unless one part alone has more slices than
-// this: such a part fills the GPU many times over, and one launch per kind
-// (the kind's own kernel, fewer registers) is faster — FE27 256³ F64 −1.0 %,
-// F32 −2.8 %; C2 (16 k slices) and C5 stay merged (−10 % / −15 %).
-// profiles/r02/open/ab_merge.jsonl; r04 again: F64 −0.6 %, F32 ±0
-// (profiles/r04/an/).  0: no limit.
-int64_t g_spmv_merge_max = 65536;
-// pa_tune("pattern_min_regular"): % of a slice's rows that must follow its
-// pattern for a pattern slice (the others become side rows); 0 = auto: 70 %
-// for slices of 128 rows, 50 % for Float32's 256-row slices.  A/B on C5
-// (profiles/r04/y/, copies per variant): F64 50 % 0.1195 ms, 70 % 0.1131,
-// 90 % 0.1124 (the side SELL's duplicate values and ids gone: 621 -> 589 MB
-// per mul!); F32 0.0737 / 0.0725 / 0.0742 (within noise); 30 % +11 % / +6 %.
-// A 256-row Float32 slice of a structured grid at 128³ spans two x-lines,
-// one of them on a domain face (its own pattern): 50 % keeps it a pattern
-// slice (FD7 128³: all 8192 slices).  FE27 / FD7 slices of one x-line and
-// Cartesian parts are >= 99 % regular either way.
-int g_pattern_min_pct = 0;
-int g_issue_threads = 1;   // pa_tune("issue_threads"): 1 auto (several devices), 2 always, 0 never
-int g_halo_direct = 1;     // pa_tune("halo_direct"): grouped mul! pulls ghosts straight from the owners' x
-int g_halo_transport = 0;  // pa_tune("halo_transport"): 0 parts of this process by device reads, 1 RCCL for all
-// pa_tune("cg_fuse"): the device CG's u update inside the SpMV (XV kernels)
-// instead of its own sweep.  Off: steady-state iteration on FE27 256³, sweep
-// vs fused, on four boxes: 0.958 / 1.080, 0.947 / 0.973, 0.917 / 0.882,
-// whole call 1.043 / 1.075 ms (profiles/r03/s, final, f, d) — the fused
-// SpMV gathers two vectors (r and u_old) per x value — so the default is 2:
-// measure one batch of each on this box and keep the faster (pa_cg_solve_all).
-int g_cg_fuse = 2;
+// Process defaults of the tuning knobs (pa_tune; the per-call Knobs of
+// pa_internal.h).  Why each default:
+//  * halo_pull 1: pull-unpack between parts of one process;
+//  * spmv_group 1: one launch per phase for the parts sharing a stream pair;
+//  * spmv_delta16 1: int32-column slices with 16-bit column codes where they fit;
+//  * spmv_merge 1: one launch for every slice kind of every part when no halo is in flight;
+//  * spmv_merge_max 65536: ... unless one part alone has more slices than
+//    this: such a part fills the GPU many times over, and one launch per kind
+//    (the kind's own kernel, fewer registers) is faster — FE27 256³ F64 −1.0 %,
+//    F32 −2.8 %; C2 (16 k slices) and C5 stay merged (−10 % / −15 %).
+//    profiles/r02/open/ab_merge.jsonl; r04 again: F64 −0.6 %, F32 ±0
+//    (profiles/r04/an/).  0: no limit;
+//  * pattern_min_regular 0 (auto): % of a slice's rows that must follow its
+//    pattern for a pattern slice (the others become side rows); auto = 70 %
+//    for slices of 128 rows, 50 % for Float32's 256-row slices.  A/B on C5
+//    (profiles/r04/y/, copies per variant): F64 50 % 0.1195 ms, 70 % 0.1131,
+//    90 % 0.1124 (the side SELL's duplicate values and ids gone: 621 -> 589 MB
+//    per mul!); F32 0.0737 / 0.0725 / 0.0742 (within noise); 30 % +11 % / +6 %.
+//    A 256-row Float32 slice of a structured grid at 128³ spans two x-lines,
+//    one of them on a domain face (its own pattern): 50 % keeps it a pattern
+//    slice (FD7 128³: all 8192 slices).  FE27 / FD7 slices of one x-line and
+//    Cartesian parts are >= 99 % regular either way;
+//  * issue_threads 1: 1 auto (several devices), 2 always, 0 never;
+//  * halo_direct 1: grouped mul! pulls ghosts straight from the owners' x;
+//  * halo_transport 0: parts of this process by device reads, 1 RCCL for all;
+//  * cg_fuse 2: the device CG's u update inside the SpMV (XV kernels) or its
+//    own sweep.  Steady-state iteration on FE27 256³, sweep vs fused, on four
+//    boxes: 0.958 / 1.080, 0.947 / 0.973, 0.917 / 0.882, whole call 1.043 /
+//    1.075 ms (profiles/r03/s, final, f, d) — the fused SpMV gathers two
+//    vectors (r and u_old) per x value — so 2 = measure one batch of each on
+//    this box and keep the faster (pa_cg_solve_all);
+//  * spmv_flags 93, spmv_format 1, long_rows_exact 1: pa_spmv.hip.
+const Knobs kDefaults = {
+    /*spmv_flags*/ 93, /*long_exact*/ 1, /*halo_pull*/ 1, /*spmv_delta16*/ 1, /*spmv_merge*/ 1,
+    /*spmv_merge_max*/ 65536, /*cg_fuse*/ 2, /*halo_direct*/ 1, /*halo_transport*/ 0, /*spmv_group*/ 1,
+    /*spmv_format*/ 1, /*pattern_min_pct*/ 0, /*issue_threads*/ 1, /*fault_inject*/ 0};
 // COO → CSC → SELL on the device (pa_coo.hip)
 int coo_compress(int dtype, int index_bytes, int64_t m, int64_t ncols, int64_t n, const void* dI, const void* dJ,
                  const void* dV, int csr, int64_t* nu_out, int32_t** crow, int32_t** ccol, void** cval,
@@ -140,8 +143,7 @@ void launch_stencil_count(const StencilGeom& g, const int32_t* shell, const doub
 void launch_stencil_fill(const StencilGeom& g, const int32_t* shell, const double* coef,
                          int64_t nrows, int noids, pa_mat* A, int32_t* err, hipStream_t st);
 void launch_probe(int copy, int unroll, int64_t n16, const void* a, void* b, int blocks, hipStream_t st);
-extern int g_spmv_flags;
-extern int g_long_exact;
+void launch_invalid_config();
 
 }  // namespace pa
 
@@ -321,8 +323,9 @@ int finish_sell_layout(pa_mat* A, const std::vector<int32_t>& slen, const std::v
 // The pattern slices' offset lists as a table of the distinct ones (a
 // Cartesian part has a handful: interior rows, the boundary planes' Dirichlet
 // rows): d_pat becomes that table and d_plen[s] of a pattern slice packs
-// its entries per row (low 8 bits, <= 255 by detection) with its table row
-// (bits 8-30).  A wave's pattern load then hits a small hot table instead of
+// its entries per row (bits 0-7, <= 255 by detection), the triple flag
+// (bit 8: every entry group is a consecutive column triple) and its table
+// row (bits 9-30).  A wave's pattern load then hits a small hot table instead of
 // one cold row per slice, and the slice metadata shrinks by kmax*4 B each.
 // A/B (one row per slice vs the table, profiles/r04/g/ab_pattern_dedup.jsonl):
 // FE27 256³ 0.6539 -> 0.6407 ms, FD7 128³ 0.02865 -> 0.02833 ms.
@@ -408,7 +411,7 @@ int finalize_pattern(pa_mat* A, int kmax, int64_t noids) {
   HIPC(hipMalloc((void**)&d_pghost, ns * 4));
   HIPC(hipMalloc((void**)&d_nirreg, ns * 4));
   HIPC(hipMemsetAsync(A->d_mask, 0, ns * W * 8, st));
-  const int min_pct = g_pattern_min_pct ? g_pattern_min_pct : (A->R == 4 ? 50 : 70);
+  const int min_pct = knobs().pattern_min_pct ? knobs().pattern_min_pct : (A->R == 4 ? 50 : 70);
   launch_pattern_detect(A, noids, min_pct, A->d_kind, A->d_plen, A->d_pat, A->d_mask, d_pghost, d_nirreg, st);
   HIPC(hipGetLastError());
   std::vector<int32_t> kind(ns), pghost(ns), nirreg(ns);
@@ -423,7 +426,7 @@ int finalize_pattern(pa_mat* A, int kmax, int64_t noids) {
   dev_free(d_pghost);
   dev_free(d_nirreg);
   if (dedup_patterns(A, kind)) return -1;
-  if (g_spmv_delta16) {  // int32-column slices whose columns fit 16-bit codes (kind 3)
+  if (knobs().spmv_delta16) {  // int32-column slices whose columns fit 16-bit codes (kind 3)
     int32_t* d_ok = nullptr;
     HIPC(hipMalloc((void**)&A->d_col16, std::max<int64_t>(A->slots, 1) * 2));
     HIPC(hipMalloc((void**)&A->d_gbase, ns * 4));
@@ -539,7 +542,7 @@ LocalSet local_set(int n, H* const* hs) {
   for (int i = 0; i < n; ++i) {
     const pa_ctx* c = hs[i]->ctx;
     maxp = std::max(maxp, c->nparts);
-    all_comm = all_comm && c->comm != nullptr && (c->halo_rccl || g_halo_transport == 1);
+    all_comm = all_comm && c->comm != nullptr && (c->halo_rccl || knobs().halo_transport == 1);
   }
   L.pos_of_part.assign(maxp + 1, -1);
   if (all_comm) return L;
@@ -778,7 +781,7 @@ int transport_plan(int n, pa_xchg* const xg[], int dtype, int dir, int op, pa_ve
   T->dir = dir;
   T->op = op;
   T->L = local_set(n, xg);
-  T->pull = v != nullptr && g_halo_pull;
+  T->pull = v != nullptr && knobs().halo_pull;
   for (int i = 0; i < n && T->pull; ++i) {
     if (build_pull(i, n, xg, T->L, dtype, dir)) return -1;
     T->pull = xg[i]->pull[dir].ok;
@@ -977,6 +980,7 @@ class IssuePool {
     {
       std::lock_guard<std::mutex> g(mu_);
       f_ = &f;
+      kn_ = &knobs();  // the calling thread's call: its jobs run with its knobs
       n_ = n;
       next_.store(0);
       finished_.store(0);
@@ -1002,9 +1006,20 @@ class IssuePool {
 
  private:
   static constexpr int kMaxWorkers = 15;
+  // A job's kernel launches report their errors to the thread that made
+  // them (HIP keeps the last error per thread): each job ends with this
+  // thread's hipGetLastError, so a launch that failed on a worker fails the
+  // call instead of being lost there.
   void work(const std::function<int(int)>* f, int n) {
     for (int i = next_.fetch_add(1); i < n; i = next_.fetch_add(1)) {
-      if ((*f)(i) != 0 && !failed_.exchange(true)) {
+      int rc = (*f)(i);
+      if (rc == 0 && knobs().fault_inject) launch_invalid_config();
+      const hipError_t e = hipGetLastError();
+      if (rc == 0 && e != hipSuccess) {
+        pa::set_error(std::string("kernel launch of an issue job failed: ") + hipGetErrorString(e));
+        rc = -1;
+      }
+      if (rc != 0 && !failed_.exchange(true)) {
         std::lock_guard<std::mutex> g(mu_);
         err_ = pa_last_error();
       }
@@ -1022,16 +1037,21 @@ class IssuePool {
             cv_.wait(g, [&] { return gen_.load() != seen; });
           }
           const std::function<int(int)>* f;
+          const Knobs* kn;
           int n;
           {
             std::lock_guard<std::mutex> g(mu_);
             seen = gen_.load();
             f = f_;
+            kn = kn_;
             n = n_;
             if (f) busy_.fetch_add(1);
           }
           if (!f) continue;  // woke after the call ended: wait for the next
-          work(f, n);
+          {
+            KnobBind kb(kn);
+            work(f, n);
+          }
           busy_.fetch_sub(1, std::memory_order_release);
         }
       });
@@ -1045,6 +1065,7 @@ class IssuePool {
   std::atomic<bool> failed_{false};
   std::string err_;
   const std::function<int(int)>* f_ = nullptr;  // the current call's job (under mu_)
+  const Knobs* kn_ = nullptr;                    // ... and its knobs
   int n_ = 0;
   std::vector<std::thread> workers_;
 };
@@ -1064,57 +1085,68 @@ int pa_version(void) { return 1; }
 
 // The tuning knobs (performance only, results unchanged): the process
 // defaults (pa_tune) and per-context overrides (pa_ctx_tune).  A call
-// applies the overrides of its first part's context for its duration
-// (TuneScope), so parts of one stream group always run with one setting.
+// resolves the overrides of its first part's context over the defaults into
+// its own Knobs (TuneScope), so parts of one stream group always run with
+// one setting and no global is written while a call runs.
 }  // extern "C"
 namespace {
 struct Knob {
   const char* key;
-  int* slot;           // process default (int knobs)
-  int64_t* slot64;     // ... or 64-bit
-  int64_t lo, hi;      // valid range
-  int64_t mask;        // spmv_flags: allowed bits (0: range only)
+  int Knobs::*slot;        // int knobs
+  int64_t Knobs::*slot64;  // ... or 64-bit
+  int64_t lo, hi;          // valid range
+  int64_t mask;            // spmv_flags: allowed bits (0: range only)
   const char* help;
 };
 const Knob kKnobs[] = {
-    {"spmv_flags", &g_spmv_flags, nullptr, 0, 0x7d, 0x7d,
+    {"spmv_flags", &Knobs::spmv_flags, nullptr, 0, 0x7d, 0x7d,
      "spmv_flags: bit 0 = non-temporal streams, "
      "bit 2 = 16 B x runs (pattern rows), bit 3 = masked tail batch, bit 4 = identity slice lists dropped, "
      "bit 5 = non-temporal y stores, bit 6 = short-row kernels (launches whose rows have <= 8 entries)"},
-    {"long_rows_exact", &g_long_exact, nullptr, 0, 1, 0,
+    {"long_rows_exact", &Knobs::long_exact, nullptr, 0, 1, 0,
      "long_rows_exact: 1 = reference summation order, 0 = lane-strided tree (1e-12)"},
-    {"halo_pull", &g_halo_pull, nullptr, 0, 1, 0,
+    {"halo_pull", &Knobs::halo_pull, nullptr, 0, 1, 0,
      "halo_pull: 1 = receivers read the senders' buffers (one kernel), 0 = staging copies"},
-    {"spmv_delta16", &g_spmv_delta16, nullptr, 0, 1, 0,
+    {"spmv_delta16", &Knobs::spmv_delta16, nullptr, 0, 1, 0,
      "spmv_delta16: 1 = int32-column slices whose columns fit 16-bit codes store those (matrices built "
      "afterwards; default), 0 = int32 column ids"},
-    {"spmv_merge", &g_spmv_merge, nullptr, 0, 1, 0,
+    {"spmv_merge", &Knobs::spmv_merge, nullptr, 0, 1, 0,
      "spmv_merge: 1 = mul! without a halo in flight (one part, or parts of one stream pair with the direct "
      "pull) runs every slice kind of every part as one launch (default), 0 = one launch per kind"},
-    {"spmv_merge_max", nullptr, &g_spmv_merge_max, 0, INT32_MAX, 0,
+    {"spmv_merge_max", nullptr, &Knobs::spmv_merge_max, 0, INT32_MAX, 0,
      "spmv_merge_max: one part with more slices than this runs one launch per kind (0: always merge)"},
-    {"cg_fuse", &g_cg_fuse, nullptr, 0, 2, 0,
+    {"cg_fuse", &Knobs::cg_fuse, nullptr, 0, 2, 0,
      "cg_fuse: 1 = the device CG computes u = r .+ beta.*u inside the SpMV, 0 = a separate sweep, "
      "2 = auto (default: one batch of each, then the faster; all parts in one process, else the sweep)"},
-    {"halo_direct", &g_halo_direct, nullptr, 0, 1, 0,
+    {"halo_direct", &Knobs::halo_direct, nullptr, 0, 1, 0,
      "halo_direct: 1 = mul! over parts sharing a stream pair reads the ghosts straight from the owners' x "
      "on the compute stream (default), 0 = pack + pull on the comm stream"},
-    {"halo_transport", &g_halo_transport, nullptr, 0, 1, 0,
+    {"halo_transport", &Knobs::halo_transport, nullptr, 0, 1, 0,
      "halo_transport: 0 = parts of this process by device reads/copies, 1 = RCCL send/recv for every part "
      "with a communicator (pa_comm_init_all)"},
-    {"spmv_group", &g_spmv_group, nullptr, 0, 1, 0,
+    {"spmv_group", &Knobs::spmv_group, nullptr, 0, 1, 0,
      "spmv_group: 1 = one launch per phase for parts sharing a stream pair, 0 = per part"},
-    {"spmv_format", &g_spmv_format, nullptr, 0, 1, 0, "spmv_format: 0 = int32 columns, 1 = pattern slices"},
-    {"pattern_min_regular", &g_pattern_min_pct, nullptr, 0, 100, 0,
+    {"spmv_format", &Knobs::spmv_format, nullptr, 0, 1, 0, "spmv_format: 0 = int32 columns, 1 = pattern slices"},
+    {"pattern_min_regular", &Knobs::pattern_min_pct, nullptr, 0, 100, 0,
      "pattern_min_regular: a slice becomes a pattern slice when at least this % of its rows follow its pattern "
      "(matrices built afterwards); 0 = auto (default): 70 for 128-row slices, 50 for Float32's 256-row slices"},
-    {"issue_threads", &g_issue_threads, nullptr, 0, 2, 0,
+    {"issue_threads", &Knobs::issue_threads, nullptr, 0, 2, 0,
      "issue_threads: a call over parts with their own stream pairs is issued from host threads, one part "
      "per thread: 1 = when the parts span several devices (default), 2 = always, 0 = never (the calling "
      "thread, one part after the other)"},
+    {"fault_inject", &Knobs::fault_inject, nullptr, 0, 1, 0,
+     "fault_inject: 1 = every job of a threaded issue (IssuePool) also issues an invalid kernel launch (tests "
+     "of the error path; test_exception.jl's role), 0 = off (default)"},
 };
 constexpr int kNumKnobs = (int)(sizeof(kKnobs) / sizeof(kKnobs[0]));
 static_assert(kNumKnobs <= pa_ctx::kMaxKnobs, "pa_ctx::over too small");
+
+// the process defaults: written by pa_tune, copied by every call's
+// TuneScope, both under g_knob_mu
+std::mutex g_knob_mu;
+Knobs g_knob_defaults = kDefaults;
+thread_local const Knobs* t_knobs = nullptr;   // the running call's knobs on this thread
+thread_local Knobs t_knob_snapshot;            // knobs() outside a call
 
 // the knob's index (-1: unknown key), value checked (-2: out of range)
 int knob_find(const char* key) {
@@ -1133,30 +1165,42 @@ int knob_index(const char* key, int64_t value) {
   }
   return i;
 }
-int64_t knob_get(int i) { return kKnobs[i].slot ? (int64_t)*kKnobs[i].slot : *kKnobs[i].slot64; }
-void knob_set(int i, int64_t v) {
-  if (kKnobs[i].slot) *kKnobs[i].slot = (int)v;
-  else *kKnobs[i].slot64 = v;
+int64_t knob_get(const Knobs& K, int i) { return kKnobs[i].slot ? (int64_t)(K.*kKnobs[i].slot) : K.*kKnobs[i].slot64; }
+void knob_set(Knobs& K, int i, int64_t v) {
+  if (kKnobs[i].slot) K.*kKnobs[i].slot = (int)v;
+  else K.*kKnobs[i].slot64 = v;
 }
 }  // namespace
 
+namespace pa {
+const Knobs& knobs() {
+  if (t_knobs) return *t_knobs;
+  std::lock_guard<std::mutex> g(g_knob_mu);
+  t_knob_snapshot = g_knob_defaults;
+  return t_knob_snapshot;
+}
+KnobBind::KnobBind(const Knobs* k) : prev(t_knobs) { t_knobs = k; }
+KnobBind::~KnobBind() { t_knobs = prev; }
+}  // namespace pa
+
 // For the duration of a call: the knobs of the call's context (its
-// overrides over the process defaults), restored on exit.
-TuneScope::TuneScope(const pa_ctx* c) {
-  if (!c) return;
-  for (int i = 0; i < kNumKnobs; ++i)
-    if (c->has_over[i]) {
-      if (!active) saved.assign(kNumKnobs, 0), set.assign(kNumKnobs, false), active = true;
-      saved[i] = knob_get(i);
-      set[i] = true;
-      knob_set(i, c->over[i]);
-    }
+// overrides over the process defaults) in the scope's own Knobs, current on
+// this thread (and on the IssuePool workers the call's jobs run on).  A call
+// nested in another (a library entry point calling another) keeps the outer
+// call's knobs.
+TuneScope::TuneScope(const pa_ctx* c) : prev(t_knobs) {
+  if (prev) {
+    k = *prev;
+  } else {
+    std::lock_guard<std::mutex> g(g_knob_mu);
+    k = g_knob_defaults;
+  }
+  if (c && !prev)
+    for (int i = 0; i < kNumKnobs; ++i)
+      if (c->has_over[i]) knob_set(k, i, c->over[i]);
+  t_knobs = &k;
 }
-TuneScope::~TuneScope() {
-  if (!active) return;
-  for (int i = 0; i < kNumKnobs; ++i)
-    if (set[i]) knob_set(i, saved[i]);
-}
+TuneScope::~TuneScope() { t_knobs = prev; }
 
 extern "C" {
 
@@ -1164,8 +1208,9 @@ int pa_tune(const char* key, int value, int* previous) {
   CHECK_ARG(key, "null key");
   const int i = knob_index(key, value);
   if (i < 0) return -1;
-  if (previous) *previous = (int)std::min<int64_t>(knob_get(i), INT32_MAX);
-  knob_set(i, value);
+  std::lock_guard<std::mutex> g(g_knob_mu);
+  if (previous) *previous = (int)std::min<int64_t>(knob_get(g_knob_defaults, i), INT32_MAX);
+  knob_set(g_knob_defaults, i, value);
   return 0;
 }
 
@@ -1176,6 +1221,48 @@ int pa_ctx_tune(pa_ctx* c, const char* key, int value, int* previous) {
   if (previous) *previous = c->has_over[i] ? (int)c->over[i] : -1;
   c->has_over[i] = value != -1;
   c->over[i] = value;
+  return 0;
+}
+
+// Test support, no device needed: `nthreads` host threads, each with its
+// own context whose override of "spmv_merge_max" is 1000 + t, resolve a
+// call's knobs `iters` times (TuneScope) and read them on the calling thread
+// and in IssuePool jobs, while the process default of the same knob changes
+// underneath; *mismatches counts the resolutions that saw a value other than
+// their own context's (0: the knobs of concurrent calls are independent).
+int pa_knob_selftest(int nthreads, int iters, int* mismatches) {
+  CHECK_ARG(nthreads >= 1 && nthreads <= 64 && iters >= 0 && mismatches, "bad arguments");
+  const int ki = knob_find("spmv_merge_max");
+  std::vector<std::unique_ptr<pa_ctx>> cs;
+  for (int t = 0; t < nthreads; ++t) {
+    cs.emplace_back(new pa_ctx());
+    cs.back()->has_over[ki] = true;
+    cs.back()->over[ki] = 1000 + t;
+  }
+  std::atomic<int> bad{0};
+  std::atomic<bool> stop{false};
+  std::thread tuner([&]() {  // the process default moves while the calls run
+    for (int v = 0; !stop.load(); v = (v + 1) % 997) (void)pa_tune("spmv_merge_max", v, nullptr);
+  });
+  std::vector<std::thread> ths;
+  for (int t = 0; t < nthreads; ++t)
+    ths.emplace_back([&, t]() {
+      for (int it = 0; it < iters; ++it) {
+        TuneScope ts(cs[t].get());
+        if (knobs().spmv_merge_max != 1000 + t) bad.fetch_add(1);
+        if (it % 16 == 0) {  // jobs on the pool's threads see the caller's knobs
+          (void)IssuePool::get().run(2, [&](int) -> int {
+            if (knobs().spmv_merge_max != 1000 + t) bad.fetch_add(1);
+            return 0;
+          });
+        }
+      }
+    });
+  for (auto& th : ths) th.join();
+  stop.store(true);
+  tuner.join();
+  (void)pa_tune("spmv_merge_max", (int)kDefaults.spmv_merge_max, nullptr);
+  *mismatches = bad.load();
   return 0;
 }
 
@@ -2627,7 +2714,7 @@ int pa_mat_traffic(const pa_mat* A, int64_t* value_bytes, int64_t* index_bytes, 
   CHECK_ARG(A, "null matrix");
   TuneScope ts(A->ctx);
   const int64_t S = (int64_t)dtype_size(A->dtype), H = A->H, W = H / 64;
-  const bool pat = g_spmv_format == 1 && A->has_pat;
+  const bool pat = knobs().spmv_format == 1 && A->has_pat;
   const bool split = A->d_bnd_list != nullptr;
   int64_t v = 0, ix = 0, m = 0;
   for (int64_t s = 0; s < A->nslices; ++s) {
@@ -2704,12 +2791,12 @@ static void cg_ghosts(const CGFuse* fz, int i, const pa_mat* A, const pa_vec* r,
 // the ghosts read straight from the owners' x on the compute stream, one
 // in-order chain without cross-stream events, pa_tune("halo_direct")).
 static int group_ok(int n, pa_mat* const A[], pa_xchg* const xg[], bool any_x, int dt) {
-  if (!g_spmv_group || (n < 2 && any_x)) return 0;  // one part without a halo: the merged launch
+  if (!knobs().spmv_group || (n < 2 && any_x)) return 0;  // one part without a halo: the merged launch
   const pa_ctx* c0 = A[0]->ctx;
   for (int i = 0; i < n; ++i)
     if (A[i]->ctx->s_main != c0->s_main || A[i]->ctx->s_comm != c0->s_comm) return 0;
   if (!any_x) return 1;
-  if (!g_halo_pull) return 0;
+  if (!knobs().halo_pull) return 0;
   LocalSet L = local_set(n, xg);
   for (int i = 0; i < n; ++i)
     for (const auto* lst : {&xg[i]->parts_snd, &xg[i]->parts_rcv})
@@ -2717,7 +2804,7 @@ static int group_ok(int n, pa_mat* const A[], pa_xchg* const xg[], bool any_x, i
         if (L.find(q) < 0) return 0;
   for (int i = 0; i < n; ++i)
     if (!xg[i]->plan_fwd.unique) return 0;
-  if (g_halo_direct) {
+  if (knobs().halo_direct) {
     bool ok = true;
     for (int i = 0; i < n && ok; ++i) {
       if (build_direct(i, n, xg, L)) return 0;
@@ -2838,9 +2925,9 @@ static int spmv_grouped(int n, pa_mat* const A[], pa_vec* const y[], const pa_in
   // kind of every part in one launch — side rows and int32 slices first, so
   // their few long waves start early, then delta16, multi-pattern, pattern
   int merged = 1;
-  bool big_part = false;  // one part alone fills the GPU many times: per-kind launches (g_spmv_merge_max)
-  if (g_spmv_merge_max > 0 && n == 1) big_part = A[0]->nslices > g_spmv_merge_max;
-  if (g_spmv_merge && !big_part && (!any_x || direct)) {
+  bool big_part = false;  // one part alone fills the GPU many times: per-kind launches (knobs().spmv_merge_max)
+  if (knobs().spmv_merge_max > 0 && n == 1) big_part = A[0]->nslices > knobs().spmv_merge_max;
+  if (knobs().spmv_merge && !big_part && (!any_x || direct)) {
     std::vector<SpmvPart> E;
     std::vector<int> W;
     auto add = [&](int which, int i, int64_t nwork, const int32_t* list) {
@@ -2849,9 +2936,9 @@ static int spmv_grouped(int n, pa_mat* const A[], pa_vec* const y[], const pa_in
       W.push_back(which);
     };
     for (int i = 0; i < n; ++i)
-      if (g_spmv_format == 1 && A[i]->has_pat) add(2, i, A[i]->s_nslices, nullptr);
+      if (knobs().spmv_format == 1 && A[i]->has_pat) add(2, i, A[i]->s_nslices, nullptr);
     for (int i = 0; i < n; ++i) {
-      if (g_spmv_format == 1 && A[i]->has_pat) {
+      if (knobs().spmv_format == 1 && A[i]->has_pat) {
         add(1, i, A[i]->nx_int, A[i]->d_xint_list);
         add(1, i, A[i]->nx_bnd, A[i]->d_xbnd_list);
       } else if (A[i]->d_bnd_list) {
@@ -2862,12 +2949,12 @@ static int spmv_grouped(int n, pa_mat* const A[], pa_vec* const y[], const pa_in
       }
     }
     for (int i = 0; i < n; ++i)
-      if (g_spmv_format == 1 && A[i]->has_pat) {
+      if (knobs().spmv_format == 1 && A[i]->has_pat) {
         add(4, i, A[i]->nd_int, A[i]->d_dint_list);
         add(4, i, A[i]->nd_bnd, A[i]->d_dbnd_list);
       }
     for (int i = 0; i < n; ++i)
-      if (g_spmv_format == 1 && A[i]->has_pat) {
+      if (knobs().spmv_format == 1 && A[i]->has_pat) {
         add(0, i, A[i]->np_int, A[i]->d_pint_list);
         add(0, i, A[i]->np_bnd, A[i]->d_pbnd_list);
       }
@@ -2879,7 +2966,7 @@ static int spmv_grouped(int n, pa_mat* const A[], pa_vec* const y[], const pa_in
   if (merged) {
   // interior slices (no ghost column): overlap with the pulls on the comm stream
   for (int i = 0; i < n; ++i) {
-    if (g_spmv_format == 1 && A[i]->has_pat) {
+    if (knobs().spmv_format == 1 && A[i]->has_pat) {
       P0.push_back(part(i, A[i]->np_int, A[i]->d_pint_list));
       P1.push_back(part(i, A[i]->nx_int, A[i]->d_xint_list));
       P4.push_back(part(i, A[i]->nd_int, A[i]->d_dint_list));
@@ -2898,7 +2985,7 @@ static int spmv_grouped(int n, pa_mat* const A[], pa_vec* const y[], const pa_in
   P0.clear(); P1.clear(); P4.clear();
   std::vector<SpmvPart> P2;
   for (int i = 0; i < n; ++i) {
-    if (g_spmv_format == 1 && A[i]->has_pat) {
+    if (knobs().spmv_format == 1 && A[i]->has_pat) {
       P0.push_back(part(i, A[i]->np_bnd, A[i]->d_pbnd_list));
       P4.push_back(part(i, A[i]->nd_bnd, A[i]->d_dbnd_list));
       P1.push_back(part(i, A[i]->nx_bnd, A[i]->d_xbnd_list));
@@ -2914,7 +3001,7 @@ static int spmv_grouped(int n, pa_mat* const A[], pa_vec* const y[], const pa_in
   }  // per-kind launches
   for (int i = 0; i < n; ++i) {
     const int32_t* ymap = y_idx[i]->own_contig ? nullptr : y_idx[i]->d_oid_to_lid;
-    const bool pat = g_spmv_format == 1 && A[i]->has_pat;
+    const bool pat = knobs().spmv_format == 1 && A[i]->has_pat;
     const int64_t long_base = A[i]->nslices + (pat ? A[i]->s_nslices : 0);
     cg_ghosts(fz, i, A[i], x[i], sm);
     launch_spmv_long(A[i], x[i]->d, y[i]->d, ymap, has_alpha, bmode, alpha, beta, dotp[i], long_base, sm);
@@ -2955,7 +3042,7 @@ static int launch_phase(int phase, pa_mat* A, const void* x, void* y, const int3
     E.push_back(q);
     W.push_back(which);
   };
-  if (g_spmv_format == 1 && A->has_pat) {
+  if (knobs().spmv_format == 1 && A->has_pat) {
     if (phase == 0) {
       add(1, A->nx_int, A->d_xint_list);
       add(4, A->nd_int, A->d_dint_list);
@@ -2973,7 +3060,7 @@ static int launch_phase(int phase, pa_mat* A, const void* x, void* y, const int3
     add(1, A->nslices, nullptr);
   }
   if (E.empty()) return 0;
-  if (E.size() > 1 && g_spmv_merge && !(g_spmv_merge_max > 0 && A->nslices > g_spmv_merge_max)) {
+  if (E.size() > 1 && knobs().spmv_merge && !(knobs().spmv_merge_max > 0 && A->nslices > knobs().spmv_merge_max)) {
     const int rc = launch_spmv_merged((int)E.size(), W.data(), E.data(), has_alpha, bmode, alpha, beta, A->ctx,
                                       g_capture_tables, st);
     if (rc < 0) PA_FAIL("mul!: merged launch table (device allocation or copy) failed");
@@ -3079,7 +3166,7 @@ static int spmv_impl(int n, pa_mat* const A[], pa_vec* const y[], const pa_index
     if (launch_phase(1, A[i], x[i]->d, y[i]->d, ymap, has_alpha, bmode, alpha, beta, dotp[i], SM(c), fz, i)) return -1;
     cg_ghosts(fz, i, A[i], x[i], SM(c));
     // long rows (after the halo: they may read ghost columns)
-    const bool pat = g_spmv_format == 1 && A[i]->has_pat;
+    const bool pat = knobs().spmv_format == 1 && A[i]->has_pat;
     const int64_t long_base = A[i]->nslices + (pat ? A[i]->s_nslices : 0);
     launch_spmv_long(A[i], x[i]->d, y[i]->d, ymap, has_alpha, bmode, alpha, beta, dotp[i], long_base, SM(c));
     if (want_dot) {  // fold the partials (main slices, side slices, long rows) in order
@@ -3104,14 +3191,14 @@ static int spmv_impl(int n, pa_mat* const A[], pa_vec* const y[], const pa_index
   // one device the parts' streams share its hardware queues and the serial
   // order keeps the device time lower (1.44 vs 1.70 ms for 8 parts of the
   // 256³ (2,2,2) problem, profiles/r04/k/host_issue_3round.json); 2: always
-  bool threads = g_issue_threads && n >= 2 && !g_capture_stream;
+  bool threads = knobs().issue_threads && n >= 2 && !g_capture_stream;
   bool multi_dev = false;
   for (int i = 0; threads && i < n; ++i) {
     multi_dev = multi_dev || A[i]->ctx->device != A[0]->ctx->device;
     for (int j = 0; j < i; ++j)
       if (A[i]->ctx->s_main == A[j]->ctx->s_main || A[i]->ctx->s_comm == A[j]->ctx->s_comm) threads = false;
   }
-  if (g_issue_threads == 1 && !multi_dev) threads = false;
+  if (knobs().issue_threads == 1 && !multi_dev) threads = false;
   TransportPlan T;
   if (any_x && transport_plan(n, xg, dt, 0, PA_REPLACE, x, &T)) return -1;
   if (threads && !(any_x && T.remote)) {
@@ -3202,11 +3289,11 @@ int pa_spmv_graph_create(int n, pa_mat* const A[], pa_vec* const y[], const pa_i
     }
   }
   HIPC(hipSetDevice(dev));
-  if (xg && g_halo_pull) {  // lazily built device tables must exist before the capture
+  if (xg && knobs().halo_pull) {  // lazily built device tables must exist before the capture
     LocalSet L = local_set(n, xg);
     for (int i = 0; i < n; ++i)
       if (build_pull(i, n, xg, L, A[0]->dtype, 0)) return -1;
-    if (g_halo_direct) {
+    if (knobs().halo_direct) {
       for (int i = 0; i < n; ++i)
         if (build_direct(i, n, xg, L)) return -1;
       if (!direct_bases(A[0]->ctx, n, x)) return -1;
@@ -3654,7 +3741,7 @@ int pa_cg_solve_all(int n, pa_mat* const A[], pa_vec* const x[], const pa_vec* c
   // directly).
   bool can_fuse = true;
   for (int i = 0; i < n; ++i) can_fuse = can_fuse && A[i]->n_long == 0;
-  int mode = can_fuse ? g_cg_fuse : 0;
+  int mode = can_fuse ? knobs().cg_fuse : 0;
   if (mode == 2 && (R.remote || maxiter < 3 * (int64_t)batch)) mode = A[0]->cg_fuse_choice >= 0 ? A[0]->cg_fuse_choice : 0;
   if (mode == 2 && A[0]->cg_fuse_choice >= 0) mode = A[0]->cg_fuse_choice;
   std::vector<pa_vec*> u2(n, nullptr);

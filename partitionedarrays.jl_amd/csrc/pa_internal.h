@@ -314,15 +314,49 @@ struct pa_ctx {
   int64_t over[kMaxKnobs] = {};
 };
 
+// The tuning knobs of one call (performance only, results unchanged; the
+// table with their meaning is kKnobs in pa_api.cpp).  A call resolves them
+// once — the process defaults (pa_tune) under its first part's context
+// overrides (pa_ctx_tune) — into its own Knobs, which the launchers and the
+// IssuePool jobs of that call read through pa::knobs(): no process-global
+// knob is written while a call runs, so concurrent calls from several host
+// threads each see their own context's values.
+namespace pa {
+struct Knobs {
+  int spmv_flags;        // SPMV_* bits of pa_spmv.hip
+  int long_exact;
+  int halo_pull;
+  int spmv_delta16;
+  int spmv_merge;
+  int64_t spmv_merge_max;
+  int cg_fuse;
+  int halo_direct;
+  int halo_transport;
+  int spmv_group;
+  int spmv_format;
+  int pattern_min_pct;
+  int issue_threads;
+  int fault_inject;      // tests only: the IssuePool jobs issue an invalid launch
+};
+// the knobs of the call running on this thread (outside a call: a snapshot
+// of the process defaults)
+const Knobs& knobs();
+// this thread runs work of a call whose knobs are *k (IssuePool workers)
+struct KnobBind {
+  explicit KnobBind(const Knobs* k);
+  ~KnobBind();
+  const Knobs* prev;
+};
+}  // namespace pa
+
 // the knobs of a call's (first part's) context for the call's duration
 struct TuneScope {
   explicit TuneScope(const pa_ctx* c);
   ~TuneScope();
   TuneScope(const TuneScope&) = delete;
   TuneScope& operator=(const TuneScope&) = delete;
-  bool active = false;
-  std::vector<int64_t> saved;
-  std::vector<bool> set;
+  pa::Knobs k;
+  const pa::Knobs* prev;
 };
 
 struct pa_index {
@@ -470,7 +504,7 @@ struct pa_mat {
   bool has_pat = false;
   int kmax = 0;                      // pattern stride per slice
   int32_t* d_kind = nullptr;         // per slice: 1 pattern, 0 int32 columns
-  int32_t* d_plen = nullptr;         // per slice: entries per row (int32 len; pattern slices: len | pattern id << 8)
+  int32_t* d_plen = nullptr;         // per slice: entries per row (int32 len; pattern slices: len (bits 0-7) | tri flag (bit 8) | pattern id << 9)
   int32_t* d_pat = nullptr;          // npatterns*kmax offsets: the distinct patterns (dedup_patterns)
   int64_t npatterns = 0;
   uint64_t* d_mask = nullptr;        // nslices*(H/64) regular-row bits

@@ -15,6 +15,12 @@ namespace pa {
 
 // SELL SpMV kernels: pa_spmv.hip
 
+// pa_tune("fault_inject"): a launch the runtime rejects before anything runs
+// (more threads per block than the hardware allows): the error path of the
+// threaded issue, tested without a faulting kernel
+__global__ void k_never_runs() {}
+void launch_invalid_config() { hipLaunchKernelGGL(k_never_runs, dim3(1), dim3(4096), 0, nullptr); }
+
 // ---------------------------------------------------------------------------
 // Halo pack / unpack (Interfaces.jl:858-866 and 878-886).
 

@@ -60,17 +60,15 @@ typedef unsigned int spmv_u32x4 __attribute__((ext_vector_type(4)));
 // F32 −33 %, C64 −5 % kernel time), predicated tail batch on
 // (profiles/r01/ab_tail.txt: FD7 256³ F64 −31 %, F32 −42 %; FE27 −1…−3 %),
 // identity slice lists dropped (profiles/r01/ab_idlist.txt: FD7 −0.9 %, FE27 ±0).
+// (the knob defaults: pa_api.cpp kDefaults; spmv_flags 93 = NT | XPAIR |
+// TAILB | IDLIST | SHORT)
+static_assert((SPMV_NT | SPMV_XPAIR | SPMV_TAILB | SPMV_IDLIST | SPMV_SHORT) == 93, "kDefaults.spmv_flags");
 #if PA_DT_DEFINE
-int g_spmv_flags = SPMV_NT | SPMV_XPAIR | SPMV_TAILB | SPMV_IDLIST | SPMV_SHORT;
-int g_spmv_format = 1;  // 1: pattern slices where built, 0: int32 columns only
 // merged-launch tables allocated during a graph capture, copied after it ends
 // (no copies while a stream is being captured)
 std::vector<std::pair<void*, std::vector<char>>> g_capture_uploads;
-int g_long_exact = 1;  // pa_tune("long_rows_exact")
 #else
-extern int g_spmv_flags, g_spmv_format;
 extern std::vector<std::pair<void*, std::vector<char>>> g_capture_uploads;
-extern int g_long_exact;
 #endif
 
 // SpmvArgs' pointers are global memory.  The merged launch reads them from a
@@ -898,7 +896,7 @@ template <typename T, int R, bool ALPHA, int BMODE, int PAT>
 static void launch_group_t(const SpmvGroup<T>& g, hipStream_t st) {
   const int64_t blocks = (g.start[g.np] + 3) / 4;
   if (blocks == 0) return;
-  bool sh = (g_spmv_flags & SPMV_SHORT) != 0;
+  bool sh = (knobs().spmv_flags & SPMV_SHORT) != 0;
   for (int i = 0; i < g.np; ++i) sh = sh && g.a[i].maxlen <= 8;
   if constexpr (!ALPHA && BMODE == 0) {
     if (g.a[0].cg) {  // the device CG's fused u update
@@ -934,14 +932,14 @@ static void launch_t(const SpmvArgs<T>& a, hipStream_t st) {
   if (blocks == 0) return;
   if constexpr (!ALPHA && BMODE == 0) {
     if (a.cg) {  // the device CG's fused u update
-      if ((g_spmv_flags & SPMV_SHORT) && a.maxlen <= 8)
+      if ((knobs().spmv_flags & SPMV_SHORT) && a.maxlen <= 8)
         hipLaunchKernelGGL((k_spmv_sell<T, R, false, 0, 8, PAT, true, true>), dim3(blocks), dim3(256), 0, st, a);
       else
         hipLaunchKernelGGL((k_spmv_sell<T, R, false, 0, 8, PAT, false, true>), dim3(blocks), dim3(256), 0, st, a);
       return;
     }
   }
-  if ((g_spmv_flags & SPMV_SHORT) && a.maxlen <= 8)
+  if ((knobs().spmv_flags & SPMV_SHORT) && a.maxlen <= 8)
     hipLaunchKernelGGL((k_spmv_sell<T, R, ALPHA, BMODE, 8, PAT, true>), dim3(blocks), dim3(256), 0, st, a);
   else
     hipLaunchKernelGGL((k_spmv_sell<T, R, ALPHA, BMODE, 8, PAT>), dim3(blocks), dim3(256), 0, st, a);
@@ -985,10 +983,10 @@ static SpmvArgs<T> make_args(int which, int64_t nwork, const int32_t* list, cons
   a.ymap = (decltype(a.ymap))(ymap);
   a.alpha = *(const T*)alpha;
   a.beta = *(const T*)beta;
-  a.flags = g_spmv_flags | (A->csr ? SPMV_PRODA : 0);
+  a.flags = knobs().spmv_flags | (A->csr ? SPMV_PRODA : 0);
   a.maxlen = which == 0   ? A->maxlen_pat
              : which == 2 ? A->maxlen_side
-             : which == 1 ? ((g_spmv_format == 1 && A->has_pat) ? A->maxlen_pm_int : A->maxlen_all)
+             : which == 1 ? ((knobs().spmv_format == 1 && A->has_pat) ? A->maxlen_pm_int : A->maxlen_all)
              : which == 4 ? A->maxlen_d16
                           : INT32_MAX;
   if (which == 2) {
@@ -1020,7 +1018,7 @@ static SpmvArgs<T> make_args(int which, int64_t nwork, const int32_t* list, cons
     a.sflags = (decltype(a.sflags))(A->d_sflags);
     a.lmask = (decltype(a.lmask))(A->d_lmask);
     // spmv_format 0 runs the delta16 slices (Float32: interleaved rows) as int32
-    if (A->d_col16 && A->R == 4 && !(g_spmv_format == 1 && A->has_pat)) a.ilv = (decltype(a.ilv))(A->d_kind);
+    if (A->d_col16 && A->R == 4 && !(knobs().spmv_format == 1 && A->has_pat)) a.ilv = (decltype(a.ilv))(A->d_kind);
   }
   return a;
 }
@@ -1051,7 +1049,7 @@ static void group_which(int which, int np, const SpmvPart* parts, bool has_alpha
     const SpmvPart& q = parts[i];
     if (q.nwork <= 0) continue;
     const int32_t* list = q.list;
-    if ((g_spmv_flags & SPMV_IDLIST) && list && which != 2 && q.nwork == q.A->nslices) list = nullptr;
+    if ((knobs().spmv_flags & SPMV_IDLIST) && list && which != 2 && q.nwork == q.A->nslices) list = nullptr;
     g.a[g.np] = make_args<T>(which, q.nwork, list, q.A, q.x, q.y, q.ymap, alpha, beta, q.dotp, &q);
     g.start[g.np + 1] = g.start[g.np] + q.nwork;
     if (++g.np == PA_GROUP_MAX) flush();
@@ -1191,13 +1189,13 @@ static int merged_t(int n, const int* which, const SpmvPart* parts, bool has_alp
                     const void* beta, pa_ctx* owner, std::vector<void*>* pinned, hipStream_t st) {
   SpmvTable<T> h;
   std::memset(&h, 0, sizeof(h));  // the table's bytes are its cache key
-  bool sh = (g_spmv_flags & SPMV_SHORT) != 0;
+  bool sh = (knobs().spmv_flags & SPMV_SHORT) != 0;
   for (int i = 0; i < n; ++i) {
     const SpmvPart& q = parts[i];
     if (q.nwork <= 0) continue;
     if (h.n == kMergeMax) return 1;
     const int32_t* list = q.list;
-    if ((g_spmv_flags & SPMV_IDLIST) && list && which[i] != 2 && q.nwork == q.A->nslices) list = nullptr;
+    if ((knobs().spmv_flags & SPMV_IDLIST) && list && which[i] != 2 && q.nwork == q.A->nslices) list = nullptr;
     h.a[h.n] = make_args<T>(which[i], q.nwork, list, q.A, q.x, q.y, q.ymap, alpha, beta, q.dotp, &q);
     h.pk[h.n] = pk_of(which[i]);
     sh = sh && h.a[h.n].maxlen <= 8;
@@ -1426,7 +1424,7 @@ static void long_t(const pa_mat* A, const void* x, void* y, const int32_t* ymap,
                    void* dotp, int64_t dot_base, hipStream_t st) {
   const T* val = (const T*)A->d_val + A->long_off;
   const T al = *(const T*)alpha, be = *(const T*)beta;
-  if (g_long_exact) {
+  if (knobs().long_exact) {
     hipLaunchKernelGGL((k_spmv_long_exact<T, ALPHA, BMODE>), dim3((unsigned)A->n_long), dim3(64), 0, st, A->n_long,
                        A->d_long_row, A->d_long_ptr, A->d_long_col, val, (const T*)x, (T*)y, ymap, al, A->csr, be,
                        (const T*)x, dotp, dot_base);
@@ -1484,7 +1482,7 @@ void launch_spmv_part(int which, int64_t nwork, const int32_t* list, const pa_ma
                       const void* beta, void* dotp, hipStream_t st, const SpmvPart* cgp) {
   // a slice list as long as the structure is 0..nslices-1 (lists are
   // ascending subsets): launch without it, one dependent load less per wave
-  if ((g_spmv_flags & SPMV_IDLIST) && list && which != 2 && nwork == A->nslices) list = nullptr;
+  if ((knobs().spmv_flags & SPMV_IDLIST) && list && which != 2 && nwork == A->nslices) list = nullptr;
 #define spmv_part_(k) spmv_part_##k(which, nwork, list, A, x, y, ymap, has_alpha, bmode, alpha, beta, dotp, st, cgp)
   switch (A->dtype) {
     case PA_F32: spmv_part_(0); break;

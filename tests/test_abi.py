@@ -63,7 +63,7 @@ def test_tune_knobs_round_trip_and_reject_bad_values(pamd):
     per-matrix CSR flag) out of the user's reach."""
     knobs = {"spmv_merge": 0, "spmv_merge_max": 1024, "spmv_group": 0, "spmv_delta16": 0,
              "long_rows_exact": 0, "halo_direct": 0, "cg_fuse": 1, "halo_pull": 0, "spmv_format": 0,
-             "issue_threads": 0, "pattern_min_regular": 90}
+             "issue_threads": 0, "pattern_min_regular": 90, "fault_inject": 1}
     for k, v in knobs.items():
         prev = pamd._lib.tune(k, v)
         assert pamd._lib.tune(k, prev) == v, k
@@ -93,3 +93,15 @@ def test_tune_knobs_round_trip_and_reject_bad_values(pamd):
             raise AssertionError(f"{k} still accepted")
         except pamd.PAError:
             pass
+
+
+def test_knobs_of_concurrent_calls_are_independent(pamd):
+    """Each call resolves its knobs (process defaults under its context's
+    overrides) into its own Knobs instead of swapping process globals
+    (ADVICE r04): 4 and 8 host threads with different
+    context values, read on the caller and on the IssuePool's threads while
+    another thread moves the process default, never see another call's
+    value."""
+    for nthreads in (4, 8):
+        assert pamd._lib.knob_selftest(nthreads, 3000) == 0
+    assert pamd._lib.tune("spmv_merge_max", 65536) == 65536  # the selftest restored the default

@@ -46,6 +46,13 @@ def _worker(rank, world, port, shape, N, kind, q):
             out["exchange"] = pamd.exchange(data, prcv, psnd).parts[0]
             out["discover"] = [int(v) for v in pamd.discover_parts_snd(prcv).parts[0]]
             out["discover_gather"] = [int(v) for v in pamd.discover_parts_snd(prcv, method="gather").parts[0]]
+            # a non-gloo host group (nccl): alltoall falls back to the object all-gather
+            real = dist.get_backend
+            dist.get_backend = lambda group=None: "nccl"
+            try:
+                out["discover_obj"] = [int(v) for v in pamd.discover_parts_snd(prcv).parts[0]]
+            finally:
+                dist.get_backend = real
         g = pamd.gather(pamd.map_parts(lambda p: 10 * p, parts))
         out["gather"] = g.parts[0]
         out["scatter"] = pamd.scatter(pamd.map_parts(lambda p: [p * 100 for p in range(1, world + 1)] if p == 1 else [], parts)).parts[0]
@@ -106,6 +113,7 @@ def test_distributed_setup_matches_sequential(pamd, O, world, shape, N, kind):
             assert out["exchange"] == GOLD["exchange_scalar"]["expected_rcv"][r]
             assert out["discover"] == GOLD["discover"]["expected_parts_snd"][r]
             assert out["discover_gather"] == GOLD["discover"]["expected_parts_snd"][r]
+            assert out["discover_obj"] == GOLD["discover"]["expected_parts_snd"][r]
         s = cols.partition.local(p)
         assert out["lid_to_gid"] == s.lid_to_gid.tolist() == OA.cols.partition[p].lid_to_gid
         assert out["parts_rcv"] == cols.exchanger.parts_rcv.local(p).tolist()

@@ -1,6 +1,6 @@
 """BASELINE config 5 on the device: the 27-pt FE operator on an irregular
 Voronoi ("METIS-like") partition — non-box owned sets, first-touch ghosts,
-an Exchanger from the gather-based discover — for Float64, Float32,
+an Exchanger from the all-to-all discover (prange.discover_parts_snd) — for Float64, Float32,
 ComplexF64 (and ComplexF32).  SpMV, exchange! and assemble! bit-exact
 against the oracle at 128³; dot/norm to 1e-12."""
 import numpy as np

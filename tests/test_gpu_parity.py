@@ -399,3 +399,36 @@ def test_threaded_issue_matches_sequential(pamd, O):
     for a, b in zip(out[0][1], out[2][1]):
         assert np.array_equal(a, b)
     assert out[0][2] == out[2][2]
+
+
+def test_threaded_issue_reports_launch_failures(pamd, O):
+    """A kernel launch that fails inside a threaded-issue job (pa_tune
+    fault_inject: each job also issues a launch the runtime rejects) makes
+    mul! raise instead of returning with y unwritten, whichever thread ran
+    the job (HIP keeps the last error per thread); the next
+    call without the fault is correct (no sticky error on the workers)."""
+    shape, N = (2, 2, 1), (10, 9, 8)
+    prev = pamd._lib.tune("issue_threads", 2)
+    try:
+        be = pamd.HIPBackend(devices=[0], share_streams=False)
+        parts = be.get_part_ids(shape)
+        A = pamd.drivers.stencil_operator(parts, N, 27)
+        rng = np.random.default_rng(SEED + 11)
+        x = pamd.PVector.from_host(pamd.map_parts(lambda s: rng.uniform(-1, 1, s.num_lids), A.cols.partition), A.cols)
+        y = pamd.PVector.undef(A.rows).fill_(0.0)
+        pamd._lib.tune("fault_inject", 1)
+        try:
+            with pytest.raises(pamd.PAError, match="issue job failed"):
+                pamd.mul_(y, A, x)
+        finally:
+            pamd._lib.tune("fault_inject", 0)
+        pamd.mul_(y, A, x)
+        OA = O.stencil_problem(O.get_part_ids(shape), N, 27)
+        ox = O.PVector(O.map_parts(lambda s: x.to_host().local(s.part).copy(), OA.cols.partition), OA.cols)
+        oy = O.pvector_undef(OA.rows, np.float64)
+        O.mul_(oy, OA, ox)
+        for p in parts.part_ids:
+            own = A.rows.partition.local(p).oid_to_lid - 1
+            assert np.array_equal(y.to_host().local(p)[own], oy.values[p][own]), p
+    finally:
+        pamd._lib.tune("issue_threads", prev)
