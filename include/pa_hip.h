@@ -357,6 +357,14 @@ int pa_mat_format_info(const pa_mat* A, int64_t* pattern_slices,
  * signed 15-bit delta, a ghost column as the slice's smallest ghost column
  * + 15 bits — stream 2 B of column id per slot instead of 4.              */
 int pa_mat_delta16_info(const pa_mat* A, int64_t* delta16_slices);
+/* The triple SELL (pa_tune "spmv_tri16": 1 = Float64 / ComplexF32 /
+ * ComplexF64, the default; 2 = every element type): the delta16 slices'
+ * rows re-sliced — rows whose columns are consecutive triples (c, c+1, c+2)
+ * first — so that most slices keep one 16-bit code per triple and read a
+ * triple's x as one run.  Its slices and rows, and how many of them are
+ * triple slices (tri_slices, their rows tri_rows).                       */
+int pa_mat_triple_info(const pa_mat* A, int64_t* t_slices, int64_t* t_rows, int64_t* tri_slices,
+                       int64_t* tri_rows);
 
 /* device addresses of the matrix's main arrays, for placement diagnostics:
  * out[0..7] = values, int32 columns, slice offsets, slice lengths (pattern),
@@ -443,6 +451,19 @@ int pa_cg_solve_all(int n, pa_mat* const A[], pa_vec* const x[],
                     const pa_index* const idx[], pa_xchg* const xg[],
                     double reltol, double abstol, int64_t maxiter, int batch,
                     int64_t* iterations, double* residual, double* history);
+
+/* The u-update variant choice of pa_cg_solve_all's auto mode (pa_tune
+ * "cg_fuse" 2): the first timed batch runs the sweep, the second the fused
+ * update; with one part per process (RCCL) every rank reduces the two
+ * batch times with max over the ranks before choosing, so all ranks keep
+ * the same variant.  pa_cg_variant_agree runs that decision on local_ms
+ * (ms per iteration of the sweep and of the fused batch) with `fn` as the
+ * all-reduce (max, in place on n floats; null: none), *choice = 1 fused,
+ * 0 sweep, -1 no valid measurement.  pa_mat_cg_choice: the variant the
+ * matrix remembers (-1: none yet).                                        */
+typedef int (*pa_allreduce_max_fn)(float* v, int n, void* user);
+int pa_cg_variant_agree(const float local_ms[2], pa_allreduce_max_fn fn, void* user, int* choice);
+int pa_mat_cg_choice(const pa_mat* A, int* choice);
 
 /* exchange!(combine, values, exchanger) (Interfaces.jl:846-889) for the n
  * local parts; reverse != 0 uses reverse(exchanger) (Interfaces.jl:796).

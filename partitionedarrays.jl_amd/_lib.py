@@ -39,6 +39,8 @@ _SIGS = {
     "pa_tune": [C.c_char_p, C.c_int, C.POINTER(C.c_int)],
     "pa_ctx_tune": [_p, C.c_char_p, C.c_int, C.POINTER(C.c_int)],
     "pa_knob_selftest": [C.c_int, C.c_int, C.POINTER(C.c_int)],
+    "pa_cg_variant_agree": [C.POINTER(C.c_float), _p, _p, C.POINTER(C.c_int)],
+    "pa_mat_cg_choice": [_p, C.POINTER(C.c_int)],
     "pa_hbm_probe": [C.c_int, C.c_int64, C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_double)],
     "pa_ctx_create": [C.c_int, C.c_int, C.c_int, C.POINTER(_p)],
     "pa_ctx_create_shared": [C.c_int, C.c_int, _p, C.POINTER(_p)],
@@ -86,6 +88,7 @@ _SIGS = {
     "pa_mat_info": [_p, _i64p, _i64p, _i64p, _i64p, _i64p],
     "pa_mat_format_info": [_p, _i64p, _i64p, _i64p, _i64p],
     "pa_mat_delta16_info": [_p, _i64p],
+    "pa_mat_triple_info": [_p, _i64p, _i64p, _i64p, _i64p],
     "pa_mat_long_rows": [_p, _i64p, _i64p],
     "pa_mat_stencil": [_p, C.c_int, C.c_int, _i64p, _i64p, _i64p, C.c_int64, _i32p, C.POINTER(C.c_double), C.c_int, C.POINTER(_p)],
     "pa_spmv_all": [C.c_int, C.POINTER(_p), C.POINTER(_p), C.POINTER(_p), C.POINTER(_p), C.POINTER(_p), C.POINTER(_p), _p, _p],
@@ -186,6 +189,32 @@ def knob_selftest(nthreads: int = 4, iters: int = 2000) -> int:
     n = C.c_int(-1)
     call("pa_knob_selftest", int(nthreads), int(iters), C.byref(n))
     return n.value
+
+
+ALLREDUCE_MAX_FN = C.CFUNCTYPE(C.c_int, C.POINTER(C.c_float), C.c_int, C.c_void_p)
+
+
+def cg_variant_agree(local_ms, allreduce_max=None) -> int:
+    """pa_cg_variant_agree: the device CG's auto u-update choice (1 fused,
+    0 sweep, -1 none) from this rank's two batch times (ms per iteration:
+    sweep, fused), reduced with `allreduce_max(list of 2 floats) -> list`
+    over the ranks first (the library's RCCL reduction's role; None: one
+    process)."""
+    ms = (C.c_float * 2)(*[float(v) for v in local_ms])
+    cb = None
+    if allreduce_max is not None:
+        def _cb(v, n, _user):
+            try:
+                out = allreduce_max([v[i] for i in range(n)])
+                for i in range(n):
+                    v[i] = float(out[i])
+                return 0
+            except Exception:  # reported as a PAError by the library
+                return 1
+        cb = ALLREDUCE_MAX_FN(_cb)
+    ch = C.c_int(-3)
+    call("pa_cg_variant_agree", ms, C.cast(cb, C.c_void_p) if cb else None, None, C.byref(ch))
+    return ch.value
 
 
 def hbm_probe(device: int = 0, nbytes: int = 2 << 30, reps: int = 10):

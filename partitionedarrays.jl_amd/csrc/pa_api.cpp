@@ -88,7 +88,7 @@ void launch_gather_ptrs(int P, const void* const* srcs, int accsz, void* out, hi
 const Knobs kDefaults = {
     /*spmv_flags*/ 93, /*long_exact*/ 1, /*halo_pull*/ 1, /*spmv_delta16*/ 1, /*spmv_merge*/ 1,
     /*spmv_merge_max*/ 65536, /*cg_fuse*/ 2, /*halo_direct*/ 1, /*halo_transport*/ 0, /*spmv_group*/ 1,
-    /*spmv_format*/ 1, /*pattern_min_pct*/ 0, /*issue_threads*/ 1, /*fault_inject*/ 0};
+    /*spmv_format*/ 1, /*pattern_min_pct*/ 0, /*issue_threads*/ 1, /*fault_inject*/ 0, /*spmv_tri16*/ 1};
 // COO → CSC → SELL on the device (pa_coo.hip)
 int coo_compress(int dtype, int index_bytes, int64_t m, int64_t ncols, int64_t n, const void* dI, const void* dJ,
                  const void* dV, int csr, int64_t* nu_out, int32_t** crow, int32_t** ccol, void** cval,
@@ -144,6 +144,10 @@ void launch_stencil_fill(const StencilGeom& g, const int32_t* shell, const doubl
                          int64_t nrows, int noids, pa_mat* A, int32_t* err, hipStream_t st);
 void launch_probe(int copy, int unroll, int64_t n16, const void* a, void* b, int blocks, hipStream_t st);
 void launch_invalid_config();
+void launch_t_rowinfo(const pa_mat* A, int64_t n, const int32_t* rows, int64_t noids, int32_t* info, hipStream_t st);
+void launch_t_gbase(const pa_mat* A, int64_t noids, int32_t* ok, hipStream_t st);
+void launch_t_fill(const pa_mat* A, int64_t noids, bool codes, hipStream_t st);
+void launch_t_check(const pa_mat* A, unsigned* bad, hipStream_t st);
 
 }  // namespace pa
 
@@ -397,6 +401,145 @@ int remap_nz_interleaved(pa_mat* A, const std::vector<int32_t>& kind, hipStream_
   return 0;
 }
 
+void free_triple_sell(pa_mat* A) {
+  for (void* p : {(void*)A->d_t_off, (void*)A->d_t_len, (void*)A->d_t_col16, A->d_t_val, (void*)A->d_t_gbase,
+                  (void*)A->d_t_rowmap, (void*)A->d_t_src, (void*)A->d_t_rowlen, (void*)A->d_t_int_list,
+                  (void*)A->d_t_bnd_list})
+    dev_free(p);
+  A->d_t_off = nullptr;
+  A->d_t_len = A->d_t_gbase = A->d_t_rowmap = A->d_t_rowlen = A->d_t_int_list = A->d_t_bnd_list = nullptr;
+  A->d_t_col16 = nullptr;
+  A->d_t_val = nullptr;
+  A->d_t_src = nullptr;
+  A->t_nrows = A->t_nslices = A->t_slots = A->t_tri_slices = A->t_tri_rows = A->t_code_slots = 0;
+  A->nt_int = A->nt_bnd = 0;
+  A->h_t_len.clear();
+}
+
+// The triple SELL: the rows of the delta16 slices (kind 3),
+// re-sliced — rows whose columns are consecutive triples first, then the
+// others, each class by length (descending) and oid — so that most slices
+// hold only triple rows and keep one 16-bit code per triple (their lanes
+// read a triple's x as one run), and no row's values stream twice (unlike
+// the side SELL of pattern slices).  The main delta16 slices become kind 5
+// (not launched in pattern mode; spmv_format 0 still runs them as int32).
+// Returns 0 without building when a slice's ghost codes would not fit.
+int build_triple_sell(pa_mat* A, std::vector<int32_t>& kind, int64_t noids) {
+  hipStream_t st = A->ctx->s_main;
+  const int64_t ns = A->nslices, H = A->H, R = A->R;
+  std::vector<int32_t> rows;
+  for (int64_t s = 0; s < ns; ++s)
+    if (kind[s] == 3)
+      for (int64_t i = s * H; i < std::min<int64_t>(A->nrows, s * H + H); ++i) rows.push_back((int32_t)i);
+  const int64_t n = (int64_t)rows.size();
+  if (n == 0) return 0;
+  int32_t *d_rows = nullptr, *d_info = nullptr;
+  if (dev_upload(&d_rows, rows)) return -1;
+  HIPC(hipMalloc((void**)&d_info, n * 4));
+  launch_t_rowinfo(A, n, d_rows, noids, d_info, st);
+  HIPC(hipGetLastError());
+  std::vector<int32_t> info(n);
+  std::vector<int64_t> soff(ns);
+  HIPC(hipMemcpyAsync(info.data(), d_info, n * 4, hipMemcpyDeviceToHost, st));
+  HIPC(hipMemcpyAsync(soff.data(), A->d_slice_off, ns * 8, hipMemcpyDeviceToHost, st));
+  HIPC(hipStreamSynchronize(st));
+  dev_free(d_rows);
+  dev_free(d_info);
+  constexpr int32_t kLen = (1 << 28) - 1, kReg = 1 << 28, kGhost = 1 << 29, kBad = 1 << 30;
+  for (int32_t v : info)
+    if (v & kBad) return 0;
+  // order: regular rows, then the others; each by length (descending), then oid
+  std::vector<int64_t> ord(n);
+  std::iota(ord.begin(), ord.end(), 0);
+  std::stable_sort(ord.begin(), ord.end(), [&](int64_t a, int64_t b) {
+    const bool ra = (info[a] & kReg) != 0, rb = (info[b] & kReg) != 0;
+    if (ra != rb) return ra;
+    return (info[a] & kLen) > (info[b] & kLen);
+  });
+  const int64_t tns = (n + H - 1) / H;
+  std::vector<int32_t> rowmap(n), rowlen(n), tlen(tns, 0), tint, tbnd;
+  std::vector<int64_t> src(n), toff(tns);
+  std::vector<char> tri(tns, 1), ghost(tns, 0);
+  for (int64_t i = 0; i < n; ++i) {
+    const int32_t v = info[ord[i]], row = rows[ord[i]];
+    const int64_t ts = i / H, s = row / H;
+    const int w = (int)(row - s * H);
+    rowmap[i] = row;
+    rowlen[i] = v & kLen;
+    // entry 0 of the row in the main layout (as k_delta16 left it, main_slot0)
+    src[i] = R == 4 ? soff[s] + (int64_t)(w & 63) * R + (w >> 6) : soff[s] + (int64_t)(w / R) * R + (w % R);
+    tlen[ts] = std::max(tlen[ts], rowlen[i]);
+    if (!(v & kReg)) tri[ts] = 0;
+    if (v & kGhost) ghost[ts] = 1;
+  }
+  int64_t nreg = 0;
+  for (int32_t v : info) nreg += (v & kReg) ? 1 : 0;
+  if (4 * nreg < n) return 0;  // mostly rows without triples (e.g. FD7): the delta16 slices stay
+  int64_t acc = 0, codes = 0;
+  A->maxlen_t = 0;
+  for (int64_t ts = 0; ts < tns; ++ts) {
+    toff[ts] = acc;
+    acc += (int64_t)tlen[ts] * H;
+    A->maxlen_t = std::max(A->maxlen_t, (int)tlen[ts]);
+    if (tri[ts] && tlen[ts] % 3 == 0) {
+      ++A->t_tri_slices;
+      A->t_tri_rows += std::min<int64_t>(H, n - ts * H);
+      codes += (int64_t)tlen[ts] / 3 * H;
+      tlen[ts] |= kTriSlice;
+    } else {
+      codes += (int64_t)tlen[ts] * H;
+    }
+    (ghost[ts] ? tbnd : tint).push_back((int32_t)ts);
+  }
+  A->t_nrows = n;
+  A->t_nslices = tns;
+  A->t_slots = acc;
+  A->t_code_slots = codes;
+  A->h_t_len = tlen;
+  const size_t S = dtype_size(A->dtype);
+  if (dev_upload(&A->d_t_off, toff) || dev_upload(&A->d_t_len, tlen) || dev_upload(&A->d_t_rowmap, rowmap) ||
+      dev_upload(&A->d_t_rowlen, rowlen) || dev_upload(&A->d_t_src, src) || dev_upload(&A->d_t_int_list, tint) ||
+      dev_upload(&A->d_t_bnd_list, tbnd))
+    return -1;
+  A->nt_int = (int64_t)tint.size();
+  A->nt_bnd = (int64_t)tbnd.size();
+  HIPC(hipMalloc((void**)&A->d_t_col16, std::max<int64_t>(acc, 1) * 2));
+  HIPC(hipMalloc(&A->d_t_val, std::max<int64_t>(acc, 1) * S));
+  // the positions past the last row of the last slice (and code groups no
+  // row writes) are padding: codes 0xFFFF (column -1, never gathered), values 0
+  HIPC(hipMemsetAsync(A->d_t_col16, 0xFF, std::max<int64_t>(acc, 1) * 2, st));
+  HIPC(hipMemsetAsync(A->d_t_val, 0, std::max<int64_t>(acc, 1) * S, st));
+  HIPC(hipMalloc((void**)&A->d_t_gbase, tns * 4));
+  int32_t* d_ok = nullptr;
+  HIPC(hipMalloc((void**)&d_ok, tns * 4));
+  launch_t_gbase(A, noids, d_ok, st);
+  HIPC(hipGetLastError());
+  std::vector<int32_t> ok(tns);
+  HIPC(hipMemcpyAsync(ok.data(), d_ok, tns * 4, hipMemcpyDeviceToHost, st));
+  HIPC(hipStreamSynchronize(st));
+  dev_free(d_ok);
+  for (int32_t v : ok)
+    if (!v) {  // a slice's ghost columns span more than 15 bits: keep the delta16 slices
+      free_triple_sell(A);
+      return 0;
+    }
+  launch_t_fill(A, noids, true, st);
+  HIPC(hipGetLastError());
+  unsigned* d_bad = nullptr;
+  unsigned bad = 0;
+  HIPC(hipMalloc((void**)&d_bad, 4));
+  HIPC(hipMemsetAsync(d_bad, 0, 4, st));
+  launch_t_check(A, d_bad, st);
+  HIPC(hipGetLastError());
+  HIPC(hipMemcpyAsync(&bad, d_bad, 4, hipMemcpyDeviceToHost, st));
+  HIPC(hipStreamSynchronize(st));
+  dev_free(d_bad);
+  CHECK_ARG(bad == 0, "triple SELL build: a column code decodes outside x (internal error)");
+  for (int64_t s = 0; s < ns; ++s)
+    if (kind[s] == 3) kind[s] = 5;
+  return 0;
+}
+
 int finalize_pattern(pa_mat* A, int kmax, int64_t noids) {
   A->kmax = std::max(kmax, 1);
   const int64_t ns = A->nslices;
@@ -451,13 +594,21 @@ int finalize_pattern(pa_mat* A, int kmax, int64_t noids) {
       // (3), and the CSC nz → slot map follows the moved values
       HIPC(hipMemcpyAsync(A->d_kind, kind.data(), ns * 4, hipMemcpyHostToDevice, st));
       if (A->nz_map && A->R == 4 && remap_nz_interleaved(A, kind, st)) return -1;
+      // the device keeps kind 3 (the int32 kernel of spmv_format 0 reads
+      // the interleaved layout from it); the host marks moved slices 5
+      // spmv_tri16 1 (auto): Float64 / ComplexF32 / ComplexF64 (R <= 2);
+      // Float32's interleaved delta16 slices already gather compactly and
+      // its irregular rows, re-sliced together, gather from wide x spans
+      // (C5 F32 +3 %, F64 -10 %, profiles/r05/d/)
+      const int tri = knobs().spmv_tri16;
+      if ((tri == 2 || (tri == 1 && A->R <= 2)) && build_triple_sell(A, kind, noids)) return -1;
     }
   }
   std::vector<int32_t> pint, pbnd, xint, xbnd, dint, dbnd, side;
   for (int64_t s = 0; s < ns; ++s) {
     if (kind[s] == 1) (pghost[s] ? pbnd : pint).push_back((int32_t)s);
     else if (kind[s] == 3) (pghost[s] ? dbnd : dint).push_back((int32_t)s);
-    else (pghost[s] ? xbnd : xint).push_back((int32_t)s);
+    else if (kind[s] == 0) (pghost[s] ? xbnd : xint).push_back((int32_t)s);  // (5: in the triple SELL)
     if (kind[s] == 1) {
       ++A->npattern_slices;
       const int64_t nvalid = std::min<int64_t>(A->H, A->nrows - s * A->H);
@@ -1134,6 +1285,10 @@ const Knob kKnobs[] = {
      "issue_threads: a call over parts with their own stream pairs is issued from host threads, one part "
      "per thread: 1 = when the parts span several devices (default), 2 = always, 0 = never (the calling "
      "thread, one part after the other)"},
+    {"spmv_tri16", &Knobs::spmv_tri16, nullptr, 0, 2, 0,
+     "spmv_tri16: the delta16 slices' rows re-sliced into the triple SELL (rows of consecutive column triples "
+     "keep one 16-bit code per triple; matrices built afterwards): 1 = for 8 and 16 B elements (Float64, "
+     "ComplexF32, ComplexF64; default), 2 = every element type, 0 = never"},
     {"fault_inject", &Knobs::fault_inject, nullptr, 0, 1, 0,
      "fault_inject: 1 = every job of a threaded issue (IssuePool) also issues an invalid kernel launch (tests "
      "of the error path; test_exception.jl's role), 0 = off (default)"},
@@ -2551,6 +2706,10 @@ static int refresh_side(pa_mat* A, hipStream_t st) {
     launch_side_fill(A, A->d_s_rowmap, A->d_s_rowlen, st);
     HIPC(hipGetLastError());
   }
+  if (A->t_nrows > 0) {  // and the triple SELL's (values only: the columns are unchanged)
+    launch_t_fill(A, 0, false, st);
+    HIPC(hipGetLastError());
+  }
   return 0;
 }
 
@@ -2673,6 +2832,7 @@ int pa_mat_destroy(pa_mat* A) {
                   (void*)A->d_lmask, (void*)A->d_lchunk_start, (void*)A->d_lrow_chunk, A->d_lpart,
                   (void*)A->d_col16, (void*)A->d_gbase, (void*)A->d_dint_list, (void*)A->d_dbnd_list})
     dev_free(p);
+  free_triple_sell(A);
   delete A;
   return 0;
 }
@@ -2690,6 +2850,16 @@ int pa_mat_format_info(const pa_mat* A, int64_t* pattern_slices, int64_t* regula
 int pa_mat_delta16_info(const pa_mat* A, int64_t* delta16_slices) {
   CHECK_ARG(A, "null matrix");
   if (delta16_slices) *delta16_slices = A->nd_int + A->nd_bnd;
+  return 0;
+}
+
+int pa_mat_triple_info(const pa_mat* A, int64_t* t_slices, int64_t* t_rows, int64_t* tri_slices,
+                       int64_t* tri_rows) {
+  CHECK_ARG(A, "null matrix");
+  if (t_slices) *t_slices = A->t_nslices;
+  if (t_rows) *t_rows = A->t_nrows;
+  if (tri_slices) *tri_slices = A->t_tri_slices;
+  if (tri_rows) *tri_rows = A->t_tri_rows;
   return 0;
 }
 
@@ -2726,6 +2896,8 @@ int pa_mat_traffic(const pa_mat* A, int64_t* value_bytes, int64_t* index_bytes, 
       v += (int64_t)A->h_slen[s] * H * S;
       ix += (int64_t)A->h_slen[s] * H * 2;
       m += 8 + 4 + 4 + 4;  // offset, length, list entry, ghost base
+    } else if (kd == 5) {
+      // rows in the triple SELL (below)
     } else {
       v += (int64_t)A->h_slen[s] * H * S;
       ix += (int64_t)A->h_slen[s] * H * 4;
@@ -2737,6 +2909,9 @@ int pa_mat_traffic(const pa_mat* A, int64_t* value_bytes, int64_t* index_bytes, 
     v += A->s_slots * S;
     ix += A->s_slots * 4 + A->s_nrows * 4;  // column ids, row map
     m += A->s_nslices * 12;
+    v += A->t_slots * S;              // triple SELL: values (padding included)
+    ix += A->t_code_slots * 2 + A->t_nrows * 4;  // codes (one per triple in tri slices), row map
+    m += A->t_nslices * (8 + 4 + 4 + 4);  // offset, length, ghost base, list entry
   }
   v += A->n_lnz * S;
   ix += A->n_lnz * 4;
@@ -2905,7 +3080,7 @@ static int spmv_grouped(int n, pa_mat* const A[], pa_vec* const y[], const pa_in
     EV(hipEventRecord(c0->ev_recvd, sc));
   }
   HIPC(hipGetLastError());
-  std::vector<SpmvPart> P0, P1, P4;
+  std::vector<SpmvPart> P0, P1, P4, P5;
   auto part = [&](int i, int64_t nwork, const int32_t* list) {
     const int32_t* ymap = y_idx[i]->own_contig ? nullptr : y_idx[i]->d_oid_to_lid;
     SpmvPart q{nwork, list, A[i], x[i]->d, y[i]->d, ymap, dotp[i]};
@@ -2952,6 +3127,7 @@ static int spmv_grouped(int n, pa_mat* const A[], pa_vec* const y[], const pa_in
       if (knobs().spmv_format == 1 && A[i]->has_pat) {
         add(4, i, A[i]->nd_int, A[i]->d_dint_list);
         add(4, i, A[i]->nd_bnd, A[i]->d_dbnd_list);
+        add(5, i, A[i]->t_nslices, nullptr);
       }
     for (int i = 0; i < n; ++i)
       if (knobs().spmv_format == 1 && A[i]->has_pat) {
@@ -2970,6 +3146,7 @@ static int spmv_grouped(int n, pa_mat* const A[], pa_vec* const y[], const pa_in
       P0.push_back(part(i, A[i]->np_int, A[i]->d_pint_list));
       P1.push_back(part(i, A[i]->nx_int, A[i]->d_xint_list));
       P4.push_back(part(i, A[i]->nd_int, A[i]->d_dint_list));
+      P5.push_back(part(i, A[i]->nt_int, A[i]->d_t_int_list));
     } else if (A[i]->d_bnd_list) {
       P1.push_back(part(i, A[i]->nslices_int, A[i]->d_int_list));
     } else {
@@ -2977,17 +3154,19 @@ static int spmv_grouped(int n, pa_mat* const A[], pa_vec* const y[], const pa_in
     }
   }
   launch_all(0, P0);
+  launch_all(5, P5);
   launch_all(4, P4);
   launch_all(1, P1);
   if (!dmark && mark(1)) return -1;
   if (any_x && !direct) EV(hipStreamWaitEvent(sm, c0->ev_recvd, 0));
   if (!dmark && mark(2)) return -1;
-  P0.clear(); P1.clear(); P4.clear();
+  P0.clear(); P1.clear(); P4.clear(); P5.clear();
   std::vector<SpmvPart> P2;
   for (int i = 0; i < n; ++i) {
     if (knobs().spmv_format == 1 && A[i]->has_pat) {
       P0.push_back(part(i, A[i]->np_bnd, A[i]->d_pbnd_list));
       P4.push_back(part(i, A[i]->nd_bnd, A[i]->d_dbnd_list));
+      P5.push_back(part(i, A[i]->nt_bnd, A[i]->d_t_bnd_list));
       P1.push_back(part(i, A[i]->nx_bnd, A[i]->d_xbnd_list));
       P2.push_back(part(i, A[i]->s_nslices, nullptr));
     } else if (A[i]->d_bnd_list) {
@@ -2995,6 +3174,7 @@ static int spmv_grouped(int n, pa_mat* const A[], pa_vec* const y[], const pa_in
     }
   }
   launch_all(0, P0);
+  launch_all(5, P5);
   launch_all(4, P4);
   launch_all(1, P1);
   launch_all(2, P2);
@@ -3002,7 +3182,7 @@ static int spmv_grouped(int n, pa_mat* const A[], pa_vec* const y[], const pa_in
   for (int i = 0; i < n; ++i) {
     const int32_t* ymap = y_idx[i]->own_contig ? nullptr : y_idx[i]->d_oid_to_lid;
     const bool pat = knobs().spmv_format == 1 && A[i]->has_pat;
-    const int64_t long_base = A[i]->nslices + (pat ? A[i]->s_nslices : 0);
+    const int64_t long_base = A[i]->nslices + (pat ? A[i]->s_nslices + A[i]->t_nslices : 0);
     cg_ghosts(fz, i, A[i], x[i], sm);
     launch_spmv_long(A[i], x[i]->d, y[i]->d, ymap, has_alpha, bmode, alpha, beta, dotp[i], long_base, sm);
     if (want_dot) {
@@ -3046,11 +3226,13 @@ static int launch_phase(int phase, pa_mat* A, const void* x, void* y, const int3
     if (phase == 0) {
       add(1, A->nx_int, A->d_xint_list);
       add(4, A->nd_int, A->d_dint_list);
+      add(5, A->nt_int, A->d_t_int_list);
       add(0, A->np_int, A->d_pint_list);
     } else {
       add(2, A->s_nslices, nullptr);
       add(1, A->nx_bnd, A->d_xbnd_list);
       add(4, A->nd_bnd, A->d_dbnd_list);
+      add(5, A->nt_bnd, A->d_t_bnd_list);
       add(0, A->np_bnd, A->d_pbnd_list);
     }
   } else if (A->d_bnd_list) {  // split layout (the interior list may be empty)
@@ -3084,7 +3266,12 @@ static int spmv_impl(int n, pa_mat* const A[], pa_vec* const y[], const pa_index
       CHECK_ARG(x_idx && x_idx[i] && x_idx[i]->own_contig, "fused dot needs b with contiguous owned lids");
       if (!A[i]->d_dotp) {
         HIPC(hipSetDevice(A[i]->ctx->device));
-        HIPC(hipMalloc(&A[i]->d_dotp, std::max<int64_t>(A[i]->nslices + A[i]->s_nslices + A[i]->n_long, 1) * 16));
+        // one partial per main, side and triple-SELL slice and long row;
+        // zeroed once: the slices a call does not launch (moved to the
+        // triple SELL) add 0 to the fold
+        const int64_t nbp = std::max<int64_t>(A[i]->nslices + A[i]->s_nslices + A[i]->t_nslices + A[i]->n_long, 1);
+        HIPC(hipMalloc(&A[i]->d_dotp, nbp * 16));
+        HIPC(hipMemset(A[i]->d_dotp, 0, nbp * 16));
       }
       dotp[i] = A[i]->d_dotp;
     }
@@ -3167,7 +3354,7 @@ static int spmv_impl(int n, pa_mat* const A[], pa_vec* const y[], const pa_index
     cg_ghosts(fz, i, A[i], x[i], SM(c));
     // long rows (after the halo: they may read ghost columns)
     const bool pat = knobs().spmv_format == 1 && A[i]->has_pat;
-    const int64_t long_base = A[i]->nslices + (pat ? A[i]->s_nslices : 0);
+    const int64_t long_base = A[i]->nslices + (pat ? A[i]->s_nslices + A[i]->t_nslices : 0);
     launch_spmv_long(A[i], x[i]->d, y[i]->d, ymap, has_alpha, bmode, alpha, beta, dotp[i], long_base, SM(c));
     if (want_dot) {  // fold the partials (main slices, side slices, long rows) in order
       const bool cplx = dt == PA_C64 || dt == PA_C128;
@@ -3629,6 +3816,18 @@ int cg_gather(CGRun& R, size_t accsz) {
   return 0;
 }
 
+// The u-update variant of the device CG's auto mode (cg_fuse 2) from the
+// two timed batches (ms[0] the sweep, ms[1] the fused update): with one
+// part per process every rank measures its own batches, so the times are
+// first reduced with max over the ranks (the slowest rank sets the
+// iteration time), and every rank makes the same choice.  -1: no valid
+// measurement.
+int cg_agree_choice(float ms[2], const std::function<int(float*)>& allreduce_max) {
+  if (allreduce_max && allreduce_max(ms)) return -2;
+  if (!(ms[0] > 0.f) || !(ms[1] > 0.f)) return -1;
+  return ms[1] < ms[0] ? 1 : 0;
+}
+
 void scalar_one(int dt, unsigned char out[16], double v) {
   std::memset(out, 0, 16);
   switch (dt) {
@@ -3740,9 +3939,13 @@ int pa_cg_solve_all(int n, pa_mat* const A[], pa_vec* const x[], const pa_vec* c
   // result.  Fused: not for matrices with long rows (their kernel gathers x
   // directly).
   bool can_fuse = true;
-  for (int i = 0; i < n; ++i) can_fuse = can_fuse && A[i]->n_long == 0;
+  // (the fused u update is written by the main structure's waves: not for
+  // rows that long-row kernels or the triple SELL compute)
+  for (int i = 0; i < n; ++i) can_fuse = can_fuse && A[i]->n_long == 0 && A[i]->t_nrows == 0;
+  // (every rank of a one-part-per-process solve takes the same branches:
+  // maxiter, batch, the done flag and the reduced batch times agree)
   int mode = can_fuse ? knobs().cg_fuse : 0;
-  if (mode == 2 && (R.remote || maxiter < 3 * (int64_t)batch)) mode = A[0]->cg_fuse_choice >= 0 ? A[0]->cg_fuse_choice : 0;
+  if (mode == 2 && maxiter < 3 * (int64_t)batch) mode = A[0]->cg_fuse_choice >= 0 ? A[0]->cg_fuse_choice : 0;
   if (mode == 2 && A[0]->cg_fuse_choice >= 0) mode = A[0]->cg_fuse_choice;
   std::vector<pa_vec*> u2(n, nullptr);
   struct U2Free {
@@ -3844,7 +4047,20 @@ int pa_cg_solve_all(int n, pa_mat* const A[], pa_vec* const x[], const pa_vec* c
       float ms = 0.f;
       HIPC(hipEventElapsedTime(&ms, tev[0], tev[1]));
       batch_ms[nbatch] = ms / (float)(k - 1);
-      if (nbatch == 1 && batch_ms[0] > 0.f) A[0]->cg_fuse_choice = batch_ms[1] < batch_ms[0] ? 1 : 0;
+      if (nbatch == 1) {
+        std::function<int(float*)> red;
+        if (R.remote)  // the ranks' times, max over the ranks (RCCL, part 1's stream)
+          red = [&](float* v) -> int {
+            HIPC(hipMemcpyAsync(c0->d_fold, v, 2 * sizeof(float), hipMemcpyHostToDevice, c0->s_main));
+            NCCLC(ncclAllReduce(c0->d_fold, c0->d_fold, 2, ncclFloat32, ncclMax, (ncclComm_t)c0->comm, c0->s_main));
+            HIPC(hipMemcpyAsync(v, c0->d_fold, 2 * sizeof(float), hipMemcpyDeviceToHost, c0->s_main));
+            HIPC(hipStreamSynchronize(c0->s_main));
+            return 0;
+          };
+        const int ch = cg_agree_choice(batch_ms, red);
+        if (ch == -2) return -1;
+        if (ch >= 0) A[0]->cg_fuse_choice = ch;
+      }
     } else if (mode == 2 && nbatch < 2) {
       mode = A[0]->cg_fuse_choice >= 0 ? A[0]->cg_fuse_choice : 0;  // no choice this solve: keep it unset
     }
@@ -3866,6 +4082,23 @@ int pa_cg_solve_all(int n, pa_mat* const A[], pa_vec* const x[], const pa_vec* c
     HIPC(hipSetDevice(R.ctxs[0]->device));
     HIPC(hipMemcpy(history, R.hist[0], (size_t)h.it * sizeof(double), hipMemcpyDeviceToHost));
   }
+  return 0;
+}
+
+int pa_cg_variant_agree(const float local_ms[2], pa_allreduce_max_fn fn, void* user, int* choice) {
+  CHECK_ARG(local_ms && choice, "null argument");
+  float ms[2] = {local_ms[0], local_ms[1]};
+  std::function<int(float*)> red;
+  if (fn) red = [&](float* v) -> int { return fn(v, 2, user) ? (pa::set_error("allreduce callback failed"), -1) : 0; };
+  const int ch = cg_agree_choice(ms, red);
+  if (ch == -2) return -1;
+  *choice = ch;
+  return 0;
+}
+
+int pa_mat_cg_choice(const pa_mat* A, int* choice) {
+  CHECK_ARG(A && choice, "null argument");
+  *choice = A->cg_fuse_choice;
   return 0;
 }
 

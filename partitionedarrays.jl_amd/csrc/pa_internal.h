@@ -220,6 +220,7 @@ struct CGState {
 // Grouped launches (parts of one process sharing a stream pair): one launch
 // per phase covers up to PA_GROUP_MAX parts (kernel-argument tables).
 constexpr int PA_GROUP_MAX = 8;
+constexpr int32_t kTriSlice = 1 << 30;  // pa_mat::d_t_len: a triple slice
 struct SpmvPart {
   int64_t nwork;          // slices of this part in the launch
   const int32_t* list;    // slice ids (null: 0..nwork-1)
@@ -337,6 +338,7 @@ struct Knobs {
   int pattern_min_pct;
   int issue_threads;
   int fault_inject;      // tests only: the IssuePool jobs issue an invalid launch
+  int spmv_tri16;        // delta16 slices re-sliced into the triple SELL (pa_mat::d_t_*): 0 never, 1 R <= 2, 2 always
 };
 // the knobs of the call running on this thread (outside a call: a snapshot
 // of the process defaults)
@@ -533,5 +535,28 @@ struct pa_mat {
   void* d_s_val = nullptr;
   int32_t* d_s_rowmap = nullptr;
   int32_t* d_s_rowlen = nullptr;
-  void* d_dotp = nullptr;            // fused dot: one partial per (main + side) slice
+  // Triple SELL (pa_tune "spmv_tri16"): the rows of the
+  // delta16 slices, re-sliced by class — rows whose column list is
+  // consecutive triples (c, c+1, c+2) first, then the other rows, each class
+  // by length (descending) and oid — with a row map.  A "tri" slice (every
+  // row regular, length % 3 == 0) keeps one 16-bit code per triple and its
+  // lane reads a triple's x as one run; the other slices keep one code per
+  // entry.  Rows of a slice are interleaved (row i at lane i % 64, position
+  // i / 64).  Values are copies of the main slots (refreshed with the side
+  // SELL); the main delta16 slices are not launched then (host kind 5).
+  int64_t t_nrows = 0, t_nslices = 0, t_slots = 0, t_tri_slices = 0, t_tri_rows = 0, t_code_slots = 0;
+  int64_t* d_t_off = nullptr;        // slot offset per slice
+  int32_t* d_t_len = nullptr;        // entries per row (max over the slice), bit 30: tri slice (kTriSlice)
+  uint16_t* d_t_col16 = nullptr;     // codes (tri slices: one per triple, slot groups 0..len/3-1)
+  void* d_t_val = nullptr;           // values (lane-major packs of R, like the main SELL)
+  int32_t* d_t_gbase = nullptr;      // per slice: smallest ghost column
+  int32_t* d_t_rowmap = nullptr;     // structure row → oid
+  int64_t* d_t_src = nullptr;        // structure row → its main-layout slot of entry 0 (entry k: + k*64*R)
+  int32_t* d_t_rowlen = nullptr;     // structure row → its entries
+  int32_t* d_t_int_list = nullptr;   // slices without ghost reads
+  int32_t* d_t_bnd_list = nullptr;   // slices reading ghosts
+  int64_t nt_int = 0, nt_bnd = 0;
+  int maxlen_t = INT32_MAX;
+  std::vector<int32_t> h_t_len;      // host copies for pa_mat_traffic
+  void* d_dotp = nullptr;            // fused dot: one partial per (main + side + triple) slice and long row
 };

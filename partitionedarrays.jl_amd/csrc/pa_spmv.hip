@@ -182,12 +182,35 @@ __device__ __forceinline__ Pack<T, R> ld_xrun(const T* p) {
 // arithmetic, IterativeSolvers' `u .= r .+ β.*u`), so iteration k's SpMV
 // reads r and u_{k-1} instead of a materialised u_k: the same values bit for
 // bit, one vector sweep less per iteration.
+// x[j], x[j+1], x[j+2] with the fewest loads (4 B aligned: global loads of
+// several dwords need only dword alignment): one 12 B load for 4 B
+// elements, a 16 B and an 8 B load for 8 B elements, three 16 B loads for
+// 16 B elements.  j + 2 stays inside the vector's 64 B back padding.
+typedef unsigned int u3a __attribute__((ext_vector_type(3))) __attribute__((aligned(4)));
+typedef unsigned int u2a __attribute__((ext_vector_type(2))) __attribute__((aligned(4)));
+template <typename T>
+__device__ __forceinline__ void ld_xtrip(const T* p, T (&o)[3]) {
+  if constexpr (sizeof(T) == 4) {
+    const u3a r = *reinterpret_cast<const u3a*>(p);
+    __builtin_memcpy(&o[0], &r, 12);
+  } else if constexpr (sizeof(T) == 8) {
+    const u4a r = *reinterpret_cast<const u4a*>(p);
+    const u2a q = *reinterpret_cast<const u2a*>(p + 2);
+    __builtin_memcpy(&o[0], &r, 16);
+    __builtin_memcpy(&o[2], &q, 8);
+  } else {
+#pragma unroll
+    for (int j = 0; j < 3; ++j) o[j] = p[j];
+  }
+}
+
 template <typename T, bool XV>
 struct XSrc {
   const T* __restrict__ x;
   __device__ __forceinline__ T get(int64_t j) const { return x[j]; }
   template <int R>
   __device__ __forceinline__ Pack<T, R> run(int64_t j) const { return ld_xrun<T, R>(x + j); }
+  __device__ __forceinline__ void trip(int64_t j, T (&o)[3]) const { ld_xtrip<T>(x + j, o); }
 };
 template <typename T>
 struct XSrc<T, true> {
@@ -196,6 +219,10 @@ struct XSrc<T, true> {
   double b;
   __device__ __forceinline__ T f(T rv, T uv) const { return narrow<T>(widen(rv) + rscale(b, widen(uv))); }
   __device__ __forceinline__ T get(int64_t j) const { return f(r[j], u[j]); }
+  __device__ __forceinline__ void trip(int64_t j, T (&o)[3]) const {
+#pragma unroll
+    for (int k = 0; k < 3; ++k) o[k] = get(j + k);
+  }
   template <int R>
   __device__ __forceinline__ Pack<T, R> run(int64_t j) const {
     const Pack<T, R> a = ld_xrun<T, R>(r + j), c = ld_xrun<T, R>(u + j);
@@ -368,7 +395,7 @@ template <int R> constexpr int kD16RowStride = kInterleaveD16<R> ? 64 : 1;
 template <typename T, int R, bool ALPHA, bool NT, int U, bool SH = false, bool IPF = false, typename XS>
 __device__ __forceinline__ void rows_d16(T (&acc)[R], const S16Pack<R>* __restrict__ cp,
                                          const Pack<T, R>* __restrict__ vp, int len,
-                                         const XS& x, T alpha, bool pf, bool TB, int32_t row0, int32_t gb) {
+                                         const XS& x, T alpha, bool pf, bool TB, const int32_t (&rw)[R], int32_t gb) {
   int k = 0;
   if (SH) TB = true;
   if constexpr (IPF && !SH) {  // codes one batch ahead, as in rows_int32
@@ -381,7 +408,7 @@ __device__ __forceinline__ void rows_d16(T (&acc)[R], const S16Pack<R>* __restri
 #pragma unroll
         for (int u = 0; u < U; ++u)
 #pragma unroll
-          for (int r = 0; r < R; ++r) c[u][r] = d16_col(qn[u].c[r], row0 + r * kD16RowStride<R>, gb);
+          for (int r = 0; r < R; ++r) c[u][r] = d16_col(qn[u].c[r], rw[r], gb);
         Pack<T, R> v[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) v[u] = ld<NT>(&vp[(k + u) * 64]);
@@ -412,7 +439,7 @@ __device__ __forceinline__ void rows_d16(T (&acc)[R], const S16Pack<R>* __restri
 #pragma unroll
         for (int u = 0; u < U; ++u)
 #pragma unroll
-          for (int r = 0; r < R; ++r) c[u][r] = d16_col(qn[u].c[r], row0 + r * kD16RowStride<R>, gb);
+          for (int r = 0; r < R; ++r) c[u][r] = d16_col(qn[u].c[r], rw[r], gb);
         Pack<T, R> v[U];
 #pragma unroll
         for (int u = 0; u < U; ++u)
@@ -444,7 +471,7 @@ __device__ __forceinline__ void rows_d16(T (&acc)[R], const S16Pack<R>* __restri
 #pragma unroll
     for (int u = 0; u < U; ++u) {
 #pragma unroll
-      for (int r = 0; r < R; ++r) c[u][r] = d16_col(q[u].c[r], row0 + r * kD16RowStride<R>, gb);
+      for (int r = 0; r < R; ++r) c[u][r] = d16_col(q[u].c[r], rw[r], gb);
       gather_x<T, R>(xv[u], c[u], x);
     }
 #pragma unroll
@@ -471,7 +498,7 @@ __device__ __forceinline__ void rows_d16(T (&acc)[R], const S16Pack<R>* __restri
 #pragma unroll
     for (int u = 0; u < U; ++u) {
 #pragma unroll
-      for (int r = 0; r < R; ++r) c[u][r] = d16_col(q[u].c[r], row0 + r * kD16RowStride<R>, gb);
+      for (int r = 0; r < R; ++r) c[u][r] = d16_col(q[u].c[r], rw[r], gb);
       if (k + u < len) gather_x<T, R>(xv[u], c[u], x);
     }
 #pragma unroll
@@ -488,10 +515,72 @@ __device__ __forceinline__ void rows_d16(T (&acc)[R], const S16Pack<R>* __restri
     const Pack<T, R> v = ld<NT>(&vp[k * 64]);
 #pragma unroll
     for (int r = 0; r < R; ++r) {
-      const int32_t cc = d16_col(q.c[r], row0 + r * kD16RowStride<R>, gb);
+      const int32_t cc = d16_col(q.c[r], rw[r], gb);
       const T t = acc[r] + term<ALPHA>(v.v[r], x.get(cc >= 0 ? cc : 0), alpha, pf);
       acc[r] = pick(cc >= 0, t, acc[r]);
     }
+  }
+}
+
+// triples per batch: 12 entries in flight per lane (library A/B, profiles/r04/ag/: FE27
+// 256^3 2 triples 0.6590 ms, 3 0.6549-0.6554, 4 0.6500 at the same VGPR count;
+// 6: 0.6627, the merged kernel 122 -> 132 VGPRs, halo leg +12 %, r04/ai/)
+constexpr int kTriBatch = 4;
+
+// Triple-SELL tri slices: every row's columns are consecutive triples (c,
+// c+1, c+2), entry 3t..3t+2; the code of triple t (relative to the row, as
+// in rows_d16) sits in code group t, and the lane reads the triple's x with
+// ld_xtrip.  Padding triples (code 0xFFFF) are never accumulated.  Four
+// triples (12 values) in flight per lane, as in rows_pattern_tri.  The
+// terms and their order are those of rows_d16.
+template <typename T, int R, bool ALPHA, bool NT, typename XS>
+__device__ __forceinline__ void rows_t16_tri(T (&acc)[R], const S16Pack<R>* __restrict__ cp,
+                                             const Pack<T, R>* __restrict__ vp, int len, const XS& x, T alpha,
+                                             bool pf, const int32_t (&rw)[R], int32_t gb) {
+  const int ntri = len / 3;
+  constexpr int TB = kTriBatch;
+  auto step = [&](const S16Pack<R>* q, const Pack<T, R>* v, auto nb) {
+    constexpr int B = decltype(nb)::value;
+    T xv[B][3][R];
+    bool ok[B][R];
+#pragma unroll
+    for (int u = 0; u < B; ++u)
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const int32_t c = d16_col(q[u].c[r], rw[r], gb);
+        ok[u][r] = c >= 0;
+        T t3[3];
+        x.trip(c >= 0 ? c : 0, t3);
+#pragma unroll
+        for (int j = 0; j < 3; ++j) xv[u][j][r] = t3[j];
+      }
+#pragma unroll
+    for (int u = 0; u < B; ++u)
+#pragma unroll
+      for (int j = 0; j < 3; ++j)
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          const T t = acc[r] + term<ALPHA>(v[3 * u + j].v[r], xv[u][j][r], alpha, pf);
+          acc[r] = pick(ok[u][r], t, acc[r]);
+        }
+  };
+  int t = 0;
+  for (; t + TB <= ntri; t += TB) {
+    S16Pack<R> q[TB];
+    Pack<T, R> v[3 * TB];
+#pragma unroll
+    for (int u = 0; u < TB; ++u) q[u] = ld<NT>(&cp[(t + u) * 64]);
+#pragma unroll
+    for (int u = 0; u < 3 * TB; ++u) v[u] = ld<NT>(&vp[(3 * t + u) * 64]);
+    step(q, v, std::integral_constant<int, TB>{});
+  }
+  for (; t < ntri; ++t) {
+    S16Pack<R> q[1];
+    Pack<T, R> v[3];
+    q[0] = ld<NT>(&cp[t * 64]);
+#pragma unroll
+    for (int u = 0; u < 3; ++u) v[u] = ld<NT>(&vp[(3 * t + u) * 64]);
+    step(q, v, std::integral_constant<int, 1>{});
   }
 }
 
@@ -593,10 +682,6 @@ __device__ __forceinline__ void rows_pattern(T (&acc)[R], const int32_t* __restr
 // rows_pattern.  Library A/B on one box (profiles/r04/p/): FE27 256^3 one
 // part 0.6744 -> 0.6523 ms, the (2,2,2) halo leg 0.714 -> 0.688 ms, C5 F64
 // -1.0 %: one x load in three fewer relieves the per-CU memory pipeline.
-// triples per batch: 12 entries in flight per lane (library A/B, profiles/r04/ag/: FE27
-// 256^3 2 triples 0.6590 ms, 3 0.6549-0.6554, 4 0.6500 at the same VGPR count;
-// 6: 0.6627, the merged kernel 122 -> 132 VGPRs, halo leg +12 %, r04/ai/)
-constexpr int kTriBatch = 4;
 template <typename T, int R, bool ALPHA, bool NT, typename XS>
 __device__ __forceinline__ void rows_pattern_tri(T (&acc)[R], const int32_t* __restrict__ pat,
                                                  const Pack<T, R>* __restrict__ vp, int len, const XS& x,
@@ -707,9 +792,10 @@ __device__ __forceinline__ void cg_rows_update(const SpmvArgs<T>& a, const XS& x
 // BMODE: 0 → acc = 0 (β == 0: fill!(co,0)), 1 → acc = y (β == 1),
 //        2 → acc = y*β (rmul!(co,β)).  Interfaces.jl:2262-2263.
 // PK: the launch's slices are int32-column slices (0), pattern slices (1:
-// implied columns for the rows of their mask) or delta16 slices (3: 2 B
-// column codes decoded against the row); one kernel per kind keeps the hot
-// loop free of the others' code and registers.
+// implied columns for the rows of their mask), delta16 slices (3: 2 B
+// column codes decoded against the row) or the triple SELL (4: rows through
+// a row map, one code per triple in its tri slices); one kernel per kind
+// keeps the hot loop free of the others' code and registers.
 // One wave computes work item w (slice a.list[w], or w) of the structure a.
 // SH: every row of the launch has at most U entries (FD7: 7) — the masked
 // batch alone, no loop code (fewer registers, more waves per SIMD).
@@ -728,6 +814,7 @@ __device__ __forceinline__ void spmv_wave(const SpmvArgs<T>& a, const int64_t w)
   // delta16 slices, interleaved (rows r*64 + lane; k_delta16)
   bool il = false;
   if constexpr (PK == 3) il = kInterleaveD16<R>;
+  if constexpr (PK == 4) il = true;
   if constexpr (PK == 0 && kInterleaveD16<R>) il = a.ilv && a.ilv[s] == 3;
   const int rs = il ? 64 : 1;
   const int64_t row0 = s * H + (il ? (int64_t)lane : (int64_t)lane * R);  // the lane's first row
@@ -751,7 +838,8 @@ __device__ __forceinline__ void spmv_wave(const SpmvArgs<T>& a, const int64_t w)
   }
   const int64_t off = a.soff[s];
   const int32_t lraw = a.slen[s];
-  const int len = PAT ? (lraw & 0xff) : lraw;  // pattern slices: len | tri << 8 | pattern id << 9 (dedup_patterns)
+  // pattern slices: len | tri << 8 | pattern id << 9 (dedup_patterns); triple SELL: len | kTriSlice
+  const int len = PAT ? (lraw & 0xff) : (PK == 4 ? (lraw & (kTriSlice - 1)) : lraw);
   bool ok[R];
   if (PAT) {
     const uint64_t m = a.mask[s * (H / 64) + (lane * R) / 64];
@@ -809,8 +897,26 @@ __device__ __forceinline__ void spmv_wave(const SpmvArgs<T>& a, const int64_t w)
   } else if constexpr (PK == 3) {
     const S16Pack<R>* __restrict__ cp = reinterpret_cast<const S16Pack<R>*>(a.col16 + off) + lane;
     const int32_t gb = a.gbase[s];
-    if (a.flags & SPMV_NT) rows_d16<T, R, ALPHA, true, U, SH, kIdsAhead<T>>(acc, cp, vp, len, xs, a.alpha, pf, tb, (int32_t)row0, gb);
-    else rows_d16<T, R, ALPHA, false, U, SH, kIdsAhead<T>>(acc, cp, vp, len, xs, a.alpha, pf, tb, (int32_t)row0, gb);
+    int32_t rw[R];  // the rows the codes are relative to
+#pragma unroll
+    for (int r = 0; r < R; ++r) rw[r] = (int32_t)row0 + r * kD16RowStride<R>;
+    if (a.flags & SPMV_NT) rows_d16<T, R, ALPHA, true, U, SH, kIdsAhead<T>>(acc, cp, vp, len, xs, a.alpha, pf, tb, rw, gb);
+    else rows_d16<T, R, ALPHA, false, U, SH, kIdsAhead<T>>(acc, cp, vp, len, xs, a.alpha, pf, tb, rw, gb);
+  } else if constexpr (PK == 4) {
+    // triple SELL (rows through the row map, interleaved): tri slices carry
+    // one code per triple, the others one per entry (rows_d16)
+    const S16Pack<R>* __restrict__ cp = reinterpret_cast<const S16Pack<R>*>(a.col16 + off) + lane;
+    const int32_t gb = a.gbase[s];
+    int32_t rw[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) rw[r] = (int32_t)orow[r];
+    if (lraw & kTriSlice) {
+      if (a.flags & SPMV_NT) rows_t16_tri<T, R, ALPHA, true>(acc, cp, vp, len, xs, a.alpha, pf, rw, gb);
+      else rows_t16_tri<T, R, ALPHA, false>(acc, cp, vp, len, xs, a.alpha, pf, rw, gb);
+    } else {
+      if (a.flags & SPMV_NT) rows_d16<T, R, ALPHA, true, U, SH, kIdsAhead<T>>(acc, cp, vp, len, xs, a.alpha, pf, tb, rw, gb);
+      else rows_d16<T, R, ALPHA, false, U, SH, kIdsAhead<T>>(acc, cp, vp, len, xs, a.alpha, pf, tb, rw, gb);
+    }
   } else {
     const IPack<R>* __restrict__ cp = reinterpret_cast<const IPack<R>*>(a.col + off) + lane;
     if (a.flags & SPMV_NT) rows_int32<T, R, ALPHA, true, U, SH, kIdsAhead<T>>(acc, cp, vp, len, xs, a.alpha, pf, tb);
@@ -898,7 +1004,7 @@ static void launch_group_t(const SpmvGroup<T>& g, hipStream_t st) {
   if (blocks == 0) return;
   bool sh = (knobs().spmv_flags & SPMV_SHORT) != 0;
   for (int i = 0; i < g.np; ++i) sh = sh && g.a[i].maxlen <= 8;
-  if constexpr (!ALPHA && BMODE == 0) {
+  if constexpr (!ALPHA && BMODE == 0 && PAT != 4) {
     if (g.a[0].cg) {  // the device CG's fused u update
       if (sh)
         hipLaunchKernelGGL((k_spmv_sell_group<T, R, false, 0, 8, PAT, true, true>), dim3(blocks), dim3(256), 0, st, g);
@@ -930,7 +1036,7 @@ template <typename T, int R, bool ALPHA, int BMODE, int PAT>
 static void launch_t(const SpmvArgs<T>& a, hipStream_t st) {
   const int64_t blocks = (a.nwork + 3) / 4;
   if (blocks == 0) return;
-  if constexpr (!ALPHA && BMODE == 0) {
+  if constexpr (!ALPHA && BMODE == 0 && PAT != 4) {
     if (a.cg) {  // the device CG's fused u update
       if ((knobs().spmv_flags & SPMV_SHORT) && a.maxlen <= 8)
         hipLaunchKernelGGL((k_spmv_sell<T, R, false, 0, 8, PAT, true, true>), dim3(blocks), dim3(256), 0, st, a);
@@ -960,7 +1066,7 @@ static void launch_ab(const SpmvArgs<T>& a, bool has_alpha, int bmode, hipStream
 
 // which = 0: pattern slices of the main structure; 1: int32-column slices
 // of the main structure; 2: side SELL; 4: delta16 slices of the main
-// structure.  list/nwork select the slices.
+// structure; 5: triple SELL.  list/nwork select the slices.
 template <typename T>
 static SpmvArgs<T> make_args(int which, int64_t nwork, const int32_t* list, const pa_mat* A, const void* x,
                              void* y, const int32_t* ymap, const void* alpha, const void* beta, void* dotp,
@@ -974,7 +1080,7 @@ static SpmvArgs<T> make_args(int which, int64_t nwork, const int32_t* list, cons
   }
   a.dotu = (decltype(a.dotu))((const T*)x);
   a.dotp = dotp;
-  a.dot_base = which == 2 ? A->nslices : 0;
+  a.dot_base = which == 2 ? A->nslices : which == 5 ? A->nslices + A->s_nslices : 0;
   a.nwork = nwork;
   a.list = (decltype(a.list))(list);
   a.x = (decltype(a.x))((const T*)x);
@@ -988,8 +1094,17 @@ static SpmvArgs<T> make_args(int which, int64_t nwork, const int32_t* list, cons
              : which == 2 ? A->maxlen_side
              : which == 1 ? ((knobs().spmv_format == 1 && A->has_pat) ? A->maxlen_pm_int : A->maxlen_all)
              : which == 4 ? A->maxlen_d16
+             : which == 5 ? std::max(A->maxlen_t, 9)  // never the short-row kernels (merged_wave)
                           : INT32_MAX;
-  if (which == 2) {
+  if (which == 5) {  // triple SELL
+    a.soff = (decltype(a.soff))(A->d_t_off);
+    a.slen = (decltype(a.slen))(A->d_t_len);
+    a.col16 = (decltype(a.col16))(A->d_t_col16);
+    a.gbase = (decltype(a.gbase))(A->d_t_gbase);
+    a.val = (decltype(a.val))((const T*)A->d_t_val);
+    a.rowmap = (decltype(a.rowmap))(A->d_t_rowmap);
+    a.nrows = A->t_nrows;
+  } else if (which == 2) {
     a.soff = (decltype(a.soff))(A->d_s_off);
     a.slen = (decltype(a.slen))(A->d_s_len);
     a.col = (decltype(a.col))(A->d_s_col);
@@ -1030,6 +1145,7 @@ static void launch_which(int which, int64_t nwork, const int32_t* list, const pa
   const SpmvArgs<T> a = make_args<T>(which, nwork, list, A, x, y, ymap, alpha, beta, dotp, cgp);
   if (which == 0) launch_ab<T, R, 1>(a, has_alpha, bmode, st);
   else if (which == 4) launch_ab<T, R, 3>(a, has_alpha, bmode, st);
+  else if (which == 5) launch_ab<T, R, 4>(a, has_alpha, bmode, st);
   else launch_ab<T, R, 0>(a, has_alpha, bmode, st);
 }
 
@@ -1042,6 +1158,7 @@ static void group_which(int which, int np, const SpmvPart* parts, bool has_alpha
     if (g.np == 0) return;
     if (which == 0) launch_group_ab<T, R, 1>(g, has_alpha, bmode, st);
     else if (which == 4) launch_group_ab<T, R, 3>(g, has_alpha, bmode, st);
+    else if (which == 5) launch_group_ab<T, R, 4>(g, has_alpha, bmode, st);
     else launch_group_ab<T, R, 0>(g, has_alpha, bmode, st);
     g = SpmvGroup<T>{};
   };
@@ -1049,7 +1166,7 @@ static void group_which(int which, int np, const SpmvPart* parts, bool has_alpha
     const SpmvPart& q = parts[i];
     if (q.nwork <= 0) continue;
     const int32_t* list = q.list;
-    if ((knobs().spmv_flags & SPMV_IDLIST) && list && which != 2 && q.nwork == q.A->nslices) list = nullptr;
+    if ((knobs().spmv_flags & SPMV_IDLIST) && list && which != 2 && which != 5 && q.nwork == q.A->nslices) list = nullptr;
     g.a[g.np] = make_args<T>(which, q.nwork, list, q.A, q.x, q.y, q.ymap, alpha, beta, q.dotp, &q);
     g.start[g.np + 1] = g.start[g.np] + q.nwork;
     if (++g.np == PA_GROUP_MAX) flush();
@@ -1144,6 +1261,12 @@ __device__ __forceinline__ void merged_wave(const SpmvTable<T>* __restrict__ tab
   const SpmvArgs<T>& a = tab->a[p];
   if (pk == 1) spmv_wave<T, R, ALPHA, BMODE, U, 1, SH, XV>(a, lw);
   else if (pk == 3) spmv_wave<T, R, ALPHA, BMODE, U, 3, SH, XV>(a, lw);
+  else if (pk == 4) {
+    // the triple SELL never runs in the short-row (make_args: maxlen >= 9)
+    // or fused-u kernels (pa_cg_solve_all: no fused update with it): their
+    // registers stay those of the other kinds
+    if constexpr (!SH && !XV) spmv_wave<T, R, ALPHA, BMODE, U, 4, SH, XV>(a, lw);
+  }
   else spmv_wave<T, R, ALPHA, BMODE, U, 0, SH, XV>(a, lw);
 }
 
@@ -1182,7 +1305,7 @@ static void launch_merged_t(const SpmvTable<T>* d, int n, int64_t waves, bool sh
     hipLaunchKernelGGL((k_spmv_merged<T, R, ALPHA, BMODE, 8, false>), dim3(blocks), dim3(256), 0, st, d, n, waves);
 }
 
-static int pk_of(int which) { return which == 0 ? 1 : which == 4 ? 3 : 0; }
+static int pk_of(int which) { return which == 0 ? 1 : which == 4 ? 3 : which == 5 ? 4 : 0; }
 
 template <typename T, int R>
 static int merged_t(int n, const int* which, const SpmvPart* parts, bool has_alpha, int bmode, const void* alpha,
@@ -1195,7 +1318,7 @@ static int merged_t(int n, const int* which, const SpmvPart* parts, bool has_alp
     if (q.nwork <= 0) continue;
     if (h.n == kMergeMax) return 1;
     const int32_t* list = q.list;
-    if ((knobs().spmv_flags & SPMV_IDLIST) && list && which[i] != 2 && q.nwork == q.A->nslices) list = nullptr;
+    if ((knobs().spmv_flags & SPMV_IDLIST) && list && which[i] != 2 && which[i] != 5 && q.nwork == q.A->nslices) list = nullptr;
     h.a[h.n] = make_args<T>(which[i], q.nwork, list, q.A, q.x, q.y, q.ymap, alpha, beta, q.dotp, &q);
     h.pk[h.n] = pk_of(which[i]);
     sh = sh && h.a[h.n].maxlen <= 8;
@@ -1482,7 +1605,7 @@ void launch_spmv_part(int which, int64_t nwork, const int32_t* list, const pa_ma
                       const void* beta, void* dotp, hipStream_t st, const SpmvPart* cgp) {
   // a slice list as long as the structure is 0..nslices-1 (lists are
   // ascending subsets): launch without it, one dependent load less per wave
-  if ((knobs().spmv_flags & SPMV_IDLIST) && list && which != 2 && nwork == A->nslices) list = nullptr;
+  if ((knobs().spmv_flags & SPMV_IDLIST) && list && which != 2 && which != 5 && nwork == A->nslices) list = nullptr;
 #define spmv_part_(k) spmv_part_##k(which, nwork, list, A, x, y, ymap, has_alpha, bmode, alpha, beta, dotp, st, cgp)
   switch (A->dtype) {
     case PA_F32: spmv_part_(0); break;
@@ -2182,6 +2305,183 @@ void launch_side_fill(pa_mat* A, const int32_t* rows, const int32_t* len, hipStr
     case PA_C64: side_fill_t<c64, 2>(A, rows, len, st); break;
     case PA_C128: side_fill_t<c128, 1>(A, rows, len, st); break;
   }
+}
+
+// ---------------------------------------------------------------------------
+// Triple SELL build (pa_api.cpp build_triple_sell).  Main-layout slot of
+// entry k of row w of slice s (after k_delta16): Float32 delta16 slices are
+// interleaved (lane w % 64, position w / 64), the others blocked (lane
+// w / R, position w % R).
+template <int R>
+__device__ __forceinline__ int64_t main_slot0(int64_t soff, int w) {
+  return kInterleaveD16<R> ? soff + (int64_t)(w & 63) * R + (w >> 6) : soff + (int64_t)(w / R) * R + (w % R);
+}
+
+// per candidate row (oids of the delta16 slices): entries, consecutive
+// triples (len % 3 == 0 and c[3t+1] = c[3t]+1, c[3t+2] = c[3t]+2), ghost
+// reads; info = len | regular << 28 | ghost << 29 | bad << 30 (a column
+// after padding: the layout is not one the triple SELL can take)
+template <int R>
+__global__ void k_t_rowinfo(int64_t n, const int32_t* __restrict__ rows, int H, const int64_t* __restrict__ soff,
+                            const int32_t* __restrict__ slen, const int32_t* __restrict__ col, int64_t noids,
+                            int32_t* __restrict__ info) {
+  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int64_t row = rows[i], s = row / H;
+  const int64_t b = main_slot0<R>(soff[s], (int)(row - s * H));
+  const int L = slen[s];
+  int len = 0;
+  bool reg = true, ghost = false, pad = false, bad = false;
+  int32_t prev = 0;
+  for (int k = 0; k < L; ++k) {
+    const int32_t c = col[b + (int64_t)k * 64 * R];
+    if (c < 0) { pad = true; continue; }
+    if (pad) bad = true;
+    if (len % 3 != 0 && c != prev + 1) reg = false;
+    ghost = ghost || c >= noids;
+    prev = c;
+    ++len;
+  }
+  reg = reg && len > 0 && len % 3 == 0;
+  info[i] = len | (reg ? 1 << 28 : 0) | (ghost ? 1 << 29 : 0) | (bad ? 1 << 30 : 0);
+}
+
+// one wave per triple-SELL slice: the smallest ghost column of its rows
+// (the ghost codes' base) and whether every ghost code fits 15 bits
+template <int R>
+__global__ __launch_bounds__(256) void k_t_gbase(int64_t ns, int64_t nrows, int H, const int32_t* __restrict__ rowlen,
+                                                 const int64_t* __restrict__ src, const int32_t* __restrict__ col,
+                                                 int64_t noids, int32_t* __restrict__ gbase, int32_t* __restrict__ ok) {
+  const int64_t s = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (s >= ns) return;
+  const int lane = threadIdx.x & 63;
+  int32_t gmin = INT32_MAX, gmax = -1;
+  for (int w = lane; w < H; w += 64) {
+    const int64_t i = s * H + w;
+    if (i >= nrows) break;
+    for (int k = 0; k < rowlen[i]; ++k) {
+      const int32_t c = col[src[i] + (int64_t)k * 64 * R];
+      if (c >= noids) { gmin = min(gmin, c); gmax = max(gmax, c); }
+    }
+  }
+  for (int d = 32; d >= 1; d >>= 1) {
+    gmin = min(gmin, __shfl_xor(gmin, d, 64));
+    gmax = max(gmax, __shfl_xor(gmax, d, 64));
+  }
+  if (lane == 0) {
+    gbase[s] = gmin == INT32_MAX ? 0 : gmin;
+    ok[s] = gmin == INT32_MAX || (int64_t)gmax - gmin <= 32766;
+  }
+}
+
+// one thread per triple-SELL row: its values (and, with codes, its 16-bit
+// codes relative to its oid: tri slices one per triple in code group t,
+// the others one per entry) from the main layout; padding: value 0, code
+// 0xFFFF.  values only (codes false): the refresh after new values.
+template <typename E, int R>
+__global__ void k_t_fill(int64_t nrows, int H, const int32_t* __restrict__ rowmap, const int32_t* __restrict__ rowlen,
+                         const int64_t* __restrict__ src, const int64_t* __restrict__ toff,
+                         const int32_t* __restrict__ tlen, const int32_t* __restrict__ gbase,
+                         const int32_t* __restrict__ col, const E* __restrict__ val, int64_t noids, bool codes,
+                         uint16_t* __restrict__ col16, E* __restrict__ tval) {
+  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (i >= nrows) return;
+  const int64_t ts = i / H;
+  const int w = (int)(i - ts * H), lane = w & 63, r = w >> 6;
+  const int32_t lraw = tlen[ts];
+  const int L = lraw & (kTriSlice - 1);
+  const bool tri = (lraw & kTriSlice) != 0;
+  const int n = rowlen[i];
+  const int64_t b = src[i], d = toff[ts];
+  const int32_t oid = rowmap[i], gb = gbase[ts];
+  for (int k = 0; k < L; ++k) {
+    const int64_t sk = b + (int64_t)k * 64 * R;
+    E v;
+    __builtin_memset(&v, 0, sizeof(E));
+    if (k < n) v = val[sk];
+    tval[d + ((int64_t)k * 64 + lane) * R + r] = v;
+    if (!codes || (tri && k % 3 != 0)) continue;
+    uint16_t q = 0xFFFFu;
+    if (k < n) {
+      const int32_t c = col[sk];
+      q = c < noids ? (uint16_t)((uint32_t)(c - oid) & 0x7FFFu) : (uint16_t)(0x8000u | (uint32_t)(c - gb));
+    }
+    const int g = tri ? k / 3 : k;
+    col16[d + ((int64_t)g * 64 + lane) * R + r] = q;
+  }
+}
+
+// build check, one thread per row position of every slice (past the last
+// row too): every code the SpMV will decode gives a column in [-1, ncols)
+// (a tri slice's run c, c+1, c+2 inside x); *bad counts the others
+__global__ void k_t_check(int64_t npos, int64_t nrows, int H, int R, const int32_t* __restrict__ rowmap,
+                          const int64_t* __restrict__ toff, const int32_t* __restrict__ tlen,
+                          const int32_t* __restrict__ gbase, const uint16_t* __restrict__ col16, int64_t ncols,
+                          unsigned* bad) {
+  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (i >= npos) return;
+  const int64_t ts = i / H;
+  const int w = (int)(i - ts * H), lane = w & 63, r = w >> 6;
+  const int32_t lraw = tlen[ts];
+  const bool tri = (lraw & kTriSlice) != 0;
+  const int L = lraw & (kTriSlice - 1), G = tri ? L / 3 : L;
+  const int32_t row = i < nrows ? rowmap[i] : 0;
+  unsigned nb = 0;
+  for (int g = 0; g < G; ++g) {
+    const int32_t c = d16_col(col16[toff[ts] + ((int64_t)g * 64 + lane) * R + r], row, gbase[ts]);
+    if (c < -1 || (c >= 0 && c + (tri ? 2 : 0) >= ncols)) ++nb;
+  }
+  if (nb) atomicAdd(bad, nb);
+}
+
+void launch_t_check(const pa_mat* A, unsigned* bad, hipStream_t st) {
+  const int64_t npos = A->t_nslices * A->H;
+  if (npos == 0) return;
+  hipLaunchKernelGGL(k_t_check, dim3((unsigned)((npos + 255) / 256)), dim3(256), 0, st, npos, A->t_nrows, A->H, A->R,
+                     A->d_t_rowmap, A->d_t_off, A->d_t_len, A->d_t_gbase, A->d_t_col16, A->ncols_lids, bad);
+}
+
+void launch_t_rowinfo(const pa_mat* A, int64_t n, const int32_t* rows, int64_t noids, int32_t* info, hipStream_t st) {
+  if (n == 0) return;
+  const dim3 g((unsigned)((n + 255) / 256)), b(256);
+#define PA_TRI(RR) hipLaunchKernelGGL(k_t_rowinfo<RR>, g, b, 0, st, n, rows, A->H, A->d_slice_off, A->d_slice_len, \
+                                      A->d_col, noids, info)
+  switch (A->R) {
+    case 1: PA_TRI(1); break;
+    case 2: PA_TRI(2); break;
+    case 4: PA_TRI(4); break;
+  }
+#undef PA_TRI
+}
+
+void launch_t_gbase(const pa_mat* A, int64_t noids, int32_t* ok, hipStream_t st) {
+  const int64_t blocks = (A->t_nslices + 3) / 4;
+  if (blocks == 0) return;
+#define PA_TGB(RR) hipLaunchKernelGGL(k_t_gbase<RR>, dim3((unsigned)blocks), dim3(256), 0, st, A->t_nslices, \
+                                      A->t_nrows, A->H, A->d_t_rowlen, A->d_t_src, A->d_col, noids, A->d_t_gbase, ok)
+  switch (A->R) {
+    case 1: PA_TGB(1); break;
+    case 2: PA_TGB(2); break;
+    case 4: PA_TGB(4); break;
+  }
+#undef PA_TGB
+}
+
+// codes false: values only (pa_mat_set_values, fillstored, exchange!(A))
+void launch_t_fill(const pa_mat* A, int64_t noids, bool codes, hipStream_t st) {
+  if (A->t_nrows == 0) return;
+  const dim3 g((unsigned)((A->t_nrows + 255) / 256)), b(256);
+#define PA_TF(E, RR)                                                                                           \
+  hipLaunchKernelGGL((k_t_fill<E, RR>), g, b, 0, st, A->t_nrows, A->H, A->d_t_rowmap, A->d_t_rowlen, A->d_t_src, \
+                     A->d_t_off, A->d_t_len, A->d_t_gbase, A->d_col, (const E*)A->d_val, noids, codes,          \
+                     A->d_t_col16, (E*)A->d_t_val)
+  switch (A->dtype) {
+    case PA_F32: PA_TF(float, 4); break;
+    case PA_F64: PA_TF(double, 2); break;
+    case PA_C64: PA_TF(c64, 2); break;
+    case PA_C128: PA_TF(c128, 1); break;
+  }
+#undef PA_TF
 }
 
 #endif  // PA_DT_DEFINE

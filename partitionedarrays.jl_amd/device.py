@@ -499,6 +499,13 @@ class DeviceMatrix:
         _lib.call("pa_mat_get_values", self.h, a.ctypes.data_as(C.c_void_p))
         return a
 
+    def cg_choice(self) -> int:
+        """the device CG's remembered u-update variant (pa_mat_cg_choice:
+        1 fused, 0 sweep, -1 none yet)"""
+        v = C.c_int(-1)
+        _lib.call("pa_mat_cg_choice", self.h, C.byref(v))
+        return v.value
+
     def info(self):
         v = [C.c_int64() for _ in range(5)]
         _lib.call("pa_mat_info", self.h, *[C.byref(x) for x in v])
@@ -509,6 +516,9 @@ class DeviceMatrix:
         dd = C.c_int64()
         _lib.call("pa_mat_delta16_info", self.h, C.byref(dd))
         d["delta16_slices"] = dd.value
+        t = [C.c_int64() for _ in range(4)]
+        _lib.call("pa_mat_triple_info", self.h, *[C.byref(x) for x in t])
+        d.update(zip(["triple_sell_slices", "triple_sell_rows", "tri_slices", "tri_rows"], [x.value for x in t]))
         lr = [C.c_int64() for _ in range(2)]
         _lib.call("pa_mat_long_rows", self.h, *[C.byref(x) for x in lr])
         d.update(zip(["long_rows", "long_nnz"], [x.value for x in lr]))

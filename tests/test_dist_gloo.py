@@ -278,3 +278,56 @@ def test_rccl_segment_pairing(world, shape):
                 assert any(m[0] == b for m in allm[peer][direction][0]), f"{direction}: {b} waits on {peer}"
     n_nbrs = {2: 1, 4: 3, 8: 7}[world]
     assert npairs == 2 * world * n_nbrs  # every part talks to all others, both directions
+
+
+def _worker_cg_agree(rank, world, port, q):
+    try:
+        sys.path.insert(0, ROOT)
+        os.environ["MASTER_ADDR"] = "127.0.0.1"
+        os.environ["MASTER_PORT"] = str(port)
+        import torch
+        import torch.distributed as dist
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        import pamd
+
+        def allreduce_max(v):
+            t = torch.tensor(v, dtype=torch.float32)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            return t.tolist()
+        # rank-local batch times (ms per iteration: sweep, fused) whose local
+        # choices disagree: rank 0 alone would keep the sweep, rank 1 the
+        # fused update; the max over the ranks is (3.0, 2.5): fused for all
+        local = [[1.0, 2.0], [3.0, 2.5], [2.0, 2.2], [0.5, 0.4]][rank]
+        out = {"local": pamd._lib.cg_variant_agree(local),
+               "agreed": pamd._lib.cg_variant_agree(local, allreduce_max),
+               "invalid": pamd._lib.cg_variant_agree([0.0, 1.0], allreduce_max)}
+        dist.barrier()
+        dist.destroy_process_group()
+        q.put((rank, out))
+    except Exception as e:  # pragma: no cover - surfaced by the parent
+        import traceback
+        q.put((rank, {"error": repr(e) + traceback.format_exc()}))
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_cg_variant_agreement_over_ranks(world):
+    """The device CG's auto u-update choice with one part per process
+    (VERDICT r04 item 7): each rank times its own two batches, the library
+    reduces them with max over the ranks (RCCL in pa_cg_solve_all; here the
+    same decision through pa_cg_variant_agree with a gloo all-reduce), and
+    every rank keeps the same variant even where its local times disagree;
+    without a valid time on any rank there is no choice (-1) on all."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_worker_cg_agree, args=(r, world, port, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = dict(q.get(timeout=240) for _ in range(world))
+    for p in ps:
+        p.join(timeout=60)
+    for r, out in res.items():
+        assert "error" not in out, out.get("error")
+    assert res[0]["local"] == 0 and res[1]["local"] == 1
+    assert {res[r]["agreed"] for r in range(world)} == {1}
+    assert {res[r]["invalid"] for r in range(world)} == {-1}

@@ -55,8 +55,12 @@ def _eq(O, got, ref):
     ((24, 22, 20), 8, np.complex64, 1), ((24, 22, 20), 8, np.float64, 0),
     (BIG[0], 8, np.float64, 1), (BIG[0], 8, np.float32, 1),       # C5 as benched: 8 parts of one device
     ((24, 22, 20), 12, np.float64, 1), ((24, 22, 20), 12, np.complex128, 0)])  # > PA_GROUP_MAX parts
-def test_irregular_spmv_bitexact(be, pamd, O, N, nparts, dtype, fmt):
+@pytest.mark.parametrize("tri16", [2, 0])
+def test_irregular_spmv_bitexact(be, pamd, O, N, nparts, dtype, fmt, tri16):
+    if fmt == 0 and tri16 == 0:
+        pytest.skip("spmv_format 0 runs every slice as int32 ids: the triple SELL is not used")
     prev = pamd._lib.tune("spmv_format", fmt)
+    prev_tri = pamd._lib.tune("spmv_tri16", tri16)
     # pattern slices from 40 % regular rows (default 70): the side SELL gets
     # the rest, so both the pattern and the side-row paths run
     prev_pct = pamd._lib.tune("pattern_min_regular", 40)
@@ -82,6 +86,7 @@ def test_irregular_spmv_bitexact(be, pamd, O, N, nparts, dtype, fmt):
             assert any(i["side_rows"] > 0 for i in info.parts)
     finally:
         pamd._lib.tune("spmv_format", prev)
+        pamd._lib.tune("spmv_tri16", prev_tri)
         pamd._lib.tune("pattern_min_regular", prev_pct)
 
 
@@ -176,8 +181,10 @@ def test_grouped_launches_equal_per_part(be, pamd, dtype, fmt):
 @pytest.mark.parametrize("dtype", [np.float64, np.float32, np.complex128, np.complex64])
 def test_delta16_slices_equal_int32(be, pamd, O, dtype):
     """C5 Voronoi parts: most int32-column slices become delta16 slices (2 B
-    column codes, pa_tune spmv_delta16); mul! is bit-identical with and
-    without them and equals the oracle."""
+    column codes, pa_tune spmv_delta16), re-sliced into the triple SELL (one
+    code per consecutive column triple, spmv_tri16: Float64 / complex by
+    default); mul! is
+    bit-identical with and without them and equals the oracle."""
     N, nparts = (40, 36, 32), 8
     parts = be.get_part_ids(nparts)
     OA = _oracle(O, N, nparts, dtype)
@@ -189,7 +196,7 @@ def test_delta16_slices_equal_int32(be, pamd, O, dtype):
             A = pamd.drivers.irregular_problem(parts, N, 27, dtype)
         finally:
             pamd._lib.tune("spmv_delta16", prev)
-        nd = sum(i["delta16_slices"] for i in A.info().parts)
+        nd = sum(i["delta16_slices"] + i["triple_sell_slices"] for i in A.info().parts)
         assert (nd > 0) == bool(d16)
         if d16:
             xs = {p: _rand(rng, A.cols.partition.local(p).num_lids, dtype) for p in parts.part_ids}
@@ -238,19 +245,27 @@ def test_launch_paths_equal_oracle(be, pamd, O, merge, direct, d16):
 
 
 @pytest.mark.parametrize("dtype", [np.float64, np.float32, np.complex64, np.complex128])
-@pytest.mark.parametrize("d16", [1, 0])
+@pytest.mark.parametrize("d16,tri16", [(1, 2), (1, 0), (0, 0)])
 @pytest.mark.parametrize("tail", [8, 0])
-def test_voronoi_column_loops_equal_oracle(be, pamd, O, dtype, d16, tail):
-    """The int32 / delta16 column loops (Float64: ids one batch ahead;
-    Float32: interleaved delta16 rows), with and without the masked tail
-    batch, α != 1: the Voronoi parts' SpMV gives the oracle's bits for both
-    column encodings and every element type."""
+def test_voronoi_column_loops_equal_oracle(be, pamd, O, dtype, d16, tri16, tail):
+    """The int32 / delta16 / triple-SELL column loops (Float64: ids one
+    batch ahead; Float32: interleaved delta16 rows; the triple SELL: one
+    code and one x run per consecutive column triple), with and without the
+    masked tail batch, α != 1: the Voronoi parts' SpMV gives the oracle's
+    bits for every column encoding and element type."""
     N, nparts = (30, 28, 26), 8
     prev = {"spmv_delta16": pamd._lib.tune("spmv_delta16", d16),
+            "spmv_tri16": pamd._lib.tune("spmv_tri16", tri16),
             "spmv_flags": pamd._lib.tune("spmv_flags", 1 | 4 | 16 | 64 | tail)}
     try:
         parts = be.get_part_ids(nparts)
         A = pamd.drivers.irregular_problem(parts, N, 27, dtype)
+        info = [A.values.local(p).info() for p in parts.part_ids]
+        if tri16:  # the encoding is on and used: triple slices exist; a part with them has no delta16 slice left
+            assert sum(i["tri_rows"] for i in info) > 0
+            assert all(i["delta16_slices"] == 0 for i in info if i["triple_sell_rows"] > 0)
+        else:
+            assert all(i["triple_sell_rows"] == 0 for i in info)
         OA = _oracle(O, N, nparts, dtype)
         rng = np.random.default_rng(SEED + 23)
         xs = {p: _rand(rng, A.cols.partition.local(p).num_lids, dtype) for p in parts.part_ids}
@@ -272,7 +287,8 @@ def test_voronoi_column_loops_equal_oracle(be, pamd, O, dtype, d16, tail):
 @pytest.mark.parametrize("dtype", [np.float32, np.float64])
 def test_voronoi_values_round_trip_through_moved_slots(be, pamd, O, dtype):
     """Float32 delta16 slices move their values to interleaved rows at
-    build time and the CSC nz → slot map follows: get_values returns the
+    build time and the CSC nz → slot map follows, and the triple SELL's
+    copies are refreshed from those slots: get_values returns the
     oracle's nzval in CSC order, set_values writes new values to the right
     slots (mul! with them equals the oracle's), for both element types."""
     N, nparts = (30, 28, 26), 8
@@ -280,7 +296,8 @@ def test_voronoi_values_round_trip_through_moved_slots(be, pamd, O, dtype):
     A = pamd.drivers.irregular_problem(parts, N, 27, dtype)
     OA = _oracle(O, N, nparts, dtype)
     if np.dtype(dtype) == np.float32:
-        assert any(A.values.local(p).info()["delta16_slices"] > 0 for p in parts.part_ids)
+        assert any(A.values.local(p).info()["delta16_slices"] + A.values.local(p).info()["tri_rows"] > 0
+                   for p in parts.part_ids)
     for i, p in enumerate(parts.part_ids):
         assert np.array_equal(A.values.local(p).get_values(), OA.values.parts[i].nzval), p
     rng = np.random.default_rng(SEED + 31)
