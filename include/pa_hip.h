@@ -365,6 +365,10 @@ int pa_mat_delta16_info(const pa_mat* A, int64_t* delta16_slices);
  * triple slices (tri_slices, their rows tri_rows).                       */
 int pa_mat_triple_info(const pa_mat* A, int64_t* t_slices, int64_t* t_rows, int64_t* tri_slices,
                        int64_t* tri_rows);
+/* Rows of pattern slices whose only entry is their diagonal (Dirichlet
+ * rows; pa_tune "spmv_diag_rows", default on): computed inside their slice
+ * from its entry 0 instead of as side rows.                              */
+int pa_mat_diag_rows(const pa_mat* A, int64_t* diag_rows);
 
 /* device addresses of the matrix's main arrays, for placement diagnostics:
  * out[0..7] = values, int32 columns, slice offsets, slice lengths (pattern),

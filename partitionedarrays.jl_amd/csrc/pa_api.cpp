@@ -38,7 +38,7 @@ void launch_delta16(pa_mat* A, int64_t noids, const int32_t* kind, int32_t* ok, 
 void launch_pattern_detect(pa_mat* A, int64_t noids, int min_pct, int32_t* kind, int32_t* plen, int32_t* pat,
                            uint64_t* mask, int32_t* pghost, int32_t* nirreg, hipStream_t st);
 void launch_side_len(pa_mat* A, int64_t n, const int32_t* rows, int32_t* len, int64_t noids,
-                     int32_t* sghost, hipStream_t st);
+                     int32_t* sghost, hipStream_t st, int32_t* diag = nullptr);
 void launch_side_fill(pa_mat* A, const int32_t* rows, const int32_t* len, hipStream_t st);
 void launch_fold(int cplx, int nb, const void* in, void* scratch, void* out, unsigned* ticket, hipStream_t st);
 void launch_fold_cg_alpha(int dtype, int nb, const void* in, void* scratch, void* out, unsigned* ticket,
@@ -88,7 +88,7 @@ void launch_gather_ptrs(int P, const void* const* srcs, int accsz, void* out, hi
 const Knobs kDefaults = {
     /*spmv_flags*/ 93, /*long_exact*/ 1, /*halo_pull*/ 1, /*spmv_delta16*/ 1, /*spmv_merge*/ 1,
     /*spmv_merge_max*/ 65536, /*cg_fuse*/ 2, /*halo_direct*/ 1, /*halo_transport*/ 0, /*spmv_group*/ 1,
-    /*spmv_format*/ 1, /*pattern_min_pct*/ 0, /*issue_threads*/ 1, /*fault_inject*/ 0, /*spmv_tri16*/ 1};
+    /*spmv_format*/ 1, /*pattern_min_pct*/ 0, /*issue_threads*/ 1, /*fault_inject*/ 0, /*spmv_xcd_chunk*/ 0, /*spmv_tri16*/ 1, /*spmv_diag_rows*/ 1};
 // COO → CSC → SELL on the device (pa_coo.hip)
 int coo_compress(int dtype, int index_bytes, int64_t m, int64_t ncols, int64_t n, const void* dI, const void* dJ,
                  const void* dV, int csr, int64_t* nu_out, int32_t** crow, int32_t** ccol, void** cval,
@@ -637,21 +637,59 @@ int finalize_pattern(pa_mat* A, int kmax, int64_t noids) {
     return -1;
   // side SELL
   A->s_nrows = (int64_t)side.size();
+  std::vector<int32_t> rl;  // entries per side row
   if (A->s_nrows > 0) {
     // the side rows (oids = structure rows) through d_s_rowmap
     if (dev_upload(&A->d_s_rowmap, side)) return -1;
     int32_t* srow = A->d_s_rowmap;
-    int32_t* d_dummy = nullptr;
+    int32_t *d_dummy = nullptr, *d_diag = nullptr;
     A->s_nslices = (A->s_nrows + A->H - 1) / A->H;
     HIPC(hipMalloc((void**)&A->d_s_rowlen, A->s_nrows * 4));
     HIPC(hipMalloc((void**)&d_dummy, A->s_nslices * 4));
+    HIPC(hipMalloc((void**)&d_diag, A->s_nrows * 4));
     HIPC(hipMemsetAsync(d_dummy, 0, A->s_nslices * 4, st));
-    launch_side_len(A, A->s_nrows, srow, A->d_s_rowlen, noids, d_dummy, st);
+    launch_side_len(A, A->s_nrows, srow, A->d_s_rowlen, noids, d_dummy, st, d_diag);
     HIPC(hipGetLastError());
-    std::vector<int32_t> rl(A->s_nrows);
+    std::vector<int32_t> dg(A->s_nrows);
+    rl.resize(A->s_nrows);
     HIPC(hipMemcpyAsync(rl.data(), A->d_s_rowlen, A->s_nrows * 4, hipMemcpyDeviceToHost, st));
+    HIPC(hipMemcpyAsync(dg.data(), d_diag, A->s_nrows * 4, hipMemcpyDeviceToHost, st));
     HIPC(hipStreamSynchronize(st));
     dev_free(d_dummy);
+    dev_free(d_diag);
+    // diagonal-only rows (pa_tune "spmv_diag_rows"): computed in their
+    // pattern slice from entry 0 (the dmask bit), not as side rows
+    if (knobs().spmv_diag_rows) {
+      std::vector<uint64_t> dmask(ns * W, 0);
+      std::vector<int32_t> keep, keep_len;
+      for (int64_t i = 0; i < A->s_nrows; ++i) {
+        if (dg[i]) {
+          const int64_t row = side[i], s = row / A->H, w = row - s * A->H;
+          dmask[s * W + w / 64] |= 1ull << (w & 63);
+          ++A->n_diag_rows;
+        } else {
+          keep.push_back(side[i]);
+          keep_len.push_back(rl[i]);
+        }
+      }
+      if (A->n_diag_rows > 0) {
+        if (dev_upload(&A->d_dmask, dmask)) return -1;
+        side = std::move(keep);
+        rl = std::move(keep_len);
+        A->s_nrows = (int64_t)side.size();
+        dev_free(A->d_s_rowmap);
+        dev_free(A->d_s_rowlen);
+        A->d_s_rowmap = A->d_s_rowlen = nullptr;
+        A->s_nslices = 0;
+        if (A->s_nrows > 0) {
+          if (dev_upload(&A->d_s_rowmap, side) || dev_upload(&A->d_s_rowlen, rl)) return -1;
+          A->s_nslices = (A->s_nrows + A->H - 1) / A->H;
+        }
+      }
+    }
+  }
+  if (A->s_nrows > 0) {
+    int32_t* srow = A->d_s_rowmap;
     std::vector<int32_t> slen(A->s_nslices, 0);
     std::vector<int64_t> soff(A->s_nslices);
     for (int64_t i = 0; i < A->s_nrows; ++i) slen[i / A->H] = std::max(slen[i / A->H], rl[i]);
@@ -1289,6 +1327,12 @@ const Knob kKnobs[] = {
      "spmv_tri16: the delta16 slices' rows re-sliced into the triple SELL (rows of consecutive column triples "
      "keep one 16-bit code per triple; matrices built afterwards): 1 = for 8 and 16 B elements (Float64, "
      "ComplexF32, ComplexF64; default), 2 = every element type, 0 = never"},
+    {"spmv_diag_rows", &Knobs::spmv_diag_rows, nullptr, 0, 1, 0,
+     "spmv_diag_rows: 1 = a pattern slice's rows whose only entry is the diagonal (Dirichlet rows) are "
+     "computed in the slice from entry 0 (matrices built afterwards; default), 0 = as side rows"},
+    {"spmv_xcd_chunk", &Knobs::spmv_xcd_chunk, nullptr, 0, 64, 0,
+     "spmv_xcd_chunk: C > 0 = the SpMV launches' workgroups in runs of C consecutive blocks per XCD (x lines "
+     "of neighbouring slices shared in one L2), 0 = the hardware's round robin (default)"},
     {"fault_inject", &Knobs::fault_inject, nullptr, 0, 1, 0,
      "fault_inject: 1 = every job of a threaded issue (IssuePool) also issues an invalid kernel launch (tests "
      "of the error path; test_exception.jl's role), 0 = off (default)"},
@@ -2830,7 +2874,8 @@ int pa_mat_destroy(pa_mat* A) {
                   (void*)A->d_s_col, A->d_s_val, (void*)A->d_s_rowmap, (void*)A->d_s_rowlen, A->d_dotp,
                   (void*)A->d_long_row, (void*)A->d_long_ptr, (void*)A->d_long_col, (void*)A->d_sflags,
                   (void*)A->d_lmask, (void*)A->d_lchunk_start, (void*)A->d_lrow_chunk, A->d_lpart,
-                  (void*)A->d_col16, (void*)A->d_gbase, (void*)A->d_dint_list, (void*)A->d_dbnd_list})
+                  (void*)A->d_col16, (void*)A->d_gbase, (void*)A->d_dint_list, (void*)A->d_dbnd_list,
+                  (void*)A->d_dmask})
     dev_free(p);
   free_triple_sell(A);
   delete A;
@@ -2850,6 +2895,12 @@ int pa_mat_format_info(const pa_mat* A, int64_t* pattern_slices, int64_t* regula
 int pa_mat_delta16_info(const pa_mat* A, int64_t* delta16_slices) {
   CHECK_ARG(A, "null matrix");
   if (delta16_slices) *delta16_slices = A->nd_int + A->nd_bnd;
+  return 0;
+}
+
+int pa_mat_diag_rows(const pa_mat* A, int64_t* diag_rows) {
+  CHECK_ARG(A && diag_rows, "null argument");
+  *diag_rows = A->n_diag_rows;
   return 0;
 }
 
@@ -2892,6 +2943,7 @@ int pa_mat_traffic(const pa_mat* A, int64_t* value_bytes, int64_t* index_bytes, 
     if (kd == 1) {
       v += (int64_t)A->h_plen[s] * H * S;
       m += W * 8 + 8 + 4 + 4;  // mask, offset, length | pattern id, list entry
+      if (A->d_dmask) m += W * 8;  // diagonal-only rows
     } else if (kd == 3) {
       v += (int64_t)A->h_slen[s] * H * S;
       ix += (int64_t)A->h_slen[s] * H * 2;

@@ -310,7 +310,7 @@ struct pa_ctx {
   std::vector<std::pair<std::vector<char>, void*>> merged_cache;
   // pa_ctx_tune: this context's knob values over the process defaults,
   // applied to the calls it leads (TuneScope)
-  static constexpr int kMaxKnobs = 16;
+  static constexpr int kMaxKnobs = 24;
   bool has_over[kMaxKnobs] = {};
   int64_t over[kMaxKnobs] = {};
 };
@@ -338,7 +338,9 @@ struct Knobs {
   int pattern_min_pct;
   int issue_threads;
   int fault_inject;      // tests only: the IssuePool jobs issue an invalid launch
+  int spmv_xcd_chunk;    // XCD-chunked block order of the SpMV launches (pa_spmv.hip xcd_block), 0 off
   int spmv_tri16;        // delta16 slices re-sliced into the triple SELL (pa_mat::d_t_*): 0 never, 1 R <= 2, 2 always
+  int spmv_diag_rows;    // pattern slices compute their diagonal-only rows (pa_mat::d_dmask)
 };
 // the knobs of the call running on this thread (outside a call: a snapshot
 // of the process defaults)
@@ -510,6 +512,11 @@ struct pa_mat {
   int32_t* d_pat = nullptr;          // npatterns*kmax offsets: the distinct patterns (dedup_patterns)
   int64_t npatterns = 0;
   uint64_t* d_mask = nullptr;        // nslices*(H/64) regular-row bits
+  // diagonal-only rows of pattern slices (Dirichlet rows: one entry, column
+  // == row; pa_tune "spmv_diag_rows"): computed in the slice from entry 0
+  // instead of as side rows; null: none
+  uint64_t* d_dmask = nullptr;       // nslices*(H/64) bits
+  int64_t n_diag_rows = 0;
   int32_t* d_pint_list = nullptr;    // pattern mode: pattern slices without ghost reads
   int32_t* d_pbnd_list = nullptr;    // pattern mode: pattern slices reading ghosts
   int64_t np_int = 0, np_bnd = 0;

@@ -108,6 +108,7 @@ struct SpmvArgs {
   const PA_GLB T* val;
   const PA_GLB int32_t* pat;       // kmax offsets per slice
   const PA_GLB uint64_t* mask;     // H/64 words per slice
+  const PA_GLB uint64_t* dmask;    // pattern slices: diagonal-only rows (null: none)
   int kmax;
   const PA_GLB int32_t* rowmap;    // structure row → oid (side SELL), null: identity
   int64_t nrows;            // rows of this structure
@@ -141,6 +142,7 @@ struct SpmvArgs {
   PA_GLB T* un;
   PA_GLB T* xacc;
   const PA_GLB CGState* cg;
+  int xcd_chunk;            // xcd_block (the k_spmv_sell / _group launches; merged: a kernel argument)
 };
 
 template <typename T> struct DAcc { using type = double; };
@@ -587,11 +589,14 @@ __device__ __forceinline__ void rows_t16_tri(T (&acc)[R], const S16Pack<R>* __re
 // pattern rows: column of row `rbase + r` at entry k is rbase + r + pat[k].
 // XP: the lane's R rows read R consecutive x values per entry, fetched as
 // one 16 B run (rows that are not regular get values they never use).
-template <typename T, int R, bool ALPHA, bool NT, int U, bool XP, bool SH = false, typename XS>
+// v0 (DG): the lane's value pack of entry 0 (the diagonal-only rows' one
+// value, spmv_wave), kept from the first batch instead of loaded twice.
+template <typename T, int R, bool ALPHA, bool NT, int U, bool XP, bool SH = false, bool DG = false, typename XS>
 __device__ __forceinline__ void rows_pattern(T (&acc)[R], const int32_t* __restrict__ pat,
                                              const Pack<T, R>* __restrict__ vp, int len,
                                              const XS& x, int64_t rbase,
-                                             const bool (&ok)[R], T alpha, bool pf, bool TB) {
+                                             const bool (&ok)[R], T alpha, bool pf, bool TB,
+                                             Pack<T, R>* v0 = nullptr) {
   if (SH) TB = true;  // short rows (len <= U): the one masked batch is the whole row
   int64_t xb[R];
   bool any = false;
@@ -608,6 +613,7 @@ __device__ __forceinline__ void rows_pattern(T (&acc)[R], const int32_t* __restr
     for (int u = 0; u < U; ++u) o[u] = pat[k + u];
 #pragma unroll
     for (int u = 0; u < U; ++u) v[u] = ld<NT>(&vp[(k + u) * 64]);
+    if (DG && k == 0) *v0 = v[0];
     T xv[U][R];
     if constexpr (XP && R > 1) {
 #pragma unroll
@@ -637,6 +643,7 @@ __device__ __forceinline__ void rows_pattern(T (&acc)[R], const int32_t* __restr
 #pragma unroll
     for (int u = 0; u < U; ++u)
       if (k + u < len) v[u] = ld<NT>(&vp[(k + u) * 64]);
+    if (DG && k == 0) *v0 = v[0];
     T xv[U][R];
     if constexpr (XP && R > 1) {
 #pragma unroll
@@ -666,6 +673,7 @@ __device__ __forceinline__ void rows_pattern(T (&acc)[R], const int32_t* __restr
   for (; !SH && k < len; ++k) {
     const int32_t o = pat[k];
     const Pack<T, R> v = ld<NT>(&vp[k * 64]);
+    if (DG && k == 0) *v0 = v;
 #pragma unroll
     for (int r = 0; r < R; ++r) {
       acc[r] = acc[r] + term<ALPHA>(v.v[r], x.get(xb[r] >= 0 ? xb[r] + o : 0), alpha, pf);
@@ -682,10 +690,11 @@ __device__ __forceinline__ void rows_pattern(T (&acc)[R], const int32_t* __restr
 // rows_pattern.  Library A/B on one box (profiles/r04/p/): FE27 256^3 one
 // part 0.6744 -> 0.6523 ms, the (2,2,2) halo leg 0.714 -> 0.688 ms, C5 F64
 // -1.0 %: one x load in three fewer relieves the per-CU memory pipeline.
-template <typename T, int R, bool ALPHA, bool NT, typename XS>
+template <typename T, int R, bool ALPHA, bool NT, bool DG = false, typename XS>
 __device__ __forceinline__ void rows_pattern_tri(T (&acc)[R], const int32_t* __restrict__ pat,
                                                  const Pack<T, R>* __restrict__ vp, int len, const XS& x,
-                                                 int64_t rbase, const bool (&ok)[R], T alpha, bool pf) {
+                                                 int64_t rbase, const bool (&ok)[R], T alpha, bool pf,
+                                                 Pack<T, R>* v0 = nullptr) {
   static_assert(R > 1, "runs of R > 1 values");
   bool any = false;
 #pragma unroll
@@ -709,6 +718,7 @@ __device__ __forceinline__ void rows_pattern_tri(T (&acc)[R], const int32_t* __r
     Pack<T, R> v[3 * TB];
 #pragma unroll
     for (int u = 0; u < 3 * TB; ++u) v[u] = ld<NT>(&vp[(k + u) * 64]);
+    if (DG && k == 0) *v0 = v[0];
     T xv[TB][3][R];
 #pragma unroll
     for (int t = 0; t < TB; ++t) triple(o[t], xv[t]);
@@ -724,6 +734,7 @@ __device__ __forceinline__ void rows_pattern_tri(T (&acc)[R], const int32_t* __r
     Pack<T, R> v[3];
 #pragma unroll
     for (int j = 0; j < 3; ++j) v[j] = ld<NT>(&vp[(k + j) * 64]);
+    if (DG && k == 0) *v0 = v[0];
     T xv[3][R];
     triple(o, xv);
 #pragma unroll
@@ -876,6 +887,32 @@ __device__ __forceinline__ void spmv_wave(const SpmvArgs<T>& a, const int64_t w)
   const Pack<T, R>* __restrict__ vp = reinterpret_cast<const Pack<T, R>*>(a.val + off) + lane;
   const bool tb = (a.flags & SPMV_TAILB) != 0;
   const bool pf = (a.flags & SPMV_PRODA) != 0;
+  // Diagonal-only rows of a pattern slice (pa_tune "spmv_diag_rows": a
+  // Dirichlet row, its one entry at column == row, e.g. the domain-face rows
+  // at both ends of every x-line): not on the slice's pattern, yet no side
+  // rows — before the pattern loop, the lanes holding one read their entry-0
+  // pack and store y = β-init + v·x[row], the reference's one term
+  // (SparseUtils.jl:176-185 over one entry); the loop's sum for the row is
+  // never stored (ok false).  Nothing stays live across the loop.
+  unsigned dbits = 0;
+  if constexpr (PK == 1) {
+    if (a.dmask) {
+      const uint64_t dm = a.dmask[s * (H / 64) + (lane * R) / 64];
+      dbits = (unsigned)(dm >> ((lane * R) & 63)) & ((1u << R) - 1u);
+      if (dbits) {
+        const Pack<T, R> v0 = ld<false>(&vp[0]);
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          const int64_t i = row0 + r;
+          if (!((dbits >> r) & 1u) || i >= a.nrows) continue;
+          const int64_t yl = a.ymap ? (int64_t)a.ymap[i] : i;
+          T init = zero_of<T>();
+          if (BMODE != 0) init = (BMODE == 2) ? a.y[yl] * a.beta : a.y[yl];
+          a.y[yl] = init + term<ALPHA>(v0.v[r], xs.get(i), a.alpha, pf);
+        }
+      }
+    }
+  }
   if constexpr (PK == 1) {
     const int32_t* pat = a.pat + (int64_t)(lraw >> 9) * a.kmax;
     bool tri_done = false;
@@ -937,6 +974,12 @@ __device__ __forceinline__ void spmv_wave(const SpmvArgs<T>& a, const int64_t w)
       if constexpr (XV) uv = main_rows ? un[r] : xs.get(orow[r]);
       else uv = a.dotu[orow[r]];
       if (ok[r]) part = part + dacc(cdot(uv, acc[r]));
+      if (PK == 1 && ((dbits >> r) & 1u) && row0 + r < a.nrows) {  // a diagonal-only row: its stored y
+        const int64_t i = row0 + r;
+        if constexpr (XV) uv = main_rows ? un[r] : xs.get(i);
+        else uv = a.dotu[i];
+        part = part + dacc(cdot(uv, a.y[a.ymap ? (int64_t)a.ymap[i] : i]));
+      }
     }
 #pragma unroll
     for (int d = 32; d >= 1; d >>= 1) part = part + shfl_down_acc(part, d);
@@ -968,9 +1011,26 @@ __device__ __forceinline__ void spmv_wave(const SpmvArgs<T>& a, const int64_t w)
   }
 }
 
+// XCD-chunked block order (pa_tune "spmv_xcd_chunk" C > 0): the hardware
+// deals workgroups to the 8 XCDs round robin (block b on XCD b % 8), so
+// consecutive slices land on different XCDs and each XCD's L2 fetches the x
+// lines of its neighbours' slices too (C2: x fetched 1.59 times,
+// profiles/r05/a/c2_pmc_per_kind.json).  With C, XCD k works on runs of C
+// consecutive logical blocks: logical = (b / 8C)·8C + (b % 8)·C + (b / 8) % C
+// (blocks past the last full group of 8C keep their order).  C = 4 keeps a
+// block and the one 32 blocks away (128 slices: FD7 128³'s z neighbour; a
+// divisor of FE27 256³'s) on the same XCD, as the round robin does.
+__device__ __forceinline__ int64_t xcd_block(int chunk) {
+  const int64_t b = blockIdx.x;
+  if (chunk <= 0) return b;
+  const int64_t G = 8 * (int64_t)chunk, full = ((int64_t)gridDim.x / G) * G;
+  if (b >= full) return b;
+  return (b / G) * G + (b % 8) * chunk + (b / 8) % chunk;
+}
+
 template <typename T, int R, bool ALPHA, int BMODE, int U, int PK, bool SH = false, bool XV = false>
 __global__ __launch_bounds__(256) void k_spmv_sell(SpmvArgs<T> a) {
-  const int64_t w = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int64_t w = xcd_block(a.xcd_chunk) * 4 + (threadIdx.x >> 6);
   if (w >= a.nwork) return;
   spmv_wave<T, R, ALPHA, BMODE, U, PK, SH, XV>(a, w);
 }
@@ -990,7 +1050,7 @@ struct SpmvGroup {
 template <typename T, int R, bool ALPHA, int BMODE, int U, int PK, bool SH = false, bool XV = false>
 __global__ __launch_bounds__(256) void k_spmv_sell_group(const SpmvGroup<T> g) {
   // wave-uniform: the part's arguments are read with scalar loads
-  const int64_t w = (int64_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const int64_t w = xcd_block(g.a[0].xcd_chunk) * 4 + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   if (w >= g.start[g.np]) return;
   int p = 0;
   while (p + 1 < g.np && w >= g.start[p + 1]) ++p;
@@ -1090,6 +1150,7 @@ static SpmvArgs<T> make_args(int which, int64_t nwork, const int32_t* list, cons
   a.alpha = *(const T*)alpha;
   a.beta = *(const T*)beta;
   a.flags = knobs().spmv_flags | (A->csr ? SPMV_PRODA : 0);
+  a.xcd_chunk = knobs().spmv_xcd_chunk;
   a.maxlen = which == 0   ? A->maxlen_pat
              : which == 2 ? A->maxlen_side
              : which == 1 ? ((knobs().spmv_format == 1 && A->has_pat) ? A->maxlen_pm_int : A->maxlen_all)
@@ -1120,6 +1181,7 @@ static SpmvArgs<T> make_args(int which, int64_t nwork, const int32_t* list, cons
       a.slen = (decltype(a.slen))(A->d_plen);
       a.pat = (decltype(a.pat))(A->d_pat);
       a.mask = (decltype(a.mask))(A->d_mask);
+      a.dmask = (decltype(a.dmask))(A->d_dmask);
       a.kmax = A->kmax;
     } else {
       a.slen = (decltype(a.slen))(A->d_slice_len);
@@ -1245,10 +1307,10 @@ struct SpmvTable {
 };
 
 template <typename T, int R, bool ALPHA, int BMODE, int U, bool SH, bool XV = false>
-__device__ __forceinline__ void merged_wave(const SpmvTable<T>* __restrict__ tab, int n, int64_t waves) {
+__device__ __forceinline__ void merged_wave(const SpmvTable<T>* __restrict__ tab, int n, int64_t waves, int xc) {
   // n and the wave count come as kernel arguments (with the kernarg load, not
   // two dependent table loads ahead of the search)
-  const int64_t w = (int64_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const int64_t w = xcd_block(xc) * 4 + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   if (w >= waves) return;
   int lo = 0, hi = n;  // last entry whose start <= w
   while (hi - lo > 1) {
@@ -1275,8 +1337,8 @@ __device__ __forceinline__ void merged_wave(const SpmvTable<T>* __restrict__ tab
 // (profiles/r02/stream/ab_waves4.txt).
 template <typename T, int R, bool ALPHA, int BMODE, int U, bool SH, bool XV = false>
 __global__ __launch_bounds__(256) void k_spmv_merged(const SpmvTable<T>* __restrict__ tab, int n,
-                                                         int64_t waves) {
-  merged_wave<T, R, ALPHA, BMODE, U, SH, XV>(tab, n, waves);
+                                                         int64_t waves, int xc) {
+  merged_wave<T, R, ALPHA, BMODE, U, SH, XV>(tab, n, waves, xc);
 }
 
 // F64 short rows (FD7): 5 waves per SIMD instead of 4 (96 VGPRs instead of
@@ -1285,24 +1347,25 @@ __global__ __launch_bounds__(256) void k_spmv_merged(const SpmvTable<T>* __restr
 // F32/C64 (R = 4 / complex: ~200 spills) nor for longer rows (FE27: -10 %).
 template <typename T, int R, bool ALPHA, int BMODE>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k_spmv_merged_short(
-    const SpmvTable<T>* __restrict__ tab, int n, int64_t waves) {
-  merged_wave<T, R, ALPHA, BMODE, 8, true>(tab, n, waves);
+    const SpmvTable<T>* __restrict__ tab, int n, int64_t waves, int xc) {
+  merged_wave<T, R, ALPHA, BMODE, 8, true>(tab, n, waves, xc);
 }
 
 template <typename T, int R, bool ALPHA, int BMODE>
 static void launch_merged_t(const SpmvTable<T>* d, int n, int64_t waves, bool sh, hipStream_t st) {
+  const int xc = knobs().spmv_xcd_chunk;
   const int64_t blocks = (waves + 3) / 4;
   if (blocks == 0) return;
   if constexpr (std::is_same<T, double>::value) {
     if (sh) {
-      hipLaunchKernelGGL((k_spmv_merged_short<T, R, ALPHA, BMODE>), dim3(blocks), dim3(256), 0, st, d, n, waves);
+      hipLaunchKernelGGL((k_spmv_merged_short<T, R, ALPHA, BMODE>), dim3(blocks), dim3(256), 0, st, d, n, waves, xc);
       return;
     }
   }
   if (sh)
-    hipLaunchKernelGGL((k_spmv_merged<T, R, ALPHA, BMODE, 8, true>), dim3(blocks), dim3(256), 0, st, d, n, waves);
+    hipLaunchKernelGGL((k_spmv_merged<T, R, ALPHA, BMODE, 8, true>), dim3(blocks), dim3(256), 0, st, d, n, waves, xc);
   else
-    hipLaunchKernelGGL((k_spmv_merged<T, R, ALPHA, BMODE, 8, false>), dim3(blocks), dim3(256), 0, st, d, n, waves);
+    hipLaunchKernelGGL((k_spmv_merged<T, R, ALPHA, BMODE, 8, false>), dim3(blocks), dim3(256), 0, st, d, n, waves, xc);
 }
 
 static int pk_of(int which) { return which == 0 ? 1 : which == 4 ? 3 : which == 5 ? 4 : 0; }
@@ -1360,8 +1423,9 @@ static int merged_t(int n, const int* which, const SpmvPart* parts, bool has_alp
   if (h.a[0].cg) {  // the device CG's fused u update (α = 1, β = 0)
     const int64_t blocks = (waves + 3) / 4;
     if (blocks == 0) return 0;
-    if (sh) hipLaunchKernelGGL((k_spmv_merged<T, R, false, 0, 8, true, true>), dim3(blocks), dim3(256), 0, st, dt, h.n, waves);
-    else hipLaunchKernelGGL((k_spmv_merged<T, R, false, 0, 8, false, true>), dim3(blocks), dim3(256), 0, st, dt, h.n, waves);
+    const int xc = knobs().spmv_xcd_chunk;
+    if (sh) hipLaunchKernelGGL((k_spmv_merged<T, R, false, 0, 8, true, true>), dim3(blocks), dim3(256), 0, st, dt, h.n, waves, xc);
+    else hipLaunchKernelGGL((k_spmv_merged<T, R, false, 0, 8, false, true>), dim3(blocks), dim3(256), 0, st, dt, h.n, waves, xc);
     return 0;
   }
   if (!has_alpha) {
@@ -2218,10 +2282,12 @@ void launch_pattern_detect(pa_mat* A, int64_t noids, int min_pct, int32_t* kind,
 }
 
 // Side SELL: the irregular rows (oids, ascending), copied from the int32 layout.
+// (diag: 1 for a row whose only entry is its diagonal, column == row)
 template <int R>
 __global__ void k_side_len(int64_t n, const int32_t* __restrict__ rows, const int64_t* __restrict__ soff,
                            const int32_t* __restrict__ slen, const int32_t* __restrict__ col,
-                           int32_t* __restrict__ len, int64_t noids, int32_t* __restrict__ sghost, int sH) {
+                           int32_t* __restrict__ len, int64_t noids, int32_t* __restrict__ sghost, int sH,
+                           int32_t* __restrict__ diag) {
   constexpr int H = 64 * R;
   const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   if (i >= n) return;
@@ -2239,6 +2305,7 @@ __global__ void k_side_len(int64_t n, const int32_t* __restrict__ rows, const in
   }
   len[i] = l;
   if (g) atomicOr(&sghost[i / sH], 1);
+  if (diag) diag[i] = l == 1 && col[soff[s] + (int64_t)lane * R + r] == (int32_t)row;
 }
 
 template <typename T, int R>
@@ -2279,13 +2346,13 @@ __global__ void k_side_fill(int64_t n, const int32_t* __restrict__ rows, const i
 }
 
 void launch_side_len(pa_mat* A, int64_t n, const int32_t* rows, int32_t* len, int64_t noids,
-                     int32_t* sghost, hipStream_t st) {
+                     int32_t* sghost, hipStream_t st, int32_t* diag) {
   if (n == 0) return;
   const dim3 g((unsigned)((n + 255) / 256)), b(256);
   switch (A->R) {
-    case 1: hipLaunchKernelGGL(k_side_len<1>, g, b, 0, st, n, rows, A->d_slice_off, A->d_slice_len, A->d_col, len, noids, sghost, A->H); break;
-    case 2: hipLaunchKernelGGL(k_side_len<2>, g, b, 0, st, n, rows, A->d_slice_off, A->d_slice_len, A->d_col, len, noids, sghost, A->H); break;
-    case 4: hipLaunchKernelGGL(k_side_len<4>, g, b, 0, st, n, rows, A->d_slice_off, A->d_slice_len, A->d_col, len, noids, sghost, A->H); break;
+    case 1: hipLaunchKernelGGL(k_side_len<1>, g, b, 0, st, n, rows, A->d_slice_off, A->d_slice_len, A->d_col, len, noids, sghost, A->H, diag); break;
+    case 2: hipLaunchKernelGGL(k_side_len<2>, g, b, 0, st, n, rows, A->d_slice_off, A->d_slice_len, A->d_col, len, noids, sghost, A->H, diag); break;
+    case 4: hipLaunchKernelGGL(k_side_len<4>, g, b, 0, st, n, rows, A->d_slice_off, A->d_slice_len, A->d_col, len, noids, sghost, A->H, diag); break;
   }
 }
 

@@ -432,3 +432,53 @@ def test_threaded_issue_reports_launch_failures(pamd, O):
             assert np.array_equal(y.to_host().local(p)[own], oy.values[p][own]), p
     finally:
         pamd._lib.tune("issue_threads", prev)
+
+
+@pytest.mark.parametrize("kind,N,dtype", [(27, (40, 33, 9), np.float64), (7, (36, 30, 8), np.float64),
+                                          (27, (34, 12, 10), np.float32), (27, (40, 9, 8), np.complex128)])
+@pytest.mark.parametrize("diag", [1, 0])
+def test_diagonal_only_rows_equal_oracle(be, pamd, O, kind, N, dtype, diag):
+    """Dirichlet rows (one entry, column == row) inside pattern slices
+    (pa_tune spmv_diag_rows): computed in their slice
+    from entry 0 (1) or as side rows (0); mul! with α/β, the fused dot of the
+    CG (mul_dot_) and β = 1 all give the oracle's bits, and with the knob on
+    no Dirichlet row is a side row."""
+    prev = pamd._lib.tune("spmv_diag_rows", diag)
+    try:
+        shape = (2, 1, 1)
+        parts = be.get_part_ids(shape)
+        A = pamd.drivers.stencil_operator(parts, N, kind, dtype)
+        OA = O.stencil_problem(O.get_part_ids(shape), N, kind, dtype)
+        info = [A.values.local(p).info() for p in parts.part_ids]
+        if diag:
+            assert all(i["diag_rows"] > 0 and i["side_rows"] == 0 for i in info), info
+        else:
+            assert all(i["diag_rows"] == 0 and i["side_rows"] > 0 for i in info), info
+        rng = np.random.default_rng(SEED + 41)
+        xs = {p: _rand(rng, A.cols.partition.local(p).num_lids, dtype) for p in parts.part_ids}
+        ys = {p: _rand(rng, A.rows.partition.local(p).num_lids, dtype) for p in parts.part_ids}
+        x = pamd.PVector.from_host(pamd.map_parts(lambda s: xs[s.part], A.cols.partition), A.cols)
+        ox = O.PVector(O.map_parts(lambda s: _to_oracle(O, xs[s.part]), OA.cols.partition), OA.cols)
+        sc = np.float32 if np.dtype(dtype) in (np.float32, np.complex64) else np.float64
+        for alpha, beta in ((1.0, 0.0), (0.7, 0.0), (1.0, 1.0), (-1.3, 0.5)):
+            y = pamd.PVector.from_host(pamd.map_parts(lambda s: ys[s.part], A.rows.partition), A.rows)
+            oy = O.PVector(O.map_parts(lambda s: _to_oracle(O, ys[s.part]), OA.rows.partition), OA.rows)
+            pamd.mul_(y, A, x, alpha, beta)
+            O.mul_(oy, OA, ox, sc(alpha), sc(beta))
+            got = y.to_host()
+            for p in parts.part_ids:
+                own = A.rows.partition.local(p).oid_to_lid - 1
+                assert _eq(O, got.local(p)[own], _sel(O, oy.values[p], own)), (alpha, beta, p)
+        if np.dtype(dtype) == np.float64 and kind == 27:  # the CG's fused dot(x, A*x) over the owned rows
+            xc = pamd.PVector.from_host(pamd.map_parts(lambda s: xs[s.part][:s.num_lids], A.cols.partition), A.cols)
+            yc = pamd.PVector.undef(A.cols)
+            d = pamd.mul_dot_(yc, A, xc)
+            oyc = O.pvector_undef(OA.cols, np.float64)
+            O.mul_(oyc, OA, ox)
+            ref = 0.0
+            for p in parts.part_ids:
+                own = np.asarray(OA.cols.partition[p].oid_to_lid) - 1
+                ref += float(np.dot(xs[p][own], oyc.values[p][own]))
+            assert abs(d - ref) <= 1e-12 * max(1.0, abs(ref)), (d, ref)
+    finally:
+        pamd._lib.tune("spmv_diag_rows", prev)
