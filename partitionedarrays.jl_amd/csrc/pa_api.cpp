@@ -53,6 +53,7 @@ void launch_cg_ghost(int dtype, int64_t lo, int64_t hi, const void* r, const voi
 void launch_cg_alpha(int dtype, int P, const void* gathered, CGState* cst, hipStream_t st);
 void launch_cg_step(int dtype, int P, const double* gathered, CGState* cst, double* history, hipStream_t st);
 void launch_gather_ptrs(int P, const void* const* srcs, int accsz, void* out, hipStream_t st);
+void launch_gather_scatter(int P, const void* const* srcs, int accsz, int nd, void* const* dsts, hipStream_t st);
 // Process defaults of the tuning knobs (pa_tune; the per-call Knobs of
 // pa_internal.h).  Why each default:
 //  * halo_pull 1: pull-unpack between parts of one process;
@@ -88,7 +89,8 @@ void launch_gather_ptrs(int P, const void* const* srcs, int accsz, void* out, hi
 const Knobs kDefaults = {
     /*spmv_flags*/ 93, /*long_exact*/ 1, /*halo_pull*/ 1, /*spmv_delta16*/ 1, /*spmv_merge*/ 1,
     /*spmv_merge_max*/ 65536, /*cg_fuse*/ 2, /*halo_direct*/ 1, /*halo_transport*/ 0, /*spmv_group*/ 1,
-    /*spmv_format*/ 1, /*pattern_min_pct*/ 0, /*issue_threads*/ 1, /*fault_inject*/ 0, /*spmv_xcd_chunk*/ 0, /*spmv_tri16*/ 1, /*spmv_diag_rows*/ 1};
+    /*spmv_format*/ 1, /*pattern_min_pct*/ 0, /*issue_threads*/ 1, /*fault_inject*/ 0, /*spmv_xcd_chunk*/ 0, /*spmv_tri16*/ 1, /*spmv_diag_rows*/ 0,
+    /*halo_barrier*/ 1, /*side_fork*/ 0};
 // COO → CSC → SELL on the device (pa_coo.hip)
 int coo_compress(int dtype, int index_bytes, int64_t m, int64_t ncols, int64_t n, const void* dI, const void* dJ,
                  const void* dV, int csr, int64_t* nu_out, int32_t** crow, int32_t** ccol, void** cval,
@@ -114,12 +116,13 @@ int coo_assemble_pack(int dtype, int64_t n, const int64_t* I, const int64_t* J, 
                       void** sV, std::vector<int64_t>* cnt, hipStream_t st);
 int gids_first_touch(int64_t n, const int64_t* gids, const uint64_t* sgid, const int64_t* slid, int64_t nl,
                      int64_t** out, int64_t* m_out, hipStream_t st);
+// ev (optional): recorded on st when the kernel completes (one runtime call)
 void launch_pack(int dtype, int64_t n, const int32_t* lids, const void* v, void* buf,
-                 hipStream_t st);
+                 hipStream_t st, hipEvent_t ev = nullptr);
 void launch_unpack(int dtype, int64_t n, const int32_t* lids, const pa_combine_plan& plan, int op,
                    const void* buf, void* v, hipStream_t st);
 void launch_pull(int dtype, int64_t n, const int32_t* lids, const pa_combine_plan& plan, int op, const int32_t* bid,
-                 const int64_t* elem, const void* const* bases, void* v, hipStream_t st);
+                 const int64_t* elem, const void* const* bases, void* v, hipStream_t st, hipEvent_t ev = nullptr);
 void launch_fill(int dtype, int64_t n, int64_t base, const int32_t* map, void* v, const void* s,
                  hipStream_t st);
 int launch_spmv_merged(int n, const int* which, const SpmvPart* parts, bool has_alpha, int bmode,
@@ -774,11 +777,16 @@ inline hipStream_t SC(const pa_ctx* c) { return g_capture_stream ? g_capture_str
 
 // Pull table of receiver i for direction dir (see pa_pull): built once per
 // set of local senders; ok = false when a sender's device is not reachable
-// by peer access (then the staging copies below are used).
-int build_pull(int i, int n, pa_xchg* const xg[], const LocalSet& L, int dtype, int dir) {
+// by peer access (then the staging copies below are used).  alt: the
+// forward table against the senders' second send buffers (d_buf_snd2, the
+// barrier issue of spmv_impl).
+int build_pull(int i, int n, pa_xchg* const xg[], const LocalSet& L, int dtype, int dir, bool alt = false) {
   pa_xchg* X = xg[i];
   pa_ctx* c = X->ctx;
-  pa_pull& P = X->pull[dir];
+  pa_pull& P = alt ? X->pull_alt : X->pull[dir];
+  auto sender_buf = [&](const pa_xchg* Q) -> void* {
+    return alt ? Q->d_buf_snd2 : (dir == 0 ? Q->d_buf_snd : Q->d_buf_rcv);
+  };
   const auto& prcv = dir == 0 ? X->parts_rcv : X->parts_snd;
   const auto& orcv = dir == 0 ? X->ptrs_rcv : X->ptrs_snd;
   void* own = dir == 0 ? X->d_buf_rcv : X->d_buf_snd;
@@ -787,7 +795,7 @@ int build_pull(int i, int n, pa_xchg* const xg[], const LocalSet& L, int dtype, 
   for (int32_t q : prcv) {
     const int j = L.find(q);
     key.push_back(j >= 0 ? (const void*)(uintptr_t)xg[j]->id : nullptr);
-    key.push_back(j >= 0 ? (dir == 0 ? xg[j]->d_buf_snd : xg[j]->d_buf_rcv) : own);
+    key.push_back(j >= 0 ? sender_buf(xg[j]) : own);
   }
   if (P.built && P.key == key) return 0;
   dev_free(P.d_bid);
@@ -832,7 +840,7 @@ int build_pull(int i, int n, pa_xchg* const xg[], const LocalSet& L, int dtype, 
       if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) HIPC(e);
       (void)hipGetLastError();
     }
-    const int32_t b = base_id(dir == 0 ? Q->d_buf_snd : Q->d_buf_rcv);
+    const int32_t b = base_id(sender_buf(Q));
     for (int64_t t = 0; t < cnt; ++t) { bid[orcv[k] + t] = b; elem[orcv[k] + t] = qo[m] + t; }
   }
   if (dev_upload(&P.d_bid, bid) || dev_upload(&P.d_elem, elem) || dev_upload(&P.d_bases, bases)) return -1;
@@ -960,6 +968,7 @@ struct TransportPlan {
   LocalSet L;
   bool remote = false;
   bool pull = false;
+  bool alt = false;  // the pull reads the senders' second buffers (pull_alt)
   size_t S = 0;
   int dtype = 0, dir = 0, op = 0;
 };
@@ -1007,17 +1016,21 @@ int transport_local(int i, pa_xchg* const xg[], pa_vec* const v[], const Transpo
   const size_t S = T.S;
   HIPC(hipSetDevice(c->device));
   if (T.pull) {
-    const pa_pull& P = X->pull[dir];
+    const pa_pull& P = T.alt ? X->pull_alt : X->pull[dir];
     const int32_t* bid = graph_owned<int32_t>(P.d_bid, P.h_bid);
     const int64_t* elem = graph_owned<int64_t>(P.d_elem, P.h_elem);
     void* const* bases = graph_owned<void*>(P.d_bases, P.h_bases);
     CHECK_ARG(!(g_capture_tables && g_graph_owned_failed), "graph capture: table allocation failed");
+    // the pull's completion is ev_recvd (recorded with the launch; not
+    // during a graph capture)
+    hipEvent_t ev = g_capture_stream ? nullptr : c->ev_recvd;
     if (dir == 0)
       launch_pull(T.dtype, X->n_rcv_data, X->d_lids_rcv, X->plan_fwd, T.op, bid, elem, (const void* const*)bases,
-                  v[i]->d, SC(c));
+                  v[i]->d, SC(c), ev);
     else
       launch_pull(T.dtype, X->n_snd_data, X->d_lids_snd, X->plan_rev, T.op, bid, elem, (const void* const*)bases,
-                  v[i]->d, SC(c));
+                  v[i]->d, SC(c), ev);
+    return 0;
   } else {
     // staging copies: receiver r, segment k from sender q (local), which
     // holds the matching segment at the position of r in its send list
@@ -1122,6 +1135,7 @@ bool g_capturing = false;  // inside pa_spmv_graph_create: one replay never over
 // before part i packs into its send buffer: the previous exchange's reads
 // of it (its own unpack and its receivers' pulls) are done
 int pre_pack_wait_part(int i, pa_xchg* const xg[], const LocalSet& L) {
+  xg[i]->fast_key = 0;  // the next barrier call of these exchangers waits too (spmv_impl)
   if (g_capturing) return 0;
   pa_ctx* c = xg[i]->ctx;
   HIPC(hipSetDevice(c->device));
@@ -1329,7 +1343,15 @@ const Knob kKnobs[] = {
      "ComplexF32, ComplexF64; default), 2 = every element type, 0 = never"},
     {"spmv_diag_rows", &Knobs::spmv_diag_rows, nullptr, 0, 1, 0,
      "spmv_diag_rows: 1 = a pattern slice's rows whose only entry is the diagonal (Dirichlet rows) are "
-     "computed in the slice from entry 0 (matrices built afterwards; default), 0 = as side rows"},
+     "computed in the slice from entry 0 (matrices built afterwards), 0 = as side rows (default: faster, "
+     "profiles/r05/i/)"},
+    {"halo_barrier", &Knobs::halo_barrier, nullptr, 0, 1, 0,
+     "halo_barrier: mul! over parts with their own stream pairs and local neighbours (one process driving "
+     "several GPUs): 1 = one pack barrier event per call and double-buffered send buffers (default), 0 = "
+     "per-neighbour event waits before every pack and every pull"},
+    {"spmv_side_fork", &Knobs::side_fork, nullptr, 0, 1, 0,
+     "spmv_side_fork: per-kind launches without a halo in flight (big single parts): 1 = the side rows run on "
+     "the comm stream beside the pattern slices (default), 0 = after them on the compute stream"},
     {"spmv_xcd_chunk", &Knobs::spmv_xcd_chunk, nullptr, 0, 64, 0,
      "spmv_xcd_chunk: C > 0 = the SpMV launches' workgroups in runs of C consecutive blocks per XCD (x lines "
      "of neighbouring slices shared in one L2), 0 = the hardware's round robin (default)"},
@@ -1589,6 +1611,9 @@ int pa_ctx_destroy(pa_ctx* c) {
   if (c->h_pinned) (void)hipHostFree(c->h_pinned);
   for (auto& e : c->tev) (void)hipEventDestroy(e);
   for (auto& e : c->span_ev)
+    if (e) (void)hipEventDestroy(e);
+  if (c->ev_barrier) (void)hipEventDestroy(c->ev_barrier);
+  for (auto& e : c->ev_side)
     if (e) (void)hipEventDestroy(e);
   if (c->stream_refs && --c->stream_refs->n == 0) {  // the last context of a shared stream pair
     (void)hipEventDestroy(c->ev_packed);
@@ -1906,9 +1931,10 @@ int pa_xchg_destroy(pa_xchg* X) {
   dev_free(X->d_lids_snd);
   dev_free(X->d_buf_rcv);
   dev_free(X->d_buf_snd);
+  dev_free(X->d_buf_snd2);
   free_plan(X->plan_fwd);
   free_plan(X->plan_rev);
-  for (pa_pull* t : {&X->pull[0], &X->pull[1], &X->direct}) {
+  for (pa_pull* t : {&X->pull[0], &X->pull[1], &X->direct, &X->pull_alt}) {
     dev_free(t->d_bid);
     dev_free(t->d_elem);
     dev_free(t->d_bases);
@@ -3097,6 +3123,7 @@ static int spmv_grouped(int n, pa_mat* const A[], pa_vec* const y[], const pa_in
   } else if (any_x) {
     // the previous exchange's pulls read the send buffers: pack after them
     if (!g_capturing) HIPC(hipStreamWaitEvent(c0->s_main, c0->ev_recvd, 0));
+    for (int i = 0; i < n; ++i) xg[i]->fast_key = 0;
     PackGroup pg{};
     PullGroup qg{};
     for (int i0 = 0; i0 < n; i0 += PA_GROUP_MAX) {
@@ -3144,8 +3171,8 @@ static int spmv_grouped(int n, pa_mat* const A[], pa_vec* const y[], const pa_in
     }
     return q;
   };
-  auto launch_all = [&](int which, const std::vector<SpmvPart>& v) {
-    if (!v.empty()) launch_spmv_group(which, (int)v.size(), v.data(), has_alpha, bmode, alpha, beta, sm);
+  auto launch_all = [&](int which, const std::vector<SpmvPart>& v, hipStream_t st = nullptr) {
+    if (!v.empty()) launch_spmv_group(which, (int)v.size(), v.data(), has_alpha, bmode, alpha, beta, st ? st : sm);
   };
   if (dmark ? mark(2) : mark(0)) return -1;
   // no halo in flight (none, or pulled already on this stream): every slice
@@ -3191,6 +3218,28 @@ static int spmv_grouped(int n, pa_mat* const A[], pa_vec* const y[], const pa_in
     if (merged < 0) PA_FAIL("mul!: merged launch table (device allocation or copy) failed");
     if (merged == 0 && !dmark && (mark(1) || mark(2))) return -1;
   }
+  // per-kind launches with no halo in flight (or the direct pull done): the
+  // side rows (a few short waves: FE27 256³'s 129,032 domain-face rows, 6.8
+  // µs as a launch of their own after the 644 µs pattern kernel,
+  // profiles/r04/am/) run on the comm stream beside the pattern slices; they
+  // read x and write only their own rows of y; the compute stream joins
+  // before the long rows and the dot fold
+  bool side_forked = false;
+  if (merged && knobs().side_fork && (!any_x || direct) && !g_capture_stream && sm != sc) {
+    std::vector<SpmvPart> P2;
+    for (int i = 0; i < n; ++i)
+      if (knobs().spmv_format == 1 && A[i]->has_pat && A[i]->s_nslices > 0)
+        P2.push_back(part(i, A[i]->s_nslices, nullptr));
+    if (!P2.empty()) {
+      for (auto& e : c0->ev_side)
+        if (!e) HIPC(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+      HIPC(hipEventRecord(c0->ev_side[0], sm));
+      HIPC(hipStreamWaitEvent(sc, c0->ev_side[0], 0));
+      launch_all(2, P2, sc);
+      HIPC(hipEventRecord(c0->ev_side[1], sc));
+      side_forked = true;
+    }
+  }
   if (merged) {
   // interior slices (no ghost column): overlap with the pulls on the comm stream
   for (int i = 0; i < n; ++i) {
@@ -3220,7 +3269,7 @@ static int spmv_grouped(int n, pa_mat* const A[], pa_vec* const y[], const pa_in
       P4.push_back(part(i, A[i]->nd_bnd, A[i]->d_dbnd_list));
       P5.push_back(part(i, A[i]->nt_bnd, A[i]->d_t_bnd_list));
       P1.push_back(part(i, A[i]->nx_bnd, A[i]->d_xbnd_list));
-      P2.push_back(part(i, A[i]->s_nslices, nullptr));
+      if (!side_forked) P2.push_back(part(i, A[i]->s_nslices, nullptr));
     } else if (A[i]->d_bnd_list) {
       P1.push_back(part(i, A[i]->nslices - A[i]->nslices_int, A[i]->d_bnd_list));
     }
@@ -3231,6 +3280,7 @@ static int spmv_grouped(int n, pa_mat* const A[], pa_vec* const y[], const pa_in
   launch_all(1, P1);
   launch_all(2, P2);
   }  // per-kind launches
+  if (side_forked) HIPC(hipStreamWaitEvent(sm, c0->ev_side[1], 0));
   for (int i = 0; i < n; ++i) {
     const int32_t* ymap = y_idx[i]->own_contig ? nullptr : y_idx[i]->d_oid_to_lid;
     const bool pat = knobs().spmv_format == 1 && A[i]->has_pat;
@@ -3302,6 +3352,94 @@ static int launch_phase(int phase, pa_mat* A, const void* x, void* y, const int3
   }
   for (size_t k = 0; k < E.size(); ++k)
     launch_spmv_part(W[k], E[k].nwork, E[k].list, A, x, y, ymap, has_alpha, bmode, alpha, beta, dotp, st, &E[k]);
+  return 0;
+}
+
+// Barrier issue of a mul! over parts with their own stream pairs and local
+// neighbours (pa_tune "halo_barrier"; the model of one process driving
+// several GPUs, SequentialBackend.jl:52-58's map_parts over every part):
+//   A  per part: pack into send buffer b, record ev_packed, interior slices
+//      (the first call of a chain first waits for the previous exchange's
+//      reads of the send buffers, pre_pack_wait_part);
+//   B  the leading part's s_comm waits for every part's pack and records
+//      ev_barrier — one wait per part instead of one per neighbour and part;
+//   C  per part: s_comm waits ev_barrier, pulls its ghosts from the senders'
+//      buffers b and records ev_recvd; s_main waits ev_recvd, boundary slices.
+// b alternates between d_buf_snd and d_buf_snd2 from one call to the next,
+// so a pack does not wait for the readers of the previous call's buffer: the
+// last reads of b before pack(k+2) are the pulls of call k, and every part
+// issued its pack(k+1) after its boundary(k), i.e. after its pull(k); pack(k+2)
+// follows barrier(k+1) on the part's own chain (s_comm → ev_recvd → s_main).
+// That holds while consecutive calls cover the same exchanger set
+// (pa_xchg::fast_key / fast_seq); any other use of the send buffers
+// (pre_pack_wait_part, the grouped path) restarts the chain with the waits.
+// About 8 HIP calls per part and call instead of ≈24.
+static int spmv_barrier_issue(int n, pa_vec* const x[], pa_xchg* const xg[], int dt, const TransportPlan& T,
+                              bool threads, const std::function<int(int)>& interior,
+                              const std::function<int(int)>& boundary) {
+  uint64_t key = 1469598103934665603ull ^ (uint64_t)n;
+  for (int i = 0; i < n; ++i) key = (key ^ xg[i]->id) * 1099511628211ull;
+  bool chain = true;
+  for (int i = 0; i < n; ++i) chain = chain && xg[i]->fast_key == key && xg[i]->fast_seq == xg[0]->fast_seq;
+  const int parity = chain ? (xg[0]->fast_parity ^ 1) : 0;
+  for (int i = 0; i < n; ++i) xg[i]->fast_key = 0;  // set again once the call is issued
+  TransportPlan TB = T;
+  TB.alt = parity == 1;
+  if (TB.alt) {  // the second send buffers and the pull tables reading them
+    for (int i = 0; i < n; ++i)
+      if (!xg[i]->d_buf_snd2 && xg[i]->n_snd_data) {
+        HIPC(hipSetDevice(xg[i]->ctx->device));
+        HIPC(hipMalloc(&xg[i]->d_buf_snd2, xg[i]->n_snd_data * 16));
+      }
+    for (int i = 0; i < n; ++i) {
+      if (build_pull(i, n, xg, T.L, dt, 0, true)) return -1;
+      CHECK_ARG(xg[i]->pull_alt.ok, "mul!: pull table of the second send buffers (internal error)");
+    }
+  }
+  pa_ctx* c0 = xg[0]->ctx;
+  if (!c0->ev_barrier) {
+    HIPC(hipSetDevice(c0->device));
+    HIPC(hipEventCreateWithFlags(&c0->ev_barrier, hipEventDisableTiming));
+  }
+  const LocalSet& L = T.L;
+  auto stepA = [&](int i) -> int {
+    pa_xchg* X = xg[i];
+    pa_ctx* c = X->ctx;
+    if (!chain && pre_pack_wait_part(i, xg, L)) return -1;
+    HIPC(hipSetDevice(c->device));
+    launch_pack(dt, X->n_snd_data, X->d_lids_snd, x[i]->d, TB.alt ? X->d_buf_snd2 : X->d_buf_snd, c->s_main,
+                c->ev_packed);
+    return interior(i);
+  };
+  auto stepC = [&](int i) -> int {
+    pa_ctx* c = xg[i]->ctx;
+    HIPC(hipSetDevice(c->device));
+    if (i) HIPC(hipStreamWaitEvent(c->s_comm, c0->ev_barrier, 0));
+    if (transport_local(i, xg, x, TB)) return -1;
+    return boundary(i);
+  };
+  if (threads) {
+    if (IssuePool::get().run(n, stepA)) return -1;
+  } else {
+    for (int i = 0; i < n; ++i)
+      if (stepA(i)) return -1;
+  }
+  HIPC(hipSetDevice(c0->device));
+  for (int i = 0; i < n; ++i) HIPC(hipStreamWaitEvent(c0->s_comm, xg[i]->ctx->ev_packed, 0));
+  HIPC(hipEventRecord(c0->ev_barrier, c0->s_comm));
+  if (threads) {
+    if (IssuePool::get().run(n, stepC)) return -1;
+  } else {
+    for (int i = 0; i < n; ++i)
+      if (stepC(i)) return -1;
+  }
+  static std::atomic<uint64_t> seq_next{1};
+  const uint64_t seq = seq_next.fetch_add(1);
+  for (int i = 0; i < n; ++i) {
+    xg[i]->fast_key = key;
+    xg[i]->fast_seq = seq;
+    xg[i]->fast_parity = parity;
+  }
   return 0;
 }
 
@@ -3430,17 +3568,21 @@ static int spmv_impl(int n, pa_mat* const A[], pa_vec* const y[], const pa_index
   // one device the parts' streams share its hardware queues and the serial
   // order keeps the device time lower (1.44 vs 1.70 ms for 8 parts of the
   // 256³ (2,2,2) problem, profiles/r04/k/host_issue_3round.json); 2: always
-  bool threads = knobs().issue_threads && n >= 2 && !g_capture_stream;
+  bool distinct = n >= 2 && !g_capture_stream;  // every part its own stream pair
   bool multi_dev = false;
-  for (int i = 0; threads && i < n; ++i) {
+  for (int i = 0; distinct && i < n; ++i) {
     multi_dev = multi_dev || A[i]->ctx->device != A[0]->ctx->device;
     for (int j = 0; j < i; ++j)
-      if (A[i]->ctx->s_main == A[j]->ctx->s_main || A[i]->ctx->s_comm == A[j]->ctx->s_comm) threads = false;
+      if (A[i]->ctx->s_main == A[j]->ctx->s_main || A[i]->ctx->s_comm == A[j]->ctx->s_comm) distinct = false;
   }
+  bool threads = knobs().issue_threads && distinct;
   if (knobs().issue_threads == 1 && !multi_dev) threads = false;
   TransportPlan T;
   if (any_x && transport_plan(n, xg, dt, 0, PA_REPLACE, x, &T)) return -1;
-  if (threads && !(any_x && T.remote)) {
+  if (any_x && distinct && knobs().halo_barrier && T.pull && !T.remote) {
+    pulled = true;
+    if (spmv_barrier_issue(n, x, xg, dt, T, threads, interior, boundary)) return -1;
+  } else if (threads && !(any_x && T.remote)) {
     if (any_x) {
       const LocalSet L = local_set(n, xg);
       if (IssuePool::get().run(n, [&](int i) -> int { return pre_pack_wait_part(i, xg, L) || pack(i); })) return -1;
@@ -3824,8 +3966,9 @@ struct CGRun {
   std::vector<CGState*> st;
   std::vector<double*> hist;
   std::vector<void**> ptrs;         // local mode: per part, device table of the parts' d_result
+  void** dsts = nullptr;            // local mode: the local parts' d_gather (device table on part 1's device)
   std::vector<hipEvent_t> ev_red;   // local mode: part value ready
-  std::vector<hipEvent_t> ev_gat;   // local mode: part has gathered
+  std::vector<hipEvent_t> ev_gat;   // local mode: [0] the values gathered into every part
   ~CGRun() {
     for (int i = 0; i < n; ++i) {
       if (i < (int)ctxs.size()) (void)hipSetDevice(ctxs[i]->device);
@@ -3835,10 +3978,23 @@ struct CGRun {
       if (i < (int)ev_red.size() && ev_red[i]) (void)hipEventDestroy(ev_red[i]);
       if (i < (int)ev_gat.size() && ev_gat[i]) (void)hipEventDestroy(ev_gat[i]);
     }
+    if (dsts) {
+      (void)hipSetDevice(ctxs[0]->device);
+      dev_free(dsts);
+    }
   }
 };
 
-// every part's d_result (accsz bytes) → d_gather[part-1] of every part
+// every part's d_result (accsz bytes) → d_gather[part-1] of every part.
+// Local mode (all parts in this process): part 1's stream waits for every
+// part's value, one kernel copies the P values into every part's d_gather
+// (peer stores), and every other part waits for that kernel — 3n runtime
+// calls; the previous form (a gather kernel per part behind n-1 waits each,
+// then n-1 more waits each before any d_result is reused) took 2n² + 2n,
+// which at 8 stream-pair parts filled the queues with cross-stream waits
+// (tools/host_issue.py cg_host_us_per_iteration_tiny, profiles/r05/h/).
+// The kernel's reads of the d_result precede ev_gat[0], which every part
+// waits for before it writes its d_result again.
 int cg_gather(CGRun& R, size_t accsz) {
   if (R.remote) {
     pa_ctx* c = R.ctxs[0];
@@ -3846,24 +4002,18 @@ int cg_gather(CGRun& R, size_t accsz) {
     NCCLC(ncclAllGather(c->d_result, c->d_gather, accsz, ncclUint8, (ncclComm_t)c->comm, c->s_main));
     return 0;
   }
-  for (int i = 0; i < R.n; ++i) {
+  pa_ctx* c0 = R.ctxs[0];
+  for (int i = 1; i < R.n; ++i) {
     HIPC(hipSetDevice(R.ctxs[i]->device));
     HIPC(hipEventRecord(R.ev_red[i], R.ctxs[i]->s_main));
   }
-  for (int i = 0; i < R.n; ++i) {
-    pa_ctx* c = R.ctxs[i];
-    HIPC(hipSetDevice(c->device));
-    for (int j = 0; j < R.n; ++j)
-      if (j != i) HIPC(hipStreamWaitEvent(c->s_main, R.ev_red[j], 0));
-    launch_gather_ptrs(R.P, (const void* const*)R.ptrs[i], (int)accsz, c->d_gather, c->s_main);
-    HIPC(hipEventRecord(R.ev_gat[i], c->s_main));
-  }
-  // no part overwrites its d_result before every part has read it
-  for (int i = 0; i < R.n; ++i) {
-    pa_ctx* c = R.ctxs[i];
-    HIPC(hipSetDevice(c->device));
-    for (int j = 0; j < R.n; ++j)
-      if (j != i) HIPC(hipStreamWaitEvent(c->s_main, R.ev_gat[j], 0));
+  HIPC(hipSetDevice(c0->device));
+  for (int i = 1; i < R.n; ++i) HIPC(hipStreamWaitEvent(c0->s_main, R.ev_red[i], 0));
+  launch_gather_scatter(R.P, (const void* const*)R.ptrs[0], (int)accsz, R.n, R.dsts, c0->s_main);
+  HIPC(hipEventRecord(R.ev_gat[0], c0->s_main));
+  for (int i = 1; i < R.n; ++i) {
+    HIPC(hipSetDevice(R.ctxs[i]->device));
+    HIPC(hipStreamWaitEvent(R.ctxs[i]->s_main, R.ev_gat[0], 0));
   }
   return 0;
 }
@@ -3944,6 +4094,12 @@ int pa_cg_solve_all(int n, pa_mat* const A[], pa_vec* const x[], const pa_vec* c
         (void)hipGetLastError();
       }
     }
+  }
+  if (!R.remote) {  // the destinations of the one-kernel all-gather (local parts in position order)
+    std::vector<void*> d(n);
+    for (int i = 0; i < n; ++i) d[i] = R.ctxs[i]->d_gather;
+    HIPC(hipSetDevice(R.ctxs[0]->device));
+    if (dev_upload(&R.dsts, d)) return -1;
   }
   // setup (cg_iterator!): u = 0; r = b; c = A*x; r .-= c; residual = norm(r);
   // tolerance = max(reltol*norm(b), abstol)

@@ -303,6 +303,11 @@ struct pa_ctx {
   // events for the exchange pipeline
   hipEvent_t ev_packed = nullptr;
   hipEvent_t ev_recvd = nullptr;
+  // the pack barrier of stream-pair mul! calls this part leads (spmv_impl's
+  // barrier issue): recorded on its s_comm once every part of the call packed
+  hipEvent_t ev_barrier = nullptr;
+  // the side-row fork of per-kind launches (spmv_grouped): fork, join
+  hipEvent_t ev_side[2] = {nullptr, nullptr};
   // device arrays of the x pointers of grouped mul! calls led by this part
   // (the direct pull's bases), most recent first
   std::vector<std::pair<std::vector<void*>, void**>> bases_cache;
@@ -341,6 +346,8 @@ struct Knobs {
   int spmv_xcd_chunk;    // XCD-chunked block order of the SpMV launches (pa_spmv.hip xcd_block), 0 off
   int spmv_tri16;        // delta16 slices re-sliced into the triple SELL (pa_mat::d_t_*): 0 never, 1 R <= 2, 2 always
   int spmv_diag_rows;    // pattern slices compute their diagonal-only rows (pa_mat::d_dmask)
+  int halo_barrier;      // stream-pair mul!: one pack barrier + double-buffered sends (spmv_impl)
+  int side_fork;         // per-kind launches: the side rows on the comm stream beside the pattern slices
 };
 // the knobs of the call running on this thread (outside a call: a snapshot
 // of the process defaults)
@@ -423,6 +430,14 @@ struct pa_xchg {
   int32_t* d_lids_snd = nullptr;
   void* d_buf_rcv = nullptr;                   // 16 B per slot
   void* d_buf_snd = nullptr;
+  // the barrier issue of stream-pair mul! (spmv_impl): a second forward send
+  // buffer, used every other call, and the pull table against the senders'
+  // second buffers; the last barrier call these exchangers took part in
+  // (key of its exchanger set, its sequence number, the buffer it packed)
+  void* d_buf_snd2 = nullptr;
+  pa_pull pull_alt;
+  uint64_t fast_key = 0, fast_seq = 0;
+  int fast_parity = 0;
   pa_combine_plan plan_fwd;   // unpack targets = lids_rcv
   pa_combine_plan plan_rev;   // unpack targets = lids_snd (reverse/assemble)
 };

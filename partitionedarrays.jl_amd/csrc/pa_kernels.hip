@@ -11,7 +11,20 @@
 // which makes the SpMV bit-identical to SequentialBackend/MPIBackend.
 #include "pa_internal.h"
 
+#include <hip/hip_ext.h>
+
 namespace pa {
+
+// One kernel launch whose completion is recorded in ev (null: none): the
+// launch and the record as one runtime call (hipExtLaunchKernel binds ev to
+// the kernel's dispatch), what the barrier issue of a stream-pair mul! pays
+// per part for its pack and its pull (pa_api.cpp spmv_barrier_issue).
+template <typename K, typename... Args>
+static void launch_ev(K kernel, dim3 grid, hipStream_t st, hipEvent_t ev, Args... args) {
+  if (ev) hipExtLaunchKernelGGL(kernel, grid, dim3(256), 0, st, nullptr, ev, 0, args...);
+  else hipLaunchKernelGGL(kernel, grid, dim3(256), 0, st, args...);
+}
+
 
 // SELL SpMV kernels: pa_spmv.hip
 
@@ -69,9 +82,12 @@ static inline int grid_for(int64_t n, int block = 256, int64_t cap = 4096) {
 }
 
 template <typename T>
-static void pack_t(int64_t n, const int32_t* lids, const void* v, void* buf, hipStream_t st) {
-  if (n <= 0) return;
-  hipLaunchKernelGGL(k_pack<T>, dim3(grid_for(n)), dim3(256), 0, st, n, lids, (const T*)v, (T*)buf);
+static void pack_t(int64_t n, const int32_t* lids, const void* v, void* buf, hipStream_t st, hipEvent_t ev) {
+  if (n <= 0) {
+    if (ev) (void)hipEventRecord(ev, st);
+    return;
+  }
+  launch_ev(k_pack<T>, dim3(grid_for(n)), st, ev, n, lids, (const T*)v, (T*)buf);
 }
 
 template <typename T>
@@ -131,44 +147,45 @@ __global__ void k_pull_ordered(int64_t ntargets, const int32_t* __restrict__ tar
 
 template <typename T>
 static void pull_t(int64_t n, const int32_t* lids, const pa_combine_plan& plan, int op, const int32_t* bid,
-                   const int64_t* elem, const void* const* bases, void* v, hipStream_t st) {
-  if (n <= 0) return;
+                   const int64_t* elem, const void* const* bases, void* v, hipStream_t st, hipEvent_t ev) {
+  if (n <= 0) {
+    if (ev) (void)hipEventRecord(ev, st);
+    return;
+  }
   const T* const* b = (const T* const*)bases;
   if (plan.unique) {
     if (op == PA_ADD)
-      hipLaunchKernelGGL((k_pull_unique<T, PA_ADD>), dim3(grid_for(n)), dim3(256), 0, st, n, lids, bid, elem, b,
-                         (T*)v);
+      launch_ev(k_pull_unique<T, PA_ADD>, dim3(grid_for(n)), st, ev, n, lids, bid, elem, b, (T*)v);
     else
-      hipLaunchKernelGGL((k_pull_unique<T, PA_REPLACE>), dim3(grid_for(n)), dim3(256), 0, st, n, lids, bid, elem,
-                         b, (T*)v);
+      launch_ev(k_pull_unique<T, PA_REPLACE>, dim3(grid_for(n)), st, ev, n, lids, bid, elem, b, (T*)v);
   } else {
     const int64_t nt = plan.ntargets;
     if (op == PA_ADD)
-      hipLaunchKernelGGL((k_pull_ordered<T, PA_ADD>), dim3(grid_for(nt)), dim3(256), 0, st, nt, plan.d_target,
-                         plan.d_ptr, plan.d_pos, bid, elem, b, (T*)v);
+      launch_ev(k_pull_ordered<T, PA_ADD>, dim3(grid_for(nt)), st, ev, nt, (const int32_t*)plan.d_target,
+                (const int32_t*)plan.d_ptr, (const int32_t*)plan.d_pos, bid, elem, b, (T*)v);
     else
-      hipLaunchKernelGGL((k_pull_ordered<T, PA_REPLACE>), dim3(grid_for(nt)), dim3(256), 0, st, nt, plan.d_target,
-                         plan.d_ptr, plan.d_pos, bid, elem, b, (T*)v);
+      launch_ev(k_pull_ordered<T, PA_REPLACE>, dim3(grid_for(nt)), st, ev, nt, (const int32_t*)plan.d_target,
+                (const int32_t*)plan.d_ptr, (const int32_t*)plan.d_pos, bid, elem, b, (T*)v);
   }
 }
 
 void launch_pull(int dtype, int64_t n, const int32_t* lids, const pa_combine_plan& plan, int op, const int32_t* bid,
-                 const int64_t* elem, const void* const* bases, void* v, hipStream_t st) {
+                 const int64_t* elem, const void* const* bases, void* v, hipStream_t st, hipEvent_t ev) {
   switch (dtype) {
-    case PA_F32: pull_t<float>(n, lids, plan, op, bid, elem, bases, v, st); break;
-    case PA_F64: pull_t<double>(n, lids, plan, op, bid, elem, bases, v, st); break;
-    case PA_C64: pull_t<c64>(n, lids, plan, op, bid, elem, bases, v, st); break;
-    case PA_C128: pull_t<c128>(n, lids, plan, op, bid, elem, bases, v, st); break;
+    case PA_F32: pull_t<float>(n, lids, plan, op, bid, elem, bases, v, st, ev); break;
+    case PA_F64: pull_t<double>(n, lids, plan, op, bid, elem, bases, v, st, ev); break;
+    case PA_C64: pull_t<c64>(n, lids, plan, op, bid, elem, bases, v, st, ev); break;
+    case PA_C128: pull_t<c128>(n, lids, plan, op, bid, elem, bases, v, st, ev); break;
   }
 }
 
 void launch_pack(int dtype, int64_t n, const int32_t* lids, const void* v, void* buf,
-                 hipStream_t st) {
+                 hipStream_t st, hipEvent_t ev) {
   switch (dtype) {
-    case PA_F32: pack_t<float>(n, lids, v, buf, st); break;
-    case PA_F64: pack_t<double>(n, lids, v, buf, st); break;
-    case PA_C64: pack_t<c64>(n, lids, v, buf, st); break;
-    case PA_C128: pack_t<c128>(n, lids, v, buf, st); break;
+    case PA_F32: pack_t<float>(n, lids, v, buf, st, ev); break;
+    case PA_F64: pack_t<double>(n, lids, v, buf, st, ev); break;
+    case PA_C64: pack_t<c64>(n, lids, v, buf, st, ev); break;
+    case PA_C128: pack_t<c128>(n, lids, v, buf, st, ev); break;
   }
 }
 

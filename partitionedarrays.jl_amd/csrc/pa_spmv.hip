@@ -893,7 +893,12 @@ __device__ __forceinline__ void spmv_wave(const SpmvArgs<T>& a, const int64_t w)
   // rows — before the pattern loop, the lanes holding one read their entry-0
   // pack and store y = β-init + v·x[row], the reference's one term
   // (SparseUtils.jl:176-185 over one entry); the loop's sum for the row is
-  // never stored (ok false).  Nothing stays live across the loop.
+  // never stored (ok false).  Nothing stays live across the loop.  Off by
+  // default: the dmask load and the v·x round trip ahead of every wave's
+  // stream cost more than the side rows they remove (same-box A/B,
+  // profiles/r05/i/: FE27 256³ 0.6504 -> 0.6721 ms kernel, C2 FD7 128³
+  // 0.0281 -> 0.0316); testing the word after the loop instead keeps v0 and
+  // the word live across it (merged F64 kernel 124 -> 130 VGPRs, 3 waves).
   unsigned dbits = 0;
   if constexpr (PK == 1) {
     if (a.dmask) {
@@ -1936,6 +1941,21 @@ __global__ void k_gather_ptrs(int P, const void* const* __restrict__ srcs, int a
   if (accsz == 16) d[1] = s[1];
 }
 
+// dsts[d][p] = *srcs[p] for every destination d (accsz bytes each): the
+// part values gathered once and written to every local part's d_gather (peer
+// stores across the devices of one process), the device CG's one-kernel
+// all-gather (pa_api.cpp cg_gather)
+__global__ void k_gather_scatter(int P, const void* const* __restrict__ srcs, int accsz, int nd,
+                                 void* const* __restrict__ dsts) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (int64_t)P * nd) return;
+  const int p = (int)(t % P), d = (int)(t / P);
+  const double* s = (const double*)srcs[p];
+  double* o = (double*)((char*)dsts[d] + (int64_t)p * accsz);
+  o[0] = s[0];
+  if (accsz == 16) o[1] = s[1];
+}
+
 template <typename T>
 static void cg_xu_t(int64_t n, void* x, void* u, const void* r, const CGState* st, hipStream_t s) {
   constexpr int V = 16 / sizeof(T);
@@ -2036,6 +2056,12 @@ void launch_fold_cg_step(int dtype, int nb, const void* in, void* scratch, void*
 
 void launch_gather_ptrs(int P, const void* const* srcs, int accsz, void* out, hipStream_t s) {
   hipLaunchKernelGGL(k_gather_ptrs, dim3((P + 63) / 64), dim3(64), 0, s, P, srcs, accsz, (char*)out);
+}
+
+void launch_gather_scatter(int P, const void* const* srcs, int accsz, int nd, void* const* dsts, hipStream_t s) {
+  const int64_t n = (int64_t)P * nd;
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_gather_scatter, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, P, srcs, accsz, nd, dsts);
 }
 
 // ---------------------------------------------------------------------------

@@ -401,6 +401,59 @@ def test_threaded_issue_matches_sequential(pamd, O):
     assert out[0][2] == out[2][2]
 
 
+@pytest.mark.parametrize("threads", [0, 2])
+def test_barrier_issue_chain_equals_oracle(pamd, O, threads):
+    """Stream-pair mul! calls issued back to back without a host sync (the
+    one-process-drives-several-GPUs path): with the pack
+    barrier and double-buffered send buffers (halo_barrier 1) every call sees
+    the x that was copied in just before it, as with per-neighbour waits
+    (halo_barrier 0) and the oracle; an exchange! inside the sequence restarts
+    the buffer chain; the device CG is bit-identical across both."""
+    shape, N = (2, 2, 2), (14, 11, 9)
+    rng = np.random.default_rng(SEED + 13)
+    K = 9
+    vals = [rng.uniform(-1, 1, 3000) for _ in range(K)]
+    OA = O.stencil_problem(O.get_part_ids(shape), N, 27)
+    want = []
+    for v in vals:
+        ox = O.PVector(O.map_parts(lambda s, v=v: v[:s.num_lids].copy(), OA.cols.partition), OA.cols)
+        oy = O.pvector_undef(OA.rows, np.float64)
+        O.mul_(oy, OA, ox)
+        want.append(oy)
+    hist = {}
+    for barrier in (1, 0):
+        p0 = pamd._lib.tune("issue_threads", threads)
+        p1 = pamd._lib.tune("halo_barrier", barrier)
+        try:
+            be = pamd.HIPBackend(devices=[0], share_streams=False)
+            parts = be.get_part_ids(shape)
+            A = pamd.drivers.stencil_operator(parts, N, 27)
+            xs = [pamd.PVector.from_host(pamd.map_parts(lambda s, v=v: v[:s.num_lids].copy(), A.cols.partition),
+                                         A.cols) for v in vals]
+            x = pamd.PVector.undef(A.cols).fill_(0)
+            ys = [pamd.PVector.undef(A.rows).fill_(0) for _ in range(K)]
+            for k in range(K):  # no host sync in between
+                pamd.copyto_(x, xs[k])
+                if k == 4:
+                    pamd.exchange_(x)
+                pamd.mul_(ys[k], A, x)
+            for k in range(K):
+                got = ys[k].to_host()
+                for p in parts.part_ids:
+                    own = A.rows.partition.local(p).oid_to_lid - 1
+                    assert np.array_equal(got.local(p)[own], want[k].values[p][own]), (barrier, k, p)
+            xc = pamd.PVector.undef(A.cols).fill_(0)
+            h = []
+            pamd.cg_(xc, A, xs[0], reltol=0.0, maxiter=10, history=h, device=True)
+            hist[barrier] = (h, [v.copy() for v in xc.to_host().parts])
+        finally:
+            pamd._lib.tune("halo_barrier", p1)
+            pamd._lib.tune("issue_threads", p0)
+    assert hist[0][0] == hist[1][0]
+    for a, b in zip(hist[0][1], hist[1][1]):
+        assert np.array_equal(a, b)
+
+
 def test_threaded_issue_reports_launch_failures(pamd, O):
     """A kernel launch that fails inside a threaded-issue job (pa_tune
     fault_inject: each job also issues a launch the runtime rejects) makes
@@ -451,7 +504,14 @@ def test_diagonal_only_rows_equal_oracle(be, pamd, O, kind, N, dtype, diag):
         OA = O.stencil_problem(O.get_part_ids(shape), N, kind, dtype)
         info = [A.values.local(p).info() for p in parts.part_ids]
         if diag:
-            assert all(i["diag_rows"] > 0 and i["side_rows"] == 0 for i in info), info
+            # the interface rows (a ghost column off the pattern) stay side
+            # rows; every Dirichlet row left the side SELL
+            pamd._lib.tune("spmv_diag_rows", 0)
+            A0 = pamd.drivers.stencil_operator(parts, N, kind, dtype)
+            info0 = [A0.values.local(p).info() for p in parts.part_ids]
+            pamd._lib.tune("spmv_diag_rows", diag)
+            assert all(i["diag_rows"] > 0 and i["side_rows"] + i["diag_rows"] == i0["side_rows"]
+                       for i, i0 in zip(info, info0)), (info, info0)
         else:
             assert all(i["diag_rows"] == 0 and i["side_rows"] > 0 for i in info), info
         rng = np.random.default_rng(SEED + 41)
@@ -482,3 +542,47 @@ def test_diagonal_only_rows_equal_oracle(be, pamd, O, kind, N, dtype, diag):
             assert abs(d - ref) <= 1e-12 * max(1.0, abs(ref)), (d, ref)
     finally:
         pamd._lib.tune("spmv_diag_rows", prev)
+
+
+@pytest.mark.parametrize("dtype", [np.float64, np.float32, np.complex128])
+@pytest.mark.parametrize("fork", [1, 0])
+def test_side_fork_per_kind_launches_equal_oracle(be, pamd, O, dtype, fork):
+    """Per-kind launches of one part (spmv_merge_max below its slice count:
+    the headline's path) with the side rows on the comm stream beside the
+    pattern slices (spmv_side_fork 1) or after them (0): mul! with α/β, back
+    to back on changing x without a host sync, and the fused dot give the
+    oracle's bits; the side rows exist (the domain-face Dirichlet rows)."""
+    p0 = pamd._lib.tune("spmv_side_fork", fork)
+    p1 = pamd._lib.tune("spmv_merge_max", 4)
+    try:
+        shape, N = (1, 1, 1), (40, 21, 12)
+        parts = be.get_part_ids(shape)
+        A = pamd.drivers.stencil_operator(parts, N, 27, dtype)
+        OA = O.stencil_problem(O.get_part_ids(shape), N, 27, dtype)
+        assert A.values.local(1).info()["side_rows"] > 0
+        rng = np.random.default_rng(SEED + 43)
+        n = A.cols.partition.local(1).num_lids
+        xs = [_rand(rng, n, dtype) for _ in range(3)]
+        y0 = _rand(rng, A.rows.partition.local(1).num_lids, dtype)
+        sc = np.float32 if np.dtype(dtype) in (np.float32, np.complex64) else np.float64
+        cases = [(1.0, 0.0), (0.7, 0.0), (-1.3, 0.5)]
+        xd = [pamd.PVector.from_host(pamd.map_parts(lambda s, v=v: v, A.cols.partition), A.cols) for v in xs]
+        ys = [pamd.PVector.from_host(pamd.map_parts(lambda s: y0, A.rows.partition), A.rows) for _ in cases]
+        for k, (alpha, beta) in enumerate(cases):  # no host sync in between
+            pamd.mul_(ys[k], A, xd[k % 3], alpha, beta)
+        for k, (alpha, beta) in enumerate(cases):
+            ox = O.PVector(O.map_parts(lambda s: _to_oracle(O, xs[k % 3]), OA.cols.partition), OA.cols)
+            oy = O.PVector(O.map_parts(lambda s: _to_oracle(O, y0), OA.rows.partition), OA.rows)
+            O.mul_(oy, OA, ox, sc(alpha), sc(beta))
+            own = A.rows.partition.local(1).oid_to_lid - 1
+            assert _eq(O, ys[k].to_host().local(1)[own], _sel(O, oy.values[1], own)), (alpha, beta)
+        if np.dtype(dtype) == np.float64:
+            yc = pamd.PVector.undef(A.cols)
+            d = pamd.mul_dot_(yc, A, xd[0])
+            oyc = O.pvector_undef(OA.cols, np.float64)
+            O.mul_(oyc, OA, O.PVector(O.map_parts(lambda s: xs[0].copy(), OA.cols.partition), OA.cols))
+            ref = float(np.dot(xs[0], oyc.values[1]))
+            assert abs(d - ref) <= 1e-12 * max(1.0, abs(ref)), (d, ref)
+    finally:
+        pamd._lib.tune("spmv_merge_max", p1)
+        pamd._lib.tune("spmv_side_fork", p0)

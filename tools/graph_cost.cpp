@@ -92,8 +92,9 @@ static int shape(int kernels, int waits, int records, int reps) {
 
 int main() {
   setvbuf(stdout, nullptr, _IONBF, 0);
-  const int shapes[][3] = {{1, 0, 0}, {2, 0, 0}, {4, 0, 0}, {8, 0, 0}, {16, 0, 0}, {32, 0, 0},
-                           {2, 1, 1}, {2, 7, 1}, {3, 7, 1}, {1, 7, 1}, {0, 7, 1}};
+  // more than one external event-wait node per capture ({2, 7, 1}) crashed
+  // the HIP runtime of the box inside the capture (segfault, profiles/r05/g/)
+  const int shapes[][3] = {{1, 0, 0}, {2, 0, 0}, {4, 0, 0}, {8, 0, 0}, {16, 0, 0}, {32, 0, 0}, {2, 1, 1}};
   for (auto& sh : shapes)
     if (shape(sh[0], sh[1], sh[2], 200)) return 1;
   return 0;

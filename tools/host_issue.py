@@ -96,6 +96,11 @@ def main():
     res.append(measure(pamd.HIPBackend(devices=[0], share_streams=False), args.n, args.k,
                        "share_streams=False, issue_threads=2 (per-part streams, events and launches, issued from "
                        "host threads)", cg_iters=200))
+    pb = pamd._lib.tune("halo_barrier", 0)
+    res.append(measure(pamd.HIPBackend(devices=[0], share_streams=False), args.n, args.k,
+                       "share_streams=False, issue_threads=2, halo_barrier=0 (per-neighbour event waits before "
+                       "every pack and pull, the r04 issue)"))
+    pamd._lib.tune("halo_barrier", pb)
     pamd._lib.tune("issue_threads", prev)
     prev = pamd._lib.tune("issue_threads", 0)
     res.append(measure(pamd.HIPBackend(devices=[0], share_streams=False), args.n, args.k,
