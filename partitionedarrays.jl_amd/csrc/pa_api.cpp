@@ -1351,10 +1351,12 @@ const Knob kKnobs[] = {
      "per-neighbour event waits before every pack and every pull"},
     {"spmv_side_fork", &Knobs::side_fork, nullptr, 0, 1, 0,
      "spmv_side_fork: per-kind launches without a halo in flight (big single parts): 1 = the side rows run on "
-     "the comm stream beside the pattern slices (default), 0 = after them on the compute stream"},
+     "the comm stream beside the pattern slices, 0 = after them on the compute stream (default, "
+     "profiles/r05/k/)"},
     {"spmv_xcd_chunk", &Knobs::spmv_xcd_chunk, nullptr, 0, 64, 0,
      "spmv_xcd_chunk: C > 0 = the SpMV launches' workgroups in runs of C consecutive blocks per XCD (x lines "
-     "of neighbouring slices shared in one L2), 0 = the hardware's round robin (default)"},
+     "of neighbouring slices shared in one L2), 0 = the hardware's round robin (default: C = 4 lost on C2, "
+     "0.0283 -> 0.0287-0.0289 ms, profiles/r05/k/)"},
     {"fault_inject", &Knobs::fault_inject, nullptr, 0, 1, 0,
      "fault_inject: 1 = every job of a threaded issue (IssuePool) also issues an invalid kernel launch (tests "
      "of the error path; test_exception.jl's role), 0 = off (default)"},
@@ -3221,9 +3223,12 @@ static int spmv_grouped(int n, pa_mat* const A[], pa_vec* const y[], const pa_in
   // per-kind launches with no halo in flight (or the direct pull done): the
   // side rows (a few short waves: FE27 256³'s 129,032 domain-face rows, 6.8
   // µs as a launch of their own after the 644 µs pattern kernel,
-  // profiles/r04/am/) run on the comm stream beside the pattern slices; they
+  // profiles/r04/am/) can run on the comm stream beside the pattern slices; they
   // read x and write only their own rows of y; the compute stream joins
-  // before the long rows and the dot fold
+  // before the long rows and the dot fold.  Off by default: the concurrent
+  // side waves slow the pattern kernel more than their own launch costs
+  // (same-box A/B, profiles/r05/k/: 0.6459/0.6467 ms serial vs
+  // 0.6546/0.6544 forked)
   bool side_forked = false;
   if (merged && knobs().side_fork && (!any_x || direct) && !g_capture_stream && sm != sc) {
     std::vector<SpmvPart> P2;
@@ -3409,6 +3414,9 @@ static int spmv_barrier_issue(int n, pa_vec* const x[], pa_xchg* const xg[], int
     HIPC(hipSetDevice(c->device));
     launch_pack(dt, X->n_snd_data, X->d_lids_snd, x[i]->d, TB.alt ? X->d_buf_snd2 : X->d_buf_snd, c->s_main,
                 c->ev_packed);
+    // the barrier stream's wait for this pack, from this part's thread (the
+    // record of ev_barrier follows once every part's job is done)
+    HIPC(hipStreamWaitEvent(c0->s_comm, c->ev_packed, 0));
     return interior(i);
   };
   auto stepC = [&](int i) -> int {
@@ -3425,7 +3433,6 @@ static int spmv_barrier_issue(int n, pa_vec* const x[], pa_xchg* const xg[], int
       if (stepA(i)) return -1;
   }
   HIPC(hipSetDevice(c0->device));
-  for (int i = 0; i < n; ++i) HIPC(hipStreamWaitEvent(c0->s_comm, xg[i]->ctx->ev_packed, 0));
   HIPC(hipEventRecord(c0->ev_barrier, c0->s_comm));
   if (threads) {
     if (IssuePool::get().run(n, stepC)) return -1;

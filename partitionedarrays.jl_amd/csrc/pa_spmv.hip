@@ -16,6 +16,8 @@
 //   acc = β-init; acc = acc + v_k * (x_{c_k} * α)   (-ffp-contract=off)
 #include "pa_internal.h"
 
+#include <cstddef>
+
 #include <algorithm>
 #include <cstring>
 #include <type_traits>
@@ -1378,8 +1380,13 @@ static int pk_of(int which) { return which == 0 ? 1 : which == 4 ? 3 : which == 
 template <typename T, int R>
 static int merged_t(int n, const int* which, const SpmvPart* parts, bool has_alpha, int bmode, const void* alpha,
                     const void* beta, pa_ctx* owner, std::vector<void*>* pinned, hipStream_t st) {
+  // the table's used bytes (header + n entries) are its cache key: only
+  // those are zeroed, compared and uploaded (a 48-entry table is ≈15 KB, a
+  // call's tables hold 1-4 entries: per-call host work of the stream-pair
+  // path)
   SpmvTable<T> h;
-  std::memset(&h, 0, sizeof(h));  // the table's bytes are its cache key
+  constexpr size_t kHdr = offsetof(SpmvTable<T>, a);
+  std::memset(&h, 0, kHdr);
   bool sh = (knobs().spmv_flags & SPMV_SHORT) != 0;
   for (int i = 0; i < n; ++i) {
     const SpmvPart& q = parts[i];
@@ -1394,34 +1401,35 @@ static int merged_t(int n, const int* which, const SpmvPart* parts, bool has_alp
     ++h.n;
   }
   if (h.n == 0) return 0;
+  const size_t used = kHdr + (size_t)h.n * sizeof(SpmvArgs<T>);  // the device reads entries < n only
   // cached device copy of this exact table (most recent first); a graph
   // capture (pinned) gets its own copy, owned by the graph
   auto& C = owner->merged_cache;
   const char* hb = reinterpret_cast<const char*>(&h);
   void* d = nullptr;
   if (pinned) {  // during a capture: device memory now, its contents after the capture ends
-    if (hipMalloc(&d, sizeof(h)) != hipSuccess) {
+    if (hipMalloc(&d, used) != hipSuccess) {
       (void)hipGetLastError();
       return 1;  // the caller launches per kind
     }
     pinned->push_back(d);
-    g_capture_uploads.push_back({d, std::vector<char>(hb, hb + sizeof(h))});
+    g_capture_uploads.push_back({d, std::vector<char>(hb, hb + used)});
   }
   for (size_t k = 0; !d && k < C.size(); ++k)
-    if (C[k].first.size() == sizeof(h) && std::memcmp(C[k].first.data(), hb, sizeof(h)) == 0) {
+    if (C[k].first.size() == used && std::memcmp(C[k].first.data(), hb, used) == 0) {
       if (k) std::swap(C[k], C[0]);
       d = C[0].second;
       break;
     }
   if (!d) {
-    if (hipMalloc(&d, sizeof(h)) != hipSuccess) return -1;
-    if (hipMemcpy(d, &h, sizeof(h), hipMemcpyHostToDevice) != hipSuccess) { (void)hipFree(d); return -1; }
+    if (hipMalloc(&d, used) != hipSuccess) return -1;
+    if (hipMemcpy(d, &h, used, hipMemcpyHostToDevice) != hipSuccess) { (void)hipFree(d); return -1; }
     if (C.size() >= 16) {
       (void)hipStreamSynchronize(st);  // the evicted table may still be read
       (void)hipFree(C.back().second);
       C.pop_back();
     }
-    C.insert(C.begin(), {std::vector<char>(hb, hb + sizeof(h)), d});
+    C.insert(C.begin(), {std::vector<char>(hb, hb + used), d});
   }
   const SpmvTable<T>* dt = (const SpmvTable<T>*)d;
   const int64_t waves = h.start[h.n];
