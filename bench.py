@@ -216,6 +216,104 @@ def child_pmc(args):
     pamd._lib.hbm_probe(0, PROBE_BYTES, 1)
 
 
+def child_oneproc(args):
+    """The one-process-drives-every-GPU leg (SequentialBackend's role, the
+    model of julia/HIPBackend.jl): the same weak-scaling
+    problem as the N-rank line, its N parts held by ONE process, part p on
+    device p-1 with its own stream pair, issued per part from host threads
+    behind one pack barrier per call.  Run as a child of rank 0 after the
+    rank line is measured (a failure here cannot touch that line).  Prints
+    one JSON object: device time per mul!, host issue per mul! (C-ABI, the
+    calls enqueued back to back), and a bit-for-bit check of y against the
+    per-neighbour-wait issue (halo_barrier 0)."""
+    import pamd
+    devs = ([int(d) for d in args.oneproc_devices.split(",")] if args.oneproc_devices
+            else list(range(args.gpus)))
+    ngpu = len(devs)
+    shape = PART_SHAPES[ngpu]
+    N = tuple(args.n * s for s in shape)
+    dtype = DTYPES[args.dtype]
+    S = np.dtype(dtype).itemsize
+    be = pamd.HIPBackend(devices=devs, share_streams=False)
+    parts = be.get_part_ids(shape)
+    t0 = time.perf_counter()
+    A = pamd.drivers.stencil_operator(parts, N, args.kind, dtype)
+    x = pamd.PVector.from_host(pamd.map_parts(
+        lambda s: np.random.default_rng(20250114 + s.part).uniform(-1, 1, s.num_lids).astype(dtype),
+        A.cols.partition), A.cols)
+    y = pamd.PVector.undef(A.rows, dtype)
+    ctxs = [be.context(p) for p in parts.part_ids]
+
+    def sync():
+        for c in ctxs:
+            c.sync()
+    sync()
+    setup = time.perf_counter() - t0
+    B = 0
+    for p in parts.part_ids:
+        s_ = A.cols.partition.local(p)
+        B += format_bytes(A.values.local(p).info(), s_.num_hids, len(A.cols.exchanger.lids_snd.local(p).data),
+                          len(A.cols.exchanger.lids_rcv.local(p).data), S)
+    for _ in range(args.warmup):
+        pamd.mul_(y, A, x)
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        pamd.mul_(y, A, x)
+    sync()
+    wall = (time.perf_counter() - t0) / args.steps
+    cargs = pamd.pvector._spmv_args(y, A, x, 1.0, 0.0)
+    host = []
+    for _ in range(5):
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            pamd._lib.call("pa_spmv_all", *cargs)
+        host.append((time.perf_counter() - t0) / args.steps)
+        sync()
+    host.sort()
+    got = [v.copy() for v in y.to_host().parts]
+    prev = pamd._lib.tune("halo_barrier", 0)
+    try:
+        y0 = pamd.PVector.undef(A.rows, dtype)
+        pamd.mul_(y0, A, x)
+        ref = y0.to_host().parts
+    finally:
+        pamd._lib.tune("halo_barrier", prev)
+    own = [A.rows.partition.local(p).oid_to_lid - 1 for p in parts.part_ids]
+    same = all(np.array_equal(a[o], b[o]) for a, b, o in zip(got, ref, own))
+    print(json.dumps({
+        "process_model": f"{ngpu} parts in one process, part p on device {devs} [p-1], a stream pair each "
+                         "(HIPBackend(share_streams=False): SequentialBackend's role, julia/HIPBackend.jl)",
+        "devices": devs, "parts": list(shape), "global_nodes": list(N),
+        "ms_per_step": round(1e3 * wall, 4), "value": round(B / wall / 1e9, 2), "unit": "GB/s",
+        "bytes_per_step_all_parts": int(B), "frac_of_hbm_peak": round(B / wall / 1e9 / (HBM_PEAK_GBS * ngpu), 4),
+        "host_issue_us_per_mul": round(1e6 * host[len(host) // 2], 1),
+        "host_issue_us_min_max": [round(1e6 * host[0], 1), round(1e6 * host[-1], 1)],
+        "y_equals_neighbour_wait_issue": bool(same), "setup_s": round(setup, 2)}), flush=True)
+    return 0
+
+
+def one_process_leg(args):
+    """rank 0 of an N-rank run: child_oneproc as a child process (bounded)."""
+    cmd = [sys.executable, os.path.abspath(__file__), "--child-oneproc", "--gpus", str(args.gpus), "--n",
+           str(args.n), "--kind", str(args.kind), "--dtype", args.dtype, "--steps", str(args.steps), "--warmup",
+           str(args.warmup), "--tune", args.tune]
+    if args.oneproc_devices:
+        cmd += ["--oneproc-devices", args.oneproc_devices]
+    env = dict(os.environ)
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "GROUP_RANK", "ROLE_RANK",
+              "TORCHELASTIC_RUN_ID", "MASTER_PORT"):
+        env.pop(k, None)
+    try:
+        r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=420)
+    except subprocess.TimeoutExpired:
+        return {"note": "one-process leg timed out (420 s)"}
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    if r.returncode != 0 or not lines:
+        return {"note": f"one-process leg failed (rc {r.returncode})", "stderr_tail": r.stderr[-600:]}
+    return json.loads(lines[-1])
+
+
 def halo_1gpu(args, pamd, dtype, S, reps_phase=20, copies=3):
     """BASELINE config 3 on the one GPU: the SAME global operator as the
     headline (args.n^3 nodes, args.kind points) split into Cartesian parts
@@ -462,6 +560,11 @@ def main():
                     help="skip the halo_1gpu object (config 3 on (2,2,2) parts of the one GPU)")
     ap.add_argument("--child-pmc", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--child-halo", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--child-oneproc", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--oneproc-devices", default="",
+                    help="devices of the one-process leg's parts (default 0..N-1; e.g. 0,0 rehearses it on one GPU)")
+    ap.add_argument("--no-oneproc", action="store_true",
+                    help="skip the one-process leg of N > 1 runs (all N parts driven by one process)")
     ap.add_argument("--cg", type=int, default=0, help="time K CG iterations instead (own JSON line)")
     ap.add_argument("--tune", default="", help="process-default knobs before anything is built (A/B runs): "
                                                  "key=v[,key=v]")
@@ -469,12 +572,12 @@ def main():
                     help="one part per process (HIPDistributedBackend, RCCL) even for one process: "
                          "rehearses the torchrun path of --gpus N > 1 on a single GPU")
     args = ap.parse_args()
-    if args.child_pmc:
+    if args.child_pmc or args.child_oneproc:
         import pamd
         for kv in filter(None, args.tune.split(",")):
             k, v = kv.split("=")
             pamd._lib.tune(k, int(v))
-        return child_pmc(args)
+        return child_oneproc(args) if args.child_oneproc else child_pmc(args)
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         # `python bench.py --gpus N` (no torchrun around it): start the N
         # one-part-per-GPU ranks ourselves, as the driver's torchrun command
@@ -769,6 +872,14 @@ def main():
     }
     if halo_leg is not None:
         line["halo_1gpu"] = halo_leg
+    # N ranks: the same problem with all N parts in ONE process (the Julia
+    # binding's model), measured by a child of rank 0 while the other ranks
+    # wait (their GPUs idle)
+    if use_dist and not args.no_oneproc and (ngpu > 1 or args.oneproc_devices):
+        barrier()
+        if rank == 0:
+            line["one_process"] = one_process_leg(args)
+        barrier()
     if rank == 0 and not args.no_cpu_baseline:
         if ngpu == 1:
             line["cpu_baseline"] = cpu_baseline(args.kind, args.n, args.cpu_seconds)

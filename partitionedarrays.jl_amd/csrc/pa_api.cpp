@@ -90,7 +90,7 @@ const Knobs kDefaults = {
     /*spmv_flags*/ 93, /*long_exact*/ 1, /*halo_pull*/ 1, /*spmv_delta16*/ 1, /*spmv_merge*/ 1,
     /*spmv_merge_max*/ 65536, /*cg_fuse*/ 2, /*halo_direct*/ 1, /*halo_transport*/ 0, /*spmv_group*/ 1,
     /*spmv_format*/ 1, /*pattern_min_pct*/ 0, /*issue_threads*/ 1, /*fault_inject*/ 0, /*spmv_xcd_chunk*/ 0, /*spmv_tri16*/ 1, /*spmv_diag_rows*/ 0,
-    /*halo_barrier*/ 1, /*side_fork*/ 0};
+    /*halo_barrier*/ 1, /*side_fork*/ 0, /*tri_order*/ 1};
 // COO → CSC → SELL on the device (pa_coo.hip)
 int coo_compress(int dtype, int index_bytes, int64_t m, int64_t ncols, int64_t n, const void* dI, const void* dJ,
                  const void* dV, int csr, int64_t* nu_out, int32_t** crow, int32_t** ccol, void** cval,
@@ -420,8 +420,9 @@ void free_triple_sell(pa_mat* A) {
 }
 
 // The triple SELL: the rows of the delta16 slices (kind 3),
-// re-sliced — rows whose columns are consecutive triples first, then the
-// others, each class by length (descending) and oid — so that most slices
+// re-sliced — the rows whose columns are not all consecutive triples, then
+// the triple rows (spmv_tri_order), each class by length (descending) and
+// oid — so that most slices
 // hold only triple rows and keep one 16-bit code per triple (their lanes
 // read a triple's x as one run), and no row's values stream twice (unlike
 // the side SELL of pattern slices).  The main delta16 slices become kind 5
@@ -451,12 +452,14 @@ int build_triple_sell(pa_mat* A, std::vector<int32_t>& kind, int64_t noids) {
   constexpr int32_t kLen = (1 << 28) - 1, kReg = 1 << 28, kGhost = 1 << 29, kBad = 1 << 30;
   for (int32_t v : info)
     if (v & kBad) return 0;
-  // order: regular rows, then the others; each by length (descending), then oid
+  // order: the other rows, then the regular (triple) rows (spmv_tri_order 1;
+  // 0: regular first); each by length (descending), then oid
   std::vector<int64_t> ord(n);
   std::iota(ord.begin(), ord.end(), 0);
+  const bool others_first = knobs().tri_order == 1;
   std::stable_sort(ord.begin(), ord.end(), [&](int64_t a, int64_t b) {
     const bool ra = (info[a] & kReg) != 0, rb = (info[b] & kReg) != 0;
-    if (ra != rb) return ra;
+    if (ra != rb) return others_first ? rb : ra;
     return (info[a] & kLen) > (info[b] & kLen);
   });
   const int64_t tns = (n + H - 1) / H;
@@ -1341,6 +1344,10 @@ const Knob kKnobs[] = {
      "spmv_tri16: the delta16 slices' rows re-sliced into the triple SELL (rows of consecutive column triples "
      "keep one 16-bit code per triple; matrices built afterwards): 1 = for 8 and 16 B elements (Float64, "
      "ComplexF32, ComplexF64; default), 2 = every element type, 0 = never"},
+    {"spmv_tri_order", &Knobs::tri_order, nullptr, 0, 1, 0,
+     "spmv_tri_order: the triple SELL's row order (matrices built afterwards): 1 = the other rows first "
+     "(their slower waves start early, the launch ends on uniform triple slices; default: C5 F64 -1 %, "
+     "Float32 triples -4..-7 %, profiles/r05/n/), 0 = rows of column triples first"},
     {"spmv_diag_rows", &Knobs::spmv_diag_rows, nullptr, 0, 1, 0,
      "spmv_diag_rows: 1 = a pattern slice's rows whose only entry is the diagonal (Dirichlet rows) are "
      "computed in the slice from entry 0 (matrices built afterwards), 0 = as side rows (default: faster, "

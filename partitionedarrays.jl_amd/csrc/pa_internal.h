@@ -348,6 +348,7 @@ struct Knobs {
   int spmv_diag_rows;    // pattern slices compute their diagonal-only rows (pa_mat::d_dmask)
   int halo_barrier;      // stream-pair mul!: one pack barrier + double-buffered sends (spmv_impl)
   int side_fork;         // per-kind launches: the side rows on the comm stream beside the pattern slices
+  int tri_order;         // triple SELL row order: 0 triple rows first, 1 the other rows first (build_triple_sell)
 };
 // the knobs of the call running on this thread (outside a call: a snapshot
 // of the process defaults)

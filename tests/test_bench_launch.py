@@ -62,3 +62,29 @@ def test_torchrun_rank_does_not_relaunch(monkeypatch):
         raise AssertionError("the rank path did not start")
     except RuntimeError as e:
         assert "rank path reached" in str(e)
+
+
+def test_one_process_leg_runs_a_bounded_child_and_reports_failure(monkeypatch):
+    """The one-process leg of an N-rank run (bench.one_process_leg): rank 0
+    starts `bench.py --child-oneproc` with the run's problem and without the
+    torchrun rank variables, bounded by a timeout; a child that fails (here:
+    no GPU in this container) becomes a note in the line, not an exception."""
+    import argparse
+    bench = _load_bench()
+    seen = {}
+    real_run = bench.subprocess.run
+
+    def spy(cmd, env=None, **kw):
+        seen["cmd"], seen["env"], seen["kw"] = cmd, env, kw
+        return real_run(cmd, env=env, **kw)
+
+    monkeypatch.setattr(bench.subprocess, "run", spy)
+    monkeypatch.setenv("RANK", "0")
+    monkeypatch.setenv("WORLD_SIZE", "8")
+    a = argparse.Namespace(gpus=8, n=32, kind=27, dtype="f64", steps=3, warmup=1, tune="", oneproc_devices="")
+    out = bench.one_process_leg(a)
+    cmd = seen["cmd"]
+    assert "--child-oneproc" in cmd and cmd[cmd.index("--gpus") + 1] == "8" and cmd[cmd.index("--n") + 1] == "32"
+    assert "RANK" not in seen["env"] and "WORLD_SIZE" not in seen["env"]
+    assert seen["kw"].get("timeout")
+    assert "note" in out and "failed" in out["note"], out

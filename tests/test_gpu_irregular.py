@@ -55,12 +55,13 @@ def _eq(O, got, ref):
     ((24, 22, 20), 8, np.complex64, 1), ((24, 22, 20), 8, np.float64, 0),
     (BIG[0], 8, np.float64, 1), (BIG[0], 8, np.float32, 1),       # C5 as benched: 8 parts of one device
     ((24, 22, 20), 12, np.float64, 1), ((24, 22, 20), 12, np.complex128, 0)])  # > PA_GROUP_MAX parts
-@pytest.mark.parametrize("tri16", [2, 0])
+@pytest.mark.parametrize("tri16", [2, 0, 3])  # 3: the triple SELL with its other rows first (spmv_tri_order 1)
 def test_irregular_spmv_bitexact(be, pamd, O, N, nparts, dtype, fmt, tri16):
-    if fmt == 0 and tri16 == 0:
+    if fmt == 0 and tri16 != 2:
         pytest.skip("spmv_format 0 runs every slice as int32 ids: the triple SELL is not used")
     prev = pamd._lib.tune("spmv_format", fmt)
-    prev_tri = pamd._lib.tune("spmv_tri16", tri16)
+    prev_tri = pamd._lib.tune("spmv_tri16", min(tri16, 2))
+    prev_ord = pamd._lib.tune("spmv_tri_order", 1 if tri16 == 3 else 0)
     # pattern slices from 40 % regular rows (default 70): the side SELL gets
     # the rest, so both the pattern and the side-row paths run
     prev_pct = pamd._lib.tune("pattern_min_regular", 40)
@@ -87,6 +88,7 @@ def test_irregular_spmv_bitexact(be, pamd, O, N, nparts, dtype, fmt, tri16):
     finally:
         pamd._lib.tune("spmv_format", prev)
         pamd._lib.tune("spmv_tri16", prev_tri)
+        pamd._lib.tune("spmv_tri_order", prev_ord)
         pamd._lib.tune("pattern_min_regular", prev_pct)
 
 

@@ -57,15 +57,22 @@ def measure(be, n, k, label, cg_iters=0):
         pamd.mul_(y, A, x)
     host_py = (time.perf_counter() - t0) / k
     sync()
-    # bare C-ABI enqueue (argument arrays built once)
+    # bare C-ABI enqueue (argument arrays built once); 7 repetitions of k
+    # calls, each after the device drained: the median (and the range) of
+    # the per-call host time (host threads make single runs noisy)
     args = pamd.pvector._spmv_args(y, A, x, 1.0, 0.0)
-    t0 = time.perf_counter()
-    for _ in range(k):
-        pamd._lib.call("pa_spmv_all", *args)
-    host_c = (time.perf_counter() - t0) / k
-    sync()
+    reps = []
+    for _ in range(7):
+        t0 = time.perf_counter()
+        for _ in range(k):
+            pamd._lib.call("pa_spmv_all", *args)
+        reps.append((time.perf_counter() - t0) / k)
+        sync()
+    reps.sort()
+    host_c = reps[len(reps) // 2]
     out = {"path": label, "parts": 8, "mul_wall_ms": round(1e3 * wall, 4),
            "host_us_per_mul_python": round(1e6 * host_py, 1), "host_us_per_mul_cabi": round(1e6 * host_c, 1),
+           "host_us_per_mul_cabi_min_max": [round(1e6 * reps[0], 1), round(1e6 * reps[-1], 1)],
            "host_us_per_part_cabi": round(1e6 * host_c / 8, 1)}
     if cg_iters:
         # a tiny operator (8 parts of 8^3): device work is negligible, so the
