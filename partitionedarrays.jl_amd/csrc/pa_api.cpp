@@ -90,7 +90,7 @@ const Knobs kDefaults = {
     /*spmv_flags*/ 93, /*long_exact*/ 1, /*halo_pull*/ 1, /*spmv_delta16*/ 1, /*spmv_merge*/ 1,
     /*spmv_merge_max*/ 65536, /*cg_fuse*/ 2, /*halo_direct*/ 1, /*halo_transport*/ 0, /*spmv_group*/ 1,
     /*spmv_format*/ 1, /*pattern_min_pct*/ 0, /*issue_threads*/ 1, /*fault_inject*/ 0, /*spmv_xcd_chunk*/ 0, /*spmv_tri16*/ 1, /*spmv_diag_rows*/ 0,
-    /*halo_barrier*/ 1, /*side_fork*/ 0, /*tri_order*/ 1};
+    /*halo_barrier*/ 1, /*side_fork*/ 0, /*tri_order*/ 1, /*side_tail*/ 1};
 // COO → CSC → SELL on the device (pa_coo.hip)
 int coo_compress(int dtype, int index_bytes, int64_t m, int64_t ncols, int64_t n, const void* dI, const void* dJ,
                  const void* dV, int csr, int64_t* nu_out, int32_t** crow, int32_t** ccol, void** cval,
@@ -1344,6 +1344,10 @@ const Knob kKnobs[] = {
      "spmv_tri16: the delta16 slices' rows re-sliced into the triple SELL (rows of consecutive column triples "
      "keep one 16-bit code per triple; matrices built afterwards): 1 = for 8 and 16 B elements (Float64, "
      "ComplexF32, ComplexF64; default), 2 = every element type, 0 = never"},
+    {"spmv_side_tail", &Knobs::side_tail, nullptr, 0, 1, 0,
+     "spmv_side_tail: per-kind launches without a halo in flight (big single parts): 1 = the side rows (<= 8 "
+     "entries) run as the trailing waves of the pattern launch (default: FE27 256^3 -0.4 %, profiles/r05/o/), "
+     "0 = a launch of their own after it"},
     {"spmv_tri_order", &Knobs::tri_order, nullptr, 0, 1, 0,
      "spmv_tri_order: the triple SELL's row order (matrices built afterwards): 1 = the other rows first "
      "(their slower waves start early, the launch ends on uniform triple slices; default: C5 F64 -1 %, "
@@ -3198,6 +3202,8 @@ static int spmv_grouped(int n, pa_mat* const A[], pa_vec* const y[], const pa_in
       E.push_back(part(i, nwork, list));
       W.push_back(which);
     };
+    // (side rows first also when they are short: FD7's Dirichlet rows last
+    // made C2 0.7 % slower, 0.0285 -> 0.0287 ms, profiles/r05/o/)
     for (int i = 0; i < n; ++i)
       if (knobs().spmv_format == 1 && A[i]->has_pat) add(2, i, A[i]->s_nslices, nullptr);
     for (int i = 0; i < n; ++i) {
@@ -3266,7 +3272,33 @@ static int spmv_grouped(int n, pa_mat* const A[], pa_vec* const y[], const pa_in
       P1.push_back(part(i, A[i]->nslices, nullptr));
     }
   }
-  launch_all(0, P0);
+  // the side rows as the pattern launch's trailing waves (spmv_side_tail):
+  // no halo in flight, the side rows short, pattern and side entries within
+  // one group launch, no fused CG update
+  bool side_tailed = false;
+  if (knobs().side_tail && !side_forked && (!any_x || direct) && !fz && 2 * n <= PA_GROUP_MAX) {
+    bool ok = false;
+    for (int i = 0; i < n; ++i) {
+      const bool pat = knobs().spmv_format == 1 && A[i]->has_pat;
+      if (!pat) { ok = false; break; }
+      if (A[i]->s_nslices > 0) {
+        if (A[i]->maxlen_side > 8) { ok = false; break; }
+        ok = true;
+      }
+    }
+    if (ok) {
+      std::vector<SpmvPart> PT = P0;
+      for (int i = 0; i < n; ++i)
+        if (A[i]->s_nslices > 0) {
+          SpmvPart q = part(i, A[i]->s_nslices, nullptr);
+          q.side = true;
+          PT.push_back(q);
+        }
+      launch_all(6, PT);
+      side_tailed = true;
+    }
+  }
+  if (!side_tailed) launch_all(0, P0);
   launch_all(5, P5);
   launch_all(4, P4);
   launch_all(1, P1);
@@ -3281,7 +3313,7 @@ static int spmv_grouped(int n, pa_mat* const A[], pa_vec* const y[], const pa_in
       P4.push_back(part(i, A[i]->nd_bnd, A[i]->d_dbnd_list));
       P5.push_back(part(i, A[i]->nt_bnd, A[i]->d_t_bnd_list));
       P1.push_back(part(i, A[i]->nx_bnd, A[i]->d_xbnd_list));
-      if (!side_forked) P2.push_back(part(i, A[i]->s_nslices, nullptr));
+      if (!side_forked && !side_tailed) P2.push_back(part(i, A[i]->s_nslices, nullptr));
     } else if (A[i]->d_bnd_list) {
       P1.push_back(part(i, A[i]->nslices - A[i]->nslices_int, A[i]->d_bnd_list));
     }

@@ -236,6 +236,9 @@ struct SpmvPart {
   void* un = nullptr;
   void* xacc = nullptr;
   const CGState* cg = nullptr;
+  // a side-row entry (kind 2) trailing the pattern entries of one grouped
+  // launch (which 6: spmv_grouped's side tail)
+  bool side = false;
 };
 
 struct PackGroup {
@@ -349,6 +352,7 @@ struct Knobs {
   int halo_barrier;      // stream-pair mul!: one pack barrier + double-buffered sends (spmv_impl)
   int side_fork;         // per-kind launches: the side rows on the comm stream beside the pattern slices
   int tri_order;         // triple SELL row order: 0 triple rows first, 1 the other rows first (build_triple_sell)
+  int side_tail;         // per-kind launches: the side rows as the trailing waves of the pattern launch
 };
 // the knobs of the call running on this thread (outside a call: a snapshot
 // of the process defaults)

@@ -1050,11 +1050,19 @@ __global__ __launch_bounds__(256) void k_spmv_sell(SpmvArgs<T> a) {
 template <typename T>
 struct SpmvGroup {
   int np;
+  int tail0;  // entries [tail0, np) are side rows (int32 columns, <= 8 entries), TAIL kernels only
   int64_t start[PA_GROUP_MAX + 1];
   SpmvArgs<T> a[PA_GROUP_MAX];
 };
 
-template <typename T, int R, bool ALPHA, int BMODE, int U, int PK, bool SH = false, bool XV = false>
+// TAIL: the group's last entries are the parts' side rows (spmv_grouped's
+// side tail, pa_tune "spmv_side_tail"): their few short waves run as the
+// launch's trailing waves with the short-row int32 code (one masked batch:
+// few registers, so the kernel keeps the pattern code's), instead of a
+// launch of their own after the pattern slices (FE27 256³: 1,008 waves of
+// one entry each, 6.8 µs as a separate launch, profiles/r04/am/)
+template <typename T, int R, bool ALPHA, int BMODE, int U, int PK, bool SH = false, bool XV = false,
+          bool TAIL = false>
 __global__ __launch_bounds__(256) void k_spmv_sell_group(const SpmvGroup<T> g) {
   // wave-uniform: the part's arguments are read with scalar loads
   const int64_t w = xcd_block(g.a[0].xcd_chunk) * 4 + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
@@ -1062,6 +1070,12 @@ __global__ __launch_bounds__(256) void k_spmv_sell_group(const SpmvGroup<T> g) {
   int p = 0;
   while (p + 1 < g.np && w >= g.start[p + 1]) ++p;
   p = __builtin_amdgcn_readfirstlane(p);
+  if constexpr (TAIL) {
+    if (p >= g.tail0) {
+      spmv_wave<T, R, ALPHA, BMODE, U, 0, true, false>(g.a[p], w - g.start[p]);
+      return;
+    }
+  }
   spmv_wave<T, R, ALPHA, BMODE, U, PK, SH, XV>(g.a[p], w - g.start[p]);
 }
 
@@ -1070,13 +1084,20 @@ static void launch_group_t(const SpmvGroup<T>& g, hipStream_t st) {
   const int64_t blocks = (g.start[g.np] + 3) / 4;
   if (blocks == 0) return;
   bool sh = (knobs().spmv_flags & SPMV_SHORT) != 0;
-  for (int i = 0; i < g.np; ++i) sh = sh && g.a[i].maxlen <= 8;
+  for (int i = 0; i < g.np && i < g.tail0; ++i) sh = sh && g.a[i].maxlen <= 8;
   if constexpr (!ALPHA && BMODE == 0 && PAT != 4) {
     if (g.a[0].cg) {  // the device CG's fused u update
       if (sh)
         hipLaunchKernelGGL((k_spmv_sell_group<T, R, false, 0, 8, PAT, true, true>), dim3(blocks), dim3(256), 0, st, g);
       else
         hipLaunchKernelGGL((k_spmv_sell_group<T, R, false, 0, 8, PAT, false, true>), dim3(blocks), dim3(256), 0, st, g);
+      return;
+    }
+  }
+  if constexpr (PAT == 1) {
+    if (g.tail0 < g.np) {  // pattern entries, then side rows (group_which, which 6)
+      hipLaunchKernelGGL((k_spmv_sell_group<T, R, ALPHA, BMODE, 8, PAT, false, false, true>), dim3(blocks), dim3(256),
+                         0, st, g);
       return;
     }
   }
@@ -1222,21 +1243,28 @@ static void launch_which(int which, int64_t nwork, const int32_t* list, const pa
 template <typename T, int R>
 static void group_which(int which, int np, const SpmvPart* parts, bool has_alpha, int bmode, const void* alpha,
                         const void* beta, hipStream_t st) {
+  // which 6: pattern entries followed by side-row entries (SpmvPart::side;
+  // the caller passes at most PA_GROUP_MAX entries, pattern ones first): one
+  // TAIL launch
   SpmvGroup<T> g{};
+  g.tail0 = PA_GROUP_MAX + 1;
   auto flush = [&]() {
     if (g.np == 0) return;
-    if (which == 0) launch_group_ab<T, R, 1>(g, has_alpha, bmode, st);
+    if (which == 0 || which == 6) launch_group_ab<T, R, 1>(g, has_alpha, bmode, st);
     else if (which == 4) launch_group_ab<T, R, 3>(g, has_alpha, bmode, st);
     else if (which == 5) launch_group_ab<T, R, 4>(g, has_alpha, bmode, st);
     else launch_group_ab<T, R, 0>(g, has_alpha, bmode, st);
     g = SpmvGroup<T>{};
+    g.tail0 = PA_GROUP_MAX + 1;
   };
   for (int i = 0; i < np; ++i) {
     const SpmvPart& q = parts[i];
     if (q.nwork <= 0) continue;
+    const int kind = which == 6 ? (q.side ? 2 : 0) : which;
+    if (which == 6 && q.side && g.tail0 > g.np) g.tail0 = g.np;
     const int32_t* list = q.list;
-    if ((knobs().spmv_flags & SPMV_IDLIST) && list && which != 2 && which != 5 && q.nwork == q.A->nslices) list = nullptr;
-    g.a[g.np] = make_args<T>(which, q.nwork, list, q.A, q.x, q.y, q.ymap, alpha, beta, q.dotp, &q);
+    if ((knobs().spmv_flags & SPMV_IDLIST) && list && kind != 2 && kind != 5 && q.nwork == q.A->nslices) list = nullptr;
+    g.a[g.np] = make_args<T>(kind, q.nwork, list, q.A, q.x, q.y, q.ymap, alpha, beta, q.dotp, &q);
     g.start[g.np + 1] = g.start[g.np] + q.nwork;
     if (++g.np == PA_GROUP_MAX) flush();
   }

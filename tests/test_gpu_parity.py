@@ -545,14 +545,16 @@ def test_diagonal_only_rows_equal_oracle(be, pamd, O, kind, N, dtype, diag):
 
 
 @pytest.mark.parametrize("dtype", [np.float64, np.float32, np.complex128])
-@pytest.mark.parametrize("fork", [1, 0])
-def test_side_fork_per_kind_launches_equal_oracle(be, pamd, O, dtype, fork):
+@pytest.mark.parametrize("fork,tail", [(1, 0), (0, 0), (0, 1)])
+def test_side_fork_per_kind_launches_equal_oracle(be, pamd, O, dtype, fork, tail):
     """Per-kind launches of one part (spmv_merge_max below its slice count:
     the headline's path) with the side rows on the comm stream beside the
-    pattern slices (spmv_side_fork 1) or after them (0): mul! with α/β, back
+    pattern slices (spmv_side_fork 1), as the pattern launch's trailing waves
+    (spmv_side_tail 1) or as a launch after it (both 0): mul! with α/β, back
     to back on changing x without a host sync, and the fused dot give the
     oracle's bits; the side rows exist (the domain-face Dirichlet rows)."""
     p0 = pamd._lib.tune("spmv_side_fork", fork)
+    p2 = pamd._lib.tune("spmv_side_tail", tail)
     p1 = pamd._lib.tune("spmv_merge_max", 4)
     try:
         shape, N = (1, 1, 1), (40, 21, 12)
@@ -585,4 +587,5 @@ def test_side_fork_per_kind_launches_equal_oracle(be, pamd, O, dtype, fork):
             assert abs(d - ref) <= 1e-12 * max(1.0, abs(ref)), (d, ref)
     finally:
         pamd._lib.tune("spmv_merge_max", p1)
+        pamd._lib.tune("spmv_side_tail", p2)
         pamd._lib.tune("spmv_side_fork", p0)
