@@ -89,7 +89,7 @@ void launch_gather_scatter(int P, const void* const* srcs, int accsz, int nd, vo
 const Knobs kDefaults = {
     /*spmv_flags*/ 93, /*long_exact*/ 1, /*halo_pull*/ 1, /*spmv_delta16*/ 1, /*spmv_merge*/ 1,
     /*spmv_merge_max*/ 65536, /*cg_fuse*/ 2, /*halo_direct*/ 1, /*halo_transport*/ 0, /*spmv_group*/ 1,
-    /*spmv_format*/ 1, /*pattern_min_pct*/ 0, /*issue_threads*/ 1, /*fault_inject*/ 0, /*spmv_xcd_chunk*/ 0, /*spmv_tri16*/ 1, /*spmv_diag_rows*/ 0,
+    /*spmv_format*/ 1, /*pattern_min_pct*/ 0, /*issue_threads*/ 1, /*fault_inject*/ 0, /*spmv_xcd_chunk*/ -1, /*spmv_tri16*/ 1, /*spmv_diag_rows*/ 0,
     /*halo_barrier*/ 1, /*side_fork*/ 0, /*tri_order*/ 1, /*side_tail*/ 1};
 // COO → CSC → SELL on the device (pa_coo.hip)
 int coo_compress(int dtype, int index_bytes, int64_t m, int64_t ncols, int64_t n, const void* dI, const void* dJ,
@@ -344,6 +344,7 @@ int dedup_patterns(pa_mat* A, const std::vector<int32_t>& kind) {
   HIPC(hipStreamSynchronize(st));
   std::vector<int32_t> table, packed(A->h_plen);
   std::unordered_map<std::string, int32_t> ids;
+  int64_t reach = 0;  // largest |column - row| of the pattern slices' patterns
   for (int64_t s = 0; s < ns; ++s) {
     if (kind[s] != 1) continue;
     const int32_t len = A->h_plen[s];
@@ -356,6 +357,7 @@ int dedup_patterns(pa_mat* A, const std::vector<int32_t>& kind) {
       CHECK_ARG(id < (1 << 22), "more than 2^22 distinct slice patterns");
       ids.emplace(std::move(key), id);
       table.insert(table.end(), pat.begin() + s * K, pat.begin() + (s + 1) * K);
+      for (int32_t k = 0; k < len; ++k) reach = std::max<int64_t>(reach, std::llabs((long long)pat[s * K + k]));
     } else {
       id = it->second;
     }
@@ -368,6 +370,11 @@ int dedup_patterns(pa_mat* A, const std::vector<int32_t>& kind) {
     packed[s] = len | ((tri ? 1 : 0) << 8) | (id << 9);
   }
   A->npatterns = (int64_t)ids.size();
+  // spmv_xcd_chunk auto: the pattern's reach (largest |column - row|) in
+  // 4-slice blocks; runs of reach/8 blocks per XCD put a block's farthest
+  // neighbour plane (FE27: the z-neighbour, N² rows away) one run-group
+  // later on the same XCD, whose L2 still holds those x lines
+  A->xcd_auto = (int)std::min<int64_t>(64, reach / (4 * A->H) / 8);
   dev_free(A->d_pat);
   A->d_pat = nullptr;
   if (table.empty()) table.assign(K, 0);
@@ -1364,10 +1371,12 @@ const Knob kKnobs[] = {
      "spmv_side_fork: per-kind launches without a halo in flight (big single parts): 1 = the side rows run on "
      "the comm stream beside the pattern slices, 0 = after them on the compute stream (default, "
      "profiles/r05/k/)"},
-    {"spmv_xcd_chunk", &Knobs::spmv_xcd_chunk, nullptr, 0, 64, 0,
-     "spmv_xcd_chunk: C > 0 = the SpMV launches' workgroups in runs of C consecutive blocks per XCD (x lines "
-     "of neighbouring slices shared in one L2), 0 = the hardware's round robin (default: C = 4 lost on C2, "
-     "0.0283 -> 0.0287-0.0289 ms, profiles/r05/k/)"},
+    {"spmv_xcd_chunk", &Knobs::spmv_xcd_chunk, nullptr, -1, 64, 0,
+     "spmv_xcd_chunk: the SpMV launches' workgroups in runs of C consecutive blocks per XCD (C > 0; the x lines "
+     "of neighbouring slices shared in one L2), 0 = the hardware's round robin, -1 = auto (default): per-kind "
+     "launches (big single parts) take C = the pattern's reach in blocks / 8, so that a block's z-neighbour "
+     "plane runs on its XCD (FE27 256^3 F64: C = 16, -1.0..-1.2 %, profiles/r05/q,r/), merged launches keep "
+     "the round robin (C2: C = 4 +1.4 %, r05/k/)"},
     {"fault_inject", &Knobs::fault_inject, nullptr, 0, 1, 0,
      "fault_inject: 1 = every job of a threaded issue (IssuePool) also issues an invalid kernel launch (tests "
      "of the error path; test_exception.jl's role), 0 = off (default)"},

@@ -346,7 +346,7 @@ struct Knobs {
   int pattern_min_pct;
   int issue_threads;
   int fault_inject;      // tests only: the IssuePool jobs issue an invalid launch
-  int spmv_xcd_chunk;    // XCD-chunked block order of the SpMV launches (pa_spmv.hip xcd_block), 0 off
+  int spmv_xcd_chunk;    // XCD-chunked block order of the SpMV launches (pa_spmv.hip xcd_block), 0 off, -1 auto
   int spmv_tri16;        // delta16 slices re-sliced into the triple SELL (pa_mat::d_t_*): 0 never, 1 R <= 2, 2 always
   int spmv_diag_rows;    // pattern slices compute their diagonal-only rows (pa_mat::d_dmask)
   int halo_barrier;      // stream-pair mul!: one pack barrier + double-buffered sends (spmv_impl)
@@ -531,6 +531,9 @@ struct pa_mat {
   int32_t* d_plen = nullptr;         // per slice: entries per row (int32 len; pattern slices: len (bits 0-7) | tri flag (bit 8) | pattern id << 9)
   int32_t* d_pat = nullptr;          // npatterns*kmax offsets: the distinct patterns (dedup_patterns)
   int64_t npatterns = 0;
+  // XCD run length of this matrix's per-kind launches in spmv_xcd_chunk's
+  // auto mode (dedup_patterns: the pattern's reach in blocks / 8), 0 = none
+  int xcd_auto = 0;
   uint64_t* d_mask = nullptr;        // nslices*(H/64) regular-row bits
   // diagonal-only rows of pattern slices (Dirichlet rows: one entry, column
   // == row; pa_tune "spmv_diag_rows"): computed in the slice from entry 0

@@ -1178,7 +1178,7 @@ static SpmvArgs<T> make_args(int which, int64_t nwork, const int32_t* list, cons
   a.alpha = *(const T*)alpha;
   a.beta = *(const T*)beta;
   a.flags = knobs().spmv_flags | (A->csr ? SPMV_PRODA : 0);
-  a.xcd_chunk = knobs().spmv_xcd_chunk;
+  a.xcd_chunk = knobs().spmv_xcd_chunk >= 0 ? knobs().spmv_xcd_chunk : A->xcd_auto;
   a.maxlen = which == 0   ? A->maxlen_pat
              : which == 2 ? A->maxlen_side
              : which == 1 ? ((knobs().spmv_format == 1 && A->has_pat) ? A->maxlen_pm_int : A->maxlen_all)
@@ -1388,7 +1388,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
 
 template <typename T, int R, bool ALPHA, int BMODE>
 static void launch_merged_t(const SpmvTable<T>* d, int n, int64_t waves, bool sh, hipStream_t st) {
-  const int xc = knobs().spmv_xcd_chunk;
+  const int xc = std::max(knobs().spmv_xcd_chunk, 0);  // (auto: merged launches keep the round robin)
   const int64_t blocks = (waves + 3) / 4;
   if (blocks == 0) return;
   if constexpr (std::is_same<T, double>::value) {
@@ -1464,7 +1464,7 @@ static int merged_t(int n, const int* which, const SpmvPart* parts, bool has_alp
   if (h.a[0].cg) {  // the device CG's fused u update (α = 1, β = 0)
     const int64_t blocks = (waves + 3) / 4;
     if (blocks == 0) return 0;
-    const int xc = knobs().spmv_xcd_chunk;
+    const int xc = std::max(knobs().spmv_xcd_chunk, 0);  // (auto: merged launches keep the round robin)
     if (sh) hipLaunchKernelGGL((k_spmv_merged<T, R, false, 0, 8, true, true>), dim3(blocks), dim3(256), 0, st, dt, h.n, waves, xc);
     else hipLaunchKernelGGL((k_spmv_merged<T, R, false, 0, 8, false, true>), dim3(blocks), dim3(256), 0, st, dt, h.n, waves, xc);
     return 0;
