@@ -589,3 +589,40 @@ def test_side_fork_per_kind_launches_equal_oracle(be, pamd, O, dtype, fork, tail
         pamd._lib.tune("spmv_merge_max", p1)
         pamd._lib.tune("spmv_side_tail", p2)
         pamd._lib.tune("spmv_side_fork", p0)
+
+
+@pytest.mark.parametrize("chunk", [1, 3, 5, 16, 64, -1])
+def test_xcd_chunked_block_order_equals_round_robin(be, pamd, chunk):
+    """spmv_xcd_chunk maps runs of C consecutive 4-slice blocks to one XCD
+    (xcd_block, a bijection of the grid: blocks past the last full group of
+    8C keep their order); per-kind launches (spmv_merge_max below the slice
+    count) with any C, including ones that leave partial groups, and the auto
+    value compute every slice exactly once: y equals the round robin's bit
+    for bit, with α/β and the side rows as trailing waves."""
+    p0 = pamd._lib.tune("spmv_merge_max", 4)
+    try:
+        shape, N = (1, 1, 1), (64, 60, 37)
+        parts = be.get_part_ids(shape)
+        rng = np.random.default_rng(SEED + 47)
+        outs = {}
+        for c in (0, chunk):
+            p1 = pamd._lib.tune("spmv_xcd_chunk", c)
+            try:
+                A = pamd.drivers.stencil_operator(parts, N, 27)
+                n = A.cols.partition.local(1).num_lids
+                if c == 0:
+                    xv = rng.uniform(-1, 1, n)
+                    yv = rng.uniform(-1, 1, A.rows.partition.local(1).num_lids)
+                x = pamd.PVector.from_host(pamd.map_parts(lambda s: xv.copy(), A.cols.partition), A.cols)
+                res = []
+                for alpha, beta in ((1.0, 0.0), (-0.7, 0.5)):
+                    y = pamd.PVector.from_host(pamd.map_parts(lambda s: yv.copy(), A.rows.partition), A.rows)
+                    pamd.mul_(y, A, x, alpha, beta)
+                    res.append(y.to_host().local(1).copy())
+                outs[c] = res
+            finally:
+                pamd._lib.tune("spmv_xcd_chunk", p1)
+        for a, b in zip(outs[0], outs[chunk]):
+            assert np.array_equal(a, b)
+    finally:
+        pamd._lib.tune("spmv_merge_max", p0)
