@@ -322,3 +322,4 @@ def test_voronoi_values_round_trip_through_moved_slots(be, pamd, O, dtype):
     got = y.to_host()
     for p in parts.part_ids:
         assert _eq(O, got.local(p), oy.values[p]), f"part {p}: SpMV with the new values differs"
+
