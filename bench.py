@@ -841,8 +841,9 @@ def main():
             "frac": round(achieved / HBM_PEAK_GBS, 4),
             "traffic": None if traffic is None else int(traffic),
             "traffic_detail": tnote,
-            "kernel": ("k_spmv_merged / k_spmv_sell (all SpMV kernels of one mul! step: pattern + side slices"
-                       + (", halo pack/pull" if halo else "") + ")"),
+            "kernel": ("k_spmv_sell_group (one part: the pattern slices with the side rows as trailing waves, "
+                       "XCD runs) / k_spmv_merged (parts sharing a GPU): all SpMV kernels of one mul! step"
+                       + (", halo pack/pull" if halo else "") + ""),
             "kernel_ms": round(kernel_ms, 4),
             "kernel_ms_note": ("HIP events on part %d's compute stream around the K timed steps, / K" % p0
                                + ("; all parts of this process (grouped launches)" if grouped_here else "")),
