@@ -100,7 +100,22 @@ int pa_device_count(int* count);
  * "issue_threads" a mul! over several parts with their own stream pairs is
  *               issued from host threads, one part per thread: 1 when the
  *               parts span several devices (default), 2 always, 0 never
- *               (the calling thread, one part after the other). */
+ *               (the calling thread, one part after the other);
+ * "halo_barrier" 1: such a mul! (local neighbours) waits for one pack
+ *               barrier per call and alternates two send buffers (default),
+ *               0: per-neighbour event waits before every pack and pull;
+ * "spmv_tri16"  the triple SELL for delta16 slices (see below): 1 for 8 and
+ *               16 B elements (default), 2 every type, 0 never;
+ * "spmv_tri_order" 1: its other rows first (default), 0: triple rows first;
+ * "spmv_xcd_chunk" -1 (default, auto): one-launch-per-kind calls run their
+ *               workgroups in runs of (pattern reach / 8) blocks per XCD,
+ *               merged launches round robin; C > 0: runs of C; 0: round robin;
+ * "spmv_side_tail" 1: per-kind launches run short side rows as the pattern
+ *               launch's trailing waves (default), 0: their own launch;
+ * "spmv_diag_rows", "spmv_side_fork" 1: diagonal-only rows inside their
+ *               pattern slice / side rows on the comm stream (A/B levers,
+ *               default 0);
+ * "fault_inject" tests only: threaded issue jobs add an invalid launch. */
 int pa_tune(const char* key, int value, int* previous);
 /* The same knobs for one context: calls led by parts of `c` (their first
  * part's context) run with this value instead of the process default, for
