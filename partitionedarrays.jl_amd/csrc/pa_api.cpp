@@ -3203,7 +3203,20 @@ static int spmv_grouped(int n, pa_mat* const A[], pa_vec* const y[], const pa_in
   int merged = 1;
   bool big_part = false;  // one part alone fills the GPU many times: per-kind launches (knobs().spmv_merge_max)
   if (knobs().spmv_merge_max > 0 && n == 1) big_part = A[0]->nslices > knobs().spmv_merge_max;
-  if (knobs().spmv_merge && !big_part && (!any_x || direct)) {
+  // parts of pattern slices and short side rows only, no halo: the per-kind
+  // path's side tail is ONE launch too, through the group kernel (its
+  // arguments in the kernel's argument segment, no table search per wave):
+  // C2 FD7 128³ 0.0285-0.0286 -> 0.0281 ms, FE27 128³ one part 0.0843 ->
+  // 0.0817 (profiles/r05/y,z/); not for Float32's 256-row slices (C2 F32
+  // 0.0195 -> 0.0216 ms, z/)
+  bool tail_only = knobs().side_tail && !any_x && !fz && 2 * n <= PA_GROUP_MAX && A[0]->R <= 2;
+  for (int i = 0; i < n && tail_only; ++i) {
+    const pa_mat* M = A[i];
+    tail_only = knobs().spmv_format == 1 && M->has_pat && M->np_bnd == 0 && M->nx_int + M->nx_bnd == 0 &&
+                M->nd_int + M->nd_bnd == 0 && M->t_nslices == 0 && M->n_long == 0 &&
+                (M->s_nslices == 0 || M->maxlen_side <= 8);
+  }
+  if (knobs().spmv_merge && !big_part && !tail_only && (!any_x || direct)) {
     std::vector<SpmvPart> E;
     std::vector<int> W;
     auto add = [&](int which, int i, int64_t nwork, const int32_t* list) {

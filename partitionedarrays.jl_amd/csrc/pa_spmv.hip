@@ -1096,8 +1096,20 @@ static void launch_group_t(const SpmvGroup<T>& g, hipStream_t st) {
   }
   if constexpr (PAT == 1) {
     if (g.tail0 < g.np) {  // pattern entries, then side rows (group_which, which 6)
-      hipLaunchKernelGGL((k_spmv_sell_group<T, R, ALPHA, BMODE, 8, PAT, false, false, true>), dim3(blocks), dim3(256),
-                         0, st, g);
+      if (sh && knobs().spmv_xcd_chunk < 0) {
+        // short rows (one batch per wave, latency-bound): the auto XCD runs
+        // cost more than their x locality gives (C2: 0.0282 with the round
+        // robin vs 0.0283-0.0284 with runs of 4, profiles/r05/y/)
+        SpmvGroup<T> g2 = g;
+        for (int i = 0; i < g2.np; ++i) g2.a[i].xcd_chunk = 0;
+        hipLaunchKernelGGL((k_spmv_sell_group<T, R, ALPHA, BMODE, 8, PAT, true, false, true>), dim3(blocks),
+                           dim3(256), 0, st, g2);
+      } else if (sh)
+        hipLaunchKernelGGL((k_spmv_sell_group<T, R, ALPHA, BMODE, 8, PAT, true, false, true>), dim3(blocks),
+                           dim3(256), 0, st, g);
+      else
+        hipLaunchKernelGGL((k_spmv_sell_group<T, R, ALPHA, BMODE, 8, PAT, false, false, true>), dim3(blocks),
+                           dim3(256), 0, st, g);
       return;
     }
   }

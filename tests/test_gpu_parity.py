@@ -626,3 +626,34 @@ def test_xcd_chunked_block_order_equals_round_robin(be, pamd, chunk):
             assert np.array_equal(a, b)
     finally:
         pamd._lib.tune("spmv_merge_max", p0)
+
+
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+def test_short_row_side_tail_equals_oracle(be, pamd, O, dtype):
+    """The short-row kernels with the side rows as trailing waves: FD7
+    (test_fdm's operator: 7-entry rows, the domain-face identity rows as side
+    rows) in one-launch-per-kind mode (spmv_merge 0) runs its pattern slices
+    and side rows as ONE short-row launch (k_spmv_sell_group SH + TAIL): mul!
+    with α/β gives the oracle's bits."""
+    p0 = pamd._lib.tune("spmv_merge", 0)
+    try:
+        shape, N = (1, 1, 1), (40, 33, 21)
+        parts = be.get_part_ids(shape)
+        A = pamd.drivers.stencil_operator(parts, N, 7, dtype)
+        OA = O.stencil_problem(O.get_part_ids(shape), N, 7, dtype)
+        assert A.values.local(1).info()["side_rows"] > 0
+        rng = np.random.default_rng(SEED + 49)
+        xv = _rand(rng, A.cols.partition.local(1).num_lids, dtype)
+        yv = _rand(rng, A.rows.partition.local(1).num_lids, dtype)
+        x = pamd.PVector.from_host(pamd.map_parts(lambda s: xv, A.cols.partition), A.cols)
+        ox = O.PVector(O.map_parts(lambda s: _to_oracle(O, xv), OA.cols.partition), OA.cols)
+        sc = np.float32 if np.dtype(dtype) == np.float32 else np.float64
+        for alpha, beta in ((1.0, 0.0), (-1.3, 0.5)):
+            y = pamd.PVector.from_host(pamd.map_parts(lambda s: yv, A.rows.partition), A.rows)
+            oy = O.PVector(O.map_parts(lambda s: _to_oracle(O, yv), OA.rows.partition), OA.rows)
+            pamd.mul_(y, A, x, alpha, beta)
+            O.mul_(oy, OA, ox, sc(alpha), sc(beta))
+            own = A.rows.partition.local(1).oid_to_lid - 1
+            assert _eq(O, y.to_host().local(1)[own], _sel(O, oy.values[1], own)), (alpha, beta)
+    finally:
+        pamd._lib.tune("spmv_merge", p0)
