@@ -1353,18 +1353,24 @@ struct SpmvTable {
   SpmvArgs<T> a[kMergeMax];
 };
 
+// The wave -> entry map that follows a merged table in device memory (one
+// byte per wave, at the 16 B boundary after the table's n used entries):
+// a wave finds its entry with one load instead of a binary search over the
+// table's start offsets (log2(n) dependent loads ahead of every wave's
+// stream; C5's tables hold 20-40 entries)
+template <typename T>
+__host__ __device__ constexpr size_t merged_map_offset(int n) {
+  return (offsetof(SpmvTable<T>, a) + (size_t)n * sizeof(SpmvArgs<T>) + 15) & ~(size_t)15;
+}
+
 template <typename T, int R, bool ALPHA, int BMODE, int U, bool SH, bool XV = false>
 __device__ __forceinline__ void merged_wave(const SpmvTable<T>* __restrict__ tab, int n, int64_t waves, int xc) {
   // n and the wave count come as kernel arguments (with the kernarg load, not
   // two dependent table loads ahead of the search)
   const int64_t w = xcd_block(xc) * 4 + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   if (w >= waves) return;
-  int lo = 0, hi = n;  // last entry whose start <= w
-  while (hi - lo > 1) {
-    const int mid = (lo + hi) >> 1;
-    if (tab->start[mid] <= w) lo = mid; else hi = mid;
-  }
-  const int p = __builtin_amdgcn_readfirstlane(lo);
+  const uint8_t* __restrict__ map = reinterpret_cast<const uint8_t*>(tab) + merged_map_offset<T>(n);
+  const int p = __builtin_amdgcn_readfirstlane((int)map[w]);
   const int pk = __builtin_amdgcn_readfirstlane(tab->pk[p]);
   const int64_t lw = w - tab->start[p];
   const SpmvArgs<T>& a = tab->a[p];
@@ -1441,19 +1447,28 @@ static int merged_t(int n, const int* which, const SpmvPart* parts, bool has_alp
     ++h.n;
   }
   if (h.n == 0) return 0;
+  static_assert(kMergeMax <= 255, "the wave map holds entry indices in bytes");
   const size_t used = kHdr + (size_t)h.n * sizeof(SpmvArgs<T>);  // the device reads entries < n only
+  const int64_t nwaves = h.start[h.n];
+  const size_t moff = merged_map_offset<T>(h.n), total = moff + (size_t)nwaves;
+  auto wave_map = [&]() {  // entry of every wave (merged_wave)
+    std::vector<char> m((size_t)nwaves);
+    for (int e = 0; e < h.n; ++e) std::memset(m.data() + h.start[e], e, (size_t)(h.start[e + 1] - h.start[e]));
+    return m;
+  };
   // cached device copy of this exact table (most recent first); a graph
   // capture (pinned) gets its own copy, owned by the graph
   auto& C = owner->merged_cache;
   const char* hb = reinterpret_cast<const char*>(&h);
   void* d = nullptr;
   if (pinned) {  // during a capture: device memory now, its contents after the capture ends
-    if (hipMalloc(&d, used) != hipSuccess) {
+    if (hipMalloc(&d, total) != hipSuccess) {
       (void)hipGetLastError();
       return 1;  // the caller launches per kind
     }
     pinned->push_back(d);
     g_capture_uploads.push_back({d, std::vector<char>(hb, hb + used)});
+    g_capture_uploads.push_back({(char*)d + moff, wave_map()});
   }
   for (size_t k = 0; !d && k < C.size(); ++k)
     if (C[k].first.size() == used && std::memcmp(C[k].first.data(), hb, used) == 0) {
@@ -1462,8 +1477,13 @@ static int merged_t(int n, const int* which, const SpmvPart* parts, bool has_alp
       break;
     }
   if (!d) {
-    if (hipMalloc(&d, used) != hipSuccess) return -1;
-    if (hipMemcpy(d, &h, used, hipMemcpyHostToDevice) != hipSuccess) { (void)hipFree(d); return -1; }
+    if (hipMalloc(&d, total) != hipSuccess) return -1;
+    const std::vector<char> m = wave_map();
+    if (hipMemcpy(d, &h, used, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy((char*)d + moff, m.data(), m.size(), hipMemcpyHostToDevice) != hipSuccess) {
+      (void)hipFree(d);
+      return -1;
+    }
     if (C.size() >= 16) {
       (void)hipStreamSynchronize(st);  // the evicted table may still be read
       (void)hipFree(C.back().second);
