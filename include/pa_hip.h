@@ -112,6 +112,11 @@ int pa_device_count(int* count);
  *               merged launches round robin; C > 0: runs of C; 0: round robin;
  * "spmv_side_tail" 1: per-kind launches run short side rows as the pattern
  *               launch's trailing waves (default), 0: their own launch;
+ * "f32_rows"    Float32 SELL rows per lane (matrices built afterwards):
+ *               4 (16 B value packs, 256-row slices), 2 (8 B packs, 128-row
+ *               slices: the Float64 geometry, so delta16 rows take the
+ *               triple SELL), 0 (default, auto): 4, rebuilt with 2 when
+ *               fewer than 80 % of the slices are pattern slices;
  * "spmv_diag_rows", "spmv_side_fork" 1: diagonal-only rows inside their
  *               pattern slice / side rows on the comm stream (A/B levers,
  *               default 0);

@@ -90,7 +90,7 @@ const Knobs kDefaults = {
     /*spmv_flags*/ 93, /*long_exact*/ 1, /*halo_pull*/ 1, /*spmv_delta16*/ 1, /*spmv_merge*/ 1,
     /*spmv_merge_max*/ 65536, /*cg_fuse*/ 2, /*halo_direct*/ 1, /*halo_transport*/ 0, /*spmv_group*/ 1,
     /*spmv_format*/ 1, /*pattern_min_pct*/ 0, /*issue_threads*/ 1, /*fault_inject*/ 0, /*spmv_xcd_chunk*/ -1, /*spmv_tri16*/ 1, /*spmv_diag_rows*/ 0,
-    /*halo_barrier*/ 1, /*side_fork*/ 0, /*tri_order*/ 1, /*side_tail*/ 1};
+    /*halo_barrier*/ 1, /*side_fork*/ 0, /*tri_order*/ 1, /*side_tail*/ 1, /*f32_rows*/ 0};
 // COO → CSC → SELL on the device (pa_coo.hip)
 int coo_compress(int dtype, int index_bytes, int64_t m, int64_t ncols, int64_t n, const void* dI, const void* dJ,
                  const void* dV, int csr, int64_t* nu_out, int32_t** crow, int32_t** ccol, void** cval,
@@ -553,7 +553,7 @@ int build_triple_sell(pa_mat* A, std::vector<int32_t>& kind, int64_t noids) {
   return 0;
 }
 
-int finalize_pattern(pa_mat* A, int kmax, int64_t noids) {
+int finalize_pattern(pa_mat* A, int kmax, int64_t noids, bool retry_r2) {
   A->kmax = std::max(kmax, 1);
   const int64_t ns = A->nslices;
   if (ns == 0) return 0;
@@ -581,6 +581,17 @@ int finalize_pattern(pa_mat* A, int kmax, int64_t noids) {
   HIPC(hipStreamSynchronize(st));
   dev_free(d_pghost);
   dev_free(d_nirreg);
+  if (retry_r2 && A->dtype == PA_F32 && A->R == 4 && knobs().f32_rows == 0) {
+    // f32_rows auto: a Float32 matrix with int32/delta16 slices (irregular
+    // parts, C5) streams faster as 128-row slices of 8 B packs, whose delta16
+    // rows take the triple SELL (C5 F32 0.0736 -> 0.0683 ms, 345 -> 289 MB);
+    // a matrix of pattern slices keeps 256-row slices (FE27 256^3 F32 0.328
+    // -> 0.374 ms with 128: profiles/r05/ac/).  C5's parts hold 6-62 %
+    // pattern slices, a stencil's parts ~100 %: the cut is 80 %
+    int64_t np = 0;
+    for (int64_t s = 0; s < ns; ++s) np += kind[s] == 1;
+    if (5 * np < 4 * ns) return kPreferR2;
+  }
   if (dedup_patterns(A, kind)) return -1;
   if (knobs().spmv_delta16) {  // int32-column slices whose columns fit 16-bit codes (kind 3)
     int32_t* d_ok = nullptr;
@@ -1351,6 +1362,11 @@ const Knob kKnobs[] = {
      "spmv_tri16: the delta16 slices' rows re-sliced into the triple SELL (rows of consecutive column triples "
      "keep one 16-bit code per triple; matrices built afterwards): 1 = for 8 and 16 B elements (Float64, "
      "ComplexF32, ComplexF64; default), 2 = every element type, 0 = never"},
+    {"f32_rows", &Knobs::f32_rows, nullptr, 0, 4, 6,
+     "f32_rows: Float32 SELL rows per lane (matrices built afterwards): 4 = 16 B value packs in 256-row "
+     "slices, 2 = 8 B packs in 128-row slices (the Float64 geometry; delta16 rows then take the triple "
+     "SELL), 0 = auto (default): 4, rebuilt with 2 when fewer than 80 % of the slices are pattern slices "
+     "(C5 F32 -7 %, FE27 256^3 F32 +14 % with 2, profiles/r05/ac/)"},
     {"spmv_side_tail", &Knobs::side_tail, nullptr, 0, 1, 0,
      "spmv_side_tail: per-kind launches without a halo in flight (big single parts): 1 = the side rows (<= 8 "
      "entries) run as the trailing waves of the pattern launch (default: FE27 256^3 -0.4 %, profiles/r05/o/), "
@@ -1424,6 +1440,14 @@ const Knobs& knobs() {
 }
 KnobBind::KnobBind(const Knobs* k) : prev(t_knobs) { t_knobs = k; }
 KnobBind::~KnobBind() { t_knobs = prev; }
+// a rebuild of a Float32 matrix with 2 rows per lane (f32_rows auto) in progress on this thread
+thread_local int t_force_f32_rows = 0;
+int f32_rows_knob() { return t_force_f32_rows ? t_force_f32_rows : (knobs().f32_rows == 2 ? 2 : 4); }
+struct ForceF32Rows {
+  int prev;
+  explicit ForceF32Rows(int r) : prev(t_force_f32_rows) { t_force_f32_rows = r; }
+  ~ForceF32Rows() { t_force_f32_rows = prev; }
+};
 }  // namespace pa
 
 // For the duration of a call: the knobs of the call's context (its
@@ -2174,7 +2198,14 @@ int mat_from_visit(pa_ctx* c, int dtype, int64_t nrows_lids, int64_t ncols_lids,
   if (cols->own_contig && cols->ghost_contig) {
     int kmax = 0;
     for (int32_t l : slen) kmax = std::max(kmax, l);
-    if (finalize_pattern(A, kmax, cols->noids)) { pa_mat_destroy(A); return -1; }
+    const int rc = finalize_pattern(A, kmax, cols->noids, true);
+    if (rc == kPreferR2) {
+      pa_mat_destroy(A);
+      ForceF32Rows f(2);
+      return mat_from_visit(c, dtype, nrows_lids, ncols_lids, in_nnz, nzval, rows, cols, visit, range_error, csr,
+                            out);
+    }
+    if (rc) { pa_mat_destroy(A); return -1; }
   }
   *out = A;
   return 0;
@@ -2503,7 +2534,14 @@ int mat_from_coo_impl(pa_ctx* c, int dtype, int index_bytes, int ids_global, int
   if (cols->own_contig && cols->ghost_contig) {
     int kmax = 0;
     for (int32_t l : slen) kmax = std::max(kmax, l);
-    if (finalize_pattern(A, kmax, cols->noids)) { pa_mat_destroy(A); return -1; }
+    const int rc = finalize_pattern(A, kmax, cols->noids, true);
+    if (rc == kPreferR2) {
+      pa_mat_destroy(A);
+      ForceF32Rows f(2);
+      return mat_from_coo_impl(c, dtype, index_bytes, ids_global, nrows_lids, ncols_lids, ncoo, I, J, V, kind, rows,
+                               cols, csr_bi, csc_nnz, colptr_out, rowval_out, out);
+    }
+    if (rc) { pa_mat_destroy(A); return -1; }
   }
   tr.mark("pattern slices");
   *out = A;
@@ -4490,7 +4528,7 @@ int pa_mat_stencil(pa_ctx* c, int dtype, int kind, const int64_t gdims[3], const
   {
     int kmax = 0;
     for (int32_t l : slen) kmax = std::max(kmax, l);
-    if (finalize_pattern(A, kmax, nrows)) { pa_mat_destroy(A); return -1; }
+    if (finalize_pattern(A, kmax, nrows, false)) { pa_mat_destroy(A); return -1; }
   }
   *out = A;
   return 0;

@@ -189,10 +189,16 @@ inline size_t dtype_size(int dt) {
   return 0;
 }
 
-// Rows per lane of the SELL layout so that one lane's value load is 16 B.
+// Rows per lane of the SELL layout so that one lane's value load is 16 B
+// (Float32: pa_tune "f32_rows" 2 gives 8 B loads in 128-row slices, the
+// Float64 geometry, so its delta16 rows can take the triple SELL).
+int f32_rows_knob();
+// finalize_pattern's answer for a Float32 matrix built with 4 rows per lane
+// under f32_rows 0 (auto) that is better off with 2: the caller rebuilds it
+constexpr int kPreferR2 = 2;
 inline int sell_rows_per_lane(int dt) {
   switch (dt) {
-    case PA_F32: return 4;
+    case PA_F32: return f32_rows_knob();
     case PA_F64: return 2;
     case PA_C64: return 2;
     case PA_C128: return 1;
@@ -353,6 +359,7 @@ struct Knobs {
   int side_fork;         // per-kind launches: the side rows on the comm stream beside the pattern slices
   int tri_order;         // triple SELL row order: 0 triple rows first, 1 the other rows first (build_triple_sell)
   int side_tail;         // per-kind launches: the side rows as the trailing waves of the pattern launch
+  int f32_rows;          // Float32 SELL rows per lane (matrices built afterwards): 4 (16 B packs), 2 (8 B), 0 auto
 };
 // the knobs of the call running on this thread (outside a call: a snapshot
 // of the process defaults)

@@ -695,7 +695,10 @@ static void stencil_fill_t(const StencilGeom& g, const int32_t* shell, const dou
 void launch_stencil_fill(const StencilGeom& g, const int32_t* shell, const double* coef,
                          int64_t nrows, int noids, pa_mat* A, int32_t* err, hipStream_t st) {
   switch (A->dtype) {
-    case PA_F32: stencil_fill_t<float, 4>(g, shell, coef, nrows, noids, A, err, st); break;
+    case PA_F32:
+      if (A->R == 2) stencil_fill_t<float, 2>(g, shell, coef, nrows, noids, A, err, st);
+      else stencil_fill_t<float, 4>(g, shell, coef, nrows, noids, A, err, st);
+      break;
     case PA_F64: stencil_fill_t<double, 2>(g, shell, coef, nrows, noids, A, err, st); break;
     case PA_C64: stencil_fill_t<c64, 2>(g, shell, coef, nrows, noids, A, err, st); break;
     case PA_C128: stencil_fill_t<c128, 1>(g, shell, coef, nrows, noids, A, err, st); break;

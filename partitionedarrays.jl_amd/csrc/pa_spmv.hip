@@ -171,12 +171,18 @@ __device__ __forceinline__ c128 pick(bool c, c128 a, c128 b) { return c128{c ? a
 // dword-aligned: global loads need 4 B alignment); pa_vec pads 64 B on both
 // sides, so i in [-(R-1), n-1] stays inside the allocation
 typedef unsigned int u4a __attribute__((ext_vector_type(4))) __attribute__((aligned(4)));
+typedef unsigned int u2r __attribute__((ext_vector_type(2))) __attribute__((aligned(4)));
 template <typename T, int R>
 __device__ __forceinline__ Pack<T, R> ld_xrun(const T* p) {
-  static_assert(sizeof(Pack<T, R>) == 16, "16 B runs");
-  const u4a r = *reinterpret_cast<const u4a*>(p);
   Pack<T, R> v;
-  __builtin_memcpy(&v, &r, 16);
+  if constexpr (sizeof(Pack<T, R>) == 8) {  // Float32 with 2 rows per lane (pa_tune "f32_rows")
+    const u2r r = *reinterpret_cast<const u2r*>(p);
+    __builtin_memcpy(&v, &r, 8);
+  } else {
+    static_assert(sizeof(Pack<T, R>) == 16, "16 B runs");
+    const u4a r = *reinterpret_cast<const u4a*>(p);
+    __builtin_memcpy(&v, &r, 16);
+  }
   return v;
 }
 
@@ -1314,9 +1320,22 @@ constexpr int kDtR = 2;
 using DtT = c128;
 constexpr int kDtR = 1;
 #endif
+// Float32 matrices hold 4 or 2 rows per lane (pa_tune "f32_rows", fixed when
+// a matrix is built): a call's parts run as runs of equal R
+constexpr bool kDtR2 = PA_SPMV_DT == 0;
 void PA_CAT(spmv_group_, PA_SPMV_DT)(int which, int np, const SpmvPart* parts, bool has_alpha, int bmode,
                                      const void* alpha, const void* beta, hipStream_t st) {
-  group_which<DtT, kDtR>(which, np, parts, has_alpha, bmode, alpha, beta, st);
+  if constexpr (kDtR2) {
+    for (int i = 0; i < np;) {
+      int j = i + 1;
+      while (j < np && parts[j].A->R == parts[i].A->R) ++j;
+      if (parts[i].A->R == 2) group_which<DtT, 2>(which, j - i, parts + i, has_alpha, bmode, alpha, beta, st);
+      else group_which<DtT, kDtR>(which, j - i, parts + i, has_alpha, bmode, alpha, beta, st);
+      i = j;
+    }
+  } else {
+    group_which<DtT, kDtR>(which, np, parts, has_alpha, bmode, alpha, beta, st);
+  }
 }
 #else
 void launch_spmv_group(int which, int np, const SpmvPart* parts, bool has_alpha, int bmode, const void* alpha,
@@ -1519,6 +1538,26 @@ static int merged_t(int n, const int* which, const SpmvPart* parts, bool has_alp
 int PA_CAT(spmv_merged_, PA_SPMV_DT)(int n, const int* which, const SpmvPart* parts, bool has_alpha, int bmode,
                                      const void* alpha, const void* beta, pa_ctx* owner, std::vector<void*>* pinned,
                                      hipStream_t st) {
+  if constexpr (kDtR2) {
+    bool mixed = false;
+    for (int i = 1; i < n; ++i) mixed = mixed || parts[i].A->R != parts[0].A->R;
+    if (mixed) {  // parts of both layouts: one merged launch per layout
+      if (n > kMergeMax) return 1;  // (nothing launched: the caller runs per kind)
+      std::vector<int> w[2];
+      std::vector<SpmvPart> q[2];
+      for (int i = 0; i < n; ++i) {
+        const int k = parts[i].A->R == 2 ? 0 : 1;
+        w[k].push_back(which[i]);
+        q[k].push_back(parts[i]);
+      }
+      const int rc = merged_t<DtT, 2>((int)w[0].size(), w[0].data(), q[0].data(), has_alpha, bmode, alpha, beta,
+                                      owner, pinned, st);
+      if (rc) return rc;
+      return merged_t<DtT, kDtR>((int)w[1].size(), w[1].data(), q[1].data(), has_alpha, bmode, alpha, beta, owner,
+                                 pinned, st);
+    }
+    if (n > 0 && parts[0].A->R == 2) return merged_t<DtT, 2>(n, which, parts, has_alpha, bmode, alpha, beta, owner, pinned, st);
+  }
   return merged_t<DtT, kDtR>(n, which, parts, has_alpha, bmode, alpha, beta, owner, pinned, st);
 }
 #else
@@ -1720,6 +1759,12 @@ void PA_CAT(spmv_long_, PA_SPMV_DT)(const pa_mat* A, const void* x, void* y, con
 void PA_CAT(spmv_part_, PA_SPMV_DT)(int which, int64_t nwork, const int32_t* list, const pa_mat* A, const void* x,
                                     void* y, const int32_t* ymap, bool has_alpha, int bmode, const void* alpha,
                                     const void* beta, void* dotp, hipStream_t st, const SpmvPart* cgp) {
+  if constexpr (kDtR2) {
+    if (A->R == 2) {
+      launch_which<DtT, 2>(which, nwork, list, A, x, y, ymap, has_alpha, bmode, alpha, beta, dotp, st, cgp);
+      return;
+    }
+  }
   launch_which<DtT, kDtR>(which, nwork, list, A, x, y, ymap, has_alpha, bmode, alpha, beta, dotp, st, cgp);
 }
 #else
@@ -2461,7 +2506,10 @@ static void side_fill_t(pa_mat* A, const int32_t* rows, const int32_t* len, hipS
 
 void launch_side_fill(pa_mat* A, const int32_t* rows, const int32_t* len, hipStream_t st) {
   switch (A->dtype) {
-    case PA_F32: side_fill_t<float, 4>(A, rows, len, st); break;
+    case PA_F32:
+      if (A->R == 2) side_fill_t<float, 2>(A, rows, len, st);
+      else side_fill_t<float, 4>(A, rows, len, st);
+      break;
     case PA_F64: side_fill_t<double, 2>(A, rows, len, st); break;
     case PA_C64: side_fill_t<c64, 2>(A, rows, len, st); break;
     case PA_C128: side_fill_t<c128, 1>(A, rows, len, st); break;
@@ -2637,7 +2685,10 @@ void launch_t_fill(const pa_mat* A, int64_t noids, bool codes, hipStream_t st) {
                      A->d_t_off, A->d_t_len, A->d_t_gbase, A->d_col, (const E*)A->d_val, noids, codes,          \
                      A->d_t_col16, (E*)A->d_t_val)
   switch (A->dtype) {
-    case PA_F32: PA_TF(float, 4); break;
+    case PA_F32:
+      if (A->R == 2) PA_TF(float, 2);
+      else PA_TF(float, 4);
+      break;
     case PA_F64: PA_TF(double, 2); break;
     case PA_C64: PA_TF(c64, 2); break;
     case PA_C128: PA_TF(c128, 1); break;

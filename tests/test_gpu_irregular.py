@@ -323,3 +323,93 @@ def test_voronoi_values_round_trip_through_moved_slots(be, pamd, O, dtype):
     for p in parts.part_ids:
         assert _eq(O, got.local(p), oy.values[p]), f"part {p}: SpMV with the new values differs"
 
+
+
+@pytest.mark.parametrize("rows,tri16", [(0, 1), (2, 1), (2, 0), (4, 1)])
+def test_float32_rows_per_lane_equal_oracle(be, pamd, O, rows, tri16):
+    """pa_tune("f32_rows"): Float32 SELL with 4 rows per lane (16 B packs,
+    256-row slices), 2 (8 B packs, 128-row slices: the delta16 rows take the
+    triple SELL) or auto (0, the default: 2 for a matrix made mostly of
+    non-pattern slices, i.e. these Voronoi parts).  The layout never changes
+    the terms or their order per row (SparseUtils.jl:176-185): bit-exact
+    against the oracle; y and the ghosts of x compared per part."""
+    N, nparts, dtype = BIG[0], 8, np.float32
+    prev = {k: pamd._lib.tune(k, v) for k, v in {"f32_rows": rows, "spmv_tri16": tri16}.items()}
+    try:
+        parts = be.get_part_ids(nparts)
+        A = pamd.drivers.irregular_problem(parts, N, 27, dtype)
+        OA = _oracle(O, N, nparts, dtype)
+        rng = np.random.default_rng(SEED + rows)
+        xs = {p: _rand(rng, A.cols.partition.local(p).num_lids, dtype) for p in parts.part_ids}
+        x = pamd.PVector.from_host(pamd.map_parts(lambda s: xs[s.part], A.cols.partition), A.cols)
+        y = pamd.PVector.undef(A.rows, dtype)
+        pamd.mul_(y, A, x)
+        ox = O.PVector(O.map_parts(lambda s: _ox(O, xs[s.part]), OA.cols.partition), OA.cols)
+        oy = O.pvector_undef(OA.rows, dtype)
+        O.mul_(oy, OA, ox)
+        got, gx = y.to_host(), x.to_host()
+        for p in parts.part_ids:
+            assert _eq(O, got.local(p), oy.values[p]), f"part {p}: SpMV differs"
+            assert _eq(O, gx.local(p), ox.values[p]), f"part {p}: ghost values of x differ"
+        want = {p: 256 if rows == 4 else 128 for p in parts.part_ids}
+        if rows == 0:  # auto: 128-row slices where the 256-row build has < 80 % pattern slices
+            pamd._lib.tune("f32_rows", 4)
+            A4 = pamd.drivers.irregular_problem(parts, N, 27, dtype)
+            for p in parts.part_ids:
+                i4 = A4.values.local(p).info()
+                want[p] = 128 if 5 * i4["pattern_slices"] < 4 * i4["nslices"] else 256
+            pamd._lib.tune("f32_rows", 0)
+        for p in parts.part_ids:
+            i = A.values.local(p).info()
+            assert i["nslices"] == (i["nrows"] + want[p] - 1) // want[p], (p, i)
+            if want[p] == 128 and tri16 and i["tri_rows"] > 0:
+                assert i["delta16_slices"] == 0, (p, i)
+    finally:
+        for k, v in prev.items():
+            pamd._lib.tune(k, v)
+
+
+def test_float32_rows_auto_keeps_pattern_matrices(be, pamd):
+    """f32_rows auto keeps 4 rows per lane for a matrix of pattern slices
+    (the FE27 stencil: 2 would cost +14 %, profiles/r05/ac/)."""
+    parts = be.get_part_ids((1, 1, 1))
+    N = (48, 40, 32)
+    A = pamd.drivers.stencil_operator(parts, N, 27, np.float32)
+    i = A.info().parts[0]
+    assert i["pattern_slices"] * 2 >= i["nslices"], i
+    assert i["nslices"] == (i["nrows"] + 255) // 256, i
+
+
+@pytest.mark.parametrize("merge", [1, 0])
+def test_float32_mixed_rows_per_lane_parts_equal_oracle(pamd, O, merge):
+    """Parts of one Float32 matrix with different SELL layouts (pa_ctx_tune
+    "f32_rows" 2 on even parts, 4 on odd ones: what auto gives when some
+    parts are stencil-like): the merged launch runs one launch per layout,
+    the per-kind launches runs of equal layout; bit-exact against the oracle."""
+    be = pamd.HIPBackend(devices=[0])
+    N, nparts, dtype = (30, 28, 26), 8, np.float32
+    parts = be.get_part_ids(nparts)
+    for p in parts.part_ids:
+        be.context(p).tune("f32_rows", 2 if p % 2 == 0 else 4)
+    prev = pamd._lib.tune("spmv_merge", merge)
+    try:
+        A = pamd.drivers.irregular_problem(parts, N, 27, dtype)
+        hs = {p: A.values.local(p).info() for p in parts.part_ids}
+        for p, i in hs.items():
+            h = 128 if p % 2 == 0 else 256
+            assert i["nslices"] == (i["nrows"] + h - 1) // h, (p, i)
+        OA = _oracle(O, N, nparts, dtype)
+        rng = np.random.default_rng(SEED + 31)
+        xs = {p: _rand(rng, A.cols.partition.local(p).num_lids, dtype) for p in parts.part_ids}
+        x = pamd.PVector.from_host(pamd.map_parts(lambda s: xs[s.part], A.cols.partition), A.cols)
+        ox = O.PVector(O.map_parts(lambda s: _ox(O, xs[s.part]), OA.cols.partition), OA.cols)
+        for alpha in (1.0, 0.5):
+            y = pamd.PVector.undef(A.rows, dtype)
+            oy = O.pvector_undef(OA.rows, dtype)
+            pamd.mul_(y, A, x, alpha, 0.0)
+            O.mul_(oy, OA, ox, np.float32(alpha), 0.0)
+            got = y.to_host()
+            for p in parts.part_ids:
+                assert _eq(O, got.local(p), oy.values[p]), f"part {p}, alpha {alpha}: SpMV differs"
+    finally:
+        pamd._lib.tune("spmv_merge", prev)
