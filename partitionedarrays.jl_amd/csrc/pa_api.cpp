@@ -586,7 +586,7 @@ int finalize_pattern(pa_mat* A, int kmax, int64_t noids, bool retry_r2) {
     // parts, C5) streams faster as 128-row slices of 8 B packs, whose delta16
     // rows take the triple SELL (C5 F32 0.0736 -> 0.0683 ms, 345 -> 289 MB);
     // a matrix of pattern slices keeps 256-row slices (FE27 256^3 F32 0.328
-    // -> 0.374 ms with 128: profiles/r05/ac/).  C5's parts hold 6-62 %
+    // -> 0.374 ms with 128: profiles/r05/af/).  C5's parts hold 6-62 %
     // pattern slices, a stencil's parts ~100 %: the cut is 80 %
     int64_t np = 0;
     for (int64_t s = 0; s < ns; ++s) np += kind[s] == 1;
@@ -1366,7 +1366,7 @@ const Knob kKnobs[] = {
      "f32_rows: Float32 SELL rows per lane (matrices built afterwards): 4 = 16 B value packs in 256-row "
      "slices, 2 = 8 B packs in 128-row slices (the Float64 geometry; delta16 rows then take the triple "
      "SELL), 0 = auto (default): 4, rebuilt with 2 when fewer than 80 % of the slices are pattern slices "
-     "(C5 F32 -7 %, FE27 256^3 F32 +14 % with 2, profiles/r05/ac/)"},
+     "(C5 F32 -7 %, FE27 256^3 F32 +14 % with 2, profiles/r05/af/)"},
     {"spmv_side_tail", &Knobs::side_tail, nullptr, 0, 1, 0,
      "spmv_side_tail: per-kind launches without a halo in flight (big single parts): 1 = the side rows (<= 8 "
      "entries) run as the trailing waves of the pattern launch (default: FE27 256^3 -0.4 %, profiles/r05/o/), "

@@ -265,7 +265,7 @@ __device__ __forceinline__ T term(T v, T x, T alpha, bool pf) {
 // same-copy A/B (profiles/r04/i/): C5 F64 0.1240 -> 0.1217 ms (-1.9 %), FE27
 // 256^3 F64 +-0; Float32 (R = 4, 134 -> 155 VGPRs) C5 0.0832 -> 0.0852 ms
 // (+2.4 %): off.
-template <typename T> constexpr bool kIdsAhead = std::is_same<T, double>::value;
+template <typename T> constexpr bool kIdsAhead = std::is_same<T, double>::value || std::is_same<T, float>::value;
 
 // int32-column rows: c < 0 is padding (skipped: never multiplied)
 // TB: the entries past the last full U batch run as one masked batch
@@ -548,7 +548,10 @@ __device__ __forceinline__ void rows_t16_tri(T (&acc)[R], const S16Pack<R>* __re
                                              const Pack<T, R>* __restrict__ vp, int len, const XS& x, T alpha,
                                              bool pf, const int32_t (&rw)[R], int32_t gb) {
   const int ntri = len / 3;
-  constexpr int TB = kTriBatch;
+  // Float32 (2 rows per lane, f32_rows): 8 triples in the same registers
+  // (C5 F32 0.0679 -> 0.0670 ms, four alternating library rounds,
+  // profiles/r05/af/ab_f32_tri_batch8_c5.log)
+  constexpr int TB = sizeof(T) == 4 ? 8 : kTriBatch;
   auto step = [&](const S16Pack<R>* q, const Pack<T, R>* v, auto nb) {
     constexpr int B = decltype(nb)::value;
     T xv[B][3][R];

@@ -371,7 +371,7 @@ def test_float32_rows_per_lane_equal_oracle(be, pamd, O, rows, tri16):
 
 def test_float32_rows_auto_keeps_pattern_matrices(be, pamd):
     """f32_rows auto keeps 4 rows per lane for a matrix of pattern slices
-    (the FE27 stencil: 2 would cost +14 %, profiles/r05/ac/)."""
+    (the FE27 stencil: 2 would cost +14 %, profiles/r05/af/)."""
     parts = be.get_part_ids((1, 1, 1))
     N = (48, 40, 32)
     A = pamd.drivers.stencil_operator(parts, N, 27, np.float32)
