@@ -265,7 +265,11 @@ __device__ __forceinline__ T term(T v, T x, T alpha, bool pf) {
 // same-copy A/B (profiles/r04/i/): C5 F64 0.1240 -> 0.1217 ms (-1.9 %), FE27
 // 256^3 F64 +-0; Float32 (R = 4, 134 -> 155 VGPRs) C5 0.0832 -> 0.0852 ms
 // (+2.4 %): off.
-template <typename T> constexpr bool kIdsAhead = std::is_same<T, double>::value || std::is_same<T, float>::value;
+// Float32 with 2 rows per lane (f32_rows): C5 F32 median 0.0663 -> 0.0656 ms,
+// within the noise (profiles/r05/af/ab_f32_ids_ahead_c5.log); 4 rows per lane
+// keep them off (the register cost above)
+template <typename T, int R>
+constexpr bool kIdsAhead = std::is_same<T, double>::value || (std::is_same<T, float>::value && R == 2);
 
 // int32-column rows: c < 0 is padding (skipped: never multiplied)
 // TB: the entries past the last full U batch run as one masked batch
@@ -953,8 +957,8 @@ __device__ __forceinline__ void spmv_wave(const SpmvArgs<T>& a, const int64_t w)
     int32_t rw[R];  // the rows the codes are relative to
 #pragma unroll
     for (int r = 0; r < R; ++r) rw[r] = (int32_t)row0 + r * kD16RowStride<R>;
-    if (a.flags & SPMV_NT) rows_d16<T, R, ALPHA, true, U, SH, kIdsAhead<T>>(acc, cp, vp, len, xs, a.alpha, pf, tb, rw, gb);
-    else rows_d16<T, R, ALPHA, false, U, SH, kIdsAhead<T>>(acc, cp, vp, len, xs, a.alpha, pf, tb, rw, gb);
+    if (a.flags & SPMV_NT) rows_d16<T, R, ALPHA, true, U, SH, kIdsAhead<T, R>>(acc, cp, vp, len, xs, a.alpha, pf, tb, rw, gb);
+    else rows_d16<T, R, ALPHA, false, U, SH, kIdsAhead<T, R>>(acc, cp, vp, len, xs, a.alpha, pf, tb, rw, gb);
   } else if constexpr (PK == 4) {
     // triple SELL (rows through the row map, interleaved): tri slices carry
     // one code per triple, the others one per entry (rows_d16)
@@ -967,13 +971,13 @@ __device__ __forceinline__ void spmv_wave(const SpmvArgs<T>& a, const int64_t w)
       if (a.flags & SPMV_NT) rows_t16_tri<T, R, ALPHA, true>(acc, cp, vp, len, xs, a.alpha, pf, rw, gb);
       else rows_t16_tri<T, R, ALPHA, false>(acc, cp, vp, len, xs, a.alpha, pf, rw, gb);
     } else {
-      if (a.flags & SPMV_NT) rows_d16<T, R, ALPHA, true, U, SH, kIdsAhead<T>>(acc, cp, vp, len, xs, a.alpha, pf, tb, rw, gb);
-      else rows_d16<T, R, ALPHA, false, U, SH, kIdsAhead<T>>(acc, cp, vp, len, xs, a.alpha, pf, tb, rw, gb);
+      if (a.flags & SPMV_NT) rows_d16<T, R, ALPHA, true, U, SH, kIdsAhead<T, R>>(acc, cp, vp, len, xs, a.alpha, pf, tb, rw, gb);
+      else rows_d16<T, R, ALPHA, false, U, SH, kIdsAhead<T, R>>(acc, cp, vp, len, xs, a.alpha, pf, tb, rw, gb);
     }
   } else {
     const IPack<R>* __restrict__ cp = reinterpret_cast<const IPack<R>*>(a.col + off) + lane;
-    if (a.flags & SPMV_NT) rows_int32<T, R, ALPHA, true, U, SH, kIdsAhead<T>>(acc, cp, vp, len, xs, a.alpha, pf, tb);
-    else rows_int32<T, R, ALPHA, false, U, SH, kIdsAhead<T>>(acc, cp, vp, len, xs, a.alpha, pf, tb);
+    if (a.flags & SPMV_NT) rows_int32<T, R, ALPHA, true, U, SH, kIdsAhead<T, R>>(acc, cp, vp, len, xs, a.alpha, pf, tb);
+    else rows_int32<T, R, ALPHA, false, U, SH, kIdsAhead<T, R>>(acc, cp, vp, len, xs, a.alpha, pf, tb);
   }
 
   // XV: u_new (and the deferred x update) of the main structure's rows
