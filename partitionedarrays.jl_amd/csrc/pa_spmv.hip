@@ -554,7 +554,9 @@ __device__ __forceinline__ void rows_t16_tri(T (&acc)[R], const S16Pack<R>* __re
   const int ntri = len / 3;
   // Float32 (2 rows per lane, f32_rows): 8 triples in the same registers
   // (C5 F32 0.0679 -> 0.0670 ms, four alternating library rounds,
-  // profiles/r05/af/ab_f32_tri_batch8_c5.log)
+  // profiles/r05/af/ab_f32_tri_batch8_c5.log; the merged kernel then has 134
+  // VGPRs, 3 waves per SIMD; 6 triples fit 4 waves at 104 VGPRs but run
+  // 0.0679 -> 0.0682 ms, six alternating rounds, ab_f32_tri_batch6_c5.log)
   constexpr int TB = sizeof(T) == 4 ? 8 : kTriBatch;
   auto step = [&](const S16Pack<R>* q, const Pack<T, R>* v, auto nb) {
     constexpr int B = decltype(nb)::value;
