@@ -556,7 +556,9 @@ __device__ __forceinline__ void rows_t16_tri(T (&acc)[R], const S16Pack<R>* __re
   // (C5 F32 0.0679 -> 0.0670 ms, four alternating library rounds,
   // profiles/r05/af/ab_f32_tri_batch8_c5.log; the merged kernel then has 134
   // VGPRs, 3 waves per SIMD; 6 triples fit 4 waves at 104 VGPRs but run
-  // 0.0679 -> 0.0682 ms, six alternating rounds, ab_f32_tri_batch6_c5.log)
+  // 0.0679 -> 0.0682 ms, six alternating rounds, ab_f32_tri_batch6_c5.log).
+  // 8 B elements keep 4: 6 costs C5 F64 0.1056 -> 0.1094 ms, ComplexF32
+  // 0.1083 -> 0.1149 (ab_f64_c64_tri_batch6_c5.log)
   constexpr int TB = sizeof(T) == 4 ? 8 : kTriBatch;
   auto step = [&](const S16Pack<R>* q, const Pack<T, R>* v, auto nb) {
     constexpr int B = decltype(nb)::value;
