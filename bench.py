@@ -480,7 +480,7 @@ def cg_mode(args, pamd, backend, parts, A, ngpu, use_dist, sync):
             el3, hist3 = timed(kw, 3 * args.cg)
             steady[name] = 1e3 * (el3 - el) / max(1, len(hist3) - len(hist))
         for c in ctxs:
-            c.tune("cg_fuse", -1)
+            c.tune("cg_fuse", None)
     best = min(steady, key=steady.get)
     p0 = parts.part_ids[0]
     # the auto mode (cg_fuse 2, the process default): one timed batch of each
@@ -767,7 +767,7 @@ def main():
         inf, nh, ns_, nr_ = infos[p]
         bytes_int32 += format_bytes(dict(inf, **A.values.local(p).traffic()), nh, ns_, nr_, S)
     for c in ctxs:
-        c.tune("spmv_format", -1)
+        c.tune("spmv_format", None)
     # the probe reads as many bytes per launch as the timed loop cycles
     # through (ncopies operator copies when one would fit the 256 MB
     # Infinity Cache), so that neither side is served from it

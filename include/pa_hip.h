@@ -28,9 +28,9 @@
  *    call (the process defaults of pa_tune under the call's context
  *    overrides, pa_ctx_tune) and never written while a call runs, so calls
  *    on different parts from different host threads each run with their own
- *    context's knobs (pa_knob_selftest).  The graph-capture state and the
- *    per-context caches are not synchronised: concurrent calls must not
- *    share a context.  pa_last_error is per thread.
+ *    context's knobs (pa_knob_selftest).  The per-context caches are not
+ *    synchronised: concurrent calls must not share a context.
+ *    pa_last_error is per thread.
  */
 #ifndef PA_HIP_H
 #define PA_HIP_H
@@ -49,7 +49,6 @@ typedef struct pa_index pa_index;
 typedef struct pa_xchg pa_xchg;
 typedef struct pa_vec pa_vec;
 typedef struct pa_mat pa_mat;
-typedef struct pa_graph pa_graph;
 typedef struct pa_coo pa_coo;
 
 /* ---- errors / library info ------------------------------------------- */
@@ -104,8 +103,8 @@ int pa_device_count(int* count);
  * "halo_barrier" 1: such a mul! (local neighbours) waits for one pack
  *               barrier per call and alternates two send buffers (default),
  *               0: per-neighbour event waits before every pack and pull;
- * "spmv_tri16"  the triple SELL for delta16 slices (see below): 1 for 8 and
- *               16 B elements (default), 2 every type, 0 never;
+ * "spmv_tri16"  the triple SELL for delta16 slices (see below): 1 for
+ *               slices of 1-2 rows per lane (default), 0 never;
  * "spmv_tri_order" 1: its other rows first (default), 0: triple rows first;
  * "spmv_xcd_chunk" -1 (default, auto): one-launch-per-kind calls run their
  *               workgroups in runs of (pattern reach / 8) blocks per XCD,
@@ -117,15 +116,14 @@ int pa_device_count(int* count);
  *               slices: the Float64 geometry, so delta16 rows take the
  *               triple SELL), 0 (default, auto): 4, rebuilt with 2 when
  *               fewer than 80 % of the slices are pattern slices;
- * "spmv_diag_rows", "spmv_side_fork" 1: diagonal-only rows inside their
- *               pattern slice / side rows on the comm stream (A/B levers,
- *               default 0);
  * "fault_inject" tests only: threaded issue jobs add an invalid launch. */
 int pa_tune(const char* key, int value, int* previous);
 /* The same knobs for one context: calls led by parts of `c` (their first
  * part's context) run with this value instead of the process default, for
- * the duration of the call; value -1 drops the override.  *previous gets
- * the context's former override (-1: none).                             */
+ * the duration of the call; value PA_TUNE_DROP drops the override (a value
+ * outside every knob's range: -1 is a valid value, spmv_xcd_chunk's auto).
+ * *previous gets the context's former override (PA_TUNE_DROP: none).     */
+#define PA_TUNE_DROP (-2147483647 - 1)
 int pa_ctx_tune(pa_ctx* c, const char* key, int value, int* previous);
 /* Test support (no device needed): `nthreads` host threads resolve calls'
  * knobs with different context overrides, on their own threads and on the
@@ -377,18 +375,14 @@ int pa_mat_format_info(const pa_mat* A, int64_t* pattern_slices,
  * signed 15-bit delta, a ghost column as the slice's smallest ghost column
  * + 15 bits — stream 2 B of column id per slot instead of 4.              */
 int pa_mat_delta16_info(const pa_mat* A, int64_t* delta16_slices);
-/* The triple SELL (pa_tune "spmv_tri16": 1 = Float64 / ComplexF32 /
- * ComplexF64, the default; 2 = every element type): the delta16 slices'
+/* The triple SELL (pa_tune "spmv_tri16" 1, the default: Float64,
+ * ComplexF32, ComplexF64 and Float32 with 2 rows per lane): the delta16 slices'
  * rows re-sliced — rows whose columns are consecutive triples (c, c+1, c+2)
  * first — so that most slices keep one 16-bit code per triple and read a
  * triple's x as one run.  Its slices and rows, and how many of them are
  * triple slices (tri_slices, their rows tri_rows).                       */
 int pa_mat_triple_info(const pa_mat* A, int64_t* t_slices, int64_t* t_rows, int64_t* tri_slices,
                        int64_t* tri_rows);
-/* Rows of pattern slices whose only entry is their diagonal (Dirichlet
- * rows; pa_tune "spmv_diag_rows", default on): computed inside their slice
- * from its entry 0 instead of as side rows.                              */
-int pa_mat_diag_rows(const pa_mat* A, int64_t* diag_rows);
 
 /* device addresses of the matrix's main arrays, for placement diagnostics:
  * out[0..7] = values, int32 columns, slice offsets, slice lengths (pattern),
@@ -420,19 +414,6 @@ int pa_spmv_all(int n, pa_mat* const A[], pa_vec* const y[],
                 const pa_index* const y_idx[],
                 pa_vec* const x[], const pa_index* const x_idx[],
                 pa_xchg* const xg[], const void* alpha, const void* beta);
-
-/* The same mul! captured once as a HIP graph (every part of the call on one
- * device, halo neighbours in this process) and replayed with one launch:
- * for many small parts in one process, where host launch cost dominates.
- * Replays use the handles and scalars given at capture; a replay is ordered
- * after work already queued on the parts' streams and before later work.  */
-int pa_spmv_graph_create(int n, pa_mat* const A[], pa_vec* const y[],
-                         const pa_index* const y_idx[],
-                         pa_vec* const x[], const pa_index* const x_idx[],
-                         pa_xchg* const xg[], const void* alpha,
-                         const void* beta, pa_graph** out);
-int pa_graph_launch(pa_graph* g);
-int pa_graph_destroy(pa_graph* g);
 
 /* CG fusions (the caller of the hot path, IterativeSolvers.cg! at
  * test_fdm.jl:115 / test_fem_sa.jl:135):
@@ -487,6 +468,13 @@ int pa_cg_solve_all(int n, pa_mat* const A[], pa_vec* const x[],
  * matrix remembers (-1: none yet).                                        */
 typedef int (*pa_allreduce_max_fn)(float* v, int n, void* user);
 int pa_cg_variant_agree(const float local_ms[2], pa_allreduce_max_fn fn, void* user, int* choice);
+/* Whether the fused u update may run at all: only if every rank's part can
+ * (no long rows, no triple SELL: their kernels gather x directly), or the
+ * ranks would run different variants, whose halos carry different vectors
+ * (ADVICE r05).  pa_cg_solve_all max-reduces "cannot fuse" over the ranks
+ * (RCCL); this runs the same decision with fn as the all-reduce.  *agreed
+ * = 1 when every rank's local_can_fuse is 1.                             */
+int pa_cg_fuse_agree(int local_can_fuse, pa_allreduce_max_fn fn, void* user, int* agreed);
 int pa_mat_cg_choice(const pa_mat* A, int* choice);
 
 /* exchange!(combine, values, exchanger) (Interfaces.jl:846-889) for the n

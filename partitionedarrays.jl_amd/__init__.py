@@ -18,7 +18,7 @@ from .prange import (Exchanger, IndexSet, PRange, add_gids, add_gids_, discover_
                      lids_are_equal, oids_are_equal, prange_cartesian, prange_from_partition,
                      prange_linear, prange_noids, to_lids_)
 from .device import DeviceMatrix, HIPBackend, HIPDistributedBackend, device_index  # noqa: F401
-from .pvector import (COO, CSC, CSR, PSparseMatrix, PVector, SpMVGraph, assemble_, axmy_, axpy_, cg_, cg_update_,  # noqa: F401
+from .pvector import (COO, CSC, CSR, PSparseMatrix, PVector, assemble_, axmy_, axpy_, cg_, cg_update_,  # noqa: F401
                       compresscoo, copyto_, csr_init, sparsecsr, fillstored_, dot, exchange_, matvec, mul_, mul_dot_, norm, psum, rmul_,
                       sub_, xpby_)
 from .ptimers import PTimer  # noqa: F401

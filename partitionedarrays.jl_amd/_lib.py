@@ -17,6 +17,7 @@ LIB_PATH = os.environ.get("PA_HIP_LIB") or os.path.join(_HERE, "libpa_hip.so")
 
 PA_F32, PA_F64, PA_C64, PA_C128 = 0, 1, 2, 3
 PA_REPLACE, PA_ADD = 0, 1
+TUNE_DROP = -(2 ** 31)  # pa_ctx_tune: drop a context's override (PA_TUNE_DROP)
 PA_BCAST_F64, PA_BCAST_C128 = 8, 16  # pa_vec_axpby scalar kinds (Float64 / ComplexF64 scalars)
 
 DTYPES = {
@@ -40,6 +41,7 @@ _SIGS = {
     "pa_ctx_tune": [_p, C.c_char_p, C.c_int, C.POINTER(C.c_int)],
     "pa_knob_selftest": [C.c_int, C.c_int, C.POINTER(C.c_int)],
     "pa_cg_variant_agree": [C.POINTER(C.c_float), _p, _p, C.POINTER(C.c_int)],
+    "pa_cg_fuse_agree": [C.c_int, _p, _p, C.POINTER(C.c_int)],
     "pa_mat_cg_choice": [_p, C.POINTER(C.c_int)],
     "pa_hbm_probe": [C.c_int, C.c_int64, C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_double)],
     "pa_ctx_create": [C.c_int, C.c_int, C.c_int, C.POINTER(_p)],
@@ -89,14 +91,9 @@ _SIGS = {
     "pa_mat_format_info": [_p, _i64p, _i64p, _i64p, _i64p],
     "pa_mat_delta16_info": [_p, _i64p],
     "pa_mat_triple_info": [_p, _i64p, _i64p, _i64p, _i64p],
-    "pa_mat_diag_rows": [_p, _i64p],
     "pa_mat_long_rows": [_p, _i64p, _i64p],
     "pa_mat_stencil": [_p, C.c_int, C.c_int, _i64p, _i64p, _i64p, C.c_int64, _i32p, C.POINTER(C.c_double), C.c_int, C.POINTER(_p)],
     "pa_spmv_all": [C.c_int, C.POINTER(_p), C.POINTER(_p), C.POINTER(_p), C.POINTER(_p), C.POINTER(_p), C.POINTER(_p), _p, _p],
-    "pa_spmv_graph_create": [C.c_int, C.POINTER(_p), C.POINTER(_p), C.POINTER(_p), C.POINTER(_p), C.POINTER(_p),
-                             C.POINTER(_p), _p, _p, C.POINTER(_p)],
-    "pa_graph_launch": [_p],
-    "pa_graph_destroy": [_p],
     "pa_spmv_dot_all": [C.c_int, C.POINTER(_p), C.POINTER(_p), C.POINTER(_p), C.POINTER(_p), C.POINTER(_p), C.POINTER(_p), _p, _p, _p],
     "pa_cg_update_all": [C.c_int, C.POINTER(_p), C.POINTER(_p), C.POINTER(_p), C.POINTER(_p), C.POINTER(_p), _p, C.POINTER(C.c_double)],
     "pa_cg_solve_all": [C.c_int, C.POINTER(_p), C.POINTER(_p), C.POINTER(_p), C.POINTER(_p), C.POINTER(_p),
@@ -166,22 +163,11 @@ def device_count() -> int:
     return n.value
 
 
-tune_generation = 0  # bumped by every tune(): cached mul! graphs captured under older knobs are stale
-
-
 def tune(key: str, value: int) -> int:
     """pa_tune: set a process-wide kernel knob, return the previous value."""
-    global tune_generation
     prev = C.c_int(0)
     call("pa_tune", key.encode(), int(value), C.byref(prev))
-    tune_generation += 1
     return prev.value
-
-
-def tune_generation_bump():
-    """a per-context knob changed (PartContext.tune): cached graphs are stale"""
-    global tune_generation
-    tune_generation += 1
 
 
 def knob_selftest(nthreads: int = 4, iters: int = 2000) -> int:
@@ -216,6 +202,26 @@ def cg_variant_agree(local_ms, allreduce_max=None) -> int:
     ch = C.c_int(-3)
     call("pa_cg_variant_agree", ms, C.cast(cb, C.c_void_p) if cb else None, None, C.byref(ch))
     return ch.value
+
+
+def cg_fuse_agree(local_can_fuse: bool, allreduce_max=None) -> bool:
+    """pa_cg_fuse_agree: whether the device CG may run the fused u update,
+    decided over the ranks (every rank's part must allow it: no long rows,
+    no triple SELL); `allreduce_max` as in cg_variant_agree."""
+    cb = None
+    if allreduce_max is not None:
+        def _cb(v, n, _user):
+            try:
+                out = allreduce_max([v[i] for i in range(n)])
+                for i in range(n):
+                    v[i] = float(out[i])
+                return 0
+            except Exception:  # reported as a PAError by the library
+                return 1
+        cb = ALLREDUCE_MAX_FN(_cb)
+    ok = C.c_int(-1)
+    call("pa_cg_fuse_agree", int(bool(local_can_fuse)), C.cast(cb, C.c_void_p) if cb else None, None, C.byref(ok))
+    return ok.value == 1
 
 
 def hbm_probe(device: int = 0, nbytes: int = 2 << 30, reps: int = 10):

@@ -38,7 +38,7 @@ void launch_delta16(pa_mat* A, int64_t noids, const int32_t* kind, int32_t* ok, 
 void launch_pattern_detect(pa_mat* A, int64_t noids, int min_pct, int32_t* kind, int32_t* plen, int32_t* pat,
                            uint64_t* mask, int32_t* pghost, int32_t* nirreg, hipStream_t st);
 void launch_side_len(pa_mat* A, int64_t n, const int32_t* rows, int32_t* len, int64_t noids,
-                     int32_t* sghost, hipStream_t st, int32_t* diag = nullptr);
+                     int32_t* sghost, hipStream_t st);
 void launch_side_fill(pa_mat* A, const int32_t* rows, const int32_t* len, hipStream_t st);
 void launch_fold(int cplx, int nb, const void* in, void* scratch, void* out, unsigned* ticket, hipStream_t st);
 void launch_fold_cg_alpha(int dtype, int nb, const void* in, void* scratch, void* out, unsigned* ticket,
@@ -89,8 +89,8 @@ void launch_gather_scatter(int P, const void* const* srcs, int accsz, int nd, vo
 const Knobs kDefaults = {
     /*spmv_flags*/ 93, /*long_exact*/ 1, /*halo_pull*/ 1, /*spmv_delta16*/ 1, /*spmv_merge*/ 1,
     /*spmv_merge_max*/ 65536, /*cg_fuse*/ 2, /*halo_direct*/ 1, /*halo_transport*/ 0, /*spmv_group*/ 1,
-    /*spmv_format*/ 1, /*pattern_min_pct*/ 0, /*issue_threads*/ 1, /*fault_inject*/ 0, /*spmv_xcd_chunk*/ -1, /*spmv_tri16*/ 1, /*spmv_diag_rows*/ 0,
-    /*halo_barrier*/ 1, /*side_fork*/ 0, /*tri_order*/ 1, /*side_tail*/ 1, /*f32_rows*/ 0};
+    /*spmv_format*/ 1, /*pattern_min_pct*/ 0, /*issue_threads*/ 1, /*fault_inject*/ 0, /*spmv_xcd_chunk*/ -1, /*spmv_tri16*/ 1,
+    /*halo_barrier*/ 1, /*tri_order*/ 1, /*side_tail*/ 1, /*f32_rows*/ 0};
 // COO → CSC → SELL on the device (pa_coo.hip)
 int coo_compress(int dtype, int index_bytes, int64_t m, int64_t ncols, int64_t n, const void* dI, const void* dJ,
                  const void* dV, int csr, int64_t* nu_out, int32_t** crow, int32_t** ccol, void** cval,
@@ -126,9 +126,8 @@ void launch_pull(int dtype, int64_t n, const int32_t* lids, const pa_combine_pla
 void launch_fill(int dtype, int64_t n, int64_t base, const int32_t* map, void* v, const void* s,
                  hipStream_t st);
 int launch_spmv_merged(int n, const int* which, const SpmvPart* parts, bool has_alpha, int bmode,
-                       const void* alpha, const void* beta, pa_ctx* owner, std::vector<void*>* pinned,
+                       const void* alpha, const void* beta, pa_ctx* owner,
                        hipStream_t st);
-extern std::vector<std::pair<void*, std::vector<char>>> g_capture_uploads;
 void launch_spmv_group(int which, int np, const SpmvPart* parts, bool has_alpha, int bmode, const void* alpha,
                        const void* beta, hipStream_t st);
 void launch_pack_group(int dtype, const PackGroup& g, hipStream_t st);
@@ -620,12 +619,11 @@ int finalize_pattern(pa_mat* A, int kmax, int64_t noids, bool retry_r2) {
       if (A->nz_map && A->R == 4 && remap_nz_interleaved(A, kind, st)) return -1;
       // the device keeps kind 3 (the int32 kernel of spmv_format 0 reads
       // the interleaved layout from it); the host marks moved slices 5
-      // spmv_tri16 1 (auto): Float64 / ComplexF32 / ComplexF64 (R <= 2);
-      // Float32's interleaved delta16 slices already gather compactly and
-      // its irregular rows, re-sliced together, gather from wide x spans
-      // (C5 F32 +3 %, F64 -10 %, profiles/r05/d/)
-      const int tri = knobs().spmv_tri16;
-      if ((tri == 2 || (tri == 1 && A->R <= 2)) && build_triple_sell(A, kind, noids)) return -1;
+      // spmv_tri16 1: slices of R <= 2 rows per lane (Float64, complex,
+      // Float32 with 2 rows per lane); Float32's 4-row interleaved delta16
+      // slices already gather compactly (the triple SELL with R = 4: C5 F32
+      // +3 %, F64 -10 %, profiles/r05/d/; removed r06)
+      if (knobs().spmv_tri16 && A->R <= 2 && build_triple_sell(A, kind, noids)) return -1;
     }
   }
   std::vector<int32_t> pint, pbnd, xint, xbnd, dint, dbnd, side;
@@ -666,51 +664,17 @@ int finalize_pattern(pa_mat* A, int kmax, int64_t noids, bool retry_r2) {
     // the side rows (oids = structure rows) through d_s_rowmap
     if (dev_upload(&A->d_s_rowmap, side)) return -1;
     int32_t* srow = A->d_s_rowmap;
-    int32_t *d_dummy = nullptr, *d_diag = nullptr;
+    int32_t* d_dummy = nullptr;
     A->s_nslices = (A->s_nrows + A->H - 1) / A->H;
     HIPC(hipMalloc((void**)&A->d_s_rowlen, A->s_nrows * 4));
     HIPC(hipMalloc((void**)&d_dummy, A->s_nslices * 4));
-    HIPC(hipMalloc((void**)&d_diag, A->s_nrows * 4));
     HIPC(hipMemsetAsync(d_dummy, 0, A->s_nslices * 4, st));
-    launch_side_len(A, A->s_nrows, srow, A->d_s_rowlen, noids, d_dummy, st, d_diag);
+    launch_side_len(A, A->s_nrows, srow, A->d_s_rowlen, noids, d_dummy, st);
     HIPC(hipGetLastError());
-    std::vector<int32_t> dg(A->s_nrows);
     rl.resize(A->s_nrows);
     HIPC(hipMemcpyAsync(rl.data(), A->d_s_rowlen, A->s_nrows * 4, hipMemcpyDeviceToHost, st));
-    HIPC(hipMemcpyAsync(dg.data(), d_diag, A->s_nrows * 4, hipMemcpyDeviceToHost, st));
     HIPC(hipStreamSynchronize(st));
     dev_free(d_dummy);
-    dev_free(d_diag);
-    // diagonal-only rows (pa_tune "spmv_diag_rows"): computed in their
-    // pattern slice from entry 0 (the dmask bit), not as side rows
-    if (knobs().spmv_diag_rows) {
-      std::vector<uint64_t> dmask(ns * W, 0);
-      std::vector<int32_t> keep, keep_len;
-      for (int64_t i = 0; i < A->s_nrows; ++i) {
-        if (dg[i]) {
-          const int64_t row = side[i], s = row / A->H, w = row - s * A->H;
-          dmask[s * W + w / 64] |= 1ull << (w & 63);
-          ++A->n_diag_rows;
-        } else {
-          keep.push_back(side[i]);
-          keep_len.push_back(rl[i]);
-        }
-      }
-      if (A->n_diag_rows > 0) {
-        if (dev_upload(&A->d_dmask, dmask)) return -1;
-        side = std::move(keep);
-        rl = std::move(keep_len);
-        A->s_nrows = (int64_t)side.size();
-        dev_free(A->d_s_rowmap);
-        dev_free(A->d_s_rowlen);
-        A->d_s_rowmap = A->d_s_rowlen = nullptr;
-        A->s_nslices = 0;
-        if (A->s_nrows > 0) {
-          if (dev_upload(&A->d_s_rowmap, side) || dev_upload(&A->d_s_rowlen, rl)) return -1;
-          A->s_nslices = (A->s_nrows + A->H - 1) / A->H;
-        }
-      }
-    }
   }
   if (A->s_nrows > 0) {
     int32_t* srow = A->d_s_rowmap;
@@ -763,38 +727,7 @@ LocalSet local_set(int n, H* const* hs) {
   return L;
 }
 
-// During graph capture every part's work goes to one stream (a linear chain
-// of kernels; multi-stream captures with cross-stream events are not used).
-hipStream_t g_capture_stream = nullptr;
-std::vector<void*>* g_capture_tables = nullptr;  // device tables the graph being captured owns
-
-// During a graph capture: a graph-owned device copy of a table the captured
-// kernels read (allocated now, uploaded after the capture ends, freed by
-// pa_graph_destroy).  The eager path's caches (the x-pointer arrays of the
-// direct pull, the pull/direct tables) may be evicted or rebuilt while the
-// graph still replays.  Outside a capture: d itself.  Null on failure.
-bool g_graph_owned_failed = false;  // set when a graph-owned copy could not be allocated
-template <typename T>
-const T* graph_owned(const T* d, const std::vector<T>& h) {
-  if (!g_capture_tables || h.empty()) return d;
-  void* p = nullptr;
-  // PA_TEST_FAIL_GRAPH_ALLOC (tests only): the allocation fails, as on an
-  // out-of-memory device
-  const bool test_fail = std::getenv("PA_TEST_FAIL_GRAPH_ALLOC") != nullptr;
-  if (test_fail || hipMalloc(&p, h.size() * sizeof(T)) != hipSuccess) {
-    (void)hipGetLastError();
-    g_graph_owned_failed = true;
-    return nullptr;
-  }
-  g_capture_tables->push_back(p);
-  const char* b = reinterpret_cast<const char*>(h.data());
-  g_capture_uploads.push_back({p, std::vector<char>(b, b + h.size() * sizeof(T))});
-  return (const T*)p;
-}
 uint64_t g_xchg_next_id = 1;
-inline hipStream_t SM(const pa_ctx* c) { return g_capture_stream ? g_capture_stream : c->s_main; }
-inline hipStream_t SC(const pa_ctx* c) { return g_capture_stream ? g_capture_stream : c->s_comm; }
-#define EV(expr) do { if (!g_capture_stream) HIPC(expr); } while (0)
 
 // Pull table of receiver i for direction dir (see pa_pull): built once per
 // set of local senders; ok = false when a sender's device is not reachable
@@ -1020,11 +953,11 @@ int transport_wait(int i, pa_xchg* const xg[], const TransportPlan& T) {
   pa_xchg* X = xg[i];
   pa_ctx* c = X->ctx;
   HIPC(hipSetDevice(c->device));
-  EV(hipStreamWaitEvent(SC(c), c->ev_packed, 0));
+  HIPC(hipStreamWaitEvent(c->s_comm, c->ev_packed, 0));
   const auto& prcv = T.dir == 0 ? X->parts_rcv : X->parts_snd;
   for (int32_t q : prcv) {
     const int j = T.L.find(q);
-    if (j >= 0 && xg[j]->ctx->ev_packed != c->ev_packed) EV(hipStreamWaitEvent(SC(c), xg[j]->ctx->ev_packed, 0));
+    if (j >= 0 && xg[j]->ctx->ev_packed != c->ev_packed) HIPC(hipStreamWaitEvent(c->s_comm, xg[j]->ctx->ev_packed, 0));
   }
   return 0;
 }
@@ -1038,19 +971,17 @@ int transport_local(int i, pa_xchg* const xg[], pa_vec* const v[], const Transpo
   HIPC(hipSetDevice(c->device));
   if (T.pull) {
     const pa_pull& P = T.alt ? X->pull_alt : X->pull[dir];
-    const int32_t* bid = graph_owned<int32_t>(P.d_bid, P.h_bid);
-    const int64_t* elem = graph_owned<int64_t>(P.d_elem, P.h_elem);
-    void* const* bases = graph_owned<void*>(P.d_bases, P.h_bases);
-    CHECK_ARG(!(g_capture_tables && g_graph_owned_failed), "graph capture: table allocation failed");
-    // the pull's completion is ev_recvd (recorded with the launch; not
-    // during a graph capture)
-    hipEvent_t ev = g_capture_stream ? nullptr : c->ev_recvd;
+    const int32_t* bid = P.d_bid;
+    const int64_t* elem = P.d_elem;
+    void* const* bases = P.d_bases;
+    // the pull's completion is ev_recvd (recorded with the launch)
+    hipEvent_t ev = c->ev_recvd;
     if (dir == 0)
       launch_pull(T.dtype, X->n_rcv_data, X->d_lids_rcv, X->plan_fwd, T.op, bid, elem, (const void* const*)bases,
-                  v[i]->d, SC(c), ev);
+                  v[i]->d, c->s_comm, ev);
     else
       launch_pull(T.dtype, X->n_snd_data, X->d_lids_snd, X->plan_rev, T.op, bid, elem, (const void* const*)bases,
-                  v[i]->d, SC(c), ev);
+                  v[i]->d, c->s_comm, ev);
     return 0;
   } else {
     // staging copies: receiver r, segment k from sender q (local), which
@@ -1072,10 +1003,10 @@ int transport_local(int i, pa_xchg* const xg[], pa_vec* const v[], const Transpo
       const int64_t cnt = orcv[k + 1] - orcv[k];
       CHECK_ARG(cnt == qo[m + 1] - qo[m], "exchanger mismatch: segment lengths differ (SequentialBackend.jl:187)");
       if (cnt > 0)
-        HIPC(hipMemcpyAsync(brcv + orcv[k] * S, bq + qo[m] * S, (size_t)cnt * S, hipMemcpyDefault, SC(c)));
+        HIPC(hipMemcpyAsync(brcv + orcv[k] * S, bq + qo[m] * S, (size_t)cnt * S, hipMemcpyDefault, c->s_comm));
     }
   }
-  EV(hipEventRecord(c->ev_recvd, SC(c)));
+  HIPC(hipEventRecord(c->ev_recvd, c->s_comm));
   return 0;
 }
 
@@ -1101,12 +1032,12 @@ int transport_remote(int n, pa_xchg* const xg[], const TransportPlan& T) {
       const size_t cnt = (size_t)(osnd[k + 1] - osnd[k]) * S;
       // an empty segment: the peer's matching one is empty too (SequentialBackend.jl:187)
       if (T.L.find(psnd[k]) >= 0 || cnt == 0) continue;
-      ops.push_back({c->part, psnd[k], true, bsnd + osnd[k] * S, cnt, c->peer_rank(psnd[k]), comm, SC(c)});
+      ops.push_back({c->part, psnd[k], true, bsnd + osnd[k] * S, cnt, c->peer_rank(psnd[k]), comm, c->s_comm});
     }
     for (size_t k = 0; k < prcv.size(); ++k) {
       const size_t cnt = (size_t)(orcv[k + 1] - orcv[k]) * S;
       if (T.L.find(prcv[k]) >= 0 || cnt == 0) continue;
-      ops.push_back({prcv[k], c->part, false, brcv + orcv[k] * S, cnt, c->peer_rank(prcv[k]), comm, SC(c)});
+      ops.push_back({prcv[k], c->part, false, brcv + orcv[k] * S, cnt, c->peer_rank(prcv[k]), comm, c->s_comm});
     }
   }
   for (int i = 0; i < n; ++i) {
@@ -1151,13 +1082,10 @@ int check_lids(const pa_xchg* X, const pa_vec* v) {
 // Before packing into the send buffers again, wait for the copies that read
 // them in the previous exchange (local receivers record ev_recvd after their
 // copies; for RCCL sends the part's own ev_recvd covers them).
-bool g_capturing = false;  // inside pa_spmv_graph_create: one replay never overlaps the next
-
 // before part i packs into its send buffer: the previous exchange's reads
 // of it (its own unpack and its receivers' pulls) are done
 int pre_pack_wait_part(int i, pa_xchg* const xg[], const LocalSet& L) {
   xg[i]->fast_key = 0;  // the next barrier call of these exchangers waits too (spmv_impl)
-  if (g_capturing) return 0;
   pa_ctx* c = xg[i]->ctx;
   HIPC(hipSetDevice(c->device));
   HIPC(hipStreamWaitEvent(c->s_main, c->ev_recvd, 0));
@@ -1175,7 +1103,6 @@ int pre_pack_wait_part(int i, pa_xchg* const xg[], const LocalSet& L) {
 }
 
 int pre_pack_wait(int n, pa_xchg* const xg[]) {
-  if (g_capturing) return 0;
   LocalSet L = local_set(n, xg);
   for (int i = 0; i < n; ++i)
     if (pre_pack_wait_part(i, xg, L)) return -1;
@@ -1358,10 +1285,10 @@ const Knob kKnobs[] = {
      "issue_threads: a call over parts with their own stream pairs is issued from host threads, one part "
      "per thread: 1 = when the parts span several devices (default), 2 = always, 0 = never (the calling "
      "thread, one part after the other)"},
-    {"spmv_tri16", &Knobs::spmv_tri16, nullptr, 0, 2, 0,
+    {"spmv_tri16", &Knobs::spmv_tri16, nullptr, 0, 1, 0,
      "spmv_tri16: the delta16 slices' rows re-sliced into the triple SELL (rows of consecutive column triples "
-     "keep one 16-bit code per triple; matrices built afterwards): 1 = for 8 and 16 B elements (Float64, "
-     "ComplexF32, ComplexF64; default), 2 = every element type, 0 = never"},
+     "keep one 16-bit code per triple; matrices built afterwards): 1 = slices of 1-2 rows per lane (Float64, "
+     "ComplexF32, ComplexF64, Float32 with f32_rows 2; default), 0 = never"},
     {"f32_rows", &Knobs::f32_rows, nullptr, 0, 4, 6,
      "f32_rows: Float32 SELL rows per lane (matrices built afterwards): 4 = 16 B value packs in 256-row "
      "slices, 2 = 8 B packs in 128-row slices (the Float64 geometry; delta16 rows then take the triple "
@@ -1375,18 +1302,10 @@ const Knob kKnobs[] = {
      "spmv_tri_order: the triple SELL's row order (matrices built afterwards): 1 = the other rows first "
      "(their slower waves start early, the launch ends on uniform triple slices; default: C5 F64 -1 %, "
      "Float32 triples -4..-7 %, profiles/r05/n/), 0 = rows of column triples first"},
-    {"spmv_diag_rows", &Knobs::spmv_diag_rows, nullptr, 0, 1, 0,
-     "spmv_diag_rows: 1 = a pattern slice's rows whose only entry is the diagonal (Dirichlet rows) are "
-     "computed in the slice from entry 0 (matrices built afterwards), 0 = as side rows (default: faster, "
-     "profiles/r05/i/)"},
     {"halo_barrier", &Knobs::halo_barrier, nullptr, 0, 1, 0,
      "halo_barrier: mul! over parts with their own stream pairs and local neighbours (one process driving "
      "several GPUs): 1 = one pack barrier event per call and double-buffered send buffers (default), 0 = "
      "per-neighbour event waits before every pack and every pull"},
-    {"spmv_side_fork", &Knobs::side_fork, nullptr, 0, 1, 0,
-     "spmv_side_fork: per-kind launches without a halo in flight (big single parts): 1 = the side rows run on "
-     "the comm stream beside the pattern slices, 0 = after them on the compute stream (default, "
-     "profiles/r05/k/)"},
     {"spmv_xcd_chunk", &Knobs::spmv_xcd_chunk, nullptr, -1, 64, 0,
      "spmv_xcd_chunk: the SpMV launches' workgroups in runs of C consecutive blocks per XCD (C > 0; the x lines "
      "of neighbouring slices shared in one L2), 0 = the hardware's round robin, -1 = auto (default): per-kind "
@@ -1483,10 +1402,12 @@ int pa_tune(const char* key, int value, int* previous) {
 
 int pa_ctx_tune(pa_ctx* c, const char* key, int value, int* previous) {
   CHECK_ARG(c && key, "null argument");
-  const int i = value == -1 ? knob_find(key) : knob_index(key, value);  // -1: drop the override
+  // PA_TUNE_DROP (outside every knob's range: spmv_xcd_chunk's auto is -1)
+  // drops the override
+  const int i = value == PA_TUNE_DROP ? knob_find(key) : knob_index(key, value);
   if (i < 0) return -1;
-  if (previous) *previous = c->has_over[i] ? (int)c->over[i] : -1;
-  c->has_over[i] = value != -1;
+  if (previous) *previous = c->has_over[i] ? (int)c->over[i] : PA_TUNE_DROP;
+  c->has_over[i] = value != PA_TUNE_DROP;
   c->over[i] = value;
   return 0;
 }
@@ -1659,8 +1580,6 @@ int pa_ctx_destroy(pa_ctx* c) {
   for (auto& e : c->span_ev)
     if (e) (void)hipEventDestroy(e);
   if (c->ev_barrier) (void)hipEventDestroy(c->ev_barrier);
-  for (auto& e : c->ev_side)
-    if (e) (void)hipEventDestroy(e);
   if (c->stream_refs && --c->stream_refs->n == 0) {  // the last context of a shared stream pair
     (void)hipEventDestroy(c->ev_packed);
     (void)hipEventDestroy(c->ev_recvd);
@@ -2960,8 +2879,7 @@ int pa_mat_destroy(pa_mat* A) {
                   (void*)A->d_s_col, A->d_s_val, (void*)A->d_s_rowmap, (void*)A->d_s_rowlen, A->d_dotp,
                   (void*)A->d_long_row, (void*)A->d_long_ptr, (void*)A->d_long_col, (void*)A->d_sflags,
                   (void*)A->d_lmask, (void*)A->d_lchunk_start, (void*)A->d_lrow_chunk, A->d_lpart,
-                  (void*)A->d_col16, (void*)A->d_gbase, (void*)A->d_dint_list, (void*)A->d_dbnd_list,
-                  (void*)A->d_dmask})
+                  (void*)A->d_col16, (void*)A->d_gbase, (void*)A->d_dint_list, (void*)A->d_dbnd_list})
     dev_free(p);
   free_triple_sell(A);
   delete A;
@@ -2981,12 +2899,6 @@ int pa_mat_format_info(const pa_mat* A, int64_t* pattern_slices, int64_t* regula
 int pa_mat_delta16_info(const pa_mat* A, int64_t* delta16_slices) {
   CHECK_ARG(A, "null matrix");
   if (delta16_slices) *delta16_slices = A->nd_int + A->nd_bnd;
-  return 0;
-}
-
-int pa_mat_diag_rows(const pa_mat* A, int64_t* diag_rows) {
-  CHECK_ARG(A && diag_rows, "null argument");
-  *diag_rows = A->n_diag_rows;
   return 0;
 }
 
@@ -3029,7 +2941,6 @@ int pa_mat_traffic(const pa_mat* A, int64_t* value_bytes, int64_t* index_bytes, 
     if (kd == 1) {
       v += (int64_t)A->h_plen[s] * H * S;
       m += W * 8 + 8 + 4 + 4;  // mask, offset, length | pattern id, list entry
-      if (A->d_dmask) m += W * 8;  // diagonal-only rows
     } else if (kd == 3) {
       v += (int64_t)A->h_slen[s] * H * S;
       ix += (int64_t)A->h_slen[s] * H * 2;
@@ -3143,7 +3054,7 @@ static int spmv_grouped(int n, pa_mat* const A[], pa_vec* const y[], const pa_in
                         const CGFuse* fz) {
   pa_ctx* c0 = A[0]->ctx;
   HIPC(hipSetDevice(c0->device));
-  const hipStream_t sm = SM(c0), sc = SC(c0);
+  const hipStream_t sm = c0->s_main, sc = c0->s_comm;
   auto mark = [&](int k) -> int {
     for (int i = 0; i < n; ++i)
       if (tslot[i]) HIPC(hipEventRecord(tslot[i][k], sm));
@@ -3158,12 +3069,6 @@ static int spmv_grouped(int n, pa_mat* const A[], pa_vec* const y[], const pa_in
     // the slices (owned values are only read, ghosts only written)
     void** bases = direct_bases(c0, n, x);
     if (!bases) return -1;
-    if (g_capture_tables) {  // the graph's own copy: the cache may evict this one
-      std::vector<void*> xs(n);
-      for (int i = 0; i < n; ++i) xs[i] = x[i]->d;
-      bases = const_cast<void**>(graph_owned<void*>(bases, xs));
-      CHECK_ARG(!(g_capture_tables && g_graph_owned_failed), "graph capture: table allocation failed");
-    }
     PullGroup qg{};
     for (int i0 = 0; i0 < n; i0 += PA_GROUP_MAX) {
       qg.np = 0;
@@ -3172,9 +3077,8 @@ static int spmv_grouped(int n, pa_mat* const A[], pa_vec* const y[], const pa_in
         const int k = qg.np++;
         qg.n[k] = X->n_rcv_data;
         qg.lids[k] = X->d_lids_rcv;
-        qg.bid[k] = graph_owned<int32_t>(X->direct.d_bid, X->direct.h_bid);
-        qg.elem[k] = graph_owned<int64_t>(X->direct.d_elem, X->direct.h_elem);
-        CHECK_ARG(!(g_capture_tables && g_graph_owned_failed), "graph capture: table allocation failed");
+        qg.bid[k] = X->direct.d_bid;
+        qg.elem[k] = X->direct.d_elem;
         qg.bases[k] = (const void* const*)bases;
         qg.v[k] = x[i]->d;
       }
@@ -3182,7 +3086,7 @@ static int spmv_grouped(int n, pa_mat* const A[], pa_vec* const y[], const pa_in
     }
   } else if (any_x) {
     // the previous exchange's pulls read the send buffers: pack after them
-    if (!g_capturing) HIPC(hipStreamWaitEvent(c0->s_main, c0->ev_recvd, 0));
+    HIPC(hipStreamWaitEvent(c0->s_main, c0->ev_recvd, 0));
     for (int i = 0; i < n; ++i) xg[i]->fast_key = 0;
     PackGroup pg{};
     PullGroup qg{};
@@ -3198,8 +3102,8 @@ static int spmv_grouped(int n, pa_mat* const A[], pa_vec* const y[], const pa_in
       }
       launch_pack_group(dt, pg, sm);
     }
-    EV(hipEventRecord(c0->ev_packed, sm));
-    EV(hipStreamWaitEvent(sc, c0->ev_packed, 0));
+    HIPC(hipEventRecord(c0->ev_packed, sm));
+    HIPC(hipStreamWaitEvent(sc, c0->ev_packed, 0));
     for (int i0 = 0; i0 < n; i0 += PA_GROUP_MAX) {
       qg.np = 0;
       for (int i = i0; i < n && i < i0 + PA_GROUP_MAX; ++i) {
@@ -3208,15 +3112,14 @@ static int spmv_grouped(int n, pa_mat* const A[], pa_vec* const y[], const pa_in
         const int k = qg.np++;
         qg.n[k] = X->n_rcv_data;
         qg.lids[k] = X->d_lids_rcv;
-        qg.bid[k] = graph_owned<int32_t>(P.d_bid, P.h_bid);
-        qg.elem[k] = graph_owned<int64_t>(P.d_elem, P.h_elem);
-        qg.bases[k] = (const void* const*)graph_owned<void*>(P.d_bases, P.h_bases);
-        CHECK_ARG(!(g_capture_tables && g_graph_owned_failed), "graph capture: table allocation failed");
+        qg.bid[k] = P.d_bid;
+        qg.elem[k] = P.d_elem;
+        qg.bases[k] = (const void* const*)P.d_bases;
         qg.v[k] = x[i]->d;
       }
       launch_pull_group(dt, qg, sc);
     }
-    EV(hipEventRecord(c0->ev_recvd, sc));
+    HIPC(hipEventRecord(c0->ev_recvd, sc));
   }
   HIPC(hipGetLastError());
   std::vector<SpmvPart> P0, P1, P4, P5;
@@ -3289,34 +3192,9 @@ static int spmv_grouped(int n, pa_mat* const A[], pa_vec* const y[], const pa_in
         add(0, i, A[i]->np_bnd, A[i]->d_pbnd_list);
       }
     merged = launch_spmv_merged((int)E.size(), W.data(), E.data(), has_alpha, bmode, alpha, beta, c0,
-                                g_capture_tables, sm);
+                                sm);
     if (merged < 0) PA_FAIL("mul!: merged launch table (device allocation or copy) failed");
     if (merged == 0 && !dmark && (mark(1) || mark(2))) return -1;
-  }
-  // per-kind launches with no halo in flight (or the direct pull done): the
-  // side rows (a few short waves: FE27 256³'s 129,032 domain-face rows, 6.8
-  // µs as a launch of their own after the 644 µs pattern kernel,
-  // profiles/r04/am/) can run on the comm stream beside the pattern slices; they
-  // read x and write only their own rows of y; the compute stream joins
-  // before the long rows and the dot fold.  Off by default: the concurrent
-  // side waves slow the pattern kernel more than their own launch costs
-  // (same-box A/B, profiles/r05/k/: 0.6459/0.6467 ms serial vs
-  // 0.6546/0.6544 forked)
-  bool side_forked = false;
-  if (merged && knobs().side_fork && (!any_x || direct) && !g_capture_stream && sm != sc) {
-    std::vector<SpmvPart> P2;
-    for (int i = 0; i < n; ++i)
-      if (knobs().spmv_format == 1 && A[i]->has_pat && A[i]->s_nslices > 0)
-        P2.push_back(part(i, A[i]->s_nslices, nullptr));
-    if (!P2.empty()) {
-      for (auto& e : c0->ev_side)
-        if (!e) HIPC(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-      HIPC(hipEventRecord(c0->ev_side[0], sm));
-      HIPC(hipStreamWaitEvent(sc, c0->ev_side[0], 0));
-      launch_all(2, P2, sc);
-      HIPC(hipEventRecord(c0->ev_side[1], sc));
-      side_forked = true;
-    }
   }
   if (merged) {
   // interior slices (no ghost column): overlap with the pulls on the comm stream
@@ -3336,7 +3214,7 @@ static int spmv_grouped(int n, pa_mat* const A[], pa_vec* const y[], const pa_in
   // no halo in flight, the side rows short, pattern and side entries within
   // one group launch, no fused CG update
   bool side_tailed = false;
-  if (knobs().side_tail && !side_forked && (!any_x || direct) && !fz && 2 * n <= PA_GROUP_MAX) {
+  if (knobs().side_tail && (!any_x || direct) && !fz && 2 * n <= PA_GROUP_MAX) {
     bool ok = false;
     for (int i = 0; i < n; ++i) {
       const bool pat = knobs().spmv_format == 1 && A[i]->has_pat;
@@ -3363,7 +3241,7 @@ static int spmv_grouped(int n, pa_mat* const A[], pa_vec* const y[], const pa_in
   launch_all(4, P4);
   launch_all(1, P1);
   if (!dmark && mark(1)) return -1;
-  if (any_x && !direct) EV(hipStreamWaitEvent(sm, c0->ev_recvd, 0));
+  if (any_x && !direct) HIPC(hipStreamWaitEvent(sm, c0->ev_recvd, 0));
   if (!dmark && mark(2)) return -1;
   P0.clear(); P1.clear(); P4.clear(); P5.clear();
   std::vector<SpmvPart> P2;
@@ -3373,7 +3251,7 @@ static int spmv_grouped(int n, pa_mat* const A[], pa_vec* const y[], const pa_in
       P4.push_back(part(i, A[i]->nd_bnd, A[i]->d_dbnd_list));
       P5.push_back(part(i, A[i]->nt_bnd, A[i]->d_t_bnd_list));
       P1.push_back(part(i, A[i]->nx_bnd, A[i]->d_xbnd_list));
-      if (!side_forked && !side_tailed) P2.push_back(part(i, A[i]->s_nslices, nullptr));
+      if (!side_tailed) P2.push_back(part(i, A[i]->s_nslices, nullptr));
     } else if (A[i]->d_bnd_list) {
       P1.push_back(part(i, A[i]->nslices - A[i]->nslices_int, A[i]->d_bnd_list));
     }
@@ -3384,7 +3262,6 @@ static int spmv_grouped(int n, pa_mat* const A[], pa_vec* const y[], const pa_in
   launch_all(1, P1);
   launch_all(2, P2);
   }  // per-kind launches
-  if (side_forked) HIPC(hipStreamWaitEvent(sm, c0->ev_side[1], 0));
   for (int i = 0; i < n; ++i) {
     const int32_t* ymap = y_idx[i]->own_contig ? nullptr : y_idx[i]->d_oid_to_lid;
     const bool pat = knobs().spmv_format == 1 && A[i]->has_pat;
@@ -3450,7 +3327,7 @@ static int launch_phase(int phase, pa_mat* A, const void* x, void* y, const int3
   if (E.empty()) return 0;
   if (E.size() > 1 && knobs().spmv_merge && !(knobs().spmv_merge_max > 0 && A->nslices > knobs().spmv_merge_max)) {
     const int rc = launch_spmv_merged((int)E.size(), W.data(), E.data(), has_alpha, bmode, alpha, beta, A->ctx,
-                                      g_capture_tables, st);
+                                      st);
     if (rc < 0) PA_FAIL("mul!: merged launch table (device allocation or copy) failed");
     if (rc == 0) return 0;
   }
@@ -3601,7 +3478,7 @@ static int spmv_impl(int n, pa_mat* const A[], pa_vec* const y[], const pa_index
   std::vector<hipEvent_t*> tslot(n, nullptr);
   for (int i = 0; i < n; ++i) {
     pa_ctx* c = A[i]->ctx;
-    if (!c->timing || g_capture_stream || c->tn >= kMaxTimed || (grouped && i > 0)) continue;
+    if (!c->timing || c->tn >= kMaxTimed || (grouped && i > 0)) continue;
     if ((int)c->tev.size() < 4 * (c->tn + 1)) {
       HIPC(hipSetDevice(c->device));
       for (int k = 0; k < 4; ++k) {
@@ -3620,47 +3497,47 @@ static int spmv_impl(int n, pa_mat* const A[], pa_vec* const y[], const pa_index
   auto pack = [&](int i) -> int {
     pa_ctx* c = xg[i]->ctx;
     HIPC(hipSetDevice(c->device));
-    launch_pack(dt, xg[i]->n_snd_data, xg[i]->d_lids_snd, x[i]->d, xg[i]->d_buf_snd, SM(c));
-    EV(hipEventRecord(c->ev_packed, SM(c)));
+    launch_pack(dt, xg[i]->n_snd_data, xg[i]->d_lids_snd, x[i]->d, xg[i]->d_buf_snd, c->s_main);
+    HIPC(hipEventRecord(c->ev_packed, c->s_main));
     return 0;
   };
   auto interior = [&](int i) -> int {
     pa_ctx* c = A[i]->ctx;
     HIPC(hipSetDevice(c->device));
     const int32_t* ymap = y_idx[i]->own_contig ? nullptr : y_idx[i]->d_oid_to_lid;
-    if (tslot[i]) HIPC(hipEventRecord(tslot[i][0], SM(c)));
+    if (tslot[i]) HIPC(hipEventRecord(tslot[i][0], c->s_main));
     // interior slices (no ghost column): overlap with the halo transport
-    if (launch_phase(0, A[i], x[i]->d, y[i]->d, ymap, has_alpha, bmode, alpha, beta, dotp[i], SM(c), fz, i)) return -1;
-    if (tslot[i]) HIPC(hipEventRecord(tslot[i][1], SM(c)));
+    if (launch_phase(0, A[i], x[i]->d, y[i]->d, ymap, has_alpha, bmode, alpha, beta, dotp[i], c->s_main, fz, i)) return -1;
+    if (tslot[i]) HIPC(hipEventRecord(tslot[i][1], c->s_main));
     return 0;
   };
   auto boundary = [&](int i) -> int {
     pa_ctx* c = A[i]->ctx;
     HIPC(hipSetDevice(c->device));
     if (any_x) {
-      EV(hipStreamWaitEvent(SM(c), c->ev_recvd, 0));
+      HIPC(hipStreamWaitEvent(c->s_main, c->ev_recvd, 0));
       if (!pulled)
         launch_unpack(dt, xg[i]->n_rcv_data, xg[i]->d_lids_rcv, xg[i]->plan_fwd, PA_REPLACE,
-                      xg[i]->d_buf_rcv, x[i]->d, SM(c));
+                      xg[i]->d_buf_rcv, x[i]->d, c->s_main);
     }
-    if (tslot[i]) HIPC(hipEventRecord(tslot[i][2], SM(c)));
+    if (tslot[i]) HIPC(hipEventRecord(tslot[i][2], c->s_main));
     const int32_t* ymap = y_idx[i]->own_contig ? nullptr : y_idx[i]->d_oid_to_lid;
     // slices reading ghosts and the side rows (after the halo)
-    if (launch_phase(1, A[i], x[i]->d, y[i]->d, ymap, has_alpha, bmode, alpha, beta, dotp[i], SM(c), fz, i)) return -1;
-    cg_ghosts(fz, i, A[i], x[i], SM(c));
+    if (launch_phase(1, A[i], x[i]->d, y[i]->d, ymap, has_alpha, bmode, alpha, beta, dotp[i], c->s_main, fz, i)) return -1;
+    cg_ghosts(fz, i, A[i], x[i], c->s_main);
     // long rows (after the halo: they may read ghost columns)
     const bool pat = knobs().spmv_format == 1 && A[i]->has_pat;
     const int64_t long_base = A[i]->nslices + (pat ? A[i]->s_nslices + A[i]->t_nslices : 0);
-    launch_spmv_long(A[i], x[i]->d, y[i]->d, ymap, has_alpha, bmode, alpha, beta, dotp[i], long_base, SM(c));
+    launch_spmv_long(A[i], x[i]->d, y[i]->d, ymap, has_alpha, bmode, alpha, beta, dotp[i], long_base, c->s_main);
     if (want_dot) {  // fold the partials (main slices, side slices, long rows) in order
       const bool cplx = dt == PA_C64 || dt == PA_C128;
       const int nbp = (int)(long_base + A[i]->n_long);
       if (dot_tail)  // one part per process: the fold ends in the CG's α
-        launch_fold_cg_alpha(dt, nbp, A[i]->d_dotp, c->d_fold, c->d_result, c->d_ticket, dot_tail[i], SM(c));
+        launch_fold_cg_alpha(dt, nbp, A[i]->d_dotp, c->d_fold, c->d_result, c->d_ticket, dot_tail[i], c->s_main);
       else
-        launch_fold(cplx, nbp, A[i]->d_dotp, c->d_fold, c->d_result, c->d_ticket, SM(c));
+        launch_fold(cplx, nbp, A[i]->d_dotp, c->d_fold, c->d_result, c->d_ticket, c->s_main);
     }
-    if (tslot[i]) HIPC(hipEventRecord(tslot[i][3], SM(c)));
+    if (tslot[i]) HIPC(hipEventRecord(tslot[i][3], c->s_main));
     return 0;
   };
   // several parts, each with its own stream pair (one per GPU when one
@@ -3674,7 +3551,7 @@ static int spmv_impl(int n, pa_mat* const A[], pa_vec* const y[], const pa_index
   // one device the parts' streams share its hardware queues and the serial
   // order keeps the device time lower (1.44 vs 1.70 ms for 8 parts of the
   // 256³ (2,2,2) problem, profiles/r04/k/host_issue_3round.json); 2: always
-  bool distinct = n >= 2 && !g_capture_stream;  // every part its own stream pair
+  bool distinct = n >= 2;  // every part its own stream pair
   bool multi_dev = false;
   for (int i = 0; distinct && i < n; ++i) {
     multi_dev = multi_dev || A[i]->ctx->device != A[0]->ctx->device;
@@ -3724,132 +3601,6 @@ static int spmv_impl(int n, pa_mat* const A[], pa_vec* const y[], const pa_index
   HIPC(hipGetLastError());
   for (int i = 0; i < n; ++i)
     if (tslot[i]) ++A[i]->ctx->tn;
-  return 0;
-}
-
-// ---------------------------------------------------------------------------
-// HIP graph of one mul! over the parts of this process (all on one device,
-// neighbours local): pack, pull-unpack, interior and boundary slices, long
-// rows — captured once from the parts' streams, replayed with one launch.
-struct pa_graph {
-  int device = 0;
-  std::vector<void*> tables;        // merged-launch argument tables the graph's kernels read
-  hipStream_t origin = nullptr;
-  std::vector<hipStream_t> others;
-  std::vector<hipEvent_t> ev_pre;   // per other stream: its queued work, before a replay
-  hipEvent_t ev_done = nullptr;
-  hipGraph_t graph = nullptr;
-  hipGraphExec_t exec = nullptr;
-};
-
-int pa_graph_destroy(pa_graph* G) {
-  if (!G) return 0;
-  (void)hipSetDevice(G->device);
-  (void)hipStreamSynchronize(G->origin);
-  if (G->exec) (void)hipGraphExecDestroy(G->exec);
-  if (G->graph) (void)hipGraphDestroy(G->graph);
-  for (auto e : G->ev_pre) if (e) (void)hipEventDestroy(e);
-  if (G->ev_done) (void)hipEventDestroy(G->ev_done);
-  for (void* t : G->tables) dev_free(t);
-  delete G;
-  return 0;
-}
-
-int pa_spmv_graph_create(int n, pa_mat* const A[], pa_vec* const y[], const pa_index* const y_idx[],
-                         pa_vec* const x[], const pa_index* const x_idx[], pa_xchg* const xg[],
-                         const void* alpha, const void* beta, pa_graph** out) {
-  CHECK_ARG(n >= 1 && A && A[0] && y && x && out, "null argument");
-  TuneScope ts(A[0]->ctx);
-  const int dev = A[0]->ctx->device;
-  std::vector<pa_ctx*> ctxs(n);
-  for (int i = 0; i < n; ++i) {
-    CHECK_ARG(A[i], "null handle");
-    ctxs[i] = A[i]->ctx;
-    CHECK_ARG(ctxs[i]->device == dev, "graph capture: every part of the call on one device");
-  }
-  if (xg) {
-    LocalSet L = local_set(n, xg);
-    for (int i = 0; i < n; ++i) {
-      CHECK_ARG(xg[i], "null exchanger");
-      for (const auto* lst : {&xg[i]->parts_snd, &xg[i]->parts_rcv})
-        for (int32_t q : *lst) CHECK_ARG(L.find(q) >= 0, "graph capture: halo neighbours in other processes (RCCL) are not captured");
-    }
-  }
-  HIPC(hipSetDevice(dev));
-  if (xg && knobs().halo_pull) {  // lazily built device tables must exist before the capture
-    LocalSet L = local_set(n, xg);
-    for (int i = 0; i < n; ++i)
-      if (build_pull(i, n, xg, L, A[0]->dtype, 0)) return -1;
-    if (knobs().halo_direct) {
-      for (int i = 0; i < n; ++i)
-        if (build_direct(i, n, xg, L)) return -1;
-      if (!direct_bases(A[0]->ctx, n, x)) return -1;
-    }
-  }
-  HIPC(hipSetDevice(dev));
-  for (pa_ctx* c : ctxs) {
-    HIPC(hipStreamSynchronize(SM(c)));
-    HIPC(hipStreamSynchronize(SC(c)));
-  }
-  pa_graph* G = new pa_graph();
-  G->device = dev;
-  G->origin = ctxs[0]->s_main;
-  for (int i = 0; i < n; ++i)
-    for (hipStream_t s : {ctxs[i]->s_main, ctxs[i]->s_comm})
-      if (s != G->origin && std::find(G->others.begin(), G->others.end(), s) == G->others.end())
-        G->others.push_back(s);
-  auto mk = [](hipEvent_t* e) { return hipEventCreateWithFlags(e, hipEventDisableTiming); };
-  if (mk(&G->ev_done) != hipSuccess) { pa_graph_destroy(G); PA_FAIL("graph: event creation failed"); }
-  G->ev_pre.resize(G->others.size(), nullptr);
-  for (size_t k = 0; k < G->others.size(); ++k)
-    if (mk(&G->ev_pre[k]) != hipSuccess) { pa_graph_destroy(G); PA_FAIL("graph: event creation failed"); }
-  std::vector<bool> timing(n);
-  for (int i = 0; i < n; ++i) { timing[i] = ctxs[i]->timing; ctxs[i]->timing = false; }
-  hipError_t e = hipStreamBeginCapture(G->origin, hipStreamCaptureModeRelaxed);
-  int rc = -1;
-  if (e == hipSuccess) {
-    g_capturing = true;
-    g_capture_stream = G->origin;  // the parts' kernels as one chain
-    g_capture_tables = &G->tables;
-    g_capture_uploads.clear();
-    g_graph_owned_failed = false;
-    rc = spmv_impl(n, A, y, y_idx, x, x_idx, xg, alpha, beta, false);
-    g_capture_tables = nullptr;
-    g_graph_owned_failed = false;  // eager calls after a failed capture never see it
-    g_capture_stream = nullptr;
-    g_capturing = false;
-    hipError_t e2 = hipStreamEndCapture(G->origin, &G->graph);
-    if (e == hipSuccess) e = e2;
-  }
-  for (int i = 0; i < n; ++i) ctxs[i]->timing = timing[i];
-  // the merged-launch tables the captured kernels read (allocated during the
-  // capture, owned by the graph)
-  for (auto& u : g_capture_uploads)
-    if (e == hipSuccess && rc == 0) e = hipMemcpy(u.first, u.second.data(), u.second.size(), hipMemcpyHostToDevice);
-  g_capture_uploads.clear();
-  if (e != hipSuccess || rc != 0) {
-    const std::string why = rc != 0 ? pa_last_error() : std::string(hipGetErrorString(e));
-    pa_graph_destroy(G);
-    PA_FAIL("graph capture of mul! failed: " + why);
-  }
-  e = hipGraphInstantiate(&G->exec, G->graph, nullptr, nullptr, 0);
-  if (e != hipSuccess) { pa_graph_destroy(G); PA_FAIL(std::string("hipGraphInstantiate: ") + hipGetErrorString(e)); }
-  *out = G;
-  return 0;
-}
-
-// one replay, ordered after the work already queued on every part stream,
-// and before whatever is queued on them next
-int pa_graph_launch(pa_graph* G) {
-  CHECK_ARG(G && G->exec, "null graph");
-  HIPC(hipSetDevice(G->device));
-  for (size_t k = 0; k < G->others.size(); ++k) {
-    HIPC(hipEventRecord(G->ev_pre[k], G->others[k]));
-    HIPC(hipStreamWaitEvent(G->origin, G->ev_pre[k], 0));
-  }
-  HIPC(hipGraphLaunch(G->exec, G->origin));
-  HIPC(hipEventRecord(G->ev_done, G->origin));
-  for (hipStream_t s : G->others) HIPC(hipStreamWaitEvent(s, G->ev_done, 0));
   return 0;
 }
 
@@ -4136,6 +3887,16 @@ int cg_agree_choice(float ms[2], const std::function<int(float*)>& allreduce_max
   return ms[1] < ms[0] ? 1 : 0;
 }
 
+// Whether the fused u update may run: every rank must be able
+// to, since a rank that cannot runs the sweep, whose halo carries u while
+// the fused variant's carries r, and the ranks' collectives would no longer
+// pair.  "cannot fuse" is max-reduced over the ranks.  -2: reduction failed.
+int cg_agree_fuse(bool local_can_fuse, const std::function<int(float*)>& allreduce_max) {
+  float v[2] = {local_can_fuse ? 0.f : 1.f, 0.f};
+  if (allreduce_max && allreduce_max(v)) return -2;
+  return v[0] > 0.f ? 0 : 1;
+}
+
 void scalar_one(int dt, unsigned char out[16], double v) {
   std::memset(out, 0, 16);
   switch (dt) {
@@ -4256,6 +4017,20 @@ int pa_cg_solve_all(int n, pa_mat* const A[], pa_vec* const x[], const pa_vec* c
   // (the fused u update is written by the main structure's waves: not for
   // rows that long-row kernels or the triple SELL compute)
   for (int i = 0; i < n; ++i) can_fuse = can_fuse && A[i]->n_long == 0 && A[i]->t_nrows == 0;
+  if (R.remote && knobs().cg_fuse != 0) {  // every rank the same (cg_agree_fuse): RCCL max over the ranks
+    pa_ctx* c0 = R.ctxs[0];
+    const std::function<int(float*)> red = [&](float* v) -> int {
+      HIPC(hipMemcpyAsync(c0->d_fold, v, 2 * sizeof(float), hipMemcpyHostToDevice, c0->s_main));
+      NCCLC(ncclAllReduce(c0->d_fold, c0->d_fold, 2, ncclFloat32, ncclMax, (ncclComm_t)c0->comm, c0->s_main));
+      HIPC(hipMemcpyAsync(v, c0->d_fold, 2 * sizeof(float), hipMemcpyDeviceToHost, c0->s_main));
+      HIPC(hipStreamSynchronize(c0->s_main));
+      return 0;
+    };
+    HIPC(hipSetDevice(c0->device));
+    const int ok = cg_agree_fuse(can_fuse, red);
+    if (ok < 0) return -1;
+    can_fuse = ok == 1;
+  }
   // (every rank of a one-part-per-process solve takes the same branches:
   // maxiter, batch, the done flag and the reduced batch times agree)
   int mode = can_fuse ? knobs().cg_fuse : 0;
@@ -4407,6 +4182,16 @@ int pa_cg_variant_agree(const float local_ms[2], pa_allreduce_max_fn fn, void* u
   const int ch = cg_agree_choice(ms, red);
   if (ch == -2) return -1;
   *choice = ch;
+  return 0;
+}
+
+int pa_cg_fuse_agree(int local_can_fuse, pa_allreduce_max_fn fn, void* user, int* agreed) {
+  CHECK_ARG(agreed, "null argument");
+  std::function<int(float*)> red;
+  if (fn) red = [&](float* v) -> int { return fn(v, 2, user) ? (pa::set_error("allreduce callback failed"), -1) : 0; };
+  const int ok = cg_agree_fuse(local_can_fuse != 0, red);
+  if (ok < 0) return -1;
+  *agreed = ok;
   return 0;
 }
 

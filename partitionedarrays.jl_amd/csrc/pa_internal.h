@@ -315,8 +315,6 @@ struct pa_ctx {
   // the pack barrier of stream-pair mul! calls this part leads (spmv_impl's
   // barrier issue): recorded on its s_comm once every part of the call packed
   hipEvent_t ev_barrier = nullptr;
-  // the side-row fork of per-kind launches (spmv_grouped): fork, join
-  hipEvent_t ev_side[2] = {nullptr, nullptr};
   // device arrays of the x pointers of grouped mul! calls led by this part
   // (the direct pull's bases), most recent first
   std::vector<std::pair<std::vector<void*>, void**>> bases_cache;
@@ -353,10 +351,8 @@ struct Knobs {
   int issue_threads;
   int fault_inject;      // tests only: the IssuePool jobs issue an invalid launch
   int spmv_xcd_chunk;    // XCD-chunked block order of the SpMV launches (pa_spmv.hip xcd_block), 0 off, -1 auto
-  int spmv_tri16;        // delta16 slices re-sliced into the triple SELL (pa_mat::d_t_*): 0 never, 1 R <= 2, 2 always
-  int spmv_diag_rows;    // pattern slices compute their diagonal-only rows (pa_mat::d_dmask)
+  int spmv_tri16;        // delta16 slices re-sliced into the triple SELL (pa_mat::d_t_*): 0 never, 1 R <= 2
   int halo_barrier;      // stream-pair mul!: one pack barrier + double-buffered sends (spmv_impl)
-  int side_fork;         // per-kind launches: the side rows on the comm stream beside the pattern slices
   int tri_order;         // triple SELL row order: 0 triple rows first, 1 the other rows first (build_triple_sell)
   int side_tail;         // per-kind launches: the side rows as the trailing waves of the pattern launch
   int f32_rows;          // Float32 SELL rows per lane (matrices built afterwards): 4 (16 B packs), 2 (8 B), 0 auto
@@ -542,11 +538,6 @@ struct pa_mat {
   // auto mode (dedup_patterns: the pattern's reach in blocks / 8), 0 = none
   int xcd_auto = 0;
   uint64_t* d_mask = nullptr;        // nslices*(H/64) regular-row bits
-  // diagonal-only rows of pattern slices (Dirichlet rows: one entry, column
-  // == row; pa_tune "spmv_diag_rows"): computed in the slice from entry 0
-  // instead of as side rows; null: none
-  uint64_t* d_dmask = nullptr;       // nslices*(H/64) bits
-  int64_t n_diag_rows = 0;
   int32_t* d_pint_list = nullptr;    // pattern mode: pattern slices without ghost reads
   int32_t* d_pbnd_list = nullptr;    // pattern mode: pattern slices reading ghosts
   int64_t np_int = 0, np_bnd = 0;

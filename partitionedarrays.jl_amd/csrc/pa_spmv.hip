@@ -65,13 +65,6 @@ typedef unsigned int spmv_u32x4 __attribute__((ext_vector_type(4)));
 // (the knob defaults: pa_api.cpp kDefaults; spmv_flags 93 = NT | XPAIR |
 // TAILB | IDLIST | SHORT)
 static_assert((SPMV_NT | SPMV_XPAIR | SPMV_TAILB | SPMV_IDLIST | SPMV_SHORT) == 93, "kDefaults.spmv_flags");
-#if PA_DT_DEFINE
-// merged-launch tables allocated during a graph capture, copied after it ends
-// (no copies while a stream is being captured)
-std::vector<std::pair<void*, std::vector<char>>> g_capture_uploads;
-#else
-extern std::vector<std::pair<void*, std::vector<char>>> g_capture_uploads;
-#endif
 
 // SpmvArgs' pointers are global memory.  The merged launch reads them from a
 // device-resident table, where the compiler cannot see their address space:
@@ -110,7 +103,6 @@ struct SpmvArgs {
   const PA_GLB T* val;
   const PA_GLB int32_t* pat;       // kmax offsets per slice
   const PA_GLB uint64_t* mask;     // H/64 words per slice
-  const PA_GLB uint64_t* dmask;    // pattern slices: diagonal-only rows (null: none)
   int kmax;
   const PA_GLB int32_t* rowmap;    // structure row → oid (side SELL), null: identity
   int64_t nrows;            // rows of this structure
@@ -608,14 +600,11 @@ __device__ __forceinline__ void rows_t16_tri(T (&acc)[R], const S16Pack<R>* __re
 // pattern rows: column of row `rbase + r` at entry k is rbase + r + pat[k].
 // XP: the lane's R rows read R consecutive x values per entry, fetched as
 // one 16 B run (rows that are not regular get values they never use).
-// v0 (DG): the lane's value pack of entry 0 (the diagonal-only rows' one
-// value, spmv_wave), kept from the first batch instead of loaded twice.
-template <typename T, int R, bool ALPHA, bool NT, int U, bool XP, bool SH = false, bool DG = false, typename XS>
+template <typename T, int R, bool ALPHA, bool NT, int U, bool XP, bool SH = false, typename XS>
 __device__ __forceinline__ void rows_pattern(T (&acc)[R], const int32_t* __restrict__ pat,
                                              const Pack<T, R>* __restrict__ vp, int len,
                                              const XS& x, int64_t rbase,
-                                             const bool (&ok)[R], T alpha, bool pf, bool TB,
-                                             Pack<T, R>* v0 = nullptr) {
+                                             const bool (&ok)[R], T alpha, bool pf, bool TB) {
   if (SH) TB = true;  // short rows (len <= U): the one masked batch is the whole row
   int64_t xb[R];
   bool any = false;
@@ -632,7 +621,6 @@ __device__ __forceinline__ void rows_pattern(T (&acc)[R], const int32_t* __restr
     for (int u = 0; u < U; ++u) o[u] = pat[k + u];
 #pragma unroll
     for (int u = 0; u < U; ++u) v[u] = ld<NT>(&vp[(k + u) * 64]);
-    if (DG && k == 0) *v0 = v[0];
     T xv[U][R];
     if constexpr (XP && R > 1) {
 #pragma unroll
@@ -662,7 +650,6 @@ __device__ __forceinline__ void rows_pattern(T (&acc)[R], const int32_t* __restr
 #pragma unroll
     for (int u = 0; u < U; ++u)
       if (k + u < len) v[u] = ld<NT>(&vp[(k + u) * 64]);
-    if (DG && k == 0) *v0 = v[0];
     T xv[U][R];
     if constexpr (XP && R > 1) {
 #pragma unroll
@@ -692,7 +679,6 @@ __device__ __forceinline__ void rows_pattern(T (&acc)[R], const int32_t* __restr
   for (; !SH && k < len; ++k) {
     const int32_t o = pat[k];
     const Pack<T, R> v = ld<NT>(&vp[k * 64]);
-    if (DG && k == 0) *v0 = v;
 #pragma unroll
     for (int r = 0; r < R; ++r) {
       acc[r] = acc[r] + term<ALPHA>(v.v[r], x.get(xb[r] >= 0 ? xb[r] + o : 0), alpha, pf);
@@ -709,11 +695,10 @@ __device__ __forceinline__ void rows_pattern(T (&acc)[R], const int32_t* __restr
 // rows_pattern.  Library A/B on one box (profiles/r04/p/): FE27 256^3 one
 // part 0.6744 -> 0.6523 ms, the (2,2,2) halo leg 0.714 -> 0.688 ms, C5 F64
 // -1.0 %: one x load in three fewer relieves the per-CU memory pipeline.
-template <typename T, int R, bool ALPHA, bool NT, bool DG = false, typename XS>
+template <typename T, int R, bool ALPHA, bool NT, typename XS>
 __device__ __forceinline__ void rows_pattern_tri(T (&acc)[R], const int32_t* __restrict__ pat,
                                                  const Pack<T, R>* __restrict__ vp, int len, const XS& x,
-                                                 int64_t rbase, const bool (&ok)[R], T alpha, bool pf,
-                                                 Pack<T, R>* v0 = nullptr) {
+                                                 int64_t rbase, const bool (&ok)[R], T alpha, bool pf) {
   static_assert(R > 1, "runs of R > 1 values");
   bool any = false;
 #pragma unroll
@@ -737,7 +722,6 @@ __device__ __forceinline__ void rows_pattern_tri(T (&acc)[R], const int32_t* __r
     Pack<T, R> v[3 * TB];
 #pragma unroll
     for (int u = 0; u < 3 * TB; ++u) v[u] = ld<NT>(&vp[(k + u) * 64]);
-    if (DG && k == 0) *v0 = v[0];
     T xv[TB][3][R];
 #pragma unroll
     for (int t = 0; t < TB; ++t) triple(o[t], xv[t]);
@@ -753,7 +737,6 @@ __device__ __forceinline__ void rows_pattern_tri(T (&acc)[R], const int32_t* __r
     Pack<T, R> v[3];
 #pragma unroll
     for (int j = 0; j < 3; ++j) v[j] = ld<NT>(&vp[(k + j) * 64]);
-    if (DG && k == 0) *v0 = v[0];
     T xv[3][R];
     triple(o, xv);
 #pragma unroll
@@ -906,37 +889,6 @@ __device__ __forceinline__ void spmv_wave(const SpmvArgs<T>& a, const int64_t w)
   const Pack<T, R>* __restrict__ vp = reinterpret_cast<const Pack<T, R>*>(a.val + off) + lane;
   const bool tb = (a.flags & SPMV_TAILB) != 0;
   const bool pf = (a.flags & SPMV_PRODA) != 0;
-  // Diagonal-only rows of a pattern slice (pa_tune "spmv_diag_rows": a
-  // Dirichlet row, its one entry at column == row, e.g. the domain-face rows
-  // at both ends of every x-line): not on the slice's pattern, yet no side
-  // rows — before the pattern loop, the lanes holding one read their entry-0
-  // pack and store y = β-init + v·x[row], the reference's one term
-  // (SparseUtils.jl:176-185 over one entry); the loop's sum for the row is
-  // never stored (ok false).  Nothing stays live across the loop.  Off by
-  // default: the dmask load and the v·x round trip ahead of every wave's
-  // stream cost more than the side rows they remove (same-box A/B,
-  // profiles/r05/i/: FE27 256³ 0.6504 -> 0.6721 ms kernel, C2 FD7 128³
-  // 0.0281 -> 0.0316); testing the word after the loop instead keeps v0 and
-  // the word live across it (merged F64 kernel 124 -> 130 VGPRs, 3 waves).
-  unsigned dbits = 0;
-  if constexpr (PK == 1) {
-    if (a.dmask) {
-      const uint64_t dm = a.dmask[s * (H / 64) + (lane * R) / 64];
-      dbits = (unsigned)(dm >> ((lane * R) & 63)) & ((1u << R) - 1u);
-      if (dbits) {
-        const Pack<T, R> v0 = ld<false>(&vp[0]);
-#pragma unroll
-        for (int r = 0; r < R; ++r) {
-          const int64_t i = row0 + r;
-          if (!((dbits >> r) & 1u) || i >= a.nrows) continue;
-          const int64_t yl = a.ymap ? (int64_t)a.ymap[i] : i;
-          T init = zero_of<T>();
-          if (BMODE != 0) init = (BMODE == 2) ? a.y[yl] * a.beta : a.y[yl];
-          a.y[yl] = init + term<ALPHA>(v0.v[r], xs.get(i), a.alpha, pf);
-        }
-      }
-    }
-  }
   if constexpr (PK == 1) {
     const int32_t* pat = a.pat + (int64_t)(lraw >> 9) * a.kmax;
     bool tri_done = false;
@@ -998,12 +950,6 @@ __device__ __forceinline__ void spmv_wave(const SpmvArgs<T>& a, const int64_t w)
       if constexpr (XV) uv = main_rows ? un[r] : xs.get(orow[r]);
       else uv = a.dotu[orow[r]];
       if (ok[r]) part = part + dacc(cdot(uv, acc[r]));
-      if (PK == 1 && ((dbits >> r) & 1u) && row0 + r < a.nrows) {  // a diagonal-only row: its stored y
-        const int64_t i = row0 + r;
-        if constexpr (XV) uv = main_rows ? un[r] : xs.get(i);
-        else uv = a.dotu[i];
-        part = part + dacc(cdot(uv, a.y[a.ymap ? (int64_t)a.ymap[i] : i]));
-      }
     }
 #pragma unroll
     for (int d = 32; d >= 1; d >>= 1) part = part + shfl_down_acc(part, d);
@@ -1238,7 +1184,6 @@ static SpmvArgs<T> make_args(int which, int64_t nwork, const int32_t* list, cons
       a.slen = (decltype(a.slen))(A->d_plen);
       a.pat = (decltype(a.pat))(A->d_pat);
       a.mask = (decltype(a.mask))(A->d_mask);
-      a.dmask = (decltype(a.dmask))(A->d_dmask);
       a.kmax = A->kmax;
     } else {
       a.slen = (decltype(a.slen))(A->d_slice_len);
@@ -1264,8 +1209,9 @@ static void launch_which(int which, int64_t nwork, const int32_t* list, const pa
   const SpmvArgs<T> a = make_args<T>(which, nwork, list, A, x, y, ymap, alpha, beta, dotp, cgp);
   if (which == 0) launch_ab<T, R, 1>(a, has_alpha, bmode, st);
   else if (which == 4) launch_ab<T, R, 3>(a, has_alpha, bmode, st);
-  else if (which == 5) launch_ab<T, R, 4>(a, has_alpha, bmode, st);
-  else launch_ab<T, R, 0>(a, has_alpha, bmode, st);
+  else if (which == 5) {
+    if constexpr (R <= 2) launch_ab<T, R, 4>(a, has_alpha, bmode, st);  // (build_triple_sell: R <= 2 only)
+  } else launch_ab<T, R, 0>(a, has_alpha, bmode, st);
 }
 
 // the same slices of np parts as one launch per PA_GROUP_MAX parts
@@ -1281,7 +1227,9 @@ static void group_which(int which, int np, const SpmvPart* parts, bool has_alpha
     if (g.np == 0) return;
     if (which == 0 || which == 6) launch_group_ab<T, R, 1>(g, has_alpha, bmode, st);
     else if (which == 4) launch_group_ab<T, R, 3>(g, has_alpha, bmode, st);
-    else if (which == 5) launch_group_ab<T, R, 4>(g, has_alpha, bmode, st);
+    else if (which == 5) {
+      if constexpr (R <= 2) launch_group_ab<T, R, 4>(g, has_alpha, bmode, st);  // (R <= 2 only)
+    }
     else launch_group_ab<T, R, 0>(g, has_alpha, bmode, st);
     g = SpmvGroup<T>{};
     g.tail0 = PA_GROUP_MAX + 1;
@@ -1305,8 +1253,7 @@ static void group_which(int which, int np, const SpmvPart* parts, bool has_alpha
   void spmv_group_##k(int which, int np, const SpmvPart* parts, bool has_alpha, int bmode, const void* alpha,  \
                       const void* beta, hipStream_t st);                                                        \
   int spmv_merged_##k(int n, const int* which, const SpmvPart* parts, bool has_alpha, int bmode,              \
-                      const void* alpha, const void* beta, pa_ctx* owner, std::vector<void*>* pinned,         \
-                      hipStream_t st);                                                                          \
+                      const void* alpha, const void* beta, pa_ctx* owner, hipStream_t st);                     \
   void spmv_long_##k(const pa_mat* A, const void* x, void* y, const int32_t* ymap, bool has_alpha, int bmode,  \
                      const void* alpha, const void* beta, void* dotp, int64_t dot_base, hipStream_t st);       \
   void spmv_part_##k(int which, int64_t nwork, const int32_t* list, const pa_mat* A, const void* x, void* y,  \
@@ -1410,7 +1357,8 @@ __device__ __forceinline__ void merged_wave(const SpmvTable<T>* __restrict__ tab
     // the triple SELL never runs in the short-row (make_args: maxlen >= 9)
     // or fused-u kernels (pa_cg_solve_all: no fused update with it): their
     // registers stay those of the other kinds
-    if constexpr (!SH && !XV) spmv_wave<T, R, ALPHA, BMODE, U, 4, SH, XV>(a, lw);
+    // (and slices of R <= 2 rows per lane only: build_triple_sell)
+    if constexpr (!SH && !XV && R <= 2) spmv_wave<T, R, ALPHA, BMODE, U, 4, SH, XV>(a, lw);
   }
   else spmv_wave<T, R, ALPHA, BMODE, U, 0, SH, XV>(a, lw);
 }
@@ -1453,9 +1401,18 @@ static void launch_merged_t(const SpmvTable<T>* d, int n, int64_t waves, bool sh
 
 static int pk_of(int which) { return which == 0 ? 1 : which == 4 ? 3 : which == 5 ? 4 : 0; }
 
+// One merged launch, prepared: its device table (cached) and launch shape
+template <typename T>
+struct MergedLaunch {
+  const SpmvTable<T>* dt = nullptr;
+  int n = 0;
+  int64_t waves = 0;
+  bool sh = false, cg = false;
+};
+
 template <typename T, int R>
-static int merged_t(int n, const int* which, const SpmvPart* parts, bool has_alpha, int bmode, const void* alpha,
-                    const void* beta, pa_ctx* owner, std::vector<void*>* pinned, hipStream_t st) {
+static int merged_prepare(int n, const int* which, const SpmvPart* parts, bool has_alpha, int bmode,
+                          const void* alpha, const void* beta, pa_ctx* owner, hipStream_t st, MergedLaunch<T>* out) {
   // the table's used bytes (header + n entries) are its cache key: only
   // those are zeroed, compared and uploaded (a 48-entry table is ≈15 KB, a
   // call's tables hold 1-4 entries: per-call host work of the stream-pair
@@ -1476,31 +1433,17 @@ static int merged_t(int n, const int* which, const SpmvPart* parts, bool has_alp
     h.start[h.n + 1] = h.start[h.n] + q.nwork;
     ++h.n;
   }
+  *out = MergedLaunch<T>{};
   if (h.n == 0) return 0;
   static_assert(kMergeMax <= 255, "the wave map holds entry indices in bytes");
   const size_t used = kHdr + (size_t)h.n * sizeof(SpmvArgs<T>);  // the device reads entries < n only
   const int64_t nwaves = h.start[h.n];
   const size_t moff = merged_map_offset<T>(h.n), total = moff + (size_t)nwaves;
-  auto wave_map = [&]() {  // entry of every wave (merged_wave)
-    std::vector<char> m((size_t)nwaves);
-    for (int e = 0; e < h.n; ++e) std::memset(m.data() + h.start[e], e, (size_t)(h.start[e + 1] - h.start[e]));
-    return m;
-  };
-  // cached device copy of this exact table (most recent first); a graph
-  // capture (pinned) gets its own copy, owned by the graph
+  // cached device copy of this exact table (most recent first)
   auto& C = owner->merged_cache;
   const char* hb = reinterpret_cast<const char*>(&h);
   void* d = nullptr;
-  if (pinned) {  // during a capture: device memory now, its contents after the capture ends
-    if (hipMalloc(&d, total) != hipSuccess) {
-      (void)hipGetLastError();
-      return 1;  // the caller launches per kind
-    }
-    pinned->push_back(d);
-    g_capture_uploads.push_back({d, std::vector<char>(hb, hb + used)});
-    g_capture_uploads.push_back({(char*)d + moff, wave_map()});
-  }
-  for (size_t k = 0; !d && k < C.size(); ++k)
+  for (size_t k = 0; k < C.size(); ++k)
     if (C[k].first.size() == used && std::memcmp(C[k].first.data(), hb, used) == 0) {
       if (k) std::swap(C[k], C[0]);
       d = C[0].second;
@@ -1508,7 +1451,8 @@ static int merged_t(int n, const int* which, const SpmvPart* parts, bool has_alp
     }
   if (!d) {
     if (hipMalloc(&d, total) != hipSuccess) return -1;
-    const std::vector<char> m = wave_map();
+    std::vector<char> m((size_t)nwaves);  // entry of every wave (merged_wave)
+    for (int e = 0; e < h.n; ++e) std::memset(m.data() + h.start[e], e, (size_t)(h.start[e + 1] - h.start[e]));
     if (hipMemcpy(d, &h, used, hipMemcpyHostToDevice) != hipSuccess ||
         hipMemcpy((char*)d + moff, m.data(), m.size(), hipMemcpyHostToDevice) != hipSuccess) {
       (void)hipFree(d);
@@ -1521,25 +1465,43 @@ static int merged_t(int n, const int* which, const SpmvPart* parts, bool has_alp
     }
     C.insert(C.begin(), {std::vector<char>(hb, hb + used), d});
   }
-  const SpmvTable<T>* dt = (const SpmvTable<T>*)d;
-  const int64_t waves = h.start[h.n];
-  if (h.a[0].cg) {  // the device CG's fused u update (α = 1, β = 0)
-    const int64_t blocks = (waves + 3) / 4;
-    if (blocks == 0) return 0;
+  out->dt = (const SpmvTable<T>*)d;
+  out->n = h.n;
+  out->waves = nwaves;
+  out->sh = sh;
+  out->cg = h.a[0].cg != nullptr;
+  return 0;
+}
+
+template <typename T, int R>
+static void merged_launch(const MergedLaunch<T>& m, bool has_alpha, int bmode, hipStream_t st) {
+  if (m.n == 0) return;
+  if (m.cg) {  // the device CG's fused u update (α = 1, β = 0)
+    const int64_t blocks = (m.waves + 3) / 4;
+    if (blocks == 0) return;
     const int xc = std::max(knobs().spmv_xcd_chunk, 0);  // (auto: merged launches keep the round robin)
-    if (sh) hipLaunchKernelGGL((k_spmv_merged<T, R, false, 0, 8, true, true>), dim3(blocks), dim3(256), 0, st, dt, h.n, waves, xc);
-    else hipLaunchKernelGGL((k_spmv_merged<T, R, false, 0, 8, false, true>), dim3(blocks), dim3(256), 0, st, dt, h.n, waves, xc);
-    return 0;
+    if (m.sh) hipLaunchKernelGGL((k_spmv_merged<T, R, false, 0, 8, true, true>), dim3(blocks), dim3(256), 0, st, m.dt, m.n, m.waves, xc);
+    else hipLaunchKernelGGL((k_spmv_merged<T, R, false, 0, 8, false, true>), dim3(blocks), dim3(256), 0, st, m.dt, m.n, m.waves, xc);
+    return;
   }
   if (!has_alpha) {
-    if (bmode == 0) launch_merged_t<T, R, false, 0>(dt, h.n, waves, sh, st);
-    else if (bmode == 1) launch_merged_t<T, R, false, 1>(dt, h.n, waves, sh, st);
-    else launch_merged_t<T, R, false, 2>(dt, h.n, waves, sh, st);
+    if (bmode == 0) launch_merged_t<T, R, false, 0>(m.dt, m.n, m.waves, m.sh, st);
+    else if (bmode == 1) launch_merged_t<T, R, false, 1>(m.dt, m.n, m.waves, m.sh, st);
+    else launch_merged_t<T, R, false, 2>(m.dt, m.n, m.waves, m.sh, st);
   } else {
-    if (bmode == 0) launch_merged_t<T, R, true, 0>(dt, h.n, waves, sh, st);
-    else if (bmode == 1) launch_merged_t<T, R, true, 1>(dt, h.n, waves, sh, st);
-    else launch_merged_t<T, R, true, 2>(dt, h.n, waves, sh, st);
+    if (bmode == 0) launch_merged_t<T, R, true, 0>(m.dt, m.n, m.waves, m.sh, st);
+    else if (bmode == 1) launch_merged_t<T, R, true, 1>(m.dt, m.n, m.waves, m.sh, st);
+    else launch_merged_t<T, R, true, 2>(m.dt, m.n, m.waves, m.sh, st);
   }
+}
+
+template <typename T, int R>
+static int merged_t(int n, const int* which, const SpmvPart* parts, bool has_alpha, int bmode, const void* alpha,
+                    const void* beta, pa_ctx* owner, hipStream_t st) {
+  MergedLaunch<T> m;
+  const int rc = merged_prepare<T, R>(n, which, parts, has_alpha, bmode, alpha, beta, owner, st, &m);
+  if (rc) return rc;
+  merged_launch<T, R>(m, has_alpha, bmode, st);
   return 0;
 }
 
@@ -1547,8 +1509,7 @@ static int merged_t(int n, const int* which, const SpmvPart* parts, bool has_alp
 // table (the caller launches per kind), -1 on an allocation/copy error
 #if defined(PA_SPMV_DT)
 int PA_CAT(spmv_merged_, PA_SPMV_DT)(int n, const int* which, const SpmvPart* parts, bool has_alpha, int bmode,
-                                     const void* alpha, const void* beta, pa_ctx* owner, std::vector<void*>* pinned,
-                                     hipStream_t st) {
+                                     const void* alpha, const void* beta, pa_ctx* owner, hipStream_t st) {
   if constexpr (kDtR2) {
     bool mixed = false;
     for (int i = 1; i < n; ++i) mixed = mixed || parts[i].A->R != parts[0].A->R;
@@ -1561,22 +1522,29 @@ int PA_CAT(spmv_merged_, PA_SPMV_DT)(int n, const int* which, const SpmvPart* pa
         w[k].push_back(which[i]);
         q[k].push_back(parts[i]);
       }
-      const int rc = merged_t<DtT, 2>((int)w[0].size(), w[0].data(), q[0].data(), has_alpha, bmode, alpha, beta,
-                                      owner, pinned, st);
+      // both tables before either launch: a table that does not fit or
+      // fails leaves nothing launched for the caller's per-kind fallback to
+      // repeat (with β ≠ 0, y would accumulate twice)
+      MergedLaunch<DtT> m2, m4;
+      int rc = merged_prepare<DtT, 2>((int)w[0].size(), w[0].data(), q[0].data(), has_alpha, bmode, alpha, beta,
+                                      owner, st, &m2);
+      if (rc == 0)
+        rc = merged_prepare<DtT, kDtR>((int)w[1].size(), w[1].data(), q[1].data(), has_alpha, bmode, alpha, beta,
+                                       owner, st, &m4);
       if (rc) return rc;
-      return merged_t<DtT, kDtR>((int)w[1].size(), w[1].data(), q[1].data(), has_alpha, bmode, alpha, beta, owner,
-                                 pinned, st);
+      merged_launch<DtT, 2>(m2, has_alpha, bmode, st);
+      merged_launch<DtT, kDtR>(m4, has_alpha, bmode, st);
+      return 0;
     }
-    if (n > 0 && parts[0].A->R == 2) return merged_t<DtT, 2>(n, which, parts, has_alpha, bmode, alpha, beta, owner, pinned, st);
+    if (n > 0 && parts[0].A->R == 2) return merged_t<DtT, 2>(n, which, parts, has_alpha, bmode, alpha, beta, owner, st);
   }
-  return merged_t<DtT, kDtR>(n, which, parts, has_alpha, bmode, alpha, beta, owner, pinned, st);
+  return merged_t<DtT, kDtR>(n, which, parts, has_alpha, bmode, alpha, beta, owner, st);
 }
 #else
 int launch_spmv_merged(int n, const int* which, const SpmvPart* parts, bool has_alpha, int bmode,
-                       const void* alpha, const void* beta, pa_ctx* owner, std::vector<void*>* pinned,
-                       hipStream_t st) {
+                       const void* alpha, const void* beta, pa_ctx* owner, hipStream_t st) {
   if (n <= 0) return 0;
-#define spmv_merged_(k) spmv_merged_##k(n, which, parts, has_alpha, bmode, alpha, beta, owner, pinned, st)
+#define spmv_merged_(k) spmv_merged_##k(n, which, parts, has_alpha, bmode, alpha, beta, owner, st)
   switch (parts[0].A->dtype) {
     case PA_F32: return spmv_merged_(0);
     case PA_F64: return spmv_merged_(1);
@@ -2432,12 +2400,10 @@ void launch_pattern_detect(pa_mat* A, int64_t noids, int min_pct, int32_t* kind,
 }
 
 // Side SELL: the irregular rows (oids, ascending), copied from the int32 layout.
-// (diag: 1 for a row whose only entry is its diagonal, column == row)
 template <int R>
 __global__ void k_side_len(int64_t n, const int32_t* __restrict__ rows, const int64_t* __restrict__ soff,
                            const int32_t* __restrict__ slen, const int32_t* __restrict__ col,
-                           int32_t* __restrict__ len, int64_t noids, int32_t* __restrict__ sghost, int sH,
-                           int32_t* __restrict__ diag) {
+                           int32_t* __restrict__ len, int64_t noids, int32_t* __restrict__ sghost, int sH) {
   constexpr int H = 64 * R;
   const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   if (i >= n) return;
@@ -2455,7 +2421,6 @@ __global__ void k_side_len(int64_t n, const int32_t* __restrict__ rows, const in
   }
   len[i] = l;
   if (g) atomicOr(&sghost[i / sH], 1);
-  if (diag) diag[i] = l == 1 && col[soff[s] + (int64_t)lane * R + r] == (int32_t)row;
 }
 
 template <typename T, int R>
@@ -2496,13 +2461,13 @@ __global__ void k_side_fill(int64_t n, const int32_t* __restrict__ rows, const i
 }
 
 void launch_side_len(pa_mat* A, int64_t n, const int32_t* rows, int32_t* len, int64_t noids,
-                     int32_t* sghost, hipStream_t st, int32_t* diag) {
+                     int32_t* sghost, hipStream_t st) {
   if (n == 0) return;
   const dim3 g((unsigned)((n + 255) / 256)), b(256);
   switch (A->R) {
-    case 1: hipLaunchKernelGGL(k_side_len<1>, g, b, 0, st, n, rows, A->d_slice_off, A->d_slice_len, A->d_col, len, noids, sghost, A->H, diag); break;
-    case 2: hipLaunchKernelGGL(k_side_len<2>, g, b, 0, st, n, rows, A->d_slice_off, A->d_slice_len, A->d_col, len, noids, sghost, A->H, diag); break;
-    case 4: hipLaunchKernelGGL(k_side_len<4>, g, b, 0, st, n, rows, A->d_slice_off, A->d_slice_len, A->d_col, len, noids, sghost, A->H, diag); break;
+    case 1: hipLaunchKernelGGL(k_side_len<1>, g, b, 0, st, n, rows, A->d_slice_off, A->d_slice_len, A->d_col, len, noids, sghost, A->H); break;
+    case 2: hipLaunchKernelGGL(k_side_len<2>, g, b, 0, st, n, rows, A->d_slice_off, A->d_slice_len, A->d_col, len, noids, sghost, A->H); break;
+    case 4: hipLaunchKernelGGL(k_side_len<4>, g, b, 0, st, n, rows, A->d_slice_off, A->d_slice_len, A->d_col, len, noids, sghost, A->H); break;
   }
 }
 

@@ -32,14 +32,14 @@ class PartContext:
     def sync(self):
         _lib.call("pa_ctx_sync", self.h)
 
-    def tune(self, key: str, value: int) -> int:
+    def tune(self, key: str, value):
         """pa_ctx_tune: this part's value of a knob for the calls it leads
-        (-1 drops it: the process default again); returns the former
-        override (-1: none)."""
+        (None drops it: the process default again); returns the former
+        override (None: none)."""
         prev = C.c_int(0)
-        _lib.call("pa_ctx_tune", self.h, key.encode(), int(value), C.byref(prev))
-        _lib.tune_generation_bump()
-        return prev.value
+        v = _lib.TUNE_DROP if value is None else int(value)
+        _lib.call("pa_ctx_tune", self.h, key.encode(), v, C.byref(prev))
+        return None if prev.value == _lib.TUNE_DROP else prev.value
 
     def comm_stats(self):
         """(bytes sent, bytes received) this part has posted to RCCL so far"""
@@ -87,17 +87,12 @@ class HIPBackend(SequentialBackend):
     """All parts in this process, part p on device devices[(p-1) % len(devices)]
     (SequentialBackend semantics, HIP parts)."""
 
-    def __init__(self, devices=None, share_streams=True, graph_mul=False, rccl=False):
+    def __init__(self, devices=None, share_streams=True, rccl=False):
         """share_streams (default): parts on the same device share one stream
         pair, and mul! runs them as one grouped launch per phase (pack,
         pull-unpack, interior and boundary slices of every part together;
         pa_tune("spmv_group")).  False: a stream pair per part and per-part
         launches.
-        graph_mul: mul!(c, a, b, α, β) captures a HIP graph the first time
-        it sees (c, a, b, α, β) and replays it afterwards (pamd.SpMVGraph; at
-        most 16 cached, least recently used evicted; a structure that cannot
-        be captured, e.g. parts on several devices, stays eager).  Off by
-        default.
         rccl: the halo moves by RCCL grouped ncclSend/ncclRecv between the
         parts of this process (pa_comm_init_all, which marks these contexts),
         the MPIBackend transport without processes: one RCCL rank per
@@ -108,7 +103,6 @@ class HIPBackend(SequentialBackend):
             raise _lib.PAError("HIPBackend: no HIP device visible")
         self.devices = list(devices) if devices is not None else list(range(ndev))
         self.share_streams = share_streams
-        self.graph_mul = graph_mul
         self.rccl = rccl
         self.ctx = {}
         self._sets = {}  # number of parts -> {part: PartContext}
@@ -519,9 +513,6 @@ class DeviceMatrix:
         t = [C.c_int64() for _ in range(4)]
         _lib.call("pa_mat_triple_info", self.h, *[C.byref(x) for x in t])
         d.update(zip(["triple_sell_slices", "triple_sell_rows", "tri_slices", "tri_rows"], [x.value for x in t]))
-        dr = C.c_int64()
-        _lib.call("pa_mat_diag_rows", self.h, C.byref(dr))
-        d["diag_rows"] = dr.value
         lr = [C.c_int64() for _ in range(2)]
         _lib.call("pa_mat_long_rows", self.h, *[C.byref(x) for x in lr])
         d.update(zip(["long_rows", "long_nnz"], [x.value for x in lr]))

@@ -545,76 +545,9 @@ def _mat_exchange(A: "PSparseMatrix", op, reverse, zero_sent):
 
 def mul_(c: PVector, a: PSparseMatrix, b: PVector, alpha=1.0, beta=0.0) -> PVector:
     """mul!(c, a, b, α, β) (Interfaces.jl:2246-2275): halo exchange of b
-    overlapped with the interior slices, then the slices reading ghosts.
-    With HIPBackend(graph_mul=True): a cached HIP-graph replay of the same."""
-    g = _cached_graph(c, a, b, alpha, beta)
-    if g:
-        g()
-        return c
+    overlapped with the interior slices, then the slices reading ghosts."""
     _spmv(c, a, b, alpha, beta, None)
     return c
-
-
-_GRAPH_CACHE_MAX = 16
-
-
-def _cached_graph(c, a, b, alpha, beta):
-    """HIPBackend(graph_mul=True): the SpMVGraph of (c, a, b, α, β), captured
-    on first use.  The entry holds c, a and b, so their ids stay unique while
-    cached; a pa_tune call since the capture makes the entry stale (the graph
-    froze the kernel choice).  Replays do not feed pa_ctx_last_kernel_ms.  Falsy: graphs off, or this structure is not capturable (eager)."""
-    be = getattr(a.values, "backend", None)
-    if not getattr(be, "graph_mul", False):
-        return None
-    cache = be.__dict__.setdefault("_graphs", OrderedDict())
-    key = (id(c), id(a), id(b), complex(alpha), complex(beta), _lib.tune_generation)
-    if key in cache:
-        cache.move_to_end(key)
-        return cache[key]
-    try:
-        g = SpMVGraph(c, a, b, alpha, beta)
-    except _lib.PAError as e:
-        if "graph capture" not in str(e):
-            raise
-        g = _Uncapturable((c, a, b))
-    cache[key] = g
-    while len(cache) > _GRAPH_CACHE_MAX:
-        cache.popitem(last=False)
-    return g
-
-
-class _Uncapturable:
-    """cache entry of a structure that stays eager (keeps its ids unique)"""
-
-    def __init__(self, keep):
-        self._keep = keep
-
-    def __bool__(self):
-        return False
-
-
-class SpMVGraph:
-    """mul!(c, a, b, α, β) captured once as a HIP graph (pa_spmv_graph_create)
-    and replayed by calling it: one launch instead of the per-part kernels,
-    copies and event waits of the eager path.  All parts on one device."""
-
-    def __init__(self, c: PVector, a: PSparseMatrix, b: PVector, alpha=1.0, beta=0.0):
-        args = _spmv_args(c, a, b, alpha, beta)
-        self._keep = (c, a, b, args)
-        h = C.c_void_p()
-        _lib.call("pa_spmv_graph_create", *args, C.byref(h))
-        self.h = h
-
-    def __call__(self):
-        _lib.call("pa_graph_launch", self.h)
-        return self._keep[0]
-
-    def __del__(self):
-        try:
-            if getattr(self, "h", None) and _lib._lib is not None:
-                _lib._lib.pa_graph_destroy(self.h)
-        except Exception:
-            pass
 
 
 def mul_dot_(c: PVector, a: PSparseMatrix, b: PVector, alpha=1.0, beta=0.0):

@@ -63,8 +63,8 @@ def test_tune_knobs_round_trip_and_reject_bad_values(pamd):
     per-matrix CSR flag) out of the user's reach."""
     knobs = {"spmv_merge": 0, "spmv_merge_max": 1024, "spmv_group": 0, "spmv_delta16": 0,
              "long_rows_exact": 0, "halo_direct": 0, "cg_fuse": 1, "halo_pull": 0, "spmv_format": 0,
-             "issue_threads": 0, "pattern_min_regular": 90, "fault_inject": 1, "spmv_tri16": 2,
-             "spmv_diag_rows": 1, "halo_barrier": 0, "spmv_xcd_chunk": 8, "spmv_side_fork": 1,
+             "issue_threads": 0, "pattern_min_regular": 90, "fault_inject": 1, "spmv_tri16": 0,
+             "halo_barrier": 0, "spmv_xcd_chunk": 8,
              "spmv_tri_order": 0, "spmv_side_tail": 0, "f32_rows": 2}
     for k, v in knobs.items():
         prev = pamd._lib.tune(k, v)

@@ -300,7 +300,12 @@ def _worker_cg_agree(rank, world, port, q):
         local = [[1.0, 2.0], [3.0, 2.5], [2.0, 2.2], [0.5, 0.4]][rank]
         out = {"local": pamd._lib.cg_variant_agree(local),
                "agreed": pamd._lib.cg_variant_agree(local, allreduce_max),
-               "invalid": pamd._lib.cg_variant_agree([0.0, 1.0], allreduce_max)}
+               "invalid": pamd._lib.cg_variant_agree([0.0, 1.0], allreduce_max),
+               # rank 0's part cannot fuse (e.g. its Voronoi part took the
+               # triple SELL): no rank may
+               "fuse_local": pamd._lib.cg_fuse_agree(rank != 0),
+               "fuse_agreed": pamd._lib.cg_fuse_agree(rank != 0, allreduce_max),
+               "fuse_all": pamd._lib.cg_fuse_agree(True, allreduce_max)}
         dist.barrier()
         dist.destroy_process_group()
         q.put((rank, out))
@@ -316,7 +321,10 @@ def test_cg_variant_agreement_over_ranks(world):
     reduces them with max over the ranks (RCCL in pa_cg_solve_all; here the
     same decision through pa_cg_variant_agree with a gloo all-reduce), and
     every rank keeps the same variant even where its local times disagree;
-    without a valid time on any rank there is no choice (-1) on all."""
+    without a valid time on any rank there is no choice (-1) on all.  The
+    fused variant runs at all only if every rank's part allows it
+    (pa_cg_fuse_agree): one rank with long rows or a triple
+    SELL keeps every rank on the sweep."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
@@ -331,3 +339,6 @@ def test_cg_variant_agreement_over_ranks(world):
     assert res[0]["local"] == 0 and res[1]["local"] == 1
     assert {res[r]["agreed"] for r in range(world)} == {1}
     assert {res[r]["invalid"] for r in range(world)} == {-1}
+    assert res[0]["fuse_local"] is False and all(res[r]["fuse_local"] for r in range(1, world))
+    assert {res[r]["fuse_agreed"] for r in range(world)} == {False}
+    assert {res[r]["fuse_all"] for r in range(world)} == {True}

@@ -117,44 +117,6 @@ def test_hbm_probe_rates_and_arguments(be, pamd):
         pamd._lib.hbm_probe(0, 1024, 1)
 
 
-@pytest.mark.parametrize("share", [False, True])
-def test_graph_mul_cache_matches_eager(pamd, share):
-    """HIPBackend(graph_mul=True): mul! replays a cached HIP graph; results are
-    bit-identical to the eager path, follow new x values written in place
-    between replays, and keep one entry per (c, a, b, α, β)."""
-    N = (12, 10, 9)
-    rng = np.random.default_rng(5)
-    xs = [rng.uniform(-1, 1, 4000) for _ in range(2)]
-    calls = [(0, 1.0, 0.0), (1, 1.0, 0.0), (1, 2.0, 0.5), (0, 1.0, 0.0)]
-    out = {}
-    for name, flag in (("eager", False), ("graph", True)):
-        be = pamd.HIPBackend(devices=[0], share_streams=share, graph_mul=flag)
-        parts = be.get_part_ids((2, 2, 1))
-        A = pamd.drivers.stencil_operator(parts, N, 27)
-        srcs = [pamd.PVector.from_host(pamd.map_parts(lambda s, v=v: v[:s.num_lids].copy(), A.cols.partition),
-                                       A.cols) for v in xs]
-        x = srcs[0].copy()
-        y = pamd.PVector.undef(A.rows).fill_(0.25)
-        res = []
-        for k, al, bt in calls:
-            pamd.copyto_(x, srcs[k])
-            pamd.mul_(y, A, x, al, bt)
-            res.append(y.to_host())
-        out[name] = (parts, A, res)
-        if flag:
-            assert len(be._graphs) == 2 and all(bool(g) for g in be._graphs.values())
-            prev = pamd._lib.tune("spmv_format", 0)  # knob change: the next call captures afresh
-            pamd._lib.tune("spmv_format", prev)
-            pamd.mul_(y, A, x, 1.0, 0.0)
-            assert len(be._graphs) == 3
-            assert np.array_equal(y.to_host().local(1), res[-1].local(1))
-    parts, A, _ = out["eager"]
-    for r_e, r_g in zip(out["eager"][2], out["graph"][2]):
-        for p in parts.part_ids:
-            own = A.rows.partition.local(p).oid_to_lid - 1
-            assert np.array_equal(r_e.local(p)[own], r_g.local(p)[own])
-
-
 def test_mul_with_equal_copies_of_the_ranges(be, pamd, O):
     """mul!(c, a, b) with c.rows / b.rows equal copies (not the same objects)
     of a.rows / a.cols (Interfaces.jl:2253-2255 @checks pass on equal ids):
@@ -178,59 +140,6 @@ def test_mul_with_equal_copies_of_the_ranges(be, pamd, O):
         own = A.rows.partition.local(p).oid_to_lid - 1
         assert np.array_equal(y.to_host().local(p)[own], oy.values[p][own])
     assert "_eq_cache" in A.cols.__dict__ and any(k[0] == "layout" for k in A.cols._eq_cache)
-
-
-def test_graph_replay_survives_cache_eviction(pamd):
-    """A captured mul! owns its halo tables: eager mul! calls
-    over 20 other x vectors evict the x-pointer array the capture saw from
-    the direct-pull cache (16 entries) and free it; the graph must still
-    replay from its own copy and equal the eager mul! bit for bit."""
-    be = pamd.HIPBackend(devices=[0])
-    parts = be.get_part_ids((2, 2, 2))
-    N = (14, 13, 12)
-    A = pamd.drivers.stencil_operator(parts, N, 27)
-    rng = np.random.default_rng(5)
-    mk = lambda: pamd.PVector.from_host(
-        pamd.map_parts(lambda s: rng.uniform(-1, 1, s.num_lids), A.cols.partition), A.cols)
-    x = mk()
-    y_g, y_e = pamd.PVector.undef(A.rows), pamd.PVector.undef(A.rows)
-    G = pamd.SpMVGraph(y_g, A, x)
-    others = [mk() for _ in range(20)]
-    y_o = pamd.PVector.undef(A.rows)
-    for xo in others:
-        pamd.mul_(y_o, A, xo)
-    G()
-    pamd.mul_(y_e, A, x)
-    g, e = y_g.to_host(), y_e.to_host()
-    for p in parts.part_ids:
-        own = A.rows.partition.local(p).oid_to_lid - 1
-        assert np.array_equal(g.local(p)[own], e.local(p)[own]), f"part {p}: graph replay differs from eager"
-
-
-def test_eager_mul_after_failed_capture(pamd, monkeypatch):
-    """A graph capture whose table allocation fails (forced with
-    PA_TEST_FAIL_GRAPH_ALLOC, as on an out-of-memory device) raises, and
-    leaves no state behind: the eager mul! with a halo right
-    after it, and a later capture, both give the same bits as before."""
-    be = pamd.HIPBackend(devices=[0])
-    parts = be.get_part_ids((2, 2, 1))
-    A = pamd.drivers.stencil_operator(parts, (12, 11, 10), 27)
-    x = pamd.PVector.from_host(pamd.map_parts(
-        lambda s: np.random.default_rng(s.part).uniform(-1, 1, s.num_lids), A.cols.partition), A.cols)
-    y0, y1, y2 = (pamd.PVector.undef(A.rows) for _ in range(3))
-    pamd.mul_(y0, A, x)
-    monkeypatch.setenv("PA_TEST_FAIL_GRAPH_ALLOC", "1")
-    with pytest.raises(pamd._lib.PAError, match="graph capture"):
-        pamd.SpMVGraph(y1, A, x)
-    monkeypatch.delenv("PA_TEST_FAIL_GRAPH_ALLOC")
-    pamd.mul_(y1, A, x)
-    G = pamd.SpMVGraph(y2, A, x)
-    G()
-    h0, h1, h2 = y0.to_host(), y1.to_host(), y2.to_host()
-    for p in parts.part_ids:
-        own = A.rows.partition.local(p).oid_to_lid - 1
-        assert np.array_equal(h1.local(p)[own], h0.local(p)[own]), f"part {p}: eager mul! after the failed capture"
-        assert np.array_equal(h2.local(p)[own], h0.local(p)[own]), f"part {p}: graph after the failed capture"
 
 
 def test_spmv_rejects_partial_exchanger_arrays(be, pamd):
@@ -292,7 +201,7 @@ def test_mul_argument_cache_follows_objects(be, pamd, O):
 
 def test_context_knobs_override_process_defaults(pamd):
     """pa_ctx_tune: a context's knob applies to the calls its parts lead and
-    to nothing else; -1 drops it.  spmv_format 0 on one backend's contexts
+    to nothing else; None (PA_TUNE_DROP) drops it.  spmv_format 0 on one backend's contexts
     shows in its matrix's streamed bytes (int32 ids), not in another
     backend's, and the products stay bit-identical."""
     mk = lambda be: (be, be.get_part_ids((2, 1, 1)))
@@ -302,7 +211,7 @@ def test_context_knobs_override_process_defaults(pamd):
     A2 = pamd.drivers.stencil_operator(p2, N, 27)
     t1 = A1.values.local(1).traffic()["index_bytes"]
     for p in p1.part_ids:
-        assert b1.context(p).tune("spmv_format", 0) == -1
+        assert b1.context(p).tune("spmv_format", 0) is None
     assert A1.values.local(1).traffic()["index_bytes"] > t1, "override not applied to the context's calls"
     assert A2.values.local(1).traffic()["index_bytes"] == t1, "override leaked to another context"
     xs = {p: np.random.default_rng(p).uniform(-1, 1, A1.cols.partition.local(p).num_lids) for p in p1.part_ids}
@@ -315,8 +224,17 @@ def test_context_knobs_override_process_defaults(pamd):
     for p in p1.part_ids:
         assert np.array_equal(h1.local(p), h2.local(p))
     for p in p1.part_ids:
-        assert b1.context(p).tune("spmv_format", -1) == 0
+        assert b1.context(p).tune("spmv_format", None) == 0
     assert A1.values.local(1).traffic()["index_bytes"] == t1
+    # -1 is a value (spmv_xcd_chunk's auto), not a drop: a
+    # context can override a fixed process default back to auto
+    prev = pamd._lib.tune("spmv_xcd_chunk", 4)
+    try:
+        assert b1.context(1).tune("spmv_xcd_chunk", -1) is None
+        assert b1.context(1).tune("spmv_xcd_chunk", None) == -1
+        assert b1.context(1).tune("spmv_xcd_chunk", None) is None
+    finally:
+        pamd._lib.tune("spmv_xcd_chunk", prev)
     with pytest.raises(pamd._lib.PAError):
         b1.context(1).tune("spmv_format", 5)
     with pytest.raises(pamd._lib.PAError):

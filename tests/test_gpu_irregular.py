@@ -55,12 +55,12 @@ def _eq(O, got, ref):
     ((24, 22, 20), 8, np.complex64, 1), ((24, 22, 20), 8, np.float64, 0),
     (BIG[0], 8, np.float64, 1), (BIG[0], 8, np.float32, 1),       # C5 as benched: 8 parts of one device
     ((24, 22, 20), 12, np.float64, 1), ((24, 22, 20), 12, np.complex128, 0)])  # > PA_GROUP_MAX parts
-@pytest.mark.parametrize("tri16", [2, 0, 3])  # 3: the triple SELL with its other rows first (spmv_tri_order 1)
+@pytest.mark.parametrize("tri16", [1, 0, 3])  # 3: the triple SELL with its other rows first (spmv_tri_order 1)
 def test_irregular_spmv_bitexact(be, pamd, O, N, nparts, dtype, fmt, tri16):
-    if fmt == 0 and tri16 != 2:
+    if fmt == 0 and tri16 != 1:
         pytest.skip("spmv_format 0 runs every slice as int32 ids: the triple SELL is not used")
     prev = pamd._lib.tune("spmv_format", fmt)
-    prev_tri = pamd._lib.tune("spmv_tri16", min(tri16, 2))
+    prev_tri = pamd._lib.tune("spmv_tri16", min(tri16, 1))
     prev_ord = pamd._lib.tune("spmv_tri_order", 1 if tri16 == 3 else 0)
     # pattern slices from 40 % regular rows (default 70): the side SELL gets
     # the rest, so both the pattern and the side-row paths run
@@ -184,8 +184,8 @@ def test_grouped_launches_equal_per_part(be, pamd, dtype, fmt):
 def test_delta16_slices_equal_int32(be, pamd, O, dtype):
     """C5 Voronoi parts: most int32-column slices become delta16 slices (2 B
     column codes, pa_tune spmv_delta16), re-sliced into the triple SELL (one
-    code per consecutive column triple, spmv_tri16: Float64 / complex by
-    default); mul! is
+    code per consecutive column triple, spmv_tri16: slices of 1-2 rows per
+    lane); mul! is
     bit-identical with and without them and equals the oracle."""
     N, nparts = (40, 36, 32), 8
     parts = be.get_part_ids(nparts)
@@ -247,7 +247,7 @@ def test_launch_paths_equal_oracle(be, pamd, O, merge, direct, d16):
 
 
 @pytest.mark.parametrize("dtype", [np.float64, np.float32, np.complex64, np.complex128])
-@pytest.mark.parametrize("d16,tri16", [(1, 2), (1, 0), (0, 0)])
+@pytest.mark.parametrize("d16,tri16", [(1, 1), (1, 0), (0, 0)])
 @pytest.mark.parametrize("tail", [8, 0])
 def test_voronoi_column_loops_equal_oracle(be, pamd, O, dtype, d16, tri16, tail):
     """The int32 / delta16 / triple-SELL column loops (Float64: ids one

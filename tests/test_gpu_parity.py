@@ -218,32 +218,10 @@ def test_large_fe27_vs_c_oracle(be, pamd, O, fmt, tmp_path):
     assert np.array_equal(y.to_host().local(1), yref)
 
 
-@pytest.mark.parametrize("shape,N", [((2, 2, 2), (12, 11, 10)), ((1, 1, 1), (9, 8, 7))])
-def test_spmv_graph_replay(be, pamd, O, fmt, shape, N):
-    """mul! captured as a HIP graph and replayed equals the eager mul!
-    bit for bit, follows new values of x uploaded between replays, and
-    orders correctly with eager work on the parts' streams."""
-    parts = be.get_part_ids(shape)
-    A = pamd.drivers.stencil_operator(parts, N, 27)
-    rng = np.random.default_rng(SEED + 9)
-    x = pamd.PVector.from_host(pamd.map_parts(lambda s: rng.uniform(-1, 1, s.num_lids), A.cols.partition), A.cols)
-    y_g = pamd.PVector.undef(A.rows)
-    y_e = pamd.PVector.undef(A.rows)
-    G = pamd.SpMVGraph(y_g, A, x, 2.0, 0.0)
-    for it in range(3):
-        vals = {p: rng.uniform(-1, 1, A.cols.partition.local(p).num_lids) for p in parts.part_ids}
-        for dv, p in zip(x.values.parts, x.values.part_ids):
-            dv.upload(vals[p])
-        G()
-        pamd.mul_(y_e, A, x, 2.0, 0.0)
-        for p in parts.part_ids:
-            assert np.array_equal(y_g.to_host().local(p), y_e.to_host().local(p)), (it, p)
-
-
 def test_shared_stream_parts(pamd, O):
     """HIPBackend(share_streams=True): the parts on one device share one
-    stream pair; mul!, exchange!/assemble!, the graph replay and the device
-    CG give the same bits as with a stream pair per part."""
+    stream pair; mul!, exchange!/assemble! and the device CG give the same
+    bits as with a stream pair per part."""
     shape, N = (2, 2, 1), (12, 10, 9)
     out = {}
     for share in (False, True):
@@ -256,20 +234,16 @@ def test_shared_stream_parts(pamd, O):
         pamd.mul_(y, A, x)
         w = x.copy()
         pamd.assemble_(w)
-        g = pamd.PVector.undef(A.rows)
-        pamd.SpMVGraph(g, A, x)()
         b = x.copy()
         xs = pamd.PVector.undef(A.cols).fill_(0)
         h = []
         pamd.cg_(xs, A, b, reltol=0.0, maxiter=15, history=h, device=True)
         out[share] = ([v.copy() for v in y.to_host().parts], [v.copy() for v in w.to_host().parts],
-                      [v.copy() for v in g.to_host().parts], [v.copy() for v in xs.to_host().parts], h)
-    for k in range(4):
+                      [v.copy() for v in xs.to_host().parts], h)
+    for k in range(3):
         for a, b in zip(out[False][k], out[True][k]):
             assert np.array_equal(a, b), k
-    assert out[False][4] == out[True][4]
-    for a, b in zip(out[True][0], out[True][2]):
-        assert np.array_equal(a, b)
+    assert out[False][3] == out[True][3]
 
 
 @pytest.mark.parametrize("alpha", [1.0, -2.5])
@@ -489,31 +463,18 @@ def test_threaded_issue_reports_launch_failures(pamd, O):
 
 @pytest.mark.parametrize("kind,N,dtype", [(27, (40, 33, 9), np.float64), (7, (36, 30, 8), np.float64),
                                           (27, (34, 12, 10), np.float32), (27, (40, 9, 8), np.complex128)])
-@pytest.mark.parametrize("diag", [1, 0])
-def test_diagonal_only_rows_equal_oracle(be, pamd, O, kind, N, dtype, diag):
-    """Dirichlet rows (one entry, column == row) inside pattern slices
-    (pa_tune spmv_diag_rows): computed in their slice
-    from entry 0 (1) or as side rows (0); mul! with α/β, the fused dot of the
-    CG (mul_dot_) and β = 1 all give the oracle's bits, and with the knob on
-    no Dirichlet row is a side row."""
-    prev = pamd._lib.tune("spmv_diag_rows", diag)
-    try:
+def test_dirichlet_side_rows_equal_oracle(be, pamd, O, kind, N, dtype):
+    """Dirichlet rows (one entry, column == row) of pattern slices run as
+    side rows (computing them inside their slice lost,
+    profiles/r05/i/, and was removed in r06): mul! with α/β, the fused dot of
+    the CG (mul_dot_) and β = 1 all give the oracle's bits."""
+    if True:
         shape = (2, 1, 1)
         parts = be.get_part_ids(shape)
         A = pamd.drivers.stencil_operator(parts, N, kind, dtype)
         OA = O.stencil_problem(O.get_part_ids(shape), N, kind, dtype)
         info = [A.values.local(p).info() for p in parts.part_ids]
-        if diag:
-            # the interface rows (a ghost column off the pattern) stay side
-            # rows; every Dirichlet row left the side SELL
-            pamd._lib.tune("spmv_diag_rows", 0)
-            A0 = pamd.drivers.stencil_operator(parts, N, kind, dtype)
-            info0 = [A0.values.local(p).info() for p in parts.part_ids]
-            pamd._lib.tune("spmv_diag_rows", diag)
-            assert all(i["diag_rows"] > 0 and i["side_rows"] + i["diag_rows"] == i0["side_rows"]
-                       for i, i0 in zip(info, info0)), (info, info0)
-        else:
-            assert all(i["diag_rows"] == 0 and i["side_rows"] > 0 for i in info), info
+        assert all(i["side_rows"] > 0 for i in info), info
         rng = np.random.default_rng(SEED + 41)
         xs = {p: _rand(rng, A.cols.partition.local(p).num_lids, dtype) for p in parts.part_ids}
         ys = {p: _rand(rng, A.rows.partition.local(p).num_lids, dtype) for p in parts.part_ids}
@@ -540,20 +501,16 @@ def test_diagonal_only_rows_equal_oracle(be, pamd, O, kind, N, dtype, diag):
                 own = np.asarray(OA.cols.partition[p].oid_to_lid) - 1
                 ref += float(np.dot(xs[p][own], oyc.values[p][own]))
             assert abs(d - ref) <= 1e-12 * max(1.0, abs(ref)), (d, ref)
-    finally:
-        pamd._lib.tune("spmv_diag_rows", prev)
 
 
 @pytest.mark.parametrize("dtype", [np.float64, np.float32, np.complex128])
-@pytest.mark.parametrize("fork,tail", [(1, 0), (0, 0), (0, 1)])
-def test_side_fork_per_kind_launches_equal_oracle(be, pamd, O, dtype, fork, tail):
+@pytest.mark.parametrize("tail", [0, 1])
+def test_side_rows_per_kind_launches_equal_oracle(be, pamd, O, dtype, tail):
     """Per-kind launches of one part (spmv_merge_max below its slice count:
-    the headline's path) with the side rows on the comm stream beside the
-    pattern slices (spmv_side_fork 1), as the pattern launch's trailing waves
-    (spmv_side_tail 1) or as a launch after it (both 0): mul! with α/β, back
+    the headline's path) with the side rows as the pattern launch's trailing
+    waves (spmv_side_tail 1) or as a launch after it (0): mul! with α/β, back
     to back on changing x without a host sync, and the fused dot give the
     oracle's bits; the side rows exist (the domain-face Dirichlet rows)."""
-    p0 = pamd._lib.tune("spmv_side_fork", fork)
     p2 = pamd._lib.tune("spmv_side_tail", tail)
     p1 = pamd._lib.tune("spmv_merge_max", 4)
     try:
@@ -588,7 +545,6 @@ def test_side_fork_per_kind_launches_equal_oracle(be, pamd, O, dtype, fork, tail
     finally:
         pamd._lib.tune("spmv_merge_max", p1)
         pamd._lib.tune("spmv_side_tail", p2)
-        pamd._lib.tune("spmv_side_fork", p0)
 
 
 @pytest.mark.parametrize("chunk", [1, 3, 5, 16, 64, -1])

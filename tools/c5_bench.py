@@ -6,7 +6,7 @@ build also reports the parts' SpMV kernel time (HIP events on the parts'
 streams, summed over the parts).
 
     python tools/c5_bench.py [--n 128] [--parts 8] [--dtypes f64,f32,c128,c64]
-                             [--own-streams] [--group 0|1] [--graph]
+                             [--own-streams] [--group 0|1]
 """
 import argparse
 import json
@@ -27,7 +27,6 @@ ap.add_argument("--dtypes", default="f64,f32,c128,c64")
 ap.add_argument("--steps", type=int, default=20)
 ap.add_argument("--own-streams", action="store_true", help="a stream pair per part (share_streams=False)")
 ap.add_argument("--group", type=int, default=1, help="pa_tune spmv_group: 1 grouped launches (default), 0 per part")
-ap.add_argument("--graph", action="store_true", help="also time the HIP-graph replay (pamd.SpMVGraph)")
 ap.add_argument("--rccl", action="store_true", help="halo over RCCL grouped send/recv (HIPBackend(rccl=True))")
 ap.add_argument("--probe", action="store_true",
                 help="also report pa_hbm_probe's read rate over the same bytes per launch as one mul!")
@@ -88,32 +87,12 @@ for name in a.dtypes.split(","):
         km = kt[0]["interior_ms"] + kt[0]["boundary_ms"]
     else:
         km = sum(t["interior_ms"] + t["boundary_ms"] for t in kt)
-    t_graph = None
-    if a.graph:
-        ref = y.to_host()
-        g = pamd.SpMVGraph(y, A, x)
-        for _ in range(3):
-            g()
-        for p in parts.part_ids:
-            be.context(p).sync()
-        t0 = time.perf_counter()
-        for _ in range(a.steps):
-            g()
-        for p in parts.part_ids:
-            be.context(p).sync()
-        t_graph = (time.perf_counter() - t0) / a.steps
-        got = y.to_host()
-        for p in parts.part_ids:
-            own = A.rows.partition.local(p).oid_to_lid - 1
-            assert np.array_equal(got.local(p)[own], ref.local(p)[own]), "graph replay differs from eager mul!"
-        del g
     probe = pamd._lib.hbm_probe(0, int(info["format_bytes"]), 20)[0] if a.probe else None
     print(json.dumps({"config": f"C5 FE27 {a.n}^3 Voronoi {a.parts} parts on 1 GPU", "dtype": name, "halo": "rccl" if a.rccl else "device reads", "tune": a.tune,
                       "share_streams": not a.own_streams,
                       "spmv_group": a.group, "format_gbs_all_parts": round(info["format_bytes"] / t / 1e9, 1),
                       "format_gbs_kernels": round(info["format_bytes"] / km / 1e6, 1),
-                      "ms_per_mul": round(1e3 * t, 4),
-                      "ms_per_mul_graph": None if t_graph is None else round(1e3 * t_graph, 4), "gbs_algorithmic_all_parts": round(B / t / 1e9, 1),
+                      "ms_per_mul": round(1e3 * t, 4), "gbs_algorithmic_all_parts": round(B / t / 1e9, 1),
                       "kernel_ms_sum_over_parts": round(km, 4), "gbs_algorithmic_kernels": round(B / km / 1e6, 1),
                       "probe_read_gbs_same_bytes": None if probe is None else round(probe, 1),
                       "kernels_of_probe": None if probe is None else round(info["format_bytes"] / km / 1e6 / probe, 4),

@@ -4,11 +4,16 @@
 // per shape: host µs per launch (the enqueue alone, measured over back-to-back
 // launches with the device kept busy) and device µs per replay.
 //
-//   hipcc --offload-arch=gfx950 -O2 -o build/graph_cost tools/graph_cost.cpp
-//   build/graph_cost
+//   hipcc --offload-arch=gfx950 -O2 -o tools/graph_cost.bin tools/graph_cost.cpp
+//   tools/graph_cost.bin                      the shapes of profiles/r05/g/
+//   tools/graph_cost.bin K W R [--trace]      one shape (K kernels, W external
+//                                             waits, R external records); --trace
+//                                             prints a line after every HIP call
+//                                             of the capture
 #include <hip/hip_runtime.h>
 
 #include <chrono>
+#include <cstdlib>
 #include <cstdio>
 #include <vector>
 
@@ -24,6 +29,13 @@ __global__ void k_small(float* p, int n) {
       std::printf("{\"error\": \"%s: %s\"}\n", #x, hipGetErrorString(e_));       \
       return 1;                                                                  \
     }                                                                            \
+  } while (0)
+
+static bool g_trace = false;
+#define STEP(x)                                        \
+  do {                                                 \
+    CK(x);                                             \
+    if (g_trace) std::printf("ok %s\n", #x);           \
   } while (0)
 
 static double now_us() {
@@ -45,18 +57,26 @@ static int shape(int kernels, int waits, int records, int reps) {
   std::vector<hipEvent_t> ew(waits), er(records);
   for (auto& e : ew) CK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   for (auto& e : er) CK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-  for (auto& e : ew) CK(hipEventRecord(e, o));
-  CK(hipStreamSynchronize(o));
+  for (auto& e : ew) STEP(hipEventRecord(e, o));
+  STEP(hipStreamSynchronize(o));
   hipGraph_t g;
-  CK(hipStreamBeginCapture(s, hipStreamCaptureModeRelaxed));
-  for (auto& e : ew) CK(hipStreamWaitEvent(s, e, hipEventWaitExternal));
-  for (int k = 0; k < kernels; ++k) hipLaunchKernelGGL(k_small, dim3(n / 256), dim3(256), 0, s, d, n);
-  for (auto& e : er) CK(hipEventRecordWithFlags(e, s, hipEventRecordExternal));
-  CK(hipStreamEndCapture(s, &g));
+  STEP(hipStreamBeginCapture(s, hipStreamCaptureModeRelaxed));
+  for (auto& e : ew) STEP(hipStreamWaitEvent(s, e, hipEventWaitExternal));
+  for (int k = 0; k < kernels; ++k) {
+    hipLaunchKernelGGL(k_small, dim3(n / 256), dim3(256), 0, s, d, n);
+    STEP(hipGetLastError());
+  }
+  for (auto& e : er) STEP(hipEventRecordWithFlags(e, s, hipEventRecordExternal));
+  STEP(hipStreamEndCapture(s, &g));
+  if (g_trace) {
+    size_t nn = 0;
+    STEP(hipGraphGetNodes(g, nullptr, &nn));
+    std::printf("graph nodes %zu\n", nn);
+  }
   hipGraphExec_t x;
-  CK(hipGraphInstantiate(&x, g, nullptr, nullptr, 0));
-  for (int r = 0; r < 5; ++r) CK(hipGraphLaunch(x, s));
-  CK(hipStreamSynchronize(s));
+  STEP(hipGraphInstantiate(&x, g, nullptr, nullptr, 0));
+  for (int r = 0; r < 5; ++r) STEP(hipGraphLaunch(x, s));
+  STEP(hipStreamSynchronize(s));
   // host: enqueue reps launches back to back (events re-recorded on the
   // other stream before each, as the callers of the real graphs would)
   double t0 = now_us();
@@ -90,8 +110,12 @@ static int shape(int kernels, int waits, int records, int reps) {
   return 0;
 }
 
-int main() {
+int main(int argc, char** argv) {
   setvbuf(stdout, nullptr, _IONBF, 0);
+  if (argc >= 4) {
+    g_trace = argc >= 5;
+    return shape(std::atoi(argv[1]), std::atoi(argv[2]), std::atoi(argv[3]), 200);
+  }
   // more than one external event-wait node per capture ({2, 7, 1}) crashed
   // the HIP runtime of the box inside the capture (segfault, profiles/r05/g/)
   const int shapes[][3] = {{1, 0, 0}, {2, 0, 0}, {4, 0, 0}, {8, 0, 0}, {16, 0, 0}, {32, 0, 0}, {2, 1, 1}};

@@ -7,8 +7,8 @@ on cuda:0:
     transport (pull kernels on the comm streams, cross-stream events),
     interior and boundary phases — the code a process driving 8 GPUs runs;
     issued from the IssuePool's host threads (default) and, for comparison,
-    with issue_threads=0 from the calling thread; and replayed as one HIP
-    graph (HIPBackend(graph_mul=True));
+    with issue_threads=0 from the calling thread (the HIP-graph replay of
+    r05 is gone: 2.7-2.9 ms of device time against 0.94 eager, r06);
   * share_streams=True: the grouped launches of parts sharing one GPU;
   * rccl: HIPBackend(rccl=True), every halo segment through the grouped
     ncclSend/ncclRecv, the transport a one-part-per-GPU process posts.
@@ -114,8 +114,6 @@ def main():
                        "share_streams=False, issue_threads=0 (one part after the other on the calling thread)",
                        cg_iters=200))
     pamd._lib.tune("issue_threads", prev)
-    res.append(measure(pamd.HIPBackend(devices=[0], share_streams=False, graph_mul=True), args.n, args.k,
-                       "share_streams=False, graph_mul=True (the per-part call captured once, replayed as one graph)"))
     res.append(measure(pamd.HIPBackend(devices=[0], share_streams=True), args.n, args.k,
                        "share_streams=True (grouped launches)", cg_iters=200))
     res.append(measure(pamd.HIPBackend(devices=[0], rccl=True), args.n, args.k,
