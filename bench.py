@@ -110,6 +110,22 @@ def cpu_baseline_mpi(kind, dims, shape, seconds=12.0):
 PROBE_BYTES = 1 << 30
 
 
+def rccl_run_info(infos, world):
+    """The N > 1 line's proof of what ran, from every
+    rank's PartContext.comm_info(): the communicator's rank count
+    (ncclCommCount, min/max over the ranks: world on every rank), the
+    distinct devices (PCI bus ids) the ranks ran on, and the librccl each
+    rank resolved.  Fewer distinct devices than ranks is an error, not a
+    line."""
+    counts = [i["ranks"] for i in infos]
+    devices = sorted({i["pci"] for i in infos})
+    if len(devices) < world or min(counts) != world or max(counts) != world:
+        raise SystemExit(f"{world} ranks: communicator sizes {counts}, distinct devices {devices}")
+    return {"rccl_ranks": {"min": min(counts), "max": max(counts)}, "devices": devices,
+            "distinct_devices": len(devices), "librccl": sorted({i["librccl"] for i in infos}),
+            "rccl_version": sorted({i["rccl_version"] for i in infos})}
+
+
 # the kernels of one mul! step (SpMV slices, halo pull / pack / unpack)
 PMC_KERNELS = ("k_spmv_sell", "k_spmv_merged", "k_pull_", "k_pack", "k_unpack")
 
@@ -719,6 +735,13 @@ def main():
         rccl = {"bytes_sent_per_step_all_ranks": int(t[0].item()) // args.steps,
                 "bytes_recv_per_step_all_ranks": int(t[1].item()) // args.steps,
                 "gbs_all_ranks": round(float(t[1].item()) / elapsed / 1e9, 2)}
+        # what the communicator ran on: ncclCommCount per
+        # rank, the distinct devices of the ranks (PCI bus ids; the backend
+        # already refused a run with fewer distinct devices than ranks) and
+        # the librccl each rank resolved
+        infos = [None] * world
+        dist.all_gather_object(infos, ctxs[0].comm_info())
+        rccl.update(rccl_run_info(infos, world))
 
     # attribution (untimed calls): every local part's mul! phases, HIP events
     # on the stream the kernels run on, read after the last call (no

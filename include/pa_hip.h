@@ -168,6 +168,16 @@ int pa_comm_init_all(int n, pa_ctx* const ctx[]);
  * grouped ncclSend/ncclRecv carried for it; 0 when every segment moved by
  * device reads).                                                          */
 int pa_comm_stats(pa_ctx* ctx, int64_t* bytes_sent, int64_t* bytes_recv);
+/* What this part's communicator runs on, so that a multi-process run can
+ * show it (the reference asserts Comm_size == prod(nparts),
+ * MPIBackend.jl:11,17,61): *ranks = ncclCommCount (0: no communicator),
+ * *rank = ncclCommUserRank, the context's device ordinal and its PCI bus id
+ * (pci, >= 16 bytes: distinct GPUs of a node have distinct ids), the RCCL
+ * version (ncclGetVersion) and the path of the librccl the process resolved
+ * it from (lib, lib_len bytes; dladdr on ncclGetVersion: a host that loads
+ * another RCCL first, e.g. torch's bundled one, shows it here).          */
+int pa_comm_info(pa_ctx* ctx, int* ranks, int* rank, int* device, char* pci, int pci_len, int* version,
+                 char* lib, int lib_len);
 
 /* ---- index sets --------------------------------------------------------
  * Device copy of an AbstractIndexSet's oid_to_lid / hid_to_lid

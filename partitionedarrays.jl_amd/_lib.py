@@ -52,6 +52,8 @@ _SIGS = {
     "pa_comm_init_rank": [_p, C.c_char_p],
     "pa_comm_init_all": [C.c_int, C.POINTER(_p)],
     "pa_comm_stats": [_p, _i64p, _i64p],
+    "pa_comm_info": [_p, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int), C.c_char_p, C.c_int,
+                     C.POINTER(C.c_int), C.c_char_p, C.c_int],
     "pa_index_create": [_p, C.c_int64, C.c_int64, _i32p, C.c_int64, _i32p, C.POINTER(_p)],
     "pa_index_destroy": [_p],
     "pa_xchg_create": [_p, C.c_int32, _i32p, _i32p, _i32p, C.c_int32, _i32p, _i32p, _i32p, C.POINTER(_p)],

@@ -179,6 +179,19 @@ class DistributedBackend(AbstractBackend):
             raise ValueError(f"nparts={n} must equal the number of processes ({self.size})")
         return PData(self, [self.rank + 1], [self.rank + 1], shape)
 
+    def assert_distinct_devices(self, device_key):
+        """One GPU per process: every rank's device key (the PCI bus id of its
+        context's device) must differ from the others'.  A LOCAL_RANK wrapped
+        onto fewer visible devices would fold several ranks onto one GPU and
+        time another machine than the one reported (the
+        reference's Comm_size == prod(nparts) check, MPIBackend.jl:11,17,61,
+        has the same purpose).  Returns every rank's key, in rank order."""
+        keys = self._all_gather(device_key)
+        if len(set(keys)) < self.size:
+            raise RuntimeError(f"{self.size} ranks run on {len(set(keys))} distinct device(s) "
+                               f"{sorted(set(keys))}: one GPU per process is required")
+        return keys
+
     def _all_gather(self, obj):
         out = [None] * self.size
         self.dist.all_gather_object(out, obj, group=self.group)

@@ -2,6 +2,7 @@
 // include/pa_hip.h.  Contexts, index sets, the halo plan, the one-time
 // CSC → SELL conversion, the halo transport (device copies between parts of
 // one process, RCCL send/recv between processes) and the reductions' fold.
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
@@ -90,7 +91,7 @@ const Knobs kDefaults = {
     /*spmv_flags*/ 93, /*long_exact*/ 1, /*halo_pull*/ 1, /*spmv_delta16*/ 1, /*spmv_merge*/ 1,
     /*spmv_merge_max*/ 65536, /*cg_fuse*/ 2, /*halo_direct*/ 1, /*halo_transport*/ 0, /*spmv_group*/ 1,
     /*spmv_format*/ 1, /*pattern_min_pct*/ 0, /*issue_threads*/ 1, /*fault_inject*/ 0, /*spmv_xcd_chunk*/ -1, /*spmv_tri16*/ 1,
-    /*halo_barrier*/ 1, /*tri_order*/ 1, /*side_tail*/ 1, /*f32_rows*/ 0};
+    /*halo_barrier*/ 1, /*tri_order*/ 1, /*side_tail*/ 1, /*f32_rows*/ 0, /*wave_slices*/ 1};
 // COO → CSC → SELL on the device (pa_coo.hip)
 int coo_compress(int dtype, int index_bytes, int64_t m, int64_t ncols, int64_t n, const void* dI, const void* dJ,
                  const void* dV, int csr, int64_t* nu_out, int32_t** crow, int32_t** ccol, void** cval,
@@ -1312,6 +1313,9 @@ const Knob kKnobs[] = {
      "launches (big single parts) take C = the pattern's reach in blocks / 8, so that a block's z-neighbour "
      "plane runs on its XCD (FE27 256^3 F64: C = 16, -1.0..-1.2 %, profiles/r05/q,r/), merged launches keep "
      "the round robin (C2: C = 4 +1.4 %, r05/k/)"},
+    {"spmv_wave_slices", &Knobs::wave_slices, nullptr, 0, 16, 0,
+     "spmv_wave_slices: slices per SpMV wave: K > 0 = each wave runs K slices of its block's 4K, the next "
+     "slice's metadata loaded while the current one streams; 0 = auto"},
     {"fault_inject", &Knobs::fault_inject, nullptr, 0, 1, 0,
      "fault_inject: 1 = every job of a threaded issue (IssuePool) also issues an invalid kernel launch (tests "
      "of the error path; test_exception.jl's role), 0 = off (default)"},
@@ -1663,6 +1667,30 @@ int pa_comm_stats(pa_ctx* c, int64_t* bytes_sent, int64_t* bytes_recv) {
   CHECK_ARG(c && bytes_sent && bytes_recv, "null argument");
   *bytes_sent = c->rccl_bytes_sent;
   *bytes_recv = c->rccl_bytes_recv;
+  return 0;
+}
+
+int pa_comm_info(pa_ctx* c, int* ranks, int* rank, int* device, char* pci, int pci_len, int* version,
+                 char* lib, int lib_len) {
+  CHECK_ARG(c && ranks && rank && device && version, "null argument");
+  *ranks = 0;
+  *rank = -1;
+  if (c->comm) {
+    NCCLC(ncclCommCount((ncclComm_t)c->comm, ranks));
+    NCCLC(ncclCommUserRank((ncclComm_t)c->comm, rank));
+  }
+  *device = c->device;
+  if (pci && pci_len > 0) {
+    pci[0] = 0;
+    HIPC(hipDeviceGetPCIBusId(pci, pci_len, c->device));
+  }
+  NCCLC(ncclGetVersion(version));
+  if (lib && lib_len > 0) {
+    lib[0] = 0;
+    Dl_info di{};
+    if (dladdr(reinterpret_cast<void*>(&ncclGetVersion), &di) && di.dli_fname)
+      std::snprintf(lib, (size_t)lib_len, "%s", di.dli_fname);
+  }
   return 0;
 }
 

@@ -47,6 +47,17 @@ class PartContext:
         _lib.call("pa_comm_stats", self.h, C.byref(a), C.byref(b))
         return a.value, b.value
 
+    def comm_info(self):
+        """pa_comm_info: the communicator's rank count and this rank (0 / -1
+        without one), the device ordinal and PCI bus id, the RCCL version and
+        the librccl path the process resolved"""
+        ranks, rank, dev, ver = C.c_int(), C.c_int(), C.c_int(), C.c_int()
+        pci, lib = C.create_string_buffer(64), C.create_string_buffer(1024)
+        _lib.call("pa_comm_info", self.h, C.byref(ranks), C.byref(rank), C.byref(dev), pci, 64, C.byref(ver),
+                  lib, 1024)
+        return {"ranks": ranks.value, "rank": rank.value, "device": dev.value, "pci": pci.value.decode(),
+                "rccl_version": ver.value, "librccl": lib.value.decode()}
+
     def set_timing(self, on: bool):
         _lib.call("pa_ctx_set_timing", self.h, 1 if on else 0)
 
@@ -171,6 +182,8 @@ class HIPDistributedBackend(DistributedBackend):
         self.dist.broadcast_object_list(obj, src=0, group=self.group)
         _lib.call("pa_comm_init_rank", c.h, C.c_char_p(obj[0]))
         self.ctx = {part: c}
+        # one GPU per rank, or fail here (not a silently folded timing)
+        self.device_keys = self.assert_distinct_devices(c.comm_info()["pci"])
         return ids
 
     def context(self, part, nparts=None) -> PartContext:

@@ -88,3 +88,22 @@ def test_one_process_leg_runs_a_bounded_child_and_reports_failure(monkeypatch):
     assert "RANK" not in seen["env"] and "WORLD_SIZE" not in seen["env"]
     assert seen["kw"].get("timeout")
     assert "note" in out and "failed" in out["note"], out
+
+
+def test_rccl_run_info_proves_ranks_and_devices():
+    """config.rccl_halo of an N > 1 line: the
+    communicator size of every rank (ncclCommCount), the distinct devices
+    and the resolved librccl; a run whose ranks folded onto fewer GPUs, or
+    whose communicator is smaller than the world, fails instead of
+    reporting."""
+    import pytest
+    bench = _load_bench()
+    lib = "/opt/rocm/lib/librccl.so.1"
+    mk = lambda r, pci, n=2: {"ranks": n, "rank": r, "device": r, "pci": pci, "rccl_version": 22700, "librccl": lib}
+    out = bench.rccl_run_info([mk(0, "0000:05:00.0"), mk(1, "0000:15:00.0")], 2)
+    assert out["rccl_ranks"] == {"min": 2, "max": 2} and out["distinct_devices"] == 2
+    assert out["devices"] == ["0000:05:00.0", "0000:15:00.0"] and out["librccl"] == [lib]
+    with pytest.raises(SystemExit, match="distinct devices"):
+        bench.rccl_run_info([mk(0, "0000:05:00.0"), mk(1, "0000:05:00.0")], 2)
+    with pytest.raises(SystemExit, match="communicator sizes"):
+        bench.rccl_run_info([mk(0, "0000:05:00.0", 1), mk(1, "0000:15:00.0", 1)], 2)

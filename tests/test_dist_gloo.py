@@ -342,3 +342,45 @@ def test_cg_variant_agreement_over_ranks(world):
     assert res[0]["fuse_local"] is False and all(res[r]["fuse_local"] for r in range(1, world))
     assert {res[r]["fuse_agreed"] for r in range(world)} == {False}
     assert {res[r]["fuse_all"] for r in range(world)} == {True}
+
+
+def _worker_device_guard(rank, world, port, q):
+    try:
+        import torch.distributed as dist
+        dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+        import pamd
+        be = pamd.backends.DistributedBackend()
+        out = {"distinct": be.assert_distinct_devices(f"0000:{rank + 1:02x}:00.0")}
+        try:  # ranks 0 and 1 on the same device: every rank raises
+            be.assert_distinct_devices("0000:01:00.0" if rank < 2 else f"0000:{rank + 1:02x}:00.0")
+            out["folded"] = "no error"
+        except RuntimeError as e:
+            out["folded"] = str(e)
+        dist.barrier()
+        dist.destroy_process_group()
+        q.put((rank, out))
+    except Exception as e:  # pragma: no cover - surfaced by the parent
+        import traceback
+        q.put((rank, {"error": repr(e) + traceback.format_exc()}))
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_one_device_per_rank_guard(world):
+    """One GPU per process: HIPDistributedBackend
+    gathers every rank's device key (PCI bus id) and raises on every rank
+    when two ranks share a device (LOCAL_RANK wrapped onto fewer visible
+    GPUs), instead of timing a folded run; distinct keys come back in rank
+    order."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_worker_device_guard, args=(r, world, port, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = dict(q.get(timeout=240) for _ in range(world))
+    for p in ps:
+        p.join(timeout=60)
+    for r, out in res.items():
+        assert "error" not in out, out.get("error")
+        assert out["distinct"] == [f"0000:{k + 1:02x}:00.0" for k in range(world)]
+        assert "one GPU per process" in out["folded"], out["folded"]

@@ -212,6 +212,14 @@ def test_one_part_per_process_rccl_reductions(be_pull, pamd):
         (a1, a2, d1, n1, x1), (b1, b2, d2, n2, xx) = res
         assert a1 == b1 and a2 == b2 and d1 == d2 and n1 == n2
         assert np.array_equal(x1, xx)
+        # what the N > 1 bench line reports (config.rccl_halo): the
+        # communicator's size and rank, the device, the librccl resolved
+        bd = pamd.HIPDistributedBackend(device=0)
+        bd.get_part_ids(1)
+        info = bd.context(1).comm_info()
+        assert info["ranks"] == 1 and info["rank"] == 0 and info["device"] == 0, info
+        assert info["pci"] and bd.device_keys == [info["pci"]], (info, bd.device_keys)
+        assert info["rccl_version"] > 0 and "rccl" in info["librccl"], info
     finally:
         if own:
             dist.destroy_process_group()
