@@ -739,9 +739,9 @@ def main():
         # rank, the distinct devices of the ranks (PCI bus ids; the backend
         # already refused a run with fewer distinct devices than ranks) and
         # the librccl each rank resolved
-        infos = [None] * world
-        dist.all_gather_object(infos, ctxs[0].comm_info())
-        rccl.update(rccl_run_info(infos, world))
+        cinfos = [None] * world
+        dist.all_gather_object(cinfos, ctxs[0].comm_info())
+        rccl.update(rccl_run_info(cinfos, world))
 
     # attribution (untimed calls): every local part's mul! phases, HIP events
     # on the stream the kernels run on, read after the last call (no

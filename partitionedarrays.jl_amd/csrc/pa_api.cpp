@@ -91,7 +91,7 @@ const Knobs kDefaults = {
     /*spmv_flags*/ 93, /*long_exact*/ 1, /*halo_pull*/ 1, /*spmv_delta16*/ 1, /*spmv_merge*/ 1,
     /*spmv_merge_max*/ 65536, /*cg_fuse*/ 2, /*halo_direct*/ 1, /*halo_transport*/ 0, /*spmv_group*/ 1,
     /*spmv_format*/ 1, /*pattern_min_pct*/ 0, /*issue_threads*/ 1, /*fault_inject*/ 0, /*spmv_xcd_chunk*/ -1, /*spmv_tri16*/ 1,
-    /*halo_barrier*/ 1, /*tri_order*/ 1, /*side_tail*/ 1, /*f32_rows*/ 0, /*wave_slices*/ 1};
+    /*halo_barrier*/ 1, /*tri_order*/ 1, /*side_tail*/ 1, /*f32_rows*/ 0};
 // COO → CSC → SELL on the device (pa_coo.hip)
 int coo_compress(int dtype, int index_bytes, int64_t m, int64_t ncols, int64_t n, const void* dI, const void* dJ,
                  const void* dV, int csr, int64_t* nu_out, int32_t** crow, int32_t** ccol, void** cval,
@@ -924,6 +924,7 @@ struct TransportPlan {
   bool remote = false;
   bool pull = false;
   bool alt = false;  // the pull reads the senders' second buffers (pull_alt)
+  bool on_main = false;  // the pull kernel on the receiver's compute stream (halo_barrier 2)
   size_t S = 0;
   int dtype = 0, dir = 0, op = 0;
 };
@@ -977,12 +978,13 @@ int transport_local(int i, pa_xchg* const xg[], pa_vec* const v[], const Transpo
     void* const* bases = P.d_bases;
     // the pull's completion is ev_recvd (recorded with the launch)
     hipEvent_t ev = c->ev_recvd;
+    hipStream_t st = T.on_main ? c->s_main : c->s_comm;
     if (dir == 0)
       launch_pull(T.dtype, X->n_rcv_data, X->d_lids_rcv, X->plan_fwd, T.op, bid, elem, (const void* const*)bases,
-                  v[i]->d, c->s_comm, ev);
+                  v[i]->d, st, ev);
     else
       launch_pull(T.dtype, X->n_snd_data, X->d_lids_snd, X->plan_rev, T.op, bid, elem, (const void* const*)bases,
-                  v[i]->d, c->s_comm, ev);
+                  v[i]->d, st, ev);
     return 0;
   } else {
     // staging copies: receiver r, segment k from sender q (local), which
@@ -1303,19 +1305,17 @@ const Knob kKnobs[] = {
      "spmv_tri_order: the triple SELL's row order (matrices built afterwards): 1 = the other rows first "
      "(their slower waves start early, the launch ends on uniform triple slices; default: C5 F64 -1 %, "
      "Float32 triples -4..-7 %, profiles/r05/n/), 0 = rows of column triples first"},
-    {"halo_barrier", &Knobs::halo_barrier, nullptr, 0, 1, 0,
+    {"halo_barrier", &Knobs::halo_barrier, nullptr, 0, 2, 0,
      "halo_barrier: mul! over parts with their own stream pairs and local neighbours (one process driving "
-     "several GPUs): 1 = one pack barrier event per call and double-buffered send buffers (default), 0 = "
-     "per-neighbour event waits before every pack and every pull"},
+     "several GPUs): 1 = one pack barrier event per call and double-buffered send buffers (default), 2 = the "
+     "same with each part's pull on its compute stream after its interior slices (one runtime call less per "
+     "part), 0 = per-neighbour event waits before every pack and every pull"},
     {"spmv_xcd_chunk", &Knobs::spmv_xcd_chunk, nullptr, -1, 64, 0,
      "spmv_xcd_chunk: the SpMV launches' workgroups in runs of C consecutive blocks per XCD (C > 0; the x lines "
      "of neighbouring slices shared in one L2), 0 = the hardware's round robin, -1 = auto (default): per-kind "
      "launches (big single parts) take C = the pattern's reach in blocks / 8, so that a block's z-neighbour "
      "plane runs on its XCD (FE27 256^3 F64: C = 16, -1.0..-1.2 %, profiles/r05/q,r/), merged launches keep "
      "the round robin (C2: C = 4 +1.4 %, r05/k/)"},
-    {"spmv_wave_slices", &Knobs::wave_slices, nullptr, 0, 16, 0,
-     "spmv_wave_slices: slices per SpMV wave: K > 0 = each wave runs K slices of its block's 4K, the next "
-     "slice's metadata loaded while the current one streams; 0 = auto"},
     {"fault_inject", &Knobs::fault_inject, nullptr, 0, 1, 0,
      "fault_inject: 1 = every job of a threaded issue (IssuePool) also issues an invalid kernel launch (tests "
      "of the error path; test_exception.jl's role), 0 = off (default)"},
@@ -3373,7 +3373,10 @@ static int launch_phase(int phase, pa_mat* A, const void* x, void* y, const int3
 //   B  the leading part's s_comm waits for every part's pack and records
 //      ev_barrier — one wait per part instead of one per neighbour and part;
 //   C  per part: s_comm waits ev_barrier, pulls its ghosts from the senders'
-//      buffers b and records ev_recvd; s_main waits ev_recvd, boundary slices.
+//      buffers b and records ev_recvd; s_main waits ev_recvd, boundary slices
+//      (halo_barrier 2: s_main waits ev_barrier and pulls itself, after its
+//      interior slices, then the boundary slices: one runtime call less per
+//      part, the pull no longer beside the interior).
 // b alternates between d_buf_snd and d_buf_snd2 from one call to the next,
 // so a pack does not wait for the readers of the previous call's buffer: the
 // last reads of b before pack(k+2) are the pulls of call k, and every part
@@ -3385,7 +3388,7 @@ static int launch_phase(int phase, pa_mat* A, const void* x, void* y, const int3
 // About 8 HIP calls per part and call instead of ≈24.
 static int spmv_barrier_issue(int n, pa_vec* const x[], pa_xchg* const xg[], int dt, const TransportPlan& T,
                               bool threads, const std::function<int(int)>& interior,
-                              const std::function<int(int)>& boundary) {
+                              const std::function<int(int)>& boundary, bool pull_on_main) {
   uint64_t key = 1469598103934665603ull ^ (uint64_t)n;
   for (int i = 0; i < n; ++i) key = (key ^ xg[i]->id) * 1099511628211ull;
   bool chain = true;
@@ -3394,6 +3397,7 @@ static int spmv_barrier_issue(int n, pa_vec* const x[], pa_xchg* const xg[], int
   for (int i = 0; i < n; ++i) xg[i]->fast_key = 0;  // set again once the call is issued
   TransportPlan TB = T;
   TB.alt = parity == 1;
+  TB.on_main = pull_on_main;
   if (TB.alt) {  // the second send buffers and the pull tables reading them
     for (int i = 0; i < n; ++i)
       if (!xg[i]->d_buf_snd2 && xg[i]->n_snd_data) {
@@ -3426,7 +3430,8 @@ static int spmv_barrier_issue(int n, pa_vec* const x[], pa_xchg* const xg[], int
   auto stepC = [&](int i) -> int {
     pa_ctx* c = xg[i]->ctx;
     HIPC(hipSetDevice(c->device));
-    if (i) HIPC(hipStreamWaitEvent(c->s_comm, c0->ev_barrier, 0));
+    if (pull_on_main) HIPC(hipStreamWaitEvent(c->s_main, c0->ev_barrier, 0));
+    else if (i) HIPC(hipStreamWaitEvent(c->s_comm, c0->ev_barrier, 0));
     if (transport_local(i, xg, x, TB)) return -1;
     return boundary(i);
   };
@@ -3493,6 +3498,7 @@ static int spmv_impl(int n, pa_mat* const A[], pa_vec* const y[], const pa_index
   const bool has_alpha = !scalar_is(dt, alpha, 1.0);
   const int bmode = scalar_is(dt, beta, 0.0) ? 0 : (scalar_is(dt, beta, 1.0) ? 1 : 2);
   bool pulled = false;
+  bool pulled_on_main = false;  // the pull ran on s_main itself (halo_barrier 2): no ev_recvd wait
   // timing: the events of this call (slot tn of each timed context); the
   // grouped path brackets all parts with the same launches: part 1 of the
   // call records them once
@@ -3543,7 +3549,7 @@ static int spmv_impl(int n, pa_mat* const A[], pa_vec* const y[], const pa_index
     pa_ctx* c = A[i]->ctx;
     HIPC(hipSetDevice(c->device));
     if (any_x) {
-      HIPC(hipStreamWaitEvent(c->s_main, c->ev_recvd, 0));
+      if (!pulled_on_main) HIPC(hipStreamWaitEvent(c->s_main, c->ev_recvd, 0));
       if (!pulled)
         launch_unpack(dt, xg[i]->n_rcv_data, xg[i]->d_lids_rcv, xg[i]->plan_fwd, PA_REPLACE,
                       xg[i]->d_buf_rcv, x[i]->d, c->s_main);
@@ -3592,7 +3598,8 @@ static int spmv_impl(int n, pa_mat* const A[], pa_vec* const y[], const pa_index
   if (any_x && transport_plan(n, xg, dt, 0, PA_REPLACE, x, &T)) return -1;
   if (any_x && distinct && knobs().halo_barrier && T.pull && !T.remote) {
     pulled = true;
-    if (spmv_barrier_issue(n, x, xg, dt, T, threads, interior, boundary)) return -1;
+    pulled_on_main = knobs().halo_barrier == 2;
+    if (spmv_barrier_issue(n, x, xg, dt, T, threads, interior, boundary, pulled_on_main)) return -1;
   } else if (threads && !(any_x && T.remote)) {
     if (any_x) {
       const LocalSet L = local_set(n, xg);

@@ -356,7 +356,6 @@ struct Knobs {
   int tri_order;         // triple SELL row order: 0 triple rows first, 1 the other rows first (build_triple_sell)
   int side_tail;         // per-kind launches: the side rows as the trailing waves of the pattern launch
   int f32_rows;          // Float32 SELL rows per lane (matrices built afterwards): 4 (16 B packs), 2 (8 B), 0 auto
-  int wave_slices;       // slices per SpMV wave (pa_spmv.hip spmv_run): K > 0 fixed, 0 auto
 };
 // the knobs of the call running on this thread (outside a call: a snapshot
 // of the process defaults)

@@ -137,7 +137,6 @@ struct SpmvArgs {
   PA_GLB T* xacc;
   const PA_GLB CGState* cg;
   int xcd_chunk;            // xcd_block (the k_spmv_sell / _group launches; merged: a kernel argument)
-  int spw;                  // k_spmv_sell: slices per wave (spmv_run; _group / merged: their own field / argument)
 };
 
 template <typename T> struct DAcc { using type = double; };
@@ -818,98 +817,18 @@ __device__ __forceinline__ void cg_rows_update(const SpmvArgs<T>& a, const XS& x
 // main structure (no rowmap) write u_new and the deferred x update of all
 // their rows (whoever computes the row's product); once the solve is done a
 // wave only applies a pending x update.
-// The per-slice metadata a wave needs before its stream can start: the
-// slice id (through the launch's list), its slot offset and length word,
-// the lane's mask word (pattern slices: regular rows; int32 slices with long
-// rows: the rows handed to the long-row kernel), the ghost base (delta16 /
-// triple SELL), the layout kind (Float32 int32 launches over interleaved
-// slices) and the lane's rows' oids (row-mapped structures).  Loaded by
-// slice_meta with VECTOR loads, every lane the same address for the
-// wave-uniform words: a multi-slice wave (spmv_run) issues the next slice's
-// metadata before streaming the current one, and vector loads complete in
-// order, so the stream's own waits never wait for them early (a scalar
-// load would: lgkmcnt counts the scalar loads of the slice's patterns and
-// arguments too).  The uniform words are read back (readfirstlane) only in
-// spmv_slice, after the previous slice's stream.  VERDICT r05 item 1.
-template <int R>
-struct SliceMeta {
-  int64_t s;
-  int64_t off;      // (per lane, all lanes equal)
-  int32_t lraw;     // (per lane, all lanes equal)
-  int32_t aux;      // PK 3/4: ghost base; PK 0: sflags (long rows)
-  int32_t ilv;      // PK 0, 4 rows per lane: the slice's kind (3 = interleaved rows; a.ilv)
-  uint64_t mw;      // PK 1: mask word; PK 0 with sflags: long-row mask word
-  int32_t rmap[R];  // a.rowmap: the lane's rows' oids (0 past the structure's rows)
-};
-
-// an opaque 0 in a VGPR: p[lane0()] is a per-lane (vector) load of p[0]
-__device__ __forceinline__ int lane0() {
-  int z = 0;
-  asm volatile("" : "+v"(z));
-  return z;
-}
-__device__ __forceinline__ int32_t rfl32(int32_t v) { return __builtin_amdgcn_readfirstlane(v); }
-__device__ __forceinline__ int64_t rfl64(int64_t v) {
-  const int lo = __builtin_amdgcn_readfirstlane((int)(v & 0xffffffffll));
-  const int hi = __builtin_amdgcn_readfirstlane((int)(v >> 32));
-  return ((int64_t)hi << 32) | (uint32_t)lo;
-}
-
-// the slice's row layout: blocked (the lane's rows lane*R + r) or, for
-// delta16 slices, interleaved (rows r*64 + lane; k_delta16)
-template <int R, int PK>
-__device__ __forceinline__ bool slice_interleaved(int32_t ilv_kind) {
-  if constexpr (PK == 3) return kInterleaveD16<R>;
-  if constexpr (PK == 4) return true;
-  if constexpr (PK == 0 && kInterleaveD16<R>) return ilv_kind == 3;
-  return false;
-}
-
-template <typename T, int R, int PK>
-__device__ __forceinline__ void slice_meta(const SpmvArgs<T>& a, const int64_t w, SliceMeta<R>& m) {
-  constexpr int H = 64 * R;
-  const int lane = threadIdx.x & 63;
-  const int z = lane0();
-  const int64_t s = a.list ? (int64_t)rfl32(a.list[w + z]) : w;  // (the list entry: needed for the addresses below)
-  m.s = s;
-  m.off = a.soff[s + z];
-  m.lraw = a.slen[s + z];
-  m.aux = 0;
-  m.ilv = 0;
-  m.mw = 0;
-  if constexpr (PK == 1) m.mw = a.mask[s * (H / 64) + (lane * R) / 64];
-  if constexpr (PK == 3 || PK == 4) m.aux = a.gbase[s + z];
-  if constexpr (PK == 0) {
-    if (a.sflags) {
-      m.aux = a.sflags[s + z];
-      m.mw = a.lmask[s * (H / 64) + (lane * R) / 64];
-    }
-    if constexpr (kInterleaveD16<R>) {
-      if (a.ilv) m.ilv = a.ilv[s + z];
-    }
-  }
-#pragma unroll
-  for (int r = 0; r < R; ++r) m.rmap[r] = 0;
-  if constexpr (PK == 0 || PK == 4) {
-    if (a.rowmap) {  // side SELL (blocked) / triple SELL (interleaved)
-      constexpr bool il = PK == 4;
-      const int64_t row0 = s * H + (il ? (int64_t)lane : (int64_t)lane * R);
-#pragma unroll
-      for (int r = 0; r < R; ++r) {
-        const int64_t i = row0 + (int64_t)r * (il ? 64 : 1);
-        if (i < a.nrows) m.rmap[r] = a.rowmap[i];
-      }
-    }
-  }
-}
-
 template <typename T, int R, bool ALPHA, int BMODE, int U, int PK, bool SH = false, bool XV = false>
-__device__ __forceinline__ void spmv_slice(const SpmvArgs<T>& a, const SliceMeta<R>& m) {
+__device__ __forceinline__ void spmv_wave(const SpmvArgs<T>& a, const int64_t w) {
   constexpr bool PAT = PK == 1;  // implied columns (mask of regular rows)
   constexpr int H = 64 * R;
   const int lane = threadIdx.x & 63;
-  const int64_t s = m.s;
-  const bool il = slice_interleaved<R, PK>(PK == 0 && kInterleaveD16<R> ? rfl32(m.ilv) : 0);
+  const int64_t s = a.list ? (int64_t)a.list[w] : w;
+  // the slice's row layout: blocked (the lane's rows lane*R + r) or, for
+  // delta16 slices, interleaved (rows r*64 + lane; k_delta16)
+  bool il = false;
+  if constexpr (PK == 3) il = kInterleaveD16<R>;
+  if constexpr (PK == 4) il = true;
+  if constexpr (PK == 0 && kInterleaveD16<R>) il = a.ilv && a.ilv[s] == 3;
   const int rs = il ? 64 : 1;
   const int64_t row0 = s * H + (il ? (int64_t)lane : (int64_t)lane * R);  // the lane's first row
   XSrc<T, XV> xs;
@@ -930,27 +849,29 @@ __device__ __forceinline__ void spmv_slice(const SpmvArgs<T>& a, const SliceMeta
   } else {
     xs.x = (const T*)a.x;
   }
-  const int64_t off = rfl64(m.off);
-  const int32_t lraw = rfl32(m.lraw);
+  const int64_t off = a.soff[s];
+  const int32_t lraw = a.slen[s];
   // pattern slices: len | tri << 8 | pattern id << 9 (dedup_patterns); triple SELL: len | kTriSlice
   const int len = PAT ? (lraw & 0xff) : (PK == 4 ? (lraw & (kTriSlice - 1)) : lraw);
   bool ok[R];
   if (PAT) {
+    const uint64_t m = a.mask[s * (H / 64) + (lane * R) / 64];
 #pragma unroll
-    for (int r = 0; r < R; ++r) ok[r] = ((m.mw >> ((lane * R + r) & 63)) & 1ull) && (row0 + r < a.nrows);
+    for (int r = 0; r < R; ++r) ok[r] = ((m >> ((lane * R + r) & 63)) & 1ull) && (row0 + r < a.nrows);
   } else {
 #pragma unroll
     for (int r = 0; r < R; ++r) ok[r] = row0 + (int64_t)r * rs < a.nrows;
-    if (PK == 0 && a.sflags && rfl32(m.aux)) {  // rows handed to the long-row kernel (blocked slices only)
+    if (a.sflags && a.sflags[s]) {  // rows handed to the long-row kernel (blocked slices only)
+      const uint64_t m = a.lmask[s * (H / 64) + (lane * R) / 64];
 #pragma unroll
-      for (int r = 0; r < R; ++r) ok[r] = ok[r] && !((m.mw >> ((lane * R + r) & 63)) & 1ull);
+      for (int r = 0; r < R; ++r) ok[r] = ok[r] && !((m >> ((lane * R + r) & 63)) & 1ull);
     }
   }
   int64_t orow[R];
 #pragma unroll
   for (int r = 0; r < R; ++r) {
     const int64_t i = row0 + (int64_t)r * rs;
-    orow[r] = ok[r] ? (a.rowmap ? (int64_t)m.rmap[r] : i) : 0;
+    orow[r] = ok[r] ? (a.rowmap ? (int64_t)a.rowmap[i] : i) : 0;
   }
 
   T acc[R];
@@ -988,7 +909,7 @@ __device__ __forceinline__ void spmv_slice(const SpmvArgs<T>& a, const SliceMeta
     }
   } else if constexpr (PK == 3) {
     const S16Pack<R>* __restrict__ cp = reinterpret_cast<const S16Pack<R>*>(a.col16 + off) + lane;
-    const int32_t gb = rfl32(m.aux);
+    const int32_t gb = a.gbase[s];
     int32_t rw[R];  // the rows the codes are relative to
 #pragma unroll
     for (int r = 0; r < R; ++r) rw[r] = (int32_t)row0 + r * kD16RowStride<R>;
@@ -998,7 +919,7 @@ __device__ __forceinline__ void spmv_slice(const SpmvArgs<T>& a, const SliceMeta
     // triple SELL (rows through the row map, interleaved): tri slices carry
     // one code per triple, the others one per entry (rows_d16)
     const S16Pack<R>* __restrict__ cp = reinterpret_cast<const S16Pack<R>*>(a.col16 + off) + lane;
-    const int32_t gb = rfl32(m.aux);
+    const int32_t gb = a.gbase[s];
     int32_t rw[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) rw[r] = (int32_t)orow[r];
@@ -1077,52 +998,22 @@ __device__ __forceinline__ int64_t xcd_block(int chunk) {
   return (b / G) * G + (b % 8) * chunk + (b / 8) % chunk;
 }
 
-// A wave's run of slices (pa_tune "spmv_wave_slices" K, VERDICT r05 item
-// 1): a block owns 4K consecutive work items and its wave j computes items
-// w = first + j, w + 4, …, w + 4(K−1) (< a.nwork), so the block's 4 waves
-// always stream 4 neighbouring slices, as the one-slice launch does; each
-// wave issues the next slice's metadata (slice_meta) before it streams the
-// current one, and pays the launch's start (kernel arguments, the XCD
-// block map, a group's part search) once per K slices.  No atomics: the
-// assignment is static.  K = 1: one slice per wave.  Every slice is
-// computed by exactly the code of the one-slice wave: results are
-// bit-identical for every K.
-template <typename T, int R, bool ALPHA, int BMODE, int U, int PK, bool SH = false, bool XV = false>
-__device__ __forceinline__ void spmv_run(const SpmvArgs<T>& a, int64_t w, const int K) {
-  if (w >= a.nwork) return;
-  SliceMeta<R> m;
-  slice_meta<T, R, PK>(a, w, m);
-  for (int i = 1;; ++i) {
-    const int64_t wn = w + 4;
-    const bool more = i < K && wn < a.nwork;
-    SliceMeta<R> mn;
-    if (more) slice_meta<T, R, PK>(a, wn, mn);
-    spmv_slice<T, R, ALPHA, BMODE, U, PK, SH, XV>(a, m);
-    if (!more) break;
-    w = wn;
-    m = mn;
-  }
-}
-
-__device__ __forceinline__ int wave_in_block() { return __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)); }
-
 template <typename T, int R, bool ALPHA, int BMODE, int U, int PK, bool SH = false, bool XV = false>
 __global__ __launch_bounds__(256) void k_spmv_sell(SpmvArgs<T> a) {
-  const int K = a.spw;
-  spmv_run<T, R, ALPHA, BMODE, U, PK, SH, XV>(a, xcd_block(a.xcd_chunk) * 4 * K + wave_in_block(), K);
+  const int64_t w = xcd_block(a.xcd_chunk) * 4 + (threadIdx.x >> 6);
+  if (w >= a.nwork) return;
+  spmv_wave<T, R, ALPHA, BMODE, U, PK, SH, XV>(a, w);
 }
 
 // Several parts of one device in ONE launch (parts sharing a stream pair):
-// the work items of part p start at item start[p] of the grid (a multiple
-// of the 4·spw items of a block, so that a block's items belong to one
-// part), so a mul! over P small parts fills the GPU once instead of P
-// times and costs one launch per phase instead of P.  Each wave computes
-// exactly what the per-part launch computes (same slices, same order).
+// the work items of part p are [start[p], start[p+1]) of the grid's waves,
+// so a mul! over P small parts fills the GPU once instead of P times and
+// costs one launch per phase instead of P.  Each wave computes exactly what
+// the per-part launch computes (same slice, same order).
 template <typename T>
 struct SpmvGroup {
   int np;
   int tail0;  // entries [tail0, np) are side rows (int32 columns, <= 8 entries), TAIL kernels only
-  int spw;    // slices per wave (spmv_run)
   int64_t start[PA_GROUP_MAX + 1];
   SpmvArgs<T> a[PA_GROUP_MAX];
 };
@@ -1137,25 +1028,23 @@ template <typename T, int R, bool ALPHA, int BMODE, int U, int PK, bool SH = fal
           bool TAIL = false>
 __global__ __launch_bounds__(256) void k_spmv_sell_group(const SpmvGroup<T> g) {
   // wave-uniform: the part's arguments are read with scalar loads
-  const int K = g.spw;
-  const int64_t b0 = xcd_block(g.a[0].xcd_chunk) * 4 * (int64_t)K;  // the block's first item
-  if (b0 >= g.start[g.np]) return;
+  const int64_t w = xcd_block(g.a[0].xcd_chunk) * 4 + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  if (w >= g.start[g.np]) return;
   int p = 0;
-  while (p + 1 < g.np && b0 >= g.start[p + 1]) ++p;
+  while (p + 1 < g.np && w >= g.start[p + 1]) ++p;
   p = __builtin_amdgcn_readfirstlane(p);
-  const int64_t w = b0 - g.start[p] + wave_in_block();
   if constexpr (TAIL) {
     if (p >= g.tail0) {
-      spmv_run<T, R, ALPHA, BMODE, U, 0, true, false>(g.a[p], w, K);
+      spmv_wave<T, R, ALPHA, BMODE, U, 0, true, false>(g.a[p], w - g.start[p]);
       return;
     }
   }
-  spmv_run<T, R, ALPHA, BMODE, U, PK, SH, XV>(g.a[p], w, K);
+  spmv_wave<T, R, ALPHA, BMODE, U, PK, SH, XV>(g.a[p], w - g.start[p]);
 }
 
 template <typename T, int R, bool ALPHA, int BMODE, int PAT>
 static void launch_group_t(const SpmvGroup<T>& g, hipStream_t st) {
-  const int64_t blocks = g.start[g.np] / (4 * (int64_t)g.spw);
+  const int64_t blocks = (g.start[g.np] + 3) / 4;
   if (blocks == 0) return;
   bool sh = (knobs().spmv_flags & SPMV_SHORT) != 0;
   for (int i = 0; i < g.np && i < g.tail0; ++i) sh = sh && g.a[i].maxlen <= 8;
@@ -1206,18 +1095,9 @@ static void launch_group_ab(const SpmvGroup<T>& g, bool has_alpha, int bmode, hi
   }
 }
 
-// Slices per wave of a launch of `items` work items (pa_tune
-// "spmv_wave_slices": K > 0 fixed, 0 auto), and the XCD run length in
-// blocks of 4K items that keeps the one-slice launch's runs of `chunk`
-// 4-item blocks
-int wave_slices(int64_t items);
-static int chunk_for(int chunk, int K) { return chunk > 0 ? std::max(1, chunk / K) : chunk; }
-
 template <typename T, int R, bool ALPHA, int BMODE, int PAT>
-static void launch_t(SpmvArgs<T> a, hipStream_t st) {
-  a.spw = wave_slices(a.nwork);
-  a.xcd_chunk = chunk_for(a.xcd_chunk, a.spw);
-  const int64_t blocks = (a.nwork + 4 * a.spw - 1) / (4 * a.spw);
+static void launch_t(const SpmvArgs<T>& a, hipStream_t st) {
+  const int64_t blocks = (a.nwork + 3) / 4;
   if (blocks == 0) return;
   if constexpr (!ALPHA && BMODE == 0 && PAT != 4) {
     if (a.cg) {  // the device CG's fused u update
@@ -1274,7 +1154,6 @@ static SpmvArgs<T> make_args(int which, int64_t nwork, const int32_t* list, cons
   a.beta = *(const T*)beta;
   a.flags = knobs().spmv_flags | (A->csr ? SPMV_PRODA : 0);
   a.xcd_chunk = knobs().spmv_xcd_chunk >= 0 ? knobs().spmv_xcd_chunk : A->xcd_auto;
-  a.spw = 1;
   a.maxlen = which == 0   ? A->maxlen_pat
              : which == 2 ? A->maxlen_side
              : which == 1 ? ((knobs().spmv_format == 1 && A->has_pat) ? A->maxlen_pm_int : A->maxlen_all)
@@ -1342,12 +1221,8 @@ static void group_which(int which, int np, const SpmvPart* parts, bool has_alpha
   // which 6: pattern entries followed by side-row entries (SpmvPart::side;
   // the caller passes at most PA_GROUP_MAX entries, pattern ones first): one
   // TAIL launch
-  int64_t items = 0;
-  for (int i = 0; i < np; ++i) items += std::max<int64_t>(parts[i].nwork, 0);
-  const int K = wave_slices(items);
   SpmvGroup<T> g{};
   g.tail0 = PA_GROUP_MAX + 1;
-  g.spw = K;
   auto flush = [&]() {
     if (g.np == 0) return;
     if (which == 0 || which == 6) launch_group_ab<T, R, 1>(g, has_alpha, bmode, st);
@@ -1358,7 +1233,6 @@ static void group_which(int which, int np, const SpmvPart* parts, bool has_alpha
     else launch_group_ab<T, R, 0>(g, has_alpha, bmode, st);
     g = SpmvGroup<T>{};
     g.tail0 = PA_GROUP_MAX + 1;
-    g.spw = K;
   };
   for (int i = 0; i < np; ++i) {
     const SpmvPart& q = parts[i];
@@ -1368,9 +1242,7 @@ static void group_which(int which, int np, const SpmvPart* parts, bool has_alpha
     const int32_t* list = q.list;
     if ((knobs().spmv_flags & SPMV_IDLIST) && list && kind != 2 && kind != 5 && q.nwork == q.A->nslices) list = nullptr;
     g.a[g.np] = make_args<T>(kind, q.nwork, list, q.A, q.x, q.y, q.ymap, alpha, beta, q.dotp, &q);
-    g.a[g.np].xcd_chunk = chunk_for(g.a[g.np].xcd_chunk, K);
-    // (each part's items start on a block boundary: its blocks' waves see one part)
-    g.start[g.np + 1] = g.start[g.np] + (q.nwork + 4 * K - 1) / (4 * K) * (4 * K);
+    g.start[g.np + 1] = g.start[g.np] + q.nwork;
     if (++g.np == PA_GROUP_MAX) flush();
   }
   flush();
@@ -1453,45 +1325,42 @@ constexpr int kMergeMax = 48;
 template <typename T>
 struct SpmvTable {
   int n;
-  int spw;  // slices per wave: entries start on blocks of 4·spw items (part of the cache key, like the map)
   int pk[kMergeMax];
   int64_t start[kMergeMax + 1];
   SpmvArgs<T> a[kMergeMax];
 };
 
-// The block -> entry map that follows a merged table in device memory (one
-// byte per block, at the 16 B boundary after the table's n used entries;
-// every entry starts on a block boundary): a wave finds its entry with one
-// load instead of a binary search over the table's start offsets (log2(n)
-// dependent loads ahead of every wave's stream; C5's tables hold 20-40
-// entries)
+// The wave -> entry map that follows a merged table in device memory (one
+// byte per wave, at the 16 B boundary after the table's n used entries):
+// a wave finds its entry with one load instead of a binary search over the
+// table's start offsets (log2(n) dependent loads ahead of every wave's
+// stream; C5's tables hold 20-40 entries)
 template <typename T>
 __host__ __device__ constexpr size_t merged_map_offset(int n) {
   return (offsetof(SpmvTable<T>, a) + (size_t)n * sizeof(SpmvArgs<T>) + 15) & ~(size_t)15;
 }
 
 template <typename T, int R, bool ALPHA, int BMODE, int U, bool SH, bool XV = false>
-__device__ __forceinline__ void merged_wave(const SpmvTable<T>* __restrict__ tab, int n, int64_t blocks, int xc,
-                                            int K) {
-  // n, the block count and K come as kernel arguments (with the kernarg
-  // load, not dependent table loads ahead of the search)
-  const int64_t b = xcd_block(xc);
-  if (b >= blocks) return;
+__device__ __forceinline__ void merged_wave(const SpmvTable<T>* __restrict__ tab, int n, int64_t waves, int xc) {
+  // n and the wave count come as kernel arguments (with the kernarg load, not
+  // two dependent table loads ahead of the search)
+  const int64_t w = xcd_block(xc) * 4 + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  if (w >= waves) return;
   const uint8_t* __restrict__ map = reinterpret_cast<const uint8_t*>(tab) + merged_map_offset<T>(n);
-  const int p = __builtin_amdgcn_readfirstlane((int)map[b]);
+  const int p = __builtin_amdgcn_readfirstlane((int)map[w]);
   const int pk = __builtin_amdgcn_readfirstlane(tab->pk[p]);
-  const int64_t lw = b * 4 * K - tab->start[p] + wave_in_block();
+  const int64_t lw = w - tab->start[p];
   const SpmvArgs<T>& a = tab->a[p];
-  if (pk == 1) spmv_run<T, R, ALPHA, BMODE, U, 1, SH, XV>(a, lw, K);
-  else if (pk == 3) spmv_run<T, R, ALPHA, BMODE, U, 3, SH, XV>(a, lw, K);
+  if (pk == 1) spmv_wave<T, R, ALPHA, BMODE, U, 1, SH, XV>(a, lw);
+  else if (pk == 3) spmv_wave<T, R, ALPHA, BMODE, U, 3, SH, XV>(a, lw);
   else if (pk == 4) {
     // the triple SELL never runs in the short-row (make_args: maxlen >= 9)
     // or fused-u kernels (pa_cg_solve_all: no fused update with it): their
     // registers stay those of the other kinds
     // (and slices of R <= 2 rows per lane only: build_triple_sell)
-    if constexpr (!SH && !XV && R <= 2) spmv_run<T, R, ALPHA, BMODE, U, 4, SH, XV>(a, lw, K);
+    if constexpr (!SH && !XV && R <= 2) spmv_wave<T, R, ALPHA, BMODE, U, 4, SH, XV>(a, lw);
   }
-  else spmv_run<T, R, ALPHA, BMODE, U, 0, SH, XV>(a, lw, K);
+  else spmv_wave<T, R, ALPHA, BMODE, U, 0, SH, XV>(a, lw);
 }
 
 // No occupancy cap: amdgpu_waves_per_eu(4) (F32 134 -> 128 VGPRs, a small
@@ -1499,8 +1368,8 @@ __device__ __forceinline__ void merged_wave(const SpmvTable<T>* __restrict__ tab
 // (profiles/r02/stream/ab_waves4.txt).
 template <typename T, int R, bool ALPHA, int BMODE, int U, bool SH, bool XV = false>
 __global__ __launch_bounds__(256) void k_spmv_merged(const SpmvTable<T>* __restrict__ tab, int n,
-                                                         int64_t blocks, int xc, int K) {
-  merged_wave<T, R, ALPHA, BMODE, U, SH, XV>(tab, n, blocks, xc, K);
+                                                         int64_t waves, int xc) {
+  merged_wave<T, R, ALPHA, BMODE, U, SH, XV>(tab, n, waves, xc);
 }
 
 // F64 short rows (FD7): 5 waves per SIMD instead of 4 (96 VGPRs instead of
@@ -1509,25 +1378,25 @@ __global__ __launch_bounds__(256) void k_spmv_merged(const SpmvTable<T>* __restr
 // F32/C64 (R = 4 / complex: ~200 spills) nor for longer rows (FE27: -10 %).
 template <typename T, int R, bool ALPHA, int BMODE>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k_spmv_merged_short(
-    const SpmvTable<T>* __restrict__ tab, int n, int64_t blocks, int xc, int K) {
-  merged_wave<T, R, ALPHA, BMODE, 8, true>(tab, n, blocks, xc, K);
+    const SpmvTable<T>* __restrict__ tab, int n, int64_t waves, int xc) {
+  merged_wave<T, R, ALPHA, BMODE, 8, true>(tab, n, waves, xc);
 }
 
 template <typename T, int R, bool ALPHA, int BMODE>
-static void launch_merged_t(const SpmvTable<T>* d, int n, int64_t blocks, int K, bool sh, hipStream_t st) {
-  // (auto: merged launches keep the round robin)
-  const int xc = chunk_for(std::max(knobs().spmv_xcd_chunk, 0), K);
+static void launch_merged_t(const SpmvTable<T>* d, int n, int64_t waves, bool sh, hipStream_t st) {
+  const int xc = std::max(knobs().spmv_xcd_chunk, 0);  // (auto: merged launches keep the round robin)
+  const int64_t blocks = (waves + 3) / 4;
   if (blocks == 0) return;
   if constexpr (std::is_same<T, double>::value) {
     if (sh) {
-      hipLaunchKernelGGL((k_spmv_merged_short<T, R, ALPHA, BMODE>), dim3(blocks), dim3(256), 0, st, d, n, blocks, xc, K);
+      hipLaunchKernelGGL((k_spmv_merged_short<T, R, ALPHA, BMODE>), dim3(blocks), dim3(256), 0, st, d, n, waves, xc);
       return;
     }
   }
   if (sh)
-    hipLaunchKernelGGL((k_spmv_merged<T, R, ALPHA, BMODE, 8, true>), dim3(blocks), dim3(256), 0, st, d, n, blocks, xc, K);
+    hipLaunchKernelGGL((k_spmv_merged<T, R, ALPHA, BMODE, 8, true>), dim3(blocks), dim3(256), 0, st, d, n, waves, xc);
   else
-    hipLaunchKernelGGL((k_spmv_merged<T, R, ALPHA, BMODE, 8, false>), dim3(blocks), dim3(256), 0, st, d, n, blocks, xc, K);
+    hipLaunchKernelGGL((k_spmv_merged<T, R, ALPHA, BMODE, 8, false>), dim3(blocks), dim3(256), 0, st, d, n, waves, xc);
 }
 
 static int pk_of(int which) { return which == 0 ? 1 : which == 4 ? 3 : which == 5 ? 4 : 0; }
@@ -1537,8 +1406,7 @@ template <typename T>
 struct MergedLaunch {
   const SpmvTable<T>* dt = nullptr;
   int n = 0;
-  int K = 1;
-  int64_t blocks = 0;
+  int64_t waves = 0;
   bool sh = false, cg = false;
 };
 
@@ -1553,10 +1421,6 @@ static int merged_prepare(int n, const int* which, const SpmvPart* parts, bool h
   constexpr size_t kHdr = offsetof(SpmvTable<T>, a);
   std::memset(&h, 0, kHdr);
   bool sh = (knobs().spmv_flags & SPMV_SHORT) != 0;
-  int64_t items = 0;
-  for (int i = 0; i < n; ++i) items += std::max<int64_t>(parts[i].nwork, 0);
-  const int K = wave_slices(items);
-  h.spw = K;
   for (int i = 0; i < n; ++i) {
     const SpmvPart& q = parts[i];
     if (q.nwork <= 0) continue;
@@ -1566,15 +1430,15 @@ static int merged_prepare(int n, const int* which, const SpmvPart* parts, bool h
     h.a[h.n] = make_args<T>(which[i], q.nwork, list, q.A, q.x, q.y, q.ymap, alpha, beta, q.dotp, &q);
     h.pk[h.n] = pk_of(which[i]);
     sh = sh && h.a[h.n].maxlen <= 8;
-    h.start[h.n + 1] = h.start[h.n] + (q.nwork + 4 * K - 1) / (4 * K) * (4 * K);  // (on a block boundary)
+    h.start[h.n + 1] = h.start[h.n] + q.nwork;
     ++h.n;
   }
   *out = MergedLaunch<T>{};
   if (h.n == 0) return 0;
-  static_assert(kMergeMax <= 255, "the block map holds entry indices in bytes");
+  static_assert(kMergeMax <= 255, "the wave map holds entry indices in bytes");
   const size_t used = kHdr + (size_t)h.n * sizeof(SpmvArgs<T>);  // the device reads entries < n only
-  const int64_t nblocks = h.start[h.n] / (4 * K);
-  const size_t moff = merged_map_offset<T>(h.n), total = moff + (size_t)nblocks;
+  const int64_t nwaves = h.start[h.n];
+  const size_t moff = merged_map_offset<T>(h.n), total = moff + (size_t)nwaves;
   // cached device copy of this exact table (most recent first)
   auto& C = owner->merged_cache;
   const char* hb = reinterpret_cast<const char*>(&h);
@@ -1587,9 +1451,8 @@ static int merged_prepare(int n, const int* which, const SpmvPart* parts, bool h
     }
   if (!d) {
     if (hipMalloc(&d, total) != hipSuccess) return -1;
-    std::vector<char> m((size_t)nblocks);  // entry of every block (merged_wave)
-    for (int e = 0; e < h.n; ++e)
-      std::memset(m.data() + h.start[e] / (4 * K), e, (size_t)((h.start[e + 1] - h.start[e]) / (4 * K)));
+    std::vector<char> m((size_t)nwaves);  // entry of every wave (merged_wave)
+    for (int e = 0; e < h.n; ++e) std::memset(m.data() + h.start[e], e, (size_t)(h.start[e + 1] - h.start[e]));
     if (hipMemcpy(d, &h, used, hipMemcpyHostToDevice) != hipSuccess ||
         hipMemcpy((char*)d + moff, m.data(), m.size(), hipMemcpyHostToDevice) != hipSuccess) {
       (void)hipFree(d);
@@ -1604,8 +1467,7 @@ static int merged_prepare(int n, const int* which, const SpmvPart* parts, bool h
   }
   out->dt = (const SpmvTable<T>*)d;
   out->n = h.n;
-  out->K = K;
-  out->blocks = nblocks;
+  out->waves = nwaves;
   out->sh = sh;
   out->cg = h.a[0].cg != nullptr;
   return 0;
@@ -1615,20 +1477,21 @@ template <typename T, int R>
 static void merged_launch(const MergedLaunch<T>& m, bool has_alpha, int bmode, hipStream_t st) {
   if (m.n == 0) return;
   if (m.cg) {  // the device CG's fused u update (α = 1, β = 0)
-    if (m.blocks == 0) return;
-    const int xc = chunk_for(std::max(knobs().spmv_xcd_chunk, 0), m.K);  // (auto: merged launches keep the round robin)
-    if (m.sh) hipLaunchKernelGGL((k_spmv_merged<T, R, false, 0, 8, true, true>), dim3(m.blocks), dim3(256), 0, st, m.dt, m.n, m.blocks, xc, m.K);
-    else hipLaunchKernelGGL((k_spmv_merged<T, R, false, 0, 8, false, true>), dim3(m.blocks), dim3(256), 0, st, m.dt, m.n, m.blocks, xc, m.K);
+    const int64_t blocks = (m.waves + 3) / 4;
+    if (blocks == 0) return;
+    const int xc = std::max(knobs().spmv_xcd_chunk, 0);  // (auto: merged launches keep the round robin)
+    if (m.sh) hipLaunchKernelGGL((k_spmv_merged<T, R, false, 0, 8, true, true>), dim3(blocks), dim3(256), 0, st, m.dt, m.n, m.waves, xc);
+    else hipLaunchKernelGGL((k_spmv_merged<T, R, false, 0, 8, false, true>), dim3(blocks), dim3(256), 0, st, m.dt, m.n, m.waves, xc);
     return;
   }
   if (!has_alpha) {
-    if (bmode == 0) launch_merged_t<T, R, false, 0>(m.dt, m.n, m.blocks, m.K, m.sh, st);
-    else if (bmode == 1) launch_merged_t<T, R, false, 1>(m.dt, m.n, m.blocks, m.K, m.sh, st);
-    else launch_merged_t<T, R, false, 2>(m.dt, m.n, m.blocks, m.K, m.sh, st);
+    if (bmode == 0) launch_merged_t<T, R, false, 0>(m.dt, m.n, m.waves, m.sh, st);
+    else if (bmode == 1) launch_merged_t<T, R, false, 1>(m.dt, m.n, m.waves, m.sh, st);
+    else launch_merged_t<T, R, false, 2>(m.dt, m.n, m.waves, m.sh, st);
   } else {
-    if (bmode == 0) launch_merged_t<T, R, true, 0>(m.dt, m.n, m.blocks, m.K, m.sh, st);
-    else if (bmode == 1) launch_merged_t<T, R, true, 1>(m.dt, m.n, m.blocks, m.K, m.sh, st);
-    else launch_merged_t<T, R, true, 2>(m.dt, m.n, m.blocks, m.K, m.sh, st);
+    if (bmode == 0) launch_merged_t<T, R, true, 0>(m.dt, m.n, m.waves, m.sh, st);
+    else if (bmode == 1) launch_merged_t<T, R, true, 1>(m.dt, m.n, m.waves, m.sh, st);
+    else launch_merged_t<T, R, true, 2>(m.dt, m.n, m.waves, m.sh, st);
   }
 }
 
@@ -1916,13 +1779,6 @@ void launch_spmv_part(int which, int64_t nwork, const int32_t* list, const pa_ma
 #endif
 
 #if PA_DT_DEFINE  // ---- everything below: the dispatcher translation unit only
-
-int wave_slices(int64_t items) {
-  const int k = knobs().wave_slices;
-  if (k > 0) return k;
-  (void)items;
-  return 1;
-}
 
 // x .+= α.*u; r .-= α.*c (all lids, Interfaces.jl:1710-1737) and the owned
 // Σ|r|² of norm(r) (1767-1772) in one pass (contiguous owned lids

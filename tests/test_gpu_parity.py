@@ -381,8 +381,9 @@ def test_barrier_issue_chain_equals_oracle(pamd, O, threads):
     one-process-drives-several-GPUs path): with the pack
     barrier and double-buffered send buffers (halo_barrier 1) every call sees
     the x that was copied in just before it, as with per-neighbour waits
-    (halo_barrier 0) and the oracle; an exchange! inside the sequence restarts
-    the buffer chain; the device CG is bit-identical across both."""
+    (halo_barrier 0), with the pull on each part's compute stream
+    (halo_barrier 2) and the oracle; an exchange! inside the sequence
+    restarts the buffer chain; the device CG is bit-identical across all."""
     shape, N = (2, 2, 2), (14, 11, 9)
     rng = np.random.default_rng(SEED + 13)
     K = 9
@@ -395,7 +396,7 @@ def test_barrier_issue_chain_equals_oracle(pamd, O, threads):
         O.mul_(oy, OA, ox)
         want.append(oy)
     hist = {}
-    for barrier in (1, 0):
+    for barrier in (1, 2, 0):
         p0 = pamd._lib.tune("issue_threads", threads)
         p1 = pamd._lib.tune("halo_barrier", barrier)
         try:
@@ -423,9 +424,10 @@ def test_barrier_issue_chain_equals_oracle(pamd, O, threads):
         finally:
             pamd._lib.tune("halo_barrier", p1)
             pamd._lib.tune("issue_threads", p0)
-    assert hist[0][0] == hist[1][0]
-    for a, b in zip(hist[0][1], hist[1][1]):
-        assert np.array_equal(a, b)
+    for k in (1, 2):
+        assert hist[0][0] == hist[k][0]
+        for a, b in zip(hist[0][1], hist[k][1]):
+            assert np.array_equal(a, b)
 
 
 def test_threaded_issue_reports_launch_failures(pamd, O):

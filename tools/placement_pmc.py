@@ -55,9 +55,18 @@ def child(a):
             ctx.span_stop()
             ms[f"A{i}x{j}"] = round(ctx.span_ms() / a.reps, 4)
     ptrs = [{k: hex(v) for k, v in Ai.values.local(1).device_ptrs().items()} for Ai in As]
+    # every part's value and column arrays per copy (the
+    # bases modulo the interleave granularities a placement effect would
+    # follow: 4 KiB pages, 64 KiB, 2 MiB fragments)
+    allp = [{str(p): {k: hex(v) for k, v in Ai.values.local(p).device_ptrs().items() if k in ("val", "col", "mask",
+                                                                                             "slice_off")}
+             for p in parts.part_ids} for Ai in As]
+    mods = [{str(p): {f"val_mod_{m}": Ai.values.local(p).device_ptrs()["val"] % m for m in (4096, 65536, 1 << 21)}
+             for p in parts.part_ids} for Ai in As]
     print(json.dumps({"tool": "placement_pmc", "k": a.k, "reps": a.reps, "shape": shape, "event_ms": ms,
-                      "schedule": sched, "mat_ptrs": ptrs,
-                      "x": [hex(x.values.parts[0].device_ptr()) for x in xs]}), flush=True)
+                      "schedule": sched, "mat_ptrs": ptrs, "all_part_ptrs": allp, "val_base_mods": mods,
+                      "x": [hex(x.values.parts[0].device_ptr()) for x in xs],
+                      "x_all_parts": [[hex(v.device_ptr()) for v in x.values.parts] for x in xs]}), flush=True)
 
 
 def _csv(d, suffix):
