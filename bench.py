@@ -795,6 +795,14 @@ def main():
     # through (ncopies operator copies when one would fit the 256 MB
     # Infinity Cache), so that neither side is served from it
     box = box_hbm_gbs(pamd, spmv_bytes * ncopies) if world == 1 and ngpu == 1 else None
+    # ... and one launch of the operator's own size, rotating over 2 GiB (a
+    # short SpMV pays one launch's ramp-up and drain per step; C2's 149 MB)
+    box_launch = None
+    if box is not None:
+        try:
+            box_launch = pamd._lib.hbm_probe_launch(0, int(spmv_bytes), max(2 << 30, 8 * int(spmv_bytes)), 40)
+        except pamd._lib.PAError:
+            box_launch = None
     halo_leg = None
     if world == 1 and ngpu == 1 and not args.strong and not args.no_halo_leg:
         halo_leg = halo_1gpu(args, pamd, dtype, S)
@@ -888,6 +896,8 @@ def main():
             "box_read_gbs": None if box is None else round(box[0], 1),
             "box_copy_gbs": None if box is None else round(box[1], 1),
             "achieved_vs_box_read": None if box is None else round(achieved / box[0], 4),
+            "box_read_gbs_one_launch": None if box_launch is None else round(box_launch, 1),
+            "achieved_vs_box_read_one_launch": None if not box_launch else round(achieved / box_launch, 4),
             "box_note": ("pa_hbm_probe on the same box and run: best read-only / copy rate of 16 B "
                          "non-temporal sweeps reading as many bytes per launch as the timed loop cycles "
                          "through (the SpMV's format bytes times the operator copies it rotates); the attainable "

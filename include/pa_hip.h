@@ -136,6 +136,13 @@ int pa_knob_selftest(int nthreads, int iters, int* mismatches);
  * `bytes` buffer with the SpMV's 16 B non-temporal loads.  bench.py reports
  * the SpMV's PMC-measured rate against it, since boxes differ.           */
 int pa_hbm_probe(int device, int64_t bytes, int reps, double* read_gbs, double* copy_gbs);
+/* The same read sweep at the size of ONE launch: every launch reads
+ * `bytes_per_launch` (one operator's bytes), the launches rotating over
+ * `span` bytes (>= 1 GiB: from HBM, not the 256 MB Infinity Cache), so the
+ * rate includes one launch's ramp-up and drain; best of the grid sizes.  A
+ * short SpMV (C2's 149 MB) is compared with this, not with the sweep of a
+ * large buffer.                                                           */
+int pa_hbm_probe_launch(int device, int64_t bytes_per_launch, int64_t span, int reps, double* read_gbs);
 
 /* ---- part context ------------------------------------------------------
  * One context per part: its device, its streams, its scratch.
@@ -176,6 +183,11 @@ int pa_comm_stats(pa_ctx* ctx, int64_t* bytes_sent, int64_t* bytes_recv);
  * version (ncclGetVersion) and the path of the librccl the process resolved
  * it from (lib, lib_len bytes; dladdr on ncclGetVersion: a host that loads
  * another RCCL first, e.g. torch's bundled one, shows it here).          */
+/* Host time of the library's issue jobs (one part's share of a call issued
+ * from an IssuePool thread: its runtime calls and launches) since the last
+ * reset: the largest and the mean job, and their count.  The per-thread
+ * issue time of one process driving several GPUs.         */
+int pa_issue_stats(int reset, double* max_job_us, double* mean_job_us, int64_t* jobs);
 int pa_comm_info(pa_ctx* ctx, int* ranks, int* rank, int* device, char* pci, int pci_len, int* version,
                  char* lib, int lib_len);
 

@@ -44,6 +44,8 @@ _SIGS = {
     "pa_cg_fuse_agree": [C.c_int, _p, _p, C.POINTER(C.c_int)],
     "pa_mat_cg_choice": [_p, C.POINTER(C.c_int)],
     "pa_hbm_probe": [C.c_int, C.c_int64, C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_double)],
+    "pa_issue_stats": [C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_double), C.POINTER(C.c_int64)],
+    "pa_hbm_probe_launch": [C.c_int, C.c_int64, C.c_int64, C.c_int, C.POINTER(C.c_double)],
     "pa_ctx_create": [C.c_int, C.c_int, C.c_int, C.POINTER(_p)],
     "pa_ctx_create_shared": [C.c_int, C.c_int, _p, C.POINTER(_p)],
     "pa_ctx_destroy": [_p],
@@ -231,6 +233,23 @@ def hbm_probe(device: int = 0, nbytes: int = 2 << 30, reps: int = 10):
     r, c = C.c_double(), C.c_double()
     call("pa_hbm_probe", int(device), int(nbytes), int(reps), C.byref(r), C.byref(c))
     return r.value, c.value
+
+
+def issue_stats(reset=True):
+    """pa_issue_stats: (max µs, mean µs, count) of the issue jobs (one part's
+    share of a threaded call) since the last reset"""
+    mx, mean, n = C.c_double(), C.c_double(), C.c_int64()
+    call("pa_issue_stats", int(bool(reset)), C.byref(mx), C.byref(mean), C.byref(n))
+    return mx.value, mean.value, n.value
+
+
+def hbm_probe_launch(device: int, bytes_per_launch: int, span: int = 2 << 30, reps: int = 40) -> float:
+    """pa_hbm_probe_launch: read GB/s when each launch reads bytes_per_launch
+    (rotating over `span` bytes, from HBM): one launch's ramp and drain
+    included"""
+    r = C.c_double()
+    call("pa_hbm_probe_launch", int(device), int(bytes_per_launch), int(span), int(reps), C.byref(r))
+    return r.value
 
 
 def i32(a):

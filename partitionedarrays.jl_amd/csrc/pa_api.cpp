@@ -1120,6 +1120,10 @@ int pre_pack_wait(int n, pa_xchg* const xg[]) {
 // spin briefly between calls, then sleep.
 class IssuePool {
  public:
+  // host time of the jobs (one part's issue each) since the last reset
+  // (pa_issue_stats: the per-thread issue time of the one-process-per-node
+  // model)
+  std::atomic<uint64_t> job_ns_sum{0}, job_ns_max{0}, jobs{0};
   static IssuePool& get() {
     static IssuePool* p = new IssuePool();  // never destroyed: workers may outlive static destruction
     return *p;
@@ -1166,7 +1170,14 @@ class IssuePool {
   // call instead of being lost there.
   void work(const std::function<int(int)>* f, int n) {
     for (int i = next_.fetch_add(1); i < n; i = next_.fetch_add(1)) {
+      const auto t0 = std::chrono::steady_clock::now();
       int rc = (*f)(i);
+      const uint64_t ns = (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+                              std::chrono::steady_clock::now() - t0).count();
+      job_ns_sum.fetch_add(ns, std::memory_order_relaxed);
+      jobs.fetch_add(1, std::memory_order_relaxed);
+      for (uint64_t m = job_ns_max.load(); ns > m && !job_ns_max.compare_exchange_weak(m, ns);) {
+      }
       if (rc == 0 && knobs().fault_inject) launch_invalid_config();
       const hipError_t e = hipGetLastError();
       if (rc == 0 && e != hipSuccess) {
@@ -1508,6 +1519,47 @@ int pa_hbm_probe(int device, int64_t bytes, int reps, double* read_gbs, double* 
   return 0;
 }
 
+int pa_hbm_probe_launch(int device, int64_t bytes_per_launch, int64_t span, int reps, double* read_gbs) {
+  CHECK_ARG(bytes_per_launch >= (1 << 20) && span >= bytes_per_launch && reps > 0 && read_gbs,
+            "pa_hbm_probe_launch: 1 MiB <= bytes_per_launch <= span, reps > 0");
+  HIPC(hipSetDevice(device));
+  const int64_t n16 = bytes_per_launch / 16, seg = n16 * 16;
+  const int64_t nseg = std::max<int64_t>(1, span / seg);
+  void *a = nullptr, *b = nullptr;
+  hipStream_t st = nullptr;
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  auto cleanup = [&]() {
+    if (a) (void)hipFree(a);
+    if (b) (void)hipFree(b);
+    if (e0) (void)hipEventDestroy(e0);
+    if (e1) (void)hipEventDestroy(e1);
+    if (st) (void)hipStreamDestroy(st);
+  };
+#define PROBE_CALL(expr) do { if ((expr) != hipSuccess) { cleanup(); PA_FAIL(std::string("pa_hbm_probe_launch: ") + #expr); } } while (0)
+  PROBE_CALL(hipMalloc(&a, (size_t)(nseg * seg)));
+  PROBE_CALL(hipMalloc(&b, 4096));
+  PROBE_CALL(hipMemset(a, 0x5a, (size_t)(nseg * seg)));
+  PROBE_CALL(hipStreamCreate(&st));
+  PROBE_CALL(hipEventCreate(&e0));
+  PROBE_CALL(hipEventCreate(&e1));
+  double best = 0.0;
+  for (int unroll : {4, 8})
+    for (int blocks : {2048, 4096, 8192, 16384}) {
+      launch_probe(0, unroll, n16, a, b, blocks, st);  // warm
+      PROBE_CALL(hipEventRecord(e0, st));
+      for (int r = 0; r < reps; ++r) launch_probe(0, unroll, n16, (const char*)a + (r % nseg) * seg, b, blocks, st);
+      PROBE_CALL(hipEventRecord(e1, st));
+      PROBE_CALL(hipEventSynchronize(e1));
+      float ms = 0.f;
+      PROBE_CALL(hipEventElapsedTime(&ms, e0, e1));
+      best = std::max(best, (double)seg * reps / (ms * 1e-3) / 1e9);
+    }
+#undef PROBE_CALL
+  cleanup();
+  *read_gbs = best;
+  return 0;
+}
+
 static int ctx_scratch(pa_ctx* c, const pa_ctx* share_events = nullptr) {
   HIPC(hipMalloc(&c->d_partials, 8192 * 16));  // block partials (reductions, CG update)
   HIPC(hipMalloc(&c->d_fold, 256 * 16));
@@ -1690,6 +1742,20 @@ int pa_comm_info(pa_ctx* c, int* ranks, int* rank, int* device, char* pci, int p
     Dl_info di{};
     if (dladdr(reinterpret_cast<void*>(&ncclGetVersion), &di) && di.dli_fname)
       std::snprintf(lib, (size_t)lib_len, "%s", di.dli_fname);
+  }
+  return 0;
+}
+
+int pa_issue_stats(int reset, double* max_job_us, double* mean_job_us, int64_t* jobs) {
+  IssuePool& P = IssuePool::get();
+  const uint64_t n = P.jobs.load();
+  if (max_job_us) *max_job_us = 1e-3 * (double)P.job_ns_max.load();
+  if (mean_job_us) *mean_job_us = n ? 1e-3 * (double)P.job_ns_sum.load() / (double)n : 0.0;
+  if (jobs) *jobs = (int64_t)n;
+  if (reset) {
+    P.job_ns_sum.store(0);
+    P.job_ns_max.store(0);
+    P.jobs.store(0);
   }
   return 0;
 }

@@ -193,7 +193,7 @@ typedef unsigned int u2a __attribute__((ext_vector_type(2))) __attribute__((alig
 template <typename T>
 __device__ __forceinline__ void ld_xtrip(const T* p, T (&o)[3]) {
   if constexpr (sizeof(T) == 4) {
-    const u3a r = *reinterpret_cast<const u3a*>(p);
+    const u4a r = *reinterpret_cast<const u4a*>(p);  // (x[j+3] unused: within the 64 B back padding)
     __builtin_memcpy(&o[0], &r, 12);
   } else if constexpr (sizeof(T) == 8) {
     const u4a r = *reinterpret_cast<const u4a*>(p);

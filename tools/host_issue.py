@@ -62,6 +62,7 @@ def measure(be, n, k, label, cg_iters=0):
     # the per-call host time (host threads make single runs noisy)
     args = pamd.pvector._spmv_args(y, A, x, 1.0, 0.0)
     reps = []
+    pamd._lib.issue_stats(reset=True)
     for _ in range(7):
         t0 = time.perf_counter()
         for _ in range(k):
@@ -74,6 +75,11 @@ def measure(be, n, k, label, cg_iters=0):
            "host_us_per_mul_python": round(1e6 * host_py, 1), "host_us_per_mul_cabi": round(1e6 * host_c, 1),
            "host_us_per_mul_cabi_min_max": [round(1e6 * reps[0], 1), round(1e6 * reps[-1], 1)],
            "host_us_per_part_cabi": round(1e6 * host_c / 8, 1)}
+    jmax, jmean, jn = pamd._lib.issue_stats(reset=True)
+    if jn:  # threaded issue: one job = one part's share of one phase of a call (pa_issue_stats)
+        out.update({"issue_jobs": jn, "issue_job_us_mean": round(jmean, 1), "issue_job_us_max": round(jmax, 1),
+                    "issue_jobs_per_call": round(jn / (7 * k), 2),
+                    "per_part_issue_us_per_call": round(jmean * jn / (7 * k) / 8, 1)})
     if cg_iters:
         # a tiny operator (8 parts of 8^3): device work is negligible, so the
         # wall time per iteration is the host issue (+ one wait per batch)
