@@ -4393,7 +4393,16 @@ int pa_mat_stencil(pa_ctx* c, int dtype, int kind, const int64_t gdims[3], const
   int64_t nnz_owned = 0;
   (void)nnz_owned;
   hipError_t e1 = hipMalloc((void**)&A->d_col, std::max<int64_t>(A->slots, 1) * 4);
-  hipError_t e2 = hipMalloc(&A->d_val, std::max<int64_t>(A->slots, 1) * S);
+  hipError_t e2 = hipErrorMemoryAllocation;
+  // PA_DIAG_VAL_CONTIGUOUS (placement diagnostics only, tools/placement_pmc.py,
+  // DESIGN.md §4.1): the values in physically contiguous memory when the
+  // driver can provide it
+  if (std::getenv("PA_DIAG_VAL_CONTIGUOUS"))
+    e2 = hipExtMallocWithFlags(&A->d_val, std::max<int64_t>(A->slots, 1) * S, hipDeviceMallocContiguous);
+  if (e2 != hipSuccess) {
+    (void)hipGetLastError();
+    e2 = hipMalloc(&A->d_val, std::max<int64_t>(A->slots, 1) * S);
+  }
   if (e1 != hipSuccess || e2 != hipSuccess) { cleanup(); pa_mat_destroy(A); PA_FAIL("hipMalloc(matrix) failed: out of device memory"); }
   launch_stencil_fill(g, d_shell, d_coef, nrows, (int)nrows, A, d_err, c->s_main);
   HIPC(hipGetLastError());

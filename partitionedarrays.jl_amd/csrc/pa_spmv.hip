@@ -193,7 +193,7 @@ typedef unsigned int u2a __attribute__((ext_vector_type(2))) __attribute__((alig
 template <typename T>
 __device__ __forceinline__ void ld_xtrip(const T* p, T (&o)[3]) {
   if constexpr (sizeof(T) == 4) {
-    const u4a r = *reinterpret_cast<const u4a*>(p);  // (x[j+3] unused: within the 64 B back padding)
+    const u3a r = *reinterpret_cast<const u3a*>(p);
     __builtin_memcpy(&o[0], &r, 12);
   } else if constexpr (sizeof(T) == 8) {
     const u4a r = *reinterpret_cast<const u4a*>(p);
@@ -1035,7 +1035,10 @@ __global__ __launch_bounds__(256) void k_spmv_sell_group(const SpmvGroup<T> g) {
   p = __builtin_amdgcn_readfirstlane(p);
   if constexpr (TAIL) {
     if (p >= g.tail0) {
-      spmv_wave<T, R, ALPHA, BMODE, U, 0, true, false>(g.a[p], w - g.start[p]);
+      // the side rows in batches of 4 (one masked batch for the 1-entry
+      // Dirichlet rows): the short-row launch then holds the pattern code's
+      // registers (C2: 98 -> 84 VGPRs, 6 waves per SIMD instead of 5)
+      spmv_wave<T, R, ALPHA, BMODE, 4, 0, false, false>(g.a[p], w - g.start[p]);
       return;
     }
   }

@@ -54,6 +54,31 @@ def child(a):
                 pamd.mul_(y, As[i], xs[j])
             ctx.span_stop()
             ms[f"A{i}x{j}"] = round(ctx.span_ms() / a.reps, 4)
+    rebuilt = None
+    if a.rebuild:
+        # free the first half of the copies, build as many again (the driver
+        # hands their physical pages back): if a rebuilt copy runs at the
+        # rate of the copy it replaced, the rate belongs to the pages
+        import gc
+        h = a.k // 2
+        freed = {f"A{i}": ms[f"A{i}x0"] for i in range(h)}
+        for i in range(h):
+            As[i] = None
+        gc.collect()
+        ctx.sync()
+        Bs = [pamd.drivers.stencil_operator(parts, N, 27, np.float64, partition=partition) for _ in range(h)]
+        ctx.sync()
+        rebuilt = {"freed_copies_ms_x0": freed, "rebuilt_ms_x0": {}}
+        for i, Bi in enumerate(Bs):
+            pamd.mul_(y, Bi, xs[0])
+            ctx.sync()
+            ctx.span_start()
+            for _ in range(a.reps):
+                pamd.mul_(y, Bi, xs[0])
+            ctx.span_stop()
+            rebuilt["rebuilt_ms_x0"][f"B{i}"] = round(ctx.span_ms() / a.reps, 4)
+        rebuilt["rebuilt_val"] = [hex(Bi.values.local(1).device_ptrs()["val"]) for Bi in Bs]
+        As[:h] = Bs
     ptrs = [{k: hex(v) for k, v in Ai.values.local(1).device_ptrs().items()} for Ai in As]
     # every part's value and column arrays per copy (the
     # bases modulo the interleave granularities a placement effect would
@@ -64,6 +89,7 @@ def child(a):
     mods = [{str(p): {f"val_mod_{m}": Ai.values.local(p).device_ptrs()["val"] % m for m in (4096, 65536, 1 << 21)}
              for p in parts.part_ids} for Ai in As]
     print(json.dumps({"tool": "placement_pmc", "k": a.k, "reps": a.reps, "shape": shape, "event_ms": ms,
+                      "rebuild": rebuilt, "val_contiguous_env": bool(os.environ.get("PA_DIAG_VAL_CONTIGUOUS")),
                       "schedule": sched, "mat_ptrs": ptrs, "all_part_ptrs": allp, "val_base_mods": mods,
                       "x": [hex(x.values.parts[0].device_ptr()) for x in xs],
                       "x_all_parts": [[hex(v.device_ptr()) for v in x.values.parts] for x in xs]}), flush=True)
@@ -122,6 +148,8 @@ if __name__ == "__main__":
     ap.add_argument("--reps", type=int, default=6)
     ap.add_argument("--shape", default="1,1,1", help="Cartesian parts of one GPU (n^3 nodes each)")
     ap.add_argument("--analyze", nargs="+")
+    ap.add_argument("--rebuild", action="store_true",
+                    help="free the first half of the copies, rebuild them, time the new ones against x0")
     a = ap.parse_args()
     if a.analyze:
         analyze(a.analyze)
