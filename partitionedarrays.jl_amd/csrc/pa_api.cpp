@@ -4397,8 +4397,12 @@ int pa_mat_stencil(pa_ctx* c, int dtype, int kind, const int64_t gdims[3], const
   // PA_DIAG_VAL_CONTIGUOUS (placement diagnostics only, tools/placement_pmc.py,
   // DESIGN.md §4.1): the values in physically contiguous memory when the
   // driver can provide it
-  if (std::getenv("PA_DIAG_VAL_CONTIGUOUS"))
+  if (std::getenv("PA_DIAG_VAL_CONTIGUOUS")) {
     e2 = hipExtMallocWithFlags(&A->d_val, std::max<int64_t>(A->slots, 1) * S, hipDeviceMallocContiguous);
+    if (e2 != hipSuccess)
+      std::fprintf(stderr, "PA_DIAG_VAL_CONTIGUOUS: contiguous allocation of %lld B failed (%s): hipMalloc\n",
+                   (long long)(std::max<int64_t>(A->slots, 1) * S), hipGetErrorString(e2));
+  }
   if (e2 != hipSuccess) {
     (void)hipGetLastError();
     e2 = hipMalloc(&A->d_val, std::max<int64_t>(A->slots, 1) * S);

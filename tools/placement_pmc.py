@@ -30,7 +30,15 @@ def child(a):
     N = tuple(a.n * s for s in shape)
     partition = pamd.drivers.stencil_partition(parts, N, 27)
     ctx = be.context(1)
-    As = [pamd.drivers.stencil_operator(parts, N, 27, np.float64, partition=partition) for _ in range(a.k)]
+    def build(i):
+        # --contig "1010": copy i's values in physically contiguous memory
+        # when its character is 1 (PA_DIAG_VAL_CONTIGUOUS, read per build)
+        if a.contig and a.contig[i % len(a.contig)] == "1":
+            os.environ["PA_DIAG_VAL_CONTIGUOUS"] = "1"
+        else:
+            os.environ.pop("PA_DIAG_VAL_CONTIGUOUS", None)
+        return pamd.drivers.stencil_operator(parts, N, 27, np.float64, partition=partition)
+    As = [build(i) for i in range(a.k)]
     xs = [pamd.PVector.from_host(pamd.map_parts(
         lambda s: np.random.default_rng(s.part).uniform(-1, 1, s.num_lids), As[0].cols.partition), As[0].cols)
         for _ in range(a.k)]
@@ -66,7 +74,7 @@ def child(a):
             As[i] = None
         gc.collect()
         ctx.sync()
-        Bs = [pamd.drivers.stencil_operator(parts, N, 27, np.float64, partition=partition) for _ in range(h)]
+        Bs = [build(i) for i in range(h)]
         ctx.sync()
         rebuilt = {"freed_copies_ms_x0": freed, "rebuilt_ms_x0": {}}
         for i, Bi in enumerate(Bs):
@@ -89,7 +97,7 @@ def child(a):
     mods = [{str(p): {f"val_mod_{m}": Ai.values.local(p).device_ptrs()["val"] % m for m in (4096, 65536, 1 << 21)}
              for p in parts.part_ids} for Ai in As]
     print(json.dumps({"tool": "placement_pmc", "k": a.k, "reps": a.reps, "shape": shape, "event_ms": ms,
-                      "rebuild": rebuilt, "val_contiguous_env": bool(os.environ.get("PA_DIAG_VAL_CONTIGUOUS")),
+                      "rebuild": rebuilt, "contig": a.contig,
                       "schedule": sched, "mat_ptrs": ptrs, "all_part_ptrs": allp, "val_base_mods": mods,
                       "x": [hex(x.values.parts[0].device_ptr()) for x in xs],
                       "x_all_parts": [[hex(v.device_ptr()) for v in x.values.parts] for x in xs]}), flush=True)
@@ -148,6 +156,7 @@ if __name__ == "__main__":
     ap.add_argument("--reps", type=int, default=6)
     ap.add_argument("--shape", default="1,1,1", help="Cartesian parts of one GPU (n^3 nodes each)")
     ap.add_argument("--analyze", nargs="+")
+    ap.add_argument("--contig", default="", help="per copy (cyclic): 1 = values via hipDeviceMallocContiguous")
     ap.add_argument("--rebuild", action="store_true",
                     help="free the first half of the copies, rebuild them, time the new ones against x0")
     a = ap.parse_args()
