@@ -578,25 +578,13 @@ __device__ __forceinline__ void rows_t16_tri(T (&acc)[R], const S16Pack<R>* __re
         }
   };
   int t = 0;
-  // the codes one batch ahead: a batch's x loads issue with its value loads
-  // instead of one load latency after them (its codes were loaded during
-  // the previous batch)
-  S16Pack<R> qn[TB];
-  if (TB <= ntri) {
-#pragma unroll
-    for (int u = 0; u < TB; ++u) qn[u] = ld<NT>(&cp[u * 64]);
-  }
   for (; t + TB <= ntri; t += TB) {
     S16Pack<R> q[TB];
     Pack<T, R> v[3 * TB];
 #pragma unroll
-    for (int u = 0; u < TB; ++u) q[u] = qn[u];
+    for (int u = 0; u < TB; ++u) q[u] = ld<NT>(&cp[(t + u) * 64]);
 #pragma unroll
     for (int u = 0; u < 3 * TB; ++u) v[u] = ld<NT>(&vp[(3 * t + u) * 64]);
-    if (t + 2 * TB <= ntri) {
-#pragma unroll
-      for (int u = 0; u < TB; ++u) qn[u] = ld<NT>(&cp[(t + TB + u) * 64]);
-    }
     step(q, v, std::integral_constant<int, TB>{});
   }
   for (; t < ntri; ++t) {
