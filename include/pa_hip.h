@@ -64,7 +64,9 @@ int pa_device_count(int* count);
  *               covering the whole structure is launched without the list,
  *               bit 5: y written with non-temporal stores, bit 6: launches
  *               whose rows have at most 8 entries use the short-row kernels
- *               (one predicated batch, no loop: fewer registers) (default 93);
+ *               (one predicated batch, no loop: fewer registers), bit 7:
+ *               the Float64 short-row tail launch of rows <= 7 entries at
+ *               7 waves per SIMD (default 221);
  * "spmv_format" 1: pattern slices where the matrix has them (default),
  *               0: int32 column ids everywhere;
  * "long_rows_exact" 1: long rows summed in the reference's order (default),

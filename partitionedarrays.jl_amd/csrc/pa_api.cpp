@@ -86,9 +86,9 @@ void launch_gather_scatter(int P, const void* const* srcs, int accsz, int nd, vo
 //    1.075 ms (profiles/r03/s, final, f, d) — the fused SpMV gathers two
 //    vectors (r and u_old) per x value — so 2 = measure one batch of each on
 //    this box and keep the faster (pa_cg_solve_all);
-//  * spmv_flags 93, spmv_format 1, long_rows_exact 1: pa_spmv.hip.
+//  * spmv_flags 221, spmv_format 1, long_rows_exact 1: pa_spmv.hip.
 const Knobs kDefaults = {
-    /*spmv_flags*/ 93, /*long_exact*/ 1, /*halo_pull*/ 1, /*spmv_delta16*/ 1, /*spmv_merge*/ 1,
+    /*spmv_flags*/ 221, /*long_exact*/ 1, /*halo_pull*/ 1, /*spmv_delta16*/ 1, /*spmv_merge*/ 1,
     /*spmv_merge_max*/ 65536, /*cg_fuse*/ 2, /*halo_direct*/ 1, /*halo_transport*/ 0, /*spmv_group*/ 1,
     /*spmv_format*/ 1, /*pattern_min_pct*/ 0, /*issue_threads*/ 1, /*fault_inject*/ 0, /*spmv_xcd_chunk*/ -1, /*spmv_tri16*/ 1,
     /*halo_barrier*/ 1, /*tri_order*/ 1, /*side_tail*/ 1, /*f32_rows*/ 0};
@@ -1264,10 +1264,11 @@ struct Knob {
   const char* help;
 };
 const Knob kKnobs[] = {
-    {"spmv_flags", &Knobs::spmv_flags, nullptr, 0, 0x7d, 0x7d,
+    {"spmv_flags", &Knobs::spmv_flags, nullptr, 0, 0xfd, 0xfd,
      "spmv_flags: bit 0 = non-temporal streams, "
      "bit 2 = 16 B x runs (pattern rows), bit 3 = masked tail batch, bit 4 = identity slice lists dropped, "
-     "bit 5 = non-temporal y stores, bit 6 = short-row kernels (launches whose rows have <= 8 entries)"},
+     "bit 5 = non-temporal y stores, bit 6 = short-row kernels (launches whose rows have <= 8 entries), "
+     "bit 7 = the Float64 short-row tail launch at 7 entries and 7 waves per SIMD (rows <= 7 entries)"},
     {"long_rows_exact", &Knobs::long_exact, nullptr, 0, 1, 0,
      "long_rows_exact: 1 = reference summation order, 0 = lane-strided tree (1e-12)"},
     {"halo_pull", &Knobs::halo_pull, nullptr, 0, 1, 0,

@@ -50,9 +50,11 @@ struct alignas(2 * R) S16Pack {
   uint16_t c[R];
 };
 
-// Bit 1 (XCD remap), 7 (x runs in int32 slices) and 9 (lane-shared x runs)
-// were negative A/Bs of rounds 1-3 and are gone.
+// Bits 1 (XCD remap), 9 (lane-shared x runs) and the old bit 7 (x runs in
+// int32 slices) were negative A/Bs of rounds 1-3 and are
+// gone; bit 7 is SPMV_SHORT7 since r06.
 enum { SPMV_NT = 1, SPMV_XPAIR = 4, SPMV_TAILB = 8, SPMV_IDLIST = 16, SPMV_YNT = 32, SPMV_SHORT = 64,
+       SPMV_SHORT7 = 128 /* Float64 rows <= 7 entries: k_spmv_group_short7 */,
        SPMV_PRODA = 256 /* per matrix: CSR parent, α scales the product */ };
 
 typedef unsigned int spmv_u32x4 __attribute__((ext_vector_type(4)));
@@ -61,10 +63,13 @@ typedef unsigned int spmv_u32x4 __attribute__((ext_vector_type(4)));
 // streams on, U = 8, 16 B x runs on (FE27 256³: F64 −9 %,
 // F32 −33 %, C64 −5 % kernel time), predicated tail batch on
 // (profiles/r01/ab_tail.txt: FD7 256³ F64 −31 %, F32 −42 %; FE27 −1…−3 %),
-// identity slice lists dropped (profiles/r01/ab_idlist.txt: FD7 −0.9 %, FE27 ±0).
-// (the knob defaults: pa_api.cpp kDefaults; spmv_flags 93 = NT | XPAIR |
-// TAILB | IDLIST | SHORT)
-static_assert((SPMV_NT | SPMV_XPAIR | SPMV_TAILB | SPMV_IDLIST | SPMV_SHORT) == 93, "kDefaults.spmv_flags");
+// identity slice lists dropped (profiles/r01/ab_idlist.txt: FD7 −0.9 %, FE27 ±0),
+// the Float64 7-entry short-row tail launch (C2 0.0281 -> 0.0278 ms, both
+// orders of 7 interleaved rounds, profiles/r06/j/).
+// (the knob defaults: pa_api.cpp kDefaults; spmv_flags 221 = NT | XPAIR |
+// TAILB | IDLIST | SHORT | SHORT7)
+static_assert((SPMV_NT | SPMV_XPAIR | SPMV_TAILB | SPMV_IDLIST | SPMV_SHORT | SPMV_SHORT7) == 221,
+              "kDefaults.spmv_flags");
 
 // SpmvArgs' pointers are global memory.  The merged launch reads them from a
 // device-resident table, where the compiler cannot see their address space:
@@ -1026,7 +1031,7 @@ struct SpmvGroup {
 // one entry each, 6.8 µs as a separate launch, profiles/r04/am/)
 template <typename T, int R, bool ALPHA, int BMODE, int U, int PK, bool SH = false, bool XV = false,
           bool TAIL = false>
-__global__ __launch_bounds__(256) void k_spmv_sell_group(const SpmvGroup<T> g) {
+__device__ __forceinline__ void group_wave(const SpmvGroup<T>& g) {
   // wave-uniform: the part's arguments are read with scalar loads
   const int64_t w = xcd_block(g.a[0].xcd_chunk) * 4 + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   if (w >= g.start[g.np]) return;
@@ -1043,6 +1048,21 @@ __global__ __launch_bounds__(256) void k_spmv_sell_group(const SpmvGroup<T> g) {
     }
   }
   spmv_wave<T, R, ALPHA, BMODE, U, PK, SH, XV>(g.a[p], w - g.start[p]);
+}
+
+template <typename T, int R, bool ALPHA, int BMODE, int U, int PK, bool SH = false, bool XV = false,
+          bool TAIL = false>
+__global__ __launch_bounds__(256) void k_spmv_sell_group(const SpmvGroup<T> g) {
+  group_wave<T, R, ALPHA, BMODE, U, PK, SH, XV, TAIL>(g);
+}
+
+// Float64 pattern slices whose rows have at most 7 entries (FD7: C2) with
+// their side rows: the short-row batch of 7 (not 8) and 7 waves per SIMD
+// (72 VGPRs instead of 84; the rare side rows' loop spills a few)
+template <typename T, int R>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void k_spmv_group_short7(
+    const SpmvGroup<T> g) {
+  group_wave<T, R, false, 0, 7, 1, true, false, true>(g);
 }
 
 template <typename T, int R, bool ALPHA, int BMODE, int PAT>
@@ -1062,6 +1082,16 @@ static void launch_group_t(const SpmvGroup<T>& g, hipStream_t st) {
   }
   if constexpr (PAT == 1) {
     if (g.tail0 < g.np) {  // pattern entries, then side rows (group_which, which 6)
+      if constexpr (std::is_same<T, double>::value && !ALPHA && BMODE == 0) {
+        bool sh7 = sh && (knobs().spmv_flags & SPMV_SHORT7) != 0 && knobs().spmv_xcd_chunk < 0;
+        for (int i = 0; i < g.np && i < g.tail0; ++i) sh7 = sh7 && g.a[i].maxlen <= 7;
+        if (sh7) {
+          SpmvGroup<T> g2 = g;
+          for (int i = 0; i < g2.np; ++i) g2.a[i].xcd_chunk = 0;
+          hipLaunchKernelGGL((k_spmv_group_short7<T, R>), dim3(blocks), dim3(256), 0, st, g2);
+          return;
+        }
+      }
       if (sh && knobs().spmv_xcd_chunk < 0) {
         // short rows (one batch per wave, latency-bound): the auto XCD runs
         // cost more than their x locality gives (C2: 0.0282 with the round

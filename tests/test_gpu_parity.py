@@ -615,3 +615,36 @@ def test_short_row_side_tail_equals_oracle(be, pamd, O, dtype):
             assert _eq(O, y.to_host().local(1)[own], _sel(O, oy.values[1], own)), (alpha, beta)
     finally:
         pamd._lib.tune("spmv_merge", p0)
+
+
+@pytest.mark.parametrize("flags", [93, 221])
+@pytest.mark.parametrize("N", [(40, 33, 21), (128, 20, 9)])
+def test_fd7_short_row_tail_launch_equals_oracle(be, pamd, O, flags, N):
+    """One FD7 part (C2's path: the pattern slices and the side rows in ONE
+    short-row tail launch, spmv_flags bit 7 = its Float64 batch-of-7 kernel
+    at 7 waves per SIMD): mul! back to back on changing x, with α/β (those
+    fall back to the 8-entry kernel), gives the oracle's bits."""
+    prev = pamd._lib.tune("spmv_flags", flags)
+    try:
+        shape = (1, 1, 1)
+        parts = be.get_part_ids(shape)
+        A = pamd.drivers.stencil_operator(parts, N, 7)
+        OA = O.stencil_problem(O.get_part_ids(shape), N, 7)
+        assert A.values.local(1).info()["side_rows"] > 0
+        rng = np.random.default_rng(SEED + 53)
+        n = A.cols.partition.local(1).num_lids
+        xs = [rng.uniform(-1, 1, n) for _ in range(3)]
+        y0 = rng.uniform(-1, 1, A.rows.partition.local(1).num_lids)
+        cases = [(1.0, 0.0), (1.0, 0.0), (-1.3, 0.5)]
+        xd = [pamd.PVector.from_host(pamd.map_parts(lambda s, v=v: v, A.cols.partition), A.cols) for v in xs]
+        ys = [pamd.PVector.from_host(pamd.map_parts(lambda s: y0, A.rows.partition), A.rows) for _ in cases]
+        for k, (alpha, beta) in enumerate(cases):  # no host sync in between
+            pamd.mul_(ys[k], A, xd[k], alpha, beta)
+        own = A.rows.partition.local(1).oid_to_lid - 1
+        for k, (alpha, beta) in enumerate(cases):
+            ox = O.PVector(O.map_parts(lambda s: xs[k].copy(), OA.cols.partition), OA.cols)
+            oy = O.PVector(O.map_parts(lambda s: y0.copy(), OA.rows.partition), OA.rows)
+            O.mul_(oy, OA, ox, alpha, beta)
+            assert np.array_equal(ys[k].to_host().local(1)[own], oy.values[1][own]), (flags, alpha, beta)
+    finally:
+        pamd._lib.tune("spmv_flags", prev)
