@@ -127,7 +127,7 @@ def rccl_run_info(infos, world):
 
 
 # the kernels of one mul! step (SpMV slices, halo pull / pack / unpack)
-PMC_KERNELS = ("k_spmv_sell", "k_spmv_merged", "k_pull_", "k_pack", "k_unpack")
+PMC_KERNELS = ("k_spmv_sell", "k_spmv_group", "k_spmv_merged", "k_pull_", "k_pack", "k_unpack")
 
 
 def pmc_traffic(args, steps=5, halo=False):
@@ -827,6 +827,16 @@ def main():
                 hr["note"] = ("format bytes count x once per part: with the parts' x and y (2 x 134 MB) "
                               "partly held in the 256 MB MALL across steps, HBM traffic can sit below them; "
                               "actual_frac is the counter-based fraction")
+                if box is not None and hr["actual_hbm_gbs"] > box[0]:
+                    # a counter rate above the box's read
+                    # probe is not HBM: FETCH_SIZE (and TCC_EA0_RDREQ_DRAM, which
+                    # equals TCC_EA0_RDREQ on gfx950, profiles/r06/f/) counts
+                    # Infinity-Cache hits, and no counter separates them
+                    hr["actual_exceeds_box_read"] = True
+                    hr["actual_frac_hbm_bound"] = round(box[0] / HBM_PEAK_GBS, 4)
+                    hr["actual_note"] = ("the counter rate exceeds this box's read probe: it includes Infinity-Cache "
+                                         "hits (TCC_EA0_RDREQ_DRAM == TCC_EA0_RDREQ on gfx950), so HBM reads are at "
+                                         "most the probe's rate, actual_frac_hbm_bound")
     halo = s_nhids > 0
     line = {
         "metric": "SpMV+halo GB/s (frac of HBM peak), 3D Poisson 27-pt, 1/2/4/8 MI355X",
@@ -873,7 +883,8 @@ def main():
             "traffic": None if traffic is None else int(traffic),
             "traffic_detail": tnote,
             "kernel": ("k_spmv_sell_group (one part: the pattern slices with the side rows as trailing waves, "
-                       "XCD runs) / k_spmv_merged (parts sharing a GPU): all SpMV kernels of one mul! step"
+                       "XCD runs; rows <= 7 entries in Float64: k_spmv_group_short7) / k_spmv_merged (parts "
+                       "sharing a GPU): all SpMV kernels of one mul! step"
                        + (", halo pack/pull" if halo else "") + ""),
             "kernel_ms": round(kernel_ms, 4),
             "kernel_ms_note": ("HIP events on part %d's compute stream around the K timed steps, / K" % p0

@@ -18,7 +18,7 @@ import sys
 import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-SPMV = ("k_spmv_sell", "k_spmv_merged")
+SPMV = ("k_spmv_sell", "k_spmv_group", "k_spmv_merged")
 
 
 def child(a):
