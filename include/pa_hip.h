@@ -58,7 +58,9 @@ int pa_version(void);
 int pa_device_count(int* count);
 /* Process-wide tuning knobs (performance only, results unchanged); each is
  * an A/B lever kept because a configuration uses it or a test pins it:
- * "spmv_flags"  bit 0: non-temporal value/column streams, bit 2: pattern
+ * "spmv_flags"  bit 0: non-temporal value/column streams, bit 1: pattern
+ *               slices of the per-kind launches read offset, length and
+ *               mask as one descriptor load, bit 2: pattern
  *               rows fetch x as 16 B runs, bit 3: the last len % U entries
  *               of a slice as one predicated batch, bit 4: a slice list
  *               covering the whole structure is launched without the list,
@@ -66,7 +68,7 @@ int pa_device_count(int* count);
  *               whose rows have at most 8 entries use the short-row kernels
  *               (one predicated batch, no loop: fewer registers), bit 7:
  *               the Float64 short-row tail launch of rows <= 7 entries at
- *               7 waves per SIMD (default 221);
+ *               7 waves per SIMD (default 223);
  * "spmv_format" 1: pattern slices where the matrix has them (default),
  *               0: int32 column ids everywhere;
  * "long_rows_exact" 1: long rows summed in the reference's order (default),

@@ -86,9 +86,9 @@ void launch_gather_scatter(int P, const void* const* srcs, int accsz, int nd, vo
 //    1.075 ms (profiles/r03/s, final, f, d) — the fused SpMV gathers two
 //    vectors (r and u_old) per x value — so 2 = measure one batch of each on
 //    this box and keep the faster (pa_cg_solve_all);
-//  * spmv_flags 221, spmv_format 1, long_rows_exact 1: pa_spmv.hip.
+//  * spmv_flags 223, spmv_format 1, long_rows_exact 1: pa_spmv.hip.
 const Knobs kDefaults = {
-    /*spmv_flags*/ 221, /*long_exact*/ 1, /*halo_pull*/ 1, /*spmv_delta16*/ 1, /*spmv_merge*/ 1,
+    /*spmv_flags*/ 223, /*long_exact*/ 1, /*halo_pull*/ 1, /*spmv_delta16*/ 1, /*spmv_merge*/ 1,
     /*spmv_merge_max*/ 65536, /*cg_fuse*/ 2, /*halo_direct*/ 1, /*halo_transport*/ 0, /*spmv_group*/ 1,
     /*spmv_format*/ 1, /*pattern_min_pct*/ 0, /*issue_threads*/ 1, /*fault_inject*/ 0, /*spmv_xcd_chunk*/ -1, /*spmv_tri16*/ 1,
     /*halo_barrier*/ 1, /*tri_order*/ 1, /*side_tail*/ 1, /*f32_rows*/ 0};
@@ -380,6 +380,29 @@ int dedup_patterns(pa_mat* A, const std::vector<int32_t>& kind) {
   if (table.empty()) table.assign(K, 0);
   if (dev_upload(&A->d_pat, table)) return -1;
   HIPC(hipMemcpyAsync(A->d_plen, packed.data(), ns * 4, hipMemcpyHostToDevice, st));
+  {
+    // the pattern slices' descriptors (SPMV_DESC): offset / H, the length
+    // word and the mask words in one aligned record per slice, so a wave of
+    // a per-kind launch reads its slice's metadata with one scalar load
+    // (FD7 128^3: 0.0290 -> 0.0277 ms, profiles/r06/o/)
+    std::vector<int64_t> soff(ns);
+    HIPC(hipMemcpyAsync(soff.data(), A->d_slice_off, ns * 8, hipMemcpyDeviceToHost, st));
+    HIPC(hipStreamSynchronize(st));
+    const int W = A->H / 64, DW = desc_words(A->R);
+    std::vector<uint64_t> mask(ns * W);
+    HIPC(hipMemcpyAsync(mask.data(), A->d_mask, ns * W * 8, hipMemcpyDeviceToHost, st));
+    HIPC(hipStreamSynchronize(st));
+    std::vector<int32_t> desc(DW * ns, 0);
+    for (int64_t s = 0; s < ns; ++s) {
+      CHECK_ARG(soff[s] % A->H == 0 && soff[s] / A->H <= INT32_MAX, "slice offset outside the descriptor's range");
+      desc[DW * s] = (int32_t)(soff[s] / A->H);
+      desc[DW * s + 1] = packed[s];
+      std::memcpy(&desc[DW * s + 4], &mask[s * W], W * 8);
+    }
+    dev_free(A->d_pdesc);
+    A->d_pdesc = nullptr;
+    if (dev_upload(&A->d_pdesc, desc)) return -1;
+  }
   HIPC(hipStreamSynchronize(st));
   return 0;
 }
@@ -1264,8 +1287,8 @@ struct Knob {
   const char* help;
 };
 const Knob kKnobs[] = {
-    {"spmv_flags", &Knobs::spmv_flags, nullptr, 0, 0xfd, 0xfd,
-     "spmv_flags: bit 0 = non-temporal streams, "
+    {"spmv_flags", &Knobs::spmv_flags, nullptr, 0, 0xff, 0xff,
+     "spmv_flags: bit 0 = non-temporal streams, bit 1 = pattern slices' one-load descriptor (per-kind launches), "
      "bit 2 = 16 B x runs (pattern rows), bit 3 = masked tail batch, bit 4 = identity slice lists dropped, "
      "bit 5 = non-temporal y stores, bit 6 = short-row kernels (launches whose rows have <= 8 entries), "
      "bit 7 = the Float64 short-row tail launch at 7 entries and 7 waves per SIMD (rows <= 7 entries)"},
@@ -2968,7 +2991,7 @@ int pa_mat_destroy(pa_mat* A) {
   dev_free(A->d_col);
   dev_free(A->d_val);
   dev_free(A->d_nz_slot);
-  for (void* p : {(void*)A->d_kind, (void*)A->d_plen, (void*)A->d_pat, (void*)A->d_mask,
+  for (void* p : {(void*)A->d_kind, (void*)A->d_plen, (void*)A->d_pdesc, (void*)A->d_pat, (void*)A->d_mask,
                   (void*)A->d_pint_list, (void*)A->d_pbnd_list, (void*)A->d_xint_list,
                   (void*)A->d_xbnd_list, (void*)A->d_s_off, (void*)A->d_s_len,
                   (void*)A->d_s_col, A->d_s_val, (void*)A->d_s_rowmap, (void*)A->d_s_rowlen, A->d_dotp,
@@ -3035,7 +3058,10 @@ int pa_mat_traffic(const pa_mat* A, int64_t* value_bytes, int64_t* index_bytes, 
     const int kd = pat ? A->h_kind[s] : 0;
     if (kd == 1) {
       v += (int64_t)A->h_plen[s] * H * S;
-      m += W * 8 + 8 + 4 + 4;  // mask, offset, length | pattern id, list entry
+      // mask, offset, length | pattern id, list entry; the per-kind
+      // launches read the descriptor instead (desc_words, at least as many
+      // bytes): counted as the larger
+      m += std::max<int64_t>(W * 8 + 8 + 4, 4 * desc_words(A->R)) + 4;
     } else if (kd == 3) {
       v += (int64_t)A->h_slen[s] * H * S;
       ix += (int64_t)A->h_slen[s] * H * 2;

@@ -471,6 +471,10 @@ struct pa_vec {
   void* base = nullptr;   // the allocation (owned; null for views)
 };
 
+// int32 words of a pattern slice's descriptor (dedup_patterns, SPMV_DESC):
+// 4 header words + the slice's H/64 64-bit mask words, a power of two
+constexpr int desc_words(int R) { return R <= 2 ? 8 : 16; }
+
 struct pa_mat {
   pa_ctx* ctx = nullptr;
   int dtype = PA_F64;
@@ -531,6 +535,7 @@ struct pa_mat {
   bool has_pat = false;
   int kmax = 0;                      // pattern stride per slice
   int32_t* d_kind = nullptr;         // per slice: 1 pattern, 0 int32 columns
+  int32_t* d_pdesc = nullptr;        // per slice desc_words(R) int32: {offset / H, d_plen, 0, 0, mask words} (SPMV_DESC)
   int32_t* d_plen = nullptr;         // per slice: entries per row (int32 len; pattern slices: len (bits 0-7) | tri flag (bit 8) | pattern id << 9)
   int32_t* d_pat = nullptr;          // npatterns*kmax offsets: the distinct patterns (dedup_patterns)
   int64_t npatterns = 0;

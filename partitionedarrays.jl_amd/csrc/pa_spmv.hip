@@ -50,10 +50,10 @@ struct alignas(2 * R) S16Pack {
   uint16_t c[R];
 };
 
-// Bits 1 (XCD remap), 9 (lane-shared x runs) and the old bit 7 (x runs in
-// int32 slices) were negative A/Bs of rounds 1-3 and are
-// gone; bit 7 is SPMV_SHORT7 since r06.
-enum { SPMV_NT = 1, SPMV_XPAIR = 4, SPMV_TAILB = 8, SPMV_IDLIST = 16, SPMV_YNT = 32, SPMV_SHORT = 64,
+// Bits 9 (lane-shared x runs), the old bit 1 (XCD remap) and the old bit 7
+// (x runs in int32 slices) were negative A/Bs of rounds 1-3
+// and are gone; bits 7 (SPMV_SHORT7) and 1 (SPMV_DESC) are r06's.
+enum { SPMV_NT = 1, SPMV_DESC = 2 /* pattern slices: one 32 B descriptor load (make_args) */, SPMV_XPAIR = 4, SPMV_TAILB = 8, SPMV_IDLIST = 16, SPMV_YNT = 32, SPMV_SHORT = 64,
        SPMV_SHORT7 = 128 /* Float64 rows <= 7 entries: k_spmv_group_short7 */,
        SPMV_PRODA = 256 /* per matrix: CSR parent, α scales the product */ };
 
@@ -65,11 +65,14 @@ typedef unsigned int spmv_u32x4 __attribute__((ext_vector_type(4)));
 // (profiles/r01/ab_tail.txt: FD7 256³ F64 −31 %, F32 −42 %; FE27 −1…−3 %),
 // identity slice lists dropped (profiles/r01/ab_idlist.txt: FD7 −0.9 %, FE27 ±0),
 // the Float64 7-entry short-row tail launch (C2 0.0281 -> 0.0278 ms, both
-// orders of 7 interleaved rounds, profiles/r06/j/).
-// (the knob defaults: pa_api.cpp kDefaults; spmv_flags 221 = NT | XPAIR |
-// TAILB | IDLIST | SHORT | SHORT7)
-static_assert((SPMV_NT | SPMV_XPAIR | SPMV_TAILB | SPMV_IDLIST | SPMV_SHORT | SPMV_SHORT7) == 221,
+// orders of 7 interleaved rounds, profiles/r06/j/), the pattern slices'
+// one-load descriptor (C2 -4.6 %, profiles/r06/o/).
+// (the knob defaults: pa_api.cpp kDefaults; spmv_flags 223 = NT | DESC |
+// XPAIR | TAILB | IDLIST | SHORT | SHORT7)
+static_assert((SPMV_NT | SPMV_DESC | SPMV_XPAIR | SPMV_TAILB | SPMV_IDLIST | SPMV_SHORT | SPMV_SHORT7) == 223,
               "kDefaults.spmv_flags");
+template <int R>
+constexpr int kDescWords = desc_words(R);
 
 // SpmvArgs' pointers are global memory.  The merged launch reads them from a
 // device-resident table, where the compiler cannot see their address space:
@@ -142,6 +145,11 @@ struct SpmvArgs {
   PA_GLB T* xacc;
   const PA_GLB CGState* cg;
   int xcd_chunk;            // xcd_block (the k_spmv_sell / _group launches; merged: a kernel argument)
+  // pattern slices of the per-kind launches (SPMV_DESC): per slice one
+  // descriptor of kDescWords int32 {offset / H, length word, 0, 0, the
+  // slice's H/64 mask words} read with one scalar load (dedup_patterns);
+  // null: soff, slen and mask (the merged launches)
+  const PA_GLB int32_t* pdesc;
 };
 
 template <typename T> struct DAcc { using type = double; };
@@ -556,7 +564,7 @@ __device__ __forceinline__ void rows_t16_tri(T (&acc)[R], const S16Pack<R>* __re
   // 0.0679 -> 0.0682 ms, six alternating rounds, ab_f32_tri_batch6_c5.log).
   // 8 B elements keep 4: 6 costs C5 F64 0.1056 -> 0.1094 ms, ComplexF32
   // 0.1083 -> 0.1149 (ab_f64_c64_tri_batch6_c5.log)
-  constexpr int TB = sizeof(T) == 4 ? 8 : kTriBatch;
+  constexpr int TB = kTriBatch;
   auto step = [&](const S16Pack<R>* q, const Pack<T, R>* v, auto nb) {
     constexpr int B = decltype(nb)::value;
     T xv[B][3][R];
@@ -583,6 +591,49 @@ __device__ __forceinline__ void rows_t16_tri(T (&acc)[R], const S16Pack<R>* __re
         }
   };
   int t = 0;
+  if constexpr (sizeof(T) == 4) {
+    // Float32: batches of 9 triples (an FE27 row is one batch), the last
+    // batch clamped: past the row's end a lane re-reads its last triple
+    // (the same lines) and never accumulates it, so the batch stays
+    // branch-free (a predicated batch holds 186-208 VGPRs, this one 145: 3
+    // waves per SIMD like the 8-triple loop with its single-triple tail).
+    // Library A/B, six alternating rounds on one box (profiles/r06/n/): C5
+    // F32 0.0686 -> 0.0672 ms, kernels 0.0735 -> 0.0720 ms
+    constexpr int MB = 9;
+    for (; t < ntri; t += MB) {
+      S16Pack<R> q[MB];
+      Pack<T, R> v[3 * MB];
+#pragma unroll
+      for (int u = 0; u < MB; ++u) q[u] = ld<NT>(&cp[min(t + u, ntri - 1) * 64]);
+#pragma unroll
+      for (int u = 0; u < MB; ++u)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) v[3 * u + j] = ld<NT>(&vp[(3 * min(t + u, ntri - 1) + j) * 64]);
+      T xv[MB][3][R];
+      bool ok[MB][R];
+#pragma unroll
+      for (int u = 0; u < MB; ++u)
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          const int32_t c = d16_col(q[u].c[r], rw[r], gb);
+          ok[u][r] = c >= 0 && t + u < ntri;
+          T t3[3];
+          x.trip(c >= 0 ? c : 0, t3);
+#pragma unroll
+          for (int j = 0; j < 3; ++j) xv[u][j][r] = t3[j];
+        }
+#pragma unroll
+      for (int u = 0; u < MB; ++u)
+#pragma unroll
+        for (int j = 0; j < 3; ++j)
+#pragma unroll
+          for (int r = 0; r < R; ++r) {
+            const T tt = acc[r] + term<ALPHA>(v[3 * u + j].v[r], xv[u][j][r], alpha, pf);
+            acc[r] = pick(ok[u][r], tt, acc[r]);
+          }
+    }
+    return;
+  }
   for (; t + TB <= ntri; t += TB) {
     S16Pack<R> q[TB];
     Pack<T, R> v[3 * TB];
@@ -854,13 +905,36 @@ __device__ __forceinline__ void spmv_wave(const SpmvArgs<T>& a, const int64_t w)
   } else {
     xs.x = (const T*)a.x;
   }
-  const int64_t off = a.soff[s];
-  const int32_t lraw = a.slen[s];
+  // the slice's metadata: offset, length word (and, pattern slices, the
+  // lane's mask word).  Pattern slices of the per-kind launches read all of
+  // it as one 32 B (64 B for 4 rows per lane) descriptor with one scalar
+  // load instead of three loads on two paths (SPMV_DESC; same-copy A/B,
+  // profiles/r06/o/: FD7 128^3 0.0290 -> 0.0277 ms, FE27 256^3 +-0; the
+  // merged launch of the (2,2,2) halo leg +0.5 %, so it keeps the arrays)
+  int64_t off;
+  int32_t lraw;
+  uint64_t dmask = 0;
+  if (PAT && a.pdesc) {
+    constexpr int W = H / 64, DW = kDescWords<R>;
+    typedef int iv __attribute__((ext_vector_type(DW)));
+    const iv d = *reinterpret_cast<const iv*>(a.pdesc + DW * s);
+    off = (int64_t)d[0] * H;
+    lraw = d[1];
+    const int wi = (lane * R) / 64;
+#pragma unroll
+    for (int i = 0; i < W; ++i) {
+      const uint64_t mw = (uint64_t)(uint32_t)d[4 + 2 * i] | ((uint64_t)(uint32_t)d[5 + 2 * i] << 32);
+      if (i == 0 || wi == i) dmask = mw;
+    }
+  } else {
+    off = a.soff[s];
+    lraw = a.slen[s];
+  }
   // pattern slices: len | tri << 8 | pattern id << 9 (dedup_patterns); triple SELL: len | kTriSlice
   const int len = PAT ? (lraw & 0xff) : (PK == 4 ? (lraw & (kTriSlice - 1)) : lraw);
   bool ok[R];
   if (PAT) {
-    const uint64_t m = a.mask[s * (H / 64) + (lane * R) / 64];
+    const uint64_t m = a.pdesc ? dmask : a.mask[s * (H / 64) + (lane * R) / 64];
 #pragma unroll
     for (int r = 0; r < R; ++r) ok[r] = ((m >> ((lane * R + r) & 63)) & 1ull) && (row0 + r < a.nrows);
   } else {
@@ -1218,6 +1292,7 @@ static SpmvArgs<T> make_args(int which, int64_t nwork, const int32_t* list, cons
       a.pat = (decltype(a.pat))(A->d_pat);
       a.mask = (decltype(a.mask))(A->d_mask);
       a.kmax = A->kmax;
+      if (knobs().spmv_flags & SPMV_DESC) a.pdesc = (decltype(a.pdesc))(A->d_pdesc);
     } else {
       a.slen = (decltype(a.slen))(A->d_slice_len);
       if (which == 4) {
@@ -1461,6 +1536,7 @@ static int merged_prepare(int n, const int* which, const SpmvPart* parts, bool h
     const int32_t* list = q.list;
     if ((knobs().spmv_flags & SPMV_IDLIST) && list && which[i] != 2 && which[i] != 5 && q.nwork == q.A->nslices) list = nullptr;
     h.a[h.n] = make_args<T>(which[i], q.nwork, list, q.A, q.x, q.y, q.ymap, alpha, beta, q.dotp, &q);
+    h.a[h.n].pdesc = nullptr;  // the merged launch reads soff / slen / mask (SPMV_DESC: per-kind launches)
     h.pk[h.n] = pk_of(which[i]);
     sh = sh && h.a[h.n].maxlen <= 8;
     h.start[h.n + 1] = h.start[h.n] + q.nwork;

@@ -617,7 +617,7 @@ def test_short_row_side_tail_equals_oracle(be, pamd, O, dtype):
         pamd._lib.tune("spmv_merge", p0)
 
 
-@pytest.mark.parametrize("flags", [93, 221])
+@pytest.mark.parametrize("flags", [93, 221, 223])
 @pytest.mark.parametrize("N", [(40, 33, 21), (128, 20, 9)])
 def test_fd7_short_row_tail_launch_equals_oracle(be, pamd, O, flags, N):
     """One FD7 part (C2's path: the pattern slices and the side rows in ONE
@@ -646,5 +646,37 @@ def test_fd7_short_row_tail_launch_equals_oracle(be, pamd, O, flags, N):
             oy = O.PVector(O.map_parts(lambda s: y0.copy(), OA.rows.partition), OA.rows)
             O.mul_(oy, OA, ox, alpha, beta)
             assert np.array_equal(ys[k].to_host().local(1)[own], oy.values[1][own]), (flags, alpha, beta)
+    finally:
+        pamd._lib.tune("spmv_flags", prev)
+
+
+@pytest.mark.parametrize("dtype", [np.float64, np.float32, np.complex128, np.complex64])
+@pytest.mark.parametrize("flags", [221, 223])
+def test_pattern_slice_descriptor_equals_oracle(be, pamd, O, dtype, flags):
+    """One FE27 part (per-kind launches): the pattern slices' metadata read
+    as one descriptor (spmv_flags bit 1: offset / H, length word and mask
+    words, 32 B for 1-2 rows per lane, 64 B for Float32's 4) or from the
+    three arrays gives the oracle's bits, on a grid whose boundary planes
+    make several patterns and partial masks."""
+    prev = pamd._lib.tune("spmv_flags", flags)
+    try:
+        shape, N = (1, 1, 1), (70, 19, 11)
+        parts = be.get_part_ids(shape)
+        A = pamd.drivers.stencil_operator(parts, N, 27, dtype)
+        info = A.values.local(1).info()
+        assert info["pattern_slices"] > 0 and info["side_rows"] > 0
+        rng = np.random.default_rng(SEED + 61)
+        xs = _rand(rng, A.cols.partition.local(1).num_lids, dtype)
+        x = pamd.PVector.from_host(pamd.map_parts(lambda s: xs, A.cols.partition), A.cols)
+        OA = O.stencil_problem(O.get_part_ids(shape), N, 27, dtype)
+        own = A.rows.partition.local(1).oid_to_lid - 1
+        for alpha in (1.0, 0.75):
+            y = pamd.PVector.undef(A.rows, dtype)
+            pamd.mul_(y, A, x, alpha, 0.0)
+            ox = O.PVector(O.map_parts(lambda s: _to_oracle(O, xs), OA.cols.partition), OA.cols)
+            oy = O.pvector_undef(OA.rows, dtype)
+            oa = np.float32(alpha) if np.dtype(dtype) in (np.float32, np.complex64) else alpha
+            O.mul_(oy, OA, ox, oa, 0.0)
+            assert _eq(O, y.to_host().local(1)[own], _sel(O, oy.values[1], own)), (flags, alpha)
     finally:
         pamd._lib.tune("spmv_flags", prev)
