@@ -59,8 +59,8 @@ int pa_device_count(int* count);
 /* Process-wide tuning knobs (performance only, results unchanged); each is
  * an A/B lever kept because a configuration uses it or a test pins it:
  * "spmv_flags"  bit 0: non-temporal value/column streams, bit 1: pattern
- *               slices of the per-kind launches read offset, length and
- *               mask as one descriptor load, bit 2: pattern
+ *               and triple-SELL slices read their offset, length and mask /
+ *               ghost base as one descriptor load, bit 2: pattern
  *               rows fetch x as 16 B runs, bit 3: the last len % U entries
  *               of a slice as one predicated batch, bit 4: a slice list
  *               covering the whole structure is launched without the list,

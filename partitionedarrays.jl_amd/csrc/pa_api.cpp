@@ -382,9 +382,9 @@ int dedup_patterns(pa_mat* A, const std::vector<int32_t>& kind) {
   HIPC(hipMemcpyAsync(A->d_plen, packed.data(), ns * 4, hipMemcpyHostToDevice, st));
   {
     // the pattern slices' descriptors (SPMV_DESC): offset / H, the length
-    // word and the mask words in one aligned record per slice, so a wave of
-    // a per-kind launch reads its slice's metadata with one scalar load
-    // (FD7 128^3: 0.0290 -> 0.0277 ms, profiles/r06/o/)
+    // word and the mask words in one aligned record per slice, so a wave
+    // reads its slice's metadata with one scalar load (FD7 128^3: 0.0287 ->
+    // 0.0277 ms, profiles/r06/p/)
     std::vector<int64_t> soff(ns);
     HIPC(hipMemcpyAsync(soff.data(), A->d_slice_off, ns * 8, hipMemcpyDeviceToHost, st));
     HIPC(hipStreamSynchronize(st));
@@ -437,9 +437,10 @@ int remap_nz_interleaved(pa_mat* A, const std::vector<int32_t>& kind, hipStream_
 void free_triple_sell(pa_mat* A) {
   for (void* p : {(void*)A->d_t_off, (void*)A->d_t_len, (void*)A->d_t_col16, A->d_t_val, (void*)A->d_t_gbase,
                   (void*)A->d_t_rowmap, (void*)A->d_t_src, (void*)A->d_t_rowlen, (void*)A->d_t_int_list,
-                  (void*)A->d_t_bnd_list})
+                  (void*)A->d_t_bnd_list, (void*)A->d_t_desc})
     dev_free(p);
   A->d_t_off = nullptr;
+  A->d_t_desc = nullptr;
   A->d_t_len = A->d_t_gbase = A->d_t_rowmap = A->d_t_rowlen = A->d_t_int_list = A->d_t_bnd_list = nullptr;
   A->d_t_col16 = nullptr;
   A->d_t_val = nullptr;
@@ -559,6 +560,18 @@ int build_triple_sell(pa_mat* A, std::vector<int32_t>& kind, int64_t noids) {
       free_triple_sell(A);
       return 0;
     }
+  {  // one 16 B descriptor per slice (SPMV_DESC): offset / H, length word, ghost base
+    std::vector<int32_t> gbase(tns), desc(4 * tns, 0);
+    HIPC(hipMemcpyAsync(gbase.data(), A->d_t_gbase, tns * 4, hipMemcpyDeviceToHost, st));
+    HIPC(hipStreamSynchronize(st));
+    for (int64_t ts = 0; ts < tns; ++ts) {
+      CHECK_ARG(toff[ts] / H <= INT32_MAX, "slice offset outside the descriptor's range");
+      desc[4 * ts] = (int32_t)(toff[ts] / H);
+      desc[4 * ts + 1] = tlen[ts];
+      desc[4 * ts + 2] = gbase[ts];
+    }
+    if (dev_upload(&A->d_t_desc, desc)) return -1;
+  }
   launch_t_fill(A, noids, true, st);
   HIPC(hipGetLastError());
   unsigned* d_bad = nullptr;
@@ -1288,7 +1301,7 @@ struct Knob {
 };
 const Knob kKnobs[] = {
     {"spmv_flags", &Knobs::spmv_flags, nullptr, 0, 0xff, 0xff,
-     "spmv_flags: bit 0 = non-temporal streams, bit 1 = pattern slices' one-load descriptor (per-kind launches), "
+     "spmv_flags: bit 0 = non-temporal streams, bit 1 = pattern and triple-SELL slices' one-load descriptor, "
      "bit 2 = 16 B x runs (pattern rows), bit 3 = masked tail batch, bit 4 = identity slice lists dropped, "
      "bit 5 = non-temporal y stores, bit 6 = short-row kernels (launches whose rows have <= 8 entries), "
      "bit 7 = the Float64 short-row tail launch at 7 entries and 7 waves per SIMD (rows <= 7 entries)"},
@@ -3058,9 +3071,8 @@ int pa_mat_traffic(const pa_mat* A, int64_t* value_bytes, int64_t* index_bytes, 
     const int kd = pat ? A->h_kind[s] : 0;
     if (kd == 1) {
       v += (int64_t)A->h_plen[s] * H * S;
-      // mask, offset, length | pattern id, list entry; the per-kind
-      // launches read the descriptor instead (desc_words, at least as many
-      // bytes): counted as the larger
+      // mask, offset, length | pattern id, list entry; with SPMV_DESC the
+      // descriptor instead (desc_words): counted as the larger
       m += std::max<int64_t>(W * 8 + 8 + 4, 4 * desc_words(A->R)) + 4;
     } else if (kd == 3) {
       v += (int64_t)A->h_slen[s] * H * S;
@@ -3081,7 +3093,7 @@ int pa_mat_traffic(const pa_mat* A, int64_t* value_bytes, int64_t* index_bytes, 
     m += A->s_nslices * 12;
     v += A->t_slots * S;              // triple SELL: values (padding included)
     ix += A->t_code_slots * 2 + A->t_nrows * 4;  // codes (one per triple in tri slices), row map
-    m += A->t_nslices * (8 + 4 + 4 + 4);  // offset, length, ghost base, list entry
+    m += A->t_nslices * (8 + 4 + 4 + 4);  // offset, length, ghost base, list entry (the 16 B descriptor + list entry)
   }
   v += A->n_lnz * S;
   ix += A->n_lnz * 4;

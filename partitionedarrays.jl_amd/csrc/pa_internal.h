@@ -583,6 +583,7 @@ struct pa_mat {
   uint16_t* d_t_col16 = nullptr;     // codes (tri slices: one per triple, slot groups 0..len/3-1)
   void* d_t_val = nullptr;           // values (lane-major packs of R, like the main SELL)
   int32_t* d_t_gbase = nullptr;      // per slice: smallest ghost column
+  int32_t* d_t_desc = nullptr;       // per slice {offset / H, d_t_len, d_t_gbase, 0} (SPMV_DESC)
   int32_t* d_t_rowmap = nullptr;     // structure row → oid
   int64_t* d_t_src = nullptr;        // structure row → its main-layout slot of entry 0 (entry k: + k*64*R)
   int32_t* d_t_rowlen = nullptr;     // structure row → its entries

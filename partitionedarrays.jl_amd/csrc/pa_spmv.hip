@@ -53,7 +53,7 @@ struct alignas(2 * R) S16Pack {
 // Bits 9 (lane-shared x runs), the old bit 1 (XCD remap) and the old bit 7
 // (x runs in int32 slices) were negative A/Bs of rounds 1-3
 // and are gone; bits 7 (SPMV_SHORT7) and 1 (SPMV_DESC) are r06's.
-enum { SPMV_NT = 1, SPMV_DESC = 2 /* pattern slices: one 32 B descriptor load (make_args) */, SPMV_XPAIR = 4, SPMV_TAILB = 8, SPMV_IDLIST = 16, SPMV_YNT = 32, SPMV_SHORT = 64,
+enum { SPMV_NT = 1, SPMV_DESC = 2 /* pattern / triple-SELL slices: one descriptor load (make_args) */, SPMV_XPAIR = 4, SPMV_TAILB = 8, SPMV_IDLIST = 16, SPMV_YNT = 32, SPMV_SHORT = 64,
        SPMV_SHORT7 = 128 /* Float64 rows <= 7 entries: k_spmv_group_short7 */,
        SPMV_PRODA = 256 /* per matrix: CSR parent, α scales the product */ };
 
@@ -145,11 +145,12 @@ struct SpmvArgs {
   PA_GLB T* xacc;
   const PA_GLB CGState* cg;
   int xcd_chunk;            // xcd_block (the k_spmv_sell / _group launches; merged: a kernel argument)
-  // pattern slices of the per-kind launches (SPMV_DESC): per slice one
-  // descriptor of kDescWords int32 {offset / H, length word, 0, 0, the
-  // slice's H/64 mask words} read with one scalar load (dedup_patterns);
-  // null: soff, slen and mask (the merged launches)
-  const PA_GLB int32_t* pdesc;
+  // pattern slices (SPMV_DESC): per slice one descriptor of kDescWords
+  // int32 {offset / H, length word, 0, 0, the slice's H/64 mask words} read
+  // with one scalar load (dedup_patterns); null: soff, slen and mask
+  // triple-SELL slices (SPMV_DESC): 4 int32 {offset / H, length word,
+  // ghost base, 0} per slice, one scalar load (build_triple_sell)
+  const PA_GLB int32_t* desc;
 };
 
 template <typename T> struct DAcc { using type = double; };
@@ -906,18 +907,20 @@ __device__ __forceinline__ void spmv_wave(const SpmvArgs<T>& a, const int64_t w)
     xs.x = (const T*)a.x;
   }
   // the slice's metadata: offset, length word (and, pattern slices, the
-  // lane's mask word).  Pattern slices of the per-kind launches read all of
-  // it as one 32 B (64 B for 4 rows per lane) descriptor with one scalar
-  // load instead of three loads on two paths (SPMV_DESC; same-copy A/B,
-  // profiles/r06/o/: FD7 128^3 0.0290 -> 0.0277 ms, FE27 256^3 +-0; the
-  // merged launch of the (2,2,2) halo leg +0.5 %, so it keeps the arrays)
+  // lane's mask word; triple-SELL slices, the ghost base).  With SPMV_DESC
+  // pattern and triple-SELL slices read all of it as one descriptor (32 B,
+  // 64 B for 4 rows per lane; 16 B) with one scalar load instead of three
+  // loads on two paths.  Same-copy A/Bs (profiles/r06/o/, p/, q/): FD7 128^3
+  // 0.0287 -> 0.0277 ms, C5 F32 0.0658 -> 0.0649, C5 F64 -0.3 %, FE27 256^3
+  // and the (2,2,2) halo leg -0.1 %
   int64_t off;
   int32_t lraw;
   uint64_t dmask = 0;
-  if (PAT && a.pdesc) {
+  int32_t tgb = 0;
+  if (PAT && a.desc) {
     constexpr int W = H / 64, DW = kDescWords<R>;
     typedef int iv __attribute__((ext_vector_type(DW)));
-    const iv d = *reinterpret_cast<const iv*>(a.pdesc + DW * s);
+    const iv d = *reinterpret_cast<const iv*>(a.desc + DW * s);
     off = (int64_t)d[0] * H;
     lraw = d[1];
     const int wi = (lane * R) / 64;
@@ -926,6 +929,12 @@ __device__ __forceinline__ void spmv_wave(const SpmvArgs<T>& a, const int64_t w)
       const uint64_t mw = (uint64_t)(uint32_t)d[4 + 2 * i] | ((uint64_t)(uint32_t)d[5 + 2 * i] << 32);
       if (i == 0 || wi == i) dmask = mw;
     }
+  } else if (PK == 4 && a.desc) {
+    typedef int i4v __attribute__((ext_vector_type(4)));
+    const i4v d = *reinterpret_cast<const i4v*>(a.desc + 4 * s);
+    off = (int64_t)d[0] * H;
+    lraw = d[1];
+    tgb = d[2];
   } else {
     off = a.soff[s];
     lraw = a.slen[s];
@@ -934,7 +943,7 @@ __device__ __forceinline__ void spmv_wave(const SpmvArgs<T>& a, const int64_t w)
   const int len = PAT ? (lraw & 0xff) : (PK == 4 ? (lraw & (kTriSlice - 1)) : lraw);
   bool ok[R];
   if (PAT) {
-    const uint64_t m = a.pdesc ? dmask : a.mask[s * (H / 64) + (lane * R) / 64];
+    const uint64_t m = a.desc ? dmask : a.mask[s * (H / 64) + (lane * R) / 64];
 #pragma unroll
     for (int r = 0; r < R; ++r) ok[r] = ((m >> ((lane * R + r) & 63)) & 1ull) && (row0 + r < a.nrows);
   } else {
@@ -998,7 +1007,7 @@ __device__ __forceinline__ void spmv_wave(const SpmvArgs<T>& a, const int64_t w)
     // triple SELL (rows through the row map, interleaved): tri slices carry
     // one code per triple, the others one per entry (rows_d16)
     const S16Pack<R>* __restrict__ cp = reinterpret_cast<const S16Pack<R>*>(a.col16 + off) + lane;
-    const int32_t gb = a.gbase[s];
+    const int32_t gb = a.desc ? tgb : a.gbase[s];
     int32_t rw[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) rw[r] = (int32_t)orow[r];
@@ -1275,6 +1284,7 @@ static SpmvArgs<T> make_args(int which, int64_t nwork, const int32_t* list, cons
     a.val = (decltype(a.val))((const T*)A->d_t_val);
     a.rowmap = (decltype(a.rowmap))(A->d_t_rowmap);
     a.nrows = A->t_nrows;
+    if (knobs().spmv_flags & SPMV_DESC) a.desc = (decltype(a.desc))(A->d_t_desc);
   } else if (which == 2) {
     a.soff = (decltype(a.soff))(A->d_s_off);
     a.slen = (decltype(a.slen))(A->d_s_len);
@@ -1292,7 +1302,7 @@ static SpmvArgs<T> make_args(int which, int64_t nwork, const int32_t* list, cons
       a.pat = (decltype(a.pat))(A->d_pat);
       a.mask = (decltype(a.mask))(A->d_mask);
       a.kmax = A->kmax;
-      if (knobs().spmv_flags & SPMV_DESC) a.pdesc = (decltype(a.pdesc))(A->d_pdesc);
+      if (knobs().spmv_flags & SPMV_DESC) a.desc = (decltype(a.desc))(A->d_pdesc);
     } else {
       a.slen = (decltype(a.slen))(A->d_slice_len);
       if (which == 4) {
@@ -1536,7 +1546,6 @@ static int merged_prepare(int n, const int* which, const SpmvPart* parts, bool h
     const int32_t* list = q.list;
     if ((knobs().spmv_flags & SPMV_IDLIST) && list && which[i] != 2 && which[i] != 5 && q.nwork == q.A->nslices) list = nullptr;
     h.a[h.n] = make_args<T>(which[i], q.nwork, list, q.A, q.x, q.y, q.ymap, alpha, beta, q.dotp, &q);
-    h.a[h.n].pdesc = nullptr;  // the merged launch reads soff / slen / mask (SPMV_DESC: per-kind launches)
     h.pk[h.n] = pk_of(which[i]);
     sh = sh && h.a[h.n].maxlen <= 8;
     h.start[h.n + 1] = h.start[h.n] + q.nwork;
