@@ -120,6 +120,10 @@ int pa_device_count(int* count);
  *               slices: the Float64 geometry, so delta16 rows take the
  *               triple SELL), 0 (default, auto): 4, rebuilt with 2 when
  *               fewer than 80 % of the slices are pattern slices;
+ * "spmv_tri_pack" Float32 triple-SELL tri slices (2 rows per lane; matrices
+ *               built afterwards): bit 0 a triple's values as one 16 B and
+ *               one 8 B pack per lane, bit 1 a 9-triple batch's codes as
+ *               16 + 16 + 4 B packs; 3 (default) both, 0 neither;
  * "fault_inject" tests only: threaded issue jobs add an invalid launch. */
 int pa_tune(const char* key, int value, int* previous);
 /* The same knobs for one context: calls led by parts of `c` (their first

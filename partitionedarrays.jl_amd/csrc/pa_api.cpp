@@ -91,7 +91,7 @@ const Knobs kDefaults = {
     /*spmv_flags*/ 223, /*long_exact*/ 1, /*halo_pull*/ 1, /*spmv_delta16*/ 1, /*spmv_merge*/ 1,
     /*spmv_merge_max*/ 65536, /*cg_fuse*/ 2, /*halo_direct*/ 1, /*halo_transport*/ 0, /*spmv_group*/ 1,
     /*spmv_format*/ 1, /*pattern_min_pct*/ 0, /*issue_threads*/ 1, /*fault_inject*/ 0, /*spmv_xcd_chunk*/ -1, /*spmv_tri16*/ 1,
-    /*halo_barrier*/ 1, /*tri_order*/ 1, /*side_tail*/ 1, /*f32_rows*/ 0};
+    /*halo_barrier*/ 1, /*tri_order*/ 1, /*side_tail*/ 1, /*f32_rows*/ 0, /*tri_pack*/ 3};
 // COO → CSC → SELL on the device (pa_coo.hip)
 int coo_compress(int dtype, int index_bytes, int64_t m, int64_t ncols, int64_t n, const void* dI, const void* dJ,
                  const void* dV, int csr, int64_t* nu_out, int32_t** crow, int32_t** ccol, void** cval,
@@ -445,6 +445,7 @@ void free_triple_sell(pa_mat* A) {
   A->d_t_col16 = nullptr;
   A->d_t_val = nullptr;
   A->d_t_src = nullptr;
+  A->t_pack = 0;
   A->t_nrows = A->t_nslices = A->t_slots = A->t_tri_slices = A->t_tri_rows = A->t_code_slots = 0;
   A->nt_int = A->nt_bnd = 0;
   A->h_t_len.clear();
@@ -530,6 +531,7 @@ int build_triple_sell(pa_mat* A, std::vector<int32_t>& kind, int64_t noids) {
   }
   A->t_nrows = n;
   A->t_nslices = tns;
+  A->t_pack = A->dtype == PA_F32 && R == 2 ? knobs().tri_pack : 0;
   A->t_slots = acc;
   A->t_code_slots = codes;
   A->h_t_len = tlen;
@@ -1345,6 +1347,11 @@ const Knob kKnobs[] = {
      "slices, 2 = 8 B packs in 128-row slices (the Float64 geometry; delta16 rows then take the triple "
      "SELL), 0 = auto (default): 4, rebuilt with 2 when fewer than 80 % of the slices are pattern slices "
      "(C5 F32 -7 %, FE27 256^3 F32 +14 % with 2, profiles/r05/af/)"},
+    {"spmv_tri_pack", &Knobs::tri_pack, nullptr, 0, 3, 0,
+     "spmv_tri_pack: Float32 triple-SELL tri slices (2 rows per lane; matrices built afterwards): bit 0 = a "
+     "triple's values as one 16 B pack (entries 0 and 1 of both rows) and one 8 B pack (entry 2) per lane "
+     "(two loads instead of three), bit 1 = a batch of 9 triples' codes as two 16 B packs and one 4 B pack "
+     "(three loads instead of nine); 0 = one pack per entry and per triple"},
     {"spmv_side_tail", &Knobs::side_tail, nullptr, 0, 1, 0,
      "spmv_side_tail: per-kind launches without a halo in flight (big single parts): 1 = the side rows (<= 8 "
      "entries) run as the trailing waves of the pattern launch (default: FE27 256^3 -0.4 %, profiles/r05/o/), "

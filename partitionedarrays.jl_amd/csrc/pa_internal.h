@@ -356,6 +356,7 @@ struct Knobs {
   int tri_order;         // triple SELL row order: 0 triple rows first, 1 the other rows first (build_triple_sell)
   int side_tail;         // per-kind launches: the side rows as the trailing waves of the pattern launch
   int f32_rows;          // Float32 SELL rows per lane (matrices built afterwards): 4 (16 B packs), 2 (8 B), 0 auto
+  int tri_pack;          // Float32 triple-SELL tri slices: bit 0 per-triple value packs, bit 1 batch code packs
 };
 // the knobs of the call running on this thread (outside a call: a snapshot
 // of the process defaults)
@@ -581,7 +582,9 @@ struct pa_mat {
   int64_t* d_t_off = nullptr;        // slot offset per slice
   int32_t* d_t_len = nullptr;        // entries per row (max over the slice), bit 30: tri slice (kTriSlice)
   uint16_t* d_t_col16 = nullptr;     // codes (tri slices: one per triple, slot groups 0..len/3-1)
-  void* d_t_val = nullptr;           // values (lane-major packs of R, like the main SELL)
+  void* d_t_val = nullptr;           // values (lane-major packs of R, like the main SELL; t_pack: tri slices per triple)
+  int t_pack = 0;                    // Float32 tri slices (spmv_tri_pack): bit 0 triple t's values as {entries 0,1 × R
+                                     // rows} 16 B + {entry 2} 8 B per lane; bit 1 codes in batch packs (t_code_slot)
   int32_t* d_t_gbase = nullptr;      // per slice: smallest ghost column
   int32_t* d_t_desc = nullptr;       // per slice {offset / H, d_t_len, d_t_gbase, 0} (SPMV_DESC)
   int32_t* d_t_rowmap = nullptr;     // structure row → oid

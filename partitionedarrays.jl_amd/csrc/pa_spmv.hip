@@ -55,7 +55,9 @@ struct alignas(2 * R) S16Pack {
 // and are gone; bits 7 (SPMV_SHORT7) and 1 (SPMV_DESC) are r06's.
 enum { SPMV_NT = 1, SPMV_DESC = 2 /* pattern / triple-SELL slices: one descriptor load (make_args) */, SPMV_XPAIR = 4, SPMV_TAILB = 8, SPMV_IDLIST = 16, SPMV_YNT = 32, SPMV_SHORT = 64,
        SPMV_SHORT7 = 128 /* Float64 rows <= 7 entries: k_spmv_group_short7 */,
-       SPMV_PRODA = 256 /* per matrix: CSR parent, α scales the product */ };
+       SPMV_PRODA = 256 /* per matrix: CSR parent, α scales the product */,
+       SPMV_TPACK = 512 /* per matrix: Float32 tri slices with per-triple value packs (pa_mat::t_pack bit 0) */,
+       SPMV_TPACKC = 1024 /* per matrix: Float32 tri slices with batch code packs (pa_mat::t_pack bit 1) */ };
 
 typedef unsigned int spmv_u32x4 __attribute__((ext_vector_type(4)));
 // Process-wide knobs (pa_tune).  Defaults from the A/Bs in
@@ -553,7 +555,7 @@ constexpr int kTriBatch = 4;
 // ld_xtrip.  Padding triples (code 0xFFFF) are never accumulated.  Four
 // triples (12 values) in flight per lane, as in rows_pattern_tri.  The
 // terms and their order are those of rows_d16.
-template <typename T, int R, bool ALPHA, bool NT, typename XS>
+template <typename T, int R, bool ALPHA, bool NT, typename XS, bool TP = false, bool TPC = false>
 __device__ __forceinline__ void rows_t16_tri(T (&acc)[R], const S16Pack<R>* __restrict__ cp,
                                              const Pack<T, R>* __restrict__ vp, int len, const XS& x, T alpha,
                                              bool pf, const int32_t (&rw)[R], int32_t gb) {
@@ -604,12 +606,48 @@ __device__ __forceinline__ void rows_t16_tri(T (&acc)[R], const S16Pack<R>* __re
     for (; t < ntri; t += MB) {
       S16Pack<R> q[MB];
       Pack<T, R> v[3 * MB];
+      if (TPC && t + MB <= ntri) {
+        // packed codes (t_code_slot): triples 0-3 and 4-7 of the batch as
+        // one 4R-code pack each, triple 8 as an R pack: three loads, not nine
+        const S16Pack<R>* __restrict__ cb = cp - threadIdx.x % 64 + (int64_t)t * 64;
 #pragma unroll
-      for (int u = 0; u < MB; ++u) q[u] = ld<NT>(&cp[min(t + u, ntri - 1) * 64]);
+        for (int h = 0; h < 2; ++h) {
+          const S16Pack<4 * R> q4 = ld<NT>(reinterpret_cast<const S16Pack<4 * R>*>(cb + h * 4 * 64) + threadIdx.x % 64);
 #pragma unroll
-      for (int u = 0; u < MB; ++u)
+          for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 3; ++j) v[3 * u + j] = ld<NT>(&vp[(3 * min(t + u, ntri - 1) + j) * 64]);
+            for (int r = 0; r < R; ++r) q[4 * h + i].c[r] = q4.c[i * R + r];
+        }
+        q[8] = ld<NT>(cb + 8 * 64 + threadIdx.x % 64);
+      } else {
+#pragma unroll
+        for (int u = 0; u < MB; ++u) q[u] = ld<NT>(&cp[min(t + u, ntri - 1) * 64]);
+      }
+      if constexpr (TP) {
+        // spmv_tri_pack (k_t_fill): triple u's entries 0 and 1 of the lane's
+        // R rows as one 2R-value pack, entry 2 as an R pack: two loads per
+        // triple instead of three.  With the code packs (TPC) a full batch
+        // issues 3 + 18 loads instead of 9 + 27 ahead of its 18 x runs; C5
+        // F32 -3.2 % (profiles/r06/s/, two interleaved rounds: values alone
+        // -3.2 %, codes alone -1.4 %)
+        const Pack<T, R>* __restrict__ vb = vp - threadIdx.x % 64;  // the slice's values
+#pragma unroll
+        for (int u = 0; u < MB; ++u) {
+          const Pack<T, R>* tb = vb + (int64_t)min(t + u, ntri - 1) * 3 * 64;
+          const Pack<T, 2 * R> p01 = ld<NT>(reinterpret_cast<const Pack<T, 2 * R>*>(tb) + threadIdx.x % 64);
+#pragma unroll
+          for (int r = 0; r < R; ++r) {
+            v[3 * u].v[r] = p01.v[r];
+            v[3 * u + 1].v[r] = p01.v[R + r];
+          }
+          v[3 * u + 2] = ld<NT>(tb + 2 * 64 + threadIdx.x % 64);
+        }
+      } else {
+#pragma unroll
+        for (int u = 0; u < MB; ++u)
+#pragma unroll
+          for (int j = 0; j < 3; ++j) v[3 * u + j] = ld<NT>(&vp[(3 * min(t + u, ntri - 1) + j) * 64]);
+      }
       T xv[MB][3][R];
       bool ok[MB][R];
 #pragma unroll
@@ -1012,7 +1050,22 @@ __device__ __forceinline__ void spmv_wave(const SpmvArgs<T>& a, const int64_t w)
 #pragma unroll
     for (int r = 0; r < R; ++r) rw[r] = (int32_t)orow[r];
     if (lraw & kTriSlice) {
-      if (a.flags & SPMV_NT) rows_t16_tri<T, R, ALPHA, true>(acc, cp, vp, len, xs, a.alpha, pf, rw, gb);
+      bool packed = false;
+      if constexpr (sizeof(T) == 4 && R == 2) {
+        // per-triple value packs and/or batch code packs (k_t_fill, pa_mat::t_pack), non-temporal
+        if ((a.flags & (SPMV_TPACK | SPMV_TPACKC)) == (SPMV_TPACK | SPMV_TPACKC)) {
+          rows_t16_tri<T, R, ALPHA, true, XSrc<T, XV>, true, true>(acc, cp, vp, len, xs, a.alpha, pf, rw, gb);
+          packed = true;
+        } else if (a.flags & SPMV_TPACK) {
+          rows_t16_tri<T, R, ALPHA, true, XSrc<T, XV>, true, false>(acc, cp, vp, len, xs, a.alpha, pf, rw, gb);
+          packed = true;
+        } else if (a.flags & SPMV_TPACKC) {
+          rows_t16_tri<T, R, ALPHA, true, XSrc<T, XV>, false, true>(acc, cp, vp, len, xs, a.alpha, pf, rw, gb);
+          packed = true;
+        }
+      }
+      if (packed) {
+      } else if (a.flags & SPMV_NT) rows_t16_tri<T, R, ALPHA, true>(acc, cp, vp, len, xs, a.alpha, pf, rw, gb);
       else rows_t16_tri<T, R, ALPHA, false>(acc, cp, vp, len, xs, a.alpha, pf, rw, gb);
     } else {
       if (a.flags & SPMV_NT) rows_d16<T, R, ALPHA, true, U, SH, kIdsAhead<T, R>>(acc, cp, vp, len, xs, a.alpha, pf, tb, rw, gb);
@@ -1268,7 +1321,8 @@ static SpmvArgs<T> make_args(int which, int64_t nwork, const int32_t* list, cons
   a.ymap = (decltype(a.ymap))(ymap);
   a.alpha = *(const T*)alpha;
   a.beta = *(const T*)beta;
-  a.flags = knobs().spmv_flags | (A->csr ? SPMV_PRODA : 0);
+  a.flags = knobs().spmv_flags | (A->csr ? SPMV_PRODA : 0) | (which == 5 && (A->t_pack & 1) ? SPMV_TPACK : 0) |
+            (which == 5 && (A->t_pack & 2) ? SPMV_TPACKC : 0);
   a.xcd_chunk = knobs().spmv_xcd_chunk >= 0 ? knobs().spmv_xcd_chunk : A->xcd_auto;
   a.maxlen = which == 0   ? A->maxlen_pat
              : which == 2 ? A->maxlen_side
@@ -2677,6 +2731,20 @@ __global__ __launch_bounds__(256) void k_t_gbase(int64_t ns, int64_t nrows, int 
   }
 }
 
+// Slot of code group g (triple g of a tri slice, entry g otherwise) of lane
+// `lane`, row r, in a triple-SELL slice at code offset d.  Packed codes
+// (spmv_tri_pack bit 1, Float32 tri slices): each full batch of 9 triples
+// (rows_t16_tri's Float32 batch) holds triples 0-3 and 4-7 as one 4R-code
+// pack per lane each and triple 8 as an R pack; a last batch of fewer
+// triples keeps one R pack per triple, as unpacked slices do.
+__device__ __forceinline__ int64_t t_code_slot(int64_t d, int g, int ntri, int lane, int r, int R, bool packed) {
+  const int b = g / 9, i = g % 9;
+  if (!packed || 9 * (b + 1) > ntri) return d + ((int64_t)g * 64 + lane) * R + r;
+  const int64_t bb = d + (int64_t)b * 9 * 64 * R;
+  return i < 8 ? bb + (int64_t)(i / 4) * 4 * 64 * R + (int64_t)lane * 4 * R + (i % 4) * R + r
+               : bb + 8 * 64 * R + (int64_t)lane * R + r;
+}
+
 // one thread per triple-SELL row: its values (and, with codes, its 16-bit
 // codes relative to its oid: tri slices one per triple in code group t,
 // the others one per entry) from the main layout; padding: value 0, code
@@ -2686,7 +2754,7 @@ __global__ void k_t_fill(int64_t nrows, int H, const int32_t* __restrict__ rowma
                          const int64_t* __restrict__ src, const int64_t* __restrict__ toff,
                          const int32_t* __restrict__ tlen, const int32_t* __restrict__ gbase,
                          const int32_t* __restrict__ col, const E* __restrict__ val, int64_t noids, bool codes,
-                         uint16_t* __restrict__ col16, E* __restrict__ tval) {
+                         int pack, uint16_t* __restrict__ col16, E* __restrict__ tval) {
   const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   if (i >= nrows) return;
   const int64_t ts = i / H;
@@ -2702,7 +2770,13 @@ __global__ void k_t_fill(int64_t nrows, int H, const int32_t* __restrict__ rowma
     E v;
     __builtin_memset(&v, 0, sizeof(E));
     if (k < n) v = val[sk];
-    tval[d + ((int64_t)k * 64 + lane) * R + r] = v;
+    if ((pack & 1) && tri) {  // triple t: entries 3t, 3t+1 as one 2R-value pack per lane, entry 3t+2 as an R pack
+      const int64_t tb = d + (int64_t)(k / 3) * 3 * 64 * R;
+      const int j = k % 3;
+      tval[j < 2 ? tb + (int64_t)lane * 2 * R + j * R + r : tb + 2 * 64 * R + (int64_t)lane * R + r] = v;
+    } else {
+      tval[d + ((int64_t)k * 64 + lane) * R + r] = v;
+    }
     if (!codes || (tri && k % 3 != 0)) continue;
     uint16_t q = 0xFFFFu;
     if (k < n) {
@@ -2710,7 +2784,7 @@ __global__ void k_t_fill(int64_t nrows, int H, const int32_t* __restrict__ rowma
       q = c < noids ? (uint16_t)((uint32_t)(c - oid) & 0x7FFFu) : (uint16_t)(0x8000u | (uint32_t)(c - gb));
     }
     const int g = tri ? k / 3 : k;
-    col16[d + ((int64_t)g * 64 + lane) * R + r] = q;
+    col16[t_code_slot(d, g, L / 3, lane, r, R, tri && (pack & 2))] = q;
   }
 }
 
@@ -2720,7 +2794,7 @@ __global__ void k_t_fill(int64_t nrows, int H, const int32_t* __restrict__ rowma
 __global__ void k_t_check(int64_t npos, int64_t nrows, int H, int R, const int32_t* __restrict__ rowmap,
                           const int64_t* __restrict__ toff, const int32_t* __restrict__ tlen,
                           const int32_t* __restrict__ gbase, const uint16_t* __restrict__ col16, int64_t ncols,
-                          unsigned* bad) {
+                          int pack, unsigned* bad) {
   const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   if (i >= npos) return;
   const int64_t ts = i / H;
@@ -2731,7 +2805,7 @@ __global__ void k_t_check(int64_t npos, int64_t nrows, int H, int R, const int32
   const int32_t row = i < nrows ? rowmap[i] : 0;
   unsigned nb = 0;
   for (int g = 0; g < G; ++g) {
-    const int32_t c = d16_col(col16[toff[ts] + ((int64_t)g * 64 + lane) * R + r], row, gbase[ts]);
+    const int32_t c = d16_col(col16[t_code_slot(toff[ts], g, L / 3, lane, r, R, tri && (pack & 2))], row, gbase[ts]);
     if (c < -1 || (c >= 0 && c + (tri ? 2 : 0) >= ncols)) ++nb;
   }
   if (nb) atomicAdd(bad, nb);
@@ -2741,7 +2815,7 @@ void launch_t_check(const pa_mat* A, unsigned* bad, hipStream_t st) {
   const int64_t npos = A->t_nslices * A->H;
   if (npos == 0) return;
   hipLaunchKernelGGL(k_t_check, dim3((unsigned)((npos + 255) / 256)), dim3(256), 0, st, npos, A->t_nrows, A->H, A->R,
-                     A->d_t_rowmap, A->d_t_off, A->d_t_len, A->d_t_gbase, A->d_t_col16, A->ncols_lids, bad);
+                     A->d_t_rowmap, A->d_t_off, A->d_t_len, A->d_t_gbase, A->d_t_col16, A->ncols_lids, A->t_pack, bad);
 }
 
 void launch_t_rowinfo(const pa_mat* A, int64_t n, const int32_t* rows, int64_t noids, int32_t* info, hipStream_t st) {
@@ -2777,7 +2851,7 @@ void launch_t_fill(const pa_mat* A, int64_t noids, bool codes, hipStream_t st) {
 #define PA_TF(E, RR)                                                                                           \
   hipLaunchKernelGGL((k_t_fill<E, RR>), g, b, 0, st, A->t_nrows, A->H, A->d_t_rowmap, A->d_t_rowlen, A->d_t_src, \
                      A->d_t_off, A->d_t_len, A->d_t_gbase, A->d_col, (const E*)A->d_val, noids, codes,          \
-                     A->d_t_col16, (E*)A->d_t_val)
+                     A->t_pack, A->d_t_col16, (E*)A->d_t_val)
   switch (A->dtype) {
     case PA_F32:
       if (A->R == 2) PA_TF(float, 2);
