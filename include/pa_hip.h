@@ -120,10 +120,11 @@ int pa_device_count(int* count);
  *               slices: the Float64 geometry, so delta16 rows take the
  *               triple SELL), 0 (default, auto): 4, rebuilt with 2 when
  *               fewer than 80 % of the slices are pattern slices;
- * "spmv_tri_pack" Float32 triple-SELL tri slices (2 rows per lane; matrices
- *               built afterwards): bit 0 a triple's values as one 16 B and
- *               one 8 B pack per lane, bit 1 a 9-triple batch's codes as
- *               16 + 16 + 4 B packs; 3 (default) both, 0 neither;
+ * "spmv_tri_pack" triple-SELL tri slices of 2 rows per lane (matrices
+ *               built afterwards): bit 0 Float32: a triple's values as one
+ *               16 B and one 8 B pack per lane, bit 1 Float32: a batch's
+ *               codes as 16 + 16 + 4 B packs, bit 2 pair slices (every
+ *               element type, pa_mat_pair_info); 7 (default) all, 0 none;
  * "fault_inject" tests only: threaded issue jobs add an invalid launch. */
 int pa_tune(const char* key, int value, int* previous);
 /* The same knobs for one context: calls led by parts of `c` (their first
@@ -413,6 +414,11 @@ int pa_mat_delta16_info(const pa_mat* A, int64_t* delta16_slices);
  * triple slices (tri_slices, their rows tri_rows).                       */
 int pa_mat_triple_info(const pa_mat* A, int64_t* t_slices, int64_t* t_rows, int64_t* tri_slices,
                        int64_t* tri_rows);
+/* The triple SELL's pair slices (pa_tune "spmv_tri_pack" bit 2, default on;
+ * 2 rows per lane): each lane holds rows a and a + 1 whose columns differ
+ * by one, entry for entry, and reads one code and one x run per triple for
+ * both.  Its pair slices (counted in tri_slices too) and their rows.     */
+int pa_mat_pair_info(const pa_mat* A, int64_t* pair_slices, int64_t* pair_rows);
 
 /* device addresses of the matrix's main arrays, for placement diagnostics:
  * out[0..7] = values, int32 columns, slice offsets, slice lengths (pattern),

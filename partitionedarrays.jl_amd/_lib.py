@@ -95,6 +95,7 @@ _SIGS = {
     "pa_mat_format_info": [_p, _i64p, _i64p, _i64p, _i64p],
     "pa_mat_delta16_info": [_p, _i64p],
     "pa_mat_triple_info": [_p, _i64p, _i64p, _i64p, _i64p],
+    "pa_mat_pair_info": [_p, _i64p, _i64p],
     "pa_mat_long_rows": [_p, _i64p, _i64p],
     "pa_mat_stencil": [_p, C.c_int, C.c_int, _i64p, _i64p, _i64p, C.c_int64, _i32p, C.POINTER(C.c_double), C.c_int, C.POINTER(_p)],
     "pa_spmv_all": [C.c_int, C.POINTER(_p), C.POINTER(_p), C.POINTER(_p), C.POINTER(_p), C.POINTER(_p), C.POINTER(_p), _p, _p],

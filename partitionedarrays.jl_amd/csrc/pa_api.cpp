@@ -91,7 +91,7 @@ const Knobs kDefaults = {
     /*spmv_flags*/ 223, /*long_exact*/ 1, /*halo_pull*/ 1, /*spmv_delta16*/ 1, /*spmv_merge*/ 1,
     /*spmv_merge_max*/ 65536, /*cg_fuse*/ 2, /*halo_direct*/ 1, /*halo_transport*/ 0, /*spmv_group*/ 1,
     /*spmv_format*/ 1, /*pattern_min_pct*/ 0, /*issue_threads*/ 1, /*fault_inject*/ 0, /*spmv_xcd_chunk*/ -1, /*spmv_tri16*/ 1,
-    /*halo_barrier*/ 1, /*tri_order*/ 1, /*side_tail*/ 1, /*f32_rows*/ 0, /*tri_pack*/ 3};
+    /*halo_barrier*/ 1, /*tri_order*/ 1, /*side_tail*/ 1, /*f32_rows*/ 0, /*tri_pack*/ 7};
 // COO → CSC → SELL on the device (pa_coo.hip)
 int coo_compress(int dtype, int index_bytes, int64_t m, int64_t ncols, int64_t n, const void* dI, const void* dJ,
                  const void* dV, int csr, int64_t* nu_out, int32_t** crow, int32_t** ccol, void** cval,
@@ -148,6 +148,7 @@ void launch_stencil_fill(const StencilGeom& g, const int32_t* shell, const doubl
 void launch_probe(int copy, int unroll, int64_t n16, const void* a, void* b, int blocks, hipStream_t st);
 void launch_invalid_config();
 void launch_t_rowinfo(const pa_mat* A, int64_t n, const int32_t* rows, int64_t noids, int32_t* info, hipStream_t st);
+void launch_t_pairinfo(const pa_mat* A, int64_t n, const int32_t* rows, int32_t* pairable, hipStream_t st);
 void launch_t_gbase(const pa_mat* A, int64_t noids, int32_t* ok, hipStream_t st);
 void launch_t_fill(const pa_mat* A, int64_t noids, bool codes, hipStream_t st);
 void launch_t_check(const pa_mat* A, unsigned* bad, hipStream_t st);
@@ -447,6 +448,7 @@ void free_triple_sell(pa_mat* A) {
   A->d_t_src = nullptr;
   A->t_pack = 0;
   A->t_nrows = A->t_nslices = A->t_slots = A->t_tri_slices = A->t_tri_rows = A->t_code_slots = 0;
+  A->t_pair_slices = A->t_pair_rows = 0;
   A->nt_int = A->nt_bnd = 0;
   A->h_t_len.clear();
 }
@@ -484,22 +486,65 @@ int build_triple_sell(pa_mat* A, std::vector<int32_t>& kind, int64_t noids) {
   constexpr int32_t kLen = (1 << 28) - 1, kReg = 1 << 28, kGhost = 1 << 29, kBad = 1 << 30;
   for (int32_t v : info)
     if (v & kBad) return 0;
+  // spmv_tri_pack: 2 rows per lane only; value and code packs Float32 only
+  // (8 B elements with the code packs: C5 F64 +1.5 %, profiles/r06/u/)
+  const int tpack = R == 2 ? (A->dtype == PA_F32 ? knobs().tri_pack : knobs().tri_pack & 4) : 0;
+  // pair slices (spmv_tri_pack bit 2): candidate i and i + 1 (rows a, a + 1,
+  // both regular, one length) pair up when row a + 1's columns are row a's
+  // plus one, entry for entry (k_t_pairinfo); pairs are taken greedily in
+  // oid order
+  std::vector<int64_t> pairs;  // candidate index of each pair's row a
+  std::vector<char> paired(n, 0);
+  if (tpack & 4) {
+    int32_t *d_rows2 = nullptr, *d_pair = nullptr;
+    if (dev_upload(&d_rows2, rows)) return -1;
+    HIPC(hipMalloc((void**)&d_pair, n * 4));
+    launch_t_pairinfo(A, n, d_rows2, d_pair, st);
+    HIPC(hipGetLastError());
+    std::vector<int32_t> pairable(n);
+    HIPC(hipMemcpyAsync(pairable.data(), d_pair, n * 4, hipMemcpyDeviceToHost, st));
+    HIPC(hipStreamSynchronize(st));
+    dev_free(d_rows2);
+    dev_free(d_pair);
+    for (int64_t i = 0; i + 1 < n; ++i)
+      if (pairable[i] && !paired[i] && (info[i] & kReg) && (info[i + 1] & kReg) &&
+          (info[i] & kLen) == (info[i + 1] & kLen)) {
+        pairs.push_back(i);
+        paired[i] = paired[i + 1] = 1;
+      }
+  }
   // order: the other rows, then the regular (triple) rows (spmv_tri_order 1;
-  // 0: regular first); each by length (descending), then oid
-  std::vector<int64_t> ord(n);
-  std::iota(ord.begin(), ord.end(), 0);
+  // 0: regular first); each by length (descending), then oid; then, from a
+  // slice boundary, the pairs by length (descending), then oid (lane p of a
+  // pair slice: row a at position p, row a + 1 at 64 + p; padding
+  // positions: row map -1)
+  std::vector<int64_t> ord;
+  for (int64_t i = 0; i < n; ++i)
+    if (!paired[i]) ord.push_back(i);
   const bool others_first = knobs().tri_order == 1;
   std::stable_sort(ord.begin(), ord.end(), [&](int64_t a, int64_t b) {
     const bool ra = (info[a] & kReg) != 0, rb = (info[b] & kReg) != 0;
     if (ra != rb) return others_first ? rb : ra;
     return (info[a] & kLen) > (info[b] & kLen);
   });
-  const int64_t tns = (n + H - 1) / H;
-  std::vector<int32_t> rowmap(n), rowlen(n), tlen(tns, 0), tint, tbnd;
-  std::vector<int64_t> src(n), toff(tns);
+  std::stable_sort(pairs.begin(), pairs.end(), [&](int64_t a, int64_t b) { return (info[a] & kLen) > (info[b] & kLen); });
+  const int64_t nsingle = (int64_t)ord.size(), npairs = (int64_t)pairs.size();
+  const int64_t pstart = npairs ? (nsingle + H - 1) / H * H : nsingle;  // first position of the pair slices
+  const int64_t npos = npairs ? pstart + (npairs + 63) / 64 * H : nsingle;
+  std::vector<int64_t> at(npos, -1);  // position -> candidate index (-1: padding)
+  for (int64_t i = 0; i < nsingle; ++i) at[i] = ord[i];
+  for (int64_t q = 0; q < npairs; ++q) {
+    const int64_t b = pstart + q / 64 * H + q % 64;
+    at[b] = pairs[q];
+    at[b + 64] = pairs[q] + 1;
+  }
+  const int64_t tns = (npos + H - 1) / H;
+  std::vector<int32_t> rowmap(npos, -1), rowlen(npos, 0), tlen(tns, 0), tint, tbnd;
+  std::vector<int64_t> src(npos, 0), toff(tns), nreal(tns, 0);
   std::vector<char> tri(tns, 1), ghost(tns, 0);
-  for (int64_t i = 0; i < n; ++i) {
-    const int32_t v = info[ord[i]], row = rows[ord[i]];
+  for (int64_t i = 0; i < npos; ++i) {
+    if (at[i] < 0) continue;
+    const int32_t v = info[at[i]], row = rows[at[i]];
     const int64_t ts = i / H, s = row / H;
     const int w = (int)(row - s * H);
     rowmap[i] = row;
@@ -507,6 +552,7 @@ int build_triple_sell(pa_mat* A, std::vector<int32_t>& kind, int64_t noids) {
     // entry 0 of the row in the main layout (as k_delta16 left it, main_slot0)
     src[i] = R == 4 ? soff[s] + (int64_t)(w & 63) * R + (w >> 6) : soff[s] + (int64_t)(w / R) * R + (w % R);
     tlen[ts] = std::max(tlen[ts], rowlen[i]);
+    ++nreal[ts];
     if (!(v & kReg)) tri[ts] = 0;
     if (v & kGhost) ghost[ts] = 1;
   }
@@ -519,9 +565,16 @@ int build_triple_sell(pa_mat* A, std::vector<int32_t>& kind, int64_t noids) {
     toff[ts] = acc;
     acc += (int64_t)tlen[ts] * H;
     A->maxlen_t = std::max(A->maxlen_t, (int)tlen[ts]);
-    if (tri[ts] && tlen[ts] % 3 == 0) {
+    if (ts * H >= pstart && npairs) {  // pair slices (regular rows: length % 3 == 0)
       ++A->t_tri_slices;
-      A->t_tri_rows += std::min<int64_t>(H, n - ts * H);
+      ++A->t_pair_slices;
+      A->t_tri_rows += nreal[ts];
+      A->t_pair_rows += nreal[ts];
+      codes += (int64_t)tlen[ts] / 3 * 64;
+      tlen[ts] |= kTriSlice | kTriPair;
+    } else if (tri[ts] && tlen[ts] % 3 == 0) {
+      ++A->t_tri_slices;
+      A->t_tri_rows += nreal[ts];
       codes += (int64_t)tlen[ts] / 3 * H;
       tlen[ts] |= kTriSlice;
     } else {
@@ -529,9 +582,9 @@ int build_triple_sell(pa_mat* A, std::vector<int32_t>& kind, int64_t noids) {
     }
     (ghost[ts] ? tbnd : tint).push_back((int32_t)ts);
   }
-  A->t_nrows = n;
+  A->t_nrows = npos;
   A->t_nslices = tns;
-  A->t_pack = A->dtype == PA_F32 && R == 2 ? knobs().tri_pack : 0;
+  A->t_pack = tpack;
   A->t_slots = acc;
   A->t_code_slots = codes;
   A->h_t_len = tlen;
@@ -1347,11 +1400,13 @@ const Knob kKnobs[] = {
      "slices, 2 = 8 B packs in 128-row slices (the Float64 geometry; delta16 rows then take the triple "
      "SELL), 0 = auto (default): 4, rebuilt with 2 when fewer than 80 % of the slices are pattern slices "
      "(C5 F32 -7 %, FE27 256^3 F32 +14 % with 2, profiles/r05/af/)"},
-    {"spmv_tri_pack", &Knobs::tri_pack, nullptr, 0, 3, 0,
-     "spmv_tri_pack: Float32 triple-SELL tri slices (2 rows per lane; matrices built afterwards): bit 0 = a "
+    {"spmv_tri_pack", &Knobs::tri_pack, nullptr, 0, 7, 0,
+     "spmv_tri_pack: triple-SELL tri slices of 2 rows per lane (matrices built afterwards): bit 0 = Float32: a "
      "triple's values as one 16 B pack (entries 0 and 1 of both rows) and one 8 B pack (entry 2) per lane "
-     "(two loads instead of three), bit 1 = a batch of 9 triples' codes as two 16 B packs and one 4 B pack "
-     "(three loads instead of nine); 0 = one pack per entry and per triple"},
+     "(two loads instead of three), bit 1 = Float32: a 9-triple batch's codes as 16 + 16 + 4 B packs, bit 2 "
+     "= pair slices (all element types): rows a, a + 1 whose columns differ by one, entry for entry, share "
+     "one lane, one code and one x run per triple (C5 F32 -2.4 %, F64 -1 %, profiles/r06/u/); 7 = all "
+     "(default), 0 = none"},
     {"spmv_side_tail", &Knobs::side_tail, nullptr, 0, 1, 0,
      "spmv_side_tail: per-kind launches without a halo in flight (big single parts): 1 = the side rows (<= 8 "
      "entries) run as the trailing waves of the pattern launch (default: FE27 256^3 -0.4 %, profiles/r05/o/), "
@@ -3037,6 +3092,13 @@ int pa_mat_format_info(const pa_mat* A, int64_t* pattern_slices, int64_t* regula
 int pa_mat_delta16_info(const pa_mat* A, int64_t* delta16_slices) {
   CHECK_ARG(A, "null matrix");
   if (delta16_slices) *delta16_slices = A->nd_int + A->nd_bnd;
+  return 0;
+}
+
+int pa_mat_pair_info(const pa_mat* A, int64_t* pair_slices, int64_t* pair_rows) {
+  CHECK_ARG(A, "null matrix");
+  if (pair_slices) *pair_slices = A->t_pair_slices;
+  if (pair_rows) *pair_rows = A->t_pair_rows;
   return 0;
 }
 

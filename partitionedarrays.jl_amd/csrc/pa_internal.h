@@ -227,6 +227,8 @@ struct CGState {
 // per phase covers up to PA_GROUP_MAX parts (kernel-argument tables).
 constexpr int PA_GROUP_MAX = 8;
 constexpr int32_t kTriSlice = 1 << 30;  // pa_mat::d_t_len: a triple slice
+constexpr int32_t kTriPair = 1 << 29;   // pa_mat::d_t_len: a pair slice (lane l: rows a_l, a_l + 1; build_triple_sell)
+constexpr int32_t kTriLen = kTriPair - 1;  // pa_mat::d_t_len: the entries per row
 struct SpmvPart {
   int64_t nwork;          // slices of this part in the launch
   const int32_t* list;    // slice ids (null: 0..nwork-1)
@@ -356,7 +358,7 @@ struct Knobs {
   int tri_order;         // triple SELL row order: 0 triple rows first, 1 the other rows first (build_triple_sell)
   int side_tail;         // per-kind launches: the side rows as the trailing waves of the pattern launch
   int f32_rows;          // Float32 SELL rows per lane (matrices built afterwards): 4 (16 B packs), 2 (8 B), 0 auto
-  int tri_pack;          // Float32 triple-SELL tri slices: bit 0 per-triple value packs, bit 1 batch code packs
+  int tri_pack;          // triple-SELL tri slices: bit 0 Float32 per-triple value packs, bit 1 batch code packs, bit 2 pairs
 };
 // the knobs of the call running on this thread (outside a call: a snapshot
 // of the process defaults)
@@ -580,11 +582,13 @@ struct pa_mat {
   // SELL); the main delta16 slices are not launched then (host kind 5).
   int64_t t_nrows = 0, t_nslices = 0, t_slots = 0, t_tri_slices = 0, t_tri_rows = 0, t_code_slots = 0;
   int64_t* d_t_off = nullptr;        // slot offset per slice
-  int32_t* d_t_len = nullptr;        // entries per row (max over the slice), bit 30: tri slice (kTriSlice)
+  int32_t* d_t_len = nullptr;        // entries per row (max over the slice), bit 30: tri slice (kTriSlice), bit 29: pair slice
   uint16_t* d_t_col16 = nullptr;     // codes (tri slices: one per triple, slot groups 0..len/3-1)
   void* d_t_val = nullptr;           // values (lane-major packs of R, like the main SELL; t_pack: tri slices per triple)
-  int t_pack = 0;                    // Float32 tri slices (spmv_tri_pack): bit 0 triple t's values as {entries 0,1 × R
-                                     // rows} 16 B + {entry 2} 8 B per lane; bit 1 codes in batch packs (t_code_slot)
+  int t_pack = 0;                    // tri slices of 2 rows per lane (spmv_tri_pack): bit 0 (Float32) triple t's values
+                                     // as {entries 0,1 × R rows} 16 B + {entry 2} 8 B per lane; bit 1 codes in batch
+                                     // packs (t_code_slot); bit 2 pair slices
+  int64_t t_pair_slices = 0, t_pair_rows = 0;  // pair slices and the rows they hold
   int32_t* d_t_gbase = nullptr;      // per slice: smallest ghost column
   int32_t* d_t_desc = nullptr;       // per slice {offset / H, d_t_len, d_t_gbase, 0} (SPMV_DESC)
   int32_t* d_t_rowmap = nullptr;     // structure row → oid

@@ -57,7 +57,7 @@ enum { SPMV_NT = 1, SPMV_DESC = 2 /* pattern / triple-SELL slices: one descripto
        SPMV_SHORT7 = 128 /* Float64 rows <= 7 entries: k_spmv_group_short7 */,
        SPMV_PRODA = 256 /* per matrix: CSR parent, α scales the product */,
        SPMV_TPACK = 512 /* per matrix: Float32 tri slices with per-triple value packs (pa_mat::t_pack bit 0) */,
-       SPMV_TPACKC = 1024 /* per matrix: Float32 tri slices with batch code packs (pa_mat::t_pack bit 1) */ };
+       SPMV_TPACKC = 1024 /* per matrix: tri slices with batch code packs (pa_mat::t_pack bit 1) */ };
 
 typedef unsigned int spmv_u32x4 __attribute__((ext_vector_type(4)));
 // Process-wide knobs (pa_tune).  Defaults from the A/Bs in
@@ -222,10 +222,29 @@ __device__ __forceinline__ void ld_xtrip(const T* p, T (&o)[3]) {
   }
 }
 
+// x[j .. j+3] (a pair slice's triple: row a reads j..j+2, row a+1 j+1..j+3)
+// as one 16 B load for 4 B elements, two for 8 B elements
+template <typename T>
+__device__ __forceinline__ void ld_xquad(const T* p, T (&o)[4]) {
+  if constexpr (sizeof(T) == 4) {
+    const u4a r = *reinterpret_cast<const u4a*>(p);
+    __builtin_memcpy(&o[0], &r, 16);
+  } else if constexpr (sizeof(T) == 8) {
+    const u4a r0 = *reinterpret_cast<const u4a*>(p);
+    const u4a r1 = *reinterpret_cast<const u4a*>(p + 2);
+    __builtin_memcpy(&o[0], &r0, 16);
+    __builtin_memcpy(&o[2], &r1, 16);
+  } else {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) o[j] = p[j];
+  }
+}
+
 template <typename T, bool XV>
 struct XSrc {
   const T* __restrict__ x;
   __device__ __forceinline__ T get(int64_t j) const { return x[j]; }
+  __device__ __forceinline__ void quad(int64_t j, T (&o)[4]) const { ld_xquad<T>(x + j, o); }
   template <int R>
   __device__ __forceinline__ Pack<T, R> run(int64_t j) const { return ld_xrun<T, R>(x + j); }
   __device__ __forceinline__ void trip(int64_t j, T (&o)[3]) const { ld_xtrip<T>(x + j, o); }
@@ -240,6 +259,10 @@ struct XSrc<T, true> {
   __device__ __forceinline__ void trip(int64_t j, T (&o)[3]) const {
 #pragma unroll
     for (int k = 0; k < 3; ++k) o[k] = get(j + k);
+  }
+  __device__ __forceinline__ void quad(int64_t j, T (&o)[4]) const {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) o[k] = get(j + k);
   }
   template <int R>
   __device__ __forceinline__ Pack<T, R> run(int64_t j) const {
@@ -692,6 +715,94 @@ __device__ __forceinline__ void rows_t16_tri(T (&acc)[R], const S16Pack<R>* __re
   }
 }
 
+// Pair slices of the triple SELL (spmv_tri_pack bit 2, build_triple_sell):
+// lane l holds the rows a and a + 1 of one pair, whose columns are those of
+// row a plus one, entry for entry (the x-neighbours of an FE27 part: pattern
+// rows without a pattern).  One code per triple and lane (row a's, Rc = 1,
+// t_code_slot) and one x run x[c .. c+3] serve both rows: row a reads
+// x[c .. c+2], row a+1 x[c+1 .. c+3].  Values as in tri slices (Float32
+// with TP: per-triple packs).  Batches of 9 triples (4 B elements) or 4 (8 B
+// elements); full batches read their codes as 8 B packs of 4.  The terms and
+// their order per row are those of rows_t16_tri.
+// pair_batch: NB triples of a pair slice from triple t (FULL: all exist, the codes of
+// a batch of B = NB in their packs; otherwise clamped to the last triple and
+// never accumulated past it)
+template <typename T, bool ALPHA, typename XS, bool TP, int NB, bool FULL>
+__device__ __forceinline__ void pair_batch(T (&acc)[2], const uint16_t* __restrict__ cs,
+                                           const Pack<T, 2>* __restrict__ vp, int t, int ntri, const XS& x, T alpha,
+                                           bool pf, int32_t rowa, int32_t gb, bool packs) {
+  constexpr int R = 2, NQ = NB / 4;
+  const int lane = threadIdx.x % 64;
+  uint16_t q[NB];
+  if (FULL && packs) {
+    const uint16_t* __restrict__ cb = cs + (int64_t)t * 64;
+#pragma unroll
+    for (int h = 0; h < NQ; ++h) {
+      const S16Pack<4> q4 = ld<true>(reinterpret_cast<const S16Pack<4>*>(cb + h * 4 * 64) + lane);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) q[4 * h + i] = q4.c[i];
+    }
+#pragma unroll
+    for (int u = 4 * NQ; u < NB; ++u) q[u] = ld<true>(reinterpret_cast<const S16Pack<1>*>(cb + u * 64) + lane).c[0];
+  } else {
+#pragma unroll
+    for (int u = 0; u < NB; ++u)
+      q[u] = ld<true>(reinterpret_cast<const S16Pack<1>*>(cs + (int64_t)(FULL ? t + u : min(t + u, ntri - 1)) * 64) +
+                      lane).c[0];
+  }
+  Pack<T, R> v[3 * NB];
+  const Pack<T, R>* __restrict__ vb = vp - lane;  // the slice's values
+#pragma unroll
+  for (int u = 0; u < NB; ++u) {
+    const int tu = FULL ? t + u : min(t + u, ntri - 1);
+    if constexpr (TP) {
+      const Pack<T, R>* tb = vb + (int64_t)tu * 3 * 64;
+      const Pack<T, 2 * R> p01 = ld<true>(reinterpret_cast<const Pack<T, 2 * R>*>(tb) + lane);
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        v[3 * u].v[r] = p01.v[r];
+        v[3 * u + 1].v[r] = p01.v[R + r];
+      }
+      v[3 * u + 2] = ld<true>(tb + 2 * 64 + lane);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 3; ++j) v[3 * u + j] = ld<true>(&vp[(3 * tu + j) * 64]);
+    }
+  }
+  T xq[NB][4];
+  bool ok[NB];
+#pragma unroll
+  for (int u = 0; u < NB; ++u) {
+    const int32_t c = d16_col(q[u], rowa, gb);
+    ok[u] = c >= 0 && (FULL || t + u < ntri);
+    x.quad(c >= 0 ? c : 0, xq[u]);
+  }
+#pragma unroll
+  for (int u = 0; u < NB; ++u)
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      const T t0 = acc[0] + term<ALPHA>(v[3 * u + j].v[0], xq[u][j], alpha, pf);
+      const T t1 = acc[1] + term<ALPHA>(v[3 * u + j].v[1], xq[u][j + 1], alpha, pf);
+      acc[0] = pick(ok[u], t0, acc[0]);
+      acc[1] = pick(ok[u], t1, acc[1]);
+    }
+}
+
+template <typename T, bool ALPHA, typename XS, bool TP>
+__device__ __forceinline__ void rows_t16_pair(T (&acc)[2], const uint16_t* __restrict__ cs,
+                                              const Pack<T, 2>* __restrict__ vp, int len, const XS& x, T alpha,
+                                              bool pf, int32_t rowa, int32_t gb) {
+  constexpr int B = sizeof(T) == 4 ? 9 : kTriBatch;
+  const int ntri = len / 3;
+  int t = 0;
+  for (; t + B <= ntri; t += B) pair_batch<T, ALPHA, XS, TP, B, true>(acc, cs, vp, t, ntri, x, alpha, pf, rowa, gb, true);
+  if constexpr (sizeof(T) == 4) {  // the rest as one clamped batch (Float32's 9-triple batches, rows_t16_tri)
+    if (t < ntri) pair_batch<T, ALPHA, XS, TP, B, false>(acc, cs, vp, t, ntri, x, alpha, pf, rowa, gb, false);
+  } else {  // then single triples (8 B elements, as rows_t16_tri)
+    for (; t < ntri; ++t) pair_batch<T, ALPHA, XS, TP, 1, true>(acc, cs, vp, t, ntri, x, alpha, pf, rowa, gb, false);
+  }
+}
+
 // pattern rows: column of row `rbase + r` at entry k is rbase + r + pat[k].
 // XP: the lane's R rows read R consecutive x values per entry, fetched as
 // one 16 B run (rows that are not regular get values they never use).
@@ -978,7 +1089,7 @@ __device__ __forceinline__ void spmv_wave(const SpmvArgs<T>& a, const int64_t w)
     lraw = a.slen[s];
   }
   // pattern slices: len | tri << 8 | pattern id << 9 (dedup_patterns); triple SELL: len | kTriSlice
-  const int len = PAT ? (lraw & 0xff) : (PK == 4 ? (lraw & (kTriSlice - 1)) : lraw);
+  const int len = PAT ? (lraw & 0xff) : (PK == 4 ? (lraw & kTriLen) : lraw);
   bool ok[R];
   if (PAT) {
     const uint64_t m = a.desc ? dmask : a.mask[s * (H / 64) + (lane * R) / 64];
@@ -998,6 +1109,12 @@ __device__ __forceinline__ void spmv_wave(const SpmvArgs<T>& a, const int64_t w)
   for (int r = 0; r < R; ++r) {
     const int64_t i = row0 + (int64_t)r * rs;
     orow[r] = ok[r] ? (a.rowmap ? (int64_t)a.rowmap[i] : i) : 0;
+    if constexpr (PK == 4) {  // padding positions of the triple SELL (row map -1: before a pair group)
+      if (orow[r] < 0) {
+        ok[r] = false;
+        orow[r] = 0;
+      }
+    }
   }
 
   T acc[R];
@@ -1051,17 +1168,29 @@ __device__ __forceinline__ void spmv_wave(const SpmvArgs<T>& a, const int64_t w)
     for (int r = 0; r < R; ++r) rw[r] = (int32_t)orow[r];
     if (lraw & kTriSlice) {
       bool packed = false;
-      if constexpr (sizeof(T) == 4 && R == 2) {
-        // per-triple value packs and/or batch code packs (k_t_fill, pa_mat::t_pack), non-temporal
-        if ((a.flags & (SPMV_TPACK | SPMV_TPACKC)) == (SPMV_TPACK | SPMV_TPACKC)) {
-          rows_t16_tri<T, R, ALPHA, true, XSrc<T, XV>, true, true>(acc, cp, vp, len, xs, a.alpha, pf, rw, gb);
-          packed = true;
-        } else if (a.flags & SPMV_TPACK) {
-          rows_t16_tri<T, R, ALPHA, true, XSrc<T, XV>, true, false>(acc, cp, vp, len, xs, a.alpha, pf, rw, gb);
-          packed = true;
-        } else if (a.flags & SPMV_TPACKC) {
-          rows_t16_tri<T, R, ALPHA, true, XSrc<T, XV>, false, true>(acc, cp, vp, len, xs, a.alpha, pf, rw, gb);
-          packed = true;
+      if constexpr (R == 2) {
+        // pair slices, per-triple value packs (Float32) and/or batch code
+        // packs (k_t_fill, pa_mat::t_pack), non-temporal
+        using XS = XSrc<T, XV>;
+        const bool tp = sizeof(T) == 4 && (a.flags & SPMV_TPACK);
+        packed = true;
+        if (lraw & kTriPair) {
+          const uint16_t* cs = (const uint16_t*)a.col16 + off;
+          if constexpr (sizeof(T) == 4) {
+            if (tp) rows_t16_pair<T, ALPHA, XS, true>(acc, cs, vp, len, xs, a.alpha, pf, rw[0], gb);
+            else rows_t16_pair<T, ALPHA, XS, false>(acc, cs, vp, len, xs, a.alpha, pf, rw[0], gb);
+          } else {
+            rows_t16_pair<T, ALPHA, XS, false>(acc, cs, vp, len, xs, a.alpha, pf, rw[0], gb);
+          }
+        } else if (sizeof(T) == 4 && (a.flags & SPMV_TPACKC)) {  // (value and code packs: Float32 only)
+          if constexpr (sizeof(T) == 4) {
+            if (tp) rows_t16_tri<T, R, ALPHA, true, XS, true, true>(acc, cp, vp, len, xs, a.alpha, pf, rw, gb);
+            else rows_t16_tri<T, R, ALPHA, true, XS, false, true>(acc, cp, vp, len, xs, a.alpha, pf, rw, gb);
+          }
+        } else if (tp) {
+          if constexpr (sizeof(T) == 4) rows_t16_tri<T, R, ALPHA, true, XS, true, false>(acc, cp, vp, len, xs, a.alpha, pf, rw, gb);
+        } else {
+          packed = false;
         }
       }
       if (packed) {
@@ -2703,6 +2832,47 @@ __global__ void k_t_rowinfo(int64_t n, const int32_t* __restrict__ rows, int H, 
   info[i] = len | (reg ? 1 << 28 : 0) | (ghost ? 1 << 29 : 0) | (bad ? 1 << 30 : 0);
 }
 
+// per candidate row i (oids of the delta16 slices, ascending): 1 when the
+// next candidate is row + 1 and its columns are row i's plus one, entry for
+// entry (a pair of the triple SELL's pair slices), else 0
+template <int R>
+__global__ void k_t_pairinfo(int64_t n, const int32_t* __restrict__ rows, int H, const int64_t* __restrict__ soff,
+                             const int32_t* __restrict__ slen, const int32_t* __restrict__ col,
+                             int32_t* __restrict__ pairable) {
+  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  int32_t ok = 0;
+  if (i + 1 < n && rows[i + 1] == rows[i] + 1) {
+    const int64_t ra = rows[i], rb = ra + 1, sa = ra / H, sb = rb / H;
+    const int64_t ba = main_slot0<R>(soff[sa], (int)(ra - sa * H)), bb = main_slot0<R>(soff[sb], (int)(rb - sb * H));
+    const int La = slen[sa], Lb = slen[sb];
+    ok = 1;
+    for (int k = 0; k < max(La, Lb); ++k) {
+      const int32_t ca = k < La ? col[ba + (int64_t)k * 64 * R] : -1;
+      const int32_t cb = k < Lb ? col[bb + (int64_t)k * 64 * R] : -1;
+      if (ca < 0 && cb < 0) break;
+      if (ca < 0 || cb != ca + 1) {
+        ok = 0;
+        break;
+      }
+    }
+  }
+  pairable[i] = ok;
+}
+
+void launch_t_pairinfo(const pa_mat* A, int64_t n, const int32_t* rows, int32_t* pairable, hipStream_t st) {
+  if (n == 0) return;
+  const dim3 g((unsigned)((n + 255) / 256)), b(256);
+#define PA_TPI(RR) hipLaunchKernelGGL(k_t_pairinfo<RR>, g, b, 0, st, n, rows, A->H, A->d_slice_off, A->d_slice_len, \
+                                      A->d_col, pairable)
+  switch (A->R) {
+    case 1: PA_TPI(1); break;
+    case 2: PA_TPI(2); break;
+    case 4: PA_TPI(4); break;
+  }
+#undef PA_TPI
+}
+
 // one wave per triple-SELL slice: the smallest ghost column of its rows
 // (the ghost codes' base) and whether every ghost code fits 15 bits
 template <int R>
@@ -2737,12 +2907,16 @@ __global__ __launch_bounds__(256) void k_t_gbase(int64_t ns, int64_t nrows, int 
 // (rows_t16_tri's Float32 batch) holds triples 0-3 and 4-7 as one 4R-code
 // pack per lane each and triple 8 as an R pack; a last batch of fewer
 // triples keeps one R pack per triple, as unpacked slices do.
-__device__ __forceinline__ int64_t t_code_slot(int64_t d, int g, int ntri, int lane, int r, int R, bool packed) {
-  const int b = g / 9, i = g % 9;
-  if (!packed || 9 * (b + 1) > ntri) return d + ((int64_t)g * 64 + lane) * R + r;
-  const int64_t bb = d + (int64_t)b * 9 * 64 * R;
-  return i < 8 ? bb + (int64_t)(i / 4) * 4 * 64 * R + (int64_t)lane * 4 * R + (i % 4) * R + r
-               : bb + 8 * 64 * R + (int64_t)lane * R + r;
+// Generally: R codes per lane and triple (1 in pair slices), batches of B
+// triples (9 for 4 B elements, 4 for 8 B: rows_t16_tri / rows_t16_pair);
+// a full batch holds packs of 4 triples, then single triples.
+__device__ __forceinline__ int64_t t_code_slot(int64_t d, int g, int ntri, int lane, int r, int R, bool packed,
+                                               int B) {
+  const int b = g / B, i = g % B, nq = 4 * (B / 4);
+  if (!packed || B * (b + 1) > ntri) return d + ((int64_t)g * 64 + lane) * R + r;
+  const int64_t bb = d + (int64_t)b * B * 64 * R;
+  return i < nq ? bb + (int64_t)(i / 4) * 4 * 64 * R + (int64_t)lane * 4 * R + (i % 4) * R + r
+                : bb + (int64_t)i * 64 * R + (int64_t)lane * R + r;
 }
 
 // one thread per triple-SELL row: its values (and, with codes, its 16-bit
@@ -2759,9 +2933,11 @@ __global__ void k_t_fill(int64_t nrows, int H, const int32_t* __restrict__ rowma
   if (i >= nrows) return;
   const int64_t ts = i / H;
   const int w = (int)(i - ts * H), lane = w & 63, r = w >> 6;
+  if (rowmap[i] < 0) return;  // a padding position (memset: values 0, codes 0xFFFF)
   const int32_t lraw = tlen[ts];
-  const int L = lraw & (kTriSlice - 1);
-  const bool tri = (lraw & kTriSlice) != 0;
+  const int L = lraw & kTriLen;
+  const bool tri = (lraw & kTriSlice) != 0, pair = (lraw & kTriPair) != 0;
+  constexpr int B = sizeof(E) == 4 ? 9 : 4;  // rows_t16_tri's batches
   const int n = rowlen[i];
   const int64_t b = src[i], d = toff[ts];
   const int32_t oid = rowmap[i], gb = gbase[ts];
@@ -2770,21 +2946,22 @@ __global__ void k_t_fill(int64_t nrows, int H, const int32_t* __restrict__ rowma
     E v;
     __builtin_memset(&v, 0, sizeof(E));
     if (k < n) v = val[sk];
-    if ((pack & 1) && tri) {  // triple t: entries 3t, 3t+1 as one 2R-value pack per lane, entry 3t+2 as an R pack
+    if ((pack & 1) && tri && sizeof(E) == 4) {  // triple t: entries 3t, 3t+1 as one 2R-value pack per lane, entry 3t+2 as an R pack
       const int64_t tb = d + (int64_t)(k / 3) * 3 * 64 * R;
       const int j = k % 3;
       tval[j < 2 ? tb + (int64_t)lane * 2 * R + j * R + r : tb + 2 * 64 * R + (int64_t)lane * R + r] = v;
     } else {
       tval[d + ((int64_t)k * 64 + lane) * R + r] = v;
     }
-    if (!codes || (tri && k % 3 != 0)) continue;
+    if (!codes || (tri && k % 3 != 0) || (pair && r != 0)) continue;  // pair slices: row a's codes
     uint16_t q = 0xFFFFu;
     if (k < n) {
       const int32_t c = col[sk];
       q = c < noids ? (uint16_t)((uint32_t)(c - oid) & 0x7FFFu) : (uint16_t)(0x8000u | (uint32_t)(c - gb));
     }
     const int g = tri ? k / 3 : k;
-    col16[t_code_slot(d, g, L / 3, lane, r, R, tri && (pack & 2))] = q;
+    col16[pair ? t_code_slot(d, g, L / 3, lane, 0, 1, true, B)
+               : t_code_slot(d, g, L / 3, lane, r, R, tri && (pack & 2), B)] = q;
   }
 }
 
@@ -2794,19 +2971,22 @@ __global__ void k_t_fill(int64_t nrows, int H, const int32_t* __restrict__ rowma
 __global__ void k_t_check(int64_t npos, int64_t nrows, int H, int R, const int32_t* __restrict__ rowmap,
                           const int64_t* __restrict__ toff, const int32_t* __restrict__ tlen,
                           const int32_t* __restrict__ gbase, const uint16_t* __restrict__ col16, int64_t ncols,
-                          int pack, unsigned* bad) {
+                          int pack, int B, unsigned* bad) {
   const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   if (i >= npos) return;
   const int64_t ts = i / H;
   const int w = (int)(i - ts * H), lane = w & 63, r = w >> 6;
   const int32_t lraw = tlen[ts];
-  const bool tri = (lraw & kTriSlice) != 0;
-  const int L = lraw & (kTriSlice - 1), G = tri ? L / 3 : L;
+  const bool tri = (lraw & kTriSlice) != 0, pair = (lraw & kTriPair) != 0;
+  const int L = lraw & kTriLen, G = tri ? L / 3 : L;
   const int32_t row = i < nrows ? rowmap[i] : 0;
+  if (pair && r != 0) return;  // pair slices: row a's codes serve both rows
   unsigned nb = 0;
   for (int g = 0; g < G; ++g) {
-    const int32_t c = d16_col(col16[t_code_slot(toff[ts], g, L / 3, lane, r, R, tri && (pack & 2))], row, gbase[ts]);
-    if (c < -1 || (c >= 0 && c + (tri ? 2 : 0) >= ncols)) ++nb;
+    const int64_t at = pair ? t_code_slot(toff[ts], g, L / 3, lane, 0, 1, true, B)
+                            : t_code_slot(toff[ts], g, L / 3, lane, r, R, tri && (pack & 2), B);
+    const int32_t c = d16_col(col16[at], row, gbase[ts]);
+    if (c < -1 || (c >= 0 && c + (pair ? 3 : tri ? 2 : 0) >= ncols)) ++nb;
   }
   if (nb) atomicAdd(bad, nb);
 }
@@ -2815,7 +2995,8 @@ void launch_t_check(const pa_mat* A, unsigned* bad, hipStream_t st) {
   const int64_t npos = A->t_nslices * A->H;
   if (npos == 0) return;
   hipLaunchKernelGGL(k_t_check, dim3((unsigned)((npos + 255) / 256)), dim3(256), 0, st, npos, A->t_nrows, A->H, A->R,
-                     A->d_t_rowmap, A->d_t_off, A->d_t_len, A->d_t_gbase, A->d_t_col16, A->ncols_lids, A->t_pack, bad);
+                     A->d_t_rowmap, A->d_t_off, A->d_t_len, A->d_t_gbase, A->d_t_col16, A->ncols_lids, A->t_pack,
+                     dtype_size(A->dtype) == 4 ? 9 : 4, bad);
 }
 
 void launch_t_rowinfo(const pa_mat* A, int64_t n, const int32_t* rows, int64_t noids, int32_t* info, hipStream_t st) {

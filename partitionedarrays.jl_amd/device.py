@@ -526,6 +526,9 @@ class DeviceMatrix:
         t = [C.c_int64() for _ in range(4)]
         _lib.call("pa_mat_triple_info", self.h, *[C.byref(x) for x in t])
         d.update(zip(["triple_sell_slices", "triple_sell_rows", "tri_slices", "tri_rows"], [x.value for x in t]))
+        pr = [C.c_int64() for _ in range(2)]
+        _lib.call("pa_mat_pair_info", self.h, *[C.byref(x) for x in pr])
+        d.update(zip(["pair_slices", "pair_rows"], [x.value for x in pr]))
         lr = [C.c_int64() for _ in range(2)]
         _lib.call("pa_mat_long_rows", self.h, *[C.byref(x) for x in lr])
         d.update(zip(["long_rows", "long_nnz"], [x.value for x in lr]))

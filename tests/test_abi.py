@@ -82,7 +82,7 @@ def test_tune_knobs_round_trip_and_reject_bad_values(pamd):
         pamd._lib.tune("spmv_flags", prev)
     for k, bad in (("spmv_merge", 2), ("spmv_merge_max", -1), ("cg_fuse", 3), ("pattern_min_regular", -1),
                    ("pattern_min_regular", 101), ("f32_rows", 1), ("f32_rows", 3), ("f32_rows", 8),
-                   ("spmv_tri_pack", 4)):
+                   ("spmv_tri_pack", 8)):
         try:
             pamd._lib.tune(k, bad)
             raise AssertionError(f"{k} accepted {bad}")

@@ -369,43 +369,51 @@ def test_float32_rows_per_lane_equal_oracle(be, pamd, O, rows, tri16):
             pamd._lib.tune(k, v)
 
 
-@pytest.mark.parametrize("pack", [3, 1, 2, 0])
-def test_float32_triple_value_packs_equal_oracle(be, pamd, O, pack):
+@pytest.mark.parametrize("dtype,pack", [(np.float32, 7), (np.float32, 3), (np.float32, 1), (np.float32, 2),
+                                        (np.float32, 4), (np.float32, 0), (np.float64, 7), (np.float64, 2),
+                                        (np.float64, 4), (np.float64, 0), (np.complex64, 7), (np.complex64, 0)])
+def test_triple_sell_packs_and_pairs_equal_oracle(be, pamd, O, dtype, pack):
     """pa_tune("spmv_tri_pack"): the Float32 triple SELL's tri slices (2 rows
     per lane) hold a triple's values as one 16 B pack (entries 0 and 1 of
     both rows) and one 8 B pack (entry 2) per lane, or one 8 B pack per
     entry (bit 0), and a batch of 9 triples' codes as 16 + 16 + 4 B packs
-    or one 4 B pack per triple (bit 1).  The layout never changes the terms or their order per row
+    or one 4 B pack per triple (bit 1; 8 B elements: one 16 B pack per 4
+    triples), and pair slices (bit 2: rows a, a + 1 whose columns differ by
+    one share a lane, one code and one x run per triple; Float32, Float64,
+    ComplexF32).  The layout never changes the terms or their order per row
     (SparseUtils.jl:176-185): mul! with alpha != 1 and beta != 0, and mul!
     after set_values (the copies refreshed into the packed layout), give the
     oracle's bits."""
-    N, nparts, dtype = BIG[0], 8, np.float32
+    N, nparts = BIG[0], 8
     prev = {k: pamd._lib.tune(k, v) for k, v in {"f32_rows": 2, "spmv_tri16": 1, "spmv_tri_pack": pack}.items()}
     try:
         parts = be.get_part_ids(nparts)
         A = pamd.drivers.irregular_problem(parts, N, 27, dtype)
-        assert sum(A.values.local(p).info()["tri_rows"] for p in parts.part_ids) > 0
+        info = [A.values.local(p).info() for p in parts.part_ids]
+        assert sum(i["tri_rows"] for i in info) > 0
+        # pairs hold most triple rows of these parts (x-neighbours inside a part)
+        assert (sum(i["pair_rows"] for i in info) * 2 > sum(i["tri_rows"] for i in info)) == bool(pack & 4)
         OA = _oracle(O, N, nparts, dtype)
         rng = np.random.default_rng(SEED + 41 + pack)
         xs = {p: _rand(rng, A.cols.partition.local(p).num_lids, dtype) for p in parts.part_ids}
         ys = {p: _rand(rng, A.rows.partition.local(p).num_lids, dtype) for p in parts.part_ids}
         x = pamd.PVector.from_host(pamd.map_parts(lambda s: xs[s.part], A.cols.partition), A.cols)
         y = pamd.PVector.from_host(pamd.map_parts(lambda s: ys[s.part], A.rows.partition), A.rows)
-        a, b = np.float32(0.5), np.float32(-1.25)
+        a, b = (np.float32(0.5), np.float32(-1.25)) if np.dtype(dtype) in (np.float32, np.complex64) else (0.5, -1.25)
         pamd.mul_(y, A, x, a, b)
         ox = O.PVector(O.map_parts(lambda s: _ox(O, xs[s.part]), OA.cols.partition), OA.cols)
-        oy = O.PVector(O.map_parts(lambda s: ys[s.part].copy(), OA.rows.partition), OA.rows)
+        oy = O.PVector(O.map_parts(lambda s: _ox(O, ys[s.part]), OA.rows.partition), OA.rows)
         O.mul_(oy, OA, ox, a, b)
         got = y.to_host()
         for p in parts.part_ids:
             assert _eq(O, got.local(p), oy.values[p]), f"part {p}: SpMV (alpha, beta) differs"
         new = []
         for i, p in enumerate(parts.part_ids):
-            v2 = rng.uniform(-1, 1, len(OA.values.parts[i].nzval)).astype(dtype)
+            v2 = _rand(rng, len(A.values.local(p).get_values()), dtype)
             A.values.local(p).set_values(v2)
             new.append(v2)
         it = iter(new)
-        OA = O.PSparseMatrix(O.map_parts(lambda M: O.CSC(M.m, M.n, M.colptr, M.rowval, next(it).copy()),
+        OA = O.PSparseMatrix(O.map_parts(lambda M: O.CSC(M.m, M.n, M.colptr, M.rowval, _ox(O, next(it))),
                                          OA.values), OA.rows, OA.cols)
         y = pamd.PVector.undef(A.rows, dtype)
         pamd.mul_(y, A, x)
