@@ -91,7 +91,7 @@ const Knobs kDefaults = {
     /*spmv_flags*/ 223, /*long_exact*/ 1, /*halo_pull*/ 1, /*spmv_delta16*/ 1, /*spmv_merge*/ 1,
     /*spmv_merge_max*/ 65536, /*cg_fuse*/ 2, /*halo_direct*/ 1, /*halo_transport*/ 0, /*spmv_group*/ 1,
     /*spmv_format*/ 1, /*pattern_min_pct*/ 0, /*issue_threads*/ 1, /*fault_inject*/ 0, /*spmv_xcd_chunk*/ -1, /*spmv_tri16*/ 1,
-    /*halo_barrier*/ 1, /*tri_order*/ 1, /*side_tail*/ 1, /*f32_rows*/ 0, /*tri_pack*/ 7};
+    /*halo_barrier*/ 1, /*tri_order*/ 1, /*side_tail*/ 1, /*f32_rows*/ 0, /*tri_pack*/ 7, /*uniform*/ 1};
 // COO → CSC → SELL on the device (pa_coo.hip)
 int coo_compress(int dtype, int index_bytes, int64_t m, int64_t ncols, int64_t n, const void* dI, const void* dJ,
                  const void* dV, int csr, int64_t* nu_out, int32_t** crow, int32_t** ccol, void** cval,
@@ -149,6 +149,7 @@ void launch_probe(int copy, int unroll, int64_t n16, const void* a, void* b, int
 void launch_invalid_config();
 void launch_t_rowinfo(const pa_mat* A, int64_t n, const int32_t* rows, int64_t noids, int32_t* info, hipStream_t st);
 void launch_t_pairinfo(const pa_mat* A, int64_t n, const int32_t* rows, int32_t* pairable, hipStream_t st);
+void launch_u_fill(const pa_mat* A, hipStream_t st);
 void launch_t_gbase(const pa_mat* A, int64_t noids, int32_t* ok, hipStream_t st);
 void launch_t_fill(const pa_mat* A, int64_t noids, bool codes, hipStream_t st);
 void launch_t_check(const pa_mat* A, unsigned* bad, hipStream_t st);
@@ -337,6 +338,62 @@ int finish_sell_layout(pa_mat* A, const std::vector<int32_t>& slen, const std::v
 // one cold row per slice, and the slice metadata shrinks by kmax*4 B each.
 // A/B (one row per slice vs the table, profiles/r04/g/ab_pattern_dedup.jsonl):
 // FE27 256³ 0.6539 -> 0.6407 ms, FD7 128³ 0.02865 -> 0.02833 ms.
+// The uniform layout of short pattern rows (pa_tune "spmv_uniform", Float64
+// with 2 rows per lane and patterns of at most 7 entries: FD7, C2): the
+// union U of the distinct patterns' offsets (K <= 7 entries, ascending;
+// every pattern is a subsequence of it), and the pattern slices' values
+// again at slice s * H * K, entry k of the slice's pattern at U's position
+// e(k) (the others 0, never multiplied).  A wave of the short-row tail
+// launch then knows its values' and x runs' addresses from its slice index
+// and U alone and issues them before its descriptor arrives; the
+// descriptor's word 2 (emask: which of U's entries the slice's pattern
+// holds) and mask only select the terms (rows_pattern_u).
+void free_uniform(pa_mat* A) {
+  dev_free(A->d_uval);
+  dev_free(A->d_uemap);
+  A->d_uval = nullptr;
+  A->d_uemap = nullptr;
+  A->uK = 0;
+}
+
+int build_uniform(pa_mat* A, const std::vector<int32_t>& kind, const std::vector<int32_t>& table,
+                  const std::vector<int32_t>& packed, std::vector<int32_t>& desc) {
+  free_uniform(A);
+  if (!knobs().spmv_uniform || A->dtype != PA_F64 || A->R != 2 || A->npatterns == 0) return 0;
+  const int64_t ns = A->nslices, K0 = A->kmax, np = A->npatterns;
+  std::vector<int32_t> plen(np, 0);
+  for (int64_t s = 0; s < ns; ++s)
+    if (kind[s] == 1) plen[packed[s] >> 9] = packed[s] & 0xff;
+  std::vector<int32_t> U;
+  for (int64_t p = 0; p < np; ++p)
+    for (int32_t k = 0; k < plen[p]; ++k) U.push_back(table[p * K0 + k]);
+  std::sort(U.begin(), U.end());
+  U.erase(std::unique(U.begin(), U.end()), U.end());
+  if (U.size() > 7 || U.empty()) return 0;
+  const int K = (int)U.size();
+  std::vector<int32_t> emap(np * 8, 0), emask(np, 0);
+  for (int64_t p = 0; p < np; ++p)
+    for (int32_t k = 0; k < plen[p]; ++k) {
+      const int e = (int)(std::lower_bound(U.begin(), U.end(), table[p * K0 + k]) - U.begin());
+      CHECK_ARG(k == 0 || e > emap[p * 8 + k - 1], "uniform layout: a pattern out of column order (internal error)");
+      emap[p * 8 + k] = e;
+      emask[p] |= 1 << e;
+    }
+  const int DW = desc_words(A->R);
+  for (int64_t s = 0; s < ns; ++s)
+    if (kind[s] == 1) desc[DW * s + 2] = emask[packed[s] >> 9];
+  hipStream_t st = A->ctx->s_main;
+  const size_t S = dtype_size(A->dtype);
+  if (dev_upload(&A->d_uemap, emap)) return -1;
+  HIPC(hipMalloc(&A->d_uval, (size_t)ns * A->H * K * S));
+  HIPC(hipMemsetAsync(A->d_uval, 0, (size_t)ns * A->H * K * S, st));
+  A->uK = K;
+  for (int e = 0; e < 8; ++e) A->upat[e] = e < K ? U[e] : 0;
+  launch_u_fill(A, st);
+  HIPC(hipGetLastError());
+  return 0;
+}
+
 int dedup_patterns(pa_mat* A, const std::vector<int32_t>& kind) {
   const int64_t ns = A->nslices, K = A->kmax;
   hipStream_t st = A->ctx->s_main;
@@ -400,6 +457,7 @@ int dedup_patterns(pa_mat* A, const std::vector<int32_t>& kind) {
       desc[DW * s + 1] = packed[s];
       std::memcpy(&desc[DW * s + 4], &mask[s * W], W * 8);
     }
+    if (build_uniform(A, kind, table, packed, desc)) return -1;
     dev_free(A->d_pdesc);
     A->d_pdesc = nullptr;
     if (dev_upload(&A->d_pdesc, desc)) return -1;
@@ -1407,6 +1465,10 @@ const Knob kKnobs[] = {
      "= pair slices (all element types): rows a, a + 1 whose columns differ by one, entry for entry, share "
      "one lane, one code and one x run per triple (C5 F32 -2.4 %, F64 -1 %, profiles/r06/u/); 7 = all "
      "(default), 0 = none"},
+    {"spmv_uniform", &Knobs::spmv_uniform, nullptr, 0, 1, 0,
+     "spmv_uniform: Float64 pattern slices whose patterns (<= 7 entries) fit one union U (FD7; matrices built "
+     "afterwards): 1 = a copy of their values at slice * H * |U| in U's entry order, so the short-row tail "
+     "launch issues its value and x loads before the slice descriptor arrives (default), 0 = off"},
     {"spmv_side_tail", &Knobs::side_tail, nullptr, 0, 1, 0,
      "spmv_side_tail: per-kind launches without a halo in flight (big single parts): 1 = the side rows (<= 8 "
      "entries) run as the trailing waves of the pattern launch (default: FE27 256^3 -0.4 %, profiles/r05/o/), "
@@ -2952,6 +3014,10 @@ static int refresh_side(pa_mat* A, hipStream_t st) {
     launch_t_fill(A, 0, false, st);
     HIPC(hipGetLastError());
   }
+  if (A->d_uval) {  // and the uniform layout's (build_uniform)
+    launch_u_fill(A, st);
+    HIPC(hipGetLastError());
+  }
   return 0;
 }
 
@@ -3075,6 +3141,7 @@ int pa_mat_destroy(pa_mat* A) {
                   (void*)A->d_col16, (void*)A->d_gbase, (void*)A->d_dint_list, (void*)A->d_dbnd_list})
     dev_free(p);
   free_triple_sell(A);
+  free_uniform(A);
   delete A;
   return 0;
 }
@@ -3139,7 +3206,8 @@ int pa_mat_traffic(const pa_mat* A, int64_t* value_bytes, int64_t* index_bytes, 
   for (int64_t s = 0; s < A->nslices; ++s) {
     const int kd = pat ? A->h_kind[s] : 0;
     if (kd == 1) {
-      v += (int64_t)A->h_plen[s] * H * S;
+      // (the uniform layout: the short-row tail launch reads K entries)
+      v += (int64_t)(A->d_uval ? A->uK : A->h_plen[s]) * H * S;
       // mask, offset, length | pattern id, list entry; with SPMV_DESC the
       // descriptor instead (desc_words): counted as the larger
       m += std::max<int64_t>(W * 8 + 8 + 4, 4 * desc_words(A->R)) + 4;

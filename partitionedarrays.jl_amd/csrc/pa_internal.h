@@ -359,6 +359,7 @@ struct Knobs {
   int side_tail;         // per-kind launches: the side rows as the trailing waves of the pattern launch
   int f32_rows;          // Float32 SELL rows per lane (matrices built afterwards): 4 (16 B packs), 2 (8 B), 0 auto
   int tri_pack;          // triple-SELL tri slices: bit 0 Float32 per-triple value packs, bit 1 batch code packs, bit 2 pairs
+  int spmv_uniform;      // Float64 short pattern rows: the uniform layout (build_uniform)
 };
 // the knobs of the call running on this thread (outside a call: a snapshot
 // of the process defaults)
@@ -589,6 +590,12 @@ struct pa_mat {
                                      // as {entries 0,1 × R rows} 16 B + {entry 2} 8 B per lane; bit 1 codes in batch
                                      // packs (t_code_slot); bit 2 pair slices
   int64_t t_pair_slices = 0, t_pair_rows = 0;  // pair slices and the rows they hold
+  // the uniform layout of short pattern rows (build_uniform): K = |U| <= 7
+  // entries per row at slice * H * K, U's offsets, pattern id -> U position
+  void* d_uval = nullptr;
+  int32_t* d_uemap = nullptr;
+  int uK = 0;
+  int32_t upat[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   int32_t* d_t_gbase = nullptr;      // per slice: smallest ghost column
   int32_t* d_t_desc = nullptr;       // per slice {offset / H, d_t_len, d_t_gbase, 0} (SPMV_DESC)
   int32_t* d_t_rowmap = nullptr;     // structure row → oid

@@ -153,6 +153,12 @@ struct SpmvArgs {
   // triple-SELL slices (SPMV_DESC): 4 int32 {offset / H, length word,
   // ghost base, 0} per slice, one scalar load (build_triple_sell)
   const PA_GLB int32_t* desc;
+  // the uniform layout of short pattern rows (build_uniform; pattern
+  // launches of Float64 matrices with it): values at slice * H * uK in the
+  // order of the offsets upat[0 .. uK-1]
+  const PA_GLB T* uval;
+  int uK;
+  int32_t upat[8];
 };
 
 template <typename T> struct DAcc { using type = double; };
@@ -1275,6 +1281,91 @@ __global__ __launch_bounds__(256) void k_spmv_sell(SpmvArgs<T> a) {
   spmv_wave<T, R, ALPHA, BMODE, U, PK, SH, XV>(a, w);
 }
 
+// One wave of the short-row tail launch over the uniform layout
+// (build_uniform): the slice's values at s * H * K and its x runs at
+// rbase + upat[e] (clamped into x: entries and rows the slice does not hold
+// read some x and are never accumulated) are issued from the slice index
+// and the kernel arguments alone; the descriptor (scalar load) supplies
+// only the row mask and emask, which select the terms.  A lane's R rows are
+// blocked, as in rows_pattern with 16 B x runs; the terms of a row and
+// their order are rows_pattern's (U's order restricted to the slice's
+// pattern = the pattern's own order).
+template <typename T, int R, bool ALPHA, int BMODE, int U>
+__device__ __forceinline__ void spmv_wave_u(const SpmvArgs<T>& a, const int64_t w) {
+  constexpr int H = 64 * R, DW = kDescWords<R>;
+  const int lane = threadIdx.x & 63;
+  const int64_t s = a.list ? (int64_t)a.list[w] : w;
+  const int64_t row0 = s * H + (int64_t)lane * R;
+  const int K = a.uK;
+  typedef int iv __attribute__((ext_vector_type(DW)));
+  const iv d = *reinterpret_cast<const iv*>(a.desc + DW * s);
+  const Pack<T, R>* __restrict__ vp = reinterpret_cast<const Pack<T, R>*>(a.uval + s * H * K) + lane;
+  Pack<T, R> v[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u)
+    if (u < K) v[u] = ld<true>(&vp[u * 64]);
+  Pack<T, R> xr[U];
+  const int64_t xmax = a.nx - R;
+#pragma unroll
+  for (int u = 0; u < U; ++u)
+    if (u < K) {
+      const int64_t j = row0 + a.upat[u];
+      xr[u] = ld_xrun<T, R>((const T*)a.x + (j < 0 ? 0 : j > xmax ? xmax : j));
+    }
+  const int emask = d[2];
+  uint64_t m = 0;
+#pragma unroll
+  for (int i = 0; i < H / 64; ++i) {
+    const uint64_t mw = (uint64_t)(uint32_t)d[4 + 2 * i] | ((uint64_t)(uint32_t)d[5 + 2 * i] << 32);
+    if (i == 0 || (lane * R) / 64 == i) m = mw;
+  }
+  bool ok[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) ok[r] = ((m >> ((lane * R + r) & 63)) & 1ull) && (row0 + r < a.nrows);
+  T acc[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    if (BMODE == 0) {
+      acc[r] = zero_of<T>();
+    } else {
+      T yo = zero_of<T>();
+      if (ok[r]) yo = a.y[a.ymap ? (int64_t)a.ymap[row0 + r] : row0 + r];
+      acc[r] = (BMODE == 2) ? yo * a.beta : yo;
+    }
+  }
+  const bool pf = (a.flags & SPMV_PRODA) != 0;
+#pragma unroll
+  for (int u = 0; u < U; ++u)
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const T t = acc[r] + term<ALPHA>(v[u].v[r], xr[u].v[r], a.alpha, pf);
+      acc[r] = pick(u < K && ((emask >> u) & 1), t, acc[r]);
+    }
+  if (a.dotp) {  // fused dot(u, c), as in spmv_wave
+    using DA = typename DAcc<T>::type;
+    DA part = zero_of<DA>();
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+      if (ok[r]) part = part + dacc(cdot(a.dotu[row0 + r], acc[r]));
+#pragma unroll
+    for (int dd = 32; dd >= 1; dd >>= 1) part = part + shfl_down_acc(part, dd);
+    if (lane == 0) reinterpret_cast<DA*>(a.dotp)[a.dot_base + s] = part;
+  }
+  bool all = true;
+#pragma unroll
+  for (int r = 0; r < R; ++r) all = all && ok[r];
+  if (all && !a.ymap) {
+    Pack<T, R> o;
+#pragma unroll
+    for (int r = 0; r < R; ++r) o.v[r] = acc[r];
+    *reinterpret_cast<Pack<T, R>*>(a.y + row0) = o;
+  } else {
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+      if (ok[r]) a.y[a.ymap ? (int64_t)a.ymap[row0 + r] : row0 + r] = acc[r];
+  }
+}
+
 // Several parts of one device in ONE launch (parts sharing a stream pair):
 // the work items of part p are [start[p], start[p+1]) of the grid's waves,
 // so a mul! over P small parts fills the GPU once instead of P times and
@@ -1309,6 +1400,12 @@ __device__ __forceinline__ void group_wave(const SpmvGroup<T>& g) {
       // Dirichlet rows): the short-row launch then holds the pattern code's
       // registers (C2: 98 -> 84 VGPRs, 6 waves per SIMD instead of 5)
       spmv_wave<T, R, ALPHA, BMODE, 4, 0, false, false>(g.a[p], w - g.start[p]);
+      return;
+    }
+  }
+  if constexpr (PK == 1 && SH && !XV && U == 7) {
+    if (g.a[p].uval) {  // the short-row tail launch over the uniform layout
+      spmv_wave_u<T, R, ALPHA, BMODE, U>(g.a[p], w - g.start[p]);
       return;
     }
   }
@@ -1486,6 +1583,11 @@ static SpmvArgs<T> make_args(int which, int64_t nwork, const int32_t* list, cons
       a.mask = (decltype(a.mask))(A->d_mask);
       a.kmax = A->kmax;
       if (knobs().spmv_flags & SPMV_DESC) a.desc = (decltype(a.desc))(A->d_pdesc);
+      if (A->d_uval && a.desc) {
+        a.uval = (decltype(a.uval))((const T*)A->d_uval);
+        a.uK = A->uK;
+        for (int e = 0; e < 8; ++e) a.upat[e] = A->upat[e];
+      }
     } else {
       a.slen = (decltype(a.slen))(A->d_slice_len);
       if (which == 4) {
@@ -2858,6 +2960,34 @@ __global__ void k_t_pairinfo(int64_t n, const int32_t* __restrict__ rows, int H,
     }
   }
   pairable[i] = ok;
+}
+
+// the uniform layout's values (build_uniform): one thread per (slice, entry
+// < 8, lane) of the pattern slices; entry k of the slice's pattern goes to
+// U's position emap[pattern id][k]
+template <typename E, int R>
+__global__ void k_u_fill(int64_t ns, int H, int K, const int32_t* __restrict__ kind, const int64_t* __restrict__ soff,
+                         const int32_t* __restrict__ plen, const int32_t* __restrict__ emap,
+                         const E* __restrict__ val, E* __restrict__ uval) {
+  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (i >= ns * 8 * 64) return;
+  const int64_t s = i / (8 * 64);
+  const int k = (int)((i / 64) % 8), l = (int)(i % 64);
+  if (kind[s] != 1) return;
+  const int32_t lraw = plen[s];
+  if (k >= (lraw & 0xff)) return;
+  const int e = emap[(lraw >> 9) * 8 + k];
+#pragma unroll
+  for (int r = 0; r < R; ++r)
+    uval[s * H * K + ((int64_t)e * 64 + l) * R + r] = val[soff[s] + ((int64_t)k * 64 + l) * R + r];
+}
+
+void launch_u_fill(const pa_mat* A, hipStream_t st) {
+  const int64_t n = A->nslices * 8 * 64;
+  if (n == 0 || !A->d_uval) return;
+  hipLaunchKernelGGL((k_u_fill<double, 2>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, A->nslices, A->H,
+                     A->uK, A->d_kind, A->d_slice_off, A->d_plen, A->d_uemap, (const double*)A->d_val,
+                     (double*)A->d_uval);
 }
 
 void launch_t_pairinfo(const pa_mat* A, int64_t n, const int32_t* rows, int32_t* pairable, hipStream_t st) {

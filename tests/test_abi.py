@@ -65,7 +65,7 @@ def test_tune_knobs_round_trip_and_reject_bad_values(pamd):
              "long_rows_exact": 0, "halo_direct": 0, "cg_fuse": 1, "halo_pull": 0, "spmv_format": 0,
              "issue_threads": 0, "pattern_min_regular": 90, "fault_inject": 1, "spmv_tri16": 0,
              "halo_barrier": 0, "spmv_xcd_chunk": 8,
-             "spmv_tri_order": 0, "spmv_side_tail": 0, "f32_rows": 2, "spmv_tri_pack": 0}
+             "spmv_tri_order": 0, "spmv_side_tail": 0, "f32_rows": 2, "spmv_tri_pack": 0, "spmv_uniform": 0}
     for k, v in knobs.items():
         prev = pamd._lib.tune(k, v)
         assert pamd._lib.tune(k, prev) == v, k
@@ -82,7 +82,7 @@ def test_tune_knobs_round_trip_and_reject_bad_values(pamd):
         pamd._lib.tune("spmv_flags", prev)
     for k, bad in (("spmv_merge", 2), ("spmv_merge_max", -1), ("cg_fuse", 3), ("pattern_min_regular", -1),
                    ("pattern_min_regular", 101), ("f32_rows", 1), ("f32_rows", 3), ("f32_rows", 8),
-                   ("spmv_tri_pack", 8)):
+                   ("spmv_tri_pack", 8), ("spmv_uniform", 2)):
         try:
             pamd._lib.tune(k, bad)
             raise AssertionError(f"{k} accepted {bad}")

@@ -650,6 +650,47 @@ def test_fd7_short_row_tail_launch_equals_oracle(be, pamd, O, flags, N):
         pamd._lib.tune("spmv_flags", prev)
 
 
+@pytest.mark.parametrize("uniform", [1, 0])
+@pytest.mark.parametrize("N", [(40, 33, 21), (128, 20, 9)])
+def test_fd7_uniform_layout_equals_oracle(be, pamd, O, uniform, N):
+    """pa_tune("spmv_uniform"): an FD7 part's pattern slices (patterns of 5-7
+    entries, all subsequences of the 7-point union) also stored at slice ·
+    H · 7 in the union's entry order, so C2's short-row tail launch issues
+    its value and x loads from the slice index alone.  mul! gives the
+    oracle's bits with the layout on and off, and again after set_values
+    (the copy refreshed)."""
+    prev = pamd._lib.tune("spmv_uniform", uniform)
+    try:
+        shape = (1, 1, 1)
+        parts = be.get_part_ids(shape)
+        A = pamd.drivers.stencil_operator(parts, N, 7)
+        OA = O.stencil_problem(O.get_part_ids(shape), N, 7)
+        rng = np.random.default_rng(SEED + 57)
+        n = A.cols.partition.local(1).num_lids
+        own = A.rows.partition.local(1).oid_to_lid - 1
+        for rnd in range(2):
+            if rnd == 1:  # test_fdm's operator (built from COO): new values through set_values
+                A, _, _, _ = pamd.drivers.fdm_problem(parts, 24)
+                OA, _, _, _ = O.fdm_problem(O.get_part_ids(shape), 24)
+                assert A.values.local(1).info()["pattern_slices"] > 0
+                v2 = rng.uniform(-1, 1, len(OA.values.parts[0].nzval))
+                A.values.local(1).set_values(v2)
+                OA = O.PSparseMatrix(O.map_parts(lambda M: O.CSC(M.m, M.n, M.colptr, M.rowval, v2.copy()),
+                                                 OA.values), OA.rows, OA.cols)
+                n = A.cols.partition.local(1).num_lids
+                own = A.rows.partition.local(1).oid_to_lid - 1
+            xv = rng.uniform(-1, 1, n)
+            x = pamd.PVector.from_host(pamd.map_parts(lambda s: xv, A.cols.partition), A.cols)
+            y = pamd.PVector.undef(A.rows)
+            pamd.mul_(y, A, x)
+            ox = O.PVector(O.map_parts(lambda s: xv.copy(), OA.cols.partition), OA.cols)
+            oy = O.pvector_undef(OA.rows)
+            O.mul_(oy, OA, ox)
+            assert np.array_equal(y.to_host().local(1)[own], oy.values[1][own]), (uniform, rnd)
+    finally:
+        pamd._lib.tune("spmv_uniform", prev)
+
+
 @pytest.mark.parametrize("dtype", [np.float64, np.float32, np.complex128, np.complex64])
 @pytest.mark.parametrize("flags", [221, 223])
 def test_pattern_slice_descriptor_equals_oracle(be, pamd, O, dtype, flags):
