@@ -120,11 +120,11 @@ int pa_device_count(int* count);
  *               slices: the Float64 geometry, so delta16 rows take the
  *               triple SELL), 0 (default, auto): 4, rebuilt with 2 when
  *               fewer than 80 % of the slices are pattern slices;
- * "spmv_tri_pack" triple-SELL tri slices of 2 rows per lane (matrices
- *               built afterwards): bit 0 Float32: a triple's values as one
- *               16 B and one 8 B pack per lane, bit 1 Float32: a batch's
- *               codes as 16 + 16 + 4 B packs, bit 2 pair slices (every
- *               element type, pa_mat_pair_info); 7 (default) all, 0 none;
+ * "spmv_tri_pack" triple-SELL slices of 2 rows per lane (matrices built
+ *               afterwards): bit 2 pair slices (every element type,
+ *               pa_mat_pair_info), bit 0 their Float32 values as one 16 B
+ *               and one 8 B pack per triple and lane (bit 1 unused);
+ *               7 (default), 0 none;
  * "fault_inject" tests only: threaded issue jobs add an invalid launch. */
 int pa_tune(const char* key, int value, int* previous);
 /* The same knobs for one context: calls led by parts of `c` (their first

@@ -544,9 +544,8 @@ int build_triple_sell(pa_mat* A, std::vector<int32_t>& kind, int64_t noids) {
   constexpr int32_t kLen = (1 << 28) - 1, kReg = 1 << 28, kGhost = 1 << 29, kBad = 1 << 30;
   for (int32_t v : info)
     if (v & kBad) return 0;
-  // spmv_tri_pack: 2 rows per lane only; value and code packs Float32 only
-  // (8 B elements with the code packs: C5 F64 +1.5 %, profiles/r06/u/)
-  const int tpack = R == 2 ? (A->dtype == PA_F32 ? knobs().tri_pack : knobs().tri_pack & 4) : 0;
+  // spmv_tri_pack: 2 rows per lane only; the value packs Float32 only
+  const int tpack = R == 2 ? (A->dtype == PA_F32 ? knobs().tri_pack & 5 : knobs().tri_pack & 4) : 0;
   // pair slices (spmv_tri_pack bit 2): candidate i and i + 1 (rows a, a + 1,
   // both regular, one length) pair up when row a + 1's columns are row a's
   // plus one, entry for entry (k_t_pairinfo); pairs are taken greedily in
@@ -1459,12 +1458,12 @@ const Knob kKnobs[] = {
      "SELL), 0 = auto (default): 4, rebuilt with 2 when fewer than 80 % of the slices are pattern slices "
      "(C5 F32 -7 %, FE27 256^3 F32 +14 % with 2, profiles/r05/af/)"},
     {"spmv_tri_pack", &Knobs::tri_pack, nullptr, 0, 7, 0,
-     "spmv_tri_pack: triple-SELL tri slices of 2 rows per lane (matrices built afterwards): bit 0 = Float32: a "
-     "triple's values as one 16 B pack (entries 0 and 1 of both rows) and one 8 B pack (entry 2) per lane "
-     "(two loads instead of three), bit 1 = Float32: a 9-triple batch's codes as 16 + 16 + 4 B packs, bit 2 "
-     "= pair slices (all element types): rows a, a + 1 whose columns differ by one, entry for entry, share "
-     "one lane, one code and one x run per triple (C5 F32 -2.4 %, F64 -1 %, profiles/r06/u/); 7 = all "
-     "(default), 0 = none"},
+     "spmv_tri_pack: triple-SELL slices of 2 rows per lane (matrices built afterwards): bit 2 = pair slices "
+     "(all element types): rows a, a + 1 whose columns differ by one, entry for entry, share one lane, one "
+     "code and one x run per triple (C5 F32 -2.4 %, F64 -1 %, profiles/r06/u/); bit 0 = Float32 pair slices: "
+     "a triple's values as one 16 B pack (entries 0 and 1 of both rows) and one 8 B pack (entry 2) per lane "
+     "(two loads instead of three); bit 1: unused since r06/aa (the Float32 tri slices' code packs); 7 = "
+     "default, 0 = none"},
     {"spmv_uniform", &Knobs::spmv_uniform, nullptr, 0, 1, 0,
      "spmv_uniform: Float64 pattern slices whose patterns (<= 7 entries) fit one union U (FD7; matrices built "
      "afterwards): 1 = a copy of their values at slice * H * |U| in U's entry order, so the short-row tail "

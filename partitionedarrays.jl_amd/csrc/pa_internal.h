@@ -358,7 +358,7 @@ struct Knobs {
   int tri_order;         // triple SELL row order: 0 triple rows first, 1 the other rows first (build_triple_sell)
   int side_tail;         // per-kind launches: the side rows as the trailing waves of the pattern launch
   int f32_rows;          // Float32 SELL rows per lane (matrices built afterwards): 4 (16 B packs), 2 (8 B), 0 auto
-  int tri_pack;          // triple-SELL tri slices: bit 0 Float32 per-triple value packs, bit 1 batch code packs, bit 2 pairs
+  int tri_pack;          // triple SELL: bit 2 pair slices, bit 0 their Float32 per-triple value packs
   int spmv_uniform;      // Float64 short pattern rows: the uniform layout (build_uniform)
 };
 // the knobs of the call running on this thread (outside a call: a snapshot
@@ -586,9 +586,8 @@ struct pa_mat {
   int32_t* d_t_len = nullptr;        // entries per row (max over the slice), bit 30: tri slice (kTriSlice), bit 29: pair slice
   uint16_t* d_t_col16 = nullptr;     // codes (tri slices: one per triple, slot groups 0..len/3-1)
   void* d_t_val = nullptr;           // values (lane-major packs of R, like the main SELL; t_pack: tri slices per triple)
-  int t_pack = 0;                    // tri slices of 2 rows per lane (spmv_tri_pack): bit 0 (Float32) triple t's values
-                                     // as {entries 0,1 × R rows} 16 B + {entry 2} 8 B per lane; bit 1 codes in batch
-                                     // packs (t_code_slot); bit 2 pair slices
+  int t_pack = 0;                    // slices of 2 rows per lane (spmv_tri_pack): bit 2 pair slices; bit 0 (Float32)
+                                     // a pair slice's triple t as {entries 0,1 × R rows} 16 B + {entry 2} 8 B per lane
   int64_t t_pair_slices = 0, t_pair_rows = 0;  // pair slices and the rows they hold
   // the uniform layout of short pattern rows (build_uniform): K = |U| <= 7
   // entries per row at slice * H * K, U's offsets, pattern id -> U position

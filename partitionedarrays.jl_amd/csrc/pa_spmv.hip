@@ -56,8 +56,7 @@ struct alignas(2 * R) S16Pack {
 enum { SPMV_NT = 1, SPMV_DESC = 2 /* pattern / triple-SELL slices: one descriptor load (make_args) */, SPMV_XPAIR = 4, SPMV_TAILB = 8, SPMV_IDLIST = 16, SPMV_YNT = 32, SPMV_SHORT = 64,
        SPMV_SHORT7 = 128 /* Float64 rows <= 7 entries: k_spmv_group_short7 */,
        SPMV_PRODA = 256 /* per matrix: CSR parent, α scales the product */,
-       SPMV_TPACK = 512 /* per matrix: Float32 tri slices with per-triple value packs (pa_mat::t_pack bit 0) */,
-       SPMV_TPACKC = 1024 /* per matrix: tri slices with batch code packs (pa_mat::t_pack bit 1) */ };
+       SPMV_TPACK = 512 /* per matrix: Float32 pair slices with per-triple value packs (pa_mat::t_pack bit 0) */ };
 
 typedef unsigned int spmv_u32x4 __attribute__((ext_vector_type(4)));
 // Process-wide knobs (pa_tune).  Defaults from the A/Bs in
@@ -584,18 +583,20 @@ constexpr int kTriBatch = 4;
 // ld_xtrip.  Padding triples (code 0xFFFF) are never accumulated.  Four
 // triples (12 values) in flight per lane, as in rows_pattern_tri.  The
 // terms and their order are those of rows_d16.
-template <typename T, int R, bool ALPHA, bool NT, typename XS, bool TP = false, bool TPC = false>
+template <typename T, int R, bool ALPHA, bool NT, typename XS>
 __device__ __forceinline__ void rows_t16_tri(T (&acc)[R], const S16Pack<R>* __restrict__ cp,
                                              const Pack<T, R>* __restrict__ vp, int len, const XS& x, T alpha,
                                              bool pf, const int32_t (&rw)[R], int32_t gb) {
   const int ntri = len / 3;
-  // Float32 (2 rows per lane, f32_rows): 8 triples in the same registers
-  // (C5 F32 0.0679 -> 0.0670 ms, four alternating library rounds,
-  // profiles/r05/af/ab_f32_tri_batch8_c5.log; the merged kernel then has 134
-  // VGPRs, 3 waves per SIMD; 6 triples fit 4 waves at 104 VGPRs but run
-  // 0.0679 -> 0.0682 ms, six alternating rounds, ab_f32_tri_batch6_c5.log).
-  // 8 B elements keep 4: 6 costs C5 F64 0.1056 -> 0.1094 ms, ComplexF32
-  // 0.1083 -> 0.1149 (ab_f64_c64_tri_batch6_c5.log)
+  // Batches of 4 triples for every element type.  Float32 (2 rows per lane)
+  // ran batches of 9 (r05-r06: 8, then 9 triples, per-triple value packs and
+  // batch code packs, profiles/r05/af/, r06/n/, r06/s/), which held the
+  // merged Float32 kernel at 158 VGPRs (3 waves per SIMD); since the pair
+  // slices (rows_t16_pair) took most triple rows, the batches of 4 (118
+  // VGPRs, 4 waves per SIMD) run C5 F32 0.0640 -> 0.0631 ms (four
+  // alternating library rounds, profiles/r06/aa/).  8 B elements: 6 triples
+  // cost C5 F64 0.1056 -> 0.1094 ms, ComplexF32 0.1083 -> 0.1149
+  // (r05/af/ab_f64_c64_tri_batch6_c5.log)
   constexpr int TB = kTriBatch;
   auto step = [&](const S16Pack<R>* q, const Pack<T, R>* v, auto nb) {
     constexpr int B = decltype(nb)::value;
@@ -623,85 +624,6 @@ __device__ __forceinline__ void rows_t16_tri(T (&acc)[R], const S16Pack<R>* __re
         }
   };
   int t = 0;
-  if constexpr (sizeof(T) == 4) {
-    // Float32: batches of 9 triples (an FE27 row is one batch), the last
-    // batch clamped: past the row's end a lane re-reads its last triple
-    // (the same lines) and never accumulates it, so the batch stays
-    // branch-free (a predicated batch holds 186-208 VGPRs, this one 145: 3
-    // waves per SIMD like the 8-triple loop with its single-triple tail).
-    // Library A/B, six alternating rounds on one box (profiles/r06/n/): C5
-    // F32 0.0686 -> 0.0672 ms, kernels 0.0735 -> 0.0720 ms
-    constexpr int MB = 9;
-    for (; t < ntri; t += MB) {
-      S16Pack<R> q[MB];
-      Pack<T, R> v[3 * MB];
-      if (TPC && t + MB <= ntri) {
-        // packed codes (t_code_slot): triples 0-3 and 4-7 of the batch as
-        // one 4R-code pack each, triple 8 as an R pack: three loads, not nine
-        const S16Pack<R>* __restrict__ cb = cp - threadIdx.x % 64 + (int64_t)t * 64;
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          const S16Pack<4 * R> q4 = ld<NT>(reinterpret_cast<const S16Pack<4 * R>*>(cb + h * 4 * 64) + threadIdx.x % 64);
-#pragma unroll
-          for (int i = 0; i < 4; ++i)
-#pragma unroll
-            for (int r = 0; r < R; ++r) q[4 * h + i].c[r] = q4.c[i * R + r];
-        }
-        q[8] = ld<NT>(cb + 8 * 64 + threadIdx.x % 64);
-      } else {
-#pragma unroll
-        for (int u = 0; u < MB; ++u) q[u] = ld<NT>(&cp[min(t + u, ntri - 1) * 64]);
-      }
-      if constexpr (TP) {
-        // spmv_tri_pack (k_t_fill): triple u's entries 0 and 1 of the lane's
-        // R rows as one 2R-value pack, entry 2 as an R pack: two loads per
-        // triple instead of three.  With the code packs (TPC) a full batch
-        // issues 3 + 18 loads instead of 9 + 27 ahead of its 18 x runs; C5
-        // F32 -3.2 % (profiles/r06/s/, two interleaved rounds: values alone
-        // -3.2 %, codes alone -1.4 %)
-        const Pack<T, R>* __restrict__ vb = vp - threadIdx.x % 64;  // the slice's values
-#pragma unroll
-        for (int u = 0; u < MB; ++u) {
-          const Pack<T, R>* tb = vb + (int64_t)min(t + u, ntri - 1) * 3 * 64;
-          const Pack<T, 2 * R> p01 = ld<NT>(reinterpret_cast<const Pack<T, 2 * R>*>(tb) + threadIdx.x % 64);
-#pragma unroll
-          for (int r = 0; r < R; ++r) {
-            v[3 * u].v[r] = p01.v[r];
-            v[3 * u + 1].v[r] = p01.v[R + r];
-          }
-          v[3 * u + 2] = ld<NT>(tb + 2 * 64 + threadIdx.x % 64);
-        }
-      } else {
-#pragma unroll
-        for (int u = 0; u < MB; ++u)
-#pragma unroll
-          for (int j = 0; j < 3; ++j) v[3 * u + j] = ld<NT>(&vp[(3 * min(t + u, ntri - 1) + j) * 64]);
-      }
-      T xv[MB][3][R];
-      bool ok[MB][R];
-#pragma unroll
-      for (int u = 0; u < MB; ++u)
-#pragma unroll
-        for (int r = 0; r < R; ++r) {
-          const int32_t c = d16_col(q[u].c[r], rw[r], gb);
-          ok[u][r] = c >= 0 && t + u < ntri;
-          T t3[3];
-          x.trip(c >= 0 ? c : 0, t3);
-#pragma unroll
-          for (int j = 0; j < 3; ++j) xv[u][j][r] = t3[j];
-        }
-#pragma unroll
-      for (int u = 0; u < MB; ++u)
-#pragma unroll
-        for (int j = 0; j < 3; ++j)
-#pragma unroll
-          for (int r = 0; r < R; ++r) {
-            const T tt = acc[r] + term<ALPHA>(v[3 * u + j].v[r], xv[u][j][r], alpha, pf);
-            acc[r] = pick(ok[u][r], tt, acc[r]);
-          }
-    }
-    return;
-  }
   for (; t + TB <= ntri; t += TB) {
     S16Pack<R> q[TB];
     Pack<T, R> v[3 * TB];
@@ -1188,13 +1110,6 @@ __device__ __forceinline__ void spmv_wave(const SpmvArgs<T>& a, const int64_t w)
           } else {
             rows_t16_pair<T, ALPHA, XS, false>(acc, cs, vp, len, xs, a.alpha, pf, rw[0], gb);
           }
-        } else if (sizeof(T) == 4 && (a.flags & SPMV_TPACKC)) {  // (value and code packs: Float32 only)
-          if constexpr (sizeof(T) == 4) {
-            if (tp) rows_t16_tri<T, R, ALPHA, true, XS, true, true>(acc, cp, vp, len, xs, a.alpha, pf, rw, gb);
-            else rows_t16_tri<T, R, ALPHA, true, XS, false, true>(acc, cp, vp, len, xs, a.alpha, pf, rw, gb);
-          }
-        } else if (tp) {
-          if constexpr (sizeof(T) == 4) rows_t16_tri<T, R, ALPHA, true, XS, true, false>(acc, cp, vp, len, xs, a.alpha, pf, rw, gb);
         } else {
           packed = false;
         }
@@ -1547,8 +1462,7 @@ static SpmvArgs<T> make_args(int which, int64_t nwork, const int32_t* list, cons
   a.ymap = (decltype(a.ymap))(ymap);
   a.alpha = *(const T*)alpha;
   a.beta = *(const T*)beta;
-  a.flags = knobs().spmv_flags | (A->csr ? SPMV_PRODA : 0) | (which == 5 && (A->t_pack & 1) ? SPMV_TPACK : 0) |
-            (which == 5 && (A->t_pack & 2) ? SPMV_TPACKC : 0);
+  a.flags = knobs().spmv_flags | (A->csr ? SPMV_PRODA : 0) | (which == 5 && (A->t_pack & 1) ? SPMV_TPACK : 0);
   a.xcd_chunk = knobs().spmv_xcd_chunk >= 0 ? knobs().spmv_xcd_chunk : A->xcd_auto;
   a.maxlen = which == 0   ? A->maxlen_pat
              : which == 2 ? A->maxlen_side
@@ -3032,14 +2946,11 @@ __global__ __launch_bounds__(256) void k_t_gbase(int64_t ns, int64_t nrows, int 
 }
 
 // Slot of code group g (triple g of a tri slice, entry g otherwise) of lane
-// `lane`, row r, in a triple-SELL slice at code offset d.  Packed codes
-// (spmv_tri_pack bit 1, Float32 tri slices): each full batch of 9 triples
-// (rows_t16_tri's Float32 batch) holds triples 0-3 and 4-7 as one 4R-code
-// pack per lane each and triple 8 as an R pack; a last batch of fewer
-// triples keeps one R pack per triple, as unpacked slices do.
-// Generally: R codes per lane and triple (1 in pair slices), batches of B
-// triples (9 for 4 B elements, 4 for 8 B: rows_t16_tri / rows_t16_pair);
-// a full batch holds packs of 4 triples, then single triples.
+// `lane`, row r, in a triple-SELL slice at code offset d, R codes per lane
+// and triple.  Packed (pair slices, R = 1, rows_t16_pair): each full batch
+// of B triples (9 for 4 B elements, 4 for 8 B) holds packs of 4 triples per
+// lane, then single triples; a last batch of fewer triples keeps one code
+// per triple, as unpacked slices do.
 __device__ __forceinline__ int64_t t_code_slot(int64_t d, int g, int ntri, int lane, int r, int R, bool packed,
                                                int B) {
   const int b = g / B, i = g % B, nq = 4 * (B / 4);
@@ -3076,7 +2987,7 @@ __global__ void k_t_fill(int64_t nrows, int H, const int32_t* __restrict__ rowma
     E v;
     __builtin_memset(&v, 0, sizeof(E));
     if (k < n) v = val[sk];
-    if ((pack & 1) && tri && sizeof(E) == 4) {  // triple t: entries 3t, 3t+1 as one 2R-value pack per lane, entry 3t+2 as an R pack
+    if ((pack & 1) && pair && sizeof(E) == 4) {  // triple t: entries 3t, 3t+1 as one 2R-value pack per lane, entry 3t+2 as an R pack
       const int64_t tb = d + (int64_t)(k / 3) * 3 * 64 * R;
       const int j = k % 3;
       tval[j < 2 ? tb + (int64_t)lane * 2 * R + j * R + r : tb + 2 * 64 * R + (int64_t)lane * R + r] = v;
@@ -3091,7 +3002,7 @@ __global__ void k_t_fill(int64_t nrows, int H, const int32_t* __restrict__ rowma
     }
     const int g = tri ? k / 3 : k;
     col16[pair ? t_code_slot(d, g, L / 3, lane, 0, 1, true, B)
-               : t_code_slot(d, g, L / 3, lane, r, R, tri && (pack & 2), B)] = q;
+               : t_code_slot(d, g, L / 3, lane, r, R, false, B)] = q;
   }
 }
 
@@ -3114,7 +3025,7 @@ __global__ void k_t_check(int64_t npos, int64_t nrows, int H, int R, const int32
   unsigned nb = 0;
   for (int g = 0; g < G; ++g) {
     const int64_t at = pair ? t_code_slot(toff[ts], g, L / 3, lane, 0, 1, true, B)
-                            : t_code_slot(toff[ts], g, L / 3, lane, r, R, tri && (pack & 2), B);
+                            : t_code_slot(toff[ts], g, L / 3, lane, r, R, false, B);
     const int32_t c = d16_col(col16[at], row, gbase[ts]);
     if (c < -1 || (c >= 0 && c + (pair ? 3 : tri ? 2 : 0) >= ncols)) ++nb;
   }
