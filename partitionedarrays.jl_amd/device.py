@@ -527,7 +527,8 @@ class DeviceMatrix:
         _lib.call("pa_mat_triple_info", self.h, *[C.byref(x) for x in t])
         d.update(zip(["triple_sell_slices", "triple_sell_rows", "tri_slices", "tri_rows"], [x.value for x in t]))
         pr = [C.c_int64() for _ in range(2)]
-        _lib.call("pa_mat_pair_info", self.h, *[C.byref(x) for x in pr])
+        if hasattr(_lib.lib(), "pa_mat_pair_info"):  # (an older build under PA_HIP_LIB lacks it: A/B tooling)
+            _lib.call("pa_mat_pair_info", self.h, *[C.byref(x) for x in pr])
         d.update(zip(["pair_slices", "pair_rows"], [x.value for x in pr]))
         lr = [C.c_int64() for _ in range(2)]
         _lib.call("pa_mat_long_rows", self.h, *[C.byref(x) for x in lr])
