@@ -125,6 +125,11 @@ int pa_device_count(int* count);
  *               pa_mat_pair_info), bit 0 their Float32 values as one 16 B
  *               and one 8 B pack per triple and lane (bit 1 unused);
  *               7 (default), 0 none;
+ * "spmv_uniform" 1 (default): Float64 pattern slices whose patterns (<= 7
+ *               entries) are subsequences of one union U (FD7) also keep
+ *               their values at slice * H * |U| in U's order, so the
+ *               short-row tail launch issues its loads before the slice's
+ *               descriptor arrives (matrices built afterwards); 0 off;
  * "fault_inject" tests only: threaded issue jobs add an invalid launch. */
 int pa_tune(const char* key, int value, int* previous);
 /* The same knobs for one context: calls led by parts of `c` (their first
