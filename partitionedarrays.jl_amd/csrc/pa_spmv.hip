@@ -1273,7 +1273,17 @@ __device__ __forceinline__ void spmv_wave_u(const SpmvArgs<T>& a, const int64_t 
     Pack<T, R> o;
 #pragma unroll
     for (int r = 0; r < R; ++r) o.v[r] = acc[r];
-    *reinterpret_cast<Pack<T, R>*>(a.y + row0) = o;
+    if constexpr (sizeof(Pack<T, R>) == 16) {
+      if (a.flags & SPMV_YNT) {  // as spmv_wave: y as a non-temporal 16 B store per lane
+        spmv_u32x4 yw;
+        __builtin_memcpy(&yw, &o, 16);
+        __builtin_nontemporal_store(yw, reinterpret_cast<spmv_u32x4*>(a.y + row0));
+      } else {
+        *reinterpret_cast<Pack<T, R>*>(a.y + row0) = o;
+      }
+    } else {
+      *reinterpret_cast<Pack<T, R>*>(a.y + row0) = o;
+    }
   } else {
 #pragma unroll
     for (int r = 0; r < R; ++r)

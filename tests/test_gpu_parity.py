@@ -650,16 +650,17 @@ def test_fd7_short_row_tail_launch_equals_oracle(be, pamd, O, flags, N):
         pamd._lib.tune("spmv_flags", prev)
 
 
-@pytest.mark.parametrize("uniform", [1, 0])
+@pytest.mark.parametrize("uniform,flags", [(1, 223), (1, 255), (0, 223)])
 @pytest.mark.parametrize("N", [(40, 33, 21), (128, 20, 9)])
-def test_fd7_uniform_layout_equals_oracle(be, pamd, O, uniform, N):
+def test_fd7_uniform_layout_equals_oracle(be, pamd, O, uniform, flags, N):
     """pa_tune("spmv_uniform"): an FD7 part's pattern slices (patterns of 5-7
     entries, all subsequences of the 7-point union) also stored at slice ·
     H · 7 in the union's entry order, so C2's short-row tail launch issues
     its value and x loads from the slice index alone.  mul! gives the
     oracle's bits with the layout on and off, and again after set_values
-    (the copy refreshed)."""
+    (the copy refreshed); spmv_flags 255 adds the non-temporal y stores."""
     prev = pamd._lib.tune("spmv_uniform", uniform)
+    prevf = pamd._lib.tune("spmv_flags", flags)
     try:
         shape = (1, 1, 1)
         parts = be.get_part_ids(shape)
@@ -686,9 +687,10 @@ def test_fd7_uniform_layout_equals_oracle(be, pamd, O, uniform, N):
             ox = O.PVector(O.map_parts(lambda s: xv.copy(), OA.cols.partition), OA.cols)
             oy = O.pvector_undef(OA.rows)
             O.mul_(oy, OA, ox)
-            assert np.array_equal(y.to_host().local(1)[own], oy.values[1][own]), (uniform, rnd)
+            assert np.array_equal(y.to_host().local(1)[own], oy.values[1][own]), (uniform, flags, rnd)
     finally:
         pamd._lib.tune("spmv_uniform", prev)
+        pamd._lib.tune("spmv_flags", prevf)
 
 
 @pytest.mark.parametrize("dtype", [np.float64, np.float32, np.complex128, np.complex64])
