@@ -838,8 +838,18 @@ __device__ __forceinline__ void rows_pattern_tri(T (&acc)[R], const int32_t* __r
 #pragma unroll
   for (int r = 0; r < R; ++r) any = any || ok[r];
   auto triple = [&](int32_t o, T (&xv)[3][R]) {
-    const Pack<T, R> A = x.template run<R>(any ? rbase + o : 0);
-    const Pack<T, R> B = x.template run<R>(any ? rbase + o + 2 : 0);
+    Pack<T, R> A, B;
+    if constexpr (R == 2 && sizeof(T) == 4) {  // Float32, 2 rows per lane: x[o .. o+3] as one 16 B load
+      T q[4];
+      x.quad(any ? rbase + o : 0, q);
+      A.v[0] = q[0];
+      A.v[1] = q[1];
+      B.v[0] = q[2];
+      B.v[1] = q[3];
+    } else {
+      A = x.template run<R>(any ? rbase + o : 0);
+      B = x.template run<R>(any ? rbase + o + 2 : 0);
+    }
 #pragma unroll
     for (int r = 0; r < R; ++r) {
       xv[0][r] = A.v[r];
